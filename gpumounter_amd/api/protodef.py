@@ -1,0 +1,84 @@
+"""Tiny DSL that turns message/enum/service declarations into runtime protobuf classes.
+
+There is no ``protoc`` / ``grpc_tools`` in this environment, so wire-compatible
+message classes are built from ``descriptor_pb2.FileDescriptorProto`` at import time. The
+resulting classes are ordinary generated-style protobuf messages (same wire format as protoc
+output, JSON via ``json_format``).
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+F = descriptor_pb2.FieldDescriptorProto
+
+_TYPES = {
+    "string": F.TYPE_STRING, "int32": F.TYPE_INT32, "int64": F.TYPE_INT64,
+    "uint32": F.TYPE_UINT32, "uint64": F.TYPE_UINT64, "bool": F.TYPE_BOOL,
+    "double": F.TYPE_DOUBLE, "float": F.TYPE_FLOAT, "bytes": F.TYPE_BYTES,
+}
+
+# field spec: (name, number, type, label) where type is a scalar name, "msg:.pkg.Name",
+# or "enum:.pkg.Name.Enum"; label "opt" | "rep"
+FieldSpec = Tuple[str, int, str, str]
+
+
+class ProtoFile:
+    def __init__(self, name: str, package: str, pool: Optional[descriptor_pool.DescriptorPool] = None):
+        self.fdp = descriptor_pb2.FileDescriptorProto(name=name, package=package, syntax="proto3")
+        self.package = package
+        self.pool = pool or descriptor_pool.Default()
+        self._built = False
+
+    def message(self, name: str, fields: Sequence[FieldSpec] = (),
+                enums: Dict[str, Iterable[Tuple[str, int]]] = None) -> "ProtoFile":
+        m = self.fdp.message_type.add(name=name)
+        for ename, values in (enums or {}).items():
+            e = m.enum_type.add(name=ename)
+            for vname, num in values:
+                e.value.add(name=vname, number=num)
+        for fname, num, ftype, label in fields:
+            f = m.field.add(name=fname, number=num, json_name=_json_name(fname))
+            f.label = F.LABEL_REPEATED if label == "rep" else F.LABEL_OPTIONAL
+            if ftype.startswith("msg:"):
+                f.type = F.TYPE_MESSAGE
+                f.type_name = ftype[4:]
+            elif ftype.startswith("enum:"):
+                f.type = F.TYPE_ENUM
+                f.type_name = ftype[5:]
+            else:
+                f.type = _TYPES[ftype]
+        return self
+
+    def service(self, name: str, methods: Sequence[Tuple[str, str, str]]) -> "ProtoFile":
+        s = self.fdp.service.add(name=name)
+        for mname, req, resp in methods:
+            s.method.add(name=mname, input_type=f".{self.package}.{req}",
+                         output_type=f".{self.package}.{resp}")
+        return self
+
+    def build(self) -> Dict[str, type]:
+        try:
+            fd = self.pool.FindFileByName(self.fdp.name)
+        except KeyError:
+            fd = self.pool.Add(self.fdp) if hasattr(self.pool, "Add") else None
+            fd = self.pool.FindFileByName(self.fdp.name)
+        classes = {}
+        for mname in fd.message_types_by_name:
+            classes[mname] = message_factory.GetMessageClass(fd.message_types_by_name[mname])
+        self._built = True
+        return classes
+
+
+def _json_name(name: str) -> str:
+    parts = name.split("_")
+    return parts[0] + "".join(p[:1].upper() + p[1:] for p in parts[1:])
+
+
+def method_path(package: str, service: str, method: str) -> str:
+    return f"/{package}.{service}/{method}"
+
+
+def fields_of(cls) -> List[Tuple[str, int]]:
+    return [(f.name, f.number) for f in cls.DESCRIPTOR.fields]

@@ -1,0 +1,46 @@
+"""Shared enums and constants (reference: pkg/util/gpu/types.go:5-28)."""
+from __future__ import annotations
+
+import enum
+
+
+class MountType(str, enum.Enum):
+    """How a pod currently holds hot-mounted GPUs (reference types.go:21-28)."""
+
+    ENTIRE = "entire-mount"
+    SINGLE = "single-mount"
+    NONE = "no-mount"
+    UNKNOWN = "unknown-mount"
+
+
+class AllocStatus(str, enum.Enum):
+    """Placeholder lifecycle outcomes (reference types.go:12-16)."""
+
+    INSUFFICIENT = "InsufficientGPU"
+    CREATED = "SuccessfullyCreated"
+    FAILED_CREATE = "FailedCreated"
+    DELETED = "SuccessfullyDeleted"
+    FAILED_DELETE = "FailedDeleted"
+
+
+# Labels / annotations stamped on placeholder pods. The reference used only ``app: gpu-pool``
+# and the name convention ``<owner>-slave-pod-<6 hex>`` (allocator.go:197-201); the owner is
+# matched by *substring* (collector.go:158, SURVEY defect 3). Here the owner is an exact label
+# pair plus the owner UID, and the name convention is kept for operator familiarity.
+LABEL_APP = "app"
+LABEL_APP_VALUE = "gpu-pool"
+LABEL_OWNER = "gpumounter.amd.com/owner"
+LABEL_OWNER_NS = "gpumounter.amd.com/owner-namespace"
+ANN_OWNER_UID = "gpumounter.amd.com/owner-uid"
+ANN_MOUNT_MODE = "gpumounter.amd.com/mount-mode"
+ANN_PREFERRED = "gpumounter.amd.com/preferred-devices"
+ANN_ATTACH_ID = "gpumounter.amd.com/attach-id"
+ANN_CONTAINER = "gpumounter.amd.com/container"
+ANN_DEVICES = "gpumounter.amd.com/devices"
+ANN_STATE = "gpumounter.amd.com/state"      # reserved | attached | detaching
+FINALIZER = "gpumounter.amd.com/release"
+SLAVE_SUFFIX = "-slave-pod-"
+
+# Error strings carried in gRPC status details (master maps them to HTTP bodies).
+ERR_POLICY = "MountPolicyDenied"
+ERR_INTERNAL = "Service Internal Error"

@@ -1,0 +1,167 @@
+"""Single configuration object for master, worker, fakes and bench.
+
+The reference hard-codes nearly everything: ports (reference: cmd/GPUMounter-master/main.go:237,
+cmd/GPUMounter-worker/main.go:24, master dial main.go:82), namespaces (pkg/util/gpu/types.go:18,
+main.go:255-257), the kubelet socket (types.go:6-7), the slave image (allocator.go:218), the
+resource name (types.go:10, allocator.go:223) and a placeholder kubeconfig path
+(pkg/config/config.go:20); only ``CGROUP_DRIVER`` is read from the environment (cgroup.go:79).
+
+Here every knob lives in :class:`Config`, resolved in order
+``defaults → YAML file (GM_CONFIG) → environment (GM_<FIELD>) → explicit overrides``.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field, fields
+from typing import Any, Dict, Mapping, Optional
+
+import yaml
+
+
+@dataclass
+class Config:
+    # --- network ---------------------------------------------------------------------------
+    master_host: str = "0.0.0.0"
+    master_port: int = 8080
+    worker_host: str = "0.0.0.0"
+    worker_port: int = 1200
+    metrics_port: int = 9400
+    # --- kubernetes ------------------------------------------------------------------------
+    kube_api: str = ""                 # "" → in-cluster; else http(s)://host:port (fake in tests)
+    kubeconfig: str = ""
+    kube_token: str = ""
+    kube_ca: str = ""
+    kube_insecure: bool = False
+    node_name: str = ""                # worker's node (downward API NODE_NAME)
+    worker_namespace: str = "kube-system"
+    worker_label: str = "app=gpu-mounter-worker"
+    pool_namespace: str = "gpu-pool"
+    # "pool": placeholders in pool_namespace (reference layout, allocator.go:198);
+    # "tenant": placeholders next to the tenant pod, so the ownerReference is same-namespace and
+    # Kubernetes ≥1.20 GC cleans them up (SURVEY §2.6 defect 4).
+    placeholder_namespace_mode: str = "pool"
+    resource_name: str = "amd.com/gpu"
+    placeholder_image: str = "registry.k8s.io/pause:3.9"
+    placeholder_pull_policy: str = "IfNotPresent"
+    placeholder_priority_class: str = ""
+    # --- kubelet PodResources --------------------------------------------------------------
+    kubelet_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
+    kubelet_timeout_s: float = 10.0
+    podresources_api: str = "auto"     # auto | v1 | v1alpha1
+    # --- device & isolation ----------------------------------------------------------------
+    amdsmi_lib: str = ""               # "" → libamd_smi.so from ROCm; "mock" → bundled mock
+    cgroup_root: str = "/sys/fs/cgroup"
+    cgroup_mode: str = "auto"          # auto | v1 | v2
+    cgroup_driver: str = "auto"        # auto | cgroupfs | systemd
+    devnode_mode: str = "procroot"     # procroot | setns | emulate
+    proc_root: str = "/proc"
+    # For hermetic runs: containers' rootfs live at <container_root_prefix>/<container-id>/ and
+    # device-node writes go there instead of /proc/<pid>/root.
+    container_root_prefix: str = ""
+    drm_major: int = 226
+    kfd_major: int = 0                 # 0 → read /sys/class/kfd/kfd/dev (fallback 511)
+    kfd_dev_path: str = "/sys/class/kfd/kfd/dev"
+    inject_card_nodes: bool = True     # also inject /dev/dri/card<N> (rocm-smi reads it)
+    device_file_mode: int = 0o666      # reference: nvidia.go:39 "666"
+    # --- policy ----------------------------------------------------------------------------
+    topology_policy: str = "xgmi"      # xgmi | first-fit
+    max_gpus_per_request: int = 64
+    kill_signal: int = 15              # SIGTERM like the reference's `kill` (namespace.go:192)
+    kill_grace_s: float = 5.0          # then SIGKILL
+    # --- timeouts / loops ------------------------------------------------------------------
+    attach_timeout_s: float = 120.0
+    detach_timeout_s: float = 60.0
+    rpc_timeout_s: float = 180.0
+    reconcile_period_s: float = 30.0
+    watch_resync_s: float = 300.0
+    # --- observability ---------------------------------------------------------------------
+    log_level: str = "INFO"
+    log_file: str = ""
+    log_json: bool = True
+    roctx: bool = True
+    fault: str = ""                    # fault injection: "stage:prob[,stage:prob]"
+    extra: Dict[str, Any] = field(default_factory=dict)
+
+    # -------------------------------------------------------------------------------------
+    @classmethod
+    def load(cls, path: Optional[str] = None, env: Optional[Mapping[str, str]] = None,
+             **overrides: Any) -> "Config":
+        env = os.environ if env is None else env
+        cfg = cls()
+        path = path or env.get("GM_CONFIG", "")
+        if path:
+            with open(path, "r", encoding="utf-8") as fh:
+                data = yaml.safe_load(fh) or {}
+            if not isinstance(data, dict):
+                raise ValueError(f"config file {path} must hold a mapping")
+            cfg.update(data)
+        env_vals: Dict[str, Any] = {}
+        for f in fields(cls):
+            key = "GM_" + f.name.upper()
+            if key in env:
+                env_vals[f.name] = env[key]
+        # compatibility with the reference's only env knob (cgroup.go:79)
+        if "cgroup_driver" not in env_vals and env.get("CGROUP_DRIVER"):
+            env_vals["cgroup_driver"] = env["CGROUP_DRIVER"]
+        if "node_name" not in env_vals and env.get("NODE_NAME"):
+            env_vals["node_name"] = env["NODE_NAME"]
+        cfg.update(env_vals)
+        cfg.update({k: v for k, v in overrides.items() if v is not None})
+        cfg.validate()
+        return cfg
+
+    def update(self, values: Mapping[str, Any]) -> None:
+        known = {f.name: f for f in fields(self)}
+        for k, v in values.items():
+            if k not in known:
+                self.extra[k] = v
+                continue
+            setattr(self, k, _coerce(known[k], v))
+
+    def replace(self, **kw: Any) -> "Config":
+        c = dataclasses.replace(self, extra=dict(self.extra))
+        c.update(kw)
+        c.validate()
+        return c
+
+    def validate(self) -> None:
+        _choice("cgroup_mode", self.cgroup_mode, ("auto", "v1", "v2"))
+        _choice("cgroup_driver", self.cgroup_driver, ("auto", "cgroupfs", "systemd"))
+        _choice("devnode_mode", self.devnode_mode, ("procroot", "setns", "emulate"))
+        _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
+        _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))
+        _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
+        if not (0 < self.worker_port < 65536 and 0 <= self.master_port < 65536):
+            raise ValueError("ports out of range")
+
+    def as_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+
+def _choice(name: str, value: str, allowed) -> None:
+    if value not in allowed:
+        raise ValueError(f"{name}={value!r} not in {allowed}")
+
+
+def _coerce(f: dataclasses.Field, v: Any) -> Any:
+    t = f.type if isinstance(f.type, str) else getattr(f.type, "__name__", str(f.type))
+    if isinstance(v, str):
+        if t == "bool":
+            low = v.strip().lower()
+            if low in ("1", "t", "true", "yes", "on"):
+                return True
+            if low in ("0", "f", "false", "no", "off", ""):
+                return False
+            raise ValueError(f"bad boolean for {f.name}: {v!r}")
+        if t == "int":
+            return int(v, 0)
+        if t == "float":
+            return float(v)
+    if t == "int" and isinstance(v, bool):
+        raise ValueError(f"bad int for {f.name}: {v!r}")
+    if t == "int":
+        return int(v)
+    if t == "float":
+        return float(v)
+    return v

@@ -1,0 +1,136 @@
+"""Per-operation span trees with monotonic timings, mirrored to rocprofiler roctx ranges.
+
+The reference has no tracing — only Info log lines per step (e.g. reference:
+pkg/server/gpu-mount/server.go:81). Every attach/detach here produces a tree
+``attach → {ledger_reserve, placeholder_wait, ledger_read, cgroup_rule, devnodes, verify}``
+whose durations are returned to the caller (JSON API), exported as Prometheus histograms, and —
+when ``librocprofiler-sdk-roctx`` is present — emitted as roctx push/pop ranges so
+``rocprofv3 --marker-trace`` timelines show controller stages next to tenant GPU kernels.
+"""
+from __future__ import annotations
+
+import contextvars
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+_current: contextvars.ContextVar[Optional["Span"]] = contextvars.ContextVar("gm_span", default=None)
+
+_roctx_lock = threading.Lock()
+_roctx = None  # resolved lazily: native host lib or False
+_sinks: List[Callable[["Span"], None]] = []
+
+
+def _roctx_lib():
+    global _roctx
+    if _roctx is None:
+        with _roctx_lock:
+            if _roctx is None:
+                try:
+                    from gpumounter_amd import _native
+
+                    lib = _native.host()
+                    _roctx = lib if lib.gm_roctx_available() else False
+                except Exception:  # noqa: BLE001 - tracing must never break the data path
+                    _roctx = False
+    return _roctx or None
+
+
+def set_roctx_enabled(enabled: bool) -> None:
+    global _roctx
+    with _roctx_lock:
+        _roctx = None if enabled else False
+
+
+def add_sink(fn: Callable[["Span"], None]) -> None:
+    """Register a callback invoked with every finished *root* span."""
+    _sinks.append(fn)
+
+
+@dataclass
+class Span:
+    name: str
+    start_ns: int = 0
+    end_ns: int = 0
+    attrs: Dict[str, object] = field(default_factory=dict)
+    children: List["Span"] = field(default_factory=list)
+    parent: Optional["Span"] = None
+    error: Optional[str] = None
+
+    @property
+    def duration_ms(self) -> float:
+        end = self.end_ns or time.perf_counter_ns()
+        return (end - self.start_ns) / 1e6
+
+    def to_dict(self) -> dict:
+        d = {"name": self.name, "ms": round(self.duration_ms, 4)}
+        if self.attrs:
+            d["attrs"] = dict(self.attrs)
+        if self.error:
+            d["error"] = self.error
+        if self.children:
+            d["children"] = [c.to_dict() for c in self.children]
+        return d
+
+    def flat(self, prefix: str = "") -> Dict[str, float]:
+        """Stage name → total ms (children summed by name)."""
+        out: Dict[str, float] = {}
+        for c in self.children:
+            key = prefix + c.name
+            out[key] = out.get(key, 0.0) + c.duration_ms
+            for k, v in c.flat(prefix=key + ".").items():
+                out[k] = out.get(k, 0.0) + v
+        return out
+
+
+class span:
+    """``with span("cgroup_rule", gpu=3): ...`` — nests under the current span (ContextVar)."""
+
+    __slots__ = ("s", "_tok", "_lib")
+
+    def __init__(self, name: str, **attrs):
+        self.s = Span(name=name, attrs=attrs)
+
+    def __enter__(self) -> Span:
+        parent = _current.get()
+        self.s.parent = parent
+        if parent is not None:
+            parent.children.append(self.s)
+        self._tok = _current.set(self.s)
+        self._lib = _roctx_lib()
+        if self._lib is not None:
+            self._lib.gm_roctx_push(f"gm:{self.s.name}".encode())
+        self.s.start_ns = time.perf_counter_ns()
+        return self.s
+
+    def __exit__(self, et, ev, tb):
+        self.s.end_ns = time.perf_counter_ns()
+        if ev is not None:
+            self.s.error = f"{et.__name__}: {ev}"
+        if self._lib is not None:
+            self._lib.gm_roctx_pop()
+        _current.reset(self._tok)
+        if self.s.parent is None:
+            for fn in list(_sinks):
+                try:
+                    fn(self.s)
+                except Exception:  # noqa: BLE001
+                    pass
+        return False
+
+
+def current() -> Optional[Span]:
+    return _current.get()
+
+
+def annotate(**attrs) -> None:
+    s = _current.get()
+    if s is not None:
+        s.attrs.update(attrs)
+
+
+def mark(name: str) -> None:
+    lib = _roctx_lib()
+    if lib is not None:
+        lib.gm_roctx_mark(name.encode())

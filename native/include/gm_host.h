@@ -1,0 +1,116 @@
+// gm_host.h — privileged host operations of the gpumounter-amd node agent, as a flat C ABI.
+//
+// Replaces the reference's fork/exec shell pipeline (reference: pkg/util/cgroup/cgroup.go:143-169
+// `sh -c "echo 'c 195:N rw' > devices.allow"`, pkg/util/namespace/namespace.go:167-201
+// `nsenter --mount sh -c "mknod|rm|kill"`) with in-process syscalls:
+//   * cgroup v1: one write(2) per rule into devices.allow / devices.deny
+//   * cgroup v2: a BPF_PROG_TYPE_CGROUP_DEVICE allow-list generated here, loaded with bpf(2) and
+//     swapped in atomically (BPF_F_REPLACE); the container runtime's own program is preserved by
+//     tail-calling into it from ours, so its rules never need to be reverse-engineered
+//   * device nodes: mknodat/unlinkat through /proc/<pid>/root of the target container (or a
+//     setns(CLONE_NEWNS) helper thread) — no mknod binary in the tenant image (reference FAQ.md:3-4)
+//   * processes: pidfd_send_signal (no PID-reuse race), /proc/*/fd scan for device users
+//   * roctx range markers around attach/detach for rocprofv3 --marker-trace timelines
+// All functions return 0 / a count on success and -errno on failure unless stated otherwise.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GM_HOST_ABI_VERSION 1
+
+// Access bits follow BPF_DEVCG_ACC_* so the same rule feeds both cgroup versions.
+#define GM_ACC_MKNOD 1
+#define GM_ACC_READ 2
+#define GM_ACC_WRITE 4
+
+typedef struct gm_dev_rule {
+  char type;        // 'c' char, 'b' block, 'a' all
+  uint8_t access;   // GM_ACC_* bitmask
+  uint8_t allow;    // 1 allow, 0 deny
+  uint8_t pad;
+  int32_t major;    // -1 = wildcard
+  int32_t minor;    // -1 = wildcard
+} gm_dev_rule_t;
+
+// ---- cgroup v1 ------------------------------------------------------------------------------
+// Writes each rule ("c 226:128 rw") to <cgdir>/devices.allow (rule.allow=1) or devices.deny.
+// Returns number of rules written or -errno of the first failure.
+int gm_cg1_apply(const char* cgdir, const gm_dev_rule_t* rules, int n);
+// Formats a rule the way the v1 devices controller expects it; returns length.
+int gm_cg1_format_rule(const gm_dev_rule_t* rule, char* out, int cap);
+
+// ---- cgroup v2 (device eBPF) ----------------------------------------------------------------
+// Encodes the allow-list program into `out` (each entry one struct bpf_insn as uint64).
+// First matching rule wins. After the rules: if chain_map_fd >= 0 the program tail-calls slot 0
+// of that BPF_MAP_TYPE_PROG_ARRAY (the runtime's original program); if the tail call fails or no
+// map is given, it returns `default_allow`. chain_map_fd == -2 emits the tail-call sequence with a
+// placeholder fd (for offline inspection / interpretation in tests).
+// Returns instruction count, or -(needed) if cap is too small, or -EINVAL.
+int gm_bpf_dev_build(const gm_dev_rule_t* rules, int n, int default_allow, int chain_map_fd,
+                     uint64_t* out, int cap);
+// Loads instructions as a CGROUP_DEVICE program named `name`. Returns prog fd or -errno;
+// verifier log (if any) is copied to `log`.
+int gm_bpf_dev_load(const uint64_t* insns, int n, const char* name, char* log, int logcap);
+// Lists program ids attached to the cgroup-v2 directory for BPF_CGROUP_DEVICE.
+int gm_bpf_dev_query(const char* cgroup_path, uint32_t* ids, uint32_t cap, uint32_t* n,
+                     uint32_t* attach_flags);
+// Name of a loaded program (by id). Returns 0 or -errno.
+int gm_bpf_prog_name(uint32_t id, char* name, int cap);
+// Installs (or updates) the gpumounter allow-list on a cgroup-v2 directory:
+//   * our program already attached → replaced, chaining to the same original program;
+//   * one foreign program attached → ours replaces it and tail-calls into it;
+//   * nothing attached → ours is attached with default-allow (deny rules only matter then).
+// On success *prog_id is our new program id and *chained_id the preserved original (0 if none).
+int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
+                       uint32_t* prog_id, uint32_t* chained_id);
+// Removes our program, re-attaching the chained original in its place (if any).
+int gm_bpf_dev_restore(const char* cgroup_path);
+
+// ---- device nodes ---------------------------------------------------------------------------
+typedef struct gm_dev_node {
+  char path[112];   // path inside the container root, e.g. "dev/dri/renderD128"
+  uint32_t major;
+  uint32_t minor;
+  uint32_t mode;    // permission bits, e.g. 0666
+  int32_t uid;      // -1 = leave
+  int32_t gid;      // -1 = leave
+} gm_dev_node_t;
+
+#define GM_DEV_EMULATE 1    // mknod EPERM → regular marker file "gm-chr MAJ:MIN" (unprivileged tests)
+#define GM_DEV_VIA_SETNS 2  // enter the mount namespace with a helper thread instead of /proc/pid/root
+#define GM_DEV_REPLACE 4    // replace an existing node with different major:minor
+
+// Creates nodes inside the target's root: `root` if non-NULL (test prefix), else /proc/<pid>/root.
+// results[i] = 0 created, 1 already present (idempotent), or -errno. Returns #failures.
+int gm_devnodes_create(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
+                       int* results);
+// Removes nodes (only if they are the expected device). results[i] = 0 removed, 1 absent, -errno.
+int gm_devnodes_remove(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
+                       int* results);
+// Describes a node: *kind = 0 absent, 1 char device, 2 emulated marker, 3 other file.
+int gm_devnode_stat(int pid, const char* root, const char* path, int flags, int* kind,
+                    uint32_t* major, uint32_t* minor, uint32_t* mode);
+
+// ---- processes ------------------------------------------------------------------------------
+// Sends `sig` to each pid via pidfd (falls back to kill(2)). results[i] = 0 or -errno.
+int gm_proc_signal(const int32_t* pids, int n, int sig, int* results);
+// PIDs with an open fd on char device major:minor (scans /proc/*/fd). *n = total found.
+int gm_proc_dev_users(uint32_t major, uint32_t minor, int32_t* pids, int cap, int* n);
+// Parses a cgroup.procs-style file. *n = total.
+int gm_proc_read_pids(const char* path, int32_t* pids, int cap, int* n);
+
+// ---- tracing --------------------------------------------------------------------------------
+int gm_roctx_available(void);
+void gm_roctx_push(const char* name);
+void gm_roctx_pop(void);
+void gm_roctx_mark(const char* name);
+uint64_t gm_now_ns(void);
+
+int gm_host_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,827 @@
+// gm_host.cpp — in-process implementation of the node agent's privileged operations.
+// See gm_host.h for the contract; reference parity notes are inline.
+#include "gm_host.h"
+
+#include <dirent.h>
+#include <dlfcn.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <linux/bpf.h>
+#include <sched.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <sys/sysmacros.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+constexpr const char* kProgName = "gm_devallow";
+
+// ------------------------------------------------------------------ small fd helpers
+struct Fd {
+  int fd = -1;
+  Fd() = default;
+  explicit Fd(int f) : fd(f) {}
+  Fd(const Fd&) = delete;
+  Fd& operator=(const Fd&) = delete;
+  Fd(Fd&& o) noexcept : fd(o.fd) { o.fd = -1; }
+  Fd& operator=(Fd&& o) noexcept {
+    if (this != &o) {
+      reset();
+      fd = o.fd;
+      o.fd = -1;
+    }
+    return *this;
+  }
+  ~Fd() { reset(); }
+  void reset() {
+    if (fd >= 0) close(fd);
+    fd = -1;
+  }
+  bool ok() const { return fd >= 0; }
+};
+
+int write_all(int fd, const char* buf, size_t len) {
+  while (len > 0) {
+    ssize_t w = write(fd, buf, len);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return -errno;
+    }
+    buf += w;
+    len -= (size_t)w;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ bpf(2)
+long sys_bpf(int cmd, union bpf_attr* attr, unsigned size) {
+  return syscall(__NR_bpf, cmd, attr, size);
+}
+
+inline uint64_t ptr_u64(const void* p) { return (uint64_t)(uintptr_t)p; }
+
+// struct bpf_insn packed into a uint64 in host (little-endian) order.
+uint64_t insn(uint8_t code, uint8_t dst, uint8_t src, int16_t off, int32_t imm) {
+  struct bpf_insn i;
+  memset(&i, 0, sizeof(i));
+  i.code = code;
+  i.dst_reg = dst & 0xf;
+  i.src_reg = src & 0xf;
+  i.off = off;
+  i.imm = imm;
+  uint64_t v;
+  static_assert(sizeof(i) == sizeof(v), "bpf_insn is 8 bytes");
+  memcpy(&v, &i, sizeof(v));
+  return v;
+}
+
+// Opcodes used by the device filter.
+constexpr uint8_t LDX_W = BPF_LDX | BPF_MEM | BPF_W;
+constexpr uint8_t MOV64_X = BPF_ALU64 | BPF_MOV | BPF_X;
+constexpr uint8_t MOV64_K = BPF_ALU64 | BPF_MOV | BPF_K;
+constexpr uint8_t AND64_K = BPF_ALU64 | BPF_AND | BPF_K;
+constexpr uint8_t RSH64_K = BPF_ALU64 | BPF_RSH | BPF_K;
+constexpr uint8_t JNE_K = BPF_JMP | BPF_JNE | BPF_K;
+constexpr uint8_t CALL = BPF_JMP | BPF_CALL;
+constexpr uint8_t EXIT = BPF_JMP | BPF_EXIT;
+constexpr uint8_t LD_IMM64 = BPF_LD | BPF_DW | BPF_IMM;
+
+int rule_block_len(const gm_dev_rule_t& r) {
+  int n = 2;  // mov r0, allow; exit
+  if (r.type != 'a') n += 1;
+  if ((r.access & 7) != 7) n += 3;  // mov r0,r2; and r0,~acc; jne r0,0
+  if (r.major >= 0) n += 1;
+  if (r.minor >= 0) n += 1;
+  return n;
+}
+
+int get_prog_fd_by_id(uint32_t id) {
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.prog_id = id;
+  long fd = sys_bpf(BPF_PROG_GET_FD_BY_ID, &a, sizeof(a));
+  return fd < 0 ? -errno : (int)fd;
+}
+
+int prog_info(int fd, struct bpf_prog_info* info, uint32_t* map_ids, uint32_t map_cap) {
+  memset(info, 0, sizeof(*info));
+  info->nr_map_ids = map_cap;
+  info->map_ids = ptr_u64(map_ids);
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.info.bpf_fd = (uint32_t)fd;
+  a.info.info_len = sizeof(*info);
+  a.info.info = ptr_u64(info);
+  return sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a, sizeof(a)) < 0 ? -errno : 0;
+}
+
+int map_fd_by_id(uint32_t id) {
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.map_id = id;
+  long fd = sys_bpf(BPF_MAP_GET_FD_BY_ID, &a, sizeof(a));
+  return fd < 0 ? -errno : (int)fd;
+}
+
+// Prog id stored in slot 0 of a PROG_ARRAY (user-space lookups return ids, not fds).
+int prog_array_slot0(int map_fd, uint32_t* prog_id) {
+  uint32_t key = 0, val = 0;
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.map_fd = (uint32_t)map_fd;
+  a.key = ptr_u64(&key);
+  a.value = ptr_u64(&val);
+  if (sys_bpf(BPF_MAP_LOOKUP_ELEM, &a, sizeof(a)) < 0) return -errno;
+  *prog_id = val;
+  return 0;
+}
+
+int make_chain_map(int target_prog_fd) {
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.map_type = BPF_MAP_TYPE_PROG_ARRAY;
+  a.key_size = 4;
+  a.value_size = 4;
+  a.max_entries = 1;
+  snprintf(a.map_name, sizeof(a.map_name), "gm_devchain");
+  long mfd = sys_bpf(BPF_MAP_CREATE, &a, sizeof(a));
+  if (mfd < 0) return -errno;
+  uint32_t key = 0, val = (uint32_t)target_prog_fd;
+  memset(&a, 0, sizeof(a));
+  a.map_fd = (uint32_t)mfd;
+  a.key = ptr_u64(&key);
+  a.value = ptr_u64(&val);
+  a.flags = BPF_ANY;
+  if (sys_bpf(BPF_MAP_UPDATE_ELEM, &a, sizeof(a)) < 0) {
+    int e = -errno;
+    close((int)mfd);
+    return e;
+  }
+  return (int)mfd;
+}
+
+struct Attached {
+  std::vector<uint32_t> ids;
+  uint32_t flags = 0;
+};
+
+int query(int cgfd, Attached* out) {
+  uint32_t ids[64];
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.query.target_fd = (uint32_t)cgfd;
+  a.query.attach_type = BPF_CGROUP_DEVICE;
+  a.query.prog_ids = ptr_u64(ids);
+  a.query.prog_cnt = 64;
+  if (sys_bpf(BPF_PROG_QUERY, &a, sizeof(a)) < 0) return -errno;
+  out->flags = a.query.attach_flags;
+  out->ids.assign(ids, ids + (a.query.prog_cnt < 64 ? a.query.prog_cnt : 64));
+  return 0;
+}
+
+int attach(int cgfd, int prog_fd, int replace_fd, uint32_t existing_flags) {
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.target_fd = (uint32_t)cgfd;
+  a.attach_bpf_fd = (uint32_t)prog_fd;
+  a.attach_type = BPF_CGROUP_DEVICE;
+  if (existing_flags & BPF_F_ALLOW_MULTI) {
+    a.attach_flags = BPF_F_ALLOW_MULTI;
+    if (replace_fd >= 0) {
+      a.attach_flags |= BPF_F_REPLACE;
+      a.replace_bpf_fd = (uint32_t)replace_fd;
+    }
+  } else {
+    // Single-program mode (flags 0 / ALLOW_OVERRIDE): attaching again replaces the program.
+    a.attach_flags = existing_flags & BPF_F_ALLOW_OVERRIDE;
+  }
+  return sys_bpf(BPF_PROG_ATTACH, &a, sizeof(a)) < 0 ? -errno : 0;
+}
+
+bool is_ours(uint32_t id, uint32_t* chained_id) {
+  Fd pfd(get_prog_fd_by_id(id));
+  if (!pfd.ok()) return false;
+  struct bpf_prog_info info;
+  uint32_t maps[4] = {0};
+  if (prog_info(pfd.fd, &info, maps, 4) != 0) return false;
+  if (strncmp(info.name, kProgName, sizeof(info.name)) != 0) return false;
+  if (chained_id) {
+    *chained_id = 0;
+    if (info.nr_map_ids >= 1) {
+      Fd mfd(map_fd_by_id(maps[0]));
+      uint32_t pid = 0;
+      if (mfd.ok() && prog_array_slot0(mfd.fd, &pid) == 0) *chained_id = pid;
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ device nodes
+constexpr const char* kMarker = "gm-chr";
+
+int open_root(int pid, const char* root) {
+  if (root && *root) {
+    int fd = open(root, O_PATH | O_DIRECTORY | O_CLOEXEC);
+    return fd < 0 ? -errno : fd;
+  }
+  char p[64];
+  snprintf(p, sizeof(p), "/proc/%d/root", pid);
+  int fd = open(p, O_PATH | O_DIRECTORY | O_CLOEXEC);
+  return fd < 0 ? -errno : fd;
+}
+
+// Walks `path` (relative, '/'-separated) below rootfd without following symlinks, creating
+// missing directories when `create`. Returns the parent dir fd and the leaf name.
+int walk_parent(int rootfd, const char* path, bool create, Fd* parent, std::string* leaf) {
+  std::string p(path);
+  while (!p.empty() && p[0] == '/') p.erase(0, 1);
+  std::vector<std::string> comps;
+  size_t start = 0;
+  while (start <= p.size()) {
+    size_t e = p.find('/', start);
+    if (e == std::string::npos) e = p.size();
+    std::string c = p.substr(start, e - start);
+    if (!c.empty() && c != ".") {
+      if (c == "..") return -EINVAL;  // never climb out of the container root
+      comps.push_back(c);
+    }
+    start = e + 1;
+  }
+  if (comps.empty()) return -EINVAL;
+  int cur = dup(rootfd);
+  if (cur < 0) return -errno;
+  Fd curfd(cur);
+  for (size_t i = 0; i + 1 < comps.size(); ++i) {
+    int nfd = openat(curfd.fd, comps[i].c_str(), O_PATH | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
+    if (nfd < 0 && errno == ENOENT && create) {
+      if (mkdirat(curfd.fd, comps[i].c_str(), 0755) < 0 && errno != EEXIST) return -errno;
+      nfd = openat(curfd.fd, comps[i].c_str(), O_PATH | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
+    }
+    if (nfd < 0) return -errno;
+    curfd = Fd(nfd);
+  }
+  *leaf = comps.back();
+  *parent = std::move(curfd);
+  return 0;
+}
+
+// kind: 0 absent, 1 char dev, 2 emulated marker, 3 other.
+int stat_leaf(int dirfd, const std::string& leaf, int* kind, uint32_t* maj, uint32_t* min,
+              uint32_t* mode) {
+  struct stat st;
+  *kind = 0;
+  *maj = *min = *mode = 0;
+  if (fstatat(dirfd, leaf.c_str(), &st, AT_SYMLINK_NOFOLLOW) < 0) {
+    if (errno == ENOENT) return 0;
+    return -errno;
+  }
+  *mode = st.st_mode & 07777;
+  if (S_ISCHR(st.st_mode)) {
+    *kind = 1;
+    *maj = major(st.st_rdev);
+    *min = minor(st.st_rdev);
+    return 0;
+  }
+  *kind = 3;
+  if (S_ISREG(st.st_mode) && st.st_size < 64) {
+    int fd = openat(dirfd, leaf.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+    if (fd >= 0) {
+      char buf[64] = {0};
+      ssize_t r = read(fd, buf, sizeof(buf) - 1);
+      close(fd);
+      unsigned a = 0, b = 0;
+      char tag[16] = {0};
+      if (r > 0 && sscanf(buf, "%15s %u:%u", tag, &a, &b) == 3 && strcmp(tag, kMarker) == 0) {
+        *kind = 2;
+        *maj = a;
+        *min = b;
+      }
+    }
+  }
+  return 0;
+}
+
+int create_one(int rootfd, const gm_dev_node_t& n, int flags) {
+  Fd parent;
+  std::string leaf;
+  int e = walk_parent(rootfd, n.path, true, &parent, &leaf);
+  if (e < 0) return e;
+  int kind;
+  uint32_t maj, min, mode;
+  e = stat_leaf(parent.fd, leaf, &kind, &maj, &min, &mode);
+  if (e < 0) return e;
+  if (kind == 1 || kind == 2) {
+    if (maj == n.major && min == n.minor) {
+      if (kind == 1 && mode != (n.mode & 07777))
+        if (fchmodat(parent.fd, leaf.c_str(), n.mode & 07777, 0) < 0) return -errno;
+      return 1;  // idempotent re-attach
+    }
+    if (!(flags & GM_DEV_REPLACE)) return -EEXIST;
+    if (unlinkat(parent.fd, leaf.c_str(), 0) < 0) return -errno;
+  } else if (kind == 3) {
+    return -EEXIST;  // refuse to clobber an unrelated file
+  }
+  if (mknodat(parent.fd, leaf.c_str(), S_IFCHR | (n.mode & 07777), makedev(n.major, n.minor)) <
+      0) {
+    int err = errno;
+    if (!(err == EPERM && (flags & GM_DEV_EMULATE))) return -err;
+    int fd = openat(parent.fd, leaf.c_str(), O_CREAT | O_EXCL | O_WRONLY | O_NOFOLLOW | O_CLOEXEC,
+                    n.mode & 07777);
+    if (fd < 0) return -errno;
+    char buf[48];
+    int len = snprintf(buf, sizeof(buf), "%s %u:%u\n", kMarker, n.major, n.minor);
+    int w = write_all(fd, buf, (size_t)len);
+    close(fd);
+    if (w < 0) return w;
+  }
+  // mknod honours the umask; set the exact mode the tenant needs (reference used -m 666,
+  // namespace.go:168).
+  if (fchmodat(parent.fd, leaf.c_str(), n.mode & 07777, 0) < 0) return -errno;
+  if (n.uid >= 0 || n.gid >= 0) {
+    if (fchownat(parent.fd, leaf.c_str(), (uid_t)n.uid, (gid_t)n.gid, AT_SYMLINK_NOFOLLOW) < 0 &&
+        errno != EPERM)
+      return -errno;
+  }
+  return 0;
+}
+
+int remove_one(int rootfd, const gm_dev_node_t& n) {
+  Fd parent;
+  std::string leaf;
+  int e = walk_parent(rootfd, n.path, false, &parent, &leaf);
+  if (e == -ENOENT) return 1;
+  if (e < 0) return e;
+  int kind;
+  uint32_t maj, min, mode;
+  e = stat_leaf(parent.fd, leaf, &kind, &maj, &min, &mode);
+  if (e < 0) return e;
+  if (kind == 0) return 1;
+  if ((kind == 1 || kind == 2) && maj == n.major && min == n.minor) {
+    if (unlinkat(parent.fd, leaf.c_str(), 0) < 0) return -errno;
+    return 0;
+  }
+  return -EEXIST;  // something else lives there: never delete it
+}
+
+// Runs fn(rootfd) either through /proc/<pid>/root (or a test root) or, with GM_DEV_VIA_SETNS,
+// on a helper thread that privatises its fs context and joins the target's mount namespace
+// (setns(CLONE_NEWNS) is refused for threads that share CLONE_FS, hence unshare first).
+template <typename F>
+int with_root(int pid, const char* root, int flags, F fn) {
+  if (!(flags & GM_DEV_VIA_SETNS) || (root && *root)) {
+    int rfd = open_root(pid, root);
+    if (rfd < 0) return rfd;
+    Fd r(rfd);
+    return fn(r.fd);
+  }
+  int result = 0;
+  std::thread t([&]() {
+    if (unshare(CLONE_FS) < 0) {
+      result = -errno;
+      return;
+    }
+    char p[64];
+    snprintf(p, sizeof(p), "/proc/%d/ns/mnt", pid);
+    Fd ns(open(p, O_RDONLY | O_CLOEXEC));
+    if (!ns.ok()) {
+      result = -errno;
+      return;
+    }
+    if (setns(ns.fd, CLONE_NEWNS) < 0) {
+      result = -errno;
+      return;
+    }
+    Fd r(open("/", O_PATH | O_DIRECTORY | O_CLOEXEC));
+    if (!r.ok()) {
+      result = -errno;
+      return;
+    }
+    result = fn(r.fd);
+  });
+  t.join();
+  return result;
+}
+
+// ------------------------------------------------------------------ roctx
+struct Roctx {
+  std::once_flag once;
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  void (*mark)(const char*) = nullptr;
+};
+Roctx g_roctx;
+
+void roctx_init() {
+  std::call_once(g_roctx.once, []() {
+    const char* env = getenv("GM_ROCTX");
+    if (env && strcmp(env, "0") == 0) return;
+    const char* libs[] = {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                          "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"};
+    void* dl = nullptr;
+    for (const char* l : libs) {
+      dl = dlopen(l, RTLD_NOW | RTLD_GLOBAL);
+      if (dl) break;
+    }
+    if (!dl) return;
+    g_roctx.push = reinterpret_cast<int (*)(const char*)>(dlsym(dl, "roctxRangePushA"));
+    g_roctx.pop = reinterpret_cast<int (*)()>(dlsym(dl, "roctxRangePop"));
+    g_roctx.mark = reinterpret_cast<void (*)(const char*)>(dlsym(dl, "roctxMarkA"));
+  });
+}
+
+}  // namespace
+
+extern "C" {
+
+int gm_host_abi_version(void) { return GM_HOST_ABI_VERSION; }
+
+// ------------------------------------------------------------------ cgroup v1
+int gm_cg1_format_rule(const gm_dev_rule_t* r, char* out, int cap) {
+  char acc[4] = {0};
+  int k = 0;
+  if (r->access & GM_ACC_READ) acc[k++] = 'r';
+  if (r->access & GM_ACC_WRITE) acc[k++] = 'w';
+  if (r->access & GM_ACC_MKNOD) acc[k++] = 'm';
+  char maj[16], min[16];
+  if (r->major < 0) snprintf(maj, sizeof(maj), "*");
+  else snprintf(maj, sizeof(maj), "%d", r->major);
+  if (r->minor < 0) snprintf(min, sizeof(min), "*");
+  else snprintf(min, sizeof(min), "%d", r->minor);
+  if (r->type == 'a') return snprintf(out, (size_t)cap, "a");
+  return snprintf(out, (size_t)cap, "%c %s:%s %s", r->type, maj, min, acc);
+}
+
+int gm_cg1_apply(const char* cgdir, const gm_dev_rule_t* rules, int n) {
+  // One open per target file, one write(2) per rule: the kernel parses exactly one rule per write.
+  Fd allow_fd, deny_fd;
+  std::string base(cgdir);
+  for (int i = 0; i < n; ++i) {
+    Fd& f = rules[i].allow ? allow_fd : deny_fd;
+    if (!f.ok()) {
+      std::string p = base + (rules[i].allow ? "/devices.allow" : "/devices.deny");
+      int fd = open(p.c_str(), O_WRONLY | O_APPEND | O_CLOEXEC);
+      if (fd < 0) return -errno;
+      f = Fd(fd);
+    }
+    char line[64];
+    int len = gm_cg1_format_rule(&rules[i], line, sizeof(line) - 1);
+    line[len++] = '\n';
+    int e = write_all(f.fd, line, (size_t)len);
+    if (e < 0) return e;
+  }
+  return n;
+}
+
+// ------------------------------------------------------------------ cgroup v2 eBPF
+int gm_bpf_dev_build(const gm_dev_rule_t* rules, int n, int default_allow, int chain_map_fd,
+                     uint64_t* out, int cap) {
+  if (n < 0 || (n > 0 && !rules)) return -EINVAL;
+  int need = 6;  // prologue
+  for (int i = 0; i < n; ++i) {
+    if (rules[i].type != 'a' && rules[i].type != 'c' && rules[i].type != 'b') return -EINVAL;
+    need += rule_block_len(rules[i]);
+  }
+  if (chain_map_fd != -1) need += 4;  // ld_imm64 (2) + mov r3 + call
+  need += 2;                          // default: mov r0 + exit
+  if (!out || cap < need) return -need;
+
+  int k = 0;
+  // r2 = access_type; r3 = r2 & 0xffff (dev type); r2 >>= 16 (access); r4 = major; r5 = minor
+  out[k++] = insn(LDX_W, 2, 1, 0, 0);
+  out[k++] = insn(MOV64_X, 3, 2, 0, 0);
+  out[k++] = insn(AND64_K, 3, 0, 0, 0xffff);
+  out[k++] = insn(RSH64_K, 2, 0, 0, 16);
+  out[k++] = insn(LDX_W, 4, 1, 4, 0);
+  out[k++] = insn(LDX_W, 5, 1, 8, 0);
+
+  for (int i = 0; i < n; ++i) {
+    const gm_dev_rule_t& r = rules[i];
+    const int start = k;
+    const int end = start + rule_block_len(r);  // index of first insn after this block
+    auto jne = [&](int reg, int32_t imm) {
+      int16_t off = (int16_t)(end - (k + 1));
+      out[k] = insn(JNE_K, (uint8_t)reg, 0, off, imm);
+      ++k;
+    };
+    if (r.type != 'a') jne(3, r.type == 'c' ? BPF_DEVCG_DEV_CHAR : BPF_DEVCG_DEV_BLOCK);
+    if ((r.access & 7) != 7) {
+      // requested access must be a subset of the rule's: (req & ~rule) == 0
+      out[k++] = insn(MOV64_X, 0, 2, 0, 0);
+      out[k++] = insn(AND64_K, 0, 0, 0, (int32_t)(~r.access & 7));
+      // jne r0, 0 → next rule
+      int16_t off = (int16_t)(end - (k + 1));
+      out[k] = insn(JNE_K, 0, 0, off, 0);
+      ++k;
+    }
+    if (r.major >= 0) jne(4, r.major);
+    if (r.minor >= 0) jne(5, r.minor);
+    out[k++] = insn(MOV64_K, 0, 0, 0, r.allow ? 1 : 0);
+    out[k++] = insn(EXIT, 0, 0, 0, 0);
+    if (k != end) return -EINVAL;  // layout bug guard (see rule_block_len)
+  }
+  if (chain_map_fd != -1) {
+    // r1 still holds ctx. r2 = &prog_array (pseudo map fd), r3 = 0, call bpf_tail_call.
+    const int32_t mfd = chain_map_fd >= 0 ? chain_map_fd : 0;
+    out[k++] = insn(LD_IMM64, 2, BPF_PSEUDO_MAP_FD, 0, mfd);
+    out[k++] = insn(0, 0, 0, 0, 0);
+    out[k++] = insn(MOV64_K, 3, 0, 0, 0);
+    out[k++] = insn(CALL, 0, 0, 0, BPF_FUNC_tail_call);
+  }
+  out[k++] = insn(MOV64_K, 0, 0, 0, default_allow ? 1 : 0);
+  out[k++] = insn(EXIT, 0, 0, 0, 0);
+  return k;
+}
+
+int gm_bpf_dev_load(const uint64_t* insns, int n, const char* name, char* log, int logcap) {
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.prog_type = BPF_PROG_TYPE_CGROUP_DEVICE;
+  a.expected_attach_type = BPF_CGROUP_DEVICE;
+  a.insns = ptr_u64(insns);
+  a.insn_cnt = (uint32_t)n;
+  a.license = ptr_u64("Apache-2.0");
+  snprintf(a.prog_name, sizeof(a.prog_name), "%s", name && *name ? name : kProgName);
+  if (log && logcap > 0) {
+    log[0] = 0;
+    a.log_buf = ptr_u64(log);
+    a.log_size = (uint32_t)logcap;
+    a.log_level = 1;
+  }
+  long fd = sys_bpf(BPF_PROG_LOAD, &a, sizeof(a));
+  if (fd < 0 && log && logcap > 0 && errno != EINVAL && errno != EACCES) {
+    // retry without a log buffer (some kernels reject small logs with ENOSPC)
+    a.log_buf = 0;
+    a.log_size = 0;
+    a.log_level = 0;
+    fd = sys_bpf(BPF_PROG_LOAD, &a, sizeof(a));
+  }
+  return fd < 0 ? -errno : (int)fd;
+}
+
+int gm_bpf_dev_query(const char* cgroup_path, uint32_t* ids, uint32_t cap, uint32_t* n,
+                     uint32_t* attach_flags) {
+  Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
+  if (!cg.ok()) return -errno;
+  Attached at;
+  int e = query(cg.fd, &at);
+  if (e < 0) return e;
+  *n = (uint32_t)at.ids.size();
+  if (attach_flags) *attach_flags = at.flags;
+  for (uint32_t i = 0; i < at.ids.size() && i < cap; ++i) ids[i] = at.ids[i];
+  return 0;
+}
+
+int gm_bpf_prog_name(uint32_t id, char* name, int cap) {
+  Fd pfd(get_prog_fd_by_id(id));
+  if (!pfd.ok()) return pfd.fd;
+  struct bpf_prog_info info;
+  uint32_t maps[1];
+  int e = prog_info(pfd.fd, &info, maps, 0);
+  if (e < 0) return e;
+  snprintf(name, (size_t)cap, "%.*s", (int)sizeof(info.name), info.name);
+  return 0;
+}
+
+int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
+                       uint32_t* prog_id, uint32_t* chained_id) {
+  Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
+  if (!cg.ok()) return -errno;
+  Attached at;
+  int e = query(cg.fd, &at);
+  if (e < 0) return e;
+
+  uint32_t replace_id = 0, chain_id = 0;
+  int foreign = 0;
+  for (uint32_t id : at.ids) {
+    uint32_t c = 0;
+    if (is_ours(id, &c)) {
+      replace_id = id;
+      chain_id = c;
+    } else {
+      ++foreign;
+    }
+  }
+  if (!replace_id) {
+    if (foreign > 1) return -EMLINK;  // ALLOW_MULTI stack: every program must allow; refuse
+    if (foreign == 1) {
+      for (uint32_t id : at.ids) chain_id = id;
+      replace_id = chain_id;
+    }
+  }
+
+  Fd chain_prog, chain_map, replace_fd;
+  if (chain_id) {
+    chain_prog = Fd(get_prog_fd_by_id(chain_id));
+    if (!chain_prog.ok()) return chain_prog.fd;
+    chain_map = Fd(make_chain_map(chain_prog.fd));
+    if (!chain_map.ok()) return chain_map.fd;
+  }
+  if (replace_id) {
+    replace_fd = Fd(get_prog_fd_by_id(replace_id));
+    if (!replace_fd.ok()) return replace_fd.fd;
+  }
+  // With a chained original the fall-through is deny (the original already said no);
+  // without one the cgroup was unrestricted, so default-allow keeps that behaviour.
+  const int default_allow = chain_id ? 0 : 1;
+  std::vector<uint64_t> prog(16 + (size_t)n * 8);
+  int cnt = gm_bpf_dev_build(rules, n, default_allow, chain_map.ok() ? chain_map.fd : -1,
+                             prog.data(), (int)prog.size());
+  if (cnt < 0) return -EINVAL;
+  char log[4096];
+  Fd pfd(gm_bpf_dev_load(prog.data(), cnt, kProgName, log, sizeof(log)));
+  if (!pfd.ok()) return pfd.fd;
+  e = attach(cg.fd, pfd.fd, replace_fd.ok() ? replace_fd.fd : -1,
+             at.ids.empty() ? BPF_F_ALLOW_MULTI : at.flags);
+  if (e < 0) return e;
+  if (prog_id) {
+    struct bpf_prog_info info;
+    uint32_t maps[1];
+    *prog_id = prog_info(pfd.fd, &info, maps, 0) == 0 ? info.id : 0;
+  }
+  if (chained_id) *chained_id = chain_id;
+  return 0;
+}
+
+int gm_bpf_dev_restore(const char* cgroup_path) {
+  Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
+  if (!cg.ok()) return -errno;
+  Attached at;
+  int e = query(cg.fd, &at);
+  if (e < 0) return e;
+  for (uint32_t id : at.ids) {
+    uint32_t chain = 0;
+    if (!is_ours(id, &chain)) continue;
+    Fd ours(get_prog_fd_by_id(id));
+    if (!ours.ok()) return ours.fd;
+    if (chain) {
+      Fd orig(get_prog_fd_by_id(chain));
+      if (!orig.ok()) return orig.fd;
+      return attach(cg.fd, orig.fd, ours.fd, at.flags);
+    }
+    union bpf_attr a;
+    memset(&a, 0, sizeof(a));
+    a.target_fd = (uint32_t)cg.fd;
+    a.attach_bpf_fd = (uint32_t)ours.fd;
+    a.attach_type = BPF_CGROUP_DEVICE;
+    return sys_bpf(BPF_PROG_DETACH, &a, sizeof(a)) < 0 ? -errno : 0;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ device nodes
+int gm_devnodes_create(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
+                       int* results) {
+  int failures = 0;
+  int e = with_root(pid, root, flags, [&](int rootfd) {
+    for (int i = 0; i < n; ++i) {
+      results[i] = create_one(rootfd, nodes[i], flags);
+      if (results[i] < 0) ++failures;
+    }
+    return 0;
+  });
+  if (e < 0) {
+    for (int i = 0; i < n; ++i) results[i] = e;
+    return n;
+  }
+  return failures;
+}
+
+int gm_devnodes_remove(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
+                       int* results) {
+  int failures = 0;
+  int e = with_root(pid, root, flags, [&](int rootfd) {
+    for (int i = 0; i < n; ++i) {
+      results[i] = remove_one(rootfd, nodes[i]);
+      if (results[i] < 0) ++failures;
+    }
+    return 0;
+  });
+  if (e < 0) {
+    for (int i = 0; i < n; ++i) results[i] = e;
+    return n;
+  }
+  return failures;
+}
+
+int gm_devnode_stat(int pid, const char* root, const char* path, int flags, int* kind,
+                    uint32_t* maj, uint32_t* min, uint32_t* mode) {
+  return with_root(pid, root, flags, [&](int rootfd) {
+    Fd parent;
+    std::string leaf;
+    int e = walk_parent(rootfd, path, false, &parent, &leaf);
+    if (e == -ENOENT) {
+      *kind = 0;
+      *maj = *min = *mode = 0;
+      return 0;
+    }
+    if (e < 0) return e;
+    return stat_leaf(parent.fd, leaf, kind, maj, min, mode);
+  });
+}
+
+// ------------------------------------------------------------------ processes
+int gm_proc_signal(const int32_t* pids, int n, int sig, int* results) {
+  int failures = 0;
+  for (int i = 0; i < n; ++i) {
+    int r = 0;
+    long pfd = syscall(SYS_pidfd_open, pids[i], 0);
+    if (pfd >= 0) {
+      if (syscall(SYS_pidfd_send_signal, (int)pfd, sig, nullptr, 0) < 0) r = -errno;
+      close((int)pfd);
+    } else if (errno == ENOSYS) {
+      if (kill(pids[i], sig) < 0) r = -errno;
+    } else {
+      r = -errno;
+    }
+    results[i] = r;
+    if (r < 0) ++failures;
+  }
+  return failures;
+}
+
+int gm_proc_dev_users(uint32_t maj, uint32_t min, int32_t* pids, int cap, int* n) {
+  *n = 0;
+  DIR* proc = opendir("/proc");
+  if (!proc) return -errno;
+  const dev_t want = makedev(maj, min);
+  struct dirent* de;
+  while ((de = readdir(proc)) != nullptr) {
+    char* endp = nullptr;
+    long pid = strtol(de->d_name, &endp, 10);
+    if (!endp || *endp != 0 || pid <= 0) continue;
+    char p[64];
+    snprintf(p, sizeof(p), "/proc/%ld/fd", pid);
+    int dfd = open(p, O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+    if (dfd < 0) continue;
+    DIR* fds = fdopendir(dfd);
+    if (!fds) {
+      close(dfd);
+      continue;
+    }
+    struct dirent* fe;
+    bool hit = false;
+    while (!hit && (fe = readdir(fds)) != nullptr) {
+      if (fe->d_name[0] == '.') continue;
+      struct stat st;
+      if (fstatat(dirfd(fds), fe->d_name, &st, 0) == 0 && S_ISCHR(st.st_mode) &&
+          st.st_rdev == want)
+        hit = true;
+    }
+    closedir(fds);
+    if (hit) {
+      if (*n < cap) pids[*n] = (int32_t)pid;
+      ++*n;
+    }
+  }
+  closedir(proc);
+  return 0;
+}
+
+int gm_proc_read_pids(const char* path, int32_t* pids, int cap, int* n) {
+  *n = 0;
+  FILE* f = fopen(path, "re");
+  if (!f) return -errno;
+  long v;
+  while (fscanf(f, "%ld", &v) == 1) {
+    if (*n < cap) pids[*n] = (int32_t)v;
+    ++*n;
+  }
+  fclose(f);
+  return 0;
+}
+
+// ------------------------------------------------------------------ tracing
+int gm_roctx_available(void) {
+  roctx_init();
+  return g_roctx.push != nullptr;
+}
+void gm_roctx_push(const char* name) {
+  roctx_init();
+  if (g_roctx.push) g_roctx.push(name);
+}
+void gm_roctx_pop(void) {
+  roctx_init();
+  if (g_roctx.pop) g_roctx.pop();
+}
+void gm_roctx_mark(const char* name) {
+  roctx_init();
+  if (g_roctx.mark) g_roctx.mark(name);
+}
+uint64_t gm_now_ns(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+}  // extern "C"
