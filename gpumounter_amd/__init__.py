@@ -10,4 +10,9 @@ Layers (bottom → top): ``_native`` (C++/HIP libraries) → ``hw`` (amdsmi inve
 ``master`` (HTTP API). ``ops``/``parallel`` hold the gfx950 validation kernels and the RCCL/xGMI
 post-attach checks; ``fakes`` hold the hermetic apiserver/kubelet/cgroupfs used by tests and bench.
 """
+import os as _os
+
+# grpc core logs GOAWAY/shutdown chatter at INFO unless told otherwise
+_os.environ.setdefault("GRPC_VERBOSITY", "ERROR")
+
 __version__ = "0.1.0"

@@ -1,0 +1,140 @@
+"""List+watch pod cache with awaitable predicates.
+
+Replaces the reference's readiness loops, which call ``Pods.Get`` for every slave pod in a tight
+loop with no sleep and no timeout (reference: pkg/util/gpu/allocator/allocator.go:236-317 —
+SURVEY §2.6 defect 1). One watch stream per selector feeds a cache; callers ``await`` a predicate
+and are woken by the next matching event instead of polling the apiserver.
+"""
+from __future__ import annotations
+
+import asyncio
+import copy
+from typing import Callable, Dict, List, Optional, Tuple
+
+from gpumounter_amd.cluster.kube import ApiError, KubeClient
+from gpumounter_amd.utils import log
+
+_log = log.get("cluster.informer")
+
+Key = Tuple[str, str]
+
+
+class PodInformer:
+    def __init__(self, kube: KubeClient, namespace: Optional[str] = None, label_selector: str = "",
+                 field_selector: str = "", resync_s: float = 300.0) -> None:
+        self.kube = kube
+        self.namespace = namespace
+        self.label_selector = label_selector
+        self.field_selector = field_selector
+        self.resync_s = resync_s
+        self.cache: Dict[Key, dict] = {}
+        self.deleted: Dict[Key, str] = {}  # key → uid of the last deleted instance
+        self._cond: Optional[asyncio.Condition] = None
+        self._task: Optional[asyncio.Task] = None
+        self._synced: Optional[asyncio.Event] = None
+        self.rv = ""
+        self.events = 0
+        self.handlers: List[Callable[[str, dict], None]] = []
+
+    async def start(self) -> None:
+        self._cond = asyncio.Condition()
+        self._synced = asyncio.Event()
+        self._task = asyncio.ensure_future(self._run())
+        await asyncio.wait_for(self._synced.wait(), timeout=30)
+
+    async def stop(self) -> None:
+        if self._task:
+            self._task.cancel()
+            try:
+                await self._task
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                pass
+            self._task = None
+
+    async def _relist(self) -> None:
+        items, rv = await self.kube.list_pods(self.namespace, self.label_selector,
+                                              self.field_selector)
+        fresh = {(p["metadata"]["namespace"], p["metadata"]["name"]): p for p in items}
+        for k in set(self.cache) - set(fresh):
+            self.deleted[k] = self.cache[k]["metadata"].get("uid", "")
+        self.cache = fresh
+        self.rv = rv
+        await self._notify("RELIST", {})
+
+    async def _notify(self, etype: str, pod: dict) -> None:
+        for h in list(self.handlers):
+            try:
+                h(etype, pod)
+            except Exception:  # noqa: BLE001
+                _log.exception("informer handler failed")
+        async with self._cond:
+            self._cond.notify_all()
+
+    async def _run(self) -> None:
+        backoff = 0.05
+        while True:
+            try:
+                await self._relist()
+                self._synced.set()
+                async for etype, pod in self.kube.watch_pods(
+                        self.namespace, self.label_selector, self.field_selector, self.rv,
+                        timeout_s=int(self.resync_s)):
+                    backoff = 0.05
+                    md = pod.get("metadata", {})
+                    if etype == "ERROR":
+                        raise ApiError(int(pod.get("code", 500)), pod.get("message", ""))
+                    if md.get("resourceVersion"):
+                        self.rv = md["resourceVersion"]
+                    if etype == "BOOKMARK":
+                        continue
+                    key = (md.get("namespace", ""), md.get("name", ""))
+                    self.events += 1
+                    if etype == "DELETED":
+                        self.cache.pop(key, None)
+                        self.deleted[key] = md.get("uid", "")
+                    else:
+                        self.cache[key] = pod
+                        self.deleted.pop(key, None)
+                    await self._notify(etype, pod)
+                # stream ended (server timeout): resume from rv without relisting
+                continue
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                _log.warning("watch %s/%s failed: %s; relisting in %.2fs", self.namespace,
+                             self.label_selector, e, backoff)
+                await asyncio.sleep(backoff)
+                backoff = min(backoff * 2, 5.0)
+
+    # ------------------------------------------------------------------------ queries
+    def get(self, ns: str, name: str) -> Optional[dict]:
+        p = self.cache.get((ns, name))
+        return copy.deepcopy(p) if p is not None else None
+
+    def list(self, pred: Callable[[dict], bool] = lambda p: True) -> List[dict]:
+        return [p for p in self.cache.values() if pred(p)]
+
+    async def wait_for(self, pred: Callable[[], Optional[object]], timeout: float):
+        """Await until ``pred()`` returns a truthy value (re-evaluated on every event)."""
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout
+        async with self._cond:
+            while True:
+                v = pred()
+                if v:
+                    return v
+                left = deadline - loop.time()
+                if left <= 0:
+                    raise asyncio.TimeoutError()
+                try:
+                    await asyncio.wait_for(self._cond.wait(), timeout=left)
+                except asyncio.TimeoutError:
+                    v = pred()
+                    if v:
+                        return v
+                    raise
+
+    async def poke(self) -> None:
+        """Wake waiters (used when a non-watch signal, e.g. the kubelet ledger, changed)."""
+        async with self._cond:
+            self._cond.notify_all()

@@ -1,0 +1,217 @@
+"""Minimal async Kubernetes REST client (pods + watch) on aiohttp.
+
+Reference: client-go clientset singleton, always in-cluster, panicking on error, with a
+placeholder out-of-cluster kubeconfig path (reference: pkg/config/config.go:11-45). Only
+Pods Get/List/Create/Delete are used there, and readiness is found by busy-polling Get
+(allocator.go:246-316). This client adds: in-cluster / kubeconfig / explicit-URL config, one
+keep-alive session, typed errors, JSON merge-patch, and **watch streams** (the replacement for
+busy-polling).
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import json
+import os
+import ssl
+import tempfile
+from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
+
+import aiohttp
+import yaml
+
+from gpumounter_amd.utils import log
+
+_log = log.get("kube")
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class ApiError(Exception):
+    def __init__(self, status: int, reason: str, body: Any = None):
+        super().__init__(f"{status} {reason}")
+        self.status = status
+        self.reason = reason
+        self.body = body
+
+
+class NotFound(ApiError):
+    pass
+
+
+class Conflict(ApiError):
+    pass
+
+
+class KubeClient:
+    def __init__(self, base_url: str, token: str = "", ca_file: str = "",
+                 client_cert: Optional[Tuple[str, str]] = None, insecure: bool = False,
+                 timeout_s: float = 30.0) -> None:
+        self.base = base_url.rstrip("/")
+        self.token = token
+        self.timeout = aiohttp.ClientTimeout(total=timeout_s)
+        self._ssl: Any = None
+        if self.base.startswith("https"):
+            if insecure:
+                self._ssl = False
+            else:
+                ctx = ssl.create_default_context(cafile=ca_file or None)
+                if client_cert:
+                    ctx.load_cert_chain(*client_cert)
+                self._ssl = ctx
+        self._session: Optional[aiohttp.ClientSession] = None
+        self._session_loop = None
+
+    # ------------------------------------------------------------------------- construction
+    @classmethod
+    def from_config(cls, cfg) -> "KubeClient":
+        if cfg.kube_api:
+            return cls(cfg.kube_api, token=cfg.kube_token, ca_file=cfg.kube_ca,
+                       insecure=cfg.kube_insecure)
+        if cfg.kubeconfig:
+            return cls.from_kubeconfig(cfg.kubeconfig)
+        return cls.in_cluster()
+
+    @classmethod
+    def in_cluster(cls) -> "KubeClient":
+        host = os.environ.get("KUBERNETES_SERVICE_HOST")
+        port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        if not host:
+            raise RuntimeError("not in a cluster (KUBERNETES_SERVICE_HOST unset) and no "
+                               "kube_api/kubeconfig configured")
+        with open(os.path.join(SA_DIR, "token"), encoding="utf-8") as fh:
+            token = fh.read().strip()
+        if ":" in host and not host.startswith("["):
+            host = f"[{host}]"
+        return cls(f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"))
+
+    @classmethod
+    def from_kubeconfig(cls, path: str, context: str = "") -> "KubeClient":
+        with open(path, encoding="utf-8") as fh:
+            kc = yaml.safe_load(fh)
+        ctx_name = context or kc.get("current-context")
+        ctx = next(c["context"] for c in kc["contexts"] if c["name"] == ctx_name)
+        cluster = next(c["cluster"] for c in kc["clusters"] if c["name"] == ctx["cluster"])
+        user = next((u["user"] for u in kc.get("users", []) if u["name"] == ctx.get("user")), {})
+
+        def materialize(data_key: str, file_key: str, src: dict) -> str:
+            if src.get(file_key):
+                return src[file_key]
+            if src.get(data_key):
+                fd, p = tempfile.mkstemp(prefix="gm-kc-")
+                with os.fdopen(fd, "wb") as out:
+                    out.write(base64.b64decode(src[data_key]))
+                return p
+            return ""
+
+        ca = materialize("certificate-authority-data", "certificate-authority", cluster)
+        cert = materialize("client-certificate-data", "client-certificate", user)
+        key = materialize("client-key-data", "client-key", user)
+        return cls(cluster["server"], token=user.get("token", ""), ca_file=ca,
+                   client_cert=(cert, key) if cert and key else None,
+                   insecure=bool(cluster.get("insecure-skip-tls-verify")))
+
+    # ------------------------------------------------------------------------- plumbing
+    def _sess(self) -> aiohttp.ClientSession:
+        loop = asyncio.get_running_loop()
+        if self._session is None or self._session.closed or self._session_loop is not loop:
+            headers = {"Accept": "application/json"}
+            if self.token:
+                headers["Authorization"] = f"Bearer {self.token}"
+            conn = aiohttp.TCPConnector(limit=64, ssl=self._ssl if self._ssl is not None else None)
+            self._session = aiohttp.ClientSession(headers=headers, connector=conn,
+                                                  timeout=self.timeout)
+            self._session_loop = loop
+        return self._session
+
+    async def close(self) -> None:
+        if self._session is not None and not self._session.closed:
+            await self._session.close()
+        self._session = None
+
+    async def _req(self, method: str, path: str, params: Optional[dict] = None,
+                   body: Any = None, content_type: str = "application/json") -> Any:
+        sess = self._sess()
+        data = None
+        headers = {}
+        if body is not None:
+            data = json.dumps(body)
+            headers["Content-Type"] = content_type
+        async with sess.request(method, self.base + path, params=params, data=data,
+                                headers=headers) as resp:
+            text = await resp.text()
+            if resp.status >= 400:
+                try:
+                    payload = json.loads(text)
+                except ValueError:
+                    payload = text
+                reason = payload.get("message", text) if isinstance(payload, dict) else text
+                if resp.status == 404:
+                    raise NotFound(404, reason, payload)
+                if resp.status == 409:
+                    raise Conflict(409, reason, payload)
+                raise ApiError(resp.status, reason, payload)
+            return json.loads(text) if text else None
+
+    @staticmethod
+    def _pods_path(ns: Optional[str], name: str = "") -> str:
+        base = f"/api/v1/namespaces/{ns}/pods" if ns else "/api/v1/pods"
+        return f"{base}/{name}" if name else base
+
+    # ------------------------------------------------------------------------- pods
+    async def get_pod(self, ns: str, name: str) -> dict:
+        return await self._req("GET", self._pods_path(ns, name))
+
+    async def list_pods(self, ns: Optional[str] = None, label_selector: str = "",
+                        field_selector: str = "") -> Tuple[List[dict], str]:
+        params = {}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        out = await self._req("GET", self._pods_path(ns), params=params)
+        return out.get("items", []), out.get("metadata", {}).get("resourceVersion", "")
+
+    async def create_pod(self, ns: str, pod: dict) -> dict:
+        return await self._req("POST", self._pods_path(ns), body=pod)
+
+    async def delete_pod(self, ns: str, name: str, grace_period_s: Optional[int] = None,
+                         uid: str = "") -> Optional[dict]:
+        body: Dict[str, Any] = {"kind": "DeleteOptions", "apiVersion": "v1"}
+        if grace_period_s is not None:
+            body["gracePeriodSeconds"] = int(grace_period_s)
+        if uid:
+            body["preconditions"] = {"uid": uid}
+        return await self._req("DELETE", self._pods_path(ns, name), body=body)
+
+    async def patch_pod(self, ns: str, name: str, patch: dict) -> dict:
+        return await self._req("PATCH", self._pods_path(ns, name), body=patch,
+                               content_type="application/merge-patch+json")
+
+    async def watch_pods(self, ns: Optional[str] = None, label_selector: str = "",
+                         field_selector: str = "", resource_version: str = "",
+                         timeout_s: int = 300) -> AsyncIterator[Tuple[str, dict]]:
+        """Yield ``(type, pod)`` events (ADDED/MODIFIED/DELETED/BOOKMARK/ERROR)."""
+        params = {"watch": "true", "timeoutSeconds": str(timeout_s),
+                  "allowWatchBookmarks": "true"}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        if resource_version:
+            params["resourceVersion"] = resource_version
+        sess = self._sess()
+        async with sess.get(self.base + self._pods_path(ns), params=params,
+                            timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30)
+                            ) as resp:
+            if resp.status >= 400:
+                raise ApiError(resp.status, await resp.text())
+            buf = b""
+            async for chunk in resp.content.iter_any():
+                buf += chunk
+                while b"\n" in buf:
+                    line, buf = buf.split(b"\n", 1)
+                    if not line.strip():
+                        continue
+                    ev = json.loads(line)
+                    yield ev.get("type", ""), ev.get("object", {})

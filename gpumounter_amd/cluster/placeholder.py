@@ -1,0 +1,261 @@
+"""Placeholder pods — the scheduler-consistent GPU ledger.
+
+Reference: ``GetAvailableGPU`` creates ``total/perPod`` slave pods *sequentially* in ``gpu-pool``
+(``alpine:latest`` sleep loop, ``nvidia.com/gpu`` limit, nodeSelector hostname, cross-namespace
+controller ownerReference), busy-polls them until Running/Unschedulable, then reads their device
+IDs from PodResources (reference: pkg/util/gpu/allocator/allocator.go:40-99,189-282). The GPU is
+thereby held in the scheduler's books by a pod the scheduler knows about, while the tenant uses it.
+
+Kept: the ledger model, the ``<owner>-slave-pod-<hex>`` naming, nodeSelector pinning, the
+Unschedulable → InsufficientGPU mapping. Changed:
+
+* creates run concurrently; readiness is awaited on a watch (no polling of the apiserver);
+* the allocation is read as soon as the kubelet *admits* the placeholder (device-plugin Allocate
+  happens at admission) instead of after the container is Running;
+* a pre-pulled ``pause`` image with ``IfNotPresent`` (the reference's ``:latest`` forces a pull);
+  ``terminationGracePeriodSeconds: 0`` (the reference's ``sh`` loop ignores SIGTERM, so every
+  detach waited the default 30 s grace);
+* owner matching is an exact label + UID annotation (the reference's substring match lets pod
+  ``a`` see the slaves of ``xa`` and ignores namespaces — defect 3);
+* in ``tenant`` namespace mode the ownerReference is same-namespace (valid for the garbage
+  collector); in ``pool`` mode no cross-namespace ownerReference is written at all (Kubernetes
+  ≥1.20 treats it as absent and deletes the placeholder — defect 4) and the reconciler collects
+  placeholders whose owner is gone;
+* the preferred (xGMI/NUMA-aware) device set is attached as an annotation for
+  GetPreferredAllocation-capable device plugins, and any deviation is counted.
+"""
+from __future__ import annotations
+
+import asyncio
+import secrets
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from gpumounter_amd.cluster.informer import PodInformer
+from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_MOUNT_MODE,
+                                         ANN_OWNER_UID, ANN_PREFERRED, LABEL_APP, LABEL_APP_VALUE,
+                                         LABEL_OWNER, LABEL_OWNER_NS, SLAVE_SUFFIX)
+from gpumounter_amd.node.ledger import LedgerClient
+from gpumounter_amd.utils import log, trace
+
+_log = log.get("cluster.placeholder")
+LABEL_NODE = "gpumounter.amd.com/node"
+
+
+class InsufficientGPU(RuntimeError):
+    pass
+
+
+class ReserveError(RuntimeError):
+    pass
+
+
+@dataclass
+class Placeholder:
+    namespace: str
+    name: str
+    uid: str = ""
+    device_ids: Tuple[str, ...] = ()
+    mode: str = "single"
+
+
+@dataclass
+class Reservation:
+    placeholders: List[Placeholder] = field(default_factory=list)
+
+    @property
+    def device_ids(self) -> List[str]:
+        return [d for p in self.placeholders for d in p.device_ids]
+
+
+def _label_value(s: str) -> str:
+    s = s[:63]
+    return s.rstrip("-_.") or "x"
+
+
+class PlaceholderManager:
+    def __init__(self, cfg, kube: KubeClient, ledger: LedgerClient, informer: PodInformer,
+                 node_name: str) -> None:
+        self.cfg = cfg
+        self.kube = kube
+        self.ledger = ledger
+        self.informer = informer
+        self.node = node_name
+
+    # ------------------------------------------------------------------------ spec
+    def namespace_for(self, owner: dict) -> str:
+        if self.cfg.placeholder_namespace_mode == "tenant":
+            return podu.ns_of(owner)
+        return self.cfg.pool_namespace
+
+    @staticmethod
+    def selector_for_node(node: str) -> str:
+        return f"{LABEL_APP}={LABEL_APP_VALUE},{LABEL_NODE}={_label_value(node)}"
+
+    def build(self, owner: dict, n_gpus: int, mode: str, preferred: Sequence[str] = (),
+              attach_id: str = "", container: str = "") -> dict:
+        ns = self.namespace_for(owner)
+        name = podu.name_of(owner)[: 253 - 20] + SLAVE_SUFFIX + secrets.token_hex(3)
+        md = {
+            "name": name,
+            "namespace": ns,
+            "labels": {LABEL_APP: LABEL_APP_VALUE,
+                       LABEL_OWNER: _label_value(podu.name_of(owner)),
+                       LABEL_OWNER_NS: _label_value(podu.ns_of(owner)),
+                       LABEL_NODE: _label_value(self.node)},
+            "annotations": {ANN_OWNER_UID: podu.uid_of(owner), ANN_MOUNT_MODE: mode,
+                            ANN_ATTACH_ID: attach_id, ANN_CONTAINER: container,
+                            "gpumounter.amd.com/owner-name": podu.name_of(owner)},
+        }
+        if preferred:
+            md["annotations"][ANN_PREFERRED] = ",".join(preferred)
+        if ns == podu.ns_of(owner):
+            md["ownerReferences"] = [{"apiVersion": "v1", "kind": "Pod",
+                                      "name": podu.name_of(owner), "uid": podu.uid_of(owner),
+                                      "controller": True, "blockOwnerDeletion": True}]
+        spec = {
+            "nodeSelector": {"kubernetes.io/hostname": self.node},
+            "tolerations": [{"operator": "Exists"}],
+            "terminationGracePeriodSeconds": 0,
+            "automountServiceAccountToken": False,
+            "enableServiceLinks": False,
+            "restartPolicy": "Always",
+            "containers": [{
+                "name": "gpu-holder",
+                "image": self.cfg.placeholder_image,
+                "imagePullPolicy": self.cfg.placeholder_pull_policy,
+                "resources": {"limits": {self.cfg.resource_name: str(n_gpus)},
+                              "requests": {"cpu": "1m", "memory": "4Mi"}},
+            }],
+        }
+        if self.cfg.placeholder_priority_class:
+            spec["priorityClassName"] = self.cfg.placeholder_priority_class
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": spec}
+
+    # ------------------------------------------------------------------------ queries
+    def owned_by(self, owner: dict) -> List[dict]:
+        uid = podu.uid_of(owner)
+        oname, ons = _label_value(podu.name_of(owner)), _label_value(podu.ns_of(owner))
+
+        def mine(p: dict) -> bool:
+            md = p["metadata"]
+            lab = md.get("labels") or {}
+            return (lab.get(LABEL_OWNER) == oname and lab.get(LABEL_OWNER_NS) == ons
+                    and (md.get("annotations") or {}).get(ANN_OWNER_UID) == uid
+                    and not md.get("deletionTimestamp"))
+
+        return self.informer.list(mine)
+
+    # ------------------------------------------------------------------------ reserve
+    async def reserve(self, owner: dict, total: int, entire: bool, preferred: Sequence[str] = (),
+                      attach_id: str = "", container: str = "") -> Reservation:
+        """Entire mount = one placeholder holding ``total`` GPUs (all-or-nothing at the
+        scheduler, reference QuickStart.md:52); single mount = ``total`` placeholders × 1 GPU."""
+        if total <= 0:
+            raise ValueError(f"bad reservation size {total}")
+        per_pod = total if entire else 1
+        k = total // per_pod
+        mode = "entire" if entire else "single"
+        prefs = [list(preferred[i * per_pod:(i + 1) * per_pod]) for i in range(k)] \
+            if len(preferred) == total else [[] for _ in range(k)]
+        bodies = [self.build(owner, per_pod, mode, prefs[i], attach_id, container)
+                  for i in range(k)]
+        with trace.span("ledger_reserve", placeholders=k):
+            results = await asyncio.gather(
+                *[self.kube.create_pod(b["metadata"]["namespace"], b) for b in bodies],
+                return_exceptions=True)
+        created = [Placeholder(r["metadata"]["namespace"], r["metadata"]["name"],
+                               r["metadata"]["uid"], (), mode)
+                   for r in results if isinstance(r, dict)]
+        errors = [r for r in results if not isinstance(r, dict)]
+        if errors:
+            await self.release(created, wait=False)
+            raise ReserveError(f"placeholder create failed: {errors[0]}")
+        try:
+            with trace.span("placeholder_wait"):
+                await self._await_admission(created, self.cfg.attach_timeout_s)
+        except BaseException:
+            await self.release(created, wait=False)
+            raise
+        return Reservation(created)
+
+    async def _await_admission(self, phs: List[Placeholder], timeout: float) -> None:
+        """Wait until every placeholder is admitted and its devices are in the kubelet ledger."""
+        pending = {(p.namespace, p.name): p for p in phs}
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout
+        delay = 0.0005
+        while pending:
+            failure: List[str] = []
+
+            def state():
+                bound = []
+                for key in pending:
+                    pod = self.informer.cache.get(key)
+                    if pod is None:
+                        continue
+                    msg = podu.is_unschedulable(pod)
+                    if msg:
+                        failure.append(f"unschedulable: {msg}")
+                        return True
+                    if podu.phase_of(pod) == "Failed":
+                        failure.append(pod["status"].get("reason", "Failed"))
+                        return True
+                    if podu.node_of(pod):
+                        bound.append(key)
+                return bound or None
+
+            left = deadline - loop.time()
+            if left <= 0:
+                raise ReserveError(f"timeout waiting for placeholders {sorted(pending)}")
+            await self.informer.wait_for(state, timeout=left)
+            if failure:
+                reason = failure[0]
+                if reason.startswith("unschedulable") or reason.startswith("OutOf") or \
+                        reason == "UnexpectedAdmissionError":
+                    raise InsufficientGPU(reason)
+                raise ReserveError(reason)
+            # bound: the kubelet records the allocation at admission — read the ledger
+            got = await self.ledger.by_pod()
+            for key in list(pending):
+                ids = got.get(key)
+                if ids:
+                    pending.pop(key).device_ids = tuple(ids)
+            if pending:
+                await asyncio.sleep(delay)
+                delay = min(delay * 2, 0.05)
+
+    # ------------------------------------------------------------------------ release
+    async def release(self, phs: Sequence[Placeholder], wait: bool = True,
+                      timeout: Optional[float] = None) -> None:
+        if not phs:
+            return
+        with trace.span("ledger_release", placeholders=len(phs)):
+            res = await asyncio.gather(
+                *[self.kube.delete_pod(p.namespace, p.name, grace_period_s=0, uid=p.uid or "")
+                  for p in phs], return_exceptions=True)
+            for p, r in zip(phs, res):
+                if isinstance(r, Exception) and not isinstance(r, NotFound):
+                    _log.error("delete placeholder %s/%s: %s", p.namespace, p.name, r)
+            if not wait:
+                return
+            keys = {(p.namespace, p.name): p.uid for p in phs}
+
+            def gone():
+                for (ns, name), uid in keys.items():
+                    cur = self.informer.cache.get((ns, name))
+                    if cur is not None and (not uid or cur["metadata"].get("uid") == uid):
+                        return False
+                return True
+
+            await self.informer.wait_for(gone, timeout or self.cfg.detach_timeout_s)
+
+    @staticmethod
+    def from_pod(p: dict, ledger_ids: Dict[Tuple[str, str], List[str]]) -> Placeholder:
+        md = p["metadata"]
+        key = (md["namespace"], md["name"])
+        return Placeholder(md["namespace"], md["name"], md.get("uid", ""),
+                           tuple(ledger_ids.get(key, ())),
+                           (md.get("annotations") or {}).get(ANN_MOUNT_MODE, "single"))

@@ -1,0 +1,570 @@
+"""Hermetic kube-apiserver + scheduler + kubelet emulation for tests and benchmarks.
+
+Serves the subset of the core/v1 Pod API the controller uses (GET/LIST/WATCH/POST/DELETE/PATCH,
+label + field selectors, resourceVersion-based watch resume), and runs a tiny control loop:
+
+* **scheduler** — binds pods to nodes whose labels match ``nodeSelector`` and whose extended
+  resource capacity (``amd.com/gpu``) still fits; otherwise sets ``PodScheduled=False,
+  reason=Unschedulable`` (what the reference waits for: allocator.go:266) and re-queues the pod
+  when capacity frees up;
+* **kubelet** — admits bound pods (device-plugin Allocate → PodResources ledger), pulls images
+  (``Always`` pulls every time, ``IfNotPresent`` once per node), starts containers (cgroup +
+  rootfs artifacts on the :class:`FakeNode`), honours grace periods and finalizers on delete;
+* **garbage collector** — ownerReference cascade; in ``modern`` mode (Kubernetes ≥1.20) a
+  dependent whose owner lives in another namespace is treated as ownerless and collected, which is
+  exactly the hazard of the reference's cross-namespace slave pods (SURVEY §2.6 defect 4).
+
+Every phase has an optional latency (:class:`LatencyModel`) so benchmarks can model a real
+control plane; the default is zero (pure plumbing).
+"""
+from __future__ import annotations
+
+import asyncio
+import copy
+import json
+import secrets
+import threading
+import time
+import uuid
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Tuple
+
+from aiohttp import web
+
+from gpumounter_amd.fakes.node import FakeNode
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.utils import log
+
+_log = log.get("fake.apiserver")
+
+
+@dataclass
+class LatencyModel:
+    """Control-plane delays in milliseconds (0 = instantaneous)."""
+
+    api_ms: float = 0.0        # every API request
+    schedule_ms: float = 0.0   # create → bind
+    admit_ms: float = 0.0      # bind → device-plugin Allocate (ledger visible)
+    sandbox_ms: float = 0.0    # pod sandbox (pause container, CNI)
+    pull_ms: float = 0.0       # image pull when required by pull policy
+    start_ms: float = 0.0      # container start → Running
+    stop_ms: float = 0.0       # SIGTERM → exit for images that handle SIGTERM
+    grace_scale: float = 0.0   # fraction of terminationGracePeriodSeconds waited when an image
+                               # ignores SIGTERM (1.0 = real time)
+
+    @classmethod
+    def realistic(cls) -> "LatencyModel":
+        """Order-of-magnitude figures for a small on-prem cluster (documented in BASELINE.md)."""
+        return cls(api_ms=1.0, schedule_ms=10.0, admit_ms=15.0, sandbox_ms=300.0, pull_ms=1200.0,
+                   start_ms=120.0, stop_ms=50.0, grace_scale=1.0)
+
+
+def _now() -> str:
+    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+
+
+def _parse_selector(sel: str):
+    """Label selector → list of (key, op, value) with op in {=, !=, exists, !exists}."""
+    out = []
+    for part in filter(None, (p.strip() for p in (sel or "").split(","))):
+        if "!=" in part:
+            k, v = part.split("!=", 1)
+            out.append((k.strip(), "!=", v.strip()))
+        elif "==" in part:
+            k, v = part.split("==", 1)
+            out.append((k.strip(), "=", v.strip()))
+        elif "=" in part:
+            k, v = part.split("=", 1)
+            out.append((k.strip(), "=", v.strip()))
+        elif part.startswith("!"):
+            out.append((part[1:], "!exists", ""))
+        else:
+            out.append((part, "exists", ""))
+    return out
+
+
+def _match_labels(labels: Dict[str, str], sel) -> bool:
+    for k, op, v in sel:
+        if op == "=" and labels.get(k) != v:
+            return False
+        if op == "!=" and labels.get(k) == v:
+            return False
+        if op == "exists" and k not in labels:
+            return False
+        if op == "!exists" and k in labels:
+            return False
+    return True
+
+
+def _field(pod: dict, key: str) -> str:
+    cur: Any = pod
+    for part in key.split("."):
+        cur = cur.get(part, "") if isinstance(cur, dict) else ""
+    return cur or ""
+
+
+def _match_fields(pod: dict, sel) -> bool:
+    for k, op, v in sel:
+        if op == "=" and _field(pod, k) != v:
+            return False
+        if op == "!=" and _field(pod, k) == v:
+            return False
+    return True
+
+
+def merge_patch(target: Any, patch: Any) -> Any:
+    """RFC 7386 JSON merge patch."""
+    if not isinstance(patch, dict):
+        return copy.deepcopy(patch)
+    if not isinstance(target, dict):
+        target = {}
+    for k, v in patch.items():
+        if v is None:
+            target.pop(k, None)
+        else:
+            target[k] = merge_patch(target.get(k), v)
+    return target
+
+
+class FakeCluster:
+    """State + control loops; :meth:`app` exposes it over HTTP."""
+
+    HISTORY = 20000
+
+    def __init__(self, latency: Optional[LatencyModel] = None, gc_mode: str = "modern") -> None:
+        self.latency = latency or LatencyModel()
+        self.gc_mode = gc_mode
+        self.nodes: Dict[str, FakeNode] = {}
+        self.pods: Dict[Tuple[str, str], dict] = {}
+        self.rv = 1000
+        self.events: List[Tuple[int, str, dict]] = []
+        self.watchers: List[Tuple[asyncio.Queue, str, Any, Any]] = []
+        self.loop: Optional[asyncio.AbstractEventLoop] = None
+        self.request_count = 0
+        self.requests_by_verb: Dict[str, int] = {}
+        self._unschedulable: set = set()
+        self._tasks: set = set()
+        self._lock = threading.RLock()
+
+    # ------------------------------------------------------------------------ nodes
+    def add_node(self, node: FakeNode) -> FakeNode:
+        self.nodes[node.name] = node
+        return node
+
+    # ------------------------------------------------------------------------ events
+    def _bump(self, etype: str, pod: dict) -> None:
+        self.rv += 1
+        pod["metadata"]["resourceVersion"] = str(self.rv)
+        snap = copy.deepcopy(pod)
+        self.events.append((self.rv, etype, snap))
+        if len(self.events) > self.HISTORY:
+            del self.events[: len(self.events) - self.HISTORY]
+        for q, ns, lsel, fsel in list(self.watchers):
+            if self._matches(snap, ns, lsel, fsel):
+                q.put_nowait((etype, snap))
+
+    @staticmethod
+    def _matches(pod: dict, ns: str, lsel, fsel) -> bool:
+        if ns and pod["metadata"].get("namespace") != ns:
+            return False
+        return _match_labels(pod["metadata"].get("labels", {}) or {}, lsel) and \
+            _match_fields(pod, fsel)
+
+    def _spawn(self, coro) -> None:
+        t = asyncio.ensure_future(coro)
+        self._tasks.add(t)
+        t.add_done_callback(self._tasks.discard)
+
+    # ------------------------------------------------------------------------ pod CRUD
+    def create_pod(self, ns: str, body: dict, *, schedule: bool = True) -> dict:
+        pod = copy.deepcopy(body)
+        md = pod.setdefault("metadata", {})
+        if not md.get("name"):
+            gen = md.get("generateName")
+            if not gen:
+                raise web.HTTPUnprocessableEntity(text=json.dumps(
+                    {"kind": "Status", "message": "name or generateName is required"}))
+            md["name"] = gen + secrets.token_hex(3)[:5]
+        md["namespace"] = ns
+        if (ns, md["name"]) in self.pods:
+            raise web.HTTPConflict(text=json.dumps(
+                {"kind": "Status", "reason": "AlreadyExists",
+                 "message": f'pods "{md["name"]}" already exists'}), content_type="application/json")
+        md["uid"] = str(uuid.uuid4())
+        md["creationTimestamp"] = _now()
+        md.setdefault("labels", {})
+        md.setdefault("annotations", {})
+        pod.setdefault("spec", {})
+        pod["status"] = {"phase": "Pending", "conditions": []}
+        self.pods[(ns, md["name"])] = pod
+        self._bump("ADDED", pod)
+        if schedule:
+            self._spawn(self._schedule(ns, md["name"]))
+        return pod
+
+    def get(self, ns: str, name: str) -> Optional[dict]:
+        return self.pods.get((ns, name))
+
+    def _used(self, node: str, resource: str, exclude: Tuple[str, str] = ("", "")) -> int:
+        total = 0
+        for key, p in self.pods.items():
+            if key == exclude or podu.node_of(p) != node:
+                continue
+            if p["status"].get("phase") in ("Succeeded", "Failed"):
+                continue
+            total += podu.resource_limit(p, resource)
+        return total
+
+    async def _sleep(self, ms: float) -> None:
+        if ms > 0:
+            await asyncio.sleep(ms / 1e3)
+
+    async def _schedule(self, ns: str, name: str) -> None:
+        await self._sleep(self.latency.schedule_ms)
+        pod = self.pods.get((ns, name))
+        if pod is None or podu.is_terminating(pod):
+            return
+        if podu.node_of(pod):
+            node_name = podu.node_of(pod)
+        else:
+            sel = pod["spec"].get("nodeSelector", {}) or {}
+            node_name = ""
+            for n in self.nodes.values():
+                if not all(n.labels.get(k) == v for k, v in sel.items()):
+                    continue
+                want = podu.resource_limit(pod, n.resource)
+                if self._used(n.name, n.resource, (ns, name)) + want <= n.capacity:
+                    node_name = n.name
+                    break
+            if not node_name:
+                pod["status"]["conditions"] = [{
+                    "type": "PodScheduled", "status": "False", "reason": "Unschedulable",
+                    "message": "0/%d nodes are available: insufficient resources" % len(self.nodes),
+                    "lastTransitionTime": _now()}]
+                self._unschedulable.add((ns, name))
+                self._bump("MODIFIED", pod)
+                return
+            pod["spec"]["nodeName"] = node_name
+        self._unschedulable.discard((ns, name))
+        pod["status"]["conditions"] = [{"type": "PodScheduled", "status": "True",
+                                        "lastTransitionTime": _now()}]
+        self._bump("MODIFIED", pod)
+        self._spawn(self._kubelet_run(ns, name, node_name))
+
+    async def _kubelet_run(self, ns: str, name: str, node_name: str) -> None:
+        node = self.nodes.get(node_name)
+        if node is None:
+            return
+        await self._sleep(self.latency.admit_ms)
+        pod = self.pods.get((ns, name))
+        if pod is None or podu.is_terminating(pod):
+            return
+        # device-plugin Allocate per container (admission)
+        for c in pod["spec"].get("containers", []):
+            want = int(podu.parse_quantity(
+                ((c.get("resources") or {}).get("limits") or {}).get(node.resource, 0)))
+            if want:
+                pref = (pod["metadata"].get("annotations") or {}).get(
+                    "gpumounter.amd.com/preferred-devices", "")
+                ids = node.allocate(ns, name, c["name"], want,
+                                    [p for p in pref.split(",") if p])
+                if ids is None:
+                    node.release_pod(ns, name)
+                    pod["status"]["phase"] = "Failed"
+                    pod["status"]["reason"] = "UnexpectedAdmissionError"
+                    self._bump("MODIFIED", pod)
+                    return
+        pod["status"]["containerStatuses"] = [
+            {"name": c["name"], "ready": False, "restartCount": 0, "image": c.get("image", ""),
+             "state": {"waiting": {"reason": "ContainerCreating"}}}
+            for c in pod["spec"].get("containers", [])]
+        self._bump("MODIFIED", pod)
+        await self._sleep(self.latency.sandbox_ms)
+        for c in pod["spec"].get("containers", []):
+            img = c.get("image", "")
+            policy = c.get("imagePullPolicy") or ("Always" if img.endswith(":latest") or
+                                                  ":" not in img else "IfNotPresent")
+            if policy == "Always" or (policy == "IfNotPresent" and img not in node.images):
+                await self._sleep(self.latency.pull_ms)
+                node.images.add(img)
+        await self._sleep(self.latency.start_ms)
+        pod = self.pods.get((ns, name))
+        if pod is None or podu.is_terminating(pod):
+            return
+        self._start_containers(node, pod)
+
+    def _start_containers(self, node: FakeNode, pod: dict, pids=None) -> None:
+        statuses = []
+        for c in pod["spec"].get("containers", []):
+            ctr = node.start_container(pod, c["name"], (pids or {}).get(c["name"], ()))
+            statuses.append({
+                "name": c["name"], "ready": True, "restartCount": 0, "image": c.get("image", ""),
+                "containerID": f"{node.runtime}://{ctr.id}",
+                "state": {"running": {"startedAt": _now()}}})
+        pod["status"]["containerStatuses"] = statuses
+        pod["status"]["phase"] = "Running"
+        pod["status"]["podIP"] = pod["status"].get("podIP") or "10.0.0.%d" % (self.rv % 250 + 2)
+        pod["status"]["conditions"] = [
+            {"type": "PodScheduled", "status": "True"}, {"type": "Ready", "status": "True"}]
+        pod["status"]["qosClass"] = podu.qos_class(pod)
+        self._bump("MODIFIED", pod)
+
+    def create_running_pod(self, ns: str, body: dict, node: str,
+                           pids: Optional[Dict[str, List[int]]] = None) -> dict:
+        """Test helper: a tenant pod that is already bound, admitted and running."""
+        pod = self.create_pod(ns, body, schedule=False)
+        pod["spec"]["nodeName"] = node
+        n = self.nodes[node]
+        for c in pod["spec"].get("containers", []):
+            want = int(podu.parse_quantity(
+                ((c.get("resources") or {}).get("limits") or {}).get(n.resource, 0)))
+            if want and n.allocate(ns, pod["metadata"]["name"], c["name"], want) is None:
+                raise RuntimeError("tenant pod does not fit")
+        self._start_containers(n, pod, pids)
+        return pod
+
+    def delete(self, ns: str, name: str, grace: Optional[int] = None,
+               uid_precondition: str = "") -> Optional[dict]:
+        pod = self.pods.get((ns, name))
+        if pod is None:
+            return None
+        if uid_precondition and pod["metadata"]["uid"] != uid_precondition:
+            raise web.HTTPConflict(text=json.dumps({"kind": "Status", "message": "uid mismatch"}),
+                                   content_type="application/json")
+        if grace is None:
+            grace = int(pod["spec"].get("terminationGracePeriodSeconds", 30))
+        md = pod["metadata"]
+        if not md.get("deletionTimestamp"):
+            md["deletionTimestamp"] = _now()
+            md["deletionGracePeriodSeconds"] = grace
+            self._bump("MODIFIED", pod)
+        running = pod["status"].get("phase") == "Running"
+        if grace == 0 or not running:
+            self._maybe_finalize(ns, name)
+        else:
+            self._spawn(self._terminate(ns, name, grace))
+        return pod
+
+    async def _terminate(self, ns: str, name: str, grace: int) -> None:
+        pod = self.pods.get((ns, name))
+        if pod is None:
+            return
+        if self._ignores_sigterm(pod):
+            await asyncio.sleep(grace * self.latency.grace_scale)
+        else:
+            await self._sleep(self.latency.stop_ms)
+        self._maybe_finalize(ns, name)
+
+    @staticmethod
+    def _ignores_sigterm(pod: dict) -> bool:
+        # a `sh -c "while true; ...; sleep 10; done"` container (reference allocator.go:217-220)
+        # runs as PID 1 without a SIGTERM handler, so the kubelet waits the whole grace period.
+        for c in pod["spec"].get("containers", []):
+            cmd = " ".join((c.get("command") or []) + (c.get("args") or []))
+            if "while true" in cmd:
+                return True
+        return False
+
+    def _maybe_finalize(self, ns: str, name: str) -> None:
+        pod = self.pods.get((ns, name))
+        if pod is None:
+            return
+        pod["status"]["phase"] = pod["status"].get("phase", "Pending")
+        if pod["metadata"].get("finalizers"):
+            return  # wait for the controller to drop finalizers (PATCH)
+        self._remove(ns, name)
+
+    def _remove(self, ns: str, name: str) -> None:
+        pod = self.pods.pop((ns, name), None)
+        if pod is None:
+            return
+        self._unschedulable.discard((ns, name))
+        node = self.nodes.get(podu.node_of(pod))
+        if node is not None:
+            node.release_pod(ns, name)
+            node.stop_pod_containers(ns, name)
+        self._bump("DELETED", pod)
+        self._gc(pod)
+        # capacity freed: retry unschedulable pods (scheduler queue)
+        for key in list(self._unschedulable):
+            self._spawn(self._schedule(*key))
+
+    def _gc(self, owner: dict) -> None:
+        ouid = owner["metadata"]["uid"]
+        for (ns, name), p in list(self.pods.items()):
+            for ref in p["metadata"].get("ownerReferences", []) or []:
+                if ref.get("uid") != ouid:
+                    continue
+                if self.gc_mode == "modern" and ns != owner["metadata"]["namespace"]:
+                    continue  # handled by _gc_invalid_refs: owner was never visible
+                self.delete(ns, name, grace=0)
+
+    def gc_sweep(self) -> int:
+        """Modern-GC rule: a namespaced owner must be in the dependent's namespace, otherwise the
+        reference is treated as absent and the dependent is deleted. Returns #deleted."""
+        n = 0
+        for (ns, name), p in list(self.pods.items()):
+            refs = p["metadata"].get("ownerReferences", []) or []
+            if not refs:
+                continue
+            live = False
+            for ref in refs:
+                for (ons, oname), o in self.pods.items():
+                    if o["metadata"]["uid"] == ref.get("uid") and \
+                            (self.gc_mode == "legacy" or ons == ns):
+                        live = True
+            if not live:
+                self.delete(ns, name, grace=0)
+                n += 1
+        return n
+
+    def patch(self, ns: str, name: str, patch: dict) -> Optional[dict]:
+        pod = self.pods.get((ns, name))
+        if pod is None:
+            return None
+        md_patch = patch.get("metadata", {})
+        merged = merge_patch(pod["metadata"], md_patch)
+        pod["metadata"] = merged
+        if "spec" in patch:
+            pod["spec"] = merge_patch(pod["spec"], patch["spec"])
+        self._bump("MODIFIED", pod)
+        if pod["metadata"].get("deletionTimestamp") and not pod["metadata"].get("finalizers"):
+            running = pod["status"].get("phase") == "Running"
+            if not running or pod["metadata"].get("deletionGracePeriodSeconds", 0) == 0:
+                self._remove(ns, name)
+        return pod
+
+    # ------------------------------------------------------------------------ HTTP
+    def app(self) -> web.Application:
+        app = web.Application(client_max_size=8 << 20)
+        r = app.router
+        r.add_get("/api/v1/pods", self._h_list)
+        r.add_get("/api/v1/namespaces/{ns}/pods", self._h_list)
+        r.add_post("/api/v1/namespaces/{ns}/pods", self._h_create)
+        r.add_get("/api/v1/namespaces/{ns}/pods/{name}", self._h_get)
+        r.add_delete("/api/v1/namespaces/{ns}/pods/{name}", self._h_delete)
+        r.add_patch("/api/v1/namespaces/{ns}/pods/{name}", self._h_patch)
+        r.add_get("/api/v1/nodes", self._h_nodes)
+        r.add_get("/healthz", lambda req: web.Response(text="ok"))
+        return app
+
+    async def _pre(self, req: web.Request) -> None:
+        self.request_count += 1
+        key = f"{req.method} {'watch' if req.query.get('watch') else ''}".strip()
+        self.requests_by_verb[key] = self.requests_by_verb.get(key, 0) + 1
+        await self._sleep(self.latency.api_ms)
+
+    @staticmethod
+    def _not_found(ns: str, name: str) -> web.Response:
+        return web.json_response({"kind": "Status", "status": "Failure", "reason": "NotFound",
+                                  "message": f'pods "{name}" not found', "code": 404}, status=404)
+
+    async def _h_get(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        ns, name = req.match_info["ns"], req.match_info["name"]
+        pod = self.pods.get((ns, name))
+        if pod is None:
+            return self._not_found(ns, name)
+        return web.json_response(pod)
+
+    async def _h_list(self, req: web.Request):
+        await self._pre(req)
+        ns = req.match_info.get("ns", "")
+        lsel = _parse_selector(req.query.get("labelSelector", ""))
+        fsel = _parse_selector(req.query.get("fieldSelector", ""))
+        if req.query.get("watch") in ("true", "1"):
+            return await self._watch(req, ns, lsel, fsel)
+        items = [p for p in self.pods.values() if self._matches(p, ns, lsel, fsel)]
+        return web.json_response({"kind": "PodList", "apiVersion": "v1",
+                                  "metadata": {"resourceVersion": str(self.rv)}, "items": items})
+
+    async def _watch(self, req: web.Request, ns: str, lsel, fsel) -> web.StreamResponse:
+        resp = web.StreamResponse(headers={"Content-Type": "application/json"})
+        await resp.prepare(req)
+        q: asyncio.Queue = asyncio.Queue()
+        rv = req.query.get("resourceVersion", "")
+        if rv and rv != "0":
+            since = int(rv)
+            if self.events and since < self.events[0][0] - 1:
+                await resp.write(json.dumps({"type": "ERROR", "object": {
+                    "kind": "Status", "code": 410, "reason": "Expired",
+                    "message": "too old resource version"}}).encode() + b"\n")
+                return resp
+            for erv, et, obj in self.events:
+                if erv > since and self._matches(obj, ns, lsel, fsel):
+                    q.put_nowait((et, obj))
+        else:
+            for p in list(self.pods.values()):
+                if self._matches(p, ns, lsel, fsel):
+                    q.put_nowait(("ADDED", copy.deepcopy(p)))
+        entry = (q, ns, lsel, fsel)
+        self.watchers.append(entry)
+        timeout = float(req.query.get("timeoutSeconds", "300"))
+        deadline = time.monotonic() + timeout
+        try:
+            while True:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    break
+                try:
+                    et, obj = await asyncio.wait_for(q.get(), timeout=min(left, 30))
+                except asyncio.TimeoutError:
+                    await resp.write(json.dumps({"type": "BOOKMARK", "object": {
+                        "kind": "Pod", "metadata": {"resourceVersion": str(self.rv)}}}).encode()
+                        + b"\n")
+                    continue
+                await resp.write(json.dumps({"type": et, "object": obj}).encode() + b"\n")
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            if entry in self.watchers:
+                self.watchers.remove(entry)
+        return resp
+
+    async def _h_create(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        ns = req.match_info["ns"]
+        body = await req.json()
+        pod = self.create_pod(ns, body)
+        return web.json_response(pod, status=201)
+
+    async def _h_delete(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        ns, name = req.match_info["ns"], req.match_info["name"]
+        grace = None
+        uid = ""
+        if req.can_read_body:
+            try:
+                opts = await req.json()
+            except ValueError:
+                opts = {}
+            if opts.get("gracePeriodSeconds") is not None:
+                grace = int(opts["gracePeriodSeconds"])
+            uid = (opts.get("preconditions") or {}).get("uid", "")
+        if "gracePeriodSeconds" in req.query:
+            grace = int(req.query["gracePeriodSeconds"])
+        pod = self.delete(ns, name, grace, uid)
+        if pod is None:
+            return self._not_found(ns, name)
+        return web.json_response(pod)
+
+    async def _h_patch(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        ns, name = req.match_info["ns"], req.match_info["name"]
+        pod = self.patch(ns, name, await req.json())
+        if pod is None:
+            return self._not_found(ns, name)
+        return web.json_response(pod)
+
+    async def _h_nodes(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        items = [{"metadata": {"name": n.name, "labels": n.labels},
+                  "status": {"capacity": {n.resource: str(n.capacity)},
+                             "allocatable": {n.resource: str(n.capacity)}}}
+                 for n in self.nodes.values()]
+        return web.json_response({"kind": "NodeList", "items": items})
+
+    # ------------------------------------------------------------------------ audits
+    def placeholders(self) -> List[dict]:
+        return [p for p in self.pods.values()
+                if (p["metadata"].get("labels") or {}).get("app") == "gpu-pool"]

@@ -1,0 +1,249 @@
+"""LocalCluster: a complete hermetic deployment in one asyncio loop.
+
+fake apiserver (HTTP) + per-node fake kubelet (PodResources gRPC on a unix socket) + per-node
+:class:`~gpumounter_amd.worker.server.Worker` (real gRPC server, real C++ host ops against a
+temp-dir cgroupfs/rootfs) + :class:`~gpumounter_amd.master.app.Master` (real HTTP server).
+Only the Kubernetes control plane is simulated; every byte between master, worker, kubelet and
+apiserver crosses a real socket, and the node operations run the production code paths.
+
+The GPU inventory comes from the amdsmi shim: the bundled mock on CPU hosts, the real
+``libamd_smi`` on an MI355X box (``amdsmi_lib=""``).
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import shutil
+import tempfile
+import threading
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import aiohttp
+from aiohttp import web
+
+from gpumounter_amd.fakes.apiserver import FakeCluster, LatencyModel
+from gpumounter_amd.fakes.kubelet import FakeKubelet
+from gpumounter_amd.fakes.node import FakeNode
+from gpumounter_amd.hw.inventory import Inventory
+from gpumounter_amd.master.app import ANN_WORKER_PORT, Master
+from gpumounter_amd.utils.config import Config
+from gpumounter_amd.worker.server import Worker
+
+
+@dataclass
+class NodeHandle:
+    name: str
+    node: FakeNode
+    kubelet: FakeKubelet
+    worker: Optional[Worker] = None
+    cfg: Optional[Config] = None
+
+
+class LocalCluster:
+    def __init__(self, n_nodes: int = 1, amdsmi_lib: str = "mock", cgroup_mode: str = "v1",
+                 cgroup_driver: str = "cgroupfs", runtime: str = "containerd",
+                 latency: Optional[LatencyModel] = None, gc_mode: str = "modern",
+                 workdir: str = "", placeholder_namespace_mode: str = "pool",
+                 alloc_policy: str = "topology", device_id_kind: str = "bdf",
+                 devnode_mode: str = "emulate", reconcile_period_s: float = 0.0,
+                 start_master: bool = True, worker_overrides: Optional[dict] = None) -> None:
+        self.n_nodes = n_nodes
+        self.amdsmi_lib = amdsmi_lib
+        self.cgroup_mode = cgroup_mode
+        self.cgroup_driver = cgroup_driver
+        self.runtime = runtime
+        self.cluster = FakeCluster(latency, gc_mode)
+        self._own_workdir = not workdir
+        self.workdir = workdir or tempfile.mkdtemp(prefix="gm-cluster-")
+        self.placeholder_namespace_mode = placeholder_namespace_mode
+        self.alloc_policy = alloc_policy
+        self.device_id_kind = device_id_kind
+        self.devnode_mode = devnode_mode
+        self.reconcile_period_s = reconcile_period_s
+        self.start_master = start_master
+        self.worker_overrides = worker_overrides or {}
+        self.nodes: Dict[str, NodeHandle] = {}
+        self.master: Optional[Master] = None
+        self.api_runner: Optional[web.AppRunner] = None
+        self.api_url = ""
+        self.master_url = ""
+        self.inventory: Optional[Inventory] = None
+        self.session: Optional[aiohttp.ClientSession] = None
+
+    # ------------------------------------------------------------------------ lifecycle
+    async def start(self) -> "LocalCluster":
+        self.inventory = Inventory(self.amdsmi_lib)
+        self.api_runner = web.AppRunner(self.cluster.app(), access_log=None)
+        await self.api_runner.setup()
+        site = web.TCPSite(self.api_runner, "127.0.0.1", 0)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+        self.api_url = f"http://127.0.0.1:{port}"
+        self.cluster.loop = asyncio.get_running_loop()
+        for i in range(self.n_nodes):
+            await self._add_node(f"node-{i}")
+        if self.start_master:
+            mcfg = Config.load(env={}, kube_api=self.api_url, master_host="127.0.0.1",
+                               log_json=False)
+            self.master = Master(mcfg)
+            await self.master.start(port=0)
+            self.master_url = f"http://127.0.0.1:{self.master.port}"
+            await self.master.workers.informer.wait_for(
+                lambda: all(self.master.workers.target(n) for n in self.nodes), 10)
+        self.session = aiohttp.ClientSession()
+        return self
+
+    async def _add_node(self, name: str) -> NodeHandle:
+        ndir = os.path.join(self.workdir, name)
+        os.makedirs(ndir, exist_ok=True)
+        node = FakeNode(name, ndir, self.inventory.gpus(), self.inventory.links(),
+                        cgroup_mode=self.cgroup_mode, cgroup_driver=self.cgroup_driver,
+                        runtime=self.runtime, device_id_kind=self.device_id_kind,
+                        alloc_policy=self.alloc_policy)
+        self.cluster.add_node(node)
+        sock = os.path.join(ndir, "pod-resources", "kubelet.sock")
+        kubelet = FakeKubelet(node, sock)
+        await kubelet.start()
+        h = NodeHandle(name, node, kubelet)
+        self.nodes[name] = h
+        await self.start_worker(name)
+        return h
+
+    async def start_worker(self, name: str) -> Worker:
+        h = self.nodes[name]
+        ov = dict(self.worker_overrides)
+        cfg = Config.load(env={}, kube_api=self.api_url, node_name=name,
+                          kubelet_socket=h.kubelet.socket_path,
+                          cgroup_root=h.node.cgroup_root, cgroup_mode=self.cgroup_mode,
+                          devnode_mode=self.devnode_mode,
+                          container_root_prefix=h.node.rootfs_root, amdsmi_lib=self.amdsmi_lib,
+                          worker_host="127.0.0.1", worker_port=1, metrics_port=0,
+                          placeholder_namespace_mode=self.placeholder_namespace_mode,
+                          reconcile_period_s=self.reconcile_period_s, log_json=False, **ov)
+        w = Worker(cfg, inventory=self.inventory)
+        await w.start(grpc_port=0, http_port=0, reconcile=self.reconcile_period_s > 0)
+        h.worker, h.cfg = w, cfg
+        # register the worker DaemonSet pod so the master can discover it
+        wp = self.cluster.get("kube-system", f"gpu-mounter-worker-{name}")
+        if wp is not None:
+            self.cluster._remove("kube-system", wp["metadata"]["name"])  # noqa: SLF001
+        self.cluster.create_running_pod("kube-system", {
+            "metadata": {"name": f"gpu-mounter-worker-{name}",
+                         "labels": {"app": "gpu-mounter-worker"},
+                         "annotations": {ANN_WORKER_PORT: str(w.grpc_port)}},
+            "spec": {"containers": [{"name": "worker", "image": "gpumounter-amd:dev"}]}}, name)
+        wpod = self.cluster.get("kube-system", f"gpu-mounter-worker-{name}")
+        wpod["status"]["podIP"] = "127.0.0.1"
+        self.cluster._bump("MODIFIED", wpod)  # noqa: SLF001
+        return w
+
+    async def stop_worker(self, name: str) -> None:
+        h = self.nodes[name]
+        if h.worker is not None:
+            await h.worker.stop()
+            h.worker = None
+
+    async def stop(self) -> None:
+        if self.session is not None:
+            await self.session.close()
+        if self.master is not None:
+            await self.master.stop()
+        for h in self.nodes.values():
+            if h.worker is not None:
+                await h.worker.stop()
+            await h.kubelet.stop()
+        for t in list(self.cluster._tasks):  # noqa: SLF001
+            t.cancel()
+        if self.api_runner is not None:
+            await self.api_runner.cleanup()
+        if self._own_workdir:
+            shutil.rmtree(self.workdir, ignore_errors=True)
+
+    async def __aenter__(self) -> "LocalCluster":
+        return await self.start()
+
+    async def __aexit__(self, *exc) -> None:
+        await self.stop()
+
+    # ------------------------------------------------------------------------ helpers
+    def tenant(self, name: str, ns: str = "default", node: str = "node-0",
+               containers: Optional[List[str]] = None, gpus: int = 0,
+               pids: Optional[Dict[str, List[int]]] = None, qos: str = "besteffort") -> dict:
+        cs = []
+        for cname in containers or ["main"]:
+            c: dict = {"name": cname, "image": "rocm/pytorch:latest",
+                       "command": ["sleep", "infinity"]}
+            res: dict = {}
+            if qos == "guaranteed":
+                res = {"limits": {"cpu": "1", "memory": "1Gi"},
+                       "requests": {"cpu": "1", "memory": "1Gi"}}
+            elif qos == "burstable":
+                res = {"requests": {"cpu": "100m"}}
+            if gpus:
+                res.setdefault("limits", {})["amd.com/gpu"] = str(gpus)
+            if res:
+                c["resources"] = res
+            cs.append(c)
+        return self.cluster.create_running_pod(
+            ns, {"metadata": {"name": name}, "spec": {"containers": cs}}, node, pids)
+
+    def container_ids(self, ns: str, name: str) -> List[str]:
+        pod = self.cluster.get(ns, name)
+        return [cs["containerID"].split("://", 1)[1]
+                for cs in pod["status"].get("containerStatuses", []) if cs.get("containerID")]
+
+    async def add(self, ns: str, pod: str, n: int, entire: bool = False,
+                  accept_json: bool = True):
+        url = (f"{self.master_url}/addgpu/namespace/{ns}/pod/{pod}/gpu/{n}/isEntireMount/"
+               f"{'true' if entire else 'false'}")
+        headers = {"Accept": "application/json"} if accept_json else {}
+        async with self.session.get(url, headers=headers) as r:
+            return r.status, (await r.json() if accept_json else await r.text())
+
+    async def remove(self, ns: str, pod: str, uuids: List[str], force: bool = False,
+                     accept_json: bool = True):
+        url = (f"{self.master_url}/removegpu/namespace/{ns}/pod/{pod}/force/"
+               f"{'true' if force else 'false'}")
+        headers = {"Accept": "application/json"} if accept_json else {}
+        data = aiohttp.FormData()
+        for u in uuids:
+            data.add_field("uuids", u)
+        async with self.session.post(url, data=data, headers=headers) as r:
+            return r.status, (await r.json() if accept_json else await r.text())
+
+    def audit(self, ns: str, pod: str, node: str = "node-0") -> list:
+        """Ledger-vs-host consistency issues for one pod (empty list = consistent)."""
+        h = self.nodes[node]
+        svc = h.worker.service
+        p = self.cluster.get(ns, pod)
+
+        async def run():
+            st = await svc.pod_state(p)
+            return svc.hm.audit(p, st.hot, st.own)
+        return run()
+
+
+class ThreadedCluster:
+    """Runs a LocalCluster on a private event loop thread (for sync callers: bench, smoke)."""
+
+    def __init__(self, **kw) -> None:
+        self.kw = kw
+        self.loop = asyncio.new_event_loop()
+        self.thread = threading.Thread(target=self.loop.run_forever, daemon=True,
+                                       name="gm-localcluster")
+        self.lc: Optional[LocalCluster] = None
+
+    def start(self) -> LocalCluster:
+        self.thread.start()
+        self.lc = self.call(LocalCluster(**self.kw).start())
+        return self.lc
+
+    def call(self, coro, timeout: float = 600):
+        return asyncio.run_coroutine_threadsafe(coro, self.loop).result(timeout)
+
+    def stop(self) -> None:
+        if self.lc is not None:
+            self.call(self.lc.stop())
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.thread.join(timeout=10)

@@ -1,0 +1,257 @@
+"""A fake Kubernetes node: device-plugin ledger, container runtime artifacts, cgroupfs.
+
+The reference tests need a live cluster, real GPUs and root (reference: pkg/util/cgroup/
+cgroup_test.go:37-38 writes the real devices.allow; namespace_test.go:11 hard-codes a PID) —
+SURVEY §4. This node emulates exactly the host surfaces the worker touches:
+
+* the ``amd.com/gpu`` device plugin: capacity, device IDs (PCI BDFs from the node inventory) and
+  an allocation policy (``first-fit`` like a plain kubelet, or ``topology`` = GetPreferredAllocation
+  backed by :mod:`gpumounter_amd.hw.topology`);
+* the kubelet's PodResources ledger (which pod/container holds which device IDs);
+* per-container cgroup directories laid out as kubelet+runc would (cgroup v1 ``devices`` or v2
+  unified; ``cgroupfs`` or ``systemd`` driver) with ``cgroup.procs`` and — for v1 —
+  ``devices.allow/deny/list``;
+* a per-container root filesystem directory (stands in for ``/proc/<pid>/root``) with ``/dev``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import secrets
+import shutil
+import threading
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from gpumounter_amd.hw import topology
+from gpumounter_amd.models.device import AmdGpu, LinkMatrix, normalize_device_id
+from gpumounter_amd.models.pod import QOS_BESTEFFORT, QOS_BURSTABLE, qos_class
+
+FAKE_MARKER = ".gm_fake"
+# runc's default device allow-list (OCI spec defaults), v1 devices.list syntax
+RUNTIME_DEFAULT_RULES = [
+    "c *:* m", "b *:* m", "c 1:3 rwm", "c 1:5 rwm", "c 1:7 rwm", "c 1:8 rwm", "c 1:9 rwm",
+    "c 5:0 rwm", "c 5:1 rwm", "c 5:2 rwm", "c 136:* rwm", "c 10:200 rwm",
+]
+
+
+@dataclass
+class Container:
+    pod_ns: str
+    pod_name: str
+    pod_uid: str
+    name: str
+    id: str
+    runtime: str
+    cgroup_dir: str
+    root_dir: str
+    pids: List[int] = field(default_factory=list)
+
+
+def _esc(s: str) -> str:
+    return s.replace("-", "_")
+
+
+class FakeNode:
+    def __init__(self, name: str, workdir: str, gpus: Sequence[AmdGpu],
+                 links: Optional[LinkMatrix] = None, resource: str = "amd.com/gpu",
+                 cgroup_mode: str = "v1", cgroup_driver: str = "cgroupfs",
+                 runtime: str = "containerd", device_id_kind: str = "bdf",
+                 alloc_policy: str = "topology", labels: Optional[Dict[str, str]] = None) -> None:
+        self.name = name
+        self.resource = resource
+        self.gpus = list(gpus)
+        self.links = links
+        self.cgroup_mode = cgroup_mode
+        self.cgroup_driver = cgroup_driver
+        self.runtime = runtime
+        self.alloc_policy = alloc_policy
+        self.device_id_kind = device_id_kind
+        self.labels = {"kubernetes.io/hostname": name, "gpu-mounter-enable": "enable"}
+        self.labels.update(labels or {})
+        self.workdir = workdir
+        self.cgroup_root = os.path.join(workdir, "cgroup")
+        self.rootfs_root = os.path.join(workdir, "rootfs")
+        os.makedirs(self.cgroup_root, exist_ok=True)
+        os.makedirs(self.rootfs_root, exist_ok=True)
+        if cgroup_mode == "v2":
+            with open(os.path.join(self.cgroup_root, "cgroup.controllers"), "w") as fh:
+                fh.write("cpuset cpu io memory pids\n")
+        else:
+            os.makedirs(os.path.join(self.cgroup_root, "devices"), exist_ok=True)
+        self.images: set = set()
+        self._lock = threading.RLock()
+        # device id → (ns, pod, container)
+        self.allocated: Dict[str, Tuple[str, str, str]] = {}
+        self.containers: Dict[str, Container] = {}  # container id → Container
+        self.alloc_log: List[Tuple[str, str, List[str]]] = []
+
+    # ------------------------------------------------------------------------ device plugin
+    def device_id(self, g: AmdGpu) -> str:
+        return {"bdf": g.bdf, "uuid": g.uuid, "render": f"renderD{g.render_minor}"}[
+            self.device_id_kind]
+
+    @property
+    def capacity(self) -> int:
+        return len(self.gpus)
+
+    def device_ids(self) -> List[str]:
+        return [self.device_id(g) for g in self.gpus]
+
+    def free_ids(self) -> List[str]:
+        with self._lock:
+            return [d for d in self.device_ids() if d not in self.allocated]
+
+    def allocate(self, ns: str, pod: str, container: str, n: int,
+                 preferred: Sequence[str] = ()) -> Optional[List[str]]:
+        """kubelet device-manager Allocate; returns device IDs or None (insufficient)."""
+        with self._lock:
+            free = [g for g in self.gpus if self.device_id(g) not in self.allocated]
+            if len(free) < n:
+                return None
+            chosen: List[AmdGpu]
+            pref = [normalize_device_id(p) for p in preferred]
+            by_id = {normalize_device_id(self.device_id(g)): g for g in free}
+            if pref and all(p in by_id for p in pref) and len(pref) == n:
+                chosen = [by_id[p] for p in pref]
+            elif self.alloc_policy == "topology":
+                # GetPreferredAllocation: co-locate with what the same owner already holds
+                plc = topology.choose(free, n, self.links, policy="xgmi")
+                chosen = [next(g for g in free if g.index == i) for i in plc.chosen]
+            else:
+                chosen = free[:n]
+            ids = [self.device_id(g) for g in chosen]
+            for d in ids:
+                self.allocated[d] = (ns, pod, container)
+            self.alloc_log.append((ns, pod, ids))
+            return ids
+
+    def release_pod(self, ns: str, pod: str) -> List[str]:
+        with self._lock:
+            ids = [d for d, (n, p, _) in self.allocated.items() if n == ns and p == pod]
+            for d in ids:
+                del self.allocated[d]
+            return ids
+
+    def ledger(self) -> Dict[Tuple[str, str], Dict[str, Dict[str, List[str]]]]:
+        """(ns, pod) → container → resource → device IDs (PodResources List view)."""
+        out: Dict[Tuple[str, str], Dict[str, Dict[str, List[str]]]] = {}
+        with self._lock:
+            for d, (ns, pod, c) in sorted(self.allocated.items()):
+                out.setdefault((ns, pod), {}).setdefault(c, {}).setdefault(
+                    self.resource, []).append(d)
+        return out
+
+    def numa_of(self, device_id: str) -> int:
+        for g in self.gpus:
+            if self.device_id(g) == device_id:
+                return g.numa_node
+        return -1
+
+    # ------------------------------------------------------------------------ runtime
+    def pod_cgroup_rel(self, pod: dict) -> str:
+        uid = pod["metadata"]["uid"]
+        qos = qos_class(pod)
+        if self.cgroup_driver == "systemd":
+            parts = ["kubepods.slice"]
+            if qos == QOS_BURSTABLE:
+                parts.append("kubepods-burstable.slice")
+                parts.append(f"kubepods-burstable-pod{_esc(uid)}.slice")
+            elif qos == QOS_BESTEFFORT:
+                parts.append("kubepods-besteffort.slice")
+                parts.append(f"kubepods-besteffort-pod{_esc(uid)}.slice")
+            else:
+                parts.append(f"kubepods-pod{_esc(uid)}.slice")
+            return "/".join(parts)
+        parts = ["kubepods"]
+        if qos == QOS_BURSTABLE:
+            parts.append("burstable")
+        elif qos == QOS_BESTEFFORT:
+            parts.append("besteffort")
+        parts.append(f"pod{uid}")
+        return "/".join(parts)
+
+    def container_cgroup_leaf(self, cid: str) -> str:
+        if self.cgroup_driver == "systemd":
+            prefix = {"docker": "docker", "containerd": "cri-containerd", "cri-o": "crio"}[
+                self.runtime]
+            return f"{prefix}-{cid}.scope"
+        return cid
+
+    def start_container(self, pod: dict, cname: str, pids: Sequence[int] = ()) -> Container:
+        cid = secrets.token_hex(32)
+        rel = self.pod_cgroup_rel(pod) + "/" + self.container_cgroup_leaf(cid)
+        base = os.path.join(self.cgroup_root, "devices") if self.cgroup_mode == "v1" \
+            else self.cgroup_root
+        cg = os.path.join(base, rel)
+        os.makedirs(cg, exist_ok=True)
+        with open(os.path.join(cg, FAKE_MARKER), "w") as fh:
+            fh.write(json.dumps({"mode": self.cgroup_mode, "container": cid}))
+        with open(os.path.join(cg, "cgroup.procs"), "w") as fh:
+            fh.write("".join(f"{p}\n" for p in pids))
+        if self.cgroup_mode == "v1":
+            for f in ("devices.allow", "devices.deny"):
+                open(os.path.join(cg, f), "w").close()
+            with open(os.path.join(cg, "devices.list"), "w") as fh:
+                fh.write("\n".join(RUNTIME_DEFAULT_RULES) + "\n")
+        root = os.path.join(self.rootfs_root, cid)
+        os.makedirs(os.path.join(root, "dev"), exist_ok=True)
+        c = Container(pod["metadata"]["namespace"], pod["metadata"]["name"],
+                      pod["metadata"]["uid"], cname, cid, self.runtime, cg, root, list(pids))
+        with self._lock:
+            self.containers[cid] = c
+        return c
+
+    def set_container_pids(self, cid: str, pids: Sequence[int]) -> None:
+        with self._lock:
+            c = self.containers[cid]
+            c.pids = list(pids)
+            with open(os.path.join(c.cgroup_dir, "cgroup.procs"), "w") as fh:
+                fh.write("".join(f"{p}\n" for p in pids))
+
+    def stop_pod_containers(self, ns: str, pod: str) -> None:
+        with self._lock:
+            for cid, c in list(self.containers.items()):
+                if c.pod_ns == ns and c.pod_name == pod:
+                    shutil.rmtree(c.cgroup_dir, ignore_errors=True)
+                    # prune empty pod-level cgroup dir like kubelet does
+                    parent = os.path.dirname(c.cgroup_dir)
+                    try:
+                        if not [e for e in os.listdir(parent) if not e.startswith(".")]:
+                            shutil.rmtree(parent, ignore_errors=True)
+                    except OSError:
+                        pass
+                    shutil.rmtree(c.root_dir, ignore_errors=True)
+                    del self.containers[cid]
+
+    def container(self, cid: str) -> Optional[Container]:
+        with self._lock:
+            return self.containers.get(cid)
+
+    # ------------------------------------------------------------------------ audit helpers
+    @staticmethod
+    def v1_effective_extra_rules(cgdir: str) -> Dict[str, int]:
+        """Net allow count per rule written by the worker (allow lines minus deny lines)."""
+        net: Dict[str, int] = {}
+        for fname, sign in (("devices.allow", 1), ("devices.deny", -1)):
+            try:
+                with open(os.path.join(cgdir, fname)) as fh:
+                    for line in fh:
+                        line = line.strip()
+                        if line:
+                            net[line] = net.get(line, 0) + sign
+            except FileNotFoundError:
+                pass
+        return net
+
+    def container_devices(self, cid: str) -> List[str]:
+        """Device node paths present in a container's /dev (relative, sorted)."""
+        c = self.container(cid)
+        if c is None:
+            return []
+        out = []
+        dev = os.path.join(c.root_dir, "dev")
+        for dirpath, _, files in os.walk(dev):
+            for f in files:
+                out.append(os.path.relpath(os.path.join(dirpath, f), c.root_dir))
+        return sorted(out)

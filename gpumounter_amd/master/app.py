@@ -1,0 +1,321 @@
+"""Master HTTP API — reference-compatible routes, status codes and bodies, plus JSON extensions.
+
+Reference: cmd/GPUMounter-master/main.go (httprouter on ``:8080``):
+``GET /`` (19-22), ``GET /addgpu/namespace/:namespace/pod/:pod/gpu/:gpuNum/isEntireMount/
+:isEntireMount`` (24-117) and ``POST /removegpu/namespace/:namespace/pod/:pod/force/:force`` with a
+repeated ``uuids`` form field (119-225). For every request the reference GETs the pod, LISTs all
+worker pods (``findAllWorker``, 248-268) and dials a fresh insecure gRPC connection without a
+deadline (82-96, 185-199). Here worker endpoints come from a watch cache, gRPC channels are pooled
+per worker with a deadline, and the response is plain text exactly as the reference wrote it unless
+the client sends ``Accept: application/json`` (then: result, devices, per-stage timings).
+
+Extensions: ``GET /api/v1/namespaces/{ns}/pods/{pod}/gpus`` (a pod's GPUs),
+``GET /api/v1/nodes/{node}/gpus`` (worker NodeService), ``/healthz``, ``/metrics``.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import time
+from typing import Dict, Optional, Tuple
+
+import grpc
+from aiohttp import web
+
+from gpumounter_amd.api import gpu_mount as api
+from gpumounter_amd.cluster.informer import PodInformer
+from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.utils import log
+from gpumounter_amd.utils.metrics import Metrics
+
+_log = log.get("master")
+
+ANN_WORKER_PORT = "gpumounter.amd.com/grpc-port"
+_TRUE = {"1", "t", "T", "TRUE", "true", "True"}
+_FALSE = {"0", "f", "F", "FALSE", "false", "False"}
+
+
+def parse_go_bool(s: str) -> Optional[bool]:
+    """Go ``strconv.ParseBool`` (reference main.go:38,140)."""
+    if s in _TRUE:
+        return True
+    if s in _FALSE:
+        return False
+    return None
+
+
+def parse_go_int32(s: str) -> Optional[int]:
+    """Go ``strconv.ParseInt(s, 10, 32)`` (reference main.go:31)."""
+    if not s or s.strip() != s:
+        return None
+    body = s[1:] if s[0] in "+-" else s
+    if not body.isdigit() or not body.isascii():
+        return None
+    v = int(s)
+    if not -(2 ** 31) <= v < 2 ** 31:
+        return None
+    return v
+
+
+def _text(body: str, status: int = 200) -> web.Response:
+    # Go's http.Error / fmt.Fprintf write text/plain with a trailing newline
+    return web.Response(text=body if body.endswith("\n") else body + "\n", status=status,
+                        content_type="text/plain", charset="utf-8")
+
+
+class WorkerDirectory:
+    """node name → worker gRPC target, from a watch on the worker DaemonSet pods."""
+
+    def __init__(self, kube: KubeClient, namespace: str, label: str, default_port: int) -> None:
+        self.informer = PodInformer(kube, namespace, label)
+        self.default_port = default_port
+        self._channels: Dict[str, grpc.aio.Channel] = {}
+        self._loop = None
+
+    async def start(self) -> None:
+        await self.informer.start()
+
+    async def stop(self) -> None:
+        await self.informer.stop()
+        for ch in self._channels.values():
+            await ch.close()
+        self._channels.clear()
+
+    def target(self, node: str) -> Optional[str]:
+        best = None
+        for p in self.informer.cache.values():
+            if podu.node_of(p) != node or podu.is_terminating(p):
+                continue
+            ip = p.get("status", {}).get("podIP")
+            if not ip or podu.phase_of(p) != "Running":
+                continue
+            port = (p["metadata"].get("annotations") or {}).get(ANN_WORKER_PORT,
+                                                                 str(self.default_port))
+            best = f"{ip}:{port}"
+        return best
+
+    def channel(self, target: str) -> grpc.aio.Channel:
+        loop = asyncio.get_running_loop()
+        if self._loop is not loop:
+            self._channels = {}
+            self._loop = loop
+        ch = self._channels.get(target)
+        if ch is None:
+            ch = grpc.aio.insecure_channel(target, options=[
+                ("grpc.keepalive_time_ms", 30000), ("grpc.enable_retries", 1)])
+            self._channels[target] = ch
+        return ch
+
+
+class Master:
+    def __init__(self, cfg, kube: Optional[KubeClient] = None) -> None:
+        self.cfg = cfg
+        self.kube = kube or KubeClient.from_config(cfg)
+        self.workers = WorkerDirectory(self.kube, cfg.worker_namespace, cfg.worker_label,
+                                       cfg.worker_port)
+        self.metrics = Metrics()
+        self.runner: Optional[web.AppRunner] = None
+        self.port = 0
+
+    # ------------------------------------------------------------------------ app
+    def app(self) -> web.Application:
+        app = web.Application()
+        r = app.router
+        r.add_get("/", self.index)
+        r.add_get("/addgpu/namespace/{namespace}/pod/{pod}/gpu/{gpuNum}/isEntireMount/"
+                  "{isEntireMount}", self.add_gpu)
+        r.add_post("/removegpu/namespace/{namespace}/pod/{pod}/force/{force}", self.remove_gpu)
+        r.add_get("/api/v1/namespaces/{namespace}/pods/{pod}/gpus", self.pod_gpus)
+        r.add_get("/api/v1/nodes/{node}/gpus", self.node_gpus)
+        r.add_get("/healthz", lambda req: web.Response(text="ok"))
+        r.add_get("/metrics", lambda req: web.Response(body=self.metrics.render(),
+                                                       content_type="text/plain"))
+        return app
+
+    async def start(self, port: Optional[int] = None) -> None:
+        await self.workers.start()
+        self.runner = web.AppRunner(self.app(), access_log=None)
+        await self.runner.setup()
+        site = web.TCPSite(self.runner, self.cfg.master_host,
+                           self.cfg.master_port if port is None else port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+        _log.info("master serving HTTP :%d", self.port)
+
+    async def stop(self) -> None:
+        if self.runner is not None:
+            await self.runner.cleanup()
+        await self.workers.stop()
+        await self.kube.close()
+
+    # ------------------------------------------------------------------------ handlers
+    async def index(self, request: web.Request) -> web.Response:
+        return _text("This is gpu mounter api!")
+
+    @staticmethod
+    def _wants_json(request: web.Request) -> bool:
+        return "application/json" in request.headers.get("Accept", "")
+
+    def _reply(self, request, route: str, status: int, text: str, payload: dict) -> web.Response:
+        self.metrics.http_requests.labels(route=route, code=str(status)).inc()
+        if self._wants_json(request):
+            payload = dict(payload)
+            payload.setdefault("message", text.rstrip("\n"))
+            payload["code"] = status
+            return web.json_response(payload, status=status)
+        return _text(text, status)
+
+    async def _locate(self, request, route: str, ns: str, name: str
+                      ) -> Tuple[Optional[dict], Optional[str], Optional[web.Response]]:
+        try:
+            pod = await self.kube.get_pod(ns, name)
+        except NotFound:
+            return None, None, self._reply(request, route, 404,
+                                           f"No pod: {name} in namespace: {ns}", {})
+        except ApiError as e:
+            return None, None, self._reply(request, route, 500, str(e), {})
+        node = podu.node_of(pod)
+        target = self.workers.target(node)
+        if target is None:
+            _log.error("no gpu mounter worker on node %r", node)
+            return pod, None, self._reply(request, route, 500, "Service Internal Error",
+                                          {"error": f"no worker on node {node!r}"})
+        return pod, target, None
+
+    async def add_gpu(self, request: web.Request) -> web.Response:
+        route = "addgpu"
+        rid = log.new_request_id("add")
+        mi = request.match_info
+        ns, name = mi["namespace"], mi["pod"]
+        n = parse_go_int32(mi["gpuNum"])
+        if n is None:
+            return self._reply(request, route, 400, f"Invalid param gpuNum: {mi['gpuNum']}", {})
+        entire = parse_go_bool(mi["isEntireMount"])
+        if entire is None:
+            return self._reply(request, route, 400,
+                               f"Invalid param isEntireMount: {mi['isEntireMount']}"
+                               "(should be true or false)", {})
+        if n <= 0:
+            # the reference forwarded 0 and the worker divided by zero (SURVEY defect 6)
+            return self._reply(request, route, 400, f"Invalid param gpuNum: {mi['gpuNum']}", {})
+        t0 = time.perf_counter()
+        pod, target, err = await self._locate(request, route, ns, name)
+        if err is not None:
+            return err
+        stub = self.workers.channel(target).unary_unary(
+            api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
+            response_deserializer=api.AddGPUResponse.FromString)
+        try:
+            resp = await stub(api.AddGPURequest(pod_name=name, namespace=ns, gpu_num=n,
+                                                is_entire_mount=entire, request_id=rid,
+                                                container=request.query.get("container", "")),
+                              timeout=self.cfg.rpc_timeout_s)
+        except grpc.aio.AioRpcError as e:
+            _log.error("AddGPU rpc to %s failed: %s %s", target, e.code().name, e.details())
+            code = 400 if e.code() == grpc.StatusCode.INVALID_ARGUMENT else 500
+            body = "Service Internal Error" if code == 500 else e.details()
+            return self._reply(request, route, code, body, {"error": e.details()})
+        payload = self._payload(resp, t0)
+        node = podu.node_of(pod)
+        if resp.add_gpu_result == api.ADD_SUCCESS:
+            return self._reply(request, route, 200, "Add GPU Success", payload)
+        if resp.add_gpu_result == api.ADD_INSUFFICIENT:
+            return self._reply(request, route, 500, f"Insufficient GPU on Node: {node}", payload)
+        if resp.add_gpu_result == api.ADD_POD_NOT_FOUND:
+            return self._reply(request, route, 400, f"No Pod{name} on Node: {node}", payload)
+        return self._reply(request, route, 500, "Service Internal Error", payload)
+
+    async def remove_gpu(self, request: web.Request) -> web.Response:
+        route = "removegpu"
+        rid = log.new_request_id("rm")
+        mi = request.match_info
+        ns, name = mi["namespace"], mi["pod"]
+        try:
+            form = await request.post()
+        except Exception:  # noqa: BLE001
+            return self._reply(request, route, 500, "Service Internal Error", {})
+        uuids = list(form.getall("uuids", [])) + list(request.query.getall("uuids", []))
+        if not uuids:
+            return self._reply(request, route, 400, "Invalid parameter", {})
+        force = parse_go_bool(mi["force"])
+        if force is None:
+            return self._reply(request, route, 400,
+                               f"Invalid parameter force: {mi['force']}(should be true or false)",
+                               {})
+        t0 = time.perf_counter()
+        pod, target, err = await self._locate(request, route, ns, name)
+        if err is not None:
+            return err
+        stub = self.workers.channel(target).unary_unary(
+            api.REMOVE_GPU, request_serializer=api.RemoveGPURequest.SerializeToString,
+            response_deserializer=api.RemoveGPUResponse.FromString)
+        try:
+            resp = await stub(api.RemoveGPURequest(pod_name=name, namespace=ns, uuids=uuids,
+                                                   force=force, request_id=rid,
+                                                   container=request.query.get("container", "")),
+                              timeout=self.cfg.rpc_timeout_s)
+        except grpc.aio.AioRpcError as e:
+            _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name, e.details())
+            return self._reply(request, route, 500, "Service Internal Error",
+                               {"error": e.details()})
+        payload = self._payload(resp, t0)
+        node = podu.node_of(pod)
+        r = resp.remove_gpu_result
+        if r == api.REMOVE_SUCCESS:
+            return self._reply(request, route, 200, "Remove GPU Success", payload)
+        if r == api.REMOVE_POD_NOT_FOUND:
+            return self._reply(request, route, 400, f"No Pod{name} on Node: {node}", payload)
+        if r == api.REMOVE_BUSY:
+            return self._reply(request, route, 400,
+                               f"Pod: {name} has running processes on GPU: {', '.join(uuids)}",
+                               payload)
+        if r == api.REMOVE_GPU_NOT_FOUND:
+            return self._reply(request, route, 400, f"Invalid UUIDs: {', '.join(uuids)}", payload)
+        return self._reply(request, route, 500, "Service Internal Error", payload)
+
+    @staticmethod
+    def _payload(resp, t0: float) -> dict:
+        from google.protobuf import json_format
+        d = json_format.MessageToDict(resp, preserving_proto_field_name=True,
+                                     always_print_fields_with_no_presence=True)
+        d["master_ms"] = (time.perf_counter() - t0) * 1e3
+        return d
+
+    async def node_gpus(self, request: web.Request) -> web.Response:
+        node = request.match_info["node"]
+        target = self.workers.target(node)
+        if target is None:
+            return web.json_response({"error": f"no worker on node {node}"}, status=404)
+        stub = self.workers.channel(target).unary_unary(
+            api.NODE_STATUS, request_serializer=api.NodeStatusRequest.SerializeToString,
+            response_deserializer=api.NodeStatusResponse.FromString)
+        resp = await stub(api.NodeStatusRequest(
+            include_processes=request.query.get("processes") == "1"), timeout=30)
+        return web.json_response(json.loads(resp.json))
+
+    async def pod_gpus(self, request: web.Request) -> web.Response:
+        ns, name = request.match_info["namespace"], request.match_info["pod"]
+        try:
+            pod = await self.kube.get_pod(ns, name)
+        except NotFound:
+            return web.json_response({"error": "pod not found"}, status=404)
+        target = self.workers.target(podu.node_of(pod))
+        if target is None:
+            return web.json_response({"error": "no worker"}, status=500)
+        stub = self.workers.channel(target).unary_unary(
+            api.NODE_STATUS, request_serializer=api.NodeStatusRequest.SerializeToString,
+            response_deserializer=api.NodeStatusResponse.FromString)
+        st = json.loads((await stub(api.NodeStatusRequest(), timeout=30)).json)
+        mine = [g for g in st["gpus"] if g.get("pod_name", "").startswith(name)]
+        return web.json_response({"pod": f"{ns}/{name}", "node": podu.node_of(pod),
+                                  "gpus": mine})
+
+
+async def serve(cfg) -> None:
+    m = Master(cfg)
+    await m.start()
+    try:
+        await asyncio.Event().wait()
+    finally:
+        await m.stop()

@@ -1,0 +1,294 @@
+"""Container cgroup resolution and device-access backends (cgroup v1 and v2).
+
+Reference: the cgroup path is *computed* from the pod QoS and an env-selected driver, assuming
+``docker-<id>.scope`` for systemd and the v1 ``/sys/fs/cgroup/devices`` mount only; rules are
+written by forking ``sh -c "echo 'c 195:N rw' > …/devices.allow"`` (reference:
+pkg/util/cgroup/cgroup.go:78-169). Here:
+
+* :class:`CgroupResolver` auto-detects v1/v2 and the driver, tries the computed QoS path for every
+  runtime naming scheme (``docker-``, ``cri-containerd-``, ``crio-`` scopes; cgroupfs ids) and
+  falls back to a directory search under the pod cgroup — runtime-agnostic;
+* :class:`V1Backend` writes rules in-process (one ``write(2)`` per rule, C++);
+* :class:`V2BpfBackend` swaps in a generated ``BPF_PROG_TYPE_CGROUP_DEVICE`` allow-list that
+  tail-calls the runtime's original program (C++, raw ``bpf(2)``);
+* :class:`V2RecordingBackend` produces the identical program bytes without loading them (for
+  unprivileged hosts and hermetic tests), storing the rule set next to the fake cgroup.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import glob
+import json
+import os
+from abc import ABC, abstractmethod
+from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
+
+from gpumounter_amd import _native
+from gpumounter_amd.models.device import DeviceNode
+from gpumounter_amd.models.pod import (QOS_BESTEFFORT, QOS_BURSTABLE, ContainerRef, qos_class,
+                                       uid_of)
+from gpumounter_amd.utils import log
+
+_log = log.get("node.cgroup")
+
+RUNTIME_SCOPE_PREFIXES = ("cri-containerd-", "docker-", "crio-", "containerd-", "")
+FAKE_MARKER = ".gm_fake"
+BPF_STATE = "gm.bpf.json"
+
+
+class CgroupError(RuntimeError):
+    pass
+
+
+def _esc(s: str) -> str:
+    return s.replace("-", "_")
+
+
+class CgroupResolver:
+    def __init__(self, root: str = "/sys/fs/cgroup", mode: str = "auto", driver: str = "auto"):
+        self.root = root
+        self.mode = self.detect_mode(root) if mode == "auto" else mode
+        self.base = os.path.join(root, "devices") if self.mode == "v1" else root
+        self.driver = driver
+        self._cache: Dict[Tuple[str, str], str] = {}
+
+    @staticmethod
+    def detect_mode(root: str) -> str:
+        if os.path.isdir(os.path.join(root, "devices")):
+            return "v1"
+        if os.path.exists(os.path.join(root, "cgroup.controllers")):
+            return "v2"
+        # hybrid hosts mount the v1 devices controller; absent both, assume unified
+        return "v2"
+
+    def pod_dirs(self, pod: dict) -> List[str]:
+        uid = uid_of(pod)
+        qos = qos_class(pod)
+        order = [qos] + [q for q in ("Guaranteed", QOS_BURSTABLE, QOS_BESTEFFORT) if q != qos]
+        drivers = ("systemd", "cgroupfs") if self.driver == "auto" else (self.driver,)
+        out = []
+        for q in order:
+            for d in drivers:
+                if d == "systemd":
+                    if q == QOS_BURSTABLE:
+                        rel = f"kubepods.slice/kubepods-burstable.slice/kubepods-burstable-pod{_esc(uid)}.slice"
+                    elif q == QOS_BESTEFFORT:
+                        rel = f"kubepods.slice/kubepods-besteffort.slice/kubepods-besteffort-pod{_esc(uid)}.slice"
+                    else:
+                        rel = f"kubepods.slice/kubepods-pod{_esc(uid)}.slice"
+                else:
+                    if q == QOS_BURSTABLE:
+                        rel = f"kubepods/burstable/pod{uid}"
+                    elif q == QOS_BESTEFFORT:
+                        rel = f"kubepods/besteffort/pod{uid}"
+                    else:
+                        rel = f"kubepods/pod{uid}"
+                out.append(os.path.join(self.base, rel))
+        return out
+
+    def container_dir(self, pod: dict, ctr: ContainerRef) -> str:
+        key = (uid_of(pod), ctr.id)
+        hit = self._cache.get(key)
+        if hit and os.path.isdir(hit):
+            return hit
+        for pdir in self.pod_dirs(pod):
+            if not os.path.isdir(pdir):
+                continue
+            for pre in RUNTIME_SCOPE_PREFIXES:
+                for name in (f"{pre}{ctr.id}.scope", f"{pre}{ctr.id}"):
+                    cand = os.path.join(pdir, name)
+                    if os.path.isdir(cand):
+                        self._cache[key] = cand
+                        return cand
+            # unknown naming scheme: any child dir containing the id
+            for cand in glob.glob(os.path.join(pdir, f"*{ctr.id}*")):
+                if os.path.isdir(cand):
+                    self._cache[key] = cand
+                    return cand
+        raise CgroupError(f"cgroup of container {ctr.name} ({ctr.id[:12]}) of pod "
+                          f"{pod['metadata'].get('namespace')}/{pod['metadata'].get('name')} "
+                          f"not found under {self.base}")
+
+    def forget(self, pod_uid: str) -> None:
+        for k in [k for k in self._cache if k[0] == pod_uid]:
+            del self._cache[k]
+
+    @staticmethod
+    def pids(cgdir: str, recursive: bool = True) -> List[int]:
+        """PIDs in the cgroup (and, for v2 container scopes, its sub-cgroups)."""
+        lib = _native.host()
+        out: List[int] = []
+        dirs = [cgdir]
+        if recursive:
+            for dirpath, dirnames, _ in os.walk(cgdir):
+                for d in dirnames:
+                    dirs.append(os.path.join(dirpath, d))
+        for d in dirs:
+            path = os.path.join(d, "cgroup.procs")
+            if not os.path.exists(path):
+                continue
+            buf = (C.c_int32 * 4096)()
+            n = C.c_int(0)
+            rc = lib.gm_proc_read_pids(path.encode(), buf, 4096, C.byref(n))
+            if rc < 0:
+                raise CgroupError(f"read {path}: {os.strerror(-rc)}")
+            out.extend(int(buf[i]) for i in range(min(n.value, 4096)))
+        return sorted(set(out))
+
+
+# ------------------------------------------------------------------------------ rules
+def rules_for(nodes: Iterable[DeviceNode], allow: bool, access: str = "rw") -> List[_native.DevRule]:
+    acc = 0
+    if "r" in access:
+        acc |= _native.GM_ACC_READ
+    if "w" in access:
+        acc |= _native.GM_ACC_WRITE
+    if "m" in access:
+        acc |= _native.GM_ACC_MKNOD
+    return [_native.DevRule(b"c", acc, 1 if allow else 0, 0, n.major, n.minor) for n in nodes]
+
+
+def _rule_array(rules: Sequence[_native.DevRule]):
+    arr = (_native.DevRule * max(len(rules), 1))()
+    for i, r in enumerate(rules):
+        arr[i] = r
+    return arr
+
+
+def format_rule(r: _native.DevRule) -> str:
+    buf = C.create_string_buffer(64)
+    _native.host().gm_cg1_format_rule(C.byref(r), buf, 64)
+    return buf.value.decode()
+
+
+class DeviceRuleBackend(ABC):
+    name = "abstract"
+
+    @abstractmethod
+    def apply(self, cgdir: str, grant: Sequence[DeviceNode], revoke: Sequence[DeviceNode],
+              desired: Sequence[DeviceNode]) -> None:
+        """Make ``grant`` accessible and ``revoke`` inaccessible. ``desired`` is the complete set
+        of nodes gpumounter wants allowed after the call (full-state backends use it)."""
+
+    @abstractmethod
+    def allowed(self, cgdir: str) -> Set[Tuple[int, int]]:
+        """(major, minor) pairs currently granted by gpumounter."""
+
+
+class V1Backend(DeviceRuleBackend):
+    name = "cgroup-v1"
+
+    def apply(self, cgdir, grant, revoke, desired):
+        rules = rules_for(revoke, allow=False) + rules_for(grant, allow=True)
+        if not rules:
+            return
+        rc = _native.host().gm_cg1_apply(cgdir.encode(), _rule_array(rules), len(rules))
+        if rc < 0:
+            raise CgroupError(f"devices.allow/deny write in {cgdir}: {os.strerror(-rc)}")
+
+    def allowed(self, cgdir):
+        if os.path.exists(os.path.join(cgdir, FAKE_MARKER)):
+            net: Dict[str, int] = {}
+            for fname, sign in (("devices.allow", 1), ("devices.deny", -1)):
+                try:
+                    with open(os.path.join(cgdir, fname)) as fh:
+                        for line in fh:
+                            if line.strip():
+                                net[line.strip()] = net.get(line.strip(), 0) + sign
+                except FileNotFoundError:
+                    pass
+            out = set()
+            for rule, cnt in net.items():
+                if cnt > 0:
+                    parts = rule.split()
+                    if len(parts) == 3 and parts[0] == "c" and "*" not in parts[1]:
+                        ma, mi = parts[1].split(":")
+                        out.add((int(ma), int(mi)))
+            return out
+        out = set()
+        try:
+            with open(os.path.join(cgdir, "devices.list")) as fh:
+                for line in fh:
+                    parts = line.split()
+                    if len(parts) == 3 and parts[0] == "c" and "*" not in parts[1]:
+                        ma, mi = parts[1].split(":")
+                        out.add((int(ma), int(mi)))
+        except FileNotFoundError:
+            pass
+        return out
+
+
+class V2BpfBackend(DeviceRuleBackend):
+    """Real eBPF backend (needs CAP_SYS_ADMIN + CAP_BPF on a cgroup2 mount)."""
+
+    name = "cgroup-v2-bpf"
+
+    def apply(self, cgdir, grant, revoke, desired):
+        lib = _native.host()
+        if not desired:
+            rc = lib.gm_bpf_dev_restore(cgdir.encode())
+            if rc < 0:
+                raise CgroupError(f"bpf restore on {cgdir}: {os.strerror(-rc)}")
+            return
+        rules = rules_for(desired, allow=True)
+        pid, chained = C.c_uint32(0), C.c_uint32(0)
+        rc = lib.gm_bpf_dev_install(cgdir.encode(), _rule_array(rules), len(rules), C.byref(pid),
+                                    C.byref(chained))
+        if rc < 0:
+            raise CgroupError(f"bpf install on {cgdir}: {os.strerror(-rc)}")
+        log.kv(_log, 10, "bpf program installed", cgroup=cgdir, prog_id=pid.value,
+               chained=chained.value, rules=len(rules))
+
+    def allowed(self, cgdir):
+        # the loaded program is not introspected; the ledger is the source of truth for v2
+        state = os.path.join(cgdir, BPF_STATE)
+        return V2RecordingBackend().allowed(cgdir) if os.path.exists(state) else set()
+
+
+def build_program(nodes: Sequence[DeviceNode], chained: bool) -> List[int]:
+    rules = rules_for(nodes, allow=True)
+    lib = _native.host()
+    need = -lib.gm_bpf_dev_build(_rule_array(rules), len(rules), 0 if chained else 1,
+                                 -2 if chained else -1, None, 0)
+    buf = (C.c_uint64 * need)()
+    n = lib.gm_bpf_dev_build(_rule_array(rules), len(rules), 0 if chained else 1,
+                             -2 if chained else -1, buf, need)
+    if n < 0:
+        raise CgroupError("bpf program build failed")
+    return [int(buf[i]) for i in range(n)]
+
+
+class V2RecordingBackend(DeviceRuleBackend):
+    """Builds the exact program the v2 backend would load and records it beside the cgroup."""
+
+    name = "cgroup-v2-recording"
+
+    def apply(self, cgdir, grant, revoke, desired):
+        path = os.path.join(cgdir, BPF_STATE)
+        if not desired:
+            if os.path.exists(path):
+                os.unlink(path)
+            return
+        prog = build_program(desired, chained=True)
+        state = {"rules": [[n.major, n.minor, n.path] for n in desired],
+                 "chained": "runtime-default", "insns": [f"{i:016x}" for i in prog]}
+        tmp = path + ".tmp"
+        with open(tmp, "w") as fh:
+            json.dump(state, fh)
+        os.replace(tmp, path)  # atomic like BPF_F_REPLACE
+
+    def allowed(self, cgdir):
+        try:
+            with open(os.path.join(cgdir, BPF_STATE)) as fh:
+                st = json.load(fh)
+        except FileNotFoundError:
+            return set()
+        return {(int(a), int(b)) for a, b, _ in st["rules"]}
+
+
+def make_backend(mode: str, emulate: bool) -> DeviceRuleBackend:
+    if mode == "v1":
+        return V1Backend()
+    if emulate:
+        return V2RecordingBackend()
+    return V2BpfBackend()

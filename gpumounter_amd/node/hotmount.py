@@ -1,0 +1,175 @@
+"""Hot-mount transactions: grant + inject on attach, revoke + unlink on detach, with rollback.
+
+Reference: ``MountGPU`` = container ID (docker only) → cgroup path → ``devices.allow`` → first PID
+→ nsenter mknod (reference: pkg/util/util.go:17-71); ``UnmountGPU`` = busy check → ``devices.deny``
+→ ``rm`` → ``kill`` (util.go:73-147). Partial failures are not rolled back (server.go:86-91 only
+deletes slave pods — SURVEY §2.6 defect 12) and only ``ContainerStatuses[0]`` is handled
+(defect 8).
+
+Here one transaction covers every running container of the pod (or a named one), computes the
+exact node set from the ledger (the pod's own device-plugin GPUs are never touched, ``/dev/kfd``
+is granted with the first hot-mounted GPU and revoked with the last), and undoes completed steps
+in reverse order if any step fails.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+from gpumounter_amd.hw.inventory import Inventory
+from gpumounter_amd.models.device import AmdGpu, DeviceNode, kfd_node
+from gpumounter_amd.models.pod import ContainerRef, running_containers
+from gpumounter_amd.node.cgroup import CgroupResolver, DeviceRuleBackend
+from gpumounter_amd.node.devnodes import CREATED, DevNodeWriter, Target
+from gpumounter_amd.utils import log, trace
+
+_log = log.get("node.hotmount")
+
+
+class MountError(RuntimeError):
+    pass
+
+
+@dataclass
+class ContainerTarget:
+    ref: ContainerRef
+    cgdir: str
+    target: Target
+    pids: List[int] = field(default_factory=list)
+
+
+@dataclass
+class AuditIssue:
+    container: str
+    kind: str        # missing_rule | missing_node | stale_rule | stale_node
+    path: str
+    major: int
+    minor: int
+
+
+class HotMount:
+    def __init__(self, cfg, inv: Inventory, resolver: CgroupResolver, backend: DeviceRuleBackend,
+                 writer: DevNodeWriter) -> None:
+        self.cfg = cfg
+        self.inv = inv
+        self.resolver = resolver
+        self.backend = backend
+        self.writer = writer
+
+    # ------------------------------------------------------------------------ node sets
+    def kfd(self) -> DeviceNode:
+        return kfd_node(self.inv.kfd_major)
+
+    def gpu_nodes(self, gpus: Sequence[AmdGpu]) -> List[DeviceNode]:
+        out: List[DeviceNode] = []
+        for g in sorted(gpus, key=lambda g: g.index):
+            out.extend(g.device_nodes(self.cfg.drm_major, self.cfg.inject_card_nodes,
+                                      self.cfg.device_file_mode))
+        return out
+
+    def managed_nodes(self, hot: Sequence[AmdGpu], base: Sequence[AmdGpu]) -> List[DeviceNode]:
+        """Nodes gpumounter owns for a pod holding ``hot`` hot-mounted GPUs and ``base`` own GPUs."""
+        base_keys = {(n.major, n.minor) for n in self.gpu_nodes(base)}
+        nodes = [n for n in self.gpu_nodes(hot) if (n.major, n.minor) not in base_keys]
+        if hot and not base:
+            nodes.insert(0, self.kfd())
+        return nodes
+
+    # ------------------------------------------------------------------------ targets
+    def targets(self, pod: dict, container: str = "") -> List[ContainerTarget]:
+        refs = [r for r in running_containers(pod, container) if r.running]
+        if not refs:
+            raise MountError(f"pod {pod['metadata'].get('name')} has no running container"
+                             + (f" named {container}" if container else ""))
+        out = []
+        for r in refs:
+            cgdir = self.resolver.container_dir(pod, r)
+            pids = self.resolver.pids(cgdir)
+            if self.cfg.container_root_prefix:
+                t = Target(root=os.path.join(self.cfg.container_root_prefix, r.id))
+            else:
+                t = Target(pid=pids[0] if pids else 0)
+            out.append(ContainerTarget(r, cgdir, t, pids))
+        return out
+
+    # ------------------------------------------------------------------------ attach
+    def attach(self, pod: dict, new: Sequence[AmdGpu], have: Sequence[AmdGpu],
+               base: Sequence[AmdGpu] = (), container: str = "") -> List[ContainerTarget]:
+        before = self.managed_nodes(have, base)
+        after = self.managed_nodes(list(have) + list(new), base)
+        before_keys = {(n.major, n.minor) for n in before}
+        grant = [n for n in after if (n.major, n.minor) not in before_keys]
+        with trace.span("resolve"):
+            targets = self.targets(pod, container)
+        done: List[tuple] = []  # (target, granted, created_nodes)
+        try:
+            for t in targets:
+                with trace.span("cgroup_rule", backend=self.backend.name, rules=len(grant)):
+                    self.backend.apply(t.cgdir, grant, [], after)
+                done.append((t, grant, []))
+                with trace.span("devnodes", nodes=len(after)):
+                    res = self.writer.create(t.target, after)
+                done[-1] = (t, grant, [n for n, r in zip(after, res) if r == CREATED])
+        except Exception as e:
+            self._rollback_attach(done, before)
+            raise MountError(f"attach failed, rolled back: {e}") from e
+        return targets
+
+    def _rollback_attach(self, done, before: List[DeviceNode]) -> None:
+        for t, granted, created in reversed(done):
+            try:
+                self.writer.remove(t.target, created)
+            except Exception as e:  # noqa: BLE001
+                _log.error("rollback unlink in %s failed: %s", t.ref.name, e)
+            try:
+                self.backend.apply(t.cgdir, [], granted, before)
+            except Exception as e:  # noqa: BLE001
+                _log.error("rollback revoke in %s failed: %s", t.cgdir, e)
+
+    # ------------------------------------------------------------------------ detach
+    def detach(self, pod: dict, remove: Sequence[AmdGpu], keep: Sequence[AmdGpu],
+               base: Sequence[AmdGpu] = (), container: str = "",
+               targets: Optional[List[ContainerTarget]] = None) -> List[ContainerTarget]:
+        before = self.managed_nodes(list(keep) + list(remove), base)
+        after = self.managed_nodes(keep, base)
+        after_keys = {(n.major, n.minor) for n in after}
+        revoke = [n for n in before if (n.major, n.minor) not in after_keys]
+        if targets is None:
+            with trace.span("resolve"):
+                targets = self.targets(pod, container)
+        for t in targets:
+            # reference order: deny → rm → kill (util.go:112,131,139)
+            with trace.span("cgroup_rule", backend=self.backend.name, rules=len(revoke)):
+                self.backend.apply(t.cgdir, [], revoke, after)
+            with trace.span("devnodes", nodes=len(revoke)):
+                self.writer.remove(t.target, revoke)
+        return targets
+
+    # ------------------------------------------------------------------------ audit
+    def audit(self, pod: dict, hot: Sequence[AmdGpu], base: Sequence[AmdGpu] = (),
+              container: str = "") -> List[AuditIssue]:
+        """Compare the expected state (from the ledger) with cgroup rules and /dev contents."""
+        want = self.managed_nodes(hot, base)
+        want_keys = {(n.major, n.minor) for n in want}
+        issues: List[AuditIssue] = []
+        all_gpu_nodes = self.gpu_nodes(self.inv.gpus()) + [self.kfd()]
+        base_keys = {(n.major, n.minor) for n in self.gpu_nodes(base)}
+        for t in self.targets(pod, container):
+            allowed = self.backend.allowed(t.cgdir)
+            for n in want:
+                if (n.major, n.minor) not in allowed:
+                    issues.append(AuditIssue(t.ref.name, "missing_rule", n.path, n.major, n.minor))
+                if not self.writer.present(t.target, n):
+                    issues.append(AuditIssue(t.ref.name, "missing_node", n.path, n.major, n.minor))
+            for n in all_gpu_nodes:
+                k = (n.major, n.minor)
+                if k in want_keys or k in base_keys:
+                    continue
+                if base and n.path == "/dev/kfd":
+                    continue
+                if k in allowed:
+                    issues.append(AuditIssue(t.ref.name, "stale_rule", n.path, n.major, n.minor))
+                if self.writer.present(t.target, n):
+                    issues.append(AuditIssue(t.ref.name, "stale_node", n.path, n.major, n.minor))
+        return issues

@@ -1,0 +1,175 @@
+"""Reconciler: repairs drift between the placeholder ledger and the node's actual device state.
+
+The reference has no reconciliation: a container restart drops the mknod'd nodes
+while the slave pod keeps the GPU, a worker crash mid-attach leaves rules behind, and the
+cross-namespace ownerReference GC can delete slave pods under a live tenant (defects 4, 12).
+Every ``reconcile_period_s`` (and on demand) this loop, per node:
+
+1. deletes placeholders whose owner pod is gone or was replaced (UID mismatch) → ``owner_gone``;
+2. deletes placeholders stuck Unschedulable/Failed that no in-flight attach is waiting on;
+3. for every live owner, audits cgroup rules + ``/dev`` nodes against the ledger and re-applies
+   missing ones (resume after a container restart) or revokes stale ones;
+4. for every other running pod on the node, revokes hot-mount rules/nodes that no placeholder
+   backs any more (orphans) — the "zero orphaned cgroup entries" invariant.
+All repairs take the same per-pod lock as AddGPU/RemoveGPU.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List
+
+from gpumounter_amd.cluster.kube import NotFound
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.models.types import ANN_OWNER_UID
+from gpumounter_amd.node.hotmount import MountError
+from gpumounter_amd.utils import log
+
+_log = log.get("worker.reconciler")
+
+
+@dataclass
+class ReconcileReport:
+    owner_gone: List[str] = field(default_factory=list)
+    stuck: List[str] = field(default_factory=list)
+    repaired: List[str] = field(default_factory=list)
+    revoked: List[str] = field(default_factory=list)
+    orphans: int = 0
+    errors: List[str] = field(default_factory=list)
+
+    def to_dict(self) -> dict:
+        return self.__dict__.copy()
+
+
+class Reconciler:
+    def __init__(self, service, period_s: float = 30.0, stuck_after_s: float = 120.0) -> None:
+        self.svc = service
+        self.period_s = period_s
+        self.stuck_after_s = stuck_after_s
+        self._task = None
+        self.last: ReconcileReport = ReconcileReport()
+        self._first_seen: Dict[str, float] = {}
+
+    async def start(self) -> None:
+        self._task = asyncio.ensure_future(self._loop())
+
+    async def stop(self) -> None:
+        if self._task:
+            self._task.cancel()
+            try:
+                await self._task
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                pass
+
+    async def _loop(self) -> None:
+        while True:
+            await asyncio.sleep(self.period_s)
+            try:
+                await self.run_once()
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                _log.exception("reconcile failed: %s", e)
+
+    async def run_once(self) -> ReconcileReport:
+        svc = self.svc
+        rep = ReconcileReport()
+        m = svc.metrics
+        placeholders = svc.ph.informer.list(lambda p: not p["metadata"].get("deletionTimestamp"))
+        by_owner: Dict[tuple, List[dict]] = {}
+        for p in placeholders:
+            ann = p["metadata"].get("annotations") or {}
+            owner = (ann.get("gpumounter.amd.com/owner-name", ""),
+                     (p["metadata"].get("labels") or {}).get("gpumounter.amd.com/owner-namespace", ""),
+                     ann.get(ANN_OWNER_UID, ""))
+            by_owner.setdefault(owner, []).append(p)
+        now = time.monotonic()
+        for (oname, ons, ouid), phs in by_owner.items():
+            try:
+                owner = await svc.kube.get_pod(ons, oname)
+            except NotFound:
+                owner = None
+            lock = svc.pod_lock(ons, oname)
+            if owner is None or podu.uid_of(owner) != ouid or podu.phase_of(owner) in (
+                    "Succeeded", "Failed"):
+                async with lock:
+                    for p in phs:
+                        rep.owner_gone.append(p["metadata"]["name"])
+                        m.orphans.labels(kind="owner_gone").inc()
+                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in phs], wait=False)
+                continue
+            if lock.locked():
+                continue  # an attach/detach is in flight for this owner
+            async with lock:
+                # stuck placeholders (never admitted)
+                stuck = []
+                for p in phs:
+                    name = p["metadata"]["name"]
+                    if podu.is_unschedulable(p) or podu.phase_of(p) == "Failed":
+                        first = self._first_seen.setdefault(name, now)
+                        if now - first >= self.stuck_after_s:
+                            stuck.append(p)
+                if stuck:
+                    rep.stuck += [p["metadata"]["name"] for p in stuck]
+                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in stuck], wait=False)
+                if podu.phase_of(owner) != "Running":
+                    continue
+                try:
+                    st = await svc.pod_state(owner)
+                    issues = svc.hm.audit(owner, st.hot, st.own)
+                except (MountError, Exception) as e:  # noqa: BLE001
+                    rep.errors.append(f"{ons}/{oname}: {e}")
+                    continue
+                if issues:
+                    rep.orphans += sum(1 for i in issues if i.kind.startswith("stale"))
+                    try:
+                        svc.hm.attach(owner, st.hot, [], st.own)  # idempotent re-grant/re-create
+                        stale = [i for i in issues if i.kind.startswith("stale")]
+                        if stale:
+                            self._revoke_stale(owner, st, stale)
+                        rep.repaired.append(f"{ons}/{oname}")
+                        m.reconcile_actions.labels(action="repair").inc()
+                    except Exception as e:  # noqa: BLE001
+                        rep.errors.append(f"repair {ons}/{oname}: {e}")
+        # pods on this node without placeholders must not keep hot-mount state
+        owners = {(o[1], o[0]) for o in by_owner}
+        for pod in svc.node_pods.list(lambda p: podu.phase_of(p) == "Running"):
+            key = (podu.ns_of(pod), podu.name_of(pod))
+            if key in owners or (pod["metadata"].get("labels") or {}).get("app") == "gpu-pool":
+                continue
+            lock = svc.pod_lock(*key)
+            if lock.locked():
+                continue
+            async with lock:
+                try:
+                    st = await svc.pod_state(pod)
+                    if st.placeholders:
+                        continue
+                    issues = svc.hm.audit(pod, [], st.own)
+                except Exception as e:  # noqa: BLE001
+                    rep.errors.append(f"audit {key}: {e}")
+                    continue
+                stale = [i for i in issues if i.kind.startswith("stale")]
+                if stale:
+                    rep.orphans += len(stale)
+                    m.orphans.labels(kind="stale_state").inc(len(stale))
+                    self._revoke_stale(pod, st, stale)
+                    rep.revoked.append(f"{key[0]}/{key[1]}")
+                    m.reconcile_actions.labels(action="revoke").inc()
+        for name in list(self._first_seen):
+            if not any(p["metadata"]["name"] == name for p in placeholders):
+                del self._first_seen[name]
+        self.last = rep
+        if rep.owner_gone or rep.stuck or rep.repaired or rep.revoked or rep.errors:
+            log.kv(_log, 20, "reconciled", **rep.to_dict())
+        return rep
+
+    def _revoke_stale(self, pod: dict, st, stale) -> None:
+        from gpumounter_amd.models.device import DeviceNode
+        nodes = {(i.major, i.minor): DeviceNode(i.path, i.major, i.minor) for i in stale}
+        hm = self.svc.hm
+        keep = hm.managed_nodes(st.hot, st.own)
+        for t in hm.targets(pod):
+            hm.backend.apply(t.cgdir, [], list(nodes.values()), keep)
+            hm.writer.remove(t.target, list(nodes.values()))

@@ -1,0 +1,363 @@
+"""Worker-side AddGPU / RemoveGPU semantics.
+
+Reference: ``GPUMountImpl.AddGPU`` / ``RemoveGPU`` (reference: pkg/server/gpu-mount/server.go:34-179)
+with the policy helpers ``CanMount`` (pkg/util/util.go:207-226), ``GetMountType``
+(allocator.go:158-187) and ``GetRemoveGPU`` (allocator.go:101-126). Result enums and their meaning
+are identical (see gpumounter_amd/api/gpu_mount.py). Behavioural fixes, each covered by a test:
+
+* per-pod serialization (two concurrent adds on one pod raced in the reference — defect 7);
+* ``gpu_num <= 0`` is rejected (reference: division by zero / silent no-op — defect 6);
+* mount type comes from the placeholders' recorded mode, not from the "fewer slave pods than
+  GPUs" heuristic that misclassifies a pod's own GPUs as an entire mount (defect 5);
+* a pod's own device-plugin GPUs are never counted as hot-mounted nor removable (kept from
+  allocator.go:112-116), and ``/dev/kfd`` is left alone for such pods;
+* the busy check and the kill use one PID snapshot (the reference computed it twice — defect 16);
+* every running container is mounted, not just ``ContainerStatuses[0]`` (defect 8);
+* a failed mount rolls back cgroup rules and device nodes, not only the slave pods (defect 12).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import grpc
+
+from gpumounter_amd.api import gpu_mount as api
+from gpumounter_amd.cluster.informer import PodInformer
+from gpumounter_amd.cluster.kube import KubeClient, NotFound
+from gpumounter_amd.cluster.placeholder import (InsufficientGPU, Placeholder, PlaceholderManager,
+                                                ReserveError)
+from gpumounter_amd.hw import topology
+from gpumounter_amd.hw.inventory import Inventory
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.models.device import AmdGpu, gpus_by_key, normalize_device_id
+from gpumounter_amd.models.types import ERR_INTERNAL, ERR_POLICY, MountType
+from gpumounter_amd.node import procs
+from gpumounter_amd.node.hotmount import HotMount, MountError
+from gpumounter_amd.node.ledger import LedgerClient, LedgerError
+from gpumounter_amd.utils import log, trace
+from gpumounter_amd.utils.metrics import Metrics
+
+_log = log.get("worker.service")
+
+
+class RpcError(Exception):
+    def __init__(self, code: grpc.StatusCode, msg: str):
+        super().__init__(msg)
+        self.code = code
+        self.msg = msg
+
+
+@dataclass
+class PodGpuState:
+    own: List[AmdGpu] = field(default_factory=list)          # device-plugin GPUs of the pod spec
+    hot: List[AmdGpu] = field(default_factory=list)          # hot-mounted via placeholders
+    placeholders: List[Placeholder] = field(default_factory=list)
+    by_placeholder: Dict[Tuple[str, str], List[AmdGpu]] = field(default_factory=dict)
+    mount_type: MountType = MountType.NONE
+    ledger: Dict[Tuple[str, str], List[str]] = field(default_factory=dict)  # snapshot used
+
+
+def can_mount(mount_type: MountType, entire: bool) -> Tuple[bool, str]:
+    """Reference util.go:207-226, same decisions, with a reason string."""
+    if mount_type == MountType.UNKNOWN:
+        return False, "pod mount type is unknown"
+    if mount_type != MountType.NONE and entire:
+        return False, "pod already has hot-mounted GPUs; entire mount needs an unmounted pod"
+    if mount_type == MountType.ENTIRE:
+        return False, "pod is entire-mounted; remove its GPUs before adding more"
+    return True, ""
+
+
+class GpuMountService:
+    def __init__(self, cfg, kube: KubeClient, inv: Inventory, ledger: LedgerClient,
+                 placeholders: PlaceholderManager, hotmount: HotMount, node_pods: PodInformer,
+                 metrics: Optional[Metrics] = None) -> None:
+        self.cfg = cfg
+        self.kube = kube
+        self.inv = inv
+        self.ledger = ledger
+        self.ph = placeholders
+        self.hm = hotmount
+        self.node_pods = node_pods
+        self.metrics = metrics or Metrics()
+        self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}
+        self._alloc_lock = asyncio.Lock()
+
+    # ------------------------------------------------------------------------ helpers
+    def pod_lock(self, ns: str, name: str) -> asyncio.Lock:
+        lk = self._locks.get((ns, name))
+        if lk is None:
+            lk = self._locks[(ns, name)] = asyncio.Lock()
+        return lk
+
+    async def get_pod(self, ns: str, name: str, fresh: bool = False) -> Optional[dict]:
+        if not fresh:
+            p = self.node_pods.get(ns, name)
+            if p is not None and podu.phase_of(p) == "Running":
+                return p
+        try:
+            return await self.kube.get_pod(ns, name)
+        except NotFound:
+            return None
+
+    async def pod_state(self, pod: dict) -> PodGpuState:
+        st = PodGpuState()
+        try:
+            ledger = await self.ledger.by_pod()
+        except LedgerError as e:
+            _log.error("ledger read failed: %s", e)
+            st.mount_type = MountType.UNKNOWN
+            return st
+        st.ledger = ledger
+        keys = gpus_by_key(self.inv.gpus())
+
+        def resolve(ids) -> List[AmdGpu]:
+            out = []
+            for d in ids:
+                g = keys.get(normalize_device_id(d))
+                if g is None:
+                    raise LedgerError(f"device id {d!r} from the kubelet ledger is not a GPU of "
+                                      f"this node's inventory")
+                out.append(g)
+            return out
+
+        try:
+            st.own = resolve(ledger.get((podu.ns_of(pod), podu.name_of(pod)), []))
+            modes = set()
+            for p in self.ph.owned_by(pod):
+                ph = PlaceholderManager.from_pod(p, ledger)
+                gs = resolve(ph.device_ids)
+                st.placeholders.append(ph)
+                st.by_placeholder[(ph.namespace, ph.name)] = gs
+                st.hot.extend(gs)
+                modes.add(ph.mode)
+        except LedgerError as e:
+            _log.error("%s", e)
+            st.mount_type = MountType.UNKNOWN
+            return st
+        if not st.placeholders:
+            st.mount_type = MountType.NONE
+        elif "entire" in modes:
+            st.mount_type = MountType.ENTIRE
+        else:
+            st.mount_type = MountType.SINGLE
+        return st
+
+    @staticmethod
+    def _devices(gs: Sequence[AmdGpu], owner: Dict[int, str]) -> List:
+        return [api.Device(uuid=g.uuid, bdf=g.bdf, index=g.index, render_minor=g.render_minor,
+                           card_minor=g.card_minor, numa_node=g.numa_node,
+                           xgmi_hive_id=g.xgmi_hive_id, placeholder=owner.get(g.index, ""))
+                for g in gs]
+
+    @staticmethod
+    def _timings(root: trace.Span) -> List:
+        return [api.StageTiming(name=k, ms=v) for k, v in root.flat().items()]
+
+    # ------------------------------------------------------------------------ AddGPU
+    async def add_gpu(self, req) -> "api.AddGPUResponse":
+        rid = req.request_id or log.new_request_id("add")
+        with log.with_rid(rid), trace.span("attach", pod=f"{req.namespace}/{req.pod_name}",
+                                           n=req.gpu_num, entire=req.is_entire_mount) as root:
+            resp = await self._add_gpu(req)
+        resp.total_ms = root.duration_ms
+        resp.timings.extend(self._timings(root))
+        result = api.AddGPUResponse.AddGPUResult.Name(resp.add_gpu_result)
+        self.metrics.requests.labels(op="add", result=result).inc()
+        if resp.add_gpu_result == api.ADD_SUCCESS:
+            self.metrics.attach_latency.labels(
+                n_gpus=str(req.gpu_num), mode="entire" if req.is_entire_mount else "single"
+            ).observe(root.duration_ms / 1e3)
+            self.metrics.observe_trace("attach", root)
+        return resp
+
+    async def _add_gpu(self, req):
+        n = int(req.gpu_num)
+        if n <= 0 or n > self.cfg.max_gpus_per_request:
+            raise RpcError(grpc.StatusCode.INVALID_ARGUMENT, f"invalid gpu_num {n}")
+        with trace.span("pod_lookup"):
+            pod = await self.get_pod(req.namespace, req.pod_name)
+        if pod is None:
+            _log.info("no such pod %s/%s", req.namespace, req.pod_name)
+            return api.AddGPUResponse(add_gpu_result=api.ADD_POD_NOT_FOUND)
+        if self.cfg.node_name and podu.node_of(pod) != self.cfg.node_name:
+            raise RpcError(grpc.StatusCode.FAILED_PRECONDITION,
+                           f"pod is on node {podu.node_of(pod)!r}, this worker serves "
+                           f"{self.cfg.node_name!r}")
+        async with self.pod_lock(req.namespace, req.pod_name):
+            if podu.phase_of(pod) != "Running":
+                pod = await self.get_pod(req.namespace, req.pod_name, fresh=True)
+                if pod is None:
+                    return api.AddGPUResponse(add_gpu_result=api.ADD_POD_NOT_FOUND)
+                if podu.phase_of(pod) != "Running":
+                    raise RpcError(grpc.StatusCode.FAILED_PRECONDITION,
+                                   f"pod phase is {podu.phase_of(pod)}, not Running")
+            with trace.span("ledger_read"):
+                st = await self.pod_state(pod)
+            ok, why = can_mount(st.mount_type, req.is_entire_mount)
+            if not ok:
+                _log.warning("policy denied add on %s/%s: %s", req.namespace, req.pod_name, why)
+                raise RpcError(grpc.StatusCode.FAILED_PRECONDITION, f"{ERR_POLICY}: {why}")
+            with trace.span("placement"):
+                preferred = await self._preferred(n, st)
+            try:
+                res = await self.ph.reserve(pod, n, req.is_entire_mount, preferred,
+                                            attach_id=log.request_id.get(),
+                                            container=req.container)
+            except InsufficientGPU as e:
+                _log.info("insufficient GPUs on %s: %s", self.cfg.node_name, e)
+                return api.AddGPUResponse(add_gpu_result=api.ADD_INSUFFICIENT, message=str(e))
+            except (ReserveError, asyncio.TimeoutError) as e:
+                raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
+            keys = gpus_by_key(self.inv.gpus())
+            new = [keys[normalize_device_id(d)] for d in res.device_ids]
+            owner = {}
+            for ph in res.placeholders:
+                for d in ph.device_ids:
+                    owner[keys[normalize_device_id(d)].index] = ph.name
+            if preferred and sorted(normalize_device_id(d) for d in res.device_ids) != \
+                    sorted(normalize_device_id(d) for d in preferred):
+                self.metrics.placement_mismatch.inc()
+            try:
+                with trace.span("mount", gpus=len(new)):
+                    self.hm.attach(pod, new, st.hot, st.own, req.container)
+            except MountError as e:
+                _log.error("mount failed on %s/%s: %s", req.namespace, req.pod_name, e)
+                await self.ph.release(res.placeholders, wait=False)
+                raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
+            log.kv(_log, 20, "attached", pod=f"{req.namespace}/{req.pod_name}",
+                   gpus=[g.bdf for g in new])
+            return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS,
+                                      devices=self._devices(new, owner),
+                                      message="Add GPU Success")
+
+    async def _preferred(self, n: int, st: PodGpuState) -> List[str]:
+        """xGMI/NUMA-aware preferred device IDs among currently free GPUs."""
+        allocated = {normalize_device_id(d) for ids in st.ledger.values() for d in ids}
+        gpus = self.inv.gpus()
+        free = [g for g in gpus if not allocated.intersection(g.ledger_keys())]
+        plc = topology.choose(free, n, self.inv.links(), attached=st.hot + st.own,
+                              policy=self.cfg.topology_policy)
+        if plc is None:
+            return []
+        by_index = {g.index: g for g in gpus}
+        # the device plugin's own spelling of the ID is unknown here; BDF is what the ROCm plugin
+        # advertises, the fake node honours any ledger key
+        return [by_index[i].bdf for i in plc.chosen]
+
+    # ------------------------------------------------------------------------ RemoveGPU
+    async def remove_gpu(self, req) -> "api.RemoveGPUResponse":
+        rid = req.request_id or log.new_request_id("rm")
+        with log.with_rid(rid), trace.span("detach", pod=f"{req.namespace}/{req.pod_name}",
+                                           n=len(req.uuids), force=req.force) as root:
+            resp = await self._remove_gpu(req)
+        resp.total_ms = root.duration_ms
+        resp.timings.extend(self._timings(root))
+        result = api.RemoveGPUResponse.RemoveGPUResult.Name(resp.remove_gpu_result)
+        self.metrics.requests.labels(op="remove", result=result).inc()
+        if resp.remove_gpu_result == api.REMOVE_SUCCESS:
+            self.metrics.detach_latency.labels(n_gpus=str(len(req.uuids))).observe(
+                root.duration_ms / 1e3)
+            self.metrics.observe_trace("detach", root)
+        return resp
+
+    async def _remove_gpu(self, req):
+        with trace.span("pod_lookup"):
+            pod = await self.get_pod(req.namespace, req.pod_name)
+        if pod is None:
+            return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_POD_NOT_FOUND)
+        async with self.pod_lock(req.namespace, req.pod_name):
+            with trace.span("ledger_read"):
+                st = await self.pod_state(pod)
+            if st.mount_type == MountType.UNKNOWN:
+                raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: ledger unavailable")
+            selected = self.select_removal(st, list(req.uuids))
+            if not selected:
+                return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_GPU_NOT_FOUND,
+                                             message="Invalid UUIDs")
+            sel_idx = {g.index for g in selected}
+            keep = [g for g in st.hot if g.index not in sel_idx]
+            with trace.span("busy_check"):
+                targets = self.hm.targets(pod, req.container)
+                cpids = sorted({p for t in targets for p in t.pids})
+                busy = procs.busy_pids(self.inv, selected, cpids, self.cfg.drm_major)
+            if busy and not req.force:
+                _log.info("GPU busy in %s/%s: %s", req.namespace, req.pod_name, busy)
+                return api.RemoveGPUResponse(
+                    remove_gpu_result=api.REMOVE_BUSY,
+                    message=f"busy: {json.dumps({str(k): v for k, v in busy.items()})}")
+            with trace.span("unmount", gpus=len(selected)):
+                self.hm.detach(pod, selected, keep, st.own, req.container, targets)
+            killed: List[int] = sorted({p for v in busy.values() for p in v})
+            if killed:
+                with trace.span("kill", pids=len(killed)):
+                    procs.signal_pids(killed, self.cfg.kill_signal)
+                    asyncio.ensure_future(procs.terminate(killed, self.cfg.kill_signal,
+                                                          self.cfg.kill_grace_s))
+            phs = [ph for ph in st.placeholders
+                   if {g.index for g in st.by_placeholder[(ph.namespace, ph.name)]} & sel_idx]
+            try:
+                await self.ph.release(phs, wait=True)
+            except asyncio.TimeoutError as e:
+                raise RpcError(grpc.StatusCode.DEADLINE_EXCEEDED,
+                               "placeholders not deleted in time") from e
+            owner = {g.index: ph.name for ph in phs
+                     for g in st.by_placeholder[(ph.namespace, ph.name)]}
+            return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_SUCCESS,
+                                         devices=self._devices(selected, owner),
+                                         killed_pids=killed, message="Remove GPU Success")
+
+    @staticmethod
+    def select_removal(st: PodGpuState, ids: List[str]) -> List[AmdGpu]:
+        """Reference allocator.go:101-126: only hot-mounted GPUs are removable; entire mounts are
+        removed as a whole; any unmatched id makes the whole request invalid (empty result)."""
+        if not ids:
+            return []
+        want = {normalize_device_id(i) for i in ids}
+        if len(want) != len(ids):
+            return []
+        if st.mount_type == MountType.ENTIRE:
+            candidates = list(st.hot)
+            matched = {k for g in candidates for k in g.ledger_keys()}
+            if len(want) != len(candidates) or not want <= matched:
+                return []
+            return candidates
+        selected = [g for g in st.hot if want.intersection(g.ledger_keys())]
+        if len(selected) != len(want):
+            return []
+        return selected
+
+    # ------------------------------------------------------------------------ status
+    async def node_status(self, include_processes: bool) -> dict:
+        gpus = self.inv.gpus()
+        try:
+            ledger = await self.ledger.list()
+        except LedgerError as e:
+            ledger = []
+            _log.error("ledger: %s", e)
+        keys = gpus_by_key(gpus)
+        for a in ledger:
+            for d in a.device_ids:
+                g = keys.get(normalize_device_id(d))
+                if g is not None:
+                    g.pod_name, g.namespace, g.container = a.pod, a.namespace, a.container
+                    g.state = g.state.ALLOCATED
+        out = {"node": self.cfg.node_name, "gpus": [g.to_dict() for g in gpus],
+               "topology": topology.describe(gpus, self.inv.links()),
+               "ledger_api": self.ledger.api_version, "kfd_major": self.inv.kfd_major}
+        if include_processes:
+            procs_by = {}
+            for g in gpus:
+                try:
+                    procs_by[g.index] = [p.__dict__ for p in self.inv.processes(g.index)]
+                except Exception as e:  # noqa: BLE001
+                    procs_by[g.index] = str(e)
+            out["processes"] = procs_by
+        for state in ("GPU_FREE_STATE", "GPU_ALLOCATED_STATE"):
+            self.metrics.ledger_gpus.labels(state=state).set(
+                sum(1 for g in gpus if g.state.value == state))
+        return out
