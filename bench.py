@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Headline benchmark: p50 GPU attach latency at N MI355X per Pod (BASELINE.json metric).
+
+One "step" = the full hot-mount cycle a user drives through the master's HTTP API:
+  1. ``GET /addgpu/.../gpu/N/isEntireMount/true``   → placeholder ledger + cgroup rule + /dev nodes
+     (timed at the client: this is the attach latency reported as ``value``)
+  2. consistency audit: ledger == cgroup rules == device nodes for the tenant pod
+  3. every rank runs the gfx950 liveness kernel on "its" newly attached GPU (found by PCI address)
+     and, for N>1, an RCCL all-reduce over the attached set (tenant-side proof the GPUs work)
+  4. ``POST /removegpu/.../force/false``            → revoke + unlink + ledger release
+The control plane (apiserver, scheduler, kubelet PodResources) is the hermetic fake; inventory,
+topology and process tables come from the real libamd_smi through the C++ shim, the node
+operations run the production C++ code against a temp-dir cgroupfs/rootfs (the GPU box is
+unprivileged), and the probe kernels run on the real GPUs.
+
+Launch: ``python bench.py --gpus 1`` or, for N>1, under torch.distributed.run with one rank per GPU.
+Rank 0 hosts the control plane; all ranks take part in verification. Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    k = (len(xs) - 1) * q
+    lo, hi = int(k), min(int(k) + 1, len(xs) - 1)
+    return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mode", choices=("entire", "single"), default="entire")
+    ap.add_argument("--latency", choices=("zero", "realistic"), default="zero",
+                    help="fake control-plane latency model (zero = controller overhead only)")
+    ap.add_argument("--amdsmi", default="", help='"" = real libamd_smi, "mock" = bundled mock')
+    ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
+    ap.add_argument("--no-verify", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n = args.gpus
+    if world > 1 and world != n:
+        print(f"WORLD_SIZE={world} must equal --gpus={n}", file=sys.stderr)
+        return 2
+
+    import torch
+    import torch.distributed as dist
+
+    from gpumounter_amd.utils import log
+    log.setup("WARNING", json_format=False)
+    has_gpu = torch.cuda.is_available()
+    if has_gpu:
+        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from gpumounter_amd.ops import probe
+
+    visible = []
+    if has_gpu:
+        visible = [probe.props(i)["pci_bus_id"] for i in range(probe.device_count())]
+
+    tc = lc = None
+    sleeper = None
+    info = {}
+    if rank == 0:
+        from gpumounter_amd.fakes.apiserver import LatencyModel
+        from gpumounter_amd.fakes.harness import ThreadedCluster
+        from gpumounter_amd.hw.inventory import Inventory
+        amdsmi = args.amdsmi if (has_gpu or args.amdsmi) else "mock"
+        inv = Inventory(amdsmi)
+        bdfs = [g.bdf for g in inv.gpus()]
+        node_bdfs = [b for b in bdfs if b in visible] if visible else bdfs
+        if len(node_bdfs) < n:
+            print(f"need {n} GPUs visible to HIP and amdsmi; have {node_bdfs} (amdsmi {bdfs}, "
+                  f"HIP {visible})", file=sys.stderr)
+            return 3
+        lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
+        tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
+                             node_gpu_bdfs=node_bdfs)
+        lc = tc.start()
+        sleeper = subprocess.Popen(["sleep", "infinity"])
+        lc.tenant("tenant", pids={"main": [sleeper.pid]})
+        info = {"amdsmi_lib": inv.lib_path, "node_gpus": len(node_bdfs),
+                "amdsmi_gpus": len(bdfs), "gfx": sorted({g.gfx_target for g in inv.gpus()}),
+                "hives": sorted({hex(g.xgmi_hive_id) for g in inv.gpus()})}
+
+    nccl_group = None
+    attach_ms, detach_ms, audit_issues, probe_us, stage = [], [], 0, [], {}
+    ar_ms = []
+
+    def one_step(record: bool):
+        nonlocal audit_issues, nccl_group
+        obj = [None]
+        if rank == 0:
+            t0 = time.perf_counter()
+            code, body = tc.call(lc.add("default", "tenant", n, entire=args.mode == "entire"))
+            t1 = time.perf_counter()
+            if code != 200:
+                raise RuntimeError(f"attach failed: {code} {body}")
+            issues = tc.call(lc.audit("default", "tenant"))
+            obj = [{"bdfs": [d["bdf"] for d in body["devices"]],
+                    "uuids": [d["uuid"] for d in body["devices"]],
+                    "ms": (t1 - t0) * 1e3, "issues": len(issues),
+                    "timings": {t["name"]: t["ms"] for t in body.get("timings", [])}}]
+        if world > 1:
+            dist.broadcast_object_list(obj, src=0)
+        st = obj[0]
+        if has_gpu and not args.no_verify:
+            mine = st["bdfs"][rank % len(st["bdfs"])]
+            dev = probe.find_device(mine)
+            if dev < 0:
+                raise RuntimeError(f"rank {rank}: attached GPU {mine} not visible to HIP")
+            us = probe.quick(dev)
+            if record:
+                probe_us.append(us)
+            if world > 1:
+                if nccl_group is None:
+                    torch.cuda.set_device(dev)
+                    nccl_group = dist.new_group(backend="nccl")
+                x = torch.ones(1 << 20, dtype=torch.bfloat16, device=f"cuda:{dev}")
+                ta = time.perf_counter()
+                dist.all_reduce(x, group=nccl_group)
+                torch.cuda.synchronize(dev)
+                if record:
+                    ar_ms.append((time.perf_counter() - ta) * 1e3)
+                if float(x[0].item()) != float(world):
+                    raise RuntimeError("RCCL all-reduce over the attached GPUs returned wrong sum")
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            t0 = time.perf_counter()
+            code, body = tc.call(lc.remove("default", "tenant", st["uuids"]))
+            t1 = time.perf_counter()
+            if code != 200:
+                raise RuntimeError(f"detach failed: {code} {body}")
+            if record:
+                attach_ms.append(st["ms"])
+                detach_ms.append((t1 - t0) * 1e3)
+                audit_issues += st["issues"]
+                for k, v in st["timings"].items():
+                    stage.setdefault(k, []).append(v)
+
+    try:
+        for _ in range(args.warmup):
+            one_step(False)
+        if world > 1:
+            dist.barrier()
+        if has_gpu:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            one_step(True)
+        if world > 1:
+            dist.barrier()
+        if has_gpu:
+            torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ms_per_step = elapsed * 1e3 / args.steps
+        if world > 1:
+            t = torch.tensor([ms_per_step], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms_per_step = float(t.item())
+        if rank == 0:
+            orphan_issues = len(tc.call(lc.audit("default", "tenant")))
+            placeholders_left = len(lc.cluster.placeholders())
+            p50 = pct(attach_ms, 0.5)
+            out = {
+                "metric": "p50_gpu_attach_latency_ms",
+                "value": round(p50, 4),
+                "unit": "ms",
+                "n_gpus": n,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(ms_per_step, 4),
+                "higher_is_better": False,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "bf16",
+                "data": "synthetic",
+                "config": {
+                    "model": f"gpumounter-amd {args.mode}-mount, {n} MI355X per Pod",
+                    "global_batch": 1, "seq_len": None, "gpus_per_pod": n,
+                    "parallelism": f"node-local attach of {n} GPU(s); tenant RCCL check over dp{n}",
+                    "control_plane": f"hermetic fake apiserver/kubelet, latency={args.latency}",
+                    "cgroup": args.cgroup,
+                },
+                "attach_p99_ms": round(pct(attach_ms, 0.99), 4),
+                "detach_p50_ms": round(pct(detach_ms, 0.5), 4),
+                "detach_p99_ms": round(pct(detach_ms, 0.99), 4),
+                "stage_p50_ms": {k: round(statistics.median(v), 4) for k, v in sorted(stage.items())},
+                "probe_quick_p50_us": round(statistics.median(probe_us), 2) if probe_us else None,
+                "rccl_allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4) if ar_ms else None,
+                "ledger_audit_issues": audit_issues,
+                "final_orphans": orphan_issues,
+                "placeholders_left": placeholders_left,
+                "inventory": info,
+            }
+            print(json.dumps(out), flush=True)
+    finally:
+        if rank == 0:
+            if sleeper is not None:
+                sleeper.kill()
+                sleeper.wait()
+            if tc is not None:
+                tc.stop()
+        if world > 1:
+            dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

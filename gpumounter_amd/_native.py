@@ -132,8 +132,9 @@ def host() -> C.CDLL:
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.gm_bpf_prog_name.argtypes = [C.c_uint32, C.c_char_p, C.c_int]
         lib.gm_bpf_dev_install.argtypes = [C.c_char_p, C.POINTER(DevRule), C.c_int,
+                                           C.POINTER(DevRule), C.c_int, C.c_char_p,
                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
-        lib.gm_bpf_dev_restore.argtypes = [C.c_char_p]
+        lib.gm_bpf_dev_restore.argtypes = [C.c_char_p, C.c_char_p]
         lib.gm_devnodes_create.argtypes = [C.c_int, C.c_char_p, C.POINTER(DevNode), C.c_int,
                                            C.c_int, C.POINTER(C.c_int)]
         lib.gm_devnodes_remove.argtypes = lib.gm_devnodes_create.argtypes
@@ -143,6 +144,8 @@ def host() -> C.CDLL:
         lib.gm_proc_signal.argtypes = [C.POINTER(C.c_int32), C.c_int, C.c_int, C.POINTER(C.c_int)]
         lib.gm_proc_dev_users.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_int32), C.c_int,
                                           C.POINTER(C.c_int)]
+        lib.gm_proc_filter_dev_users.argtypes = [C.POINTER(C.c_int32), C.c_int, C.c_uint32,
+                                                 C.c_uint32, C.POINTER(C.c_int32)]
         lib.gm_proc_read_pids.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.c_int,
                                           C.POINTER(C.c_int)]
         lib.gm_roctx_push.argtypes = [C.c_char_p]

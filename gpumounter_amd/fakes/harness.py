@@ -47,7 +47,8 @@ class LocalCluster:
                  workdir: str = "", placeholder_namespace_mode: str = "pool",
                  alloc_policy: str = "topology", device_id_kind: str = "bdf",
                  devnode_mode: str = "emulate", reconcile_period_s: float = 0.0,
-                 start_master: bool = True, worker_overrides: Optional[dict] = None) -> None:
+                 start_master: bool = True, worker_overrides: Optional[dict] = None,
+                 node_gpu_bdfs: Optional[List[str]] = None) -> None:
         self.n_nodes = n_nodes
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
@@ -63,6 +64,7 @@ class LocalCluster:
         self.reconcile_period_s = reconcile_period_s
         self.start_master = start_master
         self.worker_overrides = worker_overrides or {}
+        self.node_gpu_bdfs = [b.lower() for b in node_gpu_bdfs] if node_gpu_bdfs else None
         self.nodes: Dict[str, NodeHandle] = {}
         self.master: Optional[Master] = None
         self.api_runner: Optional[web.AppRunner] = None
@@ -97,7 +99,10 @@ class LocalCluster:
     async def _add_node(self, name: str) -> NodeHandle:
         ndir = os.path.join(self.workdir, name)
         os.makedirs(ndir, exist_ok=True)
-        node = FakeNode(name, ndir, self.inventory.gpus(), self.inventory.links(),
+        gpus = self.inventory.gpus()
+        if self.node_gpu_bdfs is not None:
+            gpus = [g for g in gpus if g.bdf in self.node_gpu_bdfs]
+        node = FakeNode(name, ndir, gpus, self.inventory.links(),
                         cgroup_mode=self.cgroup_mode, cgroup_driver=self.cgroup_driver,
                         runtime=self.runtime, device_id_kind=self.device_id_kind,
                         alloc_policy=self.alloc_policy)

@@ -218,21 +218,44 @@ class V1Backend(DeviceRuleBackend):
         return out
 
 
+# OCI/runc default device allow-list, compiled into our program only if the tail-call chain to
+# the runtime's own program was lost (unpinned map + worker restart).
+OCI_DEFAULT_RULES = [("c", 1, -1, -1), ("b", 1, -1, -1), ("c", 7, 1, 3), ("c", 7, 1, 5),
+                     ("c", 7, 1, 7), ("c", 7, 1, 8), ("c", 7, 1, 9), ("c", 7, 5, 0),
+                     ("c", 7, 5, 1), ("c", 7, 5, 2), ("c", 7, 136, -1), ("c", 7, 10, 200)]
+
+
+def oci_default_rules() -> List[_native.DevRule]:
+    return [_native.DevRule(t.encode(), acc, 1, 0, ma, mi) for t, acc, ma, mi in OCI_DEFAULT_RULES]
+
+
 class V2BpfBackend(DeviceRuleBackend):
-    """Real eBPF backend (needs CAP_SYS_ADMIN + CAP_BPF on a cgroup2 mount)."""
+    """Real eBPF backend (needs CAP_SYS_ADMIN + CAP_BPF on a cgroup2 mount).
+
+    ``pin_dir`` is a directory on a bpffs (``/sys/fs/bpf/gpumounter`` in the DaemonSet) where the
+    tail-call map to the runtime's program is pinned so the chain survives worker restarts.
+    """
 
     name = "cgroup-v2-bpf"
 
+    def __init__(self, pin_dir: str = "") -> None:
+        self.pin_dir = pin_dir
+        if pin_dir:
+            os.makedirs(pin_dir, exist_ok=True)
+
     def apply(self, cgdir, grant, revoke, desired):
         lib = _native.host()
+        pin = self.pin_dir.encode() if self.pin_dir else None
         if not desired:
-            rc = lib.gm_bpf_dev_restore(cgdir.encode())
+            rc = lib.gm_bpf_dev_restore(cgdir.encode(), pin)
             if rc < 0:
                 raise CgroupError(f"bpf restore on {cgdir}: {os.strerror(-rc)}")
             return
         rules = rules_for(desired, allow=True)
+        base = oci_default_rules()
         pid, chained = C.c_uint32(0), C.c_uint32(0)
-        rc = lib.gm_bpf_dev_install(cgdir.encode(), _rule_array(rules), len(rules), C.byref(pid),
+        rc = lib.gm_bpf_dev_install(cgdir.encode(), _rule_array(rules), len(rules),
+                                    _rule_array(base), len(base), pin, C.byref(pid),
                                     C.byref(chained))
         if rc < 0:
             raise CgroupError(f"bpf install on {cgdir}: {os.strerror(-rc)}")
@@ -286,9 +309,9 @@ class V2RecordingBackend(DeviceRuleBackend):
         return {(int(a), int(b)) for a, b, _ in st["rules"]}
 
 
-def make_backend(mode: str, emulate: bool) -> DeviceRuleBackend:
+def make_backend(mode: str, emulate: bool, bpf_pin_dir: str = "") -> DeviceRuleBackend:
     if mode == "v1":
         return V1Backend()
     if emulate:
         return V2RecordingBackend()
-    return V2BpfBackend()
+    return V2BpfBackend(bpf_pin_dir)

@@ -40,15 +40,35 @@ def dev_users(major: int, minor: int) -> List[int]:
     return sorted(int(buf[i]) for i in range(min(n.value, 4096)))
 
 
+def filter_dev_users(pids: Sequence[int], major: int, minor: int) -> List[int]:
+    """Of ``pids``, those with an open fd on char device ``major:minor``."""
+    if not pids:
+        return []
+    arr = (C.c_int32 * len(pids))(*pids)
+    out = (C.c_int32 * len(pids))()
+    k = _native.host().gm_proc_filter_dev_users(arr, len(pids), major, minor, out)
+    return [int(out[i]) for i in range(k)]
+
+
 def busy_pids(inv: Inventory, gpus: Sequence[AmdGpu], container_pids: Iterable[int],
               drm_major: int = DRM_MAJOR) -> Dict[int, List[int]]:
-    """GPU index → container PIDs that hold that GPU."""
-    cpids = set(container_pids)
+    """GPU index → container PIDs that hold that GPU.
+
+    Union of two sources: amdsmi's per-GPU process table (KFD contexts; may be filtered for an
+    unprivileged caller) and an fd scan of *only the container's* PIDs for the GPU's render node
+    (every HIP process keeps ``/dev/dri/renderD<N>`` open).
+    """
+    cpids = sorted(set(container_pids))
     out: Dict[int, List[int]] = {}
     for g in gpus:
-        hit = sorted(cpids.intersection(gpu_pids(inv, g, drm_major)))
+        try:
+            smi = set(p.pid for p in inv.processes(g.index))
+        except NotImplementedError:
+            smi = set()
+        hit = set(cpids).intersection(smi)
+        hit.update(filter_dev_users(cpids, drm_major, g.render_minor))
         if hit:
-            out[g.index] = hit
+            out[g.index] = sorted(hit)
     return out
 
 

@@ -54,6 +54,7 @@ class Config:
     cgroup_root: str = "/sys/fs/cgroup"
     cgroup_mode: str = "auto"          # auto | v1 | v2
     cgroup_driver: str = "auto"        # auto | cgroupfs | systemd
+    bpf_pin_dir: str = "/sys/fs/bpf/gpumounter"  # bpffs dir for v2 tail-call maps ("" = keep fd)
     devnode_mode: str = "procroot"     # procroot | setns | emulate
     proc_root: str = "/proc"
     # For hermetic runs: containers' rootfs live at <container_root_prefix>/<container-id>/ and

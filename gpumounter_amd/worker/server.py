@@ -51,7 +51,7 @@ class Worker:
                                    cfg.podresources_api)
         self.resolver = CgroupResolver(cfg.cgroup_root, cfg.cgroup_mode, cfg.cgroup_driver)
         emulate = cfg.devnode_mode == "emulate" or os.environ.get("GM_BPF_EMULATE") == "1"
-        self.backend = make_backend(self.resolver.mode, emulate)
+        self.backend = make_backend(self.resolver.mode, emulate, cfg.bpf_pin_dir)
         self.writer = DevNodeWriter(cfg.devnode_mode)
         self.hotmount = HotMount(cfg, self.inv, self.resolver, self.backend, self.writer)
         ph_ns = None if cfg.placeholder_namespace_mode == "tenant" else cfg.pool_namespace

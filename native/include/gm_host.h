@@ -63,11 +63,17 @@ int gm_bpf_prog_name(uint32_t id, char* name, int cap);
 //   * our program already attached → replaced, chaining to the same original program;
 //   * one foreign program attached → ours replaces it and tail-calls into it;
 //   * nothing attached → ours is attached with default-allow (deny rules only matter then).
+// The tail-call map must outlive this process (the kernel clears PROG_ARRAY slots when the last
+// user reference goes away), so it is pinned at <pin_dir>/gm_<cgroup inode> on a bpffs; with
+// pin_dir NULL/"" the map fd is kept open in this process instead. If our program is attached but
+// its chain slot is empty (unpinned map after a restart), `base` rules (the runtime's default
+// device list) are compiled in instead of the tail call.
 // On success *prog_id is our new program id and *chained_id the preserved original (0 if none).
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
+                       const gm_dev_rule_t* base, int nbase, const char* pin_dir,
                        uint32_t* prog_id, uint32_t* chained_id);
-// Removes our program, re-attaching the chained original in its place (if any).
-int gm_bpf_dev_restore(const char* cgroup_path);
+// Removes our program, re-attaching the chained original in its place (if any), and unpins.
+int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir);
 
 // ---- device nodes ---------------------------------------------------------------------------
 typedef struct gm_dev_node {
@@ -99,6 +105,10 @@ int gm_devnode_stat(int pid, const char* root, const char* path, int flags, int*
 int gm_proc_signal(const int32_t* pids, int n, int sig, int* results);
 // PIDs with an open fd on char device major:minor (scans /proc/*/fd). *n = total found.
 int gm_proc_dev_users(uint32_t major, uint32_t minor, int32_t* pids, int cap, int* n);
+// Of `pids`, those holding an fd on char device major:minor (scans only /proc/<pid>/fd of the
+// given PIDs — cheap and exact for one container). Returns the count written to `out`.
+int gm_proc_filter_dev_users(const int32_t* pids, int n, uint32_t major, uint32_t minor,
+                             int32_t* out);
 // Parses a cgroup.procs-style file. *n = total.
 int gm_proc_read_pids(const char* path, int32_t* pids, int cap, int* n);
 

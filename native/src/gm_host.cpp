@@ -18,6 +18,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -169,6 +170,61 @@ int make_chain_map(int target_prog_fd) {
     return e;
   }
   return (int)mfd;
+}
+
+// ---- tail-call map lifetime (see gm_host.h: PROG_ARRAY slots die with the last user ref)
+std::mutex g_keep_mu;
+std::map<uint64_t, int> g_kept_maps;  // cgroup inode → map fd kept open (no bpffs available)
+
+uint64_t cgroup_ino(int cgfd) {
+  struct stat st;
+  return fstat(cgfd, &st) == 0 ? (uint64_t)st.st_ino : 0;
+}
+
+std::string pin_path(const char* pin_dir, uint64_t ino) {
+  return std::string(pin_dir) + "/gm_" + std::to_string(ino);
+}
+
+int obj_pin(int fd, const std::string& path) {
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.pathname = ptr_u64(path.c_str());
+  a.bpf_fd = (uint32_t)fd;
+  return sys_bpf(BPF_OBJ_PIN, &a, sizeof(a)) < 0 ? -errno : 0;
+}
+
+// Makes `map_fd` survive this call: pin (atomically replacing the previous pin) or keep the fd.
+int keep_map(const char* pin_dir, uint64_t ino, int map_fd) {
+  if (pin_dir && *pin_dir) {
+    const std::string final_path = pin_path(pin_dir, ino);
+    const std::string tmp = final_path + "_new";  // bpffs rejects "." in names
+    unlink(tmp.c_str());
+    int e = obj_pin(map_fd, tmp);
+    if (e < 0) return e;
+    if (rename(tmp.c_str(), final_path.c_str()) < 0) {
+      unlink(final_path.c_str());
+      unlink(tmp.c_str());
+      return obj_pin(map_fd, final_path);
+    }
+    return 0;
+  }
+  int dupfd = fcntl(map_fd, F_DUPFD_CLOEXEC, 0);
+  if (dupfd < 0) return -errno;
+  std::lock_guard<std::mutex> lk(g_keep_mu);
+  auto it = g_kept_maps.find(ino);
+  if (it != g_kept_maps.end()) close(it->second);
+  g_kept_maps[ino] = dupfd;
+  return 0;
+}
+
+void drop_map(const char* pin_dir, uint64_t ino) {
+  if (pin_dir && *pin_dir) unlink(pin_path(pin_dir, ino).c_str());
+  std::lock_guard<std::mutex> lk(g_keep_mu);
+  auto it = g_kept_maps.find(ino);
+  if (it != g_kept_maps.end()) {
+    close(it->second);
+    g_kept_maps.erase(it);
+  }
 }
 
 struct Attached {
@@ -594,20 +650,24 @@ int gm_bpf_prog_name(uint32_t id, char* name, int cap) {
 }
 
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
+                       const gm_dev_rule_t* base, int nbase, const char* pin_dir,
                        uint32_t* prog_id, uint32_t* chained_id) {
   Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
   if (!cg.ok()) return -errno;
+  const uint64_t ino = cgroup_ino(cg.fd);
   Attached at;
   int e = query(cg.fd, &at);
   if (e < 0) return e;
 
   uint32_t replace_id = 0, chain_id = 0;
+  bool ours_without_chain = false;
   int foreign = 0;
   for (uint32_t id : at.ids) {
     uint32_t c = 0;
     if (is_ours(id, &c)) {
       replace_id = id;
       chain_id = c;
+      ours_without_chain = (c == 0);
     } else {
       ++foreign;
     }
@@ -631,19 +691,27 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
     replace_fd = Fd(get_prog_fd_by_id(replace_id));
     if (!replace_fd.ok()) return replace_fd.fd;
   }
-  // With a chained original the fall-through is deny (the original already said no);
-  // without one the cgroup was unrestricted, so default-allow keeps that behaviour.
-  const int default_allow = chain_id ? 0 : 1;
-  std::vector<uint64_t> prog(16 + (size_t)n * 8);
-  int cnt = gm_bpf_dev_build(rules, n, default_allow, chain_map.ok() ? chain_map.fd : -1,
-                             prog.data(), (int)prog.size());
+  // rules = ours, then (chain lost) the runtime's default list compiled in
+  std::vector<gm_dev_rule_t> all(rules, rules + n);
+  if (ours_without_chain && base && nbase > 0) all.insert(all.end(), base, base + nbase);
+  // With a chained original (or a compiled-in base list) the fall-through is deny; with neither
+  // the cgroup was unrestricted, so default-allow keeps that behaviour.
+  const int default_allow = (chain_id || ours_without_chain) ? 0 : 1;
+  std::vector<uint64_t> prog(16 + all.size() * 12);
+  int cnt = gm_bpf_dev_build(all.data(), (int)all.size(), default_allow,
+                             chain_map.ok() ? chain_map.fd : -1, prog.data(), (int)prog.size());
   if (cnt < 0) return -EINVAL;
   char log[4096];
   Fd pfd(gm_bpf_dev_load(prog.data(), cnt, kProgName, log, sizeof(log)));
   if (!pfd.ok()) return pfd.fd;
+  if (chain_map.ok()) {
+    e = keep_map(pin_dir, ino, chain_map.fd);
+    if (e < 0) return e;
+  }
   e = attach(cg.fd, pfd.fd, replace_fd.ok() ? replace_fd.fd : -1,
              at.ids.empty() ? BPF_F_ALLOW_MULTI : at.flags);
   if (e < 0) return e;
+  if (!chain_map.ok()) drop_map(pin_dir, ino);
   if (prog_id) {
     struct bpf_prog_info info;
     uint32_t maps[1];
@@ -653,9 +721,10 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
   return 0;
 }
 
-int gm_bpf_dev_restore(const char* cgroup_path) {
+int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir) {
   Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
   if (!cg.ok()) return -errno;
+  const uint64_t ino = cgroup_ino(cg.fd);
   Attached at;
   int e = query(cg.fd, &at);
   if (e < 0) return e;
@@ -667,14 +736,18 @@ int gm_bpf_dev_restore(const char* cgroup_path) {
     if (chain) {
       Fd orig(get_prog_fd_by_id(chain));
       if (!orig.ok()) return orig.fd;
-      return attach(cg.fd, orig.fd, ours.fd, at.flags);
+      e = attach(cg.fd, orig.fd, ours.fd, at.flags);
+      if (e == 0) drop_map(pin_dir, ino);
+      return e;
     }
     union bpf_attr a;
     memset(&a, 0, sizeof(a));
     a.target_fd = (uint32_t)cg.fd;
     a.attach_bpf_fd = (uint32_t)ours.fd;
     a.attach_type = BPF_CGROUP_DEVICE;
-    return sys_bpf(BPF_PROG_DETACH, &a, sizeof(a)) < 0 ? -errno : 0;
+    e = sys_bpf(BPF_PROG_DETACH, &a, sizeof(a)) < 0 ? -errno : 0;
+    if (e == 0) drop_map(pin_dir, ino);
+    return e;
   }
   return 0;
 }
@@ -750,6 +823,39 @@ int gm_proc_signal(const int32_t* pids, int n, int sig, int* results) {
   return failures;
 }
 
+namespace {
+bool pid_uses_dev(long pid, dev_t want) {
+  char p[64];
+  snprintf(p, sizeof(p), "/proc/%ld/fd", pid);
+  int dfd = open(p, O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (dfd < 0) return false;
+  DIR* fds = fdopendir(dfd);
+  if (!fds) {
+    close(dfd);
+    return false;
+  }
+  struct dirent* fe;
+  bool hit = false;
+  while (!hit && (fe = readdir(fds)) != nullptr) {
+    if (fe->d_name[0] == '.') continue;
+    struct stat st;
+    if (fstatat(dirfd(fds), fe->d_name, &st, 0) == 0 && S_ISCHR(st.st_mode) && st.st_rdev == want)
+      hit = true;
+  }
+  closedir(fds);
+  return hit;
+}
+}  // namespace
+
+int gm_proc_filter_dev_users(const int32_t* pids, int n, uint32_t maj, uint32_t min,
+                             int32_t* out) {
+  const dev_t want = makedev(maj, min);
+  int k = 0;
+  for (int i = 0; i < n; ++i)
+    if (pid_uses_dev(pids[i], want)) out[k++] = pids[i];
+  return k;
+}
+
 int gm_proc_dev_users(uint32_t maj, uint32_t min, int32_t* pids, int cap, int* n) {
   *n = 0;
   DIR* proc = opendir("/proc");
@@ -760,25 +866,7 @@ int gm_proc_dev_users(uint32_t maj, uint32_t min, int32_t* pids, int cap, int* n
     char* endp = nullptr;
     long pid = strtol(de->d_name, &endp, 10);
     if (!endp || *endp != 0 || pid <= 0) continue;
-    char p[64];
-    snprintf(p, sizeof(p), "/proc/%ld/fd", pid);
-    int dfd = open(p, O_RDONLY | O_DIRECTORY | O_CLOEXEC);
-    if (dfd < 0) continue;
-    DIR* fds = fdopendir(dfd);
-    if (!fds) {
-      close(dfd);
-      continue;
-    }
-    struct dirent* fe;
-    bool hit = false;
-    while (!hit && (fe = readdir(fds)) != nullptr) {
-      if (fe->d_name[0] == '.') continue;
-      struct stat st;
-      if (fstatat(dirfd(fds), fe->d_name, &st, 0) == 0 && S_ISCHR(st.st_mode) &&
-          st.st_rdev == want)
-        hit = true;
-    }
-    closedir(fds);
+    const bool hit = pid_uses_dev(pid, want);
     if (hit) {
       if (*n < cap) pids[*n] = (int32_t)pid;
       ++*n;

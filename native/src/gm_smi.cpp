@@ -383,7 +383,19 @@ const char* gm_smi_strerror(int status) {
         s)
       return s;
   }
-  return "amdsmi: unknown status";
+  // The library may be unloaded (failed open): fall back to the header's names.
+  switch (status) {
+    case AMDSMI_STATUS_INVAL: return "AMDSMI_STATUS_INVAL";
+    case AMDSMI_STATUS_NOT_SUPPORTED: return "AMDSMI_STATUS_NOT_SUPPORTED";
+    case AMDSMI_STATUS_FAIL_LOAD_MODULE: return "AMDSMI_STATUS_FAIL_LOAD_MODULE";
+    case AMDSMI_STATUS_NO_PERM: return "AMDSMI_STATUS_NO_PERM";
+    case AMDSMI_STATUS_INIT_ERROR: return "AMDSMI_STATUS_INIT_ERROR";
+    case AMDSMI_STATUS_NOT_FOUND: return "AMDSMI_STATUS_NOT_FOUND";
+    case AMDSMI_STATUS_NOT_INIT: return "AMDSMI_STATUS_NOT_INIT";
+    case AMDSMI_STATUS_DRIVER_NOT_LOADED: return "AMDSMI_STATUS_DRIVER_NOT_LOADED";
+    case AMDSMI_STATUS_FILE_ERROR: return "AMDSMI_STATUS_FILE_ERROR";
+    default: return "amdsmi: unknown status";
+  }
 }
 
 }  // extern "C"

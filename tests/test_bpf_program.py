@@ -1,0 +1,111 @@
+"""Semantics of the generated cgroup-v2 device programs (gm_bpf_dev_build in native/src/gm_host.cpp),
+executed with the Python eBPF interpreter against a reference model of the device-rule rules."""
+import ctypes as C
+import itertools
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from gpumounter_amd import _native
+from gpumounter_amd.node import bpfvm
+from gpumounter_amd.node.cgroup import _rule_array
+
+TYPES = {"c": bpfvm.BPF_DEVCG_DEV_CHAR, "b": bpfvm.BPF_DEVCG_DEV_BLOCK}
+
+
+def build(rules, default_allow=0, chain=-1):
+    arr = _rule_array([_native.DevRule(t.encode(), acc, allow, 0, ma, mi)
+                       for t, acc, allow, ma, mi in rules])
+    lib = _native.host()
+    need = -lib.gm_bpf_dev_build(arr, len(rules), default_allow, chain, None, 0)
+    buf = (C.c_uint64 * need)()
+    n = lib.gm_bpf_dev_build(arr, len(rules), default_allow, chain, buf, need)
+    assert n == need
+    return [int(buf[i]) for i in range(n)]
+
+
+def model(rules, default_allow, dev_type, access, major, minor, chained=None):
+    for t, acc, allow, ma, mi in rules:
+        if t != "a" and TYPES[t] != dev_type:
+            continue
+        if access & ~acc & 7:
+            continue
+        if ma >= 0 and ma != major:
+            continue
+        if mi >= 0 and mi != minor:
+            continue
+        return allow
+    if chained is not None:
+        return chained(dev_type, access, major, minor)
+    return default_allow
+
+
+def test_simple_allow_list():
+    rules = [("c", 6, 1, 226, 128), ("c", 6, 1, 226, 0), ("c", 6, 1, 511, 0)]
+    prog = build(rules)
+    assert bpfvm.run(prog, 2, 6, 226, 128) == 1
+    assert bpfvm.run(prog, 2, 2, 226, 0) == 1          # read ⊂ rw
+    assert bpfvm.run(prog, 2, 1, 226, 128) == 0        # mknod not granted
+    assert bpfvm.run(prog, 2, 6, 226, 129) == 0        # another GPU
+    assert bpfvm.run(prog, 1, 6, 226, 128) == 0        # block device with same numbers
+
+
+def test_chained_program_falls_through_to_runtime_policy():
+    prog = build([("c", 6, 1, 226, 130)], chain=-2)
+    ch = bpfvm.runtime_default
+    assert bpfvm.run(prog, 2, 6, 226, 130, ch) == 1    # ours
+    assert bpfvm.run(prog, 2, 6, 1, 3, ch) == 1        # /dev/null from the runtime program
+    assert bpfvm.run(prog, 2, 6, 226, 131, ch) == 0    # not granted anywhere
+    assert bpfvm.run(prog, 2, 1, 8, 0, ch) == 1        # runtime allows mknod of anything
+    # with the tail-call slot empty the program denies (fails closed)
+    assert bpfvm.run(prog, 2, 6, 1, 3, None) == 0
+
+
+def test_default_allow_without_chain_keeps_unrestricted_cgroup():
+    prog = build([("c", 6, 0, 226, 131)], default_allow=1)
+    assert bpfvm.run(prog, 2, 6, 226, 131) == 0
+    assert bpfvm.run(prog, 2, 6, 226, 132) == 1
+
+
+def test_wildcards_and_first_match_wins():
+    rules = [("c", 6, 0, 226, 129), ("c", 7, 1, 226, -1), ("a", 1, 1, -1, -1)]
+    prog = build(rules)
+    assert bpfvm.run(prog, 2, 6, 226, 129) == 0   # explicit deny before the wildcard
+    assert bpfvm.run(prog, 2, 7, 226, 200) == 1
+    assert bpfvm.run(prog, 1, 1, 8, 1) == 1       # 'a' mknod wildcard
+    assert bpfvm.run(prog, 1, 2, 8, 1) == 0
+
+
+def test_exhaustive_against_model_small_grid():
+    rules = [("c", 6, 1, 226, 128), ("b", 2, 1, 8, -1), ("c", 1, 0, -1, -1),
+             ("c", 7, 1, 511, 0)]
+    prog = build(rules, chain=-2)
+    ch = bpfvm.runtime_default
+    for dt, acc, ma, mi in itertools.product((1, 2), range(1, 8), (1, 8, 226, 511),
+                                             (0, 3, 128, 129)):
+        assert bpfvm.run(prog, dt, acc, ma, mi, ch) == model(rules, 0, dt, acc, ma, mi, ch), \
+            (dt, acc, ma, mi)
+
+
+rule_st = st.tuples(st.sampled_from(["c", "b", "a"]), st.integers(1, 7), st.integers(0, 1),
+                    st.sampled_from([-1, 1, 226, 511]), st.sampled_from([-1, 0, 128, 129]))
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(rule_st, max_size=6), st.integers(0, 1), st.sampled_from([1, 2]),
+       st.integers(1, 7), st.sampled_from([1, 226, 511, 7]), st.sampled_from([0, 128, 129, 5]))
+def test_random_rule_sets_match_model(rules, default_allow, dt, acc, ma, mi):
+    prog = build(rules, default_allow=default_allow)
+    assert bpfvm.run(prog, dt, acc, ma, mi) == model(rules, default_allow, dt, acc, ma, mi)
+
+
+def test_build_rejects_bad_input():
+    lib = _native.host()
+    bad = _rule_array([_native.DevRule(b"x", 6, 1, 0, 1, 1)])
+    assert lib.gm_bpf_dev_build(bad, 1, 0, -1, None, 0) == -22
+    # too-small buffer reports the needed size
+    good = _rule_array([_native.DevRule(b"c", 6, 1, 0, 1, 1)])
+    need = -lib.gm_bpf_dev_build(good, 1, 0, -1, None, 0)
+    buf = (C.c_uint64 * 2)()
+    assert lib.gm_bpf_dev_build(good, 1, 0, -1, buf, 2) == -need

@@ -1,0 +1,179 @@
+"""On-MI355X tests (``pytest -m gpu`` on the GPU box). Each loads the in-tree native libraries:
+libgm_smi.so against the real libamd_smi, libgm_probe.so (gfx950 kernels), libgm_host.so.
+Numerics tests compare HIP kernels against plain PyTorch fp32 references.
+"""
+import asyncio
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def real_inventory():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test on a host without a GPU")
+    from gpumounter_amd.hw.inventory import Inventory
+
+    return Inventory("")
+
+
+def test_amdsmi_real_inventory(real_inventory):
+    from gpumounter_amd.ops import probe
+
+    inv = real_inventory
+    assert "mock" not in inv.lib_path
+    gpus = inv.gpus()
+    assert len(gpus) >= 1
+    hip_bdfs = {probe.props(i)["pci_bus_id"] for i in range(probe.device_count())}
+    seen = [g for g in gpus if g.bdf in hip_bdfs]
+    assert seen, (hip_bdfs, [g.bdf for g in gpus])
+    for g in seen:
+        assert g.gfx_target == "gfx950", g.gfx_target
+        assert g.render_minor >= 128
+        assert g.vram_bytes > 200 * (1 << 30)     # 288 GB HBM3E
+        assert g.num_cu >= 256 or g.num_cu == 0   # CPX partitions report fewer
+    links = inv.links()
+    assert links.n == len(gpus)
+    assert all(links.types[i][i] == 0 for i in range(links.n))
+
+
+def test_probe_props_and_quick():
+    from gpumounter_amd.ops import probe
+
+    p = probe.props(0)
+    assert p["gcn_arch"].startswith("gfx950"), p
+    assert p["warp_size"] == 64
+    us = probe.quick(0)
+    assert us < 1e6
+
+
+def test_probe_hbm_and_mfma_rates():
+    from gpumounter_amd.ops import probe
+
+    gbps = probe.hbm_gbps(0, 1 << 30, 10)
+    tf = probe.mfma_tflops(0, 20000)
+    print(f"HBM copy {gbps:.0f} GB/s, MFMA bf16 {tf:.0f} TF/s")
+    assert gbps > 2000, gbps          # MI355X measured ≈6.3 TB/s on copy; 2 TB/s = sick GPU
+    assert tf > 500, tf               # dense bf16 peak ≈2.5 PF/s
+
+
+@pytest.mark.parametrize("m,n,k", [(64, 64, 32), (128, 192, 96), (256, 256, 512)])
+def test_mfma_gemm_bf16_matches_torch_fp32(m, n, k):
+    from gpumounter_amd.ops import probe
+
+    g = torch.Generator(device="cuda:0").manual_seed(m * 7 + n * 3 + k)
+    a = torch.randn(m, k, device="cuda:0", generator=g).to(torch.bfloat16)
+    b = torch.randn(k, n, device="cuda:0", generator=g).to(torch.bfloat16)
+    c = probe.gemm_bf16(a, b)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float()
+    err = (c - ref).abs().max().item()
+    assert err <= 1e-3 * k ** 0.5 * 4, err
+
+
+def test_mfma_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches row/col swaps in the C write-back."""
+    from gpumounter_amd.ops import probe
+
+    a = torch.eye(64, 64, device="cuda:0").to(torch.bfloat16)
+    b = (torch.arange(64, device="cuda:0").view(64, 1) * 100
+         + torch.arange(64, device="cuda:0").view(1, 64)).float().to(torch.bfloat16)
+    c = probe.gemm_bf16(a.contiguous(), b.contiguous())
+    assert torch.equal(c, b.float())
+
+
+def test_gemm_check_host_reference():
+    from gpumounter_amd.ops import probe
+
+    r = probe.gemm_check(0, 128, 128, 256)
+    assert r["max_abs_err"] < 1e-3 * r["ref_scale"] + 1e-3, r
+
+
+def test_roctx_library_loads():
+    from gpumounter_amd import _native
+
+    assert _native.host().gm_roctx_available() == 1
+
+
+def test_p2p_if_multi_gpu():
+    from gpumounter_amd.ops import probe
+    from gpumounter_amd.parallel.collectives import xgmi_matrix
+
+    if probe.device_count() < 2:
+        pytest.skip("single-GPU box")
+    m = xgmi_matrix([0, 1], 64 << 20, 3)
+    assert m["peer"][0][1]
+    assert m["gbps"][0][1] > 10
+
+
+def _hip_child_code() -> str:
+    return ("import torch, time, sys; x = torch.ones(1 << 20, device='cuda:0'); "
+            "torch.cuda.synchronize(); print('ready', flush=True); time.sleep(120)")
+
+
+def test_e2e_attach_verify_detach_real_inventory(real_inventory):
+    """Full hot-mount cycle with the real amdsmi inventory; tenant-side kernel on the GPU."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+    from gpumounter_amd.ops import probe
+
+    bdf0 = probe.props(0)["pci_bus_id"]
+
+    async def run():
+        async with LocalCluster(amdsmi_lib="", cgroup_mode="v2", node_gpu_bdfs=[bdf0]) as lc:
+            lc.tenant("t")
+            code, body = await lc.add("default", "t", 1)
+            assert code == 200, body
+            assert body["devices"][0]["bdf"] == bdf0
+            assert not await lc.audit("default", "t")
+            cid = lc.container_ids("default", "t")[0]
+            rm = body["devices"][0]["render_minor"]
+            assert f"dev/dri/renderD{rm}" in lc.nodes["node-0"].node.container_devices(cid)
+            assert probe.verify([bdf0])[0].quick_us > 0
+            code, body2 = await lc.remove("default", "t", [body["devices"][0]["uuid"]])
+            assert code == 200, body2
+            assert not await lc.audit("default", "t")
+    asyncio.run(run())
+
+
+def test_busy_detection_with_real_hip_process(real_inventory):
+    """A real HIP process inside the tenant cgroup makes the GPU busy (amdsmi process list or the
+    /proc fd fallback); force=true removes it and terminates the process."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+    from gpumounter_amd.ops import probe
+
+    bdf0 = probe.props(0)["pci_bus_id"]
+    child = subprocess.Popen([sys.executable, "-c", _hip_child_code()], stdout=subprocess.PIPE,
+                             text=True)
+    try:
+        assert child.stdout.readline().strip() == "ready"
+
+        async def run():
+            async with LocalCluster(amdsmi_lib="", cgroup_mode="v2",
+                                    node_gpu_bdfs=[bdf0]) as lc:
+                lc.tenant("busy", pids={"main": [child.pid]})
+                smi_pids = [p.pid for p in lc.inventory.processes(0)]
+                print(f"amdsmi process list for gpu0: {smi_pids} (child {child.pid})")
+                code, body = await lc.add("default", "busy", 1)
+                assert code == 200, body
+                uuid = body["devices"][0]["uuid"]
+                code, b2 = await lc.remove("default", "busy", [uuid], force=False)
+                assert code == 400 and "running processes" in b2["message"], b2
+                code, b3 = await lc.remove("default", "busy", [uuid], force=True)
+                assert code == 200, b3
+                assert child.pid in b3["killed_pids"]
+        asyncio.run(run())
+        t0 = time.time()
+        while child.poll() is None and time.time() - t0 < 15:
+            time.sleep(0.1)
+        assert child.poll() is not None, "force removal did not terminate the GPU process"
+    finally:
+        if child.poll() is None:
+            child.kill()
+        child.wait()

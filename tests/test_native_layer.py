@@ -1,0 +1,239 @@
+"""C++ native layer through its Python bindings: sanitized unit tests, the amdsmi shim against the
+mock (default + JSON-configured inventories, live process table), device-node injection (real
+mknod as root, emulated markers, symlink-escape refusal), cgroup path resolution for every
+driver/runtime/QoS/version combination, and the v1/v2 backends."""
+import json
+import os
+import stat
+import subprocess
+import sys
+
+import pytest
+
+from gpumounter_amd import _native
+from gpumounter_amd.fakes.node import FakeNode
+from gpumounter_amd.models.device import DeviceNode
+from gpumounter_amd.models.pod import ContainerRef
+from gpumounter_amd.node import bpfvm
+from gpumounter_amd.node.cgroup import (CgroupError, CgroupResolver, V1Backend,
+                                        V2RecordingBackend, build_program)
+from gpumounter_amd.node.devnodes import DevNodeError, DevNodeWriter, Target
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_native_unit_tests_under_asan_ubsan():
+    res = subprocess.run(["make", "-C", os.path.join(ROOT, "native"), "check"],
+                         capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    assert "native tests OK" in res.stdout
+
+
+# ----------------------------------------------------------------------------------- amdsmi
+def test_mock_inventory_default_mi355x_node(mock_inventory):
+    inv = mock_inventory
+    gpus = inv.gpus()
+    assert len(gpus) == 8
+    assert all(g.gfx_target == "gfx950" and g.market_name == "AMD Instinct MI355X" for g in gpus)
+    assert [g.render_minor for g in gpus] == list(range(128, 136))
+    assert [g.numa_node for g in gpus] == [0] * 4 + [1] * 4
+    assert len({g.xgmi_hive_id for g in gpus}) == 1
+    assert gpus[0].vram_bytes == 294896 * 2 ** 20   # 288 GB HBM3E
+    links = inv.links()
+    assert all(links.types[i][j] == (0 if i == j else 2) for i in range(8) for j in range(8))
+    # the shim initialises amdsmi exactly once per process (reference re-inits per query)
+    assert _native.mock_smi().gm_mock_init_calls() == 1
+
+
+def test_mock_process_table_is_live(mock_inventory, tmp_path, monkeypatch):
+    # processes come from the file named by procs_file / GM_AMDSMI_MOCK_PROCS, re-read per call;
+    # the session mock was opened without one, so exercise the file path in a subprocess
+    cfg = tmp_path / "mock.json"
+    procs = tmp_path / "procs"
+    cfg.write_text(json.dumps({
+        "gpus": [{"bdf": "0000:11:00.0", "render": 140, "card": 1, "numa": 0, "hive": 7},
+                 {"bdf": "0000:12:00.0", "render": 141, "card": 2, "numa": 1, "hive": 7},
+                 {"bdf": "0000:21:00.0", "render": 142, "card": 3, "numa": 1, "hive": 9}],
+        "links": {"overrides": [{"a": 0, "b": 1, "type": 2, "hops": 1, "weight": 20}]},
+        "procs_file": str(procs)}))
+    procs.write_text("1 4242 1024 python\n0 99 0 x\n")
+    code = (
+        "import sys, json; sys.path.insert(0, %r)\n"
+        "from gpumounter_amd.hw.inventory import Inventory\n"
+        "inv = Inventory('mock')\n"
+        "print(json.dumps({'n': inv.count, 'r': [g.render_minor for g in inv.gpus()],"
+        " 't': inv.links().types, 'p1': [p.pid for p in inv.processes(1)],"
+        " 'p2': [p.pid for p in inv.processes(2)]}))\n" % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         env={**os.environ, "GM_AMDSMI_MOCK_CONFIG": str(cfg)}, timeout=60)
+    assert out.returncode == 0, out.stderr
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["n"] == 3 and d["r"] == [140, 141, 142]
+    assert d["t"][0][1] == 2 and d["t"][0][2] == 1  # cross-hive pair falls back to PCIe
+    assert d["p1"] == [4242] and d["p2"] == []
+
+
+def test_mock_init_failure_reported(tmp_path):
+    cfg = tmp_path / "bad.json"
+    cfg.write_text(json.dumps({"fail_init": 34}))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from gpumounter_amd.hw.inventory import Inventory, InventoryError\n"
+            "try:\n    Inventory('mock')\nexcept InventoryError as e:\n    print('ERR', e)\n"
+            % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         env={**os.environ, "GM_AMDSMI_MOCK_CONFIG": str(cfg)}, timeout=60)
+    assert "ERR" in out.stdout and "DRIVER_NOT_LOADED" in out.stdout, out.stdout + out.stderr
+
+
+# ----------------------------------------------------------------------------------- devnodes
+NODES = [DeviceNode("/dev/kfd", 511, 0), DeviceNode("/dev/dri/renderD130", 226, 130),
+         DeviceNode("/dev/dri/card2", 226, 2)]
+
+
+@pytest.mark.parametrize("mode", ["emulate", "procroot"])
+def test_devnodes_create_idempotent_remove(tmp_path, mode):
+    root = tmp_path / "root"
+    (root / "dev").mkdir(parents=True)
+    w = DevNodeWriter(mode)
+    t = Target(root=str(root))
+    assert w.create(t, NODES) == [0, 0, 0]
+    assert w.create(t, NODES) == [1, 1, 1]
+    for n in NODES:
+        assert w.present(t, n)
+        p = root / n.path.lstrip("/")
+        st = os.lstat(p)
+        assert stat.S_IMODE(st.st_mode) == 0o666
+        if os.geteuid() == 0 and mode == "procroot":
+            assert stat.S_ISCHR(st.st_mode) and os.major(st.st_rdev) == n.major
+    assert w.remove(t, NODES) == [0, 0, 0]
+    assert w.remove(t, NODES) == [1, 1, 1]
+    assert not (root / "dev/kfd").exists()
+
+
+def test_devnodes_refuse_symlink_escape(tmp_path):
+    root = tmp_path / "root"
+    outside = tmp_path / "outside"
+    outside.mkdir()
+    (root).mkdir()
+    os.symlink(str(outside), root / "dev")  # hostile container: /dev → host dir
+    w = DevNodeWriter("emulate")
+    with pytest.raises(DevNodeError):
+        w.create(Target(root=str(root)), [NODES[0]])
+    assert os.listdir(outside) == []
+
+
+def test_devnodes_never_clobber_foreign_file(tmp_path):
+    root = tmp_path / "root"
+    (root / "dev" / "dri").mkdir(parents=True)
+    (root / "dev" / "dri" / "renderD130").write_text("tenant data")
+    w = DevNodeWriter("emulate")
+    with pytest.raises(DevNodeError):
+        w.create(Target(root=str(root)), [NODES[1]])
+    with pytest.raises(DevNodeError):
+        w.remove(Target(root=str(root)), [NODES[1]])
+    assert (root / "dev" / "dri" / "renderD130").read_text() == "tenant data"
+
+
+def test_devnodes_procroot_by_pid_of_own_process():
+    """Target by PID resolves /proc/<pid>/root (here: our own root) — read-only stat check."""
+    w = DevNodeWriter("procroot")
+    kind, ma, mi, _ = w.stat(Target(pid=os.getpid()), "/dev/null")
+    assert (kind, ma, mi) == (1, 1, 3)
+    with pytest.raises(DevNodeError):
+        w.create(Target(pid=0), NODES[:1])  # empty container: clear error, no panic
+
+
+# ----------------------------------------------------------------------------------- cgroups
+def _pod(uid="1234-abcd", qos="besteffort"):
+    res = {}
+    if qos == "guaranteed":
+        res = {"limits": {"cpu": "1", "memory": "1Gi"}, "requests": {"cpu": "1", "memory": "1Gi"}}
+    elif qos == "burstable":
+        res = {"requests": {"cpu": "100m"}}
+    return {"metadata": {"uid": uid, "name": "p", "namespace": "ns"},
+            "spec": {"containers": [{"name": "c", "resources": res}]}, "status": {}}
+
+
+@pytest.mark.parametrize("mode", ["v1", "v2"])
+@pytest.mark.parametrize("driver", ["cgroupfs", "systemd"])
+@pytest.mark.parametrize("runtime", ["docker", "containerd", "cri-o"])
+@pytest.mark.parametrize("qos", ["guaranteed", "burstable", "besteffort"])
+def test_cgroup_resolution_matrix(tmp_path, mode, driver, runtime, qos, mock_inventory):
+    node = FakeNode("n", str(tmp_path), mock_inventory.gpus(), cgroup_mode=mode,
+                    cgroup_driver=driver, runtime=runtime)
+    pod = _pod(qos=qos)
+    ctr = node.start_container(pod, "c", [os.getpid()])
+    r = CgroupResolver(node.cgroup_root)      # auto-detect mode and driver
+    assert r.mode == mode
+    d = r.container_dir(pod, ContainerRef("c", runtime, ctr.id, True))
+    assert d == ctr.cgroup_dir
+    assert r.pids(d) == [os.getpid()]
+    if driver == "systemd":
+        assert d.endswith(".scope")
+
+
+def test_cgroup_resolution_missing_raises(tmp_path, mock_inventory):
+    FakeNode("n", str(tmp_path), mock_inventory.gpus())
+    r = CgroupResolver(os.path.join(str(tmp_path), "cgroup"))
+    with pytest.raises(CgroupError):
+        r.container_dir(_pod(), ContainerRef("c", "containerd", "deadbeef", True))
+
+
+def test_v1_backend_writes_kernel_rule_syntax(tmp_path, mock_inventory):
+    node = FakeNode("n", str(tmp_path), mock_inventory.gpus(), cgroup_mode="v1")
+    ctr = node.start_container(_pod(), "c")
+    be = V1Backend()
+    be.apply(ctr.cgroup_dir, NODES, [], NODES)
+    assert open(os.path.join(ctr.cgroup_dir, "devices.allow")).read().splitlines() == [
+        "c 511:0 rw", "c 226:130 rw", "c 226:2 rw"]
+    assert be.allowed(ctr.cgroup_dir) == {(511, 0), (226, 130), (226, 2)}
+    be.apply(ctr.cgroup_dir, [], NODES[1:], NODES[:1])
+    assert open(os.path.join(ctr.cgroup_dir, "devices.deny")).read().splitlines() == [
+        "c 226:130 rw", "c 226:2 rw"]
+    assert be.allowed(ctr.cgroup_dir) == {(511, 0)}
+
+
+def test_v2_recording_backend_program_semantics(tmp_path, mock_inventory):
+    node = FakeNode("n", str(tmp_path), mock_inventory.gpus(), cgroup_mode="v2")
+    ctr = node.start_container(_pod(), "c")
+    be = V2RecordingBackend()
+    be.apply(ctr.cgroup_dir, NODES, [], NODES)
+    st = json.load(open(os.path.join(ctr.cgroup_dir, "gm.bpf.json")))
+    prog = [int(x, 16) for x in st["insns"]]
+    allowed = bpfvm.allowed_pairs(prog, [(511, 0), (226, 130), (226, 2), (226, 131), (1, 3),
+                                         (1, 1)])
+    assert allowed == {(511, 0), (226, 130), (226, 2), (1, 3)}  # ours + runtime's /dev/null
+    assert be.allowed(ctr.cgroup_dir) == {(511, 0), (226, 130), (226, 2)}
+    be.apply(ctr.cgroup_dir, [], NODES, [])
+    assert be.allowed(ctr.cgroup_dir) == set()
+    assert build_program(NODES[:1], chained=False)[-1] == build_program(NODES, chained=False)[-1]
+
+
+def test_host_signal_and_pid_helpers():
+    from gpumounter_amd.node import procs
+
+    p = subprocess.Popen(["sleep", "30"])
+    try:
+        assert procs.alive(p.pid)
+        assert procs.signal_pids([p.pid], 15) == [0]
+        p.wait(timeout=5)
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert procs.signal_pids([2 ** 22 + 7], 0)[0] < 0   # no such process
+    # /dev/null users: our own stdin/stdout may or may not be /dev/null; open one to be sure
+    fd = os.open("/dev/null", os.O_RDONLY)
+    try:
+        assert os.getpid() in procs.filter_dev_users([os.getpid(), 1], 1, 3)
+    finally:
+        os.close(fd)
+
+
+def test_roctx_markers_are_safe_without_profiler():
+    from gpumounter_amd.utils import trace
+
+    with trace.span("outer", a=1) as s:
+        with trace.span("inner"):
+            trace.mark("tick")
+    assert s.children[0].name == "inner" and s.duration_ms >= 0
+    assert "inner" in s.flat()

@@ -1,0 +1,233 @@
+"""Real-kernel enforcement tests for the device-access backends (opt-in: GM_PRIVILEGED_TESTS=1,
+needs root with CAP_SYS_ADMIN/CAP_BPF). They mount a private cgroup2 hierarchy (or use the v1
+devices controller), put a child process into a fresh cgroup, and check that the process can open
+exactly the devices the backend granted — using harmless /dev/null, /dev/zero, /dev/full.
+
+cgroup v2: a "runtime" program (allow /dev/null only) is attached first, exactly like runc does;
+gm_bpf_dev_install then swaps in the gpumounter program that grants /dev/zero and tail-calls the
+runtime program; gm_bpf_dev_restore puts the runtime program back.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+import tempfile
+import uuid
+
+import pytest
+
+from gpumounter_amd import _native
+from gpumounter_amd.models.device import DeviceNode
+from gpumounter_amd.node.cgroup import V1Backend, V2BpfBackend, _rule_array
+
+pytestmark = [pytest.mark.privileged,
+              pytest.mark.skipif(os.environ.get("GM_PRIVILEGED_TESTS") != "1" or os.geteuid() != 0,
+                                 reason="opt-in privileged kernel test (GM_PRIVILEGED_TESTS=1)")]
+
+NULL, ZERO, FULL = DeviceNode("/dev/null", 1, 3), DeviceNode("/dev/zero", 1, 5), \
+    DeviceNode("/dev/full", 1, 7)
+
+PROBE = ("import sys\n"
+         "out=[]\n"
+         "for p in sys.argv[1:]:\n"
+         "    try:\n"
+         "        open(p,'rb').close(); out.append('1')\n"
+         "    except OSError:\n"
+         "        out.append('0')\n"
+         "print(''.join(out))\n")
+
+
+def can_open(cg_procs: str, paths):
+    """Spawn a child, move it into the cgroup before it opens anything, report per-path access."""
+    r, w = os.pipe()
+    pid = os.fork()
+    if pid == 0:  # child: wait until the parent moved us, then exec the probe
+        os.close(w)
+        os.read(r, 1)
+        os.execv(sys.executable, [sys.executable, "-c", PROBE] + list(paths))
+    os.close(r)
+    with open(cg_procs, "w") as fh:
+        fh.write(str(pid))
+    out_r, out_w = os.pipe()
+    os.close(out_r)
+    os.close(out_w)
+    os.write(w, b"x")
+    os.close(w)
+    _, status = os.waitpid(pid, 0)
+    return status
+
+
+def probe_access(cgdir, paths):
+    code = (f"import os,sys\n"
+            f"open({os.path.join(cgdir, 'cgroup.procs')!r},'w').write(str(os.getpid()))\n"
+            + PROBE)
+    res = subprocess.run([sys.executable, "-c", code] + list(paths), capture_output=True,
+                         text=True, timeout=30)
+    assert res.returncode == 0, res.stderr
+    return res.stdout.strip()
+
+
+@pytest.fixture
+def bpffs():
+    d = tempfile.mkdtemp(prefix="gm-bpffs-")
+    subprocess.run(["mount", "-t", "bpf", "bpf", d], check=True)
+    try:
+        yield d
+    finally:
+        subprocess.run(["umount", d], check=True)
+        os.rmdir(d)
+
+
+@pytest.fixture
+def cgroup2_child():
+    mnt = tempfile.mkdtemp(prefix="gm-cg2-")
+    subprocess.run(["mount", "-t", "cgroup2", "none", mnt], check=True)
+    cg = os.path.join(mnt, "gm-test-" + uuid.uuid4().hex[:8])
+    os.mkdir(cg)
+    try:
+        yield cg
+    finally:
+        # move anything left back to the root, then clean up
+        try:
+            with open(os.path.join(cg, "cgroup.procs")) as fh:
+                for pid in fh.read().split():
+                    with open(os.path.join(mnt, "cgroup.procs"), "w") as out:
+                        out.write(pid)
+        except OSError:
+            pass
+        os.rmdir(cg)
+        subprocess.run(["umount", mnt], check=True)
+        os.rmdir(mnt)
+
+
+def attach_runtime_program(cg):
+    """Mimic runc: allow /dev/null rw + mknod, deny everything else, ALLOW_MULTI."""
+    rules = _rule_array([_native.DevRule(b"c", 7, 1, 0, 1, 3)])
+    lib = _native.host()
+    need = -lib.gm_bpf_dev_build(rules, 1, 0, -1, None, 0)
+    buf = (C.c_uint64 * need)()
+    n = lib.gm_bpf_dev_build(rules, 1, 0, -1, buf, need)
+    fd = lib.gm_bpf_dev_load(buf, n, b"runc_devices", None, 0)
+    assert fd >= 0, os.strerror(-fd)
+    # BPF_PROG_ATTACH through a throwaway install path is not possible (ours would replace it),
+    # so attach with raw syscall via ctypes
+    import ctypes.util
+
+    libc = C.CDLL(ctypes.util.find_library("c"), use_errno=True)
+    cgfd = os.open(cg, os.O_RDONLY | os.O_DIRECTORY)
+    attr = (C.c_uint8 * 128)()
+    # union bpf_attr for BPF_PROG_ATTACH: target_fd, attach_bpf_fd, attach_type, attach_flags
+    C.memmove(attr, (C.c_uint32 * 4)(cgfd, fd, 6, 2), 16)   # BPF_CGROUP_DEVICE=6, ALLOW_MULTI=2
+    rc = libc.syscall(321, 8, attr, 128)  # __NR_bpf=321, BPF_PROG_ATTACH=8
+    os.close(cgfd)
+    assert rc == 0, os.strerror(C.get_errno())
+    return fd
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_cgroup_v2_bpf_install_and_restore(cgroup2_child, bpffs, pinned):
+    cg = cgroup2_child
+    paths = [NULL.path, ZERO.path, FULL.path]
+    assert probe_access(cg, paths) == "111"          # no program: unrestricted
+    attach_runtime_program(cg)
+    assert probe_access(cg, paths) == "100"          # runtime policy: only /dev/null
+    be = V2BpfBackend(bpffs if pinned else "")
+    be.apply(cg, [ZERO], [], [ZERO])                 # gpumounter grants /dev/zero
+    assert probe_access(cg, paths) == "110"
+    ids = (C.c_uint32 * 8)()
+    n, flags = C.c_uint32(0), C.c_uint32(0)
+    assert _native.host().gm_bpf_dev_query(cg.encode(), ids, 8, C.byref(n), C.byref(flags)) == 0
+    assert n.value == 1                              # replaced, not stacked
+    name = C.create_string_buffer(32)
+    _native.host().gm_bpf_prog_name(ids[0], name, 32)
+    assert name.value == b"gm_devallow"
+    be.apply(cg, [FULL], [], [ZERO, FULL])           # update: chain target preserved
+    assert probe_access(cg, paths) == "111"
+    be.apply(cg, [], [ZERO], [FULL])                 # revoke /dev/zero
+    assert probe_access(cg, paths) == "101"
+    be.apply(cg, [], [FULL], [])                     # last GPU gone: runtime program restored
+    assert probe_access(cg, paths) == "100"
+    _native.host().gm_bpf_dev_query(cg.encode(), ids, 8, C.byref(n), C.byref(flags))
+    _native.host().gm_bpf_prog_name(ids[0], name, 32)
+    assert n.value == 1 and name.value == b"runc_devices"
+    assert not [f for f in os.listdir(bpffs) if f.startswith("gm_")]  # pin removed
+
+
+def test_cgroup_v2_chain_lost_falls_back_to_oci_defaults(cgroup2_child):
+    """Unpinned map + 'worker restart' (kept fd dropped): reinstall compiles in the OCI defaults."""
+    cg = cgroup2_child
+    attach_runtime_program(cg)
+    be = V2BpfBackend("")
+    be.apply(cg, [ZERO], [], [ZERO])
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "110"
+    # simulate the worker process dying: close every kept map fd → the kernel empties the slot
+    import gc
+    lib = _native.host()
+    ino = os.stat(cg).st_ino
+    # the C++ registry holds one dup'd fd; find and close it via /proc/self/fd of bpf-map type
+    for fd in os.listdir("/proc/self/fd"):
+        try:
+            if os.readlink(f"/proc/self/fd/{fd}") == "anon_inode:bpf-map":
+                os.close(int(fd))
+        except OSError:
+            pass
+    gc.collect()
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "010"  # chain broken
+    be.apply(cg, [ZERO], [], [ZERO])                 # reconcile re-install: OCI defaults inline
+    # the OCI default list allows /dev/null, /dev/zero and /dev/full (1:3, 1:5, 1:7)
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "111"
+    assert ino
+
+
+def test_cgroup_v1_devices_controller():
+    base = "/sys/fs/cgroup/devices"
+    if not os.path.isdir(base):
+        pytest.skip("no v1 devices controller")
+    cg = os.path.join(base, "gm-test-" + uuid.uuid4().hex[:8])
+    os.mkdir(cg)
+    try:
+        with open(os.path.join(cg, "devices.deny"), "w") as fh:
+            fh.write("a")
+        with open(os.path.join(cg, "devices.allow"), "w") as fh:
+            fh.write("c 1:3 rwm")
+        paths = [NULL.path, ZERO.path]
+        assert probe_access(cg, paths) == "10"
+        be = V1Backend()
+        be.apply(cg, [ZERO], [], [ZERO])
+        assert probe_access(cg, paths) == "11"
+        assert (1, 5) in be.allowed(cg)
+        be.apply(cg, [], [ZERO], [])
+        assert probe_access(cg, paths) == "10"
+    finally:
+        with open(os.path.join(cg, "cgroup.procs")) as fh:
+            for pid in fh.read().split():
+                with open(os.path.join(base, "cgroup.procs"), "w") as out:
+                    out.write(pid)
+        os.rmdir(cg)
+
+
+def test_devnodes_real_mknod_via_setns(tmp_path):
+    """procroot + setns modes against a real process in a private mount namespace."""
+    root = tmp_path / "ctr"
+    (root / "dev").mkdir(parents=True)
+    # a sleeper in a new mount namespace whose /dev is a private tmpfs
+    child = subprocess.Popen(["unshare", "-m", "--propagation", "private", "sh", "-c",
+                              f"mount -t tmpfs tmpfs {root}/dev && echo ok && sleep 60"],
+                             stdout=subprocess.PIPE, text=True)
+    try:
+        assert child.stdout.readline().strip() == "ok"
+        from gpumounter_amd.node.devnodes import DevNodeWriter, Target
+
+        # the node created through the child's mount namespace must be invisible from ours
+        w = DevNodeWriter("setns")
+        node = DeviceNode(f"{root}/dev/dri/renderD128", 226, 128)
+        assert w.create(Target(pid=child.pid), [node]) == [0]
+        assert not os.path.exists(f"{root}/dev/dri/renderD128")
+        assert w.present(Target(pid=child.pid), node)
+        w2 = DevNodeWriter("procroot")
+        assert w2.present(Target(pid=child.pid), node)
+        assert w2.remove(Target(pid=child.pid), [node]) == [0]
+        assert not w.present(Target(pid=child.pid), node)
+    finally:
+        child.kill()
+        child.wait()

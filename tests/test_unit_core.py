@@ -1,0 +1,164 @@
+"""Pure-logic unit tests: config layering, pod helpers (QoS, quantities, container ids), the gRPC
+schema's wire compatibility with the reference api.proto, and device-model helpers."""
+import re
+
+import pytest
+
+from gpumounter_amd.api import gpu_mount as api
+from gpumounter_amd.api import podresources as pr
+from gpumounter_amd.api.protodef import fields_of
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.models.device import AmdGpu, find_gpu, normalize_device_id
+from gpumounter_amd.utils.config import Config
+
+# ----------------------------------------------------------------------------------- config
+
+
+def test_config_defaults_match_reference_ports_and_names():
+    c = Config.load(env={})
+    assert (c.master_port, c.worker_port) == (8080, 1200)        # main.go:237, worker main.go:24
+    assert c.pool_namespace == "gpu-pool"                         # types.go:18
+    assert c.worker_label == "app=gpu-mounter-worker"             # master main.go:256
+    assert c.kubelet_socket == "/var/lib/kubelet/pod-resources/kubelet.sock"  # types.go:6-7
+    assert c.resource_name == "amd.com/gpu"
+
+
+def test_config_layering_yaml_env_overrides(tmp_path):
+    f = tmp_path / "gm.yaml"
+    f.write_text("worker_port: 1300\ncgroup_mode: v1\ntopology_policy: first-fit\nfoo: 1\n")
+    env = {"GM_CONFIG": str(f), "GM_WORKER_PORT": "1400", "CGROUP_DRIVER": "systemd",
+           "NODE_NAME": "n7", "GM_ROCTX": "false", "GM_KILL_GRACE_S": "2.5"}
+    c = Config.load(env=env, master_port=9000)
+    assert c.worker_port == 1400          # env beats file
+    assert c.cgroup_mode == "v1"          # file
+    assert c.cgroup_driver == "systemd"   # reference env name honoured
+    assert c.node_name == "n7"
+    assert c.roctx is False and c.kill_grace_s == 2.5
+    assert c.master_port == 9000          # explicit override
+    assert c.extra == {"foo": 1}
+
+
+@pytest.mark.parametrize("bad", [{"GM_CGROUP_MODE": "v3"}, {"GM_DEVNODE_MODE": "x"},
+                                 {"GM_WORKER_PORT": "0"}, {"GM_ROCTX": "maybe"}])
+def test_config_rejects_invalid(bad):
+    with pytest.raises(ValueError):
+        Config.load(env=bad)
+
+
+# ----------------------------------------------------------------------------------- pods
+
+
+@pytest.mark.parametrize("q,v", [("100m", 0.1), ("1", 1), ("1Gi", 2 ** 30), ("2k", 2000),
+                                 ("1.5", 1.5), ("1e3", 1000), ("512Mi", 512 * 2 ** 20)])
+def test_parse_quantity(q, v):
+    assert float(podu.parse_quantity(q)) == pytest.approx(v)
+
+
+def _pod(*containers):
+    return {"spec": {"containers": [{"name": f"c{i}", "resources": r}
+                                    for i, r in enumerate(containers)]}, "status": {}}
+
+
+@pytest.mark.parametrize("containers,qos", [
+    ([{}], "BestEffort"),
+    ([{"limits": {"cpu": "1", "memory": "1Gi"}}], "Guaranteed"),       # requests default to limits
+    ([{"limits": {"cpu": "1", "memory": "1Gi"}, "requests": {"cpu": "1", "memory": "1Gi"}}],
+     "Guaranteed"),
+    ([{"limits": {"cpu": "2", "memory": "1Gi"}, "requests": {"cpu": "1", "memory": "1Gi"}}],
+     "Burstable"),
+    ([{"requests": {"cpu": "100m"}}], "Burstable"),
+    ([{"limits": {"cpu": "1", "memory": "1Gi"}}, {}], "Burstable"),    # one container unset
+    ([{"limits": {"amd.com/gpu": "1"}}], "BestEffort"),                # extended resources ignored
+    ([{"limits": {"cpu": "1"}}], "Burstable"),
+])
+def test_qos_classifier(containers, qos):
+    pod = _pod(*containers)
+    # kubelet defaults requests to limits when only limits are set
+    for c in pod["spec"]["containers"]:
+        lim = c["resources"].get("limits", {})
+        c["resources"].setdefault("requests", {k: v for k, v in lim.items()
+                                               if k in ("cpu", "memory")})
+    assert podu.qos_class(pod) == qos
+
+
+def test_container_id_runtimes_and_all_containers():
+    pod = {"status": {"containerStatuses": [
+        {"name": "a", "containerID": "docker://abc", "state": {"running": {}}},
+        {"name": "b", "containerID": "containerd://def", "state": {"running": {}}},
+        {"name": "c", "containerID": "cri-o://123", "state": {"waiting": {}}},
+        {"name": "d"}]}}
+    refs = podu.running_containers(pod)
+    assert [(r.name, r.runtime, r.id, r.running) for r in refs] == [
+        ("a", "docker", "abc", True), ("b", "containerd", "def", True),
+        ("c", "cri-o", "123", False)]
+    assert [r.name for r in podu.running_containers(pod, "b")] == ["b"]
+
+
+def test_unschedulable_detection_any_condition():
+    pod = {"status": {"conditions": [{"type": "Ready", "status": "False"},
+                                     {"type": "PodScheduled", "status": "False",
+                                      "reason": "Unschedulable", "message": "0/1 nodes"}]}}
+    assert podu.is_unschedulable(pod) == "0/1 nodes"
+    assert podu.is_unschedulable({"status": {}}) is None
+
+
+# ----------------------------------------------------------------------------------- schema
+
+
+def test_wire_bytes_identical_to_reference_encoding():
+    # golden bytes produced for the reference's AddGPURequest{pod_name:"p", namespace:"default",
+    # gpu_num:2} (SURVEY §0.1 probe)
+    r = api.AddGPURequest(pod_name="p", namespace="default", gpu_num=2)
+    assert r.SerializeToString() == b"\n\x01p\x12\x07default\x18\x02"
+    assert api.AddGPURequest.FromString(b"\n\x01p\x12\x07default\x18\x02 \x01").is_entire_mount
+
+
+def test_reference_field_numbers_and_enums_preserved():
+    assert fields_of(api.AddGPURequest)[:4] == [("pod_name", 1), ("namespace", 2),
+                                                ("gpu_num", 3), ("is_entire_mount", 4)]
+    assert fields_of(api.RemoveGPURequest)[:4] == [("pod_name", 1), ("namespace", 2),
+                                                   ("uuids", 3), ("force", 4)]
+    assert fields_of(api.AddGPUResponse)[0] == ("add_gpu_result", 1)
+    assert fields_of(api.RemoveGPUResponse)[0] == ("remove_gpu_result", 1)
+    assert (api.AddGPUResponse.Success, api.AddGPUResponse.InsufficientGPU,
+            api.AddGPUResponse.PodNotFound) == (0, 1, 2)
+    assert (api.RemoveGPUResponse.Success, api.RemoveGPUResponse.GPUBusy,
+            api.RemoveGPUResponse.PodNotFound, api.RemoveGPUResponse.GPUNotFound) == (0, 1, 2, 4)
+    assert api.ADD_GPU == "/gpu_mount.AddGPUService/AddGPU"
+    assert api.REMOVE_GPU == "/gpu_mount.RemoveGPUService/RemoveGPU"
+
+
+def test_proto_text_matches_runtime_descriptors():
+    import os
+
+    path = os.path.join(os.path.dirname(api.__file__), "gpu_mount.proto")
+    text = open(path).read()
+    for cls in (api.AddGPURequest, api.AddGPUResponse, api.RemoveGPURequest,
+                api.RemoveGPUResponse, api.Device, api.StageTiming):
+        body = re.search(r"message %s \{(.*?)\n\}" % cls.DESCRIPTOR.name, text, re.S).group(1)
+        declared = {(m.group(2), int(m.group(3)))
+                    for m in re.finditer(r"^\s+(repeated \S+|\S+) (\w+) = (\d+);", body, re.M)}
+        assert declared == set(fields_of(cls)), cls.DESCRIPTOR.name
+
+
+def test_podresources_v1_is_wire_compatible_with_v1alpha1():
+    r = pr.V1.ListPodResourcesResponse()
+    c = r.pod_resources.add(name="p", namespace="ns").containers.add(name="c")
+    d = c.devices.add(resource_name="amd.com/gpu", device_ids=["0000:05:00.0"])
+    d.topology.nodes.add(ID=1)
+    old = pr.V1ALPHA1.ListPodResourcesResponse.FromString(r.SerializeToString())
+    assert old.pod_resources[0].containers[0].devices[0].device_ids == ["0000:05:00.0"]
+
+
+# ----------------------------------------------------------------------------------- device
+
+
+def test_device_nodes_and_ledger_keys():
+    g = AmdGpu(index=3, uuid="u-3", bdf="0000:75:00.0", render_minor=131, card_minor=3)
+    nodes = g.device_nodes()
+    assert [(n.path, n.major, n.minor) for n in nodes] == [
+        ("/dev/dri/renderD131", 226, 131), ("/dev/dri/card3", 226, 3)]
+    assert nodes[0].cgroup_rule() == "c 226:131 rw"
+    for key in ("u-3", "0000:75:00.0", "75:00.0", "renderD131", "CARD3", "GPU-u-3"):
+        assert find_gpu([g], key) is g, key
+    assert normalize_device_id(" ABC ") == "abc"
