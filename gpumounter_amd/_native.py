@@ -101,7 +101,9 @@ def mock_smi_path() -> str:
 
 
 def mock_smi() -> C.CDLL:
-    return _load("libamd_smi_mock.so", "host")
+    lib = _load("libamd_smi_mock.so", "host")
+    lib.gm_mock_set_procs_file.argtypes = [C.c_char_p]
+    return lib
 
 
 # ------------------------------------------------------------------------------ gm_host

@@ -445,8 +445,11 @@ class FakeCluster:
         r.add_delete("/api/v1/namespaces/{ns}/pods/{name}", self._h_delete)
         r.add_patch("/api/v1/namespaces/{ns}/pods/{name}", self._h_patch)
         r.add_get("/api/v1/nodes", self._h_nodes)
-        r.add_get("/healthz", lambda req: web.Response(text="ok"))
+        r.add_get("/healthz", self._h_healthz)
         return app
+
+    async def _h_healthz(self, req: web.Request) -> web.Response:
+        return web.Response(text="ok")
 
     async def _pre(self, req: web.Request) -> None:
         self.request_count += 1
@@ -501,18 +504,25 @@ class FakeCluster:
         self.watchers.append(entry)
         timeout = float(req.query.get("timeoutSeconds", "300"))
         deadline = time.monotonic() + timeout
+        idle = 0.0
         try:
             while True:
                 left = deadline - time.monotonic()
                 if left <= 0:
                     break
+                if req.transport is None or req.transport.is_closing():
+                    break  # client went away
                 try:
-                    et, obj = await asyncio.wait_for(q.get(), timeout=min(left, 30))
+                    et, obj = await asyncio.wait_for(q.get(), timeout=min(left, 0.5))
                 except asyncio.TimeoutError:
-                    await resp.write(json.dumps({"type": "BOOKMARK", "object": {
-                        "kind": "Pod", "metadata": {"resourceVersion": str(self.rv)}}}).encode()
-                        + b"\n")
+                    idle += 0.5
+                    if idle >= 30:
+                        idle = 0.0
+                        await resp.write(json.dumps({"type": "BOOKMARK", "object": {
+                            "kind": "Pod", "metadata": {"resourceVersion": str(self.rv)}}}
+                        ).encode() + b"\n")
                     continue
+                idle = 0.0
                 await resp.write(json.dumps({"type": et, "object": obj}).encode() + b"\n")
         except (ConnectionResetError, asyncio.CancelledError):
             pass

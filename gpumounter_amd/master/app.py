@@ -128,9 +128,8 @@ class Master:
         r.add_post("/removegpu/namespace/{namespace}/pod/{pod}/force/{force}", self.remove_gpu)
         r.add_get("/api/v1/namespaces/{namespace}/pods/{pod}/gpus", self.pod_gpus)
         r.add_get("/api/v1/nodes/{node}/gpus", self.node_gpus)
-        r.add_get("/healthz", lambda req: web.Response(text="ok"))
-        r.add_get("/metrics", lambda req: web.Response(body=self.metrics.render(),
-                                                       content_type="text/plain"))
+        r.add_get("/healthz", self.healthz)
+        r.add_get("/metrics", self.metrics_handler)
         return app
 
     async def start(self, port: Optional[int] = None) -> None:
@@ -150,6 +149,12 @@ class Master:
         await self.kube.close()
 
     # ------------------------------------------------------------------------ handlers
+    async def healthz(self, request: web.Request) -> web.Response:
+        return web.Response(text="ok")
+
+    async def metrics_handler(self, request: web.Request) -> web.Response:
+        return web.Response(body=self.metrics.render(), content_type="text/plain")
+
     async def index(self, request: web.Request) -> web.Response:
         return _text("This is gpu mounter api!")
 
@@ -161,7 +166,9 @@ class Master:
         self.metrics.http_requests.labels(route=route, code=str(status)).inc()
         if self._wants_json(request):
             payload = dict(payload)
-            payload.setdefault("message", text.rstrip("\n"))
+            if payload.get("message") and payload["message"] != text.rstrip("\n"):
+                payload["detail"] = payload["message"]
+            payload["message"] = text.rstrip("\n")
             payload["code"] = status
             return web.json_response(payload, status=status)
         return _text(text, status)
@@ -307,9 +314,15 @@ class Master:
             api.NODE_STATUS, request_serializer=api.NodeStatusRequest.SerializeToString,
             response_deserializer=api.NodeStatusResponse.FromString)
         st = json.loads((await stub(api.NodeStatusRequest(), timeout=30)).json)
-        mine = [g for g in st["gpus"] if g.get("pod_name", "").startswith(name)]
+        uid = podu.uid_of(pod)
+        held = {(p["namespace"], p["name"]) for p in st.get("placeholders", [])
+                if p["owner"] == name and p["owner_namespace"] == ns and p["owner_uid"] == uid}
+        hot = [dict(g, source="hot-mount") for g in st["gpus"]
+               if (g.get("namespace"), g.get("pod_name")) in held]
+        own = [dict(g, source="pod-spec") for g in st["gpus"]
+               if (g.get("namespace"), g.get("pod_name")) == (ns, name)]
         return web.json_response({"pod": f"{ns}/{name}", "node": podu.node_of(pod),
-                                  "gpus": mine})
+                                  "gpus": own + hot})
 
 
 async def serve(cfg) -> None:

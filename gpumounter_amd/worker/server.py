@@ -120,10 +120,9 @@ class Worker:
         hp = self.cfg.metrics_port if http_port is None else http_port
         if hp is not None and hp >= 0:
             app = web.Application()
-            app.router.add_get("/healthz", lambda r: web.Response(text="ok"))
+            app.router.add_get("/healthz", self._healthz)
             app.router.add_get("/readyz", self._readyz)
-            app.router.add_get("/metrics", lambda r: web.Response(
-                body=self.metrics.render(), content_type="text/plain"))
+            app.router.add_get("/metrics", self._metrics)
             app.router.add_get("/status", self._http_status)
             self.http_runner = web.AppRunner(app, access_log=None)
             await self.http_runner.setup()
@@ -136,6 +135,12 @@ class Worker:
         _log.info("worker %s serving gRPC :%d http :%d (cgroup %s/%s, devnodes %s, ledger %s)",
                   self.cfg.node_name, self.grpc_port, self.http_port, self.resolver.mode,
                   self.backend.name, self.cfg.devnode_mode, self.ledger.api_version)
+
+    async def _healthz(self, request):
+        return web.Response(text="ok")
+
+    async def _metrics(self, request):
+        return web.Response(body=self.metrics.render(), content_type="text/plain")
 
     async def _readyz(self, request):
         return web.Response(text="ready" if self.ready else "starting",

@@ -346,7 +346,21 @@ class GpuMountService:
                 if g is not None:
                     g.pod_name, g.namespace, g.container = a.pod, a.namespace, a.container
                     g.state = g.state.ALLOCATED
+        phs = []
+        for p in self.ph.informer.list(lambda p: not p["metadata"].get("deletionTimestamp")):
+            md = p["metadata"]
+            ann = md.get("annotations") or {}
+            ids = next((a.device_ids for a in ledger
+                        if (a.namespace, a.pod) == (md["namespace"], md["name"])), ())
+            phs.append({"namespace": md["namespace"], "name": md["name"],
+                        "owner": ann.get("gpumounter.amd.com/owner-name", ""),
+                        "owner_namespace": (md.get("labels") or {}).get(
+                            "gpumounter.amd.com/owner-namespace", ""),
+                        "owner_uid": ann.get("gpumounter.amd.com/owner-uid", ""),
+                        "mode": ann.get("gpumounter.amd.com/mount-mode", ""),
+                        "device_ids": list(ids)})
         out = {"node": self.cfg.node_name, "gpus": [g.to_dict() for g in gpus],
+               "placeholders": phs,
                "topology": topology.describe(gpus, self.inv.links()),
                "ledger_api": self.ledger.api_version, "kfd_major": self.inv.kfd_major}
         if include_processes:

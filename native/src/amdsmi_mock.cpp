@@ -452,6 +452,12 @@ amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char*
   return AMDSMI_STATUS_SUCCESS;
 }
 
+// Test hook: point the live process table at another file ("" disables).
+void gm_mock_set_procs_file(const char* path) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_procs_file = path ? path : "";
+}
+
 // Test hook: number of amdsmi_init() calls since load (proves the shim does not re-init per query).
 int gm_mock_init_calls(void) {
   std::lock_guard<std::mutex> lk(g_mu);

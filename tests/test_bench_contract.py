@@ -1,0 +1,51 @@
+"""bench.py contract on CPU: single process and a 2-rank torch.distributed (gloo) launch, with the
+mock inventory. The GPU box runs the same script with the real libamd_smi + HIP verification."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+        "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _last_json(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_single_process_json_line():
+    env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
+    res = subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "1",
+                          "--amdsmi", "mock"], cwd=ROOT, capture_output=True, text=True,
+                         timeout=300, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _last_json(res.stdout)
+    assert KEYS <= set(d)
+    assert d["metric"] == "p50_gpu_attach_latency_ms" and d["higher_is_better"] is False
+    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["value"] > 0
+    assert d["ledger_audit_issues"] == 0 and d["final_orphans"] == 0
+    assert d["placeholders_left"] == 0
+
+
+def test_bench_two_rank_distributed_launch():
+    env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--steps", "4", "--warmup", "1", "--amdsmi", "mock"]
+    res = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _last_json(res.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["gpus_per_pod"] == 2
+    assert d["ledger_audit_issues"] == 0

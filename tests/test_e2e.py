@@ -1,0 +1,419 @@
+"""End-to-end behaviour through the real master HTTP API → worker gRPC → C++ node ops, on the
+hermetic control plane (reference behaviour table: SURVEY §2.5; defects fixed: §2.6)."""
+import asyncio
+import os
+import subprocess
+
+import pytest
+
+from gpumounter_amd import _native
+from gpumounter_amd.fakes.harness import LocalCluster
+from gpumounter_amd.models.types import LABEL_OWNER
+
+
+def run(coro_fn, **kw):
+    async def main():
+        async with LocalCluster(**kw) as lc:
+            return await coro_fn(lc)
+    return asyncio.run(main())
+
+
+def node_of(lc):
+    return lc.nodes["node-0"].node
+
+
+async def text_get(lc, path):
+    async with lc.session.get(lc.master_url + path) as r:
+        return r.status, await r.text()
+
+
+# ------------------------------------------------------------------------------ HTTP contract
+def test_reference_text_contract_success_path():
+    async def body(lc):
+        lc.tenant("gpu-pod")
+        assert await text_get(lc, "/") == (200, "This is gpu mounter api!\n")
+        code, text = await lc.add("default", "gpu-pod", 2, accept_json=False)
+        assert (code, text) == (200, "Add GPU Success\n")
+        # the reference QuickStart's curl: repeated urlencoded uuids, force=1
+        st = await lc.nodes["node-0"].worker.service.pod_state(lc.cluster.get("default",
+                                                                              "gpu-pod"))
+        uuids = [g.uuid for g in st.hot]
+        code, text = await lc.remove("default", "gpu-pod", uuids, force=True, accept_json=False)
+        assert (code, text) == (200, "Remove GPU Success\n")
+    run(body)
+
+
+@pytest.mark.parametrize("path,code,text", [
+    ("/addgpu/namespace/default/pod/p/gpu/abc/isEntireMount/false", 400,
+     "Invalid param gpuNum: abc\n"),
+    ("/addgpu/namespace/default/pod/p/gpu/1/isEntireMount/yes", 400,
+     "Invalid param isEntireMount: yes(should be true or false)\n"),
+    ("/addgpu/namespace/default/pod/p/gpu/99999999999/isEntireMount/false", 400,
+     "Invalid param gpuNum: 99999999999\n"),
+    ("/addgpu/namespace/default/pod/p/gpu/0/isEntireMount/true", 400,
+     "Invalid param gpuNum: 0\n"),                    # reference: worker divide-by-zero panic
+    ("/addgpu/namespace/default/pod/nope/gpu/1/isEntireMount/T", 404,
+     "No pod: nope in namespace: default\n"),
+])
+def test_add_parameter_validation(path, code, text):
+    async def body(lc):
+        lc.tenant("p")
+        assert await text_get(lc, path) == (code, text)
+    run(body)
+
+
+def test_remove_parameter_validation():
+    async def body(lc):
+        lc.tenant("p")
+        code, text = await lc.remove("default", "p", [], accept_json=False)
+        assert (code, text) == (400, "Invalid parameter\n")
+        async with lc.session.post(lc.master_url + "/removegpu/namespace/default/pod/p/force/x",
+                                   data={"uuids": "u"}) as r:
+            assert (r.status, await r.text()) == (
+                400, "Invalid parameter force: x(should be true or false)\n")
+        code, text = await lc.remove("default", "ghost", ["u"], accept_json=False)
+        assert (code, text) == (404, "No pod: ghost in namespace: default\n")
+        code, text = await lc.remove("default", "p", ["bogus"], accept_json=False)
+        assert (code, text) == (400, "Invalid UUIDs: bogus\n")
+    run(body)
+
+
+@pytest.mark.parametrize("entire", [True, False])
+def test_insufficient_gpus_is_all_or_nothing(entire):
+    async def body(lc):
+        lc.tenant("big")
+        code, text = await lc.add("default", "big", 9, entire=entire, accept_json=False)
+        assert (code, text) == (500, "Insufficient GPU on Node: node-0\n")
+        await asyncio.sleep(0.05)
+        assert lc.cluster.placeholders() == []          # rollback deleted every placeholder
+        assert node_of(lc).allocated == {}
+        assert not await lc.audit("default", "big")
+    run(body)
+
+
+# ------------------------------------------------------------------------------ policy
+def test_mount_policy_matches_reference_can_mount():
+    async def body(lc):
+        lc.tenant("e")
+        lc.tenant("s")
+        assert (await lc.add("default", "e", 2, entire=True))[0] == 200
+        code, b = await lc.add("default", "e", 1)              # entire → no more adds
+        assert code == 500 and "policy" in b["error"].lower()
+        assert (await lc.add("default", "s", 1))[0] == 200
+        code, b = await lc.add("default", "s", 2, entire=True)  # mounted → no entire
+        assert code == 500
+        assert (await lc.add("default", "s", 1))[0] == 200      # single after single: fine
+    run(body)
+
+
+def test_entire_mount_removes_as_a_whole():
+    async def body(lc):
+        lc.tenant("e")
+        code, b = await lc.add("default", "e", 3, entire=True)
+        assert code == 200 and len(b["devices"]) == 3
+        assert len(lc.cluster.placeholders()) == 1             # one placeholder holds 3 GPUs
+        ids = [d["bdf"] for d in b["devices"]]
+        code, _ = await lc.remove("default", "e", ids[:2])     # partial removal refused
+        assert code == 400
+        code, b2 = await lc.remove("default", "e", ids)
+        assert code == 200 and len(b2["devices"]) == 3
+        assert lc.cluster.placeholders() == []
+    run(body)
+
+
+def test_single_mount_partial_removal_and_any_id_spelling():
+    async def body(lc):
+        lc.tenant("s")
+        code, b = await lc.add("default", "s", 3)
+        assert code == 200 and len(lc.cluster.placeholders()) == 3
+        d0, d1 = b["devices"][0], b["devices"][1]
+        code, _ = await lc.remove("default", "s", [d0["bdf"], "bogus"])
+        assert code == 400 and len(lc.cluster.placeholders()) == 3  # nothing removed
+        code, _ = await lc.remove("default", "s", [d0["uuid"], f"renderD{d1['render_minor']}"])
+        assert code == 200 and len(lc.cluster.placeholders()) == 1
+        assert not await lc.audit("default", "s")
+        cid = lc.container_ids("default", "s")[0]
+        devs = node_of(lc).container_devices(cid)
+        assert "dev/kfd" in devs and len([d for d in devs if "renderD" in d]) == 1
+    run(body)
+
+
+def test_kfd_follows_first_and_last_gpu():
+    async def body(lc):
+        lc.tenant("k")
+        cid = lc.container_ids("default", "k")[0]
+        _, b1 = await lc.add("default", "k", 1)
+        _, b2 = await lc.add("default", "k", 1)
+        assert "dev/kfd" in node_of(lc).container_devices(cid)
+        await lc.remove("default", "k", [b1["devices"][0]["uuid"]])
+        assert "dev/kfd" in node_of(lc).container_devices(cid)
+        await lc.remove("default", "k", [b2["devices"][0]["uuid"]])
+        assert node_of(lc).container_devices(cid) == []
+        assert not await lc.audit("default", "k")
+    run(body)
+
+
+# ------------------------------------------------------------------------------ busy / force
+def test_busy_gpu_refused_then_force_kills(tmp_path, mock_inventory):
+    sleeper = subprocess.Popen(["sleep", "60"])
+    procs = tmp_path / "procs"
+    _native.mock_smi().gm_mock_set_procs_file(str(procs).encode())
+    try:
+        async def body(lc):
+            lc.tenant("busy", pids={"main": [sleeper.pid]})
+            _, b = await lc.add("default", "busy", 1)
+            dev = b["devices"][0]
+            procs.write_text(f"{dev['index']} {sleeper.pid} 4096 python\n")
+            code, text = await lc.remove("default", "busy", [dev["uuid"]], accept_json=False)
+            assert (code, text) == (400, f"Pod: busy has running processes on GPU: "
+                                         f"{dev['uuid']}\n")
+            assert len(lc.cluster.placeholders()) == 1 and not await lc.audit("default", "busy")
+            code, b2 = await lc.remove("default", "busy", [dev["uuid"]], force=True)
+            assert code == 200 and b2["killed_pids"] == [sleeper.pid]
+        run(body)
+        sleeper.wait(timeout=10)
+        assert sleeper.returncode == -15
+    finally:
+        _native.mock_smi().gm_mock_set_procs_file(b"")
+        if sleeper.poll() is None:
+            sleeper.kill()
+
+
+def test_processes_outside_the_pod_do_not_make_it_busy(tmp_path, mock_inventory):
+    procs = tmp_path / "procs"
+    _native.mock_smi().gm_mock_set_procs_file(str(procs).encode())
+    try:
+        async def body(lc):
+            lc.tenant("a", pids={"main": [os.getpid()]})
+            _, b = await lc.add("default", "a", 1)
+            procs.write_text(f"{b['devices'][0]['index']} 1 0 init\n")  # someone else's process
+            code, _ = await lc.remove("default", "a", [b["devices"][0]["uuid"]])
+            assert code == 200
+        run(body)
+    finally:
+        _native.mock_smi().gm_mock_set_procs_file(b"")
+
+
+# ------------------------------------------------------------------------------ variants
+@pytest.mark.parametrize("cgroup_mode,driver,runtime", [
+    ("v1", "cgroupfs", "docker"), ("v1", "systemd", "containerd"),
+    ("v2", "systemd", "cri-o"), ("v2", "cgroupfs", "containerd")])
+def test_runtime_and_cgroup_variants_with_multi_container_pods(cgroup_mode, driver, runtime):
+    async def body(lc):
+        lc.tenant("mc", containers=["trainer", "sidecar"], qos="burstable")
+        code, b = await lc.add("default", "mc", 2)
+        assert code == 200
+        for cid in lc.container_ids("default", "mc"):
+            devs = node_of(lc).container_devices(cid)
+            assert sum("renderD" in d for d in devs) == 2 and "dev/kfd" in devs
+        assert not await lc.audit("default", "mc")
+        await lc.remove("default", "mc", [d["uuid"] for d in b["devices"]])
+        for cid in lc.container_ids("default", "mc"):
+            assert node_of(lc).container_devices(cid) == []
+        assert not await lc.audit("default", "mc")
+    run(body, cgroup_mode=cgroup_mode, cgroup_driver=driver, runtime=runtime)
+
+
+def test_named_container_only():
+    async def body(lc):
+        lc.tenant("two", containers=["a", "b"])
+        async with lc.session.get(lc.master_url + "/addgpu/namespace/default/pod/two/gpu/1/"
+                                  "isEntireMount/false?container=b") as r:
+            assert r.status == 200
+        ca, cb = lc.container_ids("default", "two")
+        assert node_of(lc).container_devices(ca) == []
+        assert "dev/kfd" in node_of(lc).container_devices(cb)
+    run(body)
+
+
+def test_pod_with_own_gpus_keeps_them():
+    """The pod's own device-plugin GPU is neither hot-managed nor removable, and does not make the
+    pod look entire-mounted (reference defect 5)."""
+    async def body(lc):
+        lc.tenant("own", gpus=1)
+        svc = lc.nodes["node-0"].worker.service
+        st = await svc.pod_state(lc.cluster.get("default", "own"))
+        assert len(st.own) == 1 and st.mount_type.value == "no-mount"
+        assert (await lc.add("default", "own", 1))[0] == 200
+        assert (await lc.add("default", "own", 1))[0] == 200   # still allowed
+        code, _ = await lc.remove("default", "own", [st.own[0].uuid])
+        assert code == 400                                     # own GPU is not removable
+        cid = lc.container_ids("default", "own")[0]
+        assert "dev/kfd" not in node_of(lc).container_devices(cid)  # runtime provides kfd
+        assert not await lc.audit("default", "own")
+    run(body)
+
+
+# ------------------------------------------------------------------------------ topology
+def test_scale_one_pod_1_to_8_then_0_in_xgmi_order():
+    async def body(lc):
+        lc.tenant("grow")
+        got = []
+        for _ in range(8):
+            code, b = await lc.add("default", "grow", 1)
+            assert code == 200
+            got.append(b["devices"][0])
+            assert not await lc.audit("default", "grow")
+        assert [d["numa_node"] for d in got] == [0, 0, 0, 0, 1, 1, 1, 1]
+        assert len({d["xgmi_hive_id"] for d in got}) == 1
+        code, b = await lc.add("default", "grow", 1)
+        assert code == 500 and "Insufficient" in b["message"]
+        for d in reversed(got):
+            assert (await lc.remove("default", "grow", [d["uuid"]]))[0] == 200
+        assert lc.cluster.placeholders() == [] and not await lc.audit("default", "grow")
+        assert node_of(lc).container_devices(lc.container_ids("default", "grow")[0]) == []
+    run(body)
+
+
+def test_placement_hint_followed_by_topology_plugin_and_counted_when_not():
+    async def body(lc):
+        lc.tenant("t")
+        await lc.add("default", "t", 4, entire=True)
+        m = lc.nodes["node-0"].worker.metrics
+        assert m.placement_mismatch._value.get() == 0
+    run(body)
+
+
+# ------------------------------------------------------------------------------ namespaces/GC
+def test_tenant_namespace_mode_garbage_collects_with_owner():
+    async def body(lc):
+        lc.tenant("t", ns="team-a")
+        code, b = await lc.add("team-a", "t", 2)
+        assert code == 200
+        phs = lc.cluster.placeholders()
+        assert {p["metadata"]["namespace"] for p in phs} == {"team-a"}
+        assert all(p["metadata"]["ownerReferences"][0]["name"] == "t" for p in phs)
+        lc.cluster.delete("team-a", "t", grace=0)
+        await asyncio.sleep(0.05)
+        assert lc.cluster.placeholders() == [] and node_of(lc).allocated == {}
+    run(body, placeholder_namespace_mode="tenant")
+
+
+def test_pool_mode_writes_no_cross_namespace_owner_refs():
+    async def body(lc):
+        lc.tenant("t")
+        await lc.add("default", "t", 1)
+        ph = lc.cluster.placeholders()[0]
+        assert ph["metadata"]["namespace"] == "gpu-pool"
+        assert "ownerReferences" not in ph["metadata"]
+        assert lc.cluster.gc_sweep() == 0              # modern GC leaves it alone
+        assert ph["metadata"]["labels"][LABEL_OWNER] == "t"
+    run(body)
+
+
+def test_owner_match_is_exact_not_substring():
+    """Reference defect 3: pod 'a' saw the slaves of pod 'xa' (substring match)."""
+    async def body(lc):
+        lc.tenant("a")
+        lc.tenant("xa")
+        lc.tenant("a", ns="other")
+        assert (await lc.add("default", "xa", 2))[0] == 200
+        svc = lc.nodes["node-0"].worker.service
+        for ns, name in (("default", "a"), ("other", "a")):
+            st = await svc.pod_state(lc.cluster.get(ns, name))
+            assert st.hot == [] and st.mount_type.value == "no-mount"
+        assert (await lc.add("default", "a", 1, entire=True))[0] == 200
+    run(body)
+
+
+# ------------------------------------------------------------------------------ reconciler
+def test_reconciler_collects_placeholders_of_deleted_owner():
+    async def body(lc):
+        lc.tenant("gone")
+        await lc.add("default", "gone", 2)
+        lc.cluster.delete("default", "gone", grace=0)
+        rep = await lc.nodes["node-0"].worker.reconciler.run_once()
+        assert len(rep.owner_gone) == 2
+        await asyncio.sleep(0.05)
+        assert lc.cluster.placeholders() == [] and node_of(lc).allocated == {}
+    run(body)
+
+
+def test_reconciler_reinjects_after_container_restart():
+    async def body(lc):
+        lc.tenant("r")
+        _, b = await lc.add("default", "r", 2)
+        cid = lc.container_ids("default", "r")[0]
+        ctr = node_of(lc).container(cid)
+        # simulate a container restart: fresh /dev, fresh cgroup device state
+        import shutil
+        shutil.rmtree(os.path.join(ctr.root_dir, "dev"))
+        os.makedirs(os.path.join(ctr.root_dir, "dev"))
+        for f in ("devices.allow", "devices.deny"):
+            open(os.path.join(ctr.cgroup_dir, f), "w").close()
+        issues = await lc.audit("default", "r")
+        assert {i.kind for i in issues} == {"missing_rule", "missing_node"}
+        rep = await lc.nodes["node-0"].worker.reconciler.run_once()
+        assert rep.repaired == ["default/r"]
+        assert not await lc.audit("default", "r")
+    run(body)
+
+
+def test_reconciler_revokes_orphaned_state():
+    async def body(lc):
+        lc.tenant("o")
+        _, b = await lc.add("default", "o", 1)
+        # placeholder vanishes behind our back (e.g. deleted by an operator) → rules+nodes orphaned
+        ph = lc.cluster.placeholders()[0]
+        lc.cluster.delete(ph["metadata"]["namespace"], ph["metadata"]["name"], grace=0)
+        await asyncio.sleep(0.05)
+        issues = await lc.audit("default", "o")
+        assert issues and all(i.kind.startswith("stale") for i in issues)
+        rep = await lc.nodes["node-0"].worker.reconciler.run_once()
+        assert rep.revoked == ["default/o"] and rep.orphans > 0
+        assert not await lc.audit("default", "o")
+    run(body)
+
+
+# ------------------------------------------------------------------------------ multi-node
+def test_multi_node_routing_by_pod_node():
+    async def body(lc):
+        lc.tenant("n1pod", node="node-1")
+        code, b = await lc.add("default", "n1pod", 2)
+        assert code == 200
+        phs = lc.cluster.placeholders()
+        assert {p["spec"]["nodeName"] for p in phs} == {"node-1"}
+        assert lc.nodes["node-0"].node.allocated == {}
+        assert len(lc.nodes["node-1"].node.allocated) == 2
+        svc1 = lc.nodes["node-1"].worker.service
+        st = await svc1.pod_state(lc.cluster.get("default", "n1pod"))
+        assert not svc1.hm.audit(lc.cluster.get("default", "n1pod"), st.hot, st.own)
+    run(body, n_nodes=2)
+
+
+def test_worker_restart_recovers_state_from_the_ledger():
+    async def body(lc):
+        lc.tenant("w")
+        _, b = await lc.add("default", "w", 2)
+        await lc.stop_worker("node-0")
+        await lc.start_worker("node-0")
+        await lc.master.workers.informer.wait_for(
+            lambda: lc.master.workers.target("node-0") == f"127.0.0.1:"
+            f"{lc.nodes['node-0'].worker.grpc_port}", 5)
+        code, _ = await lc.remove("default", "w", [d["uuid"] for d in b["devices"]])
+        assert code == 200 and not await lc.audit("default", "w")
+    run(body)
+
+
+# ------------------------------------------------------------------------------ observability
+def test_status_endpoints_and_metrics():
+    async def body(lc):
+        lc.tenant("m")
+        _, b = await lc.add("default", "m", 2)
+        async with lc.session.get(lc.master_url + "/api/v1/nodes/node-0/gpus") as r:
+            st = await r.json()
+        assert len(st["gpus"]) == 8 and st["topology"]["all_pairs_xgmi"]
+        assert sum(g["state"] == "GPU_ALLOCATED_STATE" for g in st["gpus"]) == 2
+        async with lc.session.get(lc.master_url + "/api/v1/namespaces/default/pods/m/gpus") as r:
+            mine = await r.json()
+        assert len(mine["gpus"]) == 2
+        w = lc.nodes["node-0"].worker
+        async with lc.session.get(f"http://127.0.0.1:{w.http_port}/metrics") as r:
+            text = await r.text()
+        assert "gm_attach_latency_seconds_bucket" in text and 'stage="mount"' in text
+        async with lc.session.get(f"http://127.0.0.1:{w.http_port}/readyz") as r:
+            assert r.status == 200
+        stages = {t["name"] for t in b["timings"]}
+        assert {"ledger_reserve", "placeholder_wait", "mount", "mount.cgroup_rule",
+                "mount.devnodes"} <= stages
+    run(body)

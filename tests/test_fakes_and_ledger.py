@@ -1,0 +1,208 @@
+"""The hermetic control plane itself (apiserver CRUD/watch/scheduler/GC) and the PodResources
+client against the fake kubelet (v1, v1alpha1 fallback, allocatable, Get)."""
+import asyncio
+import os
+
+import pytest
+from aiohttp import web
+
+from gpumounter_amd.cluster.informer import PodInformer
+from gpumounter_amd.cluster.kube import KubeClient, NotFound
+from gpumounter_amd.fakes.apiserver import FakeCluster, LatencyModel, merge_patch
+from gpumounter_amd.fakes.kubelet import FakeKubelet
+from gpumounter_amd.fakes.node import FakeNode
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.node.ledger import LedgerClient
+
+
+class Env:
+    def __init__(self, tmp, inv, latency=None, gc_mode="modern", gpus=None):
+        self.cluster = FakeCluster(latency, gc_mode)
+        self.node = self.cluster.add_node(FakeNode("node-0", str(tmp), gpus or inv.gpus(),
+                                                   inv.links()))
+        self.tmp = tmp
+
+    async def __aenter__(self):
+        self.runner = web.AppRunner(self.cluster.app(), access_log=None)
+        await self.runner.setup()
+        site = web.TCPSite(self.runner, "127.0.0.1", 0)
+        await site.start()
+        self.url = f"http://127.0.0.1:{site._server.sockets[0].getsockname()[1]}"
+        self.kube = KubeClient(self.url)
+        return self
+
+    async def __aexit__(self, *exc):
+        await self.kube.close()
+        for t in list(self.cluster._tasks):
+            t.cancel()
+        await self.runner.cleanup()
+
+
+def gpu_pod(name, n, node="node-0", image="registry.k8s.io/pause:3.9", policy="IfNotPresent"):
+    return {"metadata": {"name": name, "labels": {"app": "gpu-pool"}},
+            "spec": {"nodeSelector": {"kubernetes.io/hostname": node},
+                     "containers": [{"name": "c", "image": image, "imagePullPolicy": policy,
+                                     "resources": {"limits": {"amd.com/gpu": str(n)}}}]}}
+
+
+def test_merge_patch():
+    assert merge_patch({"a": 1, "b": {"c": 2}}, {"b": {"c": None, "d": 3}, "e": [1]}) == \
+        {"a": 1, "b": {"d": 3}, "e": [1]}
+
+
+def test_crud_watch_and_scheduler(tmp_path, mock_inventory):
+    async def run():
+        async with Env(tmp_path, mock_inventory) as env:
+            k = env.kube
+            inf = PodInformer(k, "gpu-pool", "app=gpu-pool")
+            await inf.start()
+            p = await k.create_pod("gpu-pool", gpu_pod("a", 4))
+            assert p["metadata"]["uid"]
+            got = await inf.wait_for(lambda: (inf.get("gpu-pool", "a") or {}).get(
+                "status", {}).get("phase") == "Running", 5)
+            assert got
+            assert env.node.ledger()[("gpu-pool", "a")]["c"]["amd.com/gpu"]
+            # 4 more fit, a 5th does not: Unschedulable condition
+            await k.create_pod("gpu-pool", gpu_pod("b", 4))
+            await k.create_pod("gpu-pool", gpu_pod("c", 1))
+            await inf.wait_for(lambda: podu.is_unschedulable(inf.get("gpu-pool", "c") or {}), 5)
+            # deleting "a" frees capacity → the scheduler retries "c"
+            await k.delete_pod("gpu-pool", "a", grace_period_s=0)
+            await inf.wait_for(lambda: (inf.get("gpu-pool", "c") or {}).get(
+                "status", {}).get("phase") == "Running", 5)
+            items, _ = await k.list_pods("gpu-pool", "app=gpu-pool", "spec.nodeName=node-0")
+            assert sorted(i["metadata"]["name"] for i in items) == ["b", "c"]
+            with pytest.raises(NotFound):
+                await k.get_pod("gpu-pool", "a")
+            await inf.stop()
+    asyncio.run(run())
+
+
+def test_watch_resume_from_resource_version(tmp_path, mock_inventory):
+    async def run():
+        async with Env(tmp_path, mock_inventory) as env:
+            k = env.kube
+            _, rv = await k.list_pods("ns")
+            await k.create_pod("ns", {"metadata": {"name": "x"}, "spec": {"containers": []}})
+            seen = []
+            async for et, obj in k.watch_pods("ns", resource_version=rv, timeout_s=1):
+                seen.append((et, obj["metadata"].get("name")))
+                if len(seen) >= 1:
+                    break
+            assert seen[0] == ("ADDED", "x")
+    asyncio.run(run())
+
+
+def test_grace_period_and_sigterm_ignoring_image(tmp_path, mock_inventory):
+    lat = LatencyModel(grace_scale=0.02)  # 30 s grace → 0.6 s
+    async def run():
+        async with Env(tmp_path, mock_inventory, latency=lat) as env:
+            k = env.kube
+            body = gpu_pod("slave", 1, image="alpine:latest", policy="Always")
+            body["spec"]["containers"][0]["command"] = ["/bin/sh"]
+            body["spec"]["containers"][0]["args"] = ["-c", "while true; do sleep 10; done"]
+            await k.create_pod("gpu-pool", body)
+            for _ in range(200):
+                p = env.cluster.get("gpu-pool", "slave")
+                if p["status"].get("phase") == "Running":
+                    break
+                await asyncio.sleep(0.01)
+            t0 = asyncio.get_running_loop().time()
+            await k.delete_pod("gpu-pool", "slave")           # default 30 s grace
+            assert env.cluster.get("gpu-pool", "slave")["metadata"]["deletionTimestamp"]
+            while env.cluster.get("gpu-pool", "slave") is not None:
+                await asyncio.sleep(0.01)
+            assert asyncio.get_running_loop().time() - t0 >= 0.5  # waited the (scaled) grace
+    asyncio.run(run())
+
+
+def test_finalizers_block_removal(tmp_path, mock_inventory):
+    async def run():
+        async with Env(tmp_path, mock_inventory) as env:
+            k = env.kube
+            body = gpu_pod("f", 1)
+            body["metadata"]["finalizers"] = ["gpumounter.amd.com/release"]
+            await k.create_pod("gpu-pool", body)
+            await asyncio.sleep(0.05)
+            await k.delete_pod("gpu-pool", "f", grace_period_s=0)
+            assert env.cluster.get("gpu-pool", "f") is not None
+            await k.patch_pod("gpu-pool", "f", {"metadata": {"finalizers": None}})
+            assert env.cluster.get("gpu-pool", "f") is None
+    asyncio.run(run())
+
+
+@pytest.mark.parametrize("gc_mode,expect_deleted", [("modern", True), ("legacy", False)])
+def test_cross_namespace_owner_reference_gc(tmp_path, mock_inventory, gc_mode, expect_deleted):
+    """Kubernetes ≥1.20 ignores cross-namespace owners and collects the dependent (reference
+    defect 4: slave pods in gpu-pool owned by tenant pods elsewhere)."""
+    async def run():
+        async with Env(tmp_path, mock_inventory, gc_mode=gc_mode) as env:
+            owner = env.cluster.create_running_pod("default", {
+                "metadata": {"name": "tenant"}, "spec": {"containers": [{"name": "c"}]}},
+                "node-0")
+            body = gpu_pod("tenant-slave-pod-abc123", 1)
+            body["metadata"]["ownerReferences"] = [{"apiVersion": "v1", "kind": "Pod",
+                                                    "name": "tenant",
+                                                    "uid": owner["metadata"]["uid"]}]
+            await env.kube.create_pod("gpu-pool", body)
+            deleted = env.cluster.gc_sweep()
+            assert (deleted == 1) == expect_deleted
+    asyncio.run(run())
+
+
+def test_same_namespace_owner_gc_cascades(tmp_path, mock_inventory):
+    async def run():
+        async with Env(tmp_path, mock_inventory) as env:
+            owner = env.cluster.create_running_pod("default", {
+                "metadata": {"name": "tenant"}, "spec": {"containers": [{"name": "c"}]}},
+                "node-0")
+            body = gpu_pod("dep", 1)
+            body["metadata"]["ownerReferences"] = [{"uid": owner["metadata"]["uid"],
+                                                    "kind": "Pod", "name": "tenant"}]
+            await env.kube.create_pod("default", body)
+            assert env.cluster.gc_sweep() == 0
+            await env.kube.delete_pod("default", "tenant", grace_period_s=0)
+            assert env.cluster.get("default", "dep") is None
+    asyncio.run(run())
+
+
+# ----------------------------------------------------------------------------------- ledger
+@pytest.mark.parametrize("serve_v1", [True, False])
+def test_ledger_client_v1_and_v1alpha1_fallback(tmp_path, mock_inventory, serve_v1):
+    async def run():
+        node = FakeNode("n", str(tmp_path), mock_inventory.gpus(), mock_inventory.links())
+        sock = os.path.join(str(tmp_path), "kubelet.sock")
+        kl = FakeKubelet(node, sock, serve_v1=serve_v1, serve_v1alpha1=True)
+        await kl.start()
+        ids = node.allocate("gpu-pool", "p1", "c", 2)
+        node.allocate("default", "own", "main", 1)
+        lc = LedgerClient(sock, "amd.com/gpu")
+        allocs = await lc.list()
+        assert lc.api_version == ("v1" if serve_v1 else "v1alpha1")
+        by = await lc.by_pod()
+        assert sorted(by[("gpu-pool", "p1")]) == sorted(ids)
+        assert len(allocs) == 2
+        alloc = await lc.allocatable()
+        if serve_v1:
+            assert sorted(alloc) == sorted(node.device_ids())
+        else:
+            assert alloc is None
+        # a persistent channel: several calls, no reconnects needed
+        for _ in range(5):
+            await lc.list()
+        assert kl.calls["List"] >= 6
+        await lc.close()
+        await kl.stop()
+    asyncio.run(run())
+
+
+def test_fake_device_plugin_topology_policy(tmp_path, mock_inventory):
+    node = FakeNode("n", str(tmp_path), mock_inventory.gpus(), mock_inventory.links(),
+                    alloc_policy="topology")
+    node.allocate("a", "x", "c", 1)           # takes one GPU on NUMA 0
+    ids = node.allocate("a", "y", "c", 4)     # 3 left on NUMA 0 → must take NUMA 1 as a block
+    numas = {node.numa_of(i) for i in ids}
+    assert numas == {1}
+    pref = node.free_ids()[:2]
+    assert node.allocate("a", "z", "c", 2, preferred=pref) == pref
+    assert node.allocate("a", "w", "c", 5) is None
