@@ -49,6 +49,9 @@ def main() -> int:
     ap.add_argument("--amdsmi", default="", help='"" = real libamd_smi, "mock" = bundled mock')
     ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--protocol", choices=("gpumounter", "reference"), default="gpumounter",
+                    help="'reference' re-enacts the reference's call sequence on the same "
+                         "cluster (emulated baseline, see gpumounter_amd/fakes/refproto.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -95,6 +98,9 @@ def main() -> int:
         tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
                              node_gpu_bdfs=node_bdfs)
         lc = tc.start()
+        if args.protocol == "reference":
+            from gpumounter_amd.fakes import refproto
+            refproto.install(lc)
         sleeper = subprocess.Popen(["sleep", "infinity"])
         lc.tenant("tenant", pids={"main": [sleeper.pid]})
         info = {"amdsmi_lib": inv.lib_path, "node_gpus": len(node_bdfs),
@@ -102,6 +108,7 @@ def main() -> int:
                 "hives": sorted({hex(g.xgmi_hive_id) for g in inv.gpus()})}
 
     nccl_group = None
+    bound_dev = [None]
     attach_ms, detach_ms, audit_issues, probe_us, stage = [], [], 0, [], {}
     ar_ms = []
 
@@ -114,7 +121,8 @@ def main() -> int:
             t1 = time.perf_counter()
             if code != 200:
                 raise RuntimeError(f"attach failed: {code} {body}")
-            issues = tc.call(lc.audit("default", "tenant"))
+            issues = tc.call(lc.audit("default", "tenant")) if args.protocol == "gpumounter" \
+                else []
             obj = [{"bdfs": [d["bdf"] for d in body["devices"]],
                     "uuids": [d["uuid"] for d in body["devices"]],
                     "ms": (t1 - t0) * 1e3, "issues": len(issues),
@@ -123,7 +131,8 @@ def main() -> int:
             dist.broadcast_object_list(obj, src=0)
         st = obj[0]
         if has_gpu and not args.no_verify:
-            mine = st["bdfs"][rank % len(st["bdfs"])]
+            bdfs = sorted(st["bdfs"])           # stable rank → attached-GPU mapping
+            mine = bdfs[rank % len(bdfs)]
             dev = probe.find_device(mine)
             if dev < 0:
                 raise RuntimeError(f"rank {rank}: attached GPU {mine} not visible to HIP")
@@ -134,6 +143,10 @@ def main() -> int:
                 if nccl_group is None:
                     torch.cuda.set_device(dev)
                     nccl_group = dist.new_group(backend="nccl")
+                    bound_dev[0] = dev
+                elif bound_dev[0] != dev:
+                    raise RuntimeError(f"rank {rank}: attached set changed between steps "
+                                       f"({bound_dev[0]} → {dev}); placement must be stable")
                 x = torch.ones(1 << 20, dtype=torch.bfloat16, device=f"cuda:{dev}")
                 ta = time.perf_counter()
                 dist.all_reduce(x, group=nccl_group)
@@ -178,7 +191,8 @@ def main() -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ms_per_step = float(t.item())
         if rank == 0:
-            orphan_issues = len(tc.call(lc.audit("default", "tenant")))
+            orphan_issues = len(tc.call(lc.audit("default", "tenant"))) \
+                if args.protocol == "gpumounter" else None
             placeholders_left = len(lc.cluster.placeholders())
             p50 = pct(attach_ms, 0.5)
             out = {
@@ -200,6 +214,8 @@ def main() -> int:
                     "parallelism": f"node-local attach of {n} GPU(s); tenant RCCL check over dp{n}",
                     "control_plane": f"hermetic fake apiserver/kubelet, latency={args.latency}",
                     "cgroup": args.cgroup,
+                    "protocol": args.protocol if args.protocol == "gpumounter"
+                    else "reference (emulated)",
                 },
                 "attach_p99_ms": round(pct(attach_ms, 0.99), 4),
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),

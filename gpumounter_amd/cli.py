@@ -1,0 +1,230 @@
+"""Command line: daemons and operator tools.
+
+    python -m gpumounter_amd master   [--config f.yaml] [--port 8080]
+    python -m gpumounter_amd worker   [--config f.yaml] [--node NAME]
+    python -m gpumounter_amd inventory [--amdsmi mock]          # amdsmi view of this node
+    python -m gpumounter_amd topology  [--amdsmi mock] [-n 4]   # xGMI/NUMA placement preview
+    python -m gpumounter_amd probe     [--bdf 0000:05:00.0] [--full]   # gfx950 validation kernels
+    python -m gpumounter_amd add    --master URL --ns NS --pod P -n 2 [--entire]
+    python -m gpumounter_amd remove --master URL --ns NS --pod P --uuid U [--uuid U2] [--force]
+    python -m gpumounter_amd status --master URL --node NODE
+    python -m gpumounter_amd bpf-dump --allow 226:128 --allow 511:0   # generated device program
+
+The reference ships only the two daemons and documents curl calls (QuickStart.md:41-92); the
+``add``/``remove`` commands speak exactly those HTTP routes.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import sys
+from typing import List, Optional
+
+
+def _cfg(args, **over):
+    from gpumounter_amd.utils.config import Config
+
+    return Config.load(getattr(args, "config", None), **over)
+
+
+def cmd_master(args) -> int:
+    from gpumounter_amd.master.app import serve
+    from gpumounter_amd.utils import log
+
+    cfg = _cfg(args, master_port=args.port)
+    log.setup(cfg.log_level, cfg.log_json, cfg.log_file)
+    asyncio.run(serve(cfg))
+    return 0
+
+
+def cmd_worker(args) -> int:
+    from gpumounter_amd.utils import log
+    from gpumounter_amd.worker.server import serve
+
+    cfg = _cfg(args, node_name=args.node, worker_port=args.port)
+    log.setup(cfg.log_level, cfg.log_json, cfg.log_file)
+    asyncio.run(serve(cfg))
+    return 0
+
+
+def cmd_inventory(args) -> int:
+    from gpumounter_amd.hw.inventory import Inventory
+
+    inv = Inventory(args.amdsmi)
+    out = inv.summary()
+    if args.processes:
+        out["processes"] = {g.index: [p.__dict__ for p in inv.processes(g.index)]
+                            for g in inv.gpus()}
+    print(json.dumps(out, indent=2))
+    return 0
+
+
+def cmd_topology(args) -> int:
+    from gpumounter_amd.hw import topology
+    from gpumounter_amd.hw.inventory import Inventory
+
+    inv = Inventory(args.amdsmi)
+    gpus = inv.gpus()
+    out = {"describe": topology.describe(gpus, inv.links()), "plans": {}}
+    for n in ([args.n] if args.n else range(1, len(gpus) + 1)):
+        p = topology.choose(gpus, n, inv.links(), policy=args.policy)
+        out["plans"][n] = p.to_dict() if p else None
+    print(json.dumps(out, indent=2))
+    return 0
+
+
+def cmd_probe(args) -> int:
+    from gpumounter_amd.ops import probe
+
+    if args.bdf:
+        bdfs = args.bdf
+    else:
+        bdfs = [probe.props(i)["pci_bus_id"] for i in range(probe.device_count())]
+    res = [r.to_dict() for r in probe.verify(bdfs, full=args.full)]
+    print(json.dumps(res, indent=2))
+    return 0
+
+
+async def _http(method: str, url: str, data=None) -> int:
+    import aiohttp
+
+    async with aiohttp.ClientSession() as s:
+        async with s.request(method, url, data=data,
+                             headers={"Accept": "application/json"}) as r:
+            body = await r.text()
+            print(body)
+            return 0 if r.status == 200 else 1
+
+
+def cmd_add(args) -> int:
+    url = (f"{args.master.rstrip('/')}/addgpu/namespace/{args.ns}/pod/{args.pod}/gpu/{args.n}/"
+           f"isEntireMount/{'true' if args.entire else 'false'}")
+    if args.container:
+        url += f"?container={args.container}"
+    return asyncio.run(_http("GET", url))
+
+
+def cmd_remove(args) -> int:
+    import aiohttp
+
+    url = (f"{args.master.rstrip('/')}/removegpu/namespace/{args.ns}/pod/{args.pod}/force/"
+           f"{'true' if args.force else 'false'}")
+    data = aiohttp.FormData()
+    for u in args.uuid:
+        data.add_field("uuids", u)
+    return asyncio.run(_http("POST", url, data))
+
+
+def cmd_status(args) -> int:
+    if args.pod:
+        url = f"{args.master.rstrip('/')}/api/v1/namespaces/{args.ns}/pods/{args.pod}/gpus"
+    else:
+        url = f"{args.master.rstrip('/')}/api/v1/nodes/{args.node}/gpus"
+    return asyncio.run(_http("GET", url))
+
+
+def disassemble(insns: List[int]) -> List[str]:
+    from gpumounter_amd.node import bpfvm
+
+    names = {0x61: "ldxw", 0xbf: "mov64", 0xb7: "mov64", 0x57: "and64", 0x77: "rsh64",
+             0x55: "jne", 0x85: "call", 0x95: "exit", 0x18: "lddw"}
+    out = []
+    skip = False
+    for i, raw in enumerate(insns):
+        if skip:
+            skip = False
+            continue
+        code, dst, src, off, imm = bpfvm.decode(raw)
+        op = names.get(code, f"op{code:#x}")
+        if code == 0x61:
+            out.append(f"{i:3d}: r{dst} = *(u32 *)(r{src} + {off})")
+        elif code == 0xbf:
+            out.append(f"{i:3d}: r{dst} = r{src}")
+        elif code == 0xb7:
+            out.append(f"{i:3d}: r{dst} = {imm}")
+        elif code == 0x57:
+            out.append(f"{i:3d}: r{dst} &= {imm & 0xffffffff:#x}")
+        elif code == 0x77:
+            out.append(f"{i:3d}: r{dst} >>= {imm}")
+        elif code == 0x55:
+            out.append(f"{i:3d}: if r{dst} != {imm} goto +{off}")
+        elif code == 0x18:
+            out.append(f"{i:3d}: r{dst} = map[prog_array fd={imm}]")
+            skip = True
+        elif code == 0x85:
+            out.append(f"{i:3d}: call bpf_tail_call#{imm}")
+        elif code == 0x95:
+            out.append(f"{i:3d}: exit")
+        else:
+            out.append(f"{i:3d}: {op} dst=r{dst} src=r{src} off={off} imm={imm}")
+    return out
+
+
+def cmd_bpf_dump(args) -> int:
+    from gpumounter_amd.models.device import DeviceNode
+    from gpumounter_amd.node.cgroup import build_program
+
+    nodes = []
+    for a in args.allow:
+        ma, mi = a.split(":")
+        nodes.append(DeviceNode(f"/dev/x{ma}_{mi}", int(ma), int(mi)))
+    prog = build_program(nodes, chained=not args.unchained)
+    print("\n".join(disassemble(prog)))
+    return 0
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="gpumounter_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("master")
+    p.add_argument("--config")
+    p.add_argument("--port", type=int)
+    p.set_defaults(fn=cmd_master)
+    p = sub.add_parser("worker")
+    p.add_argument("--config")
+    p.add_argument("--node")
+    p.add_argument("--port", type=int)
+    p.set_defaults(fn=cmd_worker)
+    p = sub.add_parser("inventory")
+    p.add_argument("--amdsmi", default="")
+    p.add_argument("--processes", action="store_true")
+    p.set_defaults(fn=cmd_inventory)
+    p = sub.add_parser("topology")
+    p.add_argument("--amdsmi", default="")
+    p.add_argument("-n", type=int, default=0)
+    p.add_argument("--policy", default="xgmi", choices=("xgmi", "first-fit"))
+    p.set_defaults(fn=cmd_topology)
+    p = sub.add_parser("probe")
+    p.add_argument("--bdf", action="append")
+    p.add_argument("--full", action="store_true")
+    p.set_defaults(fn=cmd_probe)
+    for name, fn in (("add", cmd_add), ("remove", cmd_remove), ("status", cmd_status)):
+        p = sub.add_parser(name)
+        p.add_argument("--master", default="http://127.0.0.1:8080")
+        p.add_argument("--ns", default="default")
+        p.add_argument("--pod", default="")
+        if name == "add":
+            p.add_argument("-n", type=int, required=True)
+            p.add_argument("--entire", action="store_true")
+            p.add_argument("--container", default="")
+        if name == "remove":
+            p.add_argument("--uuid", action="append", required=True)
+            p.add_argument("--force", action="store_true")
+        if name == "status":
+            p.add_argument("--node", default="")
+        p.set_defaults(fn=fn)
+    p = sub.add_parser("bpf-dump")
+    p.add_argument("--allow", action="append", default=[])
+    p.add_argument("--unchained", action="store_true")
+    p.set_defaults(fn=cmd_bpf_dump)
+    return ap
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    args = build_parser().parse_args(argv)
+    return args.fn(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -94,10 +94,12 @@ class Worker:
         return (
             grpc.method_handlers_generic_handler("gpu_mount.AddGPUService", {
                 "AddGPU": grpc.unary_unary_rpc_method_handler(
-                    self._wrap(self.service.add_gpu), api.AddGPURequest.FromString, _ser)}),
+                    self._wrap(lambda r: self.service.add_gpu(r)), api.AddGPURequest.FromString,
+                    _ser)}),
             grpc.method_handlers_generic_handler("gpu_mount.RemoveGPUService", {
                 "RemoveGPU": grpc.unary_unary_rpc_method_handler(
-                    self._wrap(self.service.remove_gpu), api.RemoveGPURequest.FromString, _ser)}),
+                    self._wrap(lambda r: self.service.remove_gpu(r)),
+                    api.RemoveGPURequest.FromString, _ser)}),
             grpc.method_handlers_generic_handler("gpu_mount.NodeService", {
                 "GetNodeStatus": grpc.unary_unary_rpc_method_handler(
                     self._wrap(self._status), api.NodeStatusRequest.FromString, _ser)}),

@@ -1,0 +1,72 @@
+"""Deployment manifests agree with the code's defaults; CLI subcommands work on the mock."""
+import json
+import os
+import subprocess
+import sys
+
+import yaml
+
+from gpumounter_amd.utils.config import Config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(name):
+    with open(os.path.join(ROOT, "deploy", name)) as fh:
+        return [d for d in yaml.safe_load_all(fh) if d]
+
+
+def test_worker_daemonset_shape():
+    (ds,) = load("gpu-mounter-workers.yaml")
+    spec = ds["spec"]["template"]["spec"]
+    cfg = Config.load(env={})
+    assert ds["metadata"]["namespace"] == cfg.worker_namespace
+    k, v = cfg.worker_label.split("=")
+    assert ds["spec"]["template"]["metadata"]["labels"][k] == v
+    assert spec["hostPID"] is True
+    c = spec["containers"][0]
+    assert c["securityContext"]["privileged"] is True
+    assert {p["containerPort"] for p in c["ports"]} == {cfg.worker_port, cfg.metrics_port}
+    mounts = {m["mountPath"] for m in c["volumeMounts"]}
+    assert {"/sys/fs/cgroup", "/sys/fs/bpf", "/var/lib/kubelet/pod-resources", "/dev",
+            "/sys/class/kfd"} <= mounts
+    env = {e["name"]: e for e in c["env"]}
+    assert env["NODE_NAME"]["valueFrom"]["fieldRef"]["fieldPath"] == "spec.nodeName"
+    assert env["GM_BPF_PIN_DIR"]["value"].startswith("/sys/fs/bpf")
+    assert "NVIDIA_VISIBLE_DEVICES" not in env
+
+
+def test_rbac_is_least_privilege():
+    docs = load("rbac.yaml")
+    roles = [d for d in docs if d["kind"] == "ClusterRole"]
+    binding = next(d for d in docs if d["kind"] == "ClusterRoleBinding")
+    assert binding["roleRef"]["name"] != "cluster-admin"
+    resources = {r for role in roles for rule in role["rules"] for r in rule["resources"]}
+    assert resources <= {"pods", "nodes", "events"}
+    assert all("*" not in rule["verbs"] for role in roles for rule in role["rules"])
+
+
+def test_service_and_master_ports():
+    (svc,) = load("gpu-mounter-svc.yaml")
+    (dep,) = load("gpu-mounter-master.yaml")
+    cfg = Config.load(env={})
+    assert svc["spec"]["ports"][0]["port"] == 80
+    assert svc["spec"]["ports"][0]["targetPort"] == cfg.master_port
+    assert svc["spec"]["selector"] == dep["spec"]["template"]["metadata"]["labels"]
+    assert load("namespace.yaml")[0]["metadata"]["name"] == cfg.pool_namespace
+
+
+def _cli(*args):
+    res = subprocess.run([sys.executable, "-m", "gpumounter_amd", *args], cwd=ROOT,
+                         capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    return res.stdout
+
+
+def test_cli_inventory_topology_bpf_dump():
+    inv = json.loads(_cli("inventory", "--amdsmi", "mock"))
+    assert inv["count"] == 8 and inv["gpus"][0]["gfx_target"] == "gfx950"
+    topo = json.loads(_cli("topology", "--amdsmi", "mock", "-n", "4"))
+    assert topo["plans"]["4"]["numa_nodes"] == 1 and topo["describe"]["all_pairs_xgmi"]
+    dump = _cli("bpf-dump", "--allow", "226:128", "--allow", "511:0")
+    assert "if r4 != 226" in dump and "call bpf_tail_call#12" in dump
