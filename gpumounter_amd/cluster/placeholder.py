@@ -77,12 +77,34 @@ def _label_value(s: str) -> str:
 
 class PlaceholderManager:
     def __init__(self, cfg, kube: KubeClient, ledger: LedgerClient, informer: PodInformer,
-                 node_name: str) -> None:
+                 node_name: str, faults=None) -> None:
+        from gpumounter_amd.utils.faults import NONE
+
         self.cfg = cfg
         self.kube = kube
         self.ledger = ledger
         self.informer = informer
         self.node = node_name
+        self.faults = faults if faults is not None else NONE
+        # uid → device IDs of admitted placeholders (immutable for a pod's lifetime)
+        self.device_ids: Dict[str, Tuple[str, ...]] = {}
+        # uids we deleted but the watch has not reported yet: excluded from every query, so a
+        # released GPU is never seen as still attached (no need to wait for the DELETED event)
+        self.tombstones: Dict[str, float] = {}
+        informer.handlers.append(self._on_event)
+        self.last_ledger: Dict[Tuple[str, str], List[str]] = {}
+
+    def _on_event(self, etype: str, pod: dict) -> None:
+        if etype == "DELETED":
+            uid = pod.get("metadata", {}).get("uid", "")
+            self.tombstones.pop(uid, None)
+            self.device_ids.pop(uid, None)
+        elif etype == "RELIST":
+            live = {p["metadata"].get("uid") for p in self.informer.cache.values()}
+            for uid in [u for u in self.tombstones if u not in live]:
+                self.tombstones.pop(uid, None)
+            for uid in [u for u in self.device_ids if u not in live]:
+                self.device_ids.pop(uid, None)
 
     # ------------------------------------------------------------------------ spec
     def namespace_for(self, owner: dict) -> str:
@@ -135,6 +157,11 @@ class PlaceholderManager:
         return {"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": spec}
 
     # ------------------------------------------------------------------------ queries
+    def live(self) -> List[dict]:
+        """Placeholders on this node that are neither terminating nor released by us."""
+        return self.informer.list(lambda p: not p["metadata"].get("deletionTimestamp")
+                                  and p["metadata"].get("uid") not in self.tombstones)
+
     def owned_by(self, owner: dict) -> List[dict]:
         uid = podu.uid_of(owner)
         oname, ons = _label_value(podu.name_of(owner)), _label_value(podu.ns_of(owner))
@@ -144,7 +171,8 @@ class PlaceholderManager:
             lab = md.get("labels") or {}
             return (lab.get(LABEL_OWNER) == oname and lab.get(LABEL_OWNER_NS) == ons
                     and (md.get("annotations") or {}).get(ANN_OWNER_UID) == uid
-                    and not md.get("deletionTimestamp"))
+                    and not md.get("deletionTimestamp")
+                    and md.get("uid") not in self.tombstones)
 
         return self.informer.list(mine)
 
@@ -163,6 +191,7 @@ class PlaceholderManager:
         bodies = [self.build(owner, per_pod, mode, prefs[i], attach_id, container)
                   for i in range(k)]
         with trace.span("ledger_reserve", placeholders=k):
+            self.faults.check("ledger_reserve")
             results = await asyncio.gather(
                 *[self.kube.create_pod(b["metadata"]["namespace"], b) for b in bodies],
                 return_exceptions=True)
@@ -174,8 +203,11 @@ class PlaceholderManager:
             await self.release(created, wait=False)
             raise ReserveError(f"placeholder create failed: {errors[0]}")
         try:
+            self.faults.check("ledger_reserve", "after")
             with trace.span("placeholder_wait"):
+                self.faults.check("placeholder_wait")
                 await self._await_admission(created, self.cfg.attach_timeout_s)
+                self.faults.check("placeholder_wait", "after")
         except BaseException:
             await self.release(created, wait=False)
             raise
@@ -218,11 +250,15 @@ class PlaceholderManager:
                     raise InsufficientGPU(reason)
                 raise ReserveError(reason)
             # bound: the kubelet records the allocation at admission — read the ledger
+            self.faults.check("ledger_read")
             got = await self.ledger.by_pod()
+            self.last_ledger = got
             for key in list(pending):
                 ids = got.get(key)
                 if ids:
-                    pending.pop(key).device_ids = tuple(ids)
+                    ph = pending.pop(key)
+                    ph.device_ids = tuple(ids)
+                    self.device_ids[ph.uid] = ph.device_ids
             if pending:
                 await asyncio.sleep(delay)
                 delay = min(delay * 2, 0.05)
@@ -233,12 +269,24 @@ class PlaceholderManager:
         if not phs:
             return
         with trace.span("ledger_release", placeholders=len(phs)):
+            self.faults.check("ledger_release")
             res = await asyncio.gather(
                 *[self.kube.delete_pod(p.namespace, p.name, grace_period_s=0, uid=p.uid or "")
                   for p in phs], return_exceptions=True)
+            failed = []
+            now = asyncio.get_running_loop().time()
             for p, r in zip(phs, res):
                 if isinstance(r, Exception) and not isinstance(r, NotFound):
                     _log.error("delete placeholder %s/%s: %s", p.namespace, p.name, r)
+                    failed.append(p)
+                elif p.uid:
+                    # grace 0 + no finalizers: the object is gone from the apiserver (and the
+                    # scheduler's books) once DELETE returns
+                    self.tombstones[p.uid] = now
+            if failed:
+                raise ReserveError(f"could not delete {len(failed)} placeholder(s): "
+                                   f"{[p.name for p in failed]}")
+            self.faults.check("ledger_release", "after")
             if not wait:
                 return
             keys = {(p.namespace, p.name): p.uid for p in phs}
@@ -258,4 +306,13 @@ class PlaceholderManager:
         key = (md["namespace"], md["name"])
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""),
                            tuple(ledger_ids.get(key, ())),
+                           (md.get("annotations") or {}).get(ANN_MOUNT_MODE, "single"))
+
+    def cached(self, p: dict) -> Optional[Placeholder]:
+        """Placeholder with its device IDs from the admission cache (None if unknown)."""
+        md = p["metadata"]
+        ids = self.device_ids.get(md.get("uid", ""))
+        if ids is None:
+            return None
+        return Placeholder(md["namespace"], md["name"], md.get("uid", ""), ids,
                            (md.get("annotations") or {}).get(ANN_MOUNT_MODE, "single"))

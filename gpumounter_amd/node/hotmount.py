@@ -50,12 +50,15 @@ class AuditIssue:
 
 class HotMount:
     def __init__(self, cfg, inv: Inventory, resolver: CgroupResolver, backend: DeviceRuleBackend,
-                 writer: DevNodeWriter) -> None:
+                 writer: DevNodeWriter, faults=None) -> None:
+        from gpumounter_amd.utils.faults import NONE
+
         self.cfg = cfg
         self.inv = inv
         self.resolver = resolver
         self.backend = backend
         self.writer = writer
+        self.faults = faults if faults is not None else NONE
 
     # ------------------------------------------------------------------------ node sets
     def kfd(self) -> DeviceNode:
@@ -106,11 +109,15 @@ class HotMount:
         try:
             for t in targets:
                 with trace.span("cgroup_rule", backend=self.backend.name, rules=len(grant)):
+                    self.faults.check("cgroup_rule")
                     self.backend.apply(t.cgdir, grant, [], after)
                 done.append((t, grant, []))
+                self.faults.check("cgroup_rule", "after")
                 with trace.span("devnodes", nodes=len(after)):
+                    self.faults.check("devnodes")
                     res = self.writer.create(t.target, after)
                 done[-1] = (t, grant, [n for n, r in zip(after, res) if r == CREATED])
+                self.faults.check("devnodes", "after")
         except Exception as e:
             self._rollback_attach(done, before)
             raise MountError(f"attach failed, rolled back: {e}") from e
@@ -141,10 +148,39 @@ class HotMount:
         for t in targets:
             # reference order: deny → rm → kill (util.go:112,131,139)
             with trace.span("cgroup_rule", backend=self.backend.name, rules=len(revoke)):
+                self.faults.check("unmount")
                 self.backend.apply(t.cgdir, [], revoke, after)
+            self.faults.check("unmount", "after")
             with trace.span("devnodes", nodes=len(revoke)):
                 self.writer.remove(t.target, revoke)
         return targets
+
+    def repair(self, pod: dict, missing: Sequence[AuditIssue], hot: Sequence[AmdGpu],
+               base: Sequence[AmdGpu] = ()) -> None:
+        """Grant exactly the rules and create exactly the nodes :meth:`audit` reported missing
+        (never re-granting a present rule, which would unbalance v1 allow/deny bookkeeping)."""
+        desired = self.managed_nodes(hot, base)
+        for t in self.targets(pod):
+            mine = [i for i in missing if i.container == t.ref.name]
+            rules = list({(i.major, i.minor): DeviceNode(i.path, i.major, i.minor)
+                          for i in mine if i.kind == "missing_rule"}.values())
+            nodes = [n for n in desired
+                     if any(i.kind == "missing_node" and (i.major, i.minor) == (n.major, n.minor)
+                            for i in mine)]
+            if rules:
+                self.backend.apply(t.cgdir, rules, [], desired)
+            if nodes:
+                self.writer.create(t.target, nodes)
+
+    def revoke_issues(self, pod: dict, stale: Sequence[AuditIssue], hot: Sequence[AmdGpu],
+                      base: Sequence[AmdGpu] = ()) -> None:
+        """Revoke rules and unlink nodes reported as stale by :meth:`audit`."""
+        nodes = list({(i.major, i.minor): DeviceNode(i.path, i.major, i.minor)
+                      for i in stale}.values())
+        keep = self.managed_nodes(hot, base)
+        for t in self.targets(pod):
+            self.backend.apply(t.cgdir, [], nodes, keep)
+            self.writer.remove(t.target, nodes)
 
     # ------------------------------------------------------------------------ audit
     def audit(self, pod: dict, hot: Sequence[AmdGpu], base: Sequence[AmdGpu] = (),

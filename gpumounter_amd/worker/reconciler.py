@@ -23,7 +23,6 @@ from typing import Dict, List
 from gpumounter_amd.cluster.kube import NotFound
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.types import ANN_OWNER_UID
-from gpumounter_amd.node.hotmount import MountError
 from gpumounter_amd.utils import log
 
 _log = log.get("worker.reconciler")
@@ -76,7 +75,7 @@ class Reconciler:
         svc = self.svc
         rep = ReconcileReport()
         m = svc.metrics
-        placeholders = svc.ph.informer.list(lambda p: not p["metadata"].get("deletionTimestamp"))
+        placeholders = svc.ph.live()
         by_owner: Dict[tuple, List[dict]] = {}
         for p in placeholders:
             ann = p["metadata"].get("annotations") or {}
@@ -116,24 +115,22 @@ class Reconciler:
                 if podu.phase_of(owner) != "Running":
                     continue
                 try:
-                    st = await svc.pod_state(owner)
-                    issues = svc.hm.audit(owner, st.hot, st.own)
-                except (MountError, Exception) as e:  # noqa: BLE001
+                    fixed = await svc.reconcile_pod(owner)
+                except Exception as e:  # noqa: BLE001
                     rep.errors.append(f"{ons}/{oname}: {e}")
                     continue
-                if issues:
-                    rep.orphans += sum(1 for i in issues if i.kind.startswith("stale"))
-                    try:
-                        svc.hm.attach(owner, st.hot, [], st.own)  # idempotent re-grant/re-create
-                        stale = [i for i in issues if i.kind.startswith("stale")]
-                        if stale:
-                            self._revoke_stale(owner, st, stale)
-                        rep.repaired.append(f"{ons}/{oname}")
-                        m.reconcile_actions.labels(action="repair").inc()
-                    except Exception as e:  # noqa: BLE001
-                        rep.errors.append(f"repair {ons}/{oname}: {e}")
+                if fixed:
+                    rep.orphans += sum(1 for i in fixed if i.kind.startswith("stale"))
+                    rep.repaired.append(f"{ons}/{oname}")
+                    m.reconcile_actions.labels(action="repair").inc()
         # pods on this node without placeholders must not keep hot-mount state
         owners = {(o[1], o[0]) for o in by_owner}
+        try:
+            snapshot = await svc._read_ledger()  # one kubelet read for the whole sweep
+        except Exception as e:  # noqa: BLE001
+            rep.errors.append(f"ledger: {e}")
+            self.last = rep
+            return rep
         for pod in svc.node_pods.list(lambda p: podu.phase_of(p) == "Running"):
             key = (podu.ns_of(pod), podu.name_of(pod))
             if key in owners or (pod["metadata"].get("labels") or {}).get("app") == "gpu-pool":
@@ -143,18 +140,14 @@ class Reconciler:
                 continue
             async with lock:
                 try:
-                    st = await svc.pod_state(pod)
-                    if st.placeholders:
-                        continue
-                    issues = svc.hm.audit(pod, [], st.own)
+                    fixed = await svc.reconcile_pod(pod, snapshot)
                 except Exception as e:  # noqa: BLE001
                     rep.errors.append(f"audit {key}: {e}")
                     continue
-                stale = [i for i in issues if i.kind.startswith("stale")]
+                stale = [i for i in fixed if i.kind.startswith("stale")]
                 if stale:
                     rep.orphans += len(stale)
                     m.orphans.labels(kind="stale_state").inc(len(stale))
-                    self._revoke_stale(pod, st, stale)
                     rep.revoked.append(f"{key[0]}/{key[1]}")
                     m.reconcile_actions.labels(action="revoke").inc()
         for name in list(self._first_seen):
@@ -164,12 +157,3 @@ class Reconciler:
         if rep.owner_gone or rep.stuck or rep.repaired or rep.revoked or rep.errors:
             log.kv(_log, 20, "reconciled", **rep.to_dict())
         return rep
-
-    def _revoke_stale(self, pod: dict, st, stale) -> None:
-        from gpumounter_amd.models.device import DeviceNode
-        nodes = {(i.major, i.minor): DeviceNode(i.path, i.major, i.minor) for i in stale}
-        hm = self.svc.hm
-        keep = hm.managed_nodes(st.hot, st.own)
-        for t in hm.targets(pod):
-            hm.backend.apply(t.cgdir, [], list(nodes.values()), keep)
-            hm.writer.remove(t.target, list(nodes.values()))

@@ -27,6 +27,7 @@ from gpumounter_amd.node.devnodes import DevNodeWriter
 from gpumounter_amd.node.hotmount import HotMount
 from gpumounter_amd.node.ledger import LedgerClient
 from gpumounter_amd.utils import log
+from gpumounter_amd.utils.faults import FaultInjector
 from gpumounter_amd.utils.metrics import Metrics
 from gpumounter_amd.worker.reconciler import Reconciler
 from gpumounter_amd.worker.service import GpuMountService, RpcError
@@ -53,7 +54,9 @@ class Worker:
         emulate = cfg.devnode_mode == "emulate" or os.environ.get("GM_BPF_EMULATE") == "1"
         self.backend = make_backend(self.resolver.mode, emulate, cfg.bpf_pin_dir)
         self.writer = DevNodeWriter(cfg.devnode_mode)
-        self.hotmount = HotMount(cfg, self.inv, self.resolver, self.backend, self.writer)
+        self.faults = FaultInjector(cfg.fault)
+        self.hotmount = HotMount(cfg, self.inv, self.resolver, self.backend, self.writer,
+                                 self.faults)
         ph_ns = None if cfg.placeholder_namespace_mode == "tenant" else cfg.pool_namespace
         self.ph_informer = PodInformer(self.kube, ph_ns,
                                        PlaceholderManager.selector_for_node(cfg.node_name),
@@ -62,9 +65,10 @@ class Worker:
                                          f"spec.nodeName={cfg.node_name}",
                                          resync_s=cfg.watch_resync_s)
         self.placeholders = PlaceholderManager(cfg, self.kube, self.ledger, self.ph_informer,
-                                               cfg.node_name)
+                                               cfg.node_name, self.faults)
         self.service = GpuMountService(cfg, self.kube, self.inv, self.ledger, self.placeholders,
-                                       self.hotmount, self.node_informer, self.metrics)
+                                       self.hotmount, self.node_informer, self.metrics,
+                                       self.faults)
         self.reconciler = Reconciler(self.service, cfg.reconcile_period_s)
         self.grpc_server: Optional[grpc.aio.Server] = None
         self.http_runner: Optional[web.AppRunner] = None

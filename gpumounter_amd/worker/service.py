@@ -39,6 +39,7 @@ from gpumounter_amd.node import procs
 from gpumounter_amd.node.hotmount import HotMount, MountError
 from gpumounter_amd.node.ledger import LedgerClient, LedgerError
 from gpumounter_amd.utils import log, trace
+from gpumounter_amd.utils.faults import FaultInjector, InjectedFault
 from gpumounter_amd.utils.metrics import Metrics
 
 _log = log.get("worker.service")
@@ -75,7 +76,7 @@ def can_mount(mount_type: MountType, entire: bool) -> Tuple[bool, str]:
 class GpuMountService:
     def __init__(self, cfg, kube: KubeClient, inv: Inventory, ledger: LedgerClient,
                  placeholders: PlaceholderManager, hotmount: HotMount, node_pods: PodInformer,
-                 metrics: Optional[Metrics] = None) -> None:
+                 metrics: Optional[Metrics] = None, faults: Optional[FaultInjector] = None) -> None:
         self.cfg = cfg
         self.kube = kube
         self.inv = inv
@@ -84,8 +85,10 @@ class GpuMountService:
         self.hm = hotmount
         self.node_pods = node_pods
         self.metrics = metrics or Metrics()
+        self.faults = faults if faults is not None else FaultInjector(cfg.fault)
         self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}
-        self._alloc_lock = asyncio.Lock()
+        self._own: Dict[str, Tuple[str, ...]] = {}   # pod uid → its own device-plugin GPU IDs
+        self.ledger_reads = 0
 
     # ------------------------------------------------------------------------ helpers
     def pod_lock(self, ns: str, name: str) -> asyncio.Lock:
@@ -104,15 +107,41 @@ class GpuMountService:
         except NotFound:
             return None
 
-    async def pod_state(self, pod: dict) -> PodGpuState:
+    async def _read_ledger(self) -> Dict[Tuple[str, str], List[str]]:
+        self.ledger_reads += 1
+        led = await self.ledger.by_pod()
+        self.ph.last_ledger = led
+        return led
+
+    async def pod_state(self, pod: dict, fresh: bool = False,
+                        ledger_snapshot: Optional[Dict[Tuple[str, str], List[str]]] = None
+                        ) -> PodGpuState:
+        """The pod's GPUs from the ledger's point of view.
+
+        Device-plugin allocations never change during a pod's lifetime, so the device IDs of an
+        admitted placeholder and a running pod's own GPUs are cached; the kubelet is only asked
+        when something is unknown (first sight of a pod, placeholders from a previous worker
+        incarnation) or when ``fresh`` is requested (reconciler, status).
+        """
         st = PodGpuState()
-        try:
-            ledger = await self.ledger.by_pod()
-        except LedgerError as e:
-            _log.error("ledger read failed: %s", e)
-            st.mount_type = MountType.UNKNOWN
-            return st
-        st.ledger = ledger
+        owned = self.ph.owned_by(pod)
+        uid = podu.uid_of(pod)
+        cached = [self.ph.cached(p) for p in owned]
+        ledger: Optional[Dict[Tuple[str, str], List[str]]] = ledger_snapshot
+        if ledger is not None or fresh or uid not in self._own or any(c is None for c in cached):
+            try:
+                self.faults.check("ledger_read")
+                if ledger is None:
+                    ledger = await self._read_ledger()
+            except (LedgerError, InjectedFault) as e:
+                _log.error("ledger read failed: %s", e)
+                st.mount_type = MountType.UNKNOWN
+                return st
+            self._own[uid] = tuple(ledger.get((podu.ns_of(pod), podu.name_of(pod)), ()))
+            phs = [PlaceholderManager.from_pod(p, ledger) for p in owned]
+        else:
+            phs = cached
+        st.ledger = ledger if ledger is not None else self.ph.last_ledger
         keys = gpus_by_key(self.inv.gpus())
 
         def resolve(ids) -> List[AmdGpu]:
@@ -126,10 +155,9 @@ class GpuMountService:
             return out
 
         try:
-            st.own = resolve(ledger.get((podu.ns_of(pod), podu.name_of(pod)), []))
+            st.own = resolve(self._own.get(uid, ()))
             modes = set()
-            for p in self.ph.owned_by(pod):
-                ph = PlaceholderManager.from_pod(p, ledger)
+            for ph in phs:
                 gs = resolve(ph.device_ids)
                 st.placeholders.append(ph)
                 st.by_placeholder[(ph.namespace, ph.name)] = gs
@@ -146,6 +174,37 @@ class GpuMountService:
         else:
             st.mount_type = MountType.SINGLE
         return st
+
+    async def reconcile_pod(self, pod: dict,
+                            ledger_snapshot: Optional[Dict[Tuple[str, str], List[str]]] = None
+                            ) -> List:
+        """Make the pod's cgroup rules and /dev nodes equal its (fresh) ledger view.
+
+        Used after any failed attach/detach so a request either fully happens or leaves the pod
+        exactly as the ledger describes it, and by the reconciler loop. Returns the issues fixed.
+        """
+        st = await self.pod_state(pod, fresh=True, ledger_snapshot=ledger_snapshot)
+        if st.mount_type == MountType.UNKNOWN:
+            raise LedgerError("ledger unavailable")
+        issues = self.hm.audit(pod, st.hot, st.own)
+        if not issues:
+            return []
+        missing = [i for i in issues if i.kind.startswith("missing")]
+        stale = [i for i in issues if i.kind.startswith("stale")]
+        if missing:
+            self.hm.repair(pod, missing, st.hot, st.own)
+        if stale:
+            self.hm.revoke_issues(pod, stale, st.hot, st.own)
+        return issues
+
+    async def _rollback(self, pod: dict, what: str) -> None:
+        try:
+            fixed = await self.reconcile_pod(pod)
+            if fixed:
+                log.kv(_log, 30, f"{what} rolled back to ledger state",
+                       pod=f"{podu.ns_of(pod)}/{podu.name_of(pod)}", fixed=len(fixed))
+        except Exception as e:  # noqa: BLE001
+            _log.error("rollback after %s failed (the reconciler will retry): %s", what, e)
 
     @staticmethod
     def _devices(gs: Sequence[AmdGpu], owner: Dict[int, str]) -> List:
@@ -180,6 +239,7 @@ class GpuMountService:
         if n <= 0 or n > self.cfg.max_gpus_per_request:
             raise RpcError(grpc.StatusCode.INVALID_ARGUMENT, f"invalid gpu_num {n}")
         with trace.span("pod_lookup"):
+            self.faults.check("pod_lookup")
             pod = await self.get_pod(req.namespace, req.pod_name)
         if pod is None:
             _log.info("no such pod %s/%s", req.namespace, req.pod_name)
@@ -203,7 +263,7 @@ class GpuMountService:
                 _log.warning("policy denied add on %s/%s: %s", req.namespace, req.pod_name, why)
                 raise RpcError(grpc.StatusCode.FAILED_PRECONDITION, f"{ERR_POLICY}: {why}")
             with trace.span("placement"):
-                preferred = await self._preferred(n, st)
+                preferred = self._preferred(n, st)
             try:
                 res = await self.ph.reserve(pod, n, req.is_entire_mount, preferred,
                                             attach_id=log.request_id.get(),
@@ -211,7 +271,7 @@ class GpuMountService:
             except InsufficientGPU as e:
                 _log.info("insufficient GPUs on %s: %s", self.cfg.node_name, e)
                 return api.AddGPUResponse(add_gpu_result=api.ADD_INSUFFICIENT, message=str(e))
-            except (ReserveError, asyncio.TimeoutError) as e:
+            except (ReserveError, asyncio.TimeoutError, InjectedFault, LedgerError) as e:
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             keys = gpus_by_key(self.inv.gpus())
             new = [keys[normalize_device_id(d)] for d in res.device_ids]
@@ -225,9 +285,13 @@ class GpuMountService:
             try:
                 with trace.span("mount", gpus=len(new)):
                     self.hm.attach(pod, new, st.hot, st.own, req.container)
-            except MountError as e:
+            except (MountError, InjectedFault) as e:
                 _log.error("mount failed on %s/%s: %s", req.namespace, req.pod_name, e)
-                await self.ph.release(res.placeholders, wait=False)
+                try:
+                    await self.ph.release(res.placeholders, wait=False)
+                except Exception as e2:  # noqa: BLE001
+                    _log.error("placeholder release after failed mount: %s", e2)
+                await self._rollback(pod, "attach")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             log.kv(_log, 20, "attached", pod=f"{req.namespace}/{req.pod_name}",
                    gpus=[g.bdf for g in new])
@@ -235,9 +299,11 @@ class GpuMountService:
                                       devices=self._devices(new, owner),
                                       message="Add GPU Success")
 
-    async def _preferred(self, n: int, st: PodGpuState) -> List[str]:
-        """xGMI/NUMA-aware preferred device IDs among currently free GPUs."""
+    def _preferred(self, n: int, st: PodGpuState) -> List[str]:
+        """xGMI/NUMA-aware preferred device IDs among the GPUs free in the last ledger view."""
         allocated = {normalize_device_id(d) for ids in st.ledger.values() for d in ids}
+        allocated.update(normalize_device_id(d) for ids in self.ph.device_ids.values()
+                         for d in ids)
         gpus = self.inv.gpus()
         free = [g for g in gpus if not allocated.intersection(g.ledger_keys())]
         plc = topology.choose(free, n, self.inv.links(), attached=st.hot + st.own,
@@ -267,6 +333,7 @@ class GpuMountService:
 
     async def _remove_gpu(self, req):
         with trace.span("pod_lookup"):
+            self.faults.check("pod_lookup")
             pod = await self.get_pod(req.namespace, req.pod_name)
         if pod is None:
             return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_POD_NOT_FOUND)
@@ -281,30 +348,37 @@ class GpuMountService:
                                              message="Invalid UUIDs")
             sel_idx = {g.index for g in selected}
             keep = [g for g in st.hot if g.index not in sel_idx]
-            with trace.span("busy_check"):
-                targets = self.hm.targets(pod, req.container)
-                cpids = sorted({p for t in targets for p in t.pids})
-                busy = procs.busy_pids(self.inv, selected, cpids, self.cfg.drm_major)
+            try:
+                with trace.span("busy_check"):
+                    self.faults.check("busy_check")
+                    targets = self.hm.targets(pod, req.container)
+                    cpids = sorted({p for t in targets for p in t.pids})
+                    busy = procs.busy_pids(self.inv, selected, cpids, self.cfg.drm_major)
+            except (MountError, InjectedFault) as e:
+                raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             if busy and not req.force:
                 _log.info("GPU busy in %s/%s: %s", req.namespace, req.pod_name, busy)
                 return api.RemoveGPUResponse(
                     remove_gpu_result=api.REMOVE_BUSY,
                     message=f"busy: {json.dumps({str(k): v for k, v in busy.items()})}")
-            with trace.span("unmount", gpus=len(selected)):
-                self.hm.detach(pod, selected, keep, st.own, req.container, targets)
-            killed: List[int] = sorted({p for v in busy.values() for p in v})
-            if killed:
-                with trace.span("kill", pids=len(killed)):
-                    procs.signal_pids(killed, self.cfg.kill_signal)
-                    asyncio.ensure_future(procs.terminate(killed, self.cfg.kill_signal,
-                                                          self.cfg.kill_grace_s))
             phs = [ph for ph in st.placeholders
                    if {g.index for g in st.by_placeholder[(ph.namespace, ph.name)]} & sel_idx]
+            killed: List[int] = sorted({p for v in busy.values() for p in v})
             try:
-                await self.ph.release(phs, wait=True)
-            except asyncio.TimeoutError as e:
-                raise RpcError(grpc.StatusCode.DEADLINE_EXCEEDED,
-                               "placeholders not deleted in time") from e
+                # revoke before release: the GPU never becomes schedulable while the tenant can
+                # still reach it (reference order deny → rm → kill, util.go:112-139)
+                with trace.span("unmount", gpus=len(selected)):
+                    self.hm.detach(pod, selected, keep, st.own, req.container, targets)
+                if killed:
+                    with trace.span("kill", pids=len(killed)):
+                        procs.signal_pids(killed, self.cfg.kill_signal)
+                        asyncio.ensure_future(procs.terminate(killed, self.cfg.kill_signal,
+                                                              self.cfg.kill_grace_s))
+                await self.ph.release(phs, wait=False)
+            except (MountError, ReserveError, InjectedFault, OSError) as e:
+                _log.error("detach failed on %s/%s: %s", req.namespace, req.pod_name, e)
+                await self._rollback(pod, "detach")
+                raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             owner = {g.index: ph.name for ph in phs
                      for g in st.by_placeholder[(ph.namespace, ph.name)]}
             return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_SUCCESS,
