@@ -49,6 +49,8 @@ def main() -> int:
     ap.add_argument("--amdsmi", default="", help='"" = real libamd_smi, "mock" = bundled mock')
     ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--warm-pool", type=int, default=0,
+                    help="standby placeholders per node (claim instead of create); 0 = off")
     ap.add_argument("--protocol", choices=("gpumounter", "reference"), default="gpumounter",
                     help="'reference' re-enacts the reference's call sequence on the same "
                          "cluster (emulated baseline, see gpumounter_amd/fakes/refproto.py)")
@@ -96,8 +98,16 @@ def main() -> int:
             return 3
         lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
         tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
-                             node_gpu_bdfs=node_bdfs)
+                             node_gpu_bdfs=node_bdfs,
+                             worker_overrides={"warm_pool_size": args.warm_pool})
         lc = tc.start()
+        if args.warm_pool:
+            pool = lc.nodes["node-0"].worker.pool
+            t_wait = time.time()
+            while len(pool.standby()) < min(args.warm_pool, len(node_bdfs)):
+                if time.time() - t_wait > 120:
+                    raise RuntimeError("warm pool did not fill")
+                time.sleep(0.01)
         if args.protocol == "reference":
             from gpumounter_amd.fakes import refproto
             refproto.install(lc)
@@ -109,6 +119,7 @@ def main() -> int:
 
     nccl_group = None
     bound_dev = [None]
+    pool_cap = len(info.get("node_gpus", 0) and [0] * info["node_gpus"]) if rank == 0 else 0
     attach_ms, detach_ms, audit_issues, probe_us, stage = [], [], 0, [], {}
     ar_ms = []
 
@@ -163,6 +174,13 @@ def main() -> int:
             t1 = time.perf_counter()
             if code != 200:
                 raise RuntimeError(f"detach failed: {code} {body}")
+            if args.warm_pool:   # steady state: the next attach finds a full pool
+                pool = lc.nodes["node-0"].worker.pool
+                t_wait = time.time()
+                while len(pool.standby()) < min(args.warm_pool, pool_cap):
+                    if time.time() - t_wait > 120:
+                        raise RuntimeError("warm pool did not refill")
+                    time.sleep(0.001)
             if record:
                 attach_ms.append(st["ms"])
                 detach_ms.append((t1 - t0) * 1e3)
@@ -216,6 +234,7 @@ def main() -> int:
                     "cgroup": args.cgroup,
                     "protocol": args.protocol if args.protocol == "gpumounter"
                     else "reference (emulated)",
+                    "warm_pool": args.warm_pool,
                 },
                 "attach_p99_ms": round(pct(attach_ms, 0.99), 4),
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),

@@ -106,6 +106,23 @@ class PodInformer:
                 await asyncio.sleep(backoff)
                 backoff = min(backoff * 2, 5.0)
 
+    def upsert(self, pod: dict) -> None:
+        """Write-through from our own API responses (create/patch) so readers do not wait for
+        the watch echo; an older resourceVersion never overwrites a newer cached one."""
+        md = pod.get("metadata", {})
+        key = (md.get("namespace", ""), md.get("name", ""))
+        cur = self.cache.get(key)
+        if cur is not None:
+            try:
+                if int(cur["metadata"].get("resourceVersion", 0)) > \
+                        int(md.get("resourceVersion", 0)):
+                    return
+            except (TypeError, ValueError):
+                pass
+        if key in self.deleted and self.deleted[key] == md.get("uid"):
+            return
+        self.cache[key] = pod
+
     # ------------------------------------------------------------------------ queries
     def get(self, ns: str, name: str) -> Optional[dict]:
         p = self.cache.get((ns, name))

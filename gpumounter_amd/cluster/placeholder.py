@@ -198,6 +198,9 @@ class PlaceholderManager:
         created = [Placeholder(r["metadata"]["namespace"], r["metadata"]["name"],
                                r["metadata"]["uid"], (), mode)
                    for r in results if isinstance(r, dict)]
+        for r in results:
+            if isinstance(r, dict):
+                self.informer.upsert(r)  # visible to owned_by() before the watch echo
         errors = [r for r in results if not isinstance(r, dict)]
         if errors:
             await self.release(created, wait=False)

@@ -1,0 +1,253 @@
+"""Warm placeholder pool: pre-admitted GPUs that an attach claims with a metadata patch.
+
+Attach latency in a real cluster is dominated by what happens *between* creating a placeholder
+and reading its device IDs: scheduling, kubelet admission, the device plugin's Allocate — tens of
+milliseconds even when images are cached, and seconds for the reference (``alpine:latest`` pulled
+with policy Always). With ``warm_pool_size = K`` each worker keeps K single-GPU
+*standby* placeholders admitted on its node. Those GPUs are held in the scheduler's books exactly
+like any hot-mounted GPU (the ledger stays consistent), but belong to no tenant. An attach then:
+
+1. picks the best standby GPUs for the pod with the xGMI/NUMA policy,
+2. re-labels those placeholders to the pod (one PATCH each, in parallel) — no scheduling, no
+   admission, no image pull,
+3. mounts them; a detach hands them back to the pool (PATCH) and the pool tops itself up in the
+   background.
+Entire mounts claim K standby placeholders as one group (``gpumounter.amd.com/group``) and keep
+the reference's all-or-nothing add/remove semantics. When the pool cannot cover a request the
+worker falls back to creating placeholders as usual.
+"""
+from __future__ import annotations
+
+import asyncio
+import secrets
+from typing import Dict, List, Optional, Sequence
+
+from gpumounter_amd.cluster.kube import NotFound
+from gpumounter_amd.cluster.placeholder import (InsufficientGPU, LABEL_NODE, Placeholder,
+                                                PlaceholderManager, Reservation, ReserveError,
+                                                _label_value)
+from gpumounter_amd.hw import topology
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.models.device import AmdGpu, gpus_by_key, normalize_device_id
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_GROUP, ANN_MOUNT_MODE,
+                                         ANN_OWNER_NAME, ANN_OWNER_UID, LABEL_APP,
+                                         LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
+                                         MODE_STANDBY)
+from gpumounter_amd.utils import log, trace
+
+_log = log.get("cluster.pool")
+
+
+def is_standby(p: dict) -> bool:
+    return (p["metadata"].get("annotations") or {}).get(ANN_MOUNT_MODE) == MODE_STANDBY
+
+
+class WarmPool:
+    def __init__(self, cfg, ph: PlaceholderManager, inv, metrics=None) -> None:
+        self.cfg = cfg
+        self.ph = ph
+        self.inv = inv
+        self.metrics = metrics
+        self.target = cfg.warm_pool_size
+        self._lock = asyncio.Lock()          # serializes claims and give-backs on this node
+        self._claimed: set = set()           # uids claimed but not yet visible as claimed
+        self._refill_task: Optional[asyncio.Task] = None
+        self._wake: Optional[asyncio.Event] = None
+        self.exhausted = False               # last refill hit InsufficientGPU
+
+    @property
+    def enabled(self) -> bool:
+        return self.target > 0
+
+    # ------------------------------------------------------------------------ state
+    def standby(self) -> List[Placeholder]:
+        """Admitted standby placeholders (device IDs known)."""
+        out = []
+        for p in self.ph.live():
+            if not is_standby(p) or p["metadata"].get("uid") in self._claimed:
+                continue
+            c = self.ph.cached(p)
+            if c is None:
+                ids = self.ph.last_ledger.get((p["metadata"]["namespace"],
+                                               p["metadata"]["name"]))
+                if not ids:
+                    continue
+                c = PlaceholderManager.from_pod(p, self.ph.last_ledger)
+                self.ph.device_ids[c.uid] = c.device_ids
+            out.append(c)
+        return out
+
+    def pending(self) -> int:
+        return sum(1 for p in self.ph.live() if is_standby(p)
+                   and self.ph.cached(p) is None
+                   and not self.ph.last_ledger.get((p["metadata"]["namespace"],
+                                                    p["metadata"]["name"])))
+
+    # ------------------------------------------------------------------------ refill
+    def standby_body(self) -> dict:
+        name = f"gpumounter-standby-{_label_value(self.ph.node)[:40]}-{secrets.token_hex(4)}"
+        body = self.ph.build({"metadata": {"name": "standby", "namespace": "", "uid": ""}},
+                             1, MODE_STANDBY)
+        md = body["metadata"]
+        md["name"] = name
+        md["namespace"] = self.cfg.pool_namespace
+        md["labels"] = {LABEL_APP: LABEL_APP_VALUE, LABEL_NODE: _label_value(self.ph.node)}
+        md["annotations"] = {ANN_MOUNT_MODE: MODE_STANDBY}
+        md.pop("ownerReferences", None)
+        return body
+
+    async def start(self) -> None:
+        if not self.enabled:
+            return
+        self._wake = asyncio.Event()
+        self._refill_task = asyncio.ensure_future(self._refill_loop())
+        self._wake.set()
+
+    async def stop(self) -> None:
+        if self._refill_task is not None:
+            self._refill_task.cancel()
+            try:
+                await self._refill_task
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001
+                pass
+
+    def poke(self) -> None:
+        if self._wake is not None:
+            self._wake.set()
+
+    async def _refill_loop(self) -> None:
+        while True:
+            await self._wake.wait()
+            self._wake.clear()
+            try:
+                await self.refill()
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                _log.warning("pool refill failed: %s", e)
+                await asyncio.sleep(1.0)
+                self._wake.set()
+
+    async def refill(self) -> int:
+        """Create standby placeholders until ``target`` are admitted or pending."""
+        missing = self.target - len(self.standby()) - self.pending()
+        if missing <= 0:
+            return 0
+        # only ask for what the node can actually admit (allocatable − allocated)
+        led = await self.ph.ledger.by_pod()
+        self.ph.last_ledger = led
+        allocated = {normalize_device_id(d) for ids in led.values() for d in ids}
+        alloc = await self.ph.ledger.allocatable()
+        if alloc is None:
+            alloc = [g.bdf for g in self.inv.gpus()]
+        free = sum(1 for d in alloc if normalize_device_id(d) not in allocated)
+        missing = min(missing, free)
+        if missing <= 0:
+            self.exhausted = True
+            return 0
+        created = []
+        for _ in range(missing):
+            body = self.standby_body()
+            try:
+                pod = await self.ph.kube.create_pod(self.cfg.pool_namespace, body)
+            except Exception as e:  # noqa: BLE001
+                _log.warning("standby create failed: %s", e)
+                break
+            self.ph.informer.upsert(pod)
+            created.append(Placeholder(pod["metadata"]["namespace"], pod["metadata"]["name"],
+                                       pod["metadata"]["uid"], (), MODE_STANDBY))
+        if not created:
+            return 0
+        try:
+            await self.ph._await_admission(created, self.cfg.attach_timeout_s)  # noqa: SLF001
+            self.exhausted = False
+        except InsufficientGPU:
+            # the node is full: drop the standby placeholders that could not be admitted
+            self.exhausted = True
+            unadmitted = [c for c in created if not c.device_ids]
+            await self.ph.release(unadmitted, wait=False)
+        await self.ph.informer.poke()
+        return len(created)
+
+    # ------------------------------------------------------------------------ claim / return
+    async def claim(self, owner: dict, n: int, entire: bool, attached: Sequence[AmdGpu],
+                    attach_id: str = "", container: str = "") -> Optional[Reservation]:
+        """Claim ``n`` standby GPUs for ``owner``; None if the pool cannot cover the request."""
+        async with self._lock:
+            pool = self.standby()
+            if len(pool) < n:
+                return None
+            keys = gpus_by_key(self.inv.gpus())
+            by_gpu: Dict[int, Placeholder] = {}
+            cands: List[AmdGpu] = []
+            for ph in pool:
+                g = keys.get(normalize_device_id(ph.device_ids[0]))
+                if g is not None:
+                    by_gpu[g.index] = ph
+                    cands.append(g)
+            plc = topology.choose(cands, n, self.inv.links(), attached=attached,
+                                  policy=self.cfg.topology_policy)
+            if plc is None:
+                return None
+            chosen = [by_gpu[i] for i in plc.chosen]
+            mode = "entire" if entire else "single"
+            group = secrets.token_hex(4) if entire else ""
+            patch = {"metadata": {
+                "labels": {LABEL_OWNER: _label_value(podu.name_of(owner)),
+                           LABEL_OWNER_NS: _label_value(podu.ns_of(owner))},
+                "annotations": {ANN_OWNER_UID: podu.uid_of(owner),
+                                ANN_OWNER_NAME: podu.name_of(owner), ANN_MOUNT_MODE: mode,
+                                ANN_ATTACH_ID: attach_id, ANN_CONTAINER: container,
+                                ANN_GROUP: group or None}}}
+            for ph in chosen:
+                self._claimed.add(ph.uid)
+            with trace.span("pool_claim", placeholders=len(chosen)):
+                res = await asyncio.gather(
+                    *[self.ph.kube.patch_pod(ph.namespace, ph.name, patch) for ph in chosen],
+                    return_exceptions=True)
+            ok = [r for r in res if isinstance(r, dict)]
+            for r in ok:
+                self.ph.informer.upsert(r)
+            for ph in chosen:
+                self._claimed.discard(ph.uid)
+            if len(ok) != len(chosen):
+                # undo the partial claim, then let the caller fall back
+                back = [ph for ph, r in zip(chosen, res) if isinstance(r, dict)]
+                await self._standby_patch(back)
+                return None
+            for ph in chosen:
+                ph.mode = mode
+            if self.metrics is not None:
+                self.metrics.reconcile_actions.labels(action="pool_claim").inc(len(chosen))
+        self.poke()
+        return Reservation(chosen)
+
+    async def _standby_patch(self, phs: Sequence[Placeholder]) -> List[Placeholder]:
+        patch = {"metadata": {
+            "labels": {LABEL_OWNER: None, LABEL_OWNER_NS: None},
+            "annotations": {ANN_OWNER_UID: None, ANN_OWNER_NAME: None,
+                            ANN_MOUNT_MODE: MODE_STANDBY, ANN_ATTACH_ID: None,
+                            ANN_CONTAINER: None, ANN_GROUP: None}}}
+        res = await asyncio.gather(*[self.ph.kube.patch_pod(p.namespace, p.name, patch)
+                                     for p in phs], return_exceptions=True)
+        back = []
+        for p, r in zip(phs, res):
+            if isinstance(r, dict):
+                self.ph.informer.upsert(r)
+                back.append(p)
+            elif not isinstance(r, NotFound):
+                _log.error("return %s/%s to pool: %s", p.namespace, p.name, r)
+        return back
+
+    async def give_back(self, phs: Sequence[Placeholder]) -> None:
+        """Return detached placeholders to the pool (up to ``target``); delete the rest."""
+        async with self._lock:
+            room = max(self.target - len(self.standby()), 0)
+            keep = [p for p in phs if p.device_ids and len(p.device_ids) == 1][:room]
+            drop = [p for p in phs if p not in keep]
+            with trace.span("pool_return", placeholders=len(keep)):
+                back = await self._standby_patch(keep)
+            drop += [p for p in keep if p not in back]
+        if drop:
+            await self.ph.release(drop, wait=False)
+        self.poke()

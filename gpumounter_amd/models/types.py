@@ -38,6 +38,9 @@ ANN_ATTACH_ID = "gpumounter.amd.com/attach-id"
 ANN_CONTAINER = "gpumounter.amd.com/container"
 ANN_DEVICES = "gpumounter.amd.com/devices"
 ANN_STATE = "gpumounter.amd.com/state"      # reserved | attached | detaching
+ANN_OWNER_NAME = "gpumounter.amd.com/owner-name"
+ANN_GROUP = "gpumounter.amd.com/group"      # entire-mount group made of pooled placeholders
+MODE_STANDBY = "standby"
 FINALIZER = "gpumounter.amd.com/release"
 SLAVE_SUFFIX = "-slave-pod-"
 

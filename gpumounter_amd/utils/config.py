@@ -45,6 +45,10 @@ class Config:
     placeholder_image: str = "registry.k8s.io/pause:3.9"
     placeholder_pull_policy: str = "IfNotPresent"
     placeholder_priority_class: str = ""
+    # Warm pool: standby placeholders that keep this many GPUs per node pre-admitted for
+    # hot-mount (0 = off, the reference's behaviour). Claiming is a metadata patch, so attach
+    # latency no longer includes scheduling + kubelet admission; the price is reserved capacity.
+    warm_pool_size: int = 0
     # --- kubelet PodResources --------------------------------------------------------------
     kubelet_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     kubelet_timeout_s: float = 10.0

@@ -79,6 +79,8 @@ class Reconciler:
         by_owner: Dict[tuple, List[dict]] = {}
         for p in placeholders:
             ann = p["metadata"].get("annotations") or {}
+            if ann.get("gpumounter.amd.com/mount-mode") == "standby":
+                continue  # warm-pool capacity: owned by the pool, not by a tenant
             owner = (ann.get("gpumounter.amd.com/owner-name", ""),
                      (p["metadata"].get("labels") or {}).get("gpumounter.amd.com/owner-namespace", ""),
                      ann.get(ANN_OWNER_UID, ""))

@@ -21,6 +21,7 @@ from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import KubeClient
 from gpumounter_amd.cluster.placeholder import PlaceholderManager
+from gpumounter_amd.cluster.pool import WarmPool
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.node.cgroup import CgroupResolver, make_backend
 from gpumounter_amd.node.devnodes import DevNodeWriter
@@ -69,6 +70,8 @@ class Worker:
         self.service = GpuMountService(cfg, self.kube, self.inv, self.ledger, self.placeholders,
                                        self.hotmount, self.node_informer, self.metrics,
                                        self.faults)
+        self.pool = WarmPool(cfg, self.placeholders, self.inv, self.metrics)
+        self.service.pool = self.pool
         self.reconciler = Reconciler(self.service, cfg.reconcile_period_s)
         self.grpc_server: Optional[grpc.aio.Server] = None
         self.http_runner: Optional[web.AppRunner] = None
@@ -137,6 +140,7 @@ class Worker:
             self.http_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
         if reconcile and self.cfg.reconcile_period_s > 0:
             await self.reconciler.start()
+        await self.pool.start()
         self.ready = True
         _log.info("worker %s serving gRPC :%d http :%d (cgroup %s/%s, devnodes %s, ledger %s)",
                   self.cfg.node_name, self.grpc_port, self.http_port, self.resolver.mode,
@@ -158,6 +162,7 @@ class Worker:
 
     async def stop(self) -> None:
         self.ready = False
+        await self.pool.stop()
         await self.reconciler.stop()
         if self.grpc_server is not None:
             await self.grpc_server.stop(0.5)

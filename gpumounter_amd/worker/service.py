@@ -86,6 +86,7 @@ class GpuMountService:
         self.node_pods = node_pods
         self.metrics = metrics or Metrics()
         self.faults = faults if faults is not None else FaultInjector(cfg.fault)
+        self.pool = None  # WarmPool, attached by the Worker when warm_pool_size > 0
         self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}
         self._own: Dict[str, Tuple[str, ...]] = {}   # pod uid → its own device-plugin GPU IDs
         self.ledger_reads = 0
@@ -265,9 +266,7 @@ class GpuMountService:
             with trace.span("placement"):
                 preferred = self._preferred(n, st)
             try:
-                res = await self.ph.reserve(pod, n, req.is_entire_mount, preferred,
-                                            attach_id=log.request_id.get(),
-                                            container=req.container)
+                res = await self._reserve(pod, n, req, st, preferred)
             except InsufficientGPU as e:
                 _log.info("insufficient GPUs on %s: %s", self.cfg.node_name, e)
                 return api.AddGPUResponse(add_gpu_result=api.ADD_INSUFFICIENT, message=str(e))
@@ -288,7 +287,7 @@ class GpuMountService:
             except (MountError, InjectedFault) as e:
                 _log.error("mount failed on %s/%s: %s", req.namespace, req.pod_name, e)
                 try:
-                    await self.ph.release(res.placeholders, wait=False)
+                    await self._release(res.placeholders)
                 except Exception as e2:  # noqa: BLE001
                     _log.error("placeholder release after failed mount: %s", e2)
                 await self._rollback(pod, "attach")
@@ -298,6 +297,36 @@ class GpuMountService:
             return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS,
                                       devices=self._devices(new, owner),
                                       message="Add GPU Success")
+
+    async def _reserve(self, pod: dict, n: int, req, st: PodGpuState, preferred: List[str]):
+        """Claim from the warm pool first (if enabled), create placeholders for the rest."""
+        claimed = None
+        if self.pool is not None and self.pool.enabled:
+            k = min(n, len(self.pool.standby()))
+            if k:
+                claimed = await self.pool.claim(pod, k, req.is_entire_mount, st.hot + st.own,
+                                                log.request_id.get(), req.container)
+        got = len(claimed.placeholders) if claimed else 0
+        if got == n:
+            return claimed
+        try:
+            rest = await self.ph.reserve(pod, n - got, req.is_entire_mount,
+                                         preferred if not got else [],
+                                         attach_id=log.request_id.get(),
+                                         container=req.container)
+        except BaseException:
+            if claimed:
+                await self.pool.give_back(claimed.placeholders)
+            raise
+        if claimed:
+            rest.placeholders = claimed.placeholders + rest.placeholders
+        return rest
+
+    async def _release(self, phs) -> None:
+        if self.pool is not None and self.pool.enabled:
+            await self.pool.give_back(phs)
+        else:
+            await self.ph.release(phs, wait=False)
 
     def _preferred(self, n: int, st: PodGpuState) -> List[str]:
         """xGMI/NUMA-aware preferred device IDs among the GPUs free in the last ledger view."""
@@ -374,7 +403,7 @@ class GpuMountService:
                         procs.signal_pids(killed, self.cfg.kill_signal)
                         asyncio.ensure_future(procs.terminate(killed, self.cfg.kill_signal,
                                                               self.cfg.kill_grace_s))
-                await self.ph.release(phs, wait=False)
+                await self._release(phs)
             except (MountError, ReserveError, InjectedFault, OSError) as e:
                 _log.error("detach failed on %s/%s: %s", req.namespace, req.pod_name, e)
                 await self._rollback(pod, "detach")

@@ -1,0 +1,116 @@
+"""Warm placeholder pool (gpumounter_amd/cluster/pool.py): claims skip scheduling + admission,
+detaches hand GPUs back, entire mounts keep all-or-nothing semantics, the ledger stays consistent."""
+import asyncio
+import time
+
+from gpumounter_amd.cluster.pool import is_standby
+from gpumounter_amd.fakes.apiserver import LatencyModel
+from gpumounter_amd.fakes.harness import LocalCluster
+
+
+async def wait_pool(lc, n, timeout=5.0):
+    pool = lc.nodes["node-0"].worker.pool
+    t0 = time.monotonic()
+    while len(pool.standby()) < n:
+        assert time.monotonic() - t0 < timeout, (len(pool.standby()), n)
+        await asyncio.sleep(0.01)
+    return pool
+
+
+def standby_count(lc):
+    return sum(1 for p in lc.cluster.placeholders() if is_standby(p))
+
+
+def test_pool_fills_claims_and_takes_back():
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 8}) as lc:
+            await wait_pool(lc, 8)
+            assert len(lc.nodes["node-0"].node.allocated) == 8      # held in the books
+            lc.tenant("t")
+            posts = lc.cluster.requests_by_verb.get("POST", 0)
+            code, b = await lc.add("default", "t", 2)
+            assert code == 200
+            assert lc.cluster.requests_by_verb.get("POST", 0) == posts  # no placeholder created
+            assert {t["name"] for t in b["timings"]} >= {"pool_claim"}
+            assert [d["numa_node"] for d in b["devices"]] == [0, 0]
+            assert not await lc.audit("default", "t")
+            assert standby_count(lc) == 6 and len(lc.cluster.placeholders()) == 8
+            code, _ = await lc.remove("default", "t", [d["uuid"] for d in b["devices"]])
+            assert code == 200 and not await lc.audit("default", "t")
+            await wait_pool(lc, 8)
+            assert standby_count(lc) == 8 and len(lc.nodes["node-0"].node.allocated) == 8
+    asyncio.run(main())
+
+
+def test_pool_entire_mount_group_semantics():
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 8}) as lc:
+            await wait_pool(lc, 8)
+            lc.tenant("e")
+            code, b = await lc.add("default", "e", 4, entire=True)
+            assert code == 200 and len(b["devices"]) == 4
+            assert (await lc.add("default", "e", 1))[0] == 500          # entire: no more adds
+            ids = [d["uuid"] for d in b["devices"]]
+            assert (await lc.remove("default", "e", ids[:2]))[0] == 400  # whole group only
+            assert (await lc.remove("default", "e", ids))[0] == 200
+            assert not await lc.audit("default", "e")
+    asyncio.run(main())
+
+
+def test_pool_partial_cover_mixes_claim_and_create():
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 2}) as lc:
+            await wait_pool(lc, 2)
+            lc.tenant("m")
+            code, b = await lc.add("default", "m", 5)
+            assert code == 200 and len(b["devices"]) == 5
+            assert not await lc.audit("default", "m")
+            node = lc.nodes["node-0"].node
+            # 5 hot + refilled standby ≤ 8, never double-booked
+            assert len(node.allocated) <= 8 and len(set(node.allocated)) == len(node.allocated)
+            code, _ = await lc.remove("default", "m", [d["uuid"] for d in b["devices"]])
+            assert code == 200 and not await lc.audit("default", "m")
+            await wait_pool(lc, 2)
+    asyncio.run(main())
+
+
+def test_pool_cuts_attach_latency_under_realistic_control_plane():
+    lat = LatencyModel(api_ms=0.5, schedule_ms=10, admit_ms=15, sandbox_ms=50, start_ms=20)
+
+    async def measure(pool_size):
+        async with LocalCluster(latency=lat, worker_overrides={"warm_pool_size": pool_size}) as lc:
+            if pool_size:
+                await wait_pool(lc, pool_size, timeout=10)
+            lc.tenant("x")
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                code, b = await lc.add("default", "x", 1)
+                ts.append((time.perf_counter() - t0) * 1e3)
+                assert code == 200
+                await lc.remove("default", "x", [b["devices"][0]["uuid"]])
+                if pool_size:
+                    await wait_pool(lc, pool_size, timeout=10)
+            return sorted(ts)[2]
+
+    async def main():
+        cold = await measure(0)
+        warm = await measure(4)
+        assert cold > 25            # schedule + admission are on the attach path
+        assert warm < cold / 2      # a claim is a metadata patch
+    asyncio.run(main())
+
+
+def test_pool_claims_released_when_tenant_disappears():
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 4}) as lc:
+            await wait_pool(lc, 4)
+            lc.tenant("gone")
+            code, b = await lc.add("default", "gone", 2)
+            assert code == 200
+            lc.cluster.delete("default", "gone", grace=0)
+            rep = await lc.nodes["node-0"].worker.reconciler.run_once()
+            assert len(rep.owner_gone) == 2
+            await wait_pool(lc, 4)
+            assert standby_count(lc) == 4
+    asyncio.run(main())
