@@ -109,6 +109,9 @@ class WorkerDirectory:
 
 
 class Master:
+    POD_CACHE_TTL_S = 30.0
+    POD_CACHE_MAX = 4096
+
     def __init__(self, cfg, kube: Optional[KubeClient] = None) -> None:
         self.cfg = cfg
         self.kube = kube or KubeClient.from_config(cfg)
@@ -117,6 +120,7 @@ class Master:
         self.metrics = Metrics()
         self.runner: Optional[web.AppRunner] = None
         self.port = 0
+        self._pod_nodes: Dict[Tuple[str, str], Tuple[str, str, float]] = {}
 
     # ------------------------------------------------------------------------ app
     def app(self) -> web.Application:
@@ -162,6 +166,17 @@ class Master:
     def _wants_json(request: web.Request) -> bool:
         return "application/json" in request.headers.get("Accept", "")
 
+    def _unauthorized(self, request: web.Request, route: str) -> Optional[web.Response]:
+        """Bearer-token check for mutating routes (the reference has no authn: SURVEY defect 13)."""
+        if not self.cfg.api_token:
+            return None
+        import hmac
+
+        got = request.headers.get("Authorization", "")
+        if hmac.compare_digest(got, f"Bearer {self.cfg.api_token}"):
+            return None
+        return self._reply(request, route, 401, "Unauthorized", {})
+
     def _reply(self, request, route: str, status: int, text: str, payload: dict) -> web.Response:
         self.metrics.http_requests.labels(route=route, code=str(status)).inc()
         if self._wants_json(request):
@@ -173,25 +188,44 @@ class Master:
             return web.json_response(payload, status=status)
         return _text(text, status)
 
-    async def _locate(self, request, route: str, ns: str, name: str
-                      ) -> Tuple[Optional[dict], Optional[str], Optional[web.Response]]:
-        try:
-            pod = await self.kube.get_pod(ns, name)
-        except NotFound:
-            return None, None, self._reply(request, route, 404,
-                                           f"No pod: {name} in namespace: {ns}", {})
-        except ApiError as e:
-            return None, None, self._reply(request, route, 500, str(e), {})
+    async def _locate(self, request, route: str, ns: str, name: str, fresh: bool = False
+                      ) -> Tuple[Optional[dict], Optional[str], Optional[web.Response], bool]:
+        """Pod → node → worker target. Recently seen pods are served from a small cache (a pod
+        never changes node); a stale entry is detected by the worker and retried fresh."""
+        key = (ns, name)
+        hit = None if fresh else self._pod_nodes.get(key)
+        now = time.monotonic()
+        if hit is not None and now - hit[2] < self.POD_CACHE_TTL_S:
+            pod = {"metadata": {"name": name, "namespace": ns, "uid": hit[1]},
+                   "spec": {"nodeName": hit[0]}}
+            cached = True
+        else:
+            try:
+                pod = await self.kube.get_pod(ns, name)
+            except NotFound:
+                self._pod_nodes.pop(key, None)
+                return None, None, self._reply(request, route, 404,
+                                               f"No pod: {name} in namespace: {ns}", {}), False
+            except ApiError as e:
+                return None, None, self._reply(request, route, 500, str(e), {}), False
+            cached = False
+            if podu.node_of(pod):
+                self._pod_nodes[key] = (podu.node_of(pod), podu.uid_of(pod), now)
+                if len(self._pod_nodes) > self.POD_CACHE_MAX:
+                    self._pod_nodes.pop(next(iter(self._pod_nodes)))
         node = podu.node_of(pod)
         target = self.workers.target(node)
         if target is None:
             _log.error("no gpu mounter worker on node %r", node)
             return pod, None, self._reply(request, route, 500, "Service Internal Error",
-                                          {"error": f"no worker on node {node!r}"})
-        return pod, target, None
+                                          {"error": f"no worker on node {node!r}"}), cached
+        return pod, target, None, cached
 
     async def add_gpu(self, request: web.Request) -> web.Response:
         route = "addgpu"
+        denied = self._unauthorized(request, route)
+        if denied is not None:
+            return denied
         rid = log.new_request_id("add")
         mi = request.match_info
         ns, name = mi["namespace"], mi["pod"]
@@ -207,22 +241,31 @@ class Master:
             # the reference forwarded 0 and the worker divided by zero (SURVEY defect 6)
             return self._reply(request, route, 400, f"Invalid param gpuNum: {mi['gpuNum']}", {})
         t0 = time.perf_counter()
-        pod, target, err = await self._locate(request, route, ns, name)
-        if err is not None:
-            return err
-        stub = self.workers.channel(target).unary_unary(
-            api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
-            response_deserializer=api.AddGPUResponse.FromString)
-        try:
-            resp = await stub(api.AddGPURequest(pod_name=name, namespace=ns, gpu_num=n,
-                                                is_entire_mount=entire, request_id=rid,
-                                                container=request.query.get("container", "")),
-                              timeout=self.cfg.rpc_timeout_s)
-        except grpc.aio.AioRpcError as e:
-            _log.error("AddGPU rpc to %s failed: %s %s", target, e.code().name, e.details())
-            code = 400 if e.code() == grpc.StatusCode.INVALID_ARGUMENT else 500
-            body = "Service Internal Error" if code == 500 else e.details()
-            return self._reply(request, route, code, body, {"error": e.details()})
+        for fresh in (False, True):
+            pod, target, err, cached = await self._locate(request, route, ns, name, fresh)
+            if err is not None:
+                return err
+            stub = self.workers.channel(target).unary_unary(
+                api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
+                response_deserializer=api.AddGPUResponse.FromString)
+            try:
+                resp = await stub(api.AddGPURequest(
+                    pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
+                    request_id=rid, container=request.query.get("container", "")),
+                    timeout=self.cfg.rpc_timeout_s)
+            except grpc.aio.AioRpcError as e:
+                if cached and e.code() == grpc.StatusCode.FAILED_PRECONDITION and \
+                        "this worker serves" in (e.details() or ""):
+                    self._pod_nodes.pop((ns, name), None)   # pod was recreated elsewhere
+                    continue
+                _log.error("AddGPU rpc to %s failed: %s %s", target, e.code().name, e.details())
+                code = 400 if e.code() == grpc.StatusCode.INVALID_ARGUMENT else 500
+                body = "Service Internal Error" if code == 500 else e.details()
+                return self._reply(request, route, code, body, {"error": e.details()})
+            if cached and resp.add_gpu_result == api.ADD_POD_NOT_FOUND:
+                self._pod_nodes.pop((ns, name), None)       # re-check with a fresh GET (→ 404)
+                continue
+            break
         payload = self._payload(resp, t0)
         node = podu.node_of(pod)
         if resp.add_gpu_result == api.ADD_SUCCESS:
@@ -235,6 +278,9 @@ class Master:
 
     async def remove_gpu(self, request: web.Request) -> web.Response:
         route = "removegpu"
+        denied = self._unauthorized(request, route)
+        if denied is not None:
+            return denied
         rid = log.new_request_id("rm")
         mi = request.match_info
         ns, name = mi["namespace"], mi["pod"]
@@ -251,21 +297,27 @@ class Master:
                                f"Invalid parameter force: {mi['force']}(should be true or false)",
                                {})
         t0 = time.perf_counter()
-        pod, target, err = await self._locate(request, route, ns, name)
-        if err is not None:
-            return err
-        stub = self.workers.channel(target).unary_unary(
-            api.REMOVE_GPU, request_serializer=api.RemoveGPURequest.SerializeToString,
-            response_deserializer=api.RemoveGPUResponse.FromString)
-        try:
-            resp = await stub(api.RemoveGPURequest(pod_name=name, namespace=ns, uuids=uuids,
-                                                   force=force, request_id=rid,
-                                                   container=request.query.get("container", "")),
-                              timeout=self.cfg.rpc_timeout_s)
-        except grpc.aio.AioRpcError as e:
-            _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name, e.details())
-            return self._reply(request, route, 500, "Service Internal Error",
-                               {"error": e.details()})
+        for fresh in (False, True):
+            pod, target, err, cached = await self._locate(request, route, ns, name, fresh)
+            if err is not None:
+                return err
+            stub = self.workers.channel(target).unary_unary(
+                api.REMOVE_GPU, request_serializer=api.RemoveGPURequest.SerializeToString,
+                response_deserializer=api.RemoveGPUResponse.FromString)
+            try:
+                resp = await stub(api.RemoveGPURequest(
+                    pod_name=name, namespace=ns, uuids=uuids, force=force, request_id=rid,
+                    container=request.query.get("container", "")),
+                    timeout=self.cfg.rpc_timeout_s)
+            except grpc.aio.AioRpcError as e:
+                _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name,
+                           e.details())
+                return self._reply(request, route, 500, "Service Internal Error",
+                                   {"error": e.details()})
+            if cached and resp.remove_gpu_result == api.REMOVE_POD_NOT_FOUND:
+                self._pod_nodes.pop((ns, name), None)
+                continue
+            break
         payload = self._payload(resp, t0)
         node = podu.node_of(pod)
         r = resp.remove_gpu_result

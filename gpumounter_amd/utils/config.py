@@ -80,6 +80,7 @@ class Config:
     rpc_timeout_s: float = 180.0
     reconcile_period_s: float = 30.0
     watch_resync_s: float = 300.0
+    api_token: str = ""                # if set, add/remove require "Authorization: Bearer <token>"
     # --- observability ---------------------------------------------------------------------
     log_level: str = "INFO"
     log_file: str = ""

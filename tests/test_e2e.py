@@ -417,3 +417,35 @@ def test_status_endpoints_and_metrics():
         assert {"ledger_reserve", "placeholder_wait", "mount", "mount.cgroup_rule",
                 "mount.devnodes"} <= stages
     run(body)
+
+
+def test_api_token_guards_mutating_routes():
+    async def body(lc):
+        lc.tenant("p")
+        lc.master.cfg.api_token = "s3cret"
+        code, text = await lc.add("default", "p", 1, accept_json=False)
+        assert (code, text) == (401, "Unauthorized\n")
+        url = lc.master_url + "/addgpu/namespace/default/pod/p/gpu/1/isEntireMount/false"
+        async with lc.session.get(url, headers={"Authorization": "Bearer s3cret"}) as r:
+            assert r.status == 200
+        assert await text_get(lc, "/") == (200, "This is gpu mounter api!\n")  # read-only open
+    run(body)
+
+
+def test_master_pod_cache_revalidates_recreated_and_deleted_pods():
+    async def body(lc):
+        lc.tenant("p", node="node-0")
+        assert (await lc.add("default", "p", 1))[0] == 200          # fills the cache
+        gets = lc.cluster.requests_by_verb.get("GET", 0)
+        _, b = await lc.add("default", "p", 1)
+        assert lc.cluster.requests_by_verb.get("GET", 0) == gets     # cache hit: no GET
+        # pod recreated on another node under the same name → worker refuses, master re-GETs
+        lc.cluster.delete("default", "p", grace=0)
+        lc.tenant("p", node="node-1")
+        code, b = await lc.add("default", "p", 1)
+        assert code == 200 and lc.cluster.placeholders()[-1]["spec"]["nodeName"] == "node-1"
+        # pod deleted → reference semantics: 404 from the master
+        lc.cluster.delete("default", "p", grace=0)
+        code, text = await lc.add("default", "p", 1, accept_json=False)
+        assert (code, text) == (404, "No pod: p in namespace: default\n")
+    run(body, n_nodes=2)
