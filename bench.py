@@ -119,7 +119,7 @@ def main() -> int:
 
     nccl_group = None
     bound_dev = [None]
-    pool_cap = len(info.get("node_gpus", 0) and [0] * info["node_gpus"]) if rank == 0 else 0
+    pool_cap = info.get("node_gpus", 0) if rank == 0 else 0
     attach_ms, detach_ms, audit_issues, probe_us, stage = [], [], 0, [], {}
     ar_ms = []
 

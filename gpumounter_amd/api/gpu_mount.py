@@ -22,6 +22,7 @@ _pf.message("AddGPURequest", [
     # --- extensions
     ("container", 5, "string", "opt"),          # target container (default: all containers)
     ("request_id", 6, "string", "opt"),
+    ("idempotency_key", 7, "string", "opt"),    # client retry key: same key → same attach
 ])
 _pf.message("Device", [
     ("uuid", 1, "string", "opt"),

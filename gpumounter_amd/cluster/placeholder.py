@@ -34,9 +34,10 @@ from typing import Dict, List, Optional, Sequence, Tuple
 from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_MOUNT_MODE,
-                                         ANN_OWNER_UID, ANN_PREFERRED, LABEL_APP, LABEL_APP_VALUE,
-                                         LABEL_OWNER, LABEL_OWNER_NS, SLAVE_SUFFIX)
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_IDEMPOTENCY,
+                                         ANN_MOUNT_MODE, ANN_OWNER_UID, ANN_PREFERRED, LABEL_APP,
+                                         LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
+                                         SLAVE_SUFFIX)
 from gpumounter_amd.node.ledger import LedgerClient
 from gpumounter_amd.utils import log, trace
 
@@ -117,7 +118,7 @@ class PlaceholderManager:
         return f"{LABEL_APP}={LABEL_APP_VALUE},{LABEL_NODE}={_label_value(node)}"
 
     def build(self, owner: dict, n_gpus: int, mode: str, preferred: Sequence[str] = (),
-              attach_id: str = "", container: str = "") -> dict:
+              attach_id: str = "", container: str = "", idempotency_key: str = "") -> dict:
         ns = self.namespace_for(owner)
         name = podu.name_of(owner)[: 253 - 20] + SLAVE_SUFFIX + secrets.token_hex(3)
         md = {
@@ -133,6 +134,8 @@ class PlaceholderManager:
         }
         if preferred:
             md["annotations"][ANN_PREFERRED] = ",".join(preferred)
+        if idempotency_key:
+            md["annotations"][ANN_IDEMPOTENCY] = idempotency_key
         if ns == podu.ns_of(owner):
             md["ownerReferences"] = [{"apiVersion": "v1", "kind": "Pod",
                                       "name": podu.name_of(owner), "uid": podu.uid_of(owner),
@@ -178,7 +181,8 @@ class PlaceholderManager:
 
     # ------------------------------------------------------------------------ reserve
     async def reserve(self, owner: dict, total: int, entire: bool, preferred: Sequence[str] = (),
-                      attach_id: str = "", container: str = "") -> Reservation:
+                      attach_id: str = "", container: str = "",
+                      idempotency_key: str = "") -> Reservation:
         """Entire mount = one placeholder holding ``total`` GPUs (all-or-nothing at the
         scheduler, reference QuickStart.md:52); single mount = ``total`` placeholders × 1 GPU."""
         if total <= 0:
@@ -188,8 +192,8 @@ class PlaceholderManager:
         mode = "entire" if entire else "single"
         prefs = [list(preferred[i * per_pod:(i + 1) * per_pod]) for i in range(k)] \
             if len(preferred) == total else [[] for _ in range(k)]
-        bodies = [self.build(owner, per_pod, mode, prefs[i], attach_id, container)
-                  for i in range(k)]
+        bodies = [self.build(owner, per_pod, mode, prefs[i], attach_id, container,
+                             idempotency_key) for i in range(k)]
         with trace.span("ledger_reserve", placeholders=k):
             self.faults.check("ledger_reserve")
             results = await asyncio.gather(

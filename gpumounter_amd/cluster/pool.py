@@ -29,7 +29,8 @@ from gpumounter_amd.cluster.placeholder import (InsufficientGPU, LABEL_NODE, Pla
 from gpumounter_amd.hw import topology
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu, gpus_by_key, normalize_device_id
-from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_GROUP, ANN_MOUNT_MODE,
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_GROUP, ANN_IDEMPOTENCY,
+                                         ANN_MOUNT_MODE,
                                          ANN_OWNER_NAME, ANN_OWNER_UID, LABEL_APP,
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          MODE_STANDBY)
@@ -171,7 +172,8 @@ class WarmPool:
 
     # ------------------------------------------------------------------------ claim / return
     async def claim(self, owner: dict, n: int, entire: bool, attached: Sequence[AmdGpu],
-                    attach_id: str = "", container: str = "") -> Optional[Reservation]:
+                    attach_id: str = "", container: str = "",
+                    idempotency_key: str = "") -> Optional[Reservation]:
         """Claim ``n`` standby GPUs for ``owner``; None if the pool cannot cover the request."""
         async with self._lock:
             pool = self.standby()
@@ -198,6 +200,7 @@ class WarmPool:
                 "annotations": {ANN_OWNER_UID: podu.uid_of(owner),
                                 ANN_OWNER_NAME: podu.name_of(owner), ANN_MOUNT_MODE: mode,
                                 ANN_ATTACH_ID: attach_id, ANN_CONTAINER: container,
+                                ANN_IDEMPOTENCY: idempotency_key or None,
                                 ANN_GROUP: group or None}}}
             for ph in chosen:
                 self._claimed.add(ph.uid)
@@ -227,7 +230,7 @@ class WarmPool:
             "labels": {LABEL_OWNER: None, LABEL_OWNER_NS: None},
             "annotations": {ANN_OWNER_UID: None, ANN_OWNER_NAME: None,
                             ANN_MOUNT_MODE: MODE_STANDBY, ANN_ATTACH_ID: None,
-                            ANN_CONTAINER: None, ANN_GROUP: None}}}
+                            ANN_CONTAINER: None, ANN_GROUP: None, ANN_IDEMPOTENCY: None}}}
         res = await asyncio.gather(*[self.ph.kube.patch_pod(p.namespace, p.name, patch)
                                      for p in phs], return_exceptions=True)
         back = []

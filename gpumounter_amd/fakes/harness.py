@@ -48,7 +48,8 @@ class LocalCluster:
                  alloc_policy: str = "topology", device_id_kind: str = "bdf",
                  devnode_mode: str = "emulate", reconcile_period_s: float = 0.0,
                  start_master: bool = True, worker_overrides: Optional[dict] = None,
-                 node_gpu_bdfs: Optional[List[str]] = None) -> None:
+                 node_gpu_bdfs: Optional[List[str]] = None,
+                 master_overrides: Optional[dict] = None) -> None:
         self.n_nodes = n_nodes
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
@@ -64,6 +65,7 @@ class LocalCluster:
         self.reconcile_period_s = reconcile_period_s
         self.start_master = start_master
         self.worker_overrides = worker_overrides or {}
+        self.master_overrides = master_overrides or {}
         self.node_gpu_bdfs = [b.lower() for b in node_gpu_bdfs] if node_gpu_bdfs else None
         self.nodes: Dict[str, NodeHandle] = {}
         self.master: Optional[Master] = None
@@ -87,7 +89,7 @@ class LocalCluster:
             await self._add_node(f"node-{i}")
         if self.start_master:
             mcfg = Config.load(env={}, kube_api=self.api_url, master_host="127.0.0.1",
-                               log_json=False)
+                               log_json=False, **self.master_overrides)
             self.master = Master(mcfg)
             await self.master.start(port=0)
             self.master_url = f"http://127.0.0.1:{self.master.port}"
@@ -125,7 +127,8 @@ class LocalCluster:
                           container_root_prefix=h.node.rootfs_root, amdsmi_lib=self.amdsmi_lib,
                           worker_host="127.0.0.1", worker_port=1, metrics_port=0,
                           placeholder_namespace_mode=self.placeholder_namespace_mode,
-                          reconcile_period_s=self.reconcile_period_s, log_json=False, **ov)
+                          reconcile_period_s=self.reconcile_period_s, log_json=False,
+                          metrics_period_s=ov.pop("metrics_period_s", 0), **ov)
         w = Worker(cfg, inventory=self.inventory)
         await w.start(grpc_port=0, http_port=0, reconcile=self.reconcile_period_s > 0)
         h.worker, h.cfg = w, cfg

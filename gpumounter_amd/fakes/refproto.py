@@ -43,19 +43,18 @@ from gpumounter_amd.utils import trace
 class RefMaster(Master):
     """Master with the reference's per-request worker discovery and dialing."""
 
-    async def _locate(self, request, route, ns, name, fresh=False):
+    async def _locate(self, ns, name, fresh=False):
         try:
             pod = await self.kube.get_pod(ns, name)
         except NotFound:
-            return None, None, self._reply(request, route, 404,
-                                           f"No pod: {name} in namespace: {ns}", {}), False
+            return None, None, (404, f"No pod: {name} in namespace: {ns}", {}), False
         items, _ = await self.kube.list_pods(self.cfg.worker_namespace, self.cfg.worker_label)
         node = podu.node_of(pod)
         for w in items:
             if podu.node_of(w) == node:
                 port = (w["metadata"].get("annotations") or {}).get(ANN_WORKER_PORT, "1200")
                 return pod, f"{w['status']['podIP']}:{port}", None, False
-        return pod, None, self._reply(request, route, 500, "Service Internal Error", {}), False
+        return pod, None, (500, "Service Internal Error", {}), False
 
     class _OneShot:
         def __init__(self, target):

@@ -67,9 +67,11 @@ def _text(body: str, status: int = 200) -> web.Response:
 class WorkerDirectory:
     """node name → worker gRPC target, from a watch on the worker DaemonSet pods."""
 
-    def __init__(self, kube: KubeClient, namespace: str, label: str, default_port: int) -> None:
+    def __init__(self, kube: KubeClient, namespace: str, label: str, default_port: int,
+                 cfg=None) -> None:
         self.informer = PodInformer(kube, namespace, label)
         self.default_port = default_port
+        self.cfg = cfg
         self._channels: Dict[str, grpc.aio.Channel] = {}
         self._loop = None
 
@@ -102,8 +104,20 @@ class WorkerDirectory:
             self._loop = loop
         ch = self._channels.get(target)
         if ch is None:
-            ch = grpc.aio.insecure_channel(target, options=[
-                ("grpc.keepalive_time_ms", 30000), ("grpc.enable_retries", 1)])
+            opts = [("grpc.keepalive_time_ms", 30000), ("grpc.enable_retries", 1)]
+            cfg = self.cfg
+            if cfg is not None and cfg.tls_ca:
+                def rd(p):
+                    with open(p, "rb") as fh:
+                        return fh.read()
+                creds = grpc.ssl_channel_credentials(
+                    root_certificates=rd(cfg.tls_ca),
+                    private_key=rd(cfg.tls_key) if cfg.tls_key else None,
+                    certificate_chain=rd(cfg.tls_cert) if cfg.tls_cert else None)
+                opts.append(("grpc.ssl_target_name_override", cfg.tls_server_name))
+                ch = grpc.aio.secure_channel(target, creds, options=opts)
+            else:
+                ch = grpc.aio.insecure_channel(target, options=opts)
             self._channels[target] = ch
         return ch
 
@@ -116,7 +130,7 @@ class Master:
         self.cfg = cfg
         self.kube = kube or KubeClient.from_config(cfg)
         self.workers = WorkerDirectory(self.kube, cfg.worker_namespace, cfg.worker_label,
-                                       cfg.worker_port)
+                                       cfg.worker_port, cfg)
         self.metrics = Metrics()
         self.runner: Optional[web.AppRunner] = None
         self.port = 0
@@ -130,6 +144,7 @@ class Master:
         r.add_get("/addgpu/namespace/{namespace}/pod/{pod}/gpu/{gpuNum}/isEntireMount/"
                   "{isEntireMount}", self.add_gpu)
         r.add_post("/removegpu/namespace/{namespace}/pod/{pod}/force/{force}", self.remove_gpu)
+        r.add_post("/api/v1/batch", self.batch)
         r.add_get("/api/v1/namespaces/{namespace}/pods/{pod}/gpus", self.pod_gpus)
         r.add_get("/api/v1/nodes/{node}/gpus", self.node_gpus)
         r.add_get("/healthz", self.healthz)
@@ -188,10 +203,10 @@ class Master:
             return web.json_response(payload, status=status)
         return _text(text, status)
 
-    async def _locate(self, request, route: str, ns: str, name: str, fresh: bool = False
-                      ) -> Tuple[Optional[dict], Optional[str], Optional[web.Response], bool]:
-        """Pod → node → worker target. Recently seen pods are served from a small cache (a pod
-        never changes node); a stale entry is detected by the worker and retried fresh."""
+    async def _locate(self, ns: str, name: str, fresh: bool = False):
+        """Pod → node → worker target. Returns (pod, target, error, cached) where error is a
+        (status, text, payload) triple. Recently seen pods come from a small cache (a pod never
+        changes node); a stale entry is detected by the worker and retried fresh."""
         key = (ns, name)
         hit = None if fresh else self._pod_nodes.get(key)
         now = time.monotonic()
@@ -204,10 +219,9 @@ class Master:
                 pod = await self.kube.get_pod(ns, name)
             except NotFound:
                 self._pod_nodes.pop(key, None)
-                return None, None, self._reply(request, route, 404,
-                                               f"No pod: {name} in namespace: {ns}", {}), False
+                return None, None, (404, f"No pod: {name} in namespace: {ns}", {}), False
             except ApiError as e:
-                return None, None, self._reply(request, route, 500, str(e), {}), False
+                return None, None, (500, str(e), {}), False
             cached = False
             if podu.node_of(pod):
                 self._pod_nodes[key] = (podu.node_of(pod), podu.uid_of(pod), now)
@@ -217,10 +231,88 @@ class Master:
         target = self.workers.target(node)
         if target is None:
             _log.error("no gpu mounter worker on node %r", node)
-            return pod, None, self._reply(request, route, 500, "Service Internal Error",
-                                          {"error": f"no worker on node {node!r}"}), cached
+            return pod, None, (500, "Service Internal Error",
+                               {"error": f"no worker on node {node!r}"}), cached
         return pod, target, None, cached
 
+    # ------------------------------------------------------------------------ operations
+    async def _add(self, ns: str, name: str, n: int, entire: bool, container: str = "",
+                   rid: str = "", key: str = ""):
+        """AddGPU through the pod's worker → (status, text, payload) as the reference maps it
+        (reference main.go:103-116)."""
+        t0 = time.perf_counter()
+        for fresh in (False, True):
+            pod, target, err, cached = await self._locate(ns, name, fresh)
+            if err is not None:
+                return err
+            stub = self.workers.channel(target).unary_unary(
+                api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
+                response_deserializer=api.AddGPUResponse.FromString)
+            try:
+                resp = await stub(api.AddGPURequest(
+                    pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
+                    request_id=rid, container=container, idempotency_key=key),
+                    timeout=self.cfg.rpc_timeout_s)
+            except grpc.aio.AioRpcError as e:
+                if cached and e.code() == grpc.StatusCode.FAILED_PRECONDITION and \
+                        "this worker serves" in (e.details() or ""):
+                    self._pod_nodes.pop((ns, name), None)   # pod was recreated elsewhere
+                    continue
+                _log.error("AddGPU rpc to %s failed: %s %s", target, e.code().name, e.details())
+                code = 400 if e.code() == grpc.StatusCode.INVALID_ARGUMENT else 500
+                body = "Service Internal Error" if code == 500 else e.details()
+                return code, body, {"error": e.details()}
+            if cached and resp.add_gpu_result == api.ADD_POD_NOT_FOUND:
+                self._pod_nodes.pop((ns, name), None)       # re-check with a fresh GET (→ 404)
+                continue
+            break
+        payload = self._payload(resp, t0)
+        node = podu.node_of(pod)
+        if resp.add_gpu_result == api.ADD_SUCCESS:
+            return 200, "Add GPU Success", payload
+        if resp.add_gpu_result == api.ADD_INSUFFICIENT:
+            return 500, f"Insufficient GPU on Node: {node}", payload
+        if resp.add_gpu_result == api.ADD_POD_NOT_FOUND:
+            return 400, f"No Pod{name} on Node: {node}", payload
+        return 500, "Service Internal Error", payload
+
+    async def _remove(self, ns: str, name: str, uuids, force: bool, container: str = "",
+                      rid: str = ""):
+        """RemoveGPU through the pod's worker (reference main.go:206-224 mapping)."""
+        t0 = time.perf_counter()
+        for fresh in (False, True):
+            pod, target, err, cached = await self._locate(ns, name, fresh)
+            if err is not None:
+                return err
+            stub = self.workers.channel(target).unary_unary(
+                api.REMOVE_GPU, request_serializer=api.RemoveGPURequest.SerializeToString,
+                response_deserializer=api.RemoveGPUResponse.FromString)
+            try:
+                resp = await stub(api.RemoveGPURequest(
+                    pod_name=name, namespace=ns, uuids=uuids, force=force, request_id=rid,
+                    container=container), timeout=self.cfg.rpc_timeout_s)
+            except grpc.aio.AioRpcError as e:
+                _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name,
+                           e.details())
+                return 500, "Service Internal Error", {"error": e.details()}
+            if cached and resp.remove_gpu_result == api.REMOVE_POD_NOT_FOUND:
+                self._pod_nodes.pop((ns, name), None)
+                continue
+            break
+        payload = self._payload(resp, t0)
+        node = podu.node_of(pod)
+        r = resp.remove_gpu_result
+        if r == api.REMOVE_SUCCESS:
+            return 200, "Remove GPU Success", payload
+        if r == api.REMOVE_POD_NOT_FOUND:
+            return 400, f"No Pod{name} on Node: {node}", payload
+        if r == api.REMOVE_BUSY:
+            return 400, f"Pod: {name} has running processes on GPU: {', '.join(uuids)}", payload
+        if r == api.REMOVE_GPU_NOT_FOUND:
+            return 400, f"Invalid UUIDs: {', '.join(uuids)}", payload
+        return 500, "Service Internal Error", payload
+
+    # ------------------------------------------------------------------------ HTTP routes
     async def add_gpu(self, request: web.Request) -> web.Response:
         route = "addgpu"
         denied = self._unauthorized(request, route)
@@ -240,41 +332,10 @@ class Master:
         if n <= 0:
             # the reference forwarded 0 and the worker divided by zero (SURVEY defect 6)
             return self._reply(request, route, 400, f"Invalid param gpuNum: {mi['gpuNum']}", {})
-        t0 = time.perf_counter()
-        for fresh in (False, True):
-            pod, target, err, cached = await self._locate(request, route, ns, name, fresh)
-            if err is not None:
-                return err
-            stub = self.workers.channel(target).unary_unary(
-                api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
-                response_deserializer=api.AddGPUResponse.FromString)
-            try:
-                resp = await stub(api.AddGPURequest(
-                    pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
-                    request_id=rid, container=request.query.get("container", "")),
-                    timeout=self.cfg.rpc_timeout_s)
-            except grpc.aio.AioRpcError as e:
-                if cached and e.code() == grpc.StatusCode.FAILED_PRECONDITION and \
-                        "this worker serves" in (e.details() or ""):
-                    self._pod_nodes.pop((ns, name), None)   # pod was recreated elsewhere
-                    continue
-                _log.error("AddGPU rpc to %s failed: %s %s", target, e.code().name, e.details())
-                code = 400 if e.code() == grpc.StatusCode.INVALID_ARGUMENT else 500
-                body = "Service Internal Error" if code == 500 else e.details()
-                return self._reply(request, route, code, body, {"error": e.details()})
-            if cached and resp.add_gpu_result == api.ADD_POD_NOT_FOUND:
-                self._pod_nodes.pop((ns, name), None)       # re-check with a fresh GET (→ 404)
-                continue
-            break
-        payload = self._payload(resp, t0)
-        node = podu.node_of(pod)
-        if resp.add_gpu_result == api.ADD_SUCCESS:
-            return self._reply(request, route, 200, "Add GPU Success", payload)
-        if resp.add_gpu_result == api.ADD_INSUFFICIENT:
-            return self._reply(request, route, 500, f"Insufficient GPU on Node: {node}", payload)
-        if resp.add_gpu_result == api.ADD_POD_NOT_FOUND:
-            return self._reply(request, route, 400, f"No Pod{name} on Node: {node}", payload)
-        return self._reply(request, route, 500, "Service Internal Error", payload)
+        status, text, payload = await self._add(
+            ns, name, n, entire, request.query.get("container", ""), rid,
+            request.headers.get("Idempotency-Key", ""))
+        return self._reply(request, route, status, text, payload)
 
     async def remove_gpu(self, request: web.Request) -> web.Response:
         route = "removegpu"
@@ -296,42 +357,56 @@ class Master:
             return self._reply(request, route, 400,
                                f"Invalid parameter force: {mi['force']}(should be true or false)",
                                {})
-        t0 = time.perf_counter()
-        for fresh in (False, True):
-            pod, target, err, cached = await self._locate(request, route, ns, name, fresh)
-            if err is not None:
-                return err
-            stub = self.workers.channel(target).unary_unary(
-                api.REMOVE_GPU, request_serializer=api.RemoveGPURequest.SerializeToString,
-                response_deserializer=api.RemoveGPUResponse.FromString)
+        status, text, payload = await self._remove(ns, name, uuids, force,
+                                                   request.query.get("container", ""), rid)
+        return self._reply(request, route, status, text, payload)
+
+    async def batch(self, request: web.Request) -> web.Response:
+        """``POST /api/v1/batch`` {"operations": [{"op": "add", "namespace", "pod", "gpus",
+        "entire", "container", "idempotency_key"} | {"op": "remove", "namespace", "pod",
+        "uuids", "force", "container"}]} → results in order; operations run concurrently
+        (operations on one pod still serialize on the worker's per-pod lock)."""
+        route = "batch"
+        denied = self._unauthorized(request, route)
+        if denied is not None:
+            return denied
+        try:
+            body = await request.json()
+            ops = body["operations"]
+            assert isinstance(ops, list)
+        except Exception:  # noqa: BLE001
+            return web.json_response({"error": "body must be {\"operations\": [...]}"},
+                                     status=400)
+
+        async def one(op):
             try:
-                resp = await stub(api.RemoveGPURequest(
-                    pod_name=name, namespace=ns, uuids=uuids, force=force, request_id=rid,
-                    container=request.query.get("container", "")),
-                    timeout=self.cfg.rpc_timeout_s)
-            except grpc.aio.AioRpcError as e:
-                _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name,
-                           e.details())
-                return self._reply(request, route, 500, "Service Internal Error",
-                                   {"error": e.details()})
-            if cached and resp.remove_gpu_result == api.REMOVE_POD_NOT_FOUND:
-                self._pod_nodes.pop((ns, name), None)
-                continue
-            break
-        payload = self._payload(resp, t0)
-        node = podu.node_of(pod)
-        r = resp.remove_gpu_result
-        if r == api.REMOVE_SUCCESS:
-            return self._reply(request, route, 200, "Remove GPU Success", payload)
-        if r == api.REMOVE_POD_NOT_FOUND:
-            return self._reply(request, route, 400, f"No Pod{name} on Node: {node}", payload)
-        if r == api.REMOVE_BUSY:
-            return self._reply(request, route, 400,
-                               f"Pod: {name} has running processes on GPU: {', '.join(uuids)}",
-                               payload)
-        if r == api.REMOVE_GPU_NOT_FOUND:
-            return self._reply(request, route, 400, f"Invalid UUIDs: {', '.join(uuids)}", payload)
-        return self._reply(request, route, 500, "Service Internal Error", payload)
+                kind = op["op"]
+                ns, name = op.get("namespace", "default"), op["pod"]
+                if kind == "add":
+                    n = int(op["gpus"])
+                    if n <= 0:
+                        return 400, f"Invalid param gpuNum: {n}", {}
+                    return await self._add(ns, name, n, bool(op.get("entire", False)),
+                                           op.get("container", ""), log.new_request_id("add"),
+                                           op.get("idempotency_key", ""))
+                if kind == "remove":
+                    uuids = list(op["uuids"])
+                    if not uuids:
+                        return 400, "Invalid parameter", {}
+                    return await self._remove(ns, name, uuids, bool(op.get("force", False)),
+                                              op.get("container", ""), log.new_request_id("rm"))
+                return 400, f"unknown op {kind!r}", {}
+            except (KeyError, TypeError, ValueError) as e:
+                return 400, f"bad operation: {e}", {}
+
+        results = await asyncio.gather(*[one(op) for op in ops])
+        out = []
+        for status, text, payload in results:
+            d = dict(payload)
+            d.update(code=status, message=text)
+            out.append(d)
+            self.metrics.http_requests.labels(route=route, code=str(status)).inc()
+        return web.json_response({"results": out})
 
     @staticmethod
     def _payload(resp, t0: float) -> dict:

@@ -39,6 +39,7 @@ ANN_CONTAINER = "gpumounter.amd.com/container"
 ANN_DEVICES = "gpumounter.amd.com/devices"
 ANN_STATE = "gpumounter.amd.com/state"      # reserved | attached | detaching
 ANN_OWNER_NAME = "gpumounter.amd.com/owner-name"
+ANN_IDEMPOTENCY = "gpumounter.amd.com/idempotency-key"
 ANN_GROUP = "gpumounter.amd.com/group"      # entire-mount group made of pooled placeholders
 MODE_STANDBY = "standby"
 FINALIZER = "gpumounter.amd.com/release"

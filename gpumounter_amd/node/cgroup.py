@@ -45,8 +45,10 @@ def _esc(s: str) -> str:
 
 
 class CgroupResolver:
-    def __init__(self, root: str = "/sys/fs/cgroup", mode: str = "auto", driver: str = "auto"):
+    def __init__(self, root: str = "/sys/fs/cgroup", mode: str = "auto", driver: str = "auto",
+                 proc_root: str = "/proc"):
         self.root = root
+        self.proc_root = proc_root
         self.mode = self.detect_mode(root) if mode == "auto" else mode
         self.base = os.path.join(root, "devices") if self.mode == "v1" else root
         self.driver = driver
@@ -105,9 +107,39 @@ class CgroupResolver:
                 if os.path.isdir(cand):
                     self._cache[key] = cand
                     return cand
+        found = self._from_proc(ctr.id)
+        if found:
+            self._cache[key] = found
+            return found
         raise CgroupError(f"cgroup of container {ctr.name} ({ctr.id[:12]}) of pod "
                           f"{pod['metadata'].get('namespace')}/{pod['metadata'].get('name')} "
                           f"not found under {self.base}")
+
+    def _from_proc(self, container_id: str) -> Optional[str]:
+        """Last resort, runtime- and driver-agnostic: any process whose /proc/<pid>/cgroup names
+        the container id tells us its cgroup path (v2 line ``0::/…``, v1 ``N:devices:/…``)."""
+        try:
+            pids = [d for d in os.listdir(self.proc_root) if d.isdigit()]
+        except OSError:
+            return None
+        want_ctrl = "devices" if self.mode == "v1" else ""
+        for pid in pids:
+            try:
+                with open(os.path.join(self.proc_root, pid, "cgroup")) as fh:
+                    lines = fh.read().splitlines()
+            except OSError:
+                continue
+            for line in lines:
+                parts = line.split(":", 2)
+                if len(parts) != 3 or container_id not in parts[2]:
+                    continue
+                ctrls = parts[1].split(",") if parts[1] else [""]
+                if want_ctrl not in ctrls:
+                    continue
+                cand = os.path.join(self.base, parts[2].lstrip("/"))
+                if os.path.isdir(cand):
+                    return cand
+        return None
 
     def forget(self, pod_uid: str) -> None:
         for k in [k for k in self._cache if k[0] == pod_uid]:

@@ -81,6 +81,13 @@ class Config:
     reconcile_period_s: float = 30.0
     watch_resync_s: float = 300.0
     api_token: str = ""                # if set, add/remove require "Authorization: Bearer <token>"
+    # master⇄worker gRPC TLS (reference: insecure, main.go:82). cert+key on the worker enable TLS;
+    # a CA on the worker requires client certs (mTLS). The master uses the same three files.
+    tls_cert: str = ""
+    tls_key: str = ""
+    tls_ca: str = ""
+    tls_server_name: str = "gpu-mounter-worker"  # SAN the worker certificate carries
+    metrics_period_s: float = 15.0
     # --- observability ---------------------------------------------------------------------
     log_level: str = "INFO"
     log_file: str = ""

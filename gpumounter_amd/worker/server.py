@@ -40,6 +40,11 @@ def _ser(m) -> bytes:
     return m.SerializeToString()
 
 
+def _read(path: str) -> bytes:
+    with open(path, "rb") as fh:
+        return fh.read()
+
+
 class Worker:
     def __init__(self, cfg, kube: Optional[KubeClient] = None,
                  inventory: Optional[Inventory] = None) -> None:
@@ -51,7 +56,8 @@ class Worker:
         self.metrics = Metrics()
         self.ledger = LedgerClient(cfg.kubelet_socket, cfg.resource_name, cfg.kubelet_timeout_s,
                                    cfg.podresources_api)
-        self.resolver = CgroupResolver(cfg.cgroup_root, cfg.cgroup_mode, cfg.cgroup_driver)
+        self.resolver = CgroupResolver(cfg.cgroup_root, cfg.cgroup_mode, cfg.cgroup_driver,
+                                       cfg.proc_root)
         emulate = cfg.devnode_mode == "emulate" or os.environ.get("GM_BPF_EMULATE") == "1"
         self.backend = make_backend(self.resolver.mode, emulate, cfg.bpf_pin_dir)
         self.writer = DevNodeWriter(cfg.devnode_mode)
@@ -122,7 +128,15 @@ class Worker:
         self.grpc_server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])
         self.grpc_server.add_generic_rpc_handlers(self.handlers())
         port = self.cfg.worker_port if grpc_port is None else grpc_port
-        self.grpc_port = self.grpc_server.add_insecure_port(f"{self.cfg.worker_host}:{port}")
+        addr = f"{self.cfg.worker_host}:{port}"
+        if self.cfg.tls_cert and self.cfg.tls_key:
+            creds = grpc.ssl_server_credentials(
+                [(_read(self.cfg.tls_key), _read(self.cfg.tls_cert))],
+                root_certificates=_read(self.cfg.tls_ca) if self.cfg.tls_ca else None,
+                require_client_auth=bool(self.cfg.tls_ca))
+            self.grpc_port = self.grpc_server.add_secure_port(addr, creds)
+        else:
+            self.grpc_port = self.grpc_server.add_insecure_port(addr)
         if self.grpc_port == 0:
             raise OSError(f"cannot bind gRPC {self.cfg.worker_host}:{port}")
         await self.grpc_server.start()
@@ -141,6 +155,8 @@ class Worker:
         if reconcile and self.cfg.reconcile_period_s > 0:
             await self.reconciler.start()
         await self.pool.start()
+        if self.cfg.metrics_period_s > 0:
+            self._collector = asyncio.ensure_future(self._collect_loop())
         self.ready = True
         _log.info("worker %s serving gRPC :%d http :%d (cgroup %s/%s, devnodes %s, ledger %s)",
                   self.cfg.node_name, self.grpc_port, self.http_port, self.resolver.mode,
@@ -160,8 +176,30 @@ class Worker:
         st = await self.service.node_status(request.query.get("processes") == "1")
         return web.json_response(st)
 
+    async def _collect_loop(self) -> None:
+        """Per-GPU process gauges + ledger state gauges."""
+        while True:
+            try:
+                await self.collect_metrics()
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                _log.debug("metrics collection failed: %s", e)
+            await asyncio.sleep(self.cfg.metrics_period_s)
+
+    async def collect_metrics(self) -> None:
+        for g in self.inv.gpus():
+            try:
+                n = len(self.inv.processes(g.index))
+            except Exception:  # noqa: BLE001 - not supported / no permission
+                continue
+            self.metrics.gpu_busy.labels(gpu=g.bdf).set(n)
+        await self.service.node_status(False)  # refreshes gm_ledger_gpus{state}
+
     async def stop(self) -> None:
         self.ready = False
+        if getattr(self, "_collector", None) is not None:
+            self._collector.cancel()
         await self.pool.stop()
         await self.reconciler.stop()
         if self.grpc_server is not None:

@@ -34,7 +34,7 @@ from gpumounter_amd.hw import topology
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu, gpus_by_key, normalize_device_id
-from gpumounter_amd.models.types import ERR_INTERNAL, ERR_POLICY, MountType
+from gpumounter_amd.models.types import ANN_IDEMPOTENCY, ERR_INTERNAL, ERR_POLICY, MountType
 from gpumounter_amd.node import procs
 from gpumounter_amd.node.hotmount import HotMount, MountError
 from gpumounter_amd.node.ledger import LedgerClient, LedgerError
@@ -259,6 +259,10 @@ class GpuMountService:
                                    f"pod phase is {podu.phase_of(pod)}, not Running")
             with trace.span("ledger_read"):
                 st = await self.pod_state(pod)
+            if req.idempotency_key:
+                replay = self._replay(pod, st, req.idempotency_key)
+                if replay is not None:
+                    return replay
             ok, why = can_mount(st.mount_type, req.is_entire_mount)
             if not ok:
                 _log.warning("policy denied add on %s/%s: %s", req.namespace, req.pod_name, why)
@@ -298,6 +302,28 @@ class GpuMountService:
                                       devices=self._devices(new, owner),
                                       message="Add GPU Success")
 
+    def _replay(self, pod: dict, st: PodGpuState, key: str):
+        """A retried request (same idempotency key) returns the earlier attach instead of adding
+        more GPUs; the mount itself is re-checked (repair) so a half-finished attempt completes."""
+        mine = {p["metadata"]["name"] for p in self.ph.owned_by(pod)
+                if (p["metadata"].get("annotations") or {}).get(ANN_IDEMPOTENCY) == key}
+        if not mine:
+            return None
+        gs, owner = [], {}
+        for ph in st.placeholders:
+            if ph.name in mine:
+                for g in st.by_placeholder[(ph.namespace, ph.name)]:
+                    gs.append(g)
+                    owner[g.index] = ph.name
+        issues = self.hm.audit(pod, st.hot, st.own)
+        missing = [i for i in issues if i.kind.startswith("missing")]
+        if missing:
+            self.hm.repair(pod, missing, st.hot, st.own)
+        log.kv(_log, 20, "idempotent replay", key=key, gpus=[g.bdf for g in gs])
+        return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS,
+                                  devices=self._devices(gs, owner),
+                                  message="Add GPU Success (replayed)")
+
     async def _reserve(self, pod: dict, n: int, req, st: PodGpuState, preferred: List[str]):
         """Claim from the warm pool first (if enabled), create placeholders for the rest."""
         claimed = None
@@ -305,7 +331,8 @@ class GpuMountService:
             k = min(n, len(self.pool.standby()))
             if k:
                 claimed = await self.pool.claim(pod, k, req.is_entire_mount, st.hot + st.own,
-                                                log.request_id.get(), req.container)
+                                                log.request_id.get(), req.container,
+                                                req.idempotency_key)
         got = len(claimed.placeholders) if claimed else 0
         if got == n:
             return claimed
@@ -313,7 +340,8 @@ class GpuMountService:
             rest = await self.ph.reserve(pod, n - got, req.is_entire_mount,
                                          preferred if not got else [],
                                          attach_id=log.request_id.get(),
-                                         container=req.container)
+                                         container=req.container,
+                                         idempotency_key=req.idempotency_key)
         except BaseException:
             if claimed:
                 await self.pool.give_back(claimed.placeholders)

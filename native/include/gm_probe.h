@@ -33,6 +33,12 @@ int gm_probe_find_device(const char* bdf, int* dev);
 int gm_probe_quick(int dev, int* ok, double* elapsed_us);
 // HBM3E stream: float4 copy of `bytes` for `iters`; *gbps = (read+write) bytes / time.
 int gm_probe_hbm_copy(int dev, uint64_t bytes, int iters, double* gbps);
+// Tuning variants: variant 0 grid-stride, 1 chunked 4×16B/lane, 2 chunked + nontemporal.
+int gm_probe_hbm_copy_variant(int dev, int variant, uint64_t bytes, int iters,
+                              int blocks_per_cu, double* gbps);
+// shape16=1: v_mfma_f32_16x16x32_bf16, 0: v_mfma_f32_32x32x16_bf16.
+int gm_probe_mfma_peak_variant(int dev, int shape16, int iters, int blocks_per_cu,
+                               double* tflops);
 // MFMA bf16 (v_mfma_f32_32x32x16_bf16) register-resident peak; *tflops dense.
 int gm_probe_mfma_peak(int dev, int iters, double* tflops);
 // C[M,N] (fp32) = A[M,K] (bf16, row-major) · B[K,N] (bf16, row-major) on MFMA.

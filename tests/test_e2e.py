@@ -449,3 +449,44 @@ def test_master_pod_cache_revalidates_recreated_and_deleted_pods():
         code, text = await lc.add("default", "p", 1, accept_json=False)
         assert (code, text) == (404, "No pod: p in namespace: default\n")
     run(body, n_nodes=2)
+
+
+def test_idempotency_key_replays_instead_of_adding_more():
+    async def body(lc):
+        lc.tenant("i")
+        url = lc.master_url + "/addgpu/namespace/default/pod/i/gpu/2/isEntireMount/false"
+        hdr = {"Idempotency-Key": "job-42-attach", "Accept": "application/json"}
+        async with lc.session.get(url, headers=hdr) as r:
+            first = await r.json()
+        async with lc.session.get(url, headers=hdr) as r:          # client retry
+            again = await r.json()
+        assert r.status == 200 and "replayed" in again["detail"]
+        assert sorted(d["uuid"] for d in again["devices"]) == \
+            sorted(d["uuid"] for d in first["devices"])
+        assert len(lc.cluster.placeholders()) == 2                  # not 4
+        assert not await lc.audit("default", "i")
+    run(body)
+
+
+def test_batch_endpoint_runs_operations_concurrently():
+    async def body(lc):
+        for t in ("b1", "b2", "b3"):
+            lc.tenant(t)
+        ops = {"operations": [{"op": "add", "pod": "b1", "gpus": 2},
+                              {"op": "add", "pod": "b2", "gpus": 3, "entire": True},
+                              {"op": "add", "pod": "b3", "gpus": 4},
+                              {"op": "add", "pod": "ghost", "gpus": 1},
+                              {"op": "frobnicate", "pod": "b1"}]}
+        async with lc.session.post(lc.master_url + "/api/v1/batch", json=ops) as r:
+            res = (await r.json())["results"]
+        assert [x["code"] for x in res[:3]].count(200) >= 2     # 2+3+4 = 9 > 8: one must fail
+        assert res[3]["code"] == 404 and res[4]["code"] == 400
+        held = sum(len(x.get("devices", [])) for x in res[:3] if x["code"] == 200)
+        assert held == len(lc.nodes["node-0"].node.allocated) <= 8
+        rm = {"operations": [{"op": "remove", "pod": f"b{i + 1}",
+                              "uuids": [d["uuid"] for d in x["devices"]]}
+                             for i, x in enumerate(res[:3]) if x["code"] == 200]}
+        async with lc.session.post(lc.master_url + "/api/v1/batch", json=rm) as r:
+            assert all(x["code"] == 200 for x in (await r.json())["results"])
+        assert lc.nodes["node-0"].node.allocated == {}
+    run(body)

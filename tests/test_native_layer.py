@@ -172,6 +172,22 @@ def test_cgroup_resolution_matrix(tmp_path, mode, driver, runtime, qos, mock_inv
         assert d.endswith(".scope")
 
 
+def test_cgroup_resolution_via_proc_fallback(tmp_path):
+    """Unknown kubelet layout: the container's cgroup is found through /proc/<pid>/cgroup."""
+    root = tmp_path / "cg"
+    odd = root / "custom.slice" / "my-runtime-abc123def.scope"
+    odd.mkdir(parents=True)
+    (root / "cgroup.controllers").write_text("cpu io memory\n")
+    proc = tmp_path / "proc"
+    (proc / "4242").mkdir(parents=True)
+    (proc / "4242" / "cgroup").write_text("0::/custom.slice/my-runtime-abc123def.scope\n")
+    (proc / "self").mkdir()
+    r = CgroupResolver(str(root), proc_root=str(proc))
+    assert r.mode == "v2"
+    d = r.container_dir(_pod(), ContainerRef("c", "containerd", "abc123def", True))
+    assert d == str(odd)
+
+
 def test_cgroup_resolution_missing_raises(tmp_path, mock_inventory):
     FakeNode("n", str(tmp_path), mock_inventory.gpus())
     r = CgroupResolver(os.path.join(str(tmp_path), "cgroup"))
