@@ -51,6 +51,9 @@ def main() -> int:
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0,
                     help="standby placeholders per node (claim instead of create); 0 = off")
+    ap.add_argument("--placement", choices=("hint", "trim"), default="hint",
+                    help="trim = enforce the topology choice by holding every free GPU and "
+                         "releasing the surplus (placement_enforce)")
     ap.add_argument("--protocol", choices=("gpumounter", "reference"), default="gpumounter",
                     help="'reference' re-enacts the reference's call sequence on the same "
                          "cluster (emulated baseline, see gpumounter_amd/fakes/refproto.py)")
@@ -99,7 +102,8 @@ def main() -> int:
         lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
         tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
                              node_gpu_bdfs=node_bdfs,
-                             worker_overrides={"warm_pool_size": args.warm_pool})
+                             worker_overrides={"warm_pool_size": args.warm_pool,
+                                               "placement_enforce": args.placement})
         lc = tc.start()
         if args.warm_pool:
             pool = lc.nodes["node-0"].worker.pool
@@ -234,7 +238,7 @@ def main() -> int:
                     "cgroup": args.cgroup,
                     "protocol": args.protocol if args.protocol == "gpumounter"
                     else "reference (emulated)",
-                    "warm_pool": args.warm_pool,
+                    "warm_pool": args.warm_pool, "placement": args.placement,
                 },
                 "attach_p99_ms": round(pct(attach_ms, 0.99), 4),
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),

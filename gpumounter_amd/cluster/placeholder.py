@@ -22,19 +22,21 @@ Unschedulable → InsufficientGPU mapping. Changed:
   ≥1.20 treats it as absent and deletes the placeholder — defect 4) and the reconciler collects
   placeholders whose owner is gone;
 * the preferred (xGMI/NUMA-aware) device set is attached as an annotation for
-  GetPreferredAllocation-capable device plugins, and any deviation is counted.
+  GetPreferredAllocation-capable device plugins, and any deviation is counted;
+* ``reserve_trim`` enforces the placement whatever the device plugin picks: every free GPU is
+  held by a 1-GPU placeholder at once, the topology-chosen subset is kept, the rest released.
 """
 from __future__ import annotations
 
 import asyncio
 import secrets
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_IDEMPOTENCY,
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_GROUP, ANN_IDEMPOTENCY,
                                          ANN_MOUNT_MODE, ANN_OWNER_UID, ANN_PREFERRED, LABEL_APP,
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          SLAVE_SUFFIX)
@@ -194,13 +196,67 @@ class PlaceholderManager:
             if len(preferred) == total else [[] for _ in range(k)]
         bodies = [self.build(owner, per_pod, mode, prefs[i], attach_id, container,
                              idempotency_key) for i in range(k)]
-        with trace.span("ledger_reserve", placeholders=k):
+        created = await self._create(bodies)
+        try:
+            with trace.span("placeholder_wait"):
+                self.faults.check("placeholder_wait")
+                await self._await_admission(created, self.cfg.attach_timeout_s)
+                self.faults.check("placeholder_wait", "after")
+        except BaseException:
+            await self.release(created, wait=False)
+            raise
+        return Reservation(created)
+
+    async def reserve_trim(self, owner: dict, total: int, entire: bool, width: int,
+                           pick: Callable[[List[str]], Sequence[str]], attach_id: str = "",
+                           container: str = "", idempotency_key: str = ""
+                           ) -> Tuple[Reservation, List[Placeholder]]:
+        """Topology-pinned reservation. Which GPU the device plugin hands a
+        placeholder is opaque to us, so hold ``width`` (= every free GPU) 1-GPU placeholders at
+        once and keep the ``total`` whose device IDs ``pick`` returns. Returns the reservation and
+        the surplus placeholders, which the caller releases (or returns to the warm pool).
+        Entire mounts are the kept placeholders tied by one ``ANN_GROUP`` id, the same shape
+        as a warm-pool entire claim."""
+        if total <= 0 or width < total:
+            raise ValueError(f"bad trim reservation {total}/{width}")
+        mode = "entire" if entire else "single"
+        bodies = [self.build(owner, 1, mode, (), attach_id, container, idempotency_key)
+                  for _ in range(width)]
+        if entire:
+            group = secrets.token_hex(4)
+            for b in bodies:
+                b["metadata"]["annotations"][ANN_GROUP] = group
+        created = await self._create(bodies)
+        try:
+            with trace.span("placeholder_wait"):
+                self.faults.check("placeholder_wait")
+                failed = await self._await_admission(created, self.cfg.attach_timeout_s,
+                                                     tolerant=True)
+                self.faults.check("placeholder_wait", "after")
+        except BaseException:
+            await self.release(created, wait=False)
+            raise
+        admitted = [p for p in created if p not in failed]
+        if len(admitted) < total:
+            await self.release(created, wait=False)
+            raise InsufficientGPU(f"only {len(admitted)} of {total} GPUs admitted")
+        with trace.span("placement_trim"):
+            want = {d for d in pick([p.device_ids[0] for p in admitted])}
+            keep = [p for p in admitted if p.device_ids[0] in want][:total]
+            if len(keep) < total:  # pick returned ids we do not hold: fall back to any
+                keep += [p for p in admitted if p not in keep][:total - len(keep)]
+        surplus = [p for p in created if p not in keep]
+        return Reservation(keep), surplus
+
+    async def _create(self, bodies: List[dict]) -> List[Placeholder]:
+        with trace.span("ledger_reserve", placeholders=len(bodies)):
             self.faults.check("ledger_reserve")
             results = await asyncio.gather(
                 *[self.kube.create_pod(b["metadata"]["namespace"], b) for b in bodies],
                 return_exceptions=True)
         created = [Placeholder(r["metadata"]["namespace"], r["metadata"]["name"],
-                               r["metadata"]["uid"], (), mode)
+                               r["metadata"]["uid"], (),
+                               r["metadata"]["annotations"].get(ANN_MOUNT_MODE, "single"))
                    for r in results if isinstance(r, dict)]
         for r in results:
             if isinstance(r, dict):
@@ -211,23 +267,22 @@ class PlaceholderManager:
             raise ReserveError(f"placeholder create failed: {errors[0]}")
         try:
             self.faults.check("ledger_reserve", "after")
-            with trace.span("placeholder_wait"):
-                self.faults.check("placeholder_wait")
-                await self._await_admission(created, self.cfg.attach_timeout_s)
-                self.faults.check("placeholder_wait", "after")
         except BaseException:
             await self.release(created, wait=False)
             raise
-        return Reservation(created)
+        return created
 
-    async def _await_admission(self, phs: List[Placeholder], timeout: float) -> None:
-        """Wait until every placeholder is admitted and its devices are in the kubelet ledger."""
+    async def _await_admission(self, phs: List[Placeholder], timeout: float,
+                               tolerant: bool = False) -> List[Placeholder]:
+        """Wait until every placeholder is admitted and its devices are in the kubelet ledger.
+        ``tolerant``: unschedulable/failed placeholders are returned instead of raising."""
         pending = {(p.namespace, p.name): p for p in phs}
+        failed: List[Placeholder] = []
         loop = asyncio.get_running_loop()
         deadline = loop.time() + timeout
         delay = 0.0005
         while pending:
-            failure: List[str] = []
+            failure: Dict[Tuple[str, str], str] = {}
 
             def state():
                 bound = []
@@ -237,25 +292,29 @@ class PlaceholderManager:
                         continue
                     msg = podu.is_unschedulable(pod)
                     if msg:
-                        failure.append(f"unschedulable: {msg}")
-                        return True
-                    if podu.phase_of(pod) == "Failed":
-                        failure.append(pod["status"].get("reason", "Failed"))
-                        return True
-                    if podu.node_of(pod):
+                        failure[key] = f"unschedulable: {msg}"
+                    elif podu.phase_of(pod) == "Failed":
+                        failure[key] = pod["status"].get("reason", "Failed")
+                    elif podu.node_of(pod):
                         bound.append(key)
-                return bound or None
+                    if failure and not tolerant:
+                        return True
+                return True if failure else (bound or None)
 
             left = deadline - loop.time()
             if left <= 0:
                 raise ReserveError(f"timeout waiting for placeholders {sorted(pending)}")
             await self.informer.wait_for(state, timeout=left)
-            if failure:
-                reason = failure[0]
+            if failure and not tolerant:
+                reason = next(iter(failure.values()))
                 if reason.startswith("unschedulable") or reason.startswith("OutOf") or \
                         reason == "UnexpectedAdmissionError":
                     raise InsufficientGPU(reason)
                 raise ReserveError(reason)
+            for key in failure:
+                failed.append(pending.pop(key))
+            if not pending:
+                break
             # bound: the kubelet records the allocation at admission — read the ledger
             self.faults.check("ledger_read")
             got = await self.ledger.by_pod()
@@ -269,6 +328,7 @@ class PlaceholderManager:
             if pending:
                 await asyncio.sleep(delay)
                 delay = min(delay * 2, 0.05)
+        return failed
 
     # ------------------------------------------------------------------------ release
     async def release(self, phs: Sequence[Placeholder], wait: bool = True,
@@ -286,10 +346,14 @@ class PlaceholderManager:
                 if isinstance(r, Exception) and not isinstance(r, NotFound):
                     _log.error("delete placeholder %s/%s: %s", p.namespace, p.name, r)
                     failed.append(p)
-                elif p.uid:
+                else:
                     # grace 0 + no finalizers: the object is gone from the apiserver (and the
-                    # scheduler's books) once DELETE returns
-                    self.tombstones[p.uid] = now
+                    # scheduler's books) once DELETE returns; drop it from the cached views
+                    if p.uid:
+                        self.tombstones[p.uid] = now
+                        self.device_ids.pop(p.uid, None)
+                    if isinstance(self.last_ledger, dict):
+                        self.last_ledger.pop((p.namespace, p.name), None)
             if failed:
                 raise ReserveError(f"could not delete {len(failed)} placeholder(s): "
                                    f"{[p.name for p in failed]}")

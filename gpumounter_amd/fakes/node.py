@@ -112,7 +112,8 @@ class FakeNode:
             chosen: List[AmdGpu]
             pref = [normalize_device_id(p) for p in preferred]
             by_id = {normalize_device_id(self.device_id(g)): g for g in free}
-            if pref and all(p in by_id for p in pref) and len(pref) == n:
+            if self.alloc_policy != "blind" and pref and all(p in by_id for p in pref) \
+                    and len(pref) == n:
                 chosen = [by_id[p] for p in pref]
             elif self.alloc_policy == "topology":
                 # GetPreferredAllocation: co-locate with what the same owner already holds

@@ -71,6 +71,10 @@ class Config:
     device_file_mode: int = 0o666      # reference: nvidia.go:39 "666"
     # --- policy ----------------------------------------------------------------------------
     topology_policy: str = "xgmi"      # xgmi | first-fit
+    # hint: preferred set is only an annotation (the device plugin decides);
+    # trim: hold every free GPU with 1-GPU placeholders, keep the topology-chosen ones, release
+    # the rest — exact placement whatever the device plugin does
+    placement_enforce: str = "hint"
     max_gpus_per_request: int = 64
     kill_signal: int = 15              # SIGTERM like the reference's `kill` (namespace.go:192)
     kill_grace_s: float = 5.0          # then SIGKILL
@@ -143,6 +147,7 @@ class Config:
         _choice("cgroup_driver", self.cgroup_driver, ("auto", "cgroupfs", "systemd"))
         _choice("devnode_mode", self.devnode_mode, ("procroot", "setns", "emulate"))
         _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
+        _choice("placement_enforce", self.placement_enforce, ("hint", "trim"))
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))
         _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
         if not (0 < self.worker_port < 65536 and 0 <= self.master_port < 65536):

@@ -268,9 +268,10 @@ class GpuMountService:
                 _log.warning("policy denied add on %s/%s: %s", req.namespace, req.pod_name, why)
                 raise RpcError(grpc.StatusCode.FAILED_PRECONDITION, f"{ERR_POLICY}: {why}")
             with trace.span("placement"):
-                preferred = self._preferred(n, st)
+                free = self._free(st)
+                preferred = self._preferred(n, st, free)
             try:
-                res = await self._reserve(pod, n, req, st, preferred)
+                res = await self._reserve(pod, n, req, st, preferred, len(free))
             except InsufficientGPU as e:
                 _log.info("insufficient GPUs on %s: %s", self.cfg.node_name, e)
                 return api.AddGPUResponse(add_gpu_result=api.ADD_INSUFFICIENT, message=str(e))
@@ -324,8 +325,10 @@ class GpuMountService:
                                   devices=self._devices(gs, owner),
                                   message="Add GPU Success (replayed)")
 
-    async def _reserve(self, pod: dict, n: int, req, st: PodGpuState, preferred: List[str]):
-        """Claim from the warm pool first (if enabled), create placeholders for the rest."""
+    async def _reserve(self, pod: dict, n: int, req, st: PodGpuState, preferred: List[str],
+                       n_free: int = 0):
+        """Claim from the warm pool first (if enabled), create placeholders for the rest
+        (``placement_enforce=trim``: hold every free GPU, keep the topology-chosen ones)."""
         claimed = None
         if self.pool is not None and self.pool.enabled:
             k = min(n, len(self.pool.standby()))
@@ -336,6 +339,8 @@ class GpuMountService:
         got = len(claimed.placeholders) if claimed else 0
         if got == n:
             return claimed
+        if not got and preferred and self.cfg.placement_enforce == "trim" and n_free > n:
+            return await self._reserve_trim(pod, n, req, st, n_free)
         try:
             rest = await self.ph.reserve(pod, n - got, req.is_entire_mount,
                                          preferred if not got else [],
@@ -356,13 +361,43 @@ class GpuMountService:
         else:
             await self.ph.release(phs, wait=False)
 
-    def _preferred(self, n: int, st: PodGpuState) -> List[str]:
-        """xGMI/NUMA-aware preferred device IDs among the GPUs free in the last ledger view."""
+    async def _reserve_trim(self, pod: dict, n: int, req, st: PodGpuState, width: int):
+        keys = gpus_by_key(self.inv.gpus())
+        attached = st.hot + st.own
+
+        def pick(ids: List[str]) -> List[str]:
+            held = {keys[normalize_device_id(d)].index: d for d in ids
+                    if normalize_device_id(d) in keys}
+            plc = topology.choose([keys[normalize_device_id(d)] for d in held.values()], n,
+                                  self.inv.links(), attached=attached,
+                                  policy=self.cfg.topology_policy)
+            return [held[i] for i in plc.chosen] if plc else []
+
+        res, surplus = await self.ph.reserve_trim(
+            pod, n, req.is_entire_mount, width, pick, attach_id=log.request_id.get(),
+            container=req.container, idempotency_key=req.idempotency_key)
+        if surplus:
+            with trace.span("placement_release", placeholders=len(surplus)):
+                try:
+                    await self._release([p for p in surplus if p.device_ids]
+                                        + [p for p in surplus if not p.device_ids])
+                except Exception as e:  # noqa: BLE001 - the reconciler collects leftovers
+                    _log.error("releasing surplus placeholders: %s", e)
+        return res
+
+    def _free(self, st: PodGpuState) -> List[AmdGpu]:
+        """GPUs free in the last ledger view (minus placeholders we created since)."""
         allocated = {normalize_device_id(d) for ids in st.ledger.values() for d in ids}
-        allocated.update(normalize_device_id(d) for ids in self.ph.device_ids.values()
-                         for d in ids)
+        allocated.update(normalize_device_id(d) for uid, ids in self.ph.device_ids.items()
+                         if uid not in self.ph.tombstones for d in ids)
+        return [g for g in self.inv.gpus() if not allocated.intersection(g.ledger_keys())]
+
+    def _preferred(self, n: int, st: PodGpuState, free: Optional[List[AmdGpu]] = None
+                   ) -> List[str]:
+        """xGMI/NUMA-aware preferred device IDs among the GPUs free in the last ledger view."""
         gpus = self.inv.gpus()
-        free = [g for g in gpus if not allocated.intersection(g.ledger_keys())]
+        if free is None:
+            free = self._free(st)
         plc = topology.choose(free, n, self.inv.links(), attached=st.hot + st.own,
                               policy=self.cfg.topology_policy)
         if plc is None:

@@ -274,6 +274,48 @@ def test_placement_hint_followed_by_topology_plugin_and_counted_when_not():
     run(body)
 
 
+def _numa_of(lc, devices):
+    return {d["numa_node"] for d in devices}
+
+
+def test_placement_blind_plugin_hint_mode_crosses_numa_and_is_counted():
+    async def body(lc):
+        lc.tenant("other")
+        lc.tenant("t")
+        assert (await lc.add("default", "other", 3))[0] == 200      # blind plugin: GPUs 0,1,2
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200
+        assert _numa_of(lc, b["devices"]) == {0, 1}                   # 3 and 4: across sockets
+        assert lc.nodes["node-0"].worker.metrics.placement_mismatch._value.get() >= 1
+    run(body, alloc_policy="blind")
+
+
+@pytest.mark.parametrize("entire", [False, True])
+def test_placement_trim_enforces_topology_choice_with_blind_plugin(entire):
+    async def body(lc):
+        lc.tenant("other")
+        lc.tenant("t")
+        assert (await lc.add("default", "other", 3))[0] == 200
+        code, b = await lc.add("default", "t", 2, entire=entire)
+        assert code == 200
+        assert _numa_of(lc, b["devices"]) == {1} and len(b["devices"]) == 2
+        # surplus placeholders are gone; the books hold exactly 3 + 2 GPUs
+        assert len(node_of(lc).allocated) == 5
+        owners = sorted(p["metadata"]["labels"]["gpumounter.amd.com/owner"]
+                        for p in lc.cluster.placeholders())
+        assert owners == ["other"] * 3 + ["t"] * 2
+        assert not await lc.audit("default", "t")
+        if entire:   # the group removes as one entire mount
+            code, _ = await lc.remove("default", "t", [b["devices"][0]["uuid"]])
+            assert code == 400                       # all-or-nothing (allocator.go:121-123)
+            code, _ = await lc.remove("default", "t", [d["uuid"] for d in b["devices"]])
+            assert code == 200 and len(node_of(lc).allocated) == 3
+        else:        # grow by one: stays on the same socket
+            code, b2 = await lc.add("default", "t", 1)
+            assert code == 200 and _numa_of(lc, b2["devices"]) == {1}
+    run(body, alloc_policy="blind", worker_overrides={"placement_enforce": "trim"})
+
+
 # ------------------------------------------------------------------------------ namespaces/GC
 def test_tenant_namespace_mode_garbage_collects_with_owner():
     async def body(lc):
