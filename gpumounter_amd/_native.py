@@ -133,6 +133,8 @@ def host() -> C.CDLL:
         lib.gm_bpf_dev_query.argtypes = [C.c_char_p, C.POINTER(C.c_uint32), C.c_uint32,
                                          C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.gm_bpf_prog_name.argtypes = [C.c_uint32, C.c_char_p, C.c_int]
+        lib.gm_bpf_dev_program.argtypes = [C.c_char_p, C.POINTER(C.c_uint64), C.c_uint32,
+                                           C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.gm_bpf_dev_install.argtypes = [C.c_char_p, C.POINTER(DevRule), C.c_int,
                                            C.POINTER(DevRule), C.c_int, C.c_char_p,
                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]

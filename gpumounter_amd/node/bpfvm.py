@@ -87,6 +87,11 @@ def run(prog: Sequence[int], dev_type: int, access: int, major: int, minor: int,
             op = code & 0xF0
             if op == 0x90:  # exit
                 return regs[0]
+            if op == 0xF0:  # BPF_TAIL_CALL: the verifier's rewrite of bpf_tail_call (xlated)
+                if chained is None:
+                    pc += 1
+                    continue
+                return chained(dev_type, access, major, minor)
             if op == 0x80:  # call
                 if imm != 12:
                     raise BpfError(f"unsupported helper {imm}")
@@ -113,6 +118,25 @@ def runtime_default(dev_type: int, access: int, major: int, minor: int) -> int:
         return 0
     allowed = {(1, 3), (1, 5), (1, 7), (1, 8), (1, 9), (5, 0), (5, 1), (5, 2), (10, 200)}
     return 1 if (major, minor) in allowed or major == 136 else 0
+
+
+def immediates(prog: Sequence[int]) -> set:
+    """Constants the program compares against (jump-with-immediate operands): for a generated
+    allow-list these are exactly the rule majors/minors, i.e. the only interesting inputs."""
+    out = set()
+    skip = False
+    for insn in prog:
+        if skip:
+            skip = False
+            continue
+        code, _, _, _, imm = decode(insn)
+        if code == 0x18:
+            skip = True
+            continue
+        if code & 0x07 in (0x05, 0x06) and not code & 0x08 and code & 0xF0 not in (
+                0x00, 0x80, 0x90, 0xF0):
+            out.add(imm & 0xFFFFFFFF)
+    return out
 
 
 def allowed_pairs(prog: List[int], candidates, chained=runtime_default):

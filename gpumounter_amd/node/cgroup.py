@@ -17,6 +17,7 @@ pkg/util/cgroup/cgroup.go:78-169). Here:
 from __future__ import annotations
 
 import ctypes as C
+import errno
 import glob
 import json
 import os
@@ -27,6 +28,7 @@ from gpumounter_amd import _native
 from gpumounter_amd.models.device import DeviceNode
 from gpumounter_amd.models.pod import (QOS_BESTEFFORT, QOS_BURSTABLE, ContainerRef, qos_class,
                                        uid_of)
+from gpumounter_amd.node import bpfvm
 from gpumounter_amd.utils import log
 
 _log = log.get("node.cgroup")
@@ -295,9 +297,33 @@ class V2BpfBackend(DeviceRuleBackend):
                chained=chained.value, rules=len(rules))
 
     def allowed(self, cgdir):
-        # the loaded program is not introspected; the ledger is the source of truth for v2
-        state = os.path.join(cgdir, BPF_STATE)
-        return V2RecordingBackend().allowed(cgdir) if os.path.exists(state) else set()
+        """What the kernel enforces: the xlated instructions of our attached program, evaluated
+        by the interpreter (a program swapped out by systemd/the runtime reads as "nothing
+        granted", so the reconciler re-installs it)."""
+        prog = attached_program(cgdir)
+        return set() if prog is None else program_allows(prog)
+
+
+def attached_program(cgdir: str) -> Optional[List[int]]:
+    lib = _native.host()
+    n, pid = C.c_uint32(0), C.c_uint32(0)
+    rc = lib.gm_bpf_dev_program(cgdir.encode(), None, 0, C.byref(n), C.byref(pid))
+    if rc == 0 and n.value == 0:
+        return None
+    if rc not in (0, -errno.ENOSPC):
+        raise CgroupError(f"bpf introspection on {cgdir}: {os.strerror(-rc)}")
+    buf = (C.c_uint64 * n.value)()
+    rc = lib.gm_bpf_dev_program(cgdir.encode(), buf, n.value, C.byref(n), C.byref(pid))
+    if rc < 0:
+        raise CgroupError(f"bpf introspection on {cgdir}: {os.strerror(-rc)}")
+    return [int(buf[i]) for i in range(n.value)]
+
+
+def program_allows(prog: Sequence[int]) -> Set[Tuple[int, int]]:
+    """(major, minor) pairs a device program grants for rw char access, over every constant it
+    compares against; the chained runtime program is modelled by runc's default list."""
+    consts = bpfvm.immediates(prog)
+    return bpfvm.allowed_pairs(list(prog), [(a, b) for a in consts for b in consts])
 
 
 def build_program(nodes: Sequence[DeviceNode], chained: bool) -> List[int]:
@@ -338,7 +364,8 @@ class V2RecordingBackend(DeviceRuleBackend):
                 st = json.load(fh)
         except FileNotFoundError:
             return set()
-        return {(int(a), int(b)) for a, b, _ in st["rules"]}
+        # evaluate the recorded program itself (same check the real backend runs on xlated code)
+        return program_allows([int(x, 16) for x in st["insns"]])
 
 
 def make_backend(mode: str, emulate: bool, bpf_pin_dir: str = "") -> DeviceRuleBackend:

@@ -59,6 +59,11 @@ int gm_bpf_dev_query(const char* cgroup_path, uint32_t* ids, uint32_t cap, uint3
                      uint32_t* attach_flags);
 // Name of a loaded program (by id). Returns 0 or -errno.
 int gm_bpf_prog_name(uint32_t id, char* name, int cap);
+// Verifier-translated ("xlated") instructions of the gpumounter program attached to the cgroup, so
+// audits check what the kernel actually enforces. *n = 0 and *prog_id = 0 if none of ours is
+// attached; -ENOSPC (with *n = needed) if cap is too small; -EPERM if the kernel hides xlated code.
+int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, uint32_t* n,
+                       uint32_t* prog_id);
 // Installs (or updates) the gpumounter allow-list on a cgroup-v2 directory:
 //   * our program already attached → replaced, chaining to the same original program;
 //   * one foreign program attached → ours replaces it and tail-calls into it;

@@ -649,6 +649,45 @@ int gm_bpf_prog_name(uint32_t id, char* name, int cap) {
   return 0;
 }
 
+int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, uint32_t* n,
+                       uint32_t* prog_id) {
+  *n = 0;
+  if (prog_id) *prog_id = 0;
+  Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
+  if (!cg.ok()) return -errno;
+  Attached at;
+  int e = query(cg.fd, &at);
+  if (e < 0) return e;
+  for (uint32_t id : at.ids) {
+    if (!is_ours(id, nullptr)) continue;
+    Fd pfd(get_prog_fd_by_id(id));
+    if (!pfd.ok()) return pfd.fd;
+    struct bpf_prog_info info;
+    union bpf_attr a;
+    memset(&info, 0, sizeof(info));
+    memset(&a, 0, sizeof(a));
+    a.info.bpf_fd = (uint32_t)pfd.fd;
+    a.info.info_len = sizeof(info);
+    a.info.info = ptr_u64(&info);
+    if (sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a, sizeof(a)) < 0) return -errno;
+    if (prog_id) *prog_id = id;
+    const uint32_t need = info.xlated_prog_len / 8;
+    if (need == 0) return -EPERM;  // !bpf_capable(): the kernel reports no instructions
+    *n = need;
+    if (need > cap || insns == nullptr) return -ENOSPC;
+    memset(&info, 0, sizeof(info));
+    info.xlated_prog_len = need * 8;
+    info.xlated_prog_insns = ptr_u64(insns);
+    memset(&a, 0, sizeof(a));
+    a.info.bpf_fd = (uint32_t)pfd.fd;
+    a.info.info_len = sizeof(info);
+    a.info.info = ptr_u64(&info);
+    if (sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a, sizeof(a)) < 0) return -errno;
+    return 0;
+  }
+  return 0;
+}
+
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
                        const gm_dev_rule_t* base, int nbase, const char* pin_dir,
                        uint32_t* prog_id, uint32_t* chained_id) {

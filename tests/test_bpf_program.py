@@ -2,6 +2,7 @@
 executed with the Python eBPF interpreter against a reference model of the device-rule rules."""
 import ctypes as C
 import itertools
+import struct
 
 import pytest
 from hypothesis import given, settings
@@ -109,3 +110,26 @@ def test_build_rejects_bad_input():
     need = -lib.gm_bpf_dev_build(good, 1, 0, -1, None, 0)
     buf = (C.c_uint64 * 2)()
     assert lib.gm_bpf_dev_build(good, 1, 0, -1, buf, 2) == -need
+
+
+def _as_xlated(prog):
+    """Rewrite bpf_tail_call (call imm 12) the way the verifier does (BPF_JMP|BPF_TAIL_CALL)."""
+    out = []
+    for insn in prog:
+        code, dst, src, off, imm = bpfvm.decode(insn)
+        if code == 0x85 and imm == 12:
+            insn = struct.unpack("<Q", struct.pack("<BBhi", 0xF5, 0, 0, 0))[0]
+        out.append(insn)
+    return out
+
+
+def test_program_allows_reads_grants_back_from_raw_and_xlated_code():
+    from gpumounter_amd.models.device import DeviceNode
+    from gpumounter_amd.node.cgroup import build_program, program_allows
+    nodes = [DeviceNode("/dev/dri/renderD130", 226, 130), DeviceNode("/dev/dri/card2", 226, 2),
+             DeviceNode("/dev/kfd", 511, 0)]
+    prog = build_program(nodes, chained=True)
+    want = {(226, 130), (226, 2), (511, 0)}
+    gpu_keys = {(226, m) for m in range(256)} | {(511, 0)}
+    for p in (prog, _as_xlated(prog)):
+        assert program_allows(p) & gpu_keys == want

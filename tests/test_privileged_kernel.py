@@ -143,9 +143,13 @@ def test_cgroup_v2_bpf_install_and_restore(cgroup2_child, bpffs, pinned):
     assert name.value == b"gm_devallow"
     be.apply(cg, [FULL], [], [ZERO, FULL])           # update: chain target preserved
     assert probe_access(cg, paths) == "111"
+    # audit reads the grants back from the kernel's xlated program
+    assert be.allowed(cg) >= {(ZERO.major, ZERO.minor), (FULL.major, FULL.minor)}
     be.apply(cg, [], [ZERO], [FULL])                 # revoke /dev/zero
     assert probe_access(cg, paths) == "101"
+    assert (ZERO.major, ZERO.minor) not in be.allowed(cg)
     be.apply(cg, [], [FULL], [])                     # last GPU gone: runtime program restored
+    assert be.allowed(cg) == set()
     assert probe_access(cg, paths) == "100"
     _native.host().gm_bpf_dev_query(cg.encode(), ids, 8, C.byref(n), C.byref(flags))
     _native.host().gm_bpf_prog_name(ids[0], name, 32)
