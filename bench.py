@@ -54,6 +54,10 @@ def main() -> int:
     ap.add_argument("--placement", choices=("hint", "trim"), default="hint",
                     help="trim = enforce the topology choice by holding every free GPU and "
                          "releasing the surplus (placement_enforce)")
+    ap.add_argument("--ref-steps", type=int, default=20,
+                    help="after the timed loop, re-run this many attach/detach cycles with the "
+                         "emulated reference protocol on the same cluster (0 = skip; only with "
+                         "--latency zero and no warm pool)")
     ap.add_argument("--protocol", choices=("gpumounter", "reference"), default="gpumounter",
                     help="'reference' re-enacts the reference's call sequence on the same "
                          "cluster (emulated baseline, see gpumounter_amd/fakes/refproto.py)")
@@ -217,6 +221,29 @@ def main() -> int:
                 if args.protocol == "gpumounter" else None
             placeholders_left = len(lc.cluster.placeholders())
             p50 = pct(attach_ms, 0.5)
+            ref = None
+            if args.ref_steps > 0 and args.protocol == "gpumounter" and \
+                    args.latency == "zero" and not args.warm_pool:
+                from gpumounter_amd.fakes import refproto
+                refproto.install(lc)
+                ra, rd = [], []
+                for i in range(args.ref_steps + 2):
+                    ta = time.perf_counter()
+                    code, body = tc.call(lc.add("default", "tenant", n,
+                                                entire=args.mode == "entire"))
+                    tb = time.perf_counter()
+                    if code != 200:
+                        raise RuntimeError(f"reference attach failed: {code} {body}")
+                    code, body = tc.call(lc.remove("default", "tenant",
+                                                   [d["uuid"] for d in body["devices"]]))
+                    if code != 200:
+                        raise RuntimeError(f"reference detach failed: {code} {body}")
+                    if i >= 2:
+                        ra.append((tb - ta) * 1e3)
+                        rd.append((time.perf_counter() - tb) * 1e3)
+                ref = {"steps": args.ref_steps, "attach_p50_ms": round(pct(ra, 0.5), 4),
+                       "detach_p50_ms": round(pct(rd, 0.5), 4),
+                       "attach_speedup": round(pct(ra, 0.5) / p50, 2)}
             out = {
                 "metric": "p50_gpu_attach_latency_ms",
                 "value": round(p50, 4),
@@ -249,6 +276,7 @@ def main() -> int:
                 "ledger_audit_issues": audit_issues,
                 "final_orphans": orphan_issues,
                 "placeholders_left": placeholders_left,
+                "reference_emulated_same_run": ref,
                 "inventory": info,
             }
             print(json.dumps(out), flush=True)

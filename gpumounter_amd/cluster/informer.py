@@ -125,6 +125,12 @@ class PodInformer:
 
     # ------------------------------------------------------------------------ queries
     def get(self, ns: str, name: str) -> Optional[dict]:
+        """The cached object itself — read-only for callers. Entries are replaced wholesale on
+        every event (never mutated in place), so a reader's reference stays a consistent
+        snapshot; callers that need to modify use :meth:`get_copy`."""
+        return self.cache.get((ns, name))
+
+    def get_copy(self, ns: str, name: str) -> Optional[dict]:
         p = self.cache.get((ns, name))
         return copy.deepcopy(p) if p is not None else None
 

@@ -304,7 +304,7 @@ class PlaceholderManager:
             left = deadline - loop.time()
             if left <= 0:
                 raise ReserveError(f"timeout waiting for placeholders {sorted(pending)}")
-            await self.informer.wait_for(state, timeout=left)
+            ready = await self.informer.wait_for(state, timeout=left)
             if failure and not tolerant:
                 reason = next(iter(failure.values()))
                 if reason.startswith("unschedulable") or reason.startswith("OutOf") or \
@@ -317,8 +317,18 @@ class PlaceholderManager:
                 break
             # bound: the kubelet records the allocation at admission — read the ledger
             self.faults.check("ledger_read")
-            got = await self.ledger.by_pod()
-            self.last_ledger = got
+            got = None
+            bound = [k for k in ready if k in pending] if isinstance(ready, list) else []
+            if self.cfg.ledger_get and 0 < len(bound) <= 4:
+                res = await asyncio.gather(*[self.ledger.get(ns, n) for ns, n in bound])
+                if all(r is not None for r in res):
+                    got = {k: r for k, r in zip(bound, res) if r}
+                    merged = dict(self.last_ledger)
+                    merged.update(got)
+                    self.last_ledger = merged
+            if got is None:
+                got = await self.ledger.by_pod()
+                self.last_ledger = got
             for key in list(pending):
                 ids = got.get(key)
                 if ids:

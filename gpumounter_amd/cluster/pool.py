@@ -28,7 +28,7 @@ from gpumounter_amd.cluster.placeholder import (InsufficientGPU, LABEL_NODE, Pla
                                                 _label_value)
 from gpumounter_amd.hw import topology
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.device import AmdGpu, gpus_by_key, normalize_device_id
+from gpumounter_amd.models.device import AmdGpu, normalize_device_id
 from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_GROUP, ANN_IDEMPOTENCY,
                                          ANN_MOUNT_MODE,
                                          ANN_OWNER_NAME, ANN_OWNER_UID, LABEL_APP,
@@ -179,7 +179,7 @@ class WarmPool:
             pool = self.standby()
             if len(pool) < n:
                 return None
-            keys = gpus_by_key(self.inv.gpus())
+            keys = self.inv.by_key()
             by_gpu: Dict[int, Placeholder] = {}
             cands: List[AmdGpu] = []
             for ph in pool:

@@ -8,6 +8,7 @@ and only the process table is queried live.
 """
 from __future__ import annotations
 
+import copy
 import ctypes as C
 import os
 import threading
@@ -15,7 +16,8 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional
 
 from gpumounter_amd import _native
-from gpumounter_amd.models.device import DEFAULT_KFD_MAJOR, AmdGpu, LinkMatrix, find_gpu
+from gpumounter_amd.models.device import (DEFAULT_KFD_MAJOR, AmdGpu, LinkMatrix, find_gpu,
+                                          gpus_by_key)
 from gpumounter_amd.utils import log
 
 _log = log.get("hw.inventory")
@@ -85,6 +87,7 @@ class Inventory:
         self._lock = threading.Lock()
         self._gpus: List[AmdGpu] = []
         self._links: Optional[LinkMatrix] = None
+        self._keys = None
         self.refresh()
 
     # ---------------------------------------------------------------------------------- static
@@ -137,7 +140,15 @@ class Inventory:
     def gpus(self) -> List[AmdGpu]:
         """Fresh copies (callers mutate ledger fields)."""
         with self._lock:
-            return [AmdGpu(**{k: v for k, v in g.__dict__.items()}) for g in self._gpus]
+            return [copy.copy(g) for g in self._gpus]
+
+    def by_key(self) -> Dict[str, AmdGpu]:
+        """Device-ID spelling → GPU, cached per inventory snapshot. Read-only for callers (the
+        identity fields used for lookups; take :meth:`gpus` copies to record ledger state)."""
+        with self._lock:
+            if self._keys is None or self._keys[0] is not self._gpus:
+                self._keys = (self._gpus, gpus_by_key(self._gpus))
+            return self._keys[1]
 
     @property
     def count(self) -> int:

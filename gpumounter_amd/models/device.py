@@ -87,11 +87,18 @@ class AmdGpu:
 
         ROCm/k8s-device-plugin advertises PCI addresses; other plugins use UUIDs or node names.
         The join is done on all of them (lower-cased), see :func:`normalize_device_id`.
+        Memoised on the identity fields (they never change for a GPU).
         """
+        ident = (self.uuid, self.bdf, self.render_minor, self.card_minor)
+        memo = self.__dict__.get("_keys_memo")
+        if memo is not None and memo[0] == ident:
+            return memo[1]
         keys = {self.uuid, self.bdf, self.bdf.split(":", 1)[-1] if self.bdf else "",
                 f"renderD{self.render_minor}", f"card{self.card_minor}",
                 f"GPU-{self.uuid}" if self.uuid else ""}
-        return tuple(sorted(normalize_device_id(k) for k in keys if k))
+        out = tuple(sorted(normalize_device_id(k) for k in keys if k))
+        self.__dict__["_keys_memo"] = (ident, out)
+        return out
 
     def reset_state(self) -> None:
         self.state = GpuState.FREE

@@ -46,6 +46,7 @@ class LedgerClient:
         self._chan_loop = None
         self._stubs: Dict[str, object] = {}
         self.calls = 0
+        self._get_ok: Optional[bool] = None   # v1 Get served? (feature-gated in kubelets)
 
     def _channel(self) -> grpc.aio.Channel:
         loop = asyncio.get_running_loop()
@@ -130,6 +131,34 @@ class LedgerClient:
             if d.resource_name == self.resource:
                 ids.extend(d.device_ids)
         return ids
+
+    async def get(self, namespace: str, pod: str) -> Optional[List[str]]:
+        """Device IDs of our resource held by one pod, via v1 ``Get`` — one pod's record instead
+        of the whole node's (kubelet ≥ 1.27, ``KubeletPodResourcesGet`` gate). ``None`` when the
+        kubelet cannot serve it; the caller then lists."""
+        if self._get_ok is False:
+            return None
+        api = await self._resolve_api()
+        if api is not V1:
+            self._get_ok = False
+            return None
+        stub = self._stub(api.GET, api.GetPodResourcesRequest, api.GetPodResourcesResponse)
+        self.calls += 1
+        try:
+            resp = await stub(api.GetPodResourcesRequest(pod_name=pod, pod_namespace=namespace),
+                              timeout=self.timeout_s)
+        except grpc.aio.AioRpcError as e:
+            if e.code() == grpc.StatusCode.NOT_FOUND:
+                return []
+            if e.code() in (grpc.StatusCode.UNIMPLEMENTED, grpc.StatusCode.UNKNOWN):
+                # UNKNOWN: "PodResources API Get method disabled via feature gate"
+                _log.info("PodResources Get unavailable (%s); using List", e.details())
+                self._get_ok = False
+                return None
+            raise LedgerError(f"PodResources Get: {e.code().name} {e.details()}") from e
+        self._get_ok = True
+        return [i for c in resp.pod_resources.containers for d in c.devices
+                if d.resource_name == self.resource for i in d.device_ids]
 
     async def by_pod(self) -> Dict[Tuple[str, str], List[str]]:
         out: Dict[Tuple[str, str], List[str]] = {}

@@ -143,7 +143,7 @@ class GpuMountService:
         else:
             phs = cached
         st.ledger = ledger if ledger is not None else self.ph.last_ledger
-        keys = gpus_by_key(self.inv.gpus())
+        keys = self.inv.by_key()
 
         def resolve(ids) -> List[AmdGpu]:
             out = []
@@ -277,7 +277,7 @@ class GpuMountService:
                 return api.AddGPUResponse(add_gpu_result=api.ADD_INSUFFICIENT, message=str(e))
             except (ReserveError, asyncio.TimeoutError, InjectedFault, LedgerError) as e:
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
-            keys = gpus_by_key(self.inv.gpus())
+            keys = self.inv.by_key()
             new = [keys[normalize_device_id(d)] for d in res.device_ids]
             owner = {}
             for ph in res.placeholders:
@@ -362,7 +362,7 @@ class GpuMountService:
             await self.ph.release(phs, wait=False)
 
     async def _reserve_trim(self, pod: dict, n: int, req, st: PodGpuState, width: int):
-        keys = gpus_by_key(self.inv.gpus())
+        keys = self.inv.by_key()
         attached = st.hot + st.own
 
         def pick(ids: List[str]) -> List[str]:

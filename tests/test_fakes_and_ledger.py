@@ -206,3 +206,25 @@ def test_fake_device_plugin_topology_policy(tmp_path, mock_inventory):
     pref = node.free_ids()[:2]
     assert node.allocate("a", "z", "c", 2, preferred=pref) == pref
     assert node.allocate("a", "w", "c", 5) is None
+
+
+@pytest.mark.parametrize("use_get", [True, False])
+def test_admission_reads_placeholders_with_podresources_get(use_get):
+    """v1 Get reads only the admitted placeholders; with it disabled the worker lists."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+
+    async def main():
+        async with LocalCluster(worker_overrides={"ledger_get": use_get}) as lc:
+            lc.tenant("t")
+            kub = lc.nodes["node-0"].kubelet
+            before = dict(kub.calls)
+            code, b = await lc.add("default", "t", 2)
+            assert code == 200 and len(b["devices"]) == 2
+            gets = kub.calls["Get"] - before["Get"]
+            lists = kub.calls["List"] - before["List"]
+            if use_get:
+                assert gets >= 2 and lists <= 1        # ≤1: the pod-state read before placement
+            else:
+                assert gets == 0 and lists >= 2
+            assert not await lc.audit("default", "t")
+    asyncio.run(main())
