@@ -96,18 +96,34 @@ class PlaceholderManager:
         self.tombstones: Dict[str, float] = {}
         informer.handlers.append(self._on_event)
         self.last_ledger: Dict[Tuple[str, str], List[str]] = {}
+        # called with the placeholder pod when something other than us deletes it (kubectl,
+        # eviction, preemption, namespace deletion): its GPU is going back to the scheduler
+        self.on_foreign_delete: List[Callable[[dict], None]] = []
+        self._foreign_seen: Dict[str, float] = {}
 
     def _on_event(self, etype: str, pod: dict) -> None:
+        md = pod.get("metadata", {})
+        uid = md.get("uid", "")
+        if (etype == "DELETED" or (etype == "MODIFIED" and md.get("deletionTimestamp"))) \
+                and uid and uid not in self.tombstones and uid not in self._foreign_seen:
+            self._foreign_seen[uid] = 0.0
+            for cb in list(self.on_foreign_delete):
+                try:
+                    cb(pod)
+                except Exception:  # noqa: BLE001
+                    _log.exception("foreign-delete callback failed")
         if etype == "DELETED":
-            uid = pod.get("metadata", {}).get("uid", "")
             self.tombstones.pop(uid, None)
             self.device_ids.pop(uid, None)
+            self._foreign_seen.pop(uid, None)
         elif etype == "RELIST":
             live = {p["metadata"].get("uid") for p in self.informer.cache.values()}
             for uid in [u for u in self.tombstones if u not in live]:
                 self.tombstones.pop(uid, None)
             for uid in [u for u in self.device_ids if u not in live]:
                 self.device_ids.pop(uid, None)
+            for uid in [u for u in self._foreign_seen if u not in live]:
+                self._foreign_seen.pop(uid, None)
 
     # ------------------------------------------------------------------------ spec
     def namespace_for(self, owner: dict) -> str:

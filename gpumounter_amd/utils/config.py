@@ -75,7 +75,8 @@ class Config:
     # trim: hold every free GPU with 1-GPU placeholders, keep the topology-chosen ones, release
     # the rest — exact placement whatever the device plugin does
     placement_enforce: str = "hint"
-    ledger_get: bool = True            # read admitted placeholders with PodResources v1 Get
+    ledger_get: bool = True
+    reconcile_on_events: bool = True   # react to foreign placeholder / owner deletes at once            # read admitted placeholders with PodResources v1 Get
     max_gpus_per_request: int = 64
     kill_signal: int = 15              # SIGTERM like the reference's `kill` (namespace.go:192)
     kill_grace_s: float = 5.0          # then SIGKILL

@@ -12,6 +12,12 @@ Every ``reconcile_period_s`` (and on demand) this loop, per node:
 4. for every other running pod on the node, revokes hot-mount rules/nodes that no placeholder
    backs any more (orphans) — the "zero orphaned cgroup entries" invariant.
 All repairs take the same per-pod lock as AddGPU/RemoveGPU.
+
+Two events are handled immediately instead of at the next sweep (:meth:`watch_events`): a
+placeholder deleted by someone else (kubectl, eviction, preemption — its GPU goes back to the
+scheduler, so the tenant's access is revoked within milliseconds, not a period later) and a
+tenant pod that is deleted or finished (its placeholders are released at once in ``pool``
+namespace mode, where no garbage collector does it).
 """
 from __future__ import annotations
 
@@ -49,11 +55,70 @@ class Reconciler:
         self._task = None
         self.last: ReconcileReport = ReconcileReport()
         self._first_seen: Dict[str, float] = {}
+        self._kicked: set = set()
+        self._bg: set = set()
+        self.event_actions = 0
+
+    # ------------------------------------------------------------------------ events
+    def watch_events(self) -> None:
+        self.svc.ph.on_foreign_delete.append(self._on_foreign_delete)
+        self.svc.node_pods.handlers.append(self._on_node_pod)
+
+    def _on_foreign_delete(self, ph: dict) -> None:
+        md = ph["metadata"]
+        ann = md.get("annotations") or {}
+        if ann.get("gpumounter.amd.com/mount-mode") == "standby":
+            return
+        ons = (md.get("labels") or {}).get("gpumounter.amd.com/owner-namespace", "")
+        oname = ann.get("gpumounter.amd.com/owner-name", "")
+        if oname:
+            _log.warning("placeholder %s/%s deleted externally; revoking from %s/%s",
+                         md.get("namespace"), md.get("name"), ons, oname)
+            self._kick(("revoke", ons, oname))
+
+    def _on_node_pod(self, etype: str, pod: dict) -> None:
+        if etype == "DELETED" or podu.phase_of(pod) in ("Succeeded", "Failed"):
+            if self.svc.ph.owned_by(pod):
+                self._kick(("release", podu.ns_of(pod), podu.name_of(pod), podu.uid_of(pod)))
+
+    def _kick(self, key: tuple) -> None:
+        if key in self._kicked:
+            return
+        self._kicked.add(key)
+        t = asyncio.ensure_future(self._react(key))
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)
+
+    async def _react(self, key: tuple) -> None:
+        svc = self.svc
+        await asyncio.sleep(0)  # coalesce a burst of events for one owner
+        self._kicked.discard(key)
+        ns, name = key[1], key[2]
+        try:
+            async with svc.pod_lock(ns, name):
+                if key[0] == "release":
+                    stub = {"metadata": {"namespace": ns, "name": name, "uid": key[3]}}
+                    phs = svc.ph.owned_by(stub)
+                    if phs:   # back to the warm pool when one is configured
+                        await svc._release([svc.ph.cached(p) or svc.ph.from_pod(p, {})
+                                            for p in phs])
+                        svc.metrics.orphans.labels(kind="owner_gone").inc(len(phs))
+                else:
+                    owner = svc.node_pods.get(ns, name)
+                    if owner is None or podu.phase_of(owner) != "Running":
+                        return
+                    await svc.reconcile_pod(owner)
+                self.event_actions += 1
+                svc.metrics.reconcile_actions.labels(action=f"event_{key[0]}").inc()
+        except Exception as e:  # noqa: BLE001 - the periodic sweep retries
+            _log.error("event-driven reconcile %s failed: %s", key, e)
 
     async def start(self) -> None:
         self._task = asyncio.ensure_future(self._loop())
 
     async def stop(self) -> None:
+        for t in list(self._bg):
+            t.cancel()
         if self._task:
             self._task.cancel()
             try:

@@ -79,6 +79,8 @@ class Worker:
         self.pool = WarmPool(cfg, self.placeholders, self.inv, self.metrics)
         self.service.pool = self.pool
         self.reconciler = Reconciler(self.service, cfg.reconcile_period_s)
+        if cfg.reconcile_on_events:
+            self.reconciler.watch_events()
         self.grpc_server: Optional[grpc.aio.Server] = None
         self.http_runner: Optional[web.AppRunner] = None
         self.grpc_port = 0

@@ -404,7 +404,8 @@ def test_reconciler_revokes_orphaned_state():
         rep = await lc.nodes["node-0"].worker.reconciler.run_once()
         assert rep.revoked == ["default/o"] and rep.orphans > 0
         assert not await lc.audit("default", "o")
-    run(body)
+    # the periodic sweep on its own (event-driven repair is covered further down)
+    run(body, worker_overrides={"reconcile_on_events": False})
 
 
 # ------------------------------------------------------------------------------ multi-node
@@ -531,4 +532,50 @@ def test_batch_endpoint_runs_operations_concurrently():
         async with lc.session.post(lc.master_url + "/api/v1/batch", json=rm) as r:
             assert all(x["code"] == 200 for x in (await r.json())["results"])
         assert lc.nodes["node-0"].node.allocated == {}
+    run(body)
+
+
+# ------------------------------------------------------------------------------ event-driven repair
+async def _until(pred, timeout=3.0):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while loop.time() < end:
+        if await pred():
+            return True
+        await asyncio.sleep(0.01)
+    return False
+
+
+def test_external_placeholder_delete_revokes_access_immediately():
+    """kubectl delete / eviction of a placeholder returns its GPU to the scheduler: the tenant
+    must lose access right away, not at the next periodic sweep (periodic reconcile is off)."""
+    async def body(lc):
+        lc.tenant("t")
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200
+        victim = b["devices"][0]
+        lc.cluster.delete(lc.cluster.placeholders()[0]["metadata"]["namespace"],
+                          victim["placeholder"], grace=0)
+
+        async def revoked():
+            cid = lc.container_ids("default", "t")[0]
+            return len(node_of(lc).container_devices(cid)) < 5 and \
+                not await lc.audit("default", "t")
+        assert await _until(revoked)
+        st = await lc.nodes["node-0"].worker.service.pod_state(lc.cluster.get("default", "t"),
+                                                               fresh=True)
+        assert [g.bdf for g in st.hot] == [b["devices"][1]["bdf"]]
+        assert lc.nodes["node-0"].worker.reconciler.event_actions >= 1
+    run(body)
+
+
+def test_tenant_delete_releases_placeholders_without_waiting_for_the_sweep():
+    async def body(lc):
+        lc.tenant("t")
+        assert (await lc.add("default", "t", 3))[0] == 200
+        lc.cluster.delete("default", "t", grace=0)
+
+        async def released():
+            return lc.cluster.placeholders() == [] and node_of(lc).allocated == {}
+        assert await _until(released)
     run(body)
