@@ -20,7 +20,7 @@ _TYPES = {
 }
 
 # field spec: (name, number, type, label) where type is a scalar name, "msg:.pkg.Name",
-# or "enum:.pkg.Name.Enum"; label "opt" | "rep"
+# "enum:.pkg.Name.Enum" or "map:<scalar key>,<scalar value>"; label "opt" | "rep"
 FieldSpec = Tuple[str, int, str, str]
 
 
@@ -41,7 +41,19 @@ class ProtoFile:
         for fname, num, ftype, label in fields:
             f = m.field.add(name=fname, number=num, json_name=_json_name(fname))
             f.label = F.LABEL_REPEATED if label == "rep" else F.LABEL_OPTIONAL
-            if ftype.startswith("msg:"):
+            if ftype.startswith("map:"):
+                # proto3 map<K, V> = repeated nested <Field>Entry{key=1, value=2} (map_entry)
+                kt, vt = ftype[4:].split(",")
+                entry = "".join(p[:1].upper() + p[1:] for p in fname.split("_")) + "Entry"
+                e = m.nested_type.add(name=entry)
+                e.options.map_entry = True
+                for en, ev, et in (("key", 1, kt), ("value", 2, vt)):
+                    ef = e.field.add(name=en, number=ev, json_name=en, type=_TYPES[et.strip()])
+                    ef.label = F.LABEL_OPTIONAL
+                f.label = F.LABEL_REPEATED
+                f.type = F.TYPE_MESSAGE
+                f.type_name = f".{self.package}.{name}.{entry}"
+            elif ftype.startswith("msg:"):
                 f.type = F.TYPE_MESSAGE
                 f.type_name = ftype[4:]
             elif ftype.startswith("enum:"):

@@ -266,13 +266,19 @@ class FakeCluster:
             if want:
                 pref = (pod["metadata"].get("annotations") or {}).get(
                     "gpumounter.amd.com/preferred-devices", "")
-                ids = node.allocate(ns, name, c["name"], want,
-                                    [p for p in pref.split(",") if p])
+                if node.plugin is not None:      # kubelet device manager → device plugin
+                    ids = await node.plugin.plugin_allocate(ns, name, c["name"], want)
+                else:
+                    ids = node.allocate(ns, name, c["name"], want,
+                                        [p for p in pref.split(",") if p])
                 if ids is None:
                     node.release_pod(ns, name)
                     pod["status"]["phase"] = "Failed"
                     pod["status"]["reason"] = "UnexpectedAdmissionError"
                     self._bump("MODIFIED", pod)
+                    return
+                if self.pods.get((ns, name)) is not pod:   # deleted while the plugin ran
+                    node.release_pod(ns, name)
                     return
         pod["status"]["containerStatuses"] = [
             {"name": c["name"], "ready": False, "restartCount": 0, "image": c.get("image", ""),

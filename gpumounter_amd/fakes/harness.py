@@ -49,7 +49,8 @@ class LocalCluster:
                  devnode_mode: str = "emulate", reconcile_period_s: float = 0.0,
                  start_master: bool = True, worker_overrides: Optional[dict] = None,
                  node_gpu_bdfs: Optional[List[str]] = None,
-                 master_overrides: Optional[dict] = None) -> None:
+                 master_overrides: Optional[dict] = None,
+                 device_plugin: bool = False) -> None:
         self.n_nodes = n_nodes
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
@@ -66,6 +67,7 @@ class LocalCluster:
         self.start_master = start_master
         self.worker_overrides = worker_overrides or {}
         self.master_overrides = master_overrides or {}
+        self.device_plugin = device_plugin
         self.node_gpu_bdfs = [b.lower() for b in node_gpu_bdfs] if node_gpu_bdfs else None
         self.nodes: Dict[str, NodeHandle] = {}
         self.master: Optional[Master] = None
@@ -110,7 +112,8 @@ class LocalCluster:
                         alloc_policy=self.alloc_policy)
         self.cluster.add_node(node)
         sock = os.path.join(ndir, "pod-resources", "kubelet.sock")
-        kubelet = FakeKubelet(node, sock)
+        kubelet = FakeKubelet(node, sock, plugin_dir=os.path.join(ndir, "device-plugins")
+                              if self.device_plugin else "")
         await kubelet.start()
         h = NodeHandle(name, node, kubelet)
         self.nodes[name] = h
@@ -120,6 +123,9 @@ class LocalCluster:
     async def start_worker(self, name: str) -> Worker:
         h = self.nodes[name]
         ov = dict(self.worker_overrides)
+        if self.device_plugin:
+            ov.setdefault("device_plugin", True)
+            ov.setdefault("device_plugin_dir", h.kubelet.plugin_dir)
         cfg = Config.load(env={}, kube_api=self.api_url, node_name=name,
                           kubelet_socket=h.kubelet.socket_path,
                           cgroup_root=h.node.cgroup_root, cgroup_mode=self.cgroup_mode,

@@ -85,6 +85,9 @@ class FakeNode:
         self.allocated: Dict[str, Tuple[str, str, str]] = {}
         self.containers: Dict[str, Container] = {}  # container id → Container
         self.alloc_log: List[Tuple[str, str, List[str]]] = []
+        # a registered device plugin (FakeKubelet device manager) replaces allocate()
+        self.plugin = None
+        self.unhealthy: set = set()
 
     # ------------------------------------------------------------------------ device plugin
     def device_id(self, g: AmdGpu) -> str:
@@ -126,6 +129,16 @@ class FakeNode:
                 self.allocated[d] = (ns, pod, container)
             self.alloc_log.append((ns, pod, ids))
             return ids
+
+    def record(self, ns: str, pod: str, container: str, ids: Sequence[str]) -> bool:
+        """Commit an allocation chosen elsewhere (device-plugin path); False if any is taken."""
+        with self._lock:
+            if any(d in self.allocated for d in ids):
+                return False
+            for d in ids:
+                self.allocated[d] = (ns, pod, container)
+            self.alloc_log.append((ns, pod, list(ids)))
+            return True
 
     def release_pod(self, ns: str, pod: str) -> List[str]:
         with self._lock:

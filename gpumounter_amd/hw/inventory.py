@@ -177,6 +177,18 @@ class Inventory:
                            int(buf[i].cu_occupancy), buf[i].name.decode(errors="replace"))
                 for i in range(min(n.value, cap))]
 
+    def healthy(self) -> Dict[int, bool]:
+        """Per-GPU liveness for the device plugin: the device still answers amdsmi queries with
+        the identity it was enumerated with (a GPU that fell off the bus or was reset into a
+        different partition mode reads as unhealthy)."""
+        smi = _native.smi()
+        out: Dict[int, bool] = {}
+        for g in self.gpus():
+            info = _native.GpuInfo()
+            st = smi.gm_smi_gpu_info(g.index, C.byref(info))
+            out[g.index] = st == 0 and info.bdf.decode().lower() == g.bdf
+        return out
+
     def summary(self) -> Dict:
         gs = self.gpus()
         return {"lib": self.lib_path, "kfd_major": self.kfd_major, "count": len(gs),

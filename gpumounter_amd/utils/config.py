@@ -76,7 +76,13 @@ class Config:
     # the rest — exact placement whatever the device plugin does
     placement_enforce: str = "hint"
     ledger_get: bool = True
-    reconcile_on_events: bool = True   # react to foreign placeholder / owner deletes at once            # read admitted placeholders with PodResources v1 Get
+    reconcile_on_events: bool = True
+    # serve amd.com/gpu ourselves (replaces the ROCm device plugin on the node) so
+    # GetPreferredAllocation steers placeholders to the topology-chosen GPUs
+    device_plugin: bool = False
+    device_plugin_dir: str = "/var/lib/kubelet/device-plugins"
+    device_plugin_inject: bool = True     # False: no device specs (kind / mock inventory)
+    device_plugin_health_s: float = 5.0   # react to foreign placeholder / owner deletes at once            # read admitted placeholders with PodResources v1 Get
     max_gpus_per_request: int = 64
     kill_signal: int = 15              # SIGTERM like the reference's `kill` (namespace.go:192)
     kill_grace_s: float = 5.0          # then SIGKILL

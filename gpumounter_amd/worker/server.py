@@ -78,6 +78,14 @@ class Worker:
                                        self.faults)
         self.pool = WarmPool(cfg, self.placeholders, self.inv, self.metrics)
         self.service.pool = self.pool
+        self.plugin = None
+        if cfg.device_plugin:
+            from gpumounter_amd.deviceplugin.plugin import AmdGpuDevicePlugin
+            self.plugin = AmdGpuDevicePlugin(
+                self.inv, cfg.resource_name, cfg.device_plugin_dir,
+                inject_devices=cfg.device_plugin_inject,
+                health_period_s=cfg.device_plugin_health_s, policy=cfg.topology_policy)
+            self.service.plugin = self.plugin
         self.reconciler = Reconciler(self.service, cfg.reconcile_period_s)
         if cfg.reconcile_on_events:
             self.reconciler.watch_events()
@@ -156,6 +164,8 @@ class Worker:
             self.http_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
         if reconcile and self.cfg.reconcile_period_s > 0:
             await self.reconciler.start()
+        if self.plugin is not None:
+            await self.plugin.start()
         await self.pool.start()
         if self.cfg.metrics_period_s > 0:
             self._collector = asyncio.ensure_future(self._collect_loop())
@@ -204,6 +214,8 @@ class Worker:
             self._collector.cancel()
         await self.pool.stop()
         await self.reconciler.stop()
+        if self.plugin is not None:
+            await self.plugin.stop()
         if self.grpc_server is not None:
             await self.grpc_server.stop(0.5)
         if self.http_runner is not None:

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import secrets
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -87,6 +88,7 @@ class GpuMountService:
         self.metrics = metrics or Metrics()
         self.faults = faults if faults is not None else FaultInjector(cfg.fault)
         self.pool = None  # WarmPool, attached by the Worker when warm_pool_size > 0
+        self.plugin = None  # AmdGpuDevicePlugin, attached by the Worker with device_plugin=1
         self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}
         self._own: Dict[str, Tuple[str, ...]] = {}   # pod uid → its own device-plugin GPU IDs
         self.ledger_reads = 0
@@ -341,6 +343,12 @@ class GpuMountService:
             return claimed
         if not got and preferred and self.cfg.placement_enforce == "trim" and n_free > n:
             return await self._reserve_trim(pod, n, req, st, n_free)
+        token = ""
+        if self.plugin is not None and preferred and not got:
+            # our own device plugin answers GetPreferredAllocation for these placeholders
+            token = log.request_id.get() or secrets.token_hex(4)
+            for ids in ([preferred] if req.is_entire_mount else [[d] for d in preferred]):
+                self.plugin.intend(ids, token)
         try:
             rest = await self.ph.reserve(pod, n - got, req.is_entire_mount,
                                          preferred if not got else [],
@@ -351,6 +359,9 @@ class GpuMountService:
             if claimed:
                 await self.pool.give_back(claimed.placeholders)
             raise
+        finally:
+            if token:
+                self.plugin.withdraw(token)
         if claimed:
             rest.placeholders = claimed.placeholders + rest.placeholders
         return rest

@@ -36,6 +36,21 @@ def test_worker_daemonset_shape():
     assert "NVIDIA_VISIBLE_DEVICES" not in env
 
 
+def test_kind_overlay_env_is_valid_config():
+    """Every GM_* variable in the kind patch parses into the Config the worker would run with."""
+    (patch,) = load("kind/workers-mock-patch.yaml")
+    c = patch["spec"]["template"]["spec"]["containers"][0]
+    env = {e["name"]: e["value"] for e in c["env"]}
+    cfg = Config.load(env=env)
+    assert cfg.amdsmi_lib == "mock" and cfg.device_plugin and not cfg.device_plugin_inject
+    assert cfg.devnode_mode == "emulate" and cfg.kfd_major == 511
+    (ds,) = load("gpu-mounter-workers.yaml")
+    names = {v["name"] for v in ds["spec"]["template"]["spec"]["volumes"]}
+    assert {v["name"] for v in patch["spec"]["template"]["spec"]["volumes"]} <= names
+    assert "/var/lib/kubelet/device-plugins" in {
+        m["mountPath"] for m in ds["spec"]["template"]["spec"]["containers"][0]["volumeMounts"]}
+
+
 def test_rbac_is_least_privilege():
     docs = load("rbac.yaml")
     roles = [d for d in docs if d["kind"] == "ClusterRole"]
