@@ -54,6 +54,9 @@ def main() -> int:
     ap.add_argument("--placement", choices=("hint", "trim"), default="hint",
                     help="trim = enforce the topology choice by holding every free GPU and "
                          "releasing the surplus (placement_enforce)")
+    ap.add_argument("--device-plugin", action="store_true",
+                    help="the worker serves amd.com/gpu itself; the fake kubelet's device manager "
+                         "calls GetPreferredAllocation/Allocate on it at admission")
     ap.add_argument("--ref-steps", type=int, default=20,
                     help="after the timed loop, re-run this many attach/detach cycles with the "
                          "emulated reference protocol on the same cluster (0 = skip; only with "
@@ -105,7 +108,7 @@ def main() -> int:
             return 3
         lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
         tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
-                             node_gpu_bdfs=node_bdfs,
+                             node_gpu_bdfs=node_bdfs, device_plugin=args.device_plugin,
                              worker_overrides={"warm_pool_size": args.warm_pool,
                                                "placement_enforce": args.placement})
         lc = tc.start()
@@ -266,6 +269,7 @@ def main() -> int:
                     "protocol": args.protocol if args.protocol == "gpumounter"
                     else "reference (emulated)",
                     "warm_pool": args.warm_pool, "placement": args.placement,
+                    "device_plugin": args.device_plugin,
                 },
                 "attach_p99_ms": round(pct(attach_ms, 0.99), 4),
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),
