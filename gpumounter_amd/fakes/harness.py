@@ -50,7 +50,8 @@ class LocalCluster:
                  start_master: bool = True, worker_overrides: Optional[dict] = None,
                  node_gpu_bdfs: Optional[List[str]] = None,
                  master_overrides: Optional[dict] = None,
-                 device_plugin: bool = False) -> None:
+                 device_plugin: bool = False, cgroup_root: str = "",
+                 kfd_major: int = 0) -> None:
         self.n_nodes = n_nodes
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
@@ -68,6 +69,8 @@ class LocalCluster:
         self.worker_overrides = worker_overrides or {}
         self.master_overrides = master_overrides or {}
         self.device_plugin = device_plugin
+        self.real_cgroup_root = cgroup_root   # privileged tests: a real cgroup2 mount
+        self.kfd_major = kfd_major
         self.node_gpu_bdfs = [b.lower() for b in node_gpu_bdfs] if node_gpu_bdfs else None
         self.nodes: Dict[str, NodeHandle] = {}
         self.master: Optional[Master] = None
@@ -79,7 +82,7 @@ class LocalCluster:
 
     # ------------------------------------------------------------------------ lifecycle
     async def start(self) -> "LocalCluster":
-        self.inventory = Inventory(self.amdsmi_lib)
+        self.inventory = Inventory(self.amdsmi_lib, self.kfd_major)
         self.api_runner = web.AppRunner(self.cluster.app(), access_log=None)
         await self.api_runner.setup()
         site = web.TCPSite(self.api_runner, "127.0.0.1", 0)
@@ -109,7 +112,9 @@ class LocalCluster:
         node = FakeNode(name, ndir, gpus, self.inventory.links(),
                         cgroup_mode=self.cgroup_mode, cgroup_driver=self.cgroup_driver,
                         runtime=self.runtime, device_id_kind=self.device_id_kind,
-                        alloc_policy=self.alloc_policy)
+                        alloc_policy=self.alloc_policy,
+                        cgroup_root=os.path.join(self.real_cgroup_root, name)
+                        if self.real_cgroup_root else "")
         self.cluster.add_node(node)
         sock = os.path.join(ndir, "pod-resources", "kubelet.sock")
         kubelet = FakeKubelet(node, sock, plugin_dir=os.path.join(ndir, "device-plugins")
@@ -130,7 +135,9 @@ class LocalCluster:
                           kubelet_socket=h.kubelet.socket_path,
                           cgroup_root=h.node.cgroup_root, cgroup_mode=self.cgroup_mode,
                           devnode_mode=self.devnode_mode,
-                          container_root_prefix=h.node.rootfs_root, amdsmi_lib=self.amdsmi_lib,
+                          container_root_prefix=h.node.rootfs_root
+                          if self.devnode_mode == "emulate" else "",
+                          amdsmi_lib=self.amdsmi_lib,
                           worker_host="127.0.0.1", worker_port=1, metrics_port=0,
                           placeholder_namespace_mode=self.placeholder_namespace_mode,
                           reconcile_period_s=self.reconcile_period_s, log_json=False,

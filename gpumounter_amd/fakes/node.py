@@ -57,7 +57,8 @@ class FakeNode:
                  links: Optional[LinkMatrix] = None, resource: str = "amd.com/gpu",
                  cgroup_mode: str = "v1", cgroup_driver: str = "cgroupfs",
                  runtime: str = "containerd", device_id_kind: str = "bdf",
-                 alloc_policy: str = "topology", labels: Optional[Dict[str, str]] = None) -> None:
+                 alloc_policy: str = "topology", labels: Optional[Dict[str, str]] = None,
+                 cgroup_root: str = "") -> None:
         self.name = name
         self.resource = resource
         self.gpus = list(gpus)
@@ -70,11 +71,16 @@ class FakeNode:
         self.labels = {"kubernetes.io/hostname": name, "gpu-mounter-enable": "enable"}
         self.labels.update(labels or {})
         self.workdir = workdir
-        self.cgroup_root = os.path.join(workdir, "cgroup")
+        # cgroup_root given: a REAL cgroup2 mount (privileged tests) — directories are real
+        # cgroups, cgroup.procs moves real processes, nothing else is written into it
+        self.real_cgroups = bool(cgroup_root)
+        self.cgroup_root = cgroup_root or os.path.join(workdir, "cgroup")
         self.rootfs_root = os.path.join(workdir, "rootfs")
         os.makedirs(self.cgroup_root, exist_ok=True)
         os.makedirs(self.rootfs_root, exist_ok=True)
-        if cgroup_mode == "v2":
+        if self.real_cgroups:
+            pass
+        elif cgroup_mode == "v2":
             with open(os.path.join(self.cgroup_root, "cgroup.controllers"), "w") as fh:
                 fh.write("cpuset cpu io memory pids\n")
         else:
@@ -199,11 +205,16 @@ class FakeNode:
             else self.cgroup_root
         cg = os.path.join(base, rel)
         os.makedirs(cg, exist_ok=True)
-        with open(os.path.join(cg, FAKE_MARKER), "w") as fh:
-            fh.write(json.dumps({"mode": self.cgroup_mode, "container": cid}))
-        with open(os.path.join(cg, "cgroup.procs"), "w") as fh:
-            fh.write("".join(f"{p}\n" for p in pids))
-        if self.cgroup_mode == "v1":
+        if self.real_cgroups:
+            for p in pids:   # the kernel takes one PID per write
+                with open(os.path.join(cg, "cgroup.procs"), "w") as fh:
+                    fh.write(str(p))
+        else:
+            with open(os.path.join(cg, FAKE_MARKER), "w") as fh:
+                fh.write(json.dumps({"mode": self.cgroup_mode, "container": cid}))
+            with open(os.path.join(cg, "cgroup.procs"), "w") as fh:
+                fh.write("".join(f"{p}\n" for p in pids))
+        if self.cgroup_mode == "v1" and not self.real_cgroups:
             for f in ("devices.allow", "devices.deny"):
                 open(os.path.join(cg, f), "w").close()
             with open(os.path.join(cg, "devices.list"), "w") as fh:

@@ -1,0 +1,159 @@
+"""Full-stack attach/detach on a real kernel (run by tests/test_privileged_e2e.py as root).
+
+HTTP master → gRPC worker → placeholder ledger (fake apiserver/kubelet) → the production node
+path: real cgroup2 hierarchy, real BPF_PROG_TYPE_CGROUP_DEVICE program swapped over a
+runc-style program, real mknod through /proc/<pid>/root into a tenant process that lives in its
+own mount namespace (private tmpfs /dev). The mock inventory maps the "GPUs" to harmless memory
+devices (render/card minors of major 1) so a process inside the tenant cgroup can prove what the
+kernel enforces. Prints one JSON line of observations.
+"""
+import asyncio
+import ctypes as C
+import ctypes.util
+import json
+import os
+import shutil
+import stat
+import subprocess
+import sys
+import tempfile
+import uuid
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from gpumounter_amd import _native  # noqa: E402
+from gpumounter_amd.fakes.harness import LocalCluster  # noqa: E402
+from gpumounter_amd.utils import log  # noqa: E402
+
+PATHS = ["/dev/null", "/dev/zero", "/dev/full", "/dev/random"]
+PROBE = ("import os,sys\n"
+         "open(sys.argv[1]+'/cgroup.procs','w').write(str(os.getpid()))\n"
+         "out=[]\n"
+         "for p in sys.argv[2:]:\n"
+         "    try:\n"
+         "        open(p,'rb').close(); out.append('1')\n"
+         "    except OSError:\n"
+         "        out.append('0')\n"
+         "print(''.join(out))\n")
+
+
+def probe(cg):
+    r = subprocess.run([sys.executable, "-c", PROBE, cg] + PATHS, capture_output=True,
+                       text=True, timeout=30)
+    if r.returncode:
+        raise RuntimeError(r.stderr)
+    return r.stdout.strip()
+
+
+def attach_runtime_program(cg):
+    """runc-style program: /dev/null rw + mknod only, attached with BPF_F_ALLOW_MULTI."""
+    rules = (_native.DevRule * 1)(_native.DevRule(b"c", 7, 1, 0, 1, 3))
+    lib = _native.host()
+    need = -lib.gm_bpf_dev_build(rules, 1, 0, -1, None, 0)
+    buf = (C.c_uint64 * need)()
+    n = lib.gm_bpf_dev_build(rules, 1, 0, -1, buf, need)
+    fd = lib.gm_bpf_dev_load(buf, n, b"runc_devices", None, 0)
+    assert fd >= 0, os.strerror(-fd)
+    libc = C.CDLL(ctypes.util.find_library("c"), use_errno=True)
+    cgfd = os.open(cg, os.O_RDONLY | os.O_DIRECTORY)
+    attr = (C.c_uint8 * 128)()
+    C.memmove(attr, (C.c_uint32 * 4)(cgfd, fd, 6, 2), 16)
+    rc = libc.syscall(321, 8, attr, 128)
+    os.close(cgfd)
+    assert rc == 0, os.strerror(C.get_errno())
+
+
+def prog_names(cg):
+    lib = _native.host()
+    ids = (C.c_uint32 * 8)()
+    n, flags = C.c_uint32(0), C.c_uint32(0)
+    assert lib.gm_bpf_dev_query(cg.encode(), ids, 8, C.byref(n), C.byref(flags)) == 0
+    out = []
+    for i in range(n.value):
+        name = C.create_string_buffer(32)
+        lib.gm_bpf_prog_name(ids[i], name, 32)
+        out.append(name.value.decode())
+    return out
+
+
+def chr_node(pid, rel):
+    try:
+        st = os.stat(f"/proc/{pid}/root{rel}")
+    except FileNotFoundError:
+        return None
+    return [os.major(st.st_rdev), os.minor(st.st_rdev)] if stat.S_ISCHR(st.st_mode) else "notchr"
+
+
+async def flow(mnt, bpffs, tenant_pid, obs):
+    async with LocalCluster(cgroup_mode="v2", devnode_mode="procroot", cgroup_root=mnt,
+                            kfd_major=1,
+                            worker_overrides={"drm_major": 1, "bpf_pin_dir": bpffs}) as lc:
+        w = lc.nodes["node-0"].worker
+        obs["backend"] = w.backend.name
+        lc.tenant("t", pids={"main": [tenant_pid]})
+        node = lc.nodes["node-0"].node
+        (c,) = [c for c in node.containers.values() if c.pod_name == "t"]
+        cg = c.cgroup_dir
+        obs["tenant_in_cgroup"] = str(tenant_pid) in open(os.path.join(cg, "cgroup.procs")).read()
+        attach_runtime_program(cg)
+        obs["before"] = probe(cg)
+        code, b1 = await lc.add("default", "t", 1)
+        obs["add1"] = [code, [d["bdf"] for d in b1.get("devices", [])]]
+        obs["after_add1"] = probe(cg)
+        obs["progs_after_add1"] = prog_names(cg)
+        obs["nodes_after_add1"] = {p: chr_node(tenant_pid, p) for p in
+                                   ("/dev/kfd", "/dev/dri/renderD5", "/dev/dri/card7")}
+        obs["host_dev_untouched"] = not os.path.exists("/dev/dri/renderD5")
+        obs["audit_after_add1"] = [i.kind for i in await lc.audit("default", "t")]
+        code, b2 = await lc.add("default", "t", 1)
+        obs["add2"] = [code, [d["bdf"] for d in b2.get("devices", [])]]
+        obs["after_add2"] = probe(cg)
+        code, _ = await lc.remove("default", "t", [b1["devices"][0]["uuid"]])
+        obs["remove1"] = code
+        obs["after_remove1"] = probe(cg)
+        obs["nodes_after_remove1"] = {p: chr_node(tenant_pid, p) for p in
+                                      ("/dev/kfd", "/dev/dri/renderD5", "/dev/dri/renderD8")}
+        code, _ = await lc.remove("default", "t", [b2["devices"][0]["uuid"]])
+        obs["remove2"] = code
+        obs["after_remove2"] = probe(cg)
+        obs["progs_final"] = prog_names(cg)
+        obs["nodes_final"] = {p: chr_node(tenant_pid, p) for p in ("/dev/kfd",
+                                                                  "/dev/dri/renderD8")}
+        obs["audit_final"] = [i.kind for i in await lc.audit("default", "t")]
+        obs["pins_left"] = [f for f in os.listdir(bpffs) if f.startswith("gm_")]
+
+
+def main():
+    log.setup("WARNING", json_format=False)
+    obs = {}
+    mnt = tempfile.mkdtemp(prefix="gm-e2e-cg2-")
+    bpffs = tempfile.mkdtemp(prefix="gm-e2e-bpffs-")
+    subprocess.run(["mount", "-t", "cgroup2", "none", mnt], check=True)
+    subprocess.run(["mount", "-t", "bpf", "bpf", bpffs], check=True)
+    root = os.path.join(mnt, "gm-e2e-" + uuid.uuid4().hex[:8])
+    tenant = subprocess.Popen(
+        ["unshare", "-m", "--propagation", "private", "sh", "-c",
+         "set -e; mount -t tmpfs tmpfs /dev; echo ok; exec sleep 300"],
+        stdout=subprocess.PIPE, text=True)
+    try:
+        assert tenant.stdout.readline().strip() == "ok"
+        assert os.readlink(f"/proc/{tenant.pid}/ns/mnt") != os.readlink("/proc/self/ns/mnt")
+        asyncio.run(flow(root, bpffs, tenant.pid, obs))
+    finally:
+        tenant.kill()
+        tenant.wait()
+        # tear the real cgroup tree down bottom-up (processes are gone)
+        for dirpath, dirs, _ in sorted(os.walk(root), key=lambda t: -t[0].count("/")):
+            try:
+                os.rmdir(dirpath)
+            except OSError:
+                pass
+        subprocess.run(["umount", bpffs], check=False)
+        subprocess.run(["umount", mnt], check=False)
+        shutil.rmtree(bpffs, ignore_errors=True)
+        os.rmdir(mnt)
+    print(json.dumps(obs))
+
+
+if __name__ == "__main__":
+    main()

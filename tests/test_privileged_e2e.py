@@ -1,0 +1,47 @@
+"""Full-stack attach/detach against a real kernel (opt-in: GM_PRIVILEGED_TESTS=1, root).
+
+Runs tests/priv_e2e_driver.py in its own process (the mock inventory is configured through
+GM_AMDSMI_MOCK_CONFIG at amdsmi init). See the driver docstring for the setup.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = [pytest.mark.privileged,
+              pytest.mark.skipif(os.environ.get("GM_PRIVILEGED_TESTS") != "1" or os.geteuid() != 0,
+                                 reason="opt-in privileged kernel test (GM_PRIVILEGED_TESTS=1)")]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_full_stack_attach_detach_enforced_by_the_kernel(tmp_path):
+    cfg = tmp_path / "mock.json"
+    # "GPUs" whose render/card nodes are memory devices: 1:5 /dev/zero, 1:7 /dev/full,
+    # 1:8 /dev/random, 1:9 /dev/urandom (drm_major=1 in the driver); kfd → 1:0
+    cfg.write_text(json.dumps({"gpus": [
+        {"bdf": "0000:05:00.0", "render": 5, "card": 7, "numa": 0},
+        {"bdf": "0000:15:00.0", "render": 8, "card": 9, "numa": 0}]}))
+    r = subprocess.run([sys.executable, os.path.join(HERE, "priv_e2e_driver.py")],
+                       env={**os.environ, "GM_AMDSMI_MOCK_CONFIG": str(cfg)},
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    o = json.loads(r.stdout.strip().splitlines()[-1])
+    assert o["backend"] == "cgroup-v2-bpf" and o["tenant_in_cgroup"]
+    # [null, zero, full, random] as seen by a process inside the tenant's cgroup
+    assert o["before"] == "1000"                              # runc program: /dev/null only
+    assert o["add1"][0] == 200 and o["after_add1"] == "1110"  # + render 1:5, card 1:7
+    assert o["progs_after_add1"] == ["gm_devallow"]           # replaced, not stacked
+    assert o["nodes_after_add1"] == {"/dev/kfd": [1, 0], "/dev/dri/renderD5": [1, 5],
+                                     "/dev/dri/card7": [1, 7]}
+    assert o["host_dev_untouched"] and o["audit_after_add1"] == []
+    assert o["add2"][0] == 200 and o["after_add2"] == "1111"
+    assert o["remove1"] == 200 and o["after_remove1"] == "1001"
+    assert o["nodes_after_remove1"] == {"/dev/kfd": [1, 0], "/dev/dri/renderD5": None,
+                                        "/dev/dri/renderD8": [1, 8]}
+    assert o["remove2"] == 200 and o["after_remove2"] == "1000"
+    assert o["progs_final"] == ["runc_devices"]               # runtime program restored
+    assert o["nodes_final"] == {"/dev/kfd": None, "/dev/dri/renderD8": None}
+    assert o["audit_final"] == [] and o["pins_left"] == []
