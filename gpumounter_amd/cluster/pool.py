@@ -173,8 +173,10 @@ class WarmPool:
     # ------------------------------------------------------------------------ claim / return
     async def claim(self, owner: dict, n: int, entire: bool, attached: Sequence[AmdGpu],
                     attach_id: str = "", container: str = "",
-                    idempotency_key: str = "") -> Optional[Reservation]:
-        """Claim ``n`` standby GPUs for ``owner``; None if the pool cannot cover the request."""
+                    idempotency_key: str = "",
+                    want: Optional[Sequence[int]] = None) -> Optional[Reservation]:
+        """Claim ``n`` standby GPUs for ``owner`` (exactly the GPU indices ``want`` when the
+        caller planned the placement over standby ∪ free GPUs); None if the pool cannot."""
         async with self._lock:
             pool = self.standby()
             if len(pool) < n:
@@ -187,11 +189,16 @@ class WarmPool:
                 if g is not None:
                     by_gpu[g.index] = ph
                     cands.append(g)
-            plc = topology.choose(cands, n, self.inv.links(), attached=attached,
-                                  policy=self.cfg.topology_policy)
-            if plc is None:
-                return None
-            chosen = [by_gpu[i] for i in plc.chosen]
+            if want is not None:
+                if len(want) != n or any(i not in by_gpu for i in want):
+                    return None
+                chosen = [by_gpu[i] for i in want]
+            else:
+                plc = topology.choose(cands, n, self.inv.links(), attached=attached,
+                                      policy=self.cfg.topology_policy)
+                if plc is None:
+                    return None
+                chosen = [by_gpu[i] for i in plc.chosen]
             mode = "entire" if entire else "single"
             group = secrets.token_hex(4) if entire else ""
             patch = {"metadata": {

@@ -70,12 +70,15 @@ def score_set(gpus: Dict[int, AmdGpu], links: Optional[LinkMatrix], members: Seq
 
 
 def choose(candidates: Iterable[AmdGpu], n: int, links: Optional[LinkMatrix] = None,
-           attached: Iterable[AmdGpu] = (), policy: str = "xgmi") -> Optional[Placement]:
+           attached: Iterable[AmdGpu] = (), policy: str = "xgmi",
+           prefer: Iterable[int] = ()) -> Optional[Placement]:
     """Pick ``n`` GPUs out of ``candidates`` that best extend ``attached``.
 
     Returns ``None`` if fewer than ``n`` candidates exist. ``policy="first-fit"`` reproduces the
-    topology-blind behaviour (lowest indices first).
+    topology-blind behaviour (lowest indices first). Among equally scored sets the one with the
+    most ``prefer`` indices wins (warm-pool GPUs: same placement quality, lower latency).
     """
+    pref = set(prefer)
     cand = sorted({g.index: g for g in candidates}.values(), key=lambda g: g.index)
     att = sorted({g.index: g for g in attached}.values(), key=lambda g: g.index)
     if n <= 0:
@@ -95,7 +98,7 @@ def choose(candidates: Iterable[AmdGpu], n: int, links: Optional[LinkMatrix] = N
     if math.comb(len(ids), n) <= EXHAUSTIVE_LIMIT:
         for combo in itertools.combinations(ids, n):
             s = score_set(table, links, att_ids + list(combo))
-            key = (s[0], combo)
+            key = (s[0], -len(pref.intersection(combo)), combo)
             if best is None or key < best[0]:
                 best = (key, list(combo), s)
         chosen, s = best[1], best[2]
@@ -108,7 +111,7 @@ def choose(candidates: Iterable[AmdGpu], n: int, links: Optional[LinkMatrix] = N
                 if i in chosen:
                     continue
                 s = score_set(table, links, att_ids + chosen + [i])
-                key = (s[0], i)
+                key = (s[0], i not in pref, i)
                 if pick is None or key < pick[0]:
                     pick = (key, i)
             chosen.append(pick[1])

@@ -89,6 +89,11 @@ class GpuMountService:
         self.faults = faults if faults is not None else FaultInjector(cfg.fault)
         self.pool = None  # WarmPool, attached by the Worker when warm_pool_size > 0
         self.plugin = None  # AmdGpuDevicePlugin, attached by the Worker with device_plugin=1
+        # Reservations that must not interleave on a node run one at a time:
+        # * trim briefly holds every free GPU — a concurrent one would see a full node;
+        # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
+        #   two attaches' 1-GPU intents would be indistinguishable to the plugin.
+        self._node_reserve_lock = asyncio.Lock()
         self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}
         self._own: Dict[str, Tuple[str, ...]] = {}   # pod uid → its own device-plugin GPU IDs
         self.ledger_reads = 0
@@ -331,27 +336,43 @@ class GpuMountService:
                        n_free: int = 0):
         """Claim from the warm pool first (if enabled), create placeholders for the rest
         (``placement_enforce=trim``: hold every free GPU, keep the topology-chosen ones)."""
+        if self.cfg.placement_enforce != "trim" and self.plugin is None:
+            return await self._reserve_unlocked(pod, n, req, st, preferred, n_free)
+        async with self._node_reserve_lock:
+            # recompute against the ledger as it is now that we hold the node
+            free = self._free(st)
+            preferred = self._preferred(n, st, free)
+            return await self._reserve_unlocked(pod, n, req, st, preferred, len(free))
+
+    async def _reserve_unlocked(self, pod: dict, n: int, req, st: PodGpuState,
+                                preferred: List[str], n_free: int):
         claimed = None
-        if self.pool is not None and self.pool.enabled:
-            k = min(n, len(self.pool.standby()))
-            if k:
-                claimed = await self.pool.claim(pod, k, req.is_entire_mount, st.hot + st.own,
-                                                log.request_id.get(), req.container,
-                                                req.idempotency_key)
+        create_pref = preferred
+        if self.pool is not None and self.pool.enabled and self.pool.standby():
+            plan = self._plan_with_pool(n, st)
+            if plan is not None and plan[0]:
+                claim_idx, plan_pref = plan
+                claimed = await self.pool.claim(pod, len(claim_idx), req.is_entire_mount,
+                                                st.hot + st.own, log.request_id.get(),
+                                                req.container, req.idempotency_key,
+                                                want=claim_idx)
+                if claimed is not None:
+                    create_pref = plan_pref
         got = len(claimed.placeholders) if claimed else 0
         if got == n:
             return claimed
+        if got:
+            preferred = create_pref
         if not got and preferred and self.cfg.placement_enforce == "trim" and n_free > n:
             return await self._reserve_trim(pod, n, req, st, n_free)
         token = ""
-        if self.plugin is not None and preferred and not got:
+        if self.plugin is not None and preferred:
             # our own device plugin answers GetPreferredAllocation for these placeholders
             token = log.request_id.get() or secrets.token_hex(4)
             for ids in ([preferred] if req.is_entire_mount else [[d] for d in preferred]):
                 self.plugin.intend(ids, token)
         try:
-            rest = await self.ph.reserve(pod, n - got, req.is_entire_mount,
-                                         preferred if not got else [],
+            rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
                                          attach_id=log.request_id.get(),
                                          container=req.container,
                                          idempotency_key=req.idempotency_key)
@@ -371,6 +392,24 @@ class GpuMountService:
             await self.pool.give_back(phs)
         else:
             await self.ph.release(phs, wait=False)
+
+    def _plan_with_pool(self, n: int, st: PodGpuState):
+        """Place over standby ∪ free GPUs together: (standby indices to claim, device IDs to
+        create placeholders for). The pool only saves latency; it does not decide placement."""
+        keys = self.inv.by_key()
+        standby: Dict[int, AmdGpu] = {}
+        for ph in self.pool.standby():
+            g = keys.get(normalize_device_id(ph.device_ids[0])) if ph.device_ids else None
+            if g is not None:
+                standby[g.index] = g
+        cands = list(standby.values()) + [g for g in self._free(st) if g.index not in standby]
+        plc = topology.choose(cands, n, self.inv.links(), attached=st.hot + st.own,
+                              policy=self.cfg.topology_policy, prefer=standby)
+        if plc is None:
+            return None
+        by_index = {g.index: g for g in cands}
+        return ([i for i in plc.chosen if i in standby],
+                [by_index[i].bdf for i in plc.chosen if i not in standby])
 
     async def _reserve_trim(self, pod: dict, n: int, req, st: PodGpuState, width: int):
         keys = self.inv.by_key()

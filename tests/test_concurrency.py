@@ -30,7 +30,11 @@ async def check_invariants(lc, tenants):
             assert lc.cluster.get(ph.namespace, ph.name) is not None
         assert not svc.hm.audit(pod, st_.hot, st_.own), t                 # I3
     assert len(node.free_ids()) + len(node.allocated) == node.capacity   # I4
-    assert total_hot == len(node.allocated)
+    standby = sum(1 for p in lc.cluster.placeholders()                   # warm-pool capacity
+                  if (p["metadata"].get("annotations") or {}).get(
+                      "gpumounter.amd.com/mount-mode") == "standby"
+                  and not p["metadata"].get("deletionTimestamp"))
+    assert total_hot + standby == len(node.allocated)
 
 
 def test_four_pods_contending_for_eight_gpus():
@@ -117,4 +121,40 @@ def test_1000_attach_detach_cycles_leave_no_orphans():
             assert lc.cluster.placeholders() == []
             lat.sort()
             assert lat[int(0.99 * len(lat))] < 1000   # generous bound on the CPU sandbox
+    asyncio.run(main())
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("mode", ["trim", "device_plugin", "warm_pool"])
+def test_contention_under_each_placement_mode(mode):
+    """The 4-pods-for-8-GPUs contract holds whatever enforces the placement."""
+    kw = {"trim": dict(alloc_policy="blind", worker_overrides={"placement_enforce": "trim"}),
+          "device_plugin": dict(device_plugin=True),
+          "warm_pool": dict(worker_overrides={"warm_pool_size": 4})}[mode]
+
+    async def main():
+        async with LocalCluster(**kw) as lc:
+            tenants = [f"t{i}" for i in range(4)]
+            for t in tenants:
+                lc.tenant(t)
+            if mode == "warm_pool":
+                pool = lc.nodes["node-0"].worker.pool
+                for _ in range(500):
+                    if len(pool.standby()) >= 4:
+                        break
+                    await asyncio.sleep(0.01)
+            res = await asyncio.gather(*[lc.add("default", t, 3) for t in tenants])
+            codes = [c for c, _ in res]
+            assert codes.count(200) == 2 and set(codes) == {200, 500}, codes
+            await asyncio.sleep(0.05)
+            await check_invariants(lc, tenants)
+            for t, (c, b) in zip(tenants, res):
+                if c == 200:
+                    assert len({d["numa_node"] for d in b["devices"]}) == 1, b["devices"]
+                    assert (await lc.remove("default", t, [d["uuid"] for d in b["devices"]]))[0] \
+                        == 200
+            await asyncio.sleep(0.05)
+            await check_invariants(lc, tenants)
     asyncio.run(main())
