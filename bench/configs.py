@@ -1,0 +1,203 @@
+"""BASELINE.json's named configurations as runnable scenarios (one JSON line each).
+
+  scale       "scale one Pod 1→8 MI355X then back to 0 (xGMI-hive-aware attach order)":
+              per-step attach/detach latency plus the topology of the attached set.
+  contention  "4 Pods contending for 8 MI355X; k8s scheduler ledger stays consistent":
+              concurrent rounds of adds/removes from 4 pods, invariant checks after each round.
+  soak        "1000 attach/detach cycles across 8 GPUs; p99 latency + zero orphaned cgroup
+              entries": cycles of 1-4 GPUs, single and entire mounts, final orphan audit.
+
+The control plane is the hermetic fake (apiserver, scheduler, kubelet); node operations are the
+production ones (cgroup rule backends, device-node writer) in their unprivileged modes. Runs
+with the real libamd_smi when GPUs are present (``--amdsmi ""``) or the bundled 8×MI355X mock.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from gpumounter_amd.fakes.apiserver import LatencyModel  # noqa: E402
+from gpumounter_amd.fakes.harness import LocalCluster  # noqa: E402
+from gpumounter_amd.hw import topology  # noqa: E402
+from gpumounter_amd.utils import log  # noqa: E402
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    return xs[min(int(q * len(xs)), len(xs) - 1)] if xs else None
+
+
+async def invariants(lc, tenants) -> int:
+    """Number of violated ledger invariants (0 = consistent)."""
+    bad = 0
+    node = lc.nodes["node-0"].node
+    held = list(node.allocated)
+    bad += len(held) != len(set(held))
+    svc = lc.nodes["node-0"].worker.service
+    hot = 0
+    for t in tenants:
+        pod = lc.cluster.get("default", t)
+        st = await svc.pod_state(pod)
+        hot += len(st.hot)
+        bad += len(svc.hm.audit(pod, st.hot, st.own))
+    standby = sum(1 for p in lc.cluster.placeholders()
+                  if (p["metadata"].get("annotations") or {}).get(
+                      "gpumounter.amd.com/mount-mode") == "standby")
+    bad += hot + standby != len(node.allocated)
+    bad += len(node.free_ids()) + len(node.allocated) != node.capacity
+    return bad
+
+
+async def scale(lc, args) -> dict:
+    lc.tenant("scaler")
+    inv = lc.inventory
+    steps = []
+    uuids = []
+    n_gpus = len(lc.nodes["node-0"].node.gpus)
+    for k in range(1, n_gpus + 1):
+        t0 = time.perf_counter()
+        code, b = await lc.add("default", "scaler", 1)
+        ms = (time.perf_counter() - t0) * 1e3
+        if code != 200:
+            raise RuntimeError(f"attach #{k}: {code} {b}")
+        uuids.append(b["devices"][0]["uuid"])
+        svc = lc.nodes["node-0"].worker.service
+        st = await svc.pod_state(lc.cluster.get("default", "scaler"))
+        table = {g.index: g for g in st.hot}
+        s, hives, numa, non_xgmi = topology.score_set(table, inv.links(), sorted(table))
+        steps.append({"gpus": k, "attach_ms": round(ms, 3), "added": b["devices"][0]["bdf"],
+                      "numa_nodes": numa, "hives": hives, "non_xgmi_pairs": non_xgmi})
+    down = []
+    for k, u in enumerate(reversed(uuids)):
+        t0 = time.perf_counter()
+        code, _ = await lc.remove("default", "scaler", [u])
+        down.append(round((time.perf_counter() - t0) * 1e3, 3))
+        if code != 200:
+            raise RuntimeError(f"detach #{k}: {code}")
+    # NUMA nodes may only be crossed once the first socket is full
+    per_numa = {}
+    for g in lc.nodes["node-0"].node.gpus:
+        per_numa[g.numa_node] = per_numa.get(g.numa_node, 0) + 1
+    first = max(per_numa.values())
+    numa_ok = all(s["numa_nodes"] == 1 for s in steps[:first])
+    return {"steps": steps, "detach_ms": down, "numa_packed": numa_ok,
+            "audit_issues": len(await lc.audit("default", "scaler")),
+            "placeholders_left": len(lc.cluster.placeholders())}
+
+
+async def contention(lc, args) -> dict:
+    tenants = [f"c{i}" for i in range(4)]
+    for t in tenants:
+        lc.tenant(t)
+    rnd = random.Random(args.seed)
+    svc = lc.nodes["node-0"].worker.service
+    ok = fail = 0
+    lat = []
+    violations = 0
+    t_start = time.perf_counter()
+    for _ in range(args.rounds):
+        async def op(t):
+            nonlocal ok, fail
+            st = await svc.pod_state(lc.cluster.get("default", t))
+            if st.hot and rnd.random() < 0.5:
+                ids = [g.uuid for g in st.hot] if st.mount_type.value == "entire-mount" else \
+                    [g.uuid for g in rnd.sample(st.hot, rnd.randint(1, len(st.hot)))]
+                code, _ = await lc.remove("default", t, ids, force=True)
+            else:
+                t0 = time.perf_counter()
+                code, _ = await lc.add("default", t, rnd.randint(1, 4),
+                                       entire=rnd.random() < 0.3)
+                if code == 200:
+                    lat.append((time.perf_counter() - t0) * 1e3)
+            if code == 200:
+                ok += 1
+            else:
+                fail += 1
+        await asyncio.gather(*[op(t) for t in tenants])
+        violations += await invariants(lc, tenants)
+    elapsed = time.perf_counter() - t_start
+    return {"rounds": args.rounds, "ops_ok": ok, "ops_refused": fail,
+            "ops_per_s": round((ok + fail) / elapsed, 1),
+            "attach_p50_ms": round(pct(lat, 0.5), 3) if lat else None,
+            "attach_p99_ms": round(pct(lat, 0.99), 3) if lat else None,
+            "invariant_violations": violations}
+
+
+async def soak(lc, args) -> dict:
+    for i in range(2):
+        lc.tenant(f"s{i}")
+    att, det = [], []
+    for k in range(args.cycles):
+        t = f"s{k % 2}"
+        n = (k % 4) + 1
+        t0 = time.perf_counter()
+        code, b = await lc.add("default", t, n, entire=k % 3 == 0)
+        t1 = time.perf_counter()
+        if code != 200:
+            raise RuntimeError(f"cycle {k}: {code} {b}")
+        code, _ = await lc.remove("default", t, [d["uuid"] for d in b["devices"]])
+        if code != 200:
+            raise RuntimeError(f"cycle {k} detach: {code}")
+        att.append((t1 - t0) * 1e3)
+        det.append((time.perf_counter() - t1) * 1e3)
+    node = lc.nodes["node-0"].node
+    orphan_nodes = sum(len(node.container_devices(c)) for t in ("s0", "s1")
+                       for c in lc.container_ids("default", t))
+    orphan_rules = 0
+    for t in ("s0", "s1"):
+        orphan_rules += len(await lc.audit("default", t))
+    return {"cycles": args.cycles, "attach_p50_ms": round(pct(att, 0.5), 3),
+            "attach_p99_ms": round(pct(att, 0.99), 3), "detach_p50_ms": round(pct(det, 0.5), 3),
+            "detach_p99_ms": round(pct(det, 0.99), 3), "orphaned_cgroup_entries": orphan_rules,
+            "orphaned_device_nodes": orphan_nodes,
+            "placeholders_left": len(lc.cluster.placeholders()),
+            "gpus_still_allocated": len(node.allocated)}
+
+
+SCENARIOS = {"scale": scale, "contention": contention, "soak": soak}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("scenario", choices=sorted(SCENARIOS))
+    ap.add_argument("--amdsmi", default="mock", help='"mock" (default) or "" for libamd_smi')
+    ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
+    ap.add_argument("--latency", choices=("zero", "realistic"), default="zero")
+    ap.add_argument("--placement", choices=("hint", "trim"), default="hint")
+    ap.add_argument("--device-plugin", action="store_true")
+    ap.add_argument("--warm-pool", type=int, default=0)
+    ap.add_argument("--rounds", type=int, default=50)
+    ap.add_argument("--cycles", type=int, default=1000)
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+    log.setup("WARNING", json_format=False)
+
+    async def run():
+        lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
+        async with LocalCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, latency=lat,
+                                device_plugin=args.device_plugin,
+                                worker_overrides={"placement_enforce": args.placement,
+                                                  "warm_pool_size": args.warm_pool}) as lc:
+            res = await SCENARIOS[args.scenario](lc, args)
+            gpus = lc.nodes["node-0"].node.gpus
+            res["config"] = {"scenario": args.scenario, "amdsmi": args.amdsmi or "libamd_smi",
+                             "node_gpus": len(gpus),
+                             "gfx": sorted({g.gfx_target for g in gpus}),
+                             "cgroup": args.cgroup, "latency": args.latency,
+                             "placement": args.placement, "device_plugin": args.device_plugin,
+                             "warm_pool": args.warm_pool}
+            return res
+
+    print(json.dumps(asyncio.run(run())))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -49,3 +49,23 @@ def test_bench_two_rank_distributed_launch():
     d = _last_json(res.stdout)
     assert d["n_gpus"] == 2 and d["config"]["gpus_per_pod"] == 2
     assert d["ledger_audit_issues"] == 0
+
+
+def test_baseline_config_scenarios_run_and_hold_invariants():
+    """bench/configs.py: the BASELINE.json scenarios (short runs) report consistent ledgers."""
+    import json as _json
+    import subprocess as _sp
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for sc, extra in (("scale", []), ("contention", ["--rounds", "8"]),
+                      ("soak", ["--cycles", "40"])):
+        r = _sp.run([_sys.executable, os.path.join(root, "bench", "configs.py"), sc] + extra,
+                    capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[sc] = _json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["scale"]["numa_packed"] and out["scale"]["audit_issues"] == 0
+    assert [s["gpus"] for s in out["scale"]["steps"]] == list(range(1, 9))
+    assert out["contention"]["invariant_violations"] == 0
+    assert out["soak"]["orphaned_cgroup_entries"] == 0 == out["soak"]["orphaned_device_nodes"]
+    assert out["soak"]["placeholders_left"] == 0 == out["soak"]["gpus_still_allocated"]
