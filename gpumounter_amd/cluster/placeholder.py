@@ -67,6 +67,8 @@ class Placeholder:
 @dataclass
 class Reservation:
     placeholders: List[Placeholder] = field(default_factory=list)
+    # the device set placement asked for (empty: no preference) — for the mismatch metric
+    preferred: List[str] = field(default_factory=list)
 
     @property
     def device_ids(self) -> List[str]:

@@ -290,8 +290,9 @@ class GpuMountService:
             for ph in res.placeholders:
                 for d in ph.device_ids:
                     owner[keys[normalize_device_id(d)].index] = ph.name
-            if preferred and sorted(normalize_device_id(d) for d in res.device_ids) != \
-                    sorted(normalize_device_id(d) for d in preferred):
+            want = res.preferred or preferred
+            if want and sorted(normalize_device_id(d) for d in res.device_ids) != \
+                    sorted(normalize_device_id(d) for d in want):
                 self.metrics.placement_mismatch.inc()
             try:
                 with trace.span("mount", gpus=len(new)):
@@ -342,7 +343,10 @@ class GpuMountService:
             # recompute against the ledger as it is now that we hold the node
             free = self._free(st)
             preferred = self._preferred(n, st, free)
-            return await self._reserve_unlocked(pod, n, req, st, preferred, len(free))
+            res = await self._reserve_unlocked(pod, n, req, st, preferred, len(free))
+            if not res.preferred:
+                res.preferred = list(preferred)
+            return res
 
     async def _reserve_unlocked(self, pod: dict, n: int, req, st: PodGpuState,
                                 preferred: List[str], n_free: int):
@@ -360,6 +364,7 @@ class GpuMountService:
                     create_pref = plan_pref
         got = len(claimed.placeholders) if claimed else 0
         if got == n:
+            claimed.preferred = claimed.device_ids       # claimed by exact device
             return claimed
         if got:
             preferred = create_pref
@@ -385,6 +390,9 @@ class GpuMountService:
                 self.plugin.withdraw(token)
         if claimed:
             rest.placeholders = claimed.placeholders + rest.placeholders
+            rest.preferred = claimed.device_ids + list(preferred) if preferred else []
+        else:
+            rest.preferred = list(preferred)
         return rest
 
     async def _release(self, phs) -> None:
@@ -426,6 +434,7 @@ class GpuMountService:
         res, surplus = await self.ph.reserve_trim(
             pod, n, req.is_entire_mount, width, pick, attach_id=log.request_id.get(),
             container=req.container, idempotency_key=req.idempotency_key)
+        res.preferred = res.device_ids                    # trim keeps exactly what it picked
         if surplus:
             with trace.span("placement_release", placeholders=len(surplus)):
                 try:
