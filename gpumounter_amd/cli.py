@@ -48,6 +48,39 @@ def cmd_worker(args) -> int:
     return 0
 
 
+def cmd_device_plugin(args) -> int:
+    """Standalone amd.com/gpu device plugin (topology-packed allocation for ordinary pods, no
+    hot-mount worker). Runs until SIGTERM/SIGINT."""
+    import signal
+
+    from gpumounter_amd.deviceplugin.plugin import AmdGpuDevicePlugin
+    from gpumounter_amd.hw.inventory import Inventory
+    from gpumounter_amd.utils import log
+
+    cfg = _cfg(args)
+    log.setup(cfg.log_level, cfg.log_json, cfg.log_file)
+    inv = Inventory(args.amdsmi if args.amdsmi is not None else cfg.amdsmi_lib, cfg.kfd_major,
+                    cfg.kfd_dev_path)
+
+    async def run():
+        plugin = AmdGpuDevicePlugin(inv, cfg.resource_name, args.dir or cfg.device_plugin_dir,
+                                    inject_devices=cfg.device_plugin_inject,
+                                    health_period_s=cfg.device_plugin_health_s,
+                                    policy=cfg.topology_policy)
+        await plugin.start(register=not args.no_register)
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            loop.add_signal_handler(sig, stop.set)
+        print(json.dumps({"socket": plugin.socket_path, "devices": len(plugin.health)}),
+              flush=True)
+        await stop.wait()
+        await plugin.stop()
+
+    asyncio.run(run())
+    return 0
+
+
 def cmd_inventory(args) -> int:
     from gpumounter_amd.hw.inventory import Inventory
 
@@ -186,6 +219,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--node")
     p.add_argument("--port", type=int)
     p.set_defaults(fn=cmd_worker)
+    p = sub.add_parser("device-plugin")
+    p.add_argument("--config")
+    p.add_argument("--amdsmi", default=None)
+    p.add_argument("--dir", default="", help="kubelet device-plugin directory")
+    p.add_argument("--no-register", action="store_true", help="serve only (testing)")
+    p.set_defaults(fn=cmd_device_plugin)
     p = sub.add_parser("inventory")
     p.add_argument("--amdsmi", default="")
     p.add_argument("--processes", action="store_true")

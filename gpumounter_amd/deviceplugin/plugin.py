@@ -47,7 +47,7 @@ class AmdGpuDevicePlugin:
     def __init__(self, inv, resource: str = "amd.com/gpu",
                  plugin_dir: str = dp.DEVICE_PLUGIN_DIR, socket_name: str = "gpumounter-amd.sock",
                  inject_devices: bool = True, health_period_s: float = 5.0,
-                 policy: str = "xgmi", intent_ttl_s: float = 60.0) -> None:
+                 policy: str = "xgmi", intent_ttl_s: float = 60.0, metrics=None) -> None:
         self.inv = inv
         self.resource = resource
         self.plugin_dir = plugin_dir
@@ -62,10 +62,16 @@ class AmdGpuDevicePlugin:
         self.registered = 0
         self.calls: Dict[str, int] = {"Allocate": 0, "GetPreferredAllocation": 0,
                                       "ListAndWatch": 0, "steered": 0}
+        self.metrics = metrics
         self._subs: set = set()   # one event per open ListAndWatch stream
         self._tasks: List[asyncio.Task] = []
         self._sock_ino = 0
         self._stopping = False
+
+    def _count(self, rpc: str) -> None:
+        self.calls[rpc] += 1
+        if self.metrics is not None:
+            self.metrics.plugin_rpcs.labels(rpc=rpc).inc()
 
     # ------------------------------------------------------------------------ identity
     @property
@@ -106,7 +112,7 @@ class AmdGpuDevicePlugin:
             if len(it.ids) == size and all(d in avail for d in it.ids) and \
                     set(must_n) <= set(it.ids):
                 del self.intents[i]
-                self.calls["steered"] += 1
+                self._count("steered")
                 return [avail[d] for d in it.ids]
         cands = [g for d in avail if d not in must_n for g in [self._gpu(d)] if g is not None
                  and self.health.get(g.index, True)]
@@ -129,7 +135,7 @@ class AmdGpuDevicePlugin:
             ev.set()
 
     async def _list_and_watch(self, req, ctx):
-        self.calls["ListAndWatch"] += 1
+        self._count("ListAndWatch")
         ev = asyncio.Event()
         self._subs.add(ev)
         try:
@@ -141,7 +147,7 @@ class AmdGpuDevicePlugin:
             self._subs.discard(ev)
 
     async def _preferred(self, req, ctx):
-        self.calls["GetPreferredAllocation"] += 1
+        self._count("GetPreferredAllocation")
         resp = dp.PreferredAllocationResponse()
         for cr in req.container_requests:
             ids = self.prefer(list(cr.available_deviceIDs), list(cr.must_include_deviceIDs),
@@ -150,7 +156,7 @@ class AmdGpuDevicePlugin:
         return resp
 
     async def _allocate(self, req, ctx):
-        self.calls["Allocate"] += 1
+        self._count("Allocate")
         resp = dp.AllocateResponse()
         for cr in req.container_requests:
             c = resp.container_responses.add()

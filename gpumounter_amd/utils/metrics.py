@@ -34,6 +34,11 @@ class Metrics:
                                           registry=r)
         self.gpu_busy = Gauge("gm_gpu_processes", "processes on a GPU (amdsmi)", ["gpu"],
                               registry=r)
+        self.plugin_rpcs = Counter("gm_device_plugin_rpcs_total",
+                                   "device-plugin RPCs served (steered = intent consumed)",
+                                   ["rpc"], registry=r)
+        self.plugin_healthy = Gauge("gm_device_plugin_healthy_gpus",
+                                    "GPUs advertised Healthy", registry=r)
         self.http_requests = Counter("gm_http_requests_total", "master HTTP requests",
                                      ["route", "code"], registry=r)
 

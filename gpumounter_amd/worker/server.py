@@ -84,7 +84,8 @@ class Worker:
             self.plugin = AmdGpuDevicePlugin(
                 self.inv, cfg.resource_name, cfg.device_plugin_dir,
                 inject_devices=cfg.device_plugin_inject,
-                health_period_s=cfg.device_plugin_health_s, policy=cfg.topology_policy)
+                health_period_s=cfg.device_plugin_health_s, policy=cfg.topology_policy,
+                metrics=self.metrics)
             self.service.plugin = self.plugin
         self.reconciler = Reconciler(self.service, cfg.reconcile_period_s)
         if cfg.reconcile_on_events:
@@ -200,6 +201,8 @@ class Worker:
             await asyncio.sleep(self.cfg.metrics_period_s)
 
     async def collect_metrics(self) -> None:
+        if self.plugin is not None:
+            self.metrics.plugin_healthy.set(sum(1 for v in self.plugin.health.values() if v))
         for g in self.inv.gpus():
             try:
                 n = len(self.inv.processes(g.index))

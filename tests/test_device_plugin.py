@@ -111,3 +111,45 @@ def test_plugin_reregisters_after_kubelet_restart():
         lc.tenant("t")
         assert (await lc.add("default", "t", 2))[0] == 200
     run(body)
+
+
+def test_standalone_device_plugin_cli_serves_the_api(tmp_path):
+    """python -m gpumounter_amd device-plugin: the plugin without a worker."""
+    import subprocess
+    import sys
+
+    d = tmp_path / "dp"
+    d.mkdir()
+    proc = subprocess.Popen([sys.executable, "-m", "gpumounter_amd", "device-plugin",
+                             "--amdsmi", "mock", "--dir", str(d), "--no-register"],
+                            stdout=subprocess.PIPE, text=True,
+                            env={**os.environ, "GM_LOG_JSON": "0"})
+    try:
+        line = proc.stdout.readline()
+        info = __import__("json").loads(line)
+        assert info["devices"] == 8
+
+        async def call():
+            async with grpc.aio.insecure_channel(f"unix://{info['socket']}") as ch:
+                law = ch.unary_stream(dp.LIST_AND_WATCH, dp.Empty.SerializeToString,
+                                      dp.ListAndWatchResponse.FromString)
+                async for resp in law(dp.Empty()):
+                    return resp
+        resp = asyncio.run(call())
+        assert len(resp.devices) == 8 and all(x.health == dp.HEALTHY for x in resp.devices)
+        assert {x.topology.nodes[0].ID for x in resp.devices} == {0, 1}
+    finally:
+        proc.terminate()
+        assert proc.wait(timeout=20) == 0
+
+
+def test_worker_exports_device_plugin_metrics():
+    async def body(lc):
+        lc.tenant("t")
+        assert (await lc.add("default", "t", 2))[0] == 200
+        w = lc.nodes["node-0"].worker
+        await w.collect_metrics()
+        text = w.metrics.render().decode()
+        assert 'gm_device_plugin_rpcs_total{rpc="Allocate"} 2.0' in text
+        assert "gm_device_plugin_healthy_gpus 8.0" in text
+    run(body)
