@@ -33,11 +33,13 @@ int gm_probe_find_device(const char* bdf, int* dev);
 int gm_probe_quick(int dev, int* ok, double* elapsed_us);
 // HBM3E stream: float4 copy of `bytes` for `iters`; *gbps = (read+write) bytes / time.
 int gm_probe_hbm_copy(int dev, uint64_t bytes, int iters, double* gbps);
-// Tuning variants: variant 0 grid-stride, 1 chunked 4×16B/lane, 2 chunked + nontemporal.
+// Tuning variants: 0 grid-stride, 1 chunked 4×16B/lane, 2 chunked 4 + nontemporal,
+// 3 chunked 8 + nontemporal, 4 chunked 8.
 int gm_probe_hbm_copy_variant(int dev, int variant, uint64_t bytes, int iters,
                               int blocks_per_cu, double* gbps);
-// shape16=1: v_mfma_f32_16x16x32_bf16, 0: v_mfma_f32_32x32x16_bf16.
-int gm_probe_mfma_peak_variant(int dev, int shape16, int iters, int blocks_per_cu,
+// variant 0: v_mfma_f32_32x32x16_bf16 × 4 chains, 1: v_mfma_f32_16x16x32_bf16 × 4 chains,
+// 2: 16x16x32 × 8 chains.
+int gm_probe_mfma_peak_variant(int dev, int variant, int iters, int blocks_per_cu,
                                double* tflops);
 // MFMA bf16 (v_mfma_f32_32x32x16_bf16) register-resident peak; *tflops dense.
 int gm_probe_mfma_peak(int dev, int iters, double* tflops);
