@@ -434,31 +434,11 @@ int gm_probe_hbm_copy(int dev, uint64_t bytes, int iters, double* gbps) {
   return gm_probe_hbm_copy_variant(dev, 2, bytes, iters, 8, gbps);
 }
 
+// Default MFMA peak = the measured-best form on MI355X (profiles/r1_gpu_b/probe_sweep.json):
+// v_mfma_f32_16x16x32_bf16, 8 dst-tied chains per wave, 8 blocks/CU → 2.45 PF/s
+// (≈98 % of the 2.5 PF/s dense bf16 peak) vs 2.0-2.16 PF/s for 32x32x16 × 4 chains.
 int gm_probe_mfma_peak(int dev, int iters, double* tflops) {
-  *tflops = 0;
-  DeviceGuard g(dev);
-  if (!g.ok) return (int)hipErrorInvalidDevice;
-  hipDeviceProp_t p;
-  GM_CHECK(hipGetDeviceProperties(&p, dev));
-  float* out = nullptr;
-  GM_CHECK(hipMalloc(&out, 2 * sizeof(float)));
-  const int blocks = p.multiProcessorCount * 4;  // 4 blocks × 4 waves = 4 waves per SIMD
-  hipEvent_t a, b;
-  (void)hipEventCreate(&a);
-  (void)hipEventCreate(&b);
-  hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(256), 0, 0, out, 64, 1e-3f);  // warm
-  (void)hipEventRecord(a, 0);
-  hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(256), 0, 0, out, iters, 1e-3f);
-  (void)hipEventRecord(b, 0);
-  hipError_t e = hipEventSynchronize(b);
-  float ms = 0;
-  if (e == hipSuccess) e = hipEventElapsedTime(&ms, a, b);
-  const double flops = 2.0 * 32 * 32 * 16 * 4.0 * iters * (double)blocks * 4 /* waves */;
-  if (e == hipSuccess && ms > 0) *tflops = flops / (ms * 1e-3) / 1e12;
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
-  (void)hipFree(out);
-  return (int)e;
+  return gm_probe_mfma_peak_variant(dev, 2, iters, 8, tflops);
 }
 
 int gm_probe_gemm_bf16(const void* A, const void* B, float* C, int M, int N, int K,

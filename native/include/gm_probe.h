@@ -41,7 +41,7 @@ int gm_probe_hbm_copy_variant(int dev, int variant, uint64_t bytes, int iters,
 // 2: 16x16x32 × 8 chains.
 int gm_probe_mfma_peak_variant(int dev, int variant, int iters, int blocks_per_cu,
                                double* tflops);
-// MFMA bf16 (v_mfma_f32_32x32x16_bf16) register-resident peak; *tflops dense.
+// MFMA bf16 register-resident peak (best measured form: 16x16x32 × 8 chains); *tflops dense.
 int gm_probe_mfma_peak(int dev, int iters, double* tflops);
 // C[M,N] (fp32) = A[M,K] (bf16, row-major) · B[K,N] (bf16, row-major) on MFMA.
 // Requires M%64 == 0, N%64 == 0, K%32 == 0 (checked). Device pointers; stream may be NULL.
