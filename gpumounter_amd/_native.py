@@ -148,6 +148,8 @@ def host() -> C.CDLL:
         lib.gm_proc_signal.argtypes = [C.POINTER(C.c_int32), C.c_int, C.c_int, C.POINTER(C.c_int)]
         lib.gm_proc_dev_users.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_int32), C.c_int,
                                           C.POINTER(C.c_int)]
+        lib.gm_proc_scan_devs.argtypes = [C.POINTER(C.c_int32), C.c_int, C.POINTER(C.c_uint32),
+                                          C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         lib.gm_proc_filter_dev_users.argtypes = [C.POINTER(C.c_int32), C.c_int, C.c_uint32,
                                                  C.c_uint32, C.POINTER(C.c_int32)]
         lib.gm_proc_read_pids.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.c_int,

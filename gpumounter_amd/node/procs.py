@@ -14,7 +14,7 @@ import asyncio
 import ctypes as C
 import os
 import signal
-from typing import Dict, Iterable, List, Sequence
+from typing import Dict, Iterable, List, Sequence, Tuple
 
 from gpumounter_amd import _native
 from gpumounter_amd.hw.inventory import Inventory
@@ -50,23 +50,45 @@ def filter_dev_users(pids: Sequence[int], major: int, minor: int) -> List[int]:
     return [int(out[i]) for i in range(k)]
 
 
+def scan_devs(pids: Sequence[int], devs: Sequence[Tuple[int, int]]
+              ) -> Tuple[List[List[bool]], List[int]]:
+    """One read of each PID's fd table: (hits[pid][dev], PIDs whose table was unreadable)."""
+    n, k = len(pids), len(devs)
+    if not n or not k:
+        return [[False] * k for _ in range(n)], []
+    arr = (C.c_int32 * n)(*pids)
+    mm = (C.c_uint32 * (2 * k))(*[v for d in devs for v in d])
+    hits = (C.c_uint8 * (n * k))()
+    bad = (C.c_int32 * n)()
+    nbad = _native.host().gm_proc_scan_devs(arr, n, mm, k, hits, bad)
+    if nbad < 0:
+        raise OSError(-nbad, os.strerror(-nbad))
+    return ([[bool(hits[i * k + j]) for j in range(k)] for i in range(n)],
+            [int(bad[i]) for i in range(nbad)])
+
+
 def busy_pids(inv: Inventory, gpus: Sequence[AmdGpu], container_pids: Iterable[int],
-              drm_major: int = DRM_MAJOR) -> Dict[int, List[int]]:
+              drm_major: int = DRM_MAJOR, mode: str = "auto") -> Dict[int, List[int]]:
     """GPU index → container PIDs that hold that GPU.
 
-    Union of two sources: amdsmi's per-GPU process table (KFD contexts; may be filtered for an
-    unprivileged caller) and an fd scan of *only the container's* PIDs for the GPU's render node
-    (every HIP process keeps ``/dev/dri/renderD<N>`` open).
+    Primary source: one scan of *only the container's* PIDs for the GPUs' render nodes. A
+    process cannot use a GPU without that fd (KFD binds a GPU's VM through its DRM render fd,
+    and ROCr keeps it open for the process lifetime), so when every fd table is readable the
+    scan is complete. amdsmi's per-GPU process table (KFD contexts, host PIDs) covers the PIDs
+    whose fd table could not be read; ``mode="both"`` always takes the union (slower: amdsmi
+    walks every KFD process on the node).
     """
     cpids = sorted(set(container_pids))
+    hits, unreadable = scan_devs(cpids, [(drm_major, g.render_minor) for g in gpus])
+    ask = set(cpids) if mode == "both" else set(unreadable)
     out: Dict[int, List[int]] = {}
-    for g in gpus:
-        try:
-            smi = set(p.pid for p in inv.processes(g.index))
-        except NotImplementedError:
-            smi = set()
-        hit = set(cpids).intersection(smi)
-        hit.update(filter_dev_users(cpids, drm_major, g.render_minor))
+    for j, g in enumerate(gpus):
+        hit = {cpids[i] for i in range(len(cpids)) if hits[i][j]}
+        if ask:
+            try:
+                hit.update(ask.intersection(p.pid for p in inv.processes(g.index)))
+            except NotImplementedError:
+                pass
         if hit:
             out[g.index] = sorted(hit)
     return out

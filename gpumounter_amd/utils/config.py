@@ -77,6 +77,9 @@ class Config:
     placement_enforce: str = "hint"
     ledger_get: bool = True
     reconcile_on_events: bool = True
+    # auto: fd scan of the container's PIDs, amdsmi only for PIDs whose fd table is unreadable;
+    # both: always union with amdsmi's process table
+    busy_detection: str = "auto"
     # serve amd.com/gpu ourselves (replaces the ROCm device plugin on the node) so
     # GetPreferredAllocation steers placeholders to the topology-chosen GPUs
     device_plugin: bool = False
@@ -156,6 +159,7 @@ class Config:
         _choice("devnode_mode", self.devnode_mode, ("procroot", "setns", "emulate"))
         _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
         _choice("placement_enforce", self.placement_enforce, ("hint", "trim"))
+        _choice("busy_detection", self.busy_detection, ("auto", "both"))
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))
         _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
         if not (0 < self.worker_port < 65536 and 0 <= self.master_port < 65536):

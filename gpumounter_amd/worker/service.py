@@ -504,7 +504,8 @@ class GpuMountService:
                     self.faults.check("busy_check")
                     targets = self.hm.targets(pod, req.container)
                     cpids = sorted({p for t in targets for p in t.pids})
-                    busy = procs.busy_pids(self.inv, selected, cpids, self.cfg.drm_major)
+                    busy = procs.busy_pids(self.inv, selected, cpids, self.cfg.drm_major,
+                                           self.cfg.busy_detection)
             except (MountError, InjectedFault) as e:
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             if busy and not req.force:

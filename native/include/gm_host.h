@@ -112,6 +112,11 @@ int gm_proc_signal(const int32_t* pids, int n, int sig, int* results);
 int gm_proc_dev_users(uint32_t major, uint32_t minor, int32_t* pids, int cap, int* n);
 // Of `pids`, those holding an fd on char device major:minor (scans only /proc/<pid>/fd of the
 // given PIDs — cheap and exact for one container). Returns the count written to `out`.
+// One pass over each PID's fd table for up to 256 char devices (majmin = [maj0,min0,maj1,...]):
+// hits[i*ndev + j] = 1 if pids[i] holds devs[j] open. Returns how many PIDs' fd tables could
+// not be read (listed in `unreadable`, capacity n); exited PIDs count as holding nothing.
+int gm_proc_scan_devs(const int32_t* pids, int n, const uint32_t* majmin, int ndev,
+                      uint8_t* hits, int32_t* unreadable);
 int gm_proc_filter_dev_users(const int32_t* pids, int n, uint32_t major, uint32_t minor,
                              int32_t* out);
 // Parses a cgroup.procs-style file. *n = total.

@@ -884,7 +884,41 @@ bool pid_uses_dev(long pid, dev_t want) {
   closedir(fds);
   return hit;
 }
+// 1 = fd table read, 0 = process gone, -1 = not readable (permission).
+int pid_scan_devs(long pid, const dev_t* want, int ndev, uint8_t* hits) {
+  char p[64];
+  snprintf(p, sizeof(p), "/proc/%ld/fd", pid);
+  int dfd = open(p, O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (dfd < 0) return errno == ENOENT || errno == ESRCH ? 0 : -1;
+  DIR* fds = fdopendir(dfd);
+  if (!fds) {
+    close(dfd);
+    return -1;
+  }
+  struct dirent* fe;
+  while ((fe = readdir(fds)) != nullptr) {
+    if (fe->d_name[0] == '.') continue;
+    struct stat st;
+    if (fstatat(dirfd(fds), fe->d_name, &st, 0) != 0 || !S_ISCHR(st.st_mode)) continue;
+    for (int j = 0; j < ndev; ++j)
+      if (st.st_rdev == want[j]) hits[j] = 1;
+  }
+  closedir(fds);
+  return 1;
+}
 }  // namespace
+
+int gm_proc_scan_devs(const int32_t* pids, int n, const uint32_t* majmin, int ndev,
+                      uint8_t* hits, int32_t* unreadable) {
+  if (n < 0 || ndev < 0 || ndev > 256) return -EINVAL;
+  dev_t want[256];
+  for (int j = 0; j < ndev; ++j) want[j] = makedev(majmin[2 * j], majmin[2 * j + 1]);
+  memset(hits, 0, (size_t)n * (size_t)ndev);
+  int bad = 0;
+  for (int i = 0; i < n; ++i)
+    if (pid_scan_devs(pids[i], want, ndev, hits + (size_t)i * ndev) < 0) unreadable[bad++] = pids[i];
+  return bad;
+}
 
 int gm_proc_filter_dev_users(const int32_t* pids, int n, uint32_t maj, uint32_t min,
                              int32_t* out) {

@@ -245,6 +245,45 @@ def test_host_signal_and_pid_helpers():
         os.close(fd)
 
 
+def test_scan_devs_reads_each_fd_table_once_for_many_devices():
+    from gpumounter_amd.node import procs
+
+    fz = os.open("/dev/zero", os.O_RDONLY)
+    sleeper = subprocess.Popen(["sleep", "30"], stdin=subprocess.DEVNULL)
+    try:
+        hits, unreadable = procs.scan_devs([os.getpid(), sleeper.pid, 2 ** 22 + 9],
+                                           [(1, 5), (1, 7), (1, 3)])
+        assert hits[0][0] and not hits[0][1]              # we hold /dev/zero, not /dev/full
+        assert hits[1][2] and not hits[1][0]              # the sleeper's stdin is /dev/null
+        assert hits[2] == [False, False, False]           # exited PID: holds nothing
+        assert unreadable == []
+    finally:
+        os.close(fz)
+        sleeper.kill()
+        sleeper.wait()
+
+
+def test_busy_pids_auto_skips_amdsmi_when_fd_tables_are_readable(mock_inventory):
+    from gpumounter_amd.node import procs
+
+    inv = mock_inventory
+    calls = []
+    real = inv.processes
+
+    def spy(i, *a, **k):
+        calls.append(i)
+        return real(i, *a, **k)
+    inv.processes = spy
+    try:
+        g = inv.gpus()[0]
+        assert procs.busy_pids(inv, [g], [os.getpid()], mode="auto") == {}
+        assert calls == []                                 # fd scan was conclusive
+        procs.busy_pids(inv, [g], [os.getpid()], mode="both")
+        assert calls == [g.index]
+    finally:
+        inv.processes = real
+
+
 def test_roctx_markers_are_safe_without_profiler():
     from gpumounter_amd.utils import trace
 
