@@ -170,7 +170,9 @@ def test_busy_gpu_refused_then_force_kills(tmp_path, mock_inventory):
             assert len(lc.cluster.placeholders()) == 1 and not await lc.audit("default", "busy")
             code, b2 = await lc.remove("default", "busy", [dev["uuid"]], force=True)
             assert code == 200 and b2["killed_pids"] == [sleeper.pid]
-        run(body)
+        # the busy process exists only in the mock amdsmi table (emulated device nodes are not
+        # char devices an fd scan could see), so amdsmi must always be consulted
+        run(body, worker_overrides={"busy_detection": "both"})
         sleeper.wait(timeout=10)
         assert sleeper.returncode == -15
     finally:
@@ -189,7 +191,7 @@ def test_processes_outside_the_pod_do_not_make_it_busy(tmp_path, mock_inventory)
             procs.write_text(f"{b['devices'][0]['index']} 1 0 init\n")  # someone else's process
             code, _ = await lc.remove("default", "a", [b["devices"][0]["uuid"]])
             assert code == 200
-        run(body)
+        run(body, worker_overrides={"busy_detection": "both"})
     finally:
         _native.mock_smi().gm_mock_set_procs_file(b"")
 
