@@ -110,7 +110,9 @@ def main() -> int:
         tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
                              node_gpu_bdfs=node_bdfs, device_plugin=args.device_plugin,
                              worker_overrides={"warm_pool_size": args.warm_pool,
-                                               "placement_enforce": args.placement})
+                                               "placement_enforce": args.placement,
+                                               "gc_tune": True},   # as the daemons run
+                             master_overrides={"gc_tune": True})
         lc = tc.start()
         if args.warm_pool:
             pool = lc.nodes["node-0"].worker.pool

@@ -94,7 +94,8 @@ class LocalCluster:
             await self._add_node(f"node-{i}")
         if self.start_master:
             mcfg = Config.load(env={}, kube_api=self.api_url, master_host="127.0.0.1",
-                               log_json=False, **self.master_overrides)
+                               log_json=False,
+                               **{"gc_tune": False, **self.master_overrides})
             self.master = Master(mcfg)
             await self.master.start(port=0)
             self.master_url = f"http://127.0.0.1:{self.master.port}"
@@ -128,6 +129,7 @@ class LocalCluster:
     async def start_worker(self, name: str) -> Worker:
         h = self.nodes[name]
         ov = dict(self.worker_overrides)
+        ov.setdefault("gc_tune", False)   # many clusters per test process: freezing would leak
         if self.device_plugin:
             ov.setdefault("device_plugin", True)
             ov.setdefault("device_plugin_dir", h.kubelet.plugin_dir)

@@ -26,7 +26,7 @@ from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import log, runtime
 from gpumounter_amd.utils.metrics import Metrics
 
 _log = log.get("master")
@@ -159,6 +159,8 @@ class Master:
                            self.cfg.master_port if port is None else port)
         await site.start()
         self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+        if self.cfg.gc_tune:
+            runtime.tune_gc()
         _log.info("master serving HTTP :%d", self.port)
 
     async def stop(self) -> None:

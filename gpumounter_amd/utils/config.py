@@ -80,6 +80,7 @@ class Config:
     # auto: fd scan of the container's PIDs, amdsmi only for PIDs whose fd table is unreadable;
     # both: always union with amdsmi's process table
     busy_detection: str = "auto"
+    gc_tune: bool = True               # gc.freeze() after startup + larger young-gen threshold
     # serve amd.com/gpu ourselves (replaces the ROCm device plugin on the node) so
     # GetPreferredAllocation steers placeholders to the topology-chosen GPUs
     device_plugin: bool = False

@@ -27,7 +27,7 @@ from gpumounter_amd.node.cgroup import CgroupResolver, make_backend
 from gpumounter_amd.node.devnodes import DevNodeWriter
 from gpumounter_amd.node.hotmount import HotMount
 from gpumounter_amd.node.ledger import LedgerClient
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import log, runtime
 from gpumounter_amd.utils.faults import FaultInjector
 from gpumounter_amd.utils.metrics import Metrics
 from gpumounter_amd.worker.reconciler import Reconciler
@@ -170,6 +170,8 @@ class Worker:
         await self.pool.start()
         if self.cfg.metrics_period_s > 0:
             self._collector = asyncio.ensure_future(self._collect_loop())
+        if self.cfg.gc_tune:
+            runtime.tune_gc()
         self.ready = True
         _log.info("worker %s serving gRPC :%d http :%d (cgroup %s/%s, devnodes %s, ledger %s)",
                   self.cfg.node_name, self.grpc_port, self.http_port, self.resolver.mode,
