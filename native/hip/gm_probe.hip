@@ -411,7 +411,7 @@ int gm_probe_mfma_peak_variant(int dev, int variant, int iters, int blocks_per_c
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  launch(64);
+  launch(iters);  // warm-up as long as the timed run: clocks ramp before timing (DVFS)
   (void)hipEventRecord(a, 0);
   launch(iters);
   (void)hipEventRecord(b, 0);
