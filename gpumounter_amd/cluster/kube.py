@@ -188,6 +188,9 @@ class KubeClient:
         return await self._req("PATCH", self._pods_path(ns, name), body=patch,
                                content_type="application/merge-patch+json")
 
+    async def create_event(self, ns: str, event: dict) -> dict:
+        return await self._req("POST", f"/api/v1/namespaces/{ns}/events", body=event)
+
     async def watch_pods(self, ns: Optional[str] = None, label_selector: str = "",
                          field_selector: str = "", resource_version: str = "",
                          timeout_s: int = 300) -> AsyncIterator[Tuple[str, dict]]:

@@ -138,6 +138,7 @@ class FakeCluster:
         self.pods: Dict[Tuple[str, str], dict] = {}
         self.rv = 1000
         self.events: List[Tuple[int, str, dict]] = []
+        self.k8s_events: List[dict] = []     # core/v1 Event objects (not the watch history)
         self.watchers: List[Tuple[asyncio.Queue, str, Any, Any]] = []
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self.request_count = 0
@@ -451,6 +452,8 @@ class FakeCluster:
         r.add_delete("/api/v1/namespaces/{ns}/pods/{name}", self._h_delete)
         r.add_patch("/api/v1/namespaces/{ns}/pods/{name}", self._h_patch)
         r.add_get("/api/v1/nodes", self._h_nodes)
+        r.add_post("/api/v1/namespaces/{ns}/events", self._h_event_create)
+        r.add_get("/api/v1/namespaces/{ns}/events", self._h_event_list)
         r.add_get("/healthz", self._h_healthz)
         return app
 
@@ -459,7 +462,8 @@ class FakeCluster:
 
     async def _pre(self, req: web.Request) -> None:
         self.request_count += 1
-        key = f"{req.method} {'watch' if req.query.get('watch') else ''}".strip()
+        kind = "watch" if req.query.get("watch") else ("events" if "/events" in req.path else "")
+        key = f"{req.method} {kind}".strip()   # pod verbs stay "GET"/"POST"/...
         self.requests_by_verb[key] = self.requests_by_verb.get(key, 0) + 1
         await self._sleep(self.latency.api_ms)
 
@@ -571,6 +575,28 @@ class FakeCluster:
         if pod is None:
             return self._not_found(ns, name)
         return web.json_response(pod)
+
+    async def _h_event_create(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        ev = await req.json()
+        ns = req.match_info["ns"]
+        md = ev.setdefault("metadata", {})
+        md["namespace"] = ns
+        md.setdefault("name", md.pop("generateName", "event.") + uuid.uuid4().hex[:10])
+        self.rv += 1
+        md["resourceVersion"] = str(self.rv)
+        self.k8s_events.append(ev)
+        return web.json_response(ev, status=201)
+
+    async def _h_event_list(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        ns = req.match_info["ns"]
+        items = [e for e in self.k8s_events if e["metadata"]["namespace"] == ns]
+        return web.json_response({"kind": "EventList", "items": items})
+
+    def events_for(self, ns: str, pod: str) -> List[dict]:
+        return [e for e in self.k8s_events if e["metadata"]["namespace"] == ns
+                and e.get("involvedObject", {}).get("name") == pod]
 
     async def _h_nodes(self, req: web.Request) -> web.Response:
         await self._pre(req)

@@ -80,7 +80,9 @@ class Config:
     # auto: fd scan of the container's PIDs, amdsmi only for PIDs whose fd table is unreadable;
     # both: always union with amdsmi's process table
     busy_detection: str = "auto"
-    gc_tune: bool = True               # gc.freeze() after startup + larger young-gen threshold
+    gc_tune: bool = True
+    emit_events: bool = True           # core/v1 Events on the tenant pod (kubectl describe)
+    annotate_tenant: bool = False      # keep gpumounter.amd.com/devices on the tenant pod current               # gc.freeze() after startup + larger young-gen threshold
     # serve amd.com/gpu ourselves (replaces the ROCm device plugin on the node) so
     # GetPreferredAllocation steers placeholders to the topology-chosen GPUs
     device_plugin: bool = False

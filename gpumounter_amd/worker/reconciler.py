@@ -107,7 +107,12 @@ class Reconciler:
                     owner = svc.node_pods.get(ns, name)
                     if owner is None or podu.phase_of(owner) != "Running":
                         return
-                    await svc.reconcile_pod(owner)
+                    fixed = await svc.reconcile_pod(owner)
+                    if fixed:
+                        gone = sorted({i.path for i in fixed if i.kind.startswith("stale")})
+                        svc.notify.event(owner, "GPURevoked",
+                                         f"placeholder deleted outside gpumounter; access "
+                                         f"revoked: {', '.join(gone)}", warning=True)
                 self.event_actions += 1
                 svc.metrics.reconcile_actions.labels(action=f"event_{key[0]}").inc()
         except Exception as e:  # noqa: BLE001 - the periodic sweep retries

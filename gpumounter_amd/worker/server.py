@@ -219,6 +219,7 @@ class Worker:
             self._collector.cancel()
         await self.pool.stop()
         await self.reconciler.stop()
+        await self.service.notify.stop()
         if self.plugin is not None:
             await self.plugin.stop()
         if self.grpc_server is not None:

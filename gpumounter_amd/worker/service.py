@@ -42,6 +42,7 @@ from gpumounter_amd.node.ledger import LedgerClient, LedgerError
 from gpumounter_amd.utils import log, trace
 from gpumounter_amd.utils.faults import FaultInjector, InjectedFault
 from gpumounter_amd.utils.metrics import Metrics
+from gpumounter_amd.worker.notify import Notifier
 
 _log = log.get("worker.service")
 
@@ -89,6 +90,7 @@ class GpuMountService:
         self.faults = faults if faults is not None else FaultInjector(cfg.fault)
         self.pool = None  # WarmPool, attached by the Worker when warm_pool_size > 0
         self.plugin = None  # AmdGpuDevicePlugin, attached by the Worker with device_plugin=1
+        self.notify = Notifier(cfg, kube)
         # Reservations that must not interleave on a node run one at a time:
         # * trim briefly holds every free GPU — a concurrent one would see a full node;
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
@@ -281,6 +283,9 @@ class GpuMountService:
                 res = await self._reserve(pod, n, req, st, preferred, len(free))
             except InsufficientGPU as e:
                 _log.info("insufficient GPUs on %s: %s", self.cfg.node_name, e)
+                self.notify.event(pod, "GPUAttachFailed",
+                                  f"{n} GPU(s) requested, node {self.cfg.node_name} cannot "
+                                  f"provide them: {e}", warning=True)
                 return api.AddGPUResponse(add_gpu_result=api.ADD_INSUFFICIENT, message=str(e))
             except (ReserveError, asyncio.TimeoutError, InjectedFault, LedgerError) as e:
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
@@ -307,6 +312,8 @@ class GpuMountService:
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             log.kv(_log, 20, "attached", pod=f"{req.namespace}/{req.pod_name}",
                    gpus=[g.bdf for g in new])
+            self.notify.attached(pod, new, list(st.hot) + new,
+                                 "entire" if req.is_entire_mount else "single")
             return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS,
                                       devices=self._devices(new, owner),
                                       message="Add GPU Success")
@@ -533,6 +540,7 @@ class GpuMountService:
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             owner = {g.index: ph.name for ph in phs
                      for g in st.by_placeholder[(ph.namespace, ph.name)]}
+            self.notify.detached(pod, selected, keep, killed)
             return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_SUCCESS,
                                          devices=self._devices(selected, owner),
                                          killed_pids=killed, message="Remove GPU Success")

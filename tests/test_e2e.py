@@ -581,3 +581,49 @@ def test_tenant_delete_releases_placeholders_without_waiting_for_the_sweep():
             return lc.cluster.placeholders() == [] and node_of(lc).allocated == {}
         assert await _until(released)
     run(body)
+
+
+# ------------------------------------------------------------------------------ events / annotation
+def test_attach_detach_emit_events_and_keep_devices_annotation():
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200
+        await svc.notify.drain()
+        bdfs = sorted(d["bdf"] for d in b["devices"])
+        ann = lc.cluster.get("default", "t")["metadata"]["annotations"]
+        assert ann["gpumounter.amd.com/devices"] == ",".join(bdfs)
+        code, _ = await lc.remove("default", "t", [b["devices"][0]["uuid"]])
+        assert code == 200
+        await svc.notify.drain()
+        ann = lc.cluster.get("default", "t")["metadata"]["annotations"]
+        assert ann["gpumounter.amd.com/devices"] == b["devices"][1]["bdf"]
+        lc.tenant("big")
+        assert (await lc.add("default", "big", 8))[0] == 500        # 1 GPU held by t
+        await svc.notify.drain()
+        evs = lc.cluster.events_for("default", "t")
+        assert [e["reason"] for e in evs] == ["GPUAttached", "GPUDetached"]
+        assert all(e["involvedObject"]["uid"] == lc.cluster.get("default", "t")["metadata"]["uid"]
+                   for e in evs)
+        assert b["devices"][0]["bdf"] in evs[1]["message"]
+        (fail,) = lc.cluster.events_for("default", "big")
+        assert fail["reason"] == "GPUAttachFailed" and fail["type"] == "Warning"
+        assert "gpumounter.amd.com/devices" not in (
+            lc.cluster.get("default", "big")["metadata"].get("annotations") or {})
+    run(body, worker_overrides={"annotate_tenant": True})
+
+
+def test_external_delete_records_a_revocation_warning():
+    async def body(lc):
+        lc.tenant("t")
+        code, b = await lc.add("default", "t", 1)
+        lc.cluster.delete(lc.cluster.placeholders()[0]["metadata"]["namespace"],
+                          b["devices"][0]["placeholder"], grace=0)
+        svc = lc.nodes["node-0"].worker.service
+
+        async def warned():
+            await svc.notify.drain()
+            return any(e["reason"] == "GPURevoked" for e in lc.cluster.events_for("default", "t"))
+        assert await _until(warned)
+    run(body)
