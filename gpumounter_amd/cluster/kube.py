@@ -188,6 +188,23 @@ class KubeClient:
         return await self._req("PATCH", self._pods_path(ns, name), body=patch,
                                content_type="application/merge-patch+json")
 
+    async def token_review(self, token: str) -> dict:
+        out = await self._req("POST", "/apis/authentication.k8s.io/v1/tokenreviews", body={
+            "apiVersion": "authentication.k8s.io/v1", "kind": "TokenReview",
+            "spec": {"token": token}})
+        return (out or {}).get("status") or {}
+
+    async def subject_access_review(self, user: dict, resource_attributes: dict) -> dict:
+        out = await self._req("POST", "/apis/authorization.k8s.io/v1/subjectaccessreviews",
+                              body={"apiVersion": "authorization.k8s.io/v1",
+                                    "kind": "SubjectAccessReview",
+                                    "spec": {"user": user.get("username", ""),
+                                             "uid": user.get("uid", ""),
+                                             "groups": user.get("groups", []),
+                                             "extra": user.get("extra", {}),
+                                             "resourceAttributes": resource_attributes}})
+        return (out or {}).get("status") or {}
+
     async def create_event(self, ns: str, event: dict) -> dict:
         return await self._req("POST", f"/api/v1/namespaces/{ns}/events", body=event)
 

@@ -139,6 +139,9 @@ class FakeCluster:
         self.rv = 1000
         self.events: List[Tuple[int, str, dict]] = []
         self.k8s_events: List[dict] = []     # core/v1 Event objects (not the watch history)
+        self.tokens: Dict[str, dict] = {}    # TokenReview: bearer token → user info
+        self.rbac: List[dict] = []           # SubjectAccessReview rules (see grant())
+        self.sar_count = 0
         self.watchers: List[Tuple[asyncio.Queue, str, Any, Any]] = []
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self.request_count = 0
@@ -452,6 +455,8 @@ class FakeCluster:
         r.add_delete("/api/v1/namespaces/{ns}/pods/{name}", self._h_delete)
         r.add_patch("/api/v1/namespaces/{ns}/pods/{name}", self._h_patch)
         r.add_get("/api/v1/nodes", self._h_nodes)
+        r.add_post("/apis/authentication.k8s.io/v1/tokenreviews", self._h_token_review)
+        r.add_post("/apis/authorization.k8s.io/v1/subjectaccessreviews", self._h_sar)
         r.add_post("/api/v1/namespaces/{ns}/events", self._h_event_create)
         r.add_get("/api/v1/namespaces/{ns}/events", self._h_event_list)
         r.add_get("/healthz", self._h_healthz)
@@ -575,6 +580,40 @@ class FakeCluster:
         if pod is None:
             return self._not_found(ns, name)
         return web.json_response(pod)
+
+    # ------------------------------------------------------------------------ authn / authz
+    def add_user(self, token: str, username: str, groups=()) -> None:
+        self.tokens[token] = {"username": username, "uid": f"uid-{username}",
+                              "groups": list(groups) + ["system:authenticated"]}
+
+    def grant(self, subject: str, verbs, resource: str = "pods/gpumount",
+              namespaces=("*",)) -> None:
+        """RBAC-like rule: ``subject`` is a username or ``group:<name>``."""
+        self.rbac.append({"subject": subject, "verbs": set(verbs), "resource": resource,
+                          "namespaces": set(namespaces)})
+
+    async def _h_token_review(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        body = await req.json()
+        user = self.tokens.get(body.get("spec", {}).get("token", ""))
+        status = {"authenticated": user is not None}
+        if user is not None:
+            status["user"] = user
+        return web.json_response({**body, "status": status}, status=201)
+
+    async def _h_sar(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        body = await req.json()
+        spec = body.get("spec", {})
+        ra = spec.get("resourceAttributes", {})
+        res = ra.get("resource", "") + (f"/{ra['subresource']}" if ra.get("subresource") else "")
+        who = {spec.get("user", "")} | {f"group:{g}" for g in spec.get("groups", [])}
+        allowed = any(r["subject"] in who and ra.get("verb") in r["verbs"]
+                      and r["resource"] == res
+                      and ("*" in r["namespaces"] or ra.get("namespace", "") in r["namespaces"])
+                      for r in self.rbac)
+        self.sar_count += 1
+        return web.json_response({**body, "status": {"allowed": allowed}}, status=201)
 
     async def _h_event_create(self, req: web.Request) -> web.Response:
         await self._pre(req)

@@ -217,18 +217,22 @@ class LocalCluster:
                 for cs in pod["status"].get("containerStatuses", []) if cs.get("containerID")]
 
     async def add(self, ns: str, pod: str, n: int, entire: bool = False,
-                  accept_json: bool = True):
+                  accept_json: bool = True, token: str = ""):
         url = (f"{self.master_url}/addgpu/namespace/{ns}/pod/{pod}/gpu/{n}/isEntireMount/"
                f"{'true' if entire else 'false'}")
         headers = {"Accept": "application/json"} if accept_json else {}
+        if token:
+            headers["Authorization"] = f"Bearer {token}"
         async with self.session.get(url, headers=headers) as r:
             return r.status, (await r.json() if accept_json else await r.text())
 
     async def remove(self, ns: str, pod: str, uuids: List[str], force: bool = False,
-                     accept_json: bool = True):
+                     accept_json: bool = True, token: str = ""):
         url = (f"{self.master_url}/removegpu/namespace/{ns}/pod/{pod}/force/"
                f"{'true' if force else 'false'}")
         headers = {"Accept": "application/json"} if accept_json else {}
+        if token:
+            headers["Authorization"] = f"Bearer {token}"
         data = aiohttp.FormData()
         for u in uuids:
             data.add_field("uuids", u)

@@ -26,6 +26,7 @@ from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models import pod as podu
+from gpumounter_amd.master.authz import Authorizer
 from gpumounter_amd.utils import log, runtime
 from gpumounter_amd.utils.metrics import Metrics
 
@@ -132,6 +133,7 @@ class Master:
         self.workers = WorkerDirectory(self.kube, cfg.worker_namespace, cfg.worker_label,
                                        cfg.worker_port, cfg)
         self.metrics = Metrics()
+        self.authz = Authorizer(cfg, self.kube)
         self.runner: Optional[web.AppRunner] = None
         self.port = 0
         self._pod_nodes: Dict[Tuple[str, str], Tuple[str, str, float]] = {}
@@ -183,16 +185,14 @@ class Master:
     def _wants_json(request: web.Request) -> bool:
         return "application/json" in request.headers.get("Accept", "")
 
-    def _unauthorized(self, request: web.Request, route: str) -> Optional[web.Response]:
-        """Bearer-token check for mutating routes (the reference has no authn: SURVEY defect 13)."""
-        if not self.cfg.api_token:
+    async def _denied(self, request: web.Request, route: str, verb: str, ns: str = "",
+                      resource: str = "pods", name: str = "") -> Optional[web.Response]:
+        """None if allowed, else the 401/403/503 reply (master/authz.py; the reference has no
+        authn/authz at all: SURVEY defect 13)."""
+        d = await self.authz.check(request.headers, verb, ns, resource, name)
+        if d.allowed:
             return None
-        import hmac
-
-        got = request.headers.get("Authorization", "")
-        if hmac.compare_digest(got, f"Bearer {self.cfg.api_token}"):
-            return None
-        return self._reply(request, route, 401, "Unauthorized", {})
+        return self._reply(request, route, d.status, d.reason, {})
 
     def _reply(self, request, route: str, status: int, text: str, payload: dict) -> web.Response:
         self.metrics.http_requests.labels(route=route, code=str(status)).inc()
@@ -317,12 +317,12 @@ class Master:
     # ------------------------------------------------------------------------ HTTP routes
     async def add_gpu(self, request: web.Request) -> web.Response:
         route = "addgpu"
-        denied = self._unauthorized(request, route)
+        mi = request.match_info
+        ns, name = mi["namespace"], mi["pod"]
+        denied = await self._denied(request, route, "create", ns, name=name)
         if denied is not None:
             return denied
         rid = log.new_request_id("add")
-        mi = request.match_info
-        ns, name = mi["namespace"], mi["pod"]
         n = parse_go_int32(mi["gpuNum"])
         if n is None:
             return self._reply(request, route, 400, f"Invalid param gpuNum: {mi['gpuNum']}", {})
@@ -341,12 +341,12 @@ class Master:
 
     async def remove_gpu(self, request: web.Request) -> web.Response:
         route = "removegpu"
-        denied = self._unauthorized(request, route)
+        mi = request.match_info
+        ns, name = mi["namespace"], mi["pod"]
+        denied = await self._denied(request, route, "delete", ns, name=name)
         if denied is not None:
             return denied
         rid = log.new_request_id("rm")
-        mi = request.match_info
-        ns, name = mi["namespace"], mi["pod"]
         try:
             form = await request.post()
         except Exception:  # noqa: BLE001
@@ -369,9 +369,10 @@ class Master:
         "uuids", "force", "container"}]} → results in order; operations run concurrently
         (operations on one pod still serialize on the worker's per-pod lock)."""
         route = "batch"
-        denied = self._unauthorized(request, route)
-        if denied is not None:
-            return denied
+        if self.authz.mode != "kube":   # shared-token mode: one check for the whole batch
+            denied = await self._denied(request, route, "create")
+            if denied is not None:
+                return denied
         try:
             body = await request.json()
             ops = body["operations"]
@@ -384,6 +385,12 @@ class Master:
             try:
                 kind = op["op"]
                 ns, name = op.get("namespace", "default"), op["pod"]
+                if self.authz.mode == "kube":   # per operation: namespaces may differ
+                    d = await self.authz.check(request.headers,
+                                               "create" if kind == "add" else "delete", ns,
+                                               name=name)
+                    if not d.allowed:
+                        return d.status, d.reason, {}
                 if kind == "add":
                     n = int(op["gpus"])
                     if n <= 0:
@@ -420,6 +427,9 @@ class Master:
 
     async def node_gpus(self, request: web.Request) -> web.Response:
         node = request.match_info["node"]
+        denied = await self._denied(request, "nodegpus", "get", resource="nodes", name=node)
+        if denied is not None:
+            return denied
         target = self.workers.target(node)
         if target is None:
             return web.json_response({"error": f"no worker on node {node}"}, status=404)
@@ -432,6 +442,9 @@ class Master:
 
     async def pod_gpus(self, request: web.Request) -> web.Response:
         ns, name = request.match_info["namespace"], request.match_info["pod"]
+        denied = await self._denied(request, "podgpus", "get", ns, name=name)
+        if denied is not None:
+            return denied
         try:
             pod = await self.kube.get_pod(ns, name)
         except NotFound:

@@ -99,6 +99,7 @@ class Config:
     reconcile_period_s: float = 30.0
     watch_resync_s: float = 300.0
     api_token: str = ""                # if set, add/remove require "Authorization: Bearer <token>"
+    authz_mode: str = "none"           # none (| api_token) | kube: TokenReview + SAR on pods/gpumount
     # master⇄worker gRPC TLS (reference: insecure, main.go:82). cert+key on the worker enable TLS;
     # a CA on the worker requires client certs (mTLS). The master uses the same three files.
     tls_cert: str = ""
@@ -163,6 +164,7 @@ class Config:
         _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
         _choice("placement_enforce", self.placement_enforce, ("hint", "trim"))
         _choice("busy_detection", self.busy_detection, ("auto", "both"))
+        _choice("authz_mode", self.authz_mode, ("none", "kube"))
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))
         _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
         if not (0 < self.worker_port < 65536 and 0 <= self.master_port < 65536):

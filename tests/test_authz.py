@@ -1,0 +1,71 @@
+"""Per-tenant authorization on the master (authz_mode=kube): TokenReview + SubjectAccessReview
+on the virtual subresource pods/gpumount. The reference authorizes nobody (SURVEY defect 13)."""
+import asyncio
+
+from gpumounter_amd.fakes.harness import LocalCluster
+
+
+def run(body):
+    async def main():
+        async with LocalCluster(master_overrides={"authz_mode": "kube"}) as lc:
+            c = lc.cluster
+            c.add_user("tok-alice", "alice", groups=["team-a"])
+            c.add_user("tok-bob", "bob")
+            c.add_user("tok-ops", "ops", groups=["gpu-admins"])
+            c.grant("group:team-a", ["create", "delete", "get"], namespaces=["team-a"])
+            c.grant("group:gpu-admins", ["create", "delete", "get"])            # all namespaces
+            c.grant("group:gpu-admins", ["get"], resource="nodes/gpumount")
+            return await body(lc)
+    return asyncio.run(main())
+
+
+def test_kube_mode_authorizes_per_namespace_and_verb():
+    async def body(lc):
+        lc.tenant("a1", ns="team-a")
+        lc.tenant("d1", ns="default")
+        assert (await lc.add("team-a", "a1", 1))[0] == 401                      # no token
+        assert (await lc.add("team-a", "a1", 1, token="nope"))[0] == 401          # unknown token
+        code, b = await lc.add("default", "d1", 1, token="tok-alice")
+        assert code == 403 and "alice cannot create pods/gpumount in namespace default" \
+            in b["message"]
+        assert (await lc.add("team-a", "a1", 1, token="tok-bob"))[0] == 403       # no rights
+        code, b = await lc.add("team-a", "a1", 2, token="tok-alice")
+        assert code == 200 and len(b["devices"]) == 2
+        u = [d["uuid"] for d in b["devices"]]
+        assert (await lc.remove("team-a", "a1", u, token="tok-bob"))[0] == 403
+        assert (await lc.remove("team-a", "a1", u, token="tok-alice"))[0] == 200
+        assert (await lc.add("default", "d1", 1, token="tok-ops"))[0] == 200      # cluster-wide
+        # read routes are authorized too
+        async with lc.session.get(f"{lc.master_url}/api/v1/nodes/node-0/gpus",
+                                  headers={"Authorization": "Bearer tok-alice"}) as r:
+            assert r.status == 403
+        async with lc.session.get(f"{lc.master_url}/api/v1/nodes/node-0/gpus",
+                                  headers={"Authorization": "Bearer tok-ops"}) as r:
+            assert r.status == 200
+    run(body)
+
+
+def test_reviews_are_cached():
+    async def body(lc):
+        lc.tenant("a1", ns="team-a")
+        authz = lc.master.authz
+        for _ in range(3):
+            code, b = await lc.add("team-a", "a1", 1, token="tok-alice")
+            assert code == 200
+            assert (await lc.remove("team-a", "a1", [b["devices"][0]["uuid"]],
+                                    token="tok-alice"))[0] == 200
+        assert authz.reviews == {"token": 1, "sar": 2}      # one per (user, verb, ns, pod)
+    run(body)
+
+
+def test_batch_checks_every_operation():
+    async def body(lc):
+        lc.tenant("a1", ns="team-a")
+        lc.tenant("d1", ns="default")
+        async with lc.session.post(f"{lc.master_url}/api/v1/batch", json={"operations": [
+                {"op": "add", "namespace": "team-a", "pod": "a1", "gpus": 1},
+                {"op": "add", "namespace": "default", "pod": "d1", "gpus": 1}]},
+                headers={"Authorization": "Bearer tok-alice"}) as r:
+            res = (await r.json())["results"]
+        assert [x["code"] for x in res] == [200, 403]
+    run(body)

@@ -51,14 +51,28 @@ def test_kind_overlay_env_is_valid_config():
         m["mountPath"] for m in ds["spec"]["template"]["spec"]["containers"][0]["volumeMounts"]}
 
 
+def test_tenant_rbac_example_targets_the_gpumount_subresource():
+    docs = load("rbac-tenant-example.yaml")
+    roles = {d["metadata"]["name"]: d for d in docs if d["kind"] == "ClusterRole"}
+    from gpumounter_amd.master.authz import RESOURCE_SUB
+    assert roles["gpumount-user"]["rules"][0]["resources"] == [f"pods/{RESOURCE_SUB}"]
+    assert set(roles["gpumount-user"]["rules"][0]["verbs"]) == {"create", "delete", "get"}
+    (ctl,) = [d for d in load("rbac.yaml") if d["kind"] == "ClusterRole"]
+    groups = {g for r in ctl["rules"] for g in r["apiGroups"]}
+    assert {"authentication.k8s.io", "authorization.k8s.io"} <= groups
+
+
 def test_rbac_is_least_privilege():
     docs = load("rbac.yaml")
     roles = [d for d in docs if d["kind"] == "ClusterRole"]
     binding = next(d for d in docs if d["kind"] == "ClusterRoleBinding")
     assert binding["roleRef"]["name"] != "cluster-admin"
     resources = {r for role in roles for rule in role["rules"] for r in rule["resources"]}
-    assert resources <= {"pods", "nodes", "events"}
+    assert resources <= {"pods", "nodes", "events", "tokenreviews", "subjectaccessreviews"}
     assert all("*" not in rule["verbs"] for role in roles for rule in role["rules"])
+    reviews = [rule for role in roles for rule in role["rules"]
+               if set(rule["resources"]) & {"tokenreviews", "subjectaccessreviews"}]
+    assert all(rule["verbs"] == ["create"] for rule in reviews)
 
 
 def test_service_and_master_ports():
