@@ -75,20 +75,24 @@ class Config:
     # trim: hold every free GPU with 1-GPU placeholders, keep the topology-chosen ones, release
     # the rest — exact placement whatever the device plugin does
     placement_enforce: str = "hint"
-    ledger_get: bool = True
+    ledger_get: bool = True            # read admitted placeholders with PodResources v1 Get
     reconcile_on_events: bool = True
     # auto: fd scan of the container's PIDs, amdsmi only for PIDs whose fd table is unreadable;
     # both: always union with amdsmi's process table
     busy_detection: str = "auto"
-    gc_tune: bool = True
+    gc_tune: bool = True               # gc.freeze() after startup + larger young-gen threshold
     emit_events: bool = True           # core/v1 Events on the tenant pod (kubectl describe)
-    annotate_tenant: bool = False      # keep gpumounter.amd.com/devices on the tenant pod current               # gc.freeze() after startup + larger young-gen threshold
+    annotate_tenant: bool = False      # keep gpumounter.amd.com/devices on the tenant pod current
+    # Events/annotations are sent once the worker has had no attach/detach in flight for
+    # notify_idle_ms (so they never compete with a request), but at most notify_max_delay_ms late
+    notify_idle_ms: float = 2.0
+    notify_max_delay_ms: float = 1000.0
     # serve amd.com/gpu ourselves (replaces the ROCm device plugin on the node) so
     # GetPreferredAllocation steers placeholders to the topology-chosen GPUs
     device_plugin: bool = False
     device_plugin_dir: str = "/var/lib/kubelet/device-plugins"
     device_plugin_inject: bool = True     # False: no device specs (kind / mock inventory)
-    device_plugin_health_s: float = 5.0   # react to foreign placeholder / owner deletes at once            # read admitted placeholders with PodResources v1 Get
+    device_plugin_health_s: float = 5.0   # react to foreign placeholder / owner deletes at once
     max_gpus_per_request: int = 64
     kill_signal: int = 15              # SIGTERM like the reference's `kill` (namespace.go:192)
     kill_grace_s: float = 5.0          # then SIGKILL

@@ -6,13 +6,17 @@ attach/detach, forced kill and reconciler revocation becomes an Event on the ten
 ``gpumounter.amd.com/devices`` = the PCI BDFs it currently holds. A downward-API volume
 projects that into the container, where it updates without a restart.
 
-Both run after the RPC has answered (fire-and-forget tasks); failures are logged, never surfaced.
+Neither is on the request path: sends are queued and flushed once the worker has had no
+attach/detach in flight for ``notify_idle_ms`` (so the apiserver round trips never share the event
+loop with a request), or after ``notify_max_delay_ms`` under sustained load. Failures are logged,
+never surfaced.
 """
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import datetime
-from typing import Sequence, Set
+from typing import Awaitable, Callable, Dict, List, Optional, Sequence, Set, Tuple
 
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu
@@ -27,19 +31,69 @@ class Notifier:
         self.cfg = cfg
         self.kube = kube
         self._tasks: Set[asyncio.Task] = set()
+        # (coalescing key or None, send): for a key only the newest send survives a flush
+        self._queue: List[Tuple[Optional[tuple], Callable[[], Awaitable[None]]]] = []
+        self._flusher: Optional[asyncio.Task] = None
+        self._inflight = 0
+        self._idle = asyncio.Event()
+        self._idle.set()
         self.sent = 0
 
-    def _spawn(self, coro) -> None:
-        t = asyncio.ensure_future(coro)
-        self._tasks.add(t)
-        t.add_done_callback(self._tasks.discard)
+    @contextlib.contextmanager
+    def operation(self):
+        """Bracket one attach/detach: queued notifications wait until none is in flight."""
+        self._inflight += 1
+        self._idle.clear()
+        try:
+            yield
+        finally:
+            self._inflight -= 1
+            if self._inflight == 0:
+                self._idle.set()
+
+    def _spawn(self, factory: Callable[[], Awaitable[None]], key: Optional[tuple] = None) -> None:
+        self._queue.append((key, factory))
+        self._kick()
+
+    def _kick(self) -> None:
+        if self._queue and (self._flusher is None or self._flusher.done()):
+            t = self._flusher = asyncio.ensure_future(self._flush())
+            self._tasks.add(t)
+            t.add_done_callback(self._tasks.discard)
+
+    async def _wait_idle(self) -> None:
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + self.cfg.notify_max_delay_ms / 1e3
+        quiet = self.cfg.notify_idle_ms / 1e3
+        while True:
+            if self._inflight == 0:
+                await asyncio.sleep(quiet)        # lets the finished RPC's reply go out first
+                if self._inflight == 0:
+                    return
+            left = deadline - loop.time()
+            if left <= 0:
+                return
+            try:
+                await asyncio.wait_for(self._idle.wait(), left)
+            except asyncio.TimeoutError:
+                return
+
+    async def _flush(self) -> None:
+        while self._queue:
+            await self._wait_idle()
+            batch, self._queue = self._queue, []
+            latest: Dict[tuple, int] = {k: i for i, (k, _) in enumerate(batch) if k is not None}
+            sends = [f() for i, (k, f) in enumerate(batch) if k is None or latest[k] == i]
+            await asyncio.gather(*sends, return_exceptions=True)
 
     async def drain(self) -> None:
         """Wait for pending notifications (tests, shutdown)."""
-        while self._tasks:
+        while self._tasks or self._queue:
+            self._kick()
             await asyncio.gather(*list(self._tasks), return_exceptions=True)
 
     async def stop(self) -> None:
+        self._queue.clear()
         for t in list(self._tasks):
             t.cancel()
 
@@ -66,7 +120,7 @@ class Notifier:
                 self.sent += 1
             except Exception as e:  # noqa: BLE001
                 _log.debug("event %s on %s/%s not recorded: %s", reason, ns, name, e)
-        self._spawn(send())
+        self._spawn(send)
 
     # ------------------------------------------------------------------------ annotation
     def annotate(self, pod: dict, holding: Sequence[AmdGpu]) -> None:
@@ -80,7 +134,7 @@ class Notifier:
                 await self.kube.patch_pod(podu.ns_of(pod), podu.name_of(pod), patch)
             except Exception as e:  # noqa: BLE001
                 _log.debug("annotate %s/%s failed: %s", podu.ns_of(pod), podu.name_of(pod), e)
-        self._spawn(send())
+        self._spawn(send, key=("annotate", podu.ns_of(pod), podu.name_of(pod)))
 
     # ------------------------------------------------------------------------ helpers
     @staticmethod

@@ -230,8 +230,9 @@ class GpuMountService:
     # ------------------------------------------------------------------------ AddGPU
     async def add_gpu(self, req) -> "api.AddGPUResponse":
         rid = req.request_id or log.new_request_id("add")
-        with log.with_rid(rid), trace.span("attach", pod=f"{req.namespace}/{req.pod_name}",
-                                           n=req.gpu_num, entire=req.is_entire_mount) as root:
+        with self.notify.operation(), log.with_rid(rid), \
+                trace.span("attach", pod=f"{req.namespace}/{req.pod_name}",
+                           n=req.gpu_num, entire=req.is_entire_mount) as root:
             resp = await self._add_gpu(req)
         resp.total_ms = root.duration_ms
         resp.timings.extend(self._timings(root))
@@ -476,8 +477,9 @@ class GpuMountService:
     # ------------------------------------------------------------------------ RemoveGPU
     async def remove_gpu(self, req) -> "api.RemoveGPUResponse":
         rid = req.request_id or log.new_request_id("rm")
-        with log.with_rid(rid), trace.span("detach", pod=f"{req.namespace}/{req.pod_name}",
-                                           n=len(req.uuids), force=req.force) as root:
+        with self.notify.operation(), log.with_rid(rid), \
+                trace.span("detach", pod=f"{req.namespace}/{req.pod_name}",
+                           n=len(req.uuids), force=req.force) as root:
             resp = await self._remove_gpu(req)
         resp.total_ms = root.duration_ms
         resp.timings.extend(self._timings(root))

@@ -627,3 +627,45 @@ def test_external_delete_records_a_revocation_warning():
             return any(e["reason"] == "GPURevoked" for e in lc.cluster.events_for("default", "t"))
         assert await _until(warned)
     run(body)
+
+
+def test_notifications_wait_for_idle_worker_and_coalesce_annotations():
+    """Events are never sent while an attach/detach is in flight; for one pod only the newest
+    devices annotation is written (worker/notify.py)."""
+    from types import SimpleNamespace
+
+    from gpumounter_amd.worker.notify import Notifier
+
+    class Kube:
+        def __init__(self):
+            self.calls = []
+
+        async def create_event(self, ns, ev):
+            self.calls.append(("event", ev["reason"]))
+
+        async def patch_pod(self, ns, name, patch):
+            self.calls.append(("patch", patch["metadata"]["annotations"]["gpumounter.amd.com/devices"]))
+
+    async def body():
+        cfg = SimpleNamespace(emit_events=True, annotate_tenant=True, node_name="n0",
+                              notify_idle_ms=1.0, notify_max_delay_ms=10_000.0)
+        kube = Kube()
+        nt = Notifier(cfg, kube)
+        pod = {"metadata": {"name": "t", "namespace": "default", "uid": "u1"}}
+        g = lambda i: SimpleNamespace(index=i, bdf=f"0000:0{i}:00.0", render_minor=128 + i)  # noqa: E731
+        with nt.operation():
+            nt.attached(pod, [g(1)], [g(1)], "single")
+            nt.attached(pod, [g(2)], [g(1), g(2)], "single")
+            await asyncio.sleep(0.02)
+            assert kube.calls == []                  # held back while the request runs
+        await nt.drain()
+        assert [c for c in kube.calls if c[0] == "event"] == [("event", "GPUAttached")] * 2
+        assert [c for c in kube.calls if c[0] == "patch"] == [("patch", "0000:01:00.0,0000:02:00.0")]
+        # under sustained load the max delay still flushes
+        cfg.notify_max_delay_ms = 20.0
+        kube.calls.clear()
+        with nt.operation():
+            nt.event(pod, "GPUDetached", "x")
+            await asyncio.sleep(0.1)
+            assert kube.calls == [("event", "GPUDetached")]
+    asyncio.run(body())
