@@ -117,6 +117,7 @@ class DevNode(C.Structure):
                 ("mode", C.c_uint32), ("uid", C.c_int32), ("gid", C.c_int32)]
 
 
+HOST_ABI_VERSION = 2          # native/include/gm_host.h GM_HOST_ABI_VERSION
 GM_ACC_MKNOD, GM_ACC_READ, GM_ACC_WRITE = 1, 2, 4
 GM_DEV_EMULATE, GM_DEV_VIA_SETNS, GM_DEV_REPLACE = 1, 2, 4
 
@@ -124,6 +125,10 @@ GM_DEV_EMULATE, GM_DEV_VIA_SETNS, GM_DEV_REPLACE = 1, 2, 4
 def host() -> C.CDLL:
     lib = _load("libgm_host.so", "host")
     if not getattr(lib, "_gm_typed", False):
+        abi = lib.gm_host_abi_version()
+        if abi != HOST_ABI_VERSION:
+            raise RuntimeError(f"libgm_host.so ABI {abi} != {HOST_ABI_VERSION} expected: stale "
+                               f"build, run `make -C native`")
         lib.gm_cg1_apply.argtypes = [C.c_char_p, C.POINTER(DevRule), C.c_int]
         lib.gm_cg1_format_rule.argtypes = [C.POINTER(DevRule), C.c_char_p, C.c_int]
         lib.gm_bpf_dev_build.argtypes = [C.POINTER(DevRule), C.c_int, C.c_int, C.c_int,
@@ -135,6 +140,9 @@ def host() -> C.CDLL:
         lib.gm_bpf_prog_name.argtypes = [C.c_uint32, C.c_char_p, C.c_int]
         lib.gm_bpf_dev_program.argtypes = [C.c_char_p, C.POINTER(C.c_uint64), C.c_uint32,
                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        lib.gm_bpf_dev_program_at.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_uint64),
+                                              C.c_uint32, C.POINTER(C.c_uint32),
+                                              C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.gm_bpf_dev_install.argtypes = [C.c_char_p, C.POINTER(DevRule), C.c_int,
                                            C.POINTER(DevRule), C.c_int, C.c_char_p,
                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]

@@ -297,26 +297,51 @@ class V2BpfBackend(DeviceRuleBackend):
                chained=chained.value, rules=len(rules))
 
     def allowed(self, cgdir):
-        """What the kernel enforces: the xlated instructions of our attached program, evaluated
-        by the interpreter (a program swapped out by systemd/the runtime reads as "nothing
-        granted", so the reconciler re-installs it)."""
-        prog = attached_program(cgdir)
-        return set() if prog is None else program_allows(prog)
+        """What the kernel enforces: the xlated instructions of every attached program of ours,
+        evaluated by the interpreter; a pair counts only if all of them grant it. A program that
+        systemd or the runtime swapped out, or a foreign program attached next to ours (it can
+        veto any access under BPF_F_ALLOW_MULTI), reads as "nothing granted", so the reconciler
+        re-installs and wraps it."""
+        progs, foreign = attached_programs(cgdir)
+        if not progs or foreign:
+            return set()
+        out = program_allows(progs[0])
+        for p in progs[1:]:
+            out &= program_allows(p)
+        return out
 
 
-def attached_program(cgdir: str) -> Optional[List[int]]:
+def _program_at(cgdir: str, index: int) -> Tuple[Optional[List[int]], int]:
     lib = _native.host()
-    n, pid = C.c_uint32(0), C.c_uint32(0)
-    rc = lib.gm_bpf_dev_program(cgdir.encode(), None, 0, C.byref(n), C.byref(pid))
+    n, pid, foreign = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
+    rc = lib.gm_bpf_dev_program_at(cgdir.encode(), index, None, 0, C.byref(n), C.byref(pid),
+                                   C.byref(foreign))
     if rc == 0 and n.value == 0:
-        return None
+        return None, foreign.value
     if rc not in (0, -errno.ENOSPC):
         raise CgroupError(f"bpf introspection on {cgdir}: {os.strerror(-rc)}")
     buf = (C.c_uint64 * n.value)()
-    rc = lib.gm_bpf_dev_program(cgdir.encode(), buf, n.value, C.byref(n), C.byref(pid))
+    rc = lib.gm_bpf_dev_program_at(cgdir.encode(), index, buf, n.value, C.byref(n),
+                                   C.byref(pid), C.byref(foreign))
     if rc < 0:
         raise CgroupError(f"bpf introspection on {cgdir}: {os.strerror(-rc)}")
-    return [int(buf[i]) for i in range(n.value)]
+    return [int(buf[i]) for i in range(n.value)], foreign.value
+
+
+def attached_programs(cgdir: str) -> Tuple[List[List[int]], int]:
+    """(xlated instructions of each gpumounter program, number of foreign programs) attached."""
+    progs: List[List[int]] = []
+    foreign = 0
+    while True:
+        prog, foreign = _program_at(cgdir, len(progs))
+        if prog is None:
+            return progs, foreign
+        progs.append(prog)
+
+
+def attached_program(cgdir: str) -> Optional[List[int]]:
+    progs, _ = attached_programs(cgdir)
+    return progs[0] if progs else None
 
 
 def program_allows(prog: Sequence[int]) -> Set[Tuple[int, int]]:

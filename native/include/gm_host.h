@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define GM_HOST_ABI_VERSION 1
+#define GM_HOST_ABI_VERSION 2
 
 // Access bits follow BPF_DEVCG_ACC_* so the same rule feeds both cgroup versions.
 #define GM_ACC_MKNOD 1
@@ -64,20 +64,28 @@ int gm_bpf_prog_name(uint32_t id, char* name, int cap);
 // attached; -ENOSPC (with *n = needed) if cap is too small; -EPERM if the kernel hides xlated code.
 int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, uint32_t* n,
                        uint32_t* prog_id);
-// Installs (or updates) the gpumounter allow-list on a cgroup-v2 directory:
-//   * our program already attached → replaced, chaining to the same original program;
-//   * one foreign program attached → ours replaces it and tail-calls into it;
+// Same for the index-th gpumounter program (several when several programs were wrapped); *n = 0
+// past the last one. *foreign = programs attached that are not ours (each can veto an access).
+int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, uint64_t* insns, uint32_t cap,
+                          uint32_t* n, uint32_t* prog_id, uint32_t* foreign);
+// Installs (or updates) the gpumounter allow-list on a cgroup-v2 directory. Every attached
+// program is wrapped, because under BPF_F_ALLOW_MULTI each one must allow an access (runc and
+// systemd both attach one on systemd-driver hosts):
+//   * a program of ours → replaced, chaining to the same original program;
+//   * a foreign program → ours replaces it (BPF_F_REPLACE) and tail-calls into it;
 //   * nothing attached → ours is attached with default-allow (deny rules only matter then).
-// The tail-call map must outlive this process (the kernel clears PROG_ARRAY slots when the last
-// user reference goes away), so it is pinned at <pin_dir>/gm_<cgroup inode> on a bpffs; with
-// pin_dir NULL/"" the map fd is kept open in this process instead. If our program is attached but
-// its chain slot is empty (unpinned map after a restart), `base` rules (the runtime's default
-// device list) are compiled in instead of the tail call.
-// On success *prog_id is our new program id and *chained_id the preserved original (0 if none).
+// The tail-call maps must outlive this process (the kernel clears PROG_ARRAY slots when the last
+// user reference goes away), so each is pinned at <pin_dir>/gm_<cgroup inode>_<original prog id>
+// on a bpffs; with pin_dir NULL/"" the map fds are kept open in this process instead. If our
+// program is attached but its chain slot is empty (unpinned map after a restart), `base` rules
+// (the runtime's default device list) are compiled in instead of the tail call.
+// Returns the number of programs installed; *prog_id is the first of ours and *chained_id the
+// original it preserves (0 if none).
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
                        const gm_dev_rule_t* base, int nbase, const char* pin_dir,
                        uint32_t* prog_id, uint32_t* chained_id);
-// Removes our program, re-attaching the chained original in its place (if any), and unpins.
+// Removes our programs, re-attaching each chained original in its place (if any), and unpins.
+// Returns how many were removed.
 int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir);
 
 // ---- device nodes ---------------------------------------------------------------------------

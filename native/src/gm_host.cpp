@@ -173,16 +173,19 @@ int make_chain_map(int target_prog_fd) {
 }
 
 // ---- tail-call map lifetime (see gm_host.h: PROG_ARRAY slots die with the last user ref)
+// One map per wrapped program, keyed by (cgroup inode, id of the program it chains to).
 std::mutex g_keep_mu;
-std::map<uint64_t, int> g_kept_maps;  // cgroup inode → map fd kept open (no bpffs available)
+std::map<std::pair<uint64_t, uint32_t>, int> g_kept_maps;  // map fds kept open (no bpffs)
 
 uint64_t cgroup_ino(int cgfd) {
   struct stat st;
   return fstat(cgfd, &st) == 0 ? (uint64_t)st.st_ino : 0;
 }
 
-std::string pin_path(const char* pin_dir, uint64_t ino) {
-  return std::string(pin_dir) + "/gm_" + std::to_string(ino);
+std::string pin_prefix(uint64_t ino) { return "gm_" + std::to_string(ino); }
+
+std::string pin_path(const char* pin_dir, uint64_t ino, uint32_t chain) {
+  return std::string(pin_dir) + "/" + pin_prefix(ino) + "_" + std::to_string(chain);
 }
 
 int obj_pin(int fd, const std::string& path) {
@@ -194,9 +197,9 @@ int obj_pin(int fd, const std::string& path) {
 }
 
 // Makes `map_fd` survive this call: pin (atomically replacing the previous pin) or keep the fd.
-int keep_map(const char* pin_dir, uint64_t ino, int map_fd) {
+int keep_map(const char* pin_dir, uint64_t ino, uint32_t chain, int map_fd) {
   if (pin_dir && *pin_dir) {
-    const std::string final_path = pin_path(pin_dir, ino);
+    const std::string final_path = pin_path(pin_dir, ino, chain);
     const std::string tmp = final_path + "_new";  // bpffs rejects "." in names
     unlink(tmp.c_str());
     int e = obj_pin(map_fd, tmp);
@@ -211,19 +214,44 @@ int keep_map(const char* pin_dir, uint64_t ino, int map_fd) {
   int dupfd = fcntl(map_fd, F_DUPFD_CLOEXEC, 0);
   if (dupfd < 0) return -errno;
   std::lock_guard<std::mutex> lk(g_keep_mu);
-  auto it = g_kept_maps.find(ino);
+  auto key = std::make_pair(ino, chain);
+  auto it = g_kept_maps.find(key);
   if (it != g_kept_maps.end()) close(it->second);
-  g_kept_maps[ino] = dupfd;
+  g_kept_maps[key] = dupfd;
   return 0;
 }
 
-void drop_map(const char* pin_dir, uint64_t ino) {
-  if (pin_dir && *pin_dir) unlink(pin_path(pin_dir, ino).c_str());
+// Drops every kept/pinned map of the cgroup whose chain target is not in `keep`
+// (also the single-map pin name "gm_<ino>" of ABI 1).
+void drop_maps_except(const char* pin_dir, uint64_t ino, const std::vector<uint32_t>& keep) {
+  auto kept = [&](uint32_t c) {
+    for (uint32_t k : keep)
+      if (k == c) return true;
+    return false;
+  };
+  if (pin_dir && *pin_dir) {
+    const std::string pre = pin_prefix(ino);
+    unlink((std::string(pin_dir) + "/" + pre).c_str());
+    if (DIR* d = opendir(pin_dir)) {
+      while (struct dirent* de = readdir(d)) {
+        const char* nm = de->d_name;
+        if (strncmp(nm, pre.c_str(), pre.size()) != 0 || nm[pre.size()] != '_') continue;
+        char* end = nullptr;
+        unsigned long c = strtoul(nm + pre.size() + 1, &end, 10);
+        if (end && *end == 0 && kept((uint32_t)c)) continue;
+        unlinkat(dirfd(d), nm, 0);
+      }
+      closedir(d);
+    }
+  }
   std::lock_guard<std::mutex> lk(g_keep_mu);
-  auto it = g_kept_maps.find(ino);
-  if (it != g_kept_maps.end()) {
-    close(it->second);
-    g_kept_maps.erase(it);
+  for (auto it = g_kept_maps.begin(); it != g_kept_maps.end();) {
+    if (it->first.first == ino && !kept(it->first.second)) {
+      close(it->second);
+      it = g_kept_maps.erase(it);
+    } else {
+      ++it;
+    }
   }
 }
 
@@ -649,43 +677,56 @@ int gm_bpf_prog_name(uint32_t id, char* name, int cap) {
   return 0;
 }
 
-int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, uint32_t* n,
-                       uint32_t* prog_id) {
+int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, uint64_t* insns, uint32_t cap,
+                          uint32_t* n, uint32_t* prog_id, uint32_t* foreign) {
   *n = 0;
   if (prog_id) *prog_id = 0;
+  if (foreign) *foreign = 0;
   Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
   if (!cg.ok()) return -errno;
   Attached at;
   int e = query(cg.fd, &at);
   if (e < 0) return e;
+  uint32_t k = 0;
+  int found = -1;
   for (uint32_t id : at.ids) {
-    if (!is_ours(id, nullptr)) continue;
-    Fd pfd(get_prog_fd_by_id(id));
-    if (!pfd.ok()) return pfd.fd;
-    struct bpf_prog_info info;
-    union bpf_attr a;
-    memset(&info, 0, sizeof(info));
-    memset(&a, 0, sizeof(a));
-    a.info.bpf_fd = (uint32_t)pfd.fd;
-    a.info.info_len = sizeof(info);
-    a.info.info = ptr_u64(&info);
-    if (sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a, sizeof(a)) < 0) return -errno;
-    if (prog_id) *prog_id = id;
-    const uint32_t need = info.xlated_prog_len / 8;
-    if (need == 0) return -EPERM;  // !bpf_capable(): the kernel reports no instructions
-    *n = need;
-    if (need > cap || insns == nullptr) return -ENOSPC;
-    memset(&info, 0, sizeof(info));
-    info.xlated_prog_len = need * 8;
-    info.xlated_prog_insns = ptr_u64(insns);
-    memset(&a, 0, sizeof(a));
-    a.info.bpf_fd = (uint32_t)pfd.fd;
-    a.info.info_len = sizeof(info);
-    a.info.info = ptr_u64(&info);
-    if (sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a, sizeof(a)) < 0) return -errno;
-    return 0;
+    if (!is_ours(id, nullptr)) {
+      if (foreign) ++*foreign;
+      continue;
+    }
+    if (k++ == index && found < 0) found = (int)id;
   }
+  if (found < 0) return 0;
+  const uint32_t id = (uint32_t)found;
+  Fd pfd(get_prog_fd_by_id(id));
+  if (!pfd.ok()) return pfd.fd;
+  struct bpf_prog_info info;
+  union bpf_attr a;
+  memset(&info, 0, sizeof(info));
+  memset(&a, 0, sizeof(a));
+  a.info.bpf_fd = (uint32_t)pfd.fd;
+  a.info.info_len = sizeof(info);
+  a.info.info = ptr_u64(&info);
+  if (sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a, sizeof(a)) < 0) return -errno;
+  if (prog_id) *prog_id = id;
+  const uint32_t need = info.xlated_prog_len / 8;
+  if (need == 0) return -EPERM;  // !bpf_capable(): the kernel reports no instructions
+  *n = need;
+  if (need > cap || insns == nullptr) return -ENOSPC;
+  memset(&info, 0, sizeof(info));
+  info.xlated_prog_len = need * 8;
+  info.xlated_prog_insns = ptr_u64(insns);
+  memset(&a, 0, sizeof(a));
+  a.info.bpf_fd = (uint32_t)pfd.fd;
+  a.info.info_len = sizeof(info);
+  a.info.info = ptr_u64(&info);
+  if (sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a, sizeof(a)) < 0) return -errno;
   return 0;
+}
+
+int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, uint32_t* n,
+                       uint32_t* prog_id) {
+  return gm_bpf_dev_program_at(cgroup_path, 0, insns, cap, n, prog_id, nullptr);
 }
 
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
@@ -698,66 +739,75 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
   int e = query(cg.fd, &at);
   if (e < 0) return e;
 
-  uint32_t replace_id = 0, chain_id = 0;
-  bool ours_without_chain = false;
-  int foreign = 0;
+  // One slot per attached program. Under BPF_F_ALLOW_MULTI every program must allow an access,
+  // so each one is wrapped: ours (rules → allow, else tail-call the original). A program of ours
+  // is re-generated around the original it already wraps. With nothing attached, one slot with
+  // default-allow (the cgroup was unrestricted).
+  struct Slot {
+    uint32_t replace_id = 0, chain_id = 0;
+    bool ours_without_chain = false;
+  };
+  std::vector<Slot> slots;
   for (uint32_t id : at.ids) {
+    Slot sl;
     uint32_t c = 0;
+    sl.replace_id = id;
     if (is_ours(id, &c)) {
-      replace_id = id;
-      chain_id = c;
-      ours_without_chain = (c == 0);
+      sl.chain_id = c;
+      sl.ours_without_chain = (c == 0);
     } else {
-      ++foreign;
+      sl.chain_id = id;
     }
+    slots.push_back(sl);
   }
-  if (!replace_id) {
-    if (foreign > 1) return -EMLINK;  // ALLOW_MULTI stack: every program must allow; refuse
-    if (foreign == 1) {
-      for (uint32_t id : at.ids) chain_id = id;
-      replace_id = chain_id;
-    }
-  }
+  if (slots.empty()) slots.push_back(Slot{});
+  if (slots.size() > 1 && !(at.flags & BPF_F_ALLOW_MULTI)) return -EINVAL;  // impossible state
 
-  Fd chain_prog, chain_map, replace_fd;
-  if (chain_id) {
-    chain_prog = Fd(get_prog_fd_by_id(chain_id));
-    if (!chain_prog.ok()) return chain_prog.fd;
-    chain_map = Fd(make_chain_map(chain_prog.fd));
-    if (!chain_map.ok()) return chain_map.fd;
-  }
-  if (replace_id) {
-    replace_fd = Fd(get_prog_fd_by_id(replace_id));
-    if (!replace_fd.ok()) return replace_fd.fd;
-  }
-  // rules = ours, then (chain lost) the runtime's default list compiled in
-  std::vector<gm_dev_rule_t> all(rules, rules + n);
-  if (ours_without_chain && base && nbase > 0) all.insert(all.end(), base, base + nbase);
-  // With a chained original (or a compiled-in base list) the fall-through is deny; with neither
-  // the cgroup was unrestricted, so default-allow keeps that behaviour.
-  const int default_allow = (chain_id || ours_without_chain) ? 0 : 1;
-  std::vector<uint64_t> prog(16 + all.size() * 12);
-  int cnt = gm_bpf_dev_build(all.data(), (int)all.size(), default_allow,
-                             chain_map.ok() ? chain_map.fd : -1, prog.data(), (int)prog.size());
-  if (cnt < 0) return -EINVAL;
-  char log[4096];
-  Fd pfd(gm_bpf_dev_load(prog.data(), cnt, kProgName, log, sizeof(log)));
-  if (!pfd.ok()) return pfd.fd;
-  if (chain_map.ok()) {
-    e = keep_map(pin_dir, ino, chain_map.fd);
+  std::vector<uint32_t> chains;
+  uint32_t first_prog = 0;
+  for (const Slot& sl : slots) {
+    Fd chain_prog, chain_map, replace_fd;
+    if (sl.chain_id) {
+      chain_prog = Fd(get_prog_fd_by_id(sl.chain_id));
+      if (!chain_prog.ok()) return chain_prog.fd;
+      chain_map = Fd(make_chain_map(chain_prog.fd));
+      if (!chain_map.ok()) return chain_map.fd;
+    }
+    if (sl.replace_id) {
+      replace_fd = Fd(get_prog_fd_by_id(sl.replace_id));
+      if (!replace_fd.ok()) return replace_fd.fd;
+    }
+    // rules = ours, then (chain lost) the runtime's default list compiled in
+    std::vector<gm_dev_rule_t> all(rules, rules + n);
+    if (sl.ours_without_chain && base && nbase > 0) all.insert(all.end(), base, base + nbase);
+    // With a chained original (or a compiled-in base list) the fall-through is deny; with
+    // neither the cgroup was unrestricted, so default-allow keeps that behaviour.
+    const int default_allow = (sl.chain_id || sl.ours_without_chain) ? 0 : 1;
+    std::vector<uint64_t> prog(16 + all.size() * 12);
+    int cnt = gm_bpf_dev_build(all.data(), (int)all.size(), default_allow,
+                               chain_map.ok() ? chain_map.fd : -1, prog.data(), (int)prog.size());
+    if (cnt < 0) return -EINVAL;
+    char log[4096];
+    Fd pfd(gm_bpf_dev_load(prog.data(), cnt, kProgName, log, sizeof(log)));
+    if (!pfd.ok()) return pfd.fd;
+    if (chain_map.ok()) {
+      e = keep_map(pin_dir, ino, sl.chain_id, chain_map.fd);
+      if (e < 0) return e;
+      chains.push_back(sl.chain_id);
+    }
+    e = attach(cg.fd, pfd.fd, replace_fd.ok() ? replace_fd.fd : -1,
+               at.ids.empty() ? BPF_F_ALLOW_MULTI : at.flags);
     if (e < 0) return e;
+    if (!first_prog) {
+      struct bpf_prog_info info;
+      uint32_t maps[1];
+      first_prog = prog_info(pfd.fd, &info, maps, 0) == 0 ? info.id : 0;
+    }
   }
-  e = attach(cg.fd, pfd.fd, replace_fd.ok() ? replace_fd.fd : -1,
-             at.ids.empty() ? BPF_F_ALLOW_MULTI : at.flags);
-  if (e < 0) return e;
-  if (!chain_map.ok()) drop_map(pin_dir, ino);
-  if (prog_id) {
-    struct bpf_prog_info info;
-    uint32_t maps[1];
-    *prog_id = prog_info(pfd.fd, &info, maps, 0) == 0 ? info.id : 0;
-  }
-  if (chained_id) *chained_id = chain_id;
-  return 0;
+  drop_maps_except(pin_dir, ino, chains);
+  if (prog_id) *prog_id = first_prog;
+  if (chained_id) *chained_id = slots[0].chain_id;
+  return (int)slots.size();
 }
 
 int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir) {
@@ -767,6 +817,7 @@ int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir) {
   Attached at;
   int e = query(cg.fd, &at);
   if (e < 0) return e;
+  int restored = 0;
   for (uint32_t id : at.ids) {
     uint32_t chain = 0;
     if (!is_ours(id, &chain)) continue;
@@ -776,19 +827,19 @@ int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir) {
       Fd orig(get_prog_fd_by_id(chain));
       if (!orig.ok()) return orig.fd;
       e = attach(cg.fd, orig.fd, ours.fd, at.flags);
-      if (e == 0) drop_map(pin_dir, ino);
-      return e;
+    } else {
+      union bpf_attr a;
+      memset(&a, 0, sizeof(a));
+      a.target_fd = (uint32_t)cg.fd;
+      a.attach_bpf_fd = (uint32_t)ours.fd;
+      a.attach_type = BPF_CGROUP_DEVICE;
+      e = sys_bpf(BPF_PROG_DETACH, &a, sizeof(a)) < 0 ? -errno : 0;
     }
-    union bpf_attr a;
-    memset(&a, 0, sizeof(a));
-    a.target_fd = (uint32_t)cg.fd;
-    a.attach_bpf_fd = (uint32_t)ours.fd;
-    a.attach_type = BPF_CGROUP_DEVICE;
-    e = sys_bpf(BPF_PROG_DETACH, &a, sizeof(a)) < 0 ? -errno : 0;
-    if (e == 0) drop_map(pin_dir, ino);
-    return e;
+    if (e < 0) return e;
+    ++restored;
   }
-  return 0;
+  drop_maps_except(pin_dir, ino, {});
+  return restored;
 }
 
 // ------------------------------------------------------------------ device nodes

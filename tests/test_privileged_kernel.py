@@ -100,14 +100,15 @@ def cgroup2_child():
         os.rmdir(mnt)
 
 
-def attach_runtime_program(cg):
-    """Mimic runc: allow /dev/null rw + mknod, deny everything else, ALLOW_MULTI."""
-    rules = _rule_array([_native.DevRule(b"c", 7, 1, 0, 1, 3)])
+def attach_runtime_program(cg, name=b"runc_devices", nodes=((1, 3),)):
+    """Mimic runc (or systemd): allow the given nodes rw + mknod, deny everything else,
+    ALLOW_MULTI. Default: /dev/null only."""
+    rules = _rule_array([_native.DevRule(b"c", 7, 1, 0, ma, mi) for ma, mi in nodes])
     lib = _native.host()
-    need = -lib.gm_bpf_dev_build(rules, 1, 0, -1, None, 0)
+    need = -lib.gm_bpf_dev_build(rules, len(nodes), 0, -1, None, 0)
     buf = (C.c_uint64 * need)()
-    n = lib.gm_bpf_dev_build(rules, 1, 0, -1, buf, need)
-    fd = lib.gm_bpf_dev_load(buf, n, b"runc_devices", None, 0)
+    n = lib.gm_bpf_dev_build(rules, len(nodes), 0, -1, buf, need)
+    fd = lib.gm_bpf_dev_load(buf, n, name, None, 0)
     assert fd >= 0, os.strerror(-fd)
     # BPF_PROG_ATTACH through a throwaway install path is not possible (ours would replace it),
     # so attach with raw syscall via ctypes
@@ -155,6 +156,46 @@ def test_cgroup_v2_bpf_install_and_restore(cgroup2_child, bpffs, pinned):
     _native.host().gm_bpf_prog_name(ids[0], name, 32)
     assert n.value == 1 and name.value == b"runc_devices"
     assert not [f for f in os.listdir(bpffs) if f.startswith("gm_")]  # pin removed
+
+
+def _names(cg):
+    ids = (C.c_uint32 * 8)()
+    n, flags = C.c_uint32(0), C.c_uint32(0)
+    assert _native.host().gm_bpf_dev_query(cg.encode(), ids, 8, C.byref(n), C.byref(flags)) == 0
+    out = []
+    for i in range(n.value):
+        name = C.create_string_buffer(32)
+        _native.host().gm_bpf_prog_name(ids[i], name, 32)
+        out.append(name.value.decode())
+    return sorted(out)
+
+
+def test_cgroup_v2_wraps_every_program_of_an_allow_multi_stack(cgroup2_child, bpffs):
+    """systemd-driver hosts: runc's program and systemd's (from the scope's DeviceAllow) are both
+    attached, and each can veto an access. Every one gets wrapped; a program systemd attaches
+    later makes the audit report nothing granted until the reconciler wraps that one too."""
+    cg = cgroup2_child
+    paths = [NULL.path, ZERO.path, FULL.path]
+    attach_runtime_program(cg, b"runc_devices", ((1, 3), (1, 7)))     # null + full
+    attach_runtime_program(cg, b"sd_devices", ((1, 3),))              # null only
+    assert probe_access(cg, paths) == "100"          # both must allow
+    be = V2BpfBackend(bpffs)
+    be.apply(cg, [ZERO], [], [ZERO])
+    assert _names(cg) == ["gm_devallow", "gm_devallow"]
+    assert probe_access(cg, paths) == "110"          # /dev/full still vetoed by "systemd"
+    assert (ZERO.major, ZERO.minor) in be.allowed(cg)
+    assert len([f for f in os.listdir(bpffs) if f.startswith("gm_")]) == 2
+    # systemd re-realises the unit (daemon-reload) and attaches a fresh program of its own
+    attach_runtime_program(cg, b"sd_devices", ((1, 3),))
+    assert probe_access(cg, paths) == "100"
+    assert be.allowed(cg) == set()                   # audit sees the veto
+    be.apply(cg, [], [], [ZERO])                     # reconciler re-install
+    assert _names(cg) == ["gm_devallow"] * 3
+    assert probe_access(cg, paths) == "110"
+    be.apply(cg, [], [ZERO], [])                     # last GPU gone: originals back, pins gone
+    assert _names(cg) == ["runc_devices", "sd_devices", "sd_devices"]
+    assert probe_access(cg, paths) == "100"
+    assert not [f for f in os.listdir(bpffs) if f.startswith("gm_")]
 
 
 def test_cgroup_v2_chain_lost_falls_back_to_oci_defaults(cgroup2_child):
