@@ -140,7 +140,8 @@ def host() -> C.CDLL:
         lib.gm_bpf_prog_name.argtypes = [C.c_uint32, C.c_char_p, C.c_int]
         lib.gm_bpf_dev_program.argtypes = [C.c_char_p, C.POINTER(C.c_uint64), C.c_uint32,
                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
-        lib.gm_bpf_dev_program_at.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_uint64),
+        lib.gm_bpf_dev_program_at.argtypes = [C.c_char_p, C.c_uint32, C.c_int,
+                                              C.POINTER(C.c_uint64),
                                               C.c_uint32, C.POINTER(C.c_uint32),
                                               C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.gm_bpf_dev_install.argtypes = [C.c_char_p, C.POINTER(DevRule), C.c_int,
@@ -162,6 +163,12 @@ def host() -> C.CDLL:
                                                  C.c_uint32, C.POINTER(C.c_int32)]
         lib.gm_proc_read_pids.argtypes = [C.c_char_p, C.POINTER(C.c_int32), C.c_int,
                                           C.POINTER(C.c_int)]
+        lib.gm_sd_get_device_allow.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int,
+                                               C.c_char_p, C.c_int]
+        lib.gm_sd_set_device_allow.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_char_p),
+                                               C.POINTER(C.c_char_p), C.c_int, C.c_int,
+                                               C.c_char_p, C.c_int]
+        lib.gm_sd_unit_path.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
         lib.gm_roctx_push.argtypes = [C.c_char_p]
         lib.gm_roctx_mark.argtypes = [C.c_char_p]
         lib.gm_now_ns.restype = C.c_uint64

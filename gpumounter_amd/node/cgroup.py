@@ -299,29 +299,41 @@ class V2BpfBackend(DeviceRuleBackend):
     def allowed(self, cgdir):
         """What the kernel enforces: the xlated instructions of every attached program of ours,
         evaluated by the interpreter; a pair counts only if all of them grant it. A program that
-        systemd or the runtime swapped out, or a foreign program attached next to ours (it can
-        veto any access under BPF_F_ALLOW_MULTI), reads as "nothing granted", so the reconciler
-        re-installs and wraps it."""
+        systemd or the runtime swapped out reads as "nothing granted", so the reconciler
+        re-installs it. A foreign program attached next to ours (systemd re-realising its unit)
+        can veto any access under BPF_F_ALLOW_MULTI, so its own verdict is evaluated too: with
+        the unit's DeviceAllow= kept in step (node/systemd.py) it grants our nodes; otherwise the
+        pair reads as missing and the re-install wraps that program."""
         progs, foreign = attached_programs(cgdir)
-        if not progs or foreign:
+        if not progs:
             return set()
         out = program_allows(progs[0])
         for p in progs[1:]:
             out &= program_allows(p)
+        for i in range(foreign):
+            prog, _ = _program_at(cgdir, i, foreign_only=True)
+            if prog is None:
+                break
+            try:
+                out = bpfvm.allowed_pairs(prog, sorted(out), chained=lambda *a: 0)
+            except bpfvm.BpfError:
+                return set()                   # cannot judge it: assume it vetoes
         return out
 
 
-def _program_at(cgdir: str, index: int) -> Tuple[Optional[List[int]], int]:
+def _program_at(cgdir: str, index: int, foreign_only: bool = False
+                ) -> Tuple[Optional[List[int]], int]:
     lib = _native.host()
     n, pid, foreign = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
-    rc = lib.gm_bpf_dev_program_at(cgdir.encode(), index, None, 0, C.byref(n), C.byref(pid),
+    fo = 1 if foreign_only else 0
+    rc = lib.gm_bpf_dev_program_at(cgdir.encode(), index, fo, None, 0, C.byref(n), C.byref(pid),
                                    C.byref(foreign))
     if rc == 0 and n.value == 0:
         return None, foreign.value
     if rc not in (0, -errno.ENOSPC):
         raise CgroupError(f"bpf introspection on {cgdir}: {os.strerror(-rc)}")
     buf = (C.c_uint64 * n.value)()
-    rc = lib.gm_bpf_dev_program_at(cgdir.encode(), index, buf, n.value, C.byref(n),
+    rc = lib.gm_bpf_dev_program_at(cgdir.encode(), index, fo, buf, n.value, C.byref(n),
                                    C.byref(pid), C.byref(foreign))
     if rc < 0:
         raise CgroupError(f"bpf introspection on {cgdir}: {os.strerror(-rc)}")

@@ -58,6 +58,10 @@ class Config:
     cgroup_root: str = "/sys/fs/cgroup"
     cgroup_mode: str = "auto"          # auto | v1 | v2
     cgroup_driver: str = "auto"        # auto | cgroupfs | systemd
+    # record hot-mounted nodes in the container scope's DeviceAllow= so systemd keeps them when
+    # it re-realises the unit: auto (systemd-named cgroup + bus socket present) | on | off
+    systemd_device_allow: str = "auto"
+    systemd_bus: str = ""              # "" = /run/systemd/private, then the system bus socket
     bpf_pin_dir: str = "/sys/fs/bpf/gpumounter"  # bpffs dir for v2 tail-call maps ("" = keep fd)
     devnode_mode: str = "procroot"     # procroot | setns | emulate
     proc_root: str = "/proc"
@@ -164,6 +168,7 @@ class Config:
     def validate(self) -> None:
         _choice("cgroup_mode", self.cgroup_mode, ("auto", "v1", "v2"))
         _choice("cgroup_driver", self.cgroup_driver, ("auto", "cgroupfs", "systemd"))
+        _choice("systemd_device_allow", self.systemd_device_allow, ("auto", "on", "off"))
         _choice("devnode_mode", self.devnode_mode, ("procroot", "setns", "emulate"))
         _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
         _choice("placement_enforce", self.placement_enforce, ("hint", "trim"))

@@ -23,6 +23,7 @@ from gpumounter_amd.cluster.kube import KubeClient
 from gpumounter_amd.cluster.placeholder import PlaceholderManager
 from gpumounter_amd.cluster.pool import WarmPool
 from gpumounter_amd.hw.inventory import Inventory
+from gpumounter_amd.node import systemd
 from gpumounter_amd.node.cgroup import CgroupResolver, make_backend
 from gpumounter_amd.node.devnodes import DevNodeWriter
 from gpumounter_amd.node.hotmount import HotMount
@@ -60,6 +61,11 @@ class Worker:
                                        cfg.proc_root)
         emulate = cfg.devnode_mode == "emulate" or os.environ.get("GM_BPF_EMULATE") == "1"
         self.backend = make_backend(self.resolver.mode, emulate, cfg.bpf_pin_dir)
+        sd_mode = cfg.systemd_device_allow
+        if emulate and sd_mode == "auto" and not cfg.systemd_bus:
+            sd_mode = "off"          # hermetic runs never talk to the host's systemd by accident
+        self.backend = systemd.maybe_wrap(self.backend, sd_mode, cfg.systemd_bus,
+                                          self.resolver.driver)
         self.writer = DevNodeWriter(cfg.devnode_mode)
         self.faults = FaultInjector(cfg.fault)
         self.hotmount = HotMount(cfg, self.inv, self.resolver, self.backend, self.writer,
@@ -220,6 +226,8 @@ class Worker:
         await self.pool.stop()
         await self.reconciler.stop()
         await self.service.notify.stop()
+        if isinstance(self.backend, systemd.SystemdPersistingBackend):
+            self.backend.sync.stop()
         if self.plugin is not None:
             await self.plugin.stop()
         if self.grpc_server is not None:

@@ -64,10 +64,12 @@ int gm_bpf_prog_name(uint32_t id, char* name, int cap);
 // attached; -ENOSPC (with *n = needed) if cap is too small; -EPERM if the kernel hides xlated code.
 int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, uint32_t* n,
                        uint32_t* prog_id);
-// Same for the index-th gpumounter program (several when several programs were wrapped); *n = 0
-// past the last one. *foreign = programs attached that are not ours (each can veto an access).
-int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, uint64_t* insns, uint32_t cap,
-                          uint32_t* n, uint32_t* prog_id, uint32_t* foreign);
+// Same for the index-th gpumounter program (several when several programs were wrapped), or with
+// foreign_only=1 the index-th program that is not ours (each can veto an access under
+// BPF_F_ALLOW_MULTI); *n = 0 past the last one. *foreign = number of programs not ours.
+int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, int foreign_only,
+                          uint64_t* insns, uint32_t cap, uint32_t* n, uint32_t* prog_id,
+                          uint32_t* foreign);
 // Installs (or updates) the gpumounter allow-list on a cgroup-v2 directory. Every attached
 // program is wrapped, because under BPF_F_ALLOW_MULTI each one must allow an access (runc and
 // systemd both attach one on systemd-driver hosts):
@@ -129,6 +131,20 @@ int gm_proc_filter_dev_users(const int32_t* pids, int n, uint32_t major, uint32_
                              int32_t* out);
 // Parses a cgroup.procs-style file. *n = total.
 int gm_proc_read_pids(const char* path, int32_t* pids, int cap, int* n);
+
+// ---- systemd unit device policy (D-Bus; native/src/gm_sdbus.cpp) ------------------------------
+// bus_path: systemd's private socket (/run/systemd/private, peer-to-peer) or the system bus
+// socket (/run/dbus/system_bus_socket: Hello, destination org.freedesktop.systemd1). -EPROTO means
+// a D-Bus error; its name and message are copied to `err`.
+// The unit's DeviceAllow= as "path\tperm\n" lines in `out`; returns the length or -errno.
+int gm_sd_get_device_allow(const char* bus_path, const char* unit, char* out, int cap, char* err,
+                           int errcap);
+// SetUnitProperties(unit, runtime=true, DeviceAllow=...): appends the entries, or with reset=1
+// replaces the whole list by them (an empty list first, then the entries, in one call).
+int gm_sd_set_device_allow(const char* bus_path, const char* unit, const char* const* paths,
+                           const char* const* perms, int n, int reset, char* err, int errcap);
+// D-Bus object path of a unit (sd_bus_path_encode). Returns the length or -(needed).
+int gm_sd_unit_path(const char* unit, char* out, int cap);
 
 // ---- tracing --------------------------------------------------------------------------------
 int gm_roctx_available(void);

@@ -677,8 +677,9 @@ int gm_bpf_prog_name(uint32_t id, char* name, int cap) {
   return 0;
 }
 
-int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, uint64_t* insns, uint32_t cap,
-                          uint32_t* n, uint32_t* prog_id, uint32_t* foreign) {
+int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, int foreign_only,
+                          uint64_t* insns, uint32_t cap, uint32_t* n, uint32_t* prog_id,
+                          uint32_t* foreign) {
   *n = 0;
   if (prog_id) *prog_id = 0;
   if (foreign) *foreign = 0;
@@ -690,10 +691,9 @@ int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, uint64_t* ins
   uint32_t k = 0;
   int found = -1;
   for (uint32_t id : at.ids) {
-    if (!is_ours(id, nullptr)) {
-      if (foreign) ++*foreign;
-      continue;
-    }
+    const bool ours = is_ours(id, nullptr);
+    if (!ours && foreign) ++*foreign;
+    if (ours == (foreign_only != 0)) continue;
     if (k++ == index && found < 0) found = (int)id;
   }
   if (found < 0) return 0;
@@ -726,7 +726,7 @@ int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, uint64_t* ins
 
 int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, uint32_t* n,
                        uint32_t* prog_id) {
-  return gm_bpf_dev_program_at(cgroup_path, 0, insns, cap, n, prog_id, nullptr);
+  return gm_bpf_dev_program_at(cgroup_path, 0, 0, insns, cap, n, prog_id, nullptr);
 }
 
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,

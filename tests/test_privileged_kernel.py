@@ -188,7 +188,7 @@ def test_cgroup_v2_wraps_every_program_of_an_allow_multi_stack(cgroup2_child, bp
     # systemd re-realises the unit (daemon-reload) and attaches a fresh program of its own
     attach_runtime_program(cg, b"sd_devices", ((1, 3),))
     assert probe_access(cg, paths) == "100"
-    assert be.allowed(cg) == set()                   # audit sees the veto
+    assert (ZERO.major, ZERO.minor) not in be.allowed(cg)   # audit sees the veto
     be.apply(cg, [], [], [ZERO])                     # reconciler re-install
     assert _names(cg) == ["gm_devallow"] * 3
     assert probe_access(cg, paths) == "110"
@@ -196,6 +196,51 @@ def test_cgroup_v2_wraps_every_program_of_an_allow_multi_stack(cgroup2_child, bp
     assert _names(cg) == ["runc_devices", "sd_devices", "sd_devices"]
     assert probe_access(cg, paths) == "100"
     assert not [f for f in os.listdir(bpffs) if f.startswith("gm_")]
+
+
+def test_systemd_reload_keeps_hot_mounted_device_via_device_allow(cgroup2_child, bpffs, tmp_path):
+    """A fake systemd that, like the real one, realises the unit's DeviceAllow= as a fresh device
+    program on every change (ALLOW_MULTI; its previous program it tries to detach is already
+    wrapped by ours). With DeviceAllow= kept in step the hot-mounted device survives it, and the
+    audit accepts systemd's program because it evaluates it."""
+    from gpumounter_amd.fakes.systemd_bus import FakeSystemd
+    from gpumounter_amd.node.systemd import DeviceAllowSync, SystemdBus, SystemdPersistingBackend
+
+    cg = cgroup2_child
+    paths = [NULL.path, ZERO.path, FULL.path]
+    unit = "cri-containerd-" + os.path.basename(cg) + ".scope"
+    scope = os.path.join(os.path.dirname(cg), unit)
+    os.mkdir(scope)
+    try:
+        def realise(_unit, entries):
+            nodes = []
+            for p, _perm in entries:
+                st = os.stat(p)
+                nodes.append((os.major(st.st_rdev), os.minor(st.st_rdev)))
+            attach_runtime_program(scope, b"sd_devices", tuple(nodes))
+
+        fs = FakeSystemd(str(tmp_path / "private"), on_change=realise).start()
+        fs.add_unit(unit, [(NULL.path, "rwm")])
+        attach_runtime_program(scope, b"runc_devices", ((1, 3),))
+        realise(unit, fs.units[unit])                 # systemd's program from the scope's start
+        assert probe_access(scope, paths) == "100"
+        be = SystemdPersistingBackend(V2BpfBackend(bpffs),
+                                      DeviceAllowSync(SystemdBus(fs.path), retry_s=0.01))
+        be.apply(scope, [ZERO], [], [ZERO])
+        assert probe_access(scope, paths) == "110"    # effective at once (BPF, request path)
+        assert be.sync.flush()                        # DeviceAllow= follows; systemd re-realises
+        assert fs.units[unit] == [(NULL.path, "rwm"), (ZERO.path, "rw")]
+        assert _names(scope).count("sd_devices") == 1  # its new program, next to our wrappers
+        assert probe_access(scope, paths) == "110"    # …which grants /dev/zero too
+        assert (ZERO.major, ZERO.minor) in be.allowed(scope)
+        be.apply(scope, [], [ZERO], [])               # detach: DeviceAllow= shrinks back
+        assert be.sync.flush()
+        assert fs.units[unit] == [(NULL.path, "rwm")]
+        assert probe_access(scope, paths) == "100"
+        be.sync.stop()
+        fs.stop()
+    finally:
+        os.rmdir(scope)
 
 
 def test_cgroup_v2_chain_lost_falls_back_to_oci_defaults(cgroup2_child):
