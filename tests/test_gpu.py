@@ -44,6 +44,38 @@ def test_amdsmi_real_inventory(real_inventory):
     assert all(links.types[i][i] == 0 for i in range(links.n))
 
 
+def test_amd_smi_tool_sees_the_same_gpus(real_inventory):
+    """BASELINE config "rocm-smi inside the Pod sees it": the stock ROCm tool and gpumounter's
+    amdsmi shim must agree on BDF and UUID of every GPU (the ledger joins on them)."""
+    import json
+    import re
+
+    try:
+        res = subprocess.run(["amd-smi", "list", "--json"], capture_output=True, text=True,
+                             timeout=90)
+    except FileNotFoundError:
+        pytest.skip("amd-smi not installed")
+    assert res.returncode == 0, res.stderr[-2000:]
+    blob = json.loads(res.stdout[res.stdout.index("["):] if "[" in res.stdout else res.stdout)
+    found = set()
+
+    def walk(x):
+        if isinstance(x, dict):
+            for v in x.values():
+                walk(v)
+        elif isinstance(x, list):
+            for v in x:
+                walk(v)
+        elif isinstance(x, str):
+            found.add(x.lower())
+    walk(blob)
+    bdf_re = re.compile(r"^[0-9a-f]{4}:[0-9a-f]{2}:[0-9a-f]{2}\.[0-7]$")
+    tool_bdfs = {s for s in found if bdf_re.match(s)}
+    ours = real_inventory.gpus()
+    assert {g.bdf.lower() for g in ours} <= tool_bdfs, (tool_bdfs, [g.bdf for g in ours])
+    assert all(g.uuid.lower() in found for g in ours), ([g.uuid for g in ours], sorted(found))
+
+
 def test_probe_props_and_quick():
     from gpumounter_amd.ops import probe
 
