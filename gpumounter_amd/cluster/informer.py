@@ -8,10 +8,10 @@ and are woken by the next matching event instead of polling the apiserver.
 from __future__ import annotations
 
 import asyncio
-import copy
 from typing import Callable, Dict, List, Optional, Tuple
 
 from gpumounter_amd.cluster.kube import ApiError, KubeClient
+from gpumounter_amd.models.pod import jcopy
 from gpumounter_amd.utils import log
 
 _log = log.get("cluster.informer")
@@ -132,7 +132,7 @@ class PodInformer:
 
     def get_copy(self, ns: str, name: str) -> Optional[dict]:
         p = self.cache.get((ns, name))
-        return copy.deepcopy(p) if p is not None else None
+        return jcopy(p) if p is not None else None
 
     def list(self, pred: Callable[[dict], bool] = lambda p: True) -> List[dict]:
         return [p for p in self.cache.values() if pred(p)]

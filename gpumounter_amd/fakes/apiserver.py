@@ -20,7 +20,6 @@ control plane; the default is zero (pure plumbing).
 from __future__ import annotations
 
 import asyncio
-import copy
 import json
 import secrets
 import threading
@@ -115,7 +114,7 @@ def _match_fields(pod: dict, sel) -> bool:
 def merge_patch(target: Any, patch: Any) -> Any:
     """RFC 7386 JSON merge patch."""
     if not isinstance(patch, dict):
-        return copy.deepcopy(patch)
+        return podu.jcopy(patch)
     if not isinstance(target, dict):
         target = {}
     for k, v in patch.items():
@@ -159,7 +158,7 @@ class FakeCluster:
     def _bump(self, etype: str, pod: dict) -> None:
         self.rv += 1
         pod["metadata"]["resourceVersion"] = str(self.rv)
-        snap = copy.deepcopy(pod)
+        snap = podu.jcopy(pod)
         self.events.append((self.rv, etype, snap))
         if len(self.events) > self.HISTORY:
             del self.events[: len(self.events) - self.HISTORY]
@@ -181,7 +180,7 @@ class FakeCluster:
 
     # ------------------------------------------------------------------------ pod CRUD
     def create_pod(self, ns: str, body: dict, *, schedule: bool = True) -> dict:
-        pod = copy.deepcopy(body)
+        pod = podu.jcopy(body)
         md = pod.setdefault("metadata", {})
         if not md.get("name"):
             gen = md.get("generateName")
@@ -514,7 +513,7 @@ class FakeCluster:
         else:
             for p in list(self.pods.values()):
                 if self._matches(p, ns, lsel, fsel):
-                    q.put_nowait(("ADDED", copy.deepcopy(p)))
+                    q.put_nowait(("ADDED", podu.jcopy(p)))
         entry = (q, ns, lsel, fsel)
         self.watchers.append(entry)
         timeout = float(req.query.get("timeoutSeconds", "300"))
