@@ -184,7 +184,29 @@ class ProbeProps(C.Structure):
                 ("clock_khz", C.c_int32), ("mem_clock_khz", C.c_int32)]
 
 
+def _prefer_torch_hip_runtime() -> None:
+    """A process can hold only one HIP runtime, and ``libamdhip64.so.7`` is resolved by soname:
+    whichever copy is loaded first (ROCm's /opt/rocm/lib or the one PyTorch bundles) serves
+    every later user. PyTorch does not work on a newer runtime than it was built for, so when it
+    is installed its bundled runtime is loaded first (by path, without importing torch) and the
+    probe binds to it — the probe then works whether torch is imported before or after."""
+    if "libgm_probe.so" in _libs or os.environ.get("GM_PROBE_SYSTEM_HIP") == "1":
+        return
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    for loc in (spec.submodule_search_locations or []) if spec else []:
+        hip = os.path.join(loc, "lib", "libamdhip64.so")
+        if os.path.exists(hip):
+            try:
+                C.CDLL(hip, mode=C.RTLD_GLOBAL)
+            except OSError:
+                pass
+            return
+
+
 def probe() -> C.CDLL:
+    _prefer_torch_hip_runtime()
     lib = _load("libgm_probe.so", "hip")
     if not getattr(lib, "_gm_typed", False):
         lib.gm_probe_device_count.argtypes = [C.POINTER(C.c_int)]
@@ -192,6 +214,8 @@ def probe() -> C.CDLL:
         lib.gm_probe_find_device.argtypes = [C.c_char_p, C.POINTER(C.c_int)]
         lib.gm_probe_quick.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_double)]
         lib.gm_probe_hbm_copy.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+        lib.gm_probe_hbm_read.argtypes = [C.c_int, C.c_uint64, C.c_int, C.c_int,
+                                          C.POINTER(C.c_double)]
         lib.gm_probe_mfma_peak.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double)]
         lib.gm_probe_gemm_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
                                            C.c_int, C.c_void_p]

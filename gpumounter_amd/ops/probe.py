@@ -62,6 +62,14 @@ def hbm_gbps(dev: int, nbytes: int = 1 << 30, iters: int = 10) -> float:
     return g.value
 
 
+def hbm_read_gbps(dev: int, nbytes: int = 1 << 30, iters: int = 10,
+                  blocks_per_cu: int = 2) -> float:
+    g = C.c_double(0)
+    _check(_native.probe().gm_probe_hbm_read(dev, nbytes, iters, blocks_per_cu, C.byref(g)),
+           "hbm read")
+    return g.value
+
+
 def mfma_tflops(dev: int, iters: int = 20000) -> float:
     t = C.c_double(0)
     _check(_native.probe().gm_probe_mfma_peak(dev, iters, C.byref(t)), "mfma peak")

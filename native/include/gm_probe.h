@@ -33,6 +33,8 @@ int gm_probe_find_device(const char* bdf, int* dev);
 int gm_probe_quick(int dev, int* ok, double* elapsed_us);
 // HBM3E stream: float4 copy of `bytes` for `iters`; *gbps = (read+write) bytes / time.
 int gm_probe_hbm_copy(int dev, uint64_t bytes, int iters, double* gbps);
+// Read-only HBM stream over `bytes` (8 nontemporal 16-B loads in flight per lane); GB/s read.
+int gm_probe_hbm_read(int dev, uint64_t bytes, int iters, int blocks_per_cu, double* gbps);
 // Tuning variants: 0 grid-stride, 1 chunked 4×16B/lane, 2 chunked 4 + nontemporal,
 // 3 chunked 8 + nontemporal, 4 chunked 8.
 int gm_probe_hbm_copy_variant(int dev, int variant, uint64_t bytes, int iters,
