@@ -122,6 +122,7 @@ class VerifyResult:
     quick_us: float
     gcn_arch: str
     hbm_gbps: Optional[float] = None
+    hbm_read_gbps: Optional[float] = None
     mfma_tflops: Optional[float] = None
     gemm_max_abs_err: Optional[float] = None
 
@@ -140,6 +141,7 @@ def verify(bdfs: List[str], full: bool = False) -> List[VerifyResult]:
         r = VerifyResult(dev, bdf, quick(dev), pr["gcn_arch"])
         if full:
             r.hbm_gbps = hbm_gbps(dev)
+            r.hbm_read_gbps = hbm_read_gbps(dev)
             r.mfma_tflops = mfma_tflops(dev)
             r.gemm_max_abs_err = gemm_check(dev)["max_abs_err"]
         out.append(r)
