@@ -205,6 +205,10 @@ class KubeClient:
                                              "resourceAttributes": resource_attributes}})
         return (out or {}).get("status") or {}
 
+    async def list_resource_quotas(self, ns: str) -> List[dict]:
+        out = await self._req("GET", f"/api/v1/namespaces/{ns}/resourcequotas")
+        return out.get("items", [])
+
     async def create_event(self, ns: str, event: dict) -> dict:
         return await self._req("POST", f"/api/v1/namespaces/{ns}/events", body=event)
 

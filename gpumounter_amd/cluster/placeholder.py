@@ -35,6 +35,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
+from gpumounter_amd.cluster.quota import QuotaExceeded
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_GROUP, ANN_IDEMPOTENCY,
                                          ANN_MOUNT_MODE, ANN_OWNER_UID, ANN_PREFERRED, LABEL_APP,
@@ -73,6 +74,13 @@ class Reservation:
     @property
     def device_ids(self) -> List[str]:
         return [d for p in self.placeholders for d in p.device_ids]
+
+
+def _message(e: "ApiError") -> str:
+    body = e.body
+    if isinstance(body, dict):
+        return str(body.get("message") or e)
+    return str(body or e)
 
 
 def _label_value(s: str) -> str:
@@ -282,6 +290,10 @@ class PlaceholderManager:
         errors = [r for r in results if not isinstance(r, dict)]
         if errors:
             await self.release(created, wait=False)
+            quota = [e for e in errors if isinstance(e, ApiError) and e.status == 403
+                     and "exceeded quota" in _message(e)]
+            if quota:   # tenant-namespace placeholders: the apiserver's quota admission said no
+                raise QuotaExceeded(_message(quota[0]))
             raise ReserveError(f"placeholder create failed: {errors[0]}")
         try:
             self.faults.check("ledger_reserve", "after")

@@ -138,6 +138,7 @@ class FakeCluster:
         self.rv = 1000
         self.events: List[Tuple[int, str, dict]] = []
         self.k8s_events: List[dict] = []     # core/v1 Event objects (not the watch history)
+        self.quotas: Dict[Tuple[str, str], dict] = {}   # ResourceQuota objects (spec.hard)
         self.tokens: Dict[str, dict] = {}    # TokenReview: bearer token → user info
         self.rbac: List[dict] = []           # SubjectAccessReview rules (see grant())
         self.sar_count = 0
@@ -198,6 +199,7 @@ class FakeCluster:
         md.setdefault("labels", {})
         md.setdefault("annotations", {})
         pod.setdefault("spec", {})
+        self._quota_admit(ns, pod)
         pod["status"] = {"phase": "Pending", "conditions": []}
         self.pods[(ns, md["name"])] = pod
         self._bump("ADDED", pod)
@@ -207,6 +209,46 @@ class FakeCluster:
 
     def get(self, ns: str, name: str) -> Optional[dict]:
         return self.pods.get((ns, name))
+
+    # ------------------------------------------------------------------------ ResourceQuota
+    def set_quota(self, ns: str, name: str, hard: Dict[str, str]) -> dict:
+        q = {"apiVersion": "v1", "kind": "ResourceQuota",
+             "metadata": {"name": name, "namespace": ns, "uid": str(uuid.uuid4())},
+             "spec": {"hard": dict(hard)}}
+        self.quotas[(ns, name)] = q
+        return q
+
+    def _quota_used(self, ns: str, key: str) -> int:
+        """What the quota controller reports: requests of the namespace's non-terminal pods
+        (extended resources: requests == limits)."""
+        res = key[len("requests."):] if key.startswith("requests.") else key
+        if "/" not in res:
+            return 0
+        return sum(podu.resource_limit(p, res) for (pns, _), p in self.pods.items()
+                   if pns == ns and p.get("status", {}).get("phase") not in ("Succeeded", "Failed"))
+
+    def _quota_view(self, q: dict) -> dict:
+        out = podu.jcopy(q)
+        ns = q["metadata"]["namespace"]
+        out["status"] = {"hard": dict(q["spec"]["hard"]),
+                         "used": {k: str(self._quota_used(ns, k)) for k in q["spec"]["hard"]}}
+        return out
+
+    def _quota_admit(self, ns: str, pod: dict) -> None:
+        """The apiserver's ResourceQuota admission for extended resources."""
+        for (qns, qname), q in self.quotas.items():
+            if qns != ns:
+                continue
+            for key, hard in q["spec"]["hard"].items():
+                res = key[len("requests."):] if key.startswith("requests.") else key
+                want = podu.resource_limit(pod, res) if "/" in res else 0
+                if want and self._quota_used(ns, key) + want > int(hard):
+                    raise web.HTTPForbidden(text=json.dumps(
+                        {"kind": "Status", "reason": "Forbidden", "code": 403,
+                         "message": f'pods "{pod["metadata"].get("name")}" is forbidden: '
+                                    f"exceeded quota: {qname}, requested: {key}={want}, used: "
+                                    f"{key}={self._quota_used(ns, key)}, limited: {key}={hard}"}),
+                        content_type="application/json")
 
     def _used(self, node: str, resource: str, exclude: Tuple[str, str] = ("", "")) -> int:
         total = 0
@@ -454,6 +496,7 @@ class FakeCluster:
         r.add_delete("/api/v1/namespaces/{ns}/pods/{name}", self._h_delete)
         r.add_patch("/api/v1/namespaces/{ns}/pods/{name}", self._h_patch)
         r.add_get("/api/v1/nodes", self._h_nodes)
+        r.add_get("/api/v1/namespaces/{ns}/resourcequotas", self._h_quota_list)
         r.add_post("/apis/authentication.k8s.io/v1/tokenreviews", self._h_token_review)
         r.add_post("/apis/authorization.k8s.io/v1/subjectaccessreviews", self._h_sar)
         r.add_post("/api/v1/namespaces/{ns}/events", self._h_event_create)
@@ -635,6 +678,12 @@ class FakeCluster:
     def events_for(self, ns: str, pod: str) -> List[dict]:
         return [e for e in self.k8s_events if e["metadata"]["namespace"] == ns
                 and e.get("involvedObject", {}).get("name") == pod]
+
+    async def _h_quota_list(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        ns = req.match_info["ns"]
+        items = [self._quota_view(q) for (qns, _), q in self.quotas.items() if qns == ns]
+        return web.json_response({"kind": "ResourceQuotaList", "items": items})
 
     async def _h_nodes(self, req: web.Request) -> web.Response:
         await self._pre(req)

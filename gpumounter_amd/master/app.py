@@ -260,6 +260,9 @@ class Master:
                         "this worker serves" in (e.details() or ""):
                     self._pod_nodes.pop((ns, name), None)   # pod was recreated elsewhere
                     continue
+                if e.code() == grpc.StatusCode.RESOURCE_EXHAUSTED:   # namespace GPU quota
+                    _log.info("AddGPU %s/%s refused: %s", ns, name, e.details())
+                    return 403, e.details(), {"error": e.details()}
                 _log.error("AddGPU rpc to %s failed: %s %s", target, e.code().name, e.details())
                 code = 400 if e.code() == grpc.StatusCode.INVALID_ARGUMENT else 500
                 body = "Service Internal Error" if code == 500 else e.details()

@@ -47,4 +47,5 @@ SLAVE_SUFFIX = "-slave-pod-"
 
 # Error strings carried in gRPC status details (master maps them to HTTP bodies).
 ERR_POLICY = "MountPolicyDenied"
+ERR_QUOTA = "QuotaExceeded"
 ERR_INTERNAL = "Service Internal Error"

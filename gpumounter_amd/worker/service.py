@@ -18,6 +18,7 @@ are identical (see gpumounter_amd/api/gpu_mount.py). Behavioural fixes, each cov
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import json
 import secrets
 import time
@@ -28,14 +29,16 @@ import grpc
 
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.cluster.informer import PodInformer
-from gpumounter_amd.cluster.kube import KubeClient, NotFound
+from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.cluster.placeholder import (InsufficientGPU, Placeholder, PlaceholderManager,
                                                 ReserveError)
+from gpumounter_amd.cluster.quota import GpuQuota, QuotaExceeded
 from gpumounter_amd.hw import topology
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu, gpus_by_key, normalize_device_id
-from gpumounter_amd.models.types import ANN_IDEMPOTENCY, ERR_INTERNAL, ERR_POLICY, MountType
+from gpumounter_amd.models.types import (ANN_IDEMPOTENCY, ERR_INTERNAL, ERR_POLICY, ERR_QUOTA,
+                                         MountType)
 from gpumounter_amd.node import procs
 from gpumounter_amd.node.hotmount import HotMount, MountError
 from gpumounter_amd.node.ledger import LedgerClient, LedgerError
@@ -91,6 +94,7 @@ class GpuMountService:
         self.pool = None  # WarmPool, attached by the Worker when warm_pool_size > 0
         self.plugin = None  # AmdGpuDevicePlugin, attached by the Worker with device_plugin=1
         self.notify = Notifier(cfg, kube)
+        self.quota = GpuQuota(cfg, kube)
         # Reservations that must not interleave on a node run one at a time:
         # * trim briefly holds every free GPU — a concurrent one would see a full node;
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
@@ -281,7 +285,14 @@ class GpuMountService:
                 free = self._free(st)
                 preferred = self._preferred(n, st, free)
             try:
-                res = await self._reserve(pod, n, req, st, preferred, len(free))
+                async with self._quota_guard(req.namespace, n):
+                    res = await self._reserve(pod, n, req, st, preferred, len(free))
+                    await self._quota_recheck(req.namespace, n, res)
+            except QuotaExceeded as e:
+                _log.info("quota refused %d GPU(s) for %s/%s: %s", n, req.namespace,
+                          req.pod_name, e)
+                self.notify.event(pod, "GPUAttachFailed", str(e), warning=True)
+                raise RpcError(grpc.StatusCode.RESOURCE_EXHAUSTED, f"{ERR_QUOTA}: {e}") from e
             except InsufficientGPU as e:
                 _log.info("insufficient GPUs on %s: %s", self.cfg.node_name, e)
                 self.notify.event(pod, "GPUAttachFailed",
@@ -318,6 +329,30 @@ class GpuMountService:
             return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS,
                                       devices=self._devices(new, owner),
                                       message="Add GPU Success")
+
+    @contextlib.asynccontextmanager
+    async def _quota_guard(self, ns: str, n: int):
+        """Quota check before reserving; same-namespace attaches on this node serialise on it."""
+        if not self.quota.active:
+            yield
+            return
+        async with self.quota.lock(ns):
+            with trace.span("quota"):
+                try:
+                    await self.quota.check(ns, n)
+                except ApiError as e:
+                    raise RpcError(grpc.StatusCode.INTERNAL,
+                                   f"{ERR_INTERNAL}: quota lookup: {e}") from e
+            yield
+
+    async def _quota_recheck(self, ns: str, n: int, res) -> None:
+        if not self.quota.active or not (await self.quota.limits(ns)):
+            return
+        try:
+            await self.quota.recheck(ns, n)
+        except QuotaExceeded:
+            await self._release(res.placeholders)
+            raise
 
     def _replay(self, pod: dict, st: PodGpuState, key: str):
         """A retried request (same idempotency key) returns the earlier attach instead of adding
