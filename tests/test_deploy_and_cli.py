@@ -68,7 +68,8 @@ def test_rbac_is_least_privilege():
     binding = next(d for d in docs if d["kind"] == "ClusterRoleBinding")
     assert binding["roleRef"]["name"] != "cluster-admin"
     resources = {r for role in roles for rule in role["rules"] for r in rule["resources"]}
-    assert resources <= {"pods", "nodes", "events", "tokenreviews", "subjectaccessreviews"}
+    assert resources <= {"pods", "nodes", "events", "tokenreviews", "subjectaccessreviews",
+                         "resourcequotas"}
     assert all("*" not in rule["verbs"] for role in roles for rule in role["rules"])
     reviews = [rule for role in roles for rule in role["rules"]
                if set(rule["resources"]) & {"tokenreviews", "subjectaccessreviews"}]
