@@ -38,6 +38,70 @@ def pct(xs, q):
     return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
 
 
+class _LocalCP:
+    """Control-plane adapter: everything on one event loop thread (LocalCluster)."""
+
+    def __init__(self, tc, lc) -> None:
+        self.tc, self.lc = tc, lc
+
+    def add(self, n: int, entire: bool):
+        return self.tc.call(self.lc.add("default", "tenant", n, entire=entire))
+
+    def remove(self, uuids):
+        return self.tc.call(self.lc.remove("default", "tenant", uuids))
+
+    def audit(self) -> list:
+        return self.tc.call(self.lc.audit("default", "tenant"))
+
+    def placeholders_left(self) -> int:
+        return len(self.lc.cluster.placeholders())
+
+    def wait_pool(self, want: int) -> None:
+        pool = self.lc.nodes["node-0"].worker.pool
+        t_wait = time.time()
+        while len(pool.standby()) < want:
+            if time.time() - t_wait > 120:
+                raise RuntimeError("warm pool did not fill")
+            time.sleep(0.001)
+
+    def stop(self) -> None:
+        self.tc.stop()
+
+
+class _ProcCP:
+    """Control-plane adapter: apiserver, worker and master in separate processes."""
+
+    def __init__(self, pc) -> None:
+        self.pc = pc
+
+    def add(self, n: int, entire: bool):
+        return self.pc.add("default", "tenant", n, entire)
+
+    def remove(self, uuids):
+        return self.pc.remove("default", "tenant", uuids)
+
+    def audit(self) -> list:
+        return self.pc.audit("default", "tenant")
+
+    def placeholders_left(self) -> int:
+        return len(self.pc.placeholders())
+
+    def wait_pool(self, want: int) -> None:
+        from gpumounter_amd.models.types import ANN_MOUNT_MODE, MODE_STANDBY
+        t_wait = time.time()
+        while sum(1 for p in self.pc.placeholders()
+                  if (p["metadata"].get("annotations") or {}).get(ANN_MOUNT_MODE) == MODE_STANDBY
+                  and not p["metadata"].get("deletionTimestamp")) < want:
+            if time.time() - t_wait > 120:
+                raise RuntimeError("warm pool did not fill")
+            time.sleep(0.002)
+
+    def stop(self) -> None:
+        codes = self.pc.stop()
+        if any(c != 0 for c in codes.values()):
+            print(f"daemon exit codes: {codes}", file=sys.stderr)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,6 +125,10 @@ def main() -> int:
                     help="after the timed loop, re-run this many attach/detach cycles with the "
                          "emulated reference protocol on the same cluster (0 = skip; only with "
                          "--latency zero and no warm pool)")
+    ap.add_argument("--deploy", choices=("inprocess", "processes"), default="inprocess",
+                    help="processes: fake control plane, worker and master each in their own "
+                         "process via the production entry points (gpumounter_amd/fakes/"
+                         "deployment.py); inprocess: all on one event loop (LocalCluster)")
     ap.add_argument("--protocol", choices=("gpumounter", "reference"), default="gpumounter",
                     help="'reference' re-enacts the reference's call sequence on the same "
                          "cluster (emulated baseline, see gpumounter_amd/fakes/refproto.py)")
@@ -91,7 +159,7 @@ def main() -> int:
     if has_gpu:
         visible = [probe.props(i)["pci_bus_id"] for i in range(probe.device_count())]
 
-    tc = lc = None
+    tc = lc = cp = None
     sleeper = None
     info = {}
     if rank == 0:
@@ -106,26 +174,35 @@ def main() -> int:
             print(f"need {n} GPUs visible to HIP and amdsmi; have {node_bdfs} (amdsmi {bdfs}, "
                   f"HIP {visible})", file=sys.stderr)
             return 3
-        lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
-        tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
-                             node_gpu_bdfs=node_bdfs, device_plugin=args.device_plugin,
-                             worker_overrides={"warm_pool_size": args.warm_pool,
-                                               "placement_enforce": args.placement,
-                                               "gc_tune": True},   # as the daemons run
-                             master_overrides={"gc_tune": True})
-        lc = tc.start()
-        if args.warm_pool:
-            pool = lc.nodes["node-0"].worker.pool
-            t_wait = time.time()
-            while len(pool.standby()) < min(args.warm_pool, len(node_bdfs)):
-                if time.time() - t_wait > 120:
-                    raise RuntimeError("warm pool did not fill")
-                time.sleep(0.01)
-        if args.protocol == "reference":
-            from gpumounter_amd.fakes import refproto
-            refproto.install(lc)
         sleeper = subprocess.Popen(["sleep", "infinity"])
-        lc.tenant("tenant", pids={"main": [sleeper.pid]})
+        if args.deploy == "processes":
+            if args.protocol == "reference" or args.device_plugin:
+                print("--deploy processes runs the gpumounter protocol without the device "
+                      "plugin", file=sys.stderr)
+                return 2
+            from gpumounter_amd.fakes.deployment import ProcessCluster
+            pc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=args.latency,
+                                gpu_bdfs=node_bdfs,
+                                worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
+                                            "GM_PLACEMENT_ENFORCE": args.placement}).start()
+            pc.tenant("tenant", pids={"main": [sleeper.pid]})
+            cp = _ProcCP(pc)
+        else:
+            lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
+            tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
+                                 node_gpu_bdfs=node_bdfs, device_plugin=args.device_plugin,
+                                 worker_overrides={"warm_pool_size": args.warm_pool,
+                                                   "placement_enforce": args.placement,
+                                                   "gc_tune": True},   # as the daemons run
+                                 master_overrides={"gc_tune": True})
+            lc = tc.start()
+            if args.protocol == "reference":
+                from gpumounter_amd.fakes import refproto
+                refproto.install(lc)
+            lc.tenant("tenant", pids={"main": [sleeper.pid]})
+            cp = _LocalCP(tc, lc)
+        if args.warm_pool:
+            cp.wait_pool(min(args.warm_pool, len(node_bdfs)))
         info = {"amdsmi_lib": inv.lib_path, "node_gpus": len(node_bdfs),
                 "amdsmi_gpus": len(bdfs), "gfx": sorted({g.gfx_target for g in inv.gpus()}),
                 "hives": sorted({hex(g.xgmi_hive_id) for g in inv.gpus()})}
@@ -141,12 +218,11 @@ def main() -> int:
         obj = [None]
         if rank == 0:
             t0 = time.perf_counter()
-            code, body = tc.call(lc.add("default", "tenant", n, entire=args.mode == "entire"))
+            code, body = cp.add(n, args.mode == "entire")
             t1 = time.perf_counter()
             if code != 200:
                 raise RuntimeError(f"attach failed: {code} {body}")
-            issues = tc.call(lc.audit("default", "tenant")) if args.protocol == "gpumounter" \
-                else []
+            issues = cp.audit() if args.protocol == "gpumounter" else []
             obj = [{"bdfs": [d["bdf"] for d in body["devices"]],
                     "uuids": [d["uuid"] for d in body["devices"]],
                     "ms": (t1 - t0) * 1e3, "issues": len(issues),
@@ -183,17 +259,12 @@ def main() -> int:
             dist.barrier()
         if rank == 0:
             t0 = time.perf_counter()
-            code, body = tc.call(lc.remove("default", "tenant", st["uuids"]))
+            code, body = cp.remove(st["uuids"])
             t1 = time.perf_counter()
             if code != 200:
                 raise RuntimeError(f"detach failed: {code} {body}")
             if args.warm_pool:   # steady state: the next attach finds a full pool
-                pool = lc.nodes["node-0"].worker.pool
-                t_wait = time.time()
-                while len(pool.standby()) < min(args.warm_pool, pool_cap):
-                    if time.time() - t_wait > 120:
-                        raise RuntimeError("warm pool did not refill")
-                    time.sleep(0.001)
+                cp.wait_pool(min(args.warm_pool, pool_cap))
             if record:
                 attach_ms.append(st["ms"])
                 detach_ms.append((t1 - t0) * 1e3)
@@ -222,13 +293,12 @@ def main() -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ms_per_step = float(t.item())
         if rank == 0:
-            orphan_issues = len(tc.call(lc.audit("default", "tenant"))) \
-                if args.protocol == "gpumounter" else None
-            placeholders_left = len(lc.cluster.placeholders())
+            orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
+            placeholders_left = cp.placeholders_left()
             p50 = pct(attach_ms, 0.5)
             ref = None
             if args.ref_steps > 0 and args.protocol == "gpumounter" and \
-                    args.latency == "zero" and not args.warm_pool:
+                    args.latency == "zero" and not args.warm_pool and lc is not None:
                 from gpumounter_amd.fakes import refproto
                 refproto.install(lc)
                 ra, rd = [], []
@@ -271,7 +341,7 @@ def main() -> int:
                     "protocol": args.protocol if args.protocol == "gpumounter"
                     else "reference (emulated)",
                     "warm_pool": args.warm_pool, "placement": args.placement,
-                    "device_plugin": args.device_plugin,
+                    "device_plugin": args.device_plugin, "deploy": args.deploy,
                 },
                 "attach_p99_ms": round(pct(attach_ms, 0.99), 4),
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),
@@ -288,11 +358,11 @@ def main() -> int:
             print(json.dumps(out), flush=True)
     finally:
         if rank == 0:
+            if cp is not None:
+                cp.stop()
             if sleeper is not None:
                 sleeper.kill()
                 sleeper.wait()
-            if tc is not None:
-                tc.stop()
         if world > 1:
             dist.destroy_process_group()
     return 0

@@ -134,9 +134,10 @@ async def soak(lc, args) -> dict:
     for i in range(2):
         lc.tenant(f"s{i}")
     att, det = [], []
+    width = min(4, len(lc.nodes["node-0"].node.gpus))   # 1..4 GPUs per attach (fewer if small)
     for k in range(args.cycles):
         t = f"s{k % 2}"
-        n = (k % 4) + 1
+        n = (k % width) + 1
         t0 = time.perf_counter()
         code, b = await lc.add("default", t, n, entire=k % 3 == 0)
         t1 = time.perf_counter()

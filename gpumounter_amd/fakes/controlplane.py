@@ -1,0 +1,94 @@
+"""The hermetic Kubernetes control plane as a process of its own.
+
+``python -m gpumounter_amd.fakes.controlplane --workdir D --nodes 2 --info D/info.json`` serves the
+fake apiserver (with its scheduler and per-node kubelet admission), one fake kubelet PodResources
+socket per node and the per-node cgroupfs/rootfs trees — everything a real node agent talks to —
+and no gpumounter component. The real daemons (``python -m gpumounter_amd worker|master``) then run
+as separate processes against it, configured only through ``GM_*`` environment variables, as in
+the DaemonSet/Deployment (see :mod:`gpumounter_amd.fakes.deployment`).
+
+Besides the Kubernetes API it serves two test hooks:
+  ``POST /_fake/tenant``  {"name", "ns", "node", "gpus", "containers", "pids"} → a Running pod
+  ``POST /_fake/worker``  {"node", "port"}  → the worker DaemonSet pod the master discovers
+The info file lists the apiserver URL and each node's kubelet socket, cgroup root and rootfs root.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import signal
+import sys
+
+from aiohttp import web
+
+from gpumounter_amd.fakes.apiserver import LatencyModel
+from gpumounter_amd.fakes.harness import LocalCluster
+from gpumounter_amd.utils import log
+
+
+def _hooks(lc_ref: list):
+    def install(app: web.Application) -> None:
+        async def tenant(req: web.Request) -> web.Response:
+            b = await req.json()
+            pod = lc_ref[0].tenant(b["name"], ns=b.get("ns", "default"),
+                                   node=b.get("node", "node-0"), gpus=int(b.get("gpus", 0)),
+                                   containers=b.get("containers"), pids=b.get("pids"))
+            return web.json_response(pod, status=201)
+
+        async def worker(req: web.Request) -> web.Response:
+            b = await req.json()
+            lc_ref[0].register_worker(b["node"], int(b["port"]), b.get("ip", "127.0.0.1"))
+            return web.json_response({"ok": True}, status=201)
+
+        app.router.add_post("/_fake/tenant", tenant)
+        app.router.add_post("/_fake/worker", worker)
+    return install
+
+
+async def run(args) -> None:
+    ref: list = [None]
+    lc = LocalCluster(n_nodes=args.nodes, amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup,
+                      latency=LatencyModel.realistic() if args.latency == "realistic" else None,
+                      workdir=args.workdir, start_master=False, start_workers=False,
+                      node_gpu_bdfs=[b for b in args.gpu_bdfs.split(",") if b] or None,
+                      app_hook=_hooks(ref))
+    ref[0] = lc
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
+    await lc.start()
+    info = {"api_url": lc.api_url, "pid": os.getpid(),
+            "nodes": {name: {"kubelet_socket": h.kubelet.socket_path,
+                             "cgroup_root": h.node.cgroup_root,
+                             "rootfs_root": h.node.rootfs_root}
+                      for name, h in lc.nodes.items()}}
+    tmp = args.info + ".tmp"
+    with open(tmp, "w") as fh:
+        json.dump(info, fh)
+    os.replace(tmp, args.info)
+    try:
+        await stop.wait()
+    finally:
+        await lc.stop()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="gpumounter_amd.fakes.controlplane")
+    ap.add_argument("--workdir", required=True)
+    ap.add_argument("--info", required=True)
+    ap.add_argument("--nodes", type=int, default=1)
+    ap.add_argument("--amdsmi", default="mock")
+    ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
+    ap.add_argument("--latency", choices=("zero", "realistic"), default="zero")
+    ap.add_argument("--gpu-bdfs", default="", help="comma-separated: the node's GPUs (default all)")
+    args = ap.parse_args(argv)
+    log.setup("WARNING", json_format=False)
+    asyncio.run(run(args))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

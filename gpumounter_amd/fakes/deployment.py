@@ -1,0 +1,241 @@
+"""A deployment-shaped hermetic cluster: every component in its own process.
+
+``LocalCluster`` runs the fake control plane, the workers and the master in one event loop, which
+is ideal for white-box tests but is not how gpumounter-amd runs. ``ProcessCluster`` starts
+
+* the fake control plane (``python -m gpumounter_amd.fakes.controlplane``),
+* one worker per node with the production entry point (``python -m gpumounter_amd worker``),
+  configured only through ``GM_*`` environment variables like the DaemonSet,
+* the master (``python -m gpumounter_amd master``) the same way,
+
+waits until each reports ready, and talks to the master over HTTP. ``stop()`` sends SIGTERM and
+expects every daemon to exit cleanly. Used by tests/test_processes.py and ``bench.py --deploy
+processes`` (no shared interpreter, event loop or GIL between master, worker and apiserver).
+"""
+from __future__ import annotations
+
+import http.client
+import json
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+import urllib.error
+import urllib.parse
+import urllib.request
+from typing import Dict, List, Optional, Tuple
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _http(method: str, url: str, body: Optional[bytes] = None, headers: Optional[dict] = None,
+          timeout: float = 60.0) -> Tuple[int, bytes]:
+    req = urllib.request.Request(url, data=body, method=method, headers=headers or {})
+    try:
+        with urllib.request.urlopen(req, timeout=timeout) as r:
+            return r.status, r.read()
+    except urllib.error.HTTPError as e:
+        return e.code, e.read()
+
+
+class ProcessCluster:
+    def __init__(self, n_nodes: int = 1, amdsmi_lib: str = "mock", cgroup_mode: str = "v2",
+                 latency: str = "zero", gpu_bdfs: Optional[List[str]] = None,
+                 worker_env: Optional[Dict[str, str]] = None,
+                 master_env: Optional[Dict[str, str]] = None, log_dir: str = "") -> None:
+        self.n_nodes = n_nodes
+        self.amdsmi_lib = amdsmi_lib
+        self.cgroup_mode = cgroup_mode
+        self.latency = latency
+        self.gpu_bdfs = gpu_bdfs or []
+        self.worker_env = worker_env or {}
+        self.master_env = master_env or {}
+        self.workdir = tempfile.mkdtemp(prefix="gm-deploy-")
+        self.log_dir = log_dir or self.workdir
+        self.procs: Dict[str, subprocess.Popen] = {}
+        self.info: dict = {}
+        self.worker_ports: Dict[str, Tuple[int, int]] = {}   # node → (grpc, metrics)
+        self.master_url = ""
+        self._conn: Optional[http.client.HTTPConnection] = None   # keep-alive to the master
+
+    def _master(self, method: str, path: str, body: Optional[bytes] = None,
+                headers: Optional[dict] = None) -> Tuple[int, bytes]:
+        """One request on a persistent connection (as a real client library would hold)."""
+        for attempt in (0, 1):
+            if self._conn is None:
+                host, port = self.master_url[len("http://"):].split(":")
+                self._conn = http.client.HTTPConnection(host, int(port), timeout=120)
+            try:
+                self._conn.request(method, path, body=body, headers=headers or {})
+                r = self._conn.getresponse()
+                return r.status, r.read()
+            except (http.client.HTTPException, OSError):
+                self._conn.close()
+                self._conn = None
+                if attempt:
+                    raise
+        raise AssertionError("unreachable")
+
+    # ------------------------------------------------------------------------ lifecycle
+    def _spawn(self, key: str, argv: List[str], env: Dict[str, str]) -> subprocess.Popen:
+        log = open(os.path.join(self.log_dir, f"{key}.log"), "w")
+        full = {**os.environ, "PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
+                **env}
+        p = subprocess.Popen([sys.executable, *argv], cwd=ROOT, env=full, stdout=log,
+                             stderr=subprocess.STDOUT, start_new_session=True)
+        self.procs[key] = p
+        return p
+
+    def _wait(self, what: str, ok, timeout: float = 120.0) -> None:
+        end = time.time() + timeout
+        while time.time() < end:
+            for key, p in self.procs.items():
+                if p.poll() is not None:
+                    raise RuntimeError(f"{key} exited with {p.returncode} while waiting for "
+                                       f"{what}:\n{self.log(key)[-3000:]}")
+            try:
+                if ok():
+                    return
+            except (OSError, ValueError):
+                pass
+            time.sleep(0.05)
+        raise TimeoutError(f"timed out waiting for {what}")
+
+    def log(self, key: str) -> str:
+        try:
+            with open(os.path.join(self.log_dir, f"{key}.log")) as fh:
+                return fh.read()
+        except OSError:
+            return ""
+
+    def start(self) -> "ProcessCluster":
+        info_path = os.path.join(self.workdir, "info.json")
+        self._spawn("controlplane", ["-m", "gpumounter_amd.fakes.controlplane", "--workdir",
+                                     os.path.join(self.workdir, "cluster"), "--info", info_path,
+                                     "--nodes", str(self.n_nodes), "--amdsmi", self.amdsmi_lib,
+                                     "--cgroup", self.cgroup_mode, "--latency", self.latency,
+                                     "--gpu-bdfs", ",".join(self.gpu_bdfs)], {})
+        self._wait("control plane", lambda: os.path.exists(info_path))
+        with open(info_path) as fh:
+            self.info = json.load(fh)
+        api = self.info["api_url"]
+        for node, n in self.info["nodes"].items():
+            gport, mport = free_port(), free_port()
+            self.worker_ports[node] = (gport, mport)
+            env = {"GM_KUBE_API": api, "GM_NODE_NAME": node,
+                   "GM_KUBELET_SOCKET": n["kubelet_socket"], "GM_CGROUP_ROOT": n["cgroup_root"],
+                   "GM_CGROUP_MODE": self.cgroup_mode, "GM_DEVNODE_MODE": "emulate",
+                   "GM_CONTAINER_ROOT_PREFIX": n["rootfs_root"], "GM_AMDSMI_LIB": self.amdsmi_lib,
+                   "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": str(gport),
+                   "GM_METRICS_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
+                   "GM_LOG_JSON": "false", **self.worker_env}
+            self._spawn(f"worker-{node}", ["-m", "gpumounter_amd", "worker"], env)
+        for node, (gport, mport) in self.worker_ports.items():
+            self._wait(f"worker {node}",
+                       lambda m=mport: _http("GET", f"http://127.0.0.1:{m}/readyz")[0] == 200)
+            code, _ = _http("POST", f"{api}/_fake/worker",
+                            json.dumps({"node": node, "port": gport}).encode(),
+                            {"Content-Type": "application/json"})
+            if code != 201:
+                raise RuntimeError(f"worker registration for {node} failed: {code}")
+        mport = free_port()
+        self._spawn("master", ["-m", "gpumounter_amd", "master"],
+                    {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1",
+                     "GM_MASTER_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
+                     "GM_LOG_JSON": "false", **self.master_env})
+        self.master_url = f"http://127.0.0.1:{mport}"
+        for node in self.info["nodes"]:   # the master has discovered every worker
+            self._wait(f"master → {node}", lambda n=node: _http(
+                "GET", f"{self.master_url}/api/v1/nodes/{n}/gpus")[0] == 200)
+        return self
+
+    def stop(self, timeout: float = 20.0) -> Dict[str, Optional[int]]:
+        """SIGTERM every daemon (master and workers first) → their exit codes."""
+        if self._conn is not None:
+            self._conn.close()
+            self._conn = None
+        codes: Dict[str, Optional[int]] = {}
+        order = [k for k in self.procs if k == "master"] + \
+            [k for k in self.procs if k.startswith("worker-")] + \
+            [k for k in self.procs if k == "controlplane"]
+        for key in order:
+            p = self.procs[key]
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+                try:
+                    p.wait(timeout)
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait(5)
+            codes[key] = p.returncode
+        shutil.rmtree(self.workdir, ignore_errors=True)
+        return codes
+
+    def __enter__(self) -> "ProcessCluster":
+        try:
+            return self.start()
+        except BaseException:
+            self.stop()
+            raise
+
+    def __exit__(self, *exc) -> None:
+        self.stop()
+
+    # ------------------------------------------------------------------------ operations
+    def tenant(self, name: str, ns: str = "default", node: str = "node-0", gpus: int = 0,
+               pids: Optional[Dict[str, List[int]]] = None) -> dict:
+        code, body = _http("POST", f"{self.info['api_url']}/_fake/tenant",
+                           json.dumps({"name": name, "ns": ns, "node": node,
+                                       "gpus": gpus, "pids": pids}).encode(),
+                           {"Content-Type": "application/json"})
+        if code != 201:
+            raise RuntimeError(f"tenant create failed: {code} {body[:300]!r}")
+        return json.loads(body)
+
+    def add(self, ns: str, pod: str, n: int, entire: bool = False) -> Tuple[int, dict]:
+        code, body = self._master("GET", f"/addgpu/namespace/{ns}/pod/{pod}/gpu/{n}/"
+                                         f"isEntireMount/{'true' if entire else 'false'}",
+                                  headers={"Accept": "application/json"})
+        return code, json.loads(body)
+
+    def remove(self, ns: str, pod: str, uuids: List[str], force: bool = False
+               ) -> Tuple[int, dict]:
+        data = urllib.parse.urlencode([("uuids", u) for u in uuids]).encode()
+        code, body = self._master("POST", f"/removegpu/namespace/{ns}/pod/{pod}/force/"
+                                          f"{'true' if force else 'false'}", data,
+                                  {"Accept": "application/json",
+                                   "Content-Type": "application/x-www-form-urlencoded"})
+        return code, json.loads(body)
+
+    def pod_gpus(self, ns: str, pod: str) -> Tuple[int, dict]:
+        code, body = _http("GET", f"{self.master_url}/api/v1/namespaces/{ns}/pods/{pod}/gpus",
+                           headers={"Accept": "application/json"})
+        return code, json.loads(body)
+
+    def placeholders(self) -> List[dict]:
+        code, body = _http("GET", f"{self.info['api_url']}/api/v1/pods?labelSelector=app%3Dgpu-pool")
+        return json.loads(body).get("items", []) if code == 200 else []
+
+    def audit(self, ns: str, pod: str, node: str = "node-0") -> list:
+        code, body = _http("GET", f"http://127.0.0.1:{self.worker_ports[node][1]}/audit/{ns}/{pod}")
+        if code != 200:
+            raise RuntimeError(f"audit {ns}/{pod}: {code} {body[:300]!r}")
+        return json.loads(body)["issues"]
+
+    def worker_metrics(self, node: str = "node-0") -> str:
+        return _http("GET", f"http://127.0.0.1:{self.worker_ports[node][1]}/metrics")[1].decode()
+
+    def rootfs(self, node: str = "node-0") -> str:
+        return self.info["nodes"][node]["rootfs_root"]

@@ -17,7 +17,7 @@ import shutil
 import tempfile
 import threading
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import aiohttp
 from aiohttp import web
@@ -51,7 +51,8 @@ class LocalCluster:
                  node_gpu_bdfs: Optional[List[str]] = None,
                  master_overrides: Optional[dict] = None,
                  device_plugin: bool = False, cgroup_root: str = "",
-                 kfd_major: int = 0) -> None:
+                 kfd_major: int = 0, start_workers: bool = True,
+                 app_hook: Optional[Callable[[web.Application], None]] = None) -> None:
         self.n_nodes = n_nodes
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
@@ -66,6 +67,8 @@ class LocalCluster:
         self.devnode_mode = devnode_mode
         self.reconcile_period_s = reconcile_period_s
         self.start_master = start_master
+        self.start_workers = start_workers
+        self.app_hook = app_hook
         self.worker_overrides = worker_overrides or {}
         self.master_overrides = master_overrides or {}
         self.device_plugin = device_plugin
@@ -83,7 +86,10 @@ class LocalCluster:
     # ------------------------------------------------------------------------ lifecycle
     async def start(self) -> "LocalCluster":
         self.inventory = Inventory(self.amdsmi_lib, self.kfd_major)
-        self.api_runner = web.AppRunner(self.cluster.app(), access_log=None)
+        app = self.cluster.app()
+        if self.app_hook is not None:
+            self.app_hook(app)
+        self.api_runner = web.AppRunner(app, access_log=None)
         await self.api_runner.setup()
         site = web.TCPSite(self.api_runner, "127.0.0.1", 0)
         await site.start()
@@ -123,7 +129,8 @@ class LocalCluster:
         await kubelet.start()
         h = NodeHandle(name, node, kubelet)
         self.nodes[name] = h
-        await self.start_worker(name)
+        if self.start_workers:
+            await self.start_worker(name)
         return h
 
     async def start_worker(self, name: str) -> Worker:
@@ -147,19 +154,22 @@ class LocalCluster:
         w = Worker(cfg, inventory=self.inventory)
         await w.start(grpc_port=0, http_port=0, reconcile=self.reconcile_period_s > 0)
         h.worker, h.cfg = w, cfg
-        # register the worker DaemonSet pod so the master can discover it
+        self.register_worker(name, w.grpc_port)
+        return w
+
+    def register_worker(self, name: str, port: int, ip: str = "127.0.0.1") -> None:
+        """Create the worker DaemonSet pod of node ``name`` so the master can discover it."""
         wp = self.cluster.get("kube-system", f"gpu-mounter-worker-{name}")
         if wp is not None:
             self.cluster._remove("kube-system", wp["metadata"]["name"])  # noqa: SLF001
         self.cluster.create_running_pod("kube-system", {
             "metadata": {"name": f"gpu-mounter-worker-{name}",
                          "labels": {"app": "gpu-mounter-worker"},
-                         "annotations": {ANN_WORKER_PORT: str(w.grpc_port)}},
+                         "annotations": {ANN_WORKER_PORT: str(port)}},
             "spec": {"containers": [{"name": "worker", "image": "gpumounter-amd:dev"}]}}, name)
         wpod = self.cluster.get("kube-system", f"gpu-mounter-worker-{name}")
-        wpod["status"]["podIP"] = "127.0.0.1"
+        wpod["status"]["podIP"] = ip
         self.cluster._bump("MODIFIED", wpod)  # noqa: SLF001
-        return w
 
     async def stop_worker(self, name: str) -> None:
         h = self.nodes[name]

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import signal
 import time
 from typing import Dict, Optional, Tuple
 
@@ -471,9 +472,15 @@ class Master:
 
 
 async def serve(cfg) -> None:
+    """Run until SIGTERM/SIGINT, then shut down cleanly (the kubelet sends SIGTERM on pod
+    deletion; the reference's daemons just died — reference: cmd/*/main.go)."""
     m = Master(cfg)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
     await m.start()
     try:
-        await asyncio.Event().wait()
+        await stop.wait()
     finally:
         await m.stop()

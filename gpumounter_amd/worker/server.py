@@ -12,6 +12,7 @@ from __future__ import annotations
 import asyncio
 import json
 import os
+import signal
 from typing import Optional
 
 import grpc
@@ -164,6 +165,7 @@ class Worker:
             app.router.add_get("/readyz", self._readyz)
             app.router.add_get("/metrics", self._metrics)
             app.router.add_get("/status", self._http_status)
+            app.router.add_get("/audit/{namespace}/{pod}", self._http_audit)
             self.http_runner = web.AppRunner(app, access_log=None)
             await self.http_runner.setup()
             site = web.TCPSite(self.http_runner, self.cfg.worker_host, hp)
@@ -196,6 +198,18 @@ class Worker:
     async def _http_status(self, request):
         st = await self.service.node_status(request.query.get("processes") == "1")
         return web.json_response(st)
+
+    async def _http_audit(self, request):
+        """Ledger-vs-node consistency of one pod: [] when its cgroup rules and device nodes are
+        exactly what its placeholders hold (the check the reconciler runs)."""
+        ns, name = request.match_info["namespace"], request.match_info["pod"]
+        pod = await self.service.get_pod(ns, name, fresh=True)
+        if pod is None:
+            return web.json_response({"error": "pod not found"}, status=404)
+        st = await self.service.pod_state(pod, fresh=True)
+        issues = self.service.hm.audit(pod, st.hot, st.own)
+        return web.json_response({"pod": f"{ns}/{name}", "consistent": not issues,
+                                  "issues": [vars(i) for i in issues]})
 
     async def _collect_loop(self) -> None:
         """Per-GPU process gauges + ledger state gauges."""
@@ -241,9 +255,15 @@ class Worker:
 
 
 async def serve(cfg) -> None:
+    """Run until SIGTERM/SIGINT, then shut down cleanly (the kubelet sends SIGTERM on pod
+    deletion; the reference's daemons just died — reference: cmd/*/main.go)."""
     w = Worker(cfg)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
     await w.start()
     try:
-        await asyncio.Event().wait()
+        await stop.wait()
     finally:
         await w.stop()

@@ -1,0 +1,39 @@
+"""Deployment-shaped run: fake control plane, workers and master as separate processes, started
+through the production entry points (``python -m gpumounter_amd worker|master``) and configured
+only by ``GM_*`` environment variables (gpumounter_amd/fakes/deployment.py)."""
+import os
+
+from gpumounter_amd.fakes.deployment import ProcessCluster
+
+
+def test_daemons_as_processes_attach_detach_and_exit_cleanly_on_sigterm():
+    pc = ProcessCluster(n_nodes=2)
+    codes = None
+    try:
+        pc.start()
+        pc.tenant("t0", node="node-0")
+        pc.tenant("t1", node="node-1")
+        code, b0 = pc.add("default", "t0", 2)
+        assert code == 200, b0
+        code, b1 = pc.add("default", "t1", 1, entire=True)
+        assert code == 200, b1
+        assert b0["devices"][0]["bdf"] != "" and len(b0["devices"]) == 2
+        code, g = pc.pod_gpus("default", "t0")
+        assert code == 200 and [x["source"] for x in g["gpus"]] == ["hot-mount"] * 2, g
+        # the emulated device nodes exist in t0's container rootfs (worker-0's node tree)
+        root = pc.rootfs("node-0")
+        nodes = [f for d, _, fs in os.walk(root) for f in fs if f.startswith("renderD")]
+        assert len(nodes) == 2, nodes
+        assert 'gm_attach_latency_seconds_count{mode="single",n_gpus="2"} 1.0' in \
+            pc.worker_metrics("node-0")
+        assert pc.audit("default", "t0") == [] and pc.audit("default", "t1", "node-1") == []
+        code, _ = pc.remove("default", "t0", [d["uuid"] for d in b0["devices"]])
+        assert code == 200
+        code, _ = pc.remove("default", "t1", [d["uuid"] for d in b1["devices"]])
+        assert code == 200
+        nodes = [f for d, _, fs in os.walk(root) for f in fs if f.startswith("renderD")]
+        assert nodes == [] and pc.audit("default", "t0") == []
+    finally:
+        codes = pc.stop()
+    assert codes == {"master": 0, "worker-node-0": 0, "worker-node-1": 0, "controlplane": 0}, \
+        codes
