@@ -11,7 +11,11 @@ One "step" = the full hot-mount cycle a user drives through the master's HTTP AP
 The control plane (apiserver, scheduler, kubelet PodResources) is the hermetic fake; inventory,
 topology and process tables come from the real libamd_smi through the C++ shim, the node
 operations run the production C++ code against a temp-dir cgroupfs/rootfs (the GPU box is
-unprivileged), and the probe kernels run on the real GPUs.
+unprivileged), and the probe kernels run on the real GPUs. By default (``--deploy processes``)
+the fake control plane, the worker and the master are separate processes started through the
+production entry points, as deployed; ``--deploy inprocess`` runs them on one event loop.
+After the timed loop the reference's call sequence is re-enacted in the same deployment shape
+(``reference_emulated_same_run``, gpumounter_amd/fakes/refproto.py).
 
 Launch: ``python bench.py --gpus 1`` or, for N>1, under torch.distributed.run with one rank per GPU.
 Rank 0 hosts the control plane; all ranks take part in verification. Prints ONE JSON line on rank 0.
@@ -125,7 +129,7 @@ def main() -> int:
                     help="after the timed loop, re-run this many attach/detach cycles with the "
                          "emulated reference protocol on the same cluster (0 = skip; only with "
                          "--latency zero and no warm pool)")
-    ap.add_argument("--deploy", choices=("inprocess", "processes"), default="inprocess",
+    ap.add_argument("--deploy", choices=("inprocess", "processes"), default="processes",
                     help="processes: fake control plane, worker and master each in their own "
                          "process via the production entry points (gpumounter_amd/fakes/"
                          "deployment.py); inprocess: all on one event loop (LocalCluster)")
@@ -176,13 +180,13 @@ def main() -> int:
             return 3
         sleeper = subprocess.Popen(["sleep", "infinity"])
         if args.deploy == "processes":
-            if args.protocol == "reference" or args.device_plugin:
-                print("--deploy processes runs the gpumounter protocol without the device "
-                      "plugin", file=sys.stderr)
+            if args.device_plugin:
+                print("--device-plugin needs --deploy inprocess (the fake kubelet drives the "
+                      "plugin in-process)", file=sys.stderr)
                 return 2
             from gpumounter_amd.fakes.deployment import ProcessCluster
             pc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=args.latency,
-                                gpu_bdfs=node_bdfs,
+                                gpu_bdfs=node_bdfs, protocol=args.protocol,
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
                                             "GM_PLACEMENT_ENFORCE": args.placement}).start()
             pc.tenant("tenant", pids={"main": [sleeper.pid]})
@@ -298,19 +302,27 @@ def main() -> int:
             p50 = pct(attach_ms, 0.5)
             ref = None
             if args.ref_steps > 0 and args.protocol == "gpumounter" and \
-                    args.latency == "zero" and not args.warm_pool and lc is not None:
-                from gpumounter_amd.fakes import refproto
-                refproto.install(lc)
+                    args.latency == "zero" and not args.warm_pool:
+                # the reference's call sequence, emulated in the same deployment shape
+                if lc is not None:
+                    from gpumounter_amd.fakes import refproto
+                    refproto.install(lc)
+                    ref_cp = cp
+                else:
+                    cp.stop()
+                    from gpumounter_amd.fakes.deployment import ProcessCluster
+                    rpc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup,
+                                         gpu_bdfs=node_bdfs, protocol="reference").start()
+                    rpc.tenant("tenant", pids={"main": [sleeper.pid]})
+                    cp = ref_cp = _ProcCP(rpc)
                 ra, rd = [], []
                 for i in range(args.ref_steps + 2):
                     ta = time.perf_counter()
-                    code, body = tc.call(lc.add("default", "tenant", n,
-                                                entire=args.mode == "entire"))
+                    code, body = ref_cp.add(n, args.mode == "entire")
                     tb = time.perf_counter()
                     if code != 200:
                         raise RuntimeError(f"reference attach failed: {code} {body}")
-                    code, body = tc.call(lc.remove("default", "tenant",
-                                                   [d["uuid"] for d in body["devices"]]))
+                    code, body = ref_cp.remove([d["uuid"] for d in body["devices"]])
                     if code != 200:
                         raise RuntimeError(f"reference detach failed: {code} {body}")
                     if i >= 2:

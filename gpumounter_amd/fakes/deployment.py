@@ -54,8 +54,13 @@ class ProcessCluster:
     def __init__(self, n_nodes: int = 1, amdsmi_lib: str = "mock", cgroup_mode: str = "v2",
                  latency: str = "zero", gpu_bdfs: Optional[List[str]] = None,
                  worker_env: Optional[Dict[str, str]] = None,
-                 master_env: Optional[Dict[str, str]] = None, log_dir: str = "") -> None:
+                 master_env: Optional[Dict[str, str]] = None, log_dir: str = "",
+                 protocol: str = "gpumounter") -> None:
+        """``protocol="reference"`` runs worker and master with the reference's call sequence
+        (gpumounter_amd/fakes/refproto.py) in the same deployment shape, for comparison."""
         self.n_nodes = n_nodes
+        self.entry = ["-m", "gpumounter_amd"] if protocol == "gpumounter" else \
+            ["-m", "gpumounter_amd.fakes.refproto"]
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
         self.latency = latency
@@ -141,7 +146,7 @@ class ProcessCluster:
                    "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": str(gport),
                    "GM_METRICS_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
                    "GM_LOG_JSON": "false", **self.worker_env}
-            self._spawn(f"worker-{node}", ["-m", "gpumounter_amd", "worker"], env)
+            self._spawn(f"worker-{node}", [*self.entry, "worker"], env)
         for node, (gport, mport) in self.worker_ports.items():
             self._wait(f"worker {node}",
                        lambda m=mport: _http("GET", f"http://127.0.0.1:{m}/readyz")[0] == 200)
@@ -151,7 +156,7 @@ class ProcessCluster:
             if code != 201:
                 raise RuntimeError(f"worker registration for {node} failed: {code}")
         mport = free_port()
-        self._spawn("master", ["-m", "gpumounter_amd", "master"],
+        self._spawn("master", [*self.entry, "master"],
                     {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1",
                      "GM_MASTER_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
                      "GM_LOG_JSON": "false", **self.master_env})

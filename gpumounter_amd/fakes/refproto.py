@@ -277,3 +277,49 @@ def install(lc) -> None:
         h.worker.service.remove_gpu = ref.remove_gpu
     lc.master.workers.channel = lambda target: RefMaster._OneShot(target)
     lc.master._locate = RefMaster._locate.__get__(lc.master)
+
+
+# ------------------------------------------------------------------------------ as daemons
+async def _serve(role: str, cfg) -> None:
+    """The reference protocol in a worker or master *process* (ProcessCluster, protocol=
+    "reference"): the production daemon with the same substitutions :func:`install` makes."""
+    import signal
+
+    from gpumounter_amd.worker.server import Worker
+
+    if role == "worker":
+        d = Worker(cfg)
+        ref = RefProtocolService(d.service)
+        d.service.add_gpu = ref.add_gpu
+        d.service.remove_gpu = ref.remove_gpu
+    else:
+        d = Master(cfg)
+        d.workers.channel = lambda target: RefMaster._OneShot(target)
+        d._locate = RefMaster._locate.__get__(d)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
+    await d.start()
+    try:
+        await stop.wait()
+    finally:
+        await d.stop()
+
+
+def main(argv=None) -> int:
+    """``python -m gpumounter_amd.fakes.refproto worker|master`` (GM_* env as the daemons)."""
+    import sys
+
+    from gpumounter_amd.utils import log
+    from gpumounter_amd.utils.config import Config
+
+    role = (argv or sys.argv[1:])[0]
+    cfg = Config.load()
+    log.setup(cfg.log_level, cfg.log_json, cfg.log_file)
+    asyncio.run(_serve(role, cfg))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -176,6 +176,30 @@ def test_e2e_attach_verify_detach_real_inventory(real_inventory):
     asyncio.run(run())
 
 
+def test_daemons_as_processes_with_real_inventory(real_inventory):
+    """The production entry points as separate processes (worker on the real libamd_smi),
+    configured by GM_* env only; the attached GPU runs the gfx950 liveness kernel here."""
+    from gpumounter_amd.fakes.deployment import ProcessCluster
+    from gpumounter_amd.ops import probe
+
+    bdf0 = probe.props(0)["pci_bus_id"]
+    pc = ProcessCluster(amdsmi_lib="", gpu_bdfs=[bdf0])
+    try:
+        pc.start()
+        pc.tenant("t")
+        code, body = pc.add("default", "t", 1)
+        assert code == 200, body
+        assert body["devices"][0]["bdf"] == bdf0
+        assert pc.audit("default", "t") == []
+        assert probe.verify([bdf0])[0].quick_us > 0
+        code, body2 = pc.remove("default", "t", [body["devices"][0]["uuid"]])
+        assert code == 200, body2
+        assert pc.audit("default", "t") == []
+    finally:
+        codes = pc.stop()
+    assert set(codes.values()) == {0}, codes
+
+
 def test_busy_detection_with_real_hip_process(real_inventory):
     """A real HIP process inside the tenant cgroup makes the GPU busy (amdsmi process list or the
     /proc fd fallback); force=true removes it and terminates the process."""
