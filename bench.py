@@ -276,16 +276,27 @@ def main() -> int:
                 for k, v in st["timings"].items():
                     stage.setdefault(k, []).append(v)
 
+    last_note = [time.time()]
+
+    def progress(phase: str, i: int, total: int) -> None:
+        """A line on stderr at most every 10 s, so long runs (realistic control plane: the
+        reference's detach waits out a 30 s grace period) visibly make progress."""
+        if rank == 0 and time.time() - last_note[0] > 10:
+            last_note[0] = time.time()
+            print(f"bench: {phase} step {i}/{total}", file=sys.stderr, flush=True)
+
     try:
-        for _ in range(args.warmup):
+        for i in range(args.warmup):
             one_step(False)
+            progress("warmup", i + 1, args.warmup)
         if world > 1:
             dist.barrier()
         if has_gpu:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for i in range(args.steps):
             one_step(True)
+            progress("timed", i + 1, args.steps)
         if world > 1:
             dist.barrier()
         if has_gpu:
@@ -328,6 +339,7 @@ def main() -> int:
                     if i >= 2:
                         ra.append((tb - ta) * 1e3)
                         rd.append((time.perf_counter() - tb) * 1e3)
+                    progress("reference", i + 1, args.ref_steps + 2)
                 ref = {"steps": args.ref_steps, "attach_p50_ms": round(pct(ra, 0.5), 4),
                        "detach_p50_ms": round(pct(rd, 0.5), 4),
                        "attach_speedup": round(pct(ra, 0.5) / p50, 2)}
