@@ -207,6 +207,15 @@ def cmd_bpf_dump(args) -> int:
     return 0
 
 
+def cmd_doctor(args) -> int:
+    from gpumounter_amd.utils import doctor
+
+    cfg = _cfg(args)
+    checks = doctor.run(cfg, skip_cluster=args.skip_cluster)
+    print(doctor.render(checks, args.json))
+    return 1 if any(c.status == "fail" for c in checks) else 0
+
+
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="gpumounter_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -253,6 +262,13 @@ def build_parser() -> argparse.ArgumentParser:
         if name == "status":
             p.add_argument("--node", default="")
         p.set_defaults(fn=fn)
+    p = sub.add_parser("doctor", help="node preflight: amdsmi, cgroup/bpf, systemd, kubelet, "
+                                      "apiserver")
+    p.add_argument("--config")
+    p.add_argument("--json", action="store_true")
+    p.add_argument("--skip-cluster", action="store_true",
+                   help="skip the kubelet and apiserver checks")
+    p.set_defaults(fn=cmd_doctor)
     p = sub.add_parser("bpf-dump")
     p.add_argument("--allow", action="append", default=[])
     p.add_argument("--unchained", action="store_true")

@@ -1,0 +1,184 @@
+"""Node preflight: ``python -m gpumounter_amd doctor`` checks everything the worker needs on a node.
+
+The reference has no such tool; its failure modes surface as a failed attach (wrong cgroup driver
+env, missing ``mknod`` in the image, no kubelet socket — reference docs/guide/FAQ.md:3-7). Each
+check here reports ``ok``, ``warn`` (works, but a feature is degraded) or ``fail`` (attaches
+cannot work), with the detail an operator needs. Run it in the worker container (same mounts and
+privileges as the DaemonSet) or on the host with the same ``GM_*`` settings.
+"""
+from __future__ import annotations
+
+import asyncio
+import ctypes as C
+import errno
+import json
+import os
+from dataclasses import asdict, dataclass
+from typing import List
+
+from gpumounter_amd import _native
+
+BPF_FS_MAGIC = 0xCAFE4A11
+
+
+@dataclass
+class Check:
+    name: str
+    status: str          # ok | warn | fail
+    detail: str
+
+
+def _statfs_type(path: str) -> int:
+    class StatFs(C.Structure):
+        _fields_ = [("f_type", C.c_long), ("rest", C.c_byte * 120)]
+
+    libc = C.CDLL(None, use_errno=True)
+    buf = StatFs()
+    if libc.statfs(path.encode(), C.byref(buf)) != 0:
+        raise OSError(C.get_errno(), os.strerror(C.get_errno()), path)
+    return buf.f_type & 0xFFFFFFFF
+
+
+def check_inventory(cfg) -> List[Check]:
+    from gpumounter_amd.hw.inventory import Inventory
+
+    try:
+        inv = Inventory(cfg.amdsmi_lib, cfg.kfd_major, cfg.kfd_dev_path)
+        gpus = inv.gpus()
+    except Exception as e:  # noqa: BLE001
+        return [Check("amdsmi", "fail", f"inventory unavailable: {e}")]
+    out = [Check("amdsmi", "ok" if gpus else "fail",
+                 f"{len(gpus)} GPU(s) via {inv.lib_path}: "
+                 + ", ".join(sorted({g.gfx_target for g in gpus})))]
+    hives = {g.xgmi_hive_id for g in gpus}
+    out.append(Check("xgmi", "ok" if len(gpus) < 2 or len(hives) == 1 else "warn",
+                     f"{len(hives)} hive(s) for {len(gpus)} GPU(s)"))
+    kfd_src = "configured" if cfg.kfd_major else (
+        cfg.kfd_dev_path if os.path.exists(cfg.kfd_dev_path) else "fallback 511")
+    out.append(Check("kfd", "ok" if kfd_src != "fallback 511" else "warn",
+                     f"/dev/kfd major {inv.kfd_major} ({kfd_src})"))
+    return out
+
+
+def check_cgroup(cfg) -> List[Check]:
+    from gpumounter_amd.node.cgroup import CgroupResolver
+
+    root = cfg.cgroup_root
+    if not os.path.isdir(root):
+        return [Check("cgroup", "fail", f"{root} is not mounted")]
+    mode = CgroupResolver.detect_mode(root) if cfg.cgroup_mode == "auto" else cfg.cgroup_mode
+    out = []
+    if mode == "v1":
+        allow = os.path.join(root, "devices", "devices.allow")
+        ok = os.access(allow, os.W_OK)
+        out.append(Check("cgroup", "ok" if ok else "fail",
+                         f"v1 devices controller, {allow} {'writable' if ok else 'NOT writable'}"))
+        return out
+    out.append(Check("cgroup", "ok", f"v2 unified hierarchy at {root}"))
+    # can this process load a device program? (CAP_BPF + CAP_SYS_ADMIN in the DaemonSet)
+    from gpumounter_amd.node.cgroup import _rule_array, rules_for
+    from gpumounter_amd.models.device import DeviceNode
+
+    lib = _native.host()
+    rules = rules_for([DeviceNode("/dev/null", 1, 3)], allow=True)
+    need = -lib.gm_bpf_dev_build(_rule_array(rules), 1, 0, -1, None, 0)
+    buf = (C.c_uint64 * need)()
+    n = lib.gm_bpf_dev_build(_rule_array(rules), 1, 0, -1, buf, need)
+    fd = lib.gm_bpf_dev_load(buf, n, b"gm_doctor", None, 0)
+    if fd >= 0:
+        os.close(fd)
+        out.append(Check("bpf", "ok", "BPF_PROG_TYPE_CGROUP_DEVICE programs load"))
+    else:
+        out.append(Check("bpf", "fail", f"cannot load a device program: {os.strerror(-fd)} "
+                                        "(needs CAP_BPF/CAP_SYS_ADMIN: privileged DaemonSet)"))
+    pin = cfg.bpf_pin_dir
+    if pin:
+        parent = pin if os.path.isdir(pin) else os.path.dirname(pin)
+        try:
+            is_bpffs = _statfs_type(parent) == BPF_FS_MAGIC
+        except OSError as e:
+            is_bpffs = False
+            parent = f"{parent} ({e.strerror})"
+        out.append(Check("bpffs", "ok" if is_bpffs else "warn",
+                         f"{parent} is {'a' if is_bpffs else 'not a'} bpffs: tail-call maps "
+                         + ("survive worker restarts" if is_bpffs else
+                            "are kept in-process only (lost on restart until reconciled)")))
+    return out
+
+
+def check_systemd(cfg) -> List[Check]:
+    from gpumounter_amd.node import systemd
+
+    if cfg.systemd_device_allow == "off":
+        return [Check("systemd", "ok", "DeviceAllow persistence disabled")]
+    bus = systemd.find_bus(cfg.systemd_bus)
+    if bus is None:
+        status = "fail" if cfg.systemd_device_allow == "on" else (
+            "warn" if cfg.cgroup_driver == "systemd" else "ok")
+        detail = ("no systemd bus socket mounted (/run/systemd or /run/dbus): on "
+                  "systemd-driver nodes a daemon-reload can drop hot-mounted devices until the "
+                  "reconciler restores them") if status != "ok" else \
+            "no systemd bus socket (needed only with the systemd cgroup driver)"
+        return [Check("systemd", status, detail)]
+    err = C.create_string_buffer(256)
+    out = C.create_string_buffer(1 << 12)
+    rc = _native.host().gm_sd_get_device_allow(bus.encode(), b"-.slice", out, 1 << 12, err, 256)
+    if rc >= 0 or rc == -errno.EPROTO:   # a D-Bus answer (even an error) means we are talking
+        return [Check("systemd", "ok", f"systemd reachable on {bus}")]
+    return [Check("systemd", "warn", f"{bus}: {err.value.decode() or os.strerror(-rc)}")]
+
+
+async def _check_kubelet(cfg) -> List[Check]:
+    from gpumounter_amd.node.ledger import LedgerClient
+
+    if not os.path.exists(cfg.kubelet_socket):
+        return [Check("kubelet", "fail", f"PodResources socket {cfg.kubelet_socket} missing")]
+    lc = LedgerClient(cfg.kubelet_socket, cfg.resource_name, cfg.kubelet_timeout_s,
+                      cfg.podresources_api)
+    try:
+        allocs = await lc.list()
+        alloc = await lc.allocatable()
+        return [Check("kubelet", "ok",
+                      f"PodResources {lc.api_version}: {len(allocs)} {cfg.resource_name} "
+                      f"allocation(s)" + (f", {len(alloc)} allocatable" if alloc else ""))]
+    except Exception as e:  # noqa: BLE001
+        return [Check("kubelet", "fail", f"PodResources List failed: {e}")]
+    finally:
+        await lc.close()
+
+
+async def _check_apiserver(cfg) -> List[Check]:
+    from gpumounter_amd.cluster.kube import KubeClient
+
+    try:
+        kube = KubeClient.from_config(cfg)
+    except Exception as e:  # noqa: BLE001
+        return [Check("apiserver", "fail", f"no credentials: {e}")]
+    try:
+        pods, _ = await kube.list_pods(cfg.pool_namespace)
+        return [Check("apiserver", "ok", f"{kube.base}: {len(pods)} pod(s) in "
+                                         f"{cfg.pool_namespace}")]
+    except Exception as e:  # noqa: BLE001
+        return [Check("apiserver", "fail", f"{kube.base}: {e}")]
+    finally:
+        await kube.close()
+
+
+def run(cfg, skip_cluster: bool = False) -> List[Check]:
+    checks = check_inventory(cfg) + check_cgroup(cfg) + check_systemd(cfg)
+    if not skip_cluster:
+        async def both():
+            return await _check_kubelet(cfg) + await _check_apiserver(cfg)
+        checks += asyncio.run(both())
+    checks.append(Check("roctx", "ok" if _native.host().gm_roctx_available() else "warn",
+                        "rocprofiler roctx markers " + (
+                            "available" if _native.host().gm_roctx_available()
+                            else "unavailable (attach/detach ranges not traced)")))
+    return checks
+
+
+def render(checks: List[Check], as_json: bool = False) -> str:
+    if as_json:
+        return json.dumps([asdict(c) for c in checks], indent=1)
+    w = max(len(c.name) for c in checks)
+    return "\n".join(f"{c.status.upper():4}  {c.name:<{w}}  {c.detail}" for c in checks)

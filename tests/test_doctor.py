@@ -1,0 +1,41 @@
+"""``gpumounter_amd doctor``: node preflight against a hermetic node (gpumounter_amd/utils/doctor.py)."""
+import asyncio
+import os
+import subprocess
+import sys
+
+from gpumounter_amd.fakes.harness import LocalCluster
+from gpumounter_amd.utils import doctor
+from gpumounter_amd.utils.config import Config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_doctor_reports_a_healthy_hermetic_node():
+    async def main():
+        async with LocalCluster(cgroup_mode="v2", start_master=False) as lc:
+            h = lc.nodes["node-0"]
+            cfg = Config.load(env={}, amdsmi_lib="mock", kube_api=lc.api_url,
+                              kubelet_socket=h.kubelet.socket_path,
+                              cgroup_root=h.node.cgroup_root, cgroup_mode="v2",
+                              bpf_pin_dir="", systemd_device_allow="off")
+            # doctor.run drives its own event loop for the cluster checks
+            return await asyncio.get_running_loop().run_in_executor(None, doctor.run, cfg)
+    checks = {c.name: c for c in asyncio.run(main())}
+    for name in ("amdsmi", "xgmi", "cgroup", "kubelet", "apiserver", "systemd"):
+        assert checks[name].status == "ok", (name, checks[name])
+    assert "8 GPU(s)" in checks["amdsmi"].detail and "gfx950" in checks["amdsmi"].detail
+    assert "PodResources v1" in checks["kubelet"].detail
+    assert checks["bpf"].status in ("ok", "fail")       # root with CAP_BPF here, or not
+
+
+def test_doctor_cli_exit_code_and_json():
+    env = {**os.environ, "GM_AMDSMI_LIB": "mock", "GM_KUBELET_SOCKET": "/nonexistent.sock",
+           "GM_CGROUP_ROOT": "/nonexistent-cgroup"}
+    res = subprocess.run([sys.executable, "-m", "gpumounter_amd", "doctor", "--json"], cwd=ROOT,
+                         capture_output=True, text=True, timeout=120, env=env)
+    assert res.returncode == 1, res.stderr[-2000:]
+    import json
+    checks = {c["name"]: c for c in json.loads(res.stdout)}
+    assert checks["amdsmi"]["status"] == "ok"
+    assert checks["cgroup"]["status"] == "fail" and checks["kubelet"]["status"] == "fail"
