@@ -66,6 +66,16 @@ def _text(body: str, status: int = 200) -> web.Response:
                         content_type="text/plain", charset="utf-8")
 
 
+# AddGPU is retried when the worker answers UNAVAILABLE (restarting, draining). That is safe
+# because every AddGPU carries an idempotency key (the caller's Idempotency-Key header or the
+# request id): a retry of an attach that did happen replays it instead of adding more GPUs.
+# RemoveGPU is not retried (a repeated remove of removed GPUs reads as GPUNotFound).
+_SERVICE_CONFIG = json.dumps({"methodConfig": [{
+    "name": [{"service": f"{api.PACKAGE}.AddGPUService", "method": "AddGPU"}],
+    "retryPolicy": {"maxAttempts": 4, "initialBackoff": "0.05s", "maxBackoff": "1s",
+                    "backoffMultiplier": 2, "retryableStatusCodes": ["UNAVAILABLE"]}}]})
+
+
 class WorkerDirectory:
     """node name → worker gRPC target, from a watch on the worker DaemonSet pods."""
 
@@ -106,7 +116,8 @@ class WorkerDirectory:
             self._loop = loop
         ch = self._channels.get(target)
         if ch is None:
-            opts = [("grpc.keepalive_time_ms", 30000), ("grpc.enable_retries", 1)]
+            opts = [("grpc.keepalive_time_ms", 30000), ("grpc.enable_retries", 1),
+                    ("grpc.service_config", _SERVICE_CONFIG)]
             cfg = self.cfg
             if cfg is not None and cfg.tls_ca:
                 def rd(p):
@@ -340,7 +351,7 @@ class Master:
             return self._reply(request, route, 400, f"Invalid param gpuNum: {mi['gpuNum']}", {})
         status, text, payload = await self._add(
             ns, name, n, entire, request.query.get("container", ""), rid,
-            request.headers.get("Idempotency-Key", ""))
+            request.headers.get("Idempotency-Key", "") or rid)
         return self._reply(request, route, status, text, payload)
 
     async def remove_gpu(self, request: web.Request) -> web.Response:

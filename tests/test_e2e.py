@@ -669,3 +669,33 @@ def test_notifications_wait_for_idle_worker_and_coalesce_annotations():
             await asyncio.sleep(0.1)
             assert kube.calls == [("event", "GPUDetached")]
     asyncio.run(body())
+
+
+def test_master_retries_unavailable_worker_and_the_retry_replays_not_duplicates():
+    """AddGPU answered UNAVAILABLE (worker draining) is retried by the master's gRPC channel;
+    the implicit idempotency key makes a retry of an attach that already happened a replay."""
+    import grpc
+
+    from gpumounter_amd.worker.service import RpcError
+
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        real = svc.add_gpu
+        calls = []
+
+        async def flaky(req):
+            calls.append(req.idempotency_key)
+            if len(calls) == 1:
+                await real(req)                  # the attach happens, the answer is lost
+                raise RpcError(grpc.StatusCode.UNAVAILABLE, "worker draining")
+            return await real(req)
+        svc.add_gpu = flaky
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200, b
+        assert len(calls) == 2 and calls[0] == calls[1] != ""
+        assert b["message"].startswith("Add GPU Success")
+        st = await svc.pod_state(lc.cluster.get("default", "t"))
+        assert len(st.hot) == 2                  # not 4
+        assert await lc.audit("default", "t") == []
+    run(body)
