@@ -43,17 +43,25 @@ def allreduce_check(group=None, numel: int = 1 << 24, iters: int = 5, device=Non
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    x = torch.full((numel,), float(rank + 1), dtype=torch.bfloat16, device=dev)
+    on_gpu = torch.device(dev).type == "cuda"
+    # bf16 on the GPU (RCCL); gloo on the CPU reduces fp32
+    dtype = torch.bfloat16 if on_gpu else torch.float32
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(dev)
+    x = torch.full((numel,), float(rank + 1), dtype=dtype, device=dev)
     dist.all_reduce(x, group=group)  # warm-up / communicator init
     expect = world * (world + 1) / 2
-    torch.cuda.synchronize(dev)
+    sync()
     ok = bool(torch.all(x == expect).item()) if expect <= 256 else True
+    x.fill_(1.0)
     t0 = time.perf_counter()
     for _ in range(iters):
         dist.all_reduce(x, group=group)
-    torch.cuda.synchronize(dev)
+    sync()
     dt = (time.perf_counter() - t0) / iters
-    nbytes = numel * 2
+    nbytes = numel * x.element_size()
     algbw = nbytes / dt / 1e9
     busbw = algbw * 2 * (world - 1) / world if world > 1 else algbw
     return {"rank": rank, "world": world, "ok": ok, "ms": dt * 1e3, "algbw_gbps": algbw,

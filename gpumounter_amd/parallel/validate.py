@@ -1,0 +1,108 @@
+"""Tenant-side check after an attach: ``python -m gpumounter_amd.parallel.validate``.
+
+Run inside the pod once GPUs were hot-mounted. It answers the questions a tenant has before
+starting a job on them — the reference offers nothing here:
+
+1. every visible GPU runs a gfx950 kernel (wave64 liveness probe, :mod:`gpumounter_amd.ops.probe`);
+2. every pair has peer access and xGMI-class copy bandwidth (:func:`collectives.xgmi_matrix`);
+3. RCCL works across all of them: one process per GPU, ``torch.distributed`` with backend
+   ``nccl`` (RCCL on ROCm), a checked bf16 all-reduce with ring bus bandwidth
+   (:func:`collectives.allreduce_check`).
+
+Prints one JSON document; exit code 0 only if every check passed. ``--cpu-ranks N`` runs step 3
+with N gloo ranks on the CPU (hermetic tests).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+from typing import Dict, List
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank: int, world: int, port: int, cpu: bool, numel: int, out_dir: str) -> None:
+    import torch
+    import torch.distributed as dist
+
+    from gpumounter_amd.parallel.collectives import allreduce_check
+
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    if cpu:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(rank)
+        dev = torch.device("cuda", rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        res = allreduce_check(numel=numel, device=dev)
+    finally:
+        dist.destroy_process_group()
+    with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as fh:
+        json.dump(res, fh)
+
+
+def run_allreduce(world: int, cpu: bool, numel: int) -> List[Dict]:
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    out_dir = tempfile.mkdtemp(prefix="gm-validate-")
+    mp.spawn(_rank_main, args=(world, _free_port(), cpu, numel, out_dir), nprocs=world,
+             join=True)
+    res = []
+    for r in range(world):
+        with open(os.path.join(out_dir, f"rank{r}.json")) as fh:
+            res.append(json.load(fh))
+    return res
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="gpumounter_amd.parallel.validate")
+    ap.add_argument("--cpu-ranks", type=int, default=0,
+                    help="skip the GPU checks; all-reduce over N gloo ranks on the CPU")
+    ap.add_argument("--numel", type=int, default=1 << 24, help="all-reduce elements (bf16)")
+    ap.add_argument("--no-p2p", action="store_true")
+    args = ap.parse_args(argv)
+    report: Dict = {"ok": True}
+    if args.cpu_ranks:
+        world = args.cpu_ranks
+    else:
+        from gpumounter_amd.ops import probe
+        from gpumounter_amd.parallel.collectives import xgmi_matrix
+
+        n = probe.device_count()
+        if n == 0:
+            print(json.dumps({"ok": False, "error": "no GPU visible (nothing attached?)"}))
+            return 1
+        devs = list(range(n))
+        report["gpus"] = [{"device": d, "bdf": probe.props(d)["pci_bus_id"],
+                           "arch": probe.props(d)["gcn_arch"], "quick_us": probe.quick(d)}
+                          for d in devs]
+        if n > 1 and not args.no_p2p:
+            m = xgmi_matrix(devs)
+            report["p2p"] = m
+            report["ok"] &= all(all(row) for row in m["peer"])
+        world = n
+    ranks = run_allreduce(world, bool(args.cpu_ranks), args.numel)
+    report["allreduce"] = {"world": world, "ok": all(r["ok"] for r in ranks),
+                           "ms": max(r["ms"] for r in ranks),
+                           "busbw_gbps": min(r["busbw_gbps"] for r in ranks),
+                           "bytes": ranks[0]["bytes"]}
+    report["ok"] &= report["allreduce"]["ok"]
+    print(json.dumps(report))
+    return 0 if report["ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -235,3 +235,19 @@ def test_busy_detection_with_real_hip_process(real_inventory):
         if child.poll() is None:
             child.kill()
         child.wait()
+
+
+def test_tenant_validate_tool_runs_kernel_p2p_and_rccl():
+    """``python -m gpumounter_amd.parallel.validate``: liveness kernel on every visible GPU,
+    pairwise peer copies, and an RCCL all-reduce with one process per GPU."""
+    import json
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, "-m", "gpumounter_amd.parallel.validate",
+                          "--numel", str(1 << 22)], cwd=root, capture_output=True, text=True,
+                         timeout=240)
+    assert res.returncode == 0, (res.stdout[-2000:], res.stderr[-3000:])
+    rep = json.loads(res.stdout.strip().splitlines()[-1])
+    assert rep["ok"] and rep["gpus"] and all(g["arch"].startswith("gfx950") for g in rep["gpus"])
+    assert rep["allreduce"]["world"] == len(rep["gpus"]) and rep["allreduce"]["ok"]
+    print(json.dumps(rep["allreduce"]))
