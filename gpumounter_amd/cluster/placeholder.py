@@ -318,7 +318,12 @@ class PlaceholderManager:
                 bound = []
                 for key in pending:
                     pod = self.informer.cache.get(key)
-                    if pod is None:
+                    # _create put it in the cache, so gone = deleted by someone else (the
+                    # reference counted NotFound as success: allocator.go:251-253)
+                    if pod is None or pod["metadata"].get("deletionTimestamp"):
+                        failure[key] = "placeholder deleted before admission"
+                        if not tolerant:
+                            return True
                         continue
                     msg = podu.is_unschedulable(pod)
                     if msg:

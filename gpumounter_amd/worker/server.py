@@ -152,9 +152,13 @@ class Worker:
                 [(_read(self.cfg.tls_key), _read(self.cfg.tls_cert))],
                 root_certificates=_read(self.cfg.tls_ca) if self.cfg.tls_ca else None,
                 require_client_auth=bool(self.cfg.tls_ca))
-            self.grpc_port = self.grpc_server.add_secure_port(addr, creds)
-        else:
-            self.grpc_port = self.grpc_server.add_insecure_port(addr)
+        try:
+            if self.cfg.tls_cert and self.cfg.tls_key:
+                self.grpc_port = self.grpc_server.add_secure_port(addr, creds)
+            else:
+                self.grpc_port = self.grpc_server.add_insecure_port(addr)
+        except RuntimeError as e:        # grpcio reports a failed bind this way
+            raise OSError(f"cannot bind gRPC {addr}: {e}") from e
         if self.grpc_port == 0:
             raise OSError(f"cannot bind gRPC {self.cfg.worker_host}:{port}")
         await self.grpc_server.start()
