@@ -37,7 +37,6 @@ ANN_PREFERRED = "gpumounter.amd.com/preferred-devices"
 ANN_ATTACH_ID = "gpumounter.amd.com/attach-id"
 ANN_CONTAINER = "gpumounter.amd.com/container"
 ANN_DEVICES = "gpumounter.amd.com/devices"
-ANN_STATE = "gpumounter.amd.com/state"      # reserved | attached | detaching
 ANN_OWNER_NAME = "gpumounter.amd.com/owner-name"
 ANN_IDEMPOTENCY = "gpumounter.amd.com/idempotency-key"
 ANN_GROUP = "gpumounter.amd.com/group"      # entire-mount group made of pooled placeholders
