@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Sequence
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models.device import AmdGpu, DeviceNode, kfd_node
 from gpumounter_amd.models.pod import ContainerRef, running_containers
-from gpumounter_amd.node.cgroup import CgroupResolver, DeviceRuleBackend
+from gpumounter_amd.node.cgroup import CgroupError, CgroupResolver, DeviceRuleBackend
 from gpumounter_amd.node.devnodes import CREATED, DevNodeWriter, Target
 from gpumounter_amd.utils import log, trace
 
@@ -96,6 +96,14 @@ class HotMount:
             out.append(ContainerTarget(r, cgdir, t, pids))
         return out
 
+    def _resolve(self, pod: dict, container: str) -> List[ContainerTarget]:
+        """:meth:`targets` for a transaction: a container that vanished meanwhile (pod deleted
+        or restarted mid-attach) is a MountError, so the caller's rollback runs."""
+        try:
+            return self.targets(pod, container)
+        except (CgroupError, OSError) as e:
+            raise MountError(f"cannot resolve the pod's containers: {e}") from e
+
     # ------------------------------------------------------------------------ attach
     def attach(self, pod: dict, new: Sequence[AmdGpu], have: Sequence[AmdGpu],
                base: Sequence[AmdGpu] = (), container: str = "") -> List[ContainerTarget]:
@@ -104,7 +112,7 @@ class HotMount:
         before_keys = {(n.major, n.minor) for n in before}
         grant = [n for n in after if (n.major, n.minor) not in before_keys]
         with trace.span("resolve"):
-            targets = self.targets(pod, container)
+            targets = self._resolve(pod, container)
         done: List[tuple] = []  # (target, granted, created_nodes)
         try:
             for t in targets:
@@ -144,7 +152,7 @@ class HotMount:
         revoke = [n for n in before if (n.major, n.minor) not in after_keys]
         if targets is None:
             with trace.span("resolve"):
-                targets = self.targets(pod, container)
+                targets = self._resolve(pod, container)
         for t in targets:
             # reference order: deny → rm → kill (util.go:112,131,139)
             with trace.span("cgroup_rule", backend=self.backend.name, rules=len(revoke)):

@@ -211,14 +211,23 @@ class GpuMountService:
             self.hm.revoke_issues(pod, stale, st.hot, st.own)
         return issues
 
-    async def _rollback(self, pod: dict, what: str) -> None:
+    async def _rollback(self, pod: dict, what: str) -> bool:
+        """Reconcile the pod to its ledger state after a failed operation. Returns True if the
+        pod itself is gone (deleted or replaced meanwhile): nothing is left to repair then."""
         try:
-            fixed = await self.reconcile_pod(pod)
+            cur = await self.get_pod(podu.ns_of(pod), podu.name_of(pod), fresh=True)
+            if cur is None or podu.uid_of(cur) != podu.uid_of(pod) or \
+                    podu.phase_of(cur) != "Running":
+                log.kv(_log, 20, f"{what} rollback: pod is gone, nothing left on the node",
+                       pod=f"{podu.ns_of(pod)}/{podu.name_of(pod)}")
+                return True
+            fixed = await self.reconcile_pod(cur)
             if fixed:
                 log.kv(_log, 30, f"{what} rolled back to ledger state",
                        pod=f"{podu.ns_of(pod)}/{podu.name_of(pod)}", fixed=len(fixed))
         except Exception as e:  # noqa: BLE001
             _log.error("rollback after %s failed (the reconciler will retry): %s", what, e)
+        return False
 
     @staticmethod
     def _devices(gs: Sequence[AmdGpu], owner: Dict[int, str]) -> List:
@@ -320,7 +329,9 @@ class GpuMountService:
                     await self._release(res.placeholders)
                 except Exception as e2:  # noqa: BLE001
                     _log.error("placeholder release after failed mount: %s", e2)
-                await self._rollback(pod, "attach")
+                if await self._rollback(pod, "attach"):   # deleted while we were attaching
+                    return api.AddGPUResponse(add_gpu_result=api.ADD_POD_NOT_FOUND,
+                                              message=f"pod went away during the attach: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             log.kv(_log, 20, "attached", pod=f"{req.namespace}/{req.pod_name}",
                    gpus=[g.bdf for g in new])

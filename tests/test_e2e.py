@@ -699,3 +699,23 @@ def test_master_retries_unavailable_worker_and_the_retry_replays_not_duplicates(
         assert len(st.hot) == 2                  # not 4
         assert await lc.audit("default", "t") == []
     run(body)
+
+
+def test_tenant_deleted_mid_attach_reports_pod_not_found_and_leaks_nothing():
+    from gpumounter_amd.fakes.apiserver import LatencyModel
+
+    async def body(lc):
+        lc.tenant("t")
+
+        async def killer():
+            await asyncio.sleep(0.015)            # while the placeholders are being admitted
+            lc.cluster.delete("default", "t", grace=0)
+        (code, b), _ = await asyncio.gather(lc.add("default", "t", 2), killer())
+        assert code == 400 and b["add_gpu_result"] == "PodNotFound", b
+
+        async def clean():
+            live = [p for p in lc.cluster.placeholders()
+                    if not p["metadata"].get("deletionTimestamp")]
+            return not live and not node_of(lc).allocated
+        assert await _until(clean)
+    run(body, latency=LatencyModel(schedule_ms=30, admit_ms=20))
