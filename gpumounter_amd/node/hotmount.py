@@ -96,7 +96,7 @@ class HotMount:
             out.append(ContainerTarget(r, cgdir, t, pids))
         return out
 
-    def _resolve(self, pod: dict, container: str) -> List[ContainerTarget]:
+    def resolve(self, pod: dict, container: str = "") -> List[ContainerTarget]:
         """:meth:`targets` for a transaction: a container that vanished meanwhile (pod deleted
         or restarted mid-attach) is a MountError, so the caller's rollback runs."""
         try:
@@ -112,7 +112,7 @@ class HotMount:
         before_keys = {(n.major, n.minor) for n in before}
         grant = [n for n in after if (n.major, n.minor) not in before_keys]
         with trace.span("resolve"):
-            targets = self._resolve(pod, container)
+            targets = self.resolve(pod, container)
         done: List[tuple] = []  # (target, granted, created_nodes)
         try:
             for t in targets:
@@ -152,7 +152,7 @@ class HotMount:
         revoke = [n for n in before if (n.major, n.minor) not in after_keys]
         if targets is None:
             with trace.span("resolve"):
-                targets = self._resolve(pod, container)
+                targets = self.resolve(pod, container)
         for t in targets:
             # reference order: deny → rm → kill (util.go:112,131,139)
             with trace.span("cgroup_rule", backend=self.backend.name, rules=len(revoke)):

@@ -557,11 +557,14 @@ class GpuMountService:
             try:
                 with trace.span("busy_check"):
                     self.faults.check("busy_check")
-                    targets = self.hm.targets(pod, req.container)
+                    targets = self.hm.resolve(pod, req.container)
                     cpids = sorted({p for t in targets for p in t.pids})
                     busy = procs.busy_pids(self.inv, selected, cpids, self.cfg.drm_major,
                                            self.cfg.busy_detection)
             except (MountError, InjectedFault) as e:
+                if await self._rollback(pod, "detach"):   # the pod went away meanwhile
+                    return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_POD_NOT_FOUND,
+                                                 message=f"pod went away: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             if busy and not req.force:
                 _log.info("GPU busy in %s/%s: %s", req.namespace, req.pod_name, busy)
@@ -584,7 +587,9 @@ class GpuMountService:
                 await self._release(phs)
             except (MountError, ReserveError, InjectedFault, OSError) as e:
                 _log.error("detach failed on %s/%s: %s", req.namespace, req.pod_name, e)
-                await self._rollback(pod, "detach")
+                if await self._rollback(pod, "detach"):
+                    return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_POD_NOT_FOUND,
+                                                 message=f"pod went away: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             owner = {g.index: ph.name for ph in phs
                      for g in st.by_placeholder[(ph.namespace, ph.name)]}

@@ -719,3 +719,20 @@ def test_tenant_deleted_mid_attach_reports_pod_not_found_and_leaks_nothing():
             return not live and not node_of(lc).allocated
         assert await _until(clean)
     run(body, latency=LatencyModel(schedule_ms=30, admit_ms=20))
+
+
+def test_remove_after_tenant_deleted_is_pod_not_found_and_releases():
+    async def body(lc):
+        lc.tenant("t")
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200
+        lc.cluster.delete("default", "t", grace=0)
+        code, r = await lc.remove("default", "t", [d["uuid"] for d in b["devices"]])
+        assert code in (400, 404), r          # master or worker: the pod is gone
+
+        async def clean():
+            live = [p for p in lc.cluster.placeholders()
+                    if not p["metadata"].get("deletionTimestamp")]
+            return not live and not node_of(lc).allocated
+        assert await _until(clean)
+    run(body)
