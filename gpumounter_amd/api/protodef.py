@@ -7,6 +7,7 @@ output, JSON via ``json_format``).
 """
 from __future__ import annotations
 
+import base64
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
@@ -94,3 +95,64 @@ def method_path(package: str, service: str, method: str) -> str:
 
 def fields_of(cls) -> List[Tuple[str, int]]:
     return [(f.name, f.number) for f in cls.DESCRIPTOR.fields]
+
+
+# ------------------------------------------------------------------------------ fast to_dict
+_FD = None
+_CONV: Dict[object, list] = {}
+
+
+def _converters(desc) -> list:
+    """Per message type: (name, getter-kind, extra) for every field, computed once."""
+    global _FD
+    if _FD is None:
+        from google.protobuf.descriptor import FieldDescriptor as _F
+        _FD = _F
+    conv = _CONV.get(desc)
+    if conv is not None:
+        return conv
+    conv = []
+    for f in desc.fields:
+        rep = f.is_repeated if hasattr(f, "is_repeated") else f.label == _FD.LABEL_REPEATED
+        if f.type == _FD.TYPE_MESSAGE:
+            if f.message_type.GetOptions().map_entry:
+                kind = "map"
+            else:
+                kind = "msg"
+            extra = f.message_type
+        elif f.type == _FD.TYPE_ENUM:
+            kind, extra = "enum", {v.number: v.name for v in f.enum_type.values}
+        elif f.type in (_FD.TYPE_INT64, _FD.TYPE_UINT64, _FD.TYPE_SINT64, _FD.TYPE_FIXED64,
+                        _FD.TYPE_SFIXED64):
+            kind, extra = "int64", None          # proto3 JSON: 64-bit integers as strings
+        elif f.type == _FD.TYPE_BYTES:
+            kind, extra = "bytes", None
+        else:
+            kind, extra = "plain", None
+        conv.append((f.name, kind, extra, rep))
+    _CONV[desc] = conv
+    return conv
+
+
+def to_dict(msg) -> dict:
+    """``json_format.MessageToDict(msg, preserving_proto_field_name=True,
+    always_print_fields_with_no_presence=True)`` for the proto3 messages of this package, without
+    the generic reflection walk (several times faster on the master's reply path)."""
+    out = {}
+    for name, kind, extra, rep in _converters(msg.DESCRIPTOR):
+        v = getattr(msg, name)
+        if kind == "msg":
+            out[name] = [to_dict(x) for x in v] if rep else to_dict(v)
+        elif kind == "map":
+            out[name] = {str(k): (to_dict(x) if hasattr(x, "DESCRIPTOR") else x)
+                         for k, x in v.items()}
+        elif kind == "enum":
+            out[name] = [extra.get(x, x) for x in v] if rep else extra.get(v, v)
+        elif kind == "int64":
+            out[name] = [str(x) for x in v] if rep else str(v)
+        elif kind == "bytes":
+            out[name] = [base64.b64encode(x).decode() for x in v] if rep else \
+                base64.b64encode(v).decode()
+        else:
+            out[name] = list(v) if rep else v
+    return out

@@ -18,6 +18,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import os
 import sys
 from typing import List, Optional
 
@@ -28,14 +29,32 @@ def _cfg(args, **over):
     return Config.load(getattr(args, "config", None), **over)
 
 
+def _run_daemon(serve, cfg) -> int:
+    """asyncio.run(serve(cfg)); with GM_PROFILE_OUT=<file> under cProfile, stats written at
+    (SIGTERM-clean) shutdown — for finding the hot spots of a live daemon."""
+    out = os.environ.get("GM_PROFILE_OUT", "")
+    if not out:
+        asyncio.run(serve(cfg))
+        return 0
+    import cProfile
+
+    prof = cProfile.Profile()
+    prof.enable()
+    try:
+        asyncio.run(serve(cfg))
+    finally:
+        prof.disable()
+        prof.dump_stats(out)
+    return 0
+
+
 def cmd_master(args) -> int:
     from gpumounter_amd.master.app import serve
     from gpumounter_amd.utils import log
 
     cfg = _cfg(args, master_port=args.port)
     log.setup(cfg.log_level, cfg.log_json, cfg.log_file)
-    asyncio.run(serve(cfg))
-    return 0
+    return _run_daemon(serve, cfg)
 
 
 def cmd_worker(args) -> int:
@@ -44,8 +63,7 @@ def cmd_worker(args) -> int:
 
     cfg = _cfg(args, node_name=args.node, worker_port=args.port)
     log.setup(cfg.log_level, cfg.log_json, cfg.log_file)
-    asyncio.run(serve(cfg))
-    return 0
+    return _run_daemon(serve, cfg)
 
 
 def cmd_device_plugin(args) -> int:

@@ -24,6 +24,7 @@ import grpc
 from aiohttp import web
 
 from gpumounter_amd.api import gpu_mount as api
+from gpumounter_amd.api import protodef
 from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models import pod as podu
@@ -434,9 +435,7 @@ class Master:
 
     @staticmethod
     def _payload(resp, t0: float) -> dict:
-        from google.protobuf import json_format
-        d = json_format.MessageToDict(resp, preserving_proto_field_name=True,
-                                     always_print_fields_with_no_presence=True)
+        d = protodef.to_dict(resp)
         d["master_ms"] = (time.perf_counter() - t0) * 1e3
         return d
 

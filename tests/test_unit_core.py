@@ -162,3 +162,30 @@ def test_device_nodes_and_ledger_keys():
     for key in ("u-3", "0000:75:00.0", "75:00.0", "renderD131", "CARD3", "GPU-u-3"):
         assert find_gpu([g], key) is g, key
     assert normalize_device_id(" ABC ") == "abc"
+
+
+def test_fast_to_dict_matches_json_format():
+    """api/protodef.to_dict is the master's reply encoder; it must equal protobuf's MessageToDict
+    (proto field names, all fields, enums by name, 64-bit ints as strings)."""
+    from google.protobuf import json_format
+
+    from gpumounter_amd.api import gpu_mount as api
+    from gpumounter_amd.api.protodef import to_dict
+
+    def ref(m):
+        return json_format.MessageToDict(m, preserving_proto_field_name=True,
+                                         always_print_fields_with_no_presence=True)
+    msgs = [
+        api.AddGPUResponse(),
+        api.AddGPUResponse(add_gpu_result=api.ADD_INSUFFICIENT, message="x", total_ms=1.5,
+                           devices=[api.Device(uuid="u", bdf="0000:05:00.0", index=3,
+                                               render_minor=131, numa_node=1)],
+                           timings=[api.StageTiming(name="mount", ms=0.25)]),
+        api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_BUSY, killed_pids=[7, 9],
+                              message="busy"),
+        api.AddGPURequest(pod_name="p", namespace="n", gpu_num=2, is_entire_mount=True,
+                          idempotency_key="k"),
+        api.RemoveGPURequest(pod_name="p", namespace="n", uuids=["a", "b"], force=True),
+    ]
+    for m in msgs:
+        assert to_dict(m) == ref(m), type(m).__name__
