@@ -382,20 +382,30 @@ class PlaceholderManager:
             return
         with trace.span("ledger_release", placeholders=len(phs)):
             self.faults.check("ledger_release")
+            # Tombstone before the DELETE is sent: the watch can deliver the DELETED event
+            # before the DELETE response, and an un-tombstoned delete reads as a foreign one
+            # (→ a spurious revocation and GPURevoked warning on the tenant).
+            now = asyncio.get_running_loop().time()
+            for p in phs:
+                if p.uid:
+                    self.tombstones[p.uid] = now
             res = await asyncio.gather(
                 *[self.kube.delete_pod(p.namespace, p.name, grace_period_s=0, uid=p.uid or "")
                   for p in phs], return_exceptions=True)
             failed = []
-            now = asyncio.get_running_loop().time()
             for p, r in zip(phs, res):
                 if isinstance(r, Exception) and not isinstance(r, NotFound):
                     _log.error("delete placeholder %s/%s: %s", p.namespace, p.name, r)
                     failed.append(p)
+                    if p.uid:
+                        self.tombstones.pop(p.uid, None)
                 else:
                     # grace 0 + no finalizers: the object is gone from the apiserver (and the
                     # scheduler's books) once DELETE returns; drop it from the cached views
                     if p.uid:
-                        self.tombstones[p.uid] = now
+                        cur = self.informer.cache.get((p.namespace, p.name))
+                        if cur is None or cur["metadata"].get("uid") != p.uid:
+                            self.tombstones.pop(p.uid, None)   # DELETED event already seen
                         self.device_ids.pop(p.uid, None)
                     if isinstance(self.last_ledger, dict):
                         self.last_ledger.pop((p.namespace, p.name), None)

@@ -37,3 +37,30 @@ def test_daemons_as_processes_attach_detach_and_exit_cleanly_on_sigterm():
         codes = pc.stop()
     assert codes == {"master": 0, "worker-node-0": 0, "worker-node-1": 0, "controlplane": 0}, \
         codes
+
+
+def test_own_releases_are_never_mistaken_for_foreign_deletes():
+    """The watch can deliver a placeholder's DELETED event before the worker's own DELETE call
+    returns (separate processes make that common). Such a release must not be treated as a
+    foreign delete: no revocation reactions, no GPURevoked warnings on the tenant."""
+    import json
+    import urllib.request
+
+    pc = ProcessCluster()
+    try:
+        pc.start()
+        pc.tenant("t")
+        for _ in range(40):
+            code, b = pc.add("default", "t", 1, entire=True)
+            assert code == 200, b
+            code, _ = pc.remove("default", "t", [d["uuid"] for d in b["devices"]])
+            assert code == 200
+        m = pc.worker_metrics()
+        assert "gm_reconcile_actions_total{" not in m, \
+            [ln for ln in m.splitlines() if "reconcile_actions" in ln]
+        with urllib.request.urlopen(pc.info["api_url"] +
+                                    "/api/v1/namespaces/default/events") as r:
+            reasons = {e["reason"] for e in json.load(r)["items"]}
+        assert "GPURevoked" not in reasons, reasons
+    finally:
+        pc.stop()
