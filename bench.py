@@ -109,8 +109,8 @@ class _ProcCP:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mode", choices=("entire", "single"), default="entire")
     ap.add_argument("--latency", choices=("zero", "realistic"), default="zero",
                     help="fake control-plane latency model (zero = controller overhead only)")
