@@ -23,6 +23,7 @@ import socket
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 import urllib.error
 import urllib.parse
@@ -72,23 +73,27 @@ class ProcessCluster:
         self.procs: Dict[str, subprocess.Popen] = {}
         self.info: dict = {}
         self.worker_ports: Dict[str, Tuple[int, int]] = {}   # node → (grpc, metrics)
+        self._worker_env: Dict[str, Dict[str, str]] = {}
         self.master_url = ""
-        self._conn: Optional[http.client.HTTPConnection] = None   # keep-alive to the master
+        self._local = threading.local()   # one keep-alive connection to the master per thread
+        self._conns: List[http.client.HTTPConnection] = []
 
     def _master(self, method: str, path: str, body: Optional[bytes] = None,
                 headers: Optional[dict] = None) -> Tuple[int, bytes]:
         """One request on a persistent connection (as a real client library would hold)."""
         for attempt in (0, 1):
-            if self._conn is None:
+            conn = getattr(self._local, "conn", None)
+            if conn is None:
                 host, port = self.master_url[len("http://"):].split(":")
-                self._conn = http.client.HTTPConnection(host, int(port), timeout=120)
+                conn = self._local.conn = http.client.HTTPConnection(host, int(port), timeout=120)
+                self._conns.append(conn)
             try:
-                self._conn.request(method, path, body=body, headers=headers or {})
-                r = self._conn.getresponse()
+                conn.request(method, path, body=body, headers=headers or {})
+                r = conn.getresponse()
                 return r.status, r.read()
             except (http.client.HTTPException, OSError):
-                self._conn.close()
-                self._conn = None
+                conn.close()
+                self._local.conn = None
                 if attempt:
                     raise
         raise AssertionError("unreachable")
@@ -146,15 +151,10 @@ class ProcessCluster:
                    "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": str(gport),
                    "GM_METRICS_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
                    "GM_LOG_JSON": "false", **self.worker_env}
+            self._worker_env[node] = env
             self._spawn(f"worker-{node}", [*self.entry, "worker"], env)
-        for node, (gport, mport) in self.worker_ports.items():
-            self._wait(f"worker {node}",
-                       lambda m=mport: _http("GET", f"http://127.0.0.1:{m}/readyz")[0] == 200)
-            code, _ = _http("POST", f"{api}/_fake/worker",
-                            json.dumps({"node": node, "port": gport}).encode(),
-                            {"Content-Type": "application/json"})
-            if code != 201:
-                raise RuntimeError(f"worker registration for {node} failed: {code}")
+        for node in self.worker_ports:
+            self._await_worker(node)
         mport = free_port()
         self._spawn("master", [*self.entry, "master"],
                     {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1",
@@ -166,11 +166,32 @@ class ProcessCluster:
                 "GET", f"{self.master_url}/api/v1/nodes/{n}/gpus")[0] == 200)
         return self
 
+    def _await_worker(self, node: str) -> None:
+        gport, mport = self.worker_ports[node]
+        self._wait(f"worker {node}",
+                   lambda: _http("GET", f"http://127.0.0.1:{mport}/readyz")[0] == 200)
+        code, _ = _http("POST", f"{self.info['api_url']}/_fake/worker",
+                        json.dumps({"node": node, "port": gport}).encode(),
+                        {"Content-Type": "application/json"})
+        if code != 201:
+            raise RuntimeError(f"worker registration for {node} failed: {code}")
+
+    def kill_worker(self, node: str = "node-0", sig: int = signal.SIGKILL) -> int:
+        """Crash (SIGKILL) or stop a worker process; returns its exit status."""
+        p = self.procs[f"worker-{node}"]
+        p.send_signal(sig)
+        return p.wait(20)
+
+    def restart_worker(self, node: str = "node-0") -> None:
+        """Start the node's worker again (same ports and environment) and wait until ready."""
+        self._spawn(f"worker-{node}", [*self.entry, "worker"], self._worker_env[node])
+        self._await_worker(node)
+
     def stop(self, timeout: float = 20.0) -> Dict[str, Optional[int]]:
         """SIGTERM every daemon (master and workers first) → their exit codes."""
-        if self._conn is not None:
-            self._conn.close()
-            self._conn = None
+        for conn in self._conns:
+            conn.close()
+        self._conns.clear()
         codes: Dict[str, Optional[int]] = {}
         order = [k for k in self.procs if k == "master"] + \
             [k for k in self.procs if k.startswith("worker-")] + \
