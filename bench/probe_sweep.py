@@ -22,7 +22,7 @@ quick = "--quick" in sys.argv
 out = {"hbm_copy_GBps": {}, "hbm_read_GBps": {}, "mfma_TFLOPs": {}, "torch": {}}
 g = C.c_double(0)
 sizes = (1 << 30, 4 << 30)
-for variant in ((2, 3) if quick else (0, 1, 2, 3, 4)):
+for variant in ((2, 3, 5, 6) if quick else (0, 1, 2, 3, 4, 5, 6)):
     for bpc in (4, 8):
         for size in sizes:
             rc = lib.gm_probe_hbm_copy_variant(0, variant, size, 10, bpc, C.byref(g))

@@ -132,6 +132,39 @@ __global__ __launch_bounds__(256) void k_read_chunk(const float4* __restrict__ s
   if (x == 0x9e3779b9u) sink[blockIdx.x & 1023] = x;  // practically never taken, keeps the loads
 }
 
+// Software-pipelined variant: the next chunk's loads are issued before the current chunk's
+// stores, so a wave always has kChunk reads outstanding while its writes drain.
+template <int kChunk>
+__global__ __launch_bounds__(256) void k_copy_pipe(const float4* __restrict__ src_,
+                                                   float4* __restrict__ dst_, size_t n,
+                                                   size_t per_block) {
+  const v4f* __restrict__ src = reinterpret_cast<const v4f*>(src_);
+  v4f* __restrict__ dst = reinterpret_cast<v4f*>(dst_);
+  const size_t begin = (size_t)blockIdx.x * per_block;
+  const size_t end = begin + per_block < n ? begin + per_block : n;
+  constexpr size_t kStep = (size_t)kChunk * 256;
+  size_t i = begin + threadIdx.x;
+  if (i + (kChunk - 1) * 256 < end) {
+    v4f cur[kChunk];
+#pragma unroll
+    for (int c = 0; c < kChunk; ++c) cur[c] = __builtin_nontemporal_load(&src[i + c * 256]);
+    for (; i + kStep + (kChunk - 1) * 256 < end; i += kStep) {
+      v4f nxt[kChunk];
+#pragma unroll
+      for (int c = 0; c < kChunk; ++c)
+        nxt[c] = __builtin_nontemporal_load(&src[i + kStep + c * 256]);
+#pragma unroll
+      for (int c = 0; c < kChunk; ++c) __builtin_nontemporal_store(cur[c], &dst[i + c * 256]);
+#pragma unroll
+      for (int c = 0; c < kChunk; ++c) cur[c] = nxt[c];
+    }
+#pragma unroll
+    for (int c = 0; c < kChunk; ++c) __builtin_nontemporal_store(cur[c], &dst[i + c * 256]);
+    i += kStep;
+  }
+  for (; i < end; i += 256) dst[i] = src[i];
+}
+
 __global__ __launch_bounds__(256) void k_fill(float4* dst, size_t n, float v) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
@@ -389,6 +422,14 @@ int gm_probe_hbm_copy_variant(int dev, int variant, uint64_t bytes, int iters,
       case 4:
         hipLaunchKernelGGL((k_copy_chunk<8, false>), dim3(blocks), dim3(256), 0, 0, src, dst,
                            n, per_block);
+        break;
+      case 5:
+        hipLaunchKernelGGL((k_copy_pipe<4>), dim3(blocks), dim3(256), 0, 0, src, dst, n,
+                           per_block);
+        break;
+      case 6:
+        hipLaunchKernelGGL((k_copy_pipe<2>), dim3(blocks), dim3(256), 0, 0, src, dst, n,
+                           per_block);
         break;
       default:
         hipLaunchKernelGGL((k_copy_chunk<4, true>), dim3(blocks), dim3(256), 0, 0, src, dst,

@@ -36,7 +36,8 @@ int gm_probe_hbm_copy(int dev, uint64_t bytes, int iters, double* gbps);
 // Read-only HBM stream over `bytes` (8 nontemporal 16-B loads in flight per lane); GB/s read.
 int gm_probe_hbm_read(int dev, uint64_t bytes, int iters, int blocks_per_cu, double* gbps);
 // Tuning variants: 0 grid-stride, 1 chunked 4×16B/lane, 2 chunked 4 + nontemporal,
-// 3 chunked 8 + nontemporal, 4 chunked 8.
+// 3 chunked 8 + nontemporal, 4 chunked 8, 5/6 software-pipelined 4/2 (next loads before
+// current stores), nontemporal.
 int gm_probe_hbm_copy_variant(int dev, int variant, uint64_t bytes, int iters,
                               int blocks_per_cu, double* gbps);
 // variant 0: v_mfma_f32_32x32x16_bf16 × 4 chains, 1: v_mfma_f32_16x16x32_bf16 × 4 chains,
