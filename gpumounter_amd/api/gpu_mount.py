@@ -23,6 +23,7 @@ _pf.message("AddGPURequest", [
     ("container", 5, "string", "opt"),          # target container (default: all containers)
     ("request_id", 6, "string", "opt"),
     ("idempotency_key", 7, "string", "opt"),    # client retry key: same key → same attach
+    ("requested_by", 8, "string", "opt"),       # caller identity from the master's authn (audit)
 ])
 _pf.message("Device", [
     ("uuid", 1, "string", "opt"),
@@ -49,6 +50,7 @@ _pf.message("RemoveGPURequest", [
     ("force", 4, "bool", "opt"),
     ("container", 5, "string", "opt"),
     ("request_id", 6, "string", "opt"),
+    ("requested_by", 7, "string", "opt"),
 ])
 _pf.message("RemoveGPUResponse", [
     ("remove_gpu_result", 1, "enum:.gpu_mount.RemoveGPUResponse.RemoveGPUResult", "opt"),

@@ -77,6 +77,9 @@ _SERVICE_CONFIG = json.dumps({"methodConfig": [{
                     "backoffMultiplier": 2, "retryableStatusCodes": ["UNAVAILABLE"]}}]})
 
 
+USER_KEY = web.RequestKey("gm_user", str)   # the caller's identity, set by _denied()
+
+
 class WorkerDirectory:
     """node name → worker gRPC target, from a watch on the worker DaemonSet pods."""
 
@@ -204,8 +207,18 @@ class Master:
         authn/authz at all: SURVEY defect 13)."""
         d = await self.authz.check(request.headers, verb, ns, resource, name)
         if d.allowed:
+            request[USER_KEY] = self._identity(request, d)
             return None
         return self._reply(request, route, d.status, d.reason, {})
+
+    def _identity(self, request: web.Request, d) -> str:
+        """Who asked, for the audit trail (Events, logs): the authenticated Kubernetes user, the
+        shared-token holder, or the anonymous caller's address."""
+        if d.user:
+            return d.user
+        if self.cfg.api_token:
+            return "api-token"
+        return f"anonymous@{request.remote or '?'}"
 
     def _reply(self, request, route: str, status: int, text: str, payload: dict) -> web.Response:
         self.metrics.http_requests.labels(route=route, code=str(status)).inc()
@@ -252,7 +265,7 @@ class Master:
 
     # ------------------------------------------------------------------------ operations
     async def _add(self, ns: str, name: str, n: int, entire: bool, container: str = "",
-                   rid: str = "", key: str = ""):
+                   rid: str = "", key: str = "", user: str = ""):
         """AddGPU through the pod's worker → (status, text, payload) as the reference maps it
         (reference main.go:103-116)."""
         t0 = time.perf_counter()
@@ -266,7 +279,8 @@ class Master:
             try:
                 resp = await stub(api.AddGPURequest(
                     pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
-                    request_id=rid, container=container, idempotency_key=key),
+                    request_id=rid, container=container, idempotency_key=key,
+                    requested_by=user),
                     timeout=self.cfg.rpc_timeout_s)
             except grpc.aio.AioRpcError as e:
                 if cached and e.code() == grpc.StatusCode.FAILED_PRECONDITION and \
@@ -295,7 +309,7 @@ class Master:
         return 500, "Service Internal Error", payload
 
     async def _remove(self, ns: str, name: str, uuids, force: bool, container: str = "",
-                      rid: str = ""):
+                      rid: str = "", user: str = ""):
         """RemoveGPU through the pod's worker (reference main.go:206-224 mapping)."""
         t0 = time.perf_counter()
         for fresh in (False, True):
@@ -308,7 +322,7 @@ class Master:
             try:
                 resp = await stub(api.RemoveGPURequest(
                     pod_name=name, namespace=ns, uuids=uuids, force=force, request_id=rid,
-                    container=container), timeout=self.cfg.rpc_timeout_s)
+                    container=container, requested_by=user), timeout=self.cfg.rpc_timeout_s)
             except grpc.aio.AioRpcError as e:
                 _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name,
                            e.details())
@@ -352,7 +366,7 @@ class Master:
             return self._reply(request, route, 400, f"Invalid param gpuNum: {mi['gpuNum']}", {})
         status, text, payload = await self._add(
             ns, name, n, entire, request.query.get("container", ""), rid,
-            request.headers.get("Idempotency-Key", "") or rid)
+            request.headers.get("Idempotency-Key", "") or rid, request.get(USER_KEY, ""))
         return self._reply(request, route, status, text, payload)
 
     async def remove_gpu(self, request: web.Request) -> web.Response:
@@ -376,7 +390,8 @@ class Master:
                                f"Invalid parameter force: {mi['force']}(should be true or false)",
                                {})
         status, text, payload = await self._remove(ns, name, uuids, force,
-                                                   request.query.get("container", ""), rid)
+                                                   request.query.get("container", ""), rid,
+                                                   request.get(USER_KEY, ""))
         return self._reply(request, route, status, text, payload)
 
     async def batch(self, request: web.Request) -> web.Response:
@@ -401,25 +416,29 @@ class Master:
             try:
                 kind = op["op"]
                 ns, name = op.get("namespace", "default"), op["pod"]
+                user = request.get(USER_KEY, "")
                 if self.authz.mode == "kube":   # per operation: namespaces may differ
                     d = await self.authz.check(request.headers,
                                                "create" if kind == "add" else "delete", ns,
                                                name=name)
                     if not d.allowed:
                         return d.status, d.reason, {}
+                    user = self._identity(request, d)
                 if kind == "add":
                     n = int(op["gpus"])
                     if n <= 0:
                         return 400, f"Invalid param gpuNum: {n}", {}
+                    rid = log.new_request_id("add")
                     return await self._add(ns, name, n, bool(op.get("entire", False)),
-                                           op.get("container", ""), log.new_request_id("add"),
-                                           op.get("idempotency_key", ""))
+                                           op.get("container", ""), rid,
+                                           op.get("idempotency_key", "") or rid, user)
                 if kind == "remove":
                     uuids = list(op["uuids"])
                     if not uuids:
                         return 400, "Invalid parameter", {}
                     return await self._remove(ns, name, uuids, bool(op.get("force", False)),
-                                              op.get("container", ""), log.new_request_id("rm"))
+                                              op.get("container", ""), log.new_request_id("rm"),
+                                              user)
                 return 400, f"unknown op {kind!r}", {}
             except (KeyError, TypeError, ValueError) as e:
                 return 400, f"bad operation: {e}", {}

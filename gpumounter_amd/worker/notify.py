@@ -141,16 +141,20 @@ class Notifier:
     def describe(gs: Sequence[AmdGpu]) -> str:
         return ", ".join(f"{g.bdf} (renderD{g.render_minor})" for g in gs)
 
+    @staticmethod
+    def _by(user: str) -> str:
+        return f" (requested by {user})" if user else ""
+
     def attached(self, pod: dict, new: Sequence[AmdGpu], holding: Sequence[AmdGpu],
-                 mode: str) -> None:
+                 mode: str, by: str = "") -> None:
         self.event(pod, "GPUAttached",
-                   f"hot-mounted {len(new)} GPU(s) ({mode}): {self.describe(new)}")
+                   f"hot-mounted {len(new)} GPU(s) ({mode}): {self.describe(new)}{self._by(by)}")
         self.annotate(pod, holding)
 
     def detached(self, pod: dict, removed: Sequence[AmdGpu], holding: Sequence[AmdGpu],
-                 killed: Sequence[int]) -> None:
+                 killed: Sequence[int], by: str = "") -> None:
         self.event(pod, "GPUDetached",
-                   f"removed {len(removed)} GPU(s): {self.describe(removed)}")
+                   f"removed {len(removed)} GPU(s): {self.describe(removed)}{self._by(by)}")
         if killed:
             self.event(pod, "GPUProcessesTerminated",
                        f"force-removed GPUs were in use; signalled PIDs {list(killed)}",

@@ -334,9 +334,10 @@ class GpuMountService:
                                               message=f"pod went away during the attach: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             log.kv(_log, 20, "attached", pod=f"{req.namespace}/{req.pod_name}",
-                   gpus=[g.bdf for g in new])
+                   gpus=[g.bdf for g in new], by=req.requested_by)
             self.notify.attached(pod, new, list(st.hot) + new,
-                                 "entire" if req.is_entire_mount else "single")
+                                 "entire" if req.is_entire_mount else "single",
+                                 by=req.requested_by)
             return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS,
                                       devices=self._devices(new, owner),
                                       message="Add GPU Success")
@@ -593,7 +594,9 @@ class GpuMountService:
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             owner = {g.index: ph.name for ph in phs
                      for g in st.by_placeholder[(ph.namespace, ph.name)]}
-            self.notify.detached(pod, selected, keep, killed)
+            log.kv(_log, 20, "detached", pod=f"{req.namespace}/{req.pod_name}",
+                   gpus=[g.bdf for g in selected], killed=killed, by=req.requested_by)
+            self.notify.detached(pod, selected, keep, killed, by=req.requested_by)
             return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_SUCCESS,
                                          devices=self._devices(selected, owner),
                                          killed_pids=killed, message="Remove GPU Success")

@@ -69,3 +69,29 @@ def test_batch_checks_every_operation():
             res = (await r.json())["results"]
         assert [x["code"] for x in res] == [200, 403]
     run(body)
+
+
+def test_events_record_who_asked():
+    """The caller's identity travels master → worker (requested_by) into the tenant's Events."""
+    async def body(lc):
+        lc.tenant("a1", ns="team-a")
+        code, b = await lc.add("team-a", "a1", 1, token="tok-alice")
+        assert code == 200
+        code, _ = await lc.remove("team-a", "a1", [b["devices"][0]["uuid"]], token="tok-ops")
+        assert code == 200
+        await lc.nodes["node-0"].worker.service.notify.drain()
+        msgs = {e["reason"]: e["message"] for e in lc.cluster.events_for("team-a", "a1")}
+        assert msgs["GPUAttached"].endswith("(requested by alice)")
+        assert msgs["GPUDetached"].endswith("(requested by ops)")
+    run(body)
+
+
+def test_anonymous_callers_are_recorded_by_address():
+    async def main():
+        async with LocalCluster() as lc:
+            lc.tenant("t")
+            assert (await lc.add("default", "t", 1))[0] == 200
+            await lc.nodes["node-0"].worker.service.notify.drain()
+            (ev,) = lc.cluster.events_for("default", "t")
+            assert "(requested by anonymous@127.0.0.1)" in ev["message"]
+    asyncio.run(main())
