@@ -39,6 +39,9 @@ class Metrics:
                                    ["rpc"], registry=r)
         self.plugin_healthy = Gauge("gm_device_plugin_healthy_gpus",
                                     "GPUs advertised Healthy", registry=r)
+        self.hot_gpus = Gauge("gm_hot_mounted_gpus", "GPUs hot-mounted into pods, by the pods' "
+                              "namespace (sum over time = GPU-seconds for chargeback)",
+                              ["namespace"], registry=r)
         self.http_requests = Counter("gm_http_requests_total", "master HTTP requests",
                                      ["route", "code"], registry=r)
 

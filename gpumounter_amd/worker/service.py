@@ -95,6 +95,7 @@ class GpuMountService:
         self.plugin = None  # AmdGpuDevicePlugin, attached by the Worker with device_plugin=1
         self.notify = Notifier(cfg, kube)
         self.quota = GpuQuota(cfg, kube)
+        self._ns_seen: set = set()
         # Reservations that must not interleave on a node run one at a time:
         # * trim briefly holds every free GPU — a concurrent one would see a full node;
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
@@ -664,4 +665,15 @@ class GpuMountService:
         for state in ("GPU_FREE_STATE", "GPU_ALLOCATED_STATE"):
             self.metrics.ledger_gpus.labels(state=state).set(
                 sum(1 for g in gpus if g.state.value == state))
+        # hot-mounted GPUs per tenant namespace (chargeback: integrate over time in Prometheus)
+        per_ns: Dict[str, int] = {}
+        for ph in phs:
+            if ph["mode"] != "standby" and ph["owner_namespace"]:
+                per_ns[ph["owner_namespace"]] = per_ns.get(ph["owner_namespace"], 0) + \
+                    len(ph["device_ids"])
+        for ns in set(self._ns_seen) - set(per_ns):
+            self.metrics.hot_gpus.labels(namespace=ns).set(0)
+        for ns, n in per_ns.items():
+            self.metrics.hot_gpus.labels(namespace=ns).set(n)
+        self._ns_seen = set(per_ns) | set(self._ns_seen)
         return out

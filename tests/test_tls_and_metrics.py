@@ -66,3 +66,26 @@ def test_worker_metrics_collector():
             assert 'gm_ledger_gpus{state="GPU_ALLOCATED_STATE"} 3.0' in text
             assert 'gm_gpu_processes{gpu="0000:05:00.0"}' in text
     asyncio.run(main())
+
+
+def test_hot_mounted_gpus_gauge_per_namespace():
+    import asyncio
+
+    from gpumounter_amd.fakes.harness import LocalCluster
+
+    async def main():
+        async with LocalCluster() as lc:
+            lc.tenant("a", ns="team-a")
+            lc.tenant("b", ns="team-b")
+            assert (await lc.add("team-a", "a", 3))[0] == 200
+            code, b = await lc.add("team-b", "b", 2)
+            assert code == 200
+            w = lc.nodes["node-0"].worker
+            await w.collect_metrics()
+            text = w.metrics.render().decode()
+            assert 'gm_hot_mounted_gpus{namespace="team-a"} 3.0' in text
+            assert 'gm_hot_mounted_gpus{namespace="team-b"} 2.0' in text
+            assert (await lc.remove("team-b", "b", [d["uuid"] for d in b["devices"]]))[0] == 200
+            await w.collect_metrics()
+            assert 'gm_hot_mounted_gpus{namespace="team-b"} 0.0' in w.metrics.render().decode()
+    asyncio.run(main())
