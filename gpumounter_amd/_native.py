@@ -88,6 +88,8 @@ def smi() -> C.CDLL:
         lib.gm_smi_link_matrix.argtypes = [C.POINTER(LinkInfo), C.c_uint32]
         lib.gm_smi_process_list.argtypes = [C.c_uint32, C.POINTER(ProcInfo), C.c_uint32,
                                             C.POINTER(C.c_uint32)]
+        lib.gm_smi_ecc.argtypes = [C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint64)]
         lib.gm_smi_strerror.argtypes = [C.c_int]
         lib.gm_smi_strerror.restype = C.c_char_p
         lib.gm_smi_lib_path.restype = C.c_char_p
@@ -103,6 +105,7 @@ def mock_smi_path() -> str:
 def mock_smi() -> C.CDLL:
     lib = _load("libamd_smi_mock.so", "host")
     lib.gm_mock_set_procs_file.argtypes = [C.c_char_p]
+    lib.gm_mock_set_ecc.argtypes = [C.c_uint32, C.c_uint64, C.c_uint64]
     return lib
 
 

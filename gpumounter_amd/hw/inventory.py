@@ -13,7 +13,7 @@ import ctypes as C
 import os
 import threading
 from dataclasses import dataclass
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Set, Tuple
 
 from gpumounter_amd import _native
 from gpumounter_amd.models.device import (DEFAULT_KFD_MAJOR, AmdGpu, LinkMatrix, find_gpu,
@@ -88,6 +88,9 @@ class Inventory:
         self._gpus: List[AmdGpu] = []
         self._links: Optional[LinkMatrix] = None
         self._keys = None
+        self.ecc_policy = "new"                 # off | new | any (see healthy())
+        self._ecc_base: Dict[int, int] = {}
+        self._ecc_failed: Set[int] = set()
         self.refresh()
 
     # ---------------------------------------------------------------------------------- static
@@ -177,16 +180,39 @@ class Inventory:
                            int(buf[i].cu_occupancy), buf[i].name.decode(errors="replace"))
                 for i in range(min(n.value, cap))]
 
+    def ecc(self, index: int) -> Optional[Tuple[int, int, int]]:
+        """(correctable, uncorrectable, deferred) accumulated ECC errors, or None when the
+        driver does not report them."""
+        ce, ue, de = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        st = _native.smi().gm_smi_ecc(index, C.byref(ce), C.byref(ue), C.byref(de))
+        if st != 0:
+            return None
+        return ce.value, ue.value, de.value
+
     def healthy(self) -> Dict[int, bool]:
-        """Per-GPU liveness for the device plugin: the device still answers amdsmi queries with
-        the identity it was enumerated with (a GPU that fell off the bus or was reset into a
-        different partition mode reads as unhealthy)."""
+        """Per-GPU health for placement and the device plugin:
+
+        * liveness — the device still answers amdsmi queries with the identity it was enumerated
+          with (a GPU that fell off the bus or was reset into another partition mode fails);
+        * memory errors, by ``ecc_policy``: ``new`` (default) fails a GPU whose uncorrectable
+          ECC count rose since this process first looked (a fresh hardware fault), ``any``
+          fails every GPU with an uncorrectable error on record, ``off`` ignores ECC.
+        A GPU never recovers from an ECC failure within the process (drain it, then restart
+        the worker after repair)."""
         smi = _native.smi()
         out: Dict[int, bool] = {}
         for g in self.gpus():
             info = _native.GpuInfo()
             st = smi.gm_smi_gpu_info(g.index, C.byref(info))
-            out[g.index] = st == 0 and info.bdf.decode().lower() == g.bdf
+            ok = st == 0 and info.bdf.decode().lower() == g.bdf
+            if ok and self.ecc_policy != "off":
+                counts = self.ecc(g.index)
+                if counts is not None:
+                    ue = counts[1]
+                    base = self._ecc_base.setdefault(g.index, ue)
+                    if (self.ecc_policy == "any" and ue > 0) or ue > base:
+                        self._ecc_failed.add(g.index)
+            out[g.index] = ok and g.index not in self._ecc_failed
         return out
 
     def summary(self) -> Dict:

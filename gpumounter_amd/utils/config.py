@@ -98,6 +98,10 @@ class Config:
     device_plugin_inject: bool = True     # False: no device specs (kind / mock inventory)
     device_plugin_health_s: float = 5.0   # react to foreign placeholder / owner deletes at once
     max_gpus_per_request: int = 64
+    # GPUs with uncorrectable memory errors are left out of placement and reported Unhealthy by
+    # the device plugin: new (errors since the worker started) | any (any on record) | off
+    ecc_policy: str = "new"
+    health_period_s: float = 5.0       # liveness + ECC re-check period
     # pool-namespace placeholders are invisible to the tenant namespace's ResourceQuota; enforce
     # requests.<resource_name> quotas for hot-mounted GPUs ourselves (cluster/quota.py) | off
     quota_mode: str = "enforce"
@@ -173,6 +177,7 @@ class Config:
         _choice("cgroup_driver", self.cgroup_driver, ("auto", "cgroupfs", "systemd"))
         _choice("systemd_device_allow", self.systemd_device_allow, ("auto", "on", "off"))
         _choice("quota_mode", self.quota_mode, ("enforce", "off"))
+        _choice("ecc_policy", self.ecc_policy, ("new", "any", "off"))
         _choice("devnode_mode", self.devnode_mode, ("procroot", "setns", "emulate"))
         _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
         _choice("placement_enforce", self.placement_enforce, ("hint", "trim"))

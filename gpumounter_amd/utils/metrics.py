@@ -39,6 +39,8 @@ class Metrics:
                                    ["rpc"], registry=r)
         self.plugin_healthy = Gauge("gm_device_plugin_healthy_gpus",
                                     "GPUs advertised Healthy", registry=r)
+        self.gpu_healthy = Gauge("gm_gpu_healthy", "1 = usable for placement (liveness + ECC "
+                                 "policy), 0 = excluded", ["gpu"], registry=r)
         self.hot_gpus = Gauge("gm_hot_mounted_gpus", "GPUs hot-mounted into pods, by the pods' "
                               "namespace (sum over time = GPU-seconds for chargeback)",
                               ["namespace"], registry=r)

@@ -55,6 +55,7 @@ class Worker:
         self.cfg = cfg
         self.kube = kube or KubeClient.from_config(cfg)
         self.inv = inventory or Inventory(cfg.amdsmi_lib, cfg.kfd_major, cfg.kfd_dev_path)
+        self.inv.ecc_policy = cfg.ecc_policy
         self.metrics = Metrics()
         self.ledger = LedgerClient(cfg.kubelet_socket, cfg.resource_name, cfg.kubelet_timeout_s,
                                    cfg.podresources_api)
@@ -182,6 +183,9 @@ class Worker:
         await self.pool.start()
         if self.cfg.metrics_period_s > 0:
             self._collector = asyncio.ensure_future(self._collect_loop())
+        await self.check_health()          # ECC baseline before the first attach
+        if self.cfg.health_period_s > 0:
+            self._health_task = asyncio.ensure_future(self._health_loop())
         if self.cfg.gc_tune:
             runtime.tune_gc()
         self.ready = True
@@ -215,6 +219,33 @@ class Worker:
         return web.json_response({"pod": f"{ns}/{name}", "consistent": not issues,
                                   "issues": [vars(i) for i in issues]})
 
+    async def check_health(self) -> None:
+        """Refresh GPU health (liveness + ECC policy, hw/inventory.py) off the request path; the
+        attach path only reads the cached set of unhealthy GPUs."""
+        h = await asyncio.get_running_loop().run_in_executor(None, self.inv.healthy)
+        bad = {i for i, ok in h.items() if not ok}
+        if bad != self.service.unhealthy:
+            by_index = {g.index: g.bdf for g in self.inv.gpus()}
+            _log.warning("GPU health changed: unhealthy now %s",
+                         sorted(by_index.get(i, str(i)) for i in bad))
+            self.service.unhealthy = bad
+            if self.plugin is not None:
+                for i, ok in h.items():
+                    self.plugin.health[i] = ok
+                self.plugin._notify()  # noqa: SLF001 - re-send ListAndWatch
+        for g in self.inv.gpus():
+            self.metrics.gpu_healthy.labels(gpu=g.bdf).set(0 if g.index in bad else 1)
+
+    async def _health_loop(self) -> None:
+        while True:
+            await asyncio.sleep(self.cfg.health_period_s)
+            try:
+                await self.check_health()
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001
+                _log.warning("health check failed: %s", e)
+
     async def _collect_loop(self) -> None:
         """Per-GPU process gauges + ledger state gauges."""
         while True:
@@ -241,6 +272,8 @@ class Worker:
         self.ready = False
         if getattr(self, "_collector", None) is not None:
             self._collector.cancel()
+        if getattr(self, "_health_task", None) is not None:
+            self._health_task.cancel()
         await self.pool.stop()
         await self.reconciler.stop()
         await self.service.notify.stop()

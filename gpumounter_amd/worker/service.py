@@ -96,6 +96,7 @@ class GpuMountService:
         self.notify = Notifier(cfg, kube)
         self.quota = GpuQuota(cfg, kube)
         self._ns_seen: set = set()
+        self.unhealthy: set = set()   # GPU indices failing liveness/ECC (Worker.check_health)
         # Reservations that must not interleave on a node run one at a time:
         # * trim briefly holds every free GPU — a concurrent one would see a full node;
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
@@ -505,7 +506,8 @@ class GpuMountService:
         allocated = {normalize_device_id(d) for ids in st.ledger.values() for d in ids}
         allocated.update(normalize_device_id(d) for uid, ids in self.ph.device_ids.items()
                          if uid not in self.ph.tombstones for d in ids)
-        return [g for g in self.inv.gpus() if not allocated.intersection(g.ledger_keys())]
+        return [g for g in self.inv.gpus() if not allocated.intersection(g.ledger_keys())
+                and g.index not in self.unhealthy]
 
     def _preferred(self, n: int, st: PodGpuState, free: Optional[List[AmdGpu]] = None
                    ) -> List[str]:
@@ -650,7 +652,8 @@ class GpuMountService:
                         "owner_uid": ann.get("gpumounter.amd.com/owner-uid", ""),
                         "mode": ann.get("gpumounter.amd.com/mount-mode", ""),
                         "device_ids": list(ids)})
-        out = {"node": self.cfg.node_name, "gpus": [g.to_dict() for g in gpus],
+        out = {"node": self.cfg.node_name,
+               "gpus": [dict(g.to_dict(), healthy=g.index not in self.unhealthy) for g in gpus],
                "placeholders": phs,
                "topology": topology.describe(gpus, self.inv.links()),
                "ledger_api": self.ledger.api_version, "kfd_major": self.inv.kfd_major}

@@ -74,6 +74,10 @@ int gm_smi_link_matrix(gm_link_info_t* out, uint32_t cap);
 // Processes that currently hold a context on GPU `index`. *n is set to the total number even
 // if it exceeds cap (then return value is GM_SMI_MORE_DATA).
 int gm_smi_process_list(uint32_t index, gm_proc_info_t* out, uint32_t cap, uint32_t* n);
+// Accumulated ECC error counts of GPU `index` (amdsmi_get_gpu_total_ecc_count); an amdsmi status
+// such as AMDSMI_STATUS_NOT_SUPPORTED when the driver/firmware does not report them.
+int gm_smi_ecc(uint32_t index, uint64_t* correctable, uint64_t* uncorrectable,
+               uint64_t* deferred);
 const char* gm_smi_strerror(int status);
 
 #define GM_SMI_OK 0

@@ -35,6 +35,7 @@ struct MockGpu {
   uint32_t render = 128, card = 0, numa = 0, kfd_node = 0, partition = 0, cu = 256, hsa = 0,
            hip = 0, socket = 0;
   uint64_t hive = 0, xnode = 0, kfd_id = 0, gfx = 0x950, vram_mb = 294896;
+  uint64_t ecc_ce = 0, ecc_ue = 0;
   amdsmi_bdf_t bdfv{};
 };
 
@@ -129,6 +130,8 @@ bool load_config(const char* path) {
       g.hsa = (uint32_t)gv.num_or("hsa_id", i + 1);
       g.hip = (uint32_t)gv.num_or("hip_id", i);
       g.socket = (uint32_t)gv.num_or("socket", i);
+      g.ecc_ce = (uint64_t)gv.num_or("ecc_correctable", 0);
+      g.ecc_ue = (uint64_t)gv.num_or("ecc_uncorrectable", 0);
       g_gpus.push_back(g);
       ++i;
     }
@@ -439,6 +442,16 @@ amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle h, char*
   return AMDSMI_STATUS_SUCCESS;
 }
 
+amdsmi_status_t amdsmi_get_gpu_total_ecc_count(amdsmi_processor_handle h,
+                                               amdsmi_error_count_t* ec) {
+  MOCK_GPU(h, i);
+  if (!ec) return AMDSMI_STATUS_INVAL;
+  memset(ec, 0, sizeof(*ec));
+  ec->correctable_count = g_gpus[i].ecc_ce;
+  ec->uncorrectable_count = g_gpus[i].ecc_ue;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
 amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char** s) {
   switch (status) {
     case AMDSMI_STATUS_SUCCESS: *s = "AMDSMI_STATUS_SUCCESS: Call succeeded"; break;
@@ -456,6 +469,15 @@ amdsmi_status_t amdsmi_status_code_to_string(amdsmi_status_t status, const char*
 void gm_mock_set_procs_file(const char* path) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_procs_file = path ? path : "";
+}
+
+// Test hook: set a GPU's accumulated ECC counts (simulates a memory error showing up).
+int gm_mock_set_ecc(uint32_t index, uint64_t correctable, uint64_t uncorrectable) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (index >= g_gpus.size()) return -1;
+  g_gpus[index].ecc_ce = correctable;
+  g_gpus[index].ecc_ue = uncorrectable;
+  return 0;
 }
 
 // Test hook: number of amdsmi_init() calls since load (proves the shim does not re-init per query).

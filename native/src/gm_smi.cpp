@@ -49,6 +49,7 @@ struct Api {
   GM_SYM(amdsmi_get_gpu_vram_info);
   GM_SYM(amdsmi_get_gpu_compute_partition);
   GM_SYM(amdsmi_get_gpu_memory_partition);
+  GM_SYM(amdsmi_get_gpu_total_ecc_count);
 };
 
 Api g_api;
@@ -266,6 +267,7 @@ int gm_smi_open(const char* lib_path) {
   resolve(dl, g_api.amdsmi_get_gpu_vram_info, "amdsmi_get_gpu_vram_info");
   resolve(dl, g_api.amdsmi_get_gpu_compute_partition, "amdsmi_get_gpu_compute_partition");
   resolve(dl, g_api.amdsmi_get_gpu_memory_partition, "amdsmi_get_gpu_memory_partition");
+  resolve(dl, g_api.amdsmi_get_gpu_total_ecc_count, "amdsmi_get_gpu_total_ecc_count");
 
   amdsmi_status_t st = g_api.amdsmi_init(AMDSMI_INIT_AMD_GPUS);
   if (st != AMDSMI_STATUS_SUCCESS) {
@@ -366,6 +368,23 @@ int gm_smi_process_list(uint32_t index, gm_proc_info_t* out, uint32_t cap, uint3
     copy_str(out[i].name, sizeof(out[i].name), buf[i].name);
   }
   return got > cap ? GM_SMI_MORE_DATA : GM_SMI_OK;
+}
+
+int gm_smi_ecc(uint32_t index, uint64_t* correctable, uint64_t* uncorrectable,
+               uint64_t* deferred) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_open) return GM_SMI_ERR_NOT_OPEN;
+  if (index >= g_gpus.size()) return GM_SMI_ERR_RANGE;
+  *correctable = *uncorrectable = *deferred = 0;
+  if (!g_api.amdsmi_get_gpu_total_ecc_count) return AMDSMI_STATUS_NOT_SUPPORTED;
+  amdsmi_error_count_t ec;
+  memset(&ec, 0, sizeof(ec));
+  amdsmi_status_t st = g_api.amdsmi_get_gpu_total_ecc_count(g_gpus[index], &ec);
+  if (st != AMDSMI_STATUS_SUCCESS) return (int)st;
+  *correctable = ec.correctable_count;
+  *uncorrectable = ec.uncorrectable_count;
+  *deferred = ec.deferred_count;
+  return GM_SMI_OK;
 }
 
 const char* gm_smi_strerror(int status) {

@@ -153,3 +153,50 @@ def test_worker_exports_device_plugin_metrics():
         assert 'gm_device_plugin_rpcs_total{rpc="Allocate"} 2.0' in text
         assert "gm_device_plugin_healthy_gpus 8.0" in text
     run(body)
+
+
+def test_new_uncorrectable_ecc_error_takes_a_gpu_out_of_service():
+    """ecc_policy=new: a GPU whose uncorrectable ECC count rises is reported Unhealthy to the
+    kubelet (so no placeholder can get it), left out of placement, flagged in /status and in
+    gm_gpu_healthy; pre-existing errors at worker start do not count."""
+    import asyncio
+
+    from gpumounter_amd import _native
+    from gpumounter_amd.fakes.harness import LocalCluster
+
+    mock = _native.mock_smi()
+
+    async def main():
+        mock.gm_mock_set_ecc(3, 5, 2)            # errors on record before the worker starts
+        try:
+            async with LocalCluster(device_plugin=True,
+                                    worker_overrides={"health_period_s": 0}) as lc:
+                w = lc.nodes["node-0"].worker
+                await w.check_health()
+                assert w.service.unhealthy == set()          # policy "new": history is fine
+                mock.gm_mock_set_ecc(0, 0, 1)                # a fresh uncorrectable error
+                await w.check_health()
+                assert w.service.unhealthy == {0}
+                bad_bdf = next(g.bdf for g in lc.inventory.gpus() if g.index == 0)
+                text = w.metrics.render().decode()
+                assert f'gm_gpu_healthy{{gpu="{bad_bdf}"}} 0.0' in text
+
+                async def plugin_saw_it():
+                    return bool(lc.nodes["node-0"].node.unhealthy)
+                for _ in range(100):
+                    if await plugin_saw_it():
+                        break
+                    await asyncio.sleep(0.02)
+                assert await plugin_saw_it()
+                lc.tenant("t")
+                code, b = await lc.add("default", "t", 7)
+                assert code == 200, b
+                assert bad_bdf not in {d["bdf"] for d in b["devices"]}
+                lc.tenant("u")
+                assert (await lc.add("default", "u", 1))[0] == 500   # only the sick GPU is left
+                st = await w.service.node_status(False)
+                assert [g["healthy"] for g in st["gpus"] if g["index"] == 0] == [False]
+        finally:
+            mock.gm_mock_set_ecc(0, 0, 0)
+            mock.gm_mock_set_ecc(3, 0, 0)
+    asyncio.run(main())

@@ -42,6 +42,12 @@ def test_amdsmi_real_inventory(real_inventory):
     links = inv.links()
     assert links.n == len(gpus)
     assert all(links.types[i][i] == 0 for i in range(links.n))
+    # health: liveness + ECC (counts may be unsupported on some firmware → None)
+    assert all(inv.healthy().values())
+    for g in seen:
+        ecc = inv.ecc(g.index)
+        print(f"{g.bdf}: ECC (correctable, uncorrectable, deferred) = {ecc}")
+        assert ecc is None or all(v >= 0 for v in ecc)
 
 
 def test_amd_smi_tool_sees_the_same_gpus(real_inventory):
