@@ -24,6 +24,7 @@ _pf.message("AddGPURequest", [
     ("request_id", 6, "string", "opt"),
     ("idempotency_key", 7, "string", "opt"),    # client retry key: same key → same attach
     ("requested_by", 8, "string", "opt"),       # caller identity from the master's authn (audit)
+    ("lease_s", 9, "double", "opt"),            # > 0: detach automatically after this long
 ])
 _pf.message("Device", [
     ("uuid", 1, "string", "opt"),

@@ -61,6 +61,17 @@ def parse_go_int32(s: str) -> Optional[int]:
     return v
 
 
+def parse_lease(v: str) -> Optional[float]:
+    """``?lease=<seconds>``: "" → 0.0 (no lease), a positive finite number → it, else None."""
+    if v in ("", None):
+        return 0.0
+    try:
+        f = float(v)
+    except ValueError:
+        return None
+    return f if 0 < f < 10 * 365 * 86400 else None
+
+
 def _text(body: str, status: int = 200) -> web.Response:
     # Go's http.Error / fmt.Fprintf write text/plain with a trailing newline
     return web.Response(text=body if body.endswith("\n") else body + "\n", status=status,
@@ -265,7 +276,7 @@ class Master:
 
     # ------------------------------------------------------------------------ operations
     async def _add(self, ns: str, name: str, n: int, entire: bool, container: str = "",
-                   rid: str = "", key: str = "", user: str = ""):
+                   rid: str = "", key: str = "", user: str = "", lease_s: float = 0.0):
         """AddGPU through the pod's worker → (status, text, payload) as the reference maps it
         (reference main.go:103-116)."""
         t0 = time.perf_counter()
@@ -280,7 +291,7 @@ class Master:
                 resp = await stub(api.AddGPURequest(
                     pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
                     request_id=rid, container=container, idempotency_key=key,
-                    requested_by=user),
+                    requested_by=user, lease_s=lease_s),
                     timeout=self.cfg.rpc_timeout_s)
             except grpc.aio.AioRpcError as e:
                 if cached and e.code() == grpc.StatusCode.FAILED_PRECONDITION and \
@@ -364,9 +375,15 @@ class Master:
         if n <= 0:
             # the reference forwarded 0 and the worker divided by zero (SURVEY defect 6)
             return self._reply(request, route, 400, f"Invalid param gpuNum: {mi['gpuNum']}", {})
+        lease_s = parse_lease(request.query.get("lease", ""))
+        if lease_s is None:
+            return self._reply(request, route, 400,
+                               f"Invalid param lease: {request.query.get('lease')}"
+                               "(should be a positive number of seconds)", {})
         status, text, payload = await self._add(
             ns, name, n, entire, request.query.get("container", ""), rid,
-            request.headers.get("Idempotency-Key", "") or rid, request.get(USER_KEY, ""))
+            request.headers.get("Idempotency-Key", "") or rid, request.get(USER_KEY, ""),
+            lease_s)
         return self._reply(request, route, status, text, payload)
 
     async def remove_gpu(self, request: web.Request) -> web.Response:
@@ -429,9 +446,12 @@ class Master:
                     if n <= 0:
                         return 400, f"Invalid param gpuNum: {n}", {}
                     rid = log.new_request_id("add")
+                    lease_s = parse_lease(str(op.get("lease_s", "")))
+                    if lease_s is None:
+                        return 400, f"Invalid param lease_s: {op.get('lease_s')}", {}
                     return await self._add(ns, name, n, bool(op.get("entire", False)),
                                            op.get("container", ""), rid,
-                                           op.get("idempotency_key", "") or rid, user)
+                                           op.get("idempotency_key", "") or rid, user, lease_s)
                 if kind == "remove":
                     uuids = list(op["uuids"])
                     if not uuids:

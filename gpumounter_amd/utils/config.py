@@ -102,6 +102,10 @@ class Config:
     # the device plugin: new (errors since the worker started) | any (any on record) | off
     ecc_policy: str = "new"
     health_period_s: float = 5.0       # liveness + ECC re-check period
+    # leases (?lease=<s> on addgpu): detach at expiry; GPUs still in use are kept and retried
+    # unless lease_force, which signals their processes like force=1
+    lease_force: bool = False
+    lease_retry_s: float = 30.0
     # pool-namespace placeholders are invisible to the tenant namespace's ResourceQuota; enforce
     # requests.<resource_name> quotas for hot-mounted GPUs ourselves (cluster/quota.py) | off
     quota_mode: str = "enforce"

@@ -1,0 +1,128 @@
+"""GPU leases: hot-mounted GPUs that give themselves back.
+
+``GET /addgpu/...?lease=3600`` attaches GPUs for an hour. The expiry time is stored on the
+placeholder pods (annotation ``gpumounter.amd.com/lease-expires``, Unix seconds), so it survives
+worker restarts: a timer detaches on time while the worker runs, and the reconciler's sweep
+catches any lease that expired while it did not. Expiry is an ordinary RemoveGPU with the
+requester ``lease-expiry``. A GPU still in use is kept (``GPULeaseExpired`` warning Event,
+retried every ``lease_retry_s``) unless ``lease_force`` is set, in which case its processes get
+the same SIGTERM→SIGKILL treatment as ``force=1``. The reference has no notion of time-bounded
+mounts; its slave pods live until someone removes them (reference: pkg/server/gpu-mount/
+server.go:101-179).
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from typing import Dict, List, Optional, Tuple
+
+from gpumounter_amd.api import gpu_mount as api
+from gpumounter_amd.models import pod as podu
+from gpumounter_amd.models.types import LABEL_OWNER_NS
+from gpumounter_amd.utils import log
+
+_log = log.get("worker.lease")
+ANN_LEASE = "gpumounter.amd.com/lease-expires"
+
+
+def expires_of(ph: dict) -> Optional[float]:
+    v = (ph["metadata"].get("annotations") or {}).get(ANN_LEASE)
+    try:
+        return float(v) if v else None
+    except ValueError:
+        return None
+
+
+class LeaseKeeper:
+    def __init__(self, service) -> None:
+        self.svc = service
+        self._timers: Dict[str, asyncio.TimerHandle] = {}     # placeholder uid → timer
+        self._retry_after: Dict[Tuple[str, str], float] = {}   # owner → not before
+        self.expired = 0
+
+    # ------------------------------------------------------------------------ grant
+    async def grant(self, pod: dict, placeholders, lease_s: float) -> float:
+        """Stamp the expiry on the attach's placeholders and arm a timer. Returns the expiry."""
+        expires = time.time() + lease_s
+        patch = {"metadata": {"annotations": {ANN_LEASE: f"{expires:.3f}"}}}
+        await asyncio.gather(*[self.svc.kube.patch_pod(p.namespace, p.name, patch)
+                               for p in placeholders])
+        for p in placeholders:
+            self._arm(p.uid, podu.ns_of(pod), podu.name_of(pod), expires)
+        return expires
+
+    def _arm(self, uid: str, ns: str, name: str, expires: float) -> None:
+        if not uid or uid in self._timers:
+            return
+        loop = asyncio.get_running_loop()
+        self._timers[uid] = loop.call_later(
+            max(0.0, expires - time.time()),
+            lambda: asyncio.ensure_future(self.expire_owner(ns, name)))
+
+    def stop(self) -> None:
+        for t in self._timers.values():
+            t.cancel()
+        self._timers.clear()
+
+    # ------------------------------------------------------------------------ expiry
+    async def sweep(self) -> int:
+        """Expire every lease that is due (placeholder annotations: survives worker restarts)
+        and re-arm timers for the rest. Returns how many owners were handled."""
+        now = time.time()
+        due: Dict[Tuple[str, str], List[dict]] = {}
+        for p in self.svc.ph.live():
+            exp = expires_of(p)
+            if exp is None:
+                continue
+            md = p["metadata"]
+            ns = (md.get("labels") or {}).get(LABEL_OWNER_NS, "")
+            name = (md.get("annotations") or {}).get("gpumounter.amd.com/owner-name", "")
+            if not (ns and name):
+                continue
+            if exp <= now:
+                due.setdefault((ns, name), []).append(p)
+            else:
+                self._arm(md.get("uid", ""), ns, name, exp)
+        for ns, name in due:
+            await self.expire_owner(ns, name)
+        return len(due)
+
+    async def expire_owner(self, ns: str, name: str) -> None:
+        svc = self.svc
+        if time.time() < self._retry_after.get((ns, name), 0):
+            return
+        pod = await svc.get_pod(ns, name, fresh=True)
+        if pod is None:
+            return                          # the owner-gone GC releases its placeholders
+        now = time.time()
+        st = await svc.pod_state(pod, fresh=True)
+        uuids = []
+        for ph in st.placeholders:
+            raw = next((p for p in svc.ph.owned_by(pod)
+                        if p["metadata"]["name"] == ph.name), None)
+            exp = expires_of(raw) if raw is not None else None
+            if exp is not None and exp <= now + 0.001:
+                uuids += [g.uuid for g in st.by_placeholder[(ph.namespace, ph.name)]]
+                self._timers.pop(ph.uid, None)
+        if not uuids:
+            return
+        force = bool(svc.cfg.lease_force)
+        resp = await svc.remove_gpu(api.RemoveGPURequest(
+            pod_name=name, namespace=ns, uuids=uuids, force=force, requested_by="lease-expiry"))
+        if resp.remove_gpu_result == api.REMOVE_SUCCESS:
+            self.expired += 1
+            self._retry_after.pop((ns, name), None)
+            svc.notify.event(pod, "GPULeaseExpired",
+                             f"lease over: {len(uuids)} GPU(s) detached"
+                             + (f", processes {list(resp.killed_pids)} signalled"
+                                if resp.killed_pids else ""))
+            log.kv(_log, 20, "lease expired", pod=f"{ns}/{name}", gpus=len(uuids))
+            return
+        retry = svc.cfg.lease_retry_s
+        self._retry_after[(ns, name)] = time.time() + retry
+        svc.notify.event(pod, "GPULeaseExpired",
+                         f"lease over but the GPUs are still in use "
+                         f"({api.RemoveGPUResponse.RemoveGPUResult.Name(resp.remove_gpu_result)}"
+                         f"); retrying every {retry:g} s (lease_force=false)", warning=True)
+        asyncio.get_running_loop().call_later(
+            retry, lambda: asyncio.ensure_future(self.expire_owner(ns, name)))

@@ -144,6 +144,10 @@ class Reconciler:
     async def run_once(self) -> ReconcileReport:
         svc = self.svc
         rep = ReconcileReport()
+        try:
+            await svc.lease.sweep()            # leases that expired while nobody watched
+        except Exception as e:  # noqa: BLE001
+            rep.errors.append(f"lease sweep: {e}")
         m = svc.metrics
         placeholders = svc.ph.live()
         by_owner: Dict[tuple, List[dict]] = {}

@@ -184,6 +184,7 @@ class Worker:
         if self.cfg.metrics_period_s > 0:
             self._collector = asyncio.ensure_future(self._collect_loop())
         await self.check_health()          # ECC baseline before the first attach
+        await self.service.lease.sweep()   # re-arm (or expire) leases from before a restart
         if self.cfg.health_period_s > 0:
             self._health_task = asyncio.ensure_future(self._health_loop())
         if self.cfg.gc_tune:
@@ -276,6 +277,7 @@ class Worker:
             self._health_task.cancel()
         await self.pool.stop()
         await self.reconciler.stop()
+        self.service.lease.stop()
         await self.service.notify.stop()
         if isinstance(self.backend, systemd.SystemdPersistingBackend):
             self.backend.sync.stop()

@@ -45,6 +45,7 @@ from gpumounter_amd.node.ledger import LedgerClient, LedgerError
 from gpumounter_amd.utils import log, trace
 from gpumounter_amd.utils.faults import FaultInjector, InjectedFault
 from gpumounter_amd.utils.metrics import Metrics
+from gpumounter_amd.worker.lease import LeaseKeeper
 from gpumounter_amd.worker.notify import Notifier
 
 _log = log.get("worker.service")
@@ -97,6 +98,7 @@ class GpuMountService:
         self.quota = GpuQuota(cfg, kube)
         self._ns_seen: set = set()
         self.unhealthy: set = set()   # GPU indices failing liveness/ECC (Worker.check_health)
+        self.lease = LeaseKeeper(self)
         # Reservations that must not interleave on a node run one at a time:
         # * trim briefly holds every free GPU — a concurrent one would see a full node;
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
@@ -335,14 +337,24 @@ class GpuMountService:
                     return api.AddGPUResponse(add_gpu_result=api.ADD_POD_NOT_FOUND,
                                               message=f"pod went away during the attach: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
+            msg = "Add GPU Success"
+            if req.lease_s > 0:
+                try:
+                    expires = await self.lease.grant(pod, res.placeholders, req.lease_s)
+                except Exception as e:  # noqa: BLE001 - a lease must not be silently dropped
+                    _log.error("lease on %s/%s not recorded: %s", req.namespace, req.pod_name, e)
+                    await self._release(res.placeholders)
+                    await self._rollback(pod, "attach")
+                    raise RpcError(grpc.StatusCode.INTERNAL,
+                                   f"{ERR_INTERNAL}: lease not recorded: {e}") from e
+                msg += time.strftime(" (lease until %Y-%m-%dT%H:%M:%SZ)", time.gmtime(expires))
             log.kv(_log, 20, "attached", pod=f"{req.namespace}/{req.pod_name}",
-                   gpus=[g.bdf for g in new], by=req.requested_by)
+                   gpus=[g.bdf for g in new], by=req.requested_by, lease_s=req.lease_s)
             self.notify.attached(pod, new, list(st.hot) + new,
                                  "entire" if req.is_entire_mount else "single",
                                  by=req.requested_by)
             return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS,
-                                      devices=self._devices(new, owner),
-                                      message="Add GPU Success")
+                                      devices=self._devices(new, owner), message=msg)
 
     @contextlib.asynccontextmanager
     async def _quota_guard(self, ns: str, n: int):

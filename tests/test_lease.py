@@ -1,0 +1,119 @@
+"""GPU leases (gpumounter_amd/worker/lease.py): ``?lease=<s>`` attaches that detach themselves."""
+import asyncio
+import subprocess
+
+from gpumounter_amd import _native
+from gpumounter_amd.fakes.harness import LocalCluster
+from gpumounter_amd.worker.lease import ANN_LEASE
+
+
+def run(coro_fn, **kw):
+    async def main():
+        async with LocalCluster(**kw) as lc:
+            return await coro_fn(lc)
+    return asyncio.run(main())
+
+
+async def lease_add(lc, ns, pod, n, lease, entire=False):
+    url = (f"{lc.master_url}/addgpu/namespace/{ns}/pod/{pod}/gpu/{n}/isEntireMount/"
+           f"{'true' if entire else 'false'}?lease={lease}")
+    async with lc.session.get(url, headers={"Accept": "application/json"}) as r:
+        return r.status, await r.json()
+
+
+async def until(pred, timeout=5.0):
+    end = asyncio.get_running_loop().time() + timeout
+    while asyncio.get_running_loop().time() < end:
+        if await pred():
+            return True
+        await asyncio.sleep(0.02)
+    return await pred()
+
+
+def test_lease_detaches_on_time_and_only_the_leased_gpus():
+    async def body(lc):
+        lc.tenant("t")
+        code, keep = await lc.add("default", "t", 1)                  # no lease
+        assert code == 200
+        code, b = await lease_add(lc, "default", "t", 2, 0.3)
+        assert code == 200 and "(lease until " in b["detail"], b
+        leased = {p["metadata"]["name"] for p in lc.cluster.placeholders()
+                  if (p["metadata"].get("annotations") or {}).get(ANN_LEASE)}
+        assert len(leased) == 2
+        svc = lc.nodes["node-0"].worker.service
+
+        async def back_to_one():
+            st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+            return [g.uuid for g in st.hot] == [keep["devices"][0]["uuid"]]
+        assert await until(back_to_one)
+        assert await lc.audit("default", "t") == []
+        await svc.notify.drain()
+        evs = [e for e in lc.cluster.events_for("default", "t")
+               if e["reason"] == "GPULeaseExpired"]
+        assert evs and "2 GPU(s) detached" in evs[0]["message"] and evs[0]["type"] == "Normal"
+        assert svc.lease.expired == 1
+    run(body)
+
+
+def test_bad_lease_values_are_rejected():
+    async def body(lc):
+        lc.tenant("t")
+        for v in ("-1", "0", "abc", "inf"):
+            code, b = await lease_add(lc, "default", "t", 1, v)
+            assert code == 400 and "Invalid param lease" in b["message"], (v, b)
+    run(body)
+
+
+def test_expired_lease_on_a_busy_gpu_is_kept_unless_forced(tmp_path):
+    sleeper = subprocess.Popen(["sleep", "60"])
+    procs = tmp_path / "procs"
+    _native.mock_smi().gm_mock_set_procs_file(str(procs).encode())
+    try:
+        async def body(lc):
+            lc.tenant("busy", pids={"main": [sleeper.pid]})
+            code, b = await lease_add(lc, "default", "busy", 1, 0.2)
+            assert code == 200
+            procs.write_text(f"{b['devices'][0]['index']} {sleeper.pid} 4096 python\n")
+            svc = lc.nodes["node-0"].worker.service
+
+            async def warned():
+                await svc.notify.drain()
+                return any(e["reason"] == "GPULeaseExpired" and e["type"] == "Warning"
+                           for e in lc.cluster.events_for("default", "busy"))
+            assert await until(warned)
+            st = await svc.pod_state(lc.cluster.get("default", "busy"), fresh=True)
+            assert len(st.hot) == 1                       # still mounted: a process uses it
+            svc.cfg.lease_force = True                    # operator flips the policy
+            svc.lease._retry_after.clear()                # noqa: SLF001 - retry now
+            await svc.lease.sweep()
+
+            async def gone():
+                st = await svc.pod_state(lc.cluster.get("default", "busy"), fresh=True)
+                return not st.hot
+            assert await until(gone)
+            assert await lc.audit("default", "busy") == []
+        run(body, worker_overrides={"busy_detection": "both", "lease_retry_s": 0.1})
+        sleeper.wait(timeout=10)
+        assert sleeper.returncode == -15                  # SIGTERM like force=1
+    finally:
+        _native.mock_smi().gm_mock_set_procs_file(b"")
+        if sleeper.poll() is None:
+            sleeper.kill()
+
+
+def test_lease_survives_a_worker_restart():
+    async def body(lc):
+        lc.tenant("t")
+        code, _ = await lease_add(lc, "default", "t", 1, 0.4)
+        assert code == 200
+        await lc.stop_worker("node-0")                   # timers die with the process
+        await asyncio.sleep(0.6)                         # the lease expires meanwhile
+        await lc.start_worker("node-0")                  # start-up sweep finds it
+        svc = lc.nodes["node-0"].worker.service
+
+        async def gone():
+            st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+            return not st.hot
+        assert await until(gone)
+        assert await lc.audit("default", "t") == []
+    run(body)
