@@ -151,8 +151,11 @@ async def _http(method: str, url: str, data=None) -> int:
 def cmd_add(args) -> int:
     url = (f"{args.master.rstrip('/')}/addgpu/namespace/{args.ns}/pod/{args.pod}/gpu/{args.n}/"
            f"isEntireMount/{'true' if args.entire else 'false'}")
-    if args.container:
-        url += f"?container={args.container}"
+    from urllib.parse import urlencode
+
+    q = {k: v for k, v in (("container", args.container), ("lease", args.lease)) if v}
+    if q:
+        url += "?" + urlencode(q)
     return asyncio.run(_http("GET", url))
 
 
@@ -274,6 +277,7 @@ def build_parser() -> argparse.ArgumentParser:
             p.add_argument("-n", type=int, required=True)
             p.add_argument("--entire", action="store_true")
             p.add_argument("--container", default="")
+            p.add_argument("--lease", default="", help="seconds until automatic detach")
         if name == "remove":
             p.add_argument("--uuid", action="append", required=True)
             p.add_argument("--force", action="store_true")
