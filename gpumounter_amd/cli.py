@@ -5,10 +5,11 @@
     python -m gpumounter_amd inventory [--amdsmi mock]          # amdsmi view of this node
     python -m gpumounter_amd topology  [--amdsmi mock] [-n 4]   # xGMI/NUMA placement preview
     python -m gpumounter_amd probe     [--bdf 0000:05:00.0] [--full]   # gfx950 validation kernels
-    python -m gpumounter_amd add    --master URL --ns NS --pod P -n 2 [--entire]
+    python -m gpumounter_amd add    --master URL --ns NS --pod P -n 2 [--entire] [--lease 3600]
     python -m gpumounter_amd remove --master URL --ns NS --pod P --uuid U [--uuid U2] [--force]
     python -m gpumounter_amd status --master URL --node NODE
     python -m gpumounter_amd bpf-dump --allow 226:128 --allow 511:0   # generated device program
+    python -m gpumounter_amd doctor  [--json] [--skip-cluster]       # node preflight
 
 The reference ships only the two daemons and documents curl calls (QuickStart.md:41-92); the
 ``add``/``remove`` commands speak exactly those HTTP routes.
@@ -149,10 +150,10 @@ async def _http(method: str, url: str, data=None) -> int:
 
 
 def cmd_add(args) -> int:
-    url = (f"{args.master.rstrip('/')}/addgpu/namespace/{args.ns}/pod/{args.pod}/gpu/{args.n}/"
-           f"isEntireMount/{'true' if args.entire else 'false'}")
     from urllib.parse import urlencode
 
+    url = (f"{args.master.rstrip('/')}/addgpu/namespace/{args.ns}/pod/{args.pod}/gpu/{args.n}/"
+           f"isEntireMount/{'true' if args.entire else 'false'}")
     q = {k: v for k, v in (("container", args.container), ("lease", args.lease)) if v}
     if q:
         url += "?" + urlencode(q)
