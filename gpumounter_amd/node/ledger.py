@@ -48,13 +48,35 @@ class LedgerClient:
         self.calls = 0
         self._get_ok: Optional[bool] = None   # v1 Get served? (feature-gated in kubelets)
 
+    # a restarted kubelet recreates its socket within ~1 s: reconnect fast, not after gRPC's
+    # default 1 s → 120 s backoff
+    _CHANNEL_OPTS = [("grpc.initial_reconnect_backoff_ms", 50),
+                     ("grpc.min_reconnect_backoff_ms", 50),
+                     ("grpc.max_reconnect_backoff_ms", 1000)]
+
     def _channel(self) -> grpc.aio.Channel:
         loop = asyncio.get_running_loop()
         if self._chan is None or self._chan_loop is not loop:
-            self._chan = grpc.aio.insecure_channel(f"unix://{self.socket_path}")
+            self._chan = grpc.aio.insecure_channel(f"unix://{self.socket_path}",
+                                                   options=self._CHANNEL_OPTS)
             self._chan_loop = loop
             self._stubs = {}
         return self._chan
+
+    async def _call(self, path: str, req_cls, resp_cls, req):
+        """One unary call; on UNAVAILABLE (kubelet restarting: socket gone or recreated) the
+        channel is rebuilt and the call retried once, waiting up to 2 s for the new socket."""
+        try:
+            return await self._stub(path, req_cls, resp_cls)(req, timeout=self.timeout_s)
+        except grpc.aio.AioRpcError as e:
+            if e.code() != grpc.StatusCode.UNAVAILABLE:
+                raise
+        old, self._chan = self._chan, None
+        if old is not None:
+            await old.close()
+        _log.info("PodResources socket %s unavailable; reconnecting", self.socket_path)
+        return await self._stub(path, req_cls, resp_cls)(
+            req, timeout=min(self.timeout_s, 2.0), wait_for_ready=True)
 
     def _stub(self, path: str, req_cls, resp_cls):
         ch = self._channel()
@@ -71,9 +93,9 @@ class LedgerClient:
         self._chan = None
 
     async def _call_list(self, api) -> object:
-        stub = self._stub(api.LIST, api.ListPodResourcesRequest, api.ListPodResourcesResponse)
         self.calls += 1
-        return await stub(api.ListPodResourcesRequest(), timeout=self.timeout_s)
+        return await self._call(api.LIST, api.ListPodResourcesRequest,
+                                api.ListPodResourcesResponse, api.ListPodResourcesRequest())
 
     async def _resolve_api(self):
         if self._api is not None:
@@ -118,10 +140,10 @@ class LedgerClient:
         api = await self._resolve_api()
         if not api.has_allocatable:
             return None
-        stub = self._stub(api.ALLOCATABLE, api.AllocatableResourcesRequest,
-                          api.AllocatableResourcesResponse)
         try:
-            resp = await stub(api.AllocatableResourcesRequest(), timeout=self.timeout_s)
+            resp = await self._call(api.ALLOCATABLE, api.AllocatableResourcesRequest,
+                                    api.AllocatableResourcesResponse,
+                                    api.AllocatableResourcesRequest())
         except grpc.aio.AioRpcError as e:
             if e.code() == grpc.StatusCode.UNIMPLEMENTED:
                 return None
@@ -142,11 +164,12 @@ class LedgerClient:
         if api is not V1:
             self._get_ok = False
             return None
-        stub = self._stub(api.GET, api.GetPodResourcesRequest, api.GetPodResourcesResponse)
         self.calls += 1
         try:
-            resp = await stub(api.GetPodResourcesRequest(pod_name=pod, pod_namespace=namespace),
-                              timeout=self.timeout_s)
+            resp = await self._call(api.GET, api.GetPodResourcesRequest,
+                                    api.GetPodResourcesResponse,
+                                    api.GetPodResourcesRequest(pod_name=pod,
+                                                               pod_namespace=namespace))
         except grpc.aio.AioRpcError as e:
             if e.code() == grpc.StatusCode.NOT_FOUND:
                 return []

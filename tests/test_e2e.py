@@ -736,3 +736,22 @@ def test_remove_after_tenant_deleted_is_pod_not_found_and_releases():
             return not live and not node_of(lc).allocated
         assert await _until(clean)
     run(body)
+
+
+def test_kubelet_restart_is_survived_without_waiting_for_grpc_backoff():
+    """A kubelet restart recreates the PodResources socket; the ledger client rebuilds its
+    channel on UNAVAILABLE, so the first attach after the restart already succeeds."""
+    from gpumounter_amd.fakes.kubelet import FakeKubelet
+
+    async def body(lc):
+        lc.tenant("t")
+        assert (await lc.add("default", "t", 1))[0] == 200
+        h = lc.nodes["node-0"]
+        await h.kubelet.stop()
+        assert (await lc.add("default", "t", 1))[0] == 500        # kubelet down: refused
+        h.kubelet = FakeKubelet(h.node, h.kubelet.socket_path)
+        await h.kubelet.start()
+        code, b = await lc.add("default", "t", 1)
+        assert code == 200, b
+        assert await lc.audit("default", "t") == []
+    run(body)
