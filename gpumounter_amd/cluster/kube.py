@@ -129,8 +129,33 @@ class KubeClient:
             await self._session.close()
         self._session = None
 
+    # transient apiserver trouble (a control-plane node restarting, an overloaded apiserver
+    # shedding load with 429/5xx): retried with backoff for requests that are safe to repeat
+    RETRY_STATUS = (429, 500, 502, 503, 504)
+    RETRY_DELAYS = (0.01, 0.05, 0.2, 0.5)
+
     async def _req(self, method: str, path: str, params: Optional[dict] = None,
-                   body: Any = None, content_type: str = "application/json") -> Any:
+                   body: Any = None, content_type: str = "application/json",
+                   idempotent: Optional[bool] = None) -> Any:
+        """One API request. GET/PATCH/DELETE (and POSTs the caller marks ``idempotent``) are
+        retried on 429/5xx and transport errors; a transport failure surfaces as
+        ``ApiError(503)`` so callers handle one exception type."""
+        retry = idempotent if idempotent is not None else method in ("GET", "PATCH", "DELETE")
+        delays = self.RETRY_DELAYS if retry else ()
+        for attempt in range(len(delays) + 1):
+            try:
+                return await self._req_once(method, path, params, body, content_type)
+            except ApiError as e:
+                if e.status not in self.RETRY_STATUS or attempt == len(delays):
+                    raise
+            except (aiohttp.ClientError, asyncio.TimeoutError, OSError) as e:
+                if attempt == len(delays):
+                    raise ApiError(503, f"apiserver unreachable: {e!r}") from e
+            await asyncio.sleep(delays[attempt])
+        raise AssertionError("unreachable")
+
+    async def _req_once(self, method: str, path: str, params: Optional[dict], body: Any,
+                        content_type: str) -> Any:
         sess = self._sess()
         data = None
         headers = {}
@@ -173,7 +198,20 @@ class KubeClient:
         return out.get("items", []), out.get("metadata", {}).get("resourceVersion", "")
 
     async def create_pod(self, ns: str, pod: dict) -> dict:
-        return await self._req("POST", self._pods_path(ns), body=pod)
+        """Create; retried on transient errors when the name is explicit (a retry that finds
+        the pod already created by the lost first attempt returns that pod)."""
+        name = (pod.get("metadata") or {}).get("name", "")
+        try:
+            return await self._req("POST", self._pods_path(ns), body=pod, idempotent=bool(name))
+        except Conflict:
+            if not name:
+                raise
+            cur = await self.get_pod(ns, name)
+            mine = (pod.get("metadata") or {}).get("annotations") or {}
+            theirs = (cur.get("metadata") or {}).get("annotations") or {}
+            if mine and all(theirs.get(k) == v for k, v in mine.items()):
+                return cur                  # our own create went through before the error
+            raise
 
     async def delete_pod(self, ns: str, name: str, grace_period_s: Optional[int] = None,
                          uid: str = "") -> Optional[dict]:

@@ -149,6 +149,7 @@ class FakeCluster:
         self._unschedulable: set = set()
         self._tasks: set = set()
         self._lock = threading.RLock()
+        self._faults: List[Tuple[str, int, bool, str]] = []
 
     # ------------------------------------------------------------------------ nodes
     def add_node(self, node: FakeNode) -> FakeNode:
@@ -487,7 +488,7 @@ class FakeCluster:
 
     # ------------------------------------------------------------------------ HTTP
     def app(self) -> web.Application:
-        app = web.Application(client_max_size=8 << 20)
+        app = web.Application(client_max_size=8 << 20, middlewares=[self._fault_mw])
         r = app.router
         r.add_get("/api/v1/pods", self._h_list)
         r.add_get("/api/v1/namespaces/{ns}/pods", self._h_list)
@@ -506,6 +507,26 @@ class FakeCluster:
 
     async def _h_healthz(self, req: web.Request) -> web.Response:
         return web.Response(text="ok")
+
+    def fail_next(self, method: str, status: int = 503, count: int = 1,
+                  after: bool = False, path: str = "/pods") -> None:
+        """Fault injection: the next ``count`` requests with ``method`` whose path contains
+        ``path`` answer ``status``. ``after=True`` performs the request first and loses the
+        response (a dropped reply)."""
+        self._faults.extend([(method, status, after, path)] * count)
+
+    @web.middleware
+    async def _fault_mw(self, request: web.Request, handler):
+        """Serves the failures queued by :meth:`fail_next` (watch streams are never hit)."""
+        if self._faults and not request.query.get("watch"):
+            for i, (m, st, after, path) in enumerate(self._faults):
+                if m == request.method and path in request.path:
+                    del self._faults[i]
+                    if after:
+                        await handler(request)      # it happened; the reply gets lost
+                    return web.json_response({"kind": "Status", "code": st,
+                                              "message": "injected failure"}, status=st)
+        return await handler(request)
 
     async def _pre(self, req: web.Request) -> None:
         self.request_count += 1

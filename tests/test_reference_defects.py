@@ -96,3 +96,25 @@ def test_defect14_log_file_is_appended_and_rotated_not_truncated(tmp_path):
     text = open(path).read()
     assert "first start" in text and "second start" in text
     log.setup("WARNING", json_format=False)
+
+
+def test_transient_apiserver_errors_are_retried_and_lost_creates_recovered():
+    """An apiserver shedding load (503) or a create whose reply was lost must not fail or
+    duplicate an attach: reads/deletes/patches and named creates are retried; a retried create
+    that meets its own first attempt (409) adopts it."""
+    async def body(lc):
+        lc.tenant("t")
+        c = lc.cluster
+        c.fail_next("POST", 503, count=2)                  # placeholder create shed twice
+        code, b = await lc.add("default", "t", 1)
+        assert code == 200, b
+        c.fail_next("POST", 504, after=True)               # created, but the reply is lost
+        code, b2 = await lc.add("default", "t", 1)
+        assert code == 200, b2
+        live = [p for p in c.placeholders() if not p["metadata"].get("deletionTimestamp")]
+        assert len(live) == 2                              # no duplicate from the retry
+        c.fail_next("DELETE", 503)
+        code, _ = await lc.remove("default", "t", [b["devices"][0]["uuid"]])
+        assert code == 200
+        assert await lc.audit("default", "t") == []
+    run(body)
