@@ -222,6 +222,12 @@ def probe() -> C.CDLL:
         lib.gm_probe_mfma_peak.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double)]
         lib.gm_probe_gemm_bf16.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
                                            C.c_int, C.c_void_p]
+        lib.gm_probe_gemm_nt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                         C.c_int, C.c_void_p]
+        lib.gm_probe_gemm_nt_variant.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                 C.c_int, C.c_int, C.c_int, C.c_void_p]
+        lib.gm_probe_gemm_nt_tflops.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                C.POINTER(C.c_double)]
         lib.gm_probe_gemm_check.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int,
                                             C.POINTER(C.c_double), C.POINTER(C.c_double)]
         lib.gm_probe_p2p.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_int),

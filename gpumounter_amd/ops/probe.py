@@ -108,6 +108,43 @@ def gemm_bf16(a, b, out=None, stream=None):
     return out
 
 
+def gemm_nt(a, bt, out=None, stream=None, variant: Optional[int] = None):
+    """C(bf16) = A @ Btᵀ for bf16 torch tensors on a HIP device: the 256²-tile
+    global_load_lds MFMA GEMM (gm_probe_gemm_nt). Shapes: A [M,K], Bt [N,K] contiguous
+    (both K-major); M, N multiples of 256 and K a multiple of 64. ``variant`` picks a schedule
+    (0: per-k-step fragment reads, 1: whole K-tile of reads up front; default: the faster, 1)."""
+    import torch
+
+    if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
+        raise ProbeError("gemm_nt expects bf16 inputs")
+    if not (a.is_contiguous() and bt.is_contiguous()):
+        raise ProbeError("gemm_nt expects contiguous inputs")
+    m, k = a.shape
+    n, k2 = bt.shape
+    if k != k2 or m % 256 or n % 256 or k % 64:
+        raise ProbeError(f"unsupported shape A{tuple(a.shape)} Bt{tuple(bt.shape)}")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    elif out.shape != (m, n) or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        raise ProbeError("gemm_nt: out must be a contiguous bf16 [M,N] tensor")
+    s = stream if stream is not None else torch.cuda.current_stream(a.device)
+    with torch.cuda.device(a.device):
+        lib = _native.probe()
+        ptrs = (a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k, C.c_void_p(s.cuda_stream))
+        rc = (lib.gm_probe_gemm_nt(*ptrs) if variant is None
+              else lib.gm_probe_gemm_nt_variant(variant, *ptrs))
+        _check(rc, "gemm_nt")
+    return out
+
+
+def gemm_tflops(dev: int, m: int = 8192, n: int = 8192, k: int = 8192, iters: int = 10) -> float:
+    """Dense bf16 TF/s of the 256²-tile GEMM on uniform [-1,1) operands (burn-in load)."""
+    t = C.c_double(0)
+    _check(_native.probe().gm_probe_gemm_nt_tflops(dev, m, n, k, iters, C.byref(t)),
+           "gemm tflops")
+    return t.value
+
+
 def p2p(dev_a: int, dev_b: int, nbytes: int = 256 << 20, iters: int = 10) -> Dict:
     can, g = C.c_int(0), C.c_double(0)
     _check(_native.probe().gm_probe_p2p(dev_a, dev_b, nbytes, iters, C.byref(can), C.byref(g)),
@@ -125,6 +162,7 @@ class VerifyResult:
     hbm_read_gbps: Optional[float] = None
     mfma_tflops: Optional[float] = None
     gemm_max_abs_err: Optional[float] = None
+    gemm_tflops: Optional[float] = None
 
     def to_dict(self) -> Dict:
         return asdict(self)
@@ -144,5 +182,6 @@ def verify(bdfs: List[str], full: bool = False) -> List[VerifyResult]:
             r.hbm_read_gbps = hbm_read_gbps(dev)
             r.mfma_tflops = mfma_tflops(dev)
             r.gemm_max_abs_err = gemm_check(dev)["max_abs_err"]
+            r.gemm_tflops = gemm_tflops(dev, 4096, 4096, 4096, 10)
         out.append(r)
     return out

@@ -294,6 +294,163 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(const __bf16* __restrict__ A,
   }
 }
 
+// ------------------------------------------------------------------ MFMA bf16 GEMM, 256² tile
+// Throughput form of the burn-in GEMM: C[M,N] (bf16) = A[M,K] · Bt[N,K]ᵀ, both operands K-major
+// (the layout global_load_lds can stage without a transpose). Design (cdna_hip_programming.md §5):
+//   * 256×256 output tile, BK=64, 512 threads = 8 waves as 2(M)×4(N); each wave owns 128×64 as
+//     8×4 v_mfma_f32_16x16x32_bf16 accumulators (128 VGPRs), ~1 block per CU;
+//   * operands go HBM→LDS with global_load_lds_dwordx4 (no VGPR round trip), two LDS stages of
+//     64 KiB, the next stage's DMA issued before the current stage's MFMAs;
+//   * LDS image lane-linear (one 1 KiB wave instruction = 8 rows × 128 B); bank conflicts of the
+//     16-row ds_read_b128 fragment reads are removed by an XOR swizzle of the 16-B chunk index
+//     with (row>>1)&7, applied to the per-lane GLOBAL source address and to the LDS read address;
+//   * blockIdx remapped bijectively so each XCD runs a contiguous range of tiles, grouped 8 tile
+//     rows deep, so concurrently running blocks of one XCD share A/B panels in that XCD's L2.
+namespace g256 {
+constexpr int TM = 256, TN = 256, TK = 64, kThreads = 512, kGroupM = 8;
+constexpr int kTileBytes = TM * TK * 2;       // 32 KiB: one operand, one stage
+constexpr int kStageBytes = 2 * kTileBytes;   // A + Bt
+constexpr int kLdsBytes = 2 * kStageBytes;    // two stages: 128 KiB of the 160 KiB LDS
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+}  // namespace g256
+constexpr int kGemmNtDefault = 1;  // profiles/r1_gemm: V1 ≥ V0 at 4096³, +2.6 % at 8192³
+
+// V = 0: per 32-deep k-step, 12 fragment reads → wait → 32 MFMAs.
+// V = 1: all 24 fragment reads of the 64-deep K-tile issued up front, so the second k-step's
+//        reads overlap the first step's MFMAs (+48 VGPRs).
+template <int V>
+__global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A,
+                                                    const __bf16* __restrict__ Bt,
+                                                    __bf16* __restrict__ C, int M, int N, int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // XCD-aware, bijective for any grid size; then GROUP_M-deep raster over the tile grid.
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int ntm = M / TM, ntn = N / TN;
+  const int per_group = kGroupM * ntn;
+  const int first_m = (wgid / per_group) * kGroupM;
+  const int gsize = min(ntm - first_m, kGroupM);
+  const int tm = first_m + (wgid % per_group) % gsize;
+  const int tn = (wgid % per_group) / gsize;
+
+  // Staging: wave w moves 1 KiB chunks c = w + 8i (i = 0..3) of each operand's 256×64 tile.
+  // Lane l writes LDS byte c*1024 + l*16 = row 8c + (l>>3), slot l&7, which holds logical
+  // 16-B chunk (l&7) ^ ((row>>1)&7). (row>>1)&7 is the same for all i (rows differ by 64).
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
+  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
+  const size_t row64 = (size_t)64 * K;
+
+  auto stage = [&](int buf, int k0) {
+    char* base = lds + buf * kStageBytes + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row64 + k0),
+                                       (lds_void*)(base + i * 8192), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row64 + k0),
+                                       (lds_void*)(base + kTileBytes + i * 8192), 16, 0, 0);
+    }
+  };
+
+  // Fragment reads: lane l reads row (l&15) of a 16-row block at logical chunk 4kk + (l>>4).
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);  // kk = 0; kk = 1: ^ 64
+  const int a_off = wm * 128 * 128 + foff0;
+  const int b_off = kTileBytes + wn * 64 * 128 + foff0;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) stage(cur ^ 1, (t + 1) * TK);
+    const char* sb = lds + cur * kStageBytes;
+    if constexpr (V == 0) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[8], bfr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 16 * 128) ^ (kk << 6)));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 16 * 128) ^ (kk << 6)));
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    } else {
+      bf16x8 af[2][8], bfr[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[kk][j] =
+              *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 16 * 128) ^ (kk << 6)));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          af[kk][i] =
+              *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 16 * 128) ^ (kk << 6)));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j],
+                                                                acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // Epilogue: C/D map of 16x16x32: col = l&15, row = 4(l>>4) + reg.
+  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 64 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
+// Deterministic uniform [-1, 1) bf16 fill (random operands: zero-filled ones overstate a GEMM).
+__global__ __launch_bounds__(256) void k_fill_bf16(__bf16* dst, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    dst[i] = (__bf16)((float)(h >> 8) * (2.0f / 16777216.0f) - 1.0f);
+  }
+}
+
 // ------------------------------------------------------------------ scratch cache
 struct Scratch {
   uint32_t* quick = nullptr;
@@ -553,6 +710,63 @@ int gm_probe_gemm_bf16(const void* A, const void* B, float* C, int M, int N, int
   hipLaunchKernelGGL(k_gemm_bf16, dim3(N / BN, M / BM), dim3(256), 0, (hipStream_t)stream,
                      (const __bf16*)A, (const __bf16*)B, C, M, N, K);
   return (int)hipGetLastError();
+}
+
+int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C, int M, int N,
+                             int K, void* stream) {
+  using namespace g256;
+  if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % TK) return (int)hipErrorInvalidValue;
+  const dim3 grid((M / TM) * (N / TN)), block(kThreads);
+  switch (variant) {
+    case 0:
+      hipLaunchKernelGGL(k_gemm_nt256<0>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 1:
+      hipLaunchKernelGGL(k_gemm_nt256<1>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+int gm_probe_gemm_nt(const void* A, const void* Bt, void* C, int M, int N, int K,
+                     void* stream) {
+  return gm_probe_gemm_nt_variant(kGemmNtDefault, A, Bt, C, M, N, K, stream);
+}
+
+int gm_probe_gemm_nt_tflops(int dev, int M, int N, int K, int iters, double* tflops) {
+  using namespace g256;
+  *tflops = 0;
+  if (iters <= 0 || M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % TK)
+    return (int)hipErrorInvalidValue;
+  DeviceGuard g(dev);
+  if (!g.ok) return (int)hipErrorInvalidDevice;
+  __bf16 *da = nullptr, *db = nullptr, *dc = nullptr;
+  GM_CHECK(hipMalloc(&da, (size_t)M * K * 2));
+  GM_CHECK(hipMalloc(&db, (size_t)N * K * 2));
+  GM_CHECK(hipMalloc(&dc, (size_t)M * N * 2));
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, da, (size_t)M * K, 0x1234u);
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, db, (size_t)N * K, 0x9876u);
+  hipEvent_t e0, e1;
+  int e = (int)hipEventCreate(&e0);
+  if (!e) e = (int)hipEventCreate(&e1);
+  if (!e) e = gm_probe_gemm_nt(da, db, dc, M, N, K, nullptr);  // warm-up
+  if (!e) e = (int)hipEventRecord(e0, nullptr);
+  for (int i = 0; i < iters && !e; ++i) e = gm_probe_gemm_nt(da, db, dc, M, N, K, nullptr);
+  if (!e) e = (int)hipEventRecord(e1, nullptr);
+  if (!e) e = (int)hipEventSynchronize(e1);
+  float ms = 0;
+  if (!e) e = (int)hipEventElapsedTime(&ms, e0, e1);
+  if (!e && ms > 0) *tflops = 2.0 * M * N * (double)K * iters / (ms * 1e-3) / 1e12;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dc);
+  return e;
 }
 
 int gm_probe_gemm_check(int dev, int M, int N, int K, double* max_abs_err, double* ref_scale) {

@@ -49,6 +49,14 @@ int gm_probe_mfma_peak(int dev, int iters, double* tflops);
 // C[M,N] (fp32) = A[M,K] (bf16, row-major) · B[K,N] (bf16, row-major) on MFMA.
 // Requires M%64 == 0, N%64 == 0, K%32 == 0 (checked). Device pointers; stream may be NULL.
 int gm_probe_gemm_bf16(const void* A, const void* B, float* C, int M, int N, int K, void* stream);
+// C[M,N] (bf16) = A[M,K] · Bt[N,K]ᵀ (bf16, both K-major), fp32 accumulate: the 256²-tile
+// global_load_lds throughput GEMM. Requires M%256 == 0, N%256 == 0, K%64 == 0 (checked).
+int gm_probe_gemm_nt(const void* A, const void* Bt, void* C, int M, int N, int K, void* stream);
+// Schedule variants of the same kernel (A/B measurements; bench/gemm_sweep.py).
+int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C, int M, int N,
+                             int K, void* stream);
+// Dense bf16 TF/s of gm_probe_gemm_nt on uniform [-1,1) operands, `iters` back-to-back launches.
+int gm_probe_gemm_nt_tflops(int dev, int M, int N, int K, int iters, double* tflops);
 // Self-contained numerics check of gm_probe_gemm_bf16 against a host fp32 reference.
 int gm_probe_gemm_check(int dev, int M, int N, int K, double* max_abs_err, double* ref_scale);
 // xGMI / PCIe peer copy a→b; *can_access from hipDeviceCanAccessPeer.

@@ -129,6 +129,46 @@ def test_mfma_gemm_asymmetric_identity():
     assert torch.equal(c, b.float())
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 192), (1280, 1024, 640)])
+def test_gemm_nt256_matches_torch_fp32(m, n, k, variant):
+    """The 256²-tile global_load_lds GEMM (odd tile counts exercise the XCD remap's remainder
+    and the partial GROUP_M raster) against an fp32 reference of the same bf16 operands."""
+    from gpumounter_amd.ops import probe
+
+    g = torch.Generator(device="cuda:0").manual_seed(m + 5 * n + 11 * k)
+    a = (torch.rand(m, k, device="cuda:0", generator=g) * 2 - 1).to(torch.bfloat16)
+    bt = (torch.rand(n, k, device="cuda:0", generator=g) * 2 - 1).to(torch.bfloat16)
+    c = probe.gemm_nt(a, bt, variant=variant)
+    torch.cuda.synchronize()
+    ref = a.float() @ bt.float().t()
+    err = (c.float() - ref).abs()
+    # bf16 output rounding (2^-8 relative) + fp32 accumulation-order noise
+    assert (err <= ref.abs() * 2 ** -8 + 1e-3 * k ** 0.5).all(), err.max().item()
+
+
+@pytest.mark.parametrize("variant", [None, 0, 1])
+def test_gemm_nt256_asymmetric_identity(variant):
+    """A = I with an asymmetric Bt: C must equal Btᵀ exactly (catches row/col swaps, swizzle
+    mismatches between the staged source and the LDS read)."""
+    from gpumounter_amd.ops import probe
+
+    n, k = 512, 512
+    a = torch.eye(n, k, device="cuda:0").to(torch.bfloat16)
+    g = torch.Generator(device="cuda:0").manual_seed(7)
+    b = torch.randn(k, n, device="cuda:0", generator=g).to(torch.bfloat16)  # distinct values
+    c = probe.gemm_nt(a, b.t().contiguous(), variant=variant)
+    assert torch.equal(c, b)
+
+
+def test_gemm_nt256_throughput():
+    from gpumounter_amd.ops import probe
+
+    tf = probe.gemm_tflops(0, 4096, 4096, 4096, 10)
+    print(f"gemm_nt 4096^3 bf16 {tf:.0f} TF/s")
+    assert tf > 300, tf
+
+
 def test_gemm_check_host_reference():
     from gpumounter_amd.ops import probe
 
