@@ -19,7 +19,7 @@ lib = _native.probe()
 a = (torch.rand(n, n, device="cuda") * 2 - 1).to(torch.bfloat16)
 bt = (torch.rand(n, n, device="cuda") * 2 - 1).to(torch.bfloat16)
 c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
-for v in (0, 1):
+for v in (0, 1, 2):
     for _ in range(3):
         assert lib.gm_probe_gemm_nt_variant(v, a.data_ptr(), bt.data_ptr(), c.data_ptr(), n, n, n,
                                             None) == 0

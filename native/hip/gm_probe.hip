@@ -316,6 +316,22 @@ typedef __attribute__((address_space(1))) void gbl_void;
 }  // namespace g256
 constexpr int kGemmNtDefault = 1;  // profiles/r1_gemm: V1 ≥ V0 at 4096³, +2.6 % at 8192³
 
+// XCD-aware block → output tile: bijective for any grid size (the dispatcher deals block ids
+// round-robin over the 8 XCDs, so ids ≡ x mod 8 share XCD x's L2 and get a contiguous range of
+// tiles), then a GROUP_M-deep raster so co-resident tiles share A rows and B columns.
+__device__ __forceinline__ void gemm_tile_of(int M, int N, int& tm, int& tn) {
+  using namespace g256;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int ntm = M / TM, ntn = N / TN;
+  const int per_group = kGroupM * ntn;
+  const int first_m = (wgid / per_group) * kGroupM;
+  const int gsize = min(ntm - first_m, kGroupM);
+  tm = first_m + (wgid % per_group) % gsize;
+  tn = (wgid % per_group) / gsize;
+}
+
 // V = 0: per 32-deep k-step, 12 fragment reads → wait → 32 MFMAs.
 // V = 1: all 24 fragment reads of the 64-deep K-tile issued up front, so the second k-step's
 //        reads overlap the first step's MFMAs (+48 VGPRs).
@@ -329,16 +345,8 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
 
-  // XCD-aware, bijective for any grid size; then GROUP_M-deep raster over the tile grid.
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int q = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
-  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
-  const int ntm = M / TM, ntn = N / TN;
-  const int per_group = kGroupM * ntn;
-  const int first_m = (wgid / per_group) * kGroupM;
-  const int gsize = min(ntm - first_m, kGroupM);
-  const int tm = first_m + (wgid % per_group) % gsize;
-  const int tn = (wgid % per_group) / gsize;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
 
   // Staging: wave w moves 1 KiB chunks c = w + 8i (i = 0..3) of each operand's 256×64 tile.
   // Lane l writes LDS byte c*1024 + l*16 = row 8c + (l>>3), slot l&7, which holds logical
@@ -437,6 +445,168 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
+// V2 — quadrant phases with half-tile staging (same LDS budget, deeper pipeline). Measured
+// 7-8 % slower than V1 on MI355X (profiles/r1_gemm): kept as the tested counter-example.
+// Each stage's A and B tiles are split into row halves (lo = rows 0-127, hi = 128-255) of 16 KiB,
+// giving 8 half-tile slots in the 128 KiB. Wave (wm, wn) owns A rows {wm*64 + [0,64)} of both
+// halves and B rows {wn*32 + [0,32)} of both, i.e. four 64×32 output quadrants. A K-tile runs
+// as 4 phases, one quadrant each, in the order (Alo,Blo) (Alo,Bhi) (Ahi,Bhi) (Ahi,Blo). Operands
+// are carried in registers between neighbouring phases, so each half-tile is read from LDS in
+// exactly one phase.
+// Half-tiles are loaded in consumption order L[m] (m = 4t + {Alo, Blo, Bhi, Ahi}) into slot m%8.
+// Phase p issues L[p+6] and ends with a counted vmcnt that retires only what phase p+1 reads,
+// then a raw s_barrier. So 4-5 half-tiles (2 glds each) stay in flight across every barrier,
+// where V0/V1 drain to vmcnt(0) once per K-tile.
+// WAR: L[m+8] overwrites L[m]'s slot. It is issued in phase m+2, and L[m] was last read in
+// phase ≤ m, with a barrier between.
+__device__ __forceinline__ void vm_wait_glds(int n) {  // n = glds allowed in flight (uniform)
+  switch (n) {
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <int Q>
+struct QPhase {
+  static constexpr int value = Q;
+};
+
+__global__ __launch_bounds__(512) void k_gemm_nt256q(const __bf16* __restrict__ A,
+                                                     const __bf16* __restrict__ Bt,
+                                                     __bf16* __restrict__ C, int M, int N,
+                                                     int K) {
+  using namespace g256;
+  constexpr int kHalf = 16384, kAhead = 6;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+
+  // Half-tile staging: wave w moves 1 KiB chunks w and w+8 (rows 8c + (l>>3) of the half).
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
+  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
+  const size_t row64 = (size_t)64 * K, row128 = (size_t)128 * K;
+  const int nt = K / TK, last = 4 * nt - 1;
+
+  auto issue = [&](int m) {  // L[m]: kind m&3 = 0 Alo, 1 Blo, 2 Bhi, 3 Ahi; tile m>>2
+    const int kind = m & 3;
+    const __bf16* src = ((kind == 0 || kind == 3) ? a_src : b_src) +
+                        (kind >= 2 ? row128 : (size_t)0) + (m >> 2) * TK;
+    char* dst = lds + (m & 7) * kHalf + wave * 1024;
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void*)(src + row64), (lds_void*)(dst + 8192), 16, 0,
+                                     0);
+  };
+
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 64 * 128 + foff0;
+  const int b_off = wn * 32 * 128 + foff0;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[2][4], fbl[2][2], fbh[2][2];
+
+  auto read_a = [&](const char* base) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[kk][i] = *reinterpret_cast<const bf16x8*>(base + ((a_off + i * 2048) ^ (kk << 6)));
+  };
+  auto read_b = [&](const char* base, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[kk][j] = *reinterpret_cast<const bf16x8*>(base + ((b_off + j * 2048) ^ (kk << 6)));
+  };
+  auto mma = [&](f32x4 (&c)[4][2], bf16x8 (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], c[i][j], 0, 0,
+                                                            0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  auto phase = [&](auto qc, int t) {
+    constexpr int q = decltype(qc)::value;
+    const int p = 4 * t + q;
+    const char* slot = lds + ((4 * t) & 7) * kHalf;  // Alo of tile t; +1..3 halves follow
+    if constexpr (q == 0) {
+      read_b(slot + 1 * kHalf, fbl);
+      read_a(slot + 0 * kHalf);
+    } else if constexpr (q == 1) {
+      read_b(slot + 2 * kHalf, fbh);
+    } else if constexpr (q == 2) {
+      read_a(slot + 3 * kHalf);
+    }
+    if (p + kAhead <= last) issue(p + kAhead);
+    if constexpr (q == 0) mma(acc[0][0], fbl);
+    if constexpr (q == 1) mma(acc[0][1], fbh);
+    if constexpr (q == 2) mma(acc[1][1], fbh);
+    if constexpr (q == 3) mma(acc[1][0], fbl);
+    if (p < last) {
+      // phase p+1 reads up to L[need]: Bhi(t) after q0, Ahi(t) after q1/q2, Blo(t+1) after q3
+      constexpr int need_rel = q == 0 ? 2 : (q == 3 ? 5 : 3);
+      const int issued = min(p + kAhead, last);
+      vm_wait_glds(2 * (issued - (4 * t + need_rel)));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  };
+
+  // Prologue: L[0..6] in flight; retire L[0], L[1] (Alo, Blo of tile 0).
+  const int pre = min(kAhead, last);
+  for (int m = 0; m <= pre; ++m) issue(m);
+  vm_wait_glds(2 * (pre - 1));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nt; ++t) {
+    phase(QPhase<0>{}, t);
+    phase(QPhase<1>{}, t);
+    phase(QPhase<2>{}, t);
+    phase(QPhase<3>{}, t);
+  }
+
+  const int crow = tm * TM + wm * 64 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 32 + (lane & 15);
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            C[(size_t)(crow + x * 128 + i * 16 + r) * N + ccol + y * 128 + j * 16] =
+                (__bf16)acc[x][y][i][j][r];
 }
 
 // Deterministic uniform [-1, 1) bf16 fill (random operands: zero-filled ones overstate a GEMM).
@@ -724,6 +894,10 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
       break;
     case 1:
       hipLaunchKernelGGL(k_gemm_nt256<1>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_gemm_nt256q, grid, block, 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     default:
