@@ -335,6 +335,7 @@ __device__ __forceinline__ void gemm_tile_of(int M, int N, int& tm, int& tn) {
 // V = 0: per 32-deep k-step, 12 fragment reads → wait → 32 MFMAs.
 // V = 1: all 24 fragment reads of the 64-deep K-tile issued up front, so the second k-step's
 //        reads overlap the first step's MFMAs (+48 VGPRs).
+// V = 3: V1's schedule on v_mfma_f32_32x32x16_bf16 (same 128×64 per wave: 4×2 32² blocks).
 template <int V>
 __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A,
                                                     const __bf16* __restrict__ Bt,
@@ -374,11 +375,24 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
   const int a_off = wm * 128 * 128 + foff0;
   const int b_off = kTileBytes + wn * 64 * 128 + foff0;
 
-  f32x4 acc[8][4];
+  f32x4 acc[V == 3 ? 1 : 8][4];
+  f32x16 acc32[V == 3 ? 4 : 1][2];
+  if constexpr (V == 3) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int r32 = lane & 31, h32 = lane >> 5, sw32 = (r32 >> 1) & 7;
+  const int a32_off = wm * 128 * 128 + r32 * 128;
+  const int b32_off = kTileBytes + wn * 64 * 128 + r32 * 128;
 
   const int nt = K / TK;
   stage(0, 0);
@@ -407,6 +421,31 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
+    } else if constexpr (V == 3) {
+      // 32x32x16 shape, same per-wave 128×64 tile: 4×2 blocks, 4 k16-steps per K-tile.
+      // Lane l reads row (l&31) of a 32-row block at logical chunk 2s + (l>>5).
+      bf16x8 af[4][4], bfr[4][2];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfr[st][j] = *reinterpret_cast<const bf16x8*>(sb + b32_off + j * 32 * 128 +
+                                                        ((((st * 2 + h32) ^ sw32)) << 4));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[st][i] = *reinterpret_cast<const bf16x8*>(sb + a32_off + i * 32 * 128 +
+                                                       ((((st * 2 + h32) ^ sw32)) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[st][i], bfr[st][j],
+                                                                  acc32[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     } else {
       bf16x8 af[2][8], bfr[2][4];
 #pragma unroll
@@ -435,6 +474,20 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
     __syncthreads();
   }
 
+  if constexpr (V == 3) {
+    // C/D map of 32x32x16: col = l&31, row = (reg&3) + 8(reg>>2) + 4(l>>5).
+    const int crow = tm * TM + wm * 128 + 4 * h32;
+    const int ccol = tn * TN + wn * 64 + r32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          C[(size_t)(crow + i * 32 + (r & 3) + 8 * (r >> 2)) * N + ccol + j * 32] =
+              (__bf16)acc32[i][j][r];
+    return;
+  }
   // Epilogue: C/D map of 16x16x32: col = l&15, row = 4(l>>4) + reg.
   const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
   const int ccol = tn * TN + wn * 64 + (lane & 15);
@@ -894,6 +947,10 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
       break;
     case 1:
       hipLaunchKernelGGL(k_gemm_nt256<1>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 3:
+      hipLaunchKernelGGL(k_gemm_nt256<3>, grid, block, 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     case 2:
