@@ -38,6 +38,9 @@ class LeaseKeeper:
         self.svc = service
         self._timers: Dict[str, asyncio.TimerHandle] = {}     # placeholder uid → timer
         self._retry_after: Dict[Tuple[str, str], float] = {}   # owner → not before
+        self._retry_timers: Dict[Tuple[str, str], asyncio.TimerHandle] = {}
+        self._tasks: set = set()                               # running expiries
+        self._stopped = False
         self.expired = 0
 
     # ------------------------------------------------------------------------ grant
@@ -52,17 +55,34 @@ class LeaseKeeper:
         return expires
 
     def _arm(self, uid: str, ns: str, name: str, expires: float) -> None:
-        if not uid or uid in self._timers:
+        if not uid or uid in self._timers or self._stopped:
             return
         loop = asyncio.get_running_loop()
-        self._timers[uid] = loop.call_later(
-            max(0.0, expires - time.time()),
-            lambda: asyncio.ensure_future(self.expire_owner(ns, name)))
+        self._timers[uid] = loop.call_later(max(0.0, expires - time.time()),
+                                            self._spawn, ns, name)
 
-    def stop(self) -> None:
-        for t in self._timers.values():
+    def _spawn(self, ns: str, name: str) -> None:
+        """Timer callback: run one expiry as a tracked task (cancelled by stop())."""
+        if self._stopped:
+            return
+        task = asyncio.ensure_future(self.expire_owner(ns, name))
+        self._tasks.add(task)
+        task.add_done_callback(self._tasks.discard)
+
+    async def stop(self, grace_s: float = 5.0) -> None:
+        """Worker shutdown: no timer fires afterwards, and an expiry already detaching is
+        allowed ``grace_s`` to finish (it is an ordinary RemoveGPU) before it is cancelled, so
+        nothing runs against the closed clients. The next worker's start-up sweep picks the
+        remaining leases up from the placeholder annotations."""
+        self._stopped = True
+        for t in list(self._timers.values()) + list(self._retry_timers.values()):
             t.cancel()
         self._timers.clear()
+        self._retry_timers.clear()
+        if self._tasks:
+            _, late = await asyncio.wait(list(self._tasks), timeout=grace_s)
+            for task in late:
+                task.cancel()
 
     # ------------------------------------------------------------------------ expiry
     async def sweep(self) -> int:
@@ -124,5 +144,9 @@ class LeaseKeeper:
                          f"lease over but the GPUs are still in use "
                          f"({api.RemoveGPUResponse.RemoveGPUResult.Name(resp.remove_gpu_result)}"
                          f"); retrying every {retry:g} s (lease_force=false)", warning=True)
-        asyncio.get_running_loop().call_later(
-            retry, lambda: asyncio.ensure_future(self.expire_owner(ns, name)))
+        if not self._stopped:
+            old = self._retry_timers.pop((ns, name), None)
+            if old is not None:
+                old.cancel()
+            self._retry_timers[(ns, name)] = asyncio.get_running_loop().call_later(
+                retry, self._spawn, ns, name)

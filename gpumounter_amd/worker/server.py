@@ -277,7 +277,7 @@ class Worker:
             self._health_task.cancel()
         await self.pool.stop()
         await self.reconciler.stop()
-        self.service.lease.stop()
+        await self.service.lease.stop()
         await self.service.notify.stop()
         if isinstance(self.backend, systemd.SystemdPersistingBackend):
             self.backend.sync.stop()

@@ -117,3 +117,33 @@ def test_lease_survives_a_worker_restart():
         assert await until(gone)
         assert await lc.audit("default", "t") == []
     run(body)
+
+
+def test_stop_cancels_timers_and_lets_a_running_expiry_finish():
+    """Worker shutdown: armed lease timers never fire afterwards, and an expiry that is already
+    detaching finishes (within the grace) instead of running on against closed clients."""
+    from gpumounter_amd.worker.lease import LeaseKeeper
+
+    calls = []
+
+    class Svc:
+        pass
+
+    async def main():
+        lk = LeaseKeeper(Svc())
+
+        async def slow_expire(ns, name):
+            calls.append(("start", name))
+            await asyncio.sleep(0.05)
+            calls.append(("done", name))
+        lk.expire_owner = slow_expire
+        import time as _t
+        lk._arm("u1", "ns", "now", _t.time())          # noqa: SLF001 - fires at once
+        lk._arm("u2", "ns", "later", _t.time() + 0.2)  # noqa: SLF001
+        await asyncio.sleep(0.01)                        # "now" is mid-expiry
+        await lk.stop()
+        await asyncio.sleep(0.3)                         # "later" would have fired by now
+        lk._arm("u3", "ns", "after-stop", _t.time())   # noqa: SLF001 - ignored once stopped
+        await asyncio.sleep(0.02)
+    asyncio.run(main())
+    assert calls == [("start", "now"), ("done", "now")]
