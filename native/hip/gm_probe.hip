@@ -662,6 +662,95 @@ __global__ __launch_bounds__(512) void k_gemm_nt256q(const __bf16* __restrict__ 
                 (__bf16)acc[x][y][i][j][r];
 }
 
+// V4 — measured 7-13 % slower than V1 on MI355X (profiles/r1_gemm).
+// 4 waves (2×2), each 128×128 = 8×8 16x16x32 accumulators (256 fp32/lane: the MFMA
+// destinations live in AGPRs, 1 wave per SIMD). A fragment read feeds 8 MFMAs instead of 4,
+// so LDS read traffic per K-tile drops by a third against V1; latency hiding is then
+// up to the single wave's own schedule: all 32 fragment reads of the K-tile are issued
+// before its 128 MFMAs.
+__global__ __launch_bounds__(256) void k_gemm_nt256w4(const __bf16* __restrict__ A,
+                                                      const __bf16* __restrict__ Bt,
+                                                      __bf16* __restrict__ C, int M, int N,
+                                                      int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+
+  // Staging: wave w moves chunks c = w + 4i (i = 0..7), rows 8c + (l>>3): rows differ by 32
+  // between i, so (row>>1)&7 is again the same for all of a lane's chunks.
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
+  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
+  const size_t row32 = (size_t)32 * K;
+  auto stage = [&](int buf, int k0) {
+    char* base = lds + buf * kStageBytes + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row32 + k0),
+                                       (lds_void*)(base + i * 4096), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row32 + k0),
+                                       (lds_void*)(base + kTileBytes + i * 4096), 16, 0, 0);
+    }
+  };
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 128 * 128 + foff0;
+  const int b_off = kTileBytes + wn * 128 * 128 + foff0;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) stage(cur ^ 1, (t + 1) * TK);
+    const char* sb = lds + cur * kStageBytes;
+    bf16x8 af[2][8], bfr[2][8];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 2048) ^ (kk << 6)));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        af[kk][i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 2048) ^ (kk << 6)));
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 128 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
 // Deterministic uniform [-1, 1) bf16 fill (random operands: zero-filled ones overstate a GEMM).
 __global__ __launch_bounds__(256) void k_fill_bf16(__bf16* dst, size_t n, uint32_t seed) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
@@ -951,6 +1040,10 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
       break;
     case 3:
       hipLaunchKernelGGL(k_gemm_nt256<3>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 4:
+      hipLaunchKernelGGL(k_gemm_nt256w4, grid, dim3(256), 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     case 2:
