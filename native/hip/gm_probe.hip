@@ -314,7 +314,7 @@ constexpr int kLdsBytes = 2 * kStageBytes;    // two stages: 128 KiB of the 160 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 }  // namespace g256
-constexpr int kGemmNtDefault = 1;  // profiles/r1_gemm: V1 ≥ V0 at 4096³, +2.6 % at 8192³
+constexpr int kGemmNtDefault = 5;  // profiles/r1_gemm: V5 +2.9 % over V1 at 4096³, +0.9 % at 8192³
 
 // XCD-aware block → output tile: bijective for any grid size (the dispatcher deals block ids
 // round-robin over the 8 XCDs, so ids ≡ x mod 8 share XCD x's L2 and get a contiguous range of
@@ -751,6 +751,103 @@ __global__ __launch_bounds__(256) void k_gemm_nt256w4(const __bf16* __restrict__
         C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
 }
 
+// V5 — V1's geometry with a local-read prefetch across the barrier. The second k-step's MFMAs
+// of tile t are deferred past the barrier, so they run while the first k-step fragments of
+// tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
+// register use stays at two fragment sets (like V1). The barrier sits mid-tile, so the next
+// tile's DMA is issued right after it.
+__global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ A,
+                                                     const __bf16* __restrict__ Bt,
+                                                     __bf16* __restrict__ C, int M, int N,
+                                                     int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
+  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
+  const size_t row64 = (size_t)64 * K;
+  auto stage = [&](int buf, int k0) {
+    char* base = lds + buf * kStageBytes + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row64 + k0),
+                                       (lds_void*)(base + i * 8192), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row64 + k0),
+                                       (lds_void*)(base + kTileBytes + i * 8192), 16, 0, 0);
+    }
+  };
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 128 * 128 + foff0;
+  const int b_off = kTileBytes + wn * 64 * 128 + foff0;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a0[8], b0[4], a1[8], b1[4];
+  auto read = [&](const char* sb, int kk, bf16x8 (&af)[8], bf16x8 (&bf)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 2048) ^ (kk << 6)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 2048) ^ (kk << 6)));
+  };
+  auto mma = [&](bf16x8 (&af)[8], bf16x8 (&bf)[4]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nt = K / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // Waits go through __builtin_amdgcn_s_waitcnt (gfx9 simm16: vmcnt[3:0]|expcnt[6:4]|
+  // lgkmcnt[11:8]|vmcnt[5:4]<<14), not inline asm, so the compiler's own wait insertion knows
+  // the counters are clear and adds no lgkmcnt(0) in front of the MFMAs.
+  constexpr int kWaitLgkm0 = 0xC07F, kWaitVm0Lgkm0 = 0x0070;
+  // Tile t+1's DMA is issued right after the barrier that frees its buffer (mid-tile t-1), so
+  // it has a whole tile of MFMAs (64 per wave) to land before the vmcnt(0) that retires it.
+  if (nt > 1) stage(1, TK);
+  read(lds, 0, a0, b0);
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    const char* sb = lds + cur * kStageBytes;
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // a0/b0 (read behind the last 32 MFMAs) are in
+    read(sb, 1, a1, b1);
+    mma(a0, b0);
+    __builtin_amdgcn_s_waitcnt(kWaitVm0Lgkm0);  // tile t+1 landed; our reads of `cur` done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nt) stage(cur, (t + 2) * TK);   // every wave is past its reads of `cur`
+    if (t + 1 < nt) read(lds + (cur ^ 1) * kStageBytes, 0, a0, b0);
+    mma(a1, b1);
+  }
+
+  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 64 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
 // Deterministic uniform [-1, 1) bf16 fill (random operands: zero-filled ones overstate a GEMM).
 __global__ __launch_bounds__(256) void k_fill_bf16(__bf16* dst, size_t n, uint32_t seed) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
@@ -1040,6 +1137,10 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
       break;
     case 3:
       hipLaunchKernelGGL(k_gemm_nt256<3>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 5:
+      hipLaunchKernelGGL(k_gemm_nt256p, grid, block, 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     case 4:
