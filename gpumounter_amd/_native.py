@@ -228,6 +228,8 @@ def probe() -> C.CDLL:
                                                  C.c_int, C.c_int, C.c_int, C.c_void_p]
         lib.gm_probe_gemm_nt_tflops.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                                 C.POINTER(C.c_double)]
+        lib.gm_probe_burn_in.argtypes = [C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double),
+                                         C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
         lib.gm_probe_gemm_check.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int,
                                             C.POINTER(C.c_double), C.POINTER(C.c_double)]
         lib.gm_probe_p2p.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_int),

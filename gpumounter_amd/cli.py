@@ -4,7 +4,7 @@
     python -m gpumounter_amd worker   [--config f.yaml] [--node NAME]
     python -m gpumounter_amd inventory [--amdsmi mock]          # amdsmi view of this node
     python -m gpumounter_amd topology  [--amdsmi mock] [-n 4]   # xGMI/NUMA placement preview
-    python -m gpumounter_amd probe     [--bdf 0000:05:00.0] [--full]   # gfx950 validation kernels
+    python -m gpumounter_amd probe     [--bdf 0000:05:00.0] [--full] [--burn-in 60]  # gfx950 kernels
     python -m gpumounter_amd add    --master URL --ns NS --pod P -n 2 [--entire] [--lease 3600]
     python -m gpumounter_amd remove --master URL --ns NS --pod P --uuid U [--uuid U2] [--force]
     python -m gpumounter_amd status --master URL --node NODE
@@ -134,8 +134,13 @@ def cmd_probe(args) -> int:
     else:
         bdfs = [probe.props(i)["pci_bus_id"] for i in range(probe.device_count())]
     res = [r.to_dict() for r in probe.verify(bdfs, full=args.full)]
+    bad = False
+    if args.burn_in:
+        for r in res:
+            r["burn_in"] = probe.burn_in(r["device"], args.burn_in)
+            bad |= not r["burn_in"]["ok"]
     print(json.dumps(res, indent=2))
-    return 0
+    return 1 if bad else 0
 
 
 async def _http(method: str, url: str, data=None) -> int:
@@ -268,6 +273,8 @@ def build_parser() -> argparse.ArgumentParser:
     p = sub.add_parser("probe")
     p.add_argument("--bdf", action="append")
     p.add_argument("--full", action="store_true")
+    p.add_argument("--burn-in", type=float, default=0.0, metavar="SECONDS",
+                   help="sustained GEMM load with bit-exact result checks (exit 1 on mismatch)")
     p.set_defaults(fn=cmd_probe)
     for name, fn in (("add", cmd_add), ("remove", cmd_remove), ("status", cmd_status)):
         p = sub.add_parser(name)

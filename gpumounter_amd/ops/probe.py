@@ -147,6 +147,18 @@ def gemm_tflops(dev: int, m: int = 8192, n: int = 8192, k: int = 8192, iters: in
     return t.value
 
 
+def burn_in(dev: int, seconds: float = 10.0, n: int = 8192) -> Dict:
+    """Sustained-load check of an attached GPU: back-to-back n³ bf16 GEMMs for ``seconds``,
+    each compared bit-for-bit with the first result (the kernel is deterministic). Any
+    ``mismatches`` means silent data corruption. ``tflops`` is the sustained rate, so
+    throttling shows up as a low number."""
+    tf, bad, it = C.c_double(0), C.c_uint64(0), C.c_int(0)
+    _check(_native.probe().gm_probe_burn_in(dev, n, seconds, C.byref(tf), C.byref(bad),
+                                            C.byref(it)), "burn-in")
+    return {"device": dev, "n": n, "seconds": seconds, "iterations": it.value,
+            "tflops": tf.value, "mismatches": bad.value, "ok": bad.value == 0}
+
+
 def p2p(dev_a: int, dev_b: int, nbytes: int = 256 << 20, iters: int = 10) -> Dict:
     can, g = C.c_int(0), C.c_double(0)
     _check(_native.probe().gm_probe_p2p(dev_a, dev_b, nbytes, iters, C.byref(can), C.byref(g)),

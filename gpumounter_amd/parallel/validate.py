@@ -7,7 +7,10 @@ starting a job on them — the reference offers nothing here:
 2. every pair has peer access and xGMI-class copy bandwidth (:func:`collectives.xgmi_matrix`);
 3. RCCL works across all of them: one process per GPU, ``torch.distributed`` with backend
    ``nccl`` (RCCL on ROCm), a checked bf16 all-reduce with ring bus bandwidth
-   (:func:`collectives.allreduce_check`).
+   (:func:`collectives.allreduce_check`);
+4. optionally (``--burn-in SECONDS``) all GPUs under sustained MFMA load at once, each
+   result bit-compared with the first (:func:`probe.burn_in`): catches silent data corruption
+   and throttling that a short probe misses.
 
 Prints one JSON document; exit code 0 only if every check passed. ``--cpu-ranks N`` runs step 3
 with N gloo ranks on the CPU (hermetic tests).
@@ -73,6 +76,8 @@ def main(argv=None) -> int:
                     help="skip the GPU checks; all-reduce over N gloo ranks on the CPU")
     ap.add_argument("--numel", type=int, default=1 << 24, help="all-reduce elements (bf16)")
     ap.add_argument("--no-p2p", action="store_true")
+    ap.add_argument("--burn-in", type=float, default=0.0, metavar="SECONDS",
+                    help="then load every GPU at once with bit-checked GEMMs for SECONDS")
     args = ap.parse_args(argv)
     report: Dict = {"ok": True}
     if args.cpu_ranks:
@@ -100,6 +105,16 @@ def main(argv=None) -> int:
                            "busbw_gbps": min(r["busbw_gbps"] for r in ranks),
                            "bytes": ranks[0]["bytes"]}
     report["ok"] &= report["allreduce"]["ok"]
+    if args.burn_in and not args.cpu_ranks:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from gpumounter_amd.ops import probe
+
+        # all GPUs at once (shared power/thermal envelope); ctypes drops the GIL in the call
+        with ThreadPoolExecutor(max_workers=world) as ex:
+            burn = list(ex.map(lambda d: probe.burn_in(d, args.burn_in), range(world)))
+        report["burn_in"] = burn
+        report["ok"] &= all(b["ok"] for b in burn)
     print(json.dumps(report))
     return 0 if report["ok"] else 1
 

@@ -860,6 +860,42 @@ __global__ __launch_bounds__(256) void k_fill_bf16(__bf16* dst, size_t n, uint32
   }
 }
 
+// Owning device buffer / event pair for the host entry points (freed on every return path).
+struct DevBuf {
+  void* p = nullptr;
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes); }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+struct Events {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t create() {
+    hipError_t e = hipEventCreate(&e0);
+    return e != hipSuccess ? e : hipEventCreate(&e1);
+  }
+  ~Events() {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+};
+
+// Number of 16-B words that differ between a and b: one ballot + popcount per wave, one
+// atomic per wave.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_count_diff(const u32x4* __restrict__ a,
+                                                    const u32x4* __restrict__ b, size_t n,
+                                                    unsigned long long* count) {
+  unsigned long long local = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const u32x4 x = __builtin_nontemporal_load(&a[i]), y = __builtin_nontemporal_load(&b[i]);
+    local += (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
+  }
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, kWave);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
+}
+
 // ------------------------------------------------------------------ scratch cache
 struct Scratch {
   uint32_t* quick = nullptr;
@@ -1169,29 +1205,83 @@ int gm_probe_gemm_nt_tflops(int dev, int M, int N, int K, int iters, double* tfl
     return (int)hipErrorInvalidValue;
   DeviceGuard g(dev);
   if (!g.ok) return (int)hipErrorInvalidDevice;
-  __bf16 *da = nullptr, *db = nullptr, *dc = nullptr;
-  GM_CHECK(hipMalloc(&da, (size_t)M * K * 2));
-  GM_CHECK(hipMalloc(&db, (size_t)N * K * 2));
-  GM_CHECK(hipMalloc(&dc, (size_t)M * N * 2));
-  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, da, (size_t)M * K, 0x1234u);
-  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, db, (size_t)N * K, 0x9876u);
-  hipEvent_t e0, e1;
-  int e = (int)hipEventCreate(&e0);
-  if (!e) e = (int)hipEventCreate(&e1);
-  if (!e) e = gm_probe_gemm_nt(da, db, dc, M, N, K, nullptr);  // warm-up
-  if (!e) e = (int)hipEventRecord(e0, nullptr);
-  for (int i = 0; i < iters && !e; ++i) e = gm_probe_gemm_nt(da, db, dc, M, N, K, nullptr);
-  if (!e) e = (int)hipEventRecord(e1, nullptr);
-  if (!e) e = (int)hipEventSynchronize(e1);
+  DevBuf da, db, dc;
+  GM_CHECK(da.alloc((size_t)M * K * 2));
+  GM_CHECK(db.alloc((size_t)N * K * 2));
+  GM_CHECK(dc.alloc((size_t)M * N * 2));
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, (__bf16*)da.p, (size_t)M * K,
+                     0x1234u);
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, (__bf16*)db.p, (size_t)N * K,
+                     0x9876u);
+  Events ev;
+  GM_CHECK(ev.create());
+  int e = gm_probe_gemm_nt(da.p, db.p, dc.p, M, N, K, nullptr);  // warm-up
+  if (!e) e = (int)hipEventRecord(ev.e0, nullptr);
+  for (int i = 0; i < iters && !e; ++i) e = gm_probe_gemm_nt(da.p, db.p, dc.p, M, N, K, nullptr);
+  if (!e) e = (int)hipEventRecord(ev.e1, nullptr);
+  if (!e) e = (int)hipEventSynchronize(ev.e1);
   float ms = 0;
-  if (!e) e = (int)hipEventElapsedTime(&ms, e0, e1);
+  if (!e) e = (int)hipEventElapsedTime(&ms, ev.e0, ev.e1);
   if (!e && ms > 0) *tflops = 2.0 * M * N * (double)K * iters / (ms * 1e-3) / 1e12;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipFree(da);
-  (void)hipFree(db);
-  (void)hipFree(dc);
   return e;
+}
+
+int gm_probe_burn_in(int dev, int n, double seconds, double* tflops, uint64_t* mismatches,
+                     int* iters) {
+  using namespace g256;
+  *tflops = 0;
+  *mismatches = 0;
+  *iters = 0;
+  if (n <= 0 || n % TM || seconds <= 0) return (int)hipErrorInvalidValue;
+  DeviceGuard g(dev);
+  if (!g.ok) return (int)hipErrorInvalidDevice;
+  const size_t elems = (size_t)n * n;
+  DevBuf da, db, dref, dc, dcount;
+  GM_CHECK(da.alloc(elems * 2));
+  GM_CHECK(db.alloc(elems * 2));
+  GM_CHECK(dref.alloc(elems * 2));
+  GM_CHECK(dc.alloc(elems * 2));
+  GM_CHECK(dcount.alloc(sizeof(unsigned long long)));
+  GM_CHECK(hipMemset(dcount.p, 0, sizeof(unsigned long long)));
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, (__bf16*)da.p, elems, 0x5151u);
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, (__bf16*)db.p, elems, 0xa3a3u);
+  int e = gm_probe_gemm_nt(da.p, db.p, dref.p, n, n, n, nullptr);  // the reference result
+  if (e) return e;
+  Events ev;
+  GM_CHECK(ev.create());
+  GM_CHECK(hipEventRecord(ev.e0, nullptr));
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t vec = elems / 8;  // 16-B compares
+  int done = 0;
+  // Batches of 8 GEMMs, each result compared bit-for-bit with the first one: the kernel is
+  // deterministic (fixed reduction order, no atomics), so any difference is a hardware fault.
+  while (!e) {
+    for (int i = 0; i < 8 && !e; ++i) {
+      e = gm_probe_gemm_nt(da.p, db.p, dc.p, n, n, n, nullptr);
+      if (!e) {
+        hipLaunchKernelGGL(k_count_diff, dim3(2048), dim3(256), 0, 0,
+                           (const u32x4*)dc.p, (const u32x4*)dref.p, vec,
+                           (unsigned long long*)dcount.p);
+        e = (int)hipGetLastError();
+      }
+      ++done;
+    }
+    if (!e) e = (int)hipDeviceSynchronize();
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el >= seconds) break;
+  }
+  if (!e) e = (int)hipEventRecord(ev.e1, nullptr);
+  if (!e) e = (int)hipEventSynchronize(ev.e1);
+  float ms = 0;
+  if (!e) e = (int)hipEventElapsedTime(&ms, ev.e0, ev.e1);
+  unsigned long long bad = 0;
+  if (!e) e = (int)hipMemcpy(&bad, dcount.p, sizeof(bad), hipMemcpyDeviceToHost);
+  if (e) return e;
+  *iters = done;
+  *mismatches = bad;
+  // compare kernels are included in the wall time; they move 2 × n² × 2 B per GEMM (< 1 %)
+  if (ms > 0) *tflops = 2.0 * n * (double)n * n * done / (ms * 1e-3) / 1e12;
+  return 0;
 }
 
 int gm_probe_gemm_check(int dev, int M, int N, int K, double* max_abs_err, double* ref_scale) {

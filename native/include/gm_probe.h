@@ -57,6 +57,12 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
                              int K, void* stream);
 // Dense bf16 TF/s of gm_probe_gemm_nt on uniform [-1,1) operands, `iters` back-to-back launches.
 int gm_probe_gemm_nt_tflops(int dev, int M, int N, int K, int iters, double* tflops);
+// Burn-in: back-to-back n³ GEMMs (gm_probe_gemm_nt) for `seconds` on uniform [-1,1) operands;
+// every result is compared bit-for-bit with the first (the kernel is deterministic), so
+// *mismatches > 0 (16-B words that differ, summed over iterations) means silent data
+// corruption. *tflops includes the compare kernels. n % 256 == 0.
+int gm_probe_burn_in(int dev, int n, double seconds, double* tflops, uint64_t* mismatches,
+                     int* iters);
 // Self-contained numerics check of gm_probe_gemm_bf16 against a host fp32 reference.
 int gm_probe_gemm_check(int dev, int M, int N, int K, double* max_abs_err, double* ref_scale);
 // xGMI / PCIe peer copy a→b; *can_access from hipDeviceCanAccessPeer.

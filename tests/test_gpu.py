@@ -169,6 +169,24 @@ def test_gemm_nt256_throughput():
     assert tf > 300, tf
 
 
+def test_burn_in_is_bit_exact_and_sustained():
+    from gpumounter_amd.ops import probe
+
+    r = probe.burn_in(0, seconds=2.0, n=4096)
+    print(r)
+    assert r["ok"] and r["mismatches"] == 0, r
+    assert r["iterations"] >= 8 and r["tflops"] > 300, r
+
+
+def test_probe_cli_burn_in():
+    res = subprocess.run([sys.executable, "-m", "gpumounter_amd", "probe", "--burn-in", "1"],
+                         capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr[-2000:]
+    import json
+    out = json.loads(res.stdout)
+    assert out and all(r["burn_in"]["ok"] for r in out), out
+
+
 def test_gemm_check_host_reference():
     from gpumounter_amd.ops import probe
 
@@ -290,10 +308,11 @@ def test_tenant_validate_tool_runs_kernel_p2p_and_rccl():
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = subprocess.run([sys.executable, "-m", "gpumounter_amd.parallel.validate",
-                          "--numel", str(1 << 22)], cwd=root, capture_output=True, text=True,
-                         timeout=240)
+                          "--numel", str(1 << 22), "--burn-in", "1"], cwd=root,
+                         capture_output=True, text=True, timeout=240)
     assert res.returncode == 0, (res.stdout[-2000:], res.stderr[-3000:])
     rep = json.loads(res.stdout.strip().splitlines()[-1])
     assert rep["ok"] and rep["gpus"] and all(g["arch"].startswith("gfx950") for g in rep["gpus"])
     assert rep["allreduce"]["world"] == len(rep["gpus"]) and rep["allreduce"]["ok"]
+    assert len(rep["burn_in"]) == len(rep["gpus"]) and all(b["ok"] for b in rep["burn_in"])
     print(json.dumps(rep["allreduce"]))
