@@ -41,7 +41,7 @@ def timed(fn, iters):
     return a.elapsed_time(b) / iters * 1e-3
 
 
-VARIANTS = (0, 1, 5)
+VARIANTS = (1, 5, 7)
 
 
 def main():

@@ -751,11 +751,20 @@ __global__ __launch_bounds__(256) void k_gemm_nt256w4(const __bf16* __restrict__
         C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
 }
 
+// Buffer-resource LDS DMA (buffer_load_dwordx4 … lds): gfx9-family resource word 3 =
+// 0x00020000 (raw, untyped), stride 0, num_records = size in bytes (range-checked).
+typedef __attribute__((address_space(3))) void lds_any;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
 // V5 — V1's geometry with a local-read prefetch across the barrier. The second k-step's MFMAs
 // of tile t are deferred past the barrier, so they run while the first k-step fragments of
 // tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
 // register use stays at two fragment sets (like V1). The barrier sits mid-tile, so the next
 // tile's DMA is issued right after it.
+template <bool kBufDma>
 __global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ A,
                                                      const __bf16* __restrict__ Bt,
                                                      __bf16* __restrict__ C, int M, int N,
@@ -772,14 +781,28 @@ __global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ 
   const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
   const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
   const size_t row64 = (size_t)64 * K;
+  // kBufDma (V7): the same DMA as buffer_load … lds from SGPR resources plus one 32-bit
+  // per-lane offset, instead of eight per-lane 64-bit source pointers.
+  const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc(A + (size_t)tm * TM * K, (uint32_t)TM * K * 2);
+  const __amdgpu_buffer_rsrc_t b_rsrc =
+      make_rsrc(Bt + (size_t)tn * TN * K, (uint32_t)TN * K * 2);
+  const int lane_off = (srow * K + schunk * 8) * 2;
   auto stage = [&](int buf, int k0) {
     char* base = lds + buf * kStageBytes + wave * 1024;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row64 + k0),
-                                       (lds_void*)(base + i * 8192), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row64 + k0),
-                                       (lds_void*)(base + kTileBytes + i * 8192), 16, 0, 0);
+      if constexpr (kBufDma) {
+        const int soff = __builtin_amdgcn_readfirstlane((i * 64 * K + k0) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)(base + i * 8192), 16,
+                                                 lane_off, soff, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)(base + kTileBytes + i * 8192),
+                                                 16, lane_off, soff, 0, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row64 + k0),
+                                         (lds_void*)(base + i * 8192), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row64 + k0),
+                                         (lds_void*)(base + kTileBytes + i * 8192), 16, 0, 0);
+      }
     }
   };
   const int frow = lane & 15;
@@ -843,6 +866,110 @@ __global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ 
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
+// V6 — V4's geometry (4 waves × 128², AGPR accumulators) on V5's schedule.
+// (V5:) V1's geometry with a local-read prefetch across the barrier. The second k-step's MFMAs
+// of tile t are deferred past the barrier, so they run while the first k-step fragments of
+// tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
+// register use stays at two fragment sets (like V1). The barrier sits mid-tile, so the next
+// tile's DMA is issued right after it.
+__global__ __launch_bounds__(256) void k_gemm_nt256w4p(const __bf16* __restrict__ A,
+                                                     const __bf16* __restrict__ Bt,
+                                                     __bf16* __restrict__ C, int M, int N,
+                                                     int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  // buffer_load … lds: the block's A/B panels as buffer resources (SGPRs), one 32-bit per-lane
+  // byte offset, the per-load row/k offset in soffset (SGPR). Two VGPRs of addressing instead
+  // of sixteen 64-bit pointers (which spilled), and range-checked: an out-of-panel read
+  // returns zeros instead of faulting.
+  const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc(A + (size_t)tm * TM * K, (uint32_t)TM * K * 2);
+  const __amdgpu_buffer_rsrc_t b_rsrc =
+      make_rsrc(Bt + (size_t)tn * TN * K, (uint32_t)TN * K * 2);
+  const int lane_off = (srow * K + schunk * 8) * 2;
+  auto stage = [&](int buf, int k0) {
+    char* base = lds + buf * kStageBytes + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int soff = __builtin_amdgcn_readfirstlane((i * 32 * K + k0) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)(base + i * 4096), 16, lane_off,
+                                               soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)(base + kTileBytes + i * 4096),
+                                               16, lane_off, soff, 0, 0);
+    }
+  };
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 128 * 128 + foff0;
+  const int b_off = kTileBytes + wn * 128 * 128 + foff0;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  auto read = [&](const char* sb, int kk, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 2048) ^ (kk << 6)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 2048) ^ (kk << 6)));
+  };
+  auto mma = [&](bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nt = K / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // Waits go through __builtin_amdgcn_s_waitcnt (gfx9 simm16: vmcnt[3:0]|expcnt[6:4]|
+  // lgkmcnt[11:8]|vmcnt[5:4]<<14), not inline asm, so the compiler's own wait insertion knows
+  // the counters are clear and adds no lgkmcnt(0) in front of the MFMAs.
+  constexpr int kWaitLgkm0 = 0xC07F, kWaitVm0Lgkm0 = 0x0070;
+  // Tile t+1's DMA is issued right after the barrier that frees its buffer (mid-tile t-1), so
+  // it has a whole tile of MFMAs (64 per wave) to land before the vmcnt(0) that retires it.
+  if (nt > 1) stage(1, TK);
+  read(lds, 0, a0, b0);
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    const char* sb = lds + cur * kStageBytes;
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // a0/b0 (read behind the last 32 MFMAs) are in
+    read(sb, 1, a1, b1);
+    mma(a0, b0);
+    __builtin_amdgcn_s_waitcnt(kWaitVm0Lgkm0);  // tile t+1 landed; our reads of `cur` done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nt) stage(cur, (t + 2) * TK);   // every wave is past its reads of `cur`
+    if (t + 1 < nt) read(lds + (cur ^ 1) * kStageBytes, 0, a0, b0);
+    mma(a1, b1);
+  }
+
+  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 128 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
@@ -1176,7 +1303,15 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     case 5:
-      hipLaunchKernelGGL(k_gemm_nt256p, grid, block, 0, (hipStream_t)stream,
+      hipLaunchKernelGGL(k_gemm_nt256p<false>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 7:
+      hipLaunchKernelGGL(k_gemm_nt256p<true>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 6:
+      hipLaunchKernelGGL(k_gemm_nt256w4p, grid, dim3(256), 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     case 4:
