@@ -9,7 +9,7 @@
     python -m gpumounter_amd remove --master URL --ns NS --pod P --uuid U [--uuid U2] [--force]
     python -m gpumounter_amd status --master URL --node NODE
     python -m gpumounter_amd bpf-dump --allow 226:128 --allow 511:0   # generated device program
-    python -m gpumounter_amd doctor  [--json] [--skip-cluster]       # node preflight
+    python -m gpumounter_amd doctor  [--json] [--skip-cluster] [--gpu [--burn-in 30]]  # preflight
 
 The reference ships only the two daemons and documents curl calls (QuickStart.md:41-92); the
 ``add``/``remove`` commands speak exactly those HTTP routes.
@@ -238,7 +238,8 @@ def cmd_doctor(args) -> int:
     from gpumounter_amd.utils import doctor
 
     cfg = _cfg(args)
-    checks = doctor.run(cfg, skip_cluster=args.skip_cluster)
+    checks = doctor.run(cfg, skip_cluster=args.skip_cluster, gpu=args.gpu or bool(args.burn_in),
+                        burn_in_s=args.burn_in)
     print(doctor.render(checks, args.json))
     return 1 if any(c.status == "fail" for c in checks) else 0
 
@@ -298,6 +299,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--json", action="store_true")
     p.add_argument("--skip-cluster", action="store_true",
                    help="skip the kubelet and apiserver checks")
+    p.add_argument("--gpu", action="store_true",
+                   help="also run the gfx950 liveness kernel on every GPU")
+    p.add_argument("--burn-in", type=float, default=0.0, metavar="SECONDS",
+                   help="with --gpu: sustained bit-checked GEMM load per GPU")
     p.set_defaults(fn=cmd_doctor)
     p = sub.add_parser("bpf-dump")
     p.add_argument("--allow", action="append", default=[])

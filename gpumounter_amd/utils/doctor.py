@@ -164,8 +164,55 @@ async def _check_apiserver(cfg) -> List[Check]:
         await kube.close()
 
 
-def run(cfg, skip_cluster: bool = False) -> List[Check]:
+def check_gpus(cfg, burn_in_s: float = 0.0) -> List[Check]:
+    """Run the gfx950 probe kernels on every GPU of the node (``doctor --gpu``): each amdsmi GPU
+    must be visible to HIP and pass the wave64 liveness kernel. With ``burn_in_s`` also a
+    sustained bit-checked GEMM load per GPU. A GPU that fails here should not be handed out."""
+    from gpumounter_amd.hw.inventory import Inventory
+    from gpumounter_amd.ops import probe
+
+    try:
+        n = probe.device_count()
+    except Exception as e:  # noqa: BLE001 - no HIP runtime / driver
+        return [Check("gpu", "fail", f"HIP unavailable: {e}")]
+    if n == 0:
+        return [Check("gpu", "fail", "no GPU visible to HIP")]
+    try:
+        want = [g.bdf for g in Inventory(cfg.amdsmi_lib, cfg.kfd_major,
+                                         cfg.kfd_dev_path).gpus()]
+    except Exception:  # noqa: BLE001 - reported by the amdsmi check
+        want = []
+    out: List[Check] = []
+    seen = set()
+    for d in range(n):
+        try:
+            pr = probe.props(d)
+            seen.add(pr["pci_bus_id"])
+            cold = probe.quick(d)          # includes loading the code object
+            us = probe.quick(d)
+            arch = pr["gcn_arch"].split(":")[0]
+            detail = (f"{pr['pci_bus_id']} {arch}: liveness kernel {us:.0f} µs "
+                      f"(first launch {cold / 1e3:.0f} ms)")
+            status = "ok" if arch == "gfx950" else "warn"
+            if burn_in_s > 0:
+                b = probe.burn_in(d, burn_in_s)
+                detail += (f", burn-in {b['seconds']:g} s {b['tflops']:.0f} TF/s "
+                           f"{b['mismatches']} mismatching words")
+                status = status if b["ok"] else "fail"
+            out.append(Check(f"gpu{d}", status, detail))
+        except Exception as e:  # noqa: BLE001 - a faulting GPU is exactly what this finds
+            out.append(Check(f"gpu{d}", "fail", f"probe failed: {e}"))
+    missing = [b for b in want if b.lower() not in seen]
+    if missing:
+        out.append(Check("gpu", "warn", f"amdsmi GPUs not visible to HIP here: {missing}"))
+    return out
+
+
+def run(cfg, skip_cluster: bool = False, gpu: bool = False,
+        burn_in_s: float = 0.0) -> List[Check]:
     checks = check_inventory(cfg) + check_cgroup(cfg) + check_systemd(cfg)
+    if gpu:
+        checks += check_gpus(cfg, burn_in_s)
     if not skip_cluster:
         async def both():
             return await _check_kubelet(cfg) + await _check_apiserver(cfg)

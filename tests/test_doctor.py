@@ -39,3 +39,17 @@ def test_doctor_cli_exit_code_and_json():
     checks = {c["name"]: c for c in json.loads(res.stdout)}
     assert checks["amdsmi"]["status"] == "ok"
     assert checks["cgroup"]["status"] == "fail" and checks["kubelet"]["status"] == "fail"
+
+
+def test_doctor_gpu_check_fails_cleanly_without_a_gpu():
+    """``doctor --gpu`` on a host whose GPUs HIP cannot see reports a failed check (exit 1)
+    instead of crashing; on the MI355X box tests/test_gpu.py runs the passing case."""
+    import torch
+
+    if torch.cuda.is_available():
+        import pytest
+        pytest.skip("GPU present: covered by test_gpu.py::test_doctor_gpu_checks_pass")
+    cfg = Config.load(env={}, amdsmi_lib="mock")
+    checks = doctor.check_gpus(cfg)
+    assert checks and all(c.status == "fail" for c in checks), checks
+    assert checks[0].name == "gpu"

@@ -187,6 +187,21 @@ def test_probe_cli_burn_in():
     assert out and all(r["burn_in"]["ok"] for r in out), out
 
 
+def test_doctor_gpu_checks_pass():
+    """``doctor --gpu --burn-in 1``: every HIP GPU of the box runs the liveness kernel and a
+    short bit-checked GEMM load; the amdsmi inventory and HIP agree on the BDFs."""
+    import json
+
+    res = subprocess.run([sys.executable, "-m", "gpumounter_amd", "doctor", "--json",
+                          "--skip-cluster", "--gpu", "--burn-in", "1"],
+                         capture_output=True, text=True, timeout=180,
+                         env={**os.environ, "GM_SYSTEMD_DEVICE_ALLOW": "off"})
+    checks = json.loads(res.stdout)
+    gpu = [c for c in checks if c["name"].startswith("gpu")]
+    assert gpu and all(c["status"] == "ok" for c in gpu), gpu
+    assert all("0 mismatching words" in c["detail"] for c in gpu if c["name"] != "gpu"), gpu
+
+
 def test_gemm_check_host_reference():
     from gpumounter_amd.ops import probe
 
