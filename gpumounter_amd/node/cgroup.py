@@ -18,11 +18,12 @@ from __future__ import annotations
 
 import ctypes as C
 import errno
+import functools
 import glob
 import json
 import os
 from abc import ABC, abstractmethod
-from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
+from typing import Dict, FrozenSet, Iterable, List, Optional, Sequence, Set, Tuple
 
 from gpumounter_amd import _native
 from gpumounter_amd.models.device import DeviceNode
@@ -358,9 +359,16 @@ def attached_program(cgdir: str) -> Optional[List[int]]:
 
 def program_allows(prog: Sequence[int]) -> Set[Tuple[int, int]]:
     """(major, minor) pairs a device program grants for rw char access, over every constant it
-    compares against; the chained runtime program is modelled by runc's default list."""
-    consts = bpfvm.immediates(prog)
-    return bpfvm.allowed_pairs(list(prog), [(a, b) for a in consts for b in consts])
+    compares against; the chained runtime program is modelled by runc's default list. A pure
+    function of the instruction words, so the interpretation is memoised on them (the program
+    itself is still read back from the kernel on every call); callers get their own copy."""
+    return set(_program_allows(tuple(prog)))
+
+
+@functools.lru_cache(maxsize=256)
+def _program_allows(prog: Tuple[int, ...]) -> FrozenSet[Tuple[int, int]]:
+    consts = bpfvm.immediates(list(prog))
+    return frozenset(bpfvm.allowed_pairs(list(prog), [(a, b) for a in consts for b in consts]))
 
 
 def build_program(nodes: Sequence[DeviceNode], chained: bool) -> List[int]:

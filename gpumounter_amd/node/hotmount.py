@@ -191,6 +191,21 @@ class HotMount:
             self.writer.remove(t.target, nodes)
 
     # ------------------------------------------------------------------------ audit
+    def verify(self, pod: dict, gpus: Sequence[AmdGpu], container: str = "") -> List[AuditIssue]:
+        """Read back what an attach of ``gpus`` must have produced in every target container:
+        the device rules (as the kernel evaluates them) and the device nodes, /dev/kfd
+        included. A narrower, cheaper :meth:`audit` for the attach path."""
+        want = self.gpu_nodes(gpus) + [self.kfd()]
+        issues: List[AuditIssue] = []
+        for t in self.targets(pod, container):
+            allowed = self.backend.allowed(t.cgdir)
+            for n in want:
+                if (n.major, n.minor) not in allowed:
+                    issues.append(AuditIssue(t.ref.name, "missing_rule", n.path, n.major, n.minor))
+                if not self.writer.present(t.target, n):
+                    issues.append(AuditIssue(t.ref.name, "missing_node", n.path, n.major, n.minor))
+        return issues
+
     def audit(self, pod: dict, hot: Sequence[AmdGpu], base: Sequence[AmdGpu] = (),
               container: str = "") -> List[AuditIssue]:
         """Compare the expected state (from the ledger) with cgroup rules and /dev contents."""

@@ -327,6 +327,13 @@ class GpuMountService:
             try:
                 with trace.span("mount", gpus=len(new)):
                     self.hm.attach(pod, new, st.hot, st.own, req.container)
+                if self.cfg.attach_verify:
+                    with trace.span("verify"):
+                        self.faults.check("verify")
+                        issues = self.hm.verify(pod, new, req.container)
+                    if issues:
+                        raise MountError("attach did not take effect: " + ", ".join(
+                            f"{i.container}:{i.kind}:{i.path}" for i in issues[:4]))
             except (MountError, InjectedFault) as e:
                 _log.error("mount failed on %s/%s: %s", req.namespace, req.pod_name, e)
                 try:

@@ -755,3 +755,29 @@ def test_kubelet_restart_is_survived_without_waiting_for_grpc_backoff():
         assert code == 200, b
         assert await lc.audit("default", "t") == []
     run(body)
+
+
+def test_attach_verify_reads_back_rules_and_nodes_and_rolls_back_on_mismatch():
+    """attach_verify: the attach reads its device rules and nodes back (span "verify"); when
+    the kernel-side state does not match (here: the cgroup program reports nothing allowed),
+    the attach fails and is rolled back instead of reporting success."""
+    async def body(lc):
+        lc.tenant("t")
+        code, b = await lc.add("default", "t", 1)
+        assert code == 200, b
+        assert "verify" in {t["name"] for t in b["timings"]}
+        svc = lc.nodes["node-0"].worker.service
+        real = svc.hm.backend.allowed
+        svc.hm.backend.allowed = lambda cgdir: set()           # rules silently not in effect
+        try:
+            code, b2 = await lc.add("default", "t", 1)
+        finally:
+            svc.hm.backend.allowed = real
+        assert code == 500 and "did not take effect" in str(b2), b2
+        st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+        assert [g.uuid for g in st.hot] == [b["devices"][0]["uuid"]]   # only the first attach
+        assert await lc.audit("default", "t") == []
+        live = [p for p in lc.cluster.placeholders()
+                if not p["metadata"].get("deletionTimestamp")]
+        assert len(live) == 1
+    run(body, worker_overrides={"attach_verify": True})
