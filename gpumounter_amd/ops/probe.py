@@ -1,4 +1,5 @@
-"""Python side of the gfx950 post-attach validation kernels (native/hip/gm_probe.hip).
+"""Python side of the gfx950 post-attach validation kernels (native/hip/gm_probe.hip; the burn-in
+GEMM in native/hip/gm_gemm.hip).
 
 An attach is only useful if the tenant can actually run work on the GPU. After the node operations
 succeed, a tenant-side agent (or the bench ranks) call :func:`verify` on the newly attached devices:

@@ -1,0 +1,858 @@
+// gm_gemm.hip — the 256²-tile bf16 burn-in GEMM and its schedules, the bit-exact burn-in loop.
+// Part of libgm_probe.so (built with gm_probe.hip). Measurements: profiles/r1_gemm/.
+#include <chrono>
+
+#include "gm_probe.h"
+#include "gm_probe_common.h"
+
+namespace {
+
+// ------------------------------------------------------------------ MFMA bf16 GEMM, 256² tile
+// Throughput form of the burn-in GEMM: C[M,N] (bf16) = A[M,K] · Bt[N,K]ᵀ, both operands K-major
+// (the layout global_load_lds can stage without a transpose). Design (cdna_hip_programming.md §5):
+//   * 256×256 output tile, BK=64, 512 threads = 8 waves as 2(M)×4(N); each wave owns 128×64 as
+//     8×4 v_mfma_f32_16x16x32_bf16 accumulators (128 VGPRs), ~1 block per CU;
+//   * operands go HBM→LDS with global_load_lds_dwordx4 (no VGPR round trip), two LDS stages of
+//     64 KiB, the next stage's DMA issued before the current stage's MFMAs;
+//   * LDS image lane-linear (one 1 KiB wave instruction = 8 rows × 128 B); bank conflicts of the
+//     16-row ds_read_b128 fragment reads are removed by an XOR swizzle of the 16-B chunk index
+//     with (row>>1)&7, applied to the per-lane GLOBAL source address and to the LDS read address;
+//   * blockIdx remapped bijectively so each XCD runs a contiguous range of tiles, grouped 8 tile
+//     rows deep, so concurrently running blocks of one XCD share A/B panels in that XCD's L2.
+namespace g256 {
+constexpr int TM = 256, TN = 256, TK = 64, kThreads = 512, kGroupM = 8;
+constexpr int kTileBytes = TM * TK * 2;       // 32 KiB: one operand, one stage
+constexpr int kStageBytes = 2 * kTileBytes;   // A + Bt
+constexpr int kLdsBytes = 2 * kStageBytes;    // two stages: 128 KiB of the 160 KiB LDS
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+}  // namespace g256
+constexpr int kGemmNtDefault = 5;  // profiles/r1_gemm: V5 +2.9 % over V1 at 4096³, +0.9 % at 8192³
+
+// XCD-aware block → output tile: bijective for any grid size (the dispatcher deals block ids
+// round-robin over the 8 XCDs, so ids ≡ x mod 8 share XCD x's L2 and get a contiguous range of
+// tiles), then a GROUP_M-deep raster so co-resident tiles share A rows and B columns.
+__device__ __forceinline__ void gemm_tile_of(int M, int N, int& tm, int& tn) {
+  using namespace g256;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int ntm = M / TM, ntn = N / TN;
+  const int per_group = kGroupM * ntn;
+  const int first_m = (wgid / per_group) * kGroupM;
+  const int gsize = min(ntm - first_m, kGroupM);
+  tm = first_m + (wgid % per_group) % gsize;
+  tn = (wgid % per_group) / gsize;
+}
+
+// V = 0: per 32-deep k-step, 12 fragment reads → wait → 32 MFMAs.
+// V = 1: all 24 fragment reads of the 64-deep K-tile issued up front, so the second k-step's
+//        reads overlap the first step's MFMAs (+48 VGPRs).
+// V = 3: V1's schedule on v_mfma_f32_32x32x16_bf16 (same 128×64 per wave: 4×2 32² blocks).
+template <int V>
+__global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A,
+                                                    const __bf16* __restrict__ Bt,
+                                                    __bf16* __restrict__ C, int M, int N, int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+
+  // Staging: wave w moves 1 KiB chunks c = w + 8i (i = 0..3) of each operand's 256×64 tile.
+  // Lane l writes LDS byte c*1024 + l*16 = row 8c + (l>>3), slot l&7, which holds logical
+  // 16-B chunk (l&7) ^ ((row>>1)&7). (row>>1)&7 is the same for all i (rows differ by 64).
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
+  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
+  const size_t row64 = (size_t)64 * K;
+
+  auto stage = [&](int buf, int k0) {
+    char* base = lds + buf * kStageBytes + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row64 + k0),
+                                       (lds_void*)(base + i * 8192), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row64 + k0),
+                                       (lds_void*)(base + kTileBytes + i * 8192), 16, 0, 0);
+    }
+  };
+
+  // Fragment reads: lane l reads row (l&15) of a 16-row block at logical chunk 4kk + (l>>4).
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);  // kk = 0; kk = 1: ^ 64
+  const int a_off = wm * 128 * 128 + foff0;
+  const int b_off = kTileBytes + wn * 64 * 128 + foff0;
+
+  f32x4 acc[V == 3 ? 1 : 8][4];
+  f32x16 acc32[V == 3 ? 4 : 1][2];
+  if constexpr (V == 3) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int r32 = lane & 31, h32 = lane >> 5, sw32 = (r32 >> 1) & 7;
+  const int a32_off = wm * 128 * 128 + r32 * 128;
+  const int b32_off = kTileBytes + wn * 64 * 128 + r32 * 128;
+
+  const int nt = K / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) stage(cur ^ 1, (t + 1) * TK);
+    const char* sb = lds + cur * kStageBytes;
+    if constexpr (V == 0) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[8], bfr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 16 * 128) ^ (kk << 6)));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 16 * 128) ^ (kk << 6)));
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    } else if constexpr (V == 3) {
+      // 32x32x16 shape, same per-wave 128×64 tile: 4×2 blocks, 4 k16-steps per K-tile.
+      // Lane l reads row (l&31) of a 32-row block at logical chunk 2s + (l>>5).
+      bf16x8 af[4][4], bfr[4][2];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfr[st][j] = *reinterpret_cast<const bf16x8*>(sb + b32_off + j * 32 * 128 +
+                                                        ((((st * 2 + h32) ^ sw32)) << 4));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[st][i] = *reinterpret_cast<const bf16x8*>(sb + a32_off + i * 32 * 128 +
+                                                       ((((st * 2 + h32) ^ sw32)) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[st][i], bfr[st][j],
+                                                                  acc32[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+      bf16x8 af[2][8], bfr[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[kk][j] =
+              *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 16 * 128) ^ (kk << 6)));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          af[kk][i] =
+              *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 16 * 128) ^ (kk << 6)));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j],
+                                                                acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if constexpr (V == 3) {
+    // C/D map of 32x32x16: col = l&31, row = (reg&3) + 8(reg>>2) + 4(l>>5).
+    const int crow = tm * TM + wm * 128 + 4 * h32;
+    const int ccol = tn * TN + wn * 64 + r32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          C[(size_t)(crow + i * 32 + (r & 3) + 8 * (r >> 2)) * N + ccol + j * 32] =
+              (__bf16)acc32[i][j][r];
+    return;
+  }
+  // Epilogue: C/D map of 16x16x32: col = l&15, row = 4(l>>4) + reg.
+  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 64 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
+// V2 — quadrant phases with half-tile staging (same LDS budget, deeper pipeline). Measured
+// 7-8 % slower than V1 on MI355X (profiles/r1_gemm): kept as the tested counter-example.
+// Each stage's A and B tiles are split into row halves (lo = rows 0-127, hi = 128-255) of 16 KiB,
+// giving 8 half-tile slots in the 128 KiB. Wave (wm, wn) owns A rows {wm*64 + [0,64)} of both
+// halves and B rows {wn*32 + [0,32)} of both, i.e. four 64×32 output quadrants. A K-tile runs
+// as 4 phases, one quadrant each, in the order (Alo,Blo) (Alo,Bhi) (Ahi,Bhi) (Ahi,Blo). Operands
+// are carried in registers between neighbouring phases, so each half-tile is read from LDS in
+// exactly one phase.
+// Half-tiles are loaded in consumption order L[m] (m = 4t + {Alo, Blo, Bhi, Ahi}) into slot m%8.
+// Phase p issues L[p+6] and ends with a counted vmcnt that retires only what phase p+1 reads,
+// then a raw s_barrier. So 4-5 half-tiles (2 glds each) stay in flight across every barrier,
+// where V0/V1 drain to vmcnt(0) once per K-tile.
+// WAR: L[m+8] overwrites L[m]'s slot. It is issued in phase m+2, and L[m] was last read in
+// phase ≤ m, with a barrier between.
+__device__ __forceinline__ void vm_wait_glds(int n) {  // n = glds allowed in flight (uniform)
+  switch (n) {
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <int Q>
+struct QPhase {
+  static constexpr int value = Q;
+};
+
+__global__ __launch_bounds__(512) void k_gemm_nt256q(const __bf16* __restrict__ A,
+                                                     const __bf16* __restrict__ Bt,
+                                                     __bf16* __restrict__ C, int M, int N,
+                                                     int K) {
+  using namespace g256;
+  constexpr int kHalf = 16384, kAhead = 6;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+
+  // Half-tile staging: wave w moves 1 KiB chunks w and w+8 (rows 8c + (l>>3) of the half).
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
+  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
+  const size_t row64 = (size_t)64 * K, row128 = (size_t)128 * K;
+  const int nt = K / TK, last = 4 * nt - 1;
+
+  auto issue = [&](int m) {  // L[m]: kind m&3 = 0 Alo, 1 Blo, 2 Bhi, 3 Ahi; tile m>>2
+    const int kind = m & 3;
+    const __bf16* src = ((kind == 0 || kind == 3) ? a_src : b_src) +
+                        (kind >= 2 ? row128 : (size_t)0) + (m >> 2) * TK;
+    char* dst = lds + (m & 7) * kHalf + wave * 1024;
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void*)(src + row64), (lds_void*)(dst + 8192), 16, 0,
+                                     0);
+  };
+
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 64 * 128 + foff0;
+  const int b_off = wn * 32 * 128 + foff0;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[2][4], fbl[2][2], fbh[2][2];
+
+  auto read_a = [&](const char* base) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[kk][i] = *reinterpret_cast<const bf16x8*>(base + ((a_off + i * 2048) ^ (kk << 6)));
+  };
+  auto read_b = [&](const char* base, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[kk][j] = *reinterpret_cast<const bf16x8*>(base + ((b_off + j * 2048) ^ (kk << 6)));
+  };
+  auto mma = [&](f32x4 (&c)[4][2], bf16x8 (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], c[i][j], 0, 0,
+                                                            0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  auto phase = [&](auto qc, int t) {
+    constexpr int q = decltype(qc)::value;
+    const int p = 4 * t + q;
+    const char* slot = lds + ((4 * t) & 7) * kHalf;  // Alo of tile t; +1..3 halves follow
+    if constexpr (q == 0) {
+      read_b(slot + 1 * kHalf, fbl);
+      read_a(slot + 0 * kHalf);
+    } else if constexpr (q == 1) {
+      read_b(slot + 2 * kHalf, fbh);
+    } else if constexpr (q == 2) {
+      read_a(slot + 3 * kHalf);
+    }
+    if (p + kAhead <= last) issue(p + kAhead);
+    if constexpr (q == 0) mma(acc[0][0], fbl);
+    if constexpr (q == 1) mma(acc[0][1], fbh);
+    if constexpr (q == 2) mma(acc[1][1], fbh);
+    if constexpr (q == 3) mma(acc[1][0], fbl);
+    if (p < last) {
+      // phase p+1 reads up to L[need]: Bhi(t) after q0, Ahi(t) after q1/q2, Blo(t+1) after q3
+      constexpr int need_rel = q == 0 ? 2 : (q == 3 ? 5 : 3);
+      const int issued = min(p + kAhead, last);
+      vm_wait_glds(2 * (issued - (4 * t + need_rel)));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  };
+
+  // Prologue: L[0..6] in flight; retire L[0], L[1] (Alo, Blo of tile 0).
+  const int pre = min(kAhead, last);
+  for (int m = 0; m <= pre; ++m) issue(m);
+  vm_wait_glds(2 * (pre - 1));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nt; ++t) {
+    phase(QPhase<0>{}, t);
+    phase(QPhase<1>{}, t);
+    phase(QPhase<2>{}, t);
+    phase(QPhase<3>{}, t);
+  }
+
+  const int crow = tm * TM + wm * 64 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 32 + (lane & 15);
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            C[(size_t)(crow + x * 128 + i * 16 + r) * N + ccol + y * 128 + j * 16] =
+                (__bf16)acc[x][y][i][j][r];
+}
+
+// V4 — measured 7-13 % slower than V1 on MI355X (profiles/r1_gemm).
+// 4 waves (2×2), each 128×128 = 8×8 16x16x32 accumulators (256 fp32/lane: the MFMA
+// destinations live in AGPRs, 1 wave per SIMD). A fragment read feeds 8 MFMAs instead of 4,
+// so LDS read traffic per K-tile drops by a third against V1; latency hiding is then
+// up to the single wave's own schedule: all 32 fragment reads of the K-tile are issued
+// before its 128 MFMAs.
+__global__ __launch_bounds__(256) void k_gemm_nt256w4(const __bf16* __restrict__ A,
+                                                      const __bf16* __restrict__ Bt,
+                                                      __bf16* __restrict__ C, int M, int N,
+                                                      int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+
+  // Staging: wave w moves chunks c = w + 4i (i = 0..7), rows 8c + (l>>3): rows differ by 32
+  // between i, so (row>>1)&7 is again the same for all of a lane's chunks.
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
+  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
+  const size_t row32 = (size_t)32 * K;
+  auto stage = [&](int buf, int k0) {
+    char* base = lds + buf * kStageBytes + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row32 + k0),
+                                       (lds_void*)(base + i * 4096), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row32 + k0),
+                                       (lds_void*)(base + kTileBytes + i * 4096), 16, 0, 0);
+    }
+  };
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 128 * 128 + foff0;
+  const int b_off = kTileBytes + wn * 128 * 128 + foff0;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nt = K / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) stage(cur ^ 1, (t + 1) * TK);
+    const char* sb = lds + cur * kStageBytes;
+    bf16x8 af[2][8], bfr[2][8];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 2048) ^ (kk << 6)));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        af[kk][i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 2048) ^ (kk << 6)));
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 128 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
+// Buffer-resource LDS DMA (buffer_load_dwordx4 … lds): gfx9-family resource word 3 =
+// 0x00020000 (raw, untyped), stride 0, num_records = size in bytes (range-checked).
+typedef __attribute__((address_space(3))) void lds_any;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+// V5 — V1's geometry with a local-read prefetch across the barrier. The second k-step's MFMAs
+// of tile t are deferred past the barrier, so they run while the first k-step fragments of
+// tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
+// register use stays at two fragment sets (like V1). The barrier sits mid-tile, so the next
+// tile's DMA is issued right after it.
+template <bool kBufDma>
+__global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ A,
+                                                     const __bf16* __restrict__ Bt,
+                                                     __bf16* __restrict__ C, int M, int N,
+                                                     int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
+  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
+  const size_t row64 = (size_t)64 * K;
+  // kBufDma (V7): the same DMA as buffer_load … lds from SGPR resources plus one 32-bit
+  // per-lane offset, instead of eight per-lane 64-bit source pointers.
+  const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc(A + (size_t)tm * TM * K, (uint32_t)TM * K * 2);
+  const __amdgpu_buffer_rsrc_t b_rsrc =
+      make_rsrc(Bt + (size_t)tn * TN * K, (uint32_t)TN * K * 2);
+  const int lane_off = (srow * K + schunk * 8) * 2;
+  auto stage = [&](int buf, int k0) {
+    char* base = lds + buf * kStageBytes + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (kBufDma) {
+        const int soff = __builtin_amdgcn_readfirstlane((i * 64 * K + k0) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)(base + i * 8192), 16,
+                                                 lane_off, soff, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)(base + kTileBytes + i * 8192),
+                                                 16, lane_off, soff, 0, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row64 + k0),
+                                         (lds_void*)(base + i * 8192), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row64 + k0),
+                                         (lds_void*)(base + kTileBytes + i * 8192), 16, 0, 0);
+      }
+    }
+  };
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 128 * 128 + foff0;
+  const int b_off = kTileBytes + wn * 64 * 128 + foff0;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a0[8], b0[4], a1[8], b1[4];
+  auto read = [&](const char* sb, int kk, bf16x8 (&af)[8], bf16x8 (&bf)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 2048) ^ (kk << 6)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 2048) ^ (kk << 6)));
+  };
+  auto mma = [&](bf16x8 (&af)[8], bf16x8 (&bf)[4]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nt = K / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // Waits go through __builtin_amdgcn_s_waitcnt (gfx9 simm16: vmcnt[3:0]|expcnt[6:4]|
+  // lgkmcnt[11:8]|vmcnt[5:4]<<14), not inline asm, so the compiler's own wait insertion knows
+  // the counters are clear and adds no lgkmcnt(0) in front of the MFMAs.
+  constexpr int kWaitLgkm0 = 0xC07F, kWaitVm0Lgkm0 = 0x0070;
+  // Tile t+1's DMA is issued right after the barrier that frees its buffer (mid-tile t-1), so
+  // it has a whole tile of MFMAs (64 per wave) to land before the vmcnt(0) that retires it.
+  if (nt > 1) stage(1, TK);
+  read(lds, 0, a0, b0);
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    const char* sb = lds + cur * kStageBytes;
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // a0/b0 (read behind the last 32 MFMAs) are in
+    read(sb, 1, a1, b1);
+    mma(a0, b0);
+    __builtin_amdgcn_s_waitcnt(kWaitVm0Lgkm0);  // tile t+1 landed; our reads of `cur` done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nt) stage(cur, (t + 2) * TK);   // every wave is past its reads of `cur`
+    if (t + 1 < nt) read(lds + (cur ^ 1) * kStageBytes, 0, a0, b0);
+    mma(a1, b1);
+  }
+
+  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 64 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
+// V6 — V4's geometry (4 waves × 128², AGPR accumulators) on V5's schedule.
+// (V5:) V1's geometry with a local-read prefetch across the barrier. The second k-step's MFMAs
+// of tile t are deferred past the barrier, so they run while the first k-step fragments of
+// tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
+// register use stays at two fragment sets (like V1). The barrier sits mid-tile, so the next
+// tile's DMA is issued right after it.
+__global__ __launch_bounds__(256) void k_gemm_nt256w4p(const __bf16* __restrict__ A,
+                                                     const __bf16* __restrict__ Bt,
+                                                     __bf16* __restrict__ C, int M, int N,
+                                                     int K) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  // buffer_load … lds: the block's A/B panels as buffer resources (SGPRs), one 32-bit per-lane
+  // byte offset, the per-load row/k offset in soffset (SGPR). Two VGPRs of addressing instead
+  // of sixteen 64-bit pointers (which spilled), and range-checked: an out-of-panel read
+  // returns zeros instead of faulting.
+  const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc(A + (size_t)tm * TM * K, (uint32_t)TM * K * 2);
+  const __amdgpu_buffer_rsrc_t b_rsrc =
+      make_rsrc(Bt + (size_t)tn * TN * K, (uint32_t)TN * K * 2);
+  const int lane_off = (srow * K + schunk * 8) * 2;
+  auto stage = [&](int buf, int k0) {
+    char* base = lds + buf * kStageBytes + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int soff = __builtin_amdgcn_readfirstlane((i * 32 * K + k0) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)(base + i * 4096), 16, lane_off,
+                                               soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)(base + kTileBytes + i * 4096),
+                                               16, lane_off, soff, 0, 0);
+    }
+  };
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 128 * 128 + foff0;
+  const int b_off = kTileBytes + wn * 128 * 128 + foff0;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  auto read = [&](const char* sb, int kk, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 2048) ^ (kk << 6)));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 2048) ^ (kk << 6)));
+  };
+  auto mma = [&](bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nt = K / TK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // Waits go through __builtin_amdgcn_s_waitcnt (gfx9 simm16: vmcnt[3:0]|expcnt[6:4]|
+  // lgkmcnt[11:8]|vmcnt[5:4]<<14), not inline asm, so the compiler's own wait insertion knows
+  // the counters are clear and adds no lgkmcnt(0) in front of the MFMAs.
+  constexpr int kWaitLgkm0 = 0xC07F, kWaitVm0Lgkm0 = 0x0070;
+  // Tile t+1's DMA is issued right after the barrier that frees its buffer (mid-tile t-1), so
+  // it has a whole tile of MFMAs (64 per wave) to land before the vmcnt(0) that retires it.
+  if (nt > 1) stage(1, TK);
+  read(lds, 0, a0, b0);
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    const char* sb = lds + cur * kStageBytes;
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // a0/b0 (read behind the last 32 MFMAs) are in
+    read(sb, 1, a1, b1);
+    mma(a0, b0);
+    __builtin_amdgcn_s_waitcnt(kWaitVm0Lgkm0);  // tile t+1 landed; our reads of `cur` done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nt) stage(cur, (t + 2) * TK);   // every wave is past its reads of `cur`
+    if (t + 1 < nt) read(lds + (cur ^ 1) * kStageBytes, 0, a0, b0);
+    mma(a1, b1);
+  }
+
+  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 128 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
+}
+
+// Deterministic uniform [-1, 1) bf16 fill (random operands: zero-filled ones overstate a GEMM).
+__global__ __launch_bounds__(256) void k_fill_bf16(__bf16* dst, size_t n, uint32_t seed) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    dst[i] = (__bf16)((float)(h >> 8) * (2.0f / 16777216.0f) - 1.0f);
+  }
+}
+
+// Number of 16-B words that differ between a and b: one ballot + popcount per wave, one
+// atomic per wave.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_count_diff(const u32x4* __restrict__ a,
+                                                    const u32x4* __restrict__ b, size_t n,
+                                                    unsigned long long* count) {
+  unsigned long long local = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const u32x4 x = __builtin_nontemporal_load(&a[i]), y = __builtin_nontemporal_load(&b[i]);
+    local += (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
+  }
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, kWave);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
+}
+
+}  // namespace
+
+extern "C" {
+
+int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C, int M, int N,
+                             int K, void* stream) {
+  using namespace g256;
+  if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % TK) return (int)hipErrorInvalidValue;
+  const dim3 grid((M / TM) * (N / TN)), block(kThreads);
+  switch (variant) {
+    case 0:
+      hipLaunchKernelGGL(k_gemm_nt256<0>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 1:
+      hipLaunchKernelGGL(k_gemm_nt256<1>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 3:
+      hipLaunchKernelGGL(k_gemm_nt256<3>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 5:
+      hipLaunchKernelGGL(k_gemm_nt256p<false>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 7:
+      hipLaunchKernelGGL(k_gemm_nt256p<true>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 6:
+      hipLaunchKernelGGL(k_gemm_nt256w4p, grid, dim3(256), 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 4:
+      hipLaunchKernelGGL(k_gemm_nt256w4, grid, dim3(256), 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_gemm_nt256q, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+int gm_probe_gemm_nt(const void* A, const void* Bt, void* C, int M, int N, int K,
+                     void* stream) {
+  return gm_probe_gemm_nt_variant(kGemmNtDefault, A, Bt, C, M, N, K, stream);
+}
+
+int gm_probe_gemm_nt_tflops(int dev, int M, int N, int K, int iters, double* tflops) {
+  using namespace g256;
+  *tflops = 0;
+  if (iters <= 0 || M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % TK)
+    return (int)hipErrorInvalidValue;
+  DeviceGuard g(dev);
+  if (!g.ok) return (int)hipErrorInvalidDevice;
+  DevBuf da, db, dc;
+  GM_CHECK(da.alloc((size_t)M * K * 2));
+  GM_CHECK(db.alloc((size_t)N * K * 2));
+  GM_CHECK(dc.alloc((size_t)M * N * 2));
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, (__bf16*)da.p, (size_t)M * K,
+                     0x1234u);
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, (__bf16*)db.p, (size_t)N * K,
+                     0x9876u);
+  Events ev;
+  GM_CHECK(ev.create());
+  int e = gm_probe_gemm_nt(da.p, db.p, dc.p, M, N, K, nullptr);  // warm-up
+  if (!e) e = (int)hipEventRecord(ev.e0, nullptr);
+  for (int i = 0; i < iters && !e; ++i) e = gm_probe_gemm_nt(da.p, db.p, dc.p, M, N, K, nullptr);
+  if (!e) e = (int)hipEventRecord(ev.e1, nullptr);
+  if (!e) e = (int)hipEventSynchronize(ev.e1);
+  float ms = 0;
+  if (!e) e = (int)hipEventElapsedTime(&ms, ev.e0, ev.e1);
+  if (!e && ms > 0) *tflops = 2.0 * M * N * (double)K * iters / (ms * 1e-3) / 1e12;
+  return e;
+}
+
+int gm_probe_burn_in(int dev, int n, double seconds, double* tflops, uint64_t* mismatches,
+                     int* iters) {
+  using namespace g256;
+  *tflops = 0;
+  *mismatches = 0;
+  *iters = 0;
+  if (n <= 0 || n % TM || seconds <= 0) return (int)hipErrorInvalidValue;
+  DeviceGuard g(dev);
+  if (!g.ok) return (int)hipErrorInvalidDevice;
+  const size_t elems = (size_t)n * n;
+  DevBuf da, db, dref, dc, dcount;
+  GM_CHECK(da.alloc(elems * 2));
+  GM_CHECK(db.alloc(elems * 2));
+  GM_CHECK(dref.alloc(elems * 2));
+  GM_CHECK(dc.alloc(elems * 2));
+  GM_CHECK(dcount.alloc(sizeof(unsigned long long)));
+  GM_CHECK(hipMemset(dcount.p, 0, sizeof(unsigned long long)));
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, (__bf16*)da.p, elems, 0x5151u);
+  hipLaunchKernelGGL(k_fill_bf16, dim3(4096), dim3(256), 0, 0, (__bf16*)db.p, elems, 0xa3a3u);
+  int e = gm_probe_gemm_nt(da.p, db.p, dref.p, n, n, n, nullptr);  // the reference result
+  if (e) return e;
+  Events ev;
+  GM_CHECK(ev.create());
+  GM_CHECK(hipEventRecord(ev.e0, nullptr));
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t vec = elems / 8;  // 16-B compares
+  int done = 0;
+  // Batches of 8 GEMMs, each result compared bit-for-bit with the first one: the kernel is
+  // deterministic (fixed reduction order, no atomics), so any difference is a hardware fault.
+  while (!e) {
+    for (int i = 0; i < 8 && !e; ++i) {
+      e = gm_probe_gemm_nt(da.p, db.p, dc.p, n, n, n, nullptr);
+      if (!e) {
+        hipLaunchKernelGGL(k_count_diff, dim3(2048), dim3(256), 0, 0,
+                           (const u32x4*)dc.p, (const u32x4*)dref.p, vec,
+                           (unsigned long long*)dcount.p);
+        e = (int)hipGetLastError();
+      }
+      ++done;
+    }
+    if (!e) e = (int)hipDeviceSynchronize();
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el >= seconds) break;
+  }
+  if (!e) e = (int)hipEventRecord(ev.e1, nullptr);
+  if (!e) e = (int)hipEventSynchronize(ev.e1);
+  float ms = 0;
+  if (!e) e = (int)hipEventElapsedTime(&ms, ev.e0, ev.e1);
+  unsigned long long bad = 0;
+  if (!e) e = (int)hipMemcpy(&bad, dcount.p, sizeof(bad), hipMemcpyDeviceToHost);
+  if (e) return e;
+  *iters = done;
+  *mismatches = bad;
+  // compare kernels are included in the wall time; they move 2 × n² × 2 B per GEMM (< 1 %)
+  if (ms > 0) *tflops = 2.0 * n * (double)n * n * done / (ms * 1e-3) / 1e12;
+  return 0;
+}
+
+}  // extern "C"
