@@ -464,6 +464,36 @@ __global__ __launch_bounds__(256) void k_gemm_nt256w4(const __bf16* __restrict__
         C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
 }
 
+// Coalesced epilogue for one 16×16 accumulator tile. Lane l = 16q + 4a + p holds rows
+// 4q..4q+3 of column 4a+p. Two quad-local DPP exchanges (xor 1, xor 2) on packed bf16 pairs
+// transpose each 4×4 block, so lane p ends up with row 4q+p, columns 4a..4a+3, and stores them
+// with one 8-byte store. That is 32 stores per wave instead of 128 two-byte ones.
+__device__ __forceinline__ uint32_t bf16_bits(float x) {
+  const __bf16 h = (__bf16)x;
+  return (uint32_t)__builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ void store_tile_quad(__bf16* __restrict__ C, size_t ld, int row0,
+                                                int col0, const f32x4& v, int lane) {
+  const int p = lane & 3, p1 = p & 1, p2 = (p >> 1) & 1;
+  const uint32_t b0 = bf16_bits(v[0]), b1 = bf16_bits(v[1]), b2 = bf16_bits(v[2]),
+                 b3 = bf16_bits(v[3]);
+  // stage 1 (partner p^1): keep rows p1, p1+2 of my column; send the other two rows
+  const uint32_t send1 = p1 ? (b0 | (b2 << 16)) : (b1 | (b3 << 16));
+  const uint32_t recv1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)send1, 0xB1, 0xF, 0xF, false);
+  const uint32_t ka = p1 ? b1 : b0, kb = p1 ? b3 : b2;         // rows p1, p1+2 at column p
+  const uint32_t ra = recv1 & 0xFFFF, rb = recv1 >> 16;         // same rows at column p^1
+  const uint32_t rowA = p1 ? (ra | (ka << 16)) : (ka | (ra << 16));  // row p1, cols (p&~1)+0,1
+  const uint32_t rowB = p1 ? (rb | (kb << 16)) : (kb | (rb << 16));  // row p1+2
+  // stage 2 (partner p^2): keep row p = p1 + 2*p2, send the other one
+  const uint32_t keep2 = p2 ? rowB : rowA, send2 = p2 ? rowA : rowB;
+  const uint32_t recv2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)send2, 0x4E, 0xF, 0xF, false);
+  uint2 out;
+  out.x = p2 ? recv2 : keep2;                                  // columns 4a+0, 4a+1
+  out.y = p2 ? keep2 : recv2;                                  // columns 4a+2, 4a+3
+  const int q = lane >> 4, a = (lane >> 2) & 3;
+  *reinterpret_cast<uint2*>(C + (size_t)(row0 + 4 * q + p) * ld + col0 + 4 * a) = out;
+}
+
 // Buffer-resource LDS DMA (buffer_load_dwordx4 … lds): gfx9-family resource word 3 =
 // 0x00020000 (raw, untyped), stride 0, num_records = size in bytes (range-checked).
 typedef __attribute__((address_space(3))) void lds_any;
@@ -477,7 +507,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 // tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
 // register use stays at two fragment sets (like V1). The barrier sits mid-tile, so the next
 // tile's DMA is issued right after it.
-template <bool kBufDma>
+template <bool kBufDma, bool kQuadStore = false>
 __global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ A,
                                                      const __bf16* __restrict__ Bt,
                                                      __bf16* __restrict__ C, int M, int N,
@@ -573,6 +603,15 @@ __global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ 
     mma(a1, b1);
   }
 
+  if constexpr (kQuadStore) {  // V8: transposed in quads, 8-byte stores
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        store_tile_quad(C, (size_t)N, tm * TM + wm * 128 + i * 16, tn * TN + wn * 64 + j * 16,
+                        acc[i][j], lane);
+    return;
+  }
   const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
   const int ccol = tn * TN + wn * 64 + (lane & 15);
 #pragma unroll
@@ -744,6 +783,10 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
       break;
     case 7:
       hipLaunchKernelGGL(k_gemm_nt256p<true>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 8:
+      hipLaunchKernelGGL((k_gemm_nt256p<false, true>), grid, block, 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     case 6:
