@@ -32,6 +32,10 @@ class Metrics:
         self.placement_mismatch = Counter("gm_placement_mismatch_total",
                                           "device plugin chose a set other than the preferred one",
                                           registry=r)
+        self.verify_failures = Counter("gm_attach_verify_failures_total",
+                                       "attaches rolled back because the read-back "
+                                       "(attach_verify) found rules or nodes missing",
+                                       registry=r)
         self.gpu_busy = Gauge("gm_gpu_processes", "processes on a GPU (amdsmi)", ["gpu"],
                               registry=r)
         self.plugin_rpcs = Counter("gm_device_plugin_rpcs_total",

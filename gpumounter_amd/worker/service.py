@@ -332,6 +332,7 @@ class GpuMountService:
                         self.faults.check("verify")
                         issues = self.hm.verify(pod, new, req.container)
                     if issues:
+                        self.metrics.verify_failures.inc()
                         raise MountError("attach did not take effect: " + ", ".join(
                             f"{i.container}:{i.kind}:{i.path}" for i in issues[:4]))
             except (MountError, InjectedFault) as e:

@@ -774,6 +774,7 @@ def test_attach_verify_reads_back_rules_and_nodes_and_rolls_back_on_mismatch():
         finally:
             svc.hm.backend.allowed = real
         assert code == 500 and "did not take effect" in str(b2), b2
+        assert svc.metrics.verify_failures._value.get() == 1      # noqa: SLF001
         st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
         assert [g.uuid for g in st.hot] == [b["devices"][0]["uuid"]]   # only the first attach
         assert await lc.audit("default", "t") == []
