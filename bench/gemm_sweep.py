@@ -41,7 +41,7 @@ def timed(fn, iters):
     return a.elapsed_time(b) / iters * 1e-3
 
 
-VARIANTS = (5, 8)
+VARIANTS = (2, 5, 9)
 
 
 def main():

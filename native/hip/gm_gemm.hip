@@ -502,6 +502,154 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
                                            0x00020000);
 }
 
+// V9 — V2's quadrant phases with the next phase's operand read into registers during the
+// current phase's MFMAs. So the counted vmcnt at the end of phase p retires what phase p+2 reads.
+// Reads per phase: q0 reads Bhi(t), q1 reads Ahi(t), q3 reads Alo(t+1) and Blo(t+1). Blo(t) is
+// still in use in q3, so Blo alternates between two register sets by tile parity. The tile
+// loop is unrolled by two so every index stays compile-time.
+// WAR: L[m+8] is issued in phase m+2; L[m] was last read in phase ≤ m-1, with barriers between.
+__global__ __launch_bounds__(512) void k_gemm_nt256q2(const __bf16* __restrict__ A,
+                                                      const __bf16* __restrict__ Bt,
+                                                      __bf16* __restrict__ C, int M, int N,
+                                                      int K) {
+  using namespace g256;
+  constexpr int kHalf = 16384, kAhead = 6;
+  constexpr int kWaitLgkm0 = 0xC07F;
+  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int tm, tn;
+  gemm_tile_of(M, N, tm, tn);
+  const int srow = 8 * wave + (lane >> 3);
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
+  // buffer_load … lds from SGPR resources: one 32-bit per-lane offset (global_load_lds with
+  // per-lane 64-bit pointers spilled 16 VGPRs here)
+  const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc(A + (size_t)tm * TM * K, (uint32_t)TM * K * 2);
+  const __amdgpu_buffer_rsrc_t b_rsrc =
+      make_rsrc(Bt + (size_t)tn * TN * K, (uint32_t)TN * K * 2);
+  const int lane_off = (srow * K + schunk * 8) * 2;
+  const int nt = K / TK, last = 4 * nt - 1;
+  auto issue = [&](int m) {  // L[m]: kind m&3 = 0 Alo, 1 Blo, 2 Bhi, 3 Ahi; tile m>>2
+    const int kind = m & 3;
+    const int soff = __builtin_amdgcn_readfirstlane(((kind >= 2 ? 128 * K : 0) + (m >> 2) * TK) * 2);
+    char* dst = lds + (m & 7) * kHalf + wave * 1024;
+    if (kind == 0 || kind == 3) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)dst, 16, lane_off, soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)(dst + 8192), 16, lane_off,
+                                               soff + 64 * K * 2, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)dst, 16, lane_off, soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)(dst + 8192), 16, lane_off,
+                                               soff + 64 * K * 2, 0, 0);
+    }
+  };
+  const int frow = lane & 15;
+  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
+  const int a_off = wm * 64 * 128 + foff0;
+  const int b_off = wn * 32 * 128 + foff0;
+  auto slot = [&](int m) -> const char* { return lds + (m & 7) * kHalf; };
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fal[2][4], fah[2][4], fbl[2][2][2], fbh[2][2];
+  auto read_a = [&](const char* base, bf16x8 (&fa)[2][4]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[kk][i] = *reinterpret_cast<const bf16x8*>(base + ((a_off + i * 2048) ^ (kk << 6)));
+  };
+  auto read_b = [&](const char* base, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[kk][j] = *reinterpret_cast<const bf16x8*>(base + ((b_off + j * 2048) ^ (kk << 6)));
+  };
+  auto mma = [&](f32x4 (&c)[4][2], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], c[i][j], 0, 0,
+                                                            0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // end of phase p: retire what phase p+1 will read (L[p+3]; after q1 nothing new: L[p+2])
+  auto end_phase = [&](int p, int need) {
+    if (p >= last) return;
+    vm_wait_glds(2 * (min(p + kAhead, last) - min(need, last)));
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto tile = [&](auto par_c, int t) {
+    constexpr int par = decltype(par_c)::value;
+    const int p0 = 4 * t;
+    // q0: (Alo, Blo); read Bhi(t)
+    read_b(slot(p0 + 2), fbh);
+    if (p0 + kAhead <= last) issue(p0 + kAhead);
+    mma(acc[0][0], fal, fbl[par]);
+    end_phase(p0, p0 + 3);
+    // q1: (Alo, Bhi); read Ahi(t)
+    read_a(slot(p0 + 3), fah);
+    if (p0 + 1 + kAhead <= last) issue(p0 + 1 + kAhead);
+    mma(acc[0][1], fal, fbh);
+    end_phase(p0 + 1, p0 + 3);
+    // q2: (Ahi, Bhi)
+    if (p0 + 2 + kAhead <= last) issue(p0 + 2 + kAhead);
+    mma(acc[1][1], fah, fbh);
+    end_phase(p0 + 2, p0 + 5);
+    // q3: (Ahi, Blo); read Alo(t+1), Blo(t+1)
+    if (t + 1 < nt) {
+      read_a(slot(p0 + 4), fal);
+      read_b(slot(p0 + 5), fbl[par ^ 1]);
+    }
+    if (p0 + 3 + kAhead <= last) issue(p0 + 3 + kAhead);
+    mma(acc[1][0], fah, fbl[par]);
+    end_phase(p0 + 3, p0 + 6);
+  };
+
+  // Prologue: L[0..6] in flight; retire L[0..2] (q0 of tile 0 reads Bhi(0) = L[2]).
+  const int pre = min(kAhead, last);
+  for (int m = 0; m <= pre; ++m) issue(m);
+  vm_wait_glds(2 * (pre - min(2, last)));
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  read_a(slot(0), fal);
+  read_b(slot(1), fbl[0]);
+  for (int t = 0; t < nt; t += 2) {
+    tile(QPhase<0>{}, t);
+    if (t + 1 < nt) tile(QPhase<1>{}, t + 1);
+  }
+
+  const int crow = tm * TM + wm * 64 + 4 * (lane >> 4);
+  const int ccol = tn * TN + wn * 32 + (lane & 15);
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            C[(size_t)(crow + x * 128 + i * 16 + r) * N + ccol + y * 128 + j * 16] =
+                (__bf16)acc[x][y][i][j][r];
+}
+
 // V5 — V1's geometry with a local-read prefetch across the barrier. The second k-step's MFMAs
 // of tile t are deferred past the barrier, so they run while the first k-step fragments of
 // tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
@@ -783,6 +931,10 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
       break;
     case 7:
       hipLaunchKernelGGL(k_gemm_nt256p<true>, grid, block, 0, (hipStream_t)stream,
+                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
+      break;
+    case 9:
+      hipLaunchKernelGGL(k_gemm_nt256q2, grid, block, 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     case 8:

@@ -129,7 +129,7 @@ def test_mfma_gemm_asymmetric_identity():
     assert torch.equal(c, b.float())
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 192), (1280, 1024, 640)])
 def test_gemm_nt256_matches_torch_fp32(m, n, k, variant):
     """The 256²-tile global_load_lds GEMM (odd tile counts exercise the XCD remap's remainder
@@ -147,7 +147,7 @@ def test_gemm_nt256_matches_torch_fp32(m, n, k, variant):
     assert (err <= ref.abs() * 2 ** -8 + 1e-3 * k ** 0.5).all(), err.max().item()
 
 
-@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_gemm_nt256_asymmetric_identity(variant):
     """A = I with an asymmetric Bt: C must equal Btᵀ exactly (catches row/col swaps, swizzle
     mismatches between the staged source and the LDS read)."""
