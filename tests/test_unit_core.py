@@ -189,3 +189,30 @@ def test_fast_to_dict_matches_json_format():
     ]
     for m in msgs:
         assert to_dict(m) == ref(m), type(m).__name__
+
+
+def test_probe_gemm_wrappers_validate_before_touching_the_gpu():
+    """The GEMM wrappers reject what the kernels' grids assume away (tile multiples, dtype,
+    layout) on the host, before any HIP call, so a bad shape can never reach a launch."""
+    import pytest
+    import torch
+
+    from gpumounter_amd.ops import probe
+
+    bf = torch.bfloat16
+    cases = [
+        (torch.zeros(256, 64, dtype=torch.float32), torch.zeros(256, 64, dtype=bf)),   # dtype
+        (torch.zeros(256, 64, dtype=bf), torch.zeros(64, 256, dtype=bf).t()),          # layout
+        (torch.zeros(250, 64, dtype=bf), torch.zeros(256, 64, dtype=bf)),              # M % 256
+        (torch.zeros(256, 64, dtype=bf), torch.zeros(200, 64, dtype=bf)),              # N % 256
+        (torch.zeros(256, 48, dtype=bf), torch.zeros(256, 48, dtype=bf)),              # K % 64
+        (torch.zeros(256, 64, dtype=bf), torch.zeros(256, 128, dtype=bf)),             # K mismatch
+    ]
+    for a, bt in cases:
+        with pytest.raises(probe.ProbeError):
+            probe.gemm_nt(a, bt)
+    a, bt = torch.zeros(256, 64, dtype=bf), torch.zeros(256, 64, dtype=bf)
+    with pytest.raises(probe.ProbeError):
+        probe.gemm_nt(a, bt, out=torch.zeros(256, 256, dtype=torch.float32))
+    with pytest.raises(probe.ProbeError):
+        probe.gemm_bf16(torch.zeros(64, 30, dtype=bf), torch.zeros(30, 64, dtype=bf))
