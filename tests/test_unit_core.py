@@ -216,3 +216,9 @@ def test_probe_gemm_wrappers_validate_before_touching_the_gpu():
         probe.gemm_nt(a, bt, out=torch.zeros(256, 256, dtype=torch.float32))
     with pytest.raises(probe.ProbeError):
         probe.gemm_bf16(torch.zeros(64, 30, dtype=bf), torch.zeros(30, 64, dtype=bf))
+    # the native entry points check their arguments before selecting a device
+    for n, secs in ((300, 1.0), (256, 0.0), (-256, 1.0)):
+        with pytest.raises(probe.ProbeError):
+            probe.burn_in(0, secs, n)
+    with pytest.raises(probe.ProbeError):
+        probe.gemm_tflops(0, 256, 256, 100, 1)
