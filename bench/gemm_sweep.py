@@ -4,7 +4,7 @@ Same uniform [-1, 1) bf16 operands for both (zero-filled operands overstate a GE
 through DVFS, cdna_hip_programming.md §5.4 rule 25). Variants are timed in interleaved rounds in
 one process (rule 24); the JSON reports median and best TF/s per variant and shape, plus the
 max error of ours against torch's fp32 product on a 1024³ slice. Run on the GPU box:
-``python bench/gemm_sweep.py [--rounds 5]``.
+``python bench/gemm_sweep.py [--rounds 5] [--variants 1,5,9]``.
 """
 import argparse
 import ctypes as C
@@ -41,14 +41,17 @@ def timed(fn, iters):
     return a.elapsed_time(b) / iters * 1e-3
 
 
-VARIANTS = (2, 5, 9)
+VARIANTS = (1, 5)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sizes", default="4096,8192")
+    ap.add_argument("--variants", default=",".join(map(str, VARIANTS)),
+                    help="schedules of gm_probe_gemm_nt_variant to time (0-9; 5 = default)")
     args = ap.parse_args()
+    variants_sel = [int(v) for v in args.variants.split(",") if v]
     out = {"device": torch.cuda.get_device_name(0), "TFLOPs": {}, "numerics": {}}
     g = torch.Generator(device="cuda").manual_seed(0)
     for n in [int(x) for x in args.sizes.split(",")]:
@@ -56,7 +59,7 @@ def main():
         bt = (torch.rand(n, n, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
         b = bt.t().contiguous()
         c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
-        variants = {f"gm_gemm_nt_v{v}": (lambda v=v: ours(v, a, bt, c)) for v in VARIANTS}
+        variants = {f"gm_gemm_nt_v{v}": (lambda v=v: ours(v, a, bt, c)) for v in variants_sel}
         variants.update({
             "torch_nt": lambda: torch.matmul(a, bt.t(), out=c),
             "torch_nn": lambda: torch.matmul(a, b, out=c),
@@ -77,7 +80,7 @@ def main():
     bt = (torch.rand(1024, 1024, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
     ref = a.float() @ bt.float().t()
     checks = {f"gm_gemm_nt_v{v}": (lambda v=v: ours(v, a, bt, torch.empty_like(a)))
-              for v in VARIANTS}
+              for v in variants_sel}
     checks["torch_nt"] = lambda: torch.matmul(a, bt.t())
     for k, fn in checks.items():
         err = (fn().float() - ref).abs().max().item()
