@@ -63,7 +63,8 @@ async def run(args) -> None:
     info = {"api_url": lc.api_url, "pid": os.getpid(),
             "nodes": {name: {"kubelet_socket": h.kubelet.socket_path,
                              "cgroup_root": h.node.cgroup_root,
-                             "rootfs_root": h.node.rootfs_root}
+                             "rootfs_root": h.node.rootfs_root,
+                             "state_dir": h.node.state_dir, "host_dev": h.node.host_dev}
                       for name, h in lc.nodes.items()}}
     tmp = args.info + ".tmp"
     with open(tmp, "w") as fh:

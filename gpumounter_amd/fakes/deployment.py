@@ -148,6 +148,7 @@ class ProcessCluster:
                    "GM_KUBELET_SOCKET": n["kubelet_socket"], "GM_CGROUP_ROOT": n["cgroup_root"],
                    "GM_CGROUP_MODE": self.cgroup_mode, "GM_DEVNODE_MODE": "emulate",
                    "GM_CONTAINER_ROOT_PREFIX": n["rootfs_root"], "GM_AMDSMI_LIB": self.amdsmi_lib,
+                   "GM_STATE_DIR": n["state_dir"], "GM_HOST_DEV_PATH": n["host_dev"],
                    "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": str(gport),
                    "GM_METRICS_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
                    "GM_LOG_JSON": "false", **self.worker_env}

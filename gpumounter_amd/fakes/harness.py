@@ -137,6 +137,8 @@ class LocalCluster:
         h = self.nodes[name]
         ov = dict(self.worker_overrides)
         ov.setdefault("gc_tune", False)   # many clusters per test process: freezing would leak
+        ov.setdefault("state_dir", h.node.state_dir)
+        ov.setdefault("host_dev_path", h.node.host_dev)
         if self.device_plugin:
             ov.setdefault("device_plugin", True)
             ov.setdefault("device_plugin_dir", h.kubelet.plugin_dir)

@@ -78,6 +78,13 @@ class FakeNode:
         self.rootfs_root = os.path.join(workdir, "rootfs")
         os.makedirs(self.cgroup_root, exist_ok=True)
         os.makedirs(self.rootfs_root, exist_ok=True)
+        # the worker's node-local state (injection journal) and the node's own /dev, holding an
+        # (emulated) node for every GPU like a real host; containers that bind-mount the host's
+        # /dev (hostPath /dev, privileged) see exactly this directory
+        self.state_dir = os.path.join(workdir, "state")
+        self.host_root = os.path.join(workdir, "hostroot")
+        self.host_dev = os.path.join(self.host_root, "dev")
+        self._populate_host_dev()
         if self.real_cgroups:
             pass
         elif cgroup_mode == "v2":
@@ -94,6 +101,38 @@ class FakeNode:
         # a registered device plugin (FakeKubelet device manager) replaces allocate()
         self.plugin = None
         self.unhealthy: set = set()
+
+    def _populate_host_dev(self) -> None:
+        os.makedirs(os.path.join(self.host_dev, "dri"), exist_ok=True)
+        nodes = [("kfd", 0, 0)]
+        for g in self.gpus:
+            nodes.append((f"dri/renderD{g.render_minor}", 226, g.render_minor))
+            nodes.append((f"dri/card{g.card_minor}", 226, g.card_minor))
+        for rel, ma, mi in nodes:
+            with open(os.path.join(self.host_dev, rel), "w") as fh:
+                fh.write(f"gm-chr {ma}:{mi}\n")
+
+    def host_dev_nodes(self) -> List[str]:
+        out = []
+        for d, _, files in os.walk(self.host_dev):
+            out += [os.path.relpath(os.path.join(d, f), self.host_dev) for f in files]
+        return sorted(out)
+
+    @staticmethod
+    def shares_host_dev(pod: dict, cname: str) -> bool:
+        """Privileged containers and containers mounting the hostPath /dev at /dev see the
+        host's device directory itself."""
+        vols = {v.get("name"): (v.get("hostPath") or {}).get("path")
+                for v in pod.get("spec", {}).get("volumes", []) or []}
+        for c in pod.get("spec", {}).get("containers", []) or []:
+            if c.get("name") != cname:
+                continue
+            if (c.get("securityContext") or {}).get("privileged") is True:
+                return True
+            for m in c.get("volumeMounts", []) or []:
+                if m.get("mountPath") == "/dev" and vols.get(m.get("name")) == "/dev":
+                    return True
+        return False
 
     # ------------------------------------------------------------------------ device plugin
     def device_id(self, g: AmdGpu) -> str:
@@ -220,7 +259,10 @@ class FakeNode:
             with open(os.path.join(cg, "devices.list"), "w") as fh:
                 fh.write("\n".join(RUNTIME_DEFAULT_RULES) + "\n")
         root = os.path.join(self.rootfs_root, cid)
-        os.makedirs(os.path.join(root, "dev"), exist_ok=True)
+        if self.shares_host_dev(pod, cname):
+            os.symlink(self.host_root, root)     # its root's dev/ IS the host's /dev
+        else:
+            os.makedirs(os.path.join(root, "dev"), exist_ok=True)
         c = Container(pod["metadata"]["namespace"], pod["metadata"]["name"],
                       pod["metadata"]["uid"], cname, cid, self.runtime, cg, root, list(pids))
         with self._lock:
@@ -246,7 +288,10 @@ class FakeNode:
                             shutil.rmtree(parent, ignore_errors=True)
                     except OSError:
                         pass
-                    shutil.rmtree(c.root_dir, ignore_errors=True)
+                    if os.path.islink(c.root_dir):
+                        os.unlink(c.root_dir)
+                    else:
+                        shutil.rmtree(c.root_dir, ignore_errors=True)
                     del self.containers[cid]
 
     def container(self, cid: str) -> Optional[Container]:

@@ -82,6 +82,9 @@ class ContainerRef:
     runtime: str          # docker | containerd | cri-o | ""
     id: str               # bare hex id
     running: bool
+    # securityContext.privileged: the runtime already gave it every host device ("a *:* rwm"
+    # and a /dev populated from the host), so gpumounter neither grants nor revokes anything there
+    privileged: bool = False
 
 
 def parse_container_id(cid: str) -> Tuple[str, str]:
@@ -93,15 +96,23 @@ def parse_container_id(cid: str) -> Tuple[str, str]:
     return "", cid
 
 
+def privileged_containers(pod: dict) -> set:
+    """Names of the pod's containers that run privileged."""
+    return {c.get("name", "") for c in pod.get("spec", {}).get("containers", []) or []
+            if ((c.get("securityContext") or {}).get("privileged") is True)}
+
+
 def running_containers(pod: dict, only: str = "") -> List[ContainerRef]:
     out = []
+    priv = privileged_containers(pod)
     for cs in pod.get("status", {}).get("containerStatuses", []) or []:
         if only and cs.get("name") != only:
             continue
         rt, bare = parse_container_id(cs.get("containerID", ""))
         running = "running" in (cs.get("state") or {})
         if bare:
-            out.append(ContainerRef(cs.get("name", ""), rt, bare, running))
+            name = cs.get("name", "")
+            out.append(ContainerRef(name, rt, bare, running, name in priv))
     return out
 
 

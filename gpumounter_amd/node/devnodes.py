@@ -18,6 +18,7 @@ from typing import List, Optional, Sequence, Tuple
 
 from gpumounter_amd import _native
 from gpumounter_amd.models.device import DeviceNode
+from gpumounter_amd.utils import log
 
 
 class DevNodeError(RuntimeError):
@@ -34,17 +35,32 @@ class Target:
     root: str = ""             # explicit root directory (hermetic / test mode)
 
 
-CREATED, PRESENT = 0, 1
+CREATED, PRESENT, SHARED_HOST = 0, 1, 2
+
+_log = log.get("node.devnodes")
 
 
 class DevNodeWriter:
-    def __init__(self, mode: str = "procroot") -> None:
+    """``host_dev``: the host's ``/dev`` as the worker sees it. A container directory that *is*
+    that ``/dev`` (or its ``dri/``) — a hostPath ``/dev`` bind, a privileged runtime's — is never
+    written: creates and unlinks there report :data:`SHARED_HOST` and leave the host's nodes be.
+    The guard is process-wide in the native layer (the last writer constructed sets it)."""
+
+    def __init__(self, mode: str = "procroot", host_dev: str = "") -> None:
         self.mode = mode
         self.flags = 0
         if mode == "setns":
             self.flags |= _native.GM_DEV_VIA_SETNS
         if mode == "emulate":
             self.flags |= _native.GM_DEV_EMULATE
+        self.host_dev = host_dev
+        self.guarded = 0
+        if host_dev:
+            rc = _native.host().gm_devnodes_guard(host_dev.encode())
+            if rc < 0:
+                _log.warning("host /dev guard off: cannot read %s (%s)", host_dev,
+                             os.strerror(-rc))
+            self.guarded = max(rc, 0)
 
     @staticmethod
     def _array(nodes: Sequence[DeviceNode]):
@@ -96,6 +112,9 @@ class DevNodeWriter:
                 return [PRESENT if r < 0 else r for r in results]
             bad = [(n.path, os.strerror(-r)) for n, r in zip(nodes, results) if r < 0]
             raise DevNodeError(f"unlink failed: {bad}", results)
+        shared = [n.path for n, r in zip(nodes, results) if r == SHARED_HOST]
+        if shared:
+            _log.warning("not unlinking %s: the container's directory is the host's /dev", shared)
         return results
 
     def stat(self, t: Target, path: str) -> Tuple[int, int, int, int]:

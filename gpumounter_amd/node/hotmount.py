@@ -10,6 +10,14 @@ Here one transaction covers every running container of the pod (or a named one),
 exact node set from the ledger (the pod's own device-plugin GPUs are never touched, ``/dev/kfd``
 is granted with the first hot-mounted GPU and revoked with the last), and undoes completed steps
 in reverse order if any step fails.
+
+Ownership (what may ever be revoked) is scoped to what gpumounter itself injected, recorded per
+container in the :class:`~gpumounter_amd.node.journal.InjectionJournal`: the audit only reports a
+GPU rule/node as *stale* when the journal says gpumounter put it there, so pods it never touched —
+privileged pods, pods mounting the host's ``/dev``, the worker itself — are never swept. Privileged
+containers already hold every host device and are skipped entirely (ledger-only attach), and the
+native layer refuses to mknod/unlink in a directory that is the host's ``/dev`` or ``/dev/dri``
+(gm_devnodes_guard).
 """
 from __future__ import annotations
 
@@ -22,6 +30,7 @@ from gpumounter_amd.models.device import AmdGpu, DeviceNode, kfd_node
 from gpumounter_amd.models.pod import ContainerRef, running_containers
 from gpumounter_amd.node.cgroup import CgroupError, CgroupResolver, DeviceRuleBackend
 from gpumounter_amd.node.devnodes import CREATED, DevNodeWriter, Target
+from gpumounter_amd.node.journal import InjectionJournal
 from gpumounter_amd.utils import log, trace
 
 _log = log.get("node.hotmount")
@@ -50,7 +59,8 @@ class AuditIssue:
 
 class HotMount:
     def __init__(self, cfg, inv: Inventory, resolver: CgroupResolver, backend: DeviceRuleBackend,
-                 writer: DevNodeWriter, faults=None) -> None:
+                 writer: DevNodeWriter, faults=None,
+                 journal: Optional[InjectionJournal] = None) -> None:
         from gpumounter_amd.utils.faults import NONE
 
         self.cfg = cfg
@@ -59,6 +69,7 @@ class HotMount:
         self.backend = backend
         self.writer = writer
         self.faults = faults if faults is not None else NONE
+        self.journal = journal if journal is not None else InjectionJournal()
 
     # ------------------------------------------------------------------------ node sets
     def kfd(self) -> DeviceNode:
@@ -81,12 +92,17 @@ class HotMount:
 
     # ------------------------------------------------------------------------ targets
     def targets(self, pod: dict, container: str = "") -> List[ContainerTarget]:
+        """Running containers to act on. Privileged ones are left out: the runtime already gave
+        them every host device (and often the host's own ``/dev``), so there is nothing to grant
+        and nothing gpumounter may take away — an attach to them is ledger-only."""
         refs = [r for r in running_containers(pod, container) if r.running]
         if not refs:
             raise MountError(f"pod {pod['metadata'].get('name')} has no running container"
                              + (f" named {container}" if container else ""))
         out = []
         for r in refs:
+            if r.privileged:
+                continue
             cgdir = self.resolver.container_dir(pod, r)
             pids = self.resolver.pids(cgdir)
             if self.cfg.container_root_prefix:
@@ -95,6 +111,11 @@ class HotMount:
                 t = Target(pid=pids[0] if pids else 0)
             out.append(ContainerTarget(r, cgdir, t, pids))
         return out
+
+    def _owner(self, pod: dict, t: ContainerTarget) -> dict:
+        md = pod.get("metadata", {})
+        return {"namespace": md.get("namespace", ""), "pod": md.get("name", ""),
+                "pod_uid": md.get("uid", ""), "container": t.ref.name, "cgdir": t.cgdir}
 
     def resolve(self, pod: dict, container: str = "") -> List[ContainerTarget]:
         """:meth:`targets` for a transaction: a container that vanished meanwhile (pod deleted
@@ -114,8 +135,14 @@ class HotMount:
         with trace.span("resolve"):
             targets = self.resolve(pod, container)
         done: List[tuple] = []  # (target, granted, created_nodes)
+        j = self.journal
         try:
             for t in targets:
+                cid = t.ref.id
+                known = j.nodes_of(cid)
+                # write-ahead: the journal names the state before the kernel holds it
+                j.intend(cid, [((n.major, n.minor), n.path) for n in grant],
+                         [((n.major, n.minor), n.path) for n in after], **self._owner(pod, t))
                 with trace.span("cgroup_rule", backend=self.backend.name, rules=len(grant)):
                     self.faults.check("cgroup_rule")
                     self.backend.apply(t.cgdir, grant, [], after)
@@ -125,22 +152,43 @@ class HotMount:
                     self.faults.check("devnodes")
                     res = self.writer.create(t.target, after)
                 done[-1] = (t, grant, [n for n, r in zip(after, res) if r == CREATED])
+                # a node that was already there before this call (and not by our hand) stays
+                # the container's own: never recorded, so never unlinked
+                j.settle(cid, [(n.major, n.minor) for n, r in zip(after, res)
+                               if r != CREATED and (n.major, n.minor) not in known])
                 self.faults.check("devnodes", "after")
         except Exception as e:
             self._rollback_attach(done, before)
+            # intents for containers whose kernel calls never ran are withdrawn as well
+            for t in targets[len(done):]:
+                self._forget_new(t.ref.id, grant, after, before)
             raise MountError(f"attach failed, rolled back: {e}") from e
         return targets
 
+    def _forget_new(self, cid: str, granted, after, before) -> None:
+        keep = {(n.major, n.minor) for n in before}
+        self.journal.forget(cid, [(n.major, n.minor) for n in granted],
+                            [(n.major, n.minor) for n in after if (n.major, n.minor) not in keep])
+
     def _rollback_attach(self, done, before: List[DeviceNode]) -> None:
+        before_keys = {(n.major, n.minor) for n in before}
         for t, granted, created in reversed(done):
             try:
                 self.writer.remove(t.target, created)
             except Exception as e:  # noqa: BLE001
                 _log.error("rollback unlink in %s failed: %s", t.ref.name, e)
+            else:
+                self.journal.forget(t.ref.id, (), [(n.major, n.minor) for n in created
+                                                   if (n.major, n.minor) not in before_keys])
             try:
                 self.backend.apply(t.cgdir, [], granted, before)
             except Exception as e:  # noqa: BLE001
                 _log.error("rollback revoke in %s failed: %s", t.cgdir, e)
+            else:
+                self.journal.forget(t.ref.id, [(n.major, n.minor) for n in granted])
+            # intended nodes that were never created (the failing step) are not ours either
+            ent = self.journal.nodes_of(t.ref.id)
+            self.journal.forget(t.ref.id, (), [k for k in ent if k not in before_keys])
 
     # ------------------------------------------------------------------------ detach
     def detach(self, pod: dict, remove: Sequence[AmdGpu], keep: Sequence[AmdGpu],
@@ -153,14 +201,17 @@ class HotMount:
         if targets is None:
             with trace.span("resolve"):
                 targets = self.resolve(pod, container)
+        keys = [(n.major, n.minor) for n in revoke]
         for t in targets:
             # reference order: deny → rm → kill (util.go:112,131,139)
             with trace.span("cgroup_rule", backend=self.backend.name, rules=len(revoke)):
                 self.faults.check("unmount")
                 self.backend.apply(t.cgdir, [], revoke, after)
+            self.journal.forget(t.ref.id, keys)
             self.faults.check("unmount", "after")
             with trace.span("devnodes", nodes=len(revoke)):
                 self.writer.remove(t.target, revoke)
+            self.journal.forget(t.ref.id, (), keys)
         return targets
 
     def repair(self, pod: dict, missing: Sequence[AuditIssue], hot: Sequence[AmdGpu],
@@ -175,20 +226,58 @@ class HotMount:
             nodes = [n for n in desired
                      if any(i.kind == "missing_node" and (i.major, i.minor) == (n.major, n.minor)
                             for i in mine)]
+            if not rules and not nodes:
+                continue
+            known = self.journal.nodes_of(t.ref.id)
+            self.journal.intend(t.ref.id, [((n.major, n.minor), n.path) for n in rules],
+                                [((n.major, n.minor), n.path) for n in nodes],
+                                **self._owner(pod, t))
             if rules:
                 self.backend.apply(t.cgdir, rules, [], desired)
             if nodes:
-                self.writer.create(t.target, nodes)
+                res = self.writer.create(t.target, nodes)
+                self.journal.settle(t.ref.id, [(n.major, n.minor) for n, r in zip(nodes, res)
+                                               if r != CREATED and (n.major, n.minor) not in known])
 
     def revoke_issues(self, pod: dict, stale: Sequence[AuditIssue], hot: Sequence[AmdGpu],
                       base: Sequence[AmdGpu] = ()) -> None:
-        """Revoke rules and unlink nodes reported as stale by :meth:`audit`."""
-        nodes = list({(i.major, i.minor): DeviceNode(i.path, i.major, i.minor)
-                      for i in stale}.values())
+        """Revoke rules and unlink nodes reported as stale by :meth:`audit` (which only reports
+        journaled state), per container."""
         keep = self.managed_nodes(hot, base)
         for t in self.targets(pod):
-            self.backend.apply(t.cgdir, [], nodes, keep)
+            mine = [i for i in stale if i.container == t.ref.name]
+            rules = list({(i.major, i.minor): DeviceNode(i.path, i.major, i.minor)
+                          for i in mine if i.kind == "stale_rule"}.values())
+            unlink = list({(i.major, i.minor): DeviceNode(i.path, i.major, i.minor)
+                           for i in mine if i.kind == "stale_node"}.values())
+            if rules:
+                self.backend.apply(t.cgdir, [], rules, keep)
+                self.journal.forget(t.ref.id, [(n.major, n.minor) for n in rules])
+            if unlink:
+                self.writer.remove(t.target, unlink)
+                self.journal.forget(t.ref.id, (), [(n.major, n.minor) for n in unlink])
+
+    def revoke_journaled(self, pod: dict, container_id: str) -> List[AuditIssue]:
+        """Take back everything the journal says gpumounter injected into one container of a pod
+        that no placeholder backs any more (the reconciler's orphan path). Returns what was
+        revoked; state gpumounter did not record is never touched."""
+        ent = self.journal.get(container_id)
+        if ent is None:
+            return []
+        t = next((x for x in self.targets(pod) if x.ref.id == container_id), None)
+        if t is None:
+            return []
+        rules = [DeviceNode(p, ma, mi) for (ma, mi), p in sorted(ent.rules.items())]
+        nodes = [DeviceNode(p, ma, mi) for (ma, mi), p in sorted(ent.nodes.items())]
+        out = [AuditIssue(t.ref.name, "stale_rule", n.path, n.major, n.minor) for n in rules]
+        out += [AuditIssue(t.ref.name, "stale_node", n.path, n.major, n.minor) for n in nodes]
+        if rules:
+            self.backend.apply(t.cgdir, [], rules, [])
+            self.journal.forget(container_id, [(n.major, n.minor) for n in rules])
+        if nodes:
             self.writer.remove(t.target, nodes)
+            self.journal.forget(container_id, (), [(n.major, n.minor) for n in nodes])
+        return out
 
     # ------------------------------------------------------------------------ audit
     def verify(self, pod: dict, gpus: Sequence[AmdGpu], container: str = "") -> List[AuditIssue]:
@@ -212,7 +301,6 @@ class HotMount:
         want = self.managed_nodes(hot, base)
         want_keys = {(n.major, n.minor) for n in want}
         issues: List[AuditIssue] = []
-        all_gpu_nodes = self.gpu_nodes(self.inv.gpus()) + [self.kfd()]
         base_keys = {(n.major, n.minor) for n in self.gpu_nodes(base)}
         for t in self.targets(pod, container):
             allowed = self.backend.allowed(t.cgdir)
@@ -221,14 +309,25 @@ class HotMount:
                     issues.append(AuditIssue(t.ref.name, "missing_rule", n.path, n.major, n.minor))
                 if not self.writer.present(t.target, n):
                     issues.append(AuditIssue(t.ref.name, "missing_node", n.path, n.major, n.minor))
-            for n in all_gpu_nodes:
-                k = (n.major, n.minor)
+            # stale = recorded as injected by gpumounter and no longer backed by the ledger;
+            # whatever else the container holds is not gpumounter's to judge
+            ent = self.journal.get(t.ref.id)
+            if ent is None:
+                continue
+            for (ma, mi), path in sorted(ent.rules.items()):
+                k = (ma, mi)
                 if k in want_keys or k in base_keys:
                     continue
-                if base and n.path == "/dev/kfd":
-                    continue
                 if k in allowed:
-                    issues.append(AuditIssue(t.ref.name, "stale_rule", n.path, n.major, n.minor))
-                if self.writer.present(t.target, n):
-                    issues.append(AuditIssue(t.ref.name, "stale_node", n.path, n.major, n.minor))
+                    issues.append(AuditIssue(t.ref.name, "stale_rule", path, ma, mi))
+                else:
+                    self.journal.forget(t.ref.id, [k])        # already gone from the kernel
+            for (ma, mi), path in sorted(ent.nodes.items()):
+                k = (ma, mi)
+                if k in want_keys or k in base_keys:
+                    continue
+                if self.writer.present(t.target, DeviceNode(path, ma, mi)):
+                    issues.append(AuditIssue(t.ref.name, "stale_node", path, ma, mi))
+                else:
+                    self.journal.forget(t.ref.id, (), [k])
         return issues

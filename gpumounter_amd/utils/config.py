@@ -34,6 +34,8 @@ class Config:
     kube_ca: str = ""
     kube_insecure: bool = False
     node_name: str = ""                # worker's node (downward API NODE_NAME)
+    pod_name: str = ""                 # worker's own pod (downward API POD_NAME): never a target
+    pod_namespace: str = ""            # (downward API POD_NAMESPACE)
     worker_namespace: str = "kube-system"
     worker_label: str = "app=gpu-mounter-worker"
     pool_namespace: str = "gpu-pool"
@@ -68,6 +70,13 @@ class Config:
     # For hermetic runs: containers' rootfs live at <container_root_prefix>/<container-id>/ and
     # device-node writes go there instead of /proc/<pid>/root.
     container_root_prefix: str = ""
+    # node-local injection journal (what gpumounter put into which container; node/journal.py).
+    # The DaemonSet mounts it from the host so it outlives worker restarts; "" = in memory only
+    state_dir: str = "/var/lib/gpumounter"
+    # the host's /dev as the worker sees it (hostPID: /proc/1/root/dev). mknod/unlink are refused
+    # in any container directory that *is* this /dev or its dri/ (hostPath or privileged /dev);
+    # "" = no guard
+    host_dev_path: str = "/proc/1/root/dev"
     drm_major: int = 226
     kfd_major: int = 0                 # 0 → read /sys/class/kfd/kfd/dev (fallback 511)
     kfd_dev_path: str = "/sys/class/kfd/kfd/dev"
@@ -158,8 +167,10 @@ class Config:
         # compatibility with the reference's only env knob (cgroup.go:79)
         if "cgroup_driver" not in env_vals and env.get("CGROUP_DRIVER"):
             env_vals["cgroup_driver"] = env["CGROUP_DRIVER"]
-        if "node_name" not in env_vals and env.get("NODE_NAME"):
-            env_vals["node_name"] = env["NODE_NAME"]
+        for f, k in (("node_name", "NODE_NAME"), ("pod_name", "POD_NAME"),
+                     ("pod_namespace", "POD_NAMESPACE")):
+            if f not in env_vals and env.get(k):
+                env_vals[f] = env[k]
         cfg.update(env_vals)
         cfg.update({k: v for k, v in overrides.items() if v is not None})
         cfg.validate()

@@ -9,9 +9,15 @@ Every ``reconcile_period_s`` (and on demand) this loop, per node:
 2. deletes placeholders stuck Unschedulable/Failed that no in-flight attach is waiting on;
 3. for every live owner, audits cgroup rules + ``/dev`` nodes against the ledger and re-applies
    missing ones (resume after a container restart) or revokes stale ones;
-4. for every other running pod on the node, revokes hot-mount rules/nodes that no placeholder
-   backs any more (orphans) — the "zero orphaned cgroup entries" invariant.
+4. for every container the injection journal (node/journal.py) lists and no placeholder backs
+   any more, revokes exactly the rules/nodes gpumounter recorded injecting there (orphans) — the
+   "zero orphaned cgroup entries" invariant. Pods gpumounter never touched are never audited:
+   their GPU nodes (a privileged pod's, the worker's own host ``/dev``, a device plugin's) are
+   not gpumounter's state. Journal entries of containers that no longer run are dropped.
 All repairs take the same per-pod lock as AddGPU/RemoveGPU.
+
+The reference has no sweep at all; its only revocation path is RemoveGPU on the ledger-selected
+GPUs of the named pod (reference: pkg/util/util.go:73-147, allocator.go:101-126).
 
 Two events are handled immediately instead of at the next sweep (:meth:`watch_events`): a
 placeholder deleted by someone else (kubectl, eviction, preemption — its GPU goes back to the
@@ -160,19 +166,32 @@ class Reconciler:
                      ann.get(ANN_OWNER_UID, ""))
             by_owner.setdefault(owner, []).append(p)
         now = time.monotonic()
-        for (oname, ons, ouid), phs in by_owner.items():
+        async def fresh(ns: str, name: str):
             try:
-                owner = await svc.kube.get_pod(ons, oname)
+                return await svc.kube.get_pod(ns, name)
             except NotFound:
-                owner = None
+                return None
+
+        def gone(p, uid: str) -> bool:
+            return p is None or podu.uid_of(p) != uid or podu.phase_of(p) in ("Succeeded",
+                                                                              "Failed")
+
+        async def collect(ons: str, oname: str, phs: List[dict]) -> None:
+            for p in phs:
+                rep.owner_gone.append(p["metadata"]["name"])
+                m.orphans.labels(kind="owner_gone").inc()
+            await svc.ph.release([svc.ph.from_pod(p, {}) for p in phs], wait=False)
+
+        for (oname, ons, ouid), phs in by_owner.items():
+            # the node informer already holds every pod of this node; the apiserver is only
+            # asked to confirm an owner the cache shows gone/replaced, or whose repair failed
+            owner = svc.node_pods.get(ons, oname)
+            if gone(owner, ouid):
+                owner = await fresh(ons, oname)
             lock = svc.pod_lock(ons, oname)
-            if owner is None or podu.uid_of(owner) != ouid or podu.phase_of(owner) in (
-                    "Succeeded", "Failed"):
+            if gone(owner, ouid):
                 async with lock:
-                    for p in phs:
-                        rep.owner_gone.append(p["metadata"]["name"])
-                        m.orphans.labels(kind="owner_gone").inc()
-                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in phs], wait=False)
+                    await collect(ons, oname, phs)
                 continue
             if lock.locked():
                 continue  # an attach/detach is in flight for this owner
@@ -193,38 +212,53 @@ class Reconciler:
                 try:
                     fixed = await svc.reconcile_pod(owner)
                 except Exception as e:  # noqa: BLE001
-                    rep.errors.append(f"{ons}/{oname}: {e}")
+                    if gone(await fresh(ons, oname), ouid):   # the cache lagged a delete
+                        await collect(ons, oname, phs)
+                    else:
+                        rep.errors.append(f"{ons}/{oname}: {e}")
                     continue
                 if fixed:
                     rep.orphans += sum(1 for i in fixed if i.kind.startswith("stale"))
                     rep.repaired.append(f"{ons}/{oname}")
                     m.reconcile_actions.labels(action="repair").inc()
-        # pods on this node without placeholders must not keep hot-mount state
-        owners = {(o[1], o[0]) for o in by_owner}
-        try:
-            snapshot = await svc._read_ledger()  # one kubelet read for the whole sweep
-        except Exception as e:  # noqa: BLE001
-            rep.errors.append(f"ledger: {e}")
-            self.last = rep
-            return rep
-        for pod in svc.node_pods.list(lambda p: podu.phase_of(p) == "Running"):
-            key = (podu.ns_of(pod), podu.name_of(pod))
-            if key in owners or (pod["metadata"].get("labels") or {}).get("app") == "gpu-pool":
-                continue
+        # journaled hot-mount state that no placeholder backs any more must not stay behind
+        owners = {(o[1], o[0], o[2]) for o in by_owner}
+        journal = svc.hm.journal
+        for ent in journal.entries():
+            pod = svc.node_pods.get(ent.namespace, ent.pod)
+            alive = pod is not None and podu.uid_of(pod) == ent.pod_uid and \
+                podu.phase_of(pod) == "Running" and any(
+                    r.id == ent.container_id and r.running
+                    for r in podu.running_containers(pod))
+            if not alive:
+                # container gone: its cgroup and mount namespace (and our state) went with it.
+                # Confirmed with the apiserver first, so a lagging cache never loses a record
+                pod = await fresh(ent.namespace, ent.pod)
+                if pod is None or podu.uid_of(pod) != ent.pod_uid or not any(
+                        r.id == ent.container_id and r.running
+                        for r in podu.running_containers(pod)):
+                    journal.drop(ent.container_id)
+                    continue
+            if (ent.namespace, ent.pod, ent.pod_uid) in owners:
+                continue            # audited against its placeholders above
+            key = (ent.namespace, ent.pod)
             lock = svc.pod_lock(*key)
             if lock.locked():
                 continue
             async with lock:
+                if svc.ph.owned_by(pod):
+                    continue        # an attach completed meanwhile
                 try:
-                    fixed = await svc.reconcile_pod(pod, snapshot)
+                    revoked = svc.hm.revoke_journaled(pod, ent.container_id)
                 except Exception as e:  # noqa: BLE001
-                    rep.errors.append(f"audit {key}: {e}")
+                    rep.errors.append(f"revoke {key}: {e}")
                     continue
-                stale = [i for i in fixed if i.kind.startswith("stale")]
-                if stale:
-                    rep.orphans += len(stale)
-                    m.orphans.labels(kind="stale_state").inc(len(stale))
-                    rep.revoked.append(f"{key[0]}/{key[1]}")
+                if revoked:
+                    rep.orphans += len(revoked)
+                    m.orphans.labels(kind="stale_state").inc(len(revoked))
+                    name = f"{key[0]}/{key[1]}"
+                    if name not in rep.revoked:
+                        rep.revoked.append(name)
                     m.reconcile_actions.labels(action="revoke").inc()
         for name in list(self._first_seen):
             if not any(p["metadata"]["name"] == name for p in placeholders):

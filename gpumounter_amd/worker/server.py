@@ -28,6 +28,7 @@ from gpumounter_amd.node import systemd
 from gpumounter_amd.node.cgroup import CgroupResolver, make_backend
 from gpumounter_amd.node.devnodes import DevNodeWriter
 from gpumounter_amd.node.hotmount import HotMount
+from gpumounter_amd.node.journal import InjectionJournal
 from gpumounter_amd.node.ledger import LedgerClient
 from gpumounter_amd.utils import log, runtime
 from gpumounter_amd.utils.faults import FaultInjector
@@ -68,10 +69,12 @@ class Worker:
             sd_mode = "off"          # hermetic runs never talk to the host's systemd by accident
         self.backend = systemd.maybe_wrap(self.backend, sd_mode, cfg.systemd_bus,
                                           self.resolver.driver)
-        self.writer = DevNodeWriter(cfg.devnode_mode)
+        self.writer = DevNodeWriter(cfg.devnode_mode, cfg.host_dev_path)
         self.faults = FaultInjector(cfg.fault)
+        self.journal = InjectionJournal(os.path.join(cfg.state_dir, "journal")
+                                        if cfg.state_dir else "")
         self.hotmount = HotMount(cfg, self.inv, self.resolver, self.backend, self.writer,
-                                 self.faults)
+                                 self.faults, self.journal)
         ph_ns = None if cfg.placeholder_namespace_mode == "tenant" else cfg.pool_namespace
         self.ph_informer = PodInformer(self.kube, ph_ns,
                                        PlaceholderManager.selector_for_node(cfg.node_name),

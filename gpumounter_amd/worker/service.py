@@ -115,6 +115,12 @@ class GpuMountService:
             lk = self._locks[(ns, name)] = asyncio.Lock()
         return lk
 
+    def is_self(self, pod: dict) -> bool:
+        """The worker's own pod (downward API POD_NAME/POD_NAMESPACE): it mounts the host's /dev,
+        so nothing may ever be injected into or taken from it."""
+        return bool(self.cfg.pod_name) and podu.name_of(pod) == self.cfg.pod_name and \
+            podu.ns_of(pod) == (self.cfg.pod_namespace or self.cfg.worker_namespace)
+
     async def get_pod(self, ns: str, name: str, fresh: bool = False) -> Optional[dict]:
         if not fresh:
             p = self.node_pods.get(ns, name)
@@ -276,6 +282,9 @@ class GpuMountService:
             raise RpcError(grpc.StatusCode.FAILED_PRECONDITION,
                            f"pod is on node {podu.node_of(pod)!r}, this worker serves "
                            f"{self.cfg.node_name!r}")
+        if self.is_self(pod):
+            raise RpcError(grpc.StatusCode.FAILED_PRECONDITION,
+                           f"{ERR_POLICY}: the gpumounter worker pod itself is never a target")
         async with self.pod_lock(req.namespace, req.pod_name):
             if podu.phase_of(pod) != "Running":
                 pod = await self.get_pod(req.namespace, req.pod_name, fresh=True)

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define GM_HOST_ABI_VERSION 2
+#define GM_HOST_ABI_VERSION 3
 
 // Access bits follow BPF_DEVCG_ACC_* so the same rule feeds both cgroup versions.
 #define GM_ACC_MKNOD 1
@@ -104,11 +104,18 @@ typedef struct gm_dev_node {
 #define GM_DEV_VIA_SETNS 2  // enter the mount namespace with a helper thread instead of /proc/pid/root
 #define GM_DEV_REPLACE 4    // replace an existing node with different major:minor
 
+// Registers the host's /dev (and its dri/) as seen from the caller, e.g. "/proc/1/root/dev". From
+// then on create/remove leave any node whose directory *is* one of them alone (result 2): a
+// container that bind-mounts the host's /dev shares the host's nodes. NULL/"" clears the guard.
+// Returns how many directories are guarded, or -errno if host_dev cannot be read.
+int gm_devnodes_guard(const char* host_dev);
 // Creates nodes inside the target's root: `root` if non-NULL (test prefix), else /proc/<pid>/root.
-// results[i] = 0 created, 1 already present (idempotent), or -errno. Returns #failures.
+// results[i] = 0 created, 1 already present (idempotent), 2 directory is the host's (skipped), or
+// -errno. Returns #failures.
 int gm_devnodes_create(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
                        int* results);
-// Removes nodes (only if they are the expected device). results[i] = 0 removed, 1 absent, -errno.
+// Removes nodes (only if they are the expected device). results[i] = 0 removed, 1 absent,
+// 2 directory is the host's (left alone), -errno.
 int gm_devnodes_remove(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
                        int* results);
 // Describes a node: *kind = 0 absent, 1 char device, 2 emulated marker, 3 other file.

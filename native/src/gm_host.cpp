@@ -18,6 +18,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -314,6 +315,25 @@ bool is_ours(uint32_t id, uint32_t* chained_id) {
 // ------------------------------------------------------------------ device nodes
 constexpr const char* kMarker = "gm-chr";
 
+// Directories that are the host's own /dev (and /dev/dri) as seen from the worker: a container
+// whose /dev is a bind of them (hostPath /dev, privileged runtimes) shares the host's nodes, so
+// gpumounter must neither create nor unlink anything there. Set once at worker start-up.
+struct DirId {
+  std::atomic<uint64_t> dev{0}, ino{0};
+};
+DirId g_guard[2];
+
+bool guarded_dir(int dirfd) {
+  struct stat st;
+  if (fstat(dirfd, &st) < 0) return false;
+  for (auto& g : g_guard) {
+    uint64_t ino = g.ino.load(std::memory_order_acquire);
+    if (ino && ino == (uint64_t)st.st_ino && g.dev.load(std::memory_order_relaxed) == st.st_dev)
+      return true;
+  }
+  return false;
+}
+
 int open_root(int pid, const char* root) {
   if (root && *root) {
     int fd = open(root, O_PATH | O_DIRECTORY | O_CLOEXEC);
@@ -324,6 +344,8 @@ int open_root(int pid, const char* root) {
   int fd = open(p, O_PATH | O_DIRECTORY | O_CLOEXEC);
   return fd < 0 ? -errno : fd;
 }
+
+constexpr int kSharedHost = 2;  // result: the directory is the host's; left untouched
 
 // Walks `path` (relative, '/'-separated) below rootfd without following symlinks, creating
 // missing directories when `create`. Returns the parent dir fd and the leaf name.
@@ -349,6 +371,7 @@ int walk_parent(int rootfd, const char* path, bool create, Fd* parent, std::stri
   for (size_t i = 0; i + 1 < comps.size(); ++i) {
     int nfd = openat(curfd.fd, comps[i].c_str(), O_PATH | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
     if (nfd < 0 && errno == ENOENT && create) {
+      if (guarded_dir(curfd.fd)) return kSharedHost;  // never mkdir inside the host's /dev
       if (mkdirat(curfd.fd, comps[i].c_str(), 0755) < 0 && errno != EEXIST) return -errno;
       nfd = openat(curfd.fd, comps[i].c_str(), O_PATH | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
     }
@@ -400,7 +423,8 @@ int create_one(int rootfd, const gm_dev_node_t& n, int flags) {
   Fd parent;
   std::string leaf;
   int e = walk_parent(rootfd, n.path, true, &parent, &leaf);
-  if (e < 0) return e;
+  if (e != 0) return e;
+  if (guarded_dir(parent.fd)) return kSharedHost;
   int kind;
   uint32_t maj, min, mode;
   e = stat_leaf(parent.fd, leaf, &kind, &maj, &min, &mode);
@@ -445,7 +469,8 @@ int remove_one(int rootfd, const gm_dev_node_t& n) {
   std::string leaf;
   int e = walk_parent(rootfd, n.path, false, &parent, &leaf);
   if (e == -ENOENT) return 1;
-  if (e < 0) return e;
+  if (e != 0) return e;
+  if (guarded_dir(parent.fd)) return kSharedHost;
   int kind;
   uint32_t maj, min, mode;
   e = stat_leaf(parent.fd, leaf, &kind, &maj, &min, &mode);
@@ -843,6 +868,25 @@ int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir) {
 }
 
 // ------------------------------------------------------------------ device nodes
+int gm_devnodes_guard(const char* host_dev) {
+  for (auto& g : g_guard) g.ino.store(0, std::memory_order_release);
+  if (!host_dev || !*host_dev) return 0;
+  int set = 0;
+  const std::string base(host_dev);
+  const std::string dirs[2] = {base, base + "/dri"};
+  for (int i = 0; i < 2; ++i) {
+    struct stat st;
+    if (stat(dirs[i].c_str(), &st) < 0 || !S_ISDIR(st.st_mode)) {
+      if (i == 0) return -(errno ? errno : ENOTDIR);
+      continue;  // a host without /dev/dri (no GPU driver loaded) guards /dev alone
+    }
+    g_guard[i].dev.store(st.st_dev, std::memory_order_relaxed);
+    g_guard[i].ino.store(st.st_ino, std::memory_order_release);
+    ++set;
+  }
+  return set;
+}
+
 int gm_devnodes_create(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
                        int* results) {
   int failures = 0;

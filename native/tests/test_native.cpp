@@ -108,6 +108,47 @@ static void test_devnodes() {
   EXPECT(system(cmd.c_str()) == 0);
 }
 
+// A root whose dev/ is the registered host /dev: nothing is created or unlinked there (result 2),
+// including under a missing dev/dri (no mkdir inside the host's /dev).
+static void test_devnodes_guard() {
+  char tmpl[] = "/tmp/gm_guard_XXXXXX";
+  char* root = mkdtemp(tmpl);
+  EXPECT(root != nullptr);
+  std::string dev = std::string(root) + "/dev";
+  EXPECT(mkdir(dev.c_str(), 0755) == 0);
+  EXPECT(gm_devnodes_guard(dev.c_str()) == 1);  // no dri/ yet: /dev alone
+  gm_dev_node_t n[2];
+  memset(n, 0, sizeof(n));
+  snprintf(n[0].path, sizeof(n[0].path), "dev/kfd");
+  n[0].major = 511;
+  n[0].mode = 0666;
+  n[0].uid = n[0].gid = -1;
+  snprintf(n[1].path, sizeof(n[1].path), "dev/dri/renderD129");
+  n[1].major = 226;
+  n[1].minor = 129;
+  n[1].mode = 0666;
+  n[1].uid = n[1].gid = -1;
+  int res[2] = {9, 9};
+  EXPECT(gm_devnodes_create(0, root, n, 2, GM_DEV_EMULATE, res) == 0);
+  EXPECT(res[0] == 2 && res[1] == 2);
+  struct stat st;
+  EXPECT(stat((dev + "/kfd").c_str(), &st) < 0 && stat((dev + "/dri").c_str(), &st) < 0);
+  // nodes that exist in the host dir are never unlinked through a container sharing it
+  EXPECT(gm_devnodes_guard(nullptr) == 0);
+  EXPECT(gm_devnodes_create(0, root, n, 2, GM_DEV_EMULATE, res) == 0);
+  EXPECT(res[0] == 0 && res[1] == 0);
+  EXPECT(gm_devnodes_guard(dev.c_str()) == 2);  // now /dev and /dev/dri
+  EXPECT(gm_devnodes_remove(0, root, n, 2, 0, res) == 0);
+  EXPECT(res[0] == 2 && res[1] == 2);
+  EXPECT(stat((dev + "/kfd").c_str(), &st) == 0 && stat((dev + "/dri/renderD129").c_str(), &st) == 0);
+  EXPECT(gm_devnodes_guard("/nonexistent/gm/dev") == -ENOENT);
+  EXPECT(gm_devnodes_guard("") == 0);
+  EXPECT(gm_devnodes_remove(0, root, n, 2, 0, res) == 0);
+  EXPECT(res[0] == 0 && res[1] == 0);
+  std::string cmd = std::string("rm -rf ") + root;
+  EXPECT(system(cmd.c_str()) == 0);
+}
+
 static void test_pids() {
   char path[] = "/tmp/gm_pids_XXXXXX";
   int fd = mkstemp(path);
@@ -154,6 +195,7 @@ int main() {
   test_format();
   test_bpf_layout();
   test_devnodes();
+  test_devnodes_guard();
   test_pids();
   test_smi_mock();
   if (g_fail) {

@@ -84,10 +84,11 @@ def chr_node(pid, rel):
     return [os.major(st.st_rdev), os.minor(st.st_rdev)] if stat.S_ISCHR(st.st_mode) else "notchr"
 
 
-async def flow(mnt, bpffs, tenant_pid, obs):
+async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0):
     async with LocalCluster(cgroup_mode="v2", devnode_mode="procroot", cgroup_root=mnt,
                             kfd_major=1,
-                            worker_overrides={"drm_major": 1, "bpf_pin_dir": bpffs}) as lc:
+                            worker_overrides={"drm_major": 1, "bpf_pin_dir": bpffs,
+                                              "host_dev_path": hostdev}) as lc:
         w = lc.nodes["node-0"].worker
         obs["backend"] = w.backend.name
         lc.tenant("t", pids={"main": [tenant_pid]})
@@ -121,6 +122,40 @@ async def flow(mnt, bpffs, tenant_pid, obs):
                                                                   "/dev/dri/renderD8")}
         obs["audit_final"] = [i.kind for i in await lc.audit("default", "t")]
         obs["pins_left"] = [f for f in os.listdir(bpffs) if f.startswith("gm_")]
+        if shared_pid:
+            await shared_dev_flow(lc, hostdev, shared_pid, obs)
+
+
+def listing(d):
+    out = {}
+    for dp, _, files in os.walk(d):
+        for f in files:
+            st = os.lstat(os.path.join(dp, f))
+            out[os.path.relpath(os.path.join(dp, f), d)] = [os.major(st.st_rdev),
+                                                            os.minor(st.st_rdev)]
+    return out
+
+
+async def shared_dev_flow(lc, hostdev, pid, obs):
+    """A tenant whose /dev is a bind mount of the host-like dev dir (hostPath /dev): attach,
+    reconcile after its placeholder vanished, and detach must leave that directory as it was."""
+    lc.tenant("shared", pids={"main": [pid]})
+    obs["shared_sees_host_dev"] = chr_node(pid, "/dev/dri/renderD5") == [1, 5]
+    before = listing(hostdev)
+    # both GPUs: renderD8/card9 do not exist in the host dir, so only the guard keeps the
+    # worker from creating them there
+    code, b = await lc.add("default", "shared", 2)
+    obs["shared_add"] = code
+    obs["shared_gpus"] = sorted(d["render_minor"] for d in b.get("devices", []))
+    obs["shared_after_add_unchanged"] = listing(hostdev) == before
+    w = lc.nodes["node-0"].worker
+    for ph in lc.cluster.placeholders():
+        lc.cluster.delete(ph["metadata"]["namespace"], ph["metadata"]["name"], grace=0)
+    await asyncio.sleep(0.1)
+    rep = await w.reconciler.run_once()
+    obs["shared_sweep_unlinked"] = rep.orphans
+    obs["shared_after_sweep_unchanged"] = listing(hostdev) == before
+    obs["shared_host_listing"] = sorted(before)
 
 
 def main():
@@ -135,13 +170,26 @@ def main():
         ["unshare", "-m", "--propagation", "private", "sh", "-c",
          "set -e; mount -t tmpfs tmpfs /dev; echo ok; exec sleep 300"],
         stdout=subprocess.PIPE, text=True)
+    # a host-like /dev with real nodes (the worker's host_dev_path) and a second tenant that
+    # bind-mounts it at /dev, as a hostPath-/dev or privileged container does
+    hostdev = tempfile.mkdtemp(prefix="gm-e2e-hostdev-")
+    os.makedirs(os.path.join(hostdev, "dri"))
+    for rel, mi in (("kfd", 0), ("dri/renderD5", 5), ("dri/card7", 7)):
+        os.mknod(os.path.join(hostdev, rel), 0o666 | stat.S_IFCHR, os.makedev(1, mi))
+    shared = subprocess.Popen(
+        ["unshare", "-m", "--propagation", "private", "sh", "-c",
+         f"set -e; mount --bind {hostdev} /dev; echo ok; exec sleep 300"],
+        stdout=subprocess.PIPE, text=True)
     try:
         assert tenant.stdout.readline().strip() == "ok"
+        assert shared.stdout.readline().strip() == "ok"
         assert os.readlink(f"/proc/{tenant.pid}/ns/mnt") != os.readlink("/proc/self/ns/mnt")
-        asyncio.run(flow(root, bpffs, tenant.pid, obs))
+        asyncio.run(flow(root, bpffs, tenant.pid, obs, hostdev, shared.pid))
     finally:
-        tenant.kill()
-        tenant.wait()
+        for p in (tenant, shared):
+            p.kill()
+            p.wait()
+        shutil.rmtree(hostdev, ignore_errors=True)
         # tear the real cgroup tree down bottom-up (processes are gone)
         for dirpath, dirs, _ in sorted(os.walk(root), key=lambda t: -t[0].count("/")):
             try:

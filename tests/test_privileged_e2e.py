@@ -45,3 +45,7 @@ def test_full_stack_attach_detach_enforced_by_the_kernel(tmp_path):
     assert o["progs_final"] == ["runc_devices"]               # runtime program restored
     assert o["nodes_final"] == {"/dev/kfd": None, "/dev/dri/renderD8": None}
     assert o["audit_final"] == [] and o["pins_left"] == []
+    # a tenant whose /dev is a bind of the host's keeps every node through attach + sweep
+    assert o["shared_sees_host_dev"] and o["shared_add"] == 200 and o["shared_gpus"] == [5, 8]
+    assert o["shared_after_add_unchanged"] and o["shared_after_sweep_unchanged"]
+    assert o["shared_host_listing"] == ["dri/card7", "dri/renderD5", "kfd"]
