@@ -136,7 +136,18 @@ def main() -> int:
     ap.add_argument("--protocol", choices=("gpumounter", "reference"), default="gpumounter",
                     help="'reference' re-enacts the reference's call sequence on the same "
                          "cluster (emulated baseline, see gpumounter_amd/fakes/refproto.py)")
+    ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",
+                    help="real (root): a private cgroup2 mount with a runc-style device program, "
+                         "real BPF_PROG_LOAD/verify/BPF_F_REPLACE attach and mknodat into a "
+                         "tenant in its own mount namespace (gpumounter_amd/fakes/realnode.py); "
+                         "emulated: the JSON-recording cgroup-v2 backend and marker files, for "
+                         "unprivileged boxes")
     args = ap.parse_args()
+    if args.node_ops == "real":
+        if args.deploy == "processes" and "--deploy" in sys.argv:
+            print("--node-ops real runs --deploy inprocess", file=sys.stderr)
+        args.deploy = "inprocess"
+        args.cgroup = "v2"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -145,6 +156,14 @@ def main() -> int:
     if world > 1 and world != n:
         print(f"WORLD_SIZE={world} must equal --gpus={n}", file=sys.stderr)
         return 2
+
+    # Single-process N>1 (the driver may run `bench.py --gpus 8` without a launcher): the
+    # collective check needs one process per GPU, so N rank processes are spawned here, before
+    # this process touches the GPU (a GPU-initialised process must never exec anything).
+    rank_pool = None
+    if world == 1 and n > 1 and not args.no_verify:
+        from gpumounter_amd.parallel.rankpool import RankPool
+        rank_pool = RankPool(n)
 
     import torch
     import torch.distributed as dist
@@ -165,6 +184,7 @@ def main() -> int:
 
     tc = lc = cp = None
     sleeper = None
+    sandbox = None
     info = {}
     if rank == 0:
         from gpumounter_amd.fakes.apiserver import LatencyModel
@@ -178,7 +198,13 @@ def main() -> int:
             print(f"need {n} GPUs visible to HIP and amdsmi; have {node_bdfs} (amdsmi {bdfs}, "
                   f"HIP {visible})", file=sys.stderr)
             return 3
-        sleeper = subprocess.Popen(["sleep", "infinity"])
+        if args.node_ops == "real":
+            from gpumounter_amd.fakes.realnode import RealNodeSandbox
+            sandbox = RealNodeSandbox().__enter__()
+            tenant_pid = sandbox.tenant_pid
+        else:
+            sleeper = subprocess.Popen(["sleep", "infinity"])
+            tenant_pid = sleeper.pid
         if args.deploy == "processes":
             if args.device_plugin:
                 print("--device-plugin needs --deploy inprocess (the fake kubelet drives the "
@@ -189,33 +215,46 @@ def main() -> int:
                                 gpu_bdfs=node_bdfs, protocol=args.protocol,
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
                                             "GM_PLACEMENT_ENFORCE": args.placement}).start()
-            pc.tenant("tenant", pids={"main": [sleeper.pid]})
+            pc.tenant("tenant", pids={"main": [tenant_pid]})
             cp = _ProcCP(pc)
         else:
             lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
+            wov = {"warm_pool_size": args.warm_pool, "placement_enforce": args.placement,
+                   "gc_tune": True}   # as the daemons run
+            kw = {}
+            if sandbox is not None:
+                wov["bpf_pin_dir"] = sandbox.bpffs
+                kw = {"cgroup_root": sandbox.cgroup_root, "devnode_mode": "procroot"}
             tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
                                  node_gpu_bdfs=node_bdfs, device_plugin=args.device_plugin,
-                                 worker_overrides={"warm_pool_size": args.warm_pool,
-                                                   "placement_enforce": args.placement,
-                                                   "gc_tune": True},   # as the daemons run
-                                 master_overrides={"gc_tune": True})
+                                 worker_overrides=wov, master_overrides={"gc_tune": True}, **kw)
             lc = tc.start()
             if args.protocol == "reference":
                 from gpumounter_amd.fakes import refproto
                 refproto.install(lc)
-            lc.tenant("tenant", pids={"main": [sleeper.pid]})
+            lc.tenant("tenant", pids={"main": [tenant_pid]})
+            if sandbox is not None:
+                from gpumounter_amd.fakes.realnode import attach_runtime_program
+                (ctr,) = [c for c in lc.nodes["node-0"].node.containers.values()
+                          if c.pod_name == "tenant"]
+                attach_runtime_program(ctr.cgroup_dir)
             cp = _LocalCP(tc, lc)
         if args.warm_pool:
             cp.wait_pool(min(args.warm_pool, len(node_bdfs)))
         info = {"amdsmi_lib": inv.lib_path, "node_gpus": len(node_bdfs),
                 "amdsmi_gpus": len(bdfs), "gfx": sorted({g.gfx_target for g in inv.gpus()}),
                 "hives": sorted({hex(g.xgmi_hive_id) for g in inv.gpus()})}
+        gpu_by_bdf = {g.bdf: g for g in inv.gpus()}
+        link_matrix = inv.links()
 
     nccl_group = None
     bound_dev = [None]
     pool_cap = info.get("node_gpus", 0) if rank == 0 else 0
     attach_ms, detach_ms, audit_issues, probe_us, stage = [], [], 0, [], {}
     ar_ms = []
+    probe_by_gpu = {}
+    last_bdfs = []
+    ar_backend = [None]
 
     def one_step(record: bool):
         nonlocal audit_issues, nccl_group
@@ -234,15 +273,19 @@ def main() -> int:
         if world > 1:
             dist.broadcast_object_list(obj, src=0)
         st = obj[0]
+        last_bdfs[:] = st["bdfs"]
         if has_gpu and not args.no_verify:
             bdfs = sorted(st["bdfs"])           # stable rank → attached-GPU mapping
-            mine = bdfs[rank % len(bdfs)]
-            dev = probe.find_device(mine)
-            if dev < 0:
-                raise RuntimeError(f"rank {rank}: attached GPU {mine} not visible to HIP")
-            us = probe.quick(dev)
-            if record:
-                probe_us.append(us)
+            # one process per GPU: each rank checks its own; a single process checks them all
+            mine_all = bdfs if world == 1 else [bdfs[rank % len(bdfs)]]
+            for mine in mine_all:
+                dev = probe.find_device(mine)
+                if dev < 0:
+                    raise RuntimeError(f"rank {rank}: attached GPU {mine} not visible to HIP")
+                us = probe.quick(dev)
+                if record:
+                    probe_us.append(us)
+                    probe_by_gpu.setdefault(mine, []).append(us)
             if world > 1:
                 if nccl_group is None:
                     torch.cuda.set_device(dev)
@@ -259,6 +302,14 @@ def main() -> int:
                     ar_ms.append((time.perf_counter() - ta) * 1e3)
                 if float(x[0].item()) != float(world):
                     raise RuntimeError("RCCL all-reduce over the attached GPUs returned wrong sum")
+                ar_backend[0] = "nccl"
+        if rank_pool is not None:
+            r = rank_pool.allreduce(st["bdfs"])
+            if not r["ok"]:
+                raise RuntimeError(f"all-reduce over the attached GPUs failed: {r}")
+            ar_backend[0] = r["backend"]
+            if record:
+                ar_ms.append(r["ms"])
         if world > 1:
             dist.barrier()
         if rank == 0:
@@ -308,6 +359,18 @@ def main() -> int:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             ms_per_step = float(t.item())
         if rank == 0:
+            # the attached set, from amdsmi: one hive, every pair on a direct xGMI link
+            from gpumounter_amd.hw import topology
+            att = {gpu_by_bdf[b].index: gpu_by_bdf[b] for b in last_bdfs if b in gpu_by_bdf}
+            _, att_hives, att_numa, att_nx = topology.score_set(att, link_matrix, sorted(att))
+            p2p = None
+            if has_gpu and not args.no_verify and len(last_bdfs) > 1:
+                devs = [probe.find_device(b) for b in sorted(last_bdfs)]
+                pairs = [probe.p2p(a, b, 64 << 20, 3) for a in devs for b in devs if a != b]
+                p2p = {"pairs": len(pairs),
+                       "all_peer_access": all(x["peer_access"] for x in pairs),
+                       "min_gbps": round(min(x["gbps"] for x in pairs), 1),
+                       "max_gbps": round(max(x["gbps"] for x in pairs), 1)}
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
             placeholders_left = cp.placeholders_left()
             p50 = pct(attach_ms, 0.5)
@@ -354,8 +417,13 @@ def main() -> int:
                 "higher_is_better": False,
                 "scaling": "weak",
                 "vs_baseline": None,
-                "dtype": "bf16",
+                # a control-plane latency: no tensor compute is timed (the post-attach RCCL
+                # check all-reduces bf16)
+                "dtype": "none",
                 "data": "synthetic",
+                # which node operations ran: "emulated" = JSON-recording cgroup-v2 backend +
+                # marker files (unprivileged box), "real" = bpf(2) + mknodat on this kernel
+                "node_ops": args.node_ops,
                 "config": {
                     "model": f"gpumounter-amd {args.mode}-mount, {n} MI355X per Pod",
                     "global_batch": 1, "seq_len": None, "gpus_per_pod": n,
@@ -372,21 +440,40 @@ def main() -> int:
                 "detach_p99_ms": round(pct(detach_ms, 0.99), 4),
                 "stage_p50_ms": {k: round(statistics.median(v), 4) for k, v in sorted(stage.items())},
                 "probe_quick_p50_us": round(statistics.median(probe_us), 2) if probe_us else None,
-                "rccl_allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4) if ar_ms else None,
+                "probe_gpus_verified": len(probe_by_gpu) if world == 1 else None,
+                "probe_quick_p50_us_by_gpu": {b: round(statistics.median(v), 2)
+                                              for b, v in sorted(probe_by_gpu.items())}
+                if world == 1 and probe_by_gpu else None,
+                "allreduce_backend": ar_backend[0],
+                "allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4) if ar_ms else None,
+                "rccl_allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4)
+                if ar_ms and ar_backend[0] == "nccl" else None,
+                "attached_hives": att_hives, "attached_numa_nodes": att_numa,
+                "non_xgmi_pairs": att_nx, "p2p": p2p,
                 "ledger_audit_issues": audit_issues,
                 "final_orphans": orphan_issues,
                 "placeholders_left": placeholders_left,
                 "reference_emulated_same_run": ref,
                 "inventory": info,
             }
+            if args.node_ops == "real":
+                out["attach_p50_real_node_ops_ms"] = out["value"]
+                out["real_node_ops_stage_p50_ms"] = {
+                    k.split(".")[-1]: v for k, v in out["stage_p50_ms"].items()
+                    if k.startswith("mount.cgroup_rule.bpf_") or k in (
+                        "mount.cgroup_rule", "mount.devnodes", "mount")}
             print(json.dumps(out), flush=True)
     finally:
+        if rank_pool is not None:
+            rank_pool.close()
         if rank == 0:
             if cp is not None:
                 cp.stop()
             if sleeper is not None:
                 sleeper.kill()
                 sleeper.wait()
+            if sandbox is not None:
+                sandbox.__exit__(None, None, None)
         if world > 1:
             dist.destroy_process_group()
     return 0

@@ -120,6 +120,12 @@ class DevNode(C.Structure):
                 ("mode", C.c_uint32), ("uid", C.c_int32), ("gid", C.c_int32)]
 
 
+class BpfTiming(C.Structure):
+    _fields_ = [("query_ns", C.c_uint64), ("map_ns", C.c_uint64), ("build_ns", C.c_uint64),
+                ("load_ns", C.c_uint64), ("attach_ns", C.c_uint64), ("programs", C.c_uint32),
+                ("insns", C.c_uint32)]
+
+
 HOST_ABI_VERSION = 3          # native/include/gm_host.h GM_HOST_ABI_VERSION
 GM_ACC_MKNOD, GM_ACC_READ, GM_ACC_WRITE = 1, 2, 4
 GM_DEV_EMULATE, GM_DEV_VIA_SETNS, GM_DEV_REPLACE = 1, 2, 4
@@ -151,6 +157,8 @@ def host() -> C.CDLL:
                                            C.POINTER(DevRule), C.c_int, C.c_char_p,
                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.gm_bpf_dev_restore.argtypes = [C.c_char_p, C.c_char_p]
+        lib.gm_bpf_dev_last_timing.argtypes = [C.POINTER(BpfTiming)]
+        lib.gm_bpf_dev_last_timing.restype = None
         lib.gm_devnodes_create.argtypes = [C.c_int, C.c_char_p, C.POINTER(DevNode), C.c_int,
                                            C.c_int, C.POINTER(C.c_int)]
         lib.gm_devnodes_remove.argtypes = lib.gm_devnodes_create.argtypes

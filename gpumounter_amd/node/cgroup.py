@@ -30,7 +30,7 @@ from gpumounter_amd.models.device import DeviceNode
 from gpumounter_amd.models.pod import (QOS_BESTEFFORT, QOS_BURSTABLE, ContainerRef, qos_class,
                                        uid_of)
 from gpumounter_amd.node import bpfvm
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import log, trace
 
 _log = log.get("node.cgroup")
 
@@ -294,6 +294,14 @@ class V2BpfBackend(DeviceRuleBackend):
                                     C.byref(chained))
         if rc < 0:
             raise CgroupError(f"bpf install on {cgdir}: {os.strerror(-rc)}")
+        if trace.current() is not None:
+            tm = _native.BpfTiming()
+            lib.gm_bpf_dev_last_timing(C.byref(tm))
+            trace.record("bpf_query", tm.query_ns)
+            trace.record("bpf_build", tm.build_ns, insns=tm.insns)
+            trace.record("bpf_load_verify", tm.load_ns, programs=tm.programs)
+            trace.record("bpf_chain_map", tm.map_ns)
+            trace.record("bpf_attach", tm.attach_ns)
         log.kv(_log, 10, "bpf program installed", cgroup=cgdir, prog_id=pid.value,
                chained=chained.value, rules=len(rules))
 

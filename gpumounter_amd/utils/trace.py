@@ -124,6 +124,18 @@ def current() -> Optional[Span]:
     return _current.get()
 
 
+def record(name: str, duration_ns: int, **attrs) -> None:
+    """Attach an already-measured stage (e.g. timed inside one native call) as a child of the
+    current span, laid out back to back after the previous recorded sibling."""
+    parent = _current.get()
+    if parent is None or duration_ns <= 0:
+        return
+    start = parent.children[-1].end_ns if parent.children and parent.children[-1].end_ns \
+        else parent.start_ns
+    parent.children.append(Span(name=name, start_ns=start, end_ns=start + int(duration_ns),
+                                attrs=attrs, parent=parent))
+
+
 def annotate(**attrs) -> None:
     s = _current.get()
     if s is not None:

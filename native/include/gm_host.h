@@ -83,6 +83,14 @@ int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, int foreign_o
 // (the runtime's default device list) are compiled in instead of the tail call.
 // Returns the number of programs installed; *prog_id is the first of ours and *chained_id the
 // original it preserves (0 if none).
+// Where the last gm_bpf_dev_install on this thread spent its time (ns): query = open cgroup +
+// BPF_PROG_QUERY; map = chain-map create/pin + fd lookups; build = program generation;
+// load = BPF_PROG_LOAD including the verifier; attach = BPF_PROG_ATTACH (BPF_F_REPLACE).
+typedef struct gm_bpf_timing {
+  uint64_t query_ns, map_ns, build_ns, load_ns, attach_ns;
+  uint32_t programs, insns;
+} gm_bpf_timing_t;
+void gm_bpf_dev_last_timing(gm_bpf_timing_t* out);
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
                        const gm_dev_rule_t* base, int nbase, const char* pin_dir,
                        uint32_t* prog_id, uint32_t* chained_id);

@@ -754,15 +754,33 @@ int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, u
   return gm_bpf_dev_program_at(cgroup_path, 0, 0, insns, cap, n, prog_id, nullptr);
 }
 
+namespace {
+thread_local gm_bpf_timing_t t_bpf_timing;
+uint64_t mono_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+}  // namespace
+
+void gm_bpf_dev_last_timing(gm_bpf_timing_t* out) {
+  if (out) *out = t_bpf_timing;
+}
+
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
                        const gm_dev_rule_t* base, int nbase, const char* pin_dir,
                        uint32_t* prog_id, uint32_t* chained_id) {
+  gm_bpf_timing_t& tm = t_bpf_timing;
+  tm = gm_bpf_timing_t{};
+  uint64_t t0 = mono_ns();
   Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
   if (!cg.ok()) return -errno;
   const uint64_t ino = cgroup_ino(cg.fd);
   Attached at;
   int e = query(cg.fd, &at);
   if (e < 0) return e;
+  uint64_t t1 = mono_ns();
+  tm.query_ns += t1 - t0;
 
   // One slot per attached program. Under BPF_F_ALLOW_MULTI every program must allow an access,
   // so each one is wrapped: ours (rules → allow, else tail-call the original). A program of ours
@@ -792,6 +810,7 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
   uint32_t first_prog = 0;
   for (const Slot& sl : slots) {
     Fd chain_prog, chain_map, replace_fd;
+    t0 = mono_ns();
     if (sl.chain_id) {
       chain_prog = Fd(get_prog_fd_by_id(sl.chain_id));
       if (!chain_prog.ok()) return chain_prog.fd;
@@ -808,21 +827,32 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
     // With a chained original (or a compiled-in base list) the fall-through is deny; with
     // neither the cgroup was unrestricted, so default-allow keeps that behaviour.
     const int default_allow = (sl.chain_id || sl.ours_without_chain) ? 0 : 1;
+    t1 = mono_ns();
+    tm.map_ns += t1 - t0;
     std::vector<uint64_t> prog(16 + all.size() * 12);
     int cnt = gm_bpf_dev_build(all.data(), (int)all.size(), default_allow,
                                chain_map.ok() ? chain_map.fd : -1, prog.data(), (int)prog.size());
     if (cnt < 0) return -EINVAL;
+    uint64_t t2 = mono_ns();
+    tm.build_ns += t2 - t1;
     char log[4096];
     Fd pfd(gm_bpf_dev_load(prog.data(), cnt, kProgName, log, sizeof(log)));
     if (!pfd.ok()) return pfd.fd;
+    uint64_t t3 = mono_ns();
+    tm.load_ns += t3 - t2;
+    tm.insns += (uint32_t)cnt;
     if (chain_map.ok()) {
       e = keep_map(pin_dir, ino, sl.chain_id, chain_map.fd);
       if (e < 0) return e;
       chains.push_back(sl.chain_id);
     }
+    uint64_t t4 = mono_ns();
+    tm.map_ns += t4 - t3;
     e = attach(cg.fd, pfd.fd, replace_fd.ok() ? replace_fd.fd : -1,
                at.ids.empty() ? BPF_F_ALLOW_MULTI : at.flags);
     if (e < 0) return e;
+    tm.attach_ns += mono_ns() - t4;
+    ++tm.programs;
     if (!first_prog) {
       struct bpf_prog_info info;
       uint32_t maps[1];

@@ -9,7 +9,6 @@ kernel enforces. Prints one JSON line of observations.
 """
 import asyncio
 import ctypes as C
-import ctypes.util
 import json
 import os
 import shutil
@@ -23,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from gpumounter_amd import _native  # noqa: E402
 from gpumounter_amd.fakes.harness import LocalCluster  # noqa: E402
+from gpumounter_amd.fakes.realnode import attach_runtime_program  # noqa: E402
 from gpumounter_amd.utils import log  # noqa: E402
 
 PATHS = ["/dev/null", "/dev/zero", "/dev/full", "/dev/random"]
@@ -43,24 +43,6 @@ def probe(cg):
     if r.returncode:
         raise RuntimeError(r.stderr)
     return r.stdout.strip()
-
-
-def attach_runtime_program(cg):
-    """runc-style program: /dev/null rw + mknod only, attached with BPF_F_ALLOW_MULTI."""
-    rules = (_native.DevRule * 1)(_native.DevRule(b"c", 7, 1, 0, 1, 3))
-    lib = _native.host()
-    need = -lib.gm_bpf_dev_build(rules, 1, 0, -1, None, 0)
-    buf = (C.c_uint64 * need)()
-    n = lib.gm_bpf_dev_build(rules, 1, 0, -1, buf, need)
-    fd = lib.gm_bpf_dev_load(buf, n, b"runc_devices", None, 0)
-    assert fd >= 0, os.strerror(-fd)
-    libc = C.CDLL(ctypes.util.find_library("c"), use_errno=True)
-    cgfd = os.open(cg, os.O_RDONLY | os.O_DIRECTORY)
-    attr = (C.c_uint8 * 128)()
-    C.memmove(attr, (C.c_uint32 * 4)(cgfd, fd, 6, 2), 16)
-    rc = libc.syscall(321, 8, attr, 128)
-    os.close(cgfd)
-    assert rc == 0, os.strerror(C.get_errno())
 
 
 def prog_names(cg):

@@ -82,3 +82,38 @@ def test_baseline_config_scenarios_run_and_hold_invariants():
     assert out["contention"]["invariant_violations"] == 0
     assert out["soak"]["orphaned_cgroup_entries"] == 0 == out["soak"]["orphaned_device_nodes"]
     assert out["soak"]["placeholders_left"] == 0 == out["soak"]["gpus_still_allocated"]
+
+
+def test_bench_single_process_eight_gpus_verifies_every_per_n_field():
+    """`bench.py --gpus 8` without a launcher (what a driver may run): all 8 attached, a collective
+    over 8 spawned rank processes (gloo here, RCCL on MI355X), one hive, no non-xGMI pair."""
+    env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--steps", "3", "--warmup",
+                          "1", "--amdsmi", "mock", "--deploy", "inprocess", "--ref-steps", "0"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _last_json(res.stdout)
+    assert d["n_gpus"] == 8 and d["config"]["gpus_per_pod"] == 8
+    assert d["allreduce_backend"] == "gloo" and d["allreduce_2MiB_p50_ms"] > 0
+    assert d["rccl_allreduce_2MiB_p50_ms"] is None          # no RCCL claim without a GPU
+    assert d["attached_hives"] == 1 and d["non_xgmi_pairs"] == 0
+    assert d["node_ops"] == "emulated" and d["dtype"] == "none"
+    assert d["ledger_audit_issues"] == 0 and d["final_orphans"] == 0
+    assert d["placeholders_left"] == 0
+
+
+def test_bench_real_node_ops_reports_stage_split():
+    from gpumounter_amd.fakes import realnode
+    import pytest
+    if realnode.available() or os.environ.get("GM_PRIVILEGED_TESTS") != "1":
+        pytest.skip("needs root and GM_PRIVILEGED_TESTS=1 (mounts cgroup2/bpffs)")
+    env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
+    res = subprocess.run([sys.executable, "bench.py", "--steps", "10", "--warmup", "2",
+                          "--amdsmi", "mock", "--node-ops", "real", "--ref-steps", "0"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _last_json(res.stdout)
+    assert d["node_ops"] == "real" and d["attach_p50_real_node_ops_ms"] == d["value"]
+    st = d["real_node_ops_stage_p50_ms"]
+    assert {"bpf_load_verify", "bpf_attach", "devnodes", "cgroup_rule"} <= set(st)
+    assert d["ledger_audit_issues"] == 0 and d["final_orphans"] == 0
