@@ -4,7 +4,7 @@ Same uniform [-1, 1) bf16 operands for both (zero-filled operands overstate a GE
 through DVFS, cdna_hip_programming.md §5.4 rule 25). Variants are timed in interleaved rounds in
 one process (rule 24); the JSON reports median and best TF/s per variant and shape, plus the
 max error of ours against torch's fp32 product on a 1024³ slice. Run on the GPU box:
-``python bench/gemm_sweep.py [--rounds 5] [--variants 1,5,9]``.
+``python bench/gemm_sweep.py [--rounds 5] [--variants 1,5]``.
 """
 import argparse
 import ctypes as C
@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sizes", default="4096,8192")
     ap.add_argument("--variants", default=",".join(map(str, VARIANTS)),
-                    help="schedules of gm_probe_gemm_nt_variant to time (0-9; 5 = default)")
+                    help="schedules of gm_probe_gemm_nt_variant to time (1 or 5; 5 = default)")
     args = ap.parse_args()
     variants_sel = [int(v) for v in args.variants.split(",") if v]
     out = {"device": torch.cuda.get_device_name(0), "TFLOPs": {}, "numerics": {}}

@@ -183,6 +183,10 @@ def host() -> C.CDLL:
         lib.gm_sd_unit_path.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
         lib.gm_roctx_push.argtypes = [C.c_char_p]
         lib.gm_roctx_mark.argtypes = [C.c_char_p]
+        lib.gm_roctx_start.argtypes = [C.c_char_p]
+        lib.gm_roctx_start.restype = C.c_uint64
+        lib.gm_roctx_stop.argtypes = [C.c_uint64]
+        lib.gm_roctx_stop.restype = None
         lib.gm_now_ns.restype = C.c_uint64
         lib._gm_typed = True
     return lib

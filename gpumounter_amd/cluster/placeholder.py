@@ -89,6 +89,9 @@ def _label_value(s: str) -> str:
 
 
 class PlaceholderManager:
+    # admission re-read backoff when no placeholder event arrives: first wait, cap (seconds)
+    ADMISSION_BACKOFF_S = (0.010, 0.100)
+
     def __init__(self, cfg, kube: KubeClient, ledger: LedgerClient, informer: PodInformer,
                  node_name: str, faults=None) -> None:
         from gpumounter_amd.utils.faults import NONE
@@ -305,18 +308,26 @@ class PlaceholderManager:
     async def _await_admission(self, phs: List[Placeholder], timeout: float,
                                tolerant: bool = False) -> List[Placeholder]:
         """Wait until every placeholder is admitted and its devices are in the kubelet ledger.
-        ``tolerant``: unschedulable/failed placeholders are returned instead of raising."""
+        ``tolerant``: unschedulable/failed placeholders are returned instead of raising.
+
+        Event-driven: the kubelet ledger is read once per placeholder *event* after binding —
+        the bind itself, then the kubelet's first status update, which it posts only after
+        admission (device-plugin Allocate) — never in a tight loop: kubelets rate-limit the
+        PodResources server (100 qps, burst 10) and reject the excess with RESOURCE_EXHAUSTED.
+        Without a new event the ledger is re-read after a backoff of 10 ms doubling to 100 ms.
+        The reference instead spins on the apiserver with no sleep until the slave pod is
+        Running (reference: pkg/util/gpu/allocator/allocator.go:236-282)."""
         pending = {(p.namespace, p.name): p for p in phs}
         failed: List[Placeholder] = []
         loop = asyncio.get_running_loop()
         deadline = loop.time() + timeout
-        delay = 0.0005
-        misses = 0
+        seen: Dict[Tuple[str, str], str] = {}   # resourceVersion at our last ledger read
+        delay = self.ADMISSION_BACKOFF_S[0]
         while pending:
             failure: Dict[Tuple[str, str], str] = {}
 
             def state():
-                bound = []
+                fresh = []
                 for key in pending:
                     pod = self.informer.cache.get(key)
                     # _create put it in the cache, so gone = deleted by someone else (the
@@ -331,16 +342,25 @@ class PlaceholderManager:
                         failure[key] = f"unschedulable: {msg}"
                     elif podu.phase_of(pod) == "Failed":
                         failure[key] = pod["status"].get("reason", "Failed")
-                    elif podu.node_of(pod):
-                        bound.append(key)
+                    elif podu.node_of(pod) and \
+                            seen.get(key) != pod["metadata"].get("resourceVersion"):
+                        fresh.append(key)         # bound, and news since our last read
                     if failure and not tolerant:
                         return True
-                return True if failure else (bound or None)
+                return True if failure else (fresh or None)
 
             left = deadline - loop.time()
             if left <= 0:
                 raise ReserveError(f"timeout waiting for placeholders {sorted(pending)}")
-            ready = await self.informer.wait_for(state, timeout=left)
+            try:
+                ready = await self.informer.wait_for(
+                    state, timeout=min(left, delay) if seen else left)
+            except asyncio.TimeoutError:
+                if loop.time() >= deadline:
+                    raise ReserveError(f"timeout waiting for placeholders {sorted(pending)}")
+                # bound but no news: re-read what is bound, backing off
+                ready = [k for k in pending if k in seen]
+                delay = min(delay * 2, self.ADMISSION_BACKOFF_S[1])
             if failure and not tolerant:
                 reason = next(iter(failure.values()))
                 if reason.startswith("unschedulable") or reason.startswith("OutOf") or \
@@ -351,11 +371,16 @@ class PlaceholderManager:
                 failed.append(pending.pop(key))
             if not pending:
                 break
-            # bound: the kubelet records the allocation at admission — read the ledger
+            bound = [k for k in ready if k in pending] if isinstance(ready, list) else []
+            if not bound:
+                continue
+            for k in bound:
+                cur = self.informer.cache.get(k)
+                seen[k] = cur["metadata"].get("resourceVersion", "") if cur else ""
+            # the kubelet records the allocation at admission — read the ledger
             self.faults.check("ledger_read")
             got = None
-            bound = [k for k in ready if k in pending] if isinstance(ready, list) else []
-            if self.cfg.ledger_get and 0 < len(bound) <= 4:
+            if self.cfg.ledger_get and len(bound) <= 4:
                 res = await asyncio.gather(*[self.ledger.get(ns, n) for ns, n in bound])
                 if all(r is not None for r in res):
                     got = {k: r for k, r in zip(bound, res) if r}
@@ -371,13 +396,6 @@ class PlaceholderManager:
                     ph = pending.pop(key)
                     ph.device_ids = tuple(ids)
                     self.device_ids[ph.uid] = ph.device_ids
-            if pending:
-                # bound but not admitted yet: the kubelet admits within tens of ms, so poll its
-                # local socket every 0.5 ms for the first 20 ms, then back off (≤ 50 ms)
-                await asyncio.sleep(delay)
-                misses += 1
-                if misses > 40:
-                    delay = min(delay * 2, 0.05)
         return failed
 
     # ------------------------------------------------------------------------ release

@@ -52,6 +52,7 @@ class LocalCluster:
                  master_overrides: Optional[dict] = None,
                  device_plugin: bool = False, cgroup_root: str = "",
                  kfd_major: int = 0, start_workers: bool = True,
+                 kubelet_rate_limit: Optional[tuple] = (100.0, 10),
                  app_hook: Optional[Callable[[web.Application], None]] = None) -> None:
         self.n_nodes = n_nodes
         self.amdsmi_lib = amdsmi_lib
@@ -74,6 +75,7 @@ class LocalCluster:
         self.device_plugin = device_plugin
         self.real_cgroup_root = cgroup_root   # privileged tests: a real cgroup2 mount
         self.kfd_major = kfd_major
+        self.kubelet_rate_limit = kubelet_rate_limit
         self.node_gpu_bdfs = [b.lower() for b in node_gpu_bdfs] if node_gpu_bdfs else None
         self.nodes: Dict[str, NodeHandle] = {}
         self.master: Optional[Master] = None
@@ -125,7 +127,7 @@ class LocalCluster:
         self.cluster.add_node(node)
         sock = os.path.join(ndir, "pod-resources", "kubelet.sock")
         kubelet = FakeKubelet(node, sock, plugin_dir=os.path.join(ndir, "device-plugins")
-                              if self.device_plugin else "")
+                              if self.device_plugin else "", rate_limit=self.kubelet_rate_limit)
         await kubelet.start()
         h = NodeHandle(name, node, kubelet)
         self.nodes[name] = h

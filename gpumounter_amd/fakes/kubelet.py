@@ -13,26 +13,32 @@ from __future__ import annotations
 
 import asyncio
 import os
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import grpc
 
 from gpumounter_amd.api import deviceplugin as dp
 from gpumounter_amd.api.podresources import V1, V1ALPHA1
 from gpumounter_amd.fakes.node import FakeNode
+from gpumounter_amd.utils.ratelimit import TokenBucket
 
 
 class FakeKubelet:
     def __init__(self, node: FakeNode, socket_path: str, serve_v1: bool = True,
-                 serve_v1alpha1: bool = True, plugin_dir: str = "") -> None:
+                 serve_v1alpha1: bool = True, plugin_dir: str = "",
+                 rate_limit: Optional[Tuple[float, int]] = (100.0, 10)) -> None:
         self.node = node
+        # the kubelet's PodResources limiter (pkg/kubelet/apis/podresources: DefaultQPS 100,
+        # DefaultBurstTokens 10): over budget → RESOURCE_EXHAUSTED "rejected by rate limit"
+        self.limiter = TokenBucket(*rate_limit) if rate_limit else None
         self.socket_path = socket_path
         self.serve_v1 = serve_v1
         self.serve_v1alpha1 = serve_v1alpha1
         self.plugin_dir = plugin_dir
         self.server = None
         self.reg_server = None
-        self.calls = {"List": 0, "GetAllocatableResources": 0, "Get": 0, "Register": 0}
+        self.calls = {"List": 0, "GetAllocatableResources": 0, "Get": 0, "Register": 0,
+                      "rejected": 0}
         # device manager state
         self.plugin_endpoint = ""
         self.plugin_options = None
@@ -123,13 +129,20 @@ class FakeKubelet:
                             d.topology.nodes.add(ID=n)
         return resp
 
+    async def _police(self, context) -> None:
+        if self.limiter is not None and not self.limiter.allow():
+            self.calls["rejected"] += 1
+            await context.abort(grpc.StatusCode.RESOURCE_EXHAUSTED, "rejected by rate limit")
+
     def _list(self, api):
         async def handler(request, context):
+            await self._police(context)
             self.calls["List"] += 1
             return self._fill(api, api.ListPodResourcesResponse())
         return handler
 
     async def _allocatable(self, request, context):
+        await self._police(context)
         self.calls["GetAllocatableResources"] += 1
         resp = V1.AllocatableResourcesResponse()
         for g in self.node.gpus:
@@ -140,6 +153,7 @@ class FakeKubelet:
         return resp
 
     async def _get(self, request, context):
+        await self._police(context)
         self.calls["Get"] += 1
         resp = V1.GetPodResourcesResponse()
         key = (request.pod_namespace, request.pod_name)

@@ -10,6 +10,7 @@ v1alpha1 fallback, and results are returned as immutable records instead of muta
 from __future__ import annotations
 
 import asyncio
+import random
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -17,6 +18,7 @@ import grpc
 
 from gpumounter_amd.api.podresources import V1, V1ALPHA1
 from gpumounter_amd.utils import log
+from gpumounter_amd.utils.ratelimit import TokenBucket
 
 _log = log.get("node.ledger")
 
@@ -36,11 +38,15 @@ class LedgerError(RuntimeError):
 
 class LedgerClient:
     def __init__(self, socket_path: str, resource: str, timeout_s: float = 10.0,
-                 api: str = "auto") -> None:
+                 api: str = "auto", qps: float = 50.0, burst: int = 8) -> None:
         self.socket_path = socket_path
         self.resource = resource
         self.timeout_s = timeout_s
         self.api_pref = api
+        # paced under the kubelet's own limiter (100 qps, burst 10) with headroom for the
+        # device plugin, exporters and other node agents that share it; 0 = unpaced
+        self.bucket = TokenBucket(qps, burst) if qps > 0 else None
+        self.throttled = 0          # RESOURCE_EXHAUSTED answers seen (and retried)
         self._api = None
         self._chan: Optional[grpc.aio.Channel] = None
         self._chan_loop = None
@@ -64,13 +70,32 @@ class LedgerClient:
         return self._chan
 
     async def _call(self, path: str, req_cls, resp_cls, req):
-        """One unary call; on UNAVAILABLE (kubelet restarting: socket gone or recreated) the
-        channel is rebuilt and the call retried once, waiting up to 2 s for the new socket."""
-        try:
-            return await self._stub(path, req_cls, resp_cls)(req, timeout=self.timeout_s)
-        except grpc.aio.AioRpcError as e:
-            if e.code() != grpc.StatusCode.UNAVAILABLE:
-                raise
+        """One unary call, paced by the client token bucket. RESOURCE_EXHAUSTED (the kubelet's
+        rate limiter) is retried with jittered backoff (10 ms doubling to 200 ms) until the call's
+        deadline; on UNAVAILABLE (kubelet restarting: socket gone or recreated) the channel is
+        rebuilt and the call retried once, waiting up to 2 s for the new socket."""
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + self.timeout_s
+        backoff = 0.010
+        while True:
+            if self.bucket is not None:
+                await self.bucket.acquire()
+            try:
+                return await self._stub(path, req_cls, resp_cls)(
+                    req, timeout=max(deadline - loop.time(), 0.001))
+            except grpc.aio.AioRpcError as e:
+                code = e.code()
+                if code == grpc.StatusCode.RESOURCE_EXHAUSTED:
+                    self.throttled += 1
+                    wait = backoff * (0.5 + random.random())
+                    if loop.time() + wait >= deadline:
+                        raise
+                    await asyncio.sleep(wait)
+                    backoff = min(backoff * 2, 0.2)
+                    continue
+                if code != grpc.StatusCode.UNAVAILABLE:
+                    raise
+                break
         old, self._chan = self._chan, None
         if old is not None:
             await old.close()

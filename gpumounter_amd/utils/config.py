@@ -55,6 +55,10 @@ class Config:
     kubelet_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     kubelet_timeout_s: float = 10.0
     podresources_api: str = "auto"     # auto | v1 | v1alpha1
+    # client-side pacing of PodResources calls, under the kubelet's own limiter (100 qps,
+    # burst 10, RESOURCE_EXHAUSTED beyond it) which other node agents share; 0 = unpaced
+    kubelet_qps: float = 50.0
+    kubelet_burst: int = 8
     # --- device & isolation ----------------------------------------------------------------
     amdsmi_lib: str = ""               # "" → libamd_smi.so from ROCm; "mock" → bundled mock
     cgroup_root: str = "/sys/fs/cgroup"

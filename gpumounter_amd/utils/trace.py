@@ -87,7 +87,7 @@ class Span:
 class span:
     """``with span("cgroup_rule", gpu=3): ...`` — nests under the current span (ContextVar)."""
 
-    __slots__ = ("s", "_tok", "_lib")
+    __slots__ = ("s", "_tok", "_lib", "_rid")
 
     def __init__(self, name: str, **attrs):
         self.s = Span(name=name, attrs=attrs)
@@ -100,7 +100,9 @@ class span:
         self._tok = _current.set(self.s)
         self._lib = _roctx_lib()
         if self._lib is not None:
-            self._lib.gm_roctx_push(f"gm:{self.s.name}".encode())
+            # start/stop ranges, not push/pop: spans of concurrent asyncio tasks interleave on
+            # one thread, which a per-thread range stack would mis-nest
+            self._rid = self._lib.gm_roctx_start(f"gm:{self.s.name}".encode())
         self.s.start_ns = time.perf_counter_ns()
         return self.s
 
@@ -109,7 +111,7 @@ class span:
         if ev is not None:
             self.s.error = f"{et.__name__}: {ev}"
         if self._lib is not None:
-            self._lib.gm_roctx_pop()
+            self._lib.gm_roctx_stop(self._rid)
         _current.reset(self._tok)
         if self.s.parent is None:
             for fn in list(_sinks):

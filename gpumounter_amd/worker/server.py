@@ -59,7 +59,7 @@ class Worker:
         self.inv.ecc_policy = cfg.ecc_policy
         self.metrics = Metrics()
         self.ledger = LedgerClient(cfg.kubelet_socket, cfg.resource_name, cfg.kubelet_timeout_s,
-                                   cfg.podresources_api)
+                                   cfg.podresources_api, cfg.kubelet_qps, cfg.kubelet_burst)
         self.resolver = CgroupResolver(cfg.cgroup_root, cfg.cgroup_mode, cfg.cgroup_driver,
                                        cfg.proc_root)
         emulate = cfg.devnode_mode == "emulate" or os.environ.get("GM_BPF_EMULATE") == "1"

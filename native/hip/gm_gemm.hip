@@ -1,5 +1,7 @@
-// gm_gemm.hip — the 256²-tile bf16 burn-in GEMM and its schedules, the bit-exact burn-in loop.
-// Part of libgm_probe.so (built with gm_probe.hip). Measurements: profiles/r1_gemm/.
+// gm_gemm.hip — the 256²-tile bf16 burn-in GEMM (schedule V5, with V1 as its reference point)
+// and the bit-exact burn-in loop. Part of libgm_probe.so (built with gm_probe.hip).
+// Measurements: profiles/r1_gemm/ (round 1 also timed eight other schedules, V0 V2-V4 V6-V9;
+// none beat V5, and they were removed: the GEMM is a burn-in load, not a product kernel).
 #include <chrono>
 
 #include "gm_probe.h"
@@ -45,11 +47,9 @@ __device__ __forceinline__ void gemm_tile_of(int M, int N, int& tm, int& tn) {
   tn = (wgid % per_group) / gsize;
 }
 
-// V = 0: per 32-deep k-step, 12 fragment reads → wait → 32 MFMAs.
-// V = 1: all 24 fragment reads of the 64-deep K-tile issued up front, so the second k-step's
-//        reads overlap the first step's MFMAs (+48 VGPRs).
-// V = 3: V1's schedule on v_mfma_f32_32x32x16_bf16 (same 128×64 per wave: 4×2 32² blocks).
-template <int V>
+// V1 — the plain schedule, kept as the reference point for V5: all 24 fragment reads of the
+// 64-deep K-tile are issued up front, so the second k-step's reads overlap the first step's
+// MFMAs, then one vmcnt(0) + barrier per K-tile.
 __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A,
                                                     const __bf16* __restrict__ Bt,
                                                     __bf16* __restrict__ C, int M, int N, int K) {
@@ -88,24 +88,11 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
   const int a_off = wm * 128 * 128 + foff0;
   const int b_off = kTileBytes + wn * 64 * 128 + foff0;
 
-  f32x4 acc[V == 3 ? 1 : 8][4];
-  f32x16 acc32[V == 3 ? 4 : 1][2];
-  if constexpr (V == 3) {
+  f32x4 acc[8][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const int r32 = lane & 31, h32 = lane >> 5, sw32 = (r32 >> 1) & 7;
-  const int a32_off = wm * 128 * 128 + r32 * 128;
-  const int b32_off = kTileBytes + wn * 64 * 128 + r32 * 128;
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nt = K / TK;
   stage(0, 0);
@@ -115,51 +102,7 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
     const int cur = t & 1;
     if (t + 1 < nt) stage(cur ^ 1, (t + 1) * TK);
     const char* sb = lds + cur * kStageBytes;
-    if constexpr (V == 0) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[8], bfr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 16 * 128) ^ (kk << 6)));
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          af[i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 16 * 128) ^ (kk << 6)));
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    } else if constexpr (V == 3) {
-      // 32x32x16 shape, same per-wave 128×64 tile: 4×2 blocks, 4 k16-steps per K-tile.
-      // Lane l reads row (l&31) of a 32-row block at logical chunk 2s + (l>>5).
-      bf16x8 af[4][4], bfr[4][2];
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          bfr[st][j] = *reinterpret_cast<const bf16x8*>(sb + b32_off + j * 32 * 128 +
-                                                        ((((st * 2 + h32) ^ sw32)) << 4));
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          af[st][i] = *reinterpret_cast<const bf16x8*>(sb + a32_off + i * 32 * 128 +
-                                                       ((((st * 2 + h32) ^ sw32)) << 4));
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int st = 0; st < 4; ++st)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[st][i], bfr[st][j],
-                                                                  acc32[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    } else {
+    {
       bf16x8 af[2][8], bfr[2][4];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -187,20 +130,6 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
     __syncthreads();
   }
 
-  if constexpr (V == 3) {
-    // C/D map of 32x32x16: col = l&31, row = (reg&3) + 8(reg>>2) + 4(l>>5).
-    const int crow = tm * TM + wm * 128 + 4 * h32;
-    const int ccol = tn * TN + wn * 64 + r32;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          C[(size_t)(crow + i * 32 + (r & 3) + 8 * (r >> 2)) * N + ccol + j * 32] =
-              (__bf16)acc32[i][j][r];
-    return;
-  }
   // Epilogue: C/D map of 16x16x32: col = l&15, row = 4(l>>4) + reg.
   const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
   const int ccol = tn * TN + wn * 64 + (lane & 15);
@@ -213,449 +142,11 @@ __global__ __launch_bounds__(512) void k_gemm_nt256(const __bf16* __restrict__ A
         C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
 }
 
-// V2 — quadrant phases with half-tile staging (same LDS budget, deeper pipeline). Measured
-// 7-8 % slower than V1 on MI355X (profiles/r1_gemm): kept as the tested counter-example.
-// Each stage's A and B tiles are split into row halves (lo = rows 0-127, hi = 128-255) of 16 KiB,
-// giving 8 half-tile slots in the 128 KiB. Wave (wm, wn) owns A rows {wm*64 + [0,64)} of both
-// halves and B rows {wn*32 + [0,32)} of both, i.e. four 64×32 output quadrants. A K-tile runs
-// as 4 phases, one quadrant each, in the order (Alo,Blo) (Alo,Bhi) (Ahi,Bhi) (Ahi,Blo). Operands
-// are carried in registers between neighbouring phases, so each half-tile is read from LDS in
-// exactly one phase.
-// Half-tiles are loaded in consumption order L[m] (m = 4t + {Alo, Blo, Bhi, Ahi}) into slot m%8.
-// Phase p issues L[p+6] and ends with a counted vmcnt that retires only what phase p+1 reads,
-// then a raw s_barrier. So 4-5 half-tiles (2 glds each) stay in flight across every barrier,
-// where V0/V1 drain to vmcnt(0) once per K-tile.
-// WAR: L[m+8] overwrites L[m]'s slot. It is issued in phase m+2, and L[m] was last read in
-// phase ≤ m, with a barrier between.
-__device__ __forceinline__ void vm_wait_glds(int n) {  // n = glds allowed in flight (uniform)
-  switch (n) {
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-template <int Q>
-struct QPhase {
-  static constexpr int value = Q;
-};
-
-__global__ __launch_bounds__(512) void k_gemm_nt256q(const __bf16* __restrict__ A,
-                                                     const __bf16* __restrict__ Bt,
-                                                     __bf16* __restrict__ C, int M, int N,
-                                                     int K) {
-  using namespace g256;
-  constexpr int kHalf = 16384, kAhead = 6;
-  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  int tm, tn;
-  gemm_tile_of(M, N, tm, tn);
-
-  // Half-tile staging: wave w moves 1 KiB chunks w and w+8 (rows 8c + (l>>3) of the half).
-  const int srow = 8 * wave + (lane >> 3);
-  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
-  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
-  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
-  const size_t row64 = (size_t)64 * K, row128 = (size_t)128 * K;
-  const int nt = K / TK, last = 4 * nt - 1;
-
-  auto issue = [&](int m) {  // L[m]: kind m&3 = 0 Alo, 1 Blo, 2 Bhi, 3 Ahi; tile m>>2
-    const int kind = m & 3;
-    const __bf16* src = ((kind == 0 || kind == 3) ? a_src : b_src) +
-                        (kind >= 2 ? row128 : (size_t)0) + (m >> 2) * TK;
-    char* dst = lds + (m & 7) * kHalf + wave * 1024;
-    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((gbl_void*)(src + row64), (lds_void*)(dst + 8192), 16, 0,
-                                     0);
-  };
-
-  const int frow = lane & 15;
-  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
-  const int a_off = wm * 64 * 128 + foff0;
-  const int b_off = wn * 32 * 128 + foff0;
-
-  f32x4 acc[2][2][4][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[2][4], fbl[2][2], fbh[2][2];
-
-  auto read_a = [&](const char* base) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        fa[kk][i] = *reinterpret_cast<const bf16x8*>(base + ((a_off + i * 2048) ^ (kk << 6)));
-  };
-  auto read_b = [&](const char* base, bf16x8 (&fb)[2][2]) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[kk][j] = *reinterpret_cast<const bf16x8*>(base + ((b_off + j * 2048) ^ (kk << 6)));
-  };
-  auto mma = [&](f32x4 (&c)[4][2], bf16x8 (&fb)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], c[i][j], 0, 0,
-                                                            0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  auto phase = [&](auto qc, int t) {
-    constexpr int q = decltype(qc)::value;
-    const int p = 4 * t + q;
-    const char* slot = lds + ((4 * t) & 7) * kHalf;  // Alo of tile t; +1..3 halves follow
-    if constexpr (q == 0) {
-      read_b(slot + 1 * kHalf, fbl);
-      read_a(slot + 0 * kHalf);
-    } else if constexpr (q == 1) {
-      read_b(slot + 2 * kHalf, fbh);
-    } else if constexpr (q == 2) {
-      read_a(slot + 3 * kHalf);
-    }
-    if (p + kAhead <= last) issue(p + kAhead);
-    if constexpr (q == 0) mma(acc[0][0], fbl);
-    if constexpr (q == 1) mma(acc[0][1], fbh);
-    if constexpr (q == 2) mma(acc[1][1], fbh);
-    if constexpr (q == 3) mma(acc[1][0], fbl);
-    if (p < last) {
-      // phase p+1 reads up to L[need]: Bhi(t) after q0, Ahi(t) after q1/q2, Blo(t+1) after q3
-      constexpr int need_rel = q == 0 ? 2 : (q == 3 ? 5 : 3);
-      const int issued = min(p + kAhead, last);
-      vm_wait_glds(2 * (issued - (4 * t + need_rel)));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-  };
-
-  // Prologue: L[0..6] in flight; retire L[0], L[1] (Alo, Blo of tile 0).
-  const int pre = min(kAhead, last);
-  for (int m = 0; m <= pre; ++m) issue(m);
-  vm_wait_glds(2 * (pre - 1));
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  for (int t = 0; t < nt; ++t) {
-    phase(QPhase<0>{}, t);
-    phase(QPhase<1>{}, t);
-    phase(QPhase<2>{}, t);
-    phase(QPhase<3>{}, t);
-  }
-
-  const int crow = tm * TM + wm * 64 + 4 * (lane >> 4);
-  const int ccol = tn * TN + wn * 32 + (lane & 15);
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            C[(size_t)(crow + x * 128 + i * 16 + r) * N + ccol + y * 128 + j * 16] =
-                (__bf16)acc[x][y][i][j][r];
-}
-
-// V4 — measured 7-13 % slower than V1 on MI355X (profiles/r1_gemm).
-// 4 waves (2×2), each 128×128 = 8×8 16x16x32 accumulators (256 fp32/lane: the MFMA
-// destinations live in AGPRs, 1 wave per SIMD). A fragment read feeds 8 MFMAs instead of 4,
-// so LDS read traffic per K-tile drops by a third against V1; latency hiding is then
-// up to the single wave's own schedule: all 32 fragment reads of the K-tile are issued
-// before its 128 MFMAs.
-__global__ __launch_bounds__(256) void k_gemm_nt256w4(const __bf16* __restrict__ A,
-                                                      const __bf16* __restrict__ Bt,
-                                                      __bf16* __restrict__ C, int M, int N,
-                                                      int K) {
-  using namespace g256;
-  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  int tm, tn;
-  gemm_tile_of(M, N, tm, tn);
-
-  // Staging: wave w moves chunks c = w + 4i (i = 0..7), rows 8c + (l>>3): rows differ by 32
-  // between i, so (row>>1)&7 is again the same for all of a lane's chunks.
-  const int srow = 8 * wave + (lane >> 3);
-  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
-  const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
-  const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
-  const size_t row32 = (size_t)32 * K;
-  auto stage = [&](int buf, int k0) {
-    char* base = lds + buf * kStageBytes + wave * 1024;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row32 + k0),
-                                       (lds_void*)(base + i * 4096), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row32 + k0),
-                                       (lds_void*)(base + kTileBytes + i * 4096), 16, 0, 0);
-    }
-  };
-  const int frow = lane & 15;
-  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
-  const int a_off = wm * 128 * 128 + foff0;
-  const int b_off = kTileBytes + wn * 128 * 128 + foff0;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nt = K / TK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nt) stage(cur ^ 1, (t + 1) * TK);
-    const char* sb = lds + cur * kStageBytes;
-    bf16x8 af[2][8], bfr[2][8];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 2048) ^ (kk << 6)));
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        af[kk][i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 2048) ^ (kk << 6)));
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
-  const int ccol = tn * TN + wn * 128 + (lane & 15);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
-}
-
-// Coalesced epilogue for one 16×16 accumulator tile. Lane l = 16q + 4a + p holds rows
-// 4q..4q+3 of column 4a+p. Two quad-local DPP exchanges (xor 1, xor 2) on packed bf16 pairs
-// transpose each 4×4 block, so lane p ends up with row 4q+p, columns 4a..4a+3, and stores them
-// with one 8-byte store. That is 32 stores per wave instead of 128 two-byte ones.
-__device__ __forceinline__ uint32_t bf16_bits(float x) {
-  const __bf16 h = (__bf16)x;
-  return (uint32_t)__builtin_bit_cast(uint16_t, h);
-}
-__device__ __forceinline__ void store_tile_quad(__bf16* __restrict__ C, size_t ld, int row0,
-                                                int col0, const f32x4& v, int lane) {
-  const int p = lane & 3, p1 = p & 1, p2 = (p >> 1) & 1;
-  const uint32_t b0 = bf16_bits(v[0]), b1 = bf16_bits(v[1]), b2 = bf16_bits(v[2]),
-                 b3 = bf16_bits(v[3]);
-  // stage 1 (partner p^1): keep rows p1, p1+2 of my column; send the other two rows
-  const uint32_t send1 = p1 ? (b0 | (b2 << 16)) : (b1 | (b3 << 16));
-  const uint32_t recv1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)send1, 0xB1, 0xF, 0xF, false);
-  const uint32_t ka = p1 ? b1 : b0, kb = p1 ? b3 : b2;         // rows p1, p1+2 at column p
-  const uint32_t ra = recv1 & 0xFFFF, rb = recv1 >> 16;         // same rows at column p^1
-  const uint32_t rowA = p1 ? (ra | (ka << 16)) : (ka | (ra << 16));  // row p1, cols (p&~1)+0,1
-  const uint32_t rowB = p1 ? (rb | (kb << 16)) : (kb | (rb << 16));  // row p1+2
-  // stage 2 (partner p^2): keep row p = p1 + 2*p2, send the other one
-  const uint32_t keep2 = p2 ? rowB : rowA, send2 = p2 ? rowA : rowB;
-  const uint32_t recv2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)send2, 0x4E, 0xF, 0xF, false);
-  uint2 out;
-  out.x = p2 ? recv2 : keep2;                                  // columns 4a+0, 4a+1
-  out.y = p2 ? keep2 : recv2;                                  // columns 4a+2, 4a+3
-  const int q = lane >> 4, a = (lane >> 2) & 3;
-  *reinterpret_cast<uint2*>(C + (size_t)(row0 + 4 * q + p) * ld + col0 + 4 * a) = out;
-}
-
-// Buffer-resource LDS DMA (buffer_load_dwordx4 … lds): gfx9-family resource word 3 =
-// 0x00020000 (raw, untyped), stride 0, num_records = size in bytes (range-checked).
-typedef __attribute__((address_space(3))) void lds_any;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
-                                           0x00020000);
-}
-
-// V9 — V2's quadrant phases with the next phase's operand read into registers during the
-// current phase's MFMAs. So the counted vmcnt at the end of phase p retires what phase p+2 reads.
-// Reads per phase: q0 reads Bhi(t), q1 reads Ahi(t), q3 reads Alo(t+1) and Blo(t+1). Blo(t) is
-// still in use in q3, so Blo alternates between two register sets by tile parity. The tile
-// loop is unrolled by two so every index stays compile-time.
-// WAR: L[m+8] is issued in phase m+2; L[m] was last read in phase ≤ m-1, with barriers between.
-__global__ __launch_bounds__(512) void k_gemm_nt256q2(const __bf16* __restrict__ A,
-                                                      const __bf16* __restrict__ Bt,
-                                                      __bf16* __restrict__ C, int M, int N,
-                                                      int K) {
-  using namespace g256;
-  constexpr int kHalf = 16384, kAhead = 6;
-  constexpr int kWaitLgkm0 = 0xC07F;
-  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  int tm, tn;
-  gemm_tile_of(M, N, tm, tn);
-  const int srow = 8 * wave + (lane >> 3);
-  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
-  // buffer_load … lds from SGPR resources: one 32-bit per-lane offset (global_load_lds with
-  // per-lane 64-bit pointers spilled 16 VGPRs here)
-  const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc(A + (size_t)tm * TM * K, (uint32_t)TM * K * 2);
-  const __amdgpu_buffer_rsrc_t b_rsrc =
-      make_rsrc(Bt + (size_t)tn * TN * K, (uint32_t)TN * K * 2);
-  const int lane_off = (srow * K + schunk * 8) * 2;
-  const int nt = K / TK, last = 4 * nt - 1;
-  auto issue = [&](int m) {  // L[m]: kind m&3 = 0 Alo, 1 Blo, 2 Bhi, 3 Ahi; tile m>>2
-    const int kind = m & 3;
-    const int soff = __builtin_amdgcn_readfirstlane(((kind >= 2 ? 128 * K : 0) + (m >> 2) * TK) * 2);
-    char* dst = lds + (m & 7) * kHalf + wave * 1024;
-    if (kind == 0 || kind == 3) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)dst, 16, lane_off, soff, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)(dst + 8192), 16, lane_off,
-                                               soff + 64 * K * 2, 0, 0);
-    } else {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)dst, 16, lane_off, soff, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)(dst + 8192), 16, lane_off,
-                                               soff + 64 * K * 2, 0, 0);
-    }
-  };
-  const int frow = lane & 15;
-  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
-  const int a_off = wm * 64 * 128 + foff0;
-  const int b_off = wn * 32 * 128 + foff0;
-  auto slot = [&](int m) -> const char* { return lds + (m & 7) * kHalf; };
-
-  f32x4 acc[2][2][4][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fal[2][4], fah[2][4], fbl[2][2][2], fbh[2][2];
-  auto read_a = [&](const char* base, bf16x8 (&fa)[2][4]) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        fa[kk][i] = *reinterpret_cast<const bf16x8*>(base + ((a_off + i * 2048) ^ (kk << 6)));
-  };
-  auto read_b = [&](const char* base, bf16x8 (&fb)[2][2]) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[kk][j] = *reinterpret_cast<const bf16x8*>(base + ((b_off + j * 2048) ^ (kk << 6)));
-  };
-  auto mma = [&](f32x4 (&c)[4][2], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], c[i][j], 0, 0,
-                                                            0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  // end of phase p: retire what phase p+1 will read (L[p+3]; after q1 nothing new: L[p+2])
-  auto end_phase = [&](int p, int need) {
-    if (p >= last) return;
-    vm_wait_glds(2 * (min(p + kAhead, last) - min(need, last)));
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  auto tile = [&](auto par_c, int t) {
-    constexpr int par = decltype(par_c)::value;
-    const int p0 = 4 * t;
-    // q0: (Alo, Blo); read Bhi(t)
-    read_b(slot(p0 + 2), fbh);
-    if (p0 + kAhead <= last) issue(p0 + kAhead);
-    mma(acc[0][0], fal, fbl[par]);
-    end_phase(p0, p0 + 3);
-    // q1: (Alo, Bhi); read Ahi(t)
-    read_a(slot(p0 + 3), fah);
-    if (p0 + 1 + kAhead <= last) issue(p0 + 1 + kAhead);
-    mma(acc[0][1], fal, fbh);
-    end_phase(p0 + 1, p0 + 3);
-    // q2: (Ahi, Bhi)
-    if (p0 + 2 + kAhead <= last) issue(p0 + 2 + kAhead);
-    mma(acc[1][1], fah, fbh);
-    end_phase(p0 + 2, p0 + 5);
-    // q3: (Ahi, Blo); read Alo(t+1), Blo(t+1)
-    if (t + 1 < nt) {
-      read_a(slot(p0 + 4), fal);
-      read_b(slot(p0 + 5), fbl[par ^ 1]);
-    }
-    if (p0 + 3 + kAhead <= last) issue(p0 + 3 + kAhead);
-    mma(acc[1][0], fah, fbl[par]);
-    end_phase(p0 + 3, p0 + 6);
-  };
-
-  // Prologue: L[0..6] in flight; retire L[0..2] (q0 of tile 0 reads Bhi(0) = L[2]).
-  const int pre = min(kAhead, last);
-  for (int m = 0; m <= pre; ++m) issue(m);
-  vm_wait_glds(2 * (pre - min(2, last)));
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  read_a(slot(0), fal);
-  read_b(slot(1), fbl[0]);
-  for (int t = 0; t < nt; t += 2) {
-    tile(QPhase<0>{}, t);
-    if (t + 1 < nt) tile(QPhase<1>{}, t + 1);
-  }
-
-  const int crow = tm * TM + wm * 64 + 4 * (lane >> 4);
-  const int ccol = tn * TN + wn * 32 + (lane & 15);
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            C[(size_t)(crow + x * 128 + i * 16 + r) * N + ccol + y * 128 + j * 16] =
-                (__bf16)acc[x][y][i][j][r];
-}
-
 // V5 — V1's geometry with a local-read prefetch across the barrier. The second k-step's MFMAs
 // of tile t are deferred past the barrier, so they run while the first k-step fragments of
 // tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
 // register use stays at two fragment sets (like V1). The barrier sits mid-tile, so the next
 // tile's DMA is issued right after it.
-template <bool kBufDma, bool kQuadStore = false>
 __global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ A,
                                                      const __bf16* __restrict__ Bt,
                                                      __bf16* __restrict__ C, int M, int N,
@@ -672,28 +163,14 @@ __global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ 
   const __bf16* a_src = A + (size_t)(tm * TM + srow) * K + schunk * 8;
   const __bf16* b_src = Bt + (size_t)(tn * TN + srow) * K + schunk * 8;
   const size_t row64 = (size_t)64 * K;
-  // kBufDma (V7): the same DMA as buffer_load … lds from SGPR resources plus one 32-bit
-  // per-lane offset, instead of eight per-lane 64-bit source pointers.
-  const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc(A + (size_t)tm * TM * K, (uint32_t)TM * K * 2);
-  const __amdgpu_buffer_rsrc_t b_rsrc =
-      make_rsrc(Bt + (size_t)tn * TN * K, (uint32_t)TN * K * 2);
-  const int lane_off = (srow * K + schunk * 8) * 2;
   auto stage = [&](int buf, int k0) {
     char* base = lds + buf * kStageBytes + wave * 1024;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if constexpr (kBufDma) {
-        const int soff = __builtin_amdgcn_readfirstlane((i * 64 * K + k0) * 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)(base + i * 8192), 16,
-                                                 lane_off, soff, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)(base + kTileBytes + i * 8192),
-                                                 16, lane_off, soff, 0, 0);
-      } else {
-        __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row64 + k0),
-                                         (lds_void*)(base + i * 8192), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row64 + k0),
-                                         (lds_void*)(base + kTileBytes + i * 8192), 16, 0, 0);
-      }
+      __builtin_amdgcn_global_load_lds((gbl_void*)(a_src + i * row64 + k0),
+                                       (lds_void*)(base + i * 8192), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(b_src + i * row64 + k0),
+                                       (lds_void*)(base + kTileBytes + i * 8192), 16, 0, 0);
     }
   };
   const int frow = lane & 15;
@@ -751,125 +228,12 @@ __global__ __launch_bounds__(512) void k_gemm_nt256p(const __bf16* __restrict__ 
     mma(a1, b1);
   }
 
-  if constexpr (kQuadStore) {  // V8: transposed in quads, 8-byte stores
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        store_tile_quad(C, (size_t)N, tm * TM + wm * 128 + i * 16, tn * TN + wn * 64 + j * 16,
-                        acc[i][j], lane);
-    return;
-  }
   const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
   const int ccol = tn * TN + wn * 64 + (lane & 15);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
-}
-
-// V6 — V4's geometry (4 waves × 128², AGPR accumulators) on V5's schedule.
-// (V5:) V1's geometry with a local-read prefetch across the barrier. The second k-step's MFMAs
-// of tile t are deferred past the barrier, so they run while the first k-step fragments of
-// tile t+1 are read. Every fragment-read batch then overlaps 32 MFMAs of the same wave, and
-// register use stays at two fragment sets (like V1). The barrier sits mid-tile, so the next
-// tile's DMA is issued right after it.
-__global__ __launch_bounds__(256) void k_gemm_nt256w4p(const __bf16* __restrict__ A,
-                                                     const __bf16* __restrict__ Bt,
-                                                     __bf16* __restrict__ C, int M, int N,
-                                                     int K) {
-  using namespace g256;
-  __shared__ __attribute__((aligned(1024))) char lds[kLdsBytes];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  int tm, tn;
-  gemm_tile_of(M, N, tm, tn);
-  const int srow = 8 * wave + (lane >> 3);
-  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);
-  // buffer_load … lds: the block's A/B panels as buffer resources (SGPRs), one 32-bit per-lane
-  // byte offset, the per-load row/k offset in soffset (SGPR). Two VGPRs of addressing instead
-  // of sixteen 64-bit pointers (which spilled), and range-checked: an out-of-panel read
-  // returns zeros instead of faulting.
-  const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc(A + (size_t)tm * TM * K, (uint32_t)TM * K * 2);
-  const __amdgpu_buffer_rsrc_t b_rsrc =
-      make_rsrc(Bt + (size_t)tn * TN * K, (uint32_t)TN * K * 2);
-  const int lane_off = (srow * K + schunk * 8) * 2;
-  auto stage = [&](int buf, int k0) {
-    char* base = lds + buf * kStageBytes + wave * 1024;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int soff = __builtin_amdgcn_readfirstlane((i * 32 * K + k0) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_any*)(base + i * 4096), 16, lane_off,
-                                               soff, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_any*)(base + kTileBytes + i * 4096),
-                                               16, lane_off, soff, 0, 0);
-    }
-  };
-  const int frow = lane & 15;
-  const int foff0 = frow * 128 + (((lane >> 4) ^ (frow >> 1)) << 4);
-  const int a_off = wm * 128 * 128 + foff0;
-  const int b_off = kTileBytes + wn * 128 * 128 + foff0;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
-  auto read = [&](const char* sb, int kk, bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      bf[j] = *reinterpret_cast<const bf16x8*>(sb + ((b_off + j * 2048) ^ (kk << 6)));
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(sb + ((a_off + i * 2048) ^ (kk << 6)));
-  };
-  auto mma = [&](bf16x8 (&af)[8], bf16x8 (&bf)[8]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  const int nt = K / TK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // Waits go through __builtin_amdgcn_s_waitcnt (gfx9 simm16: vmcnt[3:0]|expcnt[6:4]|
-  // lgkmcnt[11:8]|vmcnt[5:4]<<14), not inline asm, so the compiler's own wait insertion knows
-  // the counters are clear and adds no lgkmcnt(0) in front of the MFMAs.
-  constexpr int kWaitLgkm0 = 0xC07F, kWaitVm0Lgkm0 = 0x0070;
-  // Tile t+1's DMA is issued right after the barrier that frees its buffer (mid-tile t-1), so
-  // it has a whole tile of MFMAs (64 per wave) to land before the vmcnt(0) that retires it.
-  if (nt > 1) stage(1, TK);
-  read(lds, 0, a0, b0);
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    const char* sb = lds + cur * kStageBytes;
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // a0/b0 (read behind the last 32 MFMAs) are in
-    read(sb, 1, a1, b1);
-    mma(a0, b0);
-    __builtin_amdgcn_s_waitcnt(kWaitVm0Lgkm0);  // tile t+1 landed; our reads of `cur` done
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + 2 < nt) stage(cur, (t + 2) * TK);   // every wave is past its reads of `cur`
-    if (t + 1 < nt) read(lds + (cur ^ 1) * kStageBytes, 0, a0, b0);
-    mma(a1, b1);
-  }
-
-  const int crow = tm * TM + wm * 128 + 4 * (lane >> 4);
-  const int ccol = tn * TN + wn * 128 + (lane & 15);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         C[(size_t)(crow + i * 16 + r) * N + ccol + j * 16] = (__bf16)acc[i][j][r];
@@ -913,44 +277,12 @@ int gm_probe_gemm_nt_variant(int variant, const void* A, const void* Bt, void* C
   if (M <= 0 || N <= 0 || K <= 0 || M % TM || N % TN || K % TK) return (int)hipErrorInvalidValue;
   const dim3 grid((M / TM) * (N / TN)), block(kThreads);
   switch (variant) {
-    case 0:
-      hipLaunchKernelGGL(k_gemm_nt256<0>, grid, block, 0, (hipStream_t)stream,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-      break;
     case 1:
-      hipLaunchKernelGGL(k_gemm_nt256<1>, grid, block, 0, (hipStream_t)stream,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-      break;
-    case 3:
-      hipLaunchKernelGGL(k_gemm_nt256<3>, grid, block, 0, (hipStream_t)stream,
+      hipLaunchKernelGGL(k_gemm_nt256, grid, block, 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     case 5:
-      hipLaunchKernelGGL(k_gemm_nt256p<false>, grid, block, 0, (hipStream_t)stream,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-      break;
-    case 7:
-      hipLaunchKernelGGL(k_gemm_nt256p<true>, grid, block, 0, (hipStream_t)stream,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-      break;
-    case 9:
-      hipLaunchKernelGGL(k_gemm_nt256q2, grid, block, 0, (hipStream_t)stream,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-      break;
-    case 8:
-      hipLaunchKernelGGL((k_gemm_nt256p<false, true>), grid, block, 0, (hipStream_t)stream,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-      break;
-    case 6:
-      hipLaunchKernelGGL(k_gemm_nt256w4p, grid, dim3(256), 0, (hipStream_t)stream,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-      break;
-    case 4:
-      hipLaunchKernelGGL(k_gemm_nt256w4, grid, dim3(256), 0, (hipStream_t)stream,
-                         (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
-      break;
-    case 2:
-      hipLaunchKernelGGL(k_gemm_nt256q, grid, block, 0, (hipStream_t)stream,
+      hipLaunchKernelGGL(k_gemm_nt256p, grid, block, 0, (hipStream_t)stream,
                          (const __bf16*)A, (const __bf16*)Bt, (__bf16*)C, M, N, K);
       break;
     default:

@@ -166,6 +166,9 @@ int gm_roctx_available(void);
 void gm_roctx_push(const char* name);
 void gm_roctx_pop(void);
 void gm_roctx_mark(const char* name);
+// Start/stop ranges (not a per-thread stack): correct for spans of interleaved asyncio tasks.
+uint64_t gm_roctx_start(const char* name);
+void gm_roctx_stop(uint64_t id);
 uint64_t gm_now_ns(void);
 
 int gm_host_abi_version(void);

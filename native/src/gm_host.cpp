@@ -528,6 +528,8 @@ struct Roctx {
   int (*push)(const char*) = nullptr;
   int (*pop)() = nullptr;
   void (*mark)(const char*) = nullptr;
+  uint64_t (*start)(const char*) = nullptr;
+  void (*stop)(uint64_t) = nullptr;
 };
 Roctx g_roctx;
 
@@ -546,6 +548,8 @@ void roctx_init() {
     g_roctx.push = reinterpret_cast<int (*)(const char*)>(dlsym(dl, "roctxRangePushA"));
     g_roctx.pop = reinterpret_cast<int (*)()>(dlsym(dl, "roctxRangePop"));
     g_roctx.mark = reinterpret_cast<void (*)(const char*)>(dlsym(dl, "roctxMarkA"));
+    g_roctx.start = reinterpret_cast<uint64_t (*)(const char*)>(dlsym(dl, "roctxRangeStartA"));
+    g_roctx.stop = reinterpret_cast<void (*)(uint64_t)>(dlsym(dl, "roctxRangeStop"));
   });
 }
 
@@ -1099,6 +1103,14 @@ void gm_roctx_push(const char* name) {
 void gm_roctx_pop(void) {
   roctx_init();
   if (g_roctx.pop) g_roctx.pop();
+}
+uint64_t gm_roctx_start(const char* name) {
+  roctx_init();
+  return g_roctx.start ? g_roctx.start(name) : 0;
+}
+void gm_roctx_stop(uint64_t id) {
+  roctx_init();
+  if (g_roctx.stop && id) g_roctx.stop(id);
 }
 void gm_roctx_mark(const char* name) {
   roctx_init();

@@ -129,7 +129,7 @@ def test_mfma_gemm_asymmetric_identity():
     assert torch.equal(c, b.float())
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [1, 5])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 64), (512, 768, 192), (1280, 1024, 640)])
 def test_gemm_nt256_matches_torch_fp32(m, n, k, variant):
     """The 256²-tile global_load_lds GEMM (odd tile counts exercise the XCD remap's remainder
@@ -147,7 +147,7 @@ def test_gemm_nt256_matches_torch_fp32(m, n, k, variant):
     assert (err <= ref.abs() * 2 ** -8 + 1e-3 * k ** 0.5).all(), err.max().item()
 
 
-@pytest.mark.parametrize("variant", [None, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("variant", [None, 1, 5])
 def test_gemm_nt256_asymmetric_identity(variant):
     """A = I with an asymmetric Bt: C must equal Btᵀ exactly (catches row/col swaps, swizzle
     mismatches between the staged source and the LDS read)."""
@@ -224,6 +224,32 @@ def test_p2p_if_multi_gpu():
     m = xgmi_matrix([0, 1], 64 << 20, 3)
     assert m["peer"][0][1]
     assert m["gbps"][0][1] > 10
+
+
+def test_rank_pool_rccl_child_on_the_attached_gpu():
+    """bench.py's single-process N>1 path: a rank process spawned by a parent that has not touched
+    the GPU binds to the attached GPU by PCI address and runs a checked RCCL all-reduce."""
+    import subprocess as sp
+    code = ("import json; from gpumounter_amd.parallel.rankpool import RankPool; "
+            "from gpumounter_amd.hw.inventory import Inventory; "
+            "bdf = Inventory('').gpus()[0].bdf; p = RankPool(1); "
+            "r = [p.allreduce([bdf]) for _ in range(2)]; print(json.dumps(r[-1])); "
+            "print(json.dumps(p.close()))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = sp.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                 timeout=180)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    import json
+    r = json.loads(out[0])
+    assert r["ok"] and r["backend"] == "nccl" and r["ms"] > 0
+    assert json.loads(out[1]) == {"0": 0}
+
+
+def test_unknown_gemm_schedule_is_rejected():
+    from gpumounter_amd import _native
+    lib = _native.probe()
+    assert lib.gm_probe_gemm_nt_variant(3, None, None, None, 256, 256, 64, None) != 0
 
 
 def _hip_child_code() -> str:
