@@ -1,11 +1,39 @@
 #!/usr/bin/env bash
 # deploy | redeploy | uninstall — same verbs as the reference's deploy.sh.
+# deploy also creates the master⇄worker mTLS Secret (gpu-mounter-tls) once, with openssl: a
+# private CA plus one certificate per identity (SAN gpu-mounter-worker / gpu-mounter-master).
 set -euo pipefail
 cd "$(dirname "$0")"
 FILES=(deploy/namespace.yaml deploy/rbac.yaml deploy/placeholder-priority.yaml
-       deploy/gpu-mounter-workers.yaml deploy/gpu-mounter-master.yaml deploy/gpu-mounter-svc.yaml)
-apply()  { for f in "${FILES[@]}"; do kubectl apply -f "$f"; done; }
-remove() { for ((i=${#FILES[@]}-1; i>=0; i--)); do kubectl delete --ignore-not-found -f "${FILES[$i]}"; done; }
+       deploy/gpu-mounter-workers.yaml deploy/gpu-mounter-master.yaml deploy/gpu-mounter-svc.yaml
+       deploy/networkpolicy.yaml)
+NS=kube-system
+SECRET=gpu-mounter-tls
+
+pki() {
+  kubectl -n "$NS" get secret "$SECRET" >/dev/null 2>&1 && return 0
+  local d
+  d=$(mktemp -d)
+  trap 'rm -rf "$d"' RETURN
+  openssl req -x509 -newkey rsa:3072 -nodes -keyout "$d/ca.key" -out "$d/ca.crt" -days 825 \
+      -subj "/CN=gpumounter-ca" 2>/dev/null
+  for id in worker master; do
+    printf 'subjectAltName=DNS:gpu-mounter-%s\nextendedKeyUsage=serverAuth,clientAuth\n' "$id" \
+        > "$d/$id.ext"
+    openssl req -newkey rsa:3072 -nodes -keyout "$d/$id.key" -out "$d/$id.csr" \
+        -subj "/CN=gpu-mounter-$id" 2>/dev/null
+    openssl x509 -req -in "$d/$id.csr" -CA "$d/ca.crt" -CAkey "$d/ca.key" -CAcreateserial \
+        -out "$d/$id.crt" -days 825 -extfile "$d/$id.ext" 2>/dev/null
+  done
+  kubectl -n "$NS" create secret generic "$SECRET" --from-file=ca.crt="$d/ca.crt" \
+      --from-file=worker.crt="$d/worker.crt" --from-file=worker.key="$d/worker.key" \
+      --from-file=master.crt="$d/master.crt" --from-file=master.key="$d/master.key"
+}
+apply()  { pki; for f in "${FILES[@]}"; do kubectl apply -f "$f"; done; }
+remove() {
+  for ((i=${#FILES[@]}-1; i>=0; i--)); do kubectl delete --ignore-not-found -f "${FILES[$i]}"; done
+  kubectl -n "$NS" delete secret --ignore-not-found "$SECRET"
+}
 case "${1:-}" in
   deploy) apply ;;
   redeploy) remove; apply ;;

@@ -149,6 +149,7 @@ class ProcessCluster:
                    "GM_CGROUP_MODE": self.cgroup_mode, "GM_DEVNODE_MODE": "emulate",
                    "GM_CONTAINER_ROOT_PREFIX": n["rootfs_root"], "GM_AMDSMI_LIB": self.amdsmi_lib,
                    "GM_STATE_DIR": n["state_dir"], "GM_HOST_DEV_PATH": n["host_dev"],
+                   "GM_WORKER_INSECURE": "1",
                    "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": str(gport),
                    "GM_METRICS_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
                    "GM_LOG_JSON": "false", **self.worker_env}
@@ -158,7 +159,7 @@ class ProcessCluster:
             self._await_worker(node)
         mport = free_port()
         self._spawn("master", [*self.entry, "master"],
-                    {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1",
+                    {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1", "GM_AUTHZ_MODE": "none",
                      "GM_MASTER_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
                      "GM_LOG_JSON": "false", **self.master_env})
         self.master_url = f"http://127.0.0.1:{mport}"

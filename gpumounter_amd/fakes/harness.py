@@ -103,7 +103,8 @@ class LocalCluster:
         if self.start_master:
             mcfg = Config.load(env={}, kube_api=self.api_url, master_host="127.0.0.1",
                                log_json=False,
-                               **{"gc_tune": False, **self.master_overrides})
+                               **{"gc_tune": False, "authz_mode": "none",
+                                  **self.master_overrides})
             self.master = Master(mcfg)
             await self.master.start(port=0)
             self.master_url = f"http://127.0.0.1:{self.master.port}"
@@ -139,6 +140,7 @@ class LocalCluster:
         h = self.nodes[name]
         ov = dict(self.worker_overrides)
         ov.setdefault("gc_tune", False)   # many clusters per test process: freezing would leak
+        ov.setdefault("worker_insecure", not ov.get("tls_ca"))   # hermetic: loopback only
         ov.setdefault("state_dir", h.node.state_dir)
         ov.setdefault("host_dev_path", h.node.host_dev)
         if self.device_plugin:

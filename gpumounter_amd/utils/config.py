@@ -134,13 +134,21 @@ class Config:
     reconcile_period_s: float = 30.0
     watch_resync_s: float = 300.0
     api_token: str = ""                # if set, add/remove require "Authorization: Bearer <token>"
-    authz_mode: str = "none"           # none (| api_token) | kube: TokenReview + SAR on pods/gpumount
+    # kube: the caller's own token, TokenReview + SubjectAccessReview on pods/gpumount (default);
+    # none: open like the reference (SURVEY defect 13) unless api_token is set — opt-in only
+    authz_mode: str = "kube"
     # master⇄worker gRPC TLS (reference: insecure, main.go:82). cert+key on the worker enable TLS;
     # a CA on the worker requires client certs (mTLS). The master uses the same three files.
     tls_cert: str = ""
     tls_key: str = ""
     tls_ca: str = ""
     tls_server_name: str = "gpu-mounter-worker"  # SAN the worker certificate carries
+    # identities (certificate SAN DNS names or CN) the worker accepts RPCs from under mTLS;
+    # "" = any certificate the CA signed
+    tls_client_names: str = "gpu-mounter-master"
+    # the worker refuses to serve its gRPC API (which can kill tenant processes) without mTLS
+    # unless this is set explicitly (hermetic tests, lab clusters)
+    worker_insecure: bool = False
     metrics_period_s: float = 15.0
     # --- observability ---------------------------------------------------------------------
     log_level: str = "INFO"

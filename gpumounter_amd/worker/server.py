@@ -108,8 +108,23 @@ class Worker:
         self.ready = False
 
     # ------------------------------------------------------------------------ gRPC glue
+    def _peer_allowed(self, context) -> bool:
+        """Under mTLS, only the configured client identities (the master's certificate) may call:
+        a certificate from the same CA for another component is not enough."""
+        names = {n.strip() for n in self.cfg.tls_client_names.split(",") if n.strip()}
+        if not self.cfg.tls_ca or not names:
+            return True
+        auth = context.auth_context() or {}
+        got = {v.decode() if isinstance(v, bytes) else str(v)
+               for k in ("x509_subject_alternative_name", "x509_common_name")
+               for v in auth.get(k, [])}
+        return bool(got & names)
+
     def _wrap(self, fn):
         async def handler(request, context):
+            if not self._peer_allowed(context):
+                await context.abort(grpc.StatusCode.PERMISSION_DENIED,
+                                    "client certificate is not an allowed gpumounter identity")
             try:
                 return await fn(request)
             except RpcError as e:
@@ -147,6 +162,15 @@ class Worker:
         await self.node_informer.start()
         # warm the ledger channel (fails fast if the kubelet socket is wrong)
         await self.ledger.list()
+        if not (self.cfg.tls_cert and self.cfg.tls_key and self.cfg.tls_ca) and \
+                not self.cfg.worker_insecure:
+            raise ValueError("worker refuses to serve gRPC without mTLS: set GM_TLS_CERT, "
+                             "GM_TLS_KEY and GM_TLS_CA (deploy.sh creates them), or "
+                             "GM_WORKER_INSECURE=1 to opt out explicitly")
+        if self.cfg.worker_insecure and not self.cfg.tls_ca:
+            _log.warning("worker gRPC is UNAUTHENTICATED (worker_insecure=1): anyone who can "
+                         "reach :%d can attach GPUs or kill tenant GPU processes",
+                         self.cfg.worker_port)
         self.grpc_server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])
         self.grpc_server.add_generic_rpc_handlers(self.handlers())
         port = self.cfg.worker_port if grpc_port is None else grpc_port

@@ -34,6 +34,12 @@ def test_worker_daemonset_shape():
     assert env["NODE_NAME"]["valueFrom"]["fieldRef"]["fieldPath"] == "spec.nodeName"
     assert env["GM_BPF_PIN_DIR"]["value"].startswith("/sys/fs/bpf")
     assert "NVIDIA_VISIBLE_DEVICES" not in env
+    # secure by default: mTLS on :1200 with the master as the only accepted identity
+    assert env["GM_TLS_CA"]["value"] and env["GM_TLS_CERT"]["value"] and env["GM_TLS_KEY"]["value"]
+    assert env["GM_TLS_CLIENT_NAMES"]["value"] == "gpu-mounter-master"
+    assert "GM_WORKER_INSECURE" not in env
+    assert env["POD_NAME"]["valueFrom"]["fieldRef"]["fieldPath"] == "metadata.name"
+    assert env["GM_STATE_DIR"]["value"] == "/var/lib/gpumounter"
 
 
 def test_kind_overlay_env_is_valid_config():
@@ -100,3 +106,23 @@ def test_cli_inventory_topology_bpf_dump():
     assert topo["plans"]["4"]["numa_nodes"] == 1 and topo["describe"]["all_pairs_xgmi"]
     dump = _cli("bpf-dump", "--allow", "226:128", "--allow", "511:0")
     assert "if r4 != 226" in dump and "call bpf_tail_call#12" in dump
+
+
+def test_master_and_network_policy_are_secure_by_default():
+    (dep,) = load("gpu-mounter-master.yaml")
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    cfg = Config.load(env={k: v for k, v in env.items() if v is not None})
+    assert cfg.authz_mode == "kube" and cfg.tls_ca and cfg.tls_cert and cfg.tls_key
+    (np,) = load("networkpolicy.yaml")
+    assert np["spec"]["podSelector"]["matchLabels"] == {"app": "gpu-mounter-worker"}
+    rules = np["spec"]["ingress"]
+    grpc_rule = [r for r in rules if any(p["port"] == 1200 for p in r["ports"])]
+    assert len(grpc_rule) == 1
+    assert grpc_rule[0]["from"] == [{"podSelector": {"matchLabels":
+                                                     {"app": "gpu-mounter-master"}}}]
+    with open(os.path.join(ROOT, "deploy", "kustomization.yaml")) as fh:
+        assert "networkpolicy.yaml" in yaml.safe_load(fh)["resources"]
+    with open(os.path.join(ROOT, "deploy.sh")) as fh:
+        text = fh.read()
+    assert "deploy/networkpolicy.yaml" in text and "gpu-mounter-tls" in text

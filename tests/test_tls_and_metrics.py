@@ -18,7 +18,8 @@ def pki(tmp_path_factory):
     d = tmp_path_factory.mktemp("pki")
     _openssl("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out",
              "ca.crt", "-days", "2", "-subj", "/CN=gm-test-ca", cwd=d)
-    for name, cn in (("server", "gpu-mounter-worker"), ("client", "gpu-mounter-master")):
+    for name, cn in (("server", "gpu-mounter-worker"), ("client", "gpu-mounter-master"),
+                     ("intruder", "some-other-pod")):
         (d / f"{name}.ext").write_text(f"subjectAltName=DNS:{cn}\n")
         _openssl("req", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{name}.key", "-out",
                  f"{name}.csr", "-subj", f"/CN={cn}", cwd=d)
@@ -88,4 +89,101 @@ def test_hot_mounted_gpus_gauge_per_namespace():
             assert (await lc.remove("team-b", "b", [d["uuid"] for d in b["devices"]]))[0] == 200
             await w.collect_metrics()
             assert 'gm_hot_mounted_gpus{namespace="team-b"} 0.0' in w.metrics.render().decode()
+    asyncio.run(main())
+
+
+def test_worker_with_a_ca_signed_but_foreign_identity_is_denied(pki):
+    """Same CA, wrong identity (another component's certificate): PERMISSION_DENIED."""
+    w = {"tls_cert": str(pki / "server.crt"), "tls_key": str(pki / "server.key"),
+         "tls_ca": str(pki / "ca.crt")}
+    m = {"tls_cert": str(pki / "client.crt"), "tls_key": str(pki / "client.key"),
+         "tls_ca": str(pki / "ca.crt")}
+
+    async def main():
+        async with LocalCluster(worker_overrides=w, master_overrides=m) as lc:
+            port = lc.nodes["node-0"].worker.grpc_port
+            creds = grpc.ssl_channel_credentials(
+                root_certificates=(pki / "ca.crt").read_bytes(),
+                private_key=(pki / "intruder.key").read_bytes(),
+                certificate_chain=(pki / "intruder.crt").read_bytes())
+            ch = grpc.aio.secure_channel(f"127.0.0.1:{port}", creds, options=[
+                ("grpc.ssl_target_name_override", "gpu-mounter-worker")])
+            from gpumounter_amd.api import gpu_mount as api
+            stub = ch.unary_unary(api.REMOVE_GPU,
+                                  request_serializer=api.RemoveGPURequest.SerializeToString,
+                                  response_deserializer=api.RemoveGPUResponse.FromString)
+            with pytest.raises(grpc.aio.AioRpcError) as ei:
+                await stub(api.RemoveGPURequest(pod_name="x", namespace="default", force=True),
+                           timeout=5)
+            assert ei.value.code() == grpc.StatusCode.PERMISSION_DENIED
+            await ch.close()
+            lc.tenant("t")                      # the master's own identity still works
+            assert (await lc.add("default", "t", 1))[0] == 200
+    asyncio.run(main())
+
+
+def test_secure_defaults():
+    """Out of the box: the master authorizes callers against Kubernetes RBAC and the worker
+    will not serve its gRPC API without mTLS (reference: neither — main.go:82,185)."""
+    from gpumounter_amd.utils.config import Config
+    cfg = Config.load(env={})
+    assert cfg.authz_mode == "kube" and cfg.worker_insecure is False
+
+    async def main():
+        async with LocalCluster(start_workers=False, start_master=False) as lc:
+            from gpumounter_amd.worker.server import Worker
+            h = lc.nodes["node-0"]
+            c = Config.load(env={}, kube_api=lc.api_url, node_name="node-0",
+                            kubelet_socket=h.kubelet.socket_path, amdsmi_lib="mock",
+                            cgroup_root=h.node.cgroup_root, devnode_mode="emulate",
+                            container_root_prefix=h.node.rootfs_root, state_dir=h.node.state_dir,
+                            host_dev_path=h.node.host_dev, worker_host="127.0.0.1")
+            w = Worker(c, inventory=lc.inventory)
+            with pytest.raises(ValueError, match="mTLS"):
+                await w.start(grpc_port=0, http_port=-1, reconcile=False)
+            await w.stop()
+        async with LocalCluster(master_overrides={"authz_mode": "kube"}) as lc:
+            lc.tenant("t")
+            # no bearer token → 401 at the master
+            async with lc.session.get(lc.master_url + "/addgpu/namespace/default/pod/t/gpu/1/"
+                                      "isEntireMount/false") as r:
+                assert r.status == 401
+            assert lc.cluster.placeholders() == []
+    asyncio.run(main())
+
+
+def test_deploy_sh_pki_works_end_to_end(tmp_path):
+    """The certificates deploy.sh creates (stub kubectl captures the Secret) carry the identities
+    the worker and master check: the master's certificate is accepted by the worker."""
+    import os
+    import stat
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "secret"
+    out.mkdir()
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    kubectl = bindir / "kubectl"
+    kubectl.write_text(f"""#!/bin/bash
+if [[ "$*" == *"get secret"* ]]; then exit 1; fi
+for a in "$@"; do
+  case "$a" in --from-file=*) kv="${{a#--from-file=}}"; cp "${{kv#*=}}" "{out}/${{kv%%=*}}";; esac
+done
+""")
+    kubectl.chmod(kubectl.stat().st_mode | stat.S_IEXEC)
+    script = (f'set -euo pipefail; source <(sed -n "/^pki()/,/^}}/p" {root}/deploy.sh); '
+              f'NS=kube-system; SECRET=gpu-mounter-tls; pki')
+    subprocess.run(["bash", "-c", script], check=True, timeout=120,
+                   env={**os.environ, "PATH": f"{bindir}:{os.environ['PATH']}"})
+    assert sorted(p.name for p in out.iterdir()) == ["ca.crt", "master.crt", "master.key",
+                                                      "worker.crt", "worker.key"]
+    w = {"tls_cert": str(out / "worker.crt"), "tls_key": str(out / "worker.key"),
+         "tls_ca": str(out / "ca.crt")}
+    m = {"tls_cert": str(out / "master.crt"), "tls_key": str(out / "master.key"),
+         "tls_ca": str(out / "ca.crt")}
+
+    async def main():
+        async with LocalCluster(worker_overrides=w, master_overrides=m) as lc:
+            lc.tenant("t")
+            code, b = await lc.add("default", "t", 1)
+            assert code == 200, b
     asyncio.run(main())
