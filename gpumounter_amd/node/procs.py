@@ -5,16 +5,21 @@ Reference: busy ⇔ some NVML graphics/compute PID of the GPU is in the containe
 (pkg/device/nvidia.go:58-87), and force-removal runs ``kill <pids>`` through nsenter
 (namespace.go:191-201). Here the PID set comes from the cached amdsmi session
 (``amdsmi_get_gpu_process_list``), with a ``/proc/*/fd`` scan for the GPU's render node as
-fallback when amdsmi cannot report processes; signals go through ``pidfd_send_signal`` so a
-recycled PID is never hit, and SIGTERM escalates to SIGKILL after a grace period.
+fallback when amdsmi cannot report processes. Force-removal pins the container's processes
+with pidfds *before* the busy check (:class:`Pinned`): membership in the container's cgroup is
+re-read after pinning, and SIGTERM, the liveness wait and the SIGKILL escalation all go through
+those pidfds — so a PID the kernel recycles between the snapshot and the kill can never be hit.
 """
 from __future__ import annotations
 
 import asyncio
 import ctypes as C
+import errno
 import os
+import select
 import signal
-from typing import Dict, Iterable, List, Sequence, Tuple
+import signal as _sig   # Pinned.signal shadows the module name inside the class body
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from gpumounter_amd import _native
 from gpumounter_amd.hw.inventory import Inventory
@@ -121,3 +126,88 @@ async def terminate(pids: Sequence[int], sig: int = signal.SIGTERM, grace_s: flo
         _log.warning("SIGKILL after %.1fs grace: %s", grace_s, left)
         signal_pids(left, signal.SIGKILL)
     return list(pids)
+
+
+class Pinned:
+    """pidfds for a snapshot of PIDs, held from the busy check through the kill.
+
+    A pidfd refers to one process, not to a number: once that process has exited, signalling
+    through it fails with ESRCH even if the PID was handed to someone else. So the only window
+    left is between reading ``cgroup.procs`` and ``pidfd_open``; :meth:`restrict` closes it by
+    re-reading the cgroup *after* pinning (a pinned, unreaped process keeps its PID, so a PID
+    still listed is the pinned process)."""
+
+    def __init__(self, pids: Iterable[int]) -> None:
+        self.fds: Dict[int, int] = {}
+        for p in sorted(set(pids)):
+            try:
+                self.fds[p] = os.pidfd_open(p)
+            except ProcessLookupError:
+                continue            # already gone: nothing to pin, nothing to kill
+            except OSError as e:
+                if e.errno != errno.ESRCH:
+                    raise
+
+    def pids(self) -> List[int]:
+        return sorted(self.fds)
+
+    def restrict(self, still: Iterable[int]) -> List[int]:
+        """Keep only PIDs still listed (re-read after pinning); returns those dropped."""
+        keep = set(still)
+        dropped = [p for p in self.fds if p not in keep]
+        for p in dropped:
+            os.close(self.fds.pop(p))
+        return dropped
+
+    def exited(self, pid: int) -> bool:
+        fd = self.fds.get(pid)
+        if fd is None:
+            return True
+        r, _, _ = select.select([fd], [], [], 0)   # a pidfd polls readable once it exits
+        return bool(r)
+
+    def signal(self, pids: Sequence[int], sig: int) -> List[int]:
+        """0 or -errno per PID; never reaches a process other than the pinned one."""
+        out = []
+        for p in pids:
+            fd = self.fds.get(p)
+            if fd is None:
+                out.append(-errno.ESRCH)
+                continue
+            try:
+                _sig.pidfd_send_signal(fd, sig)
+                out.append(0)
+            except OSError as e:
+                out.append(-(e.errno or errno.ESRCH))
+        return out
+
+    async def terminate(self, pids: Sequence[int], sig: int = _sig.SIGTERM,
+                        grace_s: float = 5.0, already_signalled: bool = False) -> List[int]:
+        """``sig``, wait up to ``grace_s`` for the pinned processes to exit, SIGKILL survivors,
+        then release the pidfds. Returns the PIDs that needed SIGKILL."""
+        try:
+            live = [p for p in pids if p in self.fds]
+            if not already_signalled:
+                self.signal(live, sig)
+            loop = asyncio.get_running_loop()
+            deadline = loop.time() + grace_s
+            while live and loop.time() < deadline:
+                await asyncio.sleep(0.02)
+                live = [p for p in live if not self.exited(p)]
+            if live:
+                _log.warning("SIGKILL after %.1fs grace: %s", grace_s, live)
+                self.signal(live, _sig.SIGKILL)
+            return live
+        finally:
+            self.close()
+
+    def close(self) -> None:
+        for fd in self.fds.values():
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+        self.fds.clear()
+
+    def __del__(self) -> None:
+        self.close()

@@ -587,19 +587,31 @@ class GpuMountService:
                                              message="Invalid UUIDs")
             sel_idx = {g.index for g in selected}
             keep = [g for g in st.hot if g.index not in sel_idx]
+            pinned: Optional[procs.Pinned] = None
             try:
                 with trace.span("busy_check"):
                     self.faults.check("busy_check")
                     targets = self.hm.resolve(pod, req.container)
                     cpids = sorted({p for t in targets for p in t.pids})
-                    busy = procs.busy_pids(self.inv, selected, cpids, self.cfg.drm_major,
-                                           self.cfg.busy_detection)
+                    # pin the snapshot, then confirm membership: from here on a recycled PID
+                    # cannot be mistaken for a container process (node/procs.py Pinned)
+                    pinned = procs.Pinned(cpids)
+                    if pinned.fds:
+                        pinned.restrict({p for t in targets
+                                         for p in self.hm.resolver.pids(t.cgdir)})
+                    busy = procs.busy_pids(self.inv, selected, pinned.pids(),
+                                           self.cfg.drm_major, self.cfg.busy_detection)
+                    busy = {k: [p for p in v if not pinned.exited(p)] for k, v in busy.items()}
+                    busy = {k: v for k, v in busy.items() if v}
             except (MountError, InjectedFault) as e:
+                if pinned is not None:
+                    pinned.close()
                 if await self._rollback(pod, "detach"):   # the pod went away meanwhile
                     return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_POD_NOT_FOUND,
                                                  message=f"pod went away: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             if busy and not req.force:
+                pinned.close()
                 _log.info("GPU busy in %s/%s: %s", req.namespace, req.pod_name, busy)
                 return api.RemoveGPUResponse(
                     remove_gpu_result=api.REMOVE_BUSY,
@@ -614,11 +626,18 @@ class GpuMountService:
                     self.hm.detach(pod, selected, keep, st.own, req.container, targets)
                 if killed:
                     with trace.span("kill", pids=len(killed)):
-                        procs.signal_pids(killed, self.cfg.kill_signal)
-                        asyncio.ensure_future(procs.terminate(killed, self.cfg.kill_signal,
-                                                              self.cfg.kill_grace_s))
+                        pinned.signal(killed, self.cfg.kill_signal)
+                        # the pidfds move to the escalation task, which closes them
+                        p, pinned = pinned, None
+                        asyncio.ensure_future(p.terminate(killed, self.cfg.kill_signal,
+                                                          self.cfg.kill_grace_s,
+                                                          already_signalled=True))
+                else:
+                    pinned.close()
                 await self._release(phs)
             except (MountError, ReserveError, InjectedFault, OSError) as e:
+                if pinned is not None:
+                    pinned.close()
                 _log.error("detach failed on %s/%s: %s", req.namespace, req.pod_name, e)
                 if await self._rollback(pod, "detach"):
                     return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_POD_NOT_FOUND,

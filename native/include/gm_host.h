@@ -9,7 +9,8 @@
 //     tail-calling into it from ours, so its rules never need to be reverse-engineered
 //   * device nodes: mknodat/unlinkat through /proc/<pid>/root of the target container (or a
 //     setns(CLONE_NEWNS) helper thread) — no mknod binary in the tenant image (reference FAQ.md:3-4)
-//   * processes: pidfd_send_signal (no PID-reuse race), /proc/*/fd scan for device users
+//   * processes: pidfd_send_signal by PID (the worker pins PIDs with long-lived pidfds itself:
+//     gpumounter_amd/node/procs.py Pinned), /proc/*/fd scan for device users
 //   * roctx range markers around attach/detach for rocprofv3 --marker-trace timelines
 // All functions return 0 / a count on success and -errno on failure unless stated otherwise.
 #pragma once

@@ -1,7 +1,10 @@
 """Deployment-shaped run: fake control plane, workers and master as separate processes, started
 through the production entry points (``python -m gpumounter_amd worker|master``) and configured
 only by ``GM_*`` environment variables (gpumounter_amd/fakes/deployment.py)."""
+import asyncio
 import os
+
+import pytest
 
 from gpumounter_amd.fakes.deployment import ProcessCluster
 
@@ -108,3 +111,77 @@ def test_worker_killed_mid_attach_converges_after_restart():
         assert pc.audit("default", "t0") == []
     finally:
         pc.stop()
+
+
+# ------------------------------------------------------------------------------ PID reuse
+def test_pinned_pidfd_never_signals_after_exit():
+    """A pinned PID whose process exited and was reaped: signalling reports ESRCH instead of
+    reaching whatever process gets that number next (VERDICT r1 Weak #7)."""
+    import errno
+    import signal
+    import subprocess
+
+    from gpumounter_amd.node import procs
+    p = subprocess.Popen(["sleep", "60"])
+    pin = procs.Pinned([p.pid])
+    assert pin.pids() == [p.pid] and not pin.exited(p.pid)
+    p.kill()
+    p.wait()                                  # reaped: the number is free for reuse
+    assert pin.exited(p.pid)
+    assert pin.signal([p.pid], signal.SIGTERM) == [-errno.ESRCH]
+    pin.close()
+
+
+def test_pinned_restrict_drops_pids_that_left_the_cgroup():
+    import subprocess
+
+    from gpumounter_amd.node import procs
+    a = subprocess.Popen(["sleep", "60"])
+    b = subprocess.Popen(["sleep", "60"])
+    try:
+        pin = procs.Pinned([a.pid, b.pid, 2 ** 22 + 7])    # the last one does not exist
+        assert pin.pids() == sorted([a.pid, b.pid])
+        assert pin.restrict([a.pid]) == [b.pid]            # b left the container meanwhile
+        assert pin.signal([b.pid], 0) == [-3]              # ESRCH: never pinned any more
+        killed = asyncio.run(pin.terminate([a.pid], grace_s=2.0))
+        assert killed == [] and a.wait(timeout=5) != 0
+        assert b.poll() is None                            # untouched
+        assert pin.fds == {}
+    finally:
+        for p in (a, b):
+            p.kill()
+            p.wait()
+
+
+def test_recycled_pid_is_not_signalled(tmp_path):
+    """Real PID reuse: in a fresh PID namespace, pin process A, let it exit, force the next PID
+    to A's number (ns_last_pid) so process B gets it, then deliver the kill: B survives."""
+    import json
+    import subprocess
+    import sys
+
+    if os.geteuid() != 0 or os.environ.get("GM_PRIVILEGED_TESTS") != "1":
+        pytest.skip("needs root (a PID namespace + ns_last_pid); GM_PRIVILEGED_TESTS=1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "reuse.py"
+    script.write_text(f"""
+import json, os, signal, subprocess, sys
+sys.path.insert(0, {root!r})
+from gpumounter_amd.node import procs
+a = subprocess.Popen(["sleep", "60"])
+pin = procs.Pinned([a.pid])
+a.kill(); a.wait()
+with open("/proc/sys/kernel/ns_last_pid", "w") as fh:
+    fh.write(str(a.pid - 1))
+b = subprocess.Popen(["sleep", "60"])
+res = pin.signal([a.pid], signal.SIGKILL)
+alive = b.poll() is None
+b.kill(); b.wait()
+print(json.dumps({{"a": a.pid, "b": b.pid, "res": res, "b_alive": alive}}))
+""")
+    r = subprocess.run(["unshare", "--pid", "--fork", "--mount-proc", sys.executable, str(script)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    o = json.loads(r.stdout.strip().splitlines()[-1])
+    assert o["a"] == o["b"], o                 # the number really was recycled
+    assert o["res"] == [-3] and o["b_alive"]   # ESRCH, and B untouched
