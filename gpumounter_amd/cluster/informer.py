@@ -8,6 +8,7 @@ and are woken by the next matching event instead of polling the apiserver.
 from __future__ import annotations
 
 import asyncio
+from collections import deque
 from typing import Callable, Dict, List, Optional, Tuple
 
 from gpumounter_amd.cluster.kube import ApiError, KubeClient
@@ -34,6 +35,9 @@ class PodInformer:
         self._synced: Optional[asyncio.Event] = None
         self.rv = ""
         self.events = 0
+        self.relists = 0
+        self.resumes = 0
+        self._seen: Dict[Key, deque] = {}    # resourceVersions the watch/list delivered per key
         self.handlers: List[Callable[[str, dict], None]] = []
 
     async def start(self) -> None:
@@ -55,6 +59,9 @@ class PodInformer:
         items, rv = await self.kube.list_pods(self.namespace, self.label_selector,
                                               self.field_selector)
         fresh = {(p["metadata"]["namespace"], p["metadata"]["name"]): p for p in items}
+        self._seen = {k: self._seen[k] for k in fresh if k in self._seen}
+        for k, p in fresh.items():
+            self._note(k, p["metadata"].get("resourceVersion", ""))
         for k in set(self.cache) - set(fresh):
             self.deleted[k] = self.cache[k]["metadata"].get("uid", "")
         self.cache = fresh
@@ -70,12 +77,21 @@ class PodInformer:
         async with self._cond:
             self._cond.notify_all()
 
-    async def _run(self) -> None:
+    async def _run(self, initial_list: bool = True) -> None:
+        """LIST once, then WATCH from the list's resourceVersion. A watch that ends cleanly (the
+        server's timeoutSeconds) is resumed from the last resourceVersion seen — events, and
+        the BOOKMARKs the server sends while idle, keep it current — so there is no relist per
+        resync period. Only an error relists: 410 Gone (the version left the server's history)
+        at once, anything else after a backoff."""
         backoff = 0.05
+        need_list = initial_list
         while True:
             try:
-                await self._relist()
-                self._synced.set()
+                if need_list:
+                    await self._relist()
+                    self._synced.set()
+                    need_list = False
+                    self.relists += 1
                 async for etype, pod in self.kube.watch_pods(
                         self.namespace, self.label_selector, self.field_selector, self.rv,
                         timeout_s=int(self.resync_s)):
@@ -89,36 +105,54 @@ class PodInformer:
                         continue
                     key = (md.get("namespace", ""), md.get("name", ""))
                     self.events += 1
+                    if etype != "DELETED":
+                        self._note(key, md.get("resourceVersion", ""))
                     if etype == "DELETED":
                         self.cache.pop(key, None)
+                        self._seen.pop(key, None)   # stale upserts: caught by `deleted`
                         self.deleted[key] = md.get("uid", "")
                     else:
                         self.cache[key] = pod
                         self.deleted.pop(key, None)
                     await self._notify(etype, pod)
-                # stream ended (server timeout): resume from rv without relisting
-                continue
+                self.resumes += 1            # clean end of stream: watch again from self.rv
             except asyncio.CancelledError:
                 raise
+            except ApiError as e:
+                need_list = True
+                if e.status == 410:          # expired version: relist now, no backoff
+                    _log.info("watch %s/%s: resourceVersion expired; relisting",
+                              self.namespace, self.label_selector)
+                    continue
+                _log.warning("watch %s/%s failed: %s; relisting in %.2fs", self.namespace,
+                             self.label_selector, e, backoff)
+                await asyncio.sleep(backoff)
+                backoff = min(backoff * 2, 5.0)
             except Exception as e:  # noqa: BLE001
+                need_list = True
                 _log.warning("watch %s/%s failed: %s; relisting in %.2fs", self.namespace,
                              self.label_selector, e, backoff)
                 await asyncio.sleep(backoff)
                 backoff = min(backoff * 2, 5.0)
 
+    def _note(self, key: Key, rv: str) -> None:
+        if rv:
+            seen = self._seen.get(key)
+            if seen is None:
+                seen = self._seen[key] = deque(maxlen=16)
+            seen.append(rv)
+
     def upsert(self, pod: dict) -> None:
         """Write-through from our own API responses (create/patch) so readers do not wait for
-        the watch echo; an older resourceVersion never overwrites a newer cached one."""
+        the watch echo. resourceVersions are opaque (only equality is meaningful), so ordering
+        comes from the watch itself: one object's events arrive in order, so if the watch has
+        already delivered this response's version, the cache is at least as new and is kept;
+        if not, the watch has not reached our write yet and the response is newer."""
         md = pod.get("metadata", {})
         key = (md.get("namespace", ""), md.get("name", ""))
-        cur = self.cache.get(key)
-        if cur is not None:
-            try:
-                if int(cur["metadata"].get("resourceVersion", 0)) > \
-                        int(md.get("resourceVersion", 0)):
-                    return
-            except (TypeError, ValueError):
-                pass
+        rv = md.get("resourceVersion", "")
+        if rv and rv in self._seen.get(key, ()):
+            return
         if key in self.deleted and self.deleted[key] == md.get("uid"):
             return
         self.cache[key] = pod
