@@ -60,6 +60,9 @@ class _LocalCP:
     def placeholders_left(self) -> int:
         return len(self.lc.cluster.placeholders())
 
+    def kubelet_calls(self) -> dict:
+        return dict(self.lc.nodes["node-0"].kubelet.calls)
+
     def wait_pool(self, want: int) -> None:
         pool = self.lc.nodes["node-0"].worker.pool
         t_wait = time.time()
@@ -89,6 +92,9 @@ class _ProcCP:
 
     def placeholders_left(self) -> int:
         return len(self.pc.placeholders())
+
+    def kubelet_calls(self) -> dict:
+        return self.pc.kubelet_calls()
 
     def wait_pool(self, want: int) -> None:
         from gpumounter_amd.models.types import ANN_MOUNT_MODE, MODE_STANDBY
@@ -373,23 +379,32 @@ def main() -> int:
                        "max_gbps": round(max(x["gbps"] for x in pairs), 1)}
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
             placeholders_left = cp.placeholders_left()
+            kcalls = cp.kubelet_calls()
             p50 = pct(attach_ms, 0.5)
             ref = None
             if args.ref_steps > 0 and args.protocol == "gpumounter" and \
                     args.latency == "zero" and not args.warm_pool:
                 # the reference's call sequence, emulated in the same deployment shape
+                # The reference dials the kubelet and Lists on every query with no retry
+                # (collector.go:90-138): against the kubelet's PodResources limiter (100 qps,
+                # burst 10) it fails requests. Its cycles are therefore timed on a kubelet that
+                # serves every call and only counts those a limited kubelet would reject.
                 if lc is not None:
                     from gpumounter_amd.fakes import refproto
                     refproto.install(lc)
+                    for h in lc.nodes.values():
+                        h.kubelet.limit_mode = "count"
                     ref_cp = cp
                 else:
                     cp.stop()
                     from gpumounter_amd.fakes.deployment import ProcessCluster
                     rpc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup,
-                                         gpu_bdfs=node_bdfs, protocol="reference").start()
+                                         gpu_bdfs=node_bdfs, protocol="reference",
+                                         kubelet_limit="count").start()
                     rpc.tenant("tenant", pids={"main": [sleeper.pid]})
                     cp = ref_cp = _ProcCP(rpc)
                 ra, rd = [], []
+                k0 = ref_cp.kubelet_calls()
                 for i in range(args.ref_steps + 2):
                     ta = time.perf_counter()
                     code, body = ref_cp.add(n, args.mode == "entire")
@@ -405,7 +420,12 @@ def main() -> int:
                     progress("reference", i + 1, args.ref_steps + 2)
                 ref = {"steps": args.ref_steps, "attach_p50_ms": round(pct(ra, 0.5), 4),
                        "detach_p50_ms": round(pct(rd, 0.5), 4),
-                       "attach_speedup": round(pct(ra, 0.5) / p50, 2)}
+                       "attach_speedup": round(pct(ra, 0.5) / p50, 2),
+                       "kubelet_limit": "count (served, not enforced)"}
+                k1 = ref_cp.kubelet_calls()
+                served = sum(k1[c] - k0[c] for c in ("List", "Get", "GetAllocatableResources"))
+                ref["kubelet_calls_per_cycle"] = round(served / (args.ref_steps + 2), 2)
+                ref["kubelet_calls_over_limit"] = k1["over_limit"] - k0["over_limit"]
             out = {
                 "metric": "p50_gpu_attach_latency_ms",
                 "value": round(p50, 4),
@@ -452,6 +472,10 @@ def main() -> int:
                 "non_xgmi_pairs": att_nx, "p2p": p2p,
                 "ledger_audit_issues": audit_issues,
                 "final_orphans": orphan_issues,
+                # PodResources traffic of this run against the limited kubelet (100 qps,
+                # burst 10): rejected calls were retried by the ledger client
+                "kubelet_calls": {k: kcalls.get(k, 0) for k in
+                                  ("List", "Get", "GetAllocatableResources", "rejected")},
                 "placeholders_left": placeholders_left,
                 "reference_emulated_same_run": ref,
                 "inventory": info,

@@ -166,6 +166,8 @@ def host() -> C.CDLL:
         lib.gm_devnode_stat.argtypes = [C.c_int, C.c_char_p, C.c_char_p, C.c_int,
                                         C.POINTER(C.c_int), C.POINTER(C.c_uint32),
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        lib.gm_devnodes_present.argtypes = [C.c_int, C.c_char_p, C.POINTER(DevNode), C.c_int,
+                                            C.c_int, C.POINTER(C.c_uint8)]
         lib.gm_proc_signal.argtypes = [C.POINTER(C.c_int32), C.c_int, C.c_int, C.POINTER(C.c_int)]
         lib.gm_proc_dev_users.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_int32), C.c_int,
                                           C.POINTER(C.c_int)]

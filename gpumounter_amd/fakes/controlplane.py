@@ -10,6 +10,7 @@ the DaemonSet/Deployment (see :mod:`gpumounter_amd.fakes.deployment`).
 Besides the Kubernetes API it serves two test hooks:
   ``POST /_fake/tenant``  {"name", "ns", "node", "gpus", "containers", "pids"} → a Running pod
   ``POST /_fake/worker``  {"node", "port"}  → the worker DaemonSet pod the master discovers
+  ``GET  /_fake/kubelet``  → each node's PodResources call counters (served, rejected, over_limit)
 The info file lists the apiserver URL and each node's kubelet socket, cgroup root and rootfs root.
 """
 from __future__ import annotations
@@ -42,8 +43,13 @@ def _hooks(lc_ref: list):
             lc_ref[0].register_worker(b["node"], int(b["port"]), b.get("ip", "127.0.0.1"))
             return web.json_response({"ok": True}, status=201)
 
+        async def kubelet(req: web.Request) -> web.Response:
+            return web.json_response({n: dict(h.kubelet.calls)
+                                      for n, h in lc_ref[0].nodes.items()})
+
         app.router.add_post("/_fake/tenant", tenant)
         app.router.add_post("/_fake/worker", worker)
+        app.router.add_get("/_fake/kubelet", kubelet)
     return install
 
 
@@ -53,7 +59,7 @@ async def run(args) -> None:
                       latency=LatencyModel.realistic() if args.latency == "realistic" else None,
                       workdir=args.workdir, start_master=False, start_workers=False,
                       node_gpu_bdfs=[b for b in args.gpu_bdfs.split(",") if b] or None,
-                      app_hook=_hooks(ref))
+                      kubelet_limit_mode=args.kubelet_limit, app_hook=_hooks(ref))
     ref[0] = lc
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
@@ -84,6 +90,9 @@ def main(argv=None) -> int:
     ap.add_argument("--amdsmi", default="mock")
     ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
     ap.add_argument("--latency", choices=("zero", "realistic"), default="zero")
+    ap.add_argument("--kubelet-limit", choices=("enforce", "count"), default="enforce",
+                    help="PodResources limiter (100 qps, burst 10): reject over-budget calls "
+                         "with RESOURCE_EXHAUSTED, or serve them and only count them")
     ap.add_argument("--gpu-bdfs", default="", help="comma-separated: the node's GPUs (default all)")
     args = ap.parse_args(argv)
     log.setup("WARNING", json_format=False)

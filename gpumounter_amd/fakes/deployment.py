@@ -56,15 +56,18 @@ class ProcessCluster:
                  latency: str = "zero", gpu_bdfs: Optional[List[str]] = None,
                  worker_env: Optional[Dict[str, str]] = None,
                  master_env: Optional[Dict[str, str]] = None, log_dir: str = "",
-                 protocol: str = "gpumounter") -> None:
+                 protocol: str = "gpumounter", kubelet_limit: str = "enforce") -> None:
         """``protocol="reference"`` runs worker and master with the reference's call sequence
-        (gpumounter_amd/fakes/refproto.py) in the same deployment shape, for comparison."""
+        (gpumounter_amd/fakes/refproto.py) in the same deployment shape, for comparison.
+        ``kubelet_limit="count"`` serves PodResources calls over the kubelet's rate budget and
+        only counts them (see :class:`FakeKubelet`)."""
         self.n_nodes = n_nodes
         self.entry = ["-m", "gpumounter_amd"] if protocol == "gpumounter" else \
             ["-m", "gpumounter_amd.fakes.refproto"]
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
         self.latency = latency
+        self.kubelet_limit = kubelet_limit
         self.gpu_bdfs = gpu_bdfs or []
         self.worker_env = worker_env or {}
         self.master_env = master_env or {}
@@ -136,6 +139,7 @@ class ProcessCluster:
                                      os.path.join(self.workdir, "cluster"), "--info", info_path,
                                      "--nodes", str(self.n_nodes), "--amdsmi", self.amdsmi_lib,
                                      "--cgroup", self.cgroup_mode, "--latency", self.latency,
+                                     "--kubelet-limit", self.kubelet_limit,
                                      "--gpu-bdfs", ",".join(self.gpu_bdfs)], {})
         self._wait("control plane", lambda: os.path.exists(info_path))
         with open(info_path) as fh:
@@ -251,6 +255,12 @@ class ProcessCluster:
         code, body = _http("GET", f"{self.master_url}/api/v1/namespaces/{ns}/pods/{pod}/gpus",
                            headers={"Accept": "application/json"})
         return code, json.loads(body)
+
+    def kubelet_calls(self, node: str = "node-0") -> Dict[str, int]:
+        code, body = _http("GET", f"{self.info['api_url']}/_fake/kubelet")
+        if code != 200:
+            raise RuntimeError(f"kubelet counters: {code}")
+        return json.loads(body)[node]
 
     def placeholders(self) -> List[dict]:
         code, body = _http("GET", f"{self.info['api_url']}/api/v1/pods?labelSelector=app%3Dgpu-pool")

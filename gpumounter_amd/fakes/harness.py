@@ -53,6 +53,7 @@ class LocalCluster:
                  device_plugin: bool = False, cgroup_root: str = "",
                  kfd_major: int = 0, start_workers: bool = True,
                  kubelet_rate_limit: Optional[tuple] = (100.0, 10),
+                 kubelet_limit_mode: str = "enforce",
                  app_hook: Optional[Callable[[web.Application], None]] = None) -> None:
         self.n_nodes = n_nodes
         self.amdsmi_lib = amdsmi_lib
@@ -76,6 +77,7 @@ class LocalCluster:
         self.real_cgroup_root = cgroup_root   # privileged tests: a real cgroup2 mount
         self.kfd_major = kfd_major
         self.kubelet_rate_limit = kubelet_rate_limit
+        self.kubelet_limit_mode = kubelet_limit_mode
         self.node_gpu_bdfs = [b.lower() for b in node_gpu_bdfs] if node_gpu_bdfs else None
         self.nodes: Dict[str, NodeHandle] = {}
         self.master: Optional[Master] = None
@@ -128,7 +130,8 @@ class LocalCluster:
         self.cluster.add_node(node)
         sock = os.path.join(ndir, "pod-resources", "kubelet.sock")
         kubelet = FakeKubelet(node, sock, plugin_dir=os.path.join(ndir, "device-plugins")
-                              if self.device_plugin else "", rate_limit=self.kubelet_rate_limit)
+                              if self.device_plugin else "", rate_limit=self.kubelet_rate_limit,
+                              limit_mode=self.kubelet_limit_mode)
         await kubelet.start()
         h = NodeHandle(name, node, kubelet)
         self.nodes[name] = h

@@ -26,11 +26,18 @@ from gpumounter_amd.utils.ratelimit import TokenBucket
 class FakeKubelet:
     def __init__(self, node: FakeNode, socket_path: str, serve_v1: bool = True,
                  serve_v1alpha1: bool = True, plugin_dir: str = "",
-                 rate_limit: Optional[Tuple[float, int]] = (100.0, 10)) -> None:
+                 rate_limit: Optional[Tuple[float, int]] = (100.0, 10),
+                 limit_mode: str = "enforce") -> None:
         self.node = node
         # the kubelet's PodResources limiter (pkg/kubelet/apis/podresources: DefaultQPS 100,
-        # DefaultBurstTokens 10): over budget → RESOURCE_EXHAUSTED "rejected by rate limit"
+        # DefaultBurstTokens 10): over budget → RESOURCE_EXHAUSTED "rejected by rate limit".
+        # limit_mode "count" serves every call but counts the ones a limited kubelet would
+        # reject (calls["over_limit"]): how the emulated reference, which has no retry, is
+        # measured without failing (it would fail against a limited kubelet).
+        if limit_mode not in ("enforce", "count"):
+            raise ValueError(f"limit_mode {limit_mode!r}")
         self.limiter = TokenBucket(*rate_limit) if rate_limit else None
+        self.limit_mode = limit_mode
         self.socket_path = socket_path
         self.serve_v1 = serve_v1
         self.serve_v1alpha1 = serve_v1alpha1
@@ -38,7 +45,7 @@ class FakeKubelet:
         self.server = None
         self.reg_server = None
         self.calls = {"List": 0, "GetAllocatableResources": 0, "Get": 0, "Register": 0,
-                      "rejected": 0}
+                      "rejected": 0, "over_limit": 0}
         # device manager state
         self.plugin_endpoint = ""
         self.plugin_options = None
@@ -131,6 +138,9 @@ class FakeKubelet:
 
     async def _police(self, context) -> None:
         if self.limiter is not None and not self.limiter.allow():
+            self.calls["over_limit"] += 1
+            if self.limit_mode == "count":
+                return
             self.calls["rejected"] += 1
             await context.abort(grpc.StatusCode.RESOURCE_EXHAUSTED, "rejected by rate limit")
 

@@ -277,10 +277,27 @@ class V2BpfBackend(DeviceRuleBackend):
         self.pin_dir = pin_dir
         if pin_dir:
             os.makedirs(pin_dir, exist_ok=True)
+        # cgroup → (attached program ids, pairs those programs grant), recorded when this
+        # process installed them. Program ids are kernel-unique while a program is loaded and
+        # a loaded program's instructions are immutable, so while the cgroup's attached id list
+        # is exactly this tuple the kernel enforces what we built — :meth:`allowed` then skips
+        # reading back and interpreting the xlated code (the attach verify step). Any other id
+        # list (systemd or the runtime swapped a program, a foreign one joined) takes the full
+        # read-back path.
+        self._installed: Dict[str, Tuple[Tuple[int, ...], FrozenSet[Tuple[int, int]]]] = {}
+
+    @staticmethod
+    def attached_ids(cgdir: str) -> Tuple[int, ...]:
+        ids, n, flags = (C.c_uint32 * 16)(), C.c_uint32(0), C.c_uint32(0)
+        rc = _native.host().gm_bpf_dev_query(cgdir.encode(), ids, 16, C.byref(n), C.byref(flags))
+        if rc < 0:
+            raise CgroupError(f"bpf query on {cgdir}: {os.strerror(-rc)}")
+        return tuple(int(ids[i]) for i in range(min(n.value, 16)))
 
     def apply(self, cgdir, grant, revoke, desired):
         lib = _native.host()
         pin = self.pin_dir.encode() if self.pin_dir else None
+        self._installed.pop(cgdir, None)
         if not desired:
             rc = lib.gm_bpf_dev_restore(cgdir.encode(), pin)
             if rc < 0:
@@ -294,6 +311,10 @@ class V2BpfBackend(DeviceRuleBackend):
                                     C.byref(chained))
         if rc < 0:
             raise CgroupError(f"bpf install on {cgdir}: {os.strerror(-rc)}")
+        if rc == 1 and pid.value:
+            # one slot: our program replaced the runtime's (which it tail-calls) in place
+            self._installed[cgdir] = ((pid.value,),
+                                      frozenset((n.major, n.minor) for n in desired))
         if trace.current() is not None:
             tm = _native.BpfTiming()
             lib.gm_bpf_dev_last_timing(C.byref(tm))
@@ -312,7 +333,18 @@ class V2BpfBackend(DeviceRuleBackend):
         re-installs it. A foreign program attached next to ours (systemd re-realising its unit)
         can veto any access under BPF_F_ALLOW_MULTI, so its own verdict is evaluated too: with
         the unit's DeviceAllow= kept in step (node/systemd.py) it grants our nodes; otherwise the
-        pair reads as missing and the re-install wraps that program."""
+        pair reads as missing and the re-install wraps that program.
+
+        Fast path: when the attached id list is exactly the one this backend installed, the
+        answer is the rule set it compiled into that program (see ``_installed``)."""
+        known = self._installed.get(cgdir)
+        if known is not None:
+            try:
+                if self.attached_ids(cgdir) == known[0]:
+                    return set(known[1])
+            except CgroupError:
+                pass
+            self._installed.pop(cgdir, None)
         progs, foreign = attached_programs(cgdir)
         if not progs:
             return set()

@@ -44,7 +44,8 @@ class DevNodeWriter:
     """``host_dev``: the host's ``/dev`` as the worker sees it. A container directory that *is*
     that ``/dev`` (or its ``dri/``) — a hostPath ``/dev`` bind, a privileged runtime's — is never
     written: creates and unlinks there report :data:`SHARED_HOST` and leave the host's nodes be.
-    The guard is process-wide in the native layer (the last writer constructed sets it)."""
+    The guard is process-wide in the native layer (the last writer constructed sets or clears
+    it; a worker process has exactly one)."""
 
     def __init__(self, mode: str = "procroot", host_dev: str = "") -> None:
         self.mode = mode
@@ -54,13 +55,12 @@ class DevNodeWriter:
         if mode == "emulate":
             self.flags |= _native.GM_DEV_EMULATE
         self.host_dev = host_dev
-        self.guarded = 0
-        if host_dev:
-            rc = _native.host().gm_devnodes_guard(host_dev.encode())
-            if rc < 0:
-                _log.warning("host /dev guard off: cannot read %s (%s)", host_dev,
-                             os.strerror(-rc))
-            self.guarded = max(rc, 0)
+        # always (re)set: a writer without host_dev clears a guard an earlier one left, whose
+        # directory may be gone and its inode number reused by an unrelated directory
+        rc = _native.host().gm_devnodes_guard(host_dev.encode() if host_dev else None)
+        if rc < 0:
+            _log.warning("host /dev guard off: cannot read %s (%s)", host_dev, os.strerror(-rc))
+        self.guarded = max(rc, 0)
 
     @staticmethod
     def _array(nodes: Sequence[DeviceNode]):
@@ -131,3 +131,17 @@ class DevNodeWriter:
     def present(self, t: Target, node: DeviceNode) -> bool:
         kind, ma, mi, _ = self.stat(t, node.path)
         return kind in (1, 2) and ma == node.major and mi == node.minor
+
+    def present_many(self, t: Target, nodes: Sequence[DeviceNode]) -> List[bool]:
+        """:meth:`present` for a whole node set in one native call (one root resolution). A
+        node in a directory that is the host's own ``/dev`` counts as present: create leaves
+        it to the host (:data:`SHARED_HOST`) and so does the read-back."""
+        if not nodes:
+            return []
+        pid, root = self._target_args(t)
+        out = (C.c_uint8 * len(nodes))()
+        rc = _native.host().gm_devnodes_present(pid, root, self._array(nodes), len(nodes),
+                                                self.flags, out)
+        if rc < 0:
+            raise DevNodeError(f"read-back of {len(nodes)} nodes: {os.strerror(-rc)}")
+        return [bool(out[i]) for i in range(len(nodes))]

@@ -280,18 +280,23 @@ class HotMount:
         return out
 
     # ------------------------------------------------------------------------ audit
-    def verify(self, pod: dict, gpus: Sequence[AmdGpu], container: str = "") -> List[AuditIssue]:
-        """Read back what an attach of ``gpus`` must have produced in every target container:
-        the device rules (as the kernel evaluates them) and the device nodes, /dev/kfd
-        included. A narrower, cheaper :meth:`audit` for the attach path."""
-        want = self.gpu_nodes(gpus) + [self.kfd()]
+    def verify(self, pod: dict, hot: Sequence[AmdGpu], base: Sequence[AmdGpu] = (),
+               container: str = "",
+               targets: Optional[List[ContainerTarget]] = None) -> List[AuditIssue]:
+        """Read back what an attach must have produced in every target container — the rules
+        (as the kernel evaluates them) and nodes of every hot-mounted GPU (``hot``, the new ones
+        included) and /dev/kfd when gpumounter manages it. A narrower, cheaper :meth:`audit`
+        for the attach path: no journal walk, the attach's resolved ``targets`` are reused and
+        every node is read back in one native call."""
+        want = self.managed_nodes(hot, base)
         issues: List[AuditIssue] = []
-        for t in self.targets(pod, container):
+        for t in targets if targets is not None else self.targets(pod, container):
             allowed = self.backend.allowed(t.cgdir)
-            for n in want:
+            present = self.writer.present_many(t.target, want)
+            for n, ok in zip(want, present):
                 if (n.major, n.minor) not in allowed:
                     issues.append(AuditIssue(t.ref.name, "missing_rule", n.path, n.major, n.minor))
-                if not self.writer.present(t.target, n):
+                if not ok:
                     issues.append(AuditIssue(t.ref.name, "missing_node", n.path, n.major, n.minor))
         return issues
 
@@ -304,10 +309,10 @@ class HotMount:
         base_keys = {(n.major, n.minor) for n in self.gpu_nodes(base)}
         for t in self.targets(pod, container):
             allowed = self.backend.allowed(t.cgdir)
-            for n in want:
+            for n, ok in zip(want, self.writer.present_many(t.target, want)):
                 if (n.major, n.minor) not in allowed:
                     issues.append(AuditIssue(t.ref.name, "missing_rule", n.path, n.major, n.minor))
-                if not self.writer.present(t.target, n):
+                if not ok:
                     issues.append(AuditIssue(t.ref.name, "missing_node", n.path, n.major, n.minor))
             # stale = recorded as injected by gpumounter and no longer backed by the ledger;
             # whatever else the container holds is not gpumounter's to judge

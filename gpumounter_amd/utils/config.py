@@ -119,9 +119,10 @@ class Config:
     # unless lease_force, which signals their processes like force=1
     lease_force: bool = False
     lease_retry_s: float = 30.0
-    # read the device rules and nodes back after each attach (span "verify") and roll back if
+    # read the device rules and nodes back after each attach (span "verify": one native
+    # read-back of every node plus the kernel's rule set per container) and roll back if
     # anything did not take effect; off = rely on the reconciler's periodic audit
-    attach_verify: bool = False
+    attach_verify: bool = True
     # pool-namespace placeholders are invisible to the tenant namespace's ResourceQuota; enforce
     # requests.<resource_name> quotas for hot-mounted GPUs ourselves (cluster/quota.py) | off
     quota_mode: str = "enforce"

@@ -335,11 +335,12 @@ class GpuMountService:
                 self.metrics.placement_mismatch.inc()
             try:
                 with trace.span("mount", gpus=len(new)):
-                    self.hm.attach(pod, new, st.hot, st.own, req.container)
+                    targets = self.hm.attach(pod, new, st.hot, st.own, req.container)
                 if self.cfg.attach_verify:
                     with trace.span("verify"):
                         self.faults.check("verify")
-                        issues = self.hm.verify(pod, new, req.container)
+                        issues = self.hm.verify(pod, list(st.hot) + new, st.own,
+                                                req.container, targets)
                     if issues:
                         self.metrics.verify_failures.inc()
                         raise MountError("attach did not take effect: " + ", ".join(

@@ -130,6 +130,12 @@ int gm_devnodes_remove(int pid, const char* root, const gm_dev_node_t* nodes, in
 // Describes a node: *kind = 0 absent, 1 char device, 2 emulated marker, 3 other file.
 int gm_devnode_stat(int pid, const char* root, const char* path, int flags, int* kind,
                     uint32_t* major, uint32_t* minor, uint32_t* mode);
+// Read-back of a whole node set in one root resolution (the attach verify step):
+// present[i] = 1 if nodes[i].path is a char device (or emulated marker) with exactly
+// nodes[i].major:minor, 2 if its directory is the host's guarded /dev (shared, never ours to
+// create), else 0. Returns the number present, or -errno if the root is unreachable.
+int gm_devnodes_present(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
+                        uint8_t* present);
 
 // ---- processes ------------------------------------------------------------------------------
 // Sends `sig` to each pid via pidfd (falls back to kill(2)). results[i] = 0 or -errno.

@@ -839,8 +839,10 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
     if (cnt < 0) return -EINVAL;
     uint64_t t2 = mono_ns();
     tm.build_ns += t2 - t1;
-    char log[4096];
-    Fd pfd(gm_bpf_dev_load(prog.data(), cnt, kProgName, log, sizeof(log)));
+    // No verifier log on the hot path: log_level 1 makes the verifier print every instruction
+    // of every explored path, which costs more than the verification itself. The program is
+    // generated, so a rejection is a bug; gm_bpf_dev_load with a log buffer reproduces it.
+    Fd pfd(gm_bpf_dev_load(prog.data(), cnt, kProgName, nullptr, 0));
     if (!pfd.ok()) return pfd.fd;
     uint64_t t3 = mono_ns();
     tm.load_ns += t3 - t2;
@@ -969,6 +971,48 @@ int gm_devnode_stat(int pid, const char* root, const char* path, int flags, int*
     if (e < 0) return e;
     return stat_leaf(parent.fd, leaf, kind, maj, min, mode);
   });
+}
+
+int gm_devnodes_present(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
+                        uint8_t* present) {
+  int count = 0;
+  int e = with_root(pid, root, flags, [&](int rootfd) {
+    for (int i = 0; i < n; ++i) {
+      present[i] = 0;
+      Fd parent;
+      std::string leaf;
+      int w = walk_parent(rootfd, nodes[i].path, false, &parent, &leaf);
+      if (w == -ENOENT) {
+        // a missing directory inside the host's /dev is one create_one would not make either
+        std::string dir(nodes[i].path);
+        const size_t cut = dir.rfind('/');
+        dir = cut == std::string::npos ? std::string() : dir.substr(0, cut);
+        Fd d2;
+        std::string l2;
+        if (!dir.empty() && walk_parent(rootfd, dir.c_str(), false, &d2, &l2) == 0 &&
+            guarded_dir(d2.fd)) {
+          present[i] = kSharedHost;
+          ++count;
+        }
+        continue;
+      }
+      if (w < 0) continue;
+      if (guarded_dir(parent.fd)) {  // the host's own /dev: not gpumounter's to provide
+        present[i] = kSharedHost;
+        ++count;
+        continue;
+      }
+      int kind = 0;
+      uint32_t ma = 0, mi = 0, mode = 0;
+      if (stat_leaf(parent.fd, leaf, &kind, &ma, &mi, &mode) < 0) continue;
+      if ((kind == 1 || kind == 2) && ma == nodes[i].major && mi == nodes[i].minor) {
+        present[i] = 1;
+        ++count;
+      }
+    }
+    return 0;
+  });
+  return e < 0 ? e : count;
 }
 
 // ------------------------------------------------------------------ processes

@@ -117,3 +117,27 @@ def test_attach_reads_the_ledger_once_per_event():
         assert code == 200
         return kl.calls["List"] + kl.calls["Get"] - before
     assert run(body) <= 4
+
+
+def test_count_mode_serves_and_counts_over_budget_calls(tmp_path):
+    """limit_mode="count" (how bench.py times the emulated reference, which has no retry):
+    every call is served, the ones a limited kubelet would reject are counted."""
+    inv = Inventory("mock")
+    node = FakeNode("n", str(tmp_path), inv.gpus())
+    sock = os.path.join(str(tmp_path), "pr", "kubelet.sock")
+
+    async def body():
+        kl = FakeKubelet(node, sock, rate_limit=(20.0, 1), limit_mode="count")
+        await kl.start()
+        client = LedgerClient(sock, "amd.com/gpu", timeout_s=5.0, qps=0)
+        try:
+            for _ in range(6):
+                assert await client.by_pod() == {}
+        finally:
+            await client.close()
+            await kl.stop()
+        return kl.calls
+    calls = asyncio.run(body())
+    assert calls["rejected"] == 0 and calls["over_limit"] >= 3
+    with pytest.raises(ValueError):
+        FakeKubelet(node, sock, limit_mode="drop")

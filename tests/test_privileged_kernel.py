@@ -321,3 +321,28 @@ def test_devnodes_real_mknod_via_setns(tmp_path):
     finally:
         child.kill()
         child.wait()
+
+
+def test_cgroup_v2_allowed_fast_path_tracks_attached_ids(cgroup2_child, bpffs, monkeypatch):
+    """attach verify: while the cgroup's attached id list is exactly what this backend installed,
+    allowed() answers from the rules it compiled (one BPF_PROG_QUERY, no xlated read-back) and
+    agrees with the kernel read-back; once anything else is attached it reads the kernel again."""
+    from gpumounter_amd.node import cgroup as cgmod
+
+    cg = cgroup2_child
+    attach_runtime_program(cg)
+    be = V2BpfBackend(bpffs)
+    be.apply(cg, [ZERO, FULL], [], [ZERO, FULL])
+    slow = cgmod.attached_programs
+    calls = []
+    monkeypatch.setattr(cgmod, "attached_programs", lambda d: calls.append(d) or slow(d))
+    fast = be.allowed(cg)
+    assert fast == {(ZERO.major, ZERO.minor), (FULL.major, FULL.minor)} and calls == []
+    be._installed.clear()                                  # the read-back agrees
+    assert be.allowed(cg) >= fast and len(calls) == 1
+    be.apply(cg, [], [FULL], [ZERO])
+    assert be.allowed(cg) == {(ZERO.major, ZERO.minor)} and len(calls) == 1
+    # a foreign program joins (systemd re-realising the unit): only /dev/null, vetoes ZERO
+    attach_runtime_program(cg, name=b"sd_devices")
+    assert (ZERO.major, ZERO.minor) not in be.allowed(cg) and len(calls) == 2
+    assert probe_access(cg, [NULL.path, ZERO.path]) == "10"
