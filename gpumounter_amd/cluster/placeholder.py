@@ -88,9 +88,22 @@ def _label_value(s: str) -> str:
     return s.rstrip("-_.") or "x"
 
 
+def _admitted(pod: Optional[dict]) -> bool:
+    """The kubelet has run admission (device-plugin Allocate) for this pod: it posts container
+    statuses (ContainerCreating) only afterwards."""
+    return bool(pod) and (bool(pod.get("status", {}).get("containerStatuses")) or
+                          podu.phase_of(pod) == "Running")
+
+
 class PlaceholderManager:
     # admission re-read backoff when no placeholder event arrives: first wait, cap (seconds)
     ADMISSION_BACKOFF_S = (0.010, 0.100)
+    # the same with the device-manager checkpoint in use: events (pod watch + inotify) carry
+    # the normal path, the RPC is only a safety net
+    ADMISSION_BACKOFF_CKPT_S = (0.050, 0.200)
+    # consecutive "admitted per the apiserver, absent from the checkpoint" reads after which
+    # the checkpoint counts as not maintained by this kubelet
+    CHECKPOINT_MISSES = 3
 
     def __init__(self, cfg, kube: KubeClient, ledger: LedgerClient, informer: PodInformer,
                  node_name: str, faults=None) -> None:
@@ -102,6 +115,11 @@ class PlaceholderManager:
         self.informer = informer
         self.node = node_name
         self.faults = faults if faults is not None else NONE
+        # the kubelet device manager's checkpoint (node/checkpoint.py), set by the worker when
+        # ledger_source=auto: admission then needs no PodResources call
+        self.checkpoint = None
+        self.checkpoint_hits = 0
+        self._checkpoint_misses = 0
         # uid → device IDs of admitted placeholders (immutable for a pod's lifetime)
         self.device_ids: Dict[str, Tuple[str, ...]] = {}
         # uids we deleted but the watch has not reported yet: excluded from every query, so a
@@ -322,12 +340,18 @@ class PlaceholderManager:
         loop = asyncio.get_running_loop()
         deadline = loop.time() + timeout
         seen: Dict[Tuple[str, str], str] = {}   # resourceVersion at our last ledger read
-        delay = self.ADMISSION_BACKOFF_S[0]
+        ck = self.checkpoint if self.checkpoint is not None and self.checkpoint.trusted else None
+        backoff = self.ADMISSION_BACKOFF_CKPT_S if ck is not None else self.ADMISSION_BACKOFF_S
+        delay = backoff[0]
         while pending:
             failure: Dict[Tuple[str, str], str] = {}
+            from_ckpt: Dict[Tuple[str, str], Tuple[str, ...]] = {}
+            bound_keys: List[Tuple[str, str]] = []
 
             def state():
                 fresh = []
+                from_ckpt.clear()
+                bound_keys.clear()
                 for key in pending:
                     pod = self.informer.cache.get(key)
                     # _create put it in the cache, so gone = deleted by someone else (the
@@ -342,25 +366,36 @@ class PlaceholderManager:
                         failure[key] = f"unschedulable: {msg}"
                     elif podu.phase_of(pod) == "Failed":
                         failure[key] = pod["status"].get("reason", "Failed")
-                    elif podu.node_of(pod) and \
-                            seen.get(key) != pod["metadata"].get("resourceVersion"):
-                        fresh.append(key)         # bound, and news since our last read
+                    elif podu.node_of(pod):
+                        bound_keys.append(key)
+                        news = seen.get(key) != pod["metadata"].get("resourceVersion")
+                        if ck is None:
+                            if news:
+                                fresh.append(key)     # bound, and news since our last read
+                        else:
+                            ids = ck.lookup(pending[key].uid)
+                            if ids:
+                                from_ckpt[key] = ids
+                            elif news and _admitted(pod):
+                                # the kubelet writes the checkpoint at Allocate, before it
+                                # posts this status: a miss here means it does not maintain it
+                                fresh.append(key)
                     if failure and not tolerant:
                         return True
-                return True if failure else (fresh or None)
+                return True if failure else (fresh or bool(from_ckpt) or None)
 
             left = deadline - loop.time()
             if left <= 0:
                 raise ReserveError(f"timeout waiting for placeholders {sorted(pending)}")
             try:
                 ready = await self.informer.wait_for(
-                    state, timeout=min(left, delay) if seen else left)
+                    state, timeout=min(left, delay) if (seen or (ck and bound_keys)) else left)
             except asyncio.TimeoutError:
                 if loop.time() >= deadline:
                     raise ReserveError(f"timeout waiting for placeholders {sorted(pending)}")
                 # bound but no news: re-read what is bound, backing off
-                ready = [k for k in pending if k in seen]
-                delay = min(delay * 2, self.ADMISSION_BACKOFF_S[1])
+                ready = [k for k in pending if k in seen or (ck is not None and k in bound_keys)]
+                delay = min(delay * 2, backoff[1])
             if failure and not tolerant:
                 reason = next(iter(failure.values()))
                 if reason.startswith("unschedulable") or reason.startswith("OutOf") or \
@@ -369,6 +404,16 @@ class PlaceholderManager:
                 raise ReserveError(reason)
             for key in failure:
                 failed.append(pending.pop(key))
+            if from_ckpt:
+                self.faults.check("ledger_read")
+            for key, ids in list(from_ckpt.items()):    # admitted: known without an RPC
+                if key in pending:
+                    ph = pending.pop(key)
+                    ph.device_ids = tuple(ids)
+                    self.device_ids[ph.uid] = ph.device_ids
+                    self.last_ledger = {**self.last_ledger, key: list(ids)}
+                    self.checkpoint_hits += 1
+                    self._checkpoint_misses = 0
             if not pending:
                 break
             bound = [k for k in ready if k in pending] if isinstance(ready, list) else []
@@ -396,6 +441,12 @@ class PlaceholderManager:
                     ph = pending.pop(key)
                     ph.device_ids = tuple(ids)
                     self.device_ids[ph.uid] = ph.device_ids
+                    if ck is not None and _admitted(self.informer.cache.get(key)) and \
+                            ck.lookup(ph.uid) is None:
+                        self._checkpoint_misses += 1
+                        if self._checkpoint_misses >= self.CHECKPOINT_MISSES:
+                            ck.distrust(f"{self._checkpoint_misses} admitted placeholders in "
+                                        f"a row had no entry in it")
         return failed
 
     # ------------------------------------------------------------------------ release

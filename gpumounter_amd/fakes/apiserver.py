@@ -313,10 +313,12 @@ class FakeCluster:
                 pref = (pod["metadata"].get("annotations") or {}).get(
                     "gpumounter.amd.com/preferred-devices", "")
                 if node.plugin is not None:      # kubelet device manager → device plugin
-                    ids = await node.plugin.plugin_allocate(ns, name, c["name"], want)
+                    ids = await node.plugin.plugin_allocate(ns, name, c["name"], want,
+                                                            uid=pod["metadata"]["uid"])
                 else:
                     ids = node.allocate(ns, name, c["name"], want,
-                                        [p for p in pref.split(",") if p])
+                                        [p for p in pref.split(",") if p],
+                                        uid=pod["metadata"]["uid"])
                 if ids is None:
                     node.release_pod(ns, name)
                     pod["status"]["phase"] = "Failed"
@@ -370,7 +372,8 @@ class FakeCluster:
         for c in pod["spec"].get("containers", []):
             want = int(podu.parse_quantity(
                 ((c.get("resources") or {}).get("limits") or {}).get(n.resource, 0)))
-            if want and n.allocate(ns, pod["metadata"]["name"], c["name"], want) is None:
+            if want and n.allocate(ns, pod["metadata"]["name"], c["name"], want,
+                                   uid=pod["metadata"]["uid"]) is None:
                 raise RuntimeError("tenant pod does not fit")
         self._start_containers(n, pod, pids)
         return pod

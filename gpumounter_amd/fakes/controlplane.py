@@ -68,6 +68,7 @@ async def run(args) -> None:
     await lc.start()
     info = {"api_url": lc.api_url, "pid": os.getpid(),
             "nodes": {name: {"kubelet_socket": h.kubelet.socket_path,
+                             "kubelet_checkpoint": h.node.checkpoint_path,
                              "cgroup_root": h.node.cgroup_root,
                              "rootfs_root": h.node.rootfs_root,
                              "state_dir": h.node.state_dir, "host_dev": h.node.host_dev}

@@ -150,6 +150,7 @@ class ProcessCluster:
             self.worker_ports[node] = (gport, mport)
             env = {"GM_KUBE_API": api, "GM_NODE_NAME": node,
                    "GM_KUBELET_SOCKET": n["kubelet_socket"], "GM_CGROUP_ROOT": n["cgroup_root"],
+                   "GM_KUBELET_CHECKPOINT": n["kubelet_checkpoint"],
                    "GM_CGROUP_MODE": self.cgroup_mode, "GM_DEVNODE_MODE": "emulate",
                    "GM_CONTAINER_ROOT_PREFIX": n["rootfs_root"], "GM_AMDSMI_LIB": self.amdsmi_lib,
                    "GM_STATE_DIR": n["state_dir"], "GM_HOST_DEV_PATH": n["host_dev"],

@@ -149,6 +149,7 @@ class LocalCluster:
         if self.device_plugin:
             ov.setdefault("device_plugin", True)
             ov.setdefault("device_plugin_dir", h.kubelet.plugin_dir)
+        ov.setdefault("kubelet_checkpoint", h.node.checkpoint_path)
         cfg = Config.load(env={}, kube_api=self.api_url, node_name=name,
                           kubelet_socket=h.kubelet.socket_path,
                           cgroup_root=h.node.cgroup_root, cgroup_mode=self.cgroup_mode,

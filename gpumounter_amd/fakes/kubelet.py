@@ -94,8 +94,8 @@ class FakeKubelet:
             await self._plugin_ch.close()
             self._plugin_ch = None
 
-    async def plugin_allocate(self, ns: str, pod: str, container: str, n: int
-                              ) -> Optional[List[str]]:
+    async def plugin_allocate(self, ns: str, pod: str, container: str, n: int,
+                              uid: str = "") -> Optional[List[str]]:
         """Device-manager admission: healthy free devices → GetPreferredAllocation → Allocate."""
         async with self._alloc_lock:
             free = [d for d in self.node.free_ids() if d not in self.node.unhealthy
@@ -119,7 +119,7 @@ class FakeKubelet:
             req = dp.AllocateRequest()
             req.container_requests.add(devices_ids=ids)
             await alloc(req, timeout=5)
-            return ids if self.node.record(ns, pod, container, ids) else None
+            return ids if self.node.record(ns, pod, container, ids, uid=uid) else None
 
     def _fill(self, api, resp, only=None):
         for (ns, pod), containers in sorted(self.node.ledger().items()):

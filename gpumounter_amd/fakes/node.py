@@ -25,6 +25,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 from gpumounter_amd.hw import topology
 from gpumounter_amd.models.device import AmdGpu, LinkMatrix, normalize_device_id
+from gpumounter_amd.node import checkpoint as ckpt
+from gpumounter_amd.node.checkpoint import CHECKPOINT_NAME
 from gpumounter_amd.models.pod import QOS_BESTEFFORT, QOS_BURSTABLE, qos_class
 
 FAKE_MARKER = ".gm_fake"
@@ -94,8 +96,16 @@ class FakeNode:
             os.makedirs(os.path.join(self.cgroup_root, "devices"), exist_ok=True)
         self.images: set = set()
         self._lock = threading.RLock()
-        # device id → (ns, pod, container)
+        # device id → (ns, pod, container), and the owning pod's UID
         self.allocated: Dict[str, Tuple[str, str, str]] = {}
+        self.alloc_uid: Dict[str, str] = {}
+        # the device manager's checkpoint, rewritten (tmp + rename) after every allocation
+        # change like the kubelet's (node/checkpoint.py); write_checkpoint=False models a kubelet
+        # that does not maintain it
+        self.plugin_dir = os.path.join(workdir, "device-plugins")
+        os.makedirs(self.plugin_dir, exist_ok=True)
+        self.checkpoint_path = os.path.join(self.plugin_dir, CHECKPOINT_NAME)
+        self.write_checkpoint = True
         self.containers: Dict[str, Container] = {}  # container id → Container
         self.alloc_log: List[Tuple[str, str, List[str]]] = []
         # a registered device plugin (FakeKubelet device manager) replaces allocate()
@@ -150,8 +160,20 @@ class FakeNode:
         with self._lock:
             return [d for d in self.device_ids() if d not in self.allocated]
 
+    def _checkpoint(self) -> None:
+        if not self.write_checkpoint:
+            return
+        per: Dict[Tuple[str, str], Dict[int, List[str]]] = {}
+        for d, (_, _, c) in sorted(self.allocated.items()):
+            uid = self.alloc_uid.get(d, "")
+            if uid:
+                per.setdefault((uid, c), {}).setdefault(max(self.numa_of(d), 0), []).append(d)
+        ckpt.write_atomic(self.checkpoint_path, ckpt.render(
+            [(uid, c, self.resource, ids) for (uid, c), ids in sorted(per.items())],
+            {self.resource: self.device_ids()}))
+
     def allocate(self, ns: str, pod: str, container: str, n: int,
-                 preferred: Sequence[str] = ()) -> Optional[List[str]]:
+                 preferred: Sequence[str] = (), uid: str = "") -> Optional[List[str]]:
         """kubelet device-manager Allocate; returns device IDs or None (insufficient)."""
         with self._lock:
             free = [g for g in self.gpus if self.device_id(g) not in self.allocated]
@@ -172,17 +194,22 @@ class FakeNode:
             ids = [self.device_id(g) for g in chosen]
             for d in ids:
                 self.allocated[d] = (ns, pod, container)
+                self.alloc_uid[d] = uid
             self.alloc_log.append((ns, pod, ids))
+            self._checkpoint()
             return ids
 
-    def record(self, ns: str, pod: str, container: str, ids: Sequence[str]) -> bool:
+    def record(self, ns: str, pod: str, container: str, ids: Sequence[str],
+               uid: str = "") -> bool:
         """Commit an allocation chosen elsewhere (device-plugin path); False if any is taken."""
         with self._lock:
             if any(d in self.allocated for d in ids):
                 return False
             for d in ids:
                 self.allocated[d] = (ns, pod, container)
+                self.alloc_uid[d] = uid
             self.alloc_log.append((ns, pod, list(ids)))
+            self._checkpoint()
             return True
 
     def release_pod(self, ns: str, pod: str) -> List[str]:
@@ -190,6 +217,9 @@ class FakeNode:
             ids = [d for d, (n, p, _) in self.allocated.items() if n == ns and p == pod]
             for d in ids:
                 del self.allocated[d]
+                self.alloc_uid.pop(d, None)
+            if ids:
+                self._checkpoint()
             return ids
 
     def ledger(self) -> Dict[Tuple[str, str], Dict[str, Dict[str, List[str]]]]:

@@ -58,6 +58,11 @@ class Config:
     # client-side pacing of PodResources calls, under the kubelet's own limiter (100 qps,
     # burst 10, RESOURCE_EXHAUSTED beyond it) which other node agents share; 0 = unpaced
     kubelet_qps: float = 50.0
+    # where admission reads a placeholder's GPUs: "auto" = the device manager's checkpoint file
+    # (by pod UID, inotify-woken, no RPC: node/checkpoint.py) with PodResources as fallback and
+    # authority; "podresources" = always the RPC
+    ledger_source: str = "auto"
+    kubelet_checkpoint: str = "/var/lib/kubelet/device-plugins/kubelet_internal_checkpoint"
     kubelet_burst: int = 8
     # --- device & isolation ----------------------------------------------------------------
     amdsmi_lib: str = ""               # "" → libamd_smi.so from ROCm; "mock" → bundled mock
@@ -216,6 +221,7 @@ class Config:
         _choice("authz_mode", self.authz_mode, ("none", "kube"))
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))
         _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
+        _choice("ledger_source", self.ledger_source, ("auto", "podresources"))
         if not (0 < self.worker_port < 65536 and 0 <= self.master_port < 65536):
             raise ValueError("ports out of range")
 

@@ -26,6 +26,7 @@ from gpumounter_amd.cluster.pool import WarmPool
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.node import systemd
 from gpumounter_amd.node.cgroup import CgroupResolver, make_backend
+from gpumounter_amd.node.checkpoint import DeviceCheckpoint
 from gpumounter_amd.node.devnodes import DevNodeWriter
 from gpumounter_amd.node.hotmount import HotMount
 from gpumounter_amd.node.journal import InjectionJournal
@@ -84,6 +85,10 @@ class Worker:
                                          resync_s=cfg.watch_resync_s)
         self.placeholders = PlaceholderManager(cfg, self.kube, self.ledger, self.ph_informer,
                                                cfg.node_name, self.faults)
+        self.checkpoint = None
+        if cfg.ledger_source == "auto" and cfg.kubelet_checkpoint:
+            self.checkpoint = DeviceCheckpoint(cfg.kubelet_checkpoint, cfg.resource_name)
+            self.placeholders.checkpoint = self.checkpoint
         self.service = GpuMountService(cfg, self.kube, self.inv, self.ledger, self.placeholders,
                                        self.hotmount, self.node_informer, self.metrics,
                                        self.faults)
@@ -162,6 +167,12 @@ class Worker:
         await self.node_informer.start()
         # warm the ledger channel (fails fast if the kubelet socket is wrong)
         await self.ledger.list()
+        if self.checkpoint is not None:
+            watched = self.checkpoint.watch(
+                lambda: asyncio.ensure_future(self.ph_informer.poke()))
+            _log.info("device-manager checkpoint %s: %s, inotify %s", self.checkpoint.path,
+                      "present" if self.checkpoint.snapshot() is not None else "absent",
+                      "on" if watched else "off")
         if not (self.cfg.tls_cert and self.cfg.tls_key and self.cfg.tls_ca) and \
                 not self.cfg.worker_insecure:
             raise ValueError("worker refuses to serve gRPC without mTLS: set GM_TLS_CERT, "
@@ -316,6 +327,8 @@ class Worker:
             await self.http_runner.cleanup()
         await self.ph_informer.stop()
         await self.node_informer.stop()
+        if self.checkpoint is not None:
+            self.checkpoint.close()
         await self.ledger.close()
         await self.kube.close()
 

@@ -1,0 +1,88 @@
+"""The kubelet device-manager checkpoint reader (gpumounter_amd/node/checkpoint.py)."""
+import asyncio
+import json
+import os
+
+import pytest
+
+from gpumounter_amd.node import checkpoint as ckpt
+
+V2 = {"Data": {"PodDeviceEntries": [
+    {"PodUID": "u1", "ContainerName": "a", "ResourceName": "amd.com/gpu",
+     "DeviceIDs": {"1": ["0000:85:00.0"], "0": ["0000:05:00.0"]}, "AllocResp": "Cg=="},
+    {"PodUID": "u1", "ContainerName": "b", "ResourceName": "amd.com/gpu",
+     "DeviceIDs": {"0": ["0000:15:00.0"]}, "AllocResp": ""},
+    {"PodUID": "u2", "ContainerName": "a", "ResourceName": "example.com/nic",
+     "DeviceIDs": {"0": ["nic0"]}, "AllocResp": ""}],
+    "RegisteredDevices": {"amd.com/gpu": ["0000:05:00.0"]}}, "Checksum": 42}
+
+
+def test_parse_v2_groups_by_uid_numa_ordered_and_filters_resource():
+    got = ckpt.parse(json.dumps(V2).encode(), "amd.com/gpu")
+    assert got == {"u1": ("0000:05:00.0", "0000:85:00.0", "0000:15:00.0")}
+
+
+def test_parse_pre_1_20_flat_list_and_empty():
+    doc = {"Data": {"PodDeviceEntries": [{"PodUID": "u", "ContainerName": "c",
+                                          "ResourceName": "amd.com/gpu",
+                                          "DeviceIDs": ["renderD128"], "AllocResp": ""}],
+                    "RegisteredDevices": {}}, "Checksum": 1}
+    assert ckpt.parse(json.dumps(doc).encode(), "amd.com/gpu") == {"u": ("renderD128",)}
+    empty = {"Data": {"PodDeviceEntries": None, "RegisteredDevices": None}, "Checksum": 0}
+    assert ckpt.parse(json.dumps(empty).encode(), "amd.com/gpu") == {}
+
+
+@pytest.mark.parametrize("blob", [b"", b"{", b"[]", b'{"Data": 3}',
+                                  b'{"Data": {"PodDeviceEntries": [1]}}',
+                                  b'{"Data": {"PodDeviceEntries": [{"PodUID": "u", '
+                                  b'"ResourceName": "amd.com/gpu", "DeviceIDs": 7}]}}'])
+def test_parse_rejects_what_is_not_a_checkpoint(blob):
+    with pytest.raises(ckpt.CheckpointFormatError):
+        ckpt.parse(blob, "amd.com/gpu")
+
+
+def test_render_round_trips():
+    blob = ckpt.render([("u9", "main", "amd.com/gpu", {0: ["a", "b"], 1: ["c"]})],
+                       {"amd.com/gpu": ["a", "b", "c"]})
+    assert ckpt.parse(blob, "amd.com/gpu") == {"u9": ("a", "b", "c")}
+
+
+def test_reader_parses_only_when_the_file_changes(tmp_path):
+    path = str(tmp_path / ckpt.CHECKPOINT_NAME)
+    r = ckpt.DeviceCheckpoint(path, "amd.com/gpu")
+    assert r.snapshot() is None and r.lookup("u1") is None      # absent
+    ckpt.write_atomic(path, json.dumps(V2).encode())
+    assert r.lookup("u1")[0] == "0000:05:00.0" and r.parses == 1
+    for _ in range(5):
+        assert r.lookup("u2") is None
+    assert r.parses == 1                                        # stat-only while unchanged
+    ckpt.write_atomic(path, ckpt.render([("u2", "c", "amd.com/gpu", {0: ["x"]})]))
+    assert r.lookup("u2") == ("x",) and r.lookup("u1") is None and r.parses == 2
+    with open(path, "wb") as fh:
+        fh.write(b"garbage")
+    assert r.snapshot() is None and r.errors == 1
+    r.distrust("test")
+    ckpt.write_atomic(path, json.dumps(V2).encode())
+    assert r.lookup("u1") is None                               # distrusted for good
+
+
+def test_inotify_wakes_on_the_kubelets_rename(tmp_path):
+    path = str(tmp_path / ckpt.CHECKPOINT_NAME)
+
+    async def body():
+        r = ckpt.DeviceCheckpoint(path, "amd.com/gpu")
+        woke = asyncio.Event()
+        assert r.watch(woke.set)
+        try:
+            with open(tmp_path / "unrelated", "w") as fh:   # other files do not wake
+                fh.write("x")
+            await asyncio.sleep(0.05)
+            assert not woke.is_set()
+            ckpt.write_atomic(path, ckpt.render([("u", "c", "amd.com/gpu", {0: ["g"]})]))
+            await asyncio.wait_for(woke.wait(), 2)
+            return r.lookup("u")
+        finally:
+            r.close()
+    assert asyncio.run(body()) == ("g",)
+    assert not ckpt.DeviceCheckpoint(str(tmp_path / "nodir" / "x"), "r").watch(lambda: None)
+    assert os.path.exists(path)

@@ -9,6 +9,7 @@ import pytest
 from gpumounter_amd import _native
 from gpumounter_amd.fakes.harness import LocalCluster
 from gpumounter_amd.models.types import LABEL_OWNER
+from gpumounter_amd.node import checkpoint as ckpt
 
 
 def run(coro_fn, **kw):
@@ -753,6 +754,45 @@ def test_kubelet_restart_is_survived_without_waiting_for_grpc_backoff():
         await h.kubelet.start()
         code, b = await lc.add("default", "t", 1)
         assert code == 200, b
+        assert await lc.audit("default", "t") == []
+    run(body, worker_overrides={"ledger_source": "podresources"})
+
+
+def test_attach_reads_the_device_manager_checkpoint_not_the_podresources_socket():
+    """ledger_source=auto (default): admission finds the placeholder's GPUs in the kubelet's
+    device-manager checkpoint by pod UID — no PodResources call on the attach path, so an
+    attach still works while that socket is down. A kubelet that does not maintain the
+    checkpoint is detected (admitted placeholder, no entry) and PodResources takes over."""
+    from gpumounter_amd.fakes.kubelet import FakeKubelet
+
+    async def body(lc):
+        lc.tenant("t")
+        h = lc.nodes["node-0"]
+        ph = h.worker.placeholders
+        assert (await lc.add("default", "t", 1))[0] == 200   # first sight: one List (own GPUs)
+        before = dict(h.kubelet.calls)
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200, b
+        assert h.kubelet.calls["Get"] == before["Get"] and \
+            h.kubelet.calls["List"] == before["List"]
+        assert ph.checkpoint_hits >= 1 and ph.checkpoint.trusted
+        await h.kubelet.stop()
+        assert (await lc.add("default", "t", 1))[0] == 200        # socket down: still served
+        h.kubelet = FakeKubelet(h.node, h.kubelet.socket_path)
+        await h.kubelet.start()
+        assert await lc.audit("default", "t") == []
+        # a kubelet without the checkpoint: three misses in a row, then PodResources only
+        h.node.write_checkpoint = False
+        os.unlink(h.node.checkpoint_path)
+        for _ in range(3):
+            code, b = await lc.add("default", "t", 1)
+            assert code == 200, b
+            code, _ = await lc.remove("default", "t", [b["devices"][0]["uuid"]])
+            assert code == 200
+        assert h.kubelet.calls["Get"] >= 3
+        h.node.write_checkpoint = True
+        ckpt.write_atomic(h.node.checkpoint_path, ckpt.render([]))
+        assert ph.checkpoint.lookup("anything") is None            # distrusted for good
         assert await lc.audit("default", "t") == []
     run(body)
 

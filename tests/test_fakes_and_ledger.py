@@ -214,7 +214,8 @@ def test_admission_reads_placeholders_with_podresources_get(use_get):
     from gpumounter_amd.fakes.harness import LocalCluster
 
     async def main():
-        async with LocalCluster(worker_overrides={"ledger_get": use_get}) as lc:
+        async with LocalCluster(worker_overrides={"ledger_get": use_get,
+                                                  "ledger_source": "podresources"}) as lc:
             lc.tenant("t")
             kub = lc.nodes["node-0"].kubelet
             before = dict(kub.calls)
