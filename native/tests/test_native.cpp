@@ -85,6 +85,14 @@ static void test_devnodes() {
   uint32_t ma = 0, mi = 0, mode = 0;
   EXPECT(gm_devnode_stat(0, root, "dev/dri/renderD128", 0, &kind, &ma, &mi, &mode) == 0);
   EXPECT((kind == 1 || kind == 2) && ma == 226 && mi == 128 && mode == 0666);
+  // batch read-back: both present; a wrong minor or a missing node reads as absent
+  gm_dev_node_t probe[4] = {nodes[0], nodes[1], nodes[1], nodes[1]};
+  probe[2].minor = 200;
+  snprintf(probe[3].path, sizeof(probe[3].path), "dev/dri/renderD200");
+  uint8_t present[4] = {9, 9, 9, 9};
+  EXPECT(gm_devnodes_present(0, root, probe, 4, GM_DEV_EMULATE, present) == 2);
+  EXPECT(present[0] == 1 && present[1] == 1 && present[2] == 0 && present[3] == 0);
+  EXPECT(gm_devnodes_present(0, "/nonexistent/gm/root", probe, 1, 0, present) == -ENOENT);
   // path escape attempts are refused
   gm_dev_node_t bad = nodes[0];
   snprintf(bad.path, sizeof(bad.path), "dev/../../etc/evil");
@@ -131,6 +139,9 @@ static void test_devnodes_guard() {
   int res[2] = {9, 9};
   EXPECT(gm_devnodes_create(0, root, n, 2, GM_DEV_EMULATE, res) == 0);
   EXPECT(res[0] == 2 && res[1] == 2);
+  uint8_t present[2] = {9, 9};  // the host's /dev is not ours to provide: reads as shared
+  EXPECT(gm_devnodes_present(0, root, n, 2, GM_DEV_EMULATE, present) == 2);
+  EXPECT(present[0] == 2 && present[1] == 2);
   struct stat st;
   EXPECT(stat((dev + "/kfd").c_str(), &st) < 0 && stat((dev + "/dri").c_str(), &st) < 0);
   // nodes that exist in the host dir are never unlinked through a container sharing it
