@@ -24,9 +24,12 @@ mounts that directory for the device-plugin socket. Placeholders are looked up b
 a stale entry of a deleted pod can never match a fresh placeholder, and an inotify watch on the
 directory wakes admission waiters the moment the kubelet renames a new checkpoint in.
 
-PodResources stays the authority: it is read when the checkpoint is missing or unreadable, when
-a placeholder the apiserver already shows as admitted has no checkpoint entry (the file then
-counts as not maintained and is no longer trusted), and by the reconciler and ``/audit``.
+PodResources stays the authority. The checkpoint serves admission and non-authoritative ledger
+views (``/audit``, leases). PodResources serves the reconciler, rollbacks and worker start-up,
+and every one of those reads is compared with the checkpoint pod by pod. The checkpoint is no
+longer trusted after three reads in a row disagree, or after three placeholders in a row that
+the apiserver shows as admitted have no entry in it. PodResources is also read whenever the
+file is missing or unreadable.
 """
 from __future__ import annotations
 
@@ -36,7 +39,7 @@ import ctypes.util
 import json
 import os
 import struct
-from typing import Callable, Dict, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 from gpumounter_amd.utils import log
 
@@ -113,6 +116,8 @@ class DeviceCheckpoint:
     :meth:`lookup` stats the file on every call and parses it again only when it changed
     (inode, size, mtime), so a read costs one ``stat`` in the steady state."""
 
+    CHECKPOINT_MISSES = 3
+
     def __init__(self, path: str, resource: str) -> None:
         self.path = path
         self.resource = resource
@@ -121,6 +126,7 @@ class DeviceCheckpoint:
         self.parses = 0
         self.errors = 0
         self.trusted = True          # cleared when the kubelet is seen not to maintain it
+        self.mismatches = 0
         self._fd = -1
         self._loop = None
 
@@ -156,6 +162,46 @@ class DeviceCheckpoint:
         if snap is None:
             return None
         return snap.get(uid) or None
+
+    def by_name(self, pods) -> Optional[Dict[Tuple[str, str], List[str]]]:
+        """The ledger keyed like a PodResources List — (namespace, name) → IDs — for the given
+        pod objects (the informers' caches); None when the checkpoint cannot be used."""
+        if not self.trusted:
+            return None
+        snap = self.snapshot()
+        if snap is None:
+            return None
+        out: Dict[Tuple[str, str], List[str]] = {}
+        for p in pods:
+            md = p["metadata"]
+            ids = snap.get(md.get("uid", ""))
+            if ids:
+                out[(md["namespace"], md["name"])] = list(ids)
+        return out
+
+    def cross_check(self, listed: Dict[Tuple[str, str], List[str]],
+                    uid_of: Callable[[Tuple[str, str]], Optional[str]]) -> bool:
+        """Compare an authoritative PodResources view with the checkpoint, pod by pod (for the
+        pods whose UID is known). ``CHECKPOINT_MISSES`` disagreeing reads in a row distrust
+        it — a single one can be the microseconds between the kubelet's in-memory update and
+        its rename. Returns whether this read agreed."""
+        if not self.trusted:
+            return False
+        snap = self.snapshot()
+        bad = snap is None and bool(listed)
+        for key, ids in listed.items():
+            if bad:
+                break
+            uid = uid_of(key)
+            if uid and sorted(snap.get(uid, ())) != sorted(ids):
+                bad = True
+        if not bad:
+            self.mismatches = 0
+            return True
+        self.mismatches += 1
+        if self.mismatches >= self.CHECKPOINT_MISSES:
+            self.distrust(f"{self.mismatches} PodResources reads in a row disagreed with it")
+        return False
 
     def distrust(self, why: str) -> None:
         if self.trusted:

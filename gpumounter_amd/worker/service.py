@@ -107,6 +107,7 @@ class GpuMountService:
         self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}
         self._own: Dict[str, Tuple[str, ...]] = {}   # pod uid → its own device-plugin GPU IDs
         self.ledger_reads = 0
+        self.ledger_reads_checkpoint = 0
 
     # ------------------------------------------------------------------------ helpers
     def pod_lock(self, ns: str, name: str) -> asyncio.Lock:
@@ -131,15 +132,35 @@ class GpuMountService:
         except NotFound:
             return None
 
-    async def _read_ledger(self) -> Dict[Tuple[str, str], List[str]]:
+    def _uid_of(self, key: Tuple[str, str]) -> Optional[str]:
+        p = self.node_pods.cache.get(key) or self.ph.informer.cache.get(key)
+        return podu.uid_of(p) if p else None
+
+    async def _read_ledger(self, authoritative: bool = True, pods: Sequence[dict] = ()
+                           ) -> Dict[Tuple[str, str], List[str]]:
+        """The node's allocations by (namespace, pod). Non-authoritative reads come from the
+        kubelet's device-manager checkpoint when it is in use (no RPC against the rate-limited
+        PodResources server); authoritative ones List PodResources and cross-check the
+        checkpoint with the answer, so a checkpoint that drifts stops being used."""
+        ck = self.ph.checkpoint
+        if not authoritative and ck is not None:
+            # ``pods``: the ones the caller asks about, which the caches may not hold yet
+            led = ck.by_name(list(pods) + list(self.node_pods.cache.values()) +
+                             list(self.ph.informer.cache.values()))
+            if led is not None:
+                self.ledger_reads_checkpoint += 1
+                self.ph.last_ledger = led
+                return led
         self.ledger_reads += 1
         led = await self.ledger.by_pod()
         self.ph.last_ledger = led
+        if ck is not None:
+            ck.cross_check(led, self._uid_of)
         return led
 
     async def pod_state(self, pod: dict, fresh: bool = False,
-                        ledger_snapshot: Optional[Dict[Tuple[str, str], List[str]]] = None
-                        ) -> PodGpuState:
+                        ledger_snapshot: Optional[Dict[Tuple[str, str], List[str]]] = None,
+                        authoritative: bool = False) -> PodGpuState:
         """The pod's GPUs from the ledger's point of view.
 
         Device-plugin allocations never change during a pod's lifetime, so the device IDs of an
@@ -156,7 +177,7 @@ class GpuMountService:
             try:
                 self.faults.check("ledger_read")
                 if ledger is None:
-                    ledger = await self._read_ledger()
+                    ledger = await self._read_ledger(authoritative, [pod, *owned])
             except (LedgerError, InjectedFault) as e:
                 _log.error("ledger read failed: %s", e)
                 st.mount_type = MountType.UNKNOWN
@@ -207,7 +228,8 @@ class GpuMountService:
         Used after any failed attach/detach so a request either fully happens or leaves the pod
         exactly as the ledger describes it, and by the reconciler loop. Returns the issues fixed.
         """
-        st = await self.pod_state(pod, fresh=True, ledger_snapshot=ledger_snapshot)
+        st = await self.pod_state(pod, fresh=True, ledger_snapshot=ledger_snapshot,
+                                  authoritative=True)
         if st.mount_type == MountType.UNKNOWN:
             raise LedgerError("ledger unavailable")
         issues = self.hm.audit(pod, st.hot, st.own)

@@ -86,3 +86,20 @@ def test_inotify_wakes_on_the_kubelets_rename(tmp_path):
     assert asyncio.run(body()) == ("g",)
     assert not ckpt.DeviceCheckpoint(str(tmp_path / "nodir" / "x"), "r").watch(lambda: None)
     assert os.path.exists(path)
+
+
+def test_cross_check_distrusts_after_consecutive_disagreements(tmp_path):
+    path = str(tmp_path / ckpt.CHECKPOINT_NAME)
+    ckpt.write_atomic(path, ckpt.render([("u1", "c", "amd.com/gpu", {0: ["a"]})]))
+    r = ckpt.DeviceCheckpoint(path, "amd.com/gpu")
+    uids = {("ns", "p1"): "u1", ("ns", "p2"): "u2"}
+    assert r.cross_check({("ns", "p1"): ["a"]}, uids.get)
+    assert r.cross_check({("ns", "p1"): ["a"], ("ns", "x"): ["b"]}, uids.get)  # unknown uid
+    assert r.by_name([{"metadata": {"namespace": "ns", "name": "p1", "uid": "u1"}},
+                      {"metadata": {"namespace": "ns", "name": "p2", "uid": "u2"}}]) == \
+        {("ns", "p1"): ["a"]}
+    assert not r.cross_check({("ns", "p2"): ["b"]}, uids.get)                  # 1st miss
+    assert r.cross_check({("ns", "p1"): ["a"]}, uids.get) and r.mismatches == 0  # reset
+    for _ in range(3):
+        assert not r.cross_check({("ns", "p1"): ["z"]}, uids.get)
+    assert not r.trusted and r.by_name([]) is None and r.lookup("u1") is None
