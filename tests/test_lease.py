@@ -47,9 +47,13 @@ def test_lease_detaches_on_time_and_only_the_leased_gpus():
             return [g.uuid for g in st.hot] == [keep["devices"][0]["uuid"]]
         assert await until(back_to_one)
         assert await lc.audit("default", "t") == []
-        await svc.notify.drain()
-        evs = [e for e in lc.cluster.events_for("default", "t")
-               if e["reason"] == "GPULeaseExpired"]
+
+        async def expired_events():   # emitted once remove_gpu has returned to the lease
+            await svc.notify.drain()
+            return [e for e in lc.cluster.events_for("default", "t")
+                    if e["reason"] == "GPULeaseExpired"]
+        assert await until(expired_events)
+        evs = await expired_events()
         assert evs and "2 GPU(s) detached" in evs[0]["message"] and evs[0]["type"] == "Normal"
         assert svc.lease.expired == 1
     run(body)
@@ -67,11 +71,12 @@ def test_bad_lease_values_are_rejected():
 def test_expired_lease_on_a_busy_gpu_is_kept_unless_forced(tmp_path):
     sleeper = subprocess.Popen(["sleep", "60"])
     procs = tmp_path / "procs"
-    _native.mock_smi().gm_mock_set_procs_file(str(procs).encode())
     try:
         async def body(lc):
+            # after the cluster's inventory ran amdsmi_init, which resets the mock's settings
+            _native.mock_smi().gm_mock_set_procs_file(str(procs).encode())
             lc.tenant("busy", pids={"main": [sleeper.pid]})
-            code, b = await lease_add(lc, "default", "busy", 1, 0.2)
+            code, b = await lease_add(lc, "default", "busy", 1, 1.0)   # > procs write under load
             assert code == 200
             procs.write_text(f"{b['devices'][0]['index']} {sleeper.pid} 4096 python\n")
             svc = lc.nodes["node-0"].worker.service
