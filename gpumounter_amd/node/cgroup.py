@@ -431,6 +431,7 @@ class V2RecordingBackend(DeviceRuleBackend):
 
     def apply(self, cgdir, grant, revoke, desired):
         path = os.path.join(cgdir, BPF_STATE)
+        self._installed.pop(cgdir, None)
         if not desired:
             if os.path.exists(path):
                 os.unlink(path)
@@ -442,10 +443,31 @@ class V2RecordingBackend(DeviceRuleBackend):
         with open(tmp, "w") as fh:
             json.dump(state, fh)
         os.replace(tmp, path)  # atomic like BPF_F_REPLACE
+        # the recorded file stands in for the attached program: its identity plays the role of
+        # the program id in V2BpfBackend's fast path
+        try:
+            st = os.stat(path)
+            self._installed[cgdir] = ((st.st_ino, st.st_mtime_ns, st.st_size),
+                                      frozenset((n.major, n.minor) for n in desired))
+        except OSError:
+            self._installed.pop(cgdir, None)
+
+    def __init__(self) -> None:
+        self._installed: Dict[str, Tuple[tuple, FrozenSet[Tuple[int, int]]]] = {}
 
     def allowed(self, cgdir):
+        path = os.path.join(cgdir, BPF_STATE)
+        known = self._installed.get(cgdir)
+        if known is not None:
+            try:
+                st = os.stat(path)
+                if (st.st_ino, st.st_mtime_ns, st.st_size) == known[0]:
+                    return set(known[1])
+            except OSError:
+                pass
+            self._installed.pop(cgdir, None)
         try:
-            with open(os.path.join(cgdir, BPF_STATE)) as fh:
+            with open(path) as fh:
                 st = json.load(fh)
         except FileNotFoundError:
             return set()

@@ -155,6 +155,16 @@ class Reconciler:
         except Exception as e:  # noqa: BLE001
             rep.errors.append(f"lease sweep: {e}")
         m = svc.metrics
+        # One authoritative PodResources read per sweep. It cross-checks the device-manager
+        # checkpoint, and while that stays trusted every owner is audited from it (re-read
+        # under the owner's lock, no RPC). That is O(1) kubelet calls per sweep instead of one
+        # per owner.
+        try:
+            await svc._read_ledger(authoritative=True)  # noqa: SLF001
+        except Exception as e:  # noqa: BLE001
+            rep.errors.append(f"ledger: {e}")
+        ck = svc.ph.checkpoint
+        from_ckpt = ck is not None and ck.trusted and ck.snapshot() is not None
         placeholders = svc.ph.live()
         by_owner: Dict[tuple, List[dict]] = {}
         for p in placeholders:
@@ -210,7 +220,7 @@ class Reconciler:
                 if podu.phase_of(owner) != "Running":
                     continue
                 try:
-                    fixed = await svc.reconcile_pod(owner)
+                    fixed = await svc.reconcile_pod(owner, authoritative=not from_ckpt)
                 except Exception as e:  # noqa: BLE001
                     if gone(await fresh(ons, oname), ouid):   # the cache lagged a delete
                         await collect(ons, oname, phs)

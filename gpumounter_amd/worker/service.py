@@ -221,15 +221,17 @@ class GpuMountService:
         return st
 
     async def reconcile_pod(self, pod: dict,
-                            ledger_snapshot: Optional[Dict[Tuple[str, str], List[str]]] = None
-                            ) -> List:
+                            ledger_snapshot: Optional[Dict[Tuple[str, str], List[str]]] = None,
+                            authoritative: bool = True) -> List:
         """Make the pod's cgroup rules and /dev nodes equal its (fresh) ledger view.
 
         Used after any failed attach/detach so a request either fully happens or leaves the pod
         exactly as the ledger describes it, and by the reconciler loop. Returns the issues fixed.
+        ``authoritative=False`` (the reconciler, once its sweep has cross-checked the checkpoint
+        against PodResources) reads the ledger from the device-manager checkpoint.
         """
         st = await self.pod_state(pod, fresh=True, ledger_snapshot=ledger_snapshot,
-                                  authoritative=True)
+                                  authoritative=authoritative)
         if st.mount_type == MountType.UNKNOWN:
             raise LedgerError("ledger unavailable")
         issues = self.hm.audit(pod, st.hot, st.own)

@@ -371,7 +371,8 @@ def test_reconciler_collects_placeholders_of_deleted_owner():
         assert len(rep.owner_gone) == 2
         await asyncio.sleep(0.05)
         assert lc.cluster.placeholders() == [] and node_of(lc).allocated == {}
-    run(body)
+    # the periodic sweep itself (the DELETED event would otherwise release them first)
+    run(body, worker_overrides={"reconcile_on_events": False})
 
 
 def test_reconciler_reinjects_after_container_restart():
@@ -794,6 +795,23 @@ def test_attach_reads_the_device_manager_checkpoint_not_the_podresources_socket(
         ckpt.write_atomic(h.node.checkpoint_path, ckpt.render([]))
         assert ph.checkpoint.lookup("anything") is None            # distrusted for good
         assert await lc.audit("default", "t") == []
+    run(body)
+
+
+def test_reconciler_sweep_makes_one_podresources_call_for_any_number_of_owners():
+    """One authoritative List per sweep cross-checks the checkpoint; every owner is then
+    audited from the checkpoint under its lock (the reference's pattern would be a kubelet
+    dial per query: collector.go:90-138)."""
+    async def body(lc):
+        for i in range(4):
+            lc.tenant(f"o{i}")
+            assert (await lc.add("default", f"o{i}", 1))[0] == 200
+        h = lc.nodes["node-0"]
+        before = h.kubelet.calls["List"] + h.kubelet.calls["Get"]
+        rep = await h.worker.reconciler.run_once()
+        assert not rep.errors and not rep.repaired and not rep.revoked
+        assert h.kubelet.calls["List"] + h.kubelet.calls["Get"] - before == 1
+        assert h.worker.placeholders.checkpoint.trusted
     run(body)
 
 
