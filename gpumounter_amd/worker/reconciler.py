@@ -160,7 +160,7 @@ class Reconciler:
         # under the owner's lock, no RPC). That is O(1) kubelet calls per sweep instead of one
         # per owner.
         try:
-            await svc._read_ledger(authoritative=True)  # noqa: SLF001
+            await svc.read_ledger(authoritative=True)
         except Exception as e:  # noqa: BLE001
             rep.errors.append(f"ledger: {e}")
         ck = svc.ph.checkpoint

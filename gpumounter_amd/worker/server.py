@@ -167,7 +167,7 @@ class Worker:
         await self.node_informer.start()
         # warm the ledger channel (fails fast if the kubelet socket is wrong); the authoritative
         # read also cross-checks the device-manager checkpoint before admission relies on it
-        await self.service._read_ledger(authoritative=True)  # noqa: SLF001
+        await self.service.read_ledger(authoritative=True)
         if self.checkpoint is not None:
             watched = self.checkpoint.watch(
                 lambda: asyncio.ensure_future(self.ph_informer.poke()))

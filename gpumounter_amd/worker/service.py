@@ -136,7 +136,7 @@ class GpuMountService:
         p = self.node_pods.cache.get(key) or self.ph.informer.cache.get(key)
         return podu.uid_of(p) if p else None
 
-    async def _read_ledger(self, authoritative: bool = True, pods: Sequence[dict] = ()
+    async def read_ledger(self, authoritative: bool = True, pods: Sequence[dict] = ()
                            ) -> Dict[Tuple[str, str], List[str]]:
         """The node's allocations by (namespace, pod). Non-authoritative reads come from the
         kubelet's device-manager checkpoint when it is in use (no RPC against the rate-limited
@@ -177,7 +177,7 @@ class GpuMountService:
             try:
                 self.faults.check("ledger_read")
                 if ledger is None:
-                    ledger = await self._read_ledger(authoritative, [pod, *owned])
+                    ledger = await self.read_ledger(authoritative, [pod, *owned])
             except (LedgerError, InjectedFault) as e:
                 _log.error("ledger read failed: %s", e)
                 st.mount_type = MountType.UNKNOWN
