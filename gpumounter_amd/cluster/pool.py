@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import asyncio
 import secrets
+import time
 from typing import Dict, List, Optional, Sequence
 
 from gpumounter_amd.cluster.kube import NotFound
@@ -44,6 +45,8 @@ def is_standby(p: dict) -> bool:
 
 
 class WarmPool:
+    ALLOCATABLE_TTL_S = 30.0
+
     def __init__(self, cfg, ph: PlaceholderManager, inv, metrics=None) -> None:
         self.cfg = cfg
         self.ph = ph
@@ -55,6 +58,7 @@ class WarmPool:
         self._refill_task: Optional[asyncio.Task] = None
         self._wake: Optional[asyncio.Event] = None
         self.exhausted = False               # last refill hit InsufficientGPU
+        self._alloc_cache: Optional[tuple] = None   # (monotonic time, allocatable IDs)
 
     @property
     def enabled(self) -> bool:
@@ -134,11 +138,23 @@ class WarmPool:
         missing = self.target - len(self.standby()) - self.pending()
         if missing <= 0:
             return 0
-        # only ask for what the node can actually admit (allocatable − allocated)
-        led = await self.ph.ledger.by_pod()
-        self.ph.last_ledger = led
-        allocated = {normalize_device_id(d) for ids in led.values() for d in ids}
-        alloc = await self.ph.ledger.allocatable()
+        # only ask for what the node can actually admit (allocatable − allocated). Allocated
+        # comes from the device-manager checkpoint when it is in use (a terminated pod's entry
+        # can linger there until the kubelet's next Allocate: that only under-fills the pool),
+        # else from PodResources; the allocatable set changes only with the plugin's device
+        # list and is re-read every ALLOCATABLE_TTL_S
+        ck = self.ph.checkpoint
+        snap = ck.snapshot() if ck is not None and ck.trusted else None
+        if snap is not None:
+            allocated = {normalize_device_id(d) for ids in snap.values() for d in ids}
+        else:
+            led = await self.ph.ledger.by_pod()
+            self.ph.last_ledger = led
+            allocated = {normalize_device_id(d) for ids in led.values() for d in ids}
+        now = time.monotonic()
+        if self._alloc_cache is None or now - self._alloc_cache[0] > self.ALLOCATABLE_TTL_S:
+            self._alloc_cache = (now, await self.ph.ledger.allocatable())
+        alloc = self._alloc_cache[1]
         if alloc is None:
             alloc = [g.bdf for g in self.inv.gpus()]
         free = sum(1 for d in alloc if normalize_device_id(d) not in allocated)
