@@ -439,38 +439,31 @@ class V2RecordingBackend(DeviceRuleBackend):
         prog = build_program(desired, chained=True)
         state = {"rules": [[n.major, n.minor, n.path] for n in desired],
                  "chained": "runtime-default", "insns": [f"{i:016x}" for i in prog]}
+        blob = json.dumps(state).encode()
         tmp = path + ".tmp"
-        with open(tmp, "w") as fh:
-            json.dump(state, fh)
+        with open(tmp, "wb") as fh:
+            fh.write(blob)
         os.replace(tmp, path)  # atomic like BPF_F_REPLACE
-        # the recorded file stands in for the attached program: its identity plays the role of
-        # the program id in V2BpfBackend's fast path
-        try:
-            st = os.stat(path)
-            self._installed[cgdir] = ((st.st_ino, st.st_mtime_ns, st.st_size),
-                                      frozenset((n.major, n.minor) for n in desired))
-        except OSError:
-            self._installed.pop(cgdir, None)
+        # the recorded file stands in for the attached program, and its exact bytes play the
+        # role of the program id in V2BpfBackend's fast path (stat metadata would not do: the
+        # rename reuses inode numbers and rewrites within one tick share an mtime)
+        self._installed[cgdir] = (blob, frozenset((n.major, n.minor) for n in desired))
 
     def __init__(self) -> None:
-        self._installed: Dict[str, Tuple[tuple, FrozenSet[Tuple[int, int]]]] = {}
+        self._installed: Dict[str, Tuple[bytes, FrozenSet[Tuple[int, int]]]] = {}
 
     def allowed(self, cgdir):
         path = os.path.join(cgdir, BPF_STATE)
-        known = self._installed.get(cgdir)
-        if known is not None:
-            try:
-                st = os.stat(path)
-                if (st.st_ino, st.st_mtime_ns, st.st_size) == known[0]:
-                    return set(known[1])
-            except OSError:
-                pass
-            self._installed.pop(cgdir, None)
         try:
-            with open(path) as fh:
-                st = json.load(fh)
+            with open(path, "rb") as fh:
+                blob = fh.read()
         except FileNotFoundError:
+            self._installed.pop(cgdir, None)
             return set()
+        known = self._installed.get(cgdir)
+        if known is not None and known[0] == blob:
+            return set(known[1])
+        st = json.loads(blob)
         # evaluate the recorded program itself (same check the real backend runs on xlated code)
         return program_allows([int(x, 16) for x in st["insns"]])
 

@@ -113,15 +113,15 @@ def write_atomic(path: str, blob: bytes) -> None:
 class DeviceCheckpoint:
     """Reader of the device-manager checkpoint with an inotify wake-up.
 
-    :meth:`lookup` stats the file on every call and parses it again only when it changed
-    (inode, size, mtime), so a read costs one ``stat`` in the steady state."""
+    :meth:`lookup` reads the file on every call and parses it again only when its bytes
+    changed, so a read costs one small ``read`` in the steady state."""
 
     CHECKPOINT_MISSES = 3
 
     def __init__(self, path: str, resource: str) -> None:
         self.path = path
         self.resource = resource
-        self._key: Optional[tuple] = None
+        self._blob: Optional[bytes] = None
         self._by_uid: Dict[str, Tuple[str, ...]] = {}
         self.parses = 0
         self.errors = 0
@@ -132,25 +132,28 @@ class DeviceCheckpoint:
 
     # ------------------------------------------------------------------------ reads
     def snapshot(self) -> Optional[Dict[str, Tuple[str, ...]]]:
-        """uid → IDs, or None if the file is absent or unreadable."""
+        """uid → IDs, or None if the file is absent or unreadable.
+
+        The file is read on every call and parsed again only when its bytes changed. Stat
+        metadata cannot stand in for the content: the kubelet's tmp-and-rename reuses the inode
+        number just freed, two rewrites within one timestamp tick share an mtime, and a rewrite
+        that swaps one UID for another keeps the size."""
         try:
-            st = os.stat(self.path)
+            with open(self.path, "rb") as fh:
+                blob = fh.read()
         except OSError:
-            self._key = None
+            self._blob = None
             return None
-        key = (st.st_ino, st.st_size, st.st_mtime_ns)
-        if key != self._key:
+        if blob != self._blob:
             try:
-                with open(self.path, "rb") as fh:
-                    blob = fh.read()
                 self._by_uid = parse(blob, self.resource)
-            except (OSError, CheckpointFormatError) as e:
+            except CheckpointFormatError as e:
                 self.errors += 1
                 if self.errors == 1 or self.errors % 100 == 0:
                     _log.warning("device-manager checkpoint %s unreadable: %s", self.path, e)
-                self._key = None
+                self._blob = None
                 return None
-            self._key = key
+            self._blob = blob
             self.parses += 1
         return self._by_uid
 

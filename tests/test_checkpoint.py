@@ -55,7 +55,7 @@ def test_reader_parses_only_when_the_file_changes(tmp_path):
     assert r.lookup("u1")[0] == "0000:05:00.0" and r.parses == 1
     for _ in range(5):
         assert r.lookup("u2") is None
-    assert r.parses == 1                                        # stat-only while unchanged
+    assert r.parses == 1                                        # no re-parse while unchanged
     ckpt.write_atomic(path, ckpt.render([("u2", "c", "amd.com/gpu", {0: ["x"]})]))
     assert r.lookup("u2") == ("x",) and r.lookup("u1") is None and r.parses == 2
     with open(path, "wb") as fh:
@@ -103,3 +103,18 @@ def test_cross_check_distrusts_after_consecutive_disagreements(tmp_path):
     for _ in range(3):
         assert not r.cross_check({("ns", "p1"): ["z"]}, uids.get)
     assert not r.trusted and r.by_name([]) is None and r.lookup("u1") is None
+
+
+def test_same_size_rewrite_in_the_same_tick_is_seen(tmp_path):
+    """The kubelet's tmp + rename reuses the inode just freed and two rewrites inside one
+    timestamp tick share an mtime: a swap of one UID for another of the same length must still
+    be seen (stat metadata cannot key the cache)."""
+    path = str(tmp_path / ckpt.CHECKPOINT_NAME)
+    r = ckpt.DeviceCheckpoint(path, "amd.com/gpu")
+    ckpt.write_atomic(path, ckpt.render([("uid-a", "c", "amd.com/gpu", {0: ["g0"]})]))
+    st = os.stat(path)
+    assert r.lookup("uid-a") == ("g0",)
+    ckpt.write_atomic(path, ckpt.render([("uid-b", "c", "amd.com/gpu", {0: ["g0"]})]))
+    os.utime(path, ns=(st.st_atime_ns, st.st_mtime_ns))        # same tick
+    assert os.stat(path).st_size == st.st_size
+    assert r.lookup("uid-b") == ("g0",) and r.lookup("uid-a") is None
