@@ -126,9 +126,9 @@ class BpfTiming(C.Structure):
                 ("insns", C.c_uint32)]
 
 
-HOST_ABI_VERSION = 3          # native/include/gm_host.h GM_HOST_ABI_VERSION
+HOST_ABI_VERSION = 4          # native/include/gm_host.h GM_HOST_ABI_VERSION
 GM_ACC_MKNOD, GM_ACC_READ, GM_ACC_WRITE = 1, 2, 4
-GM_DEV_EMULATE, GM_DEV_VIA_SETNS, GM_DEV_REPLACE = 1, 2, 4
+GM_DEV_EMULATE, GM_DEV_VIA_SETNS, GM_DEV_REPLACE, GM_DEV_BIND = 1, 2, 4, 8
 
 
 def host() -> C.CDLL:
@@ -163,6 +163,7 @@ def host() -> C.CDLL:
                                            C.c_int, C.POINTER(C.c_int)]
         lib.gm_devnodes_remove.argtypes = lib.gm_devnodes_create.argtypes
         lib.gm_devnodes_guard.argtypes = [C.c_char_p]
+        lib.gm_devnodes_stage.argtypes = [C.c_char_p, C.c_int]
         lib.gm_devnode_stat.argtypes = [C.c_int, C.c_char_p, C.c_char_p, C.c_int,
                                         C.POINTER(C.c_int), C.POINTER(C.c_uint32),
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]

@@ -7,6 +7,14 @@ C call handles every node of an attach: it resolves the container root through
 ``/proc/<pid>/root`` (or a setns helper thread, or — hermetic mode — a per-container directory),
 walks ``dev/dri`` with ``O_NOFOLLOW`` (a hostile container cannot redirect the write with a
 symlink), ``mknodat``s with an exact mode, and is idempotent.
+
+Containers in their own user namespace (Kubernetes ``hostUsers: false``) cannot use such nodes:
+their ``/dev`` is a tmpfs mounted inside that namespace, which the kernel treats as ``nodev``, so
+an mknod'ed node there exists (and passes a naive read-back) but every ``open`` fails with EACCES.
+The reference's ``mknod`` has the same defect. For those containers the writer switches to bind
+mode (``GM_DEV_BIND``): the node is made once in a staging tmpfs the worker mounts itself, cloned
+with ``open_tree`` and ``move_mount``ed over an empty placeholder in the container, owned by the
+container's root as mapped through its ``uid_map``; the read-back then requires the mount.
 """
 from __future__ import annotations
 
@@ -47,8 +55,14 @@ class DevNodeWriter:
     The guard is process-wide in the native layer (the last writer constructed sets or clears
     it; a worker process has exactly one)."""
 
-    def __init__(self, mode: str = "procroot", host_dev: str = "") -> None:
+    def __init__(self, mode: str = "procroot", host_dev: str = "", userns: str = "auto",
+                 stage_dir: str = "", proc_root: str = "/proc") -> None:
         self.mode = mode
+        self.userns = userns            # auto | bind | off (see _bind)
+        self.stage_dir = stage_dir
+        self.proc_root = proc_root
+        self._staged = False
+        self._own_userns = self._userns_id("self")
         self.flags = 0
         if mode == "setns":
             self.flags |= _native.GM_DEV_VIA_SETNS
@@ -63,7 +77,7 @@ class DevNodeWriter:
         self.guarded = max(rc, 0)
 
     @staticmethod
-    def _array(nodes: Sequence[DeviceNode]):
+    def _array(nodes: Sequence[DeviceNode], owner: Tuple[int, int] = (-1, -1)):
         arr = (_native.DevNode * max(len(nodes), 1))()
         for i, n in enumerate(nodes):
             rel = n.path.lstrip("/").encode()
@@ -73,9 +87,64 @@ class DevNodeWriter:
             arr[i].major = n.major
             arr[i].minor = n.minor
             arr[i].mode = n.mode
-            arr[i].uid = -1
-            arr[i].gid = -1
+            arr[i].uid, arr[i].gid = owner
         return arr
+
+    # ------------------------------------------------------------------ user-namespaced targets
+    def _userns_id(self, pid) -> Optional[Tuple[int, int]]:
+        try:
+            st = os.stat(f"{self.proc_root}/{pid}/ns/user")
+        except OSError:
+            return None
+        return st.st_dev, st.st_ino
+
+    def _bind(self, t: Target) -> bool:
+        """Bind mode for this target? ``bind``: always; ``off``: never; ``auto``: when the
+        container's process lives in a user namespace other than the worker's."""
+        if self.userns == "bind":
+            return True
+        if self.userns != "auto" or self.mode == "emulate" or t.root or t.pid <= 0:
+            return False
+        theirs = self._userns_id(t.pid)
+        return theirs is not None and self._own_userns is not None and theirs != self._own_userns
+
+    def _mapped_root(self, t: Target) -> Tuple[int, int]:
+        """Host uid/gid of the container's root (its uid_map/gid_map entry for id 0), so the
+        bind-mounted nodes show up as root-owned inside; (-1, -1) = leave as created."""
+        if t.pid <= 0:
+            return -1, -1
+        out = []
+        for f in ("uid_map", "gid_map"):
+            host = -1
+            try:
+                with open(f"{self.proc_root}/{t.pid}/{f}") as fh:
+                    for line in fh:
+                        parts = line.split()
+                        if len(parts) == 3 and int(parts[0]) == 0:
+                            host = int(parts[1])
+                            break
+            except (OSError, ValueError):
+                pass
+            out.append(host)
+        return out[0], out[1]
+
+    def _ensure_stage(self) -> None:
+        if self._staged:
+            return
+        if not self.stage_dir:
+            raise DevNodeError("bind-mode device nodes need a staging directory "
+                               "(devnode_stage_dir)")
+        rc = _native.host().gm_devnodes_stage(self.stage_dir.encode(), 1)
+        if rc < 0:
+            raise DevNodeError(f"staging tmpfs at {self.stage_dir}: {os.strerror(-rc)}")
+        self._staged = True
+
+    def _call(self, t: Target):
+        """(flags, owner) for one target; sets up the staging tmpfs on first bind."""
+        if not self._bind(t):
+            return self.flags, (-1, -1)
+        self._ensure_stage()
+        return self.flags | _native.GM_DEV_BIND, self._mapped_root(t)
 
     def _target_args(self, t: Target) -> Tuple[int, Optional[bytes]]:
         if t.root:
@@ -89,23 +158,39 @@ class DevNodeWriter:
         if not nodes:
             return []
         pid, root = self._target_args(t)
+        flags, owner = self._call(t)
         res = (C.c_int * len(nodes))()
-        fails = _native.host().gm_devnodes_create(pid, root, self._array(nodes), len(nodes),
-                                                  self.flags, res)
+        fails = _native.host().gm_devnodes_create(pid, root, self._array(nodes, owner),
+                                                  len(nodes), flags, res)
         results = [int(res[i]) for i in range(len(nodes))]
         if fails:
             bad = [(n.path, os.strerror(-r)) for n, r in zip(nodes, results) if r < 0]
-            raise DevNodeError(f"mknod failed: {bad}", results)
+            what = "bind mount" if flags & _native.GM_DEV_BIND else "mknod"
+            raise DevNodeError(f"{what} failed: {bad}", results)
         return results
 
     def remove(self, t: Target, nodes: Sequence[DeviceNode]) -> List[int]:
         if not nodes:
             return []
         pid, root = self._target_args(t)
+        flags, _ = self._call(t)
         res = (C.c_int * len(nodes))()
         fails = _native.host().gm_devnodes_remove(pid, root, self._array(nodes), len(nodes),
-                                                  self.flags, res)
+                                                  flags, res)
         results = [int(res[i]) for i in range(len(nodes))]
+        if fails and not flags & _native.GM_DEV_BIND and \
+                any(r == -errno.EBUSY for r in results) and self.mode != "emulate":
+            # a bind-mounted node (attached while the container was handled in bind mode):
+            # unmount those through the container's mount namespace
+            busy = [i for i, r in enumerate(results) if r == -errno.EBUSY]
+            self._ensure_stage()
+            sub = [nodes[i] for i in busy]
+            res2 = (C.c_int * len(sub))()
+            _native.host().gm_devnodes_remove(pid, root, self._array(sub), len(sub),
+                                              flags | _native.GM_DEV_BIND, res2)
+            for k, i in enumerate(busy):
+                results[i] = int(res2[k])
+            fails = sum(1 for r in results if r < 0)
         if fails:
             # ESRCH/ENOENT on the root means the container is gone: nothing left to remove
             if all(r in (-errno.ESRCH, -errno.ENOENT) for r in results if r < 0):
@@ -121,7 +206,8 @@ class DevNodeWriter:
         """(kind, major, minor, mode): kind 0 absent, 1 char device, 2 marker, 3 other."""
         pid, root = self._target_args(t)
         kind, ma, mi, mode = C.c_int(0), C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
-        rc = _native.host().gm_devnode_stat(pid, root, path.lstrip("/").encode(), self.flags,
+        rc = _native.host().gm_devnode_stat(pid, root, path.lstrip("/").encode(),
+                                            self._call(t)[0],
                                             C.byref(kind), C.byref(ma), C.byref(mi),
                                             C.byref(mode))
         if rc < 0:
@@ -141,7 +227,7 @@ class DevNodeWriter:
         pid, root = self._target_args(t)
         out = (C.c_uint8 * len(nodes))()
         rc = _native.host().gm_devnodes_present(pid, root, self._array(nodes), len(nodes),
-                                                self.flags, out)
+                                                self._call(t)[0], out)
         if rc < 0:
             raise DevNodeError(f"read-back of {len(nodes)} nodes: {os.strerror(-rc)}")
         return [bool(out[i]) for i in range(len(nodes))]

@@ -75,6 +75,11 @@ class Config:
     systemd_bus: str = ""              # "" = /run/systemd/private, then the system bus socket
     bpf_pin_dir: str = "/sys/fs/bpf/gpumounter"  # bpffs dir for v2 tail-call maps ("" = keep fd)
     devnode_mode: str = "procroot"     # procroot | setns | emulate
+    # containers in their own user namespace (hostUsers: false) get bind-mounted nodes, because
+    # mknod'ed ones on their nodev /dev cannot be opened: auto (detect per container) | bind
+    # (every container) | off (always mknod)
+    devnode_userns: str = "auto"
+    devnode_stage_dir: str = "/run/gpumounter/devstage"  # worker-private tmpfs for bind mode
     proc_root: str = "/proc"
     # For hermetic runs: containers' rootfs live at <container_root_prefix>/<container-id>/ and
     # device-node writes go there instead of /proc/<pid>/root.
@@ -215,6 +220,7 @@ class Config:
         _choice("quota_mode", self.quota_mode, ("enforce", "off"))
         _choice("ecc_policy", self.ecc_policy, ("new", "any", "off"))
         _choice("devnode_mode", self.devnode_mode, ("procroot", "setns", "emulate"))
+        _choice("devnode_userns", self.devnode_userns, ("auto", "bind", "off"))
         _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
         _choice("placement_enforce", self.placement_enforce, ("hint", "trim"))
         _choice("busy_detection", self.busy_detection, ("auto", "both"))

@@ -70,7 +70,8 @@ class Worker:
             sd_mode = "off"          # hermetic runs never talk to the host's systemd by accident
         self.backend = systemd.maybe_wrap(self.backend, sd_mode, cfg.systemd_bus,
                                           self.resolver.driver)
-        self.writer = DevNodeWriter(cfg.devnode_mode, cfg.host_dev_path)
+        self.writer = DevNodeWriter(cfg.devnode_mode, cfg.host_dev_path, cfg.devnode_userns,
+                                    cfg.devnode_stage_dir, cfg.proc_root)
         self.faults = FaultInjector(cfg.fault)
         self.journal = InjectionJournal(os.path.join(cfg.state_dir, "journal")
                                         if cfg.state_dir else "")

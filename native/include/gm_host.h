@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define GM_HOST_ABI_VERSION 3
+#define GM_HOST_ABI_VERSION 4
 
 // Access bits follow BPF_DEVCG_ACC_* so the same rule feeds both cgroup versions.
 #define GM_ACC_MKNOD 1
@@ -112,12 +112,25 @@ typedef struct gm_dev_node {
 #define GM_DEV_EMULATE 1    // mknod EPERM → regular marker file "gm-chr MAJ:MIN" (unprivileged tests)
 #define GM_DEV_VIA_SETNS 2  // enter the mount namespace with a helper thread instead of /proc/pid/root
 #define GM_DEV_REPLACE 4    // replace an existing node with different major:minor
+// Bind mode, for containers in their own user namespace (Kubernetes `hostUsers: false`): their
+// /dev is a tmpfs mounted inside that namespace, so the kernel treats it as nodev and a node
+// mknod'ed there exists but cannot be opened. Instead each node is made once in the staging
+// directory (gm_devnodes_stage), cloned with open_tree(OPEN_TREE_CLONE) and attached over an
+// empty placeholder file in the container with move_mount; removal detaches the mount and
+// unlinks the placeholder. Implies the setns helper (the mount must be made from inside the
+// container's mount namespace) unless `root` is given. In bind mode a node counts as present
+// only if it is such a mount: an mknod'ed node on a nodev /dev is reported absent.
+#define GM_DEV_BIND 8
 
 // Registers the host's /dev (and its dri/) as seen from the caller, e.g. "/proc/1/root/dev". From
 // then on create/remove leave any node whose directory *is* one of them alone (result 2): a
 // container that bind-mounts the host's /dev shares the host's nodes. NULL/"" clears the guard.
 // Returns how many directories are guarded, or -errno if host_dev cannot be read.
 int gm_devnodes_guard(const char* host_dev);
+// Sets the staging directory of bind mode (process-wide). With `mount_tmpfs` a private tmpfs is
+// mounted there first (nosuid, noexec, mode 0711), so the staged nodes live on a filesystem
+// mounted in the caller's (initial) user namespace. Returns 0 or -errno. NULL/"" unsets it.
+int gm_devnodes_stage(const char* dir, int mount_tmpfs);
 // Creates nodes inside the target's root: `root` if non-NULL (test prefix), else /proc/<pid>/root.
 // results[i] = 0 created, 1 already present (idempotent), 2 directory is the host's (skipped), or
 // -errno. Returns #failures.

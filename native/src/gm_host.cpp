@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mount.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <sys/sysmacros.h>
@@ -486,9 +487,12 @@ int remove_one(int rootfd, const gm_dev_node_t& n) {
 // Runs fn(rootfd) either through /proc/<pid>/root (or a test root) or, with GM_DEV_VIA_SETNS,
 // on a helper thread that privatises its fs context and joins the target's mount namespace
 // (setns(CLONE_NEWNS) is refused for threads that share CLONE_FS, hence unshare first).
+// GM_DEV_BIND always runs on such a thread: mounts are made from inside the target namespace
+// (an explicit test root is in ours already) and unmounting changes the thread's cwd.
 template <typename F>
 int with_root(int pid, const char* root, int flags, F fn) {
-  if (!(flags & GM_DEV_VIA_SETNS) || (root && *root)) {
+  const bool explicit_root = root && *root;
+  if (!(flags & GM_DEV_BIND) && (!(flags & GM_DEV_VIA_SETNS) || explicit_root)) {
     int rfd = open_root(pid, root);
     if (rfd < 0) return rfd;
     Fd r(rfd);
@@ -498,6 +502,16 @@ int with_root(int pid, const char* root, int flags, F fn) {
   std::thread t([&]() {
     if (unshare(CLONE_FS) < 0) {
       result = -errno;
+      return;
+    }
+    if (explicit_root) {
+      int rfd = open_root(pid, root);
+      if (rfd < 0) {
+        result = rfd;
+        return;
+      }
+      Fd r(rfd);
+      result = fn(r.fd);
       return;
     }
     char p[64];
@@ -520,6 +534,149 @@ int with_root(int pid, const char* root, int flags, F fn) {
   });
   t.join();
   return result;
+}
+
+// ---- bind mode (containers in their own user namespace, see GM_DEV_BIND) -----------------------
+#ifndef OPEN_TREE_CLONE
+#define OPEN_TREE_CLONE 1
+#endif
+#ifndef MOVE_MOUNT_F_EMPTY_PATH
+#define MOVE_MOUNT_F_EMPTY_PATH 0x00000004
+#endif
+#ifndef STATX_ATTR_MOUNT_ROOT
+#define STATX_ATTR_MOUNT_ROOT 0x00002000
+#endif
+#ifndef SYS_open_tree
+#define SYS_open_tree 428
+#endif
+#ifndef SYS_move_mount
+#define SYS_move_mount 429
+#endif
+
+std::mutex g_stage_mu;
+int g_stage_fd = -1;  // O_PATH dir fd of the staging directory (in the worker's mount namespace)
+
+// 1 if dirfd/leaf is the root of a mount (a bind-mounted node), 0 if not, -errno.
+int is_mount_leaf(int dirfd, const std::string& leaf) {
+  struct statx sx;
+  if (statx(dirfd, leaf.c_str(), AT_SYMLINK_NOFOLLOW | AT_NO_AUTOMOUNT, STATX_BASIC_STATS, &sx) <
+      0)
+    return -errno;
+  if (sx.stx_attributes_mask & STATX_ATTR_MOUNT_ROOT)
+    return (sx.stx_attributes & STATX_ATTR_MOUNT_ROOT) ? 1 : 0;
+  struct stat dir;  // pre-5.8 kernels: a different filesystem than the directory's
+  if (fstat(dirfd, &dir) < 0) return -errno;
+  return makedev(sx.stx_dev_major, sx.stx_dev_minor) != dir.st_dev ? 1 : 0;
+}
+
+// A detached clone (open_tree) of the staged node for `n`, creating the staged node on first use.
+// Must run in the worker's own mount namespace, i.e. before any setns.
+int staged_tree(const gm_dev_node_t& n) {
+  std::lock_guard<std::mutex> lk(g_stage_mu);
+  if (g_stage_fd < 0) return -ENOTCONN;
+  char name[96];
+  snprintf(name, sizeof(name), "c%u_%u_%o_%d_%d", n.major, n.minor, n.mode & 07777, n.uid, n.gid);
+  struct stat st;
+  bool ok = fstatat(g_stage_fd, name, &st, AT_SYMLINK_NOFOLLOW) == 0 && S_ISCHR(st.st_mode) &&
+            st.st_rdev == makedev(n.major, n.minor) && (st.st_mode & 07777) == (n.mode & 07777);
+  if (!ok) {
+    if (unlinkat(g_stage_fd, name, 0) < 0 && errno != ENOENT) return -errno;
+    // the staging dir is an O_PATH fd: mknodat/fchmodat need a real directory fd
+    Fd dir(openat(g_stage_fd, ".", O_RDONLY | O_DIRECTORY | O_CLOEXEC));
+    if (!dir.ok()) return -errno;
+    if (mknodat(dir.fd, name, S_IFCHR | (n.mode & 07777), makedev(n.major, n.minor)) < 0)
+      return -errno;
+    if (fchmodat(dir.fd, name, n.mode & 07777, 0) < 0) return -errno;
+    if ((n.uid >= 0 || n.gid >= 0) &&
+        fchownat(dir.fd, name, (uid_t)n.uid, (gid_t)n.gid, AT_SYMLINK_NOFOLLOW) < 0)
+      return -errno;
+  }
+  long fd = syscall(SYS_open_tree, g_stage_fd, name, OPEN_TREE_CLONE | O_CLOEXEC |
+                                                          AT_SYMLINK_NOFOLLOW);
+  return fd < 0 ? -errno : (int)fd;
+}
+
+// Detaches every mount stacked on dirfd/leaf (the thread's cwd becomes dirfd). 0 or -errno.
+int unmount_leaf(int dirfd, const std::string& leaf) {
+  if (fchdir(dirfd) < 0) return -errno;
+  for (int i = 0; i < 8; ++i) {
+    int m = is_mount_leaf(dirfd, leaf);
+    if (m <= 0) return m;
+    if (umount2(leaf.c_str(), MNT_DETACH | UMOUNT_NOFOLLOW) < 0) return -errno;
+  }
+  return -EBUSY;
+}
+
+// The placeholder a bind mount sits on: an empty regular file.
+bool is_placeholder(int dirfd, const std::string& leaf) {
+  struct stat st;
+  return fstatat(dirfd, leaf.c_str(), &st, AT_SYMLINK_NOFOLLOW) == 0 && S_ISREG(st.st_mode) &&
+         st.st_size == 0;
+}
+
+int create_bound(int rootfd, const gm_dev_node_t& n, int tree_fd, int flags) {
+  Fd parent;
+  std::string leaf;
+  int e = walk_parent(rootfd, n.path, true, &parent, &leaf);
+  if (e != 0) return e;
+  if (guarded_dir(parent.fd)) return kSharedHost;
+  int kind;
+  uint32_t maj, min, mode;
+  e = stat_leaf(parent.fd, leaf, &kind, &maj, &min, &mode);
+  if (e < 0) return e;
+  int mounted = kind ? is_mount_leaf(parent.fd, leaf) : 0;
+  if (mounted < 0) return mounted;
+  bool same = (kind == 1 || kind == 2) && maj == n.major && min == n.minor;
+  if (same && mounted) return 1;  // idempotent re-attach
+  if (kind != 0) {
+    if (!same && (kind == 1 || kind == 2) && !(flags & GM_DEV_REPLACE)) return -EEXIST;
+    if (kind == 3 && (mounted || !is_placeholder(parent.fd, leaf))) return -EEXIST;
+    // a node of ours that cannot be opened (mknod'ed on the nodev /dev), an older mount, or a
+    // placeholder left by an interrupted attach: clear it and bind over a fresh placeholder
+    if (mounted && (e = unmount_leaf(parent.fd, leaf)) < 0) return e;
+    if (!is_placeholder(parent.fd, leaf) && unlinkat(parent.fd, leaf.c_str(), 0) < 0)
+      return -errno;
+  }
+  if (!is_placeholder(parent.fd, leaf)) {
+    int fd = openat(parent.fd, leaf.c_str(), O_CREAT | O_EXCL | O_WRONLY | O_NOFOLLOW | O_CLOEXEC,
+                    0);
+    if (fd < 0) return -errno;
+    close(fd);
+  }
+  if (syscall(SYS_move_mount, tree_fd, "", parent.fd, leaf.c_str(), MOVE_MOUNT_F_EMPTY_PATH) < 0) {
+    int err = errno;
+    unlinkat(parent.fd, leaf.c_str(), 0);
+    return -err;
+  }
+  return 0;
+}
+
+// Removal that also handles bind-mounted nodes: unmount (if ours), then unlink the placeholder.
+int remove_bound(int rootfd, const gm_dev_node_t& n) {
+  Fd parent;
+  std::string leaf;
+  int e = walk_parent(rootfd, n.path, false, &parent, &leaf);
+  if (e == -ENOENT) return 1;
+  if (e != 0) return e;
+  if (guarded_dir(parent.fd)) return kSharedHost;
+  int kind;
+  uint32_t maj, min, mode;
+  e = stat_leaf(parent.fd, leaf, &kind, &maj, &min, &mode);
+  if (e < 0) return e;
+  if (kind == 0) return 1;
+  int mounted = is_mount_leaf(parent.fd, leaf);
+  if (mounted < 0) return mounted;
+  if (!mounted) {
+    if (kind == 3 && is_placeholder(parent.fd, leaf)) {  // interrupted attach
+      if (unlinkat(parent.fd, leaf.c_str(), 0) < 0) return -errno;
+      return 0;
+    }
+    return remove_one(rootfd, n);
+  }
+  if (!(kind == 1 && maj == n.major && min == n.minor)) return -EEXIST;
+  if ((e = unmount_leaf(parent.fd, leaf)) < 0) return e;
+  if (is_placeholder(parent.fd, leaf) && unlinkat(parent.fd, leaf.c_str(), 0) < 0) return -errno;
+  return 0;
 }
 
 // ------------------------------------------------------------------ roctx
@@ -923,12 +1080,46 @@ int gm_devnodes_guard(const char* host_dev) {
   return set;
 }
 
+int gm_devnodes_stage(const char* dir, int mount_tmpfs) {
+  std::lock_guard<std::mutex> lk(g_stage_mu);
+  if (g_stage_fd >= 0) close(g_stage_fd);
+  g_stage_fd = -1;
+  if (!dir || !*dir) return 0;
+  if (mkdir(dir, 0711) < 0 && errno != EEXIST) return -errno;
+  if (mount_tmpfs) {
+    Fd d(open(dir, O_PATH | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC));
+    if (!d.ok()) return -errno;
+    std::string up = std::string(dir) + "/..";
+    struct stat self, parent;
+    if (fstat(d.fd, &self) < 0 || stat(up.c_str(), &parent) < 0) return -errno;
+    if (self.st_dev == parent.st_dev &&  // not mounted yet (a restarted worker reuses its own)
+        mount("gm-devstage", dir, "tmpfs", MS_NOSUID | MS_NOEXEC, "mode=0711") < 0)
+      return -errno;
+  }
+  int fd = open(dir, O_PATH | O_DIRECTORY | O_NOFOLLOW | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  g_stage_fd = fd;
+  return 0;
+}
+
 int gm_devnodes_create(int pid, const char* root, const gm_dev_node_t* nodes, int n, int flags,
                        int* results) {
   int failures = 0;
+  std::vector<Fd> trees;
+  if (flags & GM_DEV_BIND) {  // clone the staged nodes while still in our own mount namespace
+    for (int i = 0; i < n; ++i) {
+      int t = staged_tree(nodes[i]);
+      if (t < 0) {
+        for (int j = 0; j < n; ++j) results[j] = t;
+        return n;
+      }
+      trees.emplace_back(t);
+    }
+  }
   int e = with_root(pid, root, flags, [&](int rootfd) {
     for (int i = 0; i < n; ++i) {
-      results[i] = create_one(rootfd, nodes[i], flags);
+      results[i] = (flags & GM_DEV_BIND) ? create_bound(rootfd, nodes[i], trees[i].fd, flags)
+                                         : create_one(rootfd, nodes[i], flags);
       if (results[i] < 0) ++failures;
     }
     return 0;
@@ -945,7 +1136,8 @@ int gm_devnodes_remove(int pid, const char* root, const gm_dev_node_t* nodes, in
   int failures = 0;
   int e = with_root(pid, root, flags, [&](int rootfd) {
     for (int i = 0; i < n; ++i) {
-      results[i] = remove_one(rootfd, nodes[i]);
+      results[i] = (flags & GM_DEV_BIND) ? remove_bound(rootfd, nodes[i])
+                                         : remove_one(rootfd, nodes[i]);
       if (results[i] < 0) ++failures;
     }
     return 0;
@@ -1005,7 +1197,8 @@ int gm_devnodes_present(int pid, const char* root, const gm_dev_node_t* nodes, i
       int kind = 0;
       uint32_t ma = 0, mi = 0, mode = 0;
       if (stat_leaf(parent.fd, leaf, &kind, &ma, &mi, &mode) < 0) continue;
-      if ((kind == 1 || kind == 2) && ma == nodes[i].major && mi == nodes[i].minor) {
+      if ((kind == 1 || kind == 2) && ma == nodes[i].major && mi == nodes[i].minor &&
+          (!(flags & GM_DEV_BIND) || is_mount_leaf(parent.fd, leaf) == 1)) {
         present[i] = 1;
         ++count;
       }

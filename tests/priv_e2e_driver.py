@@ -3,7 +3,9 @@
 HTTP master → gRPC worker → placeholder ledger (fake apiserver/kubelet) → the production node
 path: real cgroup2 hierarchy, real BPF_PROG_TYPE_CGROUP_DEVICE program swapped over a
 runc-style program, real mknod through /proc/<pid>/root into a tenant process that lives in its
-own mount namespace (private tmpfs /dev). The mock inventory maps the "GPUs" to harmless memory
+own mount namespace (private tmpfs /dev), and — for a tenant in its own user namespace as well
+(Kubernetes `hostUsers: false`), whose /dev tmpfs is nodev — real bind mounts of staged nodes
+(open_tree + move_mount). The mock inventory maps the "GPUs" to harmless memory
 devices (render/card minors of major 1) so a process inside the tenant cgroup can prove what the
 kernel enforces. Prints one JSON line of observations.
 """
@@ -66,11 +68,13 @@ def chr_node(pid, rel):
     return [os.major(st.st_rdev), os.minor(st.st_rdev)] if stat.S_ISCHR(st.st_mode) else "notchr"
 
 
-async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0):
+async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0, userns_pid=0,
+               stage=""):
     async with LocalCluster(cgroup_mode="v2", devnode_mode="procroot", cgroup_root=mnt,
                             kfd_major=1,
                             worker_overrides={"drm_major": 1, "bpf_pin_dir": bpffs,
-                                              "host_dev_path": hostdev}) as lc:
+                                              "host_dev_path": hostdev,
+                                              "devnode_stage_dir": stage}) as lc:
         w = lc.nodes["node-0"].worker
         obs["backend"] = w.backend.name
         lc.tenant("t", pids={"main": [tenant_pid]})
@@ -106,6 +110,50 @@ async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0):
         obs["pins_left"] = [f for f in os.listdir(bpffs) if f.startswith("gm_")]
         if shared_pid:
             await shared_dev_flow(lc, hostdev, shared_pid, obs)
+        if userns_pid:
+            await userns_flow(lc, userns_pid, obs)
+
+
+USERNS_PROBE = ("import sys\n"
+                "sys.stdin.readline()\n"          # wait until moved into the tenant's cgroup
+                "out=[]\n"
+                "for p in sys.argv[1:]:\n"
+                "    try:\n"
+                "        open(p,'rb').close(); out.append('1')\n"
+                "    except OSError:\n"
+                "        out.append('0')\n"
+                "print(''.join(out))\n")
+
+
+def probe_inside(pid, cg, paths):
+    """Opens `paths` from a process inside the tenant's user + mount namespaces *and* its
+    cgroup: the device nodes must exist there and be openable, and the device program allow."""
+    p = subprocess.Popen(["nsenter", "-t", str(pid), "-U", "-m", sys.executable, "-c",
+                          USERNS_PROBE] + paths, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    with open(os.path.join(cg, "cgroup.procs"), "w") as fh:
+        fh.write(str(p.pid))
+    out, err = p.communicate("go\n", timeout=30)
+    if p.returncode:
+        raise RuntimeError(err)
+    return out.strip()
+
+
+async def userns_flow(lc, pid, obs):
+    lc.tenant("u", pids={"main": [pid]})
+    node = lc.nodes["node-0"].node
+    (c,) = [c for c in node.containers.values() if c.pod_name == "u"]
+    attach_runtime_program(c.cgroup_dir)
+    paths = ["/dev/dri/renderD5", "/dev/dri/card7"]
+    obs["userns_before"] = probe_inside(pid, c.cgroup_dir, paths)
+    code, b = await lc.add("default", "u", 1)
+    obs["userns_add"] = [code, sorted(d["render_minor"] for d in b.get("devices", []))]
+    obs["userns_after_add"] = probe_inside(pid, c.cgroup_dir, paths)
+    obs["userns_audit"] = [i.kind for i in await lc.audit("default", "u")]
+    code, _ = await lc.remove("default", "u", [d["uuid"] for d in b["devices"]])
+    obs["userns_remove"] = code
+    obs["userns_after_remove"] = probe_inside(pid, c.cgroup_dir, paths)
+    obs["userns_nodes_final"] = {p: chr_node(pid, p) for p in paths + ["/dev/kfd"]}
 
 
 def listing(d):
@@ -162,15 +210,25 @@ def main():
         ["unshare", "-m", "--propagation", "private", "sh", "-c",
          f"set -e; mount --bind {hostdev} /dev; echo ok; exec sleep 300"],
         stdout=subprocess.PIPE, text=True)
+    # a tenant in its own user namespace: its /dev tmpfs is mounted from inside it (nodev)
+    userns = subprocess.Popen(
+        ["unshare", "-U", "--map-user=0", "--map-group=0", "-m", "--propagation", "private",
+         "sh", "-c", "set -e; mount -t tmpfs tmpfs /dev; echo ok; exec sleep 300"],
+        stdout=subprocess.PIPE, text=True)
+    stage = tempfile.mkdtemp(prefix="gm-e2e-stage-")
     try:
         assert tenant.stdout.readline().strip() == "ok"
         assert shared.stdout.readline().strip() == "ok"
+        assert userns.stdout.readline().strip() == "ok"
         assert os.readlink(f"/proc/{tenant.pid}/ns/mnt") != os.readlink("/proc/self/ns/mnt")
-        asyncio.run(flow(root, bpffs, tenant.pid, obs, hostdev, shared.pid))
+        asyncio.run(flow(root, bpffs, tenant.pid, obs, hostdev, shared.pid, userns.pid, stage))
     finally:
-        for p in (tenant, shared):
+        for p in (tenant, shared, userns):
             p.kill()
             p.wait()
+        _native.host().gm_devnodes_stage(None, 0)
+        subprocess.run(["umount", "-l", stage], check=False)
+        shutil.rmtree(stage, ignore_errors=True)
         shutil.rmtree(hostdev, ignore_errors=True)
         # tear the real cgroup tree down bottom-up (processes are gone)
         for dirpath, dirs, _ in sorted(os.walk(root), key=lambda t: -t[0].count("/")):

@@ -292,3 +292,36 @@ def test_roctx_markers_are_safe_without_profiler():
             trace.mark("tick")
     assert s.children[0].name == "inner" and s.duration_ms >= 0
     assert "inner" in s.flat()
+
+
+def test_devnodes_bind_mode_policy(tmp_path):
+    """Which containers get bind-mounted nodes (GM_DEV_BIND): auto = those whose process is in
+    a user namespace other than the worker's (read from <proc_root>/<pid>/ns/user), with the
+    nodes owned by the container's mapped root (uid_map/gid_map entry for id 0). The kernel
+    side is tests/test_privileged_userns.py."""
+    proc = tmp_path / "proc"
+    for pid in ("self", "100", "200"):
+        (proc / pid / "ns").mkdir(parents=True)
+    os.link(__file__, proc / "self/ns/user")          # same inode as the worker: host userns
+    os.link(__file__, proc / "100/ns/user")
+    (proc / "200/ns/user").write_text("")            # another user namespace
+    (proc / "200/uid_map").write_text("         0     165536      65536\n")
+    (proc / "200/gid_map").write_text("         0     165536      65536\n")
+    auto = DevNodeWriter("procroot", userns="auto", stage_dir=str(tmp_path / "st"),
+                         proc_root=str(proc))
+    assert not auto._bind(Target(pid=100))
+    assert auto._bind(Target(pid=200))
+    assert not auto._bind(Target(pid=300))            # gone: nothing to decide
+    assert not auto._bind(Target(root=str(tmp_path)))  # hermetic root
+    assert auto._mapped_root(Target(pid=200)) == (165536, 165536)
+    assert auto._mapped_root(Target(pid=100)) == (-1, -1)
+    off = DevNodeWriter("procroot", userns="off", proc_root=str(proc))
+    assert not off._bind(Target(pid=200))
+    assert DevNodeWriter("procroot", userns="bind", proc_root=str(proc))._bind(Target(pid=100))
+    # emulate (unprivileged hermetic runs) never binds in auto mode
+    assert not DevNodeWriter("emulate", userns="auto", proc_root=str(proc))._bind(
+        Target(pid=200))
+    # bind mode without a staging directory is refused before any native call
+    with pytest.raises(DevNodeError, match="staging"):
+        DevNodeWriter("procroot", userns="bind", proc_root=str(proc)).create(
+            Target(pid=200), NODES[:1])

@@ -49,3 +49,11 @@ def test_full_stack_attach_detach_enforced_by_the_kernel(tmp_path):
     assert o["shared_sees_host_dev"] and o["shared_add"] == 200 and o["shared_gpus"] == [5, 8]
     assert o["shared_after_add_unchanged"] and o["shared_after_sweep_unchanged"]
     assert o["shared_host_listing"] == ["dri/card7", "dri/renderD5", "kfd"]
+    # a tenant in its own user namespace (nodev /dev): bind-mounted nodes it can open, allowed
+    # by the device program; nothing left after the detach
+    assert o["userns_before"] == "00"
+    assert o["userns_add"] == [200, [5]] and o["userns_after_add"] == "11"
+    assert o["userns_audit"] == [] and o["userns_remove"] == 200
+    assert o["userns_after_remove"] == "00"
+    assert o["userns_nodes_final"] == {"/dev/dri/renderD5": None, "/dev/dri/card7": None,
+                                       "/dev/kfd": None}
