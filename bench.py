@@ -148,6 +148,10 @@ def main() -> int:
                          "tenant in its own mount namespace (gpumounter_amd/fakes/realnode.py); "
                          "emulated: the JSON-recording cgroup-v2 backend and marker files, for "
                          "unprivileged boxes")
+    ap.add_argument("--security", choices=("shipped", "off"), default="shipped",
+                    help="shipped: master⇄worker mTLS and TokenReview/SubjectAccessReview authz "
+                         "as the manifests deploy them (--deploy processes); off: insecure gRPC, "
+                         "no authz (the reference's posture)")
     args = ap.parse_args()
     if args.node_ops == "real":
         if args.deploy == "processes" and "--deploy" in sys.argv:
@@ -219,6 +223,7 @@ def main() -> int:
             from gpumounter_amd.fakes.deployment import ProcessCluster
             pc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=args.latency,
                                 gpu_bdfs=node_bdfs, protocol=args.protocol,
+                                secure=args.security == "shipped" and args.protocol == "gpumounter",
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
                                             "GM_PLACEMENT_ENFORCE": args.placement}).start()
             pc.tenant("tenant", pids={"main": [tenant_pid]})
@@ -454,6 +459,9 @@ def main() -> int:
                     else "reference (emulated)",
                     "warm_pool": args.warm_pool, "placement": args.placement,
                     "device_plugin": args.device_plugin, "deploy": args.deploy,
+                    "security": "mTLS master-worker + TokenReview/SAR authz (cached)"
+                    if args.deploy == "processes" and args.security == "shipped" and
+                    args.protocol == "gpumounter" else "off (insecure gRPC, no authz)",
                 },
                 "attach_p99_ms": round(pct(attach_ms, 0.99), 4),
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),

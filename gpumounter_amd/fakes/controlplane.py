@@ -7,10 +7,12 @@ and no gpumounter component. The real daemons (``python -m gpumounter_amd worker
 as separate processes against it, configured only through ``GM_*`` environment variables, as in
 the DaemonSet/Deployment (see :mod:`gpumounter_amd.fakes.deployment`).
 
-Besides the Kubernetes API it serves two test hooks:
+Besides the Kubernetes API it serves these test hooks:
   ``POST /_fake/tenant``  {"name", "ns", "node", "gpus", "containers", "pids"} → a Running pod
   ``POST /_fake/worker``  {"node", "port"}  → the worker DaemonSet pod the master discovers
   ``GET  /_fake/kubelet``  → each node's PodResources call counters (served, rejected, over_limit)
+  ``POST /_fake/user``    {"token", "user", "verbs", "resource", "namespaces"} → a bearer token
+                          TokenReview accepts, and an RBAC rule SubjectAccessReview honours
 The info file lists the apiserver URL and each node's kubelet socket, cgroup root and rootfs root.
 """
 from __future__ import annotations
@@ -47,7 +49,16 @@ def _hooks(lc_ref: list):
             return web.json_response({n: dict(h.kubelet.calls)
                                       for n, h in lc_ref[0].nodes.items()})
 
+        async def user(req: web.Request) -> web.Response:
+            b = await req.json()
+            api = lc_ref[0].cluster
+            api.add_user(b["token"], b["user"])
+            api.grant(b["user"], b.get("verbs", ["create", "delete", "get"]),
+                      b.get("resource", "pods/gpumount"), b.get("namespaces", ["*"]))
+            return web.json_response({"ok": True}, status=201)
+
         app.router.add_post("/_fake/tenant", tenant)
+        app.router.add_post("/_fake/user", user)
         app.router.add_post("/_fake/worker", worker)
         app.router.add_get("/_fake/kubelet", kubelet)
     return install

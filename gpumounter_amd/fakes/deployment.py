@@ -9,7 +9,11 @@ is ideal for white-box tests but is not how gpumounter-amd runs. ``ProcessCluste
 * the master (``python -m gpumounter_amd master``) the same way,
 
 waits until each reports ready, and talks to the master over HTTP. ``stop()`` sends SIGTERM and
-expects every daemon to exit cleanly. Used by tests/test_processes.py and ``bench.py --deploy
+expects every daemon to exit cleanly. ``secure=True`` (the default for the gpumounter protocol)
+runs them as the shipped manifests do: master⇄worker mTLS with certificates from a throw-away CA
+(:mod:`gpumounter_amd.fakes.pki`) and the master authorizing every call with TokenReview +
+SubjectAccessReview (``GM_AUTHZ_MODE=kube``); the client sends a bearer token the fake apiserver
+knows. Used by tests/test_processes.py and ``bench.py --deploy
 processes`` (no shared interpreter, event loop or GIL between master, worker and apiserver).
 """
 from __future__ import annotations
@@ -56,12 +60,17 @@ class ProcessCluster:
                  latency: str = "zero", gpu_bdfs: Optional[List[str]] = None,
                  worker_env: Optional[Dict[str, str]] = None,
                  master_env: Optional[Dict[str, str]] = None, log_dir: str = "",
-                 protocol: str = "gpumounter", kubelet_limit: str = "enforce") -> None:
+                 protocol: str = "gpumounter", kubelet_limit: str = "enforce",
+                 secure: Optional[bool] = None) -> None:
         """``protocol="reference"`` runs worker and master with the reference's call sequence
-        (gpumounter_amd/fakes/refproto.py) in the same deployment shape, for comparison.
+        (gpumounter_amd/fakes/refproto.py) in the same deployment shape, for comparison; it is
+        insecure like the reference unless ``secure`` says otherwise.
         ``kubelet_limit="count"`` serves PodResources calls over the kubelet's rate budget and
         only counts them (see :class:`FakeKubelet`)."""
         self.n_nodes = n_nodes
+        self.secure = protocol == "gpumounter" if secure is None else secure
+        self.token = "gm-hermetic-client-token" if self.secure else ""
+        self._auth = {"Authorization": f"Bearer {self.token}"} if self.token else {}
         self.entry = ["-m", "gpumounter_amd"] if protocol == "gpumounter" else \
             ["-m", "gpumounter_amd.fakes.refproto"]
         self.amdsmi_lib = amdsmi_lib
@@ -91,7 +100,7 @@ class ProcessCluster:
                 conn = self._local.conn = http.client.HTTPConnection(host, int(port), timeout=120)
                 self._conns.append(conn)
             try:
-                conn.request(method, path, body=body, headers=headers or {})
+                conn.request(method, path, body=body, headers={**self._auth, **(headers or {})})
                 r = conn.getresponse()
                 return r.status, r.read()
             except (http.client.HTTPException, OSError):
@@ -145,6 +154,23 @@ class ProcessCluster:
         with open(info_path) as fh:
             self.info = json.load(fh)
         api = self.info["api_url"]
+        tls_w, tls_m = {}, {"GM_AUTHZ_MODE": "none"}
+        if self.secure:
+            from gpumounter_amd.fakes.pki import make_pki
+            pki = make_pki(os.path.join(self.workdir, "pki"))
+            tls_w = {"GM_TLS_CERT": pki["worker.crt"], "GM_TLS_KEY": pki["worker.key"],
+                     "GM_TLS_CA": pki["ca"]}
+            tls_m = {"GM_TLS_CERT": pki["master.crt"], "GM_TLS_KEY": pki["master.key"],
+                     "GM_TLS_CA": pki["ca"], "GM_AUTHZ_MODE": "kube"}
+            code, _ = _http("POST", f"{api}/_fake/user", json.dumps(
+                {"token": self.token, "user": "gm-hermetic-client",
+                 "verbs": ["create", "delete", "get"], "resource": "pods/gpumount"}).encode(),
+                {"Content-Type": "application/json"})
+            if code != 201:
+                raise RuntimeError(f"client token registration failed: {code}")
+            _http("POST", f"{api}/_fake/user", json.dumps(
+                {"token": self.token, "user": "gm-hermetic-client", "verbs": ["get"],
+                 "resource": "nodes/gpumount"}).encode(), {"Content-Type": "application/json"})
         for node, n in self.info["nodes"].items():
             gport, mport = free_port(), free_port()
             self.worker_ports[node] = (gport, mport)
@@ -154,7 +180,7 @@ class ProcessCluster:
                    "GM_CGROUP_MODE": self.cgroup_mode, "GM_DEVNODE_MODE": "emulate",
                    "GM_CONTAINER_ROOT_PREFIX": n["rootfs_root"], "GM_AMDSMI_LIB": self.amdsmi_lib,
                    "GM_STATE_DIR": n["state_dir"], "GM_HOST_DEV_PATH": n["host_dev"],
-                   "GM_WORKER_INSECURE": "1",
+                   **({} if self.secure else {"GM_WORKER_INSECURE": "1"}), **tls_w,
                    "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": str(gport),
                    "GM_METRICS_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
                    "GM_LOG_JSON": "false", **self.worker_env}
@@ -164,13 +190,13 @@ class ProcessCluster:
             self._await_worker(node)
         mport = free_port()
         self._spawn("master", [*self.entry, "master"],
-                    {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1", "GM_AUTHZ_MODE": "none",
+                    {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1", **tls_m,
                      "GM_MASTER_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
                      "GM_LOG_JSON": "false", **self.master_env})
         self.master_url = f"http://127.0.0.1:{mport}"
         for node in self.info["nodes"]:   # the master has discovered every worker
             self._wait(f"master → {node}", lambda n=node: _http(
-                "GET", f"{self.master_url}/api/v1/nodes/{n}/gpus")[0] == 200)
+                "GET", f"{self.master_url}/api/v1/nodes/{n}/gpus", headers=self._auth)[0] == 200)
         return self
 
     def _await_worker(self, node: str) -> None:
@@ -254,7 +280,7 @@ class ProcessCluster:
 
     def pod_gpus(self, ns: str, pod: str) -> Tuple[int, dict]:
         code, body = _http("GET", f"{self.master_url}/api/v1/namespaces/{ns}/pods/{pod}/gpus",
-                           headers={"Accept": "application/json"})
+                           headers={"Accept": "application/json", **self._auth})
         return code, json.loads(body)
 
     def kubelet_calls(self, node: str = "node-0") -> Dict[str, int]:

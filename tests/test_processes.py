@@ -36,6 +36,22 @@ def test_daemons_as_processes_attach_detach_and_exit_cleanly_on_sigterm():
         assert code == 200
         nodes = [f for d, _, fs in os.walk(root) for f in fs if f.startswith("renderD")]
         assert nodes == [] and pc.audit("default", "t0") == []
+        # deployed as shipped: no bearer token → 401 at the master; the worker's gRPC port
+        # refuses a caller without the master's client certificate
+        from gpumounter_amd.fakes.deployment import _http
+        code, body = _http("GET", f"{pc.master_url}/addgpu/namespace/default/pod/t0/gpu/1/"
+                                  "isEntireMount/false")
+        assert code == 401, body
+        import grpc
+
+        from gpumounter_amd.api import gpu_mount as api
+        ch = grpc.insecure_channel(f"127.0.0.1:{pc.worker_ports['node-0'][0]}")
+        stub = ch.unary_unary(api.NODE_STATUS,
+                              request_serializer=api.NodeStatusRequest.SerializeToString,
+                              response_deserializer=api.NodeStatusResponse.FromString)
+        with pytest.raises(grpc.RpcError):
+            stub(api.NodeStatusRequest(), timeout=5)
+        ch.close()
     finally:
         codes = pc.stop()
     assert codes == {"master": 0, "worker-node-0": 0, "worker-node-1": 0, "controlplane": 0}, \
