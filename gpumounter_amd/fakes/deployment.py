@@ -23,7 +23,6 @@ import json
 import os
 import shutil
 import signal
-import socket
 import subprocess
 import sys
 import tempfile
@@ -35,14 +34,6 @@ import urllib.request
 from typing import Dict, List, Optional, Tuple
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-
-
-def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _http(method: str, url: str, body: Optional[bytes] = None, headers: Optional[dict] = None,
@@ -172,8 +163,8 @@ class ProcessCluster:
                 {"token": self.token, "user": "gm-hermetic-client", "verbs": ["get"],
                  "resource": "nodes/gpumount"}).encode(), {"Content-Type": "application/json"})
         for node, n in self.info["nodes"].items():
-            gport, mport = free_port(), free_port()
-            self.worker_ports[node] = (gport, mport)
+            # ephemeral ports, published by the daemon itself (GM_READY_FILE): a port picked
+            # here and bound later can be taken by another process in between
             env = {"GM_KUBE_API": api, "GM_NODE_NAME": node,
                    "GM_KUBELET_SOCKET": n["kubelet_socket"], "GM_CGROUP_ROOT": n["cgroup_root"],
                    "GM_KUBELET_CHECKPOINT": n["kubelet_checkpoint"],
@@ -181,26 +172,37 @@ class ProcessCluster:
                    "GM_CONTAINER_ROOT_PREFIX": n["rootfs_root"], "GM_AMDSMI_LIB": self.amdsmi_lib,
                    "GM_STATE_DIR": n["state_dir"], "GM_HOST_DEV_PATH": n["host_dev"],
                    **({} if self.secure else {"GM_WORKER_INSECURE": "1"}), **tls_w,
-                   "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": str(gport),
-                   "GM_METRICS_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
+                   "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": "0",
+                   "GM_METRICS_PORT": "0", "GM_READY_FILE": self._ready_path(f"worker-{node}"),
+                   "GM_LOG_LEVEL": "WARNING",
                    "GM_LOG_JSON": "false", **self.worker_env}
             self._worker_env[node] = env
             self._spawn(f"worker-{node}", [*self.entry, "worker"], env)
-        for node in self.worker_ports:
+        for node in self._worker_env:
             self._await_worker(node)
-        mport = free_port()
         self._spawn("master", [*self.entry, "master"],
                     {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1", **tls_m,
-                     "GM_MASTER_PORT": str(mport), "GM_LOG_LEVEL": "WARNING",
-                     "GM_LOG_JSON": "false", **self.master_env})
-        self.master_url = f"http://127.0.0.1:{mport}"
+                     "GM_MASTER_PORT": "0", "GM_READY_FILE": self._ready_path("master"),
+                     "GM_LOG_LEVEL": "WARNING", "GM_LOG_JSON": "false", **self.master_env})
+        self.master_url = f"http://127.0.0.1:{self._ready('master')['port']}"
         for node in self.info["nodes"]:   # the master has discovered every worker
             self._wait(f"master → {node}", lambda n=node: _http(
                 "GET", f"{self.master_url}/api/v1/nodes/{n}/gpus", headers=self._auth)[0] == 200)
         return self
 
+    def _ready_path(self, key: str) -> str:
+        return os.path.join(self.workdir, f"{key}.ready")
+
+    def _ready(self, key: str) -> dict:
+        """The ports daemon ``key`` bound, once it has published them."""
+        path = self._ready_path(key)
+        self._wait(f"{key} ready file", lambda: os.path.exists(path))
+        with open(path) as fh:
+            return json.load(fh)
+
     def _await_worker(self, node: str) -> None:
-        gport, mport = self.worker_ports[node]
+        r = self._ready(f"worker-{node}")
+        gport, mport = self.worker_ports[node] = (int(r["grpc_port"]), int(r["http_port"]))
         self._wait(f"worker {node}",
                    lambda: _http("GET", f"http://127.0.0.1:{mport}/readyz")[0] == 200)
         code, _ = _http("POST", f"{self.info['api_url']}/_fake/worker",
@@ -216,7 +218,12 @@ class ProcessCluster:
         return p.wait(20)
 
     def restart_worker(self, node: str = "node-0") -> None:
-        """Start the node's worker again (same ports and environment) and wait until ready."""
+        """Start the node's worker again (same environment, fresh ports) and wait until it is
+        ready and registered under its new port."""
+        try:
+            os.unlink(self._ready_path(f"worker-{node}"))
+        except FileNotFoundError:
+            pass
         self._spawn(f"worker-{node}", [*self.entry, "worker"], self._worker_env[node])
         self._await_worker(node)
 

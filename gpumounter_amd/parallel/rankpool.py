@@ -21,9 +21,9 @@ import argparse
 import json
 import os
 import select
-import socket
 import subprocess
 import sys
+import tempfile
 import time
 from typing import Dict, List, Optional
 
@@ -31,20 +31,14 @@ from typing import Dict, List, Optional
 _TAG = "@@gm-rank "
 
 
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
 class RankPool:
     def __init__(self, world: int, timeout_s: float = 180.0) -> None:
         self.world = world
         self.timeout_s = timeout_s
-        port = _free_port()
-        env = {**os.environ, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+        # file:// rendezvous: no TCP port to pick ahead of time (one picked with bind(0) and
+        # bound later by rank 0 can be taken meanwhile, e.g. as a connection's local port)
+        self._rdv_dir = tempfile.mkdtemp(prefix="gm-rankpool-")
+        env = {**os.environ, "GM_RANKPOOL_RDV": "file://" + os.path.join(self._rdv_dir, "store"),
                "WORLD_SIZE": str(world)}
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -106,6 +100,8 @@ class RankPool:
             except subprocess.TimeoutExpired:
                 p.kill()
                 codes[i] = p.wait()
+        import shutil
+        shutil.rmtree(self._rdv_dir, ignore_errors=True)
         return codes
 
 
@@ -120,6 +116,7 @@ def _rank_main(rank: int, world: int) -> int:
     import torch
     import torch.distributed as dist
 
+    rdv = os.environ.get("GM_RANKPOOL_RDV") or "env://"
     on_gpu = torch.cuda.is_available()
     backend = "nccl" if on_gpu else "gloo"
     dev = None
@@ -140,10 +137,12 @@ def _rank_main(rank: int, world: int) -> int:
                         raise RuntimeError(f"attached GPU {mine} not visible to HIP")
                     torch.cuda.set_device(d)
                     dev = torch.device("cuda", d)
-                    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+                    dist.init_process_group("nccl", init_method=rdv, rank=rank,
+                                            world_size=world, device_id=dev)
                 else:
                     dev = torch.device("cpu")
-                    dist.init_process_group("gloo", rank=rank, world_size=world)
+                    dist.init_process_group("gloo", init_method=rdv, rank=rank,
+                                            world_size=world)
                 bound = mine
             elif mine != bound:
                 raise RuntimeError(f"attached set changed between steps ({bound} → {mine})")

@@ -27,6 +27,10 @@ class Config:
     worker_host: str = "0.0.0.0"
     worker_port: int = 1200
     metrics_port: int = 9400
+    # after start-up the daemon writes the ports it actually bound ({"grpc_port", "http_port"}
+    # or {"port"}) here, atomically; with ports 0 (ephemeral) that is how a supervisor finds
+    # them without racing another process for a pre-picked free port. "" = off
+    ready_file: str = ""
     # --- kubernetes ------------------------------------------------------------------------
     kube_api: str = ""                 # "" → in-cluster; else http(s)://host:port (fake in tests)
     kubeconfig: str = ""
@@ -228,7 +232,7 @@ class Config:
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))
         _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
         _choice("ledger_source", self.ledger_source, ("auto", "podresources"))
-        if not (0 < self.worker_port < 65536 and 0 <= self.master_port < 65536):
+        if not (0 <= self.worker_port < 65536 and 0 <= self.master_port < 65536):
             raise ValueError("ports out of range")
 
     def as_dict(self) -> Dict[str, Any]:

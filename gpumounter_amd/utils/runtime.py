@@ -10,9 +10,21 @@ sub-ms pauses for rare 25-40 ms ones, which is worse for the p99.
 from __future__ import annotations
 
 import gc
+import json
+import os
 
 
 def tune_gc(freeze: bool = True) -> None:
     if freeze:
         gc.collect()
         gc.freeze()
+
+
+def write_ready_file(path: str, info: dict) -> None:
+    """Atomically publish what a daemon bound (config ``ready_file``)."""
+    if not path:
+        return
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "w") as fh:
+        json.dump(info, fh)
+    os.replace(tmp, path)

@@ -230,6 +230,8 @@ class Worker:
         if self.cfg.gc_tune:
             runtime.tune_gc()
         self.ready = True
+        runtime.write_ready_file(self.cfg.ready_file, {"grpc_port": self.grpc_port,
+                                                       "http_port": self.http_port})
         _log.info("worker %s serving gRPC :%d http :%d (cgroup %s/%s, devnodes %s, ledger %s)",
                   self.cfg.node_name, self.grpc_port, self.http_port, self.resolver.mode,
                   self.backend.name, self.cfg.devnode_mode, self.ledger.api_version)

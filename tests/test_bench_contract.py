@@ -117,3 +117,19 @@ def test_bench_real_node_ops_reports_stage_split():
     st = d["real_node_ops_stage_p50_ms"]
     assert {"bpf_load_verify", "bpf_attach", "devnodes", "cgroup_rule"} <= set(st)
     assert d["ledger_audit_issues"] == 0 and d["final_orphans"] == 0
+
+
+def test_rank_pool_two_ranks_on_cpu():
+    """bench.py --gpus N without a launcher: the spawned rank processes rendezvous through a
+    file (no pre-picked TCP port) and all-reduce; gloo on the CPU here, RCCL on a GPU node."""
+    code = ("import json; from gpumounter_amd.parallel.rankpool import RankPool; "
+            "p = RankPool(2); r = p.allreduce(['0000:15:00.0', '0000:05:00.0'], 1024); "
+            "r2 = p.allreduce(['0000:15:00.0', '0000:05:00.0'], 1024); "
+            "print(json.dumps([r, r2, p.close()]))")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=180, cwd=ROOT, env={**os.environ, "CUDA_VISIBLE_DEVICES": ""})
+    assert out.returncode == 0, out.stderr[-3000:]
+    r, r2, codes = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["ok"] and r2["ok"] and r["backend"] == "gloo"
+    assert r["bdfs"] == ["0000:05:00.0", "0000:15:00.0"]      # rank r ↔ sorted(bdfs)[r]
+    assert codes == {"0": 0, "1": 0}

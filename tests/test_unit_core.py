@@ -39,7 +39,8 @@ def test_config_layering_yaml_env_overrides(tmp_path):
 
 
 @pytest.mark.parametrize("bad", [{"GM_CGROUP_MODE": "v3"}, {"GM_DEVNODE_MODE": "x"},
-                                 {"GM_WORKER_PORT": "0"}, {"GM_ROCTX": "maybe"}])
+                                 {"GM_WORKER_PORT": "-1"}, {"GM_WORKER_PORT": "70000"},
+                                 {"GM_ROCTX": "maybe"}, {"GM_DEVNODE_USERNS": "maybe"}])
 def test_config_rejects_invalid(bad):
     with pytest.raises(ValueError):
         Config.load(env=bad)
