@@ -162,6 +162,80 @@ async def soak(lc, args) -> dict:
             "gpus_still_allocated": len(node.allocated)}
 
 
+def contention_processes(args) -> dict:
+    """The contention scenario against the deployment shape: master, worker and control plane
+    as separate processes (ProcessCluster, deployed as shipped: mTLS + authz), one client thread
+    per Pod issuing its adds/removes over HTTP concurrently with the others. Invariants after
+    every round, read through the public APIs only: each Pod's hot-mounted set equals what its
+    client attached, no GPU is hot-mounted twice, the placeholders hold exactly the hot-mounted
+    GPUs, and every Pod's audit is clean."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from gpumounter_amd.fakes.deployment import ProcessCluster
+    tenants = [f"c{i}" for i in range(4)]
+    lat, ok, fail, problems = [], 0, 0, []
+    mine = {t: [] for t in tenants}          # client-side record: [(uuids, entire)]
+    rnds = {t: random.Random(args.seed * 31 + i) for i, t in enumerate(tenants)}
+    with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup) as pc:
+        for t in tenants:
+            pc.tenant(t)
+
+        def op(t):
+            rnd = rnds[t]
+            if mine[t] and rnd.random() < 0.5:
+                groups = mine[t]
+                if any(e for _, e in groups):
+                    pick = list(groups)
+                else:
+                    pick = rnd.sample(groups, rnd.randint(1, len(groups)))
+                code, _ = pc.remove("default", t, [u for g, _ in pick for u in g], force=True)
+                if code == 200:
+                    for g in pick:
+                        groups.remove(g)
+                return code, None
+            n, entire = rnd.randint(1, 4), rnd.random() < 0.3
+            t0 = time.perf_counter()
+            code, b = pc.add("default", t, n, entire=entire)
+            ms = (time.perf_counter() - t0) * 1e3
+            if code == 200:
+                uu = [d["uuid"] for d in b["devices"]]
+                mine[t].extend([(uu, True)] if entire else [([u], False) for u in uu])
+            return code, ms
+
+        t_start = time.perf_counter()
+        with ThreadPoolExecutor(len(tenants)) as ex:
+            for _ in range(args.rounds):
+                for code, ms in ex.map(op, tenants):
+                    ok += code == 200
+                    fail += code != 200
+                    if code == 200 and ms is not None:
+                        lat.append(ms)
+                hot_all = []
+                for t in tenants:
+                    code, g = pc.pod_gpus("default", t)
+                    hot = sorted(x["uuid"] for x in g.get("gpus", [])
+                                 if x.get("source") == "hot-mount")
+                    hot_all += hot
+                    want = sorted(u for grp, _ in mine[t] for u in grp)
+                    if hot != want:
+                        problems.append(f"{t}: ledger {hot} != attached {want}")
+                    issues = pc.audit("default", t)
+                    if issues:
+                        problems.append(f"{t}: audit {issues}")
+                if len(hot_all) != len(set(hot_all)):
+                    problems.append(f"GPU hot-mounted twice: {sorted(hot_all)}")
+                held = sum(int(c.get("resources", {}).get("limits", {}).get("amd.com/gpu", 0))
+                           for p in pc.placeholders() for c in p["spec"]["containers"])
+                if held != len(hot_all):
+                    problems.append(f"placeholders hold {held} GPUs, {len(hot_all)} hot-mounted")
+        elapsed = time.perf_counter() - t_start
+    return {"rounds": args.rounds, "ops_ok": ok, "ops_refused": fail,
+            "ops_per_s": round((ok + fail) / elapsed, 1),
+            "attach_p50_ms": round(pct(lat, 0.5), 3) if lat else None,
+            "attach_p99_ms": round(pct(lat, 0.99), 3) if lat else None,
+            "invariant_violations": len(problems), "violation_examples": problems[:5]}
+
+
 SCENARIOS = {"scale": scale, "contention": contention, "soak": soak}
 
 
@@ -177,8 +251,20 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--cycles", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--deploy", choices=("inprocess", "processes"), default="inprocess",
+                    help="processes: daemons as separate processes, clients over HTTP "
+                         "(contention only)")
     args = ap.parse_args()
     log.setup("WARNING", json_format=False)
+    if args.deploy == "processes":
+        if args.scenario != "contention":
+            ap.error("--deploy processes runs the contention scenario only")
+        res = contention_processes(args)
+        res["config"] = {"scenario": "contention", "deploy": "processes",
+                         "amdsmi": args.amdsmi or "libamd_smi", "cgroup": args.cgroup,
+                         "latency": "zero", "security": "mTLS + TokenReview/SAR authz"}
+        print(json.dumps(res))
+        return 0
 
     async def run():
         lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()

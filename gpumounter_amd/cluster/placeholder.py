@@ -408,6 +408,7 @@ class PlaceholderManager:
                 self.faults.check("ledger_read")
             for key, ids in list(from_ckpt.items()):    # admitted: known without an RPC
                 if key in pending:
+                    self._check_count(key, ids)
                     ph = pending.pop(key)
                     ph.device_ids = tuple(ids)
                     self.device_ids[ph.uid] = ph.device_ids
@@ -438,6 +439,7 @@ class PlaceholderManager:
             for key in list(pending):
                 ids = got.get(key)
                 if ids:
+                    self._check_count(key, ids)
                     ph = pending.pop(key)
                     ph.device_ids = tuple(ids)
                     self.device_ids[ph.uid] = ph.device_ids
@@ -448,6 +450,19 @@ class PlaceholderManager:
                             ck.distrust(f"{self._checkpoint_misses} admitted placeholders in "
                                         f"a row had no entry in it")
         return failed
+
+    def _check_count(self, key: Tuple[str, str], ids: Sequence[str]) -> None:
+        """The kubelet allocates a placeholder exactly the devices it requests. A ledger that
+        reports a different number is inconsistent with the scheduler's accounting (which
+        counts the request): mounting those GPUs could double-book one, so the attach fails
+        (and is rolled back) instead."""
+        pod = self.informer.cache.get(key)
+        want = podu.resource_limit(pod, self.cfg.resource_name) if pod else len(ids)
+        if len(ids) != want:
+            _log.error("ledger reports %d device(s) %s for placeholder %s/%s, which requests "
+                       "%d", len(ids), list(ids), key[0], key[1], want)
+            raise ReserveError(f"ledger inconsistent: placeholder {key[1]} requests {want} "
+                               f"GPU(s), the kubelet reports {len(ids)}")
 
     # ------------------------------------------------------------------------ release
     async def release(self, phs: Sequence[Placeholder], wait: bool = True,

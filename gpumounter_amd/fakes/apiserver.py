@@ -147,6 +147,7 @@ class FakeCluster:
         self.request_count = 0
         self.requests_by_verb: Dict[str, int] = {}
         self._unschedulable: set = set()
+        self._handed_to_kubelet: set = set()   # pod UIDs bound and passed to kubelet admission
         self._tasks: set = set()
         self._lock = threading.RLock()
         self._faults: List[Tuple[str, int, bool, str]] = []
@@ -270,6 +271,11 @@ class FakeCluster:
         pod = self.pods.get((ns, name))
         if pod is None or podu.is_terminating(pod):
             return
+        uid = pod["metadata"]["uid"]
+        if uid in self._handed_to_kubelet:
+            # several capacity-freed retries can be queued for one unschedulable pod; a pod is
+            # bound and admitted once (a second admission would Allocate devices again)
+            return
         if podu.node_of(pod):
             node_name = podu.node_of(pod)
         else:
@@ -295,6 +301,7 @@ class FakeCluster:
         pod["status"]["conditions"] = [{"type": "PodScheduled", "status": "True",
                                         "lastTransitionTime": _now()}]
         self._bump("MODIFIED", pod)
+        self._handed_to_kubelet.add(uid)
         self._spawn(self._kubelet_run(ns, name, node_name))
 
     async def _kubelet_run(self, ns: str, name: str, node_name: str) -> None:
@@ -433,6 +440,7 @@ class FakeCluster:
         pod = self.pods.pop((ns, name), None)
         if pod is None:
             return
+        self._handed_to_kubelet.discard(pod["metadata"]["uid"])
         self._unschedulable.discard((ns, name))
         node = self.nodes.get(podu.node_of(pod))
         if node is not None:

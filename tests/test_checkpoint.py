@@ -118,3 +118,62 @@ def test_same_size_rewrite_in_the_same_tick_is_seen(tmp_path):
     os.utime(path, ns=(st.st_atime_ns, st.st_mtime_ns))        # same tick
     assert os.stat(path).st_size == st.st_size
     assert r.lookup("uid-b") == ("g0",) and r.lookup("uid-a") is None
+
+
+def test_ledger_reporting_more_devices_than_requested_fails_the_attach():
+    """A placeholder requesting 1 GPU for which the kubelet ledger reports 2 (a kubelet or
+    device-plugin inconsistency): mounting both would give the tenant a GPU the scheduler
+    still counts as free, so the attach fails, is rolled back, and its placeholder released."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+    from gpumounter_amd.fakes.node import FakeNode
+
+    orig = FakeNode.allocate
+
+    def over_allocate(self, ns, pod, container, n, preferred=(), uid=""):
+        ids = orig(self, ns, pod, container, n, preferred, uid)
+        if ids and "-slave-pod-" in pod:
+            extra = orig(self, ns, pod, container, 1, (), uid)   # a second Allocate
+            ids = ids + (extra or [])
+        return ids
+
+    async def main():
+        async with LocalCluster() as lc:
+            lc.tenant("t")
+            FakeNode.allocate = over_allocate
+            try:
+                code, body = await lc.add("default", "t", 1)
+            finally:
+                FakeNode.allocate = orig
+            assert code == 500, body
+            assert "ledger inconsistent" in body.get("error", ""), body
+            assert await lc.audit("default", "t") == []
+            node = lc.nodes["node-0"].node
+            (c,) = [c for c in node.containers.values() if c.pod_name == "t"]
+            assert node.container_devices(c.id) == []
+            await asyncio.sleep(0.05)
+            assert lc.cluster.placeholders() == [] and node.allocated == {}
+            code, body = await lc.add("default", "t", 1)        # consistent again
+            assert code == 200 and len(body["devices"]) == 1
+    asyncio.run(main())
+
+
+def test_fake_scheduler_admits_a_pod_once_despite_queued_retries():
+    """Several capacity-freed retries queued for one unschedulable pod bind and admit it once
+    (the fake kubelet Allocated it once per retry before: 3 devices for a 1-GPU pod)."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+
+    async def main():
+        async with LocalCluster() as lc:
+            api = lc.cluster
+            node = lc.nodes["node-0"].node
+            body = {"metadata": {"name": "p", "namespace": "gpu-pool"},
+                    "spec": {"containers": [{"name": "c", "image": "pause",
+                                             "resources": {"limits": {"amd.com/gpu": "1"}}}]}}
+            api.create_pod("gpu-pool", body)
+            await asyncio.sleep(0.05)
+            for _ in range(3):                                   # queued retries
+                api._spawn(api._schedule("gpu-pool", "p"))      # noqa: SLF001
+            await asyncio.sleep(0.1)
+            held = [d for d, (ns, pod, _) in node.allocated.items() if pod == "p"]
+            assert len(held) == 1, node.allocated
+    asyncio.run(main())
