@@ -126,7 +126,7 @@ class BpfTiming(C.Structure):
                 ("insns", C.c_uint32)]
 
 
-HOST_ABI_VERSION = 4          # native/include/gm_host.h GM_HOST_ABI_VERSION
+HOST_ABI_VERSION = 5          # native/include/gm_host.h GM_HOST_ABI_VERSION
 GM_ACC_MKNOD, GM_ACC_READ, GM_ACC_WRITE = 1, 2, 4
 GM_DEV_EMULATE, GM_DEV_VIA_SETNS, GM_DEV_REPLACE, GM_DEV_BIND = 1, 2, 4, 8
 
@@ -157,6 +157,11 @@ def host() -> C.CDLL:
                                            C.POINTER(DevRule), C.c_int, C.c_char_p,
                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.gm_bpf_dev_restore.argtypes = [C.c_char_p, C.c_char_p]
+        lib.gm_bpf_dev_build_set.argtypes = [C.c_int, C.POINTER(DevRule), C.c_int, C.c_int,
+                                             C.c_int, C.POINTER(C.c_uint64), C.c_int]
+        lib.gm_bpf_dev_set_at.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_uint32),
+                                          C.c_uint32, C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_uint32)]
         lib.gm_bpf_dev_last_timing.argtypes = [C.POINTER(BpfTiming)]
         lib.gm_bpf_dev_last_timing.restype = None
         lib.gm_devnodes_create.argtypes = [C.c_int, C.c_char_p, C.POINTER(DevNode), C.c_int,

@@ -4,12 +4,13 @@ Used (1) by tests to check the *semantics* of generated allow-lists against the 
 (first match wins; requested access must be a subset of the rule's; wildcards; tail-call into the
 runtime's original program), and (2) by the recording backend to audit what a recorded program
 would actually allow. Supports the instruction subset the generator emits plus the common
-ALU/JMP forms.
+ALU/JMP forms, a 512-byte stack, and ``bpf_map_lookup_elem`` on the allow-set HASH map of
+set-mode programs (``maps``: map fd as encoded in the program → {(type, major, minor): access}).
 """
 from __future__ import annotations
 
 import struct
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 BPF_DEVCG_DEV_BLOCK = 1
 BPF_DEVCG_DEV_CHAR = 2
@@ -27,12 +28,26 @@ def decode(insn: int):
     return code, regs & 0xF, regs >> 4, off, imm
 
 
+CTX, STACK_TOP, VALUE, MAP = 0x1000, 0x10200, 0x20000, 0x40000000
+_WIDTH = {0x00: 4, 0x08: 2, 0x10: 1, 0x18: 8}
+
+
 def run(prog: Sequence[int], dev_type: int, access: int, major: int, minor: int,
-        chained: Optional[Callable[[int, int, int, int], int]] = None, max_steps: int = 10000) -> int:
+        chained: Optional[Callable[[int, int, int, int], int]] = None, max_steps: int = 10000,
+        maps: Optional[Dict[int, Dict[Tuple[int, int, int], int]]] = None) -> int:
     """Execute ``prog`` for one device access; returns r0 (1 allow / 0 deny)."""
-    ctx = struct.pack("<III", (access << 16) | dev_type, major, minor)
+    mem = {CTX: bytearray(struct.pack("<III", (access << 16) | dev_type, major, minor)),
+           STACK_TOP - 512: bytearray(512), VALUE: bytearray(4)}
+
+    def region(addr: int, width: int):
+        for base, buf in mem.items():
+            if base <= addr and addr + width <= base + len(buf):
+                return buf, addr - base
+        raise BpfError(f"memory access out of bounds at {addr:#x}")
+
     regs = [0] * 11
-    regs[1] = 0x1000  # fake ctx pointer
+    regs[1] = CTX
+    regs[10] = STACK_TOP
     pc = 0
     steps = 0
     while True:
@@ -43,16 +58,22 @@ def run(prog: Sequence[int], dev_type: int, access: int, major: int, minor: int,
         cls = code & 0x07
         if code == 0x18:  # ld_imm64 (map fd pseudo or constant)
             _, _, _, _, imm2 = decode(prog[pc + 1])
-            regs[dst] = ((imm2 & 0xFFFFFFFF) << 32) | (imm & 0xFFFFFFFF)
+            if src == 1:   # BPF_PSEUDO_MAP_FD
+                regs[dst] = MAP + (imm & 0xFFFF)
+            else:
+                regs[dst] = ((imm2 & 0xFFFFFFFF) << 32) | (imm & 0xFFFFFFFF)
             pc += 2
             continue
         if cls == 0x01:  # LDX
-            size = code & 0x18
-            addr = regs[src] + off - 0x1000
-            width = {0x00: 4, 0x08: 2, 0x10: 1, 0x18: 8}[size]
-            if addr < 0 or addr + width > len(ctx):
-                raise BpfError(f"ctx access out of bounds: off {addr}")
-            regs[dst] = int.from_bytes(ctx[addr:addr + width], "little")
+            width = _WIDTH[code & 0x18]
+            buf, o = region(regs[src] + off, width)
+            regs[dst] = int.from_bytes(buf[o:o + width], "little")
+            pc += 1
+            continue
+        if cls == 0x03:  # STX
+            width = _WIDTH[code & 0x18]
+            buf, o = region(regs[dst] + off, width)
+            buf[o:o + width] = (regs[src] & ((1 << (8 * width)) - 1)).to_bytes(width, "little")
             pc += 1
             continue
         if cls in (0x07, 0x04):  # ALU64 / ALU
@@ -92,6 +113,21 @@ def run(prog: Sequence[int], dev_type: int, access: int, major: int, minor: int,
                     pc += 1
                     continue
                 return chained(dev_type, access, major, minor)
+            if op == 0x80 and imm == 1:  # bpf_map_lookup_elem(map, key)
+                table = (maps or {}).get(regs[1] - MAP)
+                if table is None:
+                    raise BpfError(f"lookup in unknown map {regs[1] - MAP}")
+                buf, o = region(regs[2], 12)
+                key = struct.unpack("<III", bytes(buf[o:o + 12]))
+                val = table.get(key)
+                if val is None:
+                    regs[0] = 0
+                else:
+                    mem[VALUE][:] = struct.pack("<I", val & 0xFFFFFFFF)
+                    regs[0] = VALUE
+                regs[1:6] = [0] * 5   # caller-saved registers are clobbered
+                pc += 1
+                continue
             if op == 0x80:  # call
                 if imm != 12:
                     raise BpfError(f"unsupported helper {imm}")
@@ -139,10 +175,10 @@ def immediates(prog: Sequence[int]) -> set:
     return out
 
 
-def allowed_pairs(prog: List[int], candidates, chained=runtime_default):
+def allowed_pairs(prog: List[int], candidates, chained=runtime_default, maps=None):
     """(major, minor) pairs from ``candidates`` the program allows for rw char access."""
     out = set()
     for ma, mi in candidates:
-        if run(prog, BPF_DEVCG_DEV_CHAR, ACC_READ | ACC_WRITE, ma, mi, chained):
+        if run(prog, BPF_DEVCG_DEV_CHAR, ACC_READ | ACC_WRITE, ma, mi, chained, maps=maps):
             out.add((ma, mi))
     return out

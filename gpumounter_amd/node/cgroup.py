@@ -286,6 +286,50 @@ class V2BpfBackend(DeviceRuleBackend):
         # read-back path.
         self._installed: Dict[str, Tuple[Tuple[int, ...], FrozenSet[Tuple[int, int]]]] = {}
 
+    def sweep_pins(self, cgroup_root: str) -> List[str]:
+        """Unpin the tail-call maps of cgroups that no longer exist (``gm_<cgroup inode>_<id>``
+        under ``pin_dir``). A container that exits while it holds hot-mounted GPUs takes its
+        cgroup and our attached program with it, but the pinned map would live on — and keep
+        the runtime's program it chains to loaded. Live inodes come from one walk of the cgroup
+        tree (readdir's d_ino, no stat per directory). Returns the names removed."""
+        if not self.pin_dir or not os.path.isdir(self.pin_dir):
+            return []
+        pins = [f for f in os.listdir(self.pin_dir) if f.startswith("gm_")]
+        if not pins:
+            return []
+        live = set()
+        try:
+            live.add(os.stat(cgroup_root).st_ino)
+        except OSError:
+            return []              # cannot see the hierarchy: judge nothing
+        stack = [cgroup_root]
+        while stack:
+            d = stack.pop()
+            try:
+                with os.scandir(d) as it:
+                    for e in it:
+                        if e.is_dir(follow_symlinks=False):
+                            live.add(e.inode())
+                            stack.append(e.path)
+            except OSError:
+                continue           # removed while walking
+        removed = []
+        for f in pins:
+            parts = f.split("_")
+            try:
+                ino = int(parts[1])
+            except (IndexError, ValueError):
+                continue
+            if ino not in live:
+                try:
+                    os.unlink(os.path.join(self.pin_dir, f))
+                    removed.append(f)
+                except FileNotFoundError:
+                    pass
+        if removed:
+            log.kv(_log, 20, "unpinned chain maps of removed cgroups", maps=removed)
+        return removed
+
     @staticmethod
     def attached_ids(cgdir: str) -> Tuple[int, ...]:
         ids, n, flags = (C.c_uint32 * 16)(), C.c_uint32(0), C.c_uint32(0)
@@ -311,10 +355,7 @@ class V2BpfBackend(DeviceRuleBackend):
                                     C.byref(chained))
         if rc < 0:
             raise CgroupError(f"bpf install on {cgdir}: {os.strerror(-rc)}")
-        if rc == 1 and pid.value:
-            # one slot: our program replaced the runtime's (which it tail-calls) in place
-            self._installed[cgdir] = ((pid.value,),
-                                      frozenset((n.major, n.minor) for n in desired))
+        # set mode (every hot-mount): the kernel's map is the record, read back by allowed()
         if trace.current() is not None:
             tm = _native.BpfTiming()
             lib.gm_bpf_dev_last_timing(C.byref(tm))
@@ -327,16 +368,19 @@ class V2BpfBackend(DeviceRuleBackend):
                chained=chained.value, rules=len(rules))
 
     def allowed(self, cgdir):
-        """What the kernel enforces: the xlated instructions of every attached program of ours,
-        evaluated by the interpreter; a pair counts only if all of them grant it. A program that
-        systemd or the runtime swapped out reads as "nothing granted", so the reconciler
-        re-installs it. A foreign program attached next to ours (systemd re-realising its unit)
-        can veto any access under BPF_F_ALLOW_MULTI, so its own verdict is evaluated too: with
-        the unit's DeviceAllow= kept in step (node/systemd.py) it grants our nodes; otherwise the
-        pair reads as missing and the re-install wraps that program.
+        """What the kernel enforces, read back from it: for a set-mode program of ours the
+        contents of its allow-set map (one native call); for a straight-line one its xlated
+        instructions, evaluated by the interpreter. A pair counts only if every program of ours
+        grants it. A program that systemd or the runtime swapped out reads as "nothing granted",
+        so the reconciler re-installs it. A foreign program attached next to ours (systemd
+        re-realising its unit) can veto any access under BPF_F_ALLOW_MULTI, so its own verdict
+        is evaluated too: with the unit's DeviceAllow= kept in step (node/systemd.py) it grants
+        our nodes; otherwise the pair reads as missing and the re-install wraps that program.
 
-        Fast path: when the attached id list is exactly the one this backend installed, the
-        answer is the rule set it compiled into that program (see ``_installed``)."""
+        Fast path for straight-line programs: when the attached id list is exactly the one this
+        backend installed, the answer is the rule set it compiled into that program (programs
+        are immutable; see ``_installed``). Set-mode programs keep their id while their map
+        changes, so their set is always read."""
         known = self._installed.get(cgdir)
         if known is not None:
             try:
@@ -345,12 +389,21 @@ class V2BpfBackend(DeviceRuleBackend):
             except CgroupError:
                 pass
             self._installed.pop(cgdir, None)
-        progs, foreign = attached_programs(cgdir)
-        if not progs:
+        grants: List[Set[Tuple[int, int]]] = []
+        while True:
+            kind, pairs = _set_at(cgdir, len(grants))
+            if kind is None:
+                break
+            if kind == "code":
+                prog, _ = _program_at(cgdir, len(grants))
+                pairs = program_allows(prog) if prog is not None else set()
+            grants.append(pairs)
+        if not grants:
             return set()
-        out = program_allows(progs[0])
-        for p in progs[1:]:
-            out &= program_allows(p)
+        out = grants[0]
+        for g in grants[1:]:
+            out &= g
+        foreign = _program_at(cgdir, 0, foreign_only=True)[1] if out else 0
         for i in range(foreign):
             prog, _ = _program_at(cgdir, i, foreign_only=True)
             if prog is None:
@@ -360,6 +413,30 @@ class V2BpfBackend(DeviceRuleBackend):
             except bpfvm.BpfError:
                 return set()                   # cannot judge it: assume it vetoes
         return out
+
+
+def _set_at(cgdir: str, index: int):
+    """("set", rw char pairs) for a set-mode program of ours at ``index``, ("code", None) for a
+    straight-line one, (None, None) past the last."""
+    lib = _native.host()
+    cap = 64
+    while True:
+        ent = (C.c_uint32 * (4 * cap))()
+        n, pid = C.c_uint32(0), C.c_uint32(0)
+        rc = lib.gm_bpf_dev_set_at(cgdir.encode(), index, ent, cap, C.byref(n), C.byref(pid))
+        if rc == -errno.ENOSPC:
+            cap = n.value + 16
+            continue
+        break
+    if rc == -errno.ENOENT:
+        return None, None
+    if rc < 0:
+        raise CgroupError(f"bpf allow-set read-back on {cgdir}: {os.strerror(-rc)}")
+    if rc == 0:
+        return "code", None
+    rw = bpfvm.ACC_READ | bpfvm.ACC_WRITE
+    return "set", {(int(ent[4 * i + 1]), int(ent[4 * i + 2])) for i in range(n.value)
+                   if ent[4 * i] == bpfvm.BPF_DEVCG_DEV_CHAR and (ent[4 * i + 3] & rw) == rw}
 
 
 def _program_at(cgdir: str, index: int, foreign_only: bool = False
@@ -411,6 +488,24 @@ def _program_allows(prog: Tuple[int, ...]) -> FrozenSet[Tuple[int, int]]:
     return frozenset(bpfvm.allowed_pairs(list(prog), [(a, b) for a in consts for b in consts]))
 
 
+@functools.lru_cache(maxsize=4)
+def _set_program_words(chained: bool = True) -> Tuple[int, ...]:
+    return tuple(build_set_program(chained))
+
+
+def build_set_program(chained: bool) -> List[int]:
+    """The set-mode program (gm_bpf_dev_build_set) with placeholder map fds (0): the allow-set
+    map is ``maps={0: ...}`` for :func:`bpfvm.run`."""
+    lib = _native.host()
+    ch = -2 if chained else -1
+    need = -lib.gm_bpf_dev_build_set(-2, None, 0, 0 if chained else 1, ch, None, 0)
+    buf = (C.c_uint64 * need)()
+    n = lib.gm_bpf_dev_build_set(-2, None, 0, 0 if chained else 1, ch, buf, need)
+    if n < 0:
+        raise CgroupError("bpf set program build failed")
+    return [int(buf[i]) for i in range(n)]
+
+
 def build_program(nodes: Sequence[DeviceNode], chained: bool) -> List[int]:
     rules = rules_for(nodes, allow=True)
     lib = _native.host()
@@ -436,9 +531,12 @@ class V2RecordingBackend(DeviceRuleBackend):
             if os.path.exists(path):
                 os.unlink(path)
             return
-        prog = build_program(desired, chained=True)
+        # what V2BpfBackend installs: the set-mode program and its allow-set map
         state = {"rules": [[n.major, n.minor, n.path] for n in desired],
-                 "chained": "runtime-default", "insns": [f"{i:016x}" for i in prog]}
+                 "chained": "runtime-default", "mode": "set",
+                 "set": [[bpfvm.BPF_DEVCG_DEV_CHAR, n.major, n.minor,
+                          bpfvm.ACC_READ | bpfvm.ACC_WRITE] for n in desired],
+                 "insns": [f"{i:016x}" for i in _set_program_words()]}
         blob = json.dumps(state).encode()
         tmp = path + ".tmp"
         with open(tmp, "wb") as fh:
@@ -464,8 +562,14 @@ class V2RecordingBackend(DeviceRuleBackend):
         if known is not None and known[0] == blob:
             return set(known[1])
         st = json.loads(blob)
-        # evaluate the recorded program itself (same check the real backend runs on xlated code)
-        return program_allows([int(x, 16) for x in st["insns"]])
+        prog = [int(x, 16) for x in st["insns"]]
+        if st.get("mode") != "set":       # recorded by an older worker: a straight-line program
+            return program_allows(prog)
+        # evaluate the recorded program against its recorded map (the runtime's program, which
+        # it tail-calls, is not consulted: only what gpumounter grants counts)
+        table = {(t, ma, mi): acc for t, ma, mi, acc in st["set"]}
+        return bpfvm.allowed_pairs(prog, sorted({(k[1], k[2]) for k in table}),
+                                   chained=lambda *a: 0, maps={0: table})
 
 
 def make_backend(mode: str, emulate: bool, bpf_pin_dir: str = "") -> DeviceRuleBackend:

@@ -191,6 +191,10 @@ class SystemdPersistingBackend(DeviceRuleBackend):
     def allowed(self, cgdir):
         return self.inner.allowed(cgdir)
 
+    def sweep_pins(self, cgroup_root: str):
+        sweep = getattr(self.inner, "sweep_pins", None)
+        return sweep(cgroup_root) if sweep is not None else []
+
 
 def maybe_wrap(backend: DeviceRuleBackend, mode: str, bus_path: str,
                driver: str) -> DeviceRuleBackend:

@@ -273,6 +273,15 @@ class Reconciler:
         for name in list(self._first_seen):
             if not any(p["metadata"]["name"] == name for p in placeholders):
                 del self._first_seen[name]
+        sweep = getattr(svc.hm.backend, "sweep_pins", None)
+        if sweep is not None:
+            try:
+                gone = sweep(svc.hm.resolver.root)
+            except Exception as e:  # noqa: BLE001
+                rep.errors.append(f"bpf pin sweep: {e}")
+            else:
+                if gone:
+                    m.reconcile_actions.labels(action="unpin").inc(len(gone))
         self.last = rep
         if rep.owner_gone or rep.stuck or rep.repaired or rep.revoked or rep.errors:
             log.kv(_log, 20, "reconciled", **rep.to_dict())

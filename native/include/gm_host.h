@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define GM_HOST_ABI_VERSION 4
+#define GM_HOST_ABI_VERSION 5
 
 // Access bits follow BPF_DEVCG_ACC_* so the same rule feeds both cgroup versions.
 #define GM_ACC_MKNOD 1
@@ -52,6 +52,14 @@ int gm_cg1_format_rule(const gm_dev_rule_t* rule, char* out, int cap);
 // Returns instruction count, or -(needed) if cap is too small, or -EINVAL.
 int gm_bpf_dev_build(const gm_dev_rule_t* rules, int n, int default_allow, int chain_map_fd,
                      uint64_t* out, int cap);
+// Set-mode program: allows an access if {dev type, major, minor} is in the HASH map
+// `set_map_fd` (key 3×u32: BPF_DEVCG_DEV_*, major, minor; value: u32 GM_ACC_* bits that are
+// allowed) with every requested access bit; otherwise it evaluates `base` rules (the runtime's
+// default list when the chain is lost), tail-calls the chain map like gm_bpf_dev_build and
+// finally returns `default_allow`. The program does not grow with the number of devices. -2 for
+// either fd emits placeholders (offline inspection). Returns the count, -(needed) or -EINVAL.
+int gm_bpf_dev_build_set(int set_map_fd, const gm_dev_rule_t* base, int nbase, int default_allow,
+                         int chain_map_fd, uint64_t* out, int cap);
 // Loads instructions as a CGROUP_DEVICE program named `name`. Returns prog fd or -errno;
 // verifier log (if any) is copied to `log`.
 int gm_bpf_dev_load(const uint64_t* insns, int n, const char* name, char* log, int logcap);
@@ -71,7 +79,11 @@ int gm_bpf_dev_program(const char* cgroup_path, uint64_t* insns, uint32_t cap, u
 int gm_bpf_dev_program_at(const char* cgroup_path, uint32_t index, int foreign_only,
                           uint64_t* insns, uint32_t cap, uint32_t* n, uint32_t* prog_id,
                           uint32_t* foreign);
-// Installs (or updates) the gpumounter allow-list on a cgroup-v2 directory. Every attached
+// Installs (or updates) the gpumounter allow-list on a cgroup-v2 directory. Exact allow rules
+// (every hot-mount) use set mode: the rules go into a HASH map shared by the cgroup's
+// gpumounter programs (gm_bpf_dev_build_set), so once a cgroup is wrapped an update is a map
+// sync without loading or attaching anything; other rule lists compile a straight-line
+// program (gm_bpf_dev_build). Every attached
 // program is wrapped, because under BPF_F_ALLOW_MULTI each one must allow an access (runc and
 // systemd both attach one on systemd-driver hosts):
 //   * a program of ours → replaced, chaining to the same original program;
@@ -95,6 +107,12 @@ void gm_bpf_dev_last_timing(gm_bpf_timing_t* out);
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
                        const gm_dev_rule_t* base, int nbase, const char* pin_dir,
                        uint32_t* prog_id, uint32_t* chained_id);
+// The allow set of the index-th gpumounter program on the cgroup, as entries of 4 u32 (type,
+// major, minor, access bits). Returns 1 (set-mode program, *n entries), 0 (a straight-line
+// program: read it with gm_bpf_dev_program_at), -ENOENT past the last one, -ENOSPC (*n =
+// needed) or -errno.
+int gm_bpf_dev_set_at(const char* cgroup_path, uint32_t index, uint32_t* entries, uint32_t cap,
+                      uint32_t* n, uint32_t* prog_id);
 // Removes our programs, re-attaching each chained original in its place (if any), and unpins.
 // Returns how many were removed.
 int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir);

@@ -99,6 +99,55 @@ constexpr uint8_t JNE_K = BPF_JMP | BPF_JNE | BPF_K;
 constexpr uint8_t CALL = BPF_JMP | BPF_CALL;
 constexpr uint8_t EXIT = BPF_JMP | BPF_EXIT;
 constexpr uint8_t LD_IMM64 = BPF_LD | BPF_DW | BPF_IMM;
+constexpr uint8_t STX_W = BPF_STX | BPF_MEM | BPF_W;
+constexpr uint8_t ADD64_K = BPF_ALU64 | BPF_ADD | BPF_K;
+constexpr uint8_t XOR64_K = BPF_ALU64 | BPF_XOR | BPF_K;
+constexpr uint8_t JEQ_K = BPF_JMP | BPF_JEQ | BPF_K;
+
+// r2 = access_type; r3 = r2 & 0xffff (dev type); r2 >>= 16 (access); r4 = major; r5 = minor,
+// from the context in r1. Returns the next index.
+int emit_ctx_load(uint64_t* out, int k) {
+  out[k++] = insn(LDX_W, 2, 1, 0, 0);
+  out[k++] = insn(MOV64_X, 3, 2, 0, 0);
+  out[k++] = insn(AND64_K, 3, 0, 0, 0xffff);
+  out[k++] = insn(RSH64_K, 2, 0, 0, 16);
+  out[k++] = insn(LDX_W, 4, 1, 4, 0);
+  out[k++] = insn(LDX_W, 5, 1, 8, 0);
+  return k;
+}
+
+int rule_block_len(const gm_dev_rule_t& r);
+
+// One block per rule (first match wins): matching → return allow/deny, else fall through to
+// the next block. Expects emit_ctx_load's registers. Returns the next index or -EINVAL.
+int emit_rule_blocks(const gm_dev_rule_t* rules, int n, uint64_t* out, int k) {
+  for (int i = 0; i < n; ++i) {
+    const gm_dev_rule_t& r = rules[i];
+    const int start = k;
+    const int end = start + rule_block_len(r);  // index of first insn after this block
+    auto jne = [&](int reg, int32_t imm) {
+      int16_t off = (int16_t)(end - (k + 1));
+      out[k] = insn(JNE_K, (uint8_t)reg, 0, off, imm);
+      ++k;
+    };
+    if (r.type != 'a') jne(3, r.type == 'c' ? BPF_DEVCG_DEV_CHAR : BPF_DEVCG_DEV_BLOCK);
+    if ((r.access & 7) != 7) {
+      // requested access must be a subset of the rule's: (req & ~rule) == 0
+      out[k++] = insn(MOV64_X, 0, 2, 0, 0);
+      out[k++] = insn(AND64_K, 0, 0, 0, (int32_t)(~r.access & 7));
+      // jne r0, 0 → next rule
+      int16_t off = (int16_t)(end - (k + 1));
+      out[k] = insn(JNE_K, 0, 0, off, 0);
+      ++k;
+    }
+    if (r.major >= 0) jne(4, r.major);
+    if (r.minor >= 0) jne(5, r.minor);
+    out[k++] = insn(MOV64_K, 0, 0, 0, r.allow ? 1 : 0);
+    out[k++] = insn(EXIT, 0, 0, 0, 0);
+    if (k != end) return -EINVAL;  // layout bug guard (see rule_block_len)
+  }
+  return k;
+}
 
 int rule_block_len(const gm_dev_rule_t& r) {
   int n = 2;  // mov r0, allow; exit
@@ -295,22 +344,127 @@ int attach(int cgfd, int prog_fd, int replace_fd, uint32_t existing_flags) {
   return sys_bpf(BPF_PROG_ATTACH, &a, sizeof(a)) < 0 ? -errno : 0;
 }
 
-bool is_ours(uint32_t id, uint32_t* chained_id) {
+int map_info(int fd, struct bpf_map_info* info) {
+  memset(info, 0, sizeof(*info));
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.info.bpf_fd = (uint32_t)fd;
+  a.info.info_len = sizeof(*info);
+  a.info.info = ptr_u64(info);
+  return sys_bpf(BPF_OBJ_GET_INFO_BY_FD, &a, sizeof(a)) < 0 ? -errno : 0;
+}
+
+// Ours = named kProgName. *chained_id: the program in slot 0 of its PROG_ARRAY (0 if none);
+// *set_map_id: its allow-set HASH map (set-mode program, see gm_bpf_dev_build_set), 0 for a
+// straight-line program.
+bool is_ours(uint32_t id, uint32_t* chained_id, uint32_t* set_map_id = nullptr,
+             bool* has_chain_map = nullptr) {
   Fd pfd(get_prog_fd_by_id(id));
   if (!pfd.ok()) return false;
   struct bpf_prog_info info;
   uint32_t maps[4] = {0};
   if (prog_info(pfd.fd, &info, maps, 4) != 0) return false;
   if (strncmp(info.name, kProgName, sizeof(info.name)) != 0) return false;
-  if (chained_id) {
-    *chained_id = 0;
-    if (info.nr_map_ids >= 1) {
-      Fd mfd(map_fd_by_id(maps[0]));
+  if (chained_id) *chained_id = 0;
+  if (set_map_id) *set_map_id = 0;
+  if (has_chain_map) *has_chain_map = false;
+  if (!chained_id && !set_map_id && !has_chain_map) return true;
+  for (uint32_t i = 0; i < info.nr_map_ids && i < 4; ++i) {
+    Fd mfd(map_fd_by_id(maps[i]));
+    struct bpf_map_info mi;
+    if (!mfd.ok() || map_info(mfd.fd, &mi) != 0) continue;
+    if (mi.type == BPF_MAP_TYPE_PROG_ARRAY) {
+      if (has_chain_map) *has_chain_map = true;
       uint32_t pid = 0;
-      if (mfd.ok() && prog_array_slot0(mfd.fd, &pid) == 0) *chained_id = pid;
+      if (chained_id && prog_array_slot0(mfd.fd, &pid) == 0) *chained_id = pid;
+    } else if (mi.type == BPF_MAP_TYPE_HASH && set_map_id) {
+      *set_map_id = mi.id;
     }
   }
   return true;
+}
+
+// ---- allow-set map (set-mode programs) --------------------------------------------------------
+// key = {dev type (BPF_DEVCG_DEV_*), major, minor}, value = allowed access bits (GM_ACC_*).
+struct SetKey {
+  uint32_t type, major, minor;
+};
+constexpr uint32_t kSetMax = 512;
+
+int make_set_map() {
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.map_type = BPF_MAP_TYPE_HASH;
+  a.key_size = sizeof(SetKey);
+  a.value_size = 4;
+  a.max_entries = kSetMax;
+  snprintf(a.map_name, sizeof(a.map_name), "gm_devset");
+  long fd = sys_bpf(BPF_MAP_CREATE, &a, sizeof(a));
+  return fd < 0 ? -errno : (int)fd;
+}
+
+int set_keys(int map_fd, std::vector<SetKey>* keys) {
+  keys->clear();
+  SetKey cur{}, next{};
+  bool first = true;
+  for (uint32_t guard = 0; guard <= kSetMax; ++guard) {
+    union bpf_attr a;
+    memset(&a, 0, sizeof(a));
+    a.map_fd = (uint32_t)map_fd;
+    a.key = first ? 0 : ptr_u64(&cur);
+    a.next_key = ptr_u64(&next);
+    if (sys_bpf(BPF_MAP_GET_NEXT_KEY, &a, sizeof(a)) < 0) return errno == ENOENT ? 0 : -errno;
+    keys->push_back(next);
+    cur = next;
+    first = false;
+  }
+  return -E2BIG;
+}
+
+int set_op(int cmd, int map_fd, const SetKey& k, uint32_t* value) {
+  union bpf_attr a;
+  memset(&a, 0, sizeof(a));
+  a.map_fd = (uint32_t)map_fd;
+  a.key = ptr_u64(&k);
+  if (value) a.value = ptr_u64(value);
+  if (cmd == BPF_MAP_UPDATE_ELEM) a.flags = BPF_ANY;
+  return sys_bpf(cmd, &a, sizeof(a)) < 0 ? -errno : 0;
+}
+
+SetKey key_of(const gm_dev_rule_t& r) {
+  return SetKey{r.type == 'b' ? (uint32_t)BPF_DEVCG_DEV_BLOCK : (uint32_t)BPF_DEVCG_DEV_CHAR,
+                (uint32_t)r.major, (uint32_t)r.minor};
+}
+
+// Exact allow rules only (no wildcards, no denies): what a set-mode program can hold.
+bool set_eligible(const gm_dev_rule_t* rules, int n) {
+  for (int i = 0; i < n; ++i) {
+    const gm_dev_rule_t& r = rules[i];
+    if (!r.allow || (r.type != 'c' && r.type != 'b') || r.major < 0 || r.minor < 0) return false;
+  }
+  return n <= (int)kSetMax;
+}
+
+// Makes the map hold exactly `rules`: new and changed entries first, then stale ones deleted,
+// so a device granted before and after is never denied in between.
+int sync_set(int map_fd, const gm_dev_rule_t* rules, int n) {
+  std::vector<SetKey> have;
+  int e = set_keys(map_fd, &have);
+  if (e < 0) return e;
+  for (int i = 0; i < n; ++i) {
+    uint32_t acc = rules[i].access & 7;
+    if ((e = set_op(BPF_MAP_UPDATE_ELEM, map_fd, key_of(rules[i]), &acc)) < 0) return e;
+  }
+  for (const SetKey& k : have) {
+    bool keep = false;
+    for (int i = 0; i < n && !keep; ++i) {
+      SetKey w = key_of(rules[i]);
+      keep = w.type == k.type && w.major == k.major && w.minor == k.minor;
+    }
+    if (!keep && (e = set_op(BPF_MAP_DELETE_ELEM, map_fd, k, nullptr)) < 0 && e != -ENOENT)
+      return e;
+  }
+  return 0;
 }
 
 // ------------------------------------------------------------------ device nodes
@@ -793,42 +947,69 @@ int gm_bpf_dev_build(const gm_dev_rule_t* rules, int n, int default_allow, int c
   need += 2;                          // default: mov r0 + exit
   if (!out || cap < need) return -need;
 
-  int k = 0;
-  // r2 = access_type; r3 = r2 & 0xffff (dev type); r2 >>= 16 (access); r4 = major; r5 = minor
-  out[k++] = insn(LDX_W, 2, 1, 0, 0);
-  out[k++] = insn(MOV64_X, 3, 2, 0, 0);
-  out[k++] = insn(AND64_K, 3, 0, 0, 0xffff);
-  out[k++] = insn(RSH64_K, 2, 0, 0, 16);
-  out[k++] = insn(LDX_W, 4, 1, 4, 0);
-  out[k++] = insn(LDX_W, 5, 1, 8, 0);
-
-  for (int i = 0; i < n; ++i) {
-    const gm_dev_rule_t& r = rules[i];
-    const int start = k;
-    const int end = start + rule_block_len(r);  // index of first insn after this block
-    auto jne = [&](int reg, int32_t imm) {
-      int16_t off = (int16_t)(end - (k + 1));
-      out[k] = insn(JNE_K, (uint8_t)reg, 0, off, imm);
-      ++k;
-    };
-    if (r.type != 'a') jne(3, r.type == 'c' ? BPF_DEVCG_DEV_CHAR : BPF_DEVCG_DEV_BLOCK);
-    if ((r.access & 7) != 7) {
-      // requested access must be a subset of the rule's: (req & ~rule) == 0
-      out[k++] = insn(MOV64_X, 0, 2, 0, 0);
-      out[k++] = insn(AND64_K, 0, 0, 0, (int32_t)(~r.access & 7));
-      // jne r0, 0 → next rule
-      int16_t off = (int16_t)(end - (k + 1));
-      out[k] = insn(JNE_K, 0, 0, off, 0);
-      ++k;
-    }
-    if (r.major >= 0) jne(4, r.major);
-    if (r.minor >= 0) jne(5, r.minor);
-    out[k++] = insn(MOV64_K, 0, 0, 0, r.allow ? 1 : 0);
-    out[k++] = insn(EXIT, 0, 0, 0, 0);
-    if (k != end) return -EINVAL;  // layout bug guard (see rule_block_len)
-  }
+  int k = emit_ctx_load(out, 0);
+  k = emit_rule_blocks(rules, n, out, k);
+  if (k < 0) return k;
   if (chain_map_fd != -1) {
     // r1 still holds ctx. r2 = &prog_array (pseudo map fd), r3 = 0, call bpf_tail_call.
+    const int32_t mfd = chain_map_fd >= 0 ? chain_map_fd : 0;
+    out[k++] = insn(LD_IMM64, 2, BPF_PSEUDO_MAP_FD, 0, mfd);
+    out[k++] = insn(0, 0, 0, 0, 0);
+    out[k++] = insn(MOV64_K, 3, 0, 0, 0);
+    out[k++] = insn(CALL, 0, 0, 0, BPF_FUNC_tail_call);
+  }
+  out[k++] = insn(MOV64_K, 0, 0, 0, default_allow ? 1 : 0);
+  out[k++] = insn(EXIT, 0, 0, 0, 0);
+  return k;
+}
+
+int gm_bpf_dev_build_set(int set_map_fd, const gm_dev_rule_t* base, int nbase, int default_allow,
+                         int chain_map_fd, uint64_t* out, int cap) {
+  if (nbase < 0 || (nbase > 0 && !base)) return -EINVAL;
+  int need = 23 + 1;  // lookup + verdict, then r1 = ctx at the miss label
+  if (nbase > 0) {
+    need += 6;
+    for (int i = 0; i < nbase; ++i) need += rule_block_len(base[i]);
+  }
+  if (chain_map_fd != -1) need += 4;
+  need += 2;
+  if (!out || cap < need) return -need;
+  int k = 0;
+  const int32_t smfd = set_map_fd >= 0 ? set_map_fd : 0;
+  out[k++] = insn(MOV64_X, 6, 1, 0, 0);           // r6 = ctx (callee-saved)
+  out[k++] = insn(LDX_W, 2, 6, 0, 0);             // r2 = access_type
+  out[k++] = insn(MOV64_X, 3, 2, 0, 0);
+  out[k++] = insn(AND64_K, 3, 0, 0, 0xffff);      // r3 = dev type
+  out[k++] = insn(MOV64_X, 7, 2, 0, 0);
+  out[k++] = insn(RSH64_K, 7, 0, 0, 16);          // r7 = requested access
+  out[k++] = insn(STX_W, 10, 3, -12, 0);          // key.type
+  out[k++] = insn(LDX_W, 4, 6, 4, 0);
+  out[k++] = insn(STX_W, 10, 4, -8, 0);           // key.major
+  out[k++] = insn(LDX_W, 5, 6, 8, 0);
+  out[k++] = insn(STX_W, 10, 5, -4, 0);           // key.minor
+  out[k++] = insn(LD_IMM64, 1, BPF_PSEUDO_MAP_FD, 0, smfd);
+  out[k++] = insn(0, 0, 0, 0, 0);
+  out[k++] = insn(MOV64_X, 2, 10, 0, 0);
+  out[k++] = insn(ADD64_K, 2, 0, 0, -12);         // r2 = &key
+  out[k++] = insn(CALL, 0, 0, 0, BPF_FUNC_map_lookup_elem);
+  const int miss = 23;
+  out[k] = insn(JEQ_K, 0, 0, (int16_t)(miss - (k + 1)), 0);  // not in the set
+  ++k;
+  out[k++] = insn(LDX_W, 1, 0, 0, 0);             // r1 = allowed access
+  out[k++] = insn(XOR64_K, 1, 0, 0, -1);
+  out[k++] = insn(BPF_ALU64 | BPF_AND | BPF_X, 1, 7, 0, 0);  // requested & ~allowed
+  out[k] = insn(JNE_K, 1, 0, (int16_t)(miss - (k + 1)), 0);
+  ++k;
+  out[k++] = insn(MOV64_K, 0, 0, 0, 1);
+  out[k++] = insn(EXIT, 0, 0, 0, 0);
+  if (k != miss) return -EINVAL;
+  out[k++] = insn(MOV64_X, 1, 6, 0, 0);           // r1 = ctx again
+  if (nbase > 0) {  // chain lost: the runtime's default list, compiled in
+    k = emit_ctx_load(out, k);
+    k = emit_rule_blocks(base, nbase, out, k);
+    if (k < 0) return k;
+  }
+  if (chain_map_fd != -1) {
     const int32_t mfd = chain_map_fd >= 0 ? chain_map_fd : 0;
     out[k++] = insn(LD_IMM64, 2, BPF_PSEUDO_MAP_FD, 0, mfd);
     out[k++] = insn(0, 0, 0, 0, 0);
@@ -971,21 +1152,33 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
   tm.query_ns += t1 - t0;
 
   // One slot per attached program. Under BPF_F_ALLOW_MULTI every program must allow an access,
-  // so each one is wrapped: ours (rules → allow, else tail-call the original). A program of ours
-  // is re-generated around the original it already wraps. With nothing attached, one slot with
-  // default-allow (the cgroup was unrestricted).
+  // so each one is wrapped: ours (rules → allow, else tail-call the original). With nothing
+  // attached, one slot with default-allow (the cgroup was unrestricted).
+  //
+  // Set mode (exact allow rules, the attach path): the rules live in a HASH map the program
+  // looks up, shared by every wrapper of the cgroup. Once wrapped, an attach or detach is a
+  // map update — no program load, verification or attach — and the verifier sees the same
+  // short program whatever the number of GPUs. A straight-line program of ours (older worker,
+  // or rules a set cannot hold) is replaced.
+  const bool set_mode = set_eligible(rules, n);
   struct Slot {
-    uint32_t replace_id = 0, chain_id = 0;
-    bool ours_without_chain = false;
+    uint32_t replace_id = 0, chain_id = 0, set_id = 0;
+    bool ours = false, ours_without_chain = false, chain_lost = false;
   };
   std::vector<Slot> slots;
   for (uint32_t id : at.ids) {
     Slot sl;
-    uint32_t c = 0;
+    uint32_t c = 0, m = 0;
+    bool has_chain = false;
     sl.replace_id = id;
-    if (is_ours(id, &c)) {
+    if (is_ours(id, &c, &m, &has_chain)) {
+      sl.ours = true;
       sl.chain_id = c;
+      sl.set_id = m;
       sl.ours_without_chain = (c == 0);
+      // its PROG_ARRAY slot is empty: the map was neither pinned nor held open (a restart
+      // without bpffs), so the tail call to the runtime's program now falls through
+      sl.chain_lost = has_chain && c == 0;
     } else {
       sl.chain_id = id;
     }
@@ -995,8 +1188,34 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
   if (slots.size() > 1 && !(at.flags & BPF_F_ALLOW_MULTI)) return -EINVAL;  // impossible state
 
   std::vector<uint32_t> chains;
+  Fd set_map;
+  if (set_mode) {
+    // the cgroup's set: the one our programs already look up (a later one would be a leftover
+    // of a partial install and is re-synced too), else a new one
+    for (const Slot& sl : slots)
+      if (sl.set_id && !set_map.ok()) set_map = Fd(map_fd_by_id(sl.set_id));
+    if (!set_map.ok()) set_map = Fd(make_set_map());
+    if (!set_map.ok()) return set_map.fd;
+    if ((e = sync_set(set_map.fd, rules, n)) < 0) return e;
+    struct bpf_map_info mi;
+    const uint32_t chosen = map_info(set_map.fd, &mi) == 0 ? mi.id : 0;
+    for (const Slot& sl : slots) {
+      if (sl.set_id && sl.set_id != chosen) {
+        Fd other(map_fd_by_id(sl.set_id));
+        if (other.ok() && (e = sync_set(other.fd, rules, n)) < 0) return e;
+      }
+    }
+  }
+  uint64_t t2 = mono_ns();
+  tm.map_ns += t2 - t1;
+
   uint32_t first_prog = 0;
   for (const Slot& sl : slots) {
+    if (set_mode && sl.set_id && !sl.chain_lost) {  // a set-mode wrapper: the sync installed
+      if (sl.chain_id) chains.push_back(sl.chain_id);
+      if (!first_prog) first_prog = sl.replace_id;
+      continue;
+    }
     Fd chain_prog, chain_map, replace_fd;
     t0 = mono_ns();
     if (sl.chain_id) {
@@ -1009,19 +1228,27 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
       replace_fd = Fd(get_prog_fd_by_id(sl.replace_id));
       if (!replace_fd.ok()) return replace_fd.fd;
     }
-    // rules = ours, then (chain lost) the runtime's default list compiled in
-    std::vector<gm_dev_rule_t> all(rules, rules + n);
-    if (sl.ours_without_chain && base && nbase > 0) all.insert(all.end(), base, base + nbase);
     // With a chained original (or a compiled-in base list) the fall-through is deny; with
     // neither the cgroup was unrestricted, so default-allow keeps that behaviour.
     const int default_allow = (sl.chain_id || sl.ours_without_chain) ? 0 : 1;
+    const gm_dev_rule_t* b = sl.ours_without_chain ? base : nullptr;
+    const int nb = sl.ours_without_chain && base ? nbase : 0;
     t1 = mono_ns();
     tm.map_ns += t1 - t0;
-    std::vector<uint64_t> prog(16 + all.size() * 12);
-    int cnt = gm_bpf_dev_build(all.data(), (int)all.size(), default_allow,
-                               chain_map.ok() ? chain_map.fd : -1, prog.data(), (int)prog.size());
+    std::vector<uint64_t> prog(48 + (n + nb) * 12);
+    int cnt;
+    if (set_mode) {
+      cnt = gm_bpf_dev_build_set(set_map.fd, b, nb, default_allow,
+                                 chain_map.ok() ? chain_map.fd : -1, prog.data(), (int)prog.size());
+    } else {
+      // rules = ours, then (chain lost) the runtime's default list compiled in
+      std::vector<gm_dev_rule_t> all(rules, rules + n);
+      if (nb) all.insert(all.end(), b, b + nb);
+      cnt = gm_bpf_dev_build(all.data(), (int)all.size(), default_allow,
+                             chain_map.ok() ? chain_map.fd : -1, prog.data(), (int)prog.size());
+    }
     if (cnt < 0) return -EINVAL;
-    uint64_t t2 = mono_ns();
+    t2 = mono_ns();
     tm.build_ns += t2 - t1;
     // No verifier log on the hot path: log_level 1 makes the verifier print every instruction
     // of every explored path, which costs more than the verification itself. The program is
@@ -1053,6 +1280,44 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
   if (prog_id) *prog_id = first_prog;
   if (chained_id) *chained_id = slots[0].chain_id;
   return (int)slots.size();
+}
+
+int gm_bpf_dev_set_at(const char* cgroup_path, uint32_t index, uint32_t* entries, uint32_t cap,
+                      uint32_t* n, uint32_t* prog_id) {
+  *n = 0;
+  if (prog_id) *prog_id = 0;
+  Fd cg(open(cgroup_path, O_RDONLY | O_DIRECTORY | O_CLOEXEC));
+  if (!cg.ok()) return -errno;
+  Attached at;
+  int e = query(cg.fd, &at);
+  if (e < 0) return e;
+  uint32_t k = 0;
+  for (uint32_t id : at.ids) {
+    uint32_t set_id = 0;
+    if (!is_ours(id, nullptr, &set_id)) continue;
+    if (k++ != index) continue;
+    if (prog_id) *prog_id = id;
+    if (!set_id) return 0;  // a straight-line program: read its xlated code instead
+    Fd m(map_fd_by_id(set_id));
+    if (!m.ok()) return m.fd;
+    std::vector<SetKey> keys;
+    if ((e = set_keys(m.fd, &keys)) < 0) return e;
+    uint32_t out = 0;
+    for (const SetKey& key : keys) {
+      uint32_t acc = 0;
+      if (set_op(BPF_MAP_LOOKUP_ELEM, m.fd, key, &acc) < 0) continue;  // deleted meanwhile
+      if (out < cap && entries) {
+        entries[out * 4 + 0] = key.type;
+        entries[out * 4 + 1] = key.major;
+        entries[out * 4 + 2] = key.minor;
+        entries[out * 4 + 3] = acc;
+      }
+      ++out;
+    }
+    *n = out;
+    return out > cap ? -ENOSPC : 1;
+  }
+  return -ENOENT;
 }
 
 int gm_bpf_dev_restore(const char* cgroup_path, const char* pin_dir) {

@@ -133,3 +133,57 @@ def test_program_allows_reads_grants_back_from_raw_and_xlated_code():
     gpu_keys = {(226, m) for m in range(256)} | {(511, 0)}
     for p in (prog, _as_xlated(prog)):
         assert program_allows(p) & gpu_keys == want
+
+
+# ------------------------------------------------------------------ set-mode program
+def build_set(base=(), default_allow=0, chain=-1):
+    arr = _rule_array([_native.DevRule(t.encode(), acc, allow, 0, ma, mi)
+                       for t, acc, allow, ma, mi in base])
+    lib = _native.host()
+    need = -lib.gm_bpf_dev_build_set(-2, arr, len(base), default_allow, chain, None, 0)
+    buf = (C.c_uint64 * need)()
+    n = lib.gm_bpf_dev_build_set(-2, arr, len(base), default_allow, chain, buf, need)
+    assert n == need
+    return [int(buf[i]) for i in range(n)]
+
+
+SET_KEYS = st.tuples(st.sampled_from([bpfvm.BPF_DEVCG_DEV_CHAR, bpfvm.BPF_DEVCG_DEV_BLOCK]),
+                     st.sampled_from([1, 226, 511]), st.sampled_from([0, 3, 128, 130]))
+
+
+@settings(max_examples=150, deadline=None)
+@given(entries=st.dictionaries(SET_KEYS, st.integers(1, 7), max_size=6),
+       dev_type=st.sampled_from([bpfvm.BPF_DEVCG_DEV_CHAR, bpfvm.BPF_DEVCG_DEV_BLOCK]),
+       access=st.integers(1, 7), major=st.sampled_from([1, 226, 511, 7]),
+       minor=st.sampled_from([0, 3, 128, 130, 9]), chained=st.booleans(),
+       default_allow=st.integers(0, 1))
+def test_set_program_matches_the_set_semantics(entries, dev_type, access, major, minor, chained,
+                                               default_allow):
+    """An access is allowed iff {type, major, minor} is in the allow set with every requested
+    access bit; otherwise the runtime's chained program decides (or the default verdict). The
+    program is the same whatever the set holds."""
+    prog = build_set(default_allow=default_allow, chain=-2 if chained else -1)
+    got = bpfvm.run(prog, dev_type, access, major, minor,
+                    chained=bpfvm.runtime_default if chained else None, maps={0: entries})
+    acc = entries.get((dev_type, major, minor))
+    if acc is not None and access & ~acc == 0:
+        want = 1
+    elif chained:
+        want = bpfvm.runtime_default(dev_type, access, major, minor)
+    else:
+        want = default_allow
+    assert got == want
+
+
+def test_set_program_with_lost_chain_compiles_the_base_list_in():
+    base = [("c", 7, 1, 1, 3), ("c", 1, 1, -1, -1)]      # /dev/null rwm; mknod of any char
+    prog = build_set(base=base, default_allow=0, chain=-1)
+    table = {(bpfvm.BPF_DEVCG_DEV_CHAR, 226, 128): 6}
+    rw = bpfvm.ACC_READ | bpfvm.ACC_WRITE
+    assert bpfvm.run(prog, bpfvm.BPF_DEVCG_DEV_CHAR, rw, 226, 128, maps={0: table}) == 1
+    assert bpfvm.run(prog, bpfvm.BPF_DEVCG_DEV_CHAR, rw, 1, 3, maps={0: table}) == 1   # base
+    assert bpfvm.run(prog, bpfvm.BPF_DEVCG_DEV_CHAR, bpfvm.ACC_MKNOD, 226, 129,
+                     maps={0: table}) == 1                                          # base mknod
+    assert bpfvm.run(prog, bpfvm.BPF_DEVCG_DEV_CHAR, rw, 226, 129, maps={0: table}) == 0
+    # length: one lookup whatever the set, versus one block per device for a straight line
+    assert len(build_set()) < len(build([("c", 6, 1, 226, 128 + i) for i in range(4)]))

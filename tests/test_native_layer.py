@@ -215,9 +215,11 @@ def test_v2_recording_backend_program_semantics(tmp_path, mock_inventory):
     be = V2RecordingBackend()
     be.apply(ctr.cgroup_dir, NODES, [], NODES)
     st = json.load(open(os.path.join(ctr.cgroup_dir, "gm.bpf.json")))
+    assert st["mode"] == "set"
     prog = [int(x, 16) for x in st["insns"]]
+    table = {tuple(e[:3]): e[3] for e in st["set"]}
     allowed = bpfvm.allowed_pairs(prog, [(511, 0), (226, 130), (226, 2), (226, 131), (1, 3),
-                                         (1, 1)])
+                                         (1, 1)], maps={0: table})
     assert allowed == {(511, 0), (226, 130), (226, 2), (1, 3)}  # ours + runtime's /dev/null
     assert be.allowed(ctr.cgroup_dir) == {(511, 0), (226, 130), (226, 2)}
     be.apply(ctr.cgroup_dir, [], NODES, [])

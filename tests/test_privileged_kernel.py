@@ -323,26 +323,61 @@ def test_devnodes_real_mknod_via_setns(tmp_path):
         child.wait()
 
 
-def test_cgroup_v2_allowed_fast_path_tracks_attached_ids(cgroup2_child, bpffs, monkeypatch):
-    """attach verify: while the cgroup's attached id list is exactly what this backend installed,
-    allowed() answers from the rules it compiled (one BPF_PROG_QUERY, no xlated read-back) and
-    agrees with the kernel read-back; once anything else is attached it reads the kernel again."""
+def test_cgroup_v2_set_mode_updates_without_reloading(cgroup2_child, bpffs, monkeypatch):
+    """Set mode: the first install wraps the runtime's program once; later grants and revokes
+    are updates of the allow-set map (same program id, no load, no attach) that the kernel
+    enforces at once. allowed() reads the set back from the kernel (no xlated interpretation);
+    a foreign program joining (systemd re-realising the unit) is still evaluated."""
     from gpumounter_amd.node import cgroup as cgmod
 
     cg = cgroup2_child
     attach_runtime_program(cg)
     be = V2BpfBackend(bpffs)
-    be.apply(cg, [ZERO, FULL], [], [ZERO, FULL])
-    slow = cgmod.attached_programs
-    calls = []
-    monkeypatch.setattr(cgmod, "attached_programs", lambda d: calls.append(d) or slow(d))
-    fast = be.allowed(cg)
-    assert fast == {(ZERO.major, ZERO.minor), (FULL.major, FULL.minor)} and calls == []
-    be._installed.clear()                                  # the read-back agrees
-    assert be.allowed(cg) >= fast and len(calls) == 1
+    lib = _native.host()
+    be.apply(cg, [ZERO], [], [ZERO])
+    ids = be.attached_ids(cg)
+    tm = _native.BpfTiming()
+    lib.gm_bpf_dev_last_timing(C.byref(tm))
+    assert tm.programs == 1 and probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "110"
+    be.apply(cg, [FULL], [], [ZERO, FULL])
+    lib.gm_bpf_dev_last_timing(C.byref(tm))
+    assert tm.programs == 0 and be.attached_ids(cg) == ids     # a map update only
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "111"
+    interp = []
+    slow = cgmod.program_allows
+    monkeypatch.setattr(cgmod, "program_allows", lambda p: interp.append(1) or slow(p))
+    assert be.allowed(cg) == {(ZERO.major, ZERO.minor), (FULL.major, FULL.minor)}
+    assert interp == []                                      # read from the map
     be.apply(cg, [], [FULL], [ZERO])
-    assert be.allowed(cg) == {(ZERO.major, ZERO.minor)} and len(calls) == 1
-    # a foreign program joins (systemd re-realising the unit): only /dev/null, vetoes ZERO
+    assert be.attached_ids(cg) == ids and be.allowed(cg) == {(ZERO.major, ZERO.minor)}
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "110"
+    # a foreign program joins: only /dev/null, so it vetoes ZERO
     attach_runtime_program(cg, name=b"sd_devices")
-    assert (ZERO.major, ZERO.minor) not in be.allowed(cg) and len(calls) == 2
+    assert (ZERO.major, ZERO.minor) not in be.allowed(cg)
     assert probe_access(cg, [NULL.path, ZERO.path]) == "10"
+    # the re-install wraps the newcomer too, sharing the one allow set
+    be.apply(cg, [], [], [ZERO])
+    assert be.allowed(cg) == {(ZERO.major, ZERO.minor)}
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "110"
+
+
+def test_pinned_chain_maps_of_removed_cgroups_are_swept(cgroup2_child, bpffs):
+    """A container that exits while holding hot-mounted GPUs leaves its cgroup's pinned chain
+    map behind (it would keep the runtime's program loaded); the reconciler's sweep unpins it
+    and keeps the pins of live cgroups."""
+    root = os.path.dirname(cgroup2_child)
+    live, dead = cgroup2_child, os.path.join(root, "gm-dead-" + uuid.uuid4().hex[:8])
+    os.mkdir(dead)
+    be = V2BpfBackend(bpffs)
+    for cg in (live, dead):
+        attach_runtime_program(cg)
+        be.apply(cg, [ZERO], [], [ZERO])
+    ino_live, ino_dead = os.stat(live).st_ino, os.stat(dead).st_ino
+    pins = sorted(f for f in os.listdir(bpffs) if f.startswith("gm_"))
+    assert sorted(p.split("_")[1] for p in pins) == sorted([str(ino_live), str(ino_dead)])
+    os.rmdir(dead)                        # the container exited: its cgroup is gone
+    removed = be.sweep_pins(root)
+    assert [p.split("_")[1] for p in removed] == [str(ino_dead)]
+    assert [p.split("_")[1] for p in os.listdir(bpffs) if p.startswith("gm_")] == [str(ino_live)]
+    assert be.sweep_pins(root) == []
+    assert probe_access(live, [NULL.path, ZERO.path]) == "11"      # the live chain still works
