@@ -2,7 +2,8 @@
 
 Straight-line programs (one block per device, gm_bpf_dev_build) grow with the device count; the
 set-mode program (gm_bpf_dev_build_set) is one map lookup whatever the count. Median of 50
-loads each; prints one JSON line.
+loads each, then whole install/verify/restore cycles of the backend on a real cgroup2
+hierarchy in both modes (install_cycles); prints one JSON line.
 """
 from __future__ import annotations
 
@@ -60,8 +61,78 @@ def main() -> int:
     out["set_mode"] = {"insns": k, "load_ms": _median_load_ms(lib, buf, k)}
     os.close(chain)
     os.close(setm)
+    out["install_cycle"] = install_cycles(lib)
     print(json.dumps(out))
     return 0
+
+
+def install_cycles(lib, reps: int = 40) -> dict:
+    """The backend on a real cgroup2 hierarchy with a runc-style program attached: attach N
+    GPUs to a Pod that has none (wrap), read the grants back (the attach verify), detach them
+    all (restore); and growing a Pod 1 → 8 one GPU at a time. Medians in ms, both modes."""
+    import subprocess
+    import tempfile
+    import uuid
+
+    from gpumounter_amd.fakes.realnode import attach_runtime_program
+    from gpumounter_amd.models.device import DeviceNode
+    from gpumounter_amd.node.cgroup import V2BpfBackend
+
+    mnt = tempfile.mkdtemp(prefix="gm-bpfload-cg2-")
+    pins = tempfile.mkdtemp(prefix="gm-bpfload-pins-")
+    subprocess.run(["mount", "-t", "cgroup2", "none", mnt], check=True)
+    subprocess.run(["mount", "-t", "bpf", "bpf", pins], check=True)
+    cg = os.path.join(mnt, "gm-bpfload-" + uuid.uuid4().hex[:8])
+    os.mkdir(cg)
+    res = {}
+    try:
+        attach_runtime_program(cg)
+        gpu = [[DeviceNode(f"/dev/dri/renderD{128 + i}", 226, 128 + i),
+                DeviceNode(f"/dev/dri/card{i}", 226, i)] for i in range(8)]
+        kfd = DeviceNode("/dev/kfd", 511, 0)
+        for mode, straight in (("straight_line", 1), ("set_mode", 0)):
+            be = V2BpfBackend(pins, set_mode=not straight)
+            r = {}
+            for n in (1, 8):
+                want = [kfd] + [x for g in gpu[:n] for x in g]
+                att, ver, det = [], [], []
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    be.apply(cg, want, [], want)
+                    t1 = time.perf_counter()
+                    got = be.allowed(cg)
+                    t2 = time.perf_counter()
+                    be.apply(cg, [], want, [])
+                    t3 = time.perf_counter()
+                    assert {(x.major, x.minor) for x in want} <= got
+                    att.append(t1 - t0)
+                    ver.append(t2 - t1)
+                    det.append(t3 - t2)
+                r[f"attach_{n}gpu_ms"] = round(statistics.median(att) * 1e3, 4)
+                r[f"verify_{n}gpu_ms"] = round(statistics.median(ver) * 1e3, 4)
+                r[f"detach_all_{n}gpu_ms"] = round(statistics.median(det) * 1e3, 4)
+            grow = []
+            for _ in range(reps // 4):
+                have = [kfd]
+                for i in range(8):
+                    t0 = time.perf_counter()
+                    be.apply(cg, gpu[i], [], have + gpu[i])
+                    grow.append(time.perf_counter() - t0)
+                    have = have + gpu[i]
+                be.apply(cg, [], have, [])
+            r["grow_step_ms"] = round(statistics.median(grow) * 1e3, 4)
+            res[mode] = r
+    finally:
+        lib.gm_bpf_dev_straight_line(0)
+        try:
+            os.rmdir(cg)
+        except OSError:
+            pass
+        subprocess.run(["umount", pins], check=False)
+        subprocess.run(["umount", mnt], check=False)
+        os.rmdir(pins)
+        os.rmdir(mnt)
+    return res
 
 
 if __name__ == "__main__":

@@ -143,14 +143,51 @@ def cmd_probe(args) -> int:
     return 1 if bad else 0
 
 
-async def _http(method: str, url: str, data=None) -> int:
+SA_TOKEN = "/var/run/secrets/kubernetes.io/serviceaccount/token"
+
+
+def client_token(args) -> str:
+    """The bearer token the master authenticates (GM_AUTHZ_MODE=kube: the caller's own
+    Kubernetes token; GM_API_TOKEN: the shared one). First of: --token, $GM_TOKEN,
+    --token-file, the pod's service-account token, the current kubeconfig user's token."""
+    if getattr(args, "token", ""):
+        return args.token
+    if os.environ.get("GM_TOKEN"):
+        return os.environ["GM_TOKEN"]
+    for path in (getattr(args, "token_file", ""), SA_TOKEN):
+        if path and os.path.exists(path):
+            with open(path, encoding="utf-8") as fh:
+                return fh.read().strip()
+    kc = os.environ.get("KUBECONFIG", "").split(os.pathsep)[0] or \
+        os.path.expanduser("~/.kube/config")
+    if os.path.exists(kc):
+        import yaml
+        try:
+            with open(kc, encoding="utf-8") as fh:
+                doc = yaml.safe_load(fh) or {}
+            ctx = next(c["context"] for c in doc.get("contexts", [])
+                       if c["name"] == doc.get("current-context"))
+            user = next((u["user"] for u in doc.get("users", [])
+                         if u["name"] == ctx.get("user")), {})
+            return user.get("token", "")
+        except (OSError, ValueError, KeyError, StopIteration, yaml.YAMLError):
+            return ""
+    return ""
+
+
+async def _http(method: str, url: str, data=None, token: str = "") -> int:
     import aiohttp
 
+    headers = {"Accept": "application/json"}
+    if token:
+        headers["Authorization"] = f"Bearer {token}"
     async with aiohttp.ClientSession() as s:
-        async with s.request(method, url, data=data,
-                             headers={"Accept": "application/json"}) as r:
+        async with s.request(method, url, data=data, headers=headers) as r:
             body = await r.text()
             print(body)
+            if r.status == 401 and not token:
+                print("unauthorized: the master wants a bearer token (--token, $GM_TOKEN, "
+                      "--token-file or a kubeconfig user token)", file=sys.stderr)
             return 0 if r.status == 200 else 1
 
 
@@ -162,7 +199,7 @@ def cmd_add(args) -> int:
     q = {k: v for k, v in (("container", args.container), ("lease", args.lease)) if v}
     if q:
         url += "?" + urlencode(q)
-    return asyncio.run(_http("GET", url))
+    return asyncio.run(_http("GET", url, token=client_token(args)))
 
 
 def cmd_remove(args) -> int:
@@ -173,7 +210,7 @@ def cmd_remove(args) -> int:
     data = aiohttp.FormData()
     for u in args.uuid:
         data.add_field("uuids", u)
-    return asyncio.run(_http("POST", url, data))
+    return asyncio.run(_http("POST", url, data, token=client_token(args)))
 
 
 def cmd_status(args) -> int:
@@ -181,7 +218,7 @@ def cmd_status(args) -> int:
         url = f"{args.master.rstrip('/')}/api/v1/namespaces/{args.ns}/pods/{args.pod}/gpus"
     else:
         url = f"{args.master.rstrip('/')}/api/v1/nodes/{args.node}/gpus"
-    return asyncio.run(_http("GET", url))
+    return asyncio.run(_http("GET", url, token=client_token(args)))
 
 
 def disassemble(insns: List[int]) -> List[str]:
@@ -282,6 +319,10 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--master", default="http://127.0.0.1:8080")
         p.add_argument("--ns", default="default")
         p.add_argument("--pod", default="")
+        p.add_argument("--token", default="", help="bearer token for the master (default: "
+                       "$GM_TOKEN, --token-file, the service-account token, the kubeconfig "
+                       "user's token)")
+        p.add_argument("--token-file", default="")
         if name == "add":
             p.add_argument("-n", type=int, required=True)
             p.add_argument("--entire", action="store_true")

@@ -273,10 +273,14 @@ class V2BpfBackend(DeviceRuleBackend):
 
     name = "cgroup-v2-bpf"
 
-    def __init__(self, pin_dir: str = "") -> None:
+    def __init__(self, pin_dir: str = "", set_mode: bool = True) -> None:
         self.pin_dir = pin_dir
         if pin_dir:
             os.makedirs(pin_dir, exist_ok=True)
+        # set mode (default): rules in an allow-set map; False = straight-line programs (the
+        # native switch is process-wide; a worker has one backend)
+        self.set_mode = set_mode
+        _native.host().gm_bpf_dev_straight_line(0 if set_mode else 1)
         # cgroup → (attached program ids, pairs those programs grant), recorded when this
         # process installed them. Program ids are kernel-unique while a program is loaded and
         # a loaded program's instructions are immutable, so while the cgroup's attached id list
@@ -355,7 +359,11 @@ class V2BpfBackend(DeviceRuleBackend):
                                     C.byref(chained))
         if rc < 0:
             raise CgroupError(f"bpf install on {cgdir}: {os.strerror(-rc)}")
-        # set mode (every hot-mount): the kernel's map is the record, read back by allowed()
+        if not self.set_mode and rc == 1 and pid.value:
+            # one slot: our straight-line program replaced the runtime's in place
+            self._installed[cgdir] = ((pid.value,),
+                                      frozenset((n.major, n.minor) for n in desired))
+        # set mode: the kernel's map is the record, read back by allowed()
         if trace.current() is not None:
             tm = _native.BpfTiming()
             lib.gm_bpf_dev_last_timing(C.byref(tm))
@@ -572,9 +580,10 @@ class V2RecordingBackend(DeviceRuleBackend):
                                    chained=lambda *a: 0, maps={0: table})
 
 
-def make_backend(mode: str, emulate: bool, bpf_pin_dir: str = "") -> DeviceRuleBackend:
+def make_backend(mode: str, emulate: bool, bpf_pin_dir: str = "",
+                 bpf_set_mode: bool = True) -> DeviceRuleBackend:
     if mode == "v1":
         return V1Backend()
     if emulate:
         return V2RecordingBackend()
-    return V2BpfBackend(bpf_pin_dir)
+    return V2BpfBackend(bpf_pin_dir, bpf_set_mode)

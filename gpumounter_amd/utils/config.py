@@ -78,6 +78,9 @@ class Config:
     systemd_device_allow: str = "auto"
     systemd_bus: str = ""              # "" = /run/systemd/private, then the system bus socket
     bpf_pin_dir: str = "/sys/fs/bpf/gpumounter"  # bpffs dir for v2 tail-call maps ("" = keep fd)
+    # cgroup v2: allow-set map looked up by a fixed program (grants/revokes are map updates);
+    # false = one straight-line program per update (the previous scheme; a kill switch)
+    bpf_set_mode: bool = True
     devnode_mode: str = "procroot"     # procroot | setns | emulate
     # containers in their own user namespace (hostUsers: false) get bind-mounted nodes, because
     # mknod'ed ones on their nodev /dev cannot be opened: auto (detect per container) | bind

@@ -64,7 +64,8 @@ class Worker:
         self.resolver = CgroupResolver(cfg.cgroup_root, cfg.cgroup_mode, cfg.cgroup_driver,
                                        cfg.proc_root)
         emulate = cfg.devnode_mode == "emulate" or os.environ.get("GM_BPF_EMULATE") == "1"
-        self.backend = make_backend(self.resolver.mode, emulate, cfg.bpf_pin_dir)
+        self.backend = make_backend(self.resolver.mode, emulate, cfg.bpf_pin_dir,
+                                    cfg.bpf_set_mode)
         sd_mode = cfg.systemd_device_allow
         if emulate and sd_mode == "auto" and not cfg.systemd_bus:
             sd_mode = "off"          # hermetic runs never talk to the host's systemd by accident

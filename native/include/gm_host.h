@@ -107,6 +107,9 @@ void gm_bpf_dev_last_timing(gm_bpf_timing_t* out);
 int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int n,
                        const gm_dev_rule_t* base, int nbase, const char* pin_dir,
                        uint32_t* prog_id, uint32_t* chained_id);
+// Process-wide switch: 1 = always compile straight-line programs (set mode off; a kill switch
+// and the baseline for measurements), 0 = set mode for exact allow rules (default).
+void gm_bpf_dev_straight_line(int on);
 // The allow set of the index-th gpumounter program on the cgroup, as entries of 4 u32 (type,
 // major, minor, access bits). Returns 1 (set-mode program, *n entries), 0 (a straight-line
 // program: read it with gm_bpf_dev_program_at), -ENOENT past the last one, -ENOSPC (*n =

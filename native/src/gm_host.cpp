@@ -734,6 +734,8 @@ int with_root(int pid, const char* root, int flags, F fn) {
 #define SYS_move_mount 429
 #endif
 
+std::atomic<bool> g_straight_line{false};  // gm_bpf_dev_straight_line: set mode off
+
 std::mutex g_stage_mu;
 int g_stage_fd = -1;  // O_PATH dir fd of the staging directory (in the worker's mount namespace)
 
@@ -1160,7 +1162,7 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
   // map update — no program load, verification or attach — and the verifier sees the same
   // short program whatever the number of GPUs. A straight-line program of ours (older worker,
   // or rules a set cannot hold) is replaced.
-  const bool set_mode = set_eligible(rules, n);
+  const bool set_mode = set_eligible(rules, n) && !g_straight_line.load(std::memory_order_relaxed);
   struct Slot {
     uint32_t replace_id = 0, chain_id = 0, set_id = 0;
     bool ours = false, ours_without_chain = false, chain_lost = false;
@@ -1281,6 +1283,8 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
   if (chained_id) *chained_id = slots[0].chain_id;
   return (int)slots.size();
 }
+
+void gm_bpf_dev_straight_line(int on) { g_straight_line.store(on != 0); }
 
 int gm_bpf_dev_set_at(const char* cgroup_path, uint32_t index, uint32_t* entries, uint32_t cap,
                       uint32_t* n, uint32_t* prog_id) {

@@ -381,3 +381,25 @@ def test_pinned_chain_maps_of_removed_cgroups_are_swept(cgroup2_child, bpffs):
     assert [p.split("_")[1] for p in os.listdir(bpffs) if p.startswith("gm_")] == [str(ino_live)]
     assert be.sweep_pins(root) == []
     assert probe_access(live, [NULL.path, ZERO.path]) == "11"      # the live chain still works
+
+
+def test_straight_line_program_upgrades_to_set_mode(cgroup2_child, bpffs):
+    """GM_BPF_SET_MODE=false compiles straight-line programs (what older workers attached); a
+    set-mode worker meeting one replaces it by a set-mode wrapper around the same runtime
+    program, and the grants survive the swap."""
+    from gpumounter_amd.node.cgroup import _set_at
+
+    cg = cgroup2_child
+    attach_runtime_program(cg)
+    old = V2BpfBackend(bpffs, set_mode=False)
+    old.apply(cg, [ZERO], [], [ZERO])
+    assert _set_at(cg, 0) == ("code", None)
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "110"
+    new = V2BpfBackend(bpffs, set_mode=True)
+    new.apply(cg, [FULL], [], [ZERO, FULL])
+    kind, pairs = _set_at(cg, 0)
+    assert kind == "set" and pairs == {(ZERO.major, ZERO.minor), (FULL.major, FULL.minor)}
+    assert len(new.attached_ids(cg)) == 1                   # replaced, not stacked
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "111"
+    new.apply(cg, [], [ZERO, FULL], [])
+    assert probe_access(cg, [NULL.path, ZERO.path, FULL.path]) == "100"
