@@ -126,3 +126,29 @@ def test_master_and_network_policy_are_secure_by_default():
     with open(os.path.join(ROOT, "deploy.sh")) as fh:
         text = fh.read()
     assert "deploy/networkpolicy.yaml" in text and "gpu-mounter-tls" in text
+
+
+def test_cli_add_and_remove_authenticate_against_the_shipped_master(tmp_path):
+    """The shipped master authorizes callers (GM_AUTHZ_MODE=kube): the CLI sends a bearer
+    token (--token, $GM_TOKEN, --token-file, SA token, kubeconfig user) and is refused
+    without one."""
+    from gpumounter_amd.fakes.deployment import ProcessCluster
+
+    with ProcessCluster() as pc:
+        pc.tenant("cli")
+        env = {**os.environ, "KUBECONFIG": str(tmp_path / "none"), "GM_TOKEN": ""}
+        base = [sys.executable, "-m", "gpumounter_amd"]
+        r = subprocess.run(base + ["add", "--master", pc.master_url, "--pod", "cli", "-n", "1"],
+                           capture_output=True, text=True, cwd=ROOT, env=env, timeout=120)
+        assert r.returncode == 1 and "bearer token" in r.stderr
+        (tmp_path / "tok").write_text(pc.token + "\n")
+        r = subprocess.run(base + ["add", "--master", pc.master_url, "--pod", "cli", "-n", "1",
+                                   "--token-file", str(tmp_path / "tok")],
+                           capture_output=True, text=True, cwd=ROOT, env=env, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        uuid = json.loads(r.stdout)["devices"][0]["uuid"]
+        r = subprocess.run(base + ["remove", "--master", pc.master_url, "--pod", "cli",
+                                   "--uuid", uuid],
+                           capture_output=True, text=True, cwd=ROOT,
+                           env={**env, "GM_TOKEN": pc.token}, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
