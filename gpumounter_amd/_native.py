@@ -159,6 +159,8 @@ def host() -> C.CDLL:
         lib.gm_bpf_dev_restore.argtypes = [C.c_char_p, C.c_char_p]
         lib.gm_bpf_dev_build_set.argtypes = [C.c_int, C.POINTER(DevRule), C.c_int, C.c_int,
                                              C.c_int, C.POINTER(C.c_uint64), C.c_int]
+        lib.gm_bpf_dev_probe_set.argtypes = []
+        lib.gm_devnodes_bind_probe.argtypes = []
         lib.gm_bpf_dev_straight_line.argtypes = [C.c_int]
         lib.gm_bpf_dev_straight_line.restype = None
         lib.gm_bpf_dev_set_at.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_uint32),

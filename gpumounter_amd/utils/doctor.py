@@ -91,6 +91,12 @@ def check_cgroup(cfg) -> List[Check]:
     else:
         out.append(Check("bpf", "fail", f"cannot load a device program: {os.strerror(-fd)} "
                                         "(needs CAP_BPF/CAP_SYS_ADMIN: privileged DaemonSet)"))
+    if fd >= 0 and cfg.bpf_set_mode:
+        rc = lib.gm_bpf_dev_probe_set()
+        out.append(Check("bpf-set", "ok" if rc == 0 else "warn",
+                         "allow-set programs load (grants are map updates)" if rc == 0 else
+                         f"allow-set program refused ({os.strerror(-rc)}): set "
+                         "GM_BPF_SET_MODE=false for straight-line programs"))
     pin = cfg.bpf_pin_dir
     if pin:
         parent = pin if os.path.isdir(pin) else os.path.dirname(pin)
@@ -104,6 +110,21 @@ def check_cgroup(cfg) -> List[Check]:
                          + ("survive worker restarts" if is_bpffs else
                             "are kept in-process only (lost on restart until reconciled)")))
     return out
+
+
+def check_devnodes(cfg) -> List[Check]:
+    """User-namespaced Pods (hostUsers: false) get bind-mounted nodes (open_tree + move_mount,
+    node/devnodes.py), which needs CAP_SYS_ADMIN and a ≥5.2 kernel."""
+    if cfg.devnode_userns == "off" or cfg.devnode_mode == "emulate":
+        return [Check("devnodes-userns", "ok", f"bind mode not used (devnode_userns="
+                                               f"{cfg.devnode_userns}, mode={cfg.devnode_mode})")]
+    rc = _native.host().gm_devnodes_bind_probe()
+    if rc == 0:
+        return [Check("devnodes-userns", "ok", "open_tree/move_mount available: user-namespaced "
+                                               "Pods get bind-mounted device nodes")]
+    return [Check("devnodes-userns", "warn",
+                  f"open_tree refused ({os.strerror(-rc)}): attaches to user-namespaced Pods "
+                  "(hostUsers: false) will fail; other Pods are unaffected")]
 
 
 def check_systemd(cfg) -> List[Check]:
@@ -210,7 +231,8 @@ def check_gpus(cfg, burn_in_s: float = 0.0) -> List[Check]:
 
 def run(cfg, skip_cluster: bool = False, gpu: bool = False,
         burn_in_s: float = 0.0) -> List[Check]:
-    checks = check_inventory(cfg) + check_cgroup(cfg) + check_systemd(cfg)
+    checks = check_inventory(cfg) + check_cgroup(cfg) + check_devnodes(cfg) + \
+        check_systemd(cfg)
     if gpu:
         checks += check_gpus(cfg, burn_in_s)
     if not skip_cluster:

@@ -110,6 +110,8 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
 // Process-wide switch: 1 = always compile straight-line programs (set mode off; a kill switch
 // and the baseline for measurements), 0 = set mode for exact allow rules (default).
 void gm_bpf_dev_straight_line(int on);
+// 0 if a set-mode program (HASH map + lookup) loads here, else -errno (node preflight).
+int gm_bpf_dev_probe_set(void);
 // The allow set of the index-th gpumounter program on the cgroup, as entries of 4 u32 (type,
 // major, minor, access bits). Returns 1 (set-mode program, *n entries), 0 (a straight-line
 // program: read it with gm_bpf_dev_program_at), -ENOENT past the last one, -ENOSPC (*n =
@@ -152,6 +154,8 @@ int gm_devnodes_guard(const char* host_dev);
 // mounted there first (nosuid, noexec, mode 0711), so the staged nodes live on a filesystem
 // mounted in the caller's (initial) user namespace. Returns 0 or -errno. NULL/"" unsets it.
 int gm_devnodes_stage(const char* dir, int mount_tmpfs);
+// 0 if bind mode can work here (open_tree(OPEN_TREE_CLONE) allowed), else -errno.
+int gm_devnodes_bind_probe(void);
 // Creates nodes inside the target's root: `root` if non-NULL (test prefix), else /proc/<pid>/root.
 // results[i] = 0 created, 1 already present (idempotent), 2 directory is the host's (skipped), or
 // -errno. Returns #failures.

@@ -1286,6 +1286,16 @@ int gm_bpf_dev_install(const char* cgroup_path, const gm_dev_rule_t* rules, int 
 
 void gm_bpf_dev_straight_line(int on) { g_straight_line.store(on != 0); }
 
+int gm_bpf_dev_probe_set(void) {
+  Fd m(make_set_map());
+  if (!m.ok()) return m.fd;
+  uint64_t prog[64];
+  int cnt = gm_bpf_dev_build_set(m.fd, nullptr, 0, 1, -1, prog, 64);
+  if (cnt < 0) return -EINVAL;
+  Fd p(gm_bpf_dev_load(prog, cnt, "gm_doctor", nullptr, 0));
+  return p.ok() ? 0 : p.fd;
+}
+
 int gm_bpf_dev_set_at(const char* cgroup_path, uint32_t index, uint32_t* entries, uint32_t cap,
                       uint32_t* n, uint32_t* prog_id) {
   *n = 0;
@@ -1374,6 +1384,13 @@ int gm_devnodes_guard(const char* host_dev) {
     ++set;
   }
   return set;
+}
+
+int gm_devnodes_bind_probe(void) {
+  long fd = syscall(SYS_open_tree, AT_FDCWD, "/", OPEN_TREE_CLONE | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  close((int)fd);
+  return 0;
 }
 
 int gm_devnodes_stage(const char* dir, int mount_tmpfs) {

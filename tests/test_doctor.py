@@ -53,3 +53,18 @@ def test_doctor_gpu_check_fails_cleanly_without_a_gpu():
     checks = doctor.check_gpus(cfg)
     assert checks and all(c.status == "fail" for c in checks), checks
     assert checks[0].name == "gpu"
+
+
+def test_doctor_reports_bind_mode_for_user_namespaced_pods():
+    import os
+
+    from gpumounter_amd.utils import doctor
+    from gpumounter_amd.utils.config import Config
+
+    (c,) = doctor.check_devnodes(Config(devnode_userns="off"))
+    assert c.status == "ok" and "not used" in c.detail
+    (c,) = doctor.check_devnodes(Config())
+    if os.geteuid() == 0:
+        assert c.status == "ok", c.detail            # CAP_SYS_ADMIN: open_tree works
+    else:
+        assert c.status == "warn" and "hostUsers" in c.detail
