@@ -469,6 +469,9 @@ def main() -> int:
                     args.protocol == "gpumounter" else "off (insecure gRPC, no authz)",
                 },
                 "attach_p99_ms": round(pct(attach_ms, 0.99), 4),
+                "attach_p999_ms": round(pct(attach_ms, 0.999), 4) if len(attach_ms) >= 1000
+                else None,
+                "attach_max_ms": round(max(attach_ms), 4) if attach_ms else None,
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),
                 "detach_p99_ms": round(pct(detach_ms, 0.99), 4),
                 "stage_p50_ms": {k: round(statistics.median(v), 4) for k, v in sorted(stage.items())},

@@ -25,7 +25,7 @@ from typing import Dict, List, Optional, Sequence
 
 from gpumounter_amd.cluster.kube import NotFound
 from gpumounter_amd.cluster.placeholder import (InsufficientGPU, LABEL_NODE, Placeholder,
-                                                PlaceholderManager, Reservation, ReserveError,
+                                                PlaceholderManager, Reservation,
                                                 _label_value)
 from gpumounter_amd.hw import topology
 from gpumounter_amd.models import pod as podu

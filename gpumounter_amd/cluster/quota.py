@@ -24,7 +24,7 @@ from __future__ import annotations
 import asyncio
 import time
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Tuple
 
 from gpumounter_amd.cluster.kube import ApiError, KubeClient
 from gpumounter_amd.models import pod as podu

@@ -26,7 +26,7 @@ from __future__ import annotations
 import asyncio
 import os
 import secrets
-from typing import List, Optional
+from typing import List
 
 import grpc
 

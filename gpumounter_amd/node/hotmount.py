@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import List, Optional, Sequence
 
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models.device import AmdGpu, DeviceNode, kfd_node

@@ -19,7 +19,7 @@ import os
 import select
 import signal
 import signal as _sig   # Pinned.signal shadows the module name inside the class body
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Dict, Iterable, List, Sequence, Tuple
 
 from gpumounter_amd import _native
 from gpumounter_amd.hw.inventory import Inventory

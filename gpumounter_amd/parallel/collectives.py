@@ -13,7 +13,7 @@ GPUs (7 links × ≈153 GB/s per GPU, point-to-point). These helpers prove that 
 from __future__ import annotations
 
 import time
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 from gpumounter_amd.ops import probe
 

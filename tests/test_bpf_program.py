@@ -4,7 +4,6 @@ import ctypes as C
 import itertools
 import struct
 
-import pytest
 from hypothesis import given, settings
 from hypothesis import strategies as st
 
