@@ -475,6 +475,7 @@ def main() -> int:
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),
                 "detach_p99_ms": round(pct(detach_ms, 0.99), 4),
                 "stage_p50_ms": {k: round(statistics.median(v), 4) for k, v in sorted(stage.items())},
+                "stage_p99_ms": {k: round(pct(v, 0.99), 4) for k, v in sorted(stage.items())},
                 "probe_quick_p50_us": round(statistics.median(probe_us), 2) if probe_us else None,
                 "probe_gpus_verified": len(probe_by_gpu) if world == 1 else None,
                 "probe_quick_p50_us_by_gpu": {b: round(statistics.median(v), 2)

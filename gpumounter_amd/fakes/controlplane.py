@@ -28,7 +28,7 @@ from aiohttp import web
 
 from gpumounter_amd.fakes.apiserver import LatencyModel
 from gpumounter_amd.fakes.harness import LocalCluster
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import log, runtime
 
 
 def _hooks(lc_ref: list):
@@ -77,6 +77,10 @@ async def run(args) -> None:
     for sig in (signal.SIGTERM, signal.SIGINT):
         loop.add_signal_handler(sig, stop.set)
     await lc.start()
+    # The stand-ins for the Go apiserver and kubelet should not add Python GC pauses of their
+    # own to the latencies measured through them: freeze what start-up allocated, as the
+    # daemons do (utils/runtime.py)
+    runtime.tune_gc()
     info = {"api_url": lc.api_url, "pid": os.getpid(),
             "nodes": {name: {"kubelet_socket": h.kubelet.socket_path,
                              "kubelet_checkpoint": h.node.checkpoint_path,

@@ -134,6 +134,10 @@ class DevNodeWriter:
         if not self.stage_dir:
             raise DevNodeError("bind-mode device nodes need a staging directory "
                                "(devnode_stage_dir)")
+        try:
+            os.makedirs(os.path.dirname(self.stage_dir.rstrip("/")) or "/", exist_ok=True)
+        except OSError as e:
+            raise DevNodeError(f"staging directory {self.stage_dir}: {e.strerror}") from e
         rc = _native.host().gm_devnodes_stage(self.stage_dir.encode(), 1)
         if rc < 0:
             raise DevNodeError(f"staging tmpfs at {self.stage_dir}: {os.strerror(-rc)}")
