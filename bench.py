@@ -352,6 +352,11 @@ def main() -> int:
             last_note[0] = time.time()
             print(f"bench: {phase} step {i}/{total}", file=sys.stderr, flush=True)
 
+    # The client side of the measurement is this process (torch imported, the fake control
+    # plane's handles): a full collection of that heap during a timed request would be charged
+    # to the attach. Freeze what exists now, as the daemons do (utils/runtime.py).
+    from gpumounter_amd.utils import runtime
+    runtime.tune_gc()
     try:
         for i in range(args.warmup):
             one_step(False)
