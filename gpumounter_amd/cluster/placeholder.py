@@ -362,10 +362,16 @@ class PlaceholderManager:
                             return True
                         continue
                     msg = podu.is_unschedulable(pod)
+                    ids = ck.lookup(pending[key].uid) if ck is not None else None
                     if msg:
                         failure[key] = f"unschedulable: {msg}"
                     elif podu.phase_of(pod) == "Failed":
                         failure[key] = pod["status"].get("reason", "Failed")
+                    elif ids:
+                        # this node's kubelet recorded its devices at Allocate: bound here and
+                        # admitted, whether or not the bind has reached our watch yet
+                        bound_keys.append(key)
+                        from_ckpt[key] = ids
                     elif podu.node_of(pod):
                         bound_keys.append(key)
                         news = seen.get(key) != pod["metadata"].get("resourceVersion")
@@ -373,10 +379,7 @@ class PlaceholderManager:
                             if news:
                                 fresh.append(key)     # bound, and news since our last read
                         else:
-                            ids = ck.lookup(pending[key].uid)
-                            if ids:
-                                from_ckpt[key] = ids
-                            elif news and _admitted(pod):
+                            if news and _admitted(pod):
                                 # the kubelet writes the checkpoint at Allocate, before it
                                 # posts this status: a miss here means it does not maintain it
                                 fresh.append(key)
