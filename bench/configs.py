@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpumounter_amd.fakes.apiserver import LatencyModel  # noqa: E402
 from gpumounter_amd.fakes.harness import LocalCluster  # noqa: E402
 from gpumounter_amd.hw import topology  # noqa: E402
-from gpumounter_amd.utils import log  # noqa: E402
+from gpumounter_amd.utils import log, runtime  # noqa: E402
 
 
 def pct(xs, q):
@@ -272,6 +272,10 @@ def main() -> int:
                                 device_plugin=args.device_plugin,
                                 worker_overrides={"placement_enforce": args.placement,
                                                   "warm_pool_size": args.warm_pool}) as lc:
+            # one process holds the fakes, the worker and the master here: freeze the
+            # start-up heap as each daemon does on its own (utils/runtime.py), so a full
+            # collection of it is not charged to whichever operation it interrupts
+            runtime.tune_gc()
             res = await SCENARIOS[args.scenario](lc, args)
             gpus = lc.nodes["node-0"].node.gpus
             res["config"] = {"scenario": args.scenario, "amdsmi": args.amdsmi or "libamd_smi",
