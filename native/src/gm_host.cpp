@@ -542,6 +542,7 @@ int walk_parent(int rootfd, const char* path, bool create, Fd* parent, std::stri
 // dev/dri/, so 8 GPUs (17 nodes) walk two directories once instead of 17 times.
 struct Walker {
   int rootfd;
+  bool mknod_denied = false;  // emulate mode: mknodat already refused with EPERM in this call
   std::map<std::string, Fd> dirs;
   explicit Walker(int r) : rootfd(r) {}
   // *dirfd stays owned by the walker. Same results as walk_parent.
@@ -622,22 +623,26 @@ int create_one(Walker& w, const gm_dev_node_t& n, int flags) {
   } else if (kind == 3) {
     return -EEXIST;  // refuse to clobber an unrelated file
   }
-  if (mknodat(pfd, leaf.c_str(), S_IFCHR | (n.mode & 07777), makedev(n.major, n.minor)) <
-      0) {
-    int err = errno;
+  const bool try_mknod = !w.mknod_denied;
+  if (!try_mknod ||
+      mknodat(pfd, leaf.c_str(), S_IFCHR | (n.mode & 07777), makedev(n.major, n.minor)) < 0) {
+    int err = try_mknod ? errno : EPERM;
     if (!(err == EPERM && (flags & GM_DEV_EMULATE))) return -err;
+    w.mknod_denied = true;  // unprivileged: the rest of this call goes straight to markers
     int fd = openat(pfd, leaf.c_str(), O_CREAT | O_EXCL | O_WRONLY | O_NOFOLLOW | O_CLOEXEC,
                     n.mode & 07777);
     if (fd < 0) return -errno;
     char buf[48];
     int len = snprintf(buf, sizeof(buf), "%s %u:%u\n", kMarker, n.major, n.minor);
-    int w = write_all(fd, buf, (size_t)len);
+    int wr = write_all(fd, buf, (size_t)len);
+    if (wr == 0 && fchmod(fd, n.mode & 07777) < 0) wr = -errno;  // exact mode despite umask
     close(fd);
-    if (w < 0) return w;
+    if (wr < 0) return wr;
+  } else if (fchmodat(pfd, leaf.c_str(), n.mode & 07777, 0) < 0) {
+    // mknod honours the umask; set the exact mode the tenant needs (reference used -m 666,
+    // namespace.go:168).
+    return -errno;
   }
-  // mknod honours the umask; set the exact mode the tenant needs (reference used -m 666,
-  // namespace.go:168).
-  if (fchmodat(pfd, leaf.c_str(), n.mode & 07777, 0) < 0) return -errno;
   if (n.uid >= 0 || n.gid >= 0) {
     if (fchownat(pfd, leaf.c_str(), (uid_t)n.uid, (gid_t)n.gid, AT_SYMLINK_NOFOLLOW) < 0 &&
         errno != EPERM)
