@@ -20,33 +20,27 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import sys
 from typing import Dict, List
 
 
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
-def _rank_main(rank: int, world: int, port: int, cpu: bool, numel: int, out_dir: str) -> None:
+def _rank_main(rank: int, world: int, cpu: bool, numel: int, out_dir: str) -> None:
     import torch
     import torch.distributed as dist
 
     from gpumounter_amd.parallel.collectives import allreduce_check
 
-    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    # file:// rendezvous in the run's own directory: no TCP port picked ahead of time (another
+    # process can take a port between the pick and rank 0's bind)
+    rdv = "file://" + os.path.join(out_dir, "rendezvous")
     if cpu:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
         dev = torch.device("cpu")
     else:
         torch.cuda.set_device(rank)
         dev = torch.device("cuda", rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        dist.init_process_group("nccl", init_method=rdv, rank=rank, world_size=world,
+                                device_id=dev)
     try:
         res = allreduce_check(numel=numel, device=dev)
     finally:
@@ -60,13 +54,12 @@ def run_allreduce(world: int, cpu: bool, numel: int) -> List[Dict]:
 
     import torch.multiprocessing as mp
 
-    out_dir = tempfile.mkdtemp(prefix="gm-validate-")
-    mp.spawn(_rank_main, args=(world, _free_port(), cpu, numel, out_dir), nprocs=world,
-             join=True)
-    res = []
-    for r in range(world):
-        with open(os.path.join(out_dir, f"rank{r}.json")) as fh:
-            res.append(json.load(fh))
+    with tempfile.TemporaryDirectory(prefix="gm-validate-") as out_dir:
+        mp.spawn(_rank_main, args=(world, cpu, numel, out_dir), nprocs=world, join=True)
+        res = []
+        for r in range(world):
+            with open(os.path.join(out_dir, f"rank{r}.json")) as fh:
+                res.append(json.load(fh))
     return res
 
 

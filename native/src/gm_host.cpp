@@ -421,6 +421,48 @@ int set_keys(int map_fd, std::vector<SetKey>* keys) {
   return -E2BIG;
 }
 
+// Every {key, value} of the set: one BPF_MAP_LOOKUP_BATCH (≥ 5.6) per kSetMax entries, or a
+// GET_NEXT_KEY + LOOKUP walk on kernels without batch ops.
+int set_entries(int map_fd, std::vector<std::pair<SetKey, uint32_t>>* out) {
+  out->clear();
+  std::vector<SetKey> keys(kSetMax);
+  std::vector<uint32_t> vals(kSetMax);
+  uint32_t token = 0;
+  bool first = true;
+  for (;;) {
+    union bpf_attr a;
+    memset(&a, 0, sizeof(a));
+    a.batch.map_fd = (uint32_t)map_fd;
+    a.batch.in_batch = first ? 0 : ptr_u64(&token);
+    a.batch.out_batch = ptr_u64(&token);
+    a.batch.keys = ptr_u64(keys.data());
+    a.batch.values = ptr_u64(vals.data());
+    a.batch.count = kSetMax;
+    long rc = sys_bpf(BPF_MAP_LOOKUP_BATCH, &a, sizeof(a));
+    int err = rc < 0 ? errno : 0;
+    if (rc < 0 && err != ENOENT) {
+      if (!first || (err != EINVAL && err != ENOTSUP && err != 524 /* ENOTSUPP */)) return -err;
+      break;  // no batch ops here: walk instead
+    }
+    for (uint32_t i = 0; i < a.batch.count; ++i) out->emplace_back(keys[i], vals[i]);
+    if (err == ENOENT || a.batch.count == 0) return 0;
+    first = false;
+  }
+  std::vector<SetKey> ks;
+  int e = set_keys(map_fd, &ks);
+  if (e < 0) return e;
+  for (const SetKey& k : ks) {
+    uint32_t acc = 0;
+    union bpf_attr a;
+    memset(&a, 0, sizeof(a));
+    a.map_fd = (uint32_t)map_fd;
+    a.key = ptr_u64(&k);
+    a.value = ptr_u64(&acc);
+    if (sys_bpf(BPF_MAP_LOOKUP_ELEM, &a, sizeof(a)) == 0) out->emplace_back(k, acc);
+  }
+  return 0;
+}
+
 int set_op(int cmd, int map_fd, const SetKey& k, uint32_t* value) {
   union bpf_attr a;
   memset(&a, 0, sizeof(a));
@@ -1319,17 +1361,15 @@ int gm_bpf_dev_set_at(const char* cgroup_path, uint32_t index, uint32_t* entries
     if (!set_id) return 0;  // a straight-line program: read its xlated code instead
     Fd m(map_fd_by_id(set_id));
     if (!m.ok()) return m.fd;
-    std::vector<SetKey> keys;
-    if ((e = set_keys(m.fd, &keys)) < 0) return e;
+    std::vector<std::pair<SetKey, uint32_t>> all;
+    if ((e = set_entries(m.fd, &all)) < 0) return e;
     uint32_t out = 0;
-    for (const SetKey& key : keys) {
-      uint32_t acc = 0;
-      if (set_op(BPF_MAP_LOOKUP_ELEM, m.fd, key, &acc) < 0) continue;  // deleted meanwhile
+    for (const auto& kv : all) {
       if (out < cap && entries) {
-        entries[out * 4 + 0] = key.type;
-        entries[out * 4 + 1] = key.major;
-        entries[out * 4 + 2] = key.minor;
-        entries[out * 4 + 3] = acc;
+        entries[out * 4 + 0] = kv.first.type;
+        entries[out * 4 + 1] = kv.first.major;
+        entries[out * 4 + 2] = kv.first.minor;
+        entries[out * 4 + 3] = kv.second;
       }
       ++out;
     }

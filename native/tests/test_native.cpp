@@ -202,9 +202,42 @@ static void test_smi_mock() {
   EXPECT(gm_smi_count(&n) == GM_SMI_ERR_NOT_OPEN);
 }
 
+// Set-mode program: fixed length whatever the device count, every jump inside the program,
+// exactly one map lookup, the chain's tail call last before the default verdict; base rules
+// (chain lost) add their blocks after the miss label.
+static void test_bpf_set_layout() {
+  int need = gm_bpf_dev_build_set(-2, nullptr, 0, 0, -2, nullptr, 0);
+  EXPECT(need < 0);
+  std::vector<uint64_t> prog(-need);
+  int n = gm_bpf_dev_build_set(-2, nullptr, 0, 0, -2, prog.data(), (int)prog.size());
+  EXPECT(n == -need && n == 30);
+  int lookups = 0, tail_calls = 0;
+  for (int i = 0; i < n; ++i) {
+    struct bpf_insn in;
+    memcpy(&in, &prog[i], 8);
+    if (in.code == (BPF_JMP | BPF_CALL)) {
+      lookups += in.imm == BPF_FUNC_map_lookup_elem;
+      tail_calls += in.imm == BPF_FUNC_tail_call;
+    }
+    if ((in.code & 0x07) == BPF_JMP && ((in.code & 0xf0) == BPF_JNE || (in.code & 0xf0) == BPF_JEQ)) {
+      const int tgt = i + 1 + in.off;
+      EXPECT(tgt > i && tgt < n);
+    }
+  }
+  EXPECT(lookups == 1 && tail_calls == 1);
+  gm_dev_rule_t base[2] = {{'c', 7, 1, 0, 1, 3}, {'c', GM_ACC_MKNOD, 1, 0, -1, -1}};
+  int need2 = gm_bpf_dev_build_set(-2, base, 2, 0, -1, nullptr, 0);
+  std::vector<uint64_t> prog2(-need2);
+  int n2 = gm_bpf_dev_build_set(-2, base, 2, 0, -1, prog2.data(), (int)prog2.size());
+  EXPECT(n2 == -need2 && n2 > n - 4);  // no chain (-4) but two rule blocks and a ctx reload
+  EXPECT(gm_bpf_dev_build_set(-2, nullptr, -1, 0, -1, prog2.data(), n2) == -EINVAL);
+  EXPECT(gm_bpf_dev_build_set(-2, nullptr, 0, 0, -2, prog.data(), 3) < 0);  // too small
+}
+
 int main() {
   test_format();
   test_bpf_layout();
+  test_bpf_set_layout();
   test_devnodes();
   test_devnodes_guard();
   test_pids();

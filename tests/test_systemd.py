@@ -4,6 +4,7 @@ systemd-driver node (systemd re-applies its own device policy on
 import asyncio
 import ctypes as C
 import os
+import shutil
 import tempfile
 
 import pytest
@@ -27,6 +28,7 @@ def fake(request):
     fs.add_unit(UNIT, [("/dev/null", "rwm"), ("char-pts", "rwm")])
     yield fs
     fs.stop()
+    shutil.rmtree(d, ignore_errors=True)
 
 
 def test_unit_object_path_encoding_matches_sd_bus():
@@ -157,3 +159,4 @@ def test_attach_detach_on_systemd_driver_node_keeps_scope_device_allow_in_step()
         asyncio.run(main())
     finally:
         fs.stop()
+        shutil.rmtree(d, ignore_errors=True)
