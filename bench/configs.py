@@ -34,6 +34,35 @@ def pct(xs, q):
     return xs[min(int(q * len(xs)), len(xs) - 1)] if xs else None
 
 
+def _real_dev_nodes(pid: int) -> list:
+    """GPU-like device nodes (DRM major 226 or the KFD major) under a real tenant's /dev."""
+    import stat
+    out = []
+    root = f"/proc/{pid}/root/dev"
+    for dirpath, _, files in os.walk(root):
+        for f in files:
+            st = os.lstat(os.path.join(dirpath, f))
+            if stat.S_ISCHR(st.st_mode) and os.major(st.st_rdev) in (226, 511):
+                out.append(os.path.relpath(os.path.join(dirpath, f), root))
+    return sorted(out)
+
+
+def _tenant(lc, args, name: str) -> None:
+    """A tenant pod; with --node-ops real its container is a real process in its own mount
+    namespace (private tmpfs /dev) inside a real cgroup2 cgroup carrying a runc-style device
+    program, so every attach loads/updates a real BPF program and mknods real nodes."""
+    sb = getattr(args, "sandbox", None)
+    if sb is None:
+        lc.tenant(name)
+        return
+    from gpumounter_amd.fakes.realnode import attach_runtime_program
+    pid = sb.spawn_tenant()
+    lc.tenant(name, pids={"main": [pid]})
+    (ctr,) = [c for c in lc.nodes["node-0"].node.containers.values() if c.pod_name == name]
+    attach_runtime_program(ctr.cgroup_dir)
+    args.tenant_pids[name] = pid
+
+
 async def invariants(lc, tenants) -> int:
     """Number of violated ledger invariants (0 = consistent)."""
     bad = 0
@@ -56,7 +85,7 @@ async def invariants(lc, tenants) -> int:
 
 
 async def scale(lc, args) -> dict:
-    lc.tenant("scaler")
+    _tenant(lc, args, "scaler")
     inv = lc.inventory
     steps = []
     uuids = []
@@ -95,7 +124,7 @@ async def scale(lc, args) -> dict:
 async def contention(lc, args) -> dict:
     tenants = [f"c{i}" for i in range(4)]
     for t in tenants:
-        lc.tenant(t)
+        _tenant(lc, args, t)
     rnd = random.Random(args.seed)
     svc = lc.nodes["node-0"].worker.service
     ok = fail = 0
@@ -132,7 +161,7 @@ async def contention(lc, args) -> dict:
 
 async def soak(lc, args) -> dict:
     for i in range(2):
-        lc.tenant(f"s{i}")
+        _tenant(lc, args, f"s{i}")
     att, det = [], []
     width = min(4, len(lc.nodes["node-0"].node.gpus))   # 1..4 GPUs per attach (fewer if small)
     for k in range(args.cycles):
@@ -149,8 +178,12 @@ async def soak(lc, args) -> dict:
         att.append((t1 - t0) * 1e3)
         det.append((time.perf_counter() - t1) * 1e3)
     node = lc.nodes["node-0"].node
-    orphan_nodes = sum(len(node.container_devices(c)) for t in ("s0", "s1")
-                       for c in lc.container_ids("default", t))
+    if getattr(args, "sandbox", None) is not None:
+        # real node: what is left in each tenant's own /dev, seen through its mount namespace
+        orphan_nodes = sum(len(_real_dev_nodes(pid)) for pid in args.tenant_pids.values())
+    else:
+        orphan_nodes = sum(len(node.container_devices(c)) for t in ("s0", "s1")
+                           for c in lc.container_ids("default", t))
     orphan_rules = 0
     for t in ("s0", "s1"):
         orphan_rules += len(await lc.audit("default", t))
@@ -251,6 +284,10 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--cycles", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",
+                    help="real (root, cgroup2): tenants are processes in their own mount "
+                         "namespaces inside real cgroups with a runc-style device program; "
+                         "attaches load/update real BPF programs and mknod real nodes")
     ap.add_argument("--deploy", choices=("inprocess", "processes"), default="inprocess",
                     help="processes: daemons as separate processes, clients over HTTP "
                          "(contention only)")
@@ -266,12 +303,20 @@ def main() -> int:
         print(json.dumps(res))
         return 0
 
+    args.sandbox, args.tenant_pids = None, {}
+    kw, wov = {}, {"placement_enforce": args.placement, "warm_pool_size": args.warm_pool}
+    if args.node_ops == "real":
+        from gpumounter_amd.fakes.realnode import RealNodeSandbox
+        args.cgroup = "v2"
+        args.sandbox = RealNodeSandbox().__enter__()
+        kw = {"cgroup_root": args.sandbox.cgroup_root, "devnode_mode": "procroot"}
+        wov["bpf_pin_dir"] = args.sandbox.bpffs
+
     async def run():
         lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
         async with LocalCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, latency=lat,
-                                device_plugin=args.device_plugin,
-                                worker_overrides={"placement_enforce": args.placement,
-                                                  "warm_pool_size": args.warm_pool}) as lc:
+                                device_plugin=args.device_plugin, worker_overrides=wov,
+                                **kw) as lc:
             # one process holds the fakes, the worker and the master here: freeze the
             # start-up heap as each daemon does on its own (utils/runtime.py), so a full
             # collection of it is not charged to whichever operation it interrupts
@@ -283,11 +328,43 @@ def main() -> int:
                              "gfx": sorted({g.gfx_target for g in gpus}),
                              "cgroup": args.cgroup, "latency": args.latency,
                              "placement": args.placement, "device_plugin": args.device_plugin,
-                             "warm_pool": args.warm_pool}
+                             "warm_pool": args.warm_pool, "node_ops": args.node_ops}
+            if args.sandbox is not None:
+                res["kernel"] = _kernel_state(lc, args)
             return res
 
-    print(json.dumps(asyncio.run(run())))
+    try:
+        print(json.dumps(asyncio.run(run())))
+    finally:
+        if args.sandbox is not None:
+            args.sandbox.__exit__(None, None, None)
     return 0
+
+
+def _kernel_state(lc, args) -> dict:
+    """After the scenario, read from the kernel: the device programs attached to each tenant's
+    cgroup (our wrapper must be gone wherever no GPU is held, the runtime's program back), the
+    grants our wrappers still hold, the GPU nodes left in each tenant's /dev, and the pins left
+    on the bpffs."""
+    import ctypes as C
+
+    from gpumounter_amd import _native
+    from gpumounter_amd.node.cgroup import V2BpfBackend
+    lib = _native.host()
+    out = {"programs": {}, "grants": {}, "dev_nodes": {}}
+    node = lc.nodes["node-0"].node
+    for name, pid in args.tenant_pids.items():
+        (ctr,) = [c for c in node.containers.values() if c.pod_name == name]
+        names = []
+        for pid_ in V2BpfBackend.attached_ids(ctr.cgroup_dir):
+            buf = C.create_string_buffer(32)
+            lib.gm_bpf_prog_name(pid_, buf, 32)
+            names.append(buf.value.decode())
+        out["programs"][name] = names
+        out["grants"][name] = sorted(V2BpfBackend("").allowed(ctr.cgroup_dir))
+        out["dev_nodes"][name] = _real_dev_nodes(pid)
+    out["pins_left"] = sorted(f for f in os.listdir(args.sandbox.bpffs) if f.startswith("gm_"))
+    return out
 
 
 if __name__ == "__main__":

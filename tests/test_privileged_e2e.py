@@ -57,3 +57,30 @@ def test_full_stack_attach_detach_enforced_by_the_kernel(tmp_path):
     assert o["userns_after_remove"] == "00"
     assert o["userns_nodes_final"] == {"/dev/dri/renderD5": None, "/dev/dri/card7": None,
                                        "/dev/kfd": None}
+
+
+def test_soak_and_contention_on_real_kernel_objects_leave_nothing_behind():
+    """bench/configs.py --node-ops real: tenants are real processes in real cgroups with a
+    runc-style program; after the soak every tenant is back to the runtime's own program with
+    no grant, no GPU node and no pin left; under contention the kernel's grants and nodes match
+    the ledger (0 invariant violations)."""
+    root = os.path.dirname(HERE)
+    for scenario, extra in (("soak", ["--cycles", "40"]), ("contention", ["--rounds", "10"])):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench", "configs.py"), scenario,
+                            "--node-ops", "real", *extra], capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-4000:]
+        o = json.loads(r.stdout.strip().splitlines()[-1])
+        k = o["kernel"]
+        if scenario == "soak":
+            assert o["orphaned_cgroup_entries"] == 0 and o["orphaned_device_nodes"] == 0
+            assert set(map(tuple, k["programs"].values())) == {("runc_devices",)}
+            assert all(g == [] for g in k["grants"].values()) and k["pins_left"] == []
+            assert all(n == [] for n in k["dev_nodes"].values())
+        else:
+            assert o["invariant_violations"] == 0
+            for t, grants in k["grants"].items():
+                # every GPU the kernel grants has its render and card node in the tenant
+                renders = {f"dri/renderD{mi}" for ma, mi in grants if ma == 226 and mi >= 128}
+                assert renders <= set(k["dev_nodes"][t]), (t, grants, k["dev_nodes"][t])
+                assert (k["programs"][t] == ["runc_devices"]) == (grants == [])
