@@ -276,7 +276,8 @@ class Reconciler:
         sweep = getattr(svc.hm.backend, "sweep_pins", None)
         if sweep is not None:
             try:
-                gone = sweep(svc.hm.resolver.root)
+                # a walk of the whole cgroup tree: off the event loop, attaches keep flowing
+                gone = await asyncio.to_thread(sweep, svc.hm.resolver.root)
             except Exception as e:  # noqa: BLE001
                 rep.errors.append(f"bpf pin sweep: {e}")
             else:
