@@ -222,6 +222,39 @@ class KubeClient:
             body["preconditions"] = {"uid": uid}
         return await self._req("DELETE", self._pods_path(ns, name), body=body)
 
+    # ---- resource.k8s.io/v1 (DRA): ResourceClaims and ResourceSlices -----------------------
+    _DRA = "/apis/resource.k8s.io/v1"
+
+    async def create_claim(self, ns: str, claim: dict) -> dict:
+        name = (claim.get("metadata") or {}).get("name", "")
+        try:
+            return await self._req("POST", f"{self._DRA}/namespaces/{ns}/resourceclaims",
+                                   body=claim, idempotent=bool(name))
+        except Conflict:
+            cur = await self.get_claim(ns, name)
+            mine = (claim.get("metadata") or {}).get("labels") or {}
+            theirs = (cur.get("metadata") or {}).get("labels") or {}
+            if mine and all(theirs.get(k) == v for k, v in mine.items()):
+                return cur                  # our own create went through before the error
+            raise
+
+    async def get_claim(self, ns: str, name: str) -> dict:
+        return await self._req("GET", f"{self._DRA}/namespaces/{ns}/resourceclaims/{name}")
+
+    async def delete_claim(self, ns: str, name: str) -> Optional[dict]:
+        return await self._req("DELETE", f"{self._DRA}/namespaces/{ns}/resourceclaims/{name}")
+
+    async def list_claims(self, ns: str = "", label_selector: str = "") -> List[dict]:
+        path = f"{self._DRA}/namespaces/{ns}/resourceclaims" if ns else \
+            f"{self._DRA}/resourceclaims"
+        params = {"labelSelector": label_selector} if label_selector else None
+        return (await self._req("GET", path, params=params)).get("items", [])
+
+    async def list_slices(self, node: str = "") -> List[dict]:
+        params = {"fieldSelector": f"spec.nodeName={node}"} if node else None
+        return (await self._req("GET", f"{self._DRA}/resourceslices", params=params)).get(
+            "items", [])
+
     async def patch_pod(self, ns: str, name: str, patch: dict) -> dict:
         return await self._req("PATCH", self._pods_path(ns, name), body=patch,
                                content_type="application/merge-patch+json")

@@ -24,7 +24,11 @@ Unschedulable → InsufficientGPU mapping. Changed:
 * the preferred (xGMI/NUMA-aware) device set is attached as an annotation for
   GetPreferredAllocation-capable device plugins, and any deviation is counted;
 * ``reserve_trim`` enforces the placement whatever the device plugin picks: every free GPU is
-  held by a 1-GPU placeholder at once, the topology-chosen subset is kept, the rest released.
+  held by a 1-GPU placeholder at once, the topology-chosen subset is kept, the rest released;
+* on DRA clusters (``gpu_allocation=dra``) a placeholder holds a ResourceClaim of its own name
+  instead of an extended-resource limit, and the topology-chosen devices are a CEL selector of
+  that claim: the scheduler allocates exactly them (no trim needed). If they were taken
+  meanwhile, the reservation is retried once without the selector.
 """
 from __future__ import annotations
 
@@ -46,6 +50,9 @@ from gpumounter_amd.utils import log, trace
 
 _log = log.get("cluster.placeholder")
 LABEL_NODE = "gpumounter.amd.com/node"
+# number of GPUs a placeholder holds (DRA mode: there is no extended-resource limit to read)
+ANN_GPUS = "gpumounter.amd.com/gpus"
+CLAIM_REQUEST = "gpus"
 
 
 class InsufficientGPU(RuntimeError):
@@ -131,6 +138,7 @@ class PlaceholderManager:
         # eviction, preemption, namespace deletion): its GPU is going back to the scheduler
         self.on_foreign_delete: List[Callable[[dict], None]] = []
         self._foreign_seen: Dict[str, float] = {}
+        self._bg: set = set()       # background claim deletions (DRA mode)
 
     def _on_event(self, etype: str, pod: dict) -> None:
         md = pod.get("metadata", {})
@@ -204,9 +212,39 @@ class PlaceholderManager:
                               "requests": {"cpu": "1m", "memory": "4Mi"}},
             }],
         }
+        md["annotations"][ANN_GPUS] = str(n_gpus)
+        if self.dra:
+            res = spec["containers"][0]["resources"]
+            res.pop("limits")
+            res["claims"] = [{"name": CLAIM_REQUEST}]
+            spec["resourceClaims"] = [{"name": CLAIM_REQUEST, "resourceClaimName": name}]
         if self.cfg.placeholder_priority_class:
             spec["priorityClassName"] = self.cfg.placeholder_priority_class
         return {"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": spec}
+
+    @property
+    def dra(self) -> bool:
+        return getattr(self.cfg, "gpu_allocation", "device-plugin") == "dra"
+
+    def claim_for(self, body: dict) -> dict:
+        """The ResourceClaim a DRA-mode placeholder references: ``count`` devices of the GPU
+        device class, narrowed to the preferred devices (by PCI address) when there are any."""
+        md = body["metadata"]
+        ann = md.get("annotations") or {}
+        n = int(ann.get(ANN_GPUS, "1"))
+        exactly = {"deviceClassName": self.cfg.dra_device_class,
+                   "allocationMode": "ExactCount", "count": n}
+        pref = [d for d in ann.get(ANN_PREFERRED, "").split(",") if d]
+        if pref and len(pref) == n:
+            vals = ", ".join(f'"{d}"' for d in pref)
+            exactly["selectors"] = [{"cel": {"expression":
+                f'device.attributes["{self.cfg.dra_driver}"].{self.cfg.dra_bdf_attribute} '
+                f'in [{vals}]'}}]
+        return {"apiVersion": "resource.k8s.io/v1", "kind": "ResourceClaim",
+                "metadata": {"name": md["name"], "namespace": md["namespace"],
+                             "labels": dict(md.get("labels") or {}),
+                             "annotations": {ANN_OWNER_UID: ann.get(ANN_OWNER_UID, "")}},
+                "spec": {"devices": {"requests": [{"name": CLAIM_REQUEST, "exactly": exactly}]}}}
 
     # ------------------------------------------------------------------------ queries
     def live(self) -> List[dict]:
@@ -249,6 +287,16 @@ class PlaceholderManager:
                 self.faults.check("placeholder_wait")
                 await self._await_admission(created, self.cfg.attach_timeout_s)
                 self.faults.check("placeholder_wait", "after")
+        except InsufficientGPU:
+            await self.release(created, wait=False)
+            if not (self.dra and len(preferred) == total):
+                raise
+            # DRA selectors are hard constraints: the chosen devices went to someone else
+            # since our ledger view; any free ones will do
+            _log.info("preferred devices %s not allocatable; retrying unpinned",
+                      list(preferred))
+            return await self.reserve(owner, total, entire, (), attach_id, container,
+                                      idempotency_key)
         except BaseException:
             await self.release(created, wait=False)
             raise
@@ -295,9 +343,31 @@ class PlaceholderManager:
         surplus = [p for p in created if p not in keep]
         return Reservation(keep), surplus
 
+    async def _create_claims(self, bodies: List[dict]) -> None:
+        """DRA mode: the placeholders' ResourceClaims, before the Pods (a Pod whose claim does
+        not exist yet is reported Unschedulable)."""
+        claims = [self.claim_for(b) for b in bodies]
+        res = await asyncio.gather(*[self.kube.create_claim(c["metadata"]["namespace"], c)
+                                     for c in claims], return_exceptions=True)
+        errors = [r for r in res if not isinstance(r, dict)]
+        if errors:
+            await self._delete_claims([(c["metadata"]["namespace"], c["metadata"]["name"])
+                                       for c, r in zip(claims, res) if isinstance(r, dict)])
+            raise ReserveError(f"resourceclaim create failed: {errors[0]}")
+
+    async def _delete_claims(self, keys: Sequence[Tuple[str, str]]) -> None:
+        res = await asyncio.gather(*[self.kube.delete_claim(ns, n) for ns, n in keys],
+                                   return_exceptions=True)
+        for (ns, n), r in zip(keys, res):
+            if isinstance(r, Exception) and not isinstance(r, NotFound):
+                # an unreserved claim holds no device; the reconciler deletes leftovers
+                _log.warning("delete resourceclaim %s/%s: %s", ns, n, r)
+
     async def _create(self, bodies: List[dict]) -> List[Placeholder]:
         with trace.span("ledger_reserve", placeholders=len(bodies)):
             self.faults.check("ledger_reserve")
+            if self.dra:
+                await self._create_claims(bodies)
             results = await asyncio.gather(
                 *[self.kube.create_pod(b["metadata"]["namespace"], b) for b in bodies],
                 return_exceptions=True)
@@ -311,6 +381,10 @@ class PlaceholderManager:
         errors = [r for r in results if not isinstance(r, dict)]
         if errors:
             await self.release(created, wait=False)
+            if self.dra:
+                await self._delete_claims([(b["metadata"]["namespace"], b["metadata"]["name"])
+                                           for b, r in zip(bodies, results)
+                                           if not isinstance(r, dict)])
             quota = [e for e in errors if isinstance(e, ApiError) and e.status == 403
                      and "exceeded quota" in _message(e)]
             if quota:   # tenant-namespace placeholders: the apiserver's quota admission said no
@@ -460,7 +534,13 @@ class PlaceholderManager:
         counts the request): mounting those GPUs could double-book one, so the attach fails
         (and is rolled back) instead."""
         pod = self.informer.cache.get(key)
-        want = podu.resource_limit(pod, self.cfg.resource_name) if pod else len(ids)
+        ann = (pod or {}).get("metadata", {}).get("annotations") or {}
+        if not pod:
+            want = len(ids)
+        elif self.dra or ANN_GPUS in ann:
+            want = int(ann.get(ANN_GPUS, len(ids)))
+        else:
+            want = podu.resource_limit(pod, self.cfg.resource_name)
         if len(ids) != want:
             _log.error("ledger reports %d device(s) %s for placeholder %s/%s, which requests "
                        "%d", len(ids), list(ids), key[0], key[1], want)
@@ -501,6 +581,14 @@ class PlaceholderManager:
                         self.device_ids.pop(p.uid, None)
                     if isinstance(self.last_ledger, dict):
                         self.last_ledger.pop((p.namespace, p.name), None)
+            if self.dra:
+                # the claims hold no device once their Pod is gone (deallocated when
+                # reservedFor empties); deleting them is cleanup, off the critical path
+                gone = [(p.namespace, p.name) for p in phs if p not in failed]
+                if gone:
+                    t = asyncio.get_running_loop().create_task(self._delete_claims(gone))
+                    self._bg.add(t)
+                    t.add_done_callback(self._bg.discard)
             if failed:
                 raise ReserveError(f"could not delete {len(failed)} placeholder(s): "
                                    f"{[p.name for p in failed]}")

@@ -24,7 +24,8 @@ import time
 from typing import Dict, List, Optional, Sequence
 
 from gpumounter_amd.cluster.kube import NotFound
-from gpumounter_amd.cluster.placeholder import (InsufficientGPU, LABEL_NODE, Placeholder,
+from gpumounter_amd.cluster.placeholder import (ANN_GPUS, InsufficientGPU, LABEL_NODE,
+                                                Placeholder,
                                                 PlaceholderManager, Reservation,
                                                 _label_value)
 from gpumounter_amd.hw import topology
@@ -97,8 +98,10 @@ class WarmPool:
         md["name"] = name
         md["namespace"] = self.cfg.pool_namespace
         md["labels"] = {LABEL_APP: LABEL_APP_VALUE, LABEL_NODE: _label_value(self.ph.node)}
-        md["annotations"] = {ANN_MOUNT_MODE: MODE_STANDBY}
+        md["annotations"] = {ANN_MOUNT_MODE: MODE_STANDBY, ANN_GPUS: "1"}
         md.pop("ownerReferences", None)
+        for rc in body["spec"].get("resourceClaims") or []:     # DRA mode: its own claim
+            rc["resourceClaimName"] = name
         return body
 
     async def start(self) -> None:
@@ -166,9 +169,14 @@ class WarmPool:
         for _ in range(missing):
             body = self.standby_body()
             try:
+                if self.ph.dra:                     # its ResourceClaim first
+                    await self.ph._create_claims([body])  # noqa: SLF001
                 pod = await self.ph.kube.create_pod(self.cfg.pool_namespace, body)
             except Exception as e:  # noqa: BLE001
                 _log.warning("standby create failed: %s", e)
+                if self.ph.dra:
+                    await self.ph._delete_claims(  # noqa: SLF001
+                        [(self.cfg.pool_namespace, body["metadata"]["name"])])
                 break
             self.ph.informer.upsert(pod)
             created.append(Placeholder(pod["metadata"]["namespace"], pod["metadata"]["name"],

@@ -151,6 +151,8 @@ class FakeCluster:
         self._tasks: set = set()
         self._lock = threading.RLock()
         self._faults: List[Tuple[str, int, bool, str]] = []
+        from gpumounter_amd.fakes.dra import DraState
+        self.dra = DraState(self)     # resource.k8s.io/v1 claims and slices (fakes/dra.py)
 
     # ------------------------------------------------------------------------ nodes
     def add_node(self, node: FakeNode) -> FakeNode:
@@ -276,7 +278,23 @@ class FakeCluster:
             # several capacity-freed retries can be queued for one unschedulable pod; a pod is
             # bound and admitted once (a second admission would Allocate devices again)
             return
-        if podu.node_of(pod):
+        if self.dra.refs(pod):
+            # DRA: the scheduler allocates the Pod's claims on a node, then binds it there
+            sel = pod["spec"].get("nodeSelector", {}) or {}
+            cands = [n for n in self.nodes.values()
+                     if all(n.labels.get(k) == v for k, v in sel.items())
+                     and (not podu.node_of(pod) or n.name == podu.node_of(pod))]
+            node_name, why = self.dra.schedule(pod, cands)
+            if not node_name:
+                pod["status"]["conditions"] = [{
+                    "type": "PodScheduled", "status": "False", "reason": "Unschedulable",
+                    "message": f"0/{len(self.nodes)} nodes are available: {why}",
+                    "lastTransitionTime": _now()}]
+                self._unschedulable.add((ns, name))
+                self._bump("MODIFIED", pod)
+                return
+            pod["spec"]["nodeName"] = node_name
+        elif podu.node_of(pod):
             node_name = podu.node_of(pod)
         else:
             sel = pod["spec"].get("nodeSelector", {}) or {}
@@ -441,6 +459,7 @@ class FakeCluster:
         if pod is None:
             return
         self._handed_to_kubelet.discard(pod["metadata"]["uid"])
+        self.dra.pod_gone(pod)
         self._unschedulable.discard((ns, name))
         node = self.nodes.get(podu.node_of(pod))
         if node is not None:
@@ -514,6 +533,7 @@ class FakeCluster:
         r.add_post("/api/v1/namespaces/{ns}/events", self._h_event_create)
         r.add_get("/api/v1/namespaces/{ns}/events", self._h_event_list)
         r.add_get("/healthz", self._h_healthz)
+        self.dra.install(r, self._pre)
         return app
 
     async def _h_healthz(self, req: web.Request) -> web.Response:

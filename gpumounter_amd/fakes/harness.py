@@ -53,7 +53,7 @@ class LocalCluster:
                  device_plugin: bool = False, cgroup_root: str = "",
                  kfd_major: int = 0, start_workers: bool = True,
                  kubelet_rate_limit: Optional[tuple] = (100.0, 10),
-                 kubelet_limit_mode: str = "enforce",
+                 kubelet_limit_mode: str = "enforce", gpu_api: str = "device-plugin",
                  app_hook: Optional[Callable[[web.Application], None]] = None) -> None:
         self.n_nodes = n_nodes
         self.amdsmi_lib = amdsmi_lib
@@ -78,6 +78,7 @@ class LocalCluster:
         self.kfd_major = kfd_major
         self.kubelet_rate_limit = kubelet_rate_limit
         self.kubelet_limit_mode = kubelet_limit_mode
+        self.gpu_api = gpu_api      # "dra": GPUs published by a DRA driver (fakes/dra.py)
         self.node_gpu_bdfs = [b.lower() for b in node_gpu_bdfs] if node_gpu_bdfs else None
         self.nodes: Dict[str, NodeHandle] = {}
         self.master: Optional[Master] = None
@@ -127,6 +128,9 @@ class LocalCluster:
                         alloc_policy=self.alloc_policy,
                         cgroup_root=os.path.join(self.real_cgroup_root, name)
                         if self.real_cgroup_root else "")
+        if self.gpu_api == "dra":
+            node.gpu_api = "dra"
+            node.write_checkpoint = False    # the device manager does not see DRA devices
         self.cluster.add_node(node)
         sock = os.path.join(ndir, "pod-resources", "kubelet.sock")
         kubelet = FakeKubelet(node, sock, plugin_dir=os.path.join(ndir, "device-plugins")
@@ -150,6 +154,8 @@ class LocalCluster:
             ov.setdefault("device_plugin", True)
             ov.setdefault("device_plugin_dir", h.kubelet.plugin_dir)
         ov.setdefault("kubelet_checkpoint", h.node.checkpoint_path)
+        if self.gpu_api == "dra":
+            ov.setdefault("gpu_allocation", "dra")
         cfg = Config.load(env={}, kube_api=self.api_url, node_name=name,
                           kubelet_socket=h.kubelet.socket_path,
                           cgroup_root=h.node.cgroup_root, cgroup_mode=self.cgroup_mode,

@@ -111,6 +111,10 @@ class FakeNode:
         # a registered device plugin (FakeKubelet device manager) replaces allocate()
         self.plugin = None
         self.unhealthy: set = set()
+        # "device-plugin": GPUs are the extended resource the kubelet's device manager hands
+        # out; "dra": a DRA driver publishes them in a ResourceSlice (fakes/dra.py) and the
+        # device manager never sees them (no checkpoint entries)
+        self.gpu_api = "device-plugin"
 
     def _populate_host_dev(self) -> None:
         os.makedirs(os.path.join(self.host_dev, "dri"), exist_ok=True)

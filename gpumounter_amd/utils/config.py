@@ -48,6 +48,13 @@ class Config:
     # Kubernetes ≥1.20 GC cleans them up (SURVEY §2.6 defect 4).
     placeholder_namespace_mode: str = "pool"
     resource_name: str = "amd.com/gpu"
+    # how the cluster hands out GPUs: "device-plugin" (the amd.com/gpu extended resource of the
+    # ROCm device plugin; the reference's model) or "dra" (a DRA driver publishes them in
+    # ResourceSlices; placeholders then hold ResourceClaims pinned to the chosen devices)
+    gpu_allocation: str = "device-plugin"
+    dra_driver: str = "gpu.amd.com"
+    dra_device_class: str = "gpu.amd.com"
+    dra_bdf_attribute: str = "pciAddr"    # ResourceSlice device attribute holding the PCI BDF
     placeholder_image: str = "registry.k8s.io/pause:3.9"
     placeholder_pull_policy: str = "IfNotPresent"
     placeholder_priority_class: str = ""
@@ -235,6 +242,10 @@ class Config:
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))
         _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
         _choice("ledger_source", self.ledger_source, ("auto", "podresources"))
+        _choice("gpu_allocation", self.gpu_allocation, ("device-plugin", "dra"))
+        if self.gpu_allocation == "dra" and self.device_plugin:
+            raise ValueError("device_plugin serves the extended resource; with "
+                             "gpu_allocation=dra the GPUs belong to the DRA driver")
         if not (0 <= self.worker_port < 65536 and 0 <= self.master_port < 65536):
             raise ValueError("ports out of range")
 

@@ -149,9 +149,49 @@ def check_systemd(cfg) -> List[Check]:
     return [Check("systemd", "warn", f"{bus}: {err.value.decode() or os.strerror(-rc)}")]
 
 
+async def _check_dra(cfg) -> List[Check]:
+    """gpu_allocation=dra: the node's ResourceSlice must publish its GPUs with a PCI address
+    the worker can map to amdsmi's inventory."""
+    from gpumounter_amd.cluster.kube import KubeClient
+    from gpumounter_amd.hw.inventory import Inventory
+    from gpumounter_amd.models.device import normalize_device_id
+    from gpumounter_amd.node.dra import DraLedger
+
+    try:
+        kube = KubeClient.from_config(cfg)
+    except Exception as e:  # noqa: BLE001
+        return [Check("dra", "fail", f"no credentials: {e}")]
+    led = DraLedger(kube, cfg.node_name, cfg.dra_driver, cfg.dra_device_class,
+                    cfg.dra_bdf_attribute)
+    try:
+        devs = await led.allocatable()
+        allocs = await led.list()
+    except Exception as e:  # noqa: BLE001
+        return [Check("dra", "fail", f"resource.k8s.io/v1: {e}")]
+    finally:
+        await kube.close()
+    if not devs:
+        return [Check("dra", "fail", f"no ResourceSlice device of driver {cfg.dra_driver} on "
+                                     f"{cfg.node_name} carries a PCI address "
+                                     f"(attribute {cfg.dra_bdf_attribute!r})")]
+    try:
+        have = {normalize_device_id(g.bdf) for g in Inventory(
+            cfg.amdsmi_lib, cfg.kfd_major, cfg.kfd_dev_path).gpus()}
+    except Exception:  # noqa: BLE001 - reported by the amdsmi check
+        have = set()
+    unknown = [d for d in devs if have and normalize_device_id(d) not in have]
+    if unknown:
+        return [Check("dra", "warn", f"ResourceSlice devices not in the amdsmi inventory: "
+                                     f"{unknown}")]
+    return [Check("dra", "ok", f"{len(devs)} {cfg.dra_driver} device(s) in ResourceSlices, "
+                               f"{len(allocs)} claim reservation(s) on this node")]
+
+
 async def _check_kubelet(cfg) -> List[Check]:
     from gpumounter_amd.node.ledger import LedgerClient
 
+    if getattr(cfg, "gpu_allocation", "device-plugin") == "dra":
+        return await _check_dra(cfg)
     if not os.path.exists(cfg.kubelet_socket):
         return [Check("kubelet", "fail", f"PodResources socket {cfg.kubelet_socket} missing")]
     lc = LedgerClient(cfg.kubelet_socket, cfg.resource_name, cfg.kubelet_timeout_s,

@@ -48,6 +48,7 @@ class ReconcileReport:
     revoked: List[str] = field(default_factory=list)
     orphans: int = 0
     errors: List[str] = field(default_factory=list)
+    claims_deleted: List[str] = field(default_factory=list)   # DRA mode: orphan claims
 
     def to_dict(self) -> dict:
         return self.__dict__.copy()
@@ -61,6 +62,7 @@ class Reconciler:
         self._task = None
         self.last: ReconcileReport = ReconcileReport()
         self._first_seen: Dict[str, float] = {}
+        self._claim_seen: Dict[tuple, float] = {}
         self._kicked: set = set()
         self._bg: set = set()
         self.event_actions = 0
@@ -146,6 +148,38 @@ class Reconciler:
                 raise
             except Exception as e:  # noqa: BLE001
                 _log.exception("reconcile failed: %s", e)
+
+    async def _sweep_claims(self) -> List[str]:
+        """DRA mode: our ResourceClaims whose placeholder Pod does not exist (a worker that died
+        between creating the claim and the Pod, a Pod deleted by someone else) and that no Pod
+        holds. They hold no device, so this is cleanup; a claim gets ``stuck_after_s`` to be
+        joined by its Pod first."""
+        svc = self.svc
+        ns = "" if svc.cfg.placeholder_namespace_mode == "tenant" else svc.cfg.pool_namespace
+        claims = await svc.kube.list_claims(ns, svc.ph.selector_for_node(svc.ph.node))
+        now = time.monotonic()
+        out, seen = [], set()
+        for c in claims:
+            md = c["metadata"]
+            key = (md.get("namespace", ""), md.get("name", ""))
+            seen.add(key)
+            if svc.ph.informer.cache.get(key) is not None or \
+                    (c.get("status") or {}).get("reservedFor"):
+                self._claim_seen.pop(key, None)
+                continue
+            if now - self._claim_seen.setdefault(key, now) < self.stuck_after_s:
+                continue
+            try:
+                await svc.kube.delete_claim(*key)
+            except NotFound:
+                pass
+            self._claim_seen.pop(key, None)
+            out.append(f"{key[0]}/{key[1]}")
+        for key in [k for k in self._claim_seen if k not in seen]:
+            del self._claim_seen[key]
+        if out:
+            svc.metrics.reconcile_actions.labels(action="claim_delete").inc(len(out))
+        return out
 
     async def run_once(self) -> ReconcileReport:
         svc = self.svc
@@ -283,7 +317,13 @@ class Reconciler:
             else:
                 if gone:
                     m.reconcile_actions.labels(action="unpin").inc(len(gone))
+        if svc.ph.dra:
+            try:
+                rep.claims_deleted = await self._sweep_claims()
+            except Exception as e:  # noqa: BLE001
+                rep.errors.append(f"resourceclaim sweep: {e}")
         self.last = rep
-        if rep.owner_gone or rep.stuck or rep.repaired or rep.revoked or rep.errors:
+        if rep.owner_gone or rep.stuck or rep.repaired or rep.revoked or rep.errors or \
+                rep.claims_deleted:
             log.kv(_log, 20, "reconciled", **rep.to_dict())
         return rep

@@ -28,6 +28,7 @@ from gpumounter_amd.node import systemd
 from gpumounter_amd.node.cgroup import CgroupResolver, make_backend
 from gpumounter_amd.node.checkpoint import DeviceCheckpoint
 from gpumounter_amd.node.devnodes import DevNodeWriter
+from gpumounter_amd.node.dra import DraLedger
 from gpumounter_amd.node.hotmount import HotMount
 from gpumounter_amd.node.journal import InjectionJournal
 from gpumounter_amd.node.ledger import LedgerClient
@@ -59,8 +60,15 @@ class Worker:
         self.inv = inventory or Inventory(cfg.amdsmi_lib, cfg.kfd_major, cfg.kfd_dev_path)
         self.inv.ecc_policy = cfg.ecc_policy
         self.metrics = Metrics()
-        self.ledger = LedgerClient(cfg.kubelet_socket, cfg.resource_name, cfg.kubelet_timeout_s,
-                                   cfg.podresources_api, cfg.kubelet_qps, cfg.kubelet_burst)
+        if cfg.gpu_allocation == "dra":
+            # GPUs come from a DRA driver: the allocations are in ResourceClaims, not in the
+            # kubelet's device manager
+            self.ledger = DraLedger(self.kube, cfg.node_name, cfg.dra_driver,
+                                    cfg.dra_device_class, cfg.dra_bdf_attribute)
+        else:
+            self.ledger = LedgerClient(cfg.kubelet_socket, cfg.resource_name,
+                                       cfg.kubelet_timeout_s, cfg.podresources_api,
+                                       cfg.kubelet_qps, cfg.kubelet_burst)
         self.resolver = CgroupResolver(cfg.cgroup_root, cfg.cgroup_mode, cfg.cgroup_driver,
                                        cfg.proc_root)
         emulate = cfg.devnode_mode == "emulate" or os.environ.get("GM_BPF_EMULATE") == "1"
@@ -87,8 +95,12 @@ class Worker:
                                          resync_s=cfg.watch_resync_s)
         self.placeholders = PlaceholderManager(cfg, self.kube, self.ledger, self.ph_informer,
                                                cfg.node_name, self.faults)
+        if isinstance(self.ledger, DraLedger):
+            self.ledger.pod_lookup = lambda ns, name: (self.ph_informer.cache.get((ns, name))
+                                                       or self.node_informer.cache.get((ns, name)))
         self.checkpoint = None
-        if cfg.ledger_source == "auto" and cfg.kubelet_checkpoint:
+        if cfg.ledger_source == "auto" and cfg.kubelet_checkpoint and \
+                cfg.gpu_allocation != "dra":
             self.checkpoint = DeviceCheckpoint(cfg.kubelet_checkpoint, cfg.resource_name)
             self.placeholders.checkpoint = self.checkpoint
         self.service = GpuMountService(cfg, self.kube, self.inv, self.ledger, self.placeholders,

@@ -448,7 +448,8 @@ class GpuMountService:
                        n_free: int = 0):
         """Claim from the warm pool first (if enabled), create placeholders for the rest
         (``placement_enforce=trim``: hold every free GPU, keep the topology-chosen ones)."""
-        if self.cfg.placement_enforce != "trim" and self.plugin is None:
+        dra = self.cfg.gpu_allocation == "dra"     # the claim's selector pins the devices
+        if (self.cfg.placement_enforce != "trim" or dra) and self.plugin is None:
             return await self._reserve_unlocked(pod, n, req, st, preferred, n_free)
         async with self._node_reserve_lock:
             # recompute against the ledger as it is now that we hold the node
@@ -479,7 +480,8 @@ class GpuMountService:
             return claimed
         if got:
             preferred = create_pref
-        if not got and preferred and self.cfg.placement_enforce == "trim" and n_free > n:
+        if not got and preferred and self.cfg.placement_enforce == "trim" and n_free > n \
+                and self.cfg.gpu_allocation != "dra":
             return await self._reserve_trim(pod, n, req, st, n_free)
         token = ""
         if self.plugin is not None and preferred:
