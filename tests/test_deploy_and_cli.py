@@ -75,7 +75,11 @@ def test_rbac_is_least_privilege():
     assert binding["roleRef"]["name"] != "cluster-admin"
     resources = {r for role in roles for rule in role["rules"] for r in rule["resources"]}
     assert resources <= {"pods", "nodes", "events", "tokenreviews", "subjectaccessreviews",
-                         "resourcequotas"}
+                         "resourcequotas", "resourceclaims", "resourceslices"}
+    dra = [rule for role in roles for rule in role["rules"]
+           if rule["apiGroups"] == ["resource.k8s.io"]]
+    assert {v for rule in dra if rule["resources"] == ["resourceslices"]
+            for v in rule["verbs"]} == {"list"}           # slices are read-only
     assert all("*" not in rule["verbs"] for role in roles for rule in role["rules"])
     reviews = [rule for role in roles for rule in role["rules"]
                if set(rule["resources"]) & {"tokenreviews", "subjectaccessreviews"}]
