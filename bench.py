@@ -152,11 +152,20 @@ def main() -> int:
                     help="shipped: master⇄worker mTLS and TokenReview/SubjectAccessReview authz "
                          "as the manifests deploy them (--deploy processes); off: insecure gRPC, "
                          "no authz (the reference's posture)")
+    ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
+                    help="dra: the node's GPUs come from a DRA driver; placeholders hold "
+                         "ResourceClaims (gpu_allocation=dra)")
     args = ap.parse_args()
     if args.amdsmi == "mock" and os.path.exists("/dev/kfd"):
         # on a GPU box the mock inventory's GPUs are not the box's: the control plane is
         # measured alone (without a GPU the rank check still runs, on gloo)
         args.no_verify = True
+    if args.gpu_api == "dra":
+        if args.protocol == "reference" or args.device_plugin:
+            print("--gpu-api dra: the reference protocol and the device plugin are "
+                  "extended-resource models", file=sys.stderr)
+            return 2
+        args.ref_steps = 0
     if args.node_ops == "real":
         if args.deploy == "processes" and "--deploy" in sys.argv:
             print("--node-ops real runs --deploy inprocess", file=sys.stderr)
@@ -229,6 +238,7 @@ def main() -> int:
             pc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=args.latency,
                                 gpu_bdfs=node_bdfs, protocol=args.protocol,
                                 secure=args.security == "shipped" and args.protocol == "gpumounter",
+                                gpu_api=args.gpu_api,
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
                                             "GM_PLACEMENT_ENFORCE": args.placement}).start()
             pc.tenant("tenant", pids={"main": [tenant_pid]})
@@ -243,7 +253,8 @@ def main() -> int:
                 kw = {"cgroup_root": sandbox.cgroup_root, "devnode_mode": "procroot"}
             tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
                                  node_gpu_bdfs=node_bdfs, device_plugin=args.device_plugin,
-                                 worker_overrides=wov, master_overrides={"gc_tune": True}, **kw)
+                                 worker_overrides=wov, master_overrides={"gc_tune": True},
+                                 gpu_api=args.gpu_api, **kw)
             lc = tc.start()
             if args.protocol == "reference":
                 from gpumounter_amd.fakes import refproto
@@ -469,6 +480,7 @@ def main() -> int:
                     else "reference (emulated)",
                     "warm_pool": args.warm_pool, "placement": args.placement,
                     "device_plugin": args.device_plugin, "deploy": args.deploy,
+                    "gpu_allocation": args.gpu_api,
                     "security": "mTLS master-worker + TokenReview/SAR authz (cached)"
                     if args.deploy == "processes" and args.security == "shipped" and
                     args.protocol == "gpumounter" else "off (insecure gRPC, no authz)",

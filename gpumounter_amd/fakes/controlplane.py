@@ -70,7 +70,8 @@ async def run(args) -> None:
                       latency=LatencyModel.realistic() if args.latency == "realistic" else None,
                       workdir=args.workdir, start_master=False, start_workers=False,
                       node_gpu_bdfs=[b for b in args.gpu_bdfs.split(",") if b] or None,
-                      kubelet_limit_mode=args.kubelet_limit, app_hook=_hooks(ref))
+                      kubelet_limit_mode=args.kubelet_limit, gpu_api=args.gpu_api,
+                      app_hook=_hooks(ref))
     ref[0] = lc
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
@@ -110,6 +111,8 @@ def main(argv=None) -> int:
                     help="PodResources limiter (100 qps, burst 10): reject over-budget calls "
                          "with RESOURCE_EXHAUSTED, or serve them and only count them")
     ap.add_argument("--gpu-bdfs", default="", help="comma-separated: the node's GPUs (default all)")
+    ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
+                    help="dra: the GPUs are published in ResourceSlices (fakes/dra.py)")
     args = ap.parse_args(argv)
     log.setup("WARNING", json_format=False)
     asyncio.run(run(args))

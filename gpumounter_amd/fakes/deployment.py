@@ -52,7 +52,7 @@ class ProcessCluster:
                  worker_env: Optional[Dict[str, str]] = None,
                  master_env: Optional[Dict[str, str]] = None, log_dir: str = "",
                  protocol: str = "gpumounter", kubelet_limit: str = "enforce",
-                 secure: Optional[bool] = None) -> None:
+                 secure: Optional[bool] = None, gpu_api: str = "device-plugin") -> None:
         """``protocol="reference"`` runs worker and master with the reference's call sequence
         (gpumounter_amd/fakes/refproto.py) in the same deployment shape, for comparison; it is
         insecure like the reference unless ``secure`` says otherwise.
@@ -69,6 +69,7 @@ class ProcessCluster:
         self.latency = latency
         self.kubelet_limit = kubelet_limit
         self.gpu_bdfs = gpu_bdfs or []
+        self.gpu_api = gpu_api
         self.worker_env = worker_env or {}
         self.master_env = master_env or {}
         self.workdir = tempfile.mkdtemp(prefix="gm-deploy-")
@@ -140,7 +141,8 @@ class ProcessCluster:
                                      "--nodes", str(self.n_nodes), "--amdsmi", self.amdsmi_lib,
                                      "--cgroup", self.cgroup_mode, "--latency", self.latency,
                                      "--kubelet-limit", self.kubelet_limit,
-                                     "--gpu-bdfs", ",".join(self.gpu_bdfs)], {})
+                                     "--gpu-bdfs", ",".join(self.gpu_bdfs),
+                                     "--gpu-api", self.gpu_api], {})
         self._wait("control plane", lambda: os.path.exists(info_path))
         with open(info_path) as fh:
             self.info = json.load(fh)
@@ -175,7 +177,8 @@ class ProcessCluster:
                    "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": "0",
                    "GM_METRICS_PORT": "0", "GM_READY_FILE": self._ready_path(f"worker-{node}"),
                    "GM_LOG_LEVEL": "WARNING",
-                   "GM_LOG_JSON": "false", **self.worker_env}
+                   "GM_LOG_JSON": "false", "GM_GPU_ALLOCATION": self.gpu_api,
+                   **self.worker_env}
             self._worker_env[node] = env
             self._spawn(f"worker-{node}", [*self.entry, "worker"], env)
         for node in self._worker_env:

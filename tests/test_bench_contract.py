@@ -52,6 +52,20 @@ def test_bench_with_daemons_as_separate_processes():
     assert "daemon exit codes" not in res.stderr
 
 
+def test_bench_dra_cluster_daemons():
+    """--gpu-api dra: the daemons run with gpu_allocation=dra against the fake apiserver's
+    resource.k8s.io/v1 (placeholders hold ResourceClaims)."""
+    env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
+    res = subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "1",
+                          "--amdsmi", "mock", "--deploy", "processes", "--gpu-api", "dra"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _last_json(res.stdout)
+    assert d["config"]["gpu_allocation"] == "dra" and d["value"] > 0
+    assert d["ledger_audit_issues"] == 0 and d["final_orphans"] == 0
+    assert d["placeholders_left"] == 0
+
+
 def test_bench_two_rank_distributed_launch():
     env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
