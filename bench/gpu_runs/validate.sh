@@ -18,9 +18,11 @@ tail -1 "$O/smoke.log"
 timeout -k 10 300 python bench.py > "$O/default.json" 2> "$O/default.err" || fail "$O/default.err"
 timeout -k 10 300 python bench.py --gpus 1 --steps "$STEPS" --warmup 20 --warm-pool 1 \
     > "$O/pool.json" 2> "$O/pool.err" || fail "$O/pool.err"
+timeout -k 10 300 python bench.py --gpus 1 --steps "$STEPS" --warmup 20 --gpu-api dra \
+    > "$O/dra.json" 2> "$O/dra.err" || fail "$O/dra.err"
 python - "$O" <<'PY'
 import json, sys
-for n in ("default", "pool"):
+for n in ("default", "pool", "dra"):
     d = json.load(open(f"{sys.argv[1]}/{n}.json"))
     print(n, d["value"], d.get("attach_p99_ms"), d.get("detach_p50_ms"),
           d.get("ledger_audit_issues"), d.get("final_orphans"))

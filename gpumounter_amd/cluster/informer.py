@@ -55,9 +55,15 @@ class PodInformer:
                 pass
             self._task = None
 
+    def _list(self):
+        return self.kube.list_pods(self.namespace, self.label_selector, self.field_selector)
+
+    def _watch(self, timeout_s: int):
+        return self.kube.watch_pods(self.namespace, self.label_selector, self.field_selector,
+                                    self.rv, timeout_s=timeout_s)
+
     async def _relist(self) -> None:
-        items, rv = await self.kube.list_pods(self.namespace, self.label_selector,
-                                              self.field_selector)
+        items, rv = await self._list()
         fresh = {(p["metadata"]["namespace"], p["metadata"]["name"]): p for p in items}
         self._seen = {k: self._seen[k] for k in fresh if k in self._seen}
         for k, p in fresh.items():
@@ -92,9 +98,7 @@ class PodInformer:
                     self._synced.set()
                     need_list = False
                     self.relists += 1
-                async for etype, pod in self.kube.watch_pods(
-                        self.namespace, self.label_selector, self.field_selector, self.rv,
-                        timeout_s=int(self.resync_s)):
+                async for etype, pod in self._watch(int(self.resync_s)):
                     backoff = 0.05
                     md = pod.get("metadata", {})
                     if etype == "ERROR":
@@ -195,3 +199,15 @@ class PodInformer:
         """Wake waiters (used when a non-watch signal, e.g. the kubelet ledger, changed)."""
         async with self._cond:
             self._cond.notify_all()
+
+
+class ClaimInformer(PodInformer):
+    """The same list+watch cache over ``resource.k8s.io/v1`` ResourceClaims (DRA mode: the
+    placeholders' claims, whose allocation then arrives with the watch instead of a GET)."""
+
+    def _list(self):
+        return self.kube.list_claims_rv(self.namespace, self.label_selector)
+
+    def _watch(self, timeout_s: int):
+        return self.kube.watch_claims(self.namespace, self.label_selector, self.field_selector,
+                                      self.rv, timeout_s=timeout_s)

@@ -245,10 +245,7 @@ class KubeClient:
         return await self._req("DELETE", f"{self._DRA}/namespaces/{ns}/resourceclaims/{name}")
 
     async def list_claims(self, ns: str = "", label_selector: str = "") -> List[dict]:
-        path = f"{self._DRA}/namespaces/{ns}/resourceclaims" if ns else \
-            f"{self._DRA}/resourceclaims"
-        params = {"labelSelector": label_selector} if label_selector else None
-        return (await self._req("GET", path, params=params)).get("items", [])
+        return (await self.list_claims_rv(ns, label_selector))[0]
 
     async def list_slices(self, node: str = "") -> List[dict]:
         params = {"fieldSelector": f"spec.nodeName={node}"} if node else None
@@ -287,6 +284,31 @@ class KubeClient:
                          field_selector: str = "", resource_version: str = "",
                          timeout_s: int = 300) -> AsyncIterator[Tuple[str, dict]]:
         """Yield ``(type, pod)`` events (ADDED/MODIFIED/DELETED/BOOKMARK/ERROR)."""
+        async for ev in self.watch(self._pods_path(ns), label_selector, field_selector,
+                                   resource_version, timeout_s):
+            yield ev
+
+    def _claims_path(self, ns: Optional[str]) -> str:
+        return f"{self._DRA}/namespaces/{ns}/resourceclaims" if ns else \
+            f"{self._DRA}/resourceclaims"
+
+    async def list_claims_rv(self, ns: Optional[str] = None, label_selector: str = ""
+                             ) -> Tuple[List[dict], str]:
+        params = {"labelSelector": label_selector} if label_selector else None
+        out = await self._req("GET", self._claims_path(ns), params=params)
+        return out.get("items", []), out.get("metadata", {}).get("resourceVersion", "")
+
+    async def watch_claims(self, ns: Optional[str] = None, label_selector: str = "",
+                           field_selector: str = "", resource_version: str = "",
+                           timeout_s: int = 300) -> AsyncIterator[Tuple[str, dict]]:
+        async for ev in self.watch(self._claims_path(ns), label_selector, field_selector,
+                                   resource_version, timeout_s):
+            yield ev
+
+    async def watch(self, path: str, label_selector: str = "", field_selector: str = "",
+                    resource_version: str = "", timeout_s: int = 300
+                    ) -> AsyncIterator[Tuple[str, dict]]:
+        """Yield ``(type, object)`` watch events of a collection path."""
         params = {"watch": "true", "timeoutSeconds": str(timeout_s),
                   "allowWatchBookmarks": "true"}
         if label_selector:
@@ -296,7 +318,7 @@ class KubeClient:
         if resource_version:
             params["resourceVersion"] = resource_version
         sess = self._sess()
-        async with sess.get(self.base + self._pods_path(ns), params=params,
+        async with sess.get(self.base + path, params=params,
                             timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30)
                             ) as resp:
             if resp.status >= 400:

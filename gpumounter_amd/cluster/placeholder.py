@@ -415,6 +415,8 @@ class PlaceholderManager:
         deadline = loop.time() + timeout
         seen: Dict[Tuple[str, str], str] = {}   # resourceVersion at our last ledger read
         ck = self.checkpoint if self.checkpoint is not None and self.checkpoint.trusted else None
+        # DRA: a placeholder's claim allocated and reserved for it (claim watch cache)
+        reserved = getattr(self.ledger, "reserved_devices", None) if self.dra else None
         backoff = self.ADMISSION_BACKOFF_CKPT_S if ck is not None else self.ADMISSION_BACKOFF_S
         delay = backoff[0]
         while pending:
@@ -437,13 +439,16 @@ class PlaceholderManager:
                         continue
                     msg = podu.is_unschedulable(pod)
                     ids = ck.lookup(pending[key].uid) if ck is not None else None
+                    if ids is None and reserved is not None:
+                        ids = reserved(key[0], key[1], pending[key].uid)
                     if msg:
                         failure[key] = f"unschedulable: {msg}"
                     elif podu.phase_of(pod) == "Failed":
                         failure[key] = pod["status"].get("reason", "Failed")
                     elif ids:
-                        # this node's kubelet recorded its devices at Allocate: bound here and
-                        # admitted, whether or not the bind has reached our watch yet
+                        # the kubelet recorded its devices at Allocate (or the scheduler reserved
+                        # the DRA claim for it): bound here, whether or not the bind has reached
+                        # our watch yet
                         bound_keys.append(key)
                         from_ckpt[key] = ids
                     elif podu.node_of(pod):
@@ -490,8 +495,9 @@ class PlaceholderManager:
                     ph.device_ids = tuple(ids)
                     self.device_ids[ph.uid] = ph.device_ids
                     self.last_ledger = {**self.last_ledger, key: list(ids)}
-                    self.checkpoint_hits += 1
-                    self._checkpoint_misses = 0
+                    if ck is not None:
+                        self.checkpoint_hits += 1
+                        self._checkpoint_misses = 0
             if not pending:
                 break
             bound = [k for k in ready if k in pending] if isinstance(ready, list) else []

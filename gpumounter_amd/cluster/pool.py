@@ -60,6 +60,7 @@ class WarmPool:
         self._wake: Optional[asyncio.Event] = None
         self.exhausted = False               # last refill hit InsufficientGPU
         self._alloc_cache: Optional[tuple] = None   # (monotonic time, allocatable IDs)
+        self._creating = 0        # standby placeholders a refill is about to create
 
     @property
     def enabled(self) -> bool:
@@ -161,26 +162,33 @@ class WarmPool:
         if alloc is None:
             alloc = [g.bdf for g in self.inv.gpus()]
         free = sum(1 for d in alloc if normalize_device_id(d) not in allocated)
-        missing = min(missing, free)
+        # recount after the awaits above: a give-back may have refilled the pool meanwhile
+        missing = min(self.target - len(self.standby()) - self.pending(), free)
         if missing <= 0:
             self.exhausted = True
             return 0
         created = []
-        for _ in range(missing):
-            body = self.standby_body()
-            try:
-                if self.ph.dra:                     # its ResourceClaim first
-                    await self.ph._create_claims([body])  # noqa: SLF001
-                pod = await self.ph.kube.create_pod(self.cfg.pool_namespace, body)
-            except Exception as e:  # noqa: BLE001
-                _log.warning("standby create failed: %s", e)
-                if self.ph.dra:
-                    await self.ph._delete_claims(  # noqa: SLF001
-                        [(self.cfg.pool_namespace, body["metadata"]["name"])])
-                break
-            self.ph.informer.upsert(pod)
-            created.append(Placeholder(pod["metadata"]["namespace"], pod["metadata"]["name"],
-                                       pod["metadata"]["uid"], (), MODE_STANDBY))
+        self._creating = missing       # counted by give_back until they exist (pending())
+        try:
+            for _ in range(missing):
+                body = self.standby_body()
+                try:
+                    if self.ph.dra:                     # its ResourceClaim first
+                        await self.ph._create_claims([body])  # noqa: SLF001
+                    pod = await self.ph.kube.create_pod(self.cfg.pool_namespace, body)
+                except Exception as e:  # noqa: BLE001
+                    _log.warning("standby create failed: %s", e)
+                    if self.ph.dra:
+                        await self.ph._delete_claims(  # noqa: SLF001
+                            [(self.cfg.pool_namespace, body["metadata"]["name"])])
+                    break
+                self.ph.informer.upsert(pod)        # pending() counts it from here on
+                self._creating -= 1
+                md = pod["metadata"]
+                created.append(Placeholder(md["namespace"], md["name"], md["uid"], (),
+                                           MODE_STANDBY))
+        finally:
+            self._creating = 0
         if not created:
             return 0
         try:
@@ -276,7 +284,8 @@ class WarmPool:
     async def give_back(self, phs: Sequence[Placeholder]) -> None:
         """Return detached placeholders to the pool (up to ``target``); delete the rest."""
         async with self._lock:
-            room = max(self.target - len(self.standby()), 0)
+            # standby being admitted count too, or a refill racing a give-back overfills
+            room = max(self.target - len(self.standby()) - self.pending() - self._creating, 0)
             keep = [p for p in phs if p.device_ids and len(p.device_ids) == 1][:room]
             drop = [p for p in phs if p not in keep]
             with trace.span("pool_return", placeholders=len(keep)):

@@ -590,27 +590,33 @@ class FakeCluster:
         return web.json_response({"kind": "PodList", "apiVersion": "v1",
                                   "metadata": {"resourceVersion": str(self.rv)}, "items": items})
 
-    async def _watch(self, req: web.Request, ns: str, lsel, fsel) -> web.StreamResponse:
+    async def _watch(self, req: web.Request, ns: str, lsel, fsel, history=None, watchers=None,
+                     current=None, kind: str = "Pod") -> web.StreamResponse:
+        """A watch stream over ``history`` (rv, type, object) and live events queued through
+        ``watchers``; pods by default, any collection (DRA claims) when given."""
+        history = self.events if history is None else history
+        watchers = self.watchers if watchers is None else watchers
+        current = (lambda: list(self.pods.values())) if current is None else current
         resp = web.StreamResponse(headers={"Content-Type": "application/json"})
         await resp.prepare(req)
         q: asyncio.Queue = asyncio.Queue()
         rv = req.query.get("resourceVersion", "")
         if rv and rv != "0":
             since = int(rv)
-            if self.events and since < self.events[0][0] - 1:
+            if history and since < history[0][0] - 1:
                 await resp.write(json.dumps({"type": "ERROR", "object": {
                     "kind": "Status", "code": 410, "reason": "Expired",
                     "message": "too old resource version"}}).encode() + b"\n")
                 return resp
-            for erv, et, obj in self.events:
+            for erv, et, obj in history:
                 if erv > since and self._matches(obj, ns, lsel, fsel):
                     q.put_nowait((et, obj))
         else:
-            for p in list(self.pods.values()):
+            for p in current():
                 if self._matches(p, ns, lsel, fsel):
                     q.put_nowait(("ADDED", podu.jcopy(p)))
         entry = (q, ns, lsel, fsel)
-        self.watchers.append(entry)
+        watchers.append(entry)
         timeout = float(req.query.get("timeoutSeconds", "300"))
         deadline = time.monotonic() + timeout
         idle = 0.0
@@ -628,7 +634,7 @@ class FakeCluster:
                     if idle >= 30:
                         idle = 0.0
                         await resp.write(json.dumps({"type": "BOOKMARK", "object": {
-                            "kind": "Pod", "metadata": {"resourceVersion": str(self.rv)}}}
+                            "kind": kind, "metadata": {"resourceVersion": str(self.rv)}}}
                         ).encode() + b"\n")
                     continue
                 idle = 0.0
@@ -636,8 +642,8 @@ class FakeCluster:
         except (ConnectionResetError, asyncio.CancelledError):
             pass
         finally:
-            if entry in self.watchers:
-                self.watchers.remove(entry)
+            if entry in watchers:
+                watchers.remove(entry)
         return resp
 
     async def _h_create(self, req: web.Request) -> web.Response:

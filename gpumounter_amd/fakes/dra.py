@@ -50,9 +50,24 @@ def parse_selector(expr: str) -> Tuple[str, str, List[str]]:
 class DraState:
     """Claims and device allocation; owned by the FakeCluster (its ``dra`` attribute)."""
 
+    HISTORY = 4096
+
     def __init__(self, cluster) -> None:
         self.cluster = cluster
         self.claims: Dict[Tuple[str, str], dict] = {}
+        self.events: List[tuple] = []          # watch history: (rv, type, snapshot)
+        self.watchers: List[tuple] = []
+
+    def _bump(self, etype: str, claim: dict) -> None:
+        self.cluster.rv += 1
+        claim["metadata"]["resourceVersion"] = str(self.cluster.rv)
+        snap = podu.jcopy(claim)
+        self.events.append((self.cluster.rv, etype, snap))
+        if len(self.events) > self.HISTORY:
+            del self.events[: len(self.events) - self.HISTORY]
+        for q, ns, lsel, fsel in list(self.watchers):
+            if self.cluster._matches(snap, ns, lsel, fsel):   # noqa: SLF001
+                q.put_nowait((etype, snap))
 
     # ------------------------------------------------------------------------ slices
     def slices(self, node_name: str = "") -> List[dict]:
@@ -100,10 +115,9 @@ class DraState:
                         content_type="application/json") from e
         md["namespace"] = ns
         md["uid"] = str(uuid.uuid4())
-        self.cluster.rv += 1
-        md["resourceVersion"] = str(self.cluster.rv)
         claim["status"] = {}
         self.claims[(ns, name)] = claim
+        self._bump("ADDED", claim)
         # Pods waiting for this claim can be scheduled now
         for key in list(self.cluster._unschedulable):   # noqa: SLF001
             self.cluster._spawn(self.cluster._schedule(*key))   # noqa: SLF001
@@ -112,14 +126,17 @@ class DraState:
     def delete(self, ns: str, name: str) -> Optional[dict]:
         claim = self.claims.pop((ns, name), None)
         if claim is not None:
-            self._deallocate(ns, claim)
+            self._deallocate(ns, claim, bump=False)
+            self._bump("DELETED", claim)
         return claim
 
-    def _deallocate(self, ns: str, claim: dict) -> None:
+    def _deallocate(self, ns: str, claim: dict, bump: bool = True) -> None:
         if claim.get("status", {}).get("allocation"):
             for n in self.cluster.nodes.values():
                 n.release_pod(ns, "claim:" + claim["metadata"]["name"])
             claim["status"].pop("allocation", None)
+            if bump:
+                self._bump("MODIFIED", claim)
             freed = True
         else:
             freed = False
@@ -165,8 +182,8 @@ class DraState:
                 if not any(r.get("uid") == podu.uid_of(pod) for r in rf):
                     rf.append({"resource": "pods", "name": podu.name_of(pod),
                                "uid": podu.uid_of(pod)})
-                self.cluster.rv += 1
-                c["metadata"]["resourceVersion"] = str(self.cluster.rv)
+                # the scheduler writes the claim's status before it binds the Pod
+                self._bump("MODIFIED", c)
             return n.name, ""
         return None, "cannot allocate all claims"
 
@@ -220,8 +237,10 @@ class DraState:
             rf = [r for r in c.get("status", {}).get("reservedFor", [])
                   if r.get("uid") != podu.uid_of(pod)]
             c.setdefault("status", {})["reservedFor"] = rf
-            if not rf:
+            if not rf and c["status"].get("allocation"):
                 self._deallocate(ns, c)
+            else:
+                self._bump("MODIFIED", c)
         # claims owned by the Pod (ownerReferences) are garbage-collected with it
         for (cns, cname), c in list(self.claims.items()):
             if cns == ns and any(o.get("uid") == podu.uid_of(pod)
@@ -243,14 +262,19 @@ class DraState:
                                       "items": self.slices(node)})
 
         async def list_claims(req):
+            from gpumounter_amd.fakes.apiserver import _parse_selector
+
             await pre(req)
             ns = req.match_info.get("ns", "")
-            want = dict(part.split("=", 1) for part in
-                        req.query.get("labelSelector", "").split(",") if "=" in part)
-            items = [c for (cns, _), c in self.claims.items() if (not ns or cns == ns) and
-                     all((c["metadata"].get("labels") or {}).get(k) == v
-                         for k, v in want.items())]
+            lsel = _parse_selector(req.query.get("labelSelector", ""))
+            if req.query.get("watch") in ("true", "1"):
+                return await self.cluster._watch(   # noqa: SLF001
+                    req, ns, lsel, [], history=self.events, watchers=self.watchers,
+                    current=lambda: list(self.claims.values()), kind="ResourceClaim")
+            items = [c for c in self.claims.values()
+                     if self.cluster._matches(c, ns, lsel, [])]   # noqa: SLF001
             return web.json_response({"kind": "ResourceClaimList", "apiVersion": API,
+                                      "metadata": {"resourceVersion": str(self.cluster.rv)},
                                       "items": items})
 
         async def create_claim(req):

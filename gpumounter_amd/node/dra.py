@@ -50,6 +50,10 @@ class DraLedger:
         self.pod_lookup = pod_lookup
         self._dev: Dict[Tuple[str, str], str] = {}    # (pool, device name) → BDF
         self._dev_at = 0.0
+        # ClaimInformer over the placeholders' claims (set by the worker): their allocation is
+        # read from its cache; other claims (a tenant's own) with a GET
+        self.claims = None
+        self.claim_cache_hits = 0
         self.calls = 0
         self.throttled = 0
 
@@ -107,6 +111,26 @@ class DraLedger:
             devs = await self.devices(refresh=True)       # a slice that changed meanwhile
         return [devs[k] for k in mine if k in devs]
 
+    def reserved_devices(self, namespace: str, claim: str, pod_uid: str
+                         ) -> Optional[Tuple[str, ...]]:
+        """BDFs of a claim in the watch cache that is allocated and reserved for ``pod_uid``,
+        without any request; None when the cache cannot tell. The scheduler writes both before
+        it binds the Pod, and from then on the devices are the claim's in its books: the DRA
+        counterpart of reading the device-manager checkpoint at admission."""
+        c = self.claims.cache.get((namespace, claim)) if self.claims is not None else None
+        if c is None:
+            return None
+        st = c.get("status") or {}
+        if not any(r.get("uid") == pod_uid for r in st.get("reservedFor") or []):
+            return None
+        keys = [(r.get("pool", ""), r.get("device", "")) for r in
+                ((st.get("allocation") or {}).get("devices") or {}).get("results") or []
+                if r.get("driver") == self.driver]
+        if not keys or any(k not in self._dev for k in keys):
+            return None
+        self.claim_cache_hits += 1
+        return tuple(self._dev[k] for k in keys)
+
     # ------------------------------------------------------------------------ ledger API
     async def get(self, namespace: str, pod: str) -> Optional[List[str]]:
         p = self.pod_lookup(namespace, pod) if self.pod_lookup else None
@@ -118,7 +142,19 @@ class DraLedger:
             except ApiError as e:
                 raise LedgerError(f"pod {namespace}/{pod}: {e}") from e
         out: List[str] = []
+        uid = p.get("metadata", {}).get("uid")
+
+        def held(c: dict) -> bool:
+            reserved = (c.get("status") or {}).get("reservedFor") or []
+            return not (reserved and uid and not any(r.get("uid") == uid for r in reserved))
+
         for cname in claim_names(p):
+            cached = self.claims.cache.get((namespace, cname)) if self.claims else None
+            if cached is not None and held(cached) and \
+                    (cached.get("status") or {}).get("allocation"):
+                self.claim_cache_hits += 1
+                out += await self.claim_devices(cached)
+                continue
             self.calls += 1
             try:
                 claim = await self.kube.get_claim(namespace, cname)
@@ -126,9 +162,7 @@ class DraLedger:
                 continue
             except ApiError as e:
                 raise LedgerError(f"resourceclaim {namespace}/{cname}: {e}") from e
-            reserved = (claim.get("status") or {}).get("reservedFor") or []
-            uid = p.get("metadata", {}).get("uid")
-            if reserved and uid and not any(r.get("uid") == uid for r in reserved):
+            if not held(claim):
                 continue       # allocated, but not (yet / any more) for this Pod
             out += await self.claim_devices(claim)
         return out

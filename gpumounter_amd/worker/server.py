@@ -19,7 +19,7 @@ import grpc
 from aiohttp import web
 
 from gpumounter_amd.api import gpu_mount as api
-from gpumounter_amd.cluster.informer import PodInformer
+from gpumounter_amd.cluster.informer import ClaimInformer, PodInformer
 from gpumounter_amd.cluster.kube import KubeClient
 from gpumounter_amd.cluster.placeholder import PlaceholderManager
 from gpumounter_amd.cluster.pool import WarmPool
@@ -95,9 +95,15 @@ class Worker:
                                          resync_s=cfg.watch_resync_s)
         self.placeholders = PlaceholderManager(cfg, self.kube, self.ledger, self.ph_informer,
                                                cfg.node_name, self.faults)
+        self.claim_informer = None
         if isinstance(self.ledger, DraLedger):
             self.ledger.pod_lookup = lambda ns, name: (self.ph_informer.cache.get((ns, name))
                                                        or self.node_informer.cache.get((ns, name)))
+            # the placeholders' claims: their allocation arrives with the watch (no GET)
+            self.claim_informer = ClaimInformer(
+                self.kube, ph_ns, PlaceholderManager.selector_for_node(cfg.node_name),
+                resync_s=cfg.watch_resync_s)
+            self.ledger.claims = self.claim_informer
         self.checkpoint = None
         if cfg.ledger_source == "auto" and cfg.kubelet_checkpoint and \
                 cfg.gpu_allocation != "dra":
@@ -179,6 +185,11 @@ class Worker:
                     reconcile: bool = True) -> None:
         await self.ph_informer.start()
         await self.node_informer.start()
+        if self.claim_informer is not None:
+            await self.claim_informer.start()
+            # a claim allocated for a placeholder can complete its admission
+            self.claim_informer.handlers.append(
+                lambda et, c: asyncio.ensure_future(self.ph_informer.poke()))
         # warm the ledger channel (fails fast if the kubelet socket is wrong); the authoritative
         # read also cross-checks the device-manager checkpoint before admission relies on it
         await self.service.read_ledger(authoritative=True)
@@ -344,6 +355,8 @@ class Worker:
             await self.http_runner.cleanup()
         await self.ph_informer.stop()
         await self.node_informer.stop()
+        if self.claim_informer is not None:
+            await self.claim_informer.stop()
         if self.checkpoint is not None:
             self.checkpoint.close()
         await self.ledger.close()

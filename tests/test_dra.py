@@ -66,6 +66,8 @@ def test_dra_attach_detach_pins_devices_with_claims():
         assert not node.write_checkpoint                     # device manager not involved
         ledger = lc.nodes["node-0"].worker.ledger
         assert ledger.api_version == "resource.k8s.io/v1"
+        # the claims' allocation came with the claim watch, not a GET per placeholder
+        assert ledger.claim_cache_hits >= 1
         code, _ = await lc.remove("default", "t", [d["uuid"] for d in b["devices"]])
         assert code == 200
         assert not await lc.audit("default", "t")
