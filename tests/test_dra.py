@@ -236,3 +236,18 @@ def test_doctor_checks_resource_slices_in_dra_mode():
     g = {c.name: c for c in good}["dra"]
     assert g.status == "ok" and "8 gpu.amd.com device(s)" in g.detail, g
     assert {c.name: c for c in bad}["dra"].status == "fail"
+
+
+def test_dra_tenant_namespace_mode():
+    """Placeholders (and so their claims) in the tenant's namespace: the claim watch covers
+    every namespace through the node label."""
+    async def body(lc):
+        lc.tenant("t", ns="team-a")
+        code, b = await lc.add("team-a", "t", 2)
+        assert code == 200, b
+        assert {ns for (ns, _) in claims(lc)} == {"team-a"}
+        assert lc.nodes["node-0"].worker.ledger.claim_cache_hits >= 2
+        assert not await lc.audit("team-a", "t")
+        assert (await lc.remove("team-a", "t", [d["uuid"] for d in b["devices"]]))[0] == 200
+        await until(lambda: not claims(lc))
+    run(body, placeholder_namespace_mode="tenant")
