@@ -353,6 +353,10 @@ class PlaceholderManager:
         if errors:
             await self._delete_claims([(c["metadata"]["namespace"], c["metadata"]["name"])
                                        for c, r in zip(claims, res) if isinstance(r, dict)])
+            quota = [e for e in errors if isinstance(e, ApiError) and e.status == 403
+                     and "exceeded quota" in _message(e)]
+            if quota:   # tenant-namespace claims: the apiserver's quota admission said no
+                raise QuotaExceeded(_message(quota[0]))
             raise ReserveError(f"resourceclaim create failed: {errors[0]}")
 
     async def _delete_claims(self, keys: Sequence[Tuple[str, str]]) -> None:

@@ -34,6 +34,9 @@ from gpumounter_amd.utils import log
 _log = log.get("cluster.quota")
 
 
+DEVICECLASS_QUOTA_SUFFIX = ".deviceclass.resource.k8s.io/devices"
+
+
 class QuotaExceeded(RuntimeError):
     pass
 
@@ -63,6 +66,9 @@ class GpuQuota:
         self.kube = kube
         self.ttl_s = ttl_s
         self.keys = (f"requests.{cfg.resource_name}", cfg.resource_name)
+        if getattr(cfg, "gpu_allocation", "device-plugin") == "dra":
+            # DRA: devices requested by the namespace's claims of the GPU device class
+            self.keys = (f"{cfg.dra_device_class}{DEVICECLASS_QUOTA_SUFFIX}",)
         self._cache: Dict[str, Tuple[float, List[Limit]]] = {}
         self._locks: Dict[str, asyncio.Lock] = {}
         self.checks = 0
@@ -111,7 +117,9 @@ class GpuQuota:
             if md.get("deletionTimestamp") or \
                     (md.get("annotations") or {}).get(ANN_MOUNT_MODE) == MODE_STANDBY:
                 continue
-            total += podu.resource_limit(p, self.cfg.resource_name)
+            gpus = (md.get("annotations") or {}).get("gpumounter.amd.com/gpus")
+            total += int(gpus) if gpus and gpus.isdigit() else \
+                podu.resource_limit(p, self.cfg.resource_name)
         return total
 
     async def check(self, ns: str, n: int, already_counted: int = 0) -> None:

@@ -62,6 +62,9 @@ def _now() -> str:
     return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
 
 
+DEVICECLASS_QUOTA_SUFFIX = ".deviceclass.resource.k8s.io/devices"
+
+
 def _parse_selector(sel: str):
     """Label selector → list of (key, op, value) with op in {=, !=, exists, !exists}."""
     out = []
@@ -225,6 +228,8 @@ class FakeCluster:
     def _quota_used(self, ns: str, key: str) -> int:
         """What the quota controller reports: requests of the namespace's non-terminal pods
         (extended resources: requests == limits)."""
+        if key.endswith(DEVICECLASS_QUOTA_SUFFIX):    # DRA: devices of the namespace's claims
+            return self.dra.quota_used(ns, key[:-len(DEVICECLASS_QUOTA_SUFFIX)])
         res = key[len("requests."):] if key.startswith("requests.") else key
         if "/" not in res:
             return 0

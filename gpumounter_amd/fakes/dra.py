@@ -113,6 +113,7 @@ class DraState:
                     raise web.HTTPUnprocessableEntity(text=json.dumps(
                         {"kind": "Status", "message": str(e)}),
                         content_type="application/json") from e
+        self._quota_admit(ns, claim)
         md["namespace"] = ns
         md["uid"] = str(uuid.uuid4())
         claim["status"] = {}
@@ -122,6 +123,38 @@ class DraState:
         for key in list(self.cluster._unschedulable):   # noqa: SLF001
             self.cluster._spawn(self.cluster._schedule(*key))   # noqa: SLF001
         return claim
+
+    @staticmethod
+    def _requested(claim: dict, device_class: str) -> int:
+        return sum(int((r.get("exactly") or {}).get("count", 1))
+                   for r in (claim.get("spec", {}).get("devices", {}).get("requests") or [])
+                   if (r.get("exactly") or {}).get("deviceClassName") == device_class)
+
+    def quota_used(self, ns: str, device_class: str) -> int:
+        """``<class>.deviceclass.resource.k8s.io/devices`` usage: devices the namespace's
+        claims request from that class."""
+        return sum(self._requested(c, device_class) for (cns, _), c in self.claims.items()
+                   if cns == ns)
+
+    def _quota_admit(self, ns: str, claim: dict) -> None:
+        from gpumounter_amd.fakes.apiserver import DEVICECLASS_QUOTA_SUFFIX
+
+        for (qns, qname), q in self.cluster.quotas.items():
+            if qns != ns:
+                continue
+            for key, hard in q["spec"]["hard"].items():
+                if not key.endswith(DEVICECLASS_QUOTA_SUFFIX):
+                    continue
+                dc = key[:-len(DEVICECLASS_QUOTA_SUFFIX)]
+                want = self._requested(claim, dc)
+                used = self.quota_used(ns, dc)
+                if want and used + want > int(hard):
+                    raise web.HTTPForbidden(text=json.dumps(
+                        {"kind": "Status", "reason": "Forbidden", "code": 403,
+                         "message": f'resourceclaims "{claim["metadata"].get("name")}" is '
+                                    f"forbidden: exceeded quota: {qname}, requested: "
+                                    f"{key}={want}, used: {key}={used}, limited: {key}={hard}"}),
+                        content_type="application/json")
 
     def delete(self, ns: str, name: str) -> Optional[dict]:
         claim = self.claims.pop((ns, name), None)

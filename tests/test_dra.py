@@ -251,3 +251,30 @@ def test_dra_tenant_namespace_mode():
         assert (await lc.remove("team-a", "t", [d["uuid"] for d in b["devices"]]))[0] == 200
         await until(lambda: not claims(lc))
     run(body, placeholder_namespace_mode="tenant")
+
+
+@pytest.mark.parametrize("mode", ["pool", "tenant"])
+def test_dra_device_class_quota(mode):
+    """ResourceQuota ``gpu.amd.com.deviceclass.resource.k8s.io/devices`` caps hot-mounted GPUs:
+    enforced by the worker for pool-namespace placeholders, by the apiserver's quota admission
+    of the claims in tenant mode; the refusal is a 403 QuotaExceeded either way."""
+    key = "gpu.amd.com.deviceclass.resource.k8s.io/devices"
+
+    async def body(lc):
+        lc.cluster.set_quota("team-a", "gpus", {key: "3"})
+        lc.cluster.dra.create("team-a", {"metadata": {"name": "own"}, "spec": {"devices": {
+            "requests": [{"name": "g", "exactly": {"deviceClassName": "gpu.amd.com",
+                                                   "count": 1}}]}}})   # the tenant's own GPU
+        lc.tenant("p1", ns="team-a")
+        lc.tenant("other", ns="team-b")
+        code, b1 = await lc.add("team-a", "p1", 1)
+        assert code == 200, b1
+        code, b = await lc.add("team-a", "p1", 2)
+        assert code == 403 and "exceeded quota" in b["message"], b
+        assert len(claims(lc)) == 2           # the refused attach left no claim behind
+        code, b2 = await lc.add("team-a", "p1", 1)                 # 1 own + 2 = 3 = hard
+        assert code == 200, b2
+        assert (await lc.add("team-a", "p1", 1))[0] == 403
+        assert (await lc.add("team-b", "other", 3))[0] == 200      # no quota there
+        assert not await lc.audit("team-a", "p1")
+    run(body, placeholder_namespace_mode=mode)
