@@ -278,3 +278,33 @@ def test_dra_device_class_quota(mode):
         assert (await lc.add("team-b", "other", 3))[0] == 200      # no quota there
         assert not await lc.audit("team-a", "p1")
     run(body, placeholder_namespace_mode=mode)
+
+
+def test_dra_tenant_own_claim_gpus_are_not_removable():
+    """A Pod that got a GPU through its own ResourceClaim: hot-mounts go to other GPUs, and its
+    own GPU can never be removed (reference allocator.go:112-123)."""
+    async def body(lc):
+        node = lc.nodes["node-0"].node
+        lc.cluster.dra.create("default", {"metadata": {"name": "own"}, "spec": {"devices": {
+            "requests": [{"name": "g", "exactly": {"deviceClassName": "gpu.amd.com",
+                                                   "count": 1}}]}}})
+        lc.cluster.create_pod("default", {
+            "metadata": {"name": "t"},
+            "spec": {"resourceClaims": [{"name": "g", "resourceClaimName": "own"}],
+                     "containers": [{"name": "main", "image": "x:1",
+                                     "resources": {"claims": [{"name": "g"}]}}]}})
+        await until(lambda: (lc.cluster.get("default", "t") or {}).get("status", {})
+                    .get("phase") == "Running")
+        (own,) = [by for by in allocated_bdfs(lc.cluster.dra.claims[("default", "own")])]
+        own_bdf = next(g.bdf for g in node.gpus if f"gpu-{g.index}" == own)
+        svc = lc.nodes["node-0"].worker.service
+        st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+        assert [g.bdf for g in st.own] == [own_bdf]
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200, b
+        assert own_bdf not in [d["bdf"] for d in b["devices"]]
+        own_uuid = next(g.uuid for g in node.gpus if g.bdf == own_bdf)
+        code, text = await lc.remove("default", "t", [own_uuid], accept_json=False)
+        assert (code, text) == (400, "Invalid UUIDs: " + own_uuid + "\n")
+        assert not await lc.audit("default", "t")
+    run(body)
