@@ -7,12 +7,15 @@ records which Pods use it (``status.reservedFor``). This module models that much
 
 * one ResourceSlice per DRA node (driver ``gpu.amd.com``, pool = node name), one device per GPU
   (``gpu-<index>``) with attributes ``pciAddr``, ``uuid``, ``index``, ``productName``;
-* ResourceClaim create/get/list/delete, with device requests of ``exactly`` count N from a
+* ResourceClaim create/get/list/watch/delete (watch events share the Pods' resourceVersion
+  sequence; quota admission for ``<class>.deviceclass.resource.k8s.io/devices``), with device
+  requests of ``exactly`` count N from a
   device class, optionally narrowed by CEL selectors of the forms
   ``device.attributes["<driver>"].pciAddr in ["…", …]`` and ``… == "…"`` (others are refused
   at create, so a test cannot silently rely on unsupported CEL);
 * scheduling of Pods that reference claims by ``resourceClaimName``: all of the Pod's claims
-  are allocated on one node or the Pod is Unschedulable; an allocated claim is reused;
+  are allocated on one node or the Pod is Unschedulable; an allocated claim is reused; the
+  claims' status (allocation, reservedFor) is written before the Pod is bound;
 * deallocation when no Pod holds the claim any more, and when it is deleted.
 
 Parity with a real scheduler and with the AMD DRA driver's attribute names is unpinned (no
