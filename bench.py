@@ -152,6 +152,9 @@ def main() -> int:
                     help="shipped: master⇄worker mTLS and TokenReview/SubjectAccessReview authz "
                          "as the manifests deploy them (--deploy processes); off: insecure gRPC, "
                          "no authz (the reference's posture)")
+    ap.add_argument("--dump-samples", default="",
+                    help="write every timed attach (wall time, client ms, worker stage ms) as "
+                         "JSON lines to this file, for tail-latency analysis")
     ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
                     help="dra: the node's GPUs come from a DRA driver; placeholders hold "
                          "ResourceClaims (gpu_allocation=dra)")
@@ -282,6 +285,7 @@ def main() -> int:
     probe_by_gpu = {}
     last_bdfs = []
     ar_backend = [None]
+    samples = [] if args.dump_samples and rank == 0 else None
 
     def one_step(record: bool):
         nonlocal audit_issues, nccl_group
@@ -350,6 +354,10 @@ def main() -> int:
             if record:
                 attach_ms.append(st["ms"])
                 detach_ms.append((t1 - t0) * 1e3)
+                if samples is not None:
+                    samples.append({"t": round(time.time(), 4), "attach_ms": round(st["ms"], 4),
+                                    "detach_ms": round((t1 - t0) * 1e3, 4),
+                                    "stages": st["timings"]})
                 audit_issues += st["issues"]
                 for k, v in st["timings"].items():
                     stage.setdefault(k, []).append(v)
@@ -520,6 +528,10 @@ def main() -> int:
                     k.split(".")[-1]: v for k, v in out["stage_p50_ms"].items()
                     if k.startswith("mount.cgroup_rule.bpf_") or k in (
                         "mount.cgroup_rule", "mount.devnodes", "mount")}
+            if samples is not None:
+                with open(args.dump_samples, "w") as fh:
+                    for smp in samples:
+                        fh.write(json.dumps(smp) + "\n")
             print(json.dumps(out), flush=True)
     finally:
         if rank_pool is not None:
