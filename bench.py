@@ -155,6 +155,8 @@ def main() -> int:
     ap.add_argument("--dump-samples", default="",
                     help="write every timed attach (wall time, client ms, worker stage ms) as "
                          "JSON lines to this file, for tail-latency analysis")
+    ap.add_argument("--log-dir", default="",
+                    help="--deploy processes: keep the daemons' logs in this directory")
     ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
                     help="dra: the node's GPUs come from a DRA driver; placeholders hold "
                          "ResourceClaims (gpu_allocation=dra)")
@@ -241,7 +243,7 @@ def main() -> int:
             pc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=args.latency,
                                 gpu_bdfs=node_bdfs, protocol=args.protocol,
                                 secure=args.security == "shipped" and args.protocol == "gpumounter",
-                                gpu_api=args.gpu_api,
+                                gpu_api=args.gpu_api, log_dir=args.log_dir,
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
                                             "GM_PLACEMENT_ENFORCE": args.placement}).start()
             pc.tenant("tenant", pids={"main": [tenant_pid]})

@@ -8,9 +8,11 @@ TAG=${1:-soak_tail}
 O=gpurun_out/$TAG
 mkdir -p "$O"
 fail() { tail -40 "$1"; exit 1; }
+mkdir -p "$O/logs_default"
 timeout -k 10 400 python bench.py --gpus 1 --steps 3000 --warmup 50 --ref-steps 0 \
-    --dump-samples "$O/default.jsonl" > "$O/default.json" 2> "$O/default.err" || fail "$O/default.err"
+    --log-dir "$O/logs_default" --dump-samples "$O/default.jsonl" > "$O/default.json" 2> "$O/default.err" || fail "$O/default.err"
+mkdir -p "$O/logs_dra"
 timeout -k 10 400 python bench.py --gpus 1 --steps 3000 --warmup 50 --gpu-api dra \
-    --dump-samples "$O/dra.jsonl" > "$O/dra.json" 2> "$O/dra.err" || fail "$O/dra.err"
+    --log-dir "$O/logs_dra" --dump-samples "$O/dra.jsonl" > "$O/dra.json" 2> "$O/dra.err" || fail "$O/dra.err"
 python bench/tail_report.py "$O/default.jsonl" "$O/dra.jsonl" > "$O/tail_report.json"
 cat "$O/tail_report.json"

@@ -132,6 +132,7 @@ class KubeClient:
     # transient apiserver trouble (a control-plane node restarting, an overloaded apiserver
     # shedding load with 429/5xx): retried with backoff for requests that are safe to repeat
     RETRY_STATUS = (429, 500, 502, 503, 504)
+    retries = 0     # requests retried (per instance once one happened)
     RETRY_DELAYS = (0.01, 0.05, 0.2, 0.5)
 
     async def _req(self, method: str, path: str, params: Optional[dict] = None,
@@ -148,9 +149,14 @@ class KubeClient:
             except ApiError as e:
                 if e.status not in self.RETRY_STATUS or attempt == len(delays):
                     raise
+                why = f"HTTP {e.status}"
             except (aiohttp.ClientError, asyncio.TimeoutError, OSError) as e:
                 if attempt == len(delays):
                     raise ApiError(503, f"apiserver unreachable: {e!r}") from e
+                why = repr(e)
+            self.retries += 1
+            _log.warning("%s %s: %s; retry %d in %.0f ms", method, path, why, attempt + 1,
+                         delays[attempt] * 1e3)
             await asyncio.sleep(delays[attempt])
         raise AssertionError("unreachable")
 

@@ -327,12 +327,19 @@ class Worker:
     async def collect_metrics(self) -> None:
         if self.plugin is not None:
             self.metrics.plugin_healthy.set(sum(1 for v in self.plugin.health.values() if v))
-        for g in self.inv.gpus():
-            try:
-                n = len(self.inv.processes(g.index))
-            except Exception:  # noqa: BLE001 - not supported / no permission
-                continue
-            self.metrics.gpu_busy.labels(gpu=g.bdf).set(n)
+        def counts():
+            out = {}
+            for g in self.inv.gpus():
+                try:
+                    out[g.bdf] = len(self.inv.processes(g.index))
+                except Exception:  # noqa: BLE001 - not supported / no permission
+                    continue
+            return out
+
+        # amdsmi walks the KFD process table per GPU: milliseconds each on a busy node, so off
+        # the event loop (attaches in flight would otherwise wait for all of them)
+        for bdf, n in (await asyncio.to_thread(counts)).items():
+            self.metrics.gpu_busy.labels(gpu=bdf).set(n)
         await self.service.node_status(False)  # refreshes gm_ledger_gpus{state}
 
     async def stop(self) -> None:

@@ -270,6 +270,8 @@ class GpuMountService:
                            xgmi_hive_id=g.xgmi_hive_id, placeholder=owner.get(g.index, ""))
                 for g in gs]
 
+    SLOW_ATTACH_MS = 50.0
+
     @staticmethod
     def _timings(root: trace.Span) -> List:
         return [api.StageTiming(name=k, ms=v) for k, v in root.flat().items()]
@@ -283,6 +285,10 @@ class GpuMountService:
             resp = await self._add_gpu(req)
         resp.total_ms = root.duration_ms
         resp.timings.extend(self._timings(root))
+        if root.duration_ms > self.SLOW_ATTACH_MS:
+            # the stage split of a slow attach, for tail-latency attribution from the logs
+            _log.warning("slow attach %s/%s: %.1f ms %s", req.namespace, req.pod_name,
+                         root.duration_ms, {k: round(v, 2) for k, v in root.flat().items()})
         result = api.AddGPUResponse.AddGPUResult.Name(resp.add_gpu_result)
         self.metrics.requests.labels(op="add", result=result).inc()
         if resp.add_gpu_result == api.ADD_SUCCESS:
@@ -733,13 +739,15 @@ class GpuMountService:
                "topology": topology.describe(gpus, self.inv.links()),
                "ledger_api": self.ledger.api_version, "kfd_major": self.inv.kfd_major}
         if include_processes:
-            procs_by = {}
-            for g in gpus:
-                try:
-                    procs_by[g.index] = [p.__dict__ for p in self.inv.processes(g.index)]
-                except Exception as e:  # noqa: BLE001
-                    procs_by[g.index] = str(e)
-            out["processes"] = procs_by
+            def procs():
+                by = {}
+                for g in gpus:
+                    try:
+                        by[g.index] = [p.__dict__ for p in self.inv.processes(g.index)]
+                    except Exception as e:  # noqa: BLE001
+                        by[g.index] = str(e)
+                return by
+            out["processes"] = await asyncio.to_thread(procs)     # amdsmi: off the loop
         for state in ("GPU_FREE_STATE", "GPU_ALLOCATED_STATE"):
             self.metrics.ledger_gpus.labels(state=state).set(
                 sum(1 for g in gpus if g.state.value == state))
