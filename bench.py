@@ -232,8 +232,12 @@ def main() -> int:
             sandbox = RealNodeSandbox().__enter__()
             tenant_pid = sandbox.tenant_pid
         else:
-            sleeper = subprocess.Popen(["sleep", "infinity"])
+            # its own stdio: if this process dies, it must not hold the caller's pipe open
+            sleeper = subprocess.Popen(["sleep", "infinity"], stdin=subprocess.DEVNULL,
+                                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
             tenant_pid = sleeper.pid
+            import atexit
+            atexit.register(sleeper.kill)      # also when the setup below fails
         if args.deploy == "processes":
             if args.device_plugin:
                 print("--device-plugin needs --deploy inprocess (the fake kubelet drives the "
@@ -378,6 +382,7 @@ def main() -> int:
     # to the attach. Freeze what exists now, as the daemons do (utils/runtime.py).
     from gpumounter_amd.utils import runtime
     runtime.tune_gc()
+    runtime.watch_gc_pauses(5.0)
     try:
         for i in range(args.warmup):
             one_step(False)
@@ -521,6 +526,8 @@ def main() -> int:
                 "kubelet_calls": {k: kcalls.get(k, 0) for k in
                                   ("List", "Get", "GetAllocatableResources", "rejected")},
                 "placeholders_left": placeholders_left,
+                # collections in this (client) process that paused it ≥ 5 ms: [generation, ms]
+                "client_gc_pauses": [list(x) for x in runtime.gc_pauses],
                 "reference_emulated_same_run": ref,
                 "inventory": info,
             }

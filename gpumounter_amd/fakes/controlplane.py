@@ -82,6 +82,7 @@ async def run(args) -> None:
     # own to the latencies measured through them: freeze what start-up allocated, as the
     # daemons do (utils/runtime.py)
     runtime.tune_gc()
+    runtime.watch_gc_pauses(5.0, log.get("fakes.controlplane"))
     info = {"api_url": lc.api_url, "pid": os.getpid(),
             "nodes": {name: {"kubelet_socket": h.kubelet.socket_path,
                              "kubelet_checkpoint": h.node.checkpoint_path,

@@ -74,6 +74,7 @@ class ProcessCluster:
         self.master_env = master_env or {}
         self.workdir = tempfile.mkdtemp(prefix="gm-deploy-")
         self.log_dir = log_dir or self.workdir
+        os.makedirs(self.log_dir, exist_ok=True)
         self.procs: Dict[str, subprocess.Popen] = {}
         self.info: dict = {}
         self.worker_ports: Dict[str, Tuple[int, int]] = {}   # node → (grpc, metrics)
@@ -135,6 +136,13 @@ class ProcessCluster:
             return ""
 
     def start(self) -> "ProcessCluster":
+        try:
+            return self._start()
+        except BaseException:
+            self.stop()          # no daemon outlives a failed start
+            raise
+
+    def _start(self) -> "ProcessCluster":
         info_path = os.path.join(self.workdir, "info.json")
         self._spawn("controlplane", ["-m", "gpumounter_amd.fakes.controlplane", "--workdir",
                                      os.path.join(self.workdir, "cluster"), "--info", info_path,

@@ -190,6 +190,7 @@ class Master:
         self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
         if self.cfg.gc_tune:
             runtime.tune_gc()
+            runtime.watch_gc_pauses(5.0, _log)
         runtime.write_ready_file(self.cfg.ready_file, {"port": self.port})
         _log.info("master serving HTTP :%d", self.port)
 

@@ -20,6 +20,33 @@ def tune_gc(freeze: bool = True) -> None:
         gc.freeze()
 
 
+_gc_t0 = [0.0]
+_gc_watching = [False]
+gc_pauses: list = []          # (generation, ms) of collections over the threshold
+
+
+def watch_gc_pauses(threshold_ms: float = 5.0, logger=None) -> None:
+    """Log every garbage collection that stops the process for more than ``threshold_ms``
+    (generation, pause, objects collected): tail-latency attribution for the daemons."""
+    import time
+
+    def cb(phase: str, info: dict) -> None:
+        if phase == "start":
+            _gc_t0[0] = time.perf_counter()
+            return
+        ms = (time.perf_counter() - _gc_t0[0]) * 1e3
+        if ms >= threshold_ms:
+            gc_pauses.append((info.get("generation"), round(ms, 2)))
+            del gc_pauses[:-100]
+            if logger is not None:
+                logger.warning("gc pause: generation %s, %.1f ms, %s collected",
+                               info.get("generation"), ms, info.get("collected"))
+
+    if not _gc_watching[0]:
+        _gc_watching[0] = True
+        gc.callbacks.append(cb)
+
+
 def write_ready_file(path: str, info: dict) -> None:
     """Atomically publish what a daemon bound (config ``ready_file``)."""
     if not path:

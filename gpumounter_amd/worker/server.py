@@ -253,6 +253,7 @@ class Worker:
             self._health_task = asyncio.ensure_future(self._health_loop())
         if self.cfg.gc_tune:
             runtime.tune_gc()
+            runtime.watch_gc_pauses(5.0, _log)
         self.ready = True
         runtime.write_ready_file(self.cfg.ready_file, {"grpc_port": self.grpc_port,
                                                        "http_port": self.http_port})
