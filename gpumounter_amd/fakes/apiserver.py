@@ -132,6 +132,7 @@ class FakeCluster:
     """State + control loops; :meth:`app` exposes it over HTTP."""
 
     HISTORY = 20000
+    EVENTS_KEPT = 5000        # core/v1 Events retained
 
     def __init__(self, latency: Optional[LatencyModel] = None, gc_mode: str = "modern") -> None:
         self.latency = latency or LatencyModel()
@@ -166,13 +167,16 @@ class FakeCluster:
     def _bump(self, etype: str, pod: dict) -> None:
         self.rv += 1
         pod["metadata"]["resourceVersion"] = str(self.rv)
-        snap = podu.jcopy(pod)
-        self.events.append((self.rv, etype, snap))
+        # history and watch queues hold the serialized object: bytes are not tracked by the
+        # cyclic GC, so a long history does not turn into long collector pauses in this
+        # stand-in for the (Go) apiserver
+        data = json.dumps(pod).encode()
+        self.events.append((self.rv, etype, data))
         if len(self.events) > self.HISTORY:
             del self.events[: len(self.events) - self.HISTORY]
         for q, ns, lsel, fsel in list(self.watchers):
-            if self._matches(snap, ns, lsel, fsel):
-                q.put_nowait((etype, snap))
+            if self._matches(pod, ns, lsel, fsel):
+                q.put_nowait((etype, data))
 
     @staticmethod
     def _matches(pod: dict, ns: str, lsel, fsel) -> bool:
@@ -613,13 +617,13 @@ class FakeCluster:
                     "kind": "Status", "code": 410, "reason": "Expired",
                     "message": "too old resource version"}}).encode() + b"\n")
                 return resp
-            for erv, et, obj in history:
-                if erv > since and self._matches(obj, ns, lsel, fsel):
-                    q.put_nowait((et, obj))
+            for erv, et, data in history:
+                if erv > since and self._matches(json.loads(data), ns, lsel, fsel):
+                    q.put_nowait((et, data))
         else:
             for p in current():
                 if self._matches(p, ns, lsel, fsel):
-                    q.put_nowait(("ADDED", podu.jcopy(p)))
+                    q.put_nowait(("ADDED", json.dumps(p).encode()))
         entry = (q, ns, lsel, fsel)
         watchers.append(entry)
         timeout = float(req.query.get("timeoutSeconds", "300"))
@@ -643,7 +647,7 @@ class FakeCluster:
                         ).encode() + b"\n")
                     continue
                 idle = 0.0
-                await resp.write(json.dumps({"type": et, "object": obj}).encode() + b"\n")
+                await resp.write(b'{"type": "' + et.encode() + b'", "object": ' + obj + b"}\n")
         except (ConnectionResetError, asyncio.CancelledError):
             pass
         finally:
@@ -730,6 +734,8 @@ class FakeCluster:
         self.rv += 1
         md["resourceVersion"] = str(self.rv)
         self.k8s_events.append(ev)
+        if len(self.k8s_events) > self.EVENTS_KEPT:     # as the apiserver's event TTL would
+            del self.k8s_events[: len(self.k8s_events) - self.EVENTS_KEPT]
         return web.json_response(ev, status=201)
 
     async def _h_event_list(self, req: web.Request) -> web.Response:

@@ -64,13 +64,13 @@ class DraState:
     def _bump(self, etype: str, claim: dict) -> None:
         self.cluster.rv += 1
         claim["metadata"]["resourceVersion"] = str(self.cluster.rv)
-        snap = podu.jcopy(claim)
-        self.events.append((self.cluster.rv, etype, snap))
+        data = json.dumps(claim).encode()        # serialized: see FakeCluster._bump
+        self.events.append((self.cluster.rv, etype, data))
         if len(self.events) > self.HISTORY:
             del self.events[: len(self.events) - self.HISTORY]
         for q, ns, lsel, fsel in list(self.watchers):
-            if self.cluster._matches(snap, ns, lsel, fsel):   # noqa: SLF001
-                q.put_nowait((etype, snap))
+            if self.cluster._matches(claim, ns, lsel, fsel):   # noqa: SLF001
+                q.put_nowait((etype, data))
 
     # ------------------------------------------------------------------------ slices
     def slices(self, node_name: str = "") -> List[dict]:

@@ -20,8 +20,9 @@ import os
 import secrets
 import shutil
 import threading
+from collections import deque
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Deque, Dict, List, Optional, Sequence, Tuple
 
 from gpumounter_amd.hw import topology
 from gpumounter_amd.models.device import AmdGpu, LinkMatrix, normalize_device_id
@@ -107,7 +108,7 @@ class FakeNode:
         self.checkpoint_path = os.path.join(self.plugin_dir, CHECKPOINT_NAME)
         self.write_checkpoint = True
         self.containers: Dict[str, Container] = {}  # container id → Container
-        self.alloc_log: List[Tuple[str, str, List[str]]] = []
+        self.alloc_log: Deque[Tuple[str, str, List[str]]] = deque(maxlen=4096)
         # a registered device plugin (FakeKubelet device manager) replaces allocate()
         self.plugin = None
         self.unhealthy: set = set()
