@@ -223,3 +223,39 @@ def test_probe_gemm_wrappers_validate_before_touching_the_gpu():
             probe.burn_in(0, secs, n)
     with pytest.raises(probe.ProbeError):
         probe.gemm_tflops(0, 256, 256, 100, 1)
+
+
+def test_gc_pause_monitor_records_collections():
+    import gc
+
+    from gpumounter_amd.utils import runtime
+    runtime.watch_gc_pauses(0.0)          # every collection counts at threshold 0
+    runtime.watch_gc_pauses(0.0)          # idempotent: one callback
+    n = len(runtime.gc_pauses)
+    gc.collect()
+    assert len(runtime.gc_pauses) == min(n + 1, 100)
+    assert runtime.gc_pauses[-1][0] == 2
+
+
+def test_tail_report_attributes_slow_cycles(tmp_path):
+    import importlib.util
+    import json
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "tail_report", os.path.join(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__))), "bench", "tail_report.py"))
+    tr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tr)
+    f = tmp_path / "s.jsonl"
+    rows = [{"t": i * 0.01, "attach_ms": 1.0, "detach_ms": 1.0,
+             "stages": {"ledger_reserve": 0.3, "mount": 0.2, "mount.devnodes": 0.1}}
+            for i in range(99)]
+    rows.append({"t": 1.0, "attach_ms": 80.0, "detach_ms": 1.0,
+                 "stages": {"ledger_reserve": 79.0, "mount": 0.2, "mount.devnodes": 0.1}})
+    f.write_text("".join(json.dumps(r) + "\n" for r in rows))
+    rep = tr.report(str(f))
+    assert rep["cycles"] == 100 and rep["attach_ms"]["max"] == 80.0
+    top = rep["slowest"][0]
+    assert top["largest_stage"] == ["ledger_reserve", 79.0]
+    assert top["worker_ms"] == 79.2 and top["outside_worker_ms"] == 0.8   # sub-stages not summed
