@@ -10,8 +10,9 @@ O=gpurun_out/$TAG
 mkdir -p "$O"
 fail() { tail -40 "$1"; exit 1; }
 
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-    > "$O/pytest_gpu.log" 2>&1 || fail "$O/pytest_gpu.log"
+# 1-2: exactly what the driver runs at round end (from the repo root, no extra flags), each under
+# a time limit of its own
+timeout -k 10 600 python -m pytest tests/ -x -q -m gpu > "$O/pytest_gpu.log" 2>&1 || fail "$O/pytest_gpu.log"
 tail -1 "$O/pytest_gpu.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || fail "$O/smoke.log"
 tail -1 "$O/smoke.log"

@@ -268,3 +268,29 @@ def probe() -> C.CDLL:
 def loaded_libraries() -> list:
     """Paths of native libraries loaded into this process (for diagnostics/tests)."""
     return sorted(lib_path(n) for n in _libs)
+
+
+def mapped_in_tree() -> list:
+    """In-tree shared objects this process has mapped (``/proc/self/maps``): what the driver's
+    round-end check observes. Used by ``GM_RECORD_MAPS`` in tests/conftest.py and smoke()."""
+    root = os.path.dirname(LIB_DIR.rstrip("/"))
+    root = os.path.dirname(root)
+    seen = set()
+    try:
+        with open("/proc/self/maps") as fh:
+            for ln in fh:
+                path = ln.rstrip("\n").split(None, 5)[-1] if ln.count(" ") >= 5 else ""
+                if path.startswith(root) and ".so" in os.path.basename(path):
+                    seen.add(path)
+    except OSError:
+        pass
+    return sorted(seen)
+
+
+def record_maps(dest: Optional[str] = None) -> None:
+    dest = dest or os.environ.get("GM_RECORD_MAPS")
+    if not dest:
+        return
+    with open(dest, "a") as fh:
+        for p in mapped_in_tree():
+            fh.write(f"{os.getpid()} {p}\n")

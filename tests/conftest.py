@@ -21,6 +21,7 @@ def _native_libs():
     _native.host()
     _native.smi()
     yield
+    _native.record_maps()          # GM_RECORD_MAPS=<file>: which in-tree .so files were mapped
 
 
 @pytest.fixture(scope="session")

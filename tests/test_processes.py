@@ -170,30 +170,44 @@ def test_pinned_restrict_drops_pids_that_left_the_cgroup():
 
 
 def test_recycled_pid_is_not_signalled(tmp_path):
-    """Real PID reuse: in a fresh PID namespace, pin process A, let it exit, force the next PID
-    to A's number (ns_last_pid) so process B gets it, then deliver the kill: B survives."""
+    """Real PID reuse: in a fresh PID namespace, pin process A, let it exit, then create
+    process B with A's number (``clone3`` with ``set_tid``, which a PID namespace's root may
+    do; no system setting is touched), then deliver the kill: B survives."""
     import json
     import subprocess
     import sys
 
     if os.geteuid() != 0 or os.environ.get("GM_PRIVILEGED_TESTS") != "1":
-        pytest.skip("needs root (a PID namespace + ns_last_pid); GM_PRIVILEGED_TESTS=1")
+        pytest.skip("needs root (a PID namespace + clone3 set_tid); GM_PRIVILEGED_TESTS=1")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     script = tmp_path / "reuse.py"
     script.write_text(f"""
-import json, os, signal, subprocess, sys
+import ctypes, json, os, shutil, signal, struct, subprocess, sys
 sys.path.insert(0, {root!r})
 from gpumounter_amd.node import procs
-a = subprocess.Popen(["sleep", "60"])
+SYS_clone3 = 435                                   # x86_64 and aarch64 alike
+sleep = shutil.which("sleep")
+a = subprocess.Popen([sleep, "60"])
 pin = procs.Pinned([a.pid])
 a.kill(); a.wait()
-with open("/proc/sys/kernel/ns_last_pid", "w") as fh:
-    fh.write(str(a.pid - 1))
-b = subprocess.Popen(["sleep", "60"])
+tid = (ctypes.c_int * 1)(a.pid)
+# struct clone_args (v1, 80 bytes): flags pidfd child_tid parent_tid exit_signal stack
+# stack_size tls set_tid set_tid_size
+args = ctypes.create_string_buffer(struct.pack("10Q", 0, 0, 0, 0, signal.SIGCHLD, 0, 0, 0,
+                                               ctypes.addressof(tid), 1), 80)
+libc = ctypes.PyDLL(None, use_errno=True)          # keep the GIL across the clone
+libc.syscall.restype = ctypes.c_long
+b = libc.syscall(ctypes.c_long(SYS_clone3), args, ctypes.c_size_t(80))
+if b == 0:
+    try:
+        os.execv(sleep, [sleep, "60"])
+    finally:
+        os._exit(127)
+assert b > 0, os.strerror(ctypes.get_errno())
 res = pin.signal([a.pid], signal.SIGKILL)
-alive = b.poll() is None
-b.kill(); b.wait()
-print(json.dumps({{"a": a.pid, "b": b.pid, "res": res, "b_alive": alive}}))
+alive = os.waitpid(b, os.WNOHANG) == (0, 0)
+os.kill(b, signal.SIGKILL); os.waitpid(b, 0)
+print(json.dumps({{"a": a.pid, "b": b, "res": res, "b_alive": alive}}))
 """)
     r = subprocess.run(["unshare", "--pid", "--fork", "--mount-proc", sys.executable, str(script)],
                        capture_output=True, text=True, timeout=60)
