@@ -126,7 +126,7 @@ class BpfTiming(C.Structure):
                 ("insns", C.c_uint32)]
 
 
-HOST_ABI_VERSION = 5          # native/include/gm_host.h GM_HOST_ABI_VERSION
+HOST_ABI_VERSION = 6          # native/include/gm_host.h GM_HOST_ABI_VERSION
 GM_ACC_MKNOD, GM_ACC_READ, GM_ACC_WRITE = 1, 2, 4
 GM_DEV_EMULATE, GM_DEV_VIA_SETNS, GM_DEV_REPLACE, GM_DEV_BIND = 1, 2, 4, 8
 
@@ -178,7 +178,6 @@ def host() -> C.CDLL:
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.gm_devnodes_present.argtypes = [C.c_int, C.c_char_p, C.POINTER(DevNode), C.c_int,
                                             C.c_int, C.POINTER(C.c_uint8)]
-        lib.gm_proc_signal.argtypes = [C.POINTER(C.c_int32), C.c_int, C.c_int, C.POINTER(C.c_int)]
         lib.gm_proc_dev_users.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_int32), C.c_int,
                                           C.POINTER(C.c_int)]
         lib.gm_proc_scan_devs.argtypes = [C.POINTER(C.c_int32), C.c_int, C.POINTER(C.c_uint32),

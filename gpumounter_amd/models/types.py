@@ -41,6 +41,10 @@ ANN_OWNER_NAME = "gpumounter.amd.com/owner-name"
 ANN_IDEMPOTENCY = "gpumounter.amd.com/idempotency-key"
 ANN_GROUP = "gpumounter.amd.com/group"      # entire-mount group made of pooled placeholders
 MODE_STANDBY = "standby"
+# a force-removed GPU whose killed processes have not exited yet (worker/drain.py)
+MODE_DRAINING = "draining"
+ANN_DRAIN_PIDS = "gpumounter.amd.com/drain-pids"      # pid:starttime,... waited on
+ANN_DRAIN_OWNER = "gpumounter.amd.com/drained-from"   # ns/name of the pod it was removed from
 FINALIZER = "gpumounter.amd.com/release"
 SLAVE_SUFFIX = "-slave-pod-"
 

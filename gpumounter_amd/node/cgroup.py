@@ -209,6 +209,12 @@ class DeviceRuleBackend(ABC):
     def allowed(self, cgdir: str) -> Set[Tuple[int, int]]:
         """(major, minor) pairs currently granted by gpumounter."""
 
+    def installed(self, cgdir: str) -> Set[Tuple[int, int]]:
+        """Pairs gpumounter's own installed state grants, whatever other parties' programs
+        decide (:meth:`allowed` is the effective verdict). The journal forgets a rule only when
+        it is gone from here — a foreign veto does not make a grant of ours go away."""
+        return self.allowed(cgdir)
+
 
 class V1Backend(DeviceRuleBackend):
     name = "cgroup-v1"
@@ -397,6 +403,21 @@ class V2BpfBackend(DeviceRuleBackend):
             except CgroupError:
                 pass
             self._installed.pop(cgdir, None)
+        out = self.installed(cgdir)
+        foreign = _program_at(cgdir, 0, foreign_only=True)[1] if out else 0
+        for i in range(foreign):
+            prog, _ = _program_at(cgdir, i, foreign_only=True)
+            if prog is None:
+                break
+            try:
+                out = bpfvm.allowed_pairs(prog, sorted(out), chained=lambda *a: 0)
+            except bpfvm.BpfError:
+                return set()                   # cannot judge it: assume it vetoes
+        return out
+
+    def installed(self, cgdir):
+        """What gpumounter's own attached programs grant together (each must allow a pair),
+        before any foreign program's verdict."""
         grants: List[Set[Tuple[int, int]]] = []
         while True:
             kind, pairs = _set_at(cgdir, len(grants))
@@ -411,15 +432,6 @@ class V2BpfBackend(DeviceRuleBackend):
         out = grants[0]
         for g in grants[1:]:
             out &= g
-        foreign = _program_at(cgdir, 0, foreign_only=True)[1] if out else 0
-        for i in range(foreign):
-            prog, _ = _program_at(cgdir, i, foreign_only=True)
-            if prog is None:
-                break
-            try:
-                out = bpfvm.allowed_pairs(prog, sorted(out), chained=lambda *a: 0)
-            except bpfvm.BpfError:
-                return set()                   # cannot judge it: assume it vetoes
         return out
 
 

@@ -226,6 +226,11 @@ class DevNodeWriter:
         """:meth:`present` for a whole node set in one native call (one root resolution). A
         node in a directory that is the host's own ``/dev`` counts as present: create leaves
         it to the host (:data:`SHARED_HOST`) and so does the read-back."""
+        return [bool(s) for s in self.present_states(t, nodes)]
+
+    def present_states(self, t: Target, nodes: Sequence[DeviceNode]) -> List[int]:
+        """Per node: 0 absent, 1 present with the right major:minor, 2 in the host's guarded
+        ``/dev`` (present, and never gpumounter's)."""
         if not nodes:
             return []
         pid, root = self._target_args(t)
@@ -234,4 +239,4 @@ class DevNodeWriter:
                                                 self._call(t)[0], out)
         if rc < 0:
             raise DevNodeError(f"read-back of {len(nodes)} nodes: {os.strerror(-rc)}")
-        return [bool(out[i]) for i in range(len(nodes))]
+        return [int(out[i]) for i in range(len(nodes))]

@@ -91,17 +91,21 @@ class HotMount:
         return nodes
 
     # ------------------------------------------------------------------------ targets
-    def targets(self, pod: dict, container: str = "") -> List[ContainerTarget]:
-        """Running containers to act on. Privileged ones are left out: the runtime already gave
-        them every host device (and often the host's own ``/dev``), so there is nothing to grant
-        and nothing gpumounter may take away — an attach to them is ledger-only."""
+    def targets(self, pod: dict, container: str = "",
+                include_privileged: bool = False) -> List[ContainerTarget]:
+        """Running containers to act on. Privileged ones are left out of rule and node writes:
+        the runtime already gave them every host device (and often the host's own ``/dev``), so
+        there is nothing to grant and nothing gpumounter may take away — an attach to them is
+        ledger-only. Their processes still use the GPUs they are given, so the busy check and
+        the force-kill take them in (``include_privileged``; the reference takes PIDs from the
+        container's cgroup whatever its privileges, pkg/util/util.go:152-196)."""
         refs = [r for r in running_containers(pod, container) if r.running]
         if not refs:
             raise MountError(f"pod {pod['metadata'].get('name')} has no running container"
                              + (f" named {container}" if container else ""))
         out = []
         for r in refs:
-            if r.privileged:
+            if r.privileged and not include_privileged:
                 continue
             cgdir = self.resolver.container_dir(pod, r)
             pids = self.resolver.pids(cgdir)
@@ -117,11 +121,12 @@ class HotMount:
         return {"namespace": md.get("namespace", ""), "pod": md.get("name", ""),
                 "pod_uid": md.get("uid", ""), "container": t.ref.name, "cgdir": t.cgdir}
 
-    def resolve(self, pod: dict, container: str = "") -> List[ContainerTarget]:
+    def resolve(self, pod: dict, container: str = "",
+                include_privileged: bool = False) -> List[ContainerTarget]:
         """:meth:`targets` for a transaction: a container that vanished meanwhile (pod deleted
         or restarted mid-attach) is a MountError, so the caller's rollback runs."""
         try:
-            return self.targets(pod, container)
+            return self.targets(pod, container, include_privileged)
         except (CgroupError, OSError) as e:
             raise MountError(f"cannot resolve the pod's containers: {e}") from e
 
@@ -140,22 +145,33 @@ class HotMount:
             for t in targets:
                 cid = t.ref.id
                 known = j.nodes_of(cid)
+                # nodes the container holds already and gpumounter did not create are never
+                # recorded, not even for the moment between the write-ahead and the create: a
+                # worker killed in that window must not leave them journaled as its own
+                with trace.span("devnodes_probe", nodes=len(after)):
+                    states = self.writer.present_states(t.target, after)
+                theirs = {(n.major, n.minor) for n, st in zip(after, states)
+                          if st and (n.major, n.minor) not in known}
                 # write-ahead: the journal names the state before the kernel holds it
                 j.intend(cid, [((n.major, n.minor), n.path) for n in grant],
-                         [((n.major, n.minor), n.path) for n in after], **self._owner(pod, t))
+                         [((n.major, n.minor), n.path) for n in after
+                          if (n.major, n.minor) not in theirs], **self._owner(pod, t))
+                # in `done` before the kernel call: an apply that fails part-way (a v1 write of
+                # several lines, a set-mode map updated before a later step fails) is revoked
+                # by the rollback like a completed one
+                done.append((t, grant, []))
                 with trace.span("cgroup_rule", backend=self.backend.name, rules=len(grant)):
                     self.faults.check("cgroup_rule")
                     self.backend.apply(t.cgdir, grant, [], after)
-                done.append((t, grant, []))
                 self.faults.check("cgroup_rule", "after")
                 with trace.span("devnodes", nodes=len(after)):
                     self.faults.check("devnodes")
                     res = self.writer.create(t.target, after)
                 done[-1] = (t, grant, [n for n, r in zip(after, res) if r == CREATED])
-                # a node that was already there before this call (and not by our hand) stays
-                # the container's own: never recorded, so never unlinked
+                # a node another party created between the probe and the create stays theirs
                 j.settle(cid, [(n.major, n.minor) for n, r in zip(after, res)
-                               if r != CREATED and (n.major, n.minor) not in known])
+                               if r != CREATED and (n.major, n.minor) not in known
+                               and (n.major, n.minor) not in theirs])
                 self.faults.check("devnodes", "after")
         except Exception as e:
             self._rollback_attach(done, before)
@@ -181,7 +197,16 @@ class HotMount:
                 self.journal.forget(t.ref.id, (), [(n.major, n.minor) for n in created
                                                    if (n.major, n.minor) not in before_keys])
             try:
-                self.backend.apply(t.cgdir, [], granted, before)
+                # revoke what the kernel holds of it: an apply that failed part-way granted
+                # some of the set or none (a v1 deny of a rule never allowed would unbalance
+                # the allow/deny bookkeeping of a later grant)
+                try:
+                    have = self.backend.installed(t.cgdir)
+                    revoke = [n for n in granted if (n.major, n.minor) in have]
+                except Exception:  # noqa: BLE001 - cannot read back: revoke all of it
+                    revoke = list(granted)
+                if revoke:
+                    self.backend.apply(t.cgdir, [], revoke, before)
             except Exception as e:  # noqa: BLE001
                 _log.error("rollback revoke in %s failed: %s", t.cgdir, e)
             else:
@@ -209,10 +234,37 @@ class HotMount:
                 self.backend.apply(t.cgdir, [], revoke, after)
             self.journal.forget(t.ref.id, keys)
             self.faults.check("unmount", "after")
-            with trace.span("devnodes", nodes=len(revoke)):
-                self.writer.remove(t.target, revoke)
+            # only nodes gpumounter created: one the container already had stays (its rule is
+            # revoked all the same, so it is as dead as it was before the attach)
+            ours = self.journal.nodes_of(t.ref.id)
+            unlink = [n for n in revoke if (n.major, n.minor) in ours]
+            with trace.span("devnodes", nodes=len(unlink)):
+                self.writer.remove(t.target, unlink)
             self.journal.forget(t.ref.id, (), keys)
         return targets
+
+    def adopt(self, pod: dict, hot: Sequence[AmdGpu], base: Sequence[AmdGpu] = ()) -> int:
+        """Seed the journal for containers of a pod that holds hot-mounted GPUs but has no
+        journal record at all: grants made by a worker without a journal (before an upgrade,
+        ``state_dir`` unset or wiped). The hot GPUs' managed rules that are granted and nodes
+        that are present are recorded as gpumounter's, so a later detach, a foreign placeholder
+        delete or the orphan sweep can revoke them. Containers with a record are left alone
+        (their record is exact); returns the number of rules + nodes adopted."""
+        want = self.managed_nodes(hot, base)
+        if not want:
+            return 0
+        n = 0
+        for t in self.targets(pod):
+            if self.journal.get(t.ref.id) is not None:
+                continue
+            granted = self.backend.installed(t.cgdir)
+            states = self.writer.present_states(t.target, want)
+            rules = [((d.major, d.minor), d.path) for d in want if (d.major, d.minor) in granted]
+            nodes = [((d.major, d.minor), d.path) for d, st in zip(want, states) if st == 1]
+            if rules or nodes:
+                self.journal.intend(t.ref.id, rules, nodes, **self._owner(pod, t))
+                n += len(rules) + len(nodes)
+        return n
 
     def repair(self, pod: dict, missing: Sequence[AuditIssue], hot: Sequence[AmdGpu],
                base: Sequence[AmdGpu] = ()) -> None:
@@ -319,11 +371,16 @@ class HotMount:
             ent = self.journal.get(t.ref.id)
             if ent is None:
                 continue
+            own = None
             for (ma, mi), path in sorted(ent.rules.items()):
                 k = (ma, mi)
                 if k in want_keys or k in base_keys:
                     continue
-                if k in allowed:
+                if own is None:
+                    # our own installed grants, not the effective verdict: a foreign program
+                    # vetoing the pair today does not make our grant go away
+                    own = self.backend.installed(t.cgdir)
+                if k in own:
                     issues.append(AuditIssue(t.ref.name, "stale_rule", path, ma, mi))
                 else:
                     self.journal.forget(t.ref.id, [k])        # already gone from the kernel

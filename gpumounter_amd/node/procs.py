@@ -9,6 +9,7 @@ fallback when amdsmi cannot report processes. Force-removal pins the container's
 with pidfds *before* the busy check (:class:`Pinned`): membership in the container's cgroup is
 re-read after pinning, and SIGTERM, the liveness wait and the SIGKILL escalation all go through
 those pidfds — so a PID the kernel recycles between the snapshot and the kill can never be hit.
+Nothing in this module signals a bare PID number.
 """
 from __future__ import annotations
 
@@ -99,33 +100,35 @@ def busy_pids(inv: Inventory, gpus: Sequence[AmdGpu], container_pids: Iterable[i
     return out
 
 
-def signal_pids(pids: Sequence[int], sig: int) -> List[int]:
-    if not pids:
-        return []
-    arr = (C.c_int32 * len(pids))(*pids)
-    res = (C.c_int * len(pids))()
-    _native.host().gm_proc_signal(arr, len(pids), sig, res)
-    return [int(res[i]) for i in range(len(pids))]
+def start_time(pid: int) -> int:
+    """Start time of ``pid`` in clock ticks since boot (``/proc/<pid>/stat`` field 22), or 0 if
+    there is no such process. (PID, start time) names one process for the node's uptime: a
+    recycled PID has a later start time. Used where no pidfd can be held — across a worker
+    restart, for the PIDs a drained placeholder waits on."""
+    try:
+        with open(f"/proc/{pid}/stat", "rb") as fh:
+            raw = fh.read()
+    except OSError:
+        return 0
+    # comm may contain spaces and parentheses: the fields after it start at the last ')'
+    rest = raw[raw.rfind(b")") + 2:].split()
+    try:
+        return int(rest[19])
+    except (IndexError, ValueError):
+        return 0
 
 
-def alive(pid: int) -> bool:
-    return signal_pids([pid], 0)[0] == 0
-
-
-async def terminate(pids: Sequence[int], sig: int = signal.SIGTERM, grace_s: float = 5.0) -> List[int]:
-    """SIGTERM, wait up to ``grace_s``, then SIGKILL survivors. Returns PIDs signalled."""
-    if not pids:
-        return []
-    signal_pids(pids, sig)
-    deadline = asyncio.get_running_loop().time() + grace_s
-    left = list(pids)
-    while left and asyncio.get_running_loop().time() < deadline:
-        await asyncio.sleep(0.02)
-        left = [p for p in left if alive(p)]
-    if left:
-        _log.warning("SIGKILL after %.1fs grace: %s", grace_s, left)
-        signal_pids(left, signal.SIGKILL)
-    return list(pids)
+def same_process(pid: int, started: int) -> bool:
+    """``pid`` is still the process that had start time ``started`` (and has not exited)."""
+    st = start_time(pid)
+    if not st or st != started:
+        return False
+    try:
+        with open(f"/proc/{pid}/stat", "rb") as fh:
+            raw = fh.read()
+        return raw[raw.rfind(b")") + 2:][:1] != b"Z"      # a zombie holds no fds any more
+    except OSError:
+        return False
 
 
 class Pinned:
@@ -181,25 +184,58 @@ class Pinned:
                 out.append(-(e.errno or errno.ESRCH))
         return out
 
-    async def terminate(self, pids: Sequence[int], sig: int = _sig.SIGTERM,
-                        grace_s: float = 5.0, already_signalled: bool = False) -> List[int]:
-        """``sig``, wait up to ``grace_s`` for the pinned processes to exit, SIGKILL survivors,
-        then release the pidfds. Returns the PIDs that needed SIGKILL."""
-        try:
-            live = [p for p in pids if p in self.fds]
-            if not already_signalled:
-                self.signal(live, sig)
-            loop = asyncio.get_running_loop()
-            deadline = loop.time() + grace_s
-            while live and loop.time() < deadline:
-                await asyncio.sleep(0.02)
-                live = [p for p in live if not self.exited(p)]
-            if live:
-                _log.warning("SIGKILL after %.1fs grace: %s", grace_s, live)
-                self.signal(live, _sig.SIGKILL)
+    async def wait_exit(self, pids: Sequence[int], timeout: float) -> List[int]:
+        """Wait up to ``timeout`` s for the pinned processes to exit (their pidfds become
+        readable: no polling); returns the ones still running."""
+        live = [p for p in pids if p in self.fds and not self.exited(p)]
+        if not live or timeout <= 0:
             return live
+        loop = asyncio.get_running_loop()
+        done = loop.create_future()
+        left = set(live)
+
+        def on_exit(pid: int) -> None:
+            loop.remove_reader(self.fds[pid])
+            left.discard(pid)
+            if not left and not done.done():
+                done.set_result(None)
+        for p in live:
+            loop.add_reader(self.fds[p], on_exit, p)
+        try:
+            await asyncio.wait_for(asyncio.shield(done), timeout)
+        except asyncio.TimeoutError:
+            pass
         finally:
-            self.close()
+            for p in list(left):
+                loop.remove_reader(self.fds[p])
+        return sorted(p for p in live if not self.exited(p))
+
+    async def reap(self, pids: Sequence[int], sig: int = _sig.SIGTERM, grace_s: float = 5.0,
+                   kill_wait_s: float = 2.0, already_signalled: bool = False
+                   ) -> Tuple[List[int], List[int]]:
+        """``sig``; wait up to ``grace_s`` for the pinned processes to exit; SIGKILL the rest
+        and wait up to ``kill_wait_s`` for them to go. Returns (PIDs that needed SIGKILL, PIDs
+        still running after it — uninterruptible sleep). The pidfds stay open: a caller that
+        must wait on survivors keeps them, then calls :meth:`close`."""
+        live = [p for p in pids if p in self.fds]
+        if not already_signalled:
+            self.signal(live, sig)
+        live = await self.wait_exit(live, grace_s)
+        if not live:
+            return [], []
+        _log.warning("SIGKILL after %.1fs grace: %s", grace_s, live)
+        self.signal(live, _sig.SIGKILL)
+        survivors = await self.wait_exit(live, kill_wait_s)
+        if survivors:
+            _log.error("still running %.1fs after SIGKILL (uninterruptible?): %s",
+                       kill_wait_s, survivors)
+        return live, survivors
+
+    def keep_only(self, pids: Iterable[int]) -> None:
+        """Close every pidfd except those of ``pids`` (the ones a drain still waits on)."""
+        want = set(pids)
+        for p in [p for p in self.fds if p not in want]:
+            os.close(self.fds.pop(p))
 
     def close(self) -> None:
         for fd in self.fds.values():

@@ -152,6 +152,9 @@ class Config:
     quota_mode: str = "enforce"
     kill_signal: int = 15              # SIGTERM like the reference's `kill` (namespace.go:192)
     kill_grace_s: float = 5.0          # then SIGKILL
+    # after SIGKILL, wait this long for the processes to exit before answering; the GPU stays
+    # booked (draining placeholder) until they have, however long that takes
+    kill_reap_s: float = 2.0
     # --- timeouts / loops ------------------------------------------------------------------
     attach_timeout_s: float = 120.0
     detach_timeout_s: float = 60.0

@@ -49,6 +49,7 @@ class ReconcileReport:
     orphans: int = 0
     errors: List[str] = field(default_factory=list)
     claims_deleted: List[str] = field(default_factory=list)   # DRA mode: orphan claims
+    drained: List[str] = field(default_factory=list)   # draining placeholders released
 
     def to_dict(self) -> dict:
         return self.__dict__.copy()
@@ -75,8 +76,8 @@ class Reconciler:
     def _on_foreign_delete(self, ph: dict) -> None:
         md = ph["metadata"]
         ann = md.get("annotations") or {}
-        if ann.get("gpumounter.amd.com/mount-mode") == "standby":
-            return
+        if ann.get("gpumounter.amd.com/mount-mode") in ("standby", "draining"):
+            return   # pool capacity / a drain: no tenant has access to revoke
         ons = (md.get("labels") or {}).get("gpumounter.amd.com/owner-namespace", "")
         oname = ann.get("gpumounter.amd.com/owner-name", "")
         if oname:
@@ -197,14 +198,21 @@ class Reconciler:
             await svc.read_ledger(authoritative=True)
         except Exception as e:  # noqa: BLE001
             rep.errors.append(f"ledger: {e}")
+        if not svc.adopted:
+            try:
+                await svc.adopt_existing()
+            except Exception as e:  # noqa: BLE001
+                rep.errors.append(f"journal adoption: {e}")
         ck = svc.ph.checkpoint
         from_ckpt = ck is not None and ck.trusted and ck.snapshot() is not None
         placeholders = svc.ph.live()
         by_owner: Dict[tuple, List[dict]] = {}
         for p in placeholders:
             ann = p["metadata"].get("annotations") or {}
-            if ann.get("gpumounter.amd.com/mount-mode") == "standby":
-                continue  # warm-pool capacity: owned by the pool, not by a tenant
+            if ann.get("gpumounter.amd.com/mount-mode") in ("standby", "draining"):
+                # warm-pool capacity (owned by the pool), or a force-removed GPU waiting for
+                # its killed processes to exit (worker/drain.py): no tenant to audit
+                continue
             owner = (ann.get("gpumounter.amd.com/owner-name", ""),
                      (p["metadata"].get("labels") or {}).get("gpumounter.amd.com/owner-namespace", ""),
                      ann.get(ANN_OWNER_UID, ""))
@@ -304,6 +312,10 @@ class Reconciler:
                     if name not in rep.revoked:
                         rep.revoked.append(name)
                     m.reconcile_actions.labels(action="revoke").inc()
+        try:
+            rep.drained = await svc.drain.sweep()
+        except Exception as e:  # noqa: BLE001
+            rep.errors.append(f"drain sweep: {e}")
         for name in list(self._first_seen):
             if not any(p["metadata"]["name"] == name for p in placeholders):
                 del self._first_seen[name]
@@ -324,6 +336,6 @@ class Reconciler:
                 rep.errors.append(f"resourceclaim sweep: {e}")
         self.last = rep
         if rep.owner_gone or rep.stuck or rep.repaired or rep.revoked or rep.errors or \
-                rep.claims_deleted:
+                rep.claims_deleted or rep.drained:
             log.kv(_log, 20, "reconciled", **rep.to_dict())
         return rep

@@ -193,6 +193,10 @@ class Worker:
         # warm the ledger channel (fails fast if the kubelet socket is wrong); the authoritative
         # read also cross-checks the device-manager checkpoint before admission relies on it
         await self.service.read_ledger(authoritative=True)
+        try:   # grants from before the journal existed become revocable (node/hotmount.py adopt)
+            await self.service.adopt_existing()
+        except Exception as e:  # noqa: BLE001 - the reconciler retries
+            _log.error("journal adoption at startup: %s", e)
         if self.checkpoint is not None:
             watched = self.checkpoint.watch(
                 lambda: asyncio.ensure_future(self.ph_informer.poke()))
@@ -352,6 +356,7 @@ class Worker:
         await self.pool.stop()
         await self.reconciler.stop()
         await self.service.lease.stop()
+        await self.service.drain.stop()
         await self.service.notify.stop()
         if isinstance(self.backend, systemd.SystemdPersistingBackend):
             self.backend.sync.stop()

@@ -37,14 +37,16 @@ from gpumounter_amd.hw import topology
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu, gpus_by_key, normalize_device_id
-from gpumounter_amd.models.types import (ANN_IDEMPOTENCY, ERR_INTERNAL, ERR_POLICY, ERR_QUOTA,
-                                         MountType)
+from gpumounter_amd.models.types import (ANN_IDEMPOTENCY, ANN_MOUNT_MODE, ANN_OWNER_UID,
+                                         ERR_INTERNAL, ERR_POLICY, ERR_QUOTA, LABEL_OWNER_NS,
+                                         MODE_DRAINING, MODE_STANDBY, MountType)
 from gpumounter_amd.node import procs
 from gpumounter_amd.node.hotmount import HotMount, MountError
 from gpumounter_amd.node.ledger import LedgerClient, LedgerError
 from gpumounter_amd.utils import log, trace
 from gpumounter_amd.utils.faults import FaultInjector, InjectedFault
 from gpumounter_amd.utils.metrics import Metrics
+from gpumounter_amd.worker.drain import DrainKeeper
 from gpumounter_amd.worker.lease import LeaseKeeper
 from gpumounter_amd.worker.notify import Notifier
 
@@ -99,6 +101,7 @@ class GpuMountService:
         self._ns_seen: set = set()
         self.unhealthy: set = set()   # GPU indices failing liveness/ECC (Worker.check_health)
         self.lease = LeaseKeeper(self)
+        self.drain = DrainKeeper(self)   # force-removed GPUs whose processes have not exited
         # Reservations that must not interleave on a node run one at a time:
         # * trim briefly holds every free GPU — a concurrent one would see a full node;
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
@@ -108,6 +111,7 @@ class GpuMountService:
         self._own: Dict[str, Tuple[str, ...]] = {}   # pod uid → its own device-plugin GPU IDs
         self.ledger_reads = 0
         self.ledger_reads_checkpoint = 0
+        self.adopted = False           # adopt_existing() has run to completion
 
     # ------------------------------------------------------------------------ helpers
     def pod_lock(self, ns: str, name: str) -> asyncio.Lock:
@@ -244,6 +248,43 @@ class GpuMountService:
         if stale:
             self.hm.revoke_issues(pod, stale, st.hot, st.own)
         return issues
+
+    async def adopt_existing(self) -> int:
+        """Seed the injection journal from the ledger for every live owner that has
+        hot-mounted GPUs but no journal record (node/hotmount.py ``adopt``): the upgrade path
+        from a worker without a journal, or one whose state_dir was lost. Runs once, before the
+        worker serves, and again from the reconciler until it has succeeded."""
+        if self.adopted:
+            return 0
+        owners: Dict[Tuple[str, str], str] = {}
+        for p in self.ph.live():
+            md = p["metadata"]
+            ann = md.get("annotations") or {}
+            if ann.get(ANN_MOUNT_MODE) in (MODE_STANDBY, MODE_DRAINING):
+                continue
+            ons = (md.get("labels") or {}).get(LABEL_OWNER_NS, "")
+            oname = ann.get("gpumounter.amd.com/owner-name", "")
+            if oname:
+                owners[(ons, oname)] = ann.get(ANN_OWNER_UID, "")
+        n = 0
+        for (ns, name), uid in owners.items():
+            pod = self.node_pods.get(ns, name)
+            if pod is None or podu.uid_of(pod) != uid or podu.phase_of(pod) != "Running" or \
+                    self.is_self(pod):
+                continue
+            async with self.pod_lock(ns, name):
+                st = await self.pod_state(pod, ledger_snapshot=self.ph.last_ledger or None)
+                if st.mount_type == MountType.UNKNOWN:
+                    return n                     # ledger unreadable: the reconciler retries
+                try:
+                    n += self.hm.adopt(pod, st.hot, st.own)
+                except Exception as e:  # noqa: BLE001 - a container that went away meanwhile
+                    _log.warning("journal adoption for %s/%s: %s", ns, name, e)
+        self.adopted = True
+        if n:
+            log.kv(_log, 30, "adopted hot-mount state with no journal record", entries=n,
+                   owners=len(owners))
+        return n
 
     async def _rollback(self, pod: dict, what: str) -> bool:
         """Reconcile the pod to its ledger state after a failed operation. Returns True if the
@@ -625,12 +666,17 @@ class GpuMountService:
                 with trace.span("busy_check"):
                     self.faults.check("busy_check")
                     targets = self.hm.resolve(pod, req.container)
-                    cpids = sorted({p for t in targets for p in t.pids})
+                    # privileged containers get no rule/node writes, but their processes use
+                    # the GPU all the same: they count for busy and are killed by force
+                    everyone = self.hm.resolve(pod, req.container, include_privileged=True) \
+                        if any(r.privileged for r in podu.running_containers(pod, req.container)) \
+                        else targets
+                    cpids = sorted({p for t in everyone for p in t.pids})
                     # pin the snapshot, then confirm membership: from here on a recycled PID
                     # cannot be mistaken for a container process (node/procs.py Pinned)
                     pinned = procs.Pinned(cpids)
                     if pinned.fds:
-                        pinned.restrict({p for t in targets
+                        pinned.restrict({p for t in everyone
                                          for p in self.hm.resolver.pids(t.cgdir)})
                     busy = procs.busy_pids(self.inv, selected, pinned.pids(),
                                            self.cfg.drm_major, self.cfg.busy_detection)
@@ -652,21 +698,36 @@ class GpuMountService:
             phs = [ph for ph in st.placeholders
                    if {g.index for g in st.by_placeholder[(ph.namespace, ph.name)]} & sel_idx]
             killed: List[int] = sorted({p for v in busy.values() for p in v})
+            survivors: List[int] = []
+            held: List[Placeholder] = []
             try:
-                # revoke before release: the GPU never becomes schedulable while the tenant can
-                # still reach it (reference order deny → rm → kill, util.go:112-139)
+                # revoke, then kill, then release (reference order deny → rm → kill,
+                # util.go:112-139, then slave deletion, server.go:170-175). The revoke only
+                # gates open(): a killed process keeps its render/KFD fds until it has exited,
+                # so the placeholder keeps the GPU booked until then (worker/drain.py)
                 with trace.span("unmount", gpus=len(selected)):
                     self.hm.detach(pod, selected, keep, st.own, req.container, targets)
                 if killed:
                     with trace.span("kill", pids=len(killed)):
                         pinned.signal(killed, self.cfg.kill_signal)
-                        # the pidfds move to the escalation task, which closes them
-                        p, pinned = pinned, None
-                        asyncio.ensure_future(p.terminate(killed, self.cfg.kill_signal,
-                                                          self.cfg.kill_grace_s,
-                                                          already_signalled=True))
+                        _, survivors = await pinned.reap(
+                            killed, self.cfg.kill_signal, self.cfg.kill_grace_s,
+                            self.cfg.kill_reap_s, already_signalled=True)
+                if survivors:
+                    left = set(survivors)
+                    stuck = {i for i, v in busy.items() if left.intersection(v)}
+                    held = [ph for ph in phs if stuck & {
+                        g.index for g in st.by_placeholder[(ph.namespace, ph.name)]}]
+                    phs = [ph for ph in phs if ph not in held]
+                    p, pinned = pinned, None
+                    with trace.span("drain_hold", placeholders=len(held)):
+                        unmarked = await self.drain.hold(pod, held, p, survivors)
+                    if unmarked:   # still the tenant's: booked, and retried by RemoveGPU
+                        _log.error("placeholders %s stay with %s/%s",
+                                   [u.name for u in unmarked], req.namespace, req.pod_name)
                 else:
                     pinned.close()
+                    pinned = None
                 await self._release(phs)
             except (MountError, ReserveError, InjectedFault, OSError) as e:
                 if pinned is not None:
@@ -676,11 +737,21 @@ class GpuMountService:
                     return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_POD_NOT_FOUND,
                                                  message=f"pod went away: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
-            owner = {g.index: ph.name for ph in phs
+            owner = {g.index: ph.name for ph in phs + held
                      for g in st.by_placeholder[(ph.namespace, ph.name)]}
             log.kv(_log, 20, "detached", pod=f"{req.namespace}/{req.pod_name}",
-                   gpus=[g.bdf for g in selected], killed=killed, by=req.requested_by)
+                   gpus=[g.bdf for g in selected], killed=killed, by=req.requested_by,
+                   still_running=survivors)
             self.notify.detached(pod, selected, keep, killed, by=req.requested_by)
+            if survivors:
+                gone = {g.index for ph in held for g in st.by_placeholder[(ph.namespace, ph.name)]}
+                uuids = [g.uuid for g in selected if g.index in gone]
+                return api.RemoveGPUResponse(
+                    remove_gpu_result=api.REMOVE_BUSY, devices=self._devices(selected, owner),
+                    killed_pids=killed,
+                    message=f"busy: processes {survivors} still running "
+                            f"{self.cfg.kill_reap_s:g}s after SIGKILL; access to {uuids} is "
+                            f"revoked and they stay reserved until those processes exit")
             return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_SUCCESS,
                                          devices=self._devices(selected, owner),
                                          killed_pids=killed, message="Remove GPU Success")

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define GM_HOST_ABI_VERSION 5
+#define GM_HOST_ABI_VERSION 6
 
 // Access bits follow BPF_DEVCG_ACC_* so the same rule feeds both cgroup versions.
 #define GM_ACC_MKNOD 1
@@ -176,8 +176,6 @@ int gm_devnodes_present(int pid, const char* root, const gm_dev_node_t* nodes, i
                         uint8_t* present);
 
 // ---- processes ------------------------------------------------------------------------------
-// Sends `sig` to each pid via pidfd (falls back to kill(2)). results[i] = 0 or -errno.
-int gm_proc_signal(const int32_t* pids, int n, int sig, int* results);
 // PIDs with an open fd on char device major:minor (scans /proc/*/fd). *n = total found.
 int gm_proc_dev_users(uint32_t major, uint32_t minor, int32_t* pids, int cap, int* n);
 // Of `pids`, those holding an fd on char device major:minor (scans only /proc/<pid>/fd of the

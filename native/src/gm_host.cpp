@@ -1569,25 +1569,6 @@ int gm_devnodes_present(int pid, const char* root, const gm_dev_node_t* nodes, i
 }
 
 // ------------------------------------------------------------------ processes
-int gm_proc_signal(const int32_t* pids, int n, int sig, int* results) {
-  int failures = 0;
-  for (int i = 0; i < n; ++i) {
-    int r = 0;
-    long pfd = syscall(SYS_pidfd_open, pids[i], 0);
-    if (pfd >= 0) {
-      if (syscall(SYS_pidfd_send_signal, (int)pfd, sig, nullptr, 0) < 0) r = -errno;
-      close((int)pfd);
-    } else if (errno == ENOSYS) {
-      if (kill(pids[i], sig) < 0) r = -errno;
-    } else {
-      r = -errno;
-    }
-    results[i] = r;
-    if (r < 0) ++failures;
-  }
-  return failures;
-}
-
 namespace {
 bool pid_uses_dev(long pid, dev_t want) {
   char p[64];

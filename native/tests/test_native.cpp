@@ -172,9 +172,6 @@ static void test_pids() {
   EXPECT(gm_proc_read_pids(path, pids, 2, &n) == 0);
   EXPECT(n == 3 && pids[0] == 12 && pids[1] == 345);
   unlink(path);
-  int32_t self = getpid();
-  int r = 1;
-  EXPECT(gm_proc_signal(&self, 1, 0, &r) == 0 && r == 0);  // signal 0 = existence probe
 }
 
 static void test_smi_mock() {

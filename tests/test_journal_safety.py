@@ -1,0 +1,252 @@
+"""Ownership bookkeeping edge cases.
+
+The reference only ever revokes what its ledger selects for the pod it was asked about
+(reference: pkg/util/util.go:73-147): a node the container already had is never removed, and a
+GPU still used by any process of the container — privileged or not — makes it busy
+(util.go:152-196). The journal (node/journal.py) must keep to that across crashes, partial
+kernel calls, upgrades and foreign BPF programs."""
+import asyncio
+import os
+import subprocess
+
+import pytest
+
+from gpumounter_amd import _native
+from gpumounter_amd.fakes.harness import LocalCluster
+from gpumounter_amd.node.hotmount import HotMount
+from gpumounter_amd.node.journal import InjectionJournal
+
+
+def run(coro_fn, **kw):
+    async def main():
+        async with LocalCluster(**kw) as lc:
+            return await coro_fn(lc)
+    return asyncio.run(main())
+
+
+def node_of(lc):
+    return lc.nodes["node-0"].node
+
+
+def _marker(path, ma, mi):
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w") as fh:
+        fh.write(f"gm-chr {ma}:{mi}\n")
+
+
+class _Crash(BaseException):
+    """A SIGKILL stand-in: nothing after it runs (no except-Exception rollback)."""
+
+
+# ------------------------------------------------------------------------------ write-ahead
+def test_crash_between_intent_and_create_never_journals_a_preexisting_node(monkeypatch):
+    """Worker killed after the write-ahead record and before the create, with the GPU's render
+    node already in the tenant's rootfs: after a restart the pre-existing node is not
+    gpumounter's, so neither the orphan sweep nor a detach unlinks it."""
+    async def body(lc):
+        lc.tenant("t")
+        cid = lc.container_ids("default", "t")[0]
+        root = node_of(lc).container(cid).root_dir
+        w = lc.nodes["node-0"].worker
+        g = lc.inventory.gpus()[0]
+        pre = os.path.join(root, f"dev/dri/renderD{g.render_minor}")
+        _marker(pre, 226, g.render_minor)
+        pod = lc.cluster.get("default", "t")
+
+        def crash(*a, **k):
+            raise _Crash()
+        monkeypatch.setattr(w.service.hm.writer, "create", crash)
+        with pytest.raises(_Crash):
+            w.service.hm.attach(pod, [g], [], [])
+        monkeypatch.undo()
+        # what a restarted worker reads from the node's state dir
+        j = InjectionJournal(os.path.join(node_of(lc).state_dir, "journal"))
+        nodes = j.nodes_of(cid)
+        assert (226, g.render_minor) not in nodes, nodes
+        assert (226, g.card_minor) in nodes and (lc.inventory.kfd_major, 0) in nodes
+        await lc.stop_worker("node-0")
+        w2 = await lc.start_worker("node-0")
+        rep = await w2.reconciler.run_once()        # no placeholder backs it: orphan sweep
+        assert rep.revoked == ["default/t"], rep
+        assert os.path.exists(pre)                  # the container's own node stays
+        assert (226, g.render_minor) not in w2.journal.nodes_of(cid)
+    run(body, worker_overrides={"reconcile_on_events": False})
+
+
+def test_attach_with_preexisting_node_then_detach_keeps_it():
+    async def body(lc):
+        lc.tenant("t")
+        cid = lc.container_ids("default", "t")[0]
+        root = node_of(lc).container(cid).root_dir
+        g = lc.inventory.gpus()[0]
+        pre = os.path.join(root, f"dev/dri/renderD{g.render_minor}")
+        _marker(pre, 226, g.render_minor)
+        code, b = await lc.add("default", "t", 1)
+        assert code == 200 and b["devices"][0]["index"] == g.index
+        assert (226, g.render_minor) not in lc.nodes["node-0"].worker.journal.nodes_of(cid)
+        code, _ = await lc.remove("default", "t", [b["devices"][0]["uuid"]])
+        assert code == 200 and os.path.exists(pre)
+        assert not os.path.exists(os.path.join(root, f"dev/dri/card{g.card_minor}"))
+    run(body)
+
+
+# ------------------------------------------------------------------------------ partial apply
+@pytest.mark.parametrize("cgroup_mode", ["v1", "v2"])
+def test_apply_failing_after_its_grant_took_effect_is_rolled_back(cgroup_mode):
+    """The backend grants, then fails (a later line of a v1 write, a set-mode program step
+    after the map update): the failing container's grant is revoked and nothing stays
+    journaled."""
+    async def body(lc):
+        lc.tenant("t")
+        w = lc.nodes["node-0"].worker
+        be = w.service.hm.backend
+        real = be.apply
+        calls = []
+
+        def flaky(cgdir, grant, revoke, desired):
+            real(cgdir, grant, revoke, desired)
+            calls.append(len(grant))
+            if grant and len(calls) == 1:
+                raise OSError("EIO after the grant")
+        be.apply = flaky
+        code, _ = await lc.add("default", "t", 1)
+        be.apply = real
+        assert code == 500
+        cid = lc.container_ids("default", "t")[0]
+        ctr = node_of(lc).container(cid)
+        assert be.allowed(ctr.cgroup_dir) == set(), "grant left behind after rollback"
+        assert w.journal.get(cid) is None
+        assert not await lc.audit("default", "t")
+        code, _ = await lc.add("default", "t", 1)      # and the next attach works normally
+        assert code == 200 and not await lc.audit("default", "t")
+    run(body, cgroup_mode=cgroup_mode)
+
+
+# ------------------------------------------------------------------------------ adoption
+def test_grants_from_a_worker_without_journal_are_adopted_and_revocable():
+    """Upgrade path: a pod hot-mounted by a worker that kept no journal (state dir wiped). The
+    new worker adopts the hot GPUs' granted rules and present nodes at startup, so a placeholder
+    deleted by someone else afterwards still gets the tenant's access revoked."""
+    async def body(lc):
+        lc.tenant("t")
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200
+        cid = lc.container_ids("default", "t")[0]
+        jdir = os.path.join(node_of(lc).state_dir, "journal")
+        await lc.stop_worker("node-0")
+        for f in os.listdir(jdir):                    # the record is lost
+            os.unlink(os.path.join(jdir, f))
+        w = await lc.start_worker("node-0")
+        assert w.service.adopted
+        assert len(w.journal.nodes_of(cid)) == 5 and len(w.journal.rules_of(cid)) == 5
+        # someone deletes one placeholder: its GPU goes back to the scheduler
+        ph = lc.cluster.placeholders()[0]
+        lc.cluster.delete(ph["metadata"]["namespace"], ph["metadata"]["name"], grace=0)
+        await asyncio.sleep(0.05)
+        rep = await w.reconciler.run_once()
+        assert rep.orphans >= 2, rep                  # its render + card rule and nodes
+        assert not await lc.audit("default", "t")
+        devs = node_of(lc).container_devices(cid)
+        assert sum("renderD" in d for d in devs) == 1 and "dev/kfd" in devs
+    run(body, worker_overrides={"reconcile_on_events": False})
+
+
+def test_adoption_leaves_containers_with_a_record_alone(mock_inventory):
+    async def body(lc):
+        lc.tenant("t")
+        await lc.add("default", "t", 1)
+        w = lc.nodes["node-0"].worker
+        w.service.adopted = False
+        assert await w.service.adopt_existing() == 0
+    run(body)
+
+
+# ------------------------------------------------------------------------------ foreign veto
+def test_audit_keeps_journaled_rule_that_a_foreign_program_vetoes():
+    """v2: a foreign program (systemd re-realising its unit) vetoes a pair gpumounter still
+    grants in its own program. The effective verdict says "not allowed", but our grant is
+    there: the journal must keep it (and report it stale once the ledger drops it), or it
+    would never be revoked once the foreign program is gone."""
+    class Backend:
+        name = "test"
+
+        def __init__(self):
+            self.own = {(226, 128)}
+
+        def allowed(self, cgdir):
+            return set()                      # vetoed by someone else's program
+
+        def installed(self, cgdir):
+            return set(self.own)
+
+        def apply(self, cgdir, grant, revoke, desired):
+            self.own -= {(n.major, n.minor) for n in revoke}
+
+    class Writer:
+        def present_many(self, t, nodes):
+            return [False] * len(nodes)
+
+        def present(self, t, n):
+            return False
+
+        def remove(self, t, nodes):
+            return [0] * len(nodes)
+
+    class Cfg:
+        drm_major, inject_card_nodes, device_file_mode, container_root_prefix = 226, True, \
+            0o666, "/nonexistent"
+
+    class Resolver:
+        def container_dir(self, pod, ref):
+            return "/cg"
+
+        def pids(self, cgdir):
+            return []
+
+    from gpumounter_amd.hw.inventory import Inventory
+    inv = Inventory("mock")
+    j = InjectionJournal()
+    hm = HotMount(Cfg(), inv, Resolver(), Backend(), Writer(), journal=j)
+    pod = {"metadata": {"name": "p", "namespace": "d", "uid": "u"},
+           "spec": {"containers": [{"name": "c"}]},
+           "status": {"phase": "Running", "containerStatuses": [
+               {"name": "c", "containerID": "containerd://abc", "state": {"running": {}}}]}}
+    j.intend("abc", [((226, 128), "/dev/dri/renderD128")], [], namespace="d", pod="p",
+             pod_uid="u", container="c", cgdir="/cg")
+    issues = hm.audit(pod, [], [])
+    assert [(i.kind, i.minor) for i in issues] == [("stale_rule", 128)]
+    assert j.rules_of("abc")                      # still ours: kept until revoked
+    hm.revoke_issues(pod, issues, [], [])
+    assert not j.rules_of("abc") and hm.backend.own == set()
+
+
+# ------------------------------------------------------------------------------ privileged busy
+def test_privileged_pod_gpu_process_is_busy_and_force_killed(tmp_path, mock_inventory):
+    """A privileged pod gets a ledger-only attach (no rules or nodes written), but its
+    processes count: RemoveGPU reports busy, and force kills them."""
+    sleeper = subprocess.Popen(["sleep", "60"])
+    table = tmp_path / "procs"
+    _native.mock_smi().gm_mock_set_procs_file(str(table).encode())
+    try:
+        async def body(lc):
+            c = {"name": "main", "image": "x", "command": ["sleep", "infinity"],
+                 "securityContext": {"privileged": True}}
+            lc.cluster.create_running_pod("default", {"metadata": {"name": "priv"},
+                                                      "spec": {"containers": [c]}},
+                                          "node-0", {"main": [sleeper.pid]})
+            code, b = await lc.add("default", "priv", 1)
+            assert code == 200
+            dev = b["devices"][0]
+            table.write_text(f"{dev['index']} {sleeper.pid} 4096 python\n")
+            code, _ = await lc.remove("default", "priv", [dev["uuid"]])
+            assert code == 400                               # busy, not silently released
+            assert len(lc.cluster.placeholders()) == 1
+            code, b2 = await lc.remove("default", "priv", [dev["uuid"]], force=True)
+            assert code == 200 and b2["killed_pids"] == [sleeper.pid]
+            assert lc.cluster.placeholders() == []
+        run(body, worker_overrides={"busy_detection": "both"})
+        assert sleeper.wait(timeout=10) == -15
+    finally:
+        _native.mock_smi().gm_mock_set_procs_file(b"")
+        if sleeper.poll() is None:
+            sleeper.kill()

@@ -227,18 +227,20 @@ def test_v2_recording_backend_program_semantics(tmp_path, mock_inventory):
     assert build_program(NODES[:1], chained=False)[-1] == build_program(NODES, chained=False)[-1]
 
 
-def test_host_signal_and_pid_helpers():
+def test_host_pid_helpers():
     from gpumounter_amd.node import procs
 
     p = subprocess.Popen(["sleep", "30"])
     try:
-        assert procs.alive(p.pid)
-        assert procs.signal_pids([p.pid], 15) == [0]
-        p.wait(timeout=5)
+        st = procs.start_time(p.pid)
+        assert st > 0 and procs.same_process(p.pid, st)
+        assert not procs.same_process(p.pid, st + 1)       # another process with that number
     finally:
-        if p.poll() is None:
-            p.kill()
-    assert procs.signal_pids([2 ** 22 + 7], 0)[0] < 0   # no such process
+        p.kill()
+        p.wait()
+    assert not procs.same_process(p.pid, st)               # exited and reaped
+    assert procs.start_time(2 ** 22 + 7) == 0              # no such process
+    assert not hasattr(procs, "signal_pids") and not hasattr(procs, "terminate")
     # /dev/null users: our own stdin/stdout may or may not be /dev/null; open one to be sure
     fd = os.open("/dev/null", os.O_RDONLY)
     try:

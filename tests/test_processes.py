@@ -159,12 +159,38 @@ def test_pinned_restrict_drops_pids_that_left_the_cgroup():
         assert pin.pids() == sorted([a.pid, b.pid])
         assert pin.restrict([a.pid]) == [b.pid]            # b left the container meanwhile
         assert pin.signal([b.pid], 0) == [-3]              # ESRCH: never pinned any more
-        killed = asyncio.run(pin.terminate([a.pid], grace_s=2.0))
-        assert killed == [] and a.wait(timeout=5) != 0
+        killed, survivors = asyncio.run(pin.reap([a.pid], grace_s=2.0))
+        assert killed == [] and survivors == [] and a.wait(timeout=5) != 0
         assert b.poll() is None                            # untouched
+        pin.close()
         assert pin.fds == {}
     finally:
         for p in (a, b):
+            p.kill()
+            p.wait()
+
+
+def test_reap_escalates_to_sigkill_and_reports_exit_without_polling():
+    import subprocess
+    import sys
+    import time
+
+    from gpumounter_amd.node import procs
+    # a process that ignores SIGTERM
+    p = subprocess.Popen([sys.executable, "-c",
+                          "import signal, time; signal.signal(signal.SIGTERM, signal.SIG_IGN); "
+                          "print('ready', flush=True); time.sleep(60)"], stdout=subprocess.PIPE)
+    try:
+        assert p.stdout.readline().strip() == b"ready"
+        pin = procs.Pinned([p.pid])
+        t0 = time.monotonic()
+        killed, survivors = asyncio.run(pin.reap([p.pid], grace_s=0.3, kill_wait_s=2.0))
+        dt = time.monotonic() - t0
+        assert killed == [p.pid] and survivors == [] and 0.3 <= dt < 1.5, (killed, dt)
+        assert p.wait(timeout=5) == -9
+        pin.close()
+    finally:
+        if p.poll() is None:
             p.kill()
             p.wait()
 
