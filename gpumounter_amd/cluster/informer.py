@@ -38,6 +38,9 @@ class PodInformer:
         self.relists = 0
         self.resumes = 0
         self._seen: Dict[Key, deque] = {}    # resourceVersions the watch/list delivered per key
+        # bumped by every relist: a write whose request went out in an earlier epoch may be
+        # older than what the list delivered (see upsert)
+        self.epoch = 0
         self.handlers: List[Callable[[str, dict], None]] = []
 
     async def start(self) -> None:
@@ -72,6 +75,7 @@ class PodInformer:
             self.deleted[k] = self.cache[k]["metadata"].get("uid", "")
         self.cache = fresh
         self.rv = rv
+        self.epoch += 1
         await self._notify("RELIST", {})
 
     async def _notify(self, etype: str, pod: dict) -> None:
@@ -146,17 +150,27 @@ class PodInformer:
                 seen = self._seen[key] = deque(maxlen=16)
             seen.append(rv)
 
-    def upsert(self, pod: dict) -> None:
+    def upsert(self, pod: dict, epoch: Optional[int] = None) -> None:
         """Write-through from our own API responses (create/patch) so readers do not wait for
         the watch echo. resourceVersions are opaque (only equality is meaningful), so ordering
         comes from the watch itself: one object's events arrive in order, so if the watch has
         already delivered this response's version, the cache is at least as new and is kept;
-        if not, the watch has not reached our write yet and the response is newer."""
+        if not, the watch has not reached our write yet and the response is newer.
+
+        ``epoch``: :attr:`epoch` when the request was sent. A relist since then breaks the
+        argument above — the list may hold a *newer* version (someone wrote after us) that the
+        watch will never deliver again — so for an object the list holds, the response is
+        dropped: the list is either newer, or older and then the watch, resumed from the list's
+        version, still delivers our write."""
         md = pod.get("metadata", {})
         key = (md.get("namespace", ""), md.get("name", ""))
         rv = md.get("resourceVersion", "")
         if rv and rv in self._seen.get(key, ()):
             return
+        if epoch is not None and epoch != self.epoch:
+            cur = self.cache.get(key)
+            if cur is not None and cur["metadata"].get("uid") == md.get("uid"):
+                return
         if key in self.deleted and self.deleted[key] == md.get("uid"):
             return
         self.cache[key] = pod

@@ -372,6 +372,7 @@ class PlaceholderManager:
             self.faults.check("ledger_reserve")
             if self.dra:
                 await self._create_claims(bodies)
+            epoch = self.informer.epoch
             results = await asyncio.gather(
                 *[self.kube.create_pod(b["metadata"]["namespace"], b) for b in bodies],
                 return_exceptions=True)
@@ -381,7 +382,7 @@ class PlaceholderManager:
                    for r in results if isinstance(r, dict)]
         for r in results:
             if isinstance(r, dict):
-                self.informer.upsert(r)  # visible to owned_by() before the watch echo
+                self.informer.upsert(r, epoch)  # visible to owned_by() before the watch echo
         errors = [r for r in results if not isinstance(r, dict)]
         if errors:
             await self.release(created, wait=False)

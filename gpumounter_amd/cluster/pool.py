@@ -175,6 +175,7 @@ class WarmPool:
                 try:
                     if self.ph.dra:                     # its ResourceClaim first
                         await self.ph._create_claims([body])  # noqa: SLF001
+                    epoch = self.ph.informer.epoch
                     pod = await self.ph.kube.create_pod(self.cfg.pool_namespace, body)
                 except Exception as e:  # noqa: BLE001
                     _log.warning("standby create failed: %s", e)
@@ -182,7 +183,7 @@ class WarmPool:
                         await self.ph._delete_claims(  # noqa: SLF001
                             [(self.cfg.pool_namespace, body["metadata"]["name"])])
                     break
-                self.ph.informer.upsert(pod)        # pending() counts it from here on
+                self.ph.informer.upsert(pod, epoch)  # pending() counts it from here on
                 self._creating -= 1
                 md = pod["metadata"]
                 created.append(Placeholder(md["namespace"], md["name"], md["uid"], (),
@@ -244,12 +245,13 @@ class WarmPool:
             for ph in chosen:
                 self._claimed.add(ph.uid)
             with trace.span("pool_claim", placeholders=len(chosen)):
+                epoch = self.ph.informer.epoch
                 res = await asyncio.gather(
                     *[self.ph.kube.patch_pod(ph.namespace, ph.name, patch) for ph in chosen],
                     return_exceptions=True)
             ok = [r for r in res if isinstance(r, dict)]
             for r in ok:
-                self.ph.informer.upsert(r)
+                self.ph.informer.upsert(r, epoch)
             for ph in chosen:
                 self._claimed.discard(ph.uid)
             if len(ok) != len(chosen):
@@ -270,12 +272,13 @@ class WarmPool:
             "annotations": {ANN_OWNER_UID: None, ANN_OWNER_NAME: None,
                             ANN_MOUNT_MODE: MODE_STANDBY, ANN_ATTACH_ID: None,
                             ANN_CONTAINER: None, ANN_GROUP: None, ANN_IDEMPOTENCY: None}}}
+        epoch = self.ph.informer.epoch
         res = await asyncio.gather(*[self.ph.kube.patch_pod(p.namespace, p.name, patch)
                                      for p in phs], return_exceptions=True)
         back = []
         for p, r in zip(phs, res):
             if isinstance(r, dict):
-                self.ph.informer.upsert(r)
+                self.ph.informer.upsert(r, epoch)
                 back.append(p)
             elif not isinstance(r, NotFound):
                 _log.error("return %s/%s to pool: %s", p.namespace, p.name, r)

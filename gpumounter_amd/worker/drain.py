@@ -71,12 +71,13 @@ class DrainKeeper:
                             ANN_DRAIN_OWNER: f"{podu.ns_of(owner)}/{podu.name_of(owner)}",
                             ANN_OWNER_UID: None, ANN_IDEMPOTENCY: None, ANN_GROUP: None}}}
         kube = self.svc.ph.kube
+        epoch = self.svc.ph.informer.epoch
         res = await asyncio.gather(*[kube.patch_pod(p.namespace, p.name, patch) for p in phs],
                                    return_exceptions=True)
         failed = []
         for ph, r in zip(phs, res):
             if isinstance(r, dict):
-                self.svc.ph.informer.upsert(r)
+                self.svc.ph.informer.upsert(r, epoch)
                 ph.mode = MODE_DRAINING
             else:
                 _log.error("mark %s/%s draining: %s", ph.namespace, ph.name, r)

@@ -259,3 +259,25 @@ def test_tail_report_attributes_slow_cycles(tmp_path):
     top = rep["slowest"][0]
     assert top["largest_stage"] == ["ledger_reserve", 79.0]
     assert top["worker_ms"] == 79.2 and top["outside_worker_ms"] == 0.8   # sub-stages not summed
+
+
+def test_informer_drops_write_through_older_than_a_relist():
+    """after a relist the cache may hold a newer version than a write response whose
+    request went out before it; that response must not overwrite it (the watch resumes from
+    the list and never redelivers the newer version)."""
+    from gpumounter_amd.cluster.informer import PodInformer
+
+    inf = PodInformer(kube=None)
+
+    def pod(rv, v, name="p", uid="u"):
+        return {"metadata": {"namespace": "ns", "name": name, "uid": uid, "resourceVersion": rv,
+                             "annotations": {"v": v}}}
+    ep = inf.epoch
+    inf.cache[("ns", "p")] = pod("12", "from-list")      # what the relist delivered
+    inf.epoch += 1
+    inf.upsert(pod("9", "our-older-patch"), ep)
+    assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "from-list"
+    inf.upsert(pod("13", "patch-after-relist"), inf.epoch)
+    assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "patch-after-relist"
+    inf.upsert(pod("14", "created", name="q", uid="w"), ep)   # not in the list: newer, kept
+    assert inf.get("ns", "q") is not None
