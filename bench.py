@@ -125,9 +125,10 @@ def main() -> int:
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0,
                     help="standby placeholders per node (claim instead of create); 0 = off")
-    ap.add_argument("--placement", choices=("hint", "trim"), default="hint",
-                    help="trim = enforce the topology choice by holding every free GPU and "
-                         "releasing the surplus (placement_enforce)")
+    ap.add_argument("--placement", choices=("auto", "hint", "trim"), default="auto",
+                    help="placement_enforce: auto (default) = correct a worse-placed plugin "
+                         "choice by holding the other free GPUs; trim = always hold every free "
+                         "GPU and release the surplus; hint = annotation only")
     ap.add_argument("--device-plugin", action="store_true",
                     help="the worker serves amd.com/gpu itself; the fake kubelet's device manager "
                          "calls GetPreferredAllocation/Allocate on it at admission")
@@ -423,7 +424,13 @@ def main() -> int:
             kcalls = cp.kubelet_calls()
             p50 = pct(attach_ms, 0.5)
             ref = None
-            if args.ref_steps > 0 and args.protocol == "gpumounter" and \
+            if args.ref_steps > 0 and args.node_ops == "real":
+                # the reference writes cgroup-v1 devices.allow/deny through `sh -c echo`
+                # (pkg/util/cgroup/cgroup.go:143-169); the real-node sandbox is cgroup2, which
+                # has no such files, so there is nothing faithful to re-enact here
+                ref = {"skipped": "the reference's node operations are cgroup-v1 only "
+                                  "(devices.allow via sh); --node-ops real runs on cgroup2"}
+            elif args.ref_steps > 0 and args.protocol == "gpumounter" and \
                     args.latency == "zero" and not args.warm_pool:
                 # the reference's call sequence, emulated in the same deployment shape
                 # The reference dials the kubelet and Lists on every query with no retry

@@ -6,6 +6,9 @@
               concurrent rounds of adds/removes from 4 pods, invariant checks after each round.
   soak        "1000 attach/detach cycles across 8 GPUs; p99 latency + zero orphaned cgroup
               entries": cycles of 1-4 GPUs, single and entire mounts, final orphan audit.
+  placement   placement quality on a fragmented node with a device plugin that ignores
+              gpumounter's hint (the honest default of the fake): attaches compared with the
+              best set the free GPUs allowed.
 
 The control plane is the hermetic fake (apiserver, scheduler, kubelet); node operations are the
 production ones (cgroup rule backends, device-node writer) in their unprivileged modes. Runs
@@ -269,7 +272,65 @@ def contention_processes(args) -> dict:
             "invariant_violations": len(problems), "violation_examples": problems[:5]}
 
 
-SCENARIOS = {"scale": scale, "contention": contention, "soak": soak}
+async def placement(lc, args) -> dict:
+    """Placement quality on a fragmented node, as a device plugin that ignores gpumounter's
+    hint leaves it. Four background pods grow and shrink by single GPUs at random; between
+    their moves a probe pod attaches N ∈ {1, 2, 4} GPUs (entire or single mount, at random) and
+    detaches again. Each attach is compared with the best set the free GPUs allowed at that
+    moment (hive split ≫ non-xGMI pair ≫ NUMA split, hw/topology.py)."""
+    rnd = random.Random(args.seed)
+    bg = [f"bg{i}" for i in range(4)]
+    for t in bg + ["probe"]:
+        _tenant(lc, args, t)
+    node = lc.nodes["node-0"].node
+    svc = lc.nodes["node-0"].worker.service
+    links = lc.inventory.links()
+    table = {g.index: g for g in node.gpus}
+    by_bdf = {g.bdf: g for g in node.gpus}
+    stats = {n: {"attaches": 0, "optimal": 0, "numa_possible": 0, "numa_packed": 0,
+                 "one_hive": 0, "ms": []} for n in (1, 2, 4)}
+    for _ in range(args.rounds):
+        for t in bg:
+            st = await svc.pod_state(lc.cluster.get("default", t))
+            if st.hot and (rnd.random() < 0.45 or len(node.allocated) >= len(node.gpus) - 2):
+                await lc.remove("default", t, [rnd.choice(st.hot).uuid], force=True)
+            elif len(node.allocated) < len(node.gpus) - 2:
+                await lc.add("default", t, 1)
+        for n in (1, 2, 4):
+            free = [g for g in node.gpus if node.device_id(g) not in node.allocated]
+            best = topology.choose(free, n, links)
+            if best is None:
+                continue
+            t0 = time.perf_counter()
+            code, b = await lc.add("default", "probe", n, entire=rnd.random() < 0.5)
+            ms = (time.perf_counter() - t0) * 1e3
+            if code != 200:
+                continue          # a background move took a GPU meanwhile: not a placement
+            got = [by_bdf[d["bdf"]].index for d in b["devices"]]
+            score, hives, numa, _ = topology.score_set(table, links, got)
+            s = stats[n]
+            s["attaches"] += 1
+            s["ms"].append(ms)
+            s["optimal"] += score <= best.score + 1e-6
+            s["one_hive"] += hives == 1
+            if best.numa_nodes == 1:
+                s["numa_possible"] += 1
+                s["numa_packed"] += numa == 1
+            code, _ = await lc.remove("default", "probe", [d["uuid"] for d in b["devices"]])
+            if code != 200:
+                raise RuntimeError(f"probe detach: {code}")
+    out = {}
+    for n, s in stats.items():
+        ms = s.pop("ms")
+        out[str(n)] = dict(s, attach_p50_ms=round(pct(ms, 0.5), 3) if ms else None,
+                           attach_p99_ms=round(pct(ms, 0.99), 3) if ms else None)
+    m = svc.metrics
+    return {"per_n": out, "placement_corrections": int(m.placement_corrections._value.get()),
+            "placement_mismatch": int(m.placement_mismatch._value.get()),
+            "audit_issues": sum([len(await lc.audit("default", t)) for t in bg + ["probe"]])}
+
+
+SCENARIOS = {"scale": scale, "contention": contention, "soak": soak, "placement": placement}
 
 
 def main() -> int:
@@ -278,7 +339,10 @@ def main() -> int:
     ap.add_argument("--amdsmi", default="mock", help='"mock" (default) or "" for libamd_smi')
     ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
     ap.add_argument("--latency", choices=("zero", "realistic"), default="zero")
-    ap.add_argument("--placement", choices=("hint", "trim"), default="hint")
+    ap.add_argument("--placement", choices=("auto", "hint", "trim"), default="auto")
+    ap.add_argument("--alloc-policy", choices=("first-free", "topology"), default="first-free",
+                    help="the fake node's device plugin: first free in device order (no "
+                         "GetPreferredAllocation), or its own pod-blind topology choice")
     ap.add_argument("--device-plugin", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=50)
@@ -316,7 +380,7 @@ def main() -> int:
         lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
         async with LocalCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, latency=lat,
                                 device_plugin=args.device_plugin, worker_overrides=wov,
-                                **kw) as lc:
+                                alloc_policy=args.alloc_policy, **kw) as lc:
             # one process holds the fakes, the worker and the master here: freeze the
             # start-up heap as each daemon does on its own (utils/runtime.py), so a full
             # collection of it is not charged to whichever operation it interrupts
@@ -328,6 +392,7 @@ def main() -> int:
                              "gfx": sorted({g.gfx_target for g in gpus}),
                              "cgroup": args.cgroup, "latency": args.latency,
                              "placement": args.placement, "device_plugin": args.device_plugin,
+                             "alloc_policy": args.alloc_policy,
                              "warm_pool": args.warm_pool, "node_ops": args.node_ops}
             if args.sandbox is not None:
                 res["kernel"] = _kernel_state(lc, args)

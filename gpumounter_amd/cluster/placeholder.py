@@ -77,6 +77,8 @@ class Reservation:
     placeholders: List[Placeholder] = field(default_factory=list)
     # the device set placement asked for (empty: no preference) — for the mismatch metric
     preferred: List[str] = field(default_factory=list)
+    # the device plugin chose these freely and other GPUs were free: placement may correct it
+    corrigible: bool = False
 
     @property
     def device_ids(self) -> List[str]:
@@ -302,23 +304,18 @@ class PlaceholderManager:
             raise
         return Reservation(created)
 
-    async def reserve_trim(self, owner: dict, total: int, entire: bool, width: int,
-                           pick: Callable[[List[str]], Sequence[str]], attach_id: str = "",
-                           container: str = "", idempotency_key: str = ""
-                           ) -> Tuple[Reservation, List[Placeholder]]:
-        """Topology-pinned reservation (SURVEY §7.4.3). Which GPU the device plugin hands a
-        placeholder is opaque to us, so hold ``width`` (= every free GPU) 1-GPU placeholders at
-        once and keep the ``total`` whose device IDs ``pick`` returns. Returns the reservation and
-        the surplus placeholders, which the caller releases (or returns to the warm pool).
-        Entire mounts are the kept placeholders tied by one ``ANN_GROUP`` id, the same shape
-        as a warm-pool entire claim."""
-        if total <= 0 or width < total:
-            raise ValueError(f"bad trim reservation {total}/{width}")
+    async def hold_singles(self, owner: dict, width: int, entire: bool, group: str = "",
+                           attach_id: str = "", container: str = "",
+                           idempotency_key: str = "") -> List[Placeholder]:
+        """Create ``width`` 1-GPU placeholders at once and wait for their admission; returns
+        the admitted ones (those the scheduler could not place are released). An entire mount
+        ties them by ``group`` (``ANN_GROUP``)."""
+        if width <= 0:
+            return []
         mode = "entire" if entire else "single"
         bodies = [self.build(owner, 1, mode, (), attach_id, container, idempotency_key)
                   for _ in range(width)]
-        if entire:
-            group = secrets.token_hex(4)
+        if group:
             for b in bodies:
                 b["metadata"]["annotations"][ANN_GROUP] = group
         created = await self._create(bodies)
@@ -331,17 +328,47 @@ class PlaceholderManager:
         except BaseException:
             await self.release(created, wait=False)
             raise
-        admitted = [p for p in created if p not in failed]
+        if failed:
+            await self.release(failed, wait=False)
+        return [p for p in created if p not in failed]
+
+    async def reserve_trim(self, owner: dict, total: int, entire: bool, width: int,
+                           pick: Callable[[List[str]], Sequence[str]], attach_id: str = "",
+                           container: str = "", idempotency_key: str = ""
+                           ) -> Tuple[Reservation, List[Placeholder]]:
+        """Topology-pinned reservation (SURVEY §7.4.3). Which GPU the device plugin hands a
+        placeholder is opaque to us, so hold ``width`` (= every free GPU) 1-GPU placeholders at
+        once and keep the ``total`` whose device IDs ``pick`` returns. Returns the reservation and
+        the surplus placeholders, which the caller releases (or returns to the warm pool).
+        Entire mounts are the kept placeholders tied by one ``ANN_GROUP`` id, the same shape
+        as a warm-pool entire claim."""
+        if total <= 0 or width < total:
+            raise ValueError(f"bad trim reservation {total}/{width}")
+        admitted = await self.hold_singles(owner, width, entire,
+                                           secrets.token_hex(4) if entire else "", attach_id,
+                                           container, idempotency_key)
         if len(admitted) < total:
-            await self.release(created, wait=False)
+            await self.release(admitted, wait=False)
             raise InsufficientGPU(f"only {len(admitted)} of {total} GPUs admitted")
+        return self.keep_picked(admitted, total, pick)
+
+    @staticmethod
+    def keep_picked(held: Sequence[Placeholder], total: int,
+                    pick: Callable[[List[str]], Sequence[str]]
+                    ) -> Tuple[Reservation, List[Placeholder]]:
+        """Of admitted placeholders, keep those whose devices ``pick`` chooses (``total`` GPUs;
+        a multi-GPU placeholder only as a whole); the rest is surplus."""
         with trace.span("placement_trim"):
-            want = {d for d in pick([p.device_ids[0] for p in admitted])}
-            keep = [p for p in admitted if p.device_ids[0] in want][:total]
-            if len(keep) < total:  # pick returned ids we do not hold: fall back to any
-                keep += [p for p in admitted if p not in keep][:total - len(keep)]
-        surplus = [p for p in created if p not in keep]
-        return Reservation(keep), surplus
+            want = set(pick([d for p in held for d in p.device_ids]))
+            keep = [p for p in held if p.device_ids and set(p.device_ids) <= want]
+            got = sum(len(p.device_ids) for p in keep)
+            for p in held:       # pick returned ids we do not hold: fill up with any
+                if got >= total:
+                    break
+                if p not in keep and got + len(p.device_ids) <= total:
+                    keep.append(p)
+                    got += len(p.device_ids)
+        return Reservation(keep), [p for p in held if p not in keep]
 
     async def _create_claims(self, bodies: List[dict]) -> None:
         """DRA mode: the placeholders' ResourceClaims, before the Pods (a Pod whose claim does

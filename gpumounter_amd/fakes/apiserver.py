@@ -344,15 +344,13 @@ class FakeCluster:
             want = int(podu.parse_quantity(
                 ((c.get("resources") or {}).get("limits") or {}).get(node.resource, 0)))
             if want:
-                pref = (pod["metadata"].get("annotations") or {}).get(
-                    "gpumounter.amd.com/preferred-devices", "")
+                # the kubelet hands a device plugin the pod's UID and container name, never its
+                # annotations: gpumounter's preferred-devices hint does not reach it
                 if node.plugin is not None:      # kubelet device manager → device plugin
                     ids = await node.plugin.plugin_allocate(ns, name, c["name"], want,
                                                             uid=pod["metadata"]["uid"])
                 else:
-                    ids = node.allocate(ns, name, c["name"], want,
-                                        [p for p in pref.split(",") if p],
-                                        uid=pod["metadata"]["uid"])
+                    ids = node.allocate(ns, name, c["name"], want, uid=pod["metadata"]["uid"])
                 if ids is None:
                     node.release_pod(ns, name)
                     pod["status"]["phase"] = "Failed"

@@ -45,7 +45,7 @@ class LocalCluster:
                  cgroup_driver: str = "cgroupfs", runtime: str = "containerd",
                  latency: Optional[LatencyModel] = None, gc_mode: str = "modern",
                  workdir: str = "", placeholder_namespace_mode: str = "pool",
-                 alloc_policy: str = "topology", device_id_kind: str = "bdf",
+                 alloc_policy: str = "first-free", device_id_kind: str = "bdf",
                  devnode_mode: str = "emulate", reconcile_period_s: float = 0.0,
                  start_master: bool = True, worker_overrides: Optional[dict] = None,
                  node_gpu_bdfs: Optional[List[str]] = None,

@@ -60,7 +60,7 @@ class FakeNode:
                  links: Optional[LinkMatrix] = None, resource: str = "amd.com/gpu",
                  cgroup_mode: str = "v1", cgroup_driver: str = "cgroupfs",
                  runtime: str = "containerd", device_id_kind: str = "bdf",
-                 alloc_policy: str = "topology", labels: Optional[Dict[str, str]] = None,
+                 alloc_policy: str = "first-free", labels: Optional[Dict[str, str]] = None,
                  cgroup_root: str = "") -> None:
         self.name = name
         self.resource = resource
@@ -69,6 +69,8 @@ class FakeNode:
         self.cgroup_mode = cgroup_mode
         self.cgroup_driver = cgroup_driver
         self.runtime = runtime
+        if alloc_policy not in ("first-free", "topology"):
+            raise ValueError(f"alloc_policy {alloc_policy!r}: first-free | topology")
         self.alloc_policy = alloc_policy
         self.device_id_kind = device_id_kind
         self.labels = {"kubernetes.io/hostname": name, "gpu-mounter-enable": "enable"}
@@ -178,20 +180,27 @@ class FakeNode:
             {self.resource: self.device_ids()}))
 
     def allocate(self, ns: str, pod: str, container: str, n: int,
-                 preferred: Sequence[str] = (), uid: str = "") -> Optional[List[str]]:
-        """kubelet device-manager Allocate; returns device IDs or None (insufficient)."""
+                 uid: str = "") -> Optional[List[str]]:
+        """kubelet device-manager Allocate; returns device IDs or None (insufficient).
+
+        Which devices a pod gets is the device plugin's business, and no plugin shipped for
+        ``amd.com/gpu`` reads gpumounter's ``preferred-devices`` annotation (the kubelet never
+        passes pod annotations to a plugin), so this fake does not read it either:
+
+        * ``first-free`` (default): the kubelet's choice without GetPreferredAllocation —
+          free devices in device order;
+        * ``topology``: a plugin with its own GetPreferredAllocation (the ROCm plugin's
+          best-effort policy): the best-connected free set, with no idea which GPUs the pod
+          that will receive them already holds.
+
+        Only gpumounter's own device plugin (``deviceplugin/plugin.py``, registered through
+        the FakeKubelet's device manager) steers placeholders to a chosen set."""
         with self._lock:
             free = [g for g in self.gpus if self.device_id(g) not in self.allocated]
             if len(free) < n:
                 return None
             chosen: List[AmdGpu]
-            pref = [normalize_device_id(p) for p in preferred]
-            by_id = {normalize_device_id(self.device_id(g)): g for g in free}
-            if self.alloc_policy != "blind" and pref and all(p in by_id for p in pref) \
-                    and len(pref) == n:
-                chosen = [by_id[p] for p in pref]
-            elif self.alloc_policy == "topology":
-                # GetPreferredAllocation: co-locate with what the same owner already holds
+            if self.alloc_policy == "topology":
                 plc = topology.choose(free, n, self.links, policy="xgmi")
                 chosen = [next(g for g in free if g.index == i) for i in plc.chosen]
             else:

@@ -112,10 +112,14 @@ class Config:
     device_file_mode: int = 0o666      # reference: nvidia.go:39 "666"
     # --- policy ----------------------------------------------------------------------------
     topology_policy: str = "xgmi"      # xgmi | first-fit
-    # hint: preferred set is only an annotation (the device plugin decides);
-    # trim: hold every free GPU with 1-GPU placeholders, keep the topology-chosen ones, release
-    # the rest — exact placement whatever the device plugin does
-    placement_enforce: str = "hint"
+    # auto: exact where the cluster offers a way (gpumounter's own device plugin, a DRA CEL
+    #   selector); otherwise take what the device plugin admits and, if it is worse-placed than
+    #   the topology choice, hold the other free GPUs and keep the best (one extra round only
+    #   when the plugin chose badly);
+    # trim: always hold every free GPU with 1-GPU placeholders, keep the topology-chosen ones
+    #   (SURVEY §7.4.3);
+    # hint: the preferred set is only an annotation (no shipped device plugin reads it)
+    placement_enforce: str = "auto"
     ledger_get: bool = True            # read admitted placeholders with PodResources v1 Get
     reconcile_on_events: bool = True
     # auto: fd scan of the container's PIDs, amdsmi only for PIDs whose fd table is unreadable;
@@ -239,7 +243,7 @@ class Config:
         _choice("devnode_mode", self.devnode_mode, ("procroot", "setns", "emulate"))
         _choice("devnode_userns", self.devnode_userns, ("auto", "bind", "off"))
         _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
-        _choice("placement_enforce", self.placement_enforce, ("hint", "trim"))
+        _choice("placement_enforce", self.placement_enforce, ("auto", "hint", "trim"))
         _choice("busy_detection", self.busy_detection, ("auto", "both"))
         _choice("authz_mode", self.authz_mode, ("none", "kube"))
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))

@@ -32,6 +32,9 @@ class Metrics:
         self.placement_mismatch = Counter("gm_placement_mismatch_total",
                                           "device plugin chose a set other than the preferred one",
                                           registry=r)
+        self.placement_corrections = Counter(
+            "gm_placement_corrections_total",
+            "attaches whose plugin-chosen GPUs were swapped for a better-placed set", registry=r)
         self.verify_failures = Counter("gm_attach_verify_failures_total",
                                        "attaches rolled back because the read-back "
                                        "(attach_verify) found rules or nodes missing",

@@ -81,6 +81,47 @@ def can_mount(mount_type: MountType, entire: bool) -> Tuple[bool, str]:
     return True, ""
 
 
+class _SharedExclusive:
+    """Reservations on one node: ordinary ones run concurrently (shared); the ones that hold
+    every free GPU for a moment (trim, placement correction) and device-plugin intents, which
+    carry no pod identity, run alone (exclusive)."""
+
+    def __init__(self) -> None:
+        self._cond = asyncio.Condition()
+        self._shared = 0
+        self._exclusive = False
+        self._waiting_exclusive = 0
+
+    @contextlib.asynccontextmanager
+    async def shared(self):
+        async with self._cond:
+            await self._cond.wait_for(lambda: not self._exclusive and
+                                      not self._waiting_exclusive)
+            self._shared += 1
+        try:
+            yield
+        finally:
+            async with self._cond:
+                self._shared -= 1
+                self._cond.notify_all()
+
+    @contextlib.asynccontextmanager
+    async def exclusive(self):
+        async with self._cond:
+            self._waiting_exclusive += 1
+            try:
+                await self._cond.wait_for(lambda: not self._exclusive and not self._shared)
+            finally:
+                self._waiting_exclusive -= 1
+            self._exclusive = True
+        try:
+            yield
+        finally:
+            async with self._cond:
+                self._exclusive = False
+                self._cond.notify_all()
+
+
 class GpuMountService:
     def __init__(self, cfg, kube: KubeClient, inv: Inventory, ledger: LedgerClient,
                  placeholders: PlaceholderManager, hotmount: HotMount, node_pods: PodInformer,
@@ -106,7 +147,7 @@ class GpuMountService:
         # * trim briefly holds every free GPU — a concurrent one would see a full node;
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
         #   two attaches' 1-GPU intents would be indistinguishable to the plugin.
-        self._node_reserve_lock = asyncio.Lock()
+        self._reserve_gate = _SharedExclusive()
         self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}
         self._own: Dict[str, Tuple[str, ...]] = {}   # pod uid → its own device-plugin GPU IDs
         self.ledger_reads = 0
@@ -493,12 +534,26 @@ class GpuMountService:
 
     async def _reserve(self, pod: dict, n: int, req, st: PodGpuState, preferred: List[str],
                        n_free: int = 0):
-        """Claim from the warm pool first (if enabled), create placeholders for the rest
-        (``placement_enforce=trim``: hold every free GPU, keep the topology-chosen ones)."""
+        """Claim from the warm pool first (if enabled), create placeholders for the rest.
+
+        Placement (``placement_enforce``): the device plugin decides which GPUs a placeholder
+        gets, and a stock plugin never sees gpumounter's preferred set. ``auto`` (default)
+        checks what was admitted against the best set and, when it is worse, corrects it by
+        holding the node's other free GPUs and keeping the best ones (:meth:`_correct`); an
+        exact path is used instead when one exists — gpumounter's own device plugin (intents
+        answered by GetPreferredAllocation) or a DRA claim pinned by a CEL selector. ``trim``
+        always holds every free GPU; ``hint`` only annotates the preferred set."""
         dra = self.cfg.gpu_allocation == "dra"     # the claim's selector pins the devices
-        if (self.cfg.placement_enforce != "trim" or dra) and self.plugin is None:
-            return await self._reserve_unlocked(pod, n, req, st, preferred, n_free)
-        async with self._node_reserve_lock:
+        mode = self.cfg.placement_enforce
+        if (mode != "trim" or dra) and self.plugin is None:
+            async with self._reserve_gate.shared():
+                res = await self._reserve_unlocked(pod, n, req, st, preferred, n_free)
+            if mode == "auto" and not dra and res.corrigible and \
+                    self._placement_worse(st, res.device_ids, preferred):
+                async with self._reserve_gate.exclusive():
+                    res = await self._correct(pod, n, req, st, res)
+            return res
+        async with self._reserve_gate.exclusive():
             # recompute against the ledger as it is now that we hold the node
             free = self._free(st)
             preferred = self._preferred(n, st, free)
@@ -506,6 +561,88 @@ class GpuMountService:
             if not res.preferred:
                 res.preferred = list(preferred)
             return res
+
+    def _placement_worse(self, st: PodGpuState, got: Sequence[str],
+                         want: Sequence[str]) -> bool:
+        """The admitted set scores worse (hive split ≫ non-xGMI pair ≫ NUMA split) with the
+        pod's GPUs than the preferred set would have."""
+        if not want or len(want) != len(got):
+            return False
+        keys = self.inv.by_key()
+        try:
+            g = [keys[normalize_device_id(d)].index for d in got]
+            w = [keys[normalize_device_id(d)].index for d in want]
+        except KeyError:
+            return False
+        if sorted(g) == sorted(w):
+            return False
+        table = {x.index: x for x in self.inv.gpus()}
+        att = [x.index for x in st.hot + st.own]
+        links = self.inv.links()
+        return topology.score_set(table, links, att + g)[0] > \
+            topology.score_set(table, links, att + w)[0] + 1e-6
+
+    async def _correct(self, pod: dict, n: int, req, st: PodGpuState, res):
+        """The plugin's choice is worse than the preferred set: hold every other free GPU with
+        1-GPU placeholders next to the admitted ones, keep the best ``n`` and release the rest.
+        An entire mount's admitted placeholder can only be kept whole; when the best set needs
+        some of its GPUs and some new ones, it is released and its GPUs taken back as 1-GPU
+        placeholders (every other free GPU is held, so the plugin can only hand out those).
+        Any failure keeps the admitted (valid, worse-placed) reservation."""
+        keys = self.inv.by_key()
+        mine = {normalize_device_id(d) for d in res.device_ids}
+        free = [g for g in self._free(st) if not mine.intersection(g.ledger_keys())]
+        if not free:
+            return res
+        attached = st.hot + st.own
+        links = self.inv.links()
+        group = secrets.token_hex(4) if req.is_entire_mount else ""
+        rid = log.request_id.get()
+
+        def best_of(ids: List[str]):
+            by = {keys[normalize_device_id(d)].index: d for d in ids
+                  if normalize_device_id(d) in keys}
+            plc = topology.choose([keys[normalize_device_id(d)] for d in by.values()], n,
+                                  links, attached=attached, policy=self.cfg.topology_policy)
+            return [by[i] for i in plc.chosen] if plc else list(res.device_ids)
+        held = list(res.placeholders)
+        extra: List[Placeholder] = []
+        try:
+            with trace.span("placement_correct", held=len(free)):
+                extra = await self.ph.hold_singles(pod, len(free), req.is_entire_mount, group,
+                                                   rid, req.container, req.idempotency_key)
+                ids = [d for p in held + extra for d in p.device_ids]
+                want = {normalize_device_id(d) for d in best_of(ids)}
+                mixed = req.is_entire_mount and want & mine and not mine <= want
+                if mixed:
+                    # the admitted n-GPU placeholder only partly belongs to the best set
+                    await self.ph.release(held, wait=False)
+                    held = []
+                    extra += await self.ph.hold_singles(pod, len(mine), True, group, rid,
+                                                        req.container, req.idempotency_key)
+                new, surplus = self.ph.keep_picked(held + extra, n, best_of)
+        except (ReserveError, InsufficientGPU, asyncio.TimeoutError, InjectedFault) as e:
+            await self._release_quiet(extra)
+            if held:
+                _log.warning("placement correction failed, keeping the plugin's choice: %s", e)
+                return res
+            raise
+        if sum(len(p.device_ids) for p in new.placeholders) != n:
+            await self._release_quiet(held + extra)
+            raise InsufficientGPU(f"placement correction could not hold {n} GPUs")
+        self.metrics.placement_corrections.inc()
+        new.preferred = new.device_ids
+        if surplus:
+            with trace.span("placement_release", placeholders=len(surplus)):
+                await self._release_quiet(surplus)
+        return new
+
+    async def _release_quiet(self, phs) -> None:
+        try:
+            await self._release([p for p in phs if p.device_ids]
+                                + [p for p in phs if not p.device_ids])
+        except Exception as e:  # noqa: BLE001 - the reconciler collects leftovers
+            _log.error("releasing placeholders: %s", e)
 
     async def _reserve_unlocked(self, pod: dict, n: int, req, st: PodGpuState,
                                 preferred: List[str], n_free: int):
@@ -553,6 +690,8 @@ class GpuMountService:
             rest.preferred = claimed.device_ids + list(preferred) if preferred else []
         else:
             rest.preferred = list(preferred)
+            # a plain reservation of the plugin's choosing, with other free GPUs to choose from
+            rest.corrigible = not token and len(preferred) == n and n_free > n
         return rest
 
     async def _release(self, phs) -> None:

@@ -122,8 +122,9 @@ def test_bench_real_node_ops_reports_stage_split():
     if realnode.available() or os.environ.get("GM_PRIVILEGED_TESTS") != "1":
         pytest.skip("needs root and GM_PRIVILEGED_TESTS=1 (mounts cgroup2/bpffs)")
     env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
+    # default --ref-steps: the reference column is skipped with its reason, never a crash
     res = subprocess.run([sys.executable, "bench.py", "--steps", "10", "--warmup", "2",
-                          "--amdsmi", "mock", "--node-ops", "real", "--ref-steps", "0"],
+                          "--amdsmi", "mock", "--node-ops", "real"],
                          cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert res.returncode == 0, res.stderr[-3000:]
     d = _last_json(res.stdout)
@@ -131,6 +132,7 @@ def test_bench_real_node_ops_reports_stage_split():
     st = d["real_node_ops_stage_p50_ms"]
     assert {"bpf_load_verify", "bpf_attach", "devnodes", "cgroup_rule"} <= set(st)
     assert d["ledger_audit_issues"] == 0 and d["final_orphans"] == 0
+    assert "cgroup-v1" in d["reference_emulated_same_run"]["skipped"]
 
 
 def test_rank_pool_two_ranks_on_cpu():

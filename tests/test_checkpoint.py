@@ -129,10 +129,10 @@ def test_ledger_reporting_more_devices_than_requested_fails_the_attach():
 
     orig = FakeNode.allocate
 
-    def over_allocate(self, ns, pod, container, n, preferred=(), uid=""):
-        ids = orig(self, ns, pod, container, n, preferred, uid)
+    def over_allocate(self, ns, pod, container, n, uid=""):
+        ids = orig(self, ns, pod, container, n, uid)
         if ids and "-slave-pod-" in pod:
-            extra = orig(self, ns, pod, container, 1, (), uid)   # a second Allocate
+            extra = orig(self, ns, pod, container, 1, uid)   # a second Allocate
             ids = ids + (extra or [])
         return ids
 

@@ -281,16 +281,40 @@ def _numa_of(lc, devices):
     return {d["numa_node"] for d in devices}
 
 
-def test_placement_blind_plugin_hint_mode_crosses_numa_and_is_counted():
+def test_placement_hint_mode_with_stock_plugin_crosses_numa_and_is_counted():
+    """hint only annotates: the stock plugin (first free in device order) never reads it."""
     async def body(lc):
         lc.tenant("other")
         lc.tenant("t")
-        assert (await lc.add("default", "other", 3))[0] == 200      # blind plugin: GPUs 0,1,2
+        assert (await lc.add("default", "other", 3))[0] == 200      # first-free: GPUs 0,1,2
         code, b = await lc.add("default", "t", 2)
         assert code == 200
         assert _numa_of(lc, b["devices"]) == {0, 1}                   # 3 and 4: across sockets
         assert lc.nodes["node-0"].worker.metrics.placement_mismatch._value.get() >= 1
-    run(body, alloc_policy="blind")
+    run(body, alloc_policy="first-free", worker_overrides={"placement_enforce": "hint"})
+
+
+@pytest.mark.parametrize("entire", [False, True])
+def test_default_placement_corrects_the_stock_plugins_choice(entire):
+    """Default (auto) with a plugin that ignores the hint: the admitted set 3,4 crosses the
+    socket, so the worker holds the other free GPUs, keeps two on NUMA 1 and releases the
+    rest. The books end with exactly 3 + 2 GPUs."""
+    async def body(lc):
+        lc.tenant("other")
+        lc.tenant("t")
+        assert (await lc.add("default", "other", 3))[0] == 200
+        code, b = await lc.add("default", "t", 2, entire=entire)
+        assert code == 200, b
+        assert _numa_of(lc, b["devices"]) == {1} and len(b["devices"]) == 2
+        m = lc.nodes["node-0"].worker.metrics
+        assert m.placement_corrections._value.get() == 1
+        assert len(node_of(lc).allocated) == 5 and not await lc.audit("default", "t")
+        code, _ = await lc.remove("default", "t", [d["uuid"] for d in b["devices"]])
+        assert code == 200 and len(node_of(lc).allocated) == 3
+        # on an empty socket the plugin's own choice is already best: no correction round
+        code, b2 = await lc.add("default", "t", 1)
+        assert code == 200 and m.placement_corrections._value.get() == 1
+    run(body, alloc_policy="first-free")
 
 
 @pytest.mark.parametrize("entire", [False, True])
@@ -316,7 +340,7 @@ def test_placement_trim_enforces_topology_choice_with_blind_plugin(entire):
         else:        # grow by one: stays on the same socket
             code, b2 = await lc.add("default", "t", 1)
             assert code == 200 and _numa_of(lc, b2["devices"]) == {1}
-    run(body, alloc_policy="blind", worker_overrides={"placement_enforce": "trim"})
+    run(body, alloc_policy="first-free", worker_overrides={"placement_enforce": "trim"})
 
 
 # ------------------------------------------------------------------------------ namespaces/GC
@@ -840,3 +864,31 @@ def test_attach_verify_reads_back_rules_and_nodes_and_rolls_back_on_mismatch():
                 if not p["metadata"].get("deletionTimestamp")]
         assert len(live) == 1
     run(body, worker_overrides={"attach_verify": True})
+
+
+def test_shipped_default_places_optimally_on_a_fragmented_node_with_a_hint_blind_plugin():
+    """with a device plugin that never reads the hint, the shipped
+    default still yields one hive and NUMA-packed sets for N ≤ 4 whenever the free GPUs allow
+    it (bench/configs.py placement; hint mode, for contrast, does not)."""
+    import importlib.util
+    import types
+
+    spec = importlib.util.spec_from_file_location(
+        "gm_configs", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench",
+                                   "configs.py"))
+    configs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(configs)
+    args = types.SimpleNamespace(seed=3, rounds=25, sandbox=None)
+
+    def scenario(mode):
+        async def body(lc):
+            return await configs.placement(lc, args)
+        return run(body, alloc_policy="first-free",
+                   worker_overrides={"placement_enforce": mode})
+    auto = scenario("auto")
+    for n, s in auto["per_n"].items():
+        assert s["attaches"] > 0 and s["optimal"] == s["attaches"], (n, s)
+        assert s["one_hive"] == s["attaches"] and s["numa_packed"] == s["numa_possible"], (n, s)
+    assert auto["placement_corrections"] > 0 and auto["audit_issues"] == 0
+    hint = scenario("hint")
+    assert sum(s["optimal"] < s["attaches"] for s in hint["per_n"].values()) > 0, hint
