@@ -63,6 +63,11 @@ class _LocalCP:
     def kubelet_calls(self) -> dict:
         return dict(self.lc.nodes["node-0"].kubelet.calls)
 
+    def tenant_view(self):
+        node = self.lc.nodes["node-0"].node
+        (c,) = [c for c in node.containers.values() if c.pod_name == "tenant"]
+        return c.root_dir, c.cgroup_dir
+
     def wait_pool(self, want: int) -> None:
         pool = self.lc.nodes["node-0"].worker.pool
         t_wait = time.time()
@@ -95,6 +100,13 @@ class _ProcCP:
 
     def kubelet_calls(self) -> dict:
         return self.pc.kubelet_calls()
+
+    def tenant_view(self):
+        from gpumounter_amd.ops import tenant
+        cs = self.pc.tenant_pod["status"]["containerStatuses"]
+        cid = cs[0]["containerID"].split("://", 1)[1]
+        n = self.pc.info["nodes"]["node-0"]
+        return tenant.locate(n["rootfs_root"], n["cgroup_root"], cid)
 
     def wait_pool(self, want: int) -> None:
         from gpumounter_amd.models.types import ANN_MOUNT_MODE, MODE_STANDBY
@@ -251,7 +263,7 @@ def main() -> int:
                                 gpu_api=args.gpu_api, log_dir=args.log_dir,
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
                                             "GM_PLACEMENT_ENFORCE": args.placement}).start()
-            pc.tenant("tenant", pids={"main": [tenant_pid]})
+            pc.tenant_pod = pc.tenant("tenant", pids={"main": [tenant_pid]})
             cp = _ProcCP(pc)
         else:
             lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
@@ -419,6 +431,28 @@ def main() -> int:
                        "all_peer_access": all(x["peer_access"] for x in pairs),
                        "min_gbps": round(min(x["gbps"] for x in pairs), 1),
                        "max_gbps": round(max(x["gbps"] for x in pairs), 1)}
+            tenant_view = None
+            if has_gpu and not args.no_verify and args.node_ops == "emulated" and \
+                    args.protocol == "gpumounter" and args.cgroup == "v2":
+                # BASELINE config "the Pod sees it", from a fresh tenant-side HIP process
+                from gpumounter_amd.ops import tenant
+                root, cg = cp.tenant_view()
+                held = {}
+
+                def _attach():
+                    code, body = cp.add(n, args.mode == "entire")
+                    if code != 200:
+                        raise RuntimeError(f"attach failed: {code} {body}")
+                    held["uuids"] = [d["uuid"] for d in body["devices"]]
+                    return [d["bdf"] for d in body["devices"]]
+
+                def _detach():
+                    code, body = cp.remove(held["uuids"])
+                    if code != 200:
+                        raise RuntimeError(f"detach failed: {code} {body}")
+                tenant_view = tenant.check_attach_cycle(_attach, _detach, root, cg)
+                if not tenant_view["ok"]:
+                    raise RuntimeError(f"tenant-side view wrong: {tenant_view}")
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
             placeholders_left = cp.placeholders_left()
             kcalls = cp.kubelet_calls()
@@ -524,6 +558,7 @@ def main() -> int:
                 "allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4) if ar_ms else None,
                 "rccl_allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4)
                 if ar_ms and ar_backend[0] == "nccl" else None,
+                "tenant_view": tenant_view,
                 "attached_hives": att_hives, "attached_numa_nodes": att_numa,
                 "non_xgmi_pairs": att_nx, "p2p": p2p,
                 "ledger_audit_issues": audit_issues,

@@ -357,3 +357,34 @@ def test_tenant_validate_tool_runs_kernel_p2p_and_rccl():
     assert rep["allreduce"]["world"] == len(rep["gpus"]) and rep["allreduce"]["ok"]
     assert len(rep["burn_in"]) == len(rep["gpus"]) and all(b["ok"] for b in rep["burn_in"])
     print(json.dumps(rep["allreduce"]))
+
+
+def test_tenant_side_hip_sees_the_gpu_only_while_attached(real_inventory):
+    """BASELINE config "attach 1 MI355X to a running Pod; the Pod sees it", from the tenant's
+    side: a fresh HIP process in the tenant's view of /dev and of its device cgroup (the
+    emulated node operations, resolved by libgm_tenant_view.so — the box allows no namespaces)
+    enumerates no GPU before the attach, exactly the attached one after it, none after the
+    detach; and it runs the gfx950 liveness kernel on it."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+    from gpumounter_amd.ops import probe, tenant
+
+    bdf0 = probe.props(0)["pci_bus_id"].lower()
+
+    async def run():
+        async with LocalCluster(amdsmi_lib="", cgroup_mode="v2", node_gpu_bdfs=[bdf0]) as lc:
+            lc.tenant("t")
+            cid = lc.container_ids("default", "t")[0]
+            ctr = lc.nodes["node-0"].node.container(cid)
+            view = (ctr.root_dir, ctr.cgroup_dir)
+            before = await asyncio.to_thread(tenant.hip_devices, *view)
+            assert before["count"] == 0, before
+            code, body = await lc.add("default", "t", 1)
+            assert code == 200, body
+            during = await asyncio.to_thread(tenant.hip_devices, *view)
+            assert during["count"] == 1 and during["bdfs"] == [bdf0], during
+            code, _ = await lc.remove("default", "t", [body["devices"][0]["uuid"]])
+            assert code == 200
+            after = await asyncio.to_thread(tenant.hip_devices, *view)
+            assert after["count"] == 0, after
+            print("tenant view:", before, during, after)
+    asyncio.run(run())

@@ -329,3 +329,31 @@ def test_devnodes_bind_mode_policy(tmp_path):
     with pytest.raises(DevNodeError, match="staging"):
         DevNodeWriter("procroot", userns="bind", proc_root=str(proc)).create(
             Target(pid=200), NODES[:1])
+
+
+def test_tenant_view_library_resolves_through_emulated_state(tmp_path):
+    """libgm_tenant_view.so: a GPU path is ENOENT without a node in the tenant rootfs, EPERM
+    without a grant in the recorded allow set, and otherwise reaches the host node with that
+    major:minor (ENXIO here: no GPU in this container); other paths are untouched."""
+    import errno
+    import json
+
+    from gpumounter_amd.ops import tenant
+
+    root, cg = tmp_path / "root", tmp_path / "cg"
+    (root / "dev" / "dri").mkdir(parents=True)
+    cg.mkdir()
+    paths = ["/dev/kfd", "/dev/dri/renderD128", "/dev/null"]
+    got = tenant.can_open(str(root), paths, str(cg))
+    assert got == {"/dev/kfd": errno.ENOENT, "/dev/dri/renderD128": errno.ENOENT,
+                   "/dev/null": 0}
+    (root / "dev" / "kfd").write_text("gm-chr 511:0\n")
+    (root / "dev" / "dri" / "renderD128").write_text("gm-chr 226:128\n")
+    got = tenant.can_open(str(root), paths[:2], str(cg))
+    assert set(got.values()) == {errno.EPERM}
+    (cg / "gm.bpf.json").write_text(json.dumps({"set": [[2, 511, 0, 6], [2, 226, 128, 2]]}))
+    got = tenant.can_open(str(root), paths[:2], str(cg))
+    assert got["/dev/dri/renderD128"] == errno.EPERM          # read-only grant: not rw
+    assert got["/dev/kfd"] in (0, errno.ENXIO)                 # granted: the host's node
+    env = tenant.tenant_env(str(root), str(cg))
+    assert env["LD_PRELOAD"].endswith("libgm_tenant_view.so")
