@@ -11,7 +11,7 @@ TAG=${1:-configs}
 O=gpurun_out/$TAG
 mkdir -p "$O"
 fail() { tail -40 "$1"; exit 1; }
-for s in scale contention soak; do
+for s in scale contention soak placement; do
     timeout -k 10 240 python bench/configs.py "$s" > "$O/${s}_mock.json" 2> "$O/${s}_mock.err" \
         || fail "$O/${s}_mock.err"
     tail -c 400 "$O/${s}_mock.json"; echo

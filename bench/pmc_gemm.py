@@ -1,4 +1,4 @@
-"""Short fixed workload for rocprofv3 PMC passes over the 256²-tile GEMM (profiles/r1_pmc_gemm):
+"""Short fixed workload for rocprofv3 PMC passes over the 256²-tile GEMM (profiles/history/r1_pmc_gemm):
 3 dispatches each of the schedules in GM_PMC_VARIANTS (default V1,V5) at 8192³, and with
 GM_PMC_TORCH=1 three of hipBLASLt's NT kernel on uniform [-1, 1) bf16 operands.
 

@@ -1,4 +1,4 @@
-"""Probe kernels as a short fixed workload for rocprofv3 PMC passes (profiles/r1_pmc_probe).
+"""Probe kernels as a short fixed workload for rocprofv3 PMC passes (profiles/history/r1_pmc_probe).
 
     rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d DIR -- python3 bench/pmc_probe.py
 

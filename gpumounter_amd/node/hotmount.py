@@ -232,7 +232,6 @@ class HotMount:
             with trace.span("cgroup_rule", backend=self.backend.name, rules=len(revoke)):
                 self.faults.check("unmount")
                 self.backend.apply(t.cgdir, [], revoke, after)
-            self.journal.forget(t.ref.id, keys)
             self.faults.check("unmount", "after")
             # only nodes gpumounter created: one the container already had stays (its rule is
             # revoked all the same, so it is as dead as it was before the attach)
@@ -240,7 +239,10 @@ class HotMount:
             unlink = [n for n in revoke if (n.major, n.minor) in ours]
             with trace.span("devnodes", nodes=len(unlink)):
                 self.writer.remove(t.target, unlink)
-            self.journal.forget(t.ref.id, (), keys)
+            # one journal update for both steps: a worker that dies in between leaves revoked
+            # rules journaled, which the audit forgets on sight (not in the kernel any more),
+            # and its nodes, which the orphan sweep unlinks
+            self.journal.forget(t.ref.id, keys, keys)
         return targets
 
     def adopt(self, pod: dict, hot: Sequence[AmdGpu], base: Sequence[AmdGpu] = ()) -> int:

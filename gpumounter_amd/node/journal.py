@@ -114,8 +114,11 @@ class InjectionJournal:
                 pass
             return
         tmp = path + ".tmp"
+        # dumps (the C encoder) + one write: json.dump streams through the pure-Python
+        # encoder, which cost more than the rest of a journal update on the attach path
+        blob = json.dumps(e.to_json(), separators=(",", ":"))
         with open(tmp, "w", encoding="utf-8") as fh:
-            json.dump(e.to_json(), fh, separators=(",", ":"))
+            fh.write(blob)
         os.replace(tmp, path)
 
     # ------------------------------------------------------------------------ queries

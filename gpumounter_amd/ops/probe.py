@@ -116,7 +116,7 @@ def gemm_nt(a, bt, out=None, stream=None, variant: Optional[int] = None):
     (0: per-k-step fragment reads, 1: whole K-tile of reads up front, 2: quadrant phases,
     3: V1 on 32x32x16, 4: 4 waves × 128², 5: local-read prefetch across the barrier, 6: V4 on
     V5's schedule with buffer_load-to-LDS staging, 7: V5 with buffer_load-to-LDS staging, 8: V5 with a DPP-transposed 8-byte-store epilogue, 9: V2 with register prefetch across phases;
-    default: the fastest measured, 5 — profiles/r1_gemm)."""
+    default: the fastest measured, 5 — profiles/history/r1_gemm)."""
     import torch
 
     if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:

@@ -1,6 +1,6 @@
 // gm_gemm.hip — the 256²-tile bf16 burn-in GEMM (schedule V5, with V1 as its reference point)
 // and the bit-exact burn-in loop. Part of libgm_probe.so (built with gm_probe.hip).
-// Measurements: profiles/r1_gemm/ (round 1 also timed eight other schedules, V0 V2-V4 V6-V9;
+// Measurements: profiles/history/r1_gemm/ (round 1 also timed eight other schedules, V0 V2-V4 V6-V9;
 // none beat V5, and they were removed: the GEMM is a burn-in load, not a product kernel).
 #include <chrono>
 
@@ -29,7 +29,7 @@ constexpr int kLdsBytes = 2 * kStageBytes;    // two stages: 128 KiB of the 160 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void gbl_void;
 }  // namespace g256
-constexpr int kGemmNtDefault = 5;  // profiles/r1_gemm: V5 +2.9 % over V1 at 4096³, +0.9 % at 8192³
+constexpr int kGemmNtDefault = 5;  // profiles/history/r1_gemm: V5 +2.9 % over V1 at 4096³, +0.9 % at 8192³
 
 // XCD-aware block → output tile: bijective for any grid size (the dispatcher deals block ids
 // round-robin over the 8 XCDs, so ids ≡ x mod 8 share XCD x's L2 and get a contiguous range of

@@ -513,13 +513,13 @@ int gm_probe_mfma_peak_variant(int dev, int variant, int iters, int blocks_per_c
   return (int)e;
 }
 
-// Default HBM stream = the measured-best variant on MI355X (profiles/r1_probe_sweep: chunked,
+// Default HBM stream = the measured-best variant on MI355X (profiles/history/r1_probe_sweep: chunked,
 // nontemporal, 8 blocks/CU → 5.57-5.65 TB/s vs 5.0-5.5 TB/s grid-stride).
 int gm_probe_hbm_copy(int dev, uint64_t bytes, int iters, double* gbps) {
   return gm_probe_hbm_copy_variant(dev, 2, bytes, iters, 8, gbps);
 }
 
-// Default MFMA peak = the measured-best form on MI355X (profiles/r1_gpu_b/probe_sweep.json):
+// Default MFMA peak = the measured-best form on MI355X (profiles/history/r1_gpu_b/probe_sweep.json):
 // v_mfma_f32_16x16x32_bf16, 8 dst-tied chains per wave, 8 blocks/CU → 2.45 PF/s
 // (≈98 % of the 2.5 PF/s dense bf16 peak) vs 2.0-2.16 PF/s for 32x32x16 × 4 chains.
 int gm_probe_mfma_peak(int dev, int iters, double* tflops) {
