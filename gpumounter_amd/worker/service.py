@@ -585,10 +585,14 @@ class GpuMountService:
     async def _correct(self, pod: dict, n: int, req, st: PodGpuState, res):
         """The plugin's choice is worse than the preferred set: hold every other free GPU with
         1-GPU placeholders next to the admitted ones, keep the best ``n`` and release the rest.
-        An entire mount's admitted placeholder can only be kept whole; when the best set needs
-        some of its GPUs and some new ones, it is released and its GPUs taken back as 1-GPU
-        placeholders (every other free GPU is held, so the plugin can only hand out those).
-        Any failure keeps the admitted (valid, worse-placed) reservation."""
+
+        An entire mount's admitted n-GPU placeholder can only be kept whole. When the best set
+        needs part of it, ``n`` of the new placeholders do as well whenever the topology is
+        symmetric (the common case on an all-to-all xGMI node); otherwise it is released and its
+        GPUs taken back as 1-GPU placeholders — every other free GPU is held by then, so the
+        plugin can only hand out those (retried briefly while the kubelet frees them). Any
+        failure before the admitted placeholder is let go keeps it: a valid, worse-placed
+        reservation rather than a failed attach."""
         keys = self.inv.by_key()
         mine = {normalize_device_id(d) for d in res.device_ids}
         free = [g for g in self._free(st) if not mine.intersection(g.ledger_keys())]
@@ -596,31 +600,48 @@ class GpuMountService:
             return res
         attached = st.hot + st.own
         links = self.inv.links()
+        table = {g.index: g for g in self.inv.gpus()}
         group = secrets.token_hex(4) if req.is_entire_mount else ""
         rid = log.request_id.get()
 
-        def best_of(ids: List[str]):
+        def best_of(ids: List[str]) -> List[str]:
             by = {keys[normalize_device_id(d)].index: d for d in ids
                   if normalize_device_id(d) in keys}
-            plc = topology.choose([keys[normalize_device_id(d)] for d in by.values()], n,
-                                  links, attached=attached, policy=self.cfg.topology_policy)
+            plc = topology.choose([table[i] for i in by], n, links, attached=attached,
+                                  policy=self.cfg.topology_policy) if len(by) >= n else None
             return [by[i] for i in plc.chosen] if plc else list(res.device_ids)
+
+        def score(ids: List[str]) -> float:
+            return topology.score_set(table, links, [g.index for g in attached] +
+                                      [keys[normalize_device_id(d)].index for d in ids])[0]
         held = list(res.placeholders)
         extra: List[Placeholder] = []
+        pick = best_of
         try:
             with trace.span("placement_correct", held=len(free)):
                 extra = await self.ph.hold_singles(pod, len(free), req.is_entire_mount, group,
                                                    rid, req.container, req.idempotency_key)
-                ids = [d for p in held + extra for d in p.device_ids]
-                want = {normalize_device_id(d) for d in best_of(ids)}
-                mixed = req.is_entire_mount and want & mine and not mine <= want
-                if mixed:
-                    # the admitted n-GPU placeholder only partly belongs to the best set
-                    await self.ph.release(held, wait=False)
-                    held = []
-                    extra += await self.ph.hold_singles(pod, len(mine), True, group, rid,
-                                                        req.container, req.idempotency_key)
-                new, surplus = self.ph.keep_picked(held + extra, n, best_of)
+                best = best_of([d for p in held + extra for d in p.device_ids])
+                want = {normalize_device_id(d) for d in best}
+                if req.is_entire_mount and want & mine and not mine <= want:
+                    new_ids = [d for p in extra for d in p.device_ids]
+                    alt = best_of(new_ids) if len(new_ids) >= n else []
+                    if alt and score(alt) <= score(best) + 1e-6:
+                        pick = lambda ids: alt          # noqa: E731 - as good, no 2nd round
+                    else:
+                        await self.ph.release(held, wait=True)
+                        held = []
+                        want_n, got = len(mine), []
+                        for delay in (0.0, 0.05, 0.2):
+                            if delay:
+                                await asyncio.sleep(delay)
+                            got += await self.ph.hold_singles(
+                                pod, want_n - len(got), True, group, rid, req.container,
+                                req.idempotency_key)
+                            if len(got) >= want_n:
+                                break
+                        extra += got
+                new, surplus = self.ph.keep_picked(held + extra, n, pick)
         except (ReserveError, InsufficientGPU, asyncio.TimeoutError, InjectedFault) as e:
             await self._release_quiet(extra)
             if held:

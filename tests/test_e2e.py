@@ -892,3 +892,28 @@ def test_shipped_default_places_optimally_on_a_fragmented_node_with_a_hint_blind
     assert auto["placement_corrections"] > 0 and auto["audit_issues"] == 0
     hint = scenario("hint")
     assert sum(s["optimal"] < s["attaches"] for s in hint["per_n"].values()) > 0, hint
+
+
+def test_entire_mount_correction_takes_part_of_the_admitted_set_back():
+    """Entire mount, best set = one GPU of the plugin's n-GPU placeholder + one other free GPU,
+    and no n of the other free GPUs are as good: the placeholder is released and its GPUs taken
+    back as 1-GPU placeholders (a second round), then the best pair is kept as a group."""
+    async def body(lc):
+        for t in ("a", "b", "t"):
+            lc.tenant(t)
+        gpus = lc.inventory.gpus()
+        assert (await lc.add("default", "a", 3))[0] == 200               # 0,1,2 (NUMA 0)
+        code, b = await lc.add("default", "b", 2)                        # a NUMA-1 pair
+        assert code == 200 and _numa_of(lc, b["devices"]) == {1}
+        held_b = {d["index"] for d in b["devices"]}
+        free = [g.index for g in gpus if g.index not in held_b | {0, 1, 2}]
+        code, c = await lc.add("default", "t", 2, entire=True)
+        assert code == 200, c
+        got = sorted(d["index"] for d in c["devices"])
+        assert _numa_of(lc, c["devices"]) == {1}, (free, got)
+        assert len(node_of(lc).allocated) == 7 and not await lc.audit("default", "t")
+        code, _ = await lc.remove("default", "t", [c["devices"][0]["uuid"]])
+        assert code == 400                                 # still one entire mount (group)
+        code, _ = await lc.remove("default", "t", [d["uuid"] for d in c["devices"]])
+        assert code == 200 and len(node_of(lc).allocated) == 5
+    run(body, alloc_policy="first-free")
