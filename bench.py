@@ -63,6 +63,9 @@ class _LocalCP:
     def kubelet_calls(self) -> dict:
         return dict(self.lc.nodes["node-0"].kubelet.calls)
 
+    def corrections(self) -> int:
+        return int(self.lc.nodes["node-0"].worker.metrics.placement_corrections._value.get())
+
     def tenant_view(self):
         node = self.lc.nodes["node-0"].node
         (c,) = [c for c in node.containers.values() if c.pod_name == "tenant"]
@@ -100,6 +103,12 @@ class _ProcCP:
 
     def kubelet_calls(self) -> dict:
         return self.pc.kubelet_calls()
+
+    def corrections(self) -> int:
+        for ln in self.pc.worker_metrics().splitlines():
+            if ln.startswith("gm_placement_corrections_total "):
+                return int(float(ln.split()[1]))
+        return 0
 
     def tenant_view(self):
         from gpumounter_amd.ops import tenant
@@ -458,6 +467,7 @@ def main() -> int:
                     print(f"bench: tenant-side view check failed: {tenant_view}",
                           file=sys.stderr)
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
+            corrections = cp.corrections() if args.protocol == "gpumounter" else None
             placeholders_left = cp.placeholders_left()
             kcalls = cp.kubelet_calls()
             p50 = pct(attach_ms, 0.5)
@@ -563,6 +573,8 @@ def main() -> int:
                 "rccl_allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4)
                 if ar_ms and ar_backend[0] == "nccl" else None,
                 "tenant_view": tenant_view,
+                # attaches whose plugin-chosen GPUs were swapped for a better-placed set
+                "placement_corrections": corrections,
                 "attached_hives": att_hives, "attached_numa_nodes": att_numa,
                 "non_xgmi_pairs": att_nx, "p2p": p2p,
                 "ledger_audit_issues": audit_issues,

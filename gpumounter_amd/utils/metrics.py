@@ -51,6 +51,8 @@ class Metrics:
         self.hot_gpus = Gauge("gm_hot_mounted_gpus", "GPUs hot-mounted into pods, by the pods' "
                               "namespace (sum over time = GPU-seconds for chargeback)",
                               ["namespace"], registry=r)
+        self.draining = Gauge("gm_draining_placeholders", "force-removed GPUs held until their "
+                              "killed processes exit (worker/drain.py)", registry=r)
         self.http_requests = Counter("gm_http_requests_total", "master HTTP requests",
                                      ["route", "code"], registry=r)
 

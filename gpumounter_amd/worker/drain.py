@@ -88,6 +88,7 @@ class DrainKeeper:
             return failed
         for ph in marked:
             self.held[ph.uid] = (ph, pinned)
+        self.svc.metrics.draining.set(len(self.held))
         self.svc.metrics.reconcile_actions.labels(action="drain_hold").inc(len(marked))
         log.kv(_log, 30, "GPU held until killed processes exit", pids=list(pids),
                placeholders=[p.name for p in marked])
@@ -113,6 +114,7 @@ class DrainKeeper:
     async def _release(self, phs: Sequence[Placeholder]) -> None:
         for ph in phs:
             self.held.pop(ph.uid, None)
+        self.svc.metrics.draining.set(len(self.held))
         await self.svc.ph.release(list(phs), wait=False)
         self.released += len(phs)
         self.svc.metrics.reconcile_actions.labels(action="drain_release").inc(len(phs))
