@@ -388,3 +388,41 @@ def test_tenant_side_hip_sees_the_gpu_only_while_attached(real_inventory):
             assert after["count"] == 0, after
             print("tenant view:", before, during, after)
     asyncio.run(run())
+
+
+def test_force_remove_waits_for_a_sigterm_ignoring_hip_process(real_inventory):
+    """A real HIP process that ignores SIGTERM and holds 16 GiB of HBM: force removal revokes
+    access, escalates to SIGKILL after the grace, and releases the placeholder only after the
+    process (and its KFD context) is gone — the GPU is never schedulable while the tenant can
+    still reach it through an open fd."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+    from gpumounter_amd.ops import probe
+
+    bdf0 = probe.props(0)["pci_bus_id"]
+    code = ("import signal, time, torch; signal.signal(signal.SIGTERM, signal.SIG_IGN); "
+            "x = torch.empty(16 << 30, dtype=torch.uint8, device='cuda:0'); x.fill_(1); "
+            "torch.cuda.synchronize(); print('ready', flush=True); time.sleep(120)")
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    try:
+        assert child.stdout.readline().strip() == "ready"
+
+        async def run():
+            async with LocalCluster(amdsmi_lib="", cgroup_mode="v2", node_gpu_bdfs=[bdf0],
+                                    worker_overrides={"kill_grace_s": 0.5}) as lc:
+                lc.tenant("busy", pids={"main": [child.pid]})
+                code, body = await lc.add("default", "busy", 1)
+                assert code == 200, body
+                t0 = time.perf_counter()
+                code, b2 = await lc.remove("default", "busy", [body["devices"][0]["uuid"]],
+                                           force=True)
+                dt = time.perf_counter() - t0
+                assert code == 200 and child.pid in b2["killed_pids"], b2
+                assert child.poll() == -9, "the GPU was released before its process exited"
+                assert lc.cluster.placeholders() == []
+                print(f"force removal with SIGKILL escalation: {dt * 1e3:.1f} ms")
+                assert dt >= 0.5
+        asyncio.run(run())
+    finally:
+        if child.poll() is None:
+            child.kill()
+        child.wait()
