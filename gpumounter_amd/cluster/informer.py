@@ -41,6 +41,9 @@ class PodInformer:
         # bumped by every relist: a write whose request went out in an earlier epoch may be
         # older than what the list delivered (see upsert)
         self.epoch = 0
+        # key → resourceVersion of a write-through the watch has not delivered yet: until it
+        # does, the watch's events for that key are older than the cached object
+        self._pending: Dict[Key, str] = {}
         self.handlers: List[Callable[[str, dict], None]] = []
 
     async def start(self) -> None:
@@ -76,6 +79,7 @@ class PodInformer:
         self.cache = fresh
         self.rv = rv
         self.epoch += 1
+        self._pending.clear()
         await self._notify("RELIST", {})
 
     async def _notify(self, etype: str, pod: dict) -> None:
@@ -118,8 +122,13 @@ class PodInformer:
                     if etype == "DELETED":
                         self.cache.pop(key, None)
                         self._seen.pop(key, None)   # stale upserts: caught by `deleted`
+                        self._pending.pop(key, None)
                         self.deleted[key] = md.get("uid", "")
+                    elif key in self._pending and \
+                            self._pending[key] != md.get("resourceVersion", ""):
+                        pass        # older than our write-through: the cache is newer
                     else:
+                        self._pending.pop(key, None)
                         self.cache[key] = pod
                         self.deleted.pop(key, None)
                     await self._notify(etype, pod)
@@ -174,6 +183,8 @@ class PodInformer:
         if key in self.deleted and self.deleted[key] == md.get("uid"):
             return
         self.cache[key] = pod
+        if rv:
+            self._pending[key] = rv
 
     # ------------------------------------------------------------------------ queries
     def get(self, ns: str, name: str) -> Optional[dict]:

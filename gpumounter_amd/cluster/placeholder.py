@@ -41,7 +41,8 @@ from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.cluster.quota import QuotaExceeded
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_GROUP, ANN_IDEMPOTENCY,
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTAINER, ANN_GROUP,
+                                         ANN_IDEMPOTENCY,
                                          ANN_MOUNT_MODE, ANN_OWNER_UID, ANN_PREFERRED, LABEL_APP,
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          SLAVE_SUFFIX)
@@ -70,6 +71,7 @@ class Placeholder:
     uid: str = ""
     device_ids: Tuple[str, ...] = ()
     mode: str = "single"
+    candidate: bool = False      # held by a trim/correction pick, not yet confirmed
 
 
 @dataclass
@@ -254,15 +256,19 @@ class PlaceholderManager:
         return self.informer.list(lambda p: not p["metadata"].get("deletionTimestamp")
                                   and p["metadata"].get("uid") not in self.tombstones)
 
-    def owned_by(self, owner: dict) -> List[dict]:
+    def owned_by(self, owner: dict, candidates: bool = False) -> List[dict]:
+        """The owner's placeholders; ``candidates``: also those a trim/correction pick holds
+        and has not confirmed (never mounted; released by the pick or the reconciler)."""
         uid = podu.uid_of(owner)
         oname, ons = _label_value(podu.name_of(owner)), _label_value(podu.ns_of(owner))
 
         def mine(p: dict) -> bool:
             md = p["metadata"]
             lab = md.get("labels") or {}
+            ann = md.get("annotations") or {}
             return (lab.get(LABEL_OWNER) == oname and lab.get(LABEL_OWNER_NS) == ons
-                    and (md.get("annotations") or {}).get(ANN_OWNER_UID) == uid
+                    and ann.get(ANN_OWNER_UID) == uid
+                    and (candidates or ANN_CANDIDATE not in ann)
                     and not md.get("deletionTimestamp")
                     and md.get("uid") not in self.tombstones)
 
@@ -315,10 +321,13 @@ class PlaceholderManager:
         mode = "entire" if entire else "single"
         bodies = [self.build(owner, 1, mode, (), attach_id, container, idempotency_key)
                   for _ in range(width)]
-        if group:
-            for b in bodies:
+        for b in bodies:
+            b["metadata"]["annotations"][ANN_CANDIDATE] = attach_id or "1"
+            if group:
                 b["metadata"]["annotations"][ANN_GROUP] = group
         created = await self._create(bodies)
+        for p in created:
+            p.candidate = True
         try:
             with trace.span("placeholder_wait"):
                 self.faults.check("placeholder_wait")
@@ -350,7 +359,32 @@ class PlaceholderManager:
         if len(admitted) < total:
             await self.release(admitted, wait=False)
             raise InsufficientGPU(f"only {len(admitted)} of {total} GPUs admitted")
-        return self.keep_picked(admitted, total, pick)
+        res, surplus = self.keep_picked(admitted, total, pick)
+        try:
+            await self.confirm(res.placeholders)
+        except BaseException:
+            await self.release(admitted, wait=False)
+            raise
+        return res, surplus
+
+    async def confirm(self, phs: Sequence[Placeholder]) -> None:
+        """Clear the candidate mark on the placeholders a pick keeps (one parallel PATCH), so
+        they count as the owner's from here on."""
+        todo = [p for p in phs if p.candidate]
+        if not todo:
+            return
+        patch = {"metadata": {"annotations": {ANN_CANDIDATE: None}}}
+        with trace.span("placement_confirm", placeholders=len(todo)):
+            epoch = self.informer.epoch
+            res = await asyncio.gather(*[self.kube.patch_pod(p.namespace, p.name, patch)
+                                         for p in todo], return_exceptions=True)
+        bad = [r for r in res if not isinstance(r, dict)]
+        for p, r in zip(todo, res):
+            if isinstance(r, dict):
+                self.informer.upsert(r, epoch)
+                p.candidate = False
+        if bad:
+            raise ReserveError(f"confirming {len(bad)} placeholder(s) failed: {bad[0]}")
 
     @staticmethod
     def keep_picked(held: Sequence[Placeholder], total: int,
@@ -648,9 +682,10 @@ class PlaceholderManager:
     def from_pod(p: dict, ledger_ids: Dict[Tuple[str, str], List[str]]) -> Placeholder:
         md = p["metadata"]
         key = (md["namespace"], md["name"])
+        ann = md.get("annotations") or {}
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""),
-                           tuple(ledger_ids.get(key, ())),
-                           (md.get("annotations") or {}).get(ANN_MOUNT_MODE, "single"))
+                           tuple(ledger_ids.get(key, ())), ann.get(ANN_MOUNT_MODE, "single"),
+                           ANN_CANDIDATE in ann)
 
     def cached(self, p: dict) -> Optional[Placeholder]:
         """Placeholder with its device IDs from the admission cache (None if unknown)."""
@@ -658,5 +693,6 @@ class PlaceholderManager:
         ids = self.device_ids.get(md.get("uid", ""))
         if ids is None:
             return None
+        ann = md.get("annotations") or {}
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""), ids,
-                           (md.get("annotations") or {}).get(ANN_MOUNT_MODE, "single"))
+                           ann.get(ANN_MOUNT_MODE, "single"), ANN_CANDIDATE in ann)

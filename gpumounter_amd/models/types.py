@@ -41,6 +41,10 @@ ANN_OWNER_NAME = "gpumounter.amd.com/owner-name"
 ANN_IDEMPOTENCY = "gpumounter.amd.com/idempotency-key"
 ANN_GROUP = "gpumounter.amd.com/group"      # entire-mount group made of pooled placeholders
 MODE_STANDBY = "standby"
+# set on the 1-GPU placeholders a trim or placement correction holds while it picks; cleared on
+# the kept ones before they are mounted. A worker that dies mid-pick leaves only candidates
+# behind, which nothing mounts and the reconciler releases.
+ANN_CANDIDATE = "gpumounter.amd.com/candidate"
 # a force-removed GPU whose killed processes have not exited yet (worker/drain.py)
 MODE_DRAINING = "draining"
 ANN_DRAIN_PIDS = "gpumounter.amd.com/drain-pids"      # pid:starttime,... waited on

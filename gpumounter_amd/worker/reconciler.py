@@ -34,7 +34,7 @@ from typing import Dict, List
 
 from gpumounter_amd.cluster.kube import NotFound
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import ANN_OWNER_UID
+from gpumounter_amd.models.types import ANN_CANDIDATE, ANN_OWNER_UID
 from gpumounter_amd.utils import log
 
 _log = log.get("worker.reconciler")
@@ -87,7 +87,7 @@ class Reconciler:
 
     def _on_node_pod(self, etype: str, pod: dict) -> None:
         if etype == "DELETED" or podu.phase_of(pod) in ("Succeeded", "Failed"):
-            if self.svc.ph.owned_by(pod):
+            if self.svc.ph.owned_by(pod, candidates=True):
                 self._kick(("release", podu.ns_of(pod), podu.name_of(pod), podu.uid_of(pod)))
 
     def _kick(self, key: tuple) -> None:
@@ -107,7 +107,7 @@ class Reconciler:
             async with svc.pod_lock(ns, name):
                 if key[0] == "release":
                     stub = {"metadata": {"namespace": ns, "name": name, "uid": key[3]}}
-                    phs = svc.ph.owned_by(stub)
+                    phs = svc.ph.owned_by(stub, candidates=True)
                     if phs:   # back to the warm pool when one is configured
                         await svc._release([svc.ph.cached(p) or svc.ph.from_pod(p, {})
                                             for p in phs])
@@ -248,6 +248,15 @@ class Reconciler:
             if lock.locked():
                 continue  # an attach/detach is in flight for this owner
             async with lock:
+                # candidates of a trim/correction pick whose attach is not running (its worker
+                # died mid-pick): never the owner's, never mounted — give the GPUs back
+                cands = [p for p in phs
+                         if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})]
+                if cands:
+                    rep.stuck += [p["metadata"]["name"] for p in cands]
+                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in cands], wait=False)
+                    phs = [p for p in phs if p not in cands]
+                    m.reconcile_actions.labels(action="candidate_release").inc(len(cands))
                 # stuck placeholders (never admitted)
                 stuck = []
                 for p in phs:

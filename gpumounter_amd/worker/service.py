@@ -642,6 +642,8 @@ class GpuMountService:
                                 break
                         extra += got
                 new, surplus = self.ph.keep_picked(held + extra, n, pick)
+                if sum(len(p.device_ids) for p in new.placeholders) == n:
+                    await self.ph.confirm(new.placeholders)
         except (ReserveError, InsufficientGPU, asyncio.TimeoutError, InjectedFault) as e:
             await self._release_quiet(extra)
             if held:

@@ -250,3 +250,27 @@ def test_privileged_pod_gpu_process_is_busy_and_force_killed(tmp_path, mock_inve
         _native.mock_smi().gm_mock_set_procs_file(b"")
         if sleeper.poll() is None:
             sleeper.kill()
+
+
+# ------------------------------------------------------------------------------ candidates
+def test_candidates_left_by_a_dead_pick_are_never_mounted_and_are_released():
+    """A trim or placement-correction pick holds 1-GPU *candidate* placeholders and confirms
+    only the ones it keeps. A worker that dies mid-pick leaves candidates owned by the tenant:
+    nothing may mount them (the tenant asked for fewer GPUs), and the reconciler gives them
+    back."""
+    async def body(lc):
+        lc.tenant("t")
+        code, b = await lc.add("default", "t", 1)
+        assert code == 200
+        w = lc.nodes["node-0"].worker
+        pod = lc.cluster.get("default", "t")
+        left = await w.service.ph.hold_singles(pod, 3, False, "", "dead-attach", "", "")
+        assert len(left) == 3 and all(p.candidate for p in left)
+        st = await w.service.pod_state(pod, fresh=True)
+        assert [g.uuid for g in st.hot] == [b["devices"][0]["uuid"]]     # not the candidates
+        assert not await lc.audit("default", "t")
+        rep = await w.reconciler.run_once()
+        assert len(rep.stuck) == 3 and not rep.repaired, rep
+        assert len(lc.cluster.placeholders()) == 1 and len(node_of(lc).allocated) == 1
+        assert not await lc.audit("default", "t")
+    run(body, worker_overrides={"reconcile_on_events": False})

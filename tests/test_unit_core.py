@@ -281,3 +281,44 @@ def test_informer_drops_write_through_older_than_a_relist():
     assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "patch-after-relist"
     inf.upsert(pod("14", "created", name="q", uid="w"), ep)   # not in the list: newer, kept
     assert inf.get("ns", "q") is not None
+
+
+def test_informer_keeps_write_through_against_older_watch_events():
+    """Our PATCH response is cached at once; watch events for that object older than it (the
+    watch lags) must not overwrite it until the watch has delivered our version."""
+    import asyncio
+
+    from gpumounter_amd.cluster.informer import PodInformer
+
+    def pod(rv, v):
+        return {"metadata": {"namespace": "ns", "name": "p", "uid": "u", "resourceVersion": rv,
+                             "annotations": {"v": v}}}
+
+    class Feed(PodInformer):
+        def __init__(self):
+            super().__init__(kube=None)
+            self.q = asyncio.Queue()
+
+        async def _list(self):
+            return [pod("1", "listed")], "1"
+
+        async def _watch(self, timeout_s):
+            while True:
+                ev = await self.q.get()
+                if ev is None:
+                    return
+                yield ev
+
+    async def main():
+        inf = Feed()
+        await inf.start()
+        inf.upsert(pod("5", "patched"), inf.epoch)         # our write, watch still at rv 1
+        await inf.q.put(("MODIFIED", pod("3", "kubelet-status")))
+        await asyncio.sleep(0.01)
+        assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "patched"
+        await inf.q.put(("MODIFIED", pod("5", "patched")))  # the watch reaches our write
+        await inf.q.put(("MODIFIED", pod("6", "later")))
+        await asyncio.sleep(0.01)
+        assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "later"
+        await inf.stop()
+    asyncio.run(main())
