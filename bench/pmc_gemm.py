@@ -5,7 +5,6 @@ GM_PMC_TORCH=1 three of hipBLASLt's NT kernel on uniform [-1, 1) bf16 operands.
     rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv \\
         -d DIR -- python3 bench/pmc_gemm.py
 """
-import ctypes as C
 import os
 import sys
 

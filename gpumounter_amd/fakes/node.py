@@ -25,7 +25,7 @@ from dataclasses import dataclass, field
 from typing import Deque, Dict, List, Optional, Sequence, Tuple
 
 from gpumounter_amd.hw import topology
-from gpumounter_amd.models.device import AmdGpu, LinkMatrix, normalize_device_id
+from gpumounter_amd.models.device import AmdGpu, LinkMatrix
 from gpumounter_amd.node import checkpoint as ckpt
 from gpumounter_amd.node.checkpoint import CHECKPOINT_NAME
 from gpumounter_amd.models.pod import QOS_BESTEFFORT, QOS_BURSTABLE, qos_class

@@ -18,7 +18,6 @@ import ctypes as C
 import errno
 import os
 import select
-import signal
 import signal as _sig   # Pinned.signal shadows the module name inside the class body
 from typing import Dict, Iterable, List, Sequence, Tuple
 
