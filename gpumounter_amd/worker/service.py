@@ -644,7 +644,10 @@ class GpuMountService:
                 new, surplus = self.ph.keep_picked(held + extra, n, pick)
                 if sum(len(p.device_ids) for p in new.placeholders) == n:
                     await self.ph.confirm(new.placeholders)
-        except (ReserveError, InsufficientGPU, asyncio.TimeoutError, InjectedFault) as e:
+        except (ReserveError, InsufficientGPU, QuotaExceeded, asyncio.TimeoutError,
+                InjectedFault) as e:
+            # QuotaExceeded: in tenant-namespace mode the extra holds count against the
+            # tenant's ResourceQuota at the apiserver
             await self._release_quiet(extra)
             if held:
                 _log.warning("placement correction failed, keeping the plugin's choice: %s", e)

@@ -99,3 +99,20 @@ def test_recheck_rolls_back_an_overshoot_from_another_node():
             await asyncio.sleep(0.01)
         assert await settled()
     run(body, n_nodes=2)
+
+
+def test_placement_correction_within_a_tight_tenant_quota_keeps_the_plugins_choice():
+    """Tenant-namespace placeholders: the quota admits exactly the request, so the correction's
+    extra holds are refused by the apiserver's quota admission. The attach still succeeds with
+    the GPUs the plugin chose (valid, worse placed) instead of failing."""
+    async def body(lc):
+        lc.cluster.set_quota("team-a", "gpus", {"requests.amd.com/gpu": "2"})
+        lc.tenant("other", ns="team-b")
+        lc.tenant("t", ns="team-a")
+        assert (await lc.add("team-b", "other", 3))[0] == 200          # GPUs 0, 1, 2
+        code, b = await lc.add("team-a", "t", 2)
+        assert code == 200, b
+        assert sorted(d["index"] for d in b["devices"]) == [3, 4]      # across the sockets
+        assert await lc.audit("team-a", "t") == []
+        assert len(lc.nodes["node-0"].node.allocated) == 5
+    run(body, placeholder_namespace_mode="tenant", alloc_policy="first-free")
