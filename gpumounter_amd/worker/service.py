@@ -692,7 +692,12 @@ class GpuMountService:
             preferred = create_pref
         if not got and preferred and self.cfg.placement_enforce == "trim" and n_free > n \
                 and self.cfg.gpu_allocation != "dra":
-            return await self._reserve_trim(pod, n, req, st, n_free)
+            try:
+                return await self._reserve_trim(pod, n, req, st, n_free)
+            except QuotaExceeded as e:
+                # tenant-namespace placeholders: holding every free GPU can exceed the
+                # tenant's quota although the request fits; reserve it plainly instead
+                _log.info("trim refused by the tenant's quota (%s); plain reservation", e)
         token = ""
         if self.plugin is not None and preferred:
             # our own device plugin answers GetPreferredAllocation for these placeholders

@@ -116,3 +116,15 @@ def test_placement_correction_within_a_tight_tenant_quota_keeps_the_plugins_choi
         assert await lc.audit("team-a", "t") == []
         assert len(lc.nodes["node-0"].node.allocated) == 5
     run(body, placeholder_namespace_mode="tenant", alloc_policy="first-free")
+
+
+def test_trim_mode_within_a_tight_tenant_quota_falls_back_to_a_plain_reservation():
+    async def body(lc):
+        lc.cluster.set_quota("team-a", "gpus", {"requests.amd.com/gpu": "2"})
+        lc.tenant("t", ns="team-a")
+        code, b = await lc.add("team-a", "t", 2)
+        assert code == 200, b
+        assert await lc.audit("team-a", "t") == []
+        assert (await lc.add("team-a", "t", 1))[0] == 403               # the quota itself holds
+    run(body, placeholder_namespace_mode="tenant", alloc_policy="first-free",
+        worker_overrides={"placement_enforce": "trim"})
