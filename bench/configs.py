@@ -340,9 +340,11 @@ def main() -> int:
     ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
     ap.add_argument("--latency", choices=("zero", "realistic"), default="zero")
     ap.add_argument("--placement", choices=("auto", "hint", "trim"), default="auto")
-    ap.add_argument("--alloc-policy", choices=("first-free", "topology"), default="first-free",
-                    help="the fake node's device plugin: first free in device order (no "
-                         "GetPreferredAllocation), or its own pod-blind topology choice")
+    ap.add_argument("--alloc-policy", choices=("first-free", "random", "topology"),
+                    default="first-free",
+                    help="the fake node's device choice: first free in device order; random "
+                         "(the kubelet's pick without GetPreferredAllocation); or a plugin's own "
+                         "pod-blind topology choice")
     ap.add_argument("--device-plugin", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=50)

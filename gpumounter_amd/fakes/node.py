@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import json
 import os
+import random
 import secrets
 import shutil
 import threading
@@ -69,9 +70,10 @@ class FakeNode:
         self.cgroup_mode = cgroup_mode
         self.cgroup_driver = cgroup_driver
         self.runtime = runtime
-        if alloc_policy not in ("first-free", "topology"):
-            raise ValueError(f"alloc_policy {alloc_policy!r}: first-free | topology")
+        if alloc_policy not in ("first-free", "random", "topology"):
+            raise ValueError(f"alloc_policy {alloc_policy!r}: first-free | random | topology")
         self.alloc_policy = alloc_policy
+        self._rng = random.Random(f"{name}-devices")
         self.device_id_kind = device_id_kind
         self.labels = {"kubernetes.io/hostname": name, "gpu-mounter-enable": "enable"}
         self.labels.update(labels or {})
@@ -187,8 +189,10 @@ class FakeNode:
         ``amd.com/gpu`` reads gpumounter's ``preferred-devices`` annotation (the kubelet never
         passes pod annotations to a plugin), so this fake does not read it either:
 
-        * ``first-free`` (default): the kubelet's choice without GetPreferredAllocation —
-          free devices in device order;
+        * ``first-free`` (default): free devices in device order;
+        * ``random``: the kubelet's own choice when the plugin offers no
+          GetPreferredAllocation — it takes devices from a Go set, whose iteration order is
+          unspecified (seeded here, so runs repeat);
         * ``topology``: a plugin with its own GetPreferredAllocation (the ROCm plugin's
           best-effort policy): the best-connected free set, with no idea which GPUs the pod
           that will receive them already holds.
@@ -203,6 +207,8 @@ class FakeNode:
             if self.alloc_policy == "topology":
                 plc = topology.choose(free, n, self.links, policy="xgmi")
                 chosen = [next(g for g in free if g.index == i) for i in plc.chosen]
+            elif self.alloc_policy == "random":
+                chosen = self._rng.sample(free, n)
             else:
                 chosen = free[:n]
             ids = [self.device_id(g) for g in chosen]
