@@ -619,6 +619,7 @@ class GpuMountService:
         pick = best_of
         try:
             with trace.span("placement_correct", held=len(free)):
+                self.faults.check("placement_correct")
                 extra = await self.ph.hold_singles(pod, len(free), req.is_entire_mount, group,
                                                    rid, req.container, req.idempotency_key)
                 best = best_of([d for p in held + extra for d in p.device_ids])
@@ -642,6 +643,7 @@ class GpuMountService:
                                 break
                         extra += got
                 new, surplus = self.ph.keep_picked(held + extra, n, pick)
+                self.faults.check("placement_correct", "after")
                 if sum(len(p.device_ids) for p in new.placeholders) == n:
                     await self.ph.confirm(new.placeholders)
         except (ReserveError, InsufficientGPU, QuotaExceeded, asyncio.TimeoutError,

@@ -117,3 +117,24 @@ def test_random_fault_storm_then_reconcile():
             assert lc.cluster.placeholders() == [] and lc.nodes["node-0"].node.allocated == {}
             assert sum(r.hits for r in w.faults.rules.values()) == 0
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("mode", ["raise", "after"])
+def test_placement_correction_fault_keeps_a_valid_attach(mode):
+    """A failure inside the placement correction (before it holds anything, or after its pick)
+    leaves the attach with the plugin's valid, worse-placed choice and nothing else held."""
+    async def main():
+        async with LocalCluster(alloc_policy="first-free") as lc:
+            lc.tenant("other")
+            lc.tenant("t")
+            assert (await lc.add("default", "other", 3))[0] == 200
+            w = lc.nodes["node-0"].worker
+            w.faults.rules = {"placement_correct": Rule(1.0, mode)}
+            code, b = await lc.add("default", "t", 2)
+            w.faults.rules = {}
+            assert code == 200, b
+            assert sorted(d["index"] for d in b["devices"]) == [3, 4]
+            await asyncio.sleep(0.05)
+            assert len(lc.nodes["node-0"].node.allocated) == 5
+            await _consistent(lc, "t", only_tenant=False)
+    asyncio.run(main())
