@@ -426,3 +426,35 @@ def test_force_remove_waits_for_a_sigterm_ignoring_hip_process(real_inventory):
         if child.poll() is None:
             child.kill()
         child.wait()
+
+
+def test_tenant_view_needs_the_render_node_and_its_grant(tmp_path, real_inventory):
+    """What the tenant-side view rests on, checked against the real ROCm stack: /dev/kfd alone
+    exposes no GPU (ROCm skips a GPU whose render node it cannot open); a render node without
+    the device-cgroup grant exposes none either; node + grant expose exactly that GPU."""
+    import json
+    import os as _os
+
+    from gpumounter_amd.ops import probe, tenant
+
+    g = next(x for x in real_inventory.gpus()
+             if x.bdf == probe.props(0)["pci_bus_id"].lower())
+    kfd = real_inventory.kfd_major
+    root, cg = tmp_path / "root", tmp_path / "cg"
+    (root / "dev" / "dri").mkdir(parents=True)
+    cg.mkdir()
+    (root / "dev" / "kfd").write_text(f"gm-chr {kfd}:0\n")
+    grants = [[2, kfd, 0, 6]]
+    (cg / "gm.bpf.json").write_text(json.dumps({"set": grants}))
+    only_kfd = tenant.hip_devices(str(root), str(cg))
+    assert only_kfd["count"] == 0, only_kfd
+    (root / "dev" / "dri" / f"renderD{g.render_minor}").write_text(
+        f"gm-chr 226:{g.render_minor}\n")
+    no_grant = tenant.hip_devices(str(root), str(cg))
+    assert no_grant["count"] == 0, no_grant
+    grants.append([2, 226, g.render_minor, 6])
+    (cg / "gm.bpf.json").write_text(json.dumps({"set": grants}))
+    both = tenant.hip_devices(str(root), str(cg))
+    assert both["count"] == 1 and both["bdfs"] == [g.bdf], both
+    print("kfd only:", only_kfd, "render without grant:", no_grant, "both:", both)
+    assert _os.path.exists("/dev/kfd")
