@@ -210,12 +210,13 @@ class Pinned:
         return sorted(p for p in live if not self.exited(p))
 
     async def reap(self, pids: Sequence[int], sig: int = _sig.SIGTERM, grace_s: float = 5.0,
-                   kill_wait_s: float = 2.0, already_signalled: bool = False
-                   ) -> Tuple[List[int], List[int]]:
+                   kill_wait_s: float = 2.0, already_signalled: bool = False,
+                   sigkill: bool = True) -> Tuple[List[int], List[int]]:
         """``sig``; wait up to ``grace_s`` for the pinned processes to exit; SIGKILL the rest
         and wait up to ``kill_wait_s`` for them to go. Returns (PIDs that needed SIGKILL, PIDs
         still running after it — uninterruptible sleep). The pidfds stay open: a caller that
-        must wait on survivors keeps them, then calls :meth:`close`."""
+        must wait on survivors keeps them, then calls :meth:`close`. ``sigkill=False`` withholds
+        the SIGKILL (fault injection: a process the kernel cannot kill yet)."""
         live = [p for p in pids if p in self.fds]
         if not already_signalled:
             self.signal(live, sig)
@@ -223,7 +224,8 @@ class Pinned:
         if not live:
             return [], []
         _log.warning("SIGKILL after %.1fs grace: %s", grace_s, live)
-        self.signal(live, _sig.SIGKILL)
+        if sigkill:
+            self.signal(live, _sig.SIGKILL)
         survivors = await self.wait_exit(live, kill_wait_s)
         if survivors:
             _log.error("still running %.1fs after SIGKILL (uninterruptible?): %s",

@@ -881,10 +881,15 @@ class GpuMountService:
                     self.hm.detach(pod, selected, keep, st.own, req.container, targets)
                 if killed:
                     with trace.span("kill", pids=len(killed)):
+                        try:    # GM_FAULT=kill_escalation:1: as if SIGKILL could not land yet
+                            self.faults.check("kill_escalation")
+                            sigkill = True
+                        except InjectedFault:
+                            sigkill = False
                         pinned.signal(killed, self.cfg.kill_signal)
                         _, survivors = await pinned.reap(
                             killed, self.cfg.kill_signal, self.cfg.kill_grace_s,
-                            self.cfg.kill_reap_s, already_signalled=True)
+                            self.cfg.kill_reap_s, already_signalled=True, sigkill=sigkill)
                 if survivors:
                     left = set(survivors)
                     stuck = {i for i, v in busy.items() if left.intersection(v)}

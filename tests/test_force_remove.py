@@ -156,3 +156,50 @@ def test_restarted_worker_releases_a_drain_only_once_its_processes_exit(stubborn
             rep = await w.reconciler.run_once()
             assert len(rep.drained) == 1 and lc.cluster.placeholders() == []
     asyncio.run(main())
+
+
+def test_drain_survives_a_real_worker_crash_in_the_process_deployment(tmp_path, mock_inventory):
+    """Daemons as processes (production entry points). SIGKILL is withheld by fault injection
+    (GM_FAULT=kill_escalation:1), so the killed process outlives the RemoveGPU call and its
+    placeholder drains. The worker is then SIGKILLed and restarted: the new incarnation holds no
+    pidfd, finds the drain's pid:starttime record, keeps the GPU booked while the process lives
+    and releases it once it has exited."""
+    from gpumounter_amd.fakes.deployment import ProcessCluster
+
+    p = subprocess.Popen([sys.executable, "-c", IGNORES_TERM], stdout=subprocess.PIPE)
+    table = tmp_path / "procs"
+    table.write_text("")
+    pc = ProcessCluster(worker_env={"GM_FAULT": "kill_escalation:1.0", "GM_KILL_GRACE_S": "0.2",
+                                    "GM_KILL_REAP_S": "0.2", "GM_BUSY_DETECTION": "both",
+                                    "GM_AMDSMI_MOCK_PROCS": str(table),
+                                    "GM_RECONCILE_PERIOD_S": "0.3"})
+    try:
+        assert p.stdout.readline().strip() == b"ready"
+        pc.start()
+        pc.tenant("busy", pids={"main": [p.pid]})
+        code, b = pc.add("default", "busy", 1)
+        assert code == 200, b
+        dev = b["devices"][0]
+        table.write_text(f"{dev['index']} {p.pid} 4096 python\n")
+        code, b2 = pc.remove("default", "busy", [dev["uuid"]], force=True)
+        assert code == 400 and str(p.pid) in b2["detail"], b2
+        assert p.poll() is None
+        assert pc.kill_worker() == -9
+        pc.restart_worker()
+        time.sleep(1.0)                                     # a few reconciler sweeps
+        phs = pc.placeholders()
+        assert len(phs) == 1, phs
+        assert phs[0]["metadata"]["annotations"]["gpumounter.amd.com/mount-mode"] == "draining"
+        assert pc.audit("default", "busy") == []            # access stays revoked
+        p.kill()
+        p.wait()
+        deadline = time.time() + 10
+        while pc.placeholders() and time.time() < deadline:
+            time.sleep(0.1)
+        assert pc.placeholders() == []
+        assert 'gm_reconcile_actions_total{action="drain_release"} 1.0' in pc.worker_metrics()
+    finally:
+        pc.stop()
+        if p.poll() is None:
+            p.kill()
+            p.wait()
