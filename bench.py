@@ -309,6 +309,7 @@ def main() -> int:
     bound_dev = [None]
     pool_cap = info.get("node_gpus", 0) if rank == 0 else 0
     attach_ms, detach_ms, audit_issues, probe_us, stage = [], [], 0, [], {}
+    hop_ms = []          # (master handler ms, worker ms) per timed attach
     ar_ms = []
     probe_by_gpu = {}
     last_bdfs = []
@@ -328,6 +329,7 @@ def main() -> int:
             obj = [{"bdfs": [d["bdf"] for d in body["devices"]],
                     "uuids": [d["uuid"] for d in body["devices"]],
                     "ms": (t1 - t0) * 1e3, "issues": len(issues),
+                    "master_ms": body.get("master_ms"), "worker_ms": body.get("total_ms"),
                     "timings": {t["name"]: t["ms"] for t in body.get("timings", [])}}]
         if world > 1:
             dist.broadcast_object_list(obj, src=0)
@@ -381,6 +383,8 @@ def main() -> int:
                 cp.wait_pool(min(args.warm_pool, pool_cap))
             if record:
                 attach_ms.append(st["ms"])
+                if st.get("master_ms") is not None and st.get("worker_ms") is not None:
+                    hop_ms.append((st["master_ms"], st["worker_ms"]))
                 detach_ms.append((t1 - t0) * 1e3)
                 if samples is not None:
                     samples.append({"t": round(time.time(), 4), "attach_ms": round(st["ms"], 4),
@@ -559,6 +563,15 @@ def main() -> int:
                 "attach_p999_ms": round(pct(attach_ms, 0.999), 4) if len(attach_ms) >= 1000
                 else None,
                 "attach_max_ms": round(max(attach_ms), 4) if attach_ms else None,
+                # where the client-side attach time goes, p50: the worker's whole attach, the
+                # master's handler (incl. the gRPC call to the worker) and what is left
+                # (client ⇄ master HTTP)
+                "attach_split_p50_ms": {
+                    "worker": round(pct([w for _, w in hop_ms], 0.5), 4),
+                    "master_minus_worker": round(pct([m - w for m, w in hop_ms], 0.5), 4),
+                    "client_minus_master": round(pct([a - m for a, (m, _) in
+                                                      zip(attach_ms, hop_ms)], 0.5), 4)}
+                if hop_ms and len(hop_ms) == len(attach_ms) else None,
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),
                 "detach_p99_ms": round(pct(detach_ms, 0.99), 4),
                 "stage_p50_ms": {k: round(statistics.median(v), 4) for k, v in sorted(stage.items())},
