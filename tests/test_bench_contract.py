@@ -119,8 +119,9 @@ def test_bench_single_process_eight_gpus_verifies_every_per_n_field():
 def test_bench_real_node_ops_reports_stage_split():
     from gpumounter_amd.fakes import realnode
     import pytest
-    if realnode.available() or os.environ.get("GM_PRIVILEGED_TESTS") != "1":
-        pytest.skip("needs root and GM_PRIVILEGED_TESTS=1 (mounts cgroup2/bpffs)")
+    from conftest import privileged_ok
+    if realnode.available() or not privileged_ok():
+        pytest.skip("needs root with mount + bpf (mounts cgroup2/bpffs)")
     env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
     # default --ref-steps: the reference column is skipped with its reason, never a crash
     res = subprocess.run([sys.executable, "bench.py", "--steps", "10", "--warmup", "2",

@@ -1,4 +1,4 @@
-"""Full-stack attach/detach against a real kernel (opt-in: GM_PRIVILEGED_TESTS=1, root).
+"""Full-stack attach/detach against a real kernel (root with mount + bpf; GM_PRIVILEGED_TESTS=0/1 forces off/on, root).
 
 Runs tests/priv_e2e_driver.py in its own process (the mock inventory is configured through
 GM_AMDSMI_MOCK_CONFIG at amdsmi init). See the driver docstring for the setup.
@@ -9,10 +9,9 @@ import subprocess
 import sys
 
 import pytest
+from conftest import privileged_skip
 
-pytestmark = [pytest.mark.privileged,
-              pytest.mark.skipif(os.environ.get("GM_PRIVILEGED_TESTS") != "1" or os.geteuid() != 0,
-                                 reason="opt-in privileged kernel test (GM_PRIVILEGED_TESTS=1)")]
+pytestmark = [pytest.mark.privileged, privileged_skip()]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 

@@ -1,4 +1,4 @@
-"""Real-kernel enforcement tests for the device-access backends (opt-in: GM_PRIVILEGED_TESTS=1,
+"""Real-kernel enforcement tests for the device-access backends (root with mount + bpf; GM_PRIVILEGED_TESTS=0/1 forces off/on,
 needs root with CAP_SYS_ADMIN/CAP_BPF). They mount a private cgroup2 hierarchy (or use the v1
 devices controller), put a child process into a fresh cgroup, and check that the process can open
 exactly the devices the backend granted — using harmless /dev/null, /dev/zero, /dev/full.
@@ -15,14 +15,13 @@ import tempfile
 import uuid
 
 import pytest
+from conftest import privileged_skip
 
 from gpumounter_amd import _native
 from gpumounter_amd.models.device import DeviceNode
 from gpumounter_amd.node.cgroup import V1Backend, V2BpfBackend, _rule_array
 
-pytestmark = [pytest.mark.privileged,
-              pytest.mark.skipif(os.environ.get("GM_PRIVILEGED_TESTS") != "1" or os.geteuid() != 0,
-                                 reason="opt-in privileged kernel test (GM_PRIVILEGED_TESTS=1)")]
+pytestmark = [pytest.mark.privileged, privileged_skip()]
 
 NULL, ZERO, FULL = DeviceNode("/dev/null", 1, 3), DeviceNode("/dev/zero", 1, 5), \
     DeviceNode("/dev/full", 1, 7)

@@ -1,4 +1,4 @@
-"""Device nodes for containers in their own user namespace (opt-in: GM_PRIVILEGED_TESTS=1, root).
+"""Device nodes for containers in their own user namespace (root with mount + bpf; GM_PRIVILEGED_TESTS=0/1 forces off/on, root).
 
 Runs tests/priv_userns_driver.py in a private mount namespace; see its docstring.
 """
@@ -8,10 +8,9 @@ import subprocess
 import sys
 
 import pytest
+from conftest import privileged_skip
 
-pytestmark = [pytest.mark.privileged,
-              pytest.mark.skipif(os.environ.get("GM_PRIVILEGED_TESTS") != "1" or os.geteuid() != 0,
-                                 reason="opt-in privileged kernel test (GM_PRIVILEGED_TESTS=1)")]
+pytestmark = [pytest.mark.privileged, privileged_skip()]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 

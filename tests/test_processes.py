@@ -203,8 +203,9 @@ def test_recycled_pid_is_not_signalled(tmp_path):
     import subprocess
     import sys
 
-    if os.geteuid() != 0 or os.environ.get("GM_PRIVILEGED_TESTS") != "1":
-        pytest.skip("needs root (a PID namespace + clone3 set_tid); GM_PRIVILEGED_TESTS=1")
+    from conftest import privileged_ok
+    if not privileged_ok():
+        pytest.skip("needs root (a PID namespace + clone3 set_tid)")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     script = tmp_path / "reuse.py"
     script.write_text(f"""
