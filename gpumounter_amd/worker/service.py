@@ -95,8 +95,10 @@ class _SharedExclusive:
     @contextlib.asynccontextmanager
     async def shared(self):
         async with self._cond:
-            await self._cond.wait_for(lambda: not self._exclusive and
-                                      not self._waiting_exclusive)
+            if self._exclusive or self._waiting_exclusive:
+                with trace.span("reserve_gate_wait"):
+                    await self._cond.wait_for(lambda: not self._exclusive and
+                                              not self._waiting_exclusive)
             self._shared += 1
         try:
             yield
@@ -110,7 +112,10 @@ class _SharedExclusive:
         async with self._cond:
             self._waiting_exclusive += 1
             try:
-                await self._cond.wait_for(lambda: not self._exclusive and not self._shared)
+                if self._exclusive or self._shared:
+                    with trace.span("reserve_gate_wait"):
+                        await self._cond.wait_for(lambda: not self._exclusive and
+                                                  not self._shared)
             finally:
                 self._waiting_exclusive -= 1
             self._exclusive = True
