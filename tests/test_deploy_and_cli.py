@@ -156,3 +156,42 @@ def test_cli_add_and_remove_authenticate_against_the_shipped_master(tmp_path):
                            capture_output=True, text=True, cwd=ROOT,
                            env={**env, "GM_TOKEN": pc.token}, timeout=120)
         assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_cluster_role_grants_every_api_call_the_daemons_make():
+    """Each KubeClient call needs one (verb, resource) in deploy/rbac.yaml's ClusterRole; a new
+    call without a grant would fail only on a real cluster (the hermetic apiserver does not
+    enforce RBAC), so the mapping is checked here."""
+    import inspect
+
+    import yaml
+
+    from gpumounter_amd.cluster.kube import KubeClient
+
+    needs = {
+        "get_pod": ("", "pods", "get"), "list_pods": ("", "pods", "list"),
+        "watch_pods": ("", "pods", "watch"), "create_pod": ("", "pods", "create"),
+        "delete_pod": ("", "pods", "delete"), "patch_pod": ("", "pods", "patch"),
+        "create_claim": ("resource.k8s.io", "resourceclaims", "create"),
+        "get_claim": ("resource.k8s.io", "resourceclaims", "get"),
+        "delete_claim": ("resource.k8s.io", "resourceclaims", "delete"),
+        "list_claims": ("resource.k8s.io", "resourceclaims", "list"),
+        "list_claims_rv": ("resource.k8s.io", "resourceclaims", "list"),
+        "watch_claims": ("resource.k8s.io", "resourceclaims", "watch"),
+        "list_slices": ("resource.k8s.io", "resourceslices", "list"),
+        "token_review": ("authentication.k8s.io", "tokenreviews", "create"),
+        "subject_access_review": ("authorization.k8s.io", "subjectaccessreviews", "create"),
+        "list_resource_quotas": ("", "resourcequotas", "list"),
+        "create_event": ("", "events", "create"),
+    }
+    calls = {n for n, f in inspect.getmembers(KubeClient)
+             if (inspect.iscoroutinefunction(f) or inspect.isasyncgenfunction(f))
+             and not n.startswith("_") and n not in ("close", "watch")}
+    assert calls == set(needs), ("map new KubeClient calls to their RBAC verb",
+                                 calls ^ set(needs))
+    docs = list(yaml.safe_load_all(open(os.path.join(ROOT, "deploy", "rbac.yaml"))))
+    role = next(d for d in docs if d and d.get("kind") == "ClusterRole")
+    granted = {(g, r, v) for rule in role["rules"] for g in rule.get("apiGroups", [])
+               for r in rule.get("resources", []) for v in rule.get("verbs", [])}
+    missing = {n: need for n, need in needs.items() if need not in granted}
+    assert not missing, missing
