@@ -74,8 +74,11 @@ def test_rbac_is_least_privilege():
     binding = next(d for d in docs if d["kind"] == "ClusterRoleBinding")
     assert binding["roleRef"]["name"] != "cluster-admin"
     resources = {r for role in roles for rule in role["rules"] for r in rule["resources"]}
-    assert resources <= {"pods", "nodes", "events", "tokenreviews", "subjectaccessreviews",
-                         "resourcequotas", "resourceclaims", "resourceslices"}
+    assert resources <= {"pods", "pods/finalizers", "nodes", "events", "tokenreviews",
+                         "subjectaccessreviews", "resourcequotas", "resourceclaims",
+                         "resourceslices"}
+    assert {v for role in roles for rule in role["rules"] if "pods/finalizers" in
+            rule["resources"] for v in rule["verbs"]} == {"update"}
     dra = [rule for role in roles for rule in role["rules"]
            if rule["apiGroups"] == ["resource.k8s.io"]]
     assert {v for rule in dra if rule["resources"] == ["resourceslices"]
