@@ -79,9 +79,12 @@ async def invariants(lc, tenants) -> int:
         st = await svc.pod_state(pod)
         hot += len(st.hot)
         bad += len(svc.hm.audit(pod, st.hot, st.own))
-    standby = sum(1 for p in lc.cluster.placeholders()
-                  if (p["metadata"].get("annotations") or {}).get(
-                      "gpumounter.amd.com/mount-mode") == "standby")
+    # GPUs held by warm-pool standby placeholders (a standby the pool's refill created while
+    # concurrent attaches filled the node stays Pending, holding nothing, until the pool drops it)
+    standby_names = {p["metadata"]["name"] for p in lc.cluster.placeholders()
+                     if (p["metadata"].get("annotations") or {}).get(
+                         "gpumounter.amd.com/mount-mode") == "standby"}
+    standby = sum(1 for _, pod, _ in node.allocated.values() if pod in standby_names)
     bad += hot + standby != len(node.allocated)
     bad += len(node.free_ids()) + len(node.allocated) != node.capacity
     return bad

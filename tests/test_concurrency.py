@@ -30,10 +30,13 @@ async def check_invariants(lc, tenants):
             assert lc.cluster.get(ph.namespace, ph.name) is not None
         assert not svc.hm.audit(pod, st_.hot, st_.own), t                 # I3
     assert len(node.free_ids()) + len(node.allocated) == node.capacity   # I4
-    standby = sum(1 for p in lc.cluster.placeholders()                   # warm-pool capacity
-                  if (p["metadata"].get("annotations") or {}).get(
-                      "gpumounter.amd.com/mount-mode") == "standby"
-                  and not p["metadata"].get("deletionTimestamp"))
+    # warm-pool capacity: GPUs held by standby placeholders (a standby the refill created while
+    # concurrent attaches filled the node is Pending and holds nothing)
+    standby_names = {p["metadata"]["name"] for p in lc.cluster.placeholders()
+                     if (p["metadata"].get("annotations") or {}).get(
+                         "gpumounter.amd.com/mount-mode") == "standby"
+                     and not p["metadata"].get("deletionTimestamp")}
+    standby = sum(1 for _, pod, _ in node.allocated.values() if pod in standby_names)
     assert total_hot + standby == len(node.allocated)
 
 
