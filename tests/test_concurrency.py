@@ -130,10 +130,11 @@ def test_1000_attach_detach_cycles_leave_no_orphans():
 import pytest  # noqa: E402
 
 
-@pytest.mark.parametrize("mode", ["auto", "trim", "device_plugin", "warm_pool"])
+@pytest.mark.parametrize("mode", ["auto", "auto_random", "trim", "device_plugin", "warm_pool"])
 def test_contention_under_each_placement_mode(mode):
     """The 4-pods-for-8-GPUs contract holds whatever enforces the placement."""
     kw = {"auto": dict(alloc_policy="first-free"),
+          "auto_random": dict(alloc_policy="random"),
           "trim": dict(alloc_policy="first-free", worker_overrides={"placement_enforce": "trim"}),
           "device_plugin": dict(device_plugin=True),
           "warm_pool": dict(worker_overrides={"warm_pool_size": 4})}[mode]
