@@ -322,3 +322,41 @@ def test_informer_keeps_write_through_against_older_watch_events():
         assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "later"
         await inf.stop()
     asyncio.run(main())
+
+
+def test_reserve_gate_shared_and_exclusive():
+    """Ordinary reservations overlap; a placement correction (exclusive) waits for them, runs
+    alone, and new ordinary ones queue behind a waiting correction (no starvation)."""
+    import asyncio
+
+    from gpumounter_amd.worker.service import _SharedExclusive
+
+    async def main():
+        g = _SharedExclusive()
+        log = []
+
+        async def shared(tag, hold):
+            async with g.shared():
+                log.append(("in", tag))
+                await asyncio.sleep(hold)
+                log.append(("out", tag))
+
+        async def exclusive(tag, hold):
+            async with g.exclusive():
+                log.append(("in", tag))
+                await asyncio.sleep(hold)
+                log.append(("out", tag))
+        a = asyncio.ensure_future(shared("s1", 0.05))
+        b = asyncio.ensure_future(shared("s2", 0.05))
+        await asyncio.sleep(0.01)
+        x = asyncio.ensure_future(exclusive("x", 0.03))
+        await asyncio.sleep(0.01)
+        c = asyncio.ensure_future(shared("s3", 0.01))
+        await asyncio.gather(a, b, x, c)
+        order = [e for e in log]
+        assert order[:2] == [("in", "s1"), ("in", "s2")]            # overlapping
+        ix = order.index(("in", "x"))
+        assert ("out", "s1") in order[:ix] and ("out", "s2") in order[:ix]
+        assert order[ix + 1] == ("out", "x")                        # alone
+        assert order.index(("in", "s3")) > ix                      # queued behind x
+    asyncio.run(main())
