@@ -8,7 +8,7 @@ and are woken by the next matching event instead of polling the apiserver.
 from __future__ import annotations
 
 import asyncio
-from collections import deque
+from collections import OrderedDict, deque
 from typing import Callable, Dict, List, Optional, Tuple
 
 from gpumounter_amd.cluster.kube import ApiError, KubeClient
@@ -18,6 +18,7 @@ from gpumounter_amd.utils import log
 _log = log.get("cluster.informer")
 
 Key = Tuple[str, str]
+DELETED_KEEP = 65536
 
 
 class PodInformer:
@@ -29,7 +30,10 @@ class PodInformer:
         self.field_selector = field_selector
         self.resync_s = resync_s
         self.cache: Dict[Key, dict] = {}
-        self.deleted: Dict[Key, str] = {}  # key → uid of the last deleted instance
+        # key → uid of the last deleted instance, for write-throughs that arrive after the
+        # DELETED event (an in-flight request's window); the oldest entries are dropped, so a
+        # worker that sees every placeholder ever created does not keep them all
+        self.deleted: "OrderedDict[Key, str]" = OrderedDict()
         self._cond: Optional[asyncio.Condition] = None
         self._task: Optional[asyncio.Task] = None
         self._synced: Optional[asyncio.Event] = None
@@ -75,7 +79,7 @@ class PodInformer:
         for k, p in fresh.items():
             self._note(k, p["metadata"].get("resourceVersion", ""))
         for k in set(self.cache) - set(fresh):
-            self.deleted[k] = self.cache[k]["metadata"].get("uid", "")
+            self._forget(k, self.cache[k]["metadata"].get("uid", ""))
         self.cache = fresh
         self.rv = rv
         self.epoch += 1
@@ -123,7 +127,7 @@ class PodInformer:
                         self.cache.pop(key, None)
                         self._seen.pop(key, None)   # stale upserts: caught by `deleted`
                         self._pending.pop(key, None)
-                        self.deleted[key] = md.get("uid", "")
+                        self._forget(key, md.get("uid", ""))
                     elif key in self._pending and \
                             self._pending[key] != md.get("resourceVersion", ""):
                         pass        # older than our write-through: the cache is newer
@@ -151,6 +155,12 @@ class PodInformer:
                              self.label_selector, e, backoff)
                 await asyncio.sleep(backoff)
                 backoff = min(backoff * 2, 5.0)
+
+    def _forget(self, key: Key, uid: str) -> None:
+        self.deleted.pop(key, None)
+        self.deleted[key] = uid
+        while len(self.deleted) > DELETED_KEEP:
+            self.deleted.popitem(last=False)
 
     def _note(self, key: Key, rv: str) -> None:
         if rv:

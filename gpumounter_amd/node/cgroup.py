@@ -215,6 +215,17 @@ class DeviceRuleBackend(ABC):
         it is gone from here — a foreign veto does not make a grant of ours go away."""
         return self.allowed(cgdir)
 
+    def prune(self) -> int:
+        """Drop cached state of cgroups that no longer exist (containers gone without a detach);
+        returns how many. Backends that cache nothing have nothing to drop."""
+        cache = getattr(self, "_installed", None)
+        if not cache:
+            return 0
+        gone = [d for d in cache if not os.path.isdir(d)]
+        for d in gone:
+            cache.pop(d, None)
+        return len(gone)
+
 
 class V1Backend(DeviceRuleBackend):
     name = "cgroup-v1"

@@ -191,6 +191,12 @@ class SystemdPersistingBackend(DeviceRuleBackend):
     def allowed(self, cgdir):
         return self.inner.allowed(cgdir)
 
+    def installed(self, cgdir):
+        return self.inner.installed(cgdir)
+
+    def prune(self):
+        return self.inner.prune()
+
     def sweep_pins(self, cgroup_root: str):
         sweep = getattr(self.inner, "sweep_pins", None)
         return sweep(cgroup_root) if sweep is not None else []

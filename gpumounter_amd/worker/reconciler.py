@@ -189,6 +189,7 @@ class Reconciler:
             await svc.lease.sweep()            # leases that expired while nobody watched
         except Exception as e:  # noqa: BLE001
             rep.errors.append(f"lease sweep: {e}")
+        svc.hm.backend.prune()
         m = svc.metrics
         # One authoritative PodResources read per sweep. It cross-checks the device-manager
         # checkpoint, and while that stays trusted every owner is audited from it (re-read

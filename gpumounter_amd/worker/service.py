@@ -22,6 +22,7 @@ import contextlib
 import json
 import secrets
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -153,8 +154,12 @@ class GpuMountService:
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
         #   two attaches' 1-GPU intents would be indistinguishable to the plugin.
         self._reserve_gate = _SharedExclusive()
-        self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}
+        # a pod's lock lives while a request holds or awaits it: no entry per pod ever seen
+        self._locks: "weakref.WeakValueDictionary[Tuple[str, str], asyncio.Lock]" = \
+            weakref.WeakValueDictionary()
         self._own: Dict[str, Tuple[str, ...]] = {}   # pod uid → its own device-plugin GPU IDs
+        if hasattr(node_pods, "handlers"):
+            node_pods.handlers.append(self._forget_pod)
         self.ledger_reads = 0
         self.ledger_reads_checkpoint = 0
         self.adopted = False           # adopt_existing() has run to completion
@@ -165,6 +170,18 @@ class GpuMountService:
         if lk is None:
             lk = self._locks[(ns, name)] = asyncio.Lock()
         return lk
+
+    def _forget_pod(self, etype: str, pod: dict) -> None:
+        """Drop per-pod caches of pods that left the node (a long-lived worker sees many)."""
+        if etype == "DELETED":
+            self._own.pop(podu.uid_of(pod), None)
+            forget = getattr(self.hm.resolver, "forget", None)
+            if forget is not None:
+                forget(podu.uid_of(pod))
+        elif etype == "RELIST":
+            live = {podu.uid_of(p) for p in self.node_pods.cache.values()}
+            for uid in [u for u in self._own if u not in live]:
+                del self._own[uid]
 
     def is_self(self, pod: dict) -> bool:
         """The worker's own pod (downward API POD_NAME/POD_NAMESPACE): it mounts the host's /dev,

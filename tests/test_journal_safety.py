@@ -274,3 +274,32 @@ def test_candidates_left_by_a_dead_pick_are_never_mounted_and_are_released():
         assert len(lc.cluster.placeholders()) == 1 and len(node_of(lc).allocated) == 1
         assert not await lc.audit("default", "t")
     run(body, worker_overrides={"reconcile_on_events": False})
+
+
+# ------------------------------------------------------------------------------ long-lived worker
+def test_per_pod_caches_do_not_grow_with_pods_that_left():
+    """A worker lives for the node's lifetime and sees many short-lived tenants: the per-pod
+    locks and own-GPU cache only hold pods that are still there."""
+    import gc
+
+    async def body(lc):
+        svc = lc.nodes["node-0"].worker.service
+        uids = set()
+        for i in range(6):
+            lc.tenant(f"t{i}")
+            uids.add(lc.cluster.get("default", f"t{i}")["metadata"]["uid"])
+            code, b = await lc.add("default", f"t{i}", 1)
+            assert code == 200
+            code, _ = await lc.remove("default", f"t{i}", [b["devices"][0]["uuid"]])
+            assert code == 200
+            assert any(k[0] in uids for k in svc.hm.resolver._cache)
+            lc.cluster.delete("default", f"t{i}", grace=0)
+        for _ in range(50):
+            await asyncio.sleep(0.02)
+            if not svc._own:
+                break
+        gc.collect()
+        assert not svc._own, svc._own
+        assert len(svc._locks) == 0, list(svc._locks)
+        assert not [k for k in svc.hm.resolver._cache if k[0] in uids]
+    run(body)

@@ -160,3 +160,35 @@ def test_attach_detach_on_systemd_driver_node_keeps_scope_device_allow_in_step()
     finally:
         fs.stop()
         shutil.rmtree(d, ignore_errors=True)
+
+
+def test_persisting_wrapper_forwards_every_backend_query():
+    """The wrapper must answer every DeviceRuleBackend query from the backend it wraps: the
+    base class's fallbacks (``installed`` = the effective verdict) would make the journal drop a
+    grant a foreign program vetoes, on exactly the nodes where the wrapper is on."""
+    import inspect
+
+    from gpumounter_amd.node.cgroup import DeviceRuleBackend
+    from gpumounter_amd.node.systemd import SystemdPersistingBackend
+
+    class Inner(DeviceRuleBackend):
+        name = "inner"
+
+        def apply(self, cgdir, grant, revoke, desired):
+            pass
+
+        def allowed(self, cgdir):
+            return set()                      # vetoed
+
+        def installed(self, cgdir):
+            return {(226, 128)}               # still ours
+
+        def prune(self):
+            return 7
+
+    w = SystemdPersistingBackend(Inner(), sync=None)
+    assert w.installed("/cg") == {(226, 128)} and w.allowed("/cg") == set() and w.prune() == 7
+    queries = {n for n, f in inspect.getmembers(DeviceRuleBackend, inspect.isfunction)
+               if not n.startswith("_")}
+    assert queries <= set(vars(SystemdPersistingBackend)), \
+        queries - set(vars(SystemdPersistingBackend))
