@@ -170,6 +170,11 @@ def main() -> int:
                          "tenant in its own mount namespace (gpumounter_amd/fakes/realnode.py); "
                          "emulated: the JSON-recording cgroup-v2 backend and marker files, for "
                          "unprivileged boxes")
+    ap.add_argument("--kernel-fs", choices=("tmpfs", "disk"), default="tmpfs",
+                    help="where the emulated node keeps its cgroupfs and container /dev trees: "
+                         "tmpfs (/dev/shm; a real node's are kernfs/tmpfs, in memory) or the "
+                         "working directory's disk. The worker's journal is on disk either way. "
+                         "The reference column uses the same choice")
     ap.add_argument("--security", choices=("shipped", "off"), default="shipped",
                     help="shipped: master⇄worker mTLS and TokenReview/SubjectAccessReview authz "
                          "as the manifests deploy them (--deploy processes); off: insecure gRPC, "
@@ -270,6 +275,7 @@ def main() -> int:
                                 gpu_bdfs=node_bdfs, protocol=args.protocol,
                                 secure=args.security == "shipped" and args.protocol == "gpumounter",
                                 gpu_api=args.gpu_api, log_dir=args.log_dir,
+                                kernel_fs=args.kernel_fs,
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
                                             "GM_PLACEMENT_ENFORCE": args.placement}).start()
             pc.tenant_pod = pc.tenant("tenant", pids={"main": [tenant_pid]})
@@ -282,6 +288,9 @@ def main() -> int:
             if sandbox is not None:
                 wov["bpf_pin_dir"] = sandbox.bpffs
                 kw = {"cgroup_root": sandbox.cgroup_root, "devnode_mode": "procroot"}
+            elif args.kernel_fs == "tmpfs" and os.access("/dev/shm", os.W_OK):
+                import tempfile
+                kw = {"kernel_fs_dir": tempfile.mkdtemp(prefix="gm-kfs-", dir="/dev/shm")}
             tc = ThreadedCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=lat,
                                  node_gpu_bdfs=node_bdfs, device_plugin=args.device_plugin,
                                  worker_overrides=wov, master_overrides={"gc_tune": True},
@@ -309,6 +318,7 @@ def main() -> int:
     bound_dev = [None]
     pool_cap = info.get("node_gpus", 0) if rank == 0 else 0
     attach_ms, detach_ms, audit_issues, probe_us, stage = [], [], 0, [], {}
+    dstage = {}          # detach: worker stage name → ms per timed detach
     hop_ms = []          # (master handler ms, worker ms) per timed attach
     ar_ms = []
     probe_by_gpu = {}
@@ -386,6 +396,8 @@ def main() -> int:
                 if st.get("master_ms") is not None and st.get("worker_ms") is not None:
                     hop_ms.append((st["master_ms"], st["worker_ms"]))
                 detach_ms.append((t1 - t0) * 1e3)
+                for t in (body.get("timings") or []) if isinstance(body, dict) else []:
+                    dstage.setdefault(t["name"], []).append(t["ms"])
                 if samples is not None:
                     samples.append({"t": round(time.time(), 4), "attach_ms": round(st["ms"], 4),
                                     "detach_ms": round((t1 - t0) * 1e3, 4),
@@ -500,7 +512,7 @@ def main() -> int:
                     from gpumounter_amd.fakes.deployment import ProcessCluster
                     rpc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup,
                                          gpu_bdfs=node_bdfs, protocol="reference",
-                                         kubelet_limit="count").start()
+                                         kubelet_limit="count", kernel_fs=args.kernel_fs).start()
                     rpc.tenant("tenant", pids={"main": [sleeper.pid]})
                     cp = ref_cp = _ProcCP(rpc)
                 ra, rd = [], []
@@ -544,6 +556,7 @@ def main() -> int:
                 # which node operations ran: "emulated" = JSON-recording cgroup-v2 backend +
                 # marker files (unprivileged box), "real" = bpf(2) + mknodat on this kernel
                 "node_ops": args.node_ops,
+                "node_fs": "real" if args.node_ops == "real" else args.kernel_fs,
                 "config": {
                     "model": f"gpumounter-amd {args.mode}-mount, {n} MI355X per Pod",
                     "global_batch": 1, "seq_len": None, "gpus_per_pod": n,
@@ -576,6 +589,8 @@ def main() -> int:
                 "detach_p99_ms": round(pct(detach_ms, 0.99), 4),
                 "stage_p50_ms": {k: round(statistics.median(v), 4) for k, v in sorted(stage.items())},
                 "stage_p99_ms": {k: round(pct(v, 0.99), 4) for k, v in sorted(stage.items())},
+                "detach_stage_p50_ms": {k: round(statistics.median(v), 4)
+                                        for k, v in sorted(dstage.items())},
                 "probe_quick_p50_us": round(statistics.median(probe_us), 2) if probe_us else None,
                 "probe_gpus_verified": len(probe_by_gpu) if world == 1 else None,
                 "probe_quick_p50_us_by_gpu": {b: round(statistics.median(v), 2)

@@ -71,7 +71,7 @@ async def run(args) -> None:
                       workdir=args.workdir, start_master=False, start_workers=False,
                       node_gpu_bdfs=[b for b in args.gpu_bdfs.split(",") if b] or None,
                       kubelet_limit_mode=args.kubelet_limit, gpu_api=args.gpu_api,
-                      app_hook=_hooks(ref))
+                      app_hook=_hooks(ref), kernel_fs_dir=args.kernel_fs_dir)
     ref[0] = lc
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
@@ -105,6 +105,8 @@ def main(argv=None) -> int:
     ap.add_argument("--workdir", required=True)
     ap.add_argument("--info", required=True)
     ap.add_argument("--nodes", type=int, default=1)
+    ap.add_argument("--kernel-fs-dir", default="",
+                    help="directory (a tmpfs) for the emulated cgroupfs and /dev trees")
     ap.add_argument("--amdsmi", default="mock")
     ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
     ap.add_argument("--latency", choices=("zero", "realistic"), default="zero")

@@ -52,12 +52,15 @@ class ProcessCluster:
                  worker_env: Optional[Dict[str, str]] = None,
                  master_env: Optional[Dict[str, str]] = None, log_dir: str = "",
                  protocol: str = "gpumounter", kubelet_limit: str = "enforce",
-                 secure: Optional[bool] = None, gpu_api: str = "device-plugin") -> None:
+                 secure: Optional[bool] = None, gpu_api: str = "device-plugin",
+                 kernel_fs: str = "disk") -> None:
         """``protocol="reference"`` runs worker and master with the reference's call sequence
         (gpumounter_amd/fakes/refproto.py) in the same deployment shape, for comparison; it is
         insecure like the reference unless ``secure`` says otherwise.
         ``kubelet_limit="count"`` serves PodResources calls over the kubelet's rate budget and
-        only counts them (see :class:`FakeKubelet`)."""
+        only counts them (see :class:`FakeKubelet`).
+        ``kernel_fs="tmpfs"`` keeps the emulated cgroupfs and /dev trees on ``/dev/shm`` (see
+        :class:`FakeNode`), when it is a writable tmpfs."""
         self.n_nodes = n_nodes
         self.secure = protocol == "gpumounter" if secure is None else secure
         self.token = "gm-hermetic-client-token" if self.secure else ""
@@ -73,6 +76,9 @@ class ProcessCluster:
         self.worker_env = worker_env or {}
         self.master_env = master_env or {}
         self.workdir = tempfile.mkdtemp(prefix="gm-deploy-")
+        self.kernel_fs_dir = ""
+        if kernel_fs == "tmpfs" and os.access("/dev/shm", os.W_OK):
+            self.kernel_fs_dir = tempfile.mkdtemp(prefix="gm-kfs-", dir="/dev/shm")
         self.log_dir = log_dir or self.workdir
         os.makedirs(self.log_dir, exist_ok=True)
         self.procs: Dict[str, subprocess.Popen] = {}
@@ -150,7 +156,8 @@ class ProcessCluster:
                                      "--cgroup", self.cgroup_mode, "--latency", self.latency,
                                      "--kubelet-limit", self.kubelet_limit,
                                      "--gpu-bdfs", ",".join(self.gpu_bdfs),
-                                     "--gpu-api", self.gpu_api], {})
+                                     "--gpu-api", self.gpu_api,
+                                     "--kernel-fs-dir", self.kernel_fs_dir], {})
         self._wait("control plane", lambda: os.path.exists(info_path))
         with open(info_path) as fh:
             self.info = json.load(fh)
@@ -258,6 +265,8 @@ class ProcessCluster:
                     p.wait(5)
             codes[key] = p.returncode
         shutil.rmtree(self.workdir, ignore_errors=True)
+        if self.kernel_fs_dir:
+            shutil.rmtree(self.kernel_fs_dir, ignore_errors=True)
         return codes
 
     def __enter__(self) -> "ProcessCluster":

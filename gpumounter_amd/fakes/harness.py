@@ -54,8 +54,10 @@ class LocalCluster:
                  kfd_major: int = 0, start_workers: bool = True,
                  kubelet_rate_limit: Optional[tuple] = (100.0, 10),
                  kubelet_limit_mode: str = "enforce", gpu_api: str = "device-plugin",
-                 app_hook: Optional[Callable[[web.Application], None]] = None) -> None:
+                 app_hook: Optional[Callable[[web.Application], None]] = None,
+                 kernel_fs_dir: str = "") -> None:
         self.n_nodes = n_nodes
+        self.kernel_fs_dir = kernel_fs_dir     # see FakeNode; removed by stop()
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
         self.cgroup_driver = cgroup_driver
@@ -127,7 +129,9 @@ class LocalCluster:
                         runtime=self.runtime, device_id_kind=self.device_id_kind,
                         alloc_policy=self.alloc_policy,
                         cgroup_root=os.path.join(self.real_cgroup_root, name)
-                        if self.real_cgroup_root else "")
+                        if self.real_cgroup_root else "",
+                        kernel_fs_dir=os.path.join(self.kernel_fs_dir, name)
+                        if self.kernel_fs_dir else "")
         if self.gpu_api == "dra":
             node.gpu_api = "dra"
             node.write_checkpoint = False    # the device manager does not see DRA devices
@@ -208,6 +212,8 @@ class LocalCluster:
             await self.api_runner.cleanup()
         if self._own_workdir:
             shutil.rmtree(self.workdir, ignore_errors=True)
+        if self.kernel_fs_dir:
+            shutil.rmtree(self.kernel_fs_dir, ignore_errors=True)
 
     async def __aenter__(self) -> "LocalCluster":
         return await self.start()

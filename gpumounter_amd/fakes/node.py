@@ -62,7 +62,7 @@ class FakeNode:
                  cgroup_mode: str = "v1", cgroup_driver: str = "cgroupfs",
                  runtime: str = "containerd", device_id_kind: str = "bdf",
                  alloc_policy: str = "first-free", labels: Optional[Dict[str, str]] = None,
-                 cgroup_root: str = "") -> None:
+                 cgroup_root: str = "", kernel_fs_dir: str = "") -> None:
         self.name = name
         self.resource = resource
         self.gpus = list(gpus)
@@ -78,18 +78,23 @@ class FakeNode:
         self.labels = {"kubernetes.io/hostname": name, "gpu-mounter-enable": "enable"}
         self.labels.update(labels or {})
         self.workdir = workdir
+        # kernel_fs_dir: where the trees a real node keeps in memory live — cgroupfs (kernfs),
+        # each container's /dev and the host's /dev (tmpfs/devtmpfs). A tmpfs there (bench.py)
+        # gives their emulation memory-speed file operations, as on a real node; the worker's
+        # own state (the journal, on disk on a real node) stays under ``workdir``.
+        kdir = kernel_fs_dir or workdir
         # cgroup_root given: a REAL cgroup2 mount (privileged tests) — directories are real
         # cgroups, cgroup.procs moves real processes, nothing else is written into it
         self.real_cgroups = bool(cgroup_root)
-        self.cgroup_root = cgroup_root or os.path.join(workdir, "cgroup")
-        self.rootfs_root = os.path.join(workdir, "rootfs")
+        self.cgroup_root = cgroup_root or os.path.join(kdir, "cgroup")
+        self.rootfs_root = os.path.join(kdir, "rootfs")
         os.makedirs(self.cgroup_root, exist_ok=True)
         os.makedirs(self.rootfs_root, exist_ok=True)
         # the worker's node-local state (injection journal) and the node's own /dev, holding an
         # (emulated) node for every GPU like a real host; containers that bind-mount the host's
         # /dev (hostPath /dev, privileged) see exactly this directory
         self.state_dir = os.path.join(workdir, "state")
-        self.host_root = os.path.join(workdir, "hostroot")
+        self.host_root = os.path.join(kdir, "hostroot")
         self.host_dev = os.path.join(self.host_root, "dev")
         self._populate_host_dev()
         if self.real_cgroups:
