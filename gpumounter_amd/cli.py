@@ -10,6 +10,7 @@
     python -m gpumounter_amd status --master URL --node NODE
     python -m gpumounter_amd bpf-dump --allow 226:128 --allow 511:0   # generated device program
     python -m gpumounter_amd doctor  [--json] [--skip-cluster] [--gpu [--burn-in 30]]  # preflight
+    python -m gpumounter_amd config-doc > docs/CONFIG.md   # every GM_* setting, from the source
 
 The reference ships only the two daemons and documents curl calls (QuickStart.md:41-92); the
 ``add``/``remove`` commands speak exactly those HTTP routes.
@@ -349,7 +350,15 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--allow", action="append", default=[])
     p.add_argument("--unchained", action="store_true")
     p.set_defaults(fn=cmd_bpf_dump)
+    p = sub.add_parser("config-doc")
+    p.set_defaults(fn=cmd_config_doc)
     return ap
+
+
+def cmd_config_doc(args) -> int:
+    from gpumounter_amd.utils.configdoc import render
+    sys.stdout.write(render())
+    return 0
 
 
 def main(argv: Optional[List[str]] = None) -> int:

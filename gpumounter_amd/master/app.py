@@ -491,8 +491,12 @@ class Master:
         stub = self.workers.channel(target).unary_unary(
             api.NODE_STATUS, request_serializer=api.NodeStatusRequest.SerializeToString,
             response_deserializer=api.NodeStatusResponse.FromString)
-        resp = await stub(api.NodeStatusRequest(
-            include_processes=request.query.get("processes") == "1"), timeout=30)
+        try:
+            resp = await stub(api.NodeStatusRequest(
+                include_processes=request.query.get("processes") == "1"), timeout=30)
+        except grpc.aio.AioRpcError as e:
+            return web.json_response({"error": f"worker on {node}: {e.code().name} "
+                                               f"{e.details()}"}, status=502)
         return web.json_response(json.loads(resp.json))
 
     async def pod_gpus(self, request: web.Request) -> web.Response:
@@ -504,13 +508,19 @@ class Master:
             pod = await self.kube.get_pod(ns, name)
         except NotFound:
             return web.json_response({"error": "pod not found"}, status=404)
+        except ApiError as e:
+            return web.json_response({"error": str(e)}, status=500)
         target = self.workers.target(podu.node_of(pod))
         if target is None:
             return web.json_response({"error": "no worker"}, status=500)
         stub = self.workers.channel(target).unary_unary(
             api.NODE_STATUS, request_serializer=api.NodeStatusRequest.SerializeToString,
             response_deserializer=api.NodeStatusResponse.FromString)
-        st = json.loads((await stub(api.NodeStatusRequest(), timeout=30)).json)
+        try:
+            st = json.loads((await stub(api.NodeStatusRequest(), timeout=30)).json)
+        except grpc.aio.AioRpcError as e:
+            return web.json_response({"error": f"worker on {podu.node_of(pod)}: "
+                                               f"{e.code().name} {e.details()}"}, status=502)
         uid = podu.uid_of(pod)
         held = {(p["namespace"], p["name"]) for p in st.get("placeholders", [])
                 if p["owner"] == name and p["owner_namespace"] == ns and p["owner_uid"] == uid}

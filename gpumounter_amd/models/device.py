@@ -107,6 +107,10 @@ class AmdGpu:
     def to_dict(self) -> Dict:
         d = asdict(self)
         d["state"] = self.state.value
+        # 64-bit ids as decimal strings, as the gRPC schema's JSON mapping renders uint64
+        # (Device.xgmi_hive_id): a JSON number that large loses digits in JS and jq
+        d["xgmi_hive_id"] = str(self.xgmi_hive_id)
+        d["xgmi_node_id"] = str(self.xgmi_node_id)
         return d
 
     def __str__(self) -> str:  # mirrors the reference's JSON String() (nvidia.go:43-50)

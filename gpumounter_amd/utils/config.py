@@ -22,49 +22,49 @@ import yaml
 @dataclass
 class Config:
     # --- network ---------------------------------------------------------------------------
-    master_host: str = "0.0.0.0"
-    master_port: int = 8080
-    worker_host: str = "0.0.0.0"
-    worker_port: int = 1200
-    metrics_port: int = 9400
+    master_host: str = "0.0.0.0"       # master HTTP API bind address
+    master_port: int = 8080            # master HTTP API (reference: main.go:237)
+    worker_host: str = "0.0.0.0"       # worker gRPC bind address
+    worker_port: int = 1200            # worker gRPC (reference: worker main.go:24)
+    metrics_port: int = 9400           # worker /metrics and /healthz
     # after start-up the daemon writes the ports it actually bound ({"grpc_port", "http_port"}
     # or {"port"}) here, atomically; with ports 0 (ephemeral) that is how a supervisor finds
     # them without racing another process for a pre-picked free port. "" = off
     ready_file: str = ""
     # --- kubernetes ------------------------------------------------------------------------
     kube_api: str = ""                 # "" → in-cluster; else http(s)://host:port (fake in tests)
-    kubeconfig: str = ""
-    kube_token: str = ""
-    kube_ca: str = ""
-    kube_insecure: bool = False
+    kubeconfig: str = ""               # kubeconfig file (out-of-cluster runs)
+    kube_token: str = ""               # bearer token for kube_api ("" = service account)
+    kube_ca: str = ""                  # CA bundle for kube_api ("" = service account CA)
+    kube_insecure: bool = False        # skip apiserver certificate checks (labs only)
     node_name: str = ""                # worker's node (downward API NODE_NAME)
     pod_name: str = ""                 # worker's own pod (downward API POD_NAME): never a target
     pod_namespace: str = ""            # (downward API POD_NAMESPACE)
-    worker_namespace: str = "kube-system"
-    worker_label: str = "app=gpu-mounter-worker"
-    pool_namespace: str = "gpu-pool"
+    worker_namespace: str = "kube-system"  # where the master looks for workers
+    worker_label: str = "app=gpu-mounter-worker"  # label selector of the worker pods
+    pool_namespace: str = "gpu-pool"   # placeholder namespace in "pool" mode
     # "pool": placeholders in pool_namespace (reference layout, allocator.go:198);
     # "tenant": placeholders next to the tenant pod, so the ownerReference is same-namespace and
     # Kubernetes ≥1.20 GC cleans them up (SURVEY §2.6 defect 4).
     placeholder_namespace_mode: str = "pool"
-    resource_name: str = "amd.com/gpu"
+    resource_name: str = "amd.com/gpu"  # extended resource placeholders request
     # how the cluster hands out GPUs: "device-plugin" (the amd.com/gpu extended resource of the
     # ROCm device plugin; the reference's model) or "dra" (a DRA driver publishes them in
     # ResourceSlices; placeholders then hold ResourceClaims pinned to the chosen devices)
     gpu_allocation: str = "device-plugin"
-    dra_driver: str = "gpu.amd.com"
-    dra_device_class: str = "gpu.amd.com"
+    dra_driver: str = "gpu.amd.com"    # DRA driver name in ResourceSlices
+    dra_device_class: str = "gpu.amd.com"  # DeviceClass placeholder claims request
     dra_bdf_attribute: str = "pciAddr"    # ResourceSlice device attribute holding the PCI BDF
-    placeholder_image: str = "registry.k8s.io/pause:3.9"
-    placeholder_pull_policy: str = "IfNotPresent"
-    placeholder_priority_class: str = ""
+    placeholder_image: str = "registry.k8s.io/pause:3.9"  # placeholder container image
+    placeholder_pull_policy: str = "IfNotPresent"  # no registry round trip per attach
+    placeholder_priority_class: str = ""  # PriorityClass of placeholders ("" = none)
     # Warm pool: standby placeholders that keep this many GPUs per node pre-admitted for
     # hot-mount (0 = off, the reference's behaviour). Claiming is a metadata patch, so attach
     # latency no longer includes scheduling + kubelet admission; the price is reserved capacity.
     warm_pool_size: int = 0
     # --- kubelet PodResources --------------------------------------------------------------
-    kubelet_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
-    kubelet_timeout_s: float = 10.0
+    kubelet_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"  # PodResources API
+    kubelet_timeout_s: float = 10.0    # per PodResources call (reference: types.go:7)
     podresources_api: str = "auto"     # auto | v1 | v1alpha1
     # client-side pacing of PodResources calls, under the kubelet's own limiter (100 qps,
     # burst 10, RESOURCE_EXHAUSTED beyond it) which other node agents share; 0 = unpaced
@@ -73,11 +73,12 @@ class Config:
     # (by pod UID, inotify-woken, no RPC: node/checkpoint.py) with PodResources as fallback and
     # authority; "podresources" = always the RPC
     ledger_source: str = "auto"
+    # the device manager's checkpoint file that ledger_source=auto reads
     kubelet_checkpoint: str = "/var/lib/kubelet/device-plugins/kubelet_internal_checkpoint"
-    kubelet_burst: int = 8
+    kubelet_burst: int = 8             # burst of the client-side PodResources pacing
     # --- device & isolation ----------------------------------------------------------------
     amdsmi_lib: str = ""               # "" → libamd_smi.so from ROCm; "mock" → bundled mock
-    cgroup_root: str = "/sys/fs/cgroup"
+    cgroup_root: str = "/sys/fs/cgroup"  # host cgroup mount as the worker sees it
     cgroup_mode: str = "auto"          # auto | v1 | v2
     cgroup_driver: str = "auto"        # auto | cgroupfs | systemd
     # record hot-mounted nodes in the container scope's DeviceAllow= so systemd keeps them when
@@ -94,7 +95,7 @@ class Config:
     # (every container) | off (always mknod)
     devnode_userns: str = "auto"
     devnode_stage_dir: str = "/run/gpumounter/devstage"  # worker-private tmpfs for bind mode
-    proc_root: str = "/proc"
+    proc_root: str = "/proc"           # host /proc (the DaemonSet runs with hostPID)
     # For hermetic runs: containers' rootfs live at <container_root_prefix>/<container-id>/ and
     # device-node writes go there instead of /proc/<pid>/root.
     container_root_prefix: str = ""
@@ -105,9 +106,9 @@ class Config:
     # in any container directory that *is* this /dev or its dri/ (hostPath or privileged /dev);
     # "" = no guard
     host_dev_path: str = "/proc/1/root/dev"
-    drm_major: int = 226
+    drm_major: int = 226               # /dev/dri/* character-device major
     kfd_major: int = 0                 # 0 → read /sys/class/kfd/kfd/dev (fallback 511)
-    kfd_dev_path: str = "/sys/class/kfd/kfd/dev"
+    kfd_dev_path: str = "/sys/class/kfd/kfd/dev"  # sysfs file holding the KFD major:minor
     inject_card_nodes: bool = True     # also inject /dev/dri/card<N> (rocm-smi reads it)
     device_file_mode: int = 0o666      # reference: nvidia.go:39 "666"
     # --- policy ----------------------------------------------------------------------------
@@ -121,7 +122,7 @@ class Config:
     # hint: the preferred set is only an annotation (no shipped device plugin reads it)
     placement_enforce: str = "auto"
     ledger_get: bool = True            # read admitted placeholders with PodResources v1 Get
-    reconcile_on_events: bool = True
+    reconcile_on_events: bool = True   # react to placeholder/tenant deletes at once
     # auto: fd scan of the container's PIDs, amdsmi only for PIDs whose fd table is unreadable;
     # both: always union with amdsmi's process table
     busy_detection: str = "auto"
@@ -131,14 +132,14 @@ class Config:
     # Events/annotations are sent once the worker has had no attach/detach in flight for
     # notify_idle_ms (so they never compete with a request), but at most notify_max_delay_ms late
     notify_idle_ms: float = 2.0
-    notify_max_delay_ms: float = 1000.0
+    notify_max_delay_ms: float = 1000.0  # upper bound on that delay
     # serve amd.com/gpu ourselves (replaces the ROCm device plugin on the node) so
     # GetPreferredAllocation steers placeholders to the topology-chosen GPUs
     device_plugin: bool = False
-    device_plugin_dir: str = "/var/lib/kubelet/device-plugins"
+    device_plugin_dir: str = "/var/lib/kubelet/device-plugins"  # kubelet registration dir
     device_plugin_inject: bool = True     # False: no device specs (kind / mock inventory)
     device_plugin_health_s: float = 5.0   # react to foreign placeholder / owner deletes at once
-    max_gpus_per_request: int = 64
+    max_gpus_per_request: int = 64     # addgpu gpuNum upper bound
     # GPUs with uncorrectable memory errors are left out of placement and reported Unhealthy by
     # the device plugin: new (errors since the worker started) | any (any on record) | off
     ecc_policy: str = "new"
@@ -146,7 +147,7 @@ class Config:
     # leases (?lease=<s> on addgpu): detach at expiry; GPUs still in use are kept and retried
     # unless lease_force, which signals their processes like force=1
     lease_force: bool = False
-    lease_retry_s: float = 30.0
+    lease_retry_s: float = 30.0        # retry period for an expired lease whose GPUs are busy
     # read the device rules and nodes back after each attach (span "verify": one native
     # read-back of every node plus the kernel's rule set per container) and roll back if
     # anything did not take effect; off = rely on the reconciler's periodic audit
@@ -160,11 +161,11 @@ class Config:
     # booked (draining placeholder) until they have, however long that takes
     kill_reap_s: float = 2.0
     # --- timeouts / loops ------------------------------------------------------------------
-    attach_timeout_s: float = 120.0
-    detach_timeout_s: float = 60.0
-    rpc_timeout_s: float = 180.0
-    reconcile_period_s: float = 30.0
-    watch_resync_s: float = 300.0
+    attach_timeout_s: float = 120.0    # placeholder admission deadline
+    detach_timeout_s: float = 60.0     # wait for placeholder deletion where waited for
+    rpc_timeout_s: float = 180.0       # master→worker gRPC deadline (reference: none)
+    reconcile_period_s: float = 30.0   # full reconciler sweep period
+    watch_resync_s: float = 300.0      # server-side timeout of one watch request
     api_token: str = ""                # if set, add/remove require "Authorization: Bearer <token>"
     # kube: the caller's own token, TokenReview + SubjectAccessReview on pods/gpumount (default);
     # none: open like the reference (SURVEY defect 13) unless api_token is set — opt-in only
@@ -172,8 +173,8 @@ class Config:
     # master⇄worker gRPC TLS (reference: insecure, main.go:82). cert+key on the worker enable TLS;
     # a CA on the worker requires client certs (mTLS). The master uses the same three files.
     tls_cert: str = ""
-    tls_key: str = ""
-    tls_ca: str = ""
+    tls_key: str = ""                  # private key of tls_cert
+    tls_ca: str = ""                   # CA that signs peers (worker: requires client certs)
     tls_server_name: str = "gpu-mounter-worker"  # SAN the worker certificate carries
     # identities (certificate SAN DNS names or CN) the worker accepts RPCs from under mTLS;
     # "" = any certificate the CA signed
@@ -181,12 +182,12 @@ class Config:
     # the worker refuses to serve its gRPC API (which can kill tenant processes) without mTLS
     # unless this is set explicitly (hermetic tests, lab clusters)
     worker_insecure: bool = False
-    metrics_period_s: float = 15.0
+    metrics_period_s: float = 15.0     # refresh of the per-GPU process and ledger gauges
     # --- observability ---------------------------------------------------------------------
-    log_level: str = "INFO"
-    log_file: str = ""
-    log_json: bool = True
-    roctx: bool = True
+    log_level: str = "INFO"            # DEBUG | INFO | WARNING | ERROR
+    log_file: str = ""                 # also log to this file, rotated ("" = stderr only)
+    log_json: bool = True              # one JSON object per line, with request ids
+    roctx: bool = True                 # roctx ranges per stage (rocprofv3 --marker-trace)
     fault: str = ""                    # fault injection: "stage:prob[,stage:prob]"
     extra: Dict[str, Any] = field(default_factory=dict)
 

@@ -198,3 +198,18 @@ def test_cluster_role_grants_every_api_call_the_daemons_make():
                for r in rule.get("resources", []) for v in rule.get("verbs", [])}
     missing = {n: need for n, need in needs.items() if need not in granted}
     assert not missing, missing
+
+
+def test_config_reference_is_current_and_documents_every_setting():
+    """docs/CONFIG.md is generated from config.py (every field, its GM_ variable, default and
+    comment); a field added without a comment, or a stale copy, fails here."""
+    from gpumounter_amd.utils.configdoc import render
+
+    text = render()
+    with open(os.path.join(ROOT, "docs", "CONFIG.md")) as fh:
+        assert fh.read() == text, "regenerate: python -m gpumounter_amd config-doc > docs/CONFIG.md"
+    rows = [ln for ln in text.splitlines() if ln.startswith("| `GM_")]
+    assert len(rows) == len(Config.__dataclass_fields__) - 1          # all but `extra`
+    assert not [r for r in rows if r.endswith("|  |")], "fields without a comment"
+    assert "| `GM_PLACEMENT_ENFORCE` | `auto` |" in text
+    assert "| `GM_DEVICE_FILE_MODE` | `0666` |" in text

@@ -917,3 +917,16 @@ def test_entire_mount_correction_takes_part_of_the_admitted_set_back():
         code, _ = await lc.remove("default", "t", [d["uuid"] for d in c["devices"]])
         assert code == 200 and len(node_of(lc).allocated) == 5
     run(body, alloc_policy="first-free")
+
+
+def test_status_endpoints_answer_json_when_the_worker_is_down():
+    async def body(lc):
+        lc.tenant("m")
+        target = lc.master.workers.target("node-0")
+        await lc.stop_worker("node-0")
+        lc.master.workers.target = lambda node: target      # the directory has not caught up
+        async with lc.session.get(lc.master_url + "/api/v1/nodes/node-0/gpus") as r:
+            assert r.status == 502 and "worker on node-0" in (await r.json())["error"]
+        async with lc.session.get(lc.master_url + "/api/v1/namespaces/default/pods/m/gpus") as r:
+            assert r.status == 502 and "UNAVAILABLE" in (await r.json())["error"]
+    run(body)
