@@ -351,13 +351,14 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--unchained", action="store_true")
     p.set_defaults(fn=cmd_bpf_dump)
     p = sub.add_parser("config-doc")
+    p.add_argument("--metrics", action="store_true", help="the metrics reference instead")
     p.set_defaults(fn=cmd_config_doc)
     return ap
 
 
 def cmd_config_doc(args) -> int:
-    from gpumounter_amd.utils.configdoc import render
-    sys.stdout.write(render())
+    from gpumounter_amd.utils.configdoc import render, render_metrics
+    sys.stdout.write(render_metrics() if args.metrics else render())
     return 0
 
 

@@ -1,10 +1,11 @@
-"""docs/CONFIG.md: every :class:`~gpumounter_amd.utils.config.Config` field with its environment
+"""docs/CONFIG.md and docs/METRICS.md: every :class:`~gpumounter_amd.utils.config.Config` field with its environment
 variable, default and the comment that documents it in ``config.py``.
 
 The reference reads one setting from the environment (``CGROUP_DRIVER``, reference:
 pkg/util/cgroup/cgroup.go:78-84) and hard-codes the rest; here every knob is a field, so the
 table is generated from the source and a test keeps the checked-in copy in step
-(``python -m gpumounter_amd config-doc > docs/CONFIG.md``).
+(``python -m gpumounter_amd config-doc > docs/CONFIG.md``). The reference exports no metrics;
+:func:`render_metrics` lists ours from the registry itself (``config-doc --metrics``).
 """
 from __future__ import annotations
 
@@ -99,4 +100,28 @@ def render() -> str:
             out += ["", f"## {sec}", "", "| variable | default | meaning |", "|---|---|---|"]
         out.append(f"| `GM_{f.name.upper()}` | `{_cell(_default(f))}` | "
                    f"{_cell(docs.get(f.name, ''))} |")
+    return "\n".join(out) + "\n"
+
+
+def render_metrics() -> str:
+    from gpumounter_amd.utils.metrics import Metrics
+
+    out = ["# Metrics reference",
+           "",
+           "Generated from `gpumounter_amd/utils/metrics.py` by",
+           "`python -m gpumounter_amd config-doc --metrics`; `tests/test_deploy_and_cli.py` checks",
+           "that this file is current.",
+           "",
+           "Workers serve these on `:9400/metrics` (`GM_METRICS_PORT`), the master on",
+           "`/metrics` of its HTTP port. Histograms are in seconds, with buckets from 0.5 ms to",
+           "120 s. Counters carry the `_total` suffix on the wire.",
+           "",
+           "| metric | type | labels | meaning |",
+           "|---|---|---|---|"]
+    for c in vars(Metrics()).values():
+        if not hasattr(c, "_documentation"):
+            continue
+        name = c._name + ("_total" if c._type == "counter" else "")
+        labels = ", ".join(f"`{x}`" for x in c._labelnames) or "—"
+        out.append(f"| `{name}` | {c._type} | {labels} | {_cell(c._documentation)} |")
     return "\n".join(out) + "\n"

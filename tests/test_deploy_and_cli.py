@@ -213,3 +213,14 @@ def test_config_reference_is_current_and_documents_every_setting():
     assert not [r for r in rows if r.endswith("|  |")], "fields without a comment"
     assert "| `GM_PLACEMENT_ENFORCE` | `auto` |" in text
     assert "| `GM_DEVICE_FILE_MODE` | `0666` |" in text
+
+
+def test_metrics_reference_is_current():
+    from gpumounter_amd.utils.configdoc import render_metrics
+
+    text = render_metrics()
+    with open(os.path.join(ROOT, "docs", "METRICS.md")) as fh:
+        assert fh.read() == text, \
+            "regenerate: python -m gpumounter_amd config-doc --metrics > docs/METRICS.md"
+    assert "| `gm_attach_latency_seconds` | histogram | `n_gpus`, `mode` |" in text
+    assert "`gm_draining_placeholders`" in text and "`gm_requests_total`" in text
