@@ -116,6 +116,12 @@ def render_metrics() -> str:
            "`/metrics` of its HTTP port. Histograms are in seconds, with buckets from 0.5 ms to",
            "120 s. Counters carry the `_total` suffix on the wire.",
            "",
+           "`gm_requests_total{result}` holds the reference's result names for answered RPCs",
+           "(`Success`, `InsufficientGPU`, `PodNotFound`, `GPUBusy`, `GPUNotFound`) and the gRPC",
+           "status for failed ones: `INTERNAL` (rolled back), `RESOURCE_EXHAUSTED` (quota),",
+           "`FAILED_PRECONDITION` (mount-type refusal). Alert rules on these metrics:",
+           "`deploy/monitoring/prometheus-rules.yaml` (Prometheus Operator).",
+           "",
            "| metric | type | labels | meaning |",
            "|---|---|---|---|"]
     for c in vars(Metrics()).values():

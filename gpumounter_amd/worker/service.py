@@ -376,6 +376,12 @@ class GpuMountService:
 
     SLOW_ATTACH_MS = 50.0
 
+    def _count_error(self, op: str, e: BaseException) -> None:
+        """RPCs that end in a gRPC error count under its status name (RESOURCE_EXHAUSTED = quota,
+        FAILED_PRECONDITION = mount-type refusal, INTERNAL = a failed and rolled-back operation)."""
+        code = e.code.name if isinstance(e, RpcError) else "INTERNAL"
+        self.metrics.requests.labels(op=op, result=code).inc()
+
     @staticmethod
     def _timings(root: trace.Span) -> List:
         return [api.StageTiming(name=k, ms=v) for k, v in root.flat().items()]
@@ -386,7 +392,11 @@ class GpuMountService:
         with self.notify.operation(), log.with_rid(rid), \
                 trace.span("attach", pod=f"{req.namespace}/{req.pod_name}",
                            n=req.gpu_num, entire=req.is_entire_mount) as root:
-            resp = await self._add_gpu(req)
+            try:
+                resp = await self._add_gpu(req)
+            except Exception as e:
+                self._count_error("add", e)
+                raise
         resp.total_ms = root.duration_ms
         resp.timings.extend(self._timings(root))
         if root.duration_ms > self.SLOW_ATTACH_MS:
@@ -827,7 +837,11 @@ class GpuMountService:
         with self.notify.operation(), log.with_rid(rid), \
                 trace.span("detach", pod=f"{req.namespace}/{req.pod_name}",
                            n=len(req.uuids), force=req.force) as root:
-            resp = await self._remove_gpu(req)
+            try:
+                resp = await self._remove_gpu(req)
+            except Exception as e:
+                self._count_error("remove", e)
+                raise
         resp.total_ms = root.duration_ms
         resp.timings.extend(self._timings(root))
         result = api.RemoveGPUResponse.RemoveGPUResult.Name(resp.remove_gpu_result)

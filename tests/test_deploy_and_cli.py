@@ -224,3 +224,21 @@ def test_metrics_reference_is_current():
             "regenerate: python -m gpumounter_amd config-doc --metrics > docs/METRICS.md"
     assert "| `gm_attach_latency_seconds` | histogram | `n_gpus`, `mode` |" in text
     assert "`gm_draining_placeholders`" in text and "`gm_requests_total`" in text
+
+
+def test_alert_rules_use_existing_metrics():
+    import re
+
+    from gpumounter_amd.utils.metrics import Metrics
+
+    (rule,) = load("monitoring/prometheus-rules.yaml")
+    names = set()
+    for c in vars(Metrics()).values():
+        if hasattr(c, "_documentation"):
+            base = c._name
+            names |= {base, base + "_total", base + "_bucket", base + "_sum", base + "_count"}
+    used = {m for g in rule["spec"]["groups"] for r in g["rules"]
+            for m in re.findall(r"\bgm_[a-z_]+", r["expr"])}
+    assert used and used <= names, used - names
+    with open(os.path.join(ROOT, "deploy", "kustomization.yaml")) as fh:
+        assert "monitoring" not in fh.read()          # needs the operator's CRDs: opt-in

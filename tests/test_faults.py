@@ -138,3 +138,22 @@ def test_placement_correction_fault_keeps_a_valid_attach(mode):
             assert len(lc.nodes["node-0"].node.allocated) == 5
             await _consistent(lc, "t", only_tenant=False)
     asyncio.run(main())
+
+
+def test_failed_rpcs_are_counted_by_grpc_status():
+    """gm_requests_total counts failures too (deploy/monitoring alerts on INTERNAL): a rolled-back
+    attach under its status name, next to the reference's result enum for answered ones."""
+    async def main():
+        async with LocalCluster() as lc:
+            lc.tenant("f")
+            w = lc.nodes["node-0"].worker
+            w.faults.rules = {"devnodes": Rule(1.0, "raise")}
+            code, _ = await lc.add("default", "f", 1)
+            w.faults.rules = {}
+            assert code == 500
+            code, b = await lc.add("default", "f", 1)
+            assert code == 200
+            m = w.service.metrics.requests
+            assert m.labels(op="add", result="INTERNAL")._value.get() == 1
+            assert m.labels(op="add", result="Success")._value.get() == 1
+    asyncio.run(main())
