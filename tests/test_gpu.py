@@ -344,8 +344,9 @@ def test_busy_detection_with_real_hip_process(real_inventory):
 
 
 def test_tenant_validate_tool_runs_kernel_p2p_and_rccl():
-    """``python -m gpumounter_amd.parallel.validate``: liveness kernel on every visible GPU,
-    pairwise peer copies, and an RCCL all-reduce with one process per GPU."""
+    """``python -m gpumounter_amd.parallel.validate``: liveness kernel and fp8 MX tile on every
+    visible GPU, pairwise peer copies, an RCCL all-reduce with one process per GPU, and the
+    bf16 + fp8/fp4 burn-in."""
     import json
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -356,7 +357,11 @@ def test_tenant_validate_tool_runs_kernel_p2p_and_rccl():
     rep = json.loads(res.stdout.strip().splitlines()[-1])
     assert rep["ok"] and rep["gpus"] and all(g["arch"].startswith("gfx950") for g in rep["gpus"])
     assert rep["allreduce"]["world"] == len(rep["gpus"]) and rep["allreduce"]["ok"]
-    assert len(rep["burn_in"]) == len(rep["gpus"]) and all(b["ok"] for b in rep["burn_in"])
+    # per GPU: the bf16 GEMM burn-in, then the fp8 and fp4 MX pipes
+    assert len(rep["burn_in"]) == 3 * len(rep["gpus"]) and all(b["ok"] for b in rep["burn_in"])
+    assert sorted(b.get("fmt", "bf16") for b in rep["burn_in"]) == \
+        sorted(["bf16", "fp8", "fp4"] * len(rep["gpus"]))
+    assert all(g["mx_fp8_tile_ok"] for g in rep["gpus"])
     print(json.dumps(rep["allreduce"]))
 
 
