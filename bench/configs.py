@@ -9,6 +9,9 @@
   placement   placement quality on a fragmented node with a device plugin that ignores
               gpumounter's hint (the honest default of the fake): attaches compared with the
               best set the free GPUs allowed.
+  chaos       contention with faults injected at every mutating worker stage and the worker
+              SIGKILLed with requests in flight every few rounds (process deployment):
+              invariants after every round, and how long the node took to converge.
 
 The control plane is the hermetic fake (apiserver, scheduler, kubelet); node operations are the
 production ones (cgroup rule backends, device-node writer) in their unprivileged modes. Runs
@@ -275,6 +278,141 @@ def contention_processes(args) -> dict:
             "invariant_violations": len(problems), "violation_examples": problems[:5]}
 
 
+CHAOS_FAULTS = ("ledger_reserve:0.04,placeholder_wait:0.03,cgroup_rule:0.04,devnodes:0.04,"
+                "cgroup_rule:0.04:after,busy_check:0.03,unmount:0.04,ledger_release:0.04,"
+                "ledger_release:0.04:after")
+
+
+def chaos(args) -> dict:
+    """Contention under failure, against the deployment shape (ProcessCluster, mTLS + authz):
+    four Pods attach and detach concurrently over HTTP while the worker injects faults at every
+    mutating stage (GM_FAULT, before and after each side effect) and is SIGKILLed with requests
+    in flight every ``--kill-every`` rounds, then restarted. After every round, once the node
+    has converged, the invariants are read through the public APIs only:
+    * every Pod's audit is clean: the device rules and nodes in its containers are exactly its
+      ledger's hot-mounted GPUs (nothing leaked into a container, nothing missing);
+    * no GPU is hot-mounted twice, and the placeholders hold exactly the hot-mounted GPUs;
+    * a Pod whose requests all succeeded since the last check holds exactly what its client
+      attached and did not remove (a failed request may or may not have taken effect, so after
+      one the client re-reads its state from the ledger).
+    ``converge_ms`` is how long the node took to satisfy the first two after a round."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from gpumounter_amd.fakes.deployment import ProcessCluster
+    tenants = [f"x{i}" for i in range(4)]
+    rnds = {t: random.Random(args.seed * 17 + i) for i, t in enumerate(tenants)}
+    mine = {t: [] for t in tenants}
+    certain = {t: True for t in tenants}
+    ok = failed = kills = 0
+    problems, converge = [], []
+    env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": "0.5"}
+    with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env) as pc:
+        for t in tenants:
+            pc.tenant(t)
+
+        def op(t):
+            rnd = rnds[t]
+            try:
+                if mine[t] and rnd.random() < 0.5:
+                    groups = mine[t]
+                    pick = list(groups) if any(e for _, e in groups) else \
+                        rnd.sample(groups, rnd.randint(1, len(groups)))
+                    code, _ = pc.remove("default", t, [u for g, _ in pick for u in g], force=True)
+                    if code == 200:
+                        for g in pick:
+                            groups.remove(g)
+                    return t, code
+                n, entire = rnd.randint(1, 3), rnd.random() < 0.3
+                code, b = pc.add("default", t, n, entire=entire)
+                if code == 200:
+                    uu = [d["uuid"] for d in b["devices"]]
+                    mine[t].extend([(uu, True)] if entire else [([u], False) for u in uu])
+                return t, code
+            except Exception:  # noqa: BLE001 - the master's connection dropped mid-kill
+                return t, -1
+
+        def ledger(t):
+            code, g = pc.pod_gpus("default", t)
+            if code != 200:
+                return None
+            return sorted(x["uuid"] for x in g.get("gpus", []) if x.get("source") == "hot-mount")
+
+        why = [""]
+
+        def converged():
+            hot_all = []
+            for t in tenants:
+                hot = ledger(t)
+                if hot is None:
+                    why[0] = f"{t}: no ledger view"
+                    return False
+                issues = pc.audit("default", t)
+                if issues:
+                    why[0] = f"{t}: audit {issues[:3]}"
+                    return False
+                hot_all += hot
+            # every placeholder left must be bound and hold GPUs of the hot-mounted set: an
+            # unbound one (its attach died) would be admitted later and hand a Pod GPUs nobody
+            # asked for
+            phs = pc.placeholders()
+            held = sum(int(c.get("resources", {}).get("limits", {}).get("amd.com/gpu", 0))
+                       for p in phs for c in p["spec"]["containers"])
+            if len(hot_all) != len(set(hot_all)) or held != len(hot_all):
+                why[0] = (f"hot {sorted(hot_all)} vs placeholders holding {held}: "
+                          f"{[(p['metadata']['name'], (p['metadata'].get('annotations') or {}).get('gpumounter.amd.com/mount-mode'), p['status'].get('phase')) for p in phs]}")
+                return False
+            return True
+
+        with ThreadPoolExecutor(len(tenants)) as ex:
+            for rnd_i in range(args.rounds):
+                futs = [ex.submit(op, t) for t in tenants]
+                if args.kill_every and rnd_i % args.kill_every == args.kill_every - 1:
+                    time.sleep(random.Random(rnd_i).uniform(0.0, 0.004))
+                    pc.kill_worker("node-0")        # SIGKILL with requests in flight
+                    kills += 1
+                    results = [f.result() for f in futs]
+                    pc.restart_worker("node-0")
+                else:
+                    results = [f.result() for f in futs]
+                for t, code in results:
+                    ok += code == 200
+                    failed += code not in (200, 400, 403)   # 400/403 are answers, not failures
+                    if code not in (200, 400, 403):
+                        certain[t] = False
+                t0 = time.perf_counter()
+                while not converged():
+                    if time.perf_counter() - t0 > 20:
+                        problems.append(f"round {rnd_i}: not converged after 20 s: {why[0]}")
+                        break
+                    time.sleep(0.05)
+                converge.append((time.perf_counter() - t0) * 1e3)
+                for t in tenants:
+                    hot = ledger(t) or []
+                    want = sorted(u for grp, _ in mine[t] for u in grp)
+                    if certain[t] and hot != want:
+                        problems.append(f"round {rnd_i} {t}: ledger {hot} != attached {want}")
+                    if not certain[t]:
+                        # resynchronise the client from the ledger: single mounts per GPU (an
+                        # entire mount's GPUs are removed together; the ledger's mount type says)
+                        code, g = pc.pod_gpus("default", t)
+                        mine[t] = [([x["uuid"]], False) for x in g.get("gpus", [])
+                                   if x.get("source") == "hot-mount"]
+                        ph = {x.get("pod_name") for x in g.get("gpus", [])
+                              if x.get("source") == "hot-mount"}
+                        if len(ph) < len(mine[t]):      # fewer placeholders than GPUs: entire
+                            mine[t] = [([u for grp, _ in mine[t] for u in grp], True)]
+                        certain[t] = True
+        metrics = pc.worker_metrics()
+    injected = sum(float(ln.split()[-1]) for ln in metrics.splitlines()
+                   if ln.startswith("gm_requests_total{") and 'result="INTERNAL"' in ln)
+    return {"rounds": args.rounds, "worker_kills": kills, "ops_ok": ok,
+            "ops_failed": failed, "internal_errors_since_last_restart": injected,
+            "converge_p50_ms": round(pct(converge, 0.5), 1),
+            "converge_max_ms": round(max(converge), 1),
+            "invariant_violations": len(problems), "violation_examples": problems[:5],
+            "faults": CHAOS_FAULTS}
+
+
 async def placement(lc, args) -> dict:
     """Placement quality on a fragmented node, as a device plugin that ignores gpumounter's
     hint leaves it. Four background pods grow and shrink by single GPUs at random; between
@@ -333,7 +471,8 @@ async def placement(lc, args) -> dict:
             "audit_issues": sum([len(await lc.audit("default", t)) for t in bg + ["probe"]])}
 
 
-SCENARIOS = {"scale": scale, "contention": contention, "soak": soak, "placement": placement}
+SCENARIOS = {"scale": scale, "contention": contention, "soak": soak, "placement": placement,
+             "chaos": None}     # process deployment only (see chaos())
 
 
 def main() -> int:
@@ -353,6 +492,8 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--cycles", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--kill-every", type=int, default=10,
+                    help="chaos: SIGKILL the worker with requests in flight every N rounds")
     ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",
                     help="real (root, cgroup2): tenants are processes in their own mount "
                          "namespaces inside real cgroups with a runc-style device program; "
@@ -362,9 +503,16 @@ def main() -> int:
                          "(contention only)")
     args = ap.parse_args()
     log.setup("WARNING", json_format=False)
+    if args.scenario == "chaos":
+        res = chaos(args)
+        res["config"] = {"scenario": "chaos", "deploy": "processes",
+                         "amdsmi": args.amdsmi or "libamd_smi", "cgroup": args.cgroup,
+                         "latency": "zero", "security": "mTLS + TokenReview/SAR authz"}
+        print(json.dumps(res))
+        return 0
     if args.deploy == "processes":
         if args.scenario != "contention":
-            ap.error("--deploy processes runs the contention scenario only")
+            ap.error("--deploy processes runs the contention and chaos scenarios only")
         res = contention_processes(args)
         res["config"] = {"scenario": "contention", "deploy": "processes",
                          "amdsmi": args.amdsmi or "libamd_smi", "cgroup": args.cgroup,

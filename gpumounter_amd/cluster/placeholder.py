@@ -42,7 +42,7 @@ from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.cluster.quota import QuotaExceeded
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTAINER, ANN_GROUP,
-                                         ANN_IDEMPOTENCY,
+                                         ANN_IDEMPOTENCY, ANN_INCARNATION,
                                          ANN_MOUNT_MODE, ANN_OWNER_UID, ANN_PREFERRED, LABEL_APP,
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          SLAVE_SUFFIX)
@@ -136,6 +136,7 @@ class PlaceholderManager:
         # uids we deleted but the watch has not reported yet: excluded from every query, so a
         # released GPU is never seen as still attached (no need to wait for the DELETED event)
         self.tombstones: Dict[str, float] = {}
+        self.incarnation = secrets.token_hex(6)     # this process (ANN_INCARNATION)
         informer.handlers.append(self._on_event)
         self.last_ledger: Dict[Tuple[str, str], List[str]] = {}
         # called with the placeholder pod when something other than us deletes it (kubectl,
@@ -191,6 +192,7 @@ class PlaceholderManager:
                        LABEL_NODE: _label_value(self.node)},
             "annotations": {ANN_OWNER_UID: podu.uid_of(owner), ANN_MOUNT_MODE: mode,
                             ANN_ATTACH_ID: attach_id, ANN_CONTAINER: container,
+                            ANN_INCARNATION: self.incarnation,
                             "gpumounter.amd.com/owner-name": podu.name_of(owner)},
         }
         if preferred:

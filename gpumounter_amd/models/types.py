@@ -35,6 +35,9 @@ ANN_OWNER_UID = "gpumounter.amd.com/owner-uid"
 ANN_MOUNT_MODE = "gpumounter.amd.com/mount-mode"
 ANN_PREFERRED = "gpumounter.amd.com/preferred-devices"
 ANN_ATTACH_ID = "gpumounter.amd.com/attach-id"
+# the worker process that created a placeholder (random per start): a never-admitted placeholder
+# from another incarnation belongs to an attach whose worker died, so nothing waits for it
+ANN_INCARNATION = "gpumounter.amd.com/worker-incarnation"
 ANN_CONTAINER = "gpumounter.amd.com/container"
 ANN_DEVICES = "gpumounter.amd.com/devices"
 ANN_OWNER_NAME = "gpumounter.amd.com/owner-name"

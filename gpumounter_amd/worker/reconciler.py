@@ -30,11 +30,11 @@ from __future__ import annotations
 import asyncio
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List
+from typing import Dict, List, Optional
 
 from gpumounter_amd.cluster.kube import NotFound
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import ANN_CANDIDATE, ANN_OWNER_UID
+from gpumounter_amd.models.types import ANN_CANDIDATE, ANN_INCARNATION, ANN_OWNER_UID
 from gpumounter_amd.utils import log
 
 _log = log.get("worker.reconciler")
@@ -195,8 +195,9 @@ class Reconciler:
         # checkpoint, and while that stays trusted every owner is audited from it (re-read
         # under the owner's lock, no RPC). That is O(1) kubelet calls per sweep instead of one
         # per owner.
+        led: Optional[Dict[tuple, List[str]]] = None
         try:
-            await svc.read_ledger(authoritative=True)
+            led = await svc.read_ledger(authoritative=True)
         except Exception as e:  # noqa: BLE001
             rep.errors.append(f"ledger: {e}")
         if not svc.adopted:
@@ -258,11 +259,22 @@ class Reconciler:
                     await svc.ph.release([svc.ph.from_pod(p, {}) for p in cands], wait=False)
                     phs = [p for p in phs if p not in cands]
                     m.reconcile_actions.labels(action="candidate_release").inc(len(cands))
-                # stuck placeholders (never admitted)
+                # stuck placeholders (never admitted). One that an earlier worker process
+                # created and that the kubelet has not allocated devices to belongs to an
+                # attach that died with that worker: nothing waits for it, and if the scheduler
+                # admitted it later the reconciler would mount GPUs nobody asks for any more —
+                # released at once. (An admitted one may be a finished attach whose reply was
+                # sent: it stays, and is audited like any other.)
                 stuck = []
                 for p in phs:
                     name = p["metadata"]["name"]
-                    if podu.is_unschedulable(p) or podu.phase_of(p) == "Failed":
+                    ann = p["metadata"].get("annotations") or {}
+                    if led is not None and podu.phase_of(p) == "Pending" and \
+                            not led.get((p["metadata"]["namespace"], name)) and \
+                            ann.get(ANN_INCARNATION) != svc.ph.incarnation:
+                        stuck.append(p)
+                        m.reconcile_actions.labels(action="dead_attach_release").inc()
+                    elif podu.is_unschedulable(p) or podu.phase_of(p) == "Failed":
                         first = self._first_seen.setdefault(name, now)
                         if now - first >= self.stuck_after_s:
                             stuck.append(p)

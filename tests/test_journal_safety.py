@@ -303,3 +303,50 @@ def test_per_pod_caches_do_not_grow_with_pods_that_left():
         assert len(svc._locks) == 0, list(svc._locks)
         assert not [k for k in svc.hm.resolver._cache if k[0] in uids]
     run(body)
+
+
+# ------------------------------------------------------------------------------ dead attaches
+def test_unadmitted_placeholder_of_a_dead_worker_is_released_at_once():
+    """A worker SIGKILLed mid-attach leaves a placeholder the scheduler has not admitted (here:
+    the node is full). Nothing will ever wait for it, and if a GPU freed up later the reconciler
+    would mount it into a Pod whose request failed long ago: the next worker releases it on its
+    first sweep instead of after stuck_after_s. An admitted one from the dead worker may be a
+    finished attach whose reply went out; it stays and is mounted."""
+    async def body(lc):
+        for t in ("t", "filler"):
+            lc.tenant(t)
+        w = lc.nodes["node-0"].worker
+        svc = w.service
+        code, b = await lc.add("default", "t", 1)
+        assert code == 200
+        code, fb = await lc.add("default", "filler", 7)          # node full
+        assert code == 200
+        tenant = lc.cluster.get("default", "t")
+        ph = svc.ph
+
+        async def dead_worker_placeholder():
+            mine = ph.incarnation
+            ph.incarnation = "dead-worker"
+            body = ph.build(tenant, 1, "single", attach_id="rq-dead")
+            ph.incarnation = mine
+            await svc.kube.create_pod(body["metadata"]["namespace"], body)
+            await asyncio.sleep(0.1)
+            return body["metadata"]["namespace"], body["metadata"]["name"]
+
+        ns, name = await dead_worker_placeholder()
+        assert lc.cluster.get(ns, name)["status"]["phase"] == "Pending"
+        rep = await w.reconciler.run_once()
+        assert name in rep.stuck, rep
+        assert not any(p["metadata"]["name"] == name for p in lc.cluster.placeholders())
+        st = await svc.pod_state(tenant, fresh=True)
+        assert [g.uuid for g in st.hot] == [b["devices"][0]["uuid"]]
+        assert not await lc.audit("default", "t")
+        # a GPU is free: the dead worker's placeholder is admitted — kept, and mounted
+        code, _ = await lc.remove("default", "filler", [fb["devices"][0]["uuid"]])
+        assert code == 200
+        ns, name = await dead_worker_placeholder()
+        rep = await w.reconciler.run_once()
+        assert name not in rep.stuck and rep.repaired == ["default/t"], rep
+        st = await svc.pod_state(tenant, fresh=True)
+        assert len(st.hot) == 2 and not await lc.audit("default", "t")
+    run(body, worker_overrides={"reconcile_on_events": False})
