@@ -278,6 +278,18 @@ def contention_processes(args) -> dict:
             "invariant_violations": len(problems), "violation_examples": problems[:5]}
 
 
+def _gpus_held(p: dict) -> int:
+    """GPUs a bound placeholder holds: its amd.com/gpu limit, or (DRA) its claim's device count
+    (the gpumounter.amd.com/gpus annotation the claim was built from)."""
+    if not p["spec"].get("nodeName"):
+        return 0
+    lim = sum(int(c.get("resources", {}).get("limits", {}).get("amd.com/gpu", 0))
+              for c in p["spec"]["containers"])
+    if lim or not p["spec"].get("resourceClaims"):
+        return lim
+    return int((p["metadata"].get("annotations") or {}).get("gpumounter.amd.com/gpus", "0"))
+
+
 CHAOS_FAULTS = ("ledger_reserve:0.04,placeholder_wait:0.03,cgroup_rule:0.04,devnodes:0.04,"
                 "cgroup_rule:0.04:after,busy_check:0.03,unmount:0.04,ledger_release:0.04,"
                 "ledger_release:0.04:after")
@@ -305,8 +317,10 @@ def chaos(args) -> dict:
     certain = {t: True for t in tenants}
     ok = failed = kills = 0
     problems, converge = [], []
-    env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": "0.5"}
-    with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env) as pc:
+    env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": "0.5",
+           "GM_WARM_POOL_SIZE": str(args.warm_pool)}
+    with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
+                        gpu_api=args.gpu_api) as pc:
         for t in tenants:
             pc.tenant(t)
 
@@ -354,9 +368,14 @@ def chaos(args) -> dict:
             # every placeholder left must be bound and hold GPUs of the hot-mounted set: an
             # unbound one (its attach died) would be admitted later and hand a Pod GPUs nobody
             # asked for
-            phs = pc.placeholders()
-            held = sum(int(c.get("resources", {}).get("limits", {}).get("amd.com/gpu", 0))
-                       for p in phs for c in p["spec"]["containers"])
+            phs = [p for p in pc.placeholders()
+                   if (p["metadata"].get("annotations") or {}).get(
+                       "gpumounter.amd.com/mount-mode") != "standby"]     # warm pool
+            unbound = [p["metadata"]["name"] for p in phs if not p["spec"].get("nodeName")]
+            if unbound:
+                why[0] = f"unbound placeholders left: {unbound}"
+                return False
+            held = sum(_gpus_held(p) for p in phs)
             if len(hot_all) != len(set(hot_all)) or held != len(hot_all):
                 why[0] = (f"hot {sorted(hot_all)} vs placeholders holding {held}: "
                           f"{[(p['metadata']['name'], (p['metadata'].get('annotations') or {}).get('gpumounter.amd.com/mount-mode'), p['status'].get('phase')) for p in phs]}")
@@ -492,6 +511,8 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--cycles", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
+                    help="chaos: GPUs from the device plugin or from a DRA driver")
     ap.add_argument("--kill-every", type=int, default=10,
                     help="chaos: SIGKILL the worker with requests in flight every N rounds")
     ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",
@@ -507,6 +528,7 @@ def main() -> int:
         res = chaos(args)
         res["config"] = {"scenario": "chaos", "deploy": "processes",
                          "amdsmi": args.amdsmi or "libamd_smi", "cgroup": args.cgroup,
+                         "warm_pool": args.warm_pool, "gpu_allocation": args.gpu_api,
                          "latency": "zero", "security": "mTLS + TokenReview/SAR authz"}
         print(json.dumps(res))
         return 0
