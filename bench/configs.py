@@ -317,12 +317,15 @@ def chaos(args) -> dict:
     certain = {t: True for t in tenants}
     ok = failed = kills = 0
     problems, converge = [], []
+    api_faults = [0]
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": "0.5",
            "GM_WARM_POOL_SIZE": str(args.warm_pool)}
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
                         gpu_api=args.gpu_api) as pc:
         for t in tenants:
             pc.tenant(t)
+        if args.api_fault_rate:
+            pc.api_faults(args.api_fault_rate, args.seed)
 
         def op(t):
             rnd = rnds[t]
@@ -398,6 +401,8 @@ def chaos(args) -> dict:
                     failed += code not in (200, 400, 403)   # 400/403 are answers, not failures
                     if code not in (200, 400, 403):
                         certain[t] = False
+                if args.api_fault_rate:
+                    api_faults[0] += pc.api_faults(0)        # the checks read a healthy API
                 t0 = time.perf_counter()
                 while not converged():
                     if time.perf_counter() - t0 > 20:
@@ -421,6 +426,8 @@ def chaos(args) -> dict:
                         if len(ph) < len(mine[t]):      # fewer placeholders than GPUs: entire
                             mine[t] = [([u for grp, _ in mine[t] for u in grp], True)]
                         certain[t] = True
+                if args.api_fault_rate:
+                    pc.api_faults(args.api_fault_rate, args.seed * 1000 + rnd_i)
         metrics = pc.worker_metrics()
     injected = sum(float(ln.split()[-1]) for ln in metrics.splitlines()
                    if ln.startswith("gm_requests_total{") and 'result="INTERNAL"' in ln)
@@ -429,7 +436,8 @@ def chaos(args) -> dict:
             "converge_p50_ms": round(pct(converge, 0.5), 1),
             "converge_max_ms": round(max(converge), 1),
             "invariant_violations": len(problems), "violation_examples": problems[:5],
-            "faults": CHAOS_FAULTS}
+            "faults": CHAOS_FAULTS, "api_fault_rate": args.api_fault_rate,
+            "api_faults_served": api_faults[0]}
 
 
 async def placement(lc, args) -> dict:
@@ -513,6 +521,9 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
                     help="chaos: GPUs from the device plugin or from a DRA driver")
+    ap.add_argument("--api-fault-rate", type=float, default=0.0,
+                    help="chaos: Pod/ResourceClaim requests to the apiserver fail at random at "
+                         "this rate (500/503/429, half after taking effect)")
     ap.add_argument("--kill-every", type=int, default=10,
                     help="chaos: SIGKILL the worker with requests in flight every N rounds")
     ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",

@@ -155,6 +155,8 @@ class FakeCluster:
         self._tasks: set = set()
         self._lock = threading.RLock()
         self._faults: List[Tuple[str, int, bool, str]] = []
+        self._random_faults: Optional[Tuple[float, Any]] = None   # (rate, random.Random)
+        self.random_faults_served = 0
         from gpumounter_amd.fakes.dra import DraState
         self.dra = DraState(self)     # resource.k8s.io/v1 claims and slices (fakes/dra.py)
 
@@ -553,9 +555,27 @@ class FakeCluster:
         response (a dropped reply)."""
         self._faults.extend([(method, status, after, path)] * count)
 
+    def random_failures(self, rate: float, seed: int = 0) -> None:
+        """Fault injection at random: each Pod or ResourceClaim request (not watches) fails with
+        probability ``rate``: 500, 503 or 429, half of them after the request took effect
+        (a lost reply). ``rate=0`` turns it off."""
+        import random
+        self._random_faults = (rate, random.Random(seed)) if rate > 0 else None
+
     @web.middleware
     async def _fault_mw(self, request: web.Request, handler):
         """Serves the failures queued by :meth:`fail_next` (watch streams are never hit)."""
+        rf = self._random_faults
+        if rf is not None and not request.query.get("watch") and (
+                "/pods" in request.path or "/resourceclaims" in request.path):
+            rate, rnd = rf
+            if rnd.random() < rate:
+                self.random_faults_served += 1
+                st = rnd.choice((500, 503, 429))
+                if rnd.random() < 0.5:
+                    await handler(request)          # it happened; the reply gets lost
+                return web.json_response({"kind": "Status", "code": st,
+                                          "message": "injected failure"}, status=st)
         if self._faults and not request.query.get("watch"):
             for i, (m, st, after, path) in enumerate(self._faults):
                 if m == request.method and path in request.path:

@@ -11,6 +11,8 @@ Besides the Kubernetes API it serves these test hooks:
   ``POST /_fake/tenant``  {"name", "ns", "node", "gpus", "containers", "pids"} → a Running pod
   ``POST /_fake/worker``  {"node", "port"}  → the worker DaemonSet pod the master discovers
   ``GET  /_fake/kubelet``  → each node's PodResources call counters (served, rejected, over_limit)
+  ``POST /_fake/faults``  {"rate", "seed"} → Pod/ResourceClaim requests fail at random (500/503/
+                          429, half after taking effect); answers how many were served so far
   ``POST /_fake/user``    {"token", "user", "verbs", "resource", "namespaces"} → a bearer token
                           TokenReview accepts, and an RBAC rule SubjectAccessReview honours
 The info file lists the apiserver URL and each node's kubelet socket, cgroup root and rootfs root.
@@ -57,6 +59,13 @@ def _hooks(lc_ref: list):
                       b.get("resource", "pods/gpumount"), b.get("namespaces", ["*"]))
             return web.json_response({"ok": True}, status=201)
 
+        async def faults(req: web.Request) -> web.Response:
+            b = await req.json()
+            api = lc_ref[0].cluster
+            api.random_failures(float(b.get("rate", 0)), int(b.get("seed", 0)))
+            return web.json_response({"served": api.random_faults_served}, status=201)
+
+        app.router.add_post("/_fake/faults", faults)
         app.router.add_post("/_fake/tenant", tenant)
         app.router.add_post("/_fake/user", user)
         app.router.add_post("/_fake/worker", worker)

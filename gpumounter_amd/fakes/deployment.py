@@ -316,6 +316,16 @@ class ProcessCluster:
             raise RuntimeError(f"kubelet counters: {code}")
         return json.loads(body)[node]
 
+    def api_faults(self, rate: float, seed: int = 0) -> int:
+        """Random apiserver failures for Pod/ResourceClaim requests (fakes/apiserver.py
+        random_failures); returns how many were served before this call."""
+        code, body = _http("POST", f"{self.info['api_url']}/_fake/faults",
+                           json.dumps({"rate": rate, "seed": seed}).encode(),
+                           {"Content-Type": "application/json"})
+        if code != 201:
+            raise RuntimeError(f"fault setup: {code}")
+        return int(json.loads(body)["served"])
+
     def placeholders(self) -> List[dict]:
         code, body = _http("GET", f"{self.info['api_url']}/api/v1/pods?labelSelector=app%3Dgpu-pool")
         return json.loads(body).get("items", []) if code == 200 else []

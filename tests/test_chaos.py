@@ -1,6 +1,7 @@
 """bench/configs.py chaos, short: four Pods attaching and detaching over HTTP against the process
 deployment while the worker injects faults at every mutating stage and is SIGKILLed twice with
-requests in flight. The ledger invariants hold after every round (see chaos() for the list)."""
+requests in flight, and 5 % of the apiserver's Pod requests fail (some after taking effect).
+The ledger invariants hold after every round (see chaos() for the list)."""
 import json
 import os
 import subprocess
@@ -11,9 +12,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_chaos_keeps_the_ledger_invariants():
     res = subprocess.run([sys.executable, "bench/configs.py", "chaos", "--rounds", "8",
-                          "--kill-every", "4", "--seed", "1"], cwd=ROOT, capture_output=True,
+                          "--kill-every", "4", "--seed", "1", "--api-fault-rate", "0.05"], cwd=ROOT, capture_output=True,
                          text=True, timeout=600)
     assert res.returncode == 0, res.stderr[-3000:]
     out = json.loads(res.stdout.strip().splitlines()[-1])
-    assert out["worker_kills"] == 2 and out["ops_ok"] > 0
+    assert out["worker_kills"] == 2 and out["ops_ok"] > 0 and out["api_faults_served"] > 0
     assert out["invariant_violations"] == 0, out["violation_examples"]
