@@ -11,7 +11,7 @@ import asyncio
 from collections import OrderedDict, deque
 from typing import Callable, Dict, List, Optional, Tuple
 
-from gpumounter_amd.cluster.kube import ApiError, KubeClient
+from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models.pod import jcopy
 from gpumounter_amd.utils import log
 
@@ -48,6 +48,8 @@ class PodInformer:
         # key → resourceVersion of a write-through the watch has not delivered yet: until it
         # does, the watch's events for that key are older than the cached object
         self._pending: Dict[Key, str] = {}
+        self.resolved = 0        # objects re-read with a GET after a relist (see _relist)
+        self._bg: set = set()
         self.handlers: List[Callable[[str, dict], None]] = []
 
     async def start(self) -> None:
@@ -57,6 +59,8 @@ class PodInformer:
         await asyncio.wait_for(self._synced.wait(), timeout=30)
 
     async def stop(self) -> None:
+        for t in list(self._bg):
+            t.cancel()
         if self._task:
             self._task.cancel()
             try:
@@ -72,9 +76,39 @@ class PodInformer:
         return self.kube.watch_pods(self.namespace, self.label_selector, self.field_selector,
                                     self.rv, timeout_s=timeout_s)
 
+    def _get(self, ns: str, name: str):
+        return self.kube.get_pod(ns, name)
+
+    async def _fetch(self, key: Key) -> Optional[dict]:
+        """The object as the apiserver has it now (None: deleted)."""
+        try:
+            return await self._get(*key)
+        except NotFound:
+            return None
+
     async def _relist(self) -> None:
         items, rv = await self._list()
         fresh = {(p["metadata"]["namespace"], p["metadata"]["name"]): p for p in items}
+        # our acknowledged writes the watch had not echoed yet: where the list holds another
+        # version, it may be older than the write (the list was served before it) or newer —
+        # resourceVersions do not say which, a GET issued now does (it is newer than both)
+        suspects = [k for k, prv in self._pending.items()
+                    if k in fresh and fresh[k]["metadata"].get("resourceVersion") != prv]
+        if suspects:
+            got = await asyncio.gather(*[self._fetch(k) for k in suspects],
+                                       return_exceptions=True)
+            pending = {}
+            for k, obj in zip(suspects, got):
+                if isinstance(obj, BaseException):
+                    continue            # keep the listed version; the watch still converges
+                if obj is None:
+                    fresh.pop(k, None)
+                else:
+                    fresh[k] = obj
+                    pending[k] = obj["metadata"].get("resourceVersion", "")
+            self.resolved += len(suspects)
+        else:
+            pending = {}
         self._seen = {k: self._seen[k] for k in fresh if k in self._seen}
         for k, p in fresh.items():
             self._note(k, p["metadata"].get("resourceVersion", ""))
@@ -83,7 +117,9 @@ class PodInformer:
         self.cache = fresh
         self.rv = rv
         self.epoch += 1
-        self._pending.clear()
+        # a fetched version is newer than the list: the resumed watch's older events for
+        # that key are skipped until it delivers this version (see _run)
+        self._pending = {k: v for k, v in pending.items() if v}
         await self._notify("RELIST", {})
 
     async def _notify(self, etype: str, pod: dict) -> None:
@@ -189,12 +225,49 @@ class PodInformer:
         if epoch is not None and epoch != self.epoch:
             cur = self.cache.get(key)
             if cur is not None and cur["metadata"].get("uid") == md.get("uid"):
+                # the relist holds this object in some version, older or newer than our
+                # write: a GET decides (until it answers, readers see the listed version)
+                self._resolve_soon(key)
                 return
         if key in self.deleted and self.deleted[key] == md.get("uid"):
             return
         self.cache[key] = pod
         if rv:
             self._pending[key] = rv
+
+    def _resolve_soon(self, key: Key) -> None:
+        try:
+            loop = asyncio.get_running_loop()
+        except RuntimeError:
+            return
+        t = loop.create_task(self._resolve(key))
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)
+
+    async def _resolve(self, key: Key, tries: int = 3) -> None:
+        """Replace the cached ``key`` with a fresh GET, unless another relist overtook the GET
+        (then the GET may be older than that list: try again)."""
+        for _ in range(tries):
+            epoch = self.epoch
+            try:
+                obj = await self._fetch(key)
+            except Exception:  # noqa: BLE001 - the watch still converges; this only shortens it
+                return
+            if epoch != self.epoch:
+                continue
+            self.resolved += 1
+            if obj is None:
+                cur = self.cache.pop(key, None)
+                if cur is not None:
+                    self._forget(key, cur["metadata"].get("uid", ""))
+                    await self._notify("DELETED", cur)
+                return
+            self.cache[key] = obj
+            rv = obj["metadata"].get("resourceVersion", "")
+            if rv:
+                self._pending[key] = rv
+            await self._notify("MODIFIED", obj)
+            return
 
     # ------------------------------------------------------------------------ queries
     def get(self, ns: str, name: str) -> Optional[dict]:
@@ -242,6 +315,9 @@ class ClaimInformer(PodInformer):
 
     def _list(self):
         return self.kube.list_claims_rv(self.namespace, self.label_selector)
+
+    def _get(self, ns: str, name: str):
+        return self.kube.get_claim(ns, name)
 
     def _watch(self, timeout_s: int):
         return self.kube.watch_claims(self.namespace, self.label_selector, self.field_selector,

@@ -255,9 +255,14 @@ class WarmPool:
             for ph in chosen:
                 self._claimed.discard(ph.uid)
             if len(ok) != len(chosen):
-                # undo the partial claim, then let the caller fall back
-                back = [ph for ph, r in zip(chosen, res) if isinstance(r, dict)]
-                await self._standby_patch(back)
+                # undo the partial claim, then let the caller fall back. A PATCH that failed may
+                # still have taken effect (its reply lost), so every chosen placeholder goes
+                # back; one that cannot be put back is deleted — the caller never mounts these,
+                # and a claim left standing would give the owner a GPU it was told it did not get
+                back = await self._standby_patch(chosen)
+                stray = [ph for ph in chosen if ph not in back]
+                if stray:
+                    await self.ph.release(stray, wait=False)
                 return None
             for ph in chosen:
                 ph.mode = mode

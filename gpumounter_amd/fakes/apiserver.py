@@ -556,9 +556,10 @@ class FakeCluster:
         self._faults.extend([(method, status, after, path)] * count)
 
     def random_failures(self, rate: float, seed: int = 0) -> None:
-        """Fault injection at random: each Pod or ResourceClaim request (not watches) fails with
-        probability ``rate``: 500, 503 or 429, half of them after the request took effect
-        (a lost reply). ``rate=0`` turns it off."""
+        """Fault injection at random: each Pod or ResourceClaim request fails with probability
+        ``rate``: 500, 503 or 429, half of them after the request took effect (a lost reply).
+        Watch streams end early before an event with probability ``rate/4`` per event (one in
+        five of those with 410 Gone, forcing a relist). ``rate=0`` turns it off."""
         import random
         self._random_faults = (rate, random.Random(seed)) if rate > 0 else None
 
@@ -665,6 +666,17 @@ class FakeCluster:
                         ).encode() + b"\n")
                     continue
                 idle = 0.0
+                rf = self._random_faults
+                if rf is not None and rf[1].random() < rf[0] / 4:
+                    # random_failures also disrupts watches: the stream ends before this event
+                    # (the client resumes from its last resourceVersion) or, rarer, answers 410
+                    # Gone (the client relists)
+                    self.random_faults_served += 1
+                    if rf[1].random() < 0.2:
+                        await resp.write(json.dumps({"type": "ERROR", "object": {
+                            "kind": "Status", "code": 410, "reason": "Expired",
+                            "message": "injected: too old resource version"}}).encode() + b"\n")
+                    break
                 await resp.write(b'{"type": "' + et.encode() + b'", "object": ' + obj + b"}\n")
         except (ConnectionResetError, asyncio.CancelledError):
             pass

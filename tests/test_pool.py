@@ -134,3 +134,29 @@ def test_pool_claims_released_when_tenant_disappears():
             await wait_pool(lc, 4)
             assert standby_count(lc) == 4
     asyncio.run(main())
+
+
+def test_failed_claim_whose_patch_took_effect_is_undone():
+    """A claim PATCH that the apiserver applied but whose reply never arrived (every retry's too)
+    looks failed. The attach falls back to other GPUs, so that placeholder must not stay the
+    tenant's: it is put back into the pool (or deleted), never left as a GPU the tenant was told
+    it did not get."""
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 2}) as lc:
+            await wait_pool(lc, 2)
+            lc.tenant("t")
+            # both claim PATCHes, first attempt and every retry (5 each): applied, reply lost
+            lc.cluster.fail_next("PATCH", 503, count=10, after=True)
+            code, b = await lc.add("default", "t", 2)
+            assert code == 200
+            got = {d["uuid"] for d in b["devices"]}
+            svc = lc.nodes["node-0"].worker.service
+            st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+            assert {g.uuid for g in st.hot} == got          # nothing beyond what was answered
+            owned = [p for p in lc.cluster.placeholders()
+                     if (p["metadata"].get("annotations") or {}).get(
+                         "gpumounter.amd.com/owner-name") == "t"]
+            assert sum(int(c["resources"]["limits"]["amd.com/gpu"])
+                       for p in owned for c in p["spec"]["containers"]) == 2
+            assert not await lc.audit("default", "t")
+    asyncio.run(main())

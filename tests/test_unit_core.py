@@ -360,3 +360,67 @@ def test_reserve_gate_shared_and_exclusive():
         assert order[ix + 1] == ("out", "x")                        # alone
         assert order.index(("in", "s3")) > ix                      # queued behind x
     asyncio.run(main())
+
+
+def test_informer_relist_resolves_our_unechoed_writes_with_a_get():
+    """A relist served before our acknowledged PATCH holds an older version than the write, and
+    a write-through that arrives after a relist cannot tell older from newer: in both cases the
+    informer asks the apiserver (a GET is newer than both) instead of serving a stale object —
+    a stale 'still a candidate' or 'still standby' view is what lets a reconciler release, or a
+    pool claim twice, a GPU that is in use."""
+    import asyncio
+
+    from gpumounter_amd.cluster.informer import PodInformer
+
+    def pod(rv, v):
+        return {"metadata": {"namespace": "ns", "name": "p", "uid": "u", "resourceVersion": rv,
+                             "annotations": {"v": v}}}
+
+    server = {"obj": pod("1", "v1")}
+
+    class Kube:
+        gets = 0
+
+        async def get_pod(self, ns, name):
+            Kube.gets += 1
+            return server["obj"]
+
+    class Feed(PodInformer):
+        def __init__(self):
+            super().__init__(kube=Kube())
+            self.q = asyncio.Queue()
+            self.listed = [pod("1", "v1")]
+
+        async def _list(self):
+            return list(self.listed), "1"
+
+        async def _watch(self, timeout_s):
+            while True:
+                ev = await self.q.get()
+                if ev is None:
+                    return
+                yield ev
+
+    async def main():
+        inf = Feed()
+        await inf.start()
+        # our PATCH is acknowledged (rv 5); then a relist arrives that was served before it
+        server["obj"] = pod("5", "patched")
+        inf.upsert(pod("5", "patched"), inf.epoch)
+        await inf._relist()                        # lists rv 1 (older than our write)
+        assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "patched"
+        assert Kube.gets == 1
+        # a write-through whose request went out before a relist: resolved by a GET as well
+        ep = inf.epoch
+        inf.listed = [pod("5", "patched")]
+        await inf._relist()
+        server["obj"] = pod("7", "patched-again")
+        inf.upsert(pod("7", "patched-again"), ep)
+        await asyncio.sleep(0.01)
+        assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "patched-again"
+        # the resumed watch replays older events: skipped until it reaches the fetched version
+        await inf.q.put(("MODIFIED", pod("6", "replayed-older")))
+        await asyncio.sleep(0.01)
+        assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "patched-again"
+        await inf.stop()
+    asyncio.run(main())
