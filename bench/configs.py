@@ -315,7 +315,8 @@ def chaos(args) -> dict:
     rnds = {t: random.Random(args.seed * 17 + i) for i, t in enumerate(tenants)}
     mine = {t: [] for t in tenants}
     certain = {t: True for t in tenants}
-    ok = failed = kills = 0
+    answered = {t: [] for t in tenants}      # (code, [(placeholder, uuid tail)]) per attach
+    ok = failed = kills = restarts = 0
     problems, converge = [], []
     api_faults = [0]
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": "0.5",
@@ -341,6 +342,9 @@ def chaos(args) -> dict:
                     return t, code
                 n, entire = rnd.randint(1, 3), rnd.random() < 0.3
                 code, b = pc.add("default", t, n, entire=entire)
+                answered[t].append((code, [(d.get("placeholder"), d["uuid"][-4:])
+                                           for d in (b.get("devices") or [])]
+                                    if isinstance(b, dict) else None))
                 if code == 200:
                     uu = [d["uuid"] for d in b["devices"]]
                     mine[t].extend([(uu, True)] if entire else [([u], False) for u in uu])
@@ -388,6 +392,10 @@ def chaos(args) -> dict:
         with ThreadPoolExecutor(len(tenants)) as ex:
             for rnd_i in range(args.rounds):
                 futs = [ex.submit(op, t) for t in tenants]
+                if args.restart_rate and random.Random(rnd_i * 7 + 1).random() < args.restart_rate:
+                    # a tenant's container crashes and comes back while requests are in flight
+                    pc.restart_container("default", random.Random(rnd_i).choice(tenants))
+                    restarts += 1
                 if args.kill_every and rnd_i % args.kill_every == args.kill_every - 1:
                     time.sleep(random.Random(rnd_i).uniform(0.0, 0.004))
                     pc.kill_worker("node-0")        # SIGKILL with requests in flight
@@ -414,7 +422,16 @@ def chaos(args) -> dict:
                     hot = ledger(t) or []
                     want = sorted(u for grp, _ in mine[t] for u in grp)
                     if certain[t] and hot != want:
-                        problems.append(f"round {rnd_i} {t}: ledger {hot} != attached {want}")
+                        mine_phs = [(p["metadata"]["name"],
+                                     {k.split("/")[-1]: v for k, v in
+                                      (p["metadata"].get("annotations") or {}).items()
+                                      if k.split("/")[-1] in ("attach-id", "mount-mode",
+                                                              "worker-incarnation")})
+                                    for p in pc.placeholders()
+                                    if (p["metadata"].get("annotations") or {}).get(
+                                        "gpumounter.amd.com/owner-name") == t]
+                        problems.append(f"round {rnd_i} {t}: ledger {hot} != attached {want}; "
+                                        f"placeholders {mine_phs}; answered {answered[t]}")
                     if not certain[t]:
                         # resynchronise the client from the ledger: single mounts per GPU (an
                         # entire mount's GPUs are removed together; the ledger's mount type says)
@@ -431,7 +448,8 @@ def chaos(args) -> dict:
         metrics = pc.worker_metrics()
     injected = sum(float(ln.split()[-1]) for ln in metrics.splitlines()
                    if ln.startswith("gm_requests_total{") and 'result="INTERNAL"' in ln)
-    return {"rounds": args.rounds, "worker_kills": kills, "ops_ok": ok,
+    return {"rounds": args.rounds, "worker_kills": kills, "container_restarts": restarts,
+            "ops_ok": ok,
             "ops_failed": failed, "internal_errors_since_last_restart": injected,
             "converge_p50_ms": round(pct(converge, 0.5), 1),
             "converge_max_ms": round(max(converge), 1),
@@ -524,6 +542,9 @@ def main() -> int:
     ap.add_argument("--api-fault-rate", type=float, default=0.0,
                     help="chaos: Pod/ResourceClaim requests to the apiserver fail at random at "
                          "this rate (500/503/429, half after taking effect)")
+    ap.add_argument("--restart-rate", type=float, default=0.0,
+                    help="chaos: per round, the probability that a tenant's container restarts "
+                         "with requests in flight")
     ap.add_argument("--kill-every", type=int, default=10,
                     help="chaos: SIGKILL the worker with requests in flight every N rounds")
     ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",

@@ -103,9 +103,15 @@ class PodInformer:
                     continue            # keep the listed version; the watch still converges
                 if obj is None:
                     fresh.pop(k, None)
-                else:
-                    fresh[k] = obj
-                    pending[k] = obj["metadata"].get("resourceVersion", "")
+                    continue
+                listed = fresh[k]["metadata"].get("resourceVersion", "")
+                fresh[k] = obj
+                grv = obj["metadata"].get("resourceVersion", "")
+                if grv != listed:
+                    # changed after the list's snapshot: the watch, resumed from the list's
+                    # version, will deliver it — older replays wait for it. (Equal: the list
+                    # was already current, and no event for it is coming to wait for.)
+                    pending[k] = grv
             self.resolved += len(suspects)
         else:
             pending = {}
@@ -256,6 +262,9 @@ class PodInformer:
             if epoch != self.epoch:
                 continue
             self.resolved += 1
+            if obj is not None and obj["metadata"].get("resourceVersion", "") in \
+                    self._seen.get(key, ()):
+                return      # the watch delivered this version meanwhile: the cache is as new
             if obj is None:
                 cur = self.cache.pop(key, None)
                 if cur is not None:

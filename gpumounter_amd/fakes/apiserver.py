@@ -397,6 +397,26 @@ class FakeCluster:
         pod["status"]["qosClass"] = podu.qos_class(pod)
         self._bump("MODIFIED", pod)
 
+    def restart_container(self, ns: str, name: str, cname: str) -> str:
+        """The container exits and the kubelet starts it again (restartPolicy Always): a new
+        container id, cgroup and root filesystem — no device gpumounter added survives — and a
+        MODIFIED event with restartCount + 1. Returns the new container id."""
+        with self._lock:
+            pod = self.pods[(ns, name)]
+            node = self.nodes[pod["spec"]["nodeName"]]
+            cs = next(c for c in pod["status"]["containerStatuses"] if c["name"] == cname)
+            old = cs["containerID"].split("://", 1)[1]
+            octr = node.container(old)
+            pids = octr.pids if octr is not None else []
+            node.stop_container(old)
+            ctr = node.start_container(pod, cname, pids)
+            cs.update({"containerID": f"{node.runtime}://{ctr.id}",
+                       "restartCount": int(cs.get("restartCount", 0)) + 1,
+                       "lastState": {"terminated": {"exitCode": 1, "finishedAt": _now()}},
+                       "state": {"running": {"startedAt": _now()}}})
+            self._bump("MODIFIED", pod)
+            return ctr.id
+
     def create_running_pod(self, ns: str, body: dict, node: str,
                            pids: Optional[Dict[str, List[int]]] = None) -> dict:
         """Test helper: a tenant pod that is already bound, admitted and running."""

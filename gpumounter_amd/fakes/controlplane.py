@@ -11,6 +11,7 @@ Besides the Kubernetes API it serves these test hooks:
   ``POST /_fake/tenant``  {"name", "ns", "node", "gpus", "containers", "pids"} → a Running pod
   ``POST /_fake/worker``  {"node", "port"}  → the worker DaemonSet pod the master discovers
   ``GET  /_fake/kubelet``  → each node's PodResources call counters (served, rejected, over_limit)
+  ``POST /_fake/restart`` {"ns", "pod", "container"} → the container restarts (new id, cgroup, /dev)
   ``POST /_fake/faults``  {"rate", "seed"} → Pod/ResourceClaim requests fail at random (500/503/
                           429, half after taking effect); answers how many were served so far
   ``POST /_fake/user``    {"token", "user", "verbs", "resource", "namespaces"} → a bearer token
@@ -65,7 +66,14 @@ def _hooks(lc_ref: list):
             api.random_failures(float(b.get("rate", 0)), int(b.get("seed", 0)))
             return web.json_response({"served": api.random_faults_served}, status=201)
 
+        async def restart(req: web.Request) -> web.Response:
+            b = await req.json()
+            cid = lc_ref[0].cluster.restart_container(b.get("ns", "default"), b["pod"],
+                                                      b.get("container", "main"))
+            return web.json_response({"container_id": cid}, status=201)
+
         app.router.add_post("/_fake/faults", faults)
+        app.router.add_post("/_fake/restart", restart)
         app.router.add_post("/_fake/tenant", tenant)
         app.router.add_post("/_fake/user", user)
         app.router.add_post("/_fake/worker", worker)

@@ -316,6 +316,15 @@ class ProcessCluster:
             raise RuntimeError(f"kubelet counters: {code}")
         return json.loads(body)[node]
 
+    def restart_container(self, ns: str, pod: str, container: str = "main") -> str:
+        """The kubelet restarts one container of a tenant Pod (fakes/apiserver.py)."""
+        code, body = _http("POST", f"{self.info['api_url']}/_fake/restart",
+                           json.dumps({"ns": ns, "pod": pod, "container": container}).encode(),
+                           {"Content-Type": "application/json"})
+        if code != 201:
+            raise RuntimeError(f"container restart: {code} {body[:200]!r}")
+        return json.loads(body)["container_id"]
+
     def api_faults(self, rate: float, seed: int = 0) -> int:
         """Random apiserver failures for Pod/ResourceClaim requests (fakes/apiserver.py
         random_failures); returns how many were served before this call."""

@@ -331,6 +331,19 @@ class FakeNode:
             with open(os.path.join(c.cgroup_dir, "cgroup.procs"), "w") as fh:
                 fh.write("".join(f"{p}\n" for p in pids))
 
+    def stop_container(self, cid: str) -> None:
+        """One container exits: its cgroup and root filesystem go (a restart starts a fresh
+        container with a new id, as a runtime does)."""
+        with self._lock:
+            c = self.containers.pop(cid, None)
+        if c is None:
+            return
+        shutil.rmtree(c.cgroup_dir, ignore_errors=True)
+        if os.path.islink(c.root_dir):
+            os.unlink(c.root_dir)
+        else:
+            shutil.rmtree(c.root_dir, ignore_errors=True)
+
     def stop_pod_containers(self, ns: str, pod: str) -> None:
         with self._lock:
             for cid, c in list(self.containers.items()):

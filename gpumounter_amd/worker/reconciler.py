@@ -34,7 +34,8 @@ from typing import Dict, List, Optional
 
 from gpumounter_amd.cluster.kube import NotFound
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import ANN_CANDIDATE, ANN_INCARNATION, ANN_OWNER_UID
+from gpumounter_amd.models.types import (ANN_CANDIDATE, ANN_CONTAINER, ANN_INCARNATION,
+                                         ANN_OWNER_UID)
 from gpumounter_amd.utils import log
 
 _log = log.get("worker.reconciler")
@@ -89,6 +90,22 @@ class Reconciler:
         if etype == "DELETED" or podu.phase_of(pod) in ("Succeeded", "Failed"):
             if self.svc.ph.owned_by(pod, candidates=True):
                 self._kick(("release", podu.ns_of(pod), podu.name_of(pod), podu.uid_of(pod)))
+        elif etype == "MODIFIED" and self._restarted(pod):
+            # a container of a Pod with hot-mounted GPUs was restarted: the new one starts with
+            # the runtime's /dev and device rules, so the GPUs go back in now — not at the next
+            # periodic sweep, by which time the restarted process has looked and found none
+            self._kick(("reinject", podu.ns_of(pod), podu.name_of(pod)))
+
+    def _restarted(self, pod: dict) -> bool:
+        """A running container of a Pod that holds hot-mounted GPUs has no injection record:
+        it started after the attach (a restart), or its record is lost."""
+        phs = self.svc.ph.owned_by(pod)
+        if not phs or podu.phase_of(pod) != "Running":
+            return False
+        wanted = {(p["metadata"].get("annotations") or {}).get(ANN_CONTAINER, "") for p in phs}
+        journal = self.svc.hm.journal
+        return any(r.running and not r.privileged and ("" in wanted or r.name in wanted)
+                   and journal.get(r.id) is None for r in podu.running_containers(pod))
 
     def _kick(self, key: tuple) -> None:
         if key in self._kicked:
@@ -117,11 +134,16 @@ class Reconciler:
                     if owner is None or podu.phase_of(owner) != "Running":
                         return
                     fixed = await svc.reconcile_pod(owner)
-                    if fixed:
-                        gone = sorted({i.path for i in fixed if i.kind.startswith("stale")})
+                    gone = sorted({i.path for i in fixed if i.kind.startswith("stale")})
+                    back = sorted({i.path for i in fixed if i.kind.startswith("missing")})
+                    if gone:
                         svc.notify.event(owner, "GPURevoked",
                                          f"placeholder deleted outside gpumounter; access "
                                          f"revoked: {', '.join(gone)}", warning=True)
+                    if back and key[0] == "reinject":
+                        svc.notify.event(owner, "GPUReinjected",
+                                         f"container restarted; hot-mounted devices restored: "
+                                         f"{', '.join(back)}")
                 self.event_actions += 1
                 svc.metrics.reconcile_actions.labels(action=f"event_{key[0]}").inc()
         except Exception as e:  # noqa: BLE001 - the periodic sweep retries

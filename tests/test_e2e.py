@@ -930,3 +930,30 @@ def test_status_endpoints_answer_json_when_the_worker_is_down():
         async with lc.session.get(lc.master_url + "/api/v1/namespaces/default/pods/m/gpus") as r:
             assert r.status == 502 and "UNAVAILABLE" in (await r.json())["error"]
     run(body)
+
+
+def test_container_restart_gets_its_gpus_back_at_once():
+    """A real restart: the runtime starts a new container (new id, cgroup and /dev). The worker
+    reacts to the Pod's MODIFIED event — no periodic sweep involved — and puts the hot-mounted
+    GPUs into the new container, with a GPUReinjected Event."""
+    async def body(lc):
+        lc.tenant("r")
+        code, b = await lc.add("default", "r", 2)
+        assert code == 200
+        old = lc.container_ids("default", "r")[0]
+        new = lc.cluster.restart_container("default", "r", "main")
+        assert new != old and node_of(lc).container(old) is None
+        w = lc.nodes["node-0"].worker
+        for _ in range(100):
+            await asyncio.sleep(0.02)
+            if not await lc.audit("default", "r"):
+                break
+        assert not await lc.audit("default", "r")
+        devs = node_of(lc).container_devices(new)
+        assert sum("renderD" in d for d in devs) == 2 and "dev/kfd" in devs
+        assert w.reconciler.event_actions >= 1
+        reasons = [e["reason"] for e in lc.cluster.events_for("default", "r")]
+        assert "GPUReinjected" in reasons
+        code, _ = await lc.remove("default", "r", [d["uuid"] for d in b["devices"]])
+        assert code == 200 and not node_of(lc).container_devices(new)
+    run(body)          # LocalCluster runs no periodic sweep (reconcile_period_s=0)

@@ -424,3 +424,49 @@ def test_informer_relist_resolves_our_unechoed_writes_with_a_get():
         assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "patched-again"
         await inf.stop()
     asyncio.run(main())
+
+
+def test_informer_relist_newer_than_our_write_does_not_stall_the_key():
+    """The list holds a version newer than our unechoed write (someone wrote after us): the GET
+    returns that same version, which the resumed watch will never deliver again — the key must
+    not wait for it, or every later event for the object would be skipped for good."""
+    import asyncio
+
+    from gpumounter_amd.cluster.informer import PodInformer
+
+    def pod(rv, v):
+        return {"metadata": {"namespace": "ns", "name": "p", "uid": "u", "resourceVersion": rv,
+                             "annotations": {"v": v}}}
+
+    class Kube:
+        async def get_pod(self, ns, name):
+            return pod("8", "someone-else")
+
+    class Feed(PodInformer):
+        def __init__(self):
+            super().__init__(kube=Kube())
+            self.q = asyncio.Queue()
+            self.listed = [pod("1", "v1")]
+
+        async def _list(self):
+            return list(self.listed), "8"
+
+        async def _watch(self, timeout_s):
+            while True:
+                ev = await self.q.get()
+                if ev is None:
+                    return
+                yield ev
+
+    async def main():
+        inf = Feed()
+        await inf.start()
+        inf.upsert(pod("5", "ours"), inf.epoch)
+        inf.listed = [pod("8", "someone-else")]
+        await inf._relist()
+        assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "someone-else"
+        await inf.q.put(("MODIFIED", pod("9", "next")))     # the next change arrives
+        await asyncio.sleep(0.01)
+        assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "next"
+        await inf.stop()
+    asyncio.run(main())
