@@ -316,7 +316,7 @@ def chaos(args) -> dict:
     mine = {t: [] for t in tenants}
     certain = {t: True for t in tenants}
     answered = {t: [] for t in tenants}      # (code, [(placeholder, uuid tail)]) per attach
-    ok = failed = kills = restarts = 0
+    ok = failed = kills = restarts = master_kills = 0
     problems, converge = [], []
     api_faults = [0]
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": "0.5",
@@ -396,6 +396,11 @@ def chaos(args) -> dict:
                     # a tenant's container crashes and comes back while requests are in flight
                     pc.restart_container("default", random.Random(rnd_i).choice(tenants))
                     restarts += 1
+                if args.master_kill_every and \
+                        rnd_i % args.master_kill_every == args.master_kill_every - 1:
+                    time.sleep(random.Random(rnd_i + 5).uniform(0.0, 0.004))
+                    pc.restart_master()             # SIGKILL with requests in flight
+                    master_kills += 1
                 if args.kill_every and rnd_i % args.kill_every == args.kill_every - 1:
                     time.sleep(random.Random(rnd_i).uniform(0.0, 0.004))
                     pc.kill_worker("node-0")        # SIGKILL with requests in flight
@@ -448,7 +453,8 @@ def chaos(args) -> dict:
         metrics = pc.worker_metrics()
     injected = sum(float(ln.split()[-1]) for ln in metrics.splitlines()
                    if ln.startswith("gm_requests_total{") and 'result="INTERNAL"' in ln)
-    return {"rounds": args.rounds, "worker_kills": kills, "container_restarts": restarts,
+    return {"rounds": args.rounds, "worker_kills": kills, "master_kills": master_kills,
+            "container_restarts": restarts,
             "ops_ok": ok,
             "ops_failed": failed, "internal_errors_since_last_restart": injected,
             "converge_p50_ms": round(pct(converge, 0.5), 1),
@@ -545,6 +551,9 @@ def main() -> int:
     ap.add_argument("--restart-rate", type=float, default=0.0,
                     help="chaos: per round, the probability that a tenant's container restarts "
                          "with requests in flight")
+    ap.add_argument("--master-kill-every", type=int, default=0,
+                    help="chaos: SIGKILL and restart the master with requests in flight every N "
+                         "rounds")
     ap.add_argument("--kill-every", type=int, default=10,
                     help="chaos: SIGKILL the worker with requests in flight every N rounds")
     ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",

@@ -198,15 +198,31 @@ class ProcessCluster:
             self._spawn(f"worker-{node}", [*self.entry, "worker"], env)
         for node in self._worker_env:
             self._await_worker(node)
-        self._spawn("master", [*self.entry, "master"],
-                    {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1", **tls_m,
-                     "GM_MASTER_PORT": "0", "GM_READY_FILE": self._ready_path("master"),
-                     "GM_LOG_LEVEL": "WARNING", "GM_LOG_JSON": "false", **self.master_env})
+        self._master_env = {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1", **tls_m,
+                            "GM_MASTER_PORT": "0", "GM_READY_FILE": self._ready_path("master"),
+                            "GM_LOG_LEVEL": "WARNING", "GM_LOG_JSON": "false",
+                            **self.master_env}
+        self._start_master()
+        return self
+
+    def _start_master(self) -> None:
+        self._spawn("master", [*self.entry, "master"], self._master_env)
         self.master_url = f"http://127.0.0.1:{self._ready('master')['port']}"
         for node in self.info["nodes"]:   # the master has discovered every worker
             self._wait(f"master → {node}", lambda n=node: _http(
                 "GET", f"{self.master_url}/api/v1/nodes/{n}/gpus", headers=self._auth)[0] == 200)
-        return self
+
+    def restart_master(self, sig: int = signal.SIGKILL) -> None:
+        """Kill the master (SIGKILL: requests in flight lose their client connection; the
+        workers carry on) and start a new one; it serves on a new port (``master_url``)."""
+        p = self.procs["master"]
+        p.send_signal(sig)
+        p.wait(20)
+        try:
+            os.unlink(self._ready_path("master"))
+        except FileNotFoundError:
+            pass
+        self._start_master()
 
     def _ready_path(self, key: str) -> str:
         return os.path.join(self.workdir, f"{key}.ready")

@@ -51,6 +51,10 @@ def _read(path: str) -> bytes:
 
 
 class Worker:
+    # SIGTERM: how long operations already running may take to finish (the DaemonSet's
+    # terminationGracePeriodSeconds is 30)
+    OPS_DRAIN_S = 20.0
+
     def __init__(self, cfg, kube: Optional[KubeClient] = None,
                  inventory: Optional[Inventory] = None) -> None:
         if not cfg.node_name:
@@ -127,6 +131,7 @@ class Worker:
         if cfg.reconcile_on_events:
             self.reconciler.watch_events()
         self.grpc_server: Optional[grpc.aio.Server] = None
+        self._ops: set = set()          # RPC operations running (see _wrap)
         self.http_runner: Optional[web.AppRunner] = None
         self.grpc_port = 0
         self.http_port = 0
@@ -150,8 +155,15 @@ class Worker:
             if not self._peer_allowed(context):
                 await context.abort(grpc.StatusCode.PERMISSION_DENIED,
                                     "client certificate is not an allowed gpumounter identity")
+            # An attach or detach, once started, runs to its end (done, or rolled back) even if
+            # the caller goes away: a master killed or a deadline passed mid-request cancels
+            # this handler, and a cancellation landing between two steps would leave a
+            # placeholder created but never admitted or mounted, or rules without nodes
+            op = asyncio.ensure_future(fn(request))
+            self._ops.add(op)
+            op.add_done_callback(self._ops.discard)
             try:
-                return await fn(request)
+                return await asyncio.shield(op)
             except RpcError as e:
                 await context.abort(e.code, e.msg)
             except grpc.aio.AbortError:
@@ -364,6 +376,8 @@ class Worker:
             await self.plugin.stop()
         if self.grpc_server is not None:
             await self.grpc_server.stop(0.5)
+        if self._ops:   # operations whose callers left: let them finish (or roll back)
+            await asyncio.wait(list(self._ops), timeout=self.OPS_DRAIN_S)
         if self.http_runner is not None:
             await self.http_runner.cleanup()
         await self.ph_informer.stop()

@@ -350,3 +350,34 @@ def test_unadmitted_placeholder_of_a_dead_worker_is_released_at_once():
         st = await svc.pod_state(tenant, fresh=True)
         assert len(st.hot) == 2 and not await lc.audit("default", "t")
     run(body, worker_overrides={"reconcile_on_events": False})
+
+
+def test_caller_going_away_mid_attach_does_not_leave_half_an_attach():
+    """The master dies, or its deadline passes, while the worker waits for the placeholder's
+    admission: gRPC cancels the handler. The attach must still run to its end — here it
+    completes — instead of stopping between two steps with a placeholder created but never
+    mounted (found by bench/configs.py chaos --master-kill-every)."""
+    import grpc
+
+    from gpumounter_amd.api import gpu_mount as api
+    from gpumounter_amd.fakes.apiserver import LatencyModel
+
+    async def body(lc):
+        lc.tenant("t")
+        ch = lc.master.workers.channel(lc.master.workers.target("node-0"))
+        stub = ch.unary_unary(api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
+                              response_deserializer=api.AddGPUResponse.FromString)
+        with pytest.raises(grpc.aio.AioRpcError) as ei:
+            await stub(api.AddGPURequest(pod_name="t", namespace="default", gpu_num=2,
+                                         is_entire_mount=False), timeout=0.05)
+        assert ei.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED
+        svc = lc.nodes["node-0"].worker.service
+        tenant = lc.cluster.get("default", "t")
+        for _ in range(100):                 # admission takes ~0.2 s here
+            await asyncio.sleep(0.02)
+            if len((await svc.pod_state(tenant, fresh=True)).hot) == 2:
+                break
+        assert len((await svc.pod_state(tenant, fresh=True)).hot) == 2
+        assert all(p["spec"].get("nodeName") for p in lc.cluster.placeholders())
+        assert not await lc.audit("default", "t")
+    run(body, latency=LatencyModel(schedule_ms=100.0, admit_ms=100.0))
