@@ -316,10 +316,11 @@ def chaos(args) -> dict:
     mine = {t: [] for t in tenants}
     certain = {t: True for t in tenants}
     answered = {t: [] for t in tenants}      # (code, [(placeholder, uuid tail)]) per attach
-    ok = failed = kills = restarts = master_kills = 0
+    ok = failed = kills = restarts = master_kills = recreates = kubelet_restarts = 0
+    recreated: set = set()
     problems, converge = [], []
     api_faults = [0]
-    env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": "0.5",
+    env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": str(args.reconcile_period),
            "GM_WARM_POOL_SIZE": str(args.warm_pool)}
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
                         gpu_api=args.gpu_api) as pc:
@@ -392,6 +393,16 @@ def chaos(args) -> dict:
         with ThreadPoolExecutor(len(tenants)) as ex:
             for rnd_i in range(args.rounds):
                 futs = [ex.submit(op, t) for t in tenants]
+                if args.recreate_rate and random.Random(rnd_i * 11 + 3).random() < args.recreate_rate:
+                    # a tenant Pod is deleted and recreated under its name (new UID) mid-round
+                    t = random.Random(rnd_i + 9).choice(tenants)
+                    pc.recreate_pod("default", t)
+                    recreated.add(t)
+                    recreates += 1
+                if args.kubelet_restart_every and \
+                        rnd_i % args.kubelet_restart_every == args.kubelet_restart_every - 1:
+                    pc.restart_kubelet("node-0", down_s=0.05)
+                    kubelet_restarts += 1
                 if args.restart_rate and random.Random(rnd_i * 7 + 1).random() < args.restart_rate:
                     # a tenant's container crashes and comes back while requests are in flight
                     pc.restart_container("default", random.Random(rnd_i).choice(tenants))
@@ -409,6 +420,9 @@ def chaos(args) -> dict:
                     pc.restart_worker("node-0")
                 else:
                     results = [f.result() for f in futs]
+                for t in recreated:
+                    certain[t] = False
+                recreated.clear()
                 for t, code in results:
                     ok += code == 200
                     failed += code not in (200, 400, 403)   # 400/403 are answers, not failures
@@ -454,13 +468,15 @@ def chaos(args) -> dict:
     injected = sum(float(ln.split()[-1]) for ln in metrics.splitlines()
                    if ln.startswith("gm_requests_total{") and 'result="INTERNAL"' in ln)
     return {"rounds": args.rounds, "worker_kills": kills, "master_kills": master_kills,
-            "container_restarts": restarts,
+            "container_restarts": restarts, "pod_recreates": recreates,
+            "kubelet_restarts": kubelet_restarts,
             "ops_ok": ok,
             "ops_failed": failed, "internal_errors_since_last_restart": injected,
             "converge_p50_ms": round(pct(converge, 0.5), 1),
             "converge_max_ms": round(max(converge), 1),
             "invariant_violations": len(problems), "violation_examples": problems[:5],
             "faults": CHAOS_FAULTS, "api_fault_rate": args.api_fault_rate,
+            "reconcile_period_s": args.reconcile_period,
             "api_faults_served": api_faults[0]}
 
 
@@ -554,6 +570,14 @@ def main() -> int:
     ap.add_argument("--master-kill-every", type=int, default=0,
                     help="chaos: SIGKILL and restart the master with requests in flight every N "
                          "rounds")
+    ap.add_argument("--recreate-rate", type=float, default=0.0,
+                    help="chaos: per round, the probability that a tenant Pod is deleted and "
+                         "recreated under the same name with requests in flight")
+    ap.add_argument("--kubelet-restart-every", type=int, default=0,
+                    help="chaos: restart the kubelet (PodResources socket recreated) every N "
+                         "rounds")
+    ap.add_argument("--reconcile-period", type=float, default=0.5,
+                    help="chaos: the worker's periodic sweep (GM_RECONCILE_PERIOD_S; shipped 30)")
     ap.add_argument("--kill-every", type=int, default=10,
                     help="chaos: SIGKILL the worker with requests in flight every N rounds")
     ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",

@@ -11,6 +11,10 @@ Besides the Kubernetes API it serves these test hooks:
   ``POST /_fake/tenant``  {"name", "ns", "node", "gpus", "containers", "pids"} → a Running pod
   ``POST /_fake/worker``  {"node", "port"}  → the worker DaemonSet pod the master discovers
   ``GET  /_fake/kubelet``  → each node's PodResources call counters (served, rejected, over_limit)
+  ``POST /_fake/kubelet/restart`` {"node", "down_s"} → kubelet down for down_s, PodResources
+                          socket recreated
+  ``POST /_fake/recreate`` {"ns", "pod", "gap_s"} → the Pod is deleted and created again under
+                          the same name (new UID)
   ``POST /_fake/restart`` {"ns", "pod", "container"} → the container restarts (new id, cgroup, /dev)
   ``POST /_fake/faults``  {"rate", "seed"} → Pod/ResourceClaim requests fail at random (500/503/
                           429, half after taking effect); answers how many were served so far
@@ -72,7 +76,28 @@ def _hooks(lc_ref: list):
                                                       b.get("container", "main"))
             return web.json_response({"container_id": cid}, status=201)
 
+        async def kubelet_restart(req: web.Request) -> web.Response:
+            from gpumounter_amd.fakes.kubelet import FakeKubelet
+            b = await req.json()
+            h = lc_ref[0].nodes[b.get("node", "node-0")]
+            await h.kubelet.stop()
+            await asyncio.sleep(float(b.get("down_s", 0.0)))
+            h.kubelet = FakeKubelet(h.node, h.kubelet.socket_path)
+            await h.kubelet.start()
+            return web.json_response({"ok": True}, status=201)
+
+        async def recreate(req: web.Request) -> web.Response:
+            b = await req.json()
+            lc = lc_ref[0]
+            ns, name = b.get("ns", "default"), b["pod"]
+            lc.cluster.delete(ns, name, grace=0)
+            await asyncio.sleep(float(b.get("gap_s", 0.0)))
+            pod = lc.tenant(name, ns=ns, node=b.get("node", "node-0"))
+            return web.json_response({"uid": pod["metadata"]["uid"]}, status=201)
+
         app.router.add_post("/_fake/faults", faults)
+        app.router.add_post("/_fake/kubelet/restart", kubelet_restart)
+        app.router.add_post("/_fake/recreate", recreate)
         app.router.add_post("/_fake/restart", restart)
         app.router.add_post("/_fake/tenant", tenant)
         app.router.add_post("/_fake/user", user)

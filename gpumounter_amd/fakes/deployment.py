@@ -341,6 +341,22 @@ class ProcessCluster:
             raise RuntimeError(f"container restart: {code} {body[:200]!r}")
         return json.loads(body)["container_id"]
 
+    def restart_kubelet(self, node: str = "node-0", down_s: float = 0.0) -> None:
+        code, body = _http("POST", f"{self.info['api_url']}/_fake/kubelet/restart",
+                           json.dumps({"node": node, "down_s": down_s}).encode(),
+                           {"Content-Type": "application/json"})
+        if code != 201:
+            raise RuntimeError(f"kubelet restart: {code} {body[:200]!r}")
+
+    def recreate_pod(self, ns: str, pod: str, gap_s: float = 0.0) -> str:
+        """Delete the tenant Pod and create it again under the same name; its new UID."""
+        code, body = _http("POST", f"{self.info['api_url']}/_fake/recreate",
+                           json.dumps({"ns": ns, "pod": pod, "gap_s": gap_s}).encode(),
+                           {"Content-Type": "application/json"})
+        if code != 201:
+            raise RuntimeError(f"recreate: {code} {body[:200]!r}")
+        return json.loads(body)["uid"]
+
     def api_faults(self, rate: float, seed: int = 0) -> int:
         """Random apiserver failures for Pod/ResourceClaim requests (fakes/apiserver.py
         random_failures); returns how many were served before this call."""

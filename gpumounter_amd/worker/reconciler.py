@@ -66,6 +66,7 @@ class Reconciler:
         self._first_seen: Dict[str, float] = {}
         self._claim_seen: Dict[tuple, float] = {}
         self._kicked: set = set()
+        self._timers: Dict[tuple, asyncio.TimerHandle] = {}   # retries of failed reactions
         self._bg: set = set()
         self.event_actions = 0
 
@@ -107,15 +108,30 @@ class Reconciler:
         return any(r.running and not r.privileged and ("" in wanted or r.name in wanted)
                    and journal.get(r.id) is None for r in podu.running_containers(pod))
 
-    def _kick(self, key: tuple) -> None:
+    # a failed reaction (apiserver error, a kernel call refused) is retried after these delays
+    # before it is left to the periodic sweep, which may be 30 s away
+    RETRY_DELAYS = (0.1, 0.5, 2.0, 5.0)
+
+    def _kick(self, key: tuple, attempt: int = 0) -> None:
         if key in self._kicked:
             return
         self._kicked.add(key)
-        t = asyncio.ensure_future(self._react(key))
+        t = asyncio.ensure_future(self._react(key, attempt))
         self._bg.add(t)
         t.add_done_callback(self._bg.discard)
 
-    async def _react(self, key: tuple) -> None:
+    def _retry(self, key: tuple, attempt: int) -> None:
+        if attempt > len(self.RETRY_DELAYS) or key in self._timers:
+            return
+        loop = asyncio.get_running_loop()
+        self._timers[key] = loop.call_later(self.RETRY_DELAYS[attempt - 1], self._fire, key,
+                                            attempt)
+
+    def _fire(self, key: tuple, attempt: int) -> None:
+        self._timers.pop(key, None)
+        self._kick(key, attempt)
+
+    async def _react(self, key: tuple, attempt: int = 0) -> None:
         svc = self.svc
         await asyncio.sleep(0)  # coalesce a burst of events for one owner
         self._kicked.discard(key)
@@ -146,13 +162,18 @@ class Reconciler:
                                          f"{', '.join(back)}")
                 self.event_actions += 1
                 svc.metrics.reconcile_actions.labels(action=f"event_{key[0]}").inc()
-        except Exception as e:  # noqa: BLE001 - the periodic sweep retries
-            _log.error("event-driven reconcile %s failed: %s", key, e)
+        except Exception as e:  # noqa: BLE001 - retried, then the periodic sweep
+            _log.error("event-driven reconcile %s failed (attempt %d): %s", key, attempt + 1, e)
+            svc.metrics.reconcile_actions.labels(action="event_retry").inc()
+            self._retry(key, attempt + 1)
 
     async def start(self) -> None:
         self._task = asyncio.ensure_future(self._loop())
 
     async def stop(self) -> None:
+        for h in list(self._timers.values()):
+            h.cancel()
+        self._timers.clear()
         for t in list(self._bg):
             t.cancel()
         if self._task:
@@ -163,8 +184,14 @@ class Reconciler:
                 pass
 
     async def _loop(self) -> None:
+        # the first sweep runs at once: whatever changed while no worker was running (a
+        # container restarted, a Pod deleted, an attach cut off by the previous worker's death)
+        # sent its events to nobody, and the next periodic sweep may be 30 s away
+        first = True
         while True:
-            await asyncio.sleep(self.period_s)
+            if not first:
+                await asyncio.sleep(self.period_s)
+            first = False
             try:
                 await self.run_once()
             except asyncio.CancelledError:

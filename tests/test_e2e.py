@@ -957,3 +957,30 @@ def test_container_restart_gets_its_gpus_back_at_once():
         code, _ = await lc.remove("default", "r", [d["uuid"] for d in b["devices"]])
         assert code == 200 and not node_of(lc).container_devices(new)
     run(body)          # LocalCluster runs no periodic sweep (reconcile_period_s=0)
+
+
+def test_failed_event_reaction_is_retried_before_the_periodic_sweep():
+    """A container restart's re-injection fails once (the kernel call is refused): the reaction
+    is retried after a short backoff instead of waiting for the periodic sweep."""
+    async def body(lc):
+        lc.tenant("r")
+        code, _ = await lc.add("default", "r", 1)
+        assert code == 200
+        w = lc.nodes["node-0"].worker
+        hm = w.service.hm
+        real, calls = hm.repair, []
+
+        def flaky(*a, **k):
+            calls.append(1)
+            if len(calls) == 1:
+                raise OSError("EBUSY: the kernel refused the program update")
+            return real(*a, **k)
+        hm.repair = flaky
+        lc.cluster.restart_container("default", "r", "main")
+        for _ in range(100):
+            await asyncio.sleep(0.02)
+            if not await lc.audit("default", "r"):
+                break
+        assert not await lc.audit("default", "r") and len(calls) == 2
+        assert w.metrics.reconcile_actions.labels(action="event_retry")._value.get() == 1
+    run(body)

@@ -129,6 +129,30 @@ def test_worker_killed_mid_attach_converges_after_restart():
         pc.stop()
 
 
+def test_changes_made_while_no_worker_ran_are_repaired_at_startup():
+    """What happens while the worker is down sends its events to nobody: here a tenant's
+    container restarts (new id, no GPUs). The restarted worker sweeps once at startup, so with
+    the shipped 30 s period the GPUs are back within a second, not a period later."""
+    import time
+
+    pc = ProcessCluster(worker_env={"GM_RECONCILE_PERIOD_S": "30"})
+    try:
+        pc.start()
+        pc.tenant("t")
+        code, b = pc.add("default", "t", 2)
+        assert code == 200
+        assert pc.kill_worker() == -9
+        pc.restart_container("default", "t")
+        pc.restart_worker()
+        t0 = time.time()
+        while pc.audit("default", "t") and time.time() - t0 < 5:
+            time.sleep(0.05)
+        assert pc.audit("default", "t") == [], "not repaired at startup"
+        assert time.time() - t0 < 5
+    finally:
+        pc.stop()
+
+
 # ------------------------------------------------------------------------------ PID reuse
 def test_pinned_pidfd_never_signals_after_exit():
     """A pinned PID whose process exited and was reaped: signalling reports ESRCH instead of
