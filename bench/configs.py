@@ -323,7 +323,7 @@ def chaos(args) -> dict:
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": str(args.reconcile_period),
            "GM_WARM_POOL_SIZE": str(args.warm_pool)}
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
-                        gpu_api=args.gpu_api) as pc:
+                        gpu_api=args.gpu_api, log_dir=args.log_dir) as pc:
         for t in tenants:
             pc.tenant(t)
         if args.api_fault_rate:
@@ -578,6 +578,8 @@ def main() -> int:
                          "rounds")
     ap.add_argument("--reconcile-period", type=float, default=0.5,
                     help="chaos: the worker's periodic sweep (GM_RECONCILE_PERIOD_S; shipped 30)")
+    ap.add_argument("--log-dir", default="",
+                    help="chaos: keep the daemons' logs here (default: the cluster's temp dir)")
     ap.add_argument("--kill-every", type=int, default=10,
                     help="chaos: SIGKILL the worker with requests in flight every N rounds")
     ap.add_argument("--node-ops", choices=("emulated", "real"), default="emulated",

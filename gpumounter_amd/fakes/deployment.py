@@ -111,7 +111,8 @@ class ProcessCluster:
 
     # ------------------------------------------------------------------------ lifecycle
     def _spawn(self, key: str, argv: List[str], env: Dict[str, str]) -> subprocess.Popen:
-        log = open(os.path.join(self.log_dir, f"{key}.log"), "w")
+        # appended: a restarted daemon's log follows its predecessor's (chaos post-mortems)
+        log = open(os.path.join(self.log_dir, f"{key}.log"), "a")
         full = {**os.environ, "PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
                 **env}
         p = subprocess.Popen([sys.executable, *argv], cwd=ROOT, env=full, stdout=log,

@@ -112,6 +112,13 @@ class Reconciler:
     # before it is left to the periodic sweep, which may be 30 s away
     RETRY_DELAYS = (0.1, 0.5, 2.0, 5.0)
 
+    def follow_up(self, ns: str, name: str, drop=()) -> None:
+        """Finish what a failed operation on ``ns/name`` left: release the placeholders in
+        ``drop`` that still exist, then reconcile the Pod to its ledger. Retried with backoff
+        (the kubelet restarting, the apiserver failing) like an event reaction."""
+        self._kick(("followup", ns, name,
+                    tuple(sorted((p.namespace, p.name, p.uid) for p in drop))))
+
     def _kick(self, key: tuple, attempt: int = 0) -> None:
         if key in self._kicked:
             return
@@ -146,6 +153,8 @@ class Reconciler:
                                             for p in phs])
                         svc.metrics.orphans.labels(kind="owner_gone").inc(len(phs))
                 else:
+                    if key[0] == "followup" and key[3]:
+                        await self._drop(key[3])
                     owner = svc.node_pods.get(ns, name)
                     if owner is None or podu.phase_of(owner) != "Running":
                         return
@@ -167,6 +176,19 @@ class Reconciler:
             svc.metrics.reconcile_actions.labels(action="event_retry").inc()
             self._retry(key, attempt + 1)
 
+    async def _drop(self, phs) -> None:
+        """Release the placeholders of a failed attach that still exist (same UID)."""
+        svc = self.svc
+        left = []
+        for ns, name, uid in phs:
+            p = svc.ph.informer.cache.get((ns, name))
+            if p is not None and (not uid or p["metadata"].get("uid") == uid) and \
+                    not p["metadata"].get("deletionTimestamp"):
+                left.append(svc.ph.cached(p) or svc.ph.from_pod(p, {}))
+        if left:
+            await svc._release(left)
+            svc.metrics.reconcile_actions.labels(action="followup_release").inc(len(left))
+
     async def start(self) -> None:
         self._task = asyncio.ensure_future(self._loop())
 
@@ -183,21 +205,31 @@ class Reconciler:
             except (asyncio.CancelledError, Exception):  # noqa: BLE001
                 pass
 
+    # a sweep that could not finish everything (the kubelet restarting, the apiserver failing, a
+    # kernel call refused) runs again after these delays rather than a whole period later
+    SWEEP_RETRY_DELAYS = (0.5, 2.0, 5.0, 10.0)
+
     async def _loop(self) -> None:
         # the first sweep runs at once: whatever changed while no worker was running (a
         # container restarted, a Pod deleted, an attach cut off by the previous worker's death)
         # sent its events to nobody, and the next periodic sweep may be 30 s away
-        first = True
+        delay, failures = 0.0, 0
         while True:
-            if not first:
-                await asyncio.sleep(self.period_s)
-            first = False
+            if delay:
+                await asyncio.sleep(delay)
             try:
-                await self.run_once()
+                ok = not (await self.run_once()).errors
             except asyncio.CancelledError:
                 raise
             except Exception as e:  # noqa: BLE001
                 _log.exception("reconcile failed: %s", e)
+                ok = False
+            if ok:
+                delay, failures = self.period_s, 0
+            else:
+                delay = min(self.period_s, self.SWEEP_RETRY_DELAYS[
+                    min(failures, len(self.SWEEP_RETRY_DELAYS) - 1)])
+                failures += 1
 
     async def _sweep_claims(self) -> List[str]:
         """DRA mode: our ResourceClaims whose placeholder Pod does not exist (a worker that died

@@ -128,6 +128,7 @@ class Worker:
                 metrics=self.metrics)
             self.service.plugin = self.plugin
         self.reconciler = Reconciler(self.service, cfg.reconcile_period_s)
+        self.service.followup = self.reconciler.follow_up
         if cfg.reconcile_on_events:
             self.reconciler.watch_events()
         self.grpc_server: Optional[grpc.aio.Server] = None

@@ -163,6 +163,10 @@ class GpuMountService:
         self.ledger_reads = 0
         self.ledger_reads_checkpoint = 0
         self.adopted = False           # adopt_existing() has run to completion
+        # the Reconciler, when the Worker runs one: what a failed operation could not finish (a
+        # placeholder release, the rollback to the ledger) is retried with backoff, not left to
+        # the periodic sweep (30 s as shipped)
+        self.followup = None
 
     # ------------------------------------------------------------------------ helpers
     def pod_lock(self, ns: str, name: str) -> asyncio.Lock:
@@ -364,8 +368,25 @@ class GpuMountService:
                 log.kv(_log, 30, f"{what} rolled back to ledger state",
                        pod=f"{podu.ns_of(pod)}/{podu.name_of(pod)}", fixed=len(fixed))
         except Exception as e:  # noqa: BLE001
-            _log.error("rollback after %s failed (the reconciler will retry): %s", what, e)
+            _log.error("rollback after %s failed (retried by the reconciler): %s", what, e)
+            self._follow_up(pod)
         return False
+
+    def _follow_up(self, pod: dict, drop: Sequence[Placeholder] = ()) -> None:
+        """Hand what this operation could not finish to the reconciler's retrying follow-up:
+        release ``drop`` (placeholders of a failed attach) and reconcile the pod to its ledger."""
+        if self.followup is not None:
+            self.followup(podu.ns_of(pod), podu.name_of(pod), drop)
+
+    async def _release_or_follow_up(self, pod: dict, phs: Sequence[Placeholder],
+                                    what: str) -> None:
+        """Release a failed attach's placeholders; one that cannot be deleted now is retried by
+        the reconciler until it is (its GPU is nobody's: the client was told the attach failed)."""
+        try:
+            await self._release(phs)
+        except Exception as e:  # noqa: BLE001
+            _log.error("placeholder release after %s: %s", what, e)
+            self._follow_up(pod, phs)
 
     @staticmethod
     def _devices(gs: Sequence[AmdGpu], owner: Dict[int, str]) -> List:
@@ -491,10 +512,7 @@ class GpuMountService:
                             f"{i.container}:{i.kind}:{i.path}" for i in issues[:4]))
             except (MountError, InjectedFault) as e:
                 _log.error("mount failed on %s/%s: %s", req.namespace, req.pod_name, e)
-                try:
-                    await self._release(res.placeholders)
-                except Exception as e2:  # noqa: BLE001
-                    _log.error("placeholder release after failed mount: %s", e2)
+                await self._release_or_follow_up(pod, res.placeholders, "a failed mount")
                 if await self._rollback(pod, "attach"):   # deleted while we were attaching
                     return api.AddGPUResponse(add_gpu_result=api.ADD_POD_NOT_FOUND,
                                               message=f"pod went away during the attach: {e}")
@@ -505,7 +523,7 @@ class GpuMountService:
                     expires = await self.lease.grant(pod, res.placeholders, req.lease_s)
                 except Exception as e:  # noqa: BLE001 - a lease must not be silently dropped
                     _log.error("lease on %s/%s not recorded: %s", req.namespace, req.pod_name, e)
-                    await self._release(res.placeholders)
+                    await self._release_or_follow_up(pod, res.placeholders, "an unrecorded lease")
                     await self._rollback(pod, "attach")
                     raise RpcError(grpc.StatusCode.INTERNAL,
                                    f"{ERR_INTERNAL}: lease not recorded: {e}") from e
@@ -682,27 +700,28 @@ class GpuMountService:
                 InjectedFault) as e:
             # QuotaExceeded: in tenant-namespace mode the extra holds count against the
             # tenant's ResourceQuota at the apiserver
-            await self._release_quiet(extra)
+            await self._release_quiet(pod, extra)
             if held:
                 _log.warning("placement correction failed, keeping the plugin's choice: %s", e)
                 return res
             raise
         if sum(len(p.device_ids) for p in new.placeholders) != n:
-            await self._release_quiet(held + extra)
+            await self._release_quiet(pod, held + extra)
             raise InsufficientGPU(f"placement correction could not hold {n} GPUs")
         self.metrics.placement_corrections.inc()
         new.preferred = new.device_ids
         if surplus:
             with trace.span("placement_release", placeholders=len(surplus)):
-                await self._release_quiet(surplus)
+                await self._release_quiet(pod, surplus)
         return new
 
-    async def _release_quiet(self, phs) -> None:
+    async def _release_quiet(self, pod: dict, phs) -> None:
         try:
             await self._release([p for p in phs if p.device_ids]
                                 + [p for p in phs if not p.device_ids])
-        except Exception as e:  # noqa: BLE001 - the reconciler collects leftovers
+        except Exception as e:  # noqa: BLE001 - the reconciler's follow-up retries
             _log.error("releasing placeholders: %s", e)
+            self._follow_up(pod, phs)
 
     async def _reserve_unlocked(self, pod: dict, n: int, req, st: PodGpuState,
                                 preferred: List[str], n_free: int):
@@ -801,11 +820,7 @@ class GpuMountService:
         res.preferred = res.device_ids                    # trim keeps exactly what it picked
         if surplus:
             with trace.span("placement_release", placeholders=len(surplus)):
-                try:
-                    await self._release([p for p in surplus if p.device_ids]
-                                        + [p for p in surplus if not p.device_ids])
-                except Exception as e:  # noqa: BLE001 - the reconciler collects leftovers
-                    _log.error("releasing surplus placeholders: %s", e)
+                await self._release_quiet(pod, surplus)
         return res
 
     def _free(self, st: PodGpuState) -> List[AmdGpu]:

@@ -984,3 +984,71 @@ def test_failed_event_reaction_is_retried_before_the_periodic_sweep():
         assert not await lc.audit("default", "r") and len(calls) == 2
         assert w.metrics.reconcile_actions.labels(action="event_retry")._value.get() == 1
     run(body)
+
+
+def test_failed_attach_whose_cleanup_fails_is_followed_up_before_the_periodic_sweep():
+    """An attach fails after its placeholder was admitted; releasing that placeholder fails
+    (apiserver error) and so does the rollback's ledger read (the kubelet restarting). Both are
+    handed to the reconciler's retrying follow-up: the placeholder is released and the Pod is
+    left exactly as its ledger says within a second — LocalCluster runs no periodic sweep."""
+    from gpumounter_amd.cluster.placeholder import ReserveError
+    from gpumounter_amd.node.ledger import LedgerError
+
+    async def body(lc):
+        lc.tenant("f")
+        w = lc.nodes["node-0"].worker
+        svc = w.service
+        real_release, real_by_pod = svc.ph.release, svc.ledger.by_pod
+        calls = {"rel": 0, "led": -1}
+
+        async def release(phs, *a, **k):
+            calls["rel"] += 1
+            if calls["rel"] == 1:
+                calls["led"] = 0          # the rollback's ledger read fails next
+                raise ReserveError("could not delete 1 placeholder(s): injected")
+            return await real_release(phs, *a, **k)
+
+        async def by_pod(*a, **k):
+            if calls["led"] >= 0:
+                calls["led"] += 1
+            if calls["led"] == 1:
+                raise LedgerError("kubelet PodResources socket unavailable")
+            return await real_by_pod(*a, **k)
+        svc.ph.release, svc.ledger.by_pod = release, by_pod
+        def held():
+            return [p for p in lc.cluster.placeholders() if (p["metadata"].get("annotations")
+                    or {}).get("gpumounter.amd.com/owner-name") == "f"]
+        code, _ = await lc.add("default", "f", 1)
+        assert code == 500
+        for _ in range(100):
+            await asyncio.sleep(0.02)
+            if not held() and not await lc.audit("default", "f"):
+                break
+        assert not held()
+        assert not await lc.audit("default", "f")
+        assert not node_of(lc).container_devices(lc.container_ids("default", "f")[0])
+        assert calls["rel"] >= 2 and calls["led"] >= 2
+        assert w.metrics.reconcile_actions.labels(action="followup_release")._value.get() == 1
+    run(body, worker_overrides={"fault": "devnodes:1.0:after"})
+
+
+def test_sweep_that_hit_errors_runs_again_before_the_next_period():
+    """A sweep that could not finish (here: its ledger read failed) is repeated after a short
+    backoff, not a whole period (30 s as shipped) later; a clean one waits the period."""
+    from gpumounter_amd.worker.reconciler import ReconcileReport, Reconciler
+
+    async def main():
+        r = Reconciler(service=None, period_s=30.0)
+        reports = [ReconcileReport(errors=["ledger: kubelet restarting"]), ReconcileReport()]
+        calls = []
+
+        async def run_once():
+            calls.append(asyncio.get_running_loop().time())
+            return reports[min(len(calls), len(reports)) - 1]
+        r.run_once = run_once
+        await r.start()
+        await asyncio.sleep(1.0)
+        await r.stop()
+        assert len(calls) == 2                       # at once, again after 0.5 s, then 30 s
+        assert 0.4 < calls[1] - calls[0] < 0.9
+    asyncio.run(main())
