@@ -322,6 +322,8 @@ def chaos(args) -> dict:
     api_faults = [0]
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": str(args.reconcile_period),
            "GM_WARM_POOL_SIZE": str(args.warm_pool)}
+    if args.log_dir:
+        env["GM_LOG_LEVEL"] = "INFO"       # kept logs are for post-mortems
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
                         gpu_api=args.gpu_api, log_dir=args.log_dir) as pc:
         for t in tenants:

@@ -29,7 +29,7 @@ from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models.device import AmdGpu, DeviceNode, kfd_node
 from gpumounter_amd.models.pod import ContainerRef, running_containers
 from gpumounter_amd.node.cgroup import CgroupError, CgroupResolver, DeviceRuleBackend
-from gpumounter_amd.node.devnodes import CREATED, DevNodeWriter, Target
+from gpumounter_amd.node.devnodes import CREATED, DevNodeError, DevNodeWriter, Target
 from gpumounter_amd.node.journal import InjectionJournal
 from gpumounter_amd.utils import log, trace
 
@@ -226,6 +226,16 @@ class HotMount:
         if targets is None:
             with trace.span("resolve"):
                 targets = self.resolve(pod, container)
+        try:
+            self._detach(targets, revoke, after)
+        except (CgroupError, DevNodeError, OSError) as e:
+            # a container that went away meanwhile (restart, deletion): the caller rolls the pod
+            # back to its ledger state, which covers the container running now
+            raise MountError(f"detach failed: {e}") from e
+        return targets
+
+    def _detach(self, targets: List[ContainerTarget], revoke: List[DeviceNode],
+                after: List[DeviceNode]) -> None:
         keys = [(n.major, n.minor) for n in revoke]
         for t in targets:
             # reference order: deny → rm → kill (util.go:112,131,139)
@@ -243,7 +253,6 @@ class HotMount:
             # rules journaled, which the audit forgets on sight (not in the kernel any more),
             # and its nodes, which the orphan sweep unlinks
             self.journal.forget(t.ref.id, keys, keys)
-        return targets
 
     def adopt(self, pod: dict, hot: Sequence[AmdGpu], base: Sequence[AmdGpu] = ()) -> int:
         """Seed the journal for containers of a pod that holds hot-mounted GPUs but has no
@@ -344,7 +353,16 @@ class HotMount:
         every node is read back in one native call."""
         want = self.managed_nodes(hot, base)
         issues: List[AuditIssue] = []
-        for t in targets if targets is not None else self.targets(pod, container):
+        try:
+            return self._verify(want, targets if targets is not None
+                                else self.targets(pod, container), issues)
+        except (CgroupError, DevNodeError, OSError) as e:
+            # a container that restarted or went away after the mount: the attach rolls back
+            raise MountError(f"read-back failed: {e}") from e
+
+    def _verify(self, want: List[DeviceNode], targets: List[ContainerTarget],
+                issues: List[AuditIssue]) -> List[AuditIssue]:
+        for t in targets:
             allowed = self.backend.allowed(t.cgdir)
             present = self.writer.present_many(t.target, want)
             for n, ok in zip(want, present):

@@ -19,11 +19,14 @@ All repairs take the same per-pod lock as AddGPU/RemoveGPU.
 The reference has no sweep at all; its only revocation path is RemoveGPU on the ledger-selected
 GPUs of the named pod (reference: pkg/util/util.go:73-147, allocator.go:101-126).
 
-Two events are handled immediately instead of at the next sweep (:meth:`watch_events`): a
+Events are handled immediately instead of at the next sweep (:meth:`watch_events`): a
 placeholder deleted by someone else (kubectl, eviction, preemption — its GPU goes back to the
-scheduler, so the tenant's access is revoked within milliseconds, not a period later) and a
-tenant pod that is deleted or finished (its placeholders are released at once in ``pool``
-namespace mode, where no garbage collector does it).
+scheduler, so the tenant's access is revoked within milliseconds, not a period later), a tenant
+pod that is deleted or finished (its placeholders are released at once in ``pool`` namespace
+mode, where no garbage collector does it) and a container restart (the hot-mounted GPUs go back
+into the new container). A failed reaction is retried with backoff, and so is what a failed
+attach/detach could not clean up (:meth:`follow_up`). A watch that relists missed events, so a
+relist wakes the sweep; a sweep that hit errors runs again after a short backoff.
 """
 from __future__ import annotations
 
@@ -69,11 +72,25 @@ class Reconciler:
         self._timers: Dict[tuple, asyncio.TimerHandle] = {}   # retries of failed reactions
         self._bg: set = set()
         self.event_actions = 0
+        self._wake = asyncio.Event()
+        self._last_sweep = 0.0
+        self.woken = 0
 
     # ------------------------------------------------------------------------ events
     def watch_events(self) -> None:
         self.svc.ph.on_foreign_delete.append(self._on_foreign_delete)
         self.svc.node_pods.handlers.append(self._on_node_pod)
+        self.svc.ph.informer.handlers.append(self._on_relist)
+
+    def _on_relist(self, etype: str, _obj: dict) -> None:
+        if etype == "RELIST":
+            self.wake()
+
+    def wake(self) -> None:
+        """Sweep now rather than at the next period: a watch relisted (410 Gone, a dropped
+        stream), so the events it missed — a container restart, a Pod or placeholder deleted —
+        reached no reaction; the sweep finds what they would have triggered."""
+        self._wake.set()
 
     def _on_foreign_delete(self, ph: dict) -> None:
         md = ph["metadata"]
@@ -88,6 +105,9 @@ class Reconciler:
             self._kick(("revoke", ons, oname))
 
     def _on_node_pod(self, etype: str, pod: dict) -> None:
+        if etype == "RELIST":
+            self.wake()
+            return
         if etype == "DELETED" or podu.phase_of(pod) in ("Succeeded", "Failed"):
             if self.svc.ph.owned_by(pod, candidates=True):
                 self._kick(("release", podu.ns_of(pod), podu.name_of(pod), podu.uid_of(pod)))
@@ -208,15 +228,27 @@ class Reconciler:
     # a sweep that could not finish everything (the kubelet restarting, the apiserver failing, a
     # kernel call refused) runs again after these delays rather than a whole period later
     SWEEP_RETRY_DELAYS = (0.5, 2.0, 5.0, 10.0)
+    # woken sweeps (relists) run at most this often: a flapping watch must not turn into a
+    # PodResources List per relist
+    WAKE_MIN_INTERVAL_S = 1.0
 
     async def _loop(self) -> None:
         # the first sweep runs at once: whatever changed while no worker was running (a
         # container restarted, a Pod deleted, an attach cut off by the previous worker's death)
         # sent its events to nobody, and the next periodic sweep may be 30 s away
         delay, failures = 0.0, 0
+        loop = asyncio.get_running_loop()
         while True:
             if delay:
-                await asyncio.sleep(delay)
+                try:
+                    await asyncio.wait_for(self._wake.wait(), delay)
+                    self.woken += 1
+                    await asyncio.sleep(max(0.0, self._last_sweep + self.WAKE_MIN_INTERVAL_S
+                                            - loop.time()))
+                except asyncio.TimeoutError:
+                    pass
+            self._wake.clear()
+            self._last_sweep = loop.time()
             try:
                 ok = not (await self.run_once()).errors
             except asyncio.CancelledError:

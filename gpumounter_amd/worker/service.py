@@ -353,6 +353,12 @@ class GpuMountService:
                    owners=len(owners))
         return n
 
+    def _current(self, pod: dict) -> dict:
+        """The pod as the node informer holds it now (same UID): a container restart seen
+        while this request waited for the pod's lock must not send it to the old container."""
+        cur = self.node_pods.get(podu.ns_of(pod), podu.name_of(pod))
+        return cur if cur is not None and podu.uid_of(cur) == podu.uid_of(pod) else pod
+
     async def _rollback(self, pod: dict, what: str) -> bool:
         """Reconcile the pod to its ledger state after a failed operation. Returns True if the
         pod itself is gone (deleted or replaced meanwhile): nothing is left to repair then."""
@@ -451,6 +457,7 @@ class GpuMountService:
             raise RpcError(grpc.StatusCode.FAILED_PRECONDITION,
                            f"{ERR_POLICY}: the gpumounter worker pod itself is never a target")
         async with self.pod_lock(req.namespace, req.pod_name):
+            pod = self._current(pod)
             if podu.phase_of(pod) != "Running":
                 pod = await self.get_pod(req.namespace, req.pod_name, fresh=True)
                 if pod is None:
@@ -499,6 +506,7 @@ class GpuMountService:
                     sorted(normalize_device_id(d) for d in want):
                 self.metrics.placement_mismatch.inc()
             try:
+                pod = self._current(pod)         # a restart seen while reserving
                 with trace.span("mount", gpus=len(new)):
                     targets = self.hm.attach(pod, new, st.hot, st.own, req.container)
                 if self.cfg.attach_verify:
@@ -874,6 +882,7 @@ class GpuMountService:
         if pod is None:
             return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_POD_NOT_FOUND)
         async with self.pod_lock(req.namespace, req.pod_name):
+            pod = self._current(pod)
             with trace.span("ledger_read"):
                 st = await self.pod_state(pod)
             if st.mount_type == MountType.UNKNOWN:

@@ -1052,3 +1052,88 @@ def test_sweep_that_hit_errors_runs_again_before_the_next_period():
         assert len(calls) == 2                       # at once, again after 0.5 s, then 30 s
         assert 0.4 < calls[1] - calls[0] < 0.9
     asyncio.run(main())
+
+
+def test_container_restart_during_an_attach_gets_the_gpus():
+    """The tenant's container restarts while its first attach is reserving: the Pod event comes
+    before the placeholder exists, so the event-driven re-injection does not see a Pod with
+    hot-mounted GPUs. The attach mounts the container running now, not the one it looked up
+    (no periodic sweep here)."""
+    async def body(lc):
+        lc.tenant("c")
+        svc = lc.nodes["node-0"].worker.service
+        real = svc.ph.reserve
+        restarted = []
+
+        async def reserve(*a, **k):
+            res = await real(*a, **k)
+            if not restarted:
+                restarted.append(lc.cluster.restart_container("default", "c", "main"))
+                await asyncio.sleep(0.05)        # the Pod event is delivered meanwhile
+            return res
+        svc.ph.reserve = reserve
+        code, b = await lc.add("default", "c", 1)
+        svc.ph.reserve = real
+        assert code == 200 and restarted
+        assert lc.container_ids("default", "c") == restarted
+        assert not await lc.audit("default", "c")
+        devs = node_of(lc).container_devices(restarted[0])
+        assert sum("renderD" in d for d in devs) == 1 and "dev/kfd" in devs
+    run(body)
+
+
+def test_container_restart_between_mount_and_read_back_rolls_the_attach_back():
+    """The container restarts between the mount and its read-back (the control plane runs in
+    another process, so this interleaving is real): the read-back fails on the vanished
+    container, and the attach is rolled back — placeholder released, nothing in the new
+    container — instead of escaping unhandled with its placeholder left behind."""
+    async def body(lc):
+        lc.tenant("v")
+        svc = lc.nodes["node-0"].worker.service
+        real_attach = svc.hm.attach
+
+        def attach(*a, **k):
+            out = real_attach(*a, **k)
+            lc.cluster.restart_container("default", "v", "main")
+            return out
+        svc.hm.attach = attach
+        code, _ = await lc.add("default", "v", 1)
+        svc.hm.attach = real_attach
+        assert code == 500
+        assert not [p for p in lc.cluster.placeholders()
+                    if (p["metadata"].get("annotations") or {}).get(
+                        "gpumounter.amd.com/owner-name") == "v"]
+        assert not await lc.audit("default", "v")
+        assert not node_of(lc).container_devices(lc.container_ids("default", "v")[0])
+        code, _ = await lc.add("default", "v", 1)       # and the next attach works
+        assert code == 200 and not await lc.audit("default", "v")
+    run(body)
+
+
+def test_relist_wakes_the_sweep():
+    """A watch that relisted (410 Gone, a dropped stream) missed events, which no reaction saw:
+    the relist wakes the sweep instead of leaving their effects to the next period (30 s)."""
+    from gpumounter_amd.worker.reconciler import ReconcileReport, Reconciler
+
+    async def main():
+        r = Reconciler(service=None, period_s=30.0)
+        calls = []
+
+        async def run_once():
+            calls.append(asyncio.get_running_loop().time())
+            return ReconcileReport()
+        r.run_once = run_once
+        r.WAKE_MIN_INTERVAL_S = 0.2
+        await r.start()
+        await asyncio.sleep(0.05)
+        r._on_node_pod("RELIST", {})
+        await asyncio.sleep(0.05)
+        r._on_relist("RELIST", {})      # before the woken sweep started: that sweep covers it
+        r._on_relist("MODIFIED", {})    # not a relist
+        await asyncio.sleep(0.3)
+        assert len(calls) == 2 and calls[1] - calls[0] >= 0.19   # at most 1 per 0.2 s
+        r._on_relist("RELIST", {})      # the placeholder informer
+        await asyncio.sleep(0.3)
+        await r.stop()
+        assert len(calls) == 3 and r.woken == 2
+    asyncio.run(main())
