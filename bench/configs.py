@@ -436,6 +436,10 @@ def chaos(args) -> dict:
                 while not converged():
                     if time.perf_counter() - t0 > 20:
                         problems.append(f"round {rnd_i}: not converged after 20 s: {why[0]}")
+                        if args.log_dir:      # what the worker is waiting for
+                            with open(os.path.join(args.log_dir,
+                                                   f"tasks_round{rnd_i}.txt"), "w") as fh:
+                                fh.write(pc.worker_tasks())
                         break
                     time.sleep(0.05)
                 converge.append((time.perf_counter() - t0) * 1e3)

@@ -378,6 +378,11 @@ class ProcessCluster:
             raise RuntimeError(f"audit {ns}/{pod}: {code} {body[:300]!r}")
         return json.loads(body)["issues"]
 
+    def worker_tasks(self, node: str = "node-0") -> str:
+        """The worker's asyncio tasks and their stacks (``/debug/tasks``)."""
+        return _http("GET", f"http://127.0.0.1:{self.worker_ports[node][1]}/debug/tasks")[1] \
+            .decode()
+
     def worker_metrics(self, node: str = "node-0") -> str:
         return _http("GET", f"http://127.0.0.1:{self.worker_ports[node][1]}/metrics")[1].decode()
 

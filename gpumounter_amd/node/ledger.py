@@ -51,6 +51,7 @@ class LedgerClient:
         self._chan: Optional[grpc.aio.Channel] = None
         self._chan_loop = None
         self._stubs: Dict[str, object] = {}
+        self._closing: set = set()
         self.calls = 0
         self._get_ok: Optional[bool] = None   # v1 Get served? (feature-gated in kubelets)
 
@@ -69,6 +70,22 @@ class LedgerClient:
             self._stubs = {}
         return self._chan
 
+    def _retire(self, failed: grpc.aio.Channel) -> None:
+        """Stop handing out a channel that answered UNAVAILABLE. It is closed only once every
+        call that may still be running on it has met its deadline: closing a grpc-aio channel
+        cancels its calls, and the CancelledError that raises in *other* coroutines (a
+        concurrent attach, the reconciler's sweep) reads as their own cancellation — it skipped
+        their error handling and ended the sweep loop."""
+        if self._chan is failed:
+            self._chan = None
+        loop = asyncio.get_running_loop()
+
+        def close() -> None:
+            t = loop.create_task(failed.close())
+            self._closing.add(t)
+            t.add_done_callback(self._closing.discard)
+        loop.call_later(self.timeout_s + 1.0, close)
+
     async def _call(self, path: str, req_cls, resp_cls, req):
         """One unary call, paced by the client token bucket. RESOURCE_EXHAUSTED (the kubelet's
         rate limiter) is retried with jittered backoff (10 ms doubling to 200 ms) until the call's
@@ -80,6 +97,7 @@ class LedgerClient:
         while True:
             if self.bucket is not None:
                 await self.bucket.acquire()
+            ch = self._channel()
             try:
                 return await self._stub(path, req_cls, resp_cls)(
                     req, timeout=max(deadline - loop.time(), 0.001))
@@ -96,9 +114,7 @@ class LedgerClient:
                 if code != grpc.StatusCode.UNAVAILABLE:
                     raise
                 break
-        old, self._chan = self._chan, None
-        if old is not None:
-            await old.close()
+        self._retire(ch)
         _log.info("PodResources socket %s unavailable; reconnecting", self.socket_path)
         return await self._stub(path, req_cls, resp_cls)(
             req, timeout=min(self.timeout_s, 2.0), wait_for_ready=True)

@@ -72,6 +72,7 @@ class Reconciler:
         self._timers: Dict[tuple, asyncio.TimerHandle] = {}   # retries of failed reactions
         self._bg: set = set()
         self.event_actions = 0
+        self._stopping = False
         self._wake = asyncio.Event()
         self._last_sweep = 0.0
         self.woken = 0
@@ -191,6 +192,13 @@ class Reconciler:
                                          f"{', '.join(back)}")
                 self.event_actions += 1
                 svc.metrics.reconcile_actions.labels(action=f"event_{key[0]}").inc()
+        except asyncio.CancelledError:
+            if self._stopping:
+                raise
+            # not ours: something this reaction awaited was cancelled under it (see _loop)
+            _log.error("event-driven reconcile %s was cancelled (attempt %d)", key, attempt + 1)
+            svc.metrics.reconcile_actions.labels(action="event_retry").inc()
+            self._retry(key, attempt + 1)
         except Exception as e:  # noqa: BLE001 - retried, then the periodic sweep
             _log.error("event-driven reconcile %s failed (attempt %d): %s", key, attempt + 1, e)
             svc.metrics.reconcile_actions.labels(action="event_retry").inc()
@@ -213,6 +221,7 @@ class Reconciler:
         self._task = asyncio.ensure_future(self._loop())
 
     async def stop(self) -> None:
+        self._stopping = True
         for h in list(self._timers.values()):
             h.cancel()
         self._timers.clear()
@@ -252,7 +261,12 @@ class Reconciler:
             try:
                 ok = not (await self.run_once()).errors
             except asyncio.CancelledError:
-                raise
+                if self._stopping:
+                    raise
+                # a CancelledError that stop() did not cause came from something the sweep
+                # awaited (a cancelled inner future): a failed sweep, not the end of the loop
+                _log.error("reconcile sweep was cancelled from within; retrying")
+                ok = False
             except Exception as e:  # noqa: BLE001
                 _log.exception("reconcile failed: %s", e)
                 ok = False

@@ -252,6 +252,7 @@ class Worker:
             app.router.add_get("/metrics", self._metrics)
             app.router.add_get("/status", self._http_status)
             app.router.add_get("/audit/{namespace}/{pod}", self._http_audit)
+            app.router.add_get("/debug/tasks", self._debug_tasks)
             self.http_runner = web.AppRunner(app, access_log=None)
             await self.http_runner.setup()
             site = web.TCPSite(self.http_runner, self.cfg.worker_host, hp)
@@ -283,6 +284,16 @@ class Worker:
 
     async def _metrics(self, request):
         return web.Response(body=self.metrics.render(), content_type="text/plain")
+
+    async def _debug_tasks(self, request):
+        """Every asyncio task of the worker with the stack it is suspended in — what a stuck
+        attach, reaction or sweep is waiting for (the goroutine dump of a Go daemon)."""
+        out = []
+        for t in sorted(asyncio.all_tasks(), key=lambda t: t.get_name()):
+            out.append(f"{t.get_name()} {t.get_coro()!r}")
+            for f in t.get_stack():
+                out.append(f"    {f.f_code.co_filename}:{f.f_lineno} {f.f_code.co_name}")
+        return web.Response(text="\n".join(out) + "\n")
 
     async def _readyz(self, request):
         return web.Response(text="ready" if self.ready else "starting",

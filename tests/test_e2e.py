@@ -1137,3 +1137,27 @@ def test_relist_wakes_the_sweep():
         await r.stop()
         assert len(calls) == 3 and r.woken == 2
     asyncio.run(main())
+
+
+def test_sweep_loop_survives_a_cancelled_inner_await():
+    """Something the sweep awaited was cancelled under it (a CancelledError that stop() did
+    not cause): that sweep failed, the loop goes on and retries after a short backoff. Only
+    stop() ends it."""
+    from gpumounter_amd.worker.reconciler import ReconcileReport, Reconciler
+
+    async def main():
+        r = Reconciler(service=None, period_s=30.0)
+        calls = []
+
+        async def run_once():
+            calls.append(1)
+            if len(calls) == 1:
+                raise asyncio.CancelledError()
+            return ReconcileReport()
+        r.run_once = run_once
+        await r.start()
+        await asyncio.sleep(0.8)
+        assert len(calls) == 2 and not r._task.done()
+        await r.stop()
+        assert r._task.done()
+    asyncio.run(main())

@@ -141,3 +141,56 @@ def test_count_mode_serves_and_counts_over_budget_calls(tmp_path):
     assert calls["rejected"] == 0 and calls["over_limit"] >= 3
     with pytest.raises(ValueError):
         FakeKubelet(node, sock, limit_mode="drop")
+
+
+def test_kubelet_restart_does_not_cancel_other_callers_calls(monkeypatch):
+    """Three PodResources calls are in flight when the kubelet restarts. The first to see
+    UNAVAILABLE moves the client to a new channel; the old one must not be closed under the
+    other two: closing a grpc-aio channel cancels its calls, and that CancelledError surfaced in
+    unrelated coroutines (a concurrent attach, the reconciler's sweep loop, which ended)."""
+    import grpc
+
+    channels = []
+
+    class Channel:
+        def __init__(self, target, options=None):
+            self.gen = len(channels)
+            self.pending = []
+            self.closed = False
+            channels.append(self)
+
+        def unary_unary(self, path, request_serializer=None, response_deserializer=None):
+            async def call(req, timeout=None, wait_for_ready=False):
+                if self.closed:
+                    raise asyncio.CancelledError()
+                if self.gen == 0:                 # the kubelet went away under these calls
+                    fut = asyncio.get_running_loop().create_future()
+                    self.pending.append(fut)
+                    await fut
+                    raise grpc.aio.AioRpcError(grpc.StatusCode.UNAVAILABLE, None, None,
+                                               "socket closed")
+                return f"listed on channel {self.gen}"
+            return call
+
+        async def close(self, grace=None):
+            self.closed = True
+            for f in self.pending:
+                if not f.done():
+                    f.cancel()
+
+    monkeypatch.setattr(grpc.aio, "insecure_channel", Channel)
+
+    async def main():
+        led = LedgerClient("/nonexistent.sock", "amd.com/gpu", timeout_s=2.0, qps=0)
+        msg = type("Msg", (), {"SerializeToString": staticmethod(lambda m: b""),
+                               "FromString": staticmethod(lambda b: b)})
+        calls = [asyncio.ensure_future(led._call("/List", msg, msg, msg())) for _ in range(3)]
+        await asyncio.sleep(0.01)
+        for f in list(channels[0].pending):      # they fail one after the other
+            if not f.done():
+                f.set_result(None)
+            await asyncio.sleep(0.01)
+        out = await asyncio.gather(*calls, return_exceptions=True)
+        assert all(isinstance(o, str) for o in out), out
+        assert len(channels) == 2 and not channels[0].closed   # retired, closed later
+    asyncio.run(main())
