@@ -321,7 +321,7 @@ def chaos(args) -> dict:
     problems, converge = [], []
     api_faults = [0]
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": str(args.reconcile_period),
-           "GM_WARM_POOL_SIZE": str(args.warm_pool)}
+           "GM_WARM_POOL_SIZE": str(args.warm_pool), "GM_PLACEMENT_ENFORCE": args.placement}
     if args.log_dir:
         env["GM_LOG_LEVEL"] = "INFO"       # kept logs are for post-mortems
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
@@ -482,7 +482,7 @@ def chaos(args) -> dict:
             "converge_max_ms": round(max(converge), 1),
             "invariant_violations": len(problems), "violation_examples": problems[:5],
             "faults": CHAOS_FAULTS, "api_fault_rate": args.api_fault_rate,
-            "reconcile_period_s": args.reconcile_period,
+            "reconcile_period_s": args.reconcile_period, "placement": args.placement,
             "api_faults_served": api_faults[0]}
 
 

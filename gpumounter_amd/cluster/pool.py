@@ -31,8 +31,8 @@ from gpumounter_amd.cluster.placeholder import (ANN_GPUS, InsufficientGPU, LABEL
 from gpumounter_amd.hw import topology
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu, normalize_device_id
-from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CONTAINER, ANN_GROUP, ANN_IDEMPOTENCY,
-                                         ANN_MOUNT_MODE,
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTAINER, ANN_GROUP,
+                                         ANN_IDEMPOTENCY, ANN_MOUNT_MODE,
                                          ANN_OWNER_NAME, ANN_OWNER_UID, LABEL_APP,
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          MODE_STANDBY)
@@ -241,7 +241,7 @@ class WarmPool:
                                 ANN_OWNER_NAME: podu.name_of(owner), ANN_MOUNT_MODE: mode,
                                 ANN_ATTACH_ID: attach_id, ANN_CONTAINER: container,
                                 ANN_IDEMPOTENCY: idempotency_key or None,
-                                ANN_GROUP: group or None}}}
+                                ANN_GROUP: group or None, ANN_CANDIDATE: None}}}
             for ph in chosen:
                 self._claimed.add(ph.uid)
             with trace.span("pool_claim", placeholders=len(chosen)):
@@ -276,7 +276,11 @@ class WarmPool:
             "labels": {LABEL_OWNER: None, LABEL_OWNER_NS: None},
             "annotations": {ANN_OWNER_UID: None, ANN_OWNER_NAME: None,
                             ANN_MOUNT_MODE: MODE_STANDBY, ANN_ATTACH_ID: None,
-                            ANN_CONTAINER: None, ANN_GROUP: None, ANN_IDEMPOTENCY: None}}}
+                            ANN_CONTAINER: None, ANN_GROUP: None, ANN_IDEMPOTENCY: None,
+                            # surplus of a trim/correction pick comes back as candidates: a
+                            # claimed one still marked would be invisible to its new owner's
+                            # ledger view, and released under it as an abandoned pick
+                            ANN_CANDIDATE: None}}}
         epoch = self.ph.informer.epoch
         res = await asyncio.gather(*[self.ph.kube.patch_pod(p.namespace, p.name, patch)
                                      for p in phs], return_exceptions=True)

@@ -160,3 +160,40 @@ def test_failed_claim_whose_patch_took_effect_is_undone():
                        for p in owned for c in p["spec"]["containers"]) == 2
             assert not await lc.audit("default", "t")
     asyncio.run(main())
+
+
+def test_pick_surplus_returned_to_the_pool_is_no_candidate_for_its_next_owner():
+    """A trim/correction pick holds every free GPU with *candidate* placeholders and gives the
+    surplus back to the warm pool. Back in the pool they must lose the candidate mark: a
+    tenant that later claimed one would otherwise not see it in its ledger view (candidates are
+    nobody's yet), the audit would call its mounted GPU stale, and the reconciler would release
+    it as an abandoned pick — the GPU back to the scheduler, the tenant still using it."""
+    from gpumounter_amd.models.types import ANN_CANDIDATE
+
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 1}) as lc:
+            pool = await wait_pool(lc, 1)
+            w = lc.nodes["node-0"].worker
+            svc = w.service
+            lc.tenant("a")
+            lc.tenant("b")
+            a = lc.cluster.get("default", "a")
+            held = await svc.ph.hold_singles(a, 2, False, "", "rid-pick", "", "")
+            assert len(held) == 2 and all(p.candidate for p in held)
+            pool.target = 3                      # room for both
+            await pool.give_back(held)
+            back = [p for p in lc.cluster.placeholders()
+                    if p["metadata"]["name"] in {h.name for h in held}]
+            assert len(back) == 2 and all(is_standby(p) for p in back)
+            assert not any(ANN_CANDIDATE in (p["metadata"].get("annotations") or {})
+                           for p in back)
+            pool.target = 1
+            code, b = await lc.add("default", "b", 3)
+            assert code == 200
+            owned = svc.ph.owned_by(lc.cluster.get("default", "b"))
+            assert sum(len(svc.ph.cached(p).device_ids) for p in owned) == 3
+            assert not await lc.audit("default", "b")
+            await w.reconciler.run_once()
+            assert len(svc.ph.owned_by(lc.cluster.get("default", "b"))) == len(owned)
+            assert not await lc.audit("default", "b")
+    asyncio.run(main())
