@@ -952,7 +952,11 @@ def test_container_restart_gets_its_gpus_back_at_once():
         devs = node_of(lc).container_devices(new)
         assert sum("renderD" in d for d in devs) == 2 and "dev/kfd" in devs
         assert w.reconciler.event_actions >= 1
-        reasons = [e["reason"] for e in lc.cluster.events_for("default", "r")]
+        for _ in range(100):        # Events are posted off the reaction's path
+            reasons = [e["reason"] for e in lc.cluster.events_for("default", "r")]
+            if "GPUReinjected" in reasons:
+                break
+            await asyncio.sleep(0.02)
         assert "GPUReinjected" in reasons
         code, _ = await lc.remove("default", "r", [d["uuid"] for d in b["devices"]])
         assert code == 200 and not node_of(lc).container_devices(new)
