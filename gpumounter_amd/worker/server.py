@@ -165,6 +165,9 @@ class Worker:
             op.add_done_callback(self._ops.discard)
             try:
                 return await asyncio.shield(op)
+            except asyncio.CancelledError:
+                op.add_done_callback(self._orphan_done)     # its outcome reaches no caller
+                raise
             except RpcError as e:
                 await context.abort(e.code, e.msg)
             except grpc.aio.AbortError:
@@ -173,6 +176,18 @@ class Worker:
                 _log.exception("rpc failed")
                 await context.abort(grpc.StatusCode.INTERNAL, f"Service Internal Error: {e}")
         return handler
+
+    @staticmethod
+    def _orphan_done(op: asyncio.Future) -> None:
+        """An operation whose caller went away has ended: log how (and retrieve its exception,
+        which nobody else will)."""
+        if op.cancelled():
+            _log.warning("operation cancelled after its caller left")
+        elif op.exception() is not None:
+            _log.warning("operation failed after its caller left (rolled back): %s",
+                         op.exception())
+        else:
+            _log.info("operation completed after its caller left")
 
     async def _status(self, req):
         st = await self.service.node_status(req.include_processes)
