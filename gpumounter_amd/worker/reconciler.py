@@ -216,6 +216,7 @@ class Reconciler:
         if left:
             await svc._release(left)
             svc.metrics.reconcile_actions.labels(action="followup_release").inc(len(left))
+        svc.abandoned.difference_update(uid for _, _, uid in phs)
 
     async def start(self) -> None:
         self._task = asyncio.ensure_future(self._loop())
@@ -379,11 +380,14 @@ class Reconciler:
             async with lock:
                 # candidates of a trim/correction pick whose attach is not running (its worker
                 # died mid-pick): never the owner's, never mounted — give the GPUs back
+                # and placeholders of failed attaches whose release the follow-up gave up on
                 cands = [p for p in phs
-                         if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})]
+                         if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})
+                         or p["metadata"].get("uid") in svc.abandoned]
                 if cands:
                     rep.stuck += [p["metadata"]["name"] for p in cands]
                     await svc.ph.release([svc.ph.from_pod(p, {}) for p in cands], wait=False)
+                    svc.abandoned.difference_update(p["metadata"].get("uid") for p in cands)
                     phs = [p for p in phs if p not in cands]
                     m.reconcile_actions.labels(action="candidate_release").inc(len(cands))
                 # stuck placeholders (never admitted). One that an earlier worker process

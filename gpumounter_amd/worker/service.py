@@ -167,6 +167,9 @@ class GpuMountService:
         # placeholder release, the rollback to the ledger) is retried with backoff, not left to
         # the periodic sweep (30 s as shipped)
         self.followup = None
+        # placeholders of failed attaches whose release is being retried: never replayed as a
+        # success under the attach's idempotency key (the client was told it failed)
+        self.abandoned: set = set()
 
     # ------------------------------------------------------------------------ helpers
     def pod_lock(self, ns: str, name: str) -> asyncio.Lock:
@@ -381,6 +384,7 @@ class GpuMountService:
     def _follow_up(self, pod: dict, drop: Sequence[Placeholder] = ()) -> None:
         """Hand what this operation could not finish to the reconciler's retrying follow-up:
         release ``drop`` (placeholders of a failed attach) and reconcile the pod to its ledger."""
+        self.abandoned.update(p.uid for p in drop if p.uid)
         if self.followup is not None:
             self.followup(podu.ns_of(pod), podu.name_of(pod), drop)
 
@@ -572,7 +576,8 @@ class GpuMountService:
         """A retried request (same idempotency key) returns the earlier attach instead of adding
         more GPUs; the mount itself is re-checked (repair) so a half-finished attempt completes."""
         mine = {p["metadata"]["name"] for p in self.ph.owned_by(pod)
-                if (p["metadata"].get("annotations") or {}).get(ANN_IDEMPOTENCY) == key}
+                if (p["metadata"].get("annotations") or {}).get(ANN_IDEMPOTENCY) == key
+                and p["metadata"].get("uid") not in self.abandoned}
         if not mine:
             return None
         gs, owner = [], {}

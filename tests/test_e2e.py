@@ -1165,3 +1165,48 @@ def test_sweep_loop_survives_a_cancelled_inner_await():
         await r.stop()
         assert r._task.done()
     asyncio.run(main())
+
+
+def test_retry_under_the_key_of_a_failed_attach_does_not_replay_its_leftover():
+    """An attach fails and its placeholder cannot be released yet (the follow-up keeps
+    retrying). The client retries under the same Idempotency-Key: the leftover must not be
+    replayed as that request's success — the client was told it failed, and the follow-up is
+    about to release it. The retry attaches afresh."""
+    from gpumounter_amd.cluster.placeholder import ReserveError
+
+    async def body(lc):
+        lc.tenant("k")
+        w = lc.nodes["node-0"].worker
+        svc = w.service
+        real_release = svc.ph.release
+        fail = {"on": True}
+
+        async def release(phs, *a, **k):
+            if fail["on"]:
+                raise ReserveError("could not delete placeholder(s): apiserver unavailable")
+            return await real_release(phs, *a, **k)
+        svc.ph.release = release
+        url = f"{lc.master_url}/addgpu/namespace/default/pod/k/gpu/1/isEntireMount/false"
+        hdr = {"Accept": "application/json", "Idempotency-Key": "req-1"}
+        async with lc.session.get(url, headers=hdr) as r:
+            assert r.status == 500
+        left = [p for p in lc.cluster.placeholders()
+                if (p["metadata"].get("annotations") or {}).get(
+                    "gpumounter.amd.com/owner-name") == "k"]
+        assert len(left) == 1 and left[0]["metadata"]["uid"] in svc.abandoned
+        svc.hm.faults.rules.pop("devnodes")
+        async with lc.session.get(url, headers=hdr) as r:
+            assert r.status == 200
+            b = await r.json()
+        assert "replayed" not in b.get("message", "")
+        assert [d["placeholder"] for d in b["devices"]] != [left[0]["metadata"]["name"]]
+        fail["on"] = False                   # the apiserver is back: the follow-up drops it
+        for _ in range(150):
+            await asyncio.sleep(0.02)
+            if not svc.abandoned:
+                break
+        assert not svc.abandoned
+        names = {p["metadata"]["name"] for p in lc.cluster.placeholders()}
+        assert left[0]["metadata"]["name"] not in names
+        assert not await lc.audit("default", "k")
+    run(body, worker_overrides={"fault": "devnodes:1.0:after"})
