@@ -37,6 +37,34 @@ print(json.dumps({"rc": rc, "count": n.value if rc == 0 else 0, "bdfs": bdfs}))
 """
 
 
+# "a running rocm/pytorch Pod": a fresh PyTorch process in the tenant's view, as a workload in
+# the Pod would start after an attach. It reports what torch enumerates and, given a GPU, runs a
+# bf16 GEMM on it and checks it against an fp32 host reference.
+#
+# The count is the HIP runtime's (``is_available()`` asks it too): what the process can open.
+# On ROCm builds ``torch.cuda.device_count()`` is answered by amd-smi before CUDA-side init, and
+# amd-smi enumerates from sysfs, which a container sees node-wide — it reports the node's GPUs
+# whether or not this process can reach them (``device_count_api`` below; the same holds for
+# ``amd-smi list`` / ``rocm-smi`` in a real container, profiles/r3_tenant_view/smi_probe.txt).
+_TORCH_CHILD = r"""
+import json, torch
+n = torch._C._cuda_getDeviceCount() if torch.cuda.is_available() else 0
+out = {"count": n, "bdfs": [], "device_count_api": torch.cuda.device_count()}
+for i in range(n):
+    p = torch.cuda.get_device_properties(i)
+    out["bdfs"].append("%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id))
+    out["arch"] = p.gcnArchName
+if n:
+    g = torch.Generator().manual_seed(0)
+    a = torch.randn(2048, 2048, generator=g)
+    b = torch.randn(2048, 2048, generator=g)
+    ref = a.bfloat16().float() @ b.bfloat16().float()
+    c = (a.bfloat16().cuda() @ b.bfloat16().cuda()).float().cpu()
+    out["gemm_max_rel_err"] = float(((c - ref).abs().max() / ref.abs().max()).item())
+print(json.dumps(out))
+"""
+
+
 def view_lib() -> str:
     path = _native.lib_path("libgm_tenant_view.so")
     if not os.path.exists(path):
@@ -69,6 +97,18 @@ def hip_devices(rootfs: str, cgroup_dir: str = "", timeout: float = 120.0) -> Di
                          timeout=timeout)
     if res.returncode != 0:
         raise RuntimeError(f"tenant-side HIP check failed ({res.returncode}): "
+                           f"{res.stderr[-2000:]}")
+    return json.loads(res.stdout.strip().splitlines()[-1])
+
+
+def torch_devices(rootfs: str, cgroup_dir: str = "", timeout: float = 300.0) -> Dict:
+    """Start a fresh PyTorch process in the tenant's view: ``{"count", "bdfs", "arch",
+    "gemm_max_rel_err"}`` (the GEMM only when a GPU is visible)."""
+    res = subprocess.run([sys.executable, "-c", _TORCH_CHILD],
+                         env=tenant_env(rootfs, cgroup_dir), capture_output=True, text=True,
+                         timeout=timeout)
+    if res.returncode != 0:
+        raise RuntimeError(f"tenant-side PyTorch check failed ({res.returncode}): "
                            f"{res.stderr[-2000:]}")
     return json.loads(res.stdout.strip().splitlines()[-1])
 

@@ -396,6 +396,37 @@ def test_tenant_side_hip_sees_the_gpu_only_while_attached(real_inventory):
     asyncio.run(run())
 
 
+def test_tenant_side_pytorch_uses_the_gpu_only_while_attached(real_inventory):
+    """The BASELINE config names a rocm/pytorch Pod: a fresh PyTorch process in the tenant's
+    view sees no GPU before the attach; after it, exactly the attached GPU (same BDF, gfx950),
+    on which a bf16 GEMM matches an fp32 host reference; none after the detach."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+    from gpumounter_amd.ops import probe, tenant
+
+    bdf0 = probe.props(0)["pci_bus_id"].lower()
+
+    async def run():
+        async with LocalCluster(amdsmi_lib="", cgroup_mode="v2", node_gpu_bdfs=[bdf0]) as lc:
+            lc.tenant("pt")
+            cid = lc.container_ids("default", "pt")[0]
+            ctr = lc.nodes["node-0"].node.container(cid)
+            view = (ctr.root_dir, ctr.cgroup_dir)
+            before = await asyncio.to_thread(tenant.torch_devices, *view)
+            assert before["count"] == 0, before
+            code, body = await lc.add("default", "pt", 1)
+            assert code == 200, body
+            during = await asyncio.to_thread(tenant.torch_devices, *view)
+            assert during["count"] == 1 and during["bdfs"] == [bdf0], during
+            assert during["arch"].startswith("gfx950"), during
+            assert during["gemm_max_rel_err"] < 1e-2, during
+            code, _ = await lc.remove("default", "pt", [body["devices"][0]["uuid"]])
+            assert code == 200
+            after = await asyncio.to_thread(tenant.torch_devices, *view)
+            assert after["count"] == 0, after
+            print("tenant-side PyTorch:", before, during, after)
+    asyncio.run(run())
+
+
 def test_force_remove_waits_for_a_sigterm_ignoring_hip_process(real_inventory):
     """A real HIP process that ignores SIGTERM and holds 16 GiB of HBM: force removal revokes
     access, escalates to SIGKILL after the grace, and releases the placeholder only after the
