@@ -456,7 +456,7 @@ def main() -> int:
                        "all_peer_access": all(x["peer_access"] for x in pairs),
                        "min_gbps": round(min(x["gbps"] for x in pairs), 1),
                        "max_gbps": round(max(x["gbps"] for x in pairs), 1)}
-            tenant_view = None
+            tenant_view = tenant_view_pt = None
             if has_gpu and not args.no_verify and args.node_ops == "emulated" and \
                     args.protocol == "gpumounter" and args.cgroup == "v2":
                 # BASELINE config "the Pod sees it", from a fresh tenant-side HIP process
@@ -481,6 +481,16 @@ def main() -> int:
                     tenant_view = {"ok": False, "error": str(e)[-500:]}
                 if not tenant_view["ok"]:
                     print(f"bench: tenant-side view check failed: {tenant_view}",
+                          file=sys.stderr)
+                # "a running rocm/pytorch Pod": the same cycle seen by a fresh PyTorch process,
+                # which runs a bf16 GEMM on what it got
+                try:
+                    tenant_view_pt = tenant.check_attach_cycle(_attach, _detach, root, cg,
+                                                               runtime="pytorch")
+                except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench
+                    tenant_view_pt = {"ok": False, "error": str(e)[-500:]}
+                if not tenant_view_pt["ok"]:
+                    print(f"bench: tenant-side PyTorch check failed: {tenant_view_pt}",
                           file=sys.stderr)
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
             corrections = cp.corrections() if args.protocol == "gpumounter" else None
@@ -600,7 +610,7 @@ def main() -> int:
                 "allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4) if ar_ms else None,
                 "rccl_allreduce_2MiB_p50_ms": round(statistics.median(ar_ms), 4)
                 if ar_ms and ar_backend[0] == "nccl" else None,
-                "tenant_view": tenant_view,
+                "tenant_view": tenant_view, "tenant_view_pytorch": tenant_view_pt,
                 # attaches whose plugin-chosen GPUs were swapped for a better-placed set
                 "placement_corrections": corrections,
                 "attached_hives": att_hives, "attached_numa_nodes": att_numa,

@@ -129,21 +129,30 @@ def locate(rootfs_root: str, cgroup_root: str, container_id: str):
     raise FileNotFoundError(f"container {container_id} not under {cgroup_root}")
 
 
-def check_attach_cycle(attach, detach, rootfs: str, cgroup_dir: str) -> Dict:
-    """Tenant-side view across one attach/detach: HIP enumeration before, during and after.
-    ``attach()`` returns the attached BDFs; ``detach()`` removes them."""
-    before = hip_devices(rootfs, cgroup_dir)
+def check_attach_cycle(attach, detach, rootfs: str, cgroup_dir: str,
+                       runtime: str = "hip") -> Dict:
+    """Tenant-side view across one attach/detach: what a fresh HIP (``runtime="hip"``) or
+    PyTorch (``"pytorch"``) process enumerates before, during and after. ``attach()`` returns
+    the attached BDFs; ``detach()`` removes them."""
+    look = torch_devices if runtime == "pytorch" else hip_devices
+    before = look(rootfs, cgroup_dir)
     bdfs = sorted(b.lower() for b in attach())
     try:
-        during = hip_devices(rootfs, cgroup_dir)
+        during = look(rootfs, cgroup_dir)
     finally:
         detach()
-    after = hip_devices(rootfs, cgroup_dir)
+    after = look(rootfs, cgroup_dir)
     ok = before["count"] == 0 and sorted(during["bdfs"]) == bdfs and after["count"] == 0
-    return {"ok": ok, "before": before["count"], "during": during["bdfs"],
-            "after": after["count"], "attached": bdfs,
-            "how": "fresh HIP process; /dev/kfd, /dev/dri/* and the device-cgroup verdict "
-                   "resolved through the emulated node state (libgm_tenant_view.so)"}
+    out = {"ok": ok, "before": before["count"], "during": during["bdfs"],
+           "after": after["count"], "attached": bdfs,
+           "how": f"fresh {'PyTorch' if runtime == 'pytorch' else 'HIP'} process; /dev/kfd, "
+                  "/dev/dri/* and the device-cgroup verdict resolved through the emulated node "
+                  "state (libgm_tenant_view.so)"}
+    if runtime == "pytorch":
+        ok = ok and during.get("gemm_max_rel_err", 1.0) < 1e-2
+        out.update(ok=ok, gemm_max_rel_err=during.get("gemm_max_rel_err"),
+                   arch=during.get("arch"), device_count_api=during.get("device_count_api"))
+    return out
 
 
 def can_open(rootfs: str, paths: List[str], cgroup_dir: str = "") -> Dict[str, int]:
