@@ -69,9 +69,10 @@ def _tenant(lc, args, name: str) -> None:
     args.tenant_pids[name] = pid
 
 
-async def invariants(lc, tenants) -> int:
-    """Number of violated ledger invariants (0 = consistent)."""
+async def invariants(lc, tenants, why=None) -> int:
+    """Number of violated ledger invariants (0 = consistent); ``why`` collects descriptions."""
     bad = 0
+    why = why if why is not None else []
     node = lc.nodes["node-0"].node
     held = list(node.allocated)
     bad += len(held) != len(set(held))
@@ -81,14 +82,20 @@ async def invariants(lc, tenants) -> int:
         pod = lc.cluster.get("default", t)
         st = await svc.pod_state(pod)
         hot += len(st.hot)
-        bad += len(svc.hm.audit(pod, st.hot, st.own))
+        issues = svc.hm.audit(pod, st.hot, st.own)
+        bad += len(issues)
+        if issues:
+            why.append(f"{t}: audit {[(i.kind, i.path) for i in issues[:4]]}")
     # GPUs held by warm-pool standby placeholders (a standby the pool's refill created while
     # concurrent attaches filled the node stays Pending, holding nothing, until the pool drops it)
     standby_names = {p["metadata"]["name"] for p in lc.cluster.placeholders()
                      if (p["metadata"].get("annotations") or {}).get(
                          "gpumounter.amd.com/mount-mode") == "standby"}
     standby = sum(1 for _, pod, _ in node.allocated.values() if pod in standby_names)
-    bad += hot + standby != len(node.allocated)
+    if hot + standby != len(node.allocated):
+        bad += 1
+        why.append(f"hot {hot} + standby {standby} != allocated {len(node.allocated)}: "
+                   f"{sorted(set(pod for _, pod, _ in node.allocated.values()))}")
     bad += len(node.free_ids()) + len(node.allocated) != node.capacity
     return bad
 
@@ -139,6 +146,7 @@ async def contention(lc, args) -> dict:
     ok = fail = 0
     lat = []
     violations = 0
+    examples: list = []
     t_start = time.perf_counter()
     for _ in range(args.rounds):
         async def op(t):
@@ -159,13 +167,24 @@ async def contention(lc, args) -> dict:
             else:
                 fail += 1
         await asyncio.gather(*[op(t) for t in tenants])
-        violations += await invariants(lc, tenants)
+        why: list = []
+        bad = await invariants(lc, tenants, why)
+        if bad and getattr(args, "faults", False):
+            # a failed operation's cleanup may be with the reconciler's follow-up (retried
+            # after 0.1-5 s): the node must converge, not be consistent the instant ops return
+            t0 = time.perf_counter()
+            while bad and time.perf_counter() - t0 < 10:
+                await asyncio.sleep(0.05)
+                why = []
+                bad = await invariants(lc, tenants, why)
+        violations += bad
+        examples.extend(why[:2])
     elapsed = time.perf_counter() - t_start
     return {"rounds": args.rounds, "ops_ok": ok, "ops_refused": fail,
             "ops_per_s": round((ok + fail) / elapsed, 1),
             "attach_p50_ms": round(pct(lat, 0.5), 3) if lat else None,
             "attach_p99_ms": round(pct(lat, 0.99), 3) if lat else None,
-            "invariant_violations": violations}
+            "invariant_violations": violations, "violation_examples": examples[:6]}
 
 
 async def soak(lc, args) -> dict:
@@ -584,6 +603,10 @@ def main() -> int:
                          "rounds")
     ap.add_argument("--reconcile-period", type=float, default=0.5,
                     help="chaos: the worker's periodic sweep (GM_RECONCILE_PERIOD_S; shipped 30)")
+    ap.add_argument("--faults", action="store_true",
+                    help="in-process scenarios: the chaos scenario's stage faults (GM_FAULT) in "
+                         "the worker; with --node-ops real every failure path runs against real "
+                         "BPF programs and device nodes")
     ap.add_argument("--log-dir", default="",
                     help="chaos: keep the daemons' logs here (default: the cluster's temp dir)")
     ap.add_argument("--kill-every", type=int, default=10,
@@ -617,6 +640,8 @@ def main() -> int:
 
     args.sandbox, args.tenant_pids = None, {}
     kw, wov = {}, {"placement_enforce": args.placement, "warm_pool_size": args.warm_pool}
+    if args.faults:
+        wov["fault"] = CHAOS_FAULTS
     if args.node_ops == "real":
         from gpumounter_amd.fakes.realnode import RealNodeSandbox
         args.cgroup = "v2"
@@ -641,7 +666,8 @@ def main() -> int:
                              "cgroup": args.cgroup, "latency": args.latency,
                              "placement": args.placement, "device_plugin": args.device_plugin,
                              "alloc_policy": args.alloc_policy,
-                             "warm_pool": args.warm_pool, "node_ops": args.node_ops}
+                             "warm_pool": args.warm_pool, "node_ops": args.node_ops,
+                             "faults": CHAOS_FAULTS if args.faults else ""}
             if args.sandbox is not None:
                 res["kernel"] = _kernel_state(lc, args)
             return res

@@ -174,9 +174,17 @@ class Reconciler:
                                             for p in phs])
                         svc.metrics.orphans.labels(kind="owner_gone").inc(len(phs))
                 else:
-                    if key[0] == "followup" and key[3]:
-                        await self._drop(key[3])
                     owner = svc.node_pods.get(ns, name)
+                    if key[0] == "followup":
+                        # candidates of a pick are never an owner's; under the pod's lock no
+                        # pick is running, so any left belong to a failed one
+                        cands = [] if owner is None else [
+                            p for p in svc.ph.owned_by(owner, candidates=True)
+                            if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})]
+                        drop = set(key[3]) | {(p["metadata"]["namespace"], p["metadata"]["name"],
+                                               p["metadata"].get("uid", "")) for p in cands}
+                        if drop:
+                            await self._drop(sorted(drop))
                     if owner is None or podu.phase_of(owner) != "Running":
                         return
                     fixed = await svc.reconcile_pod(owner)

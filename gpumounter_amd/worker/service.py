@@ -498,6 +498,10 @@ class GpuMountService:
                                   f"provide them: {e}", warning=True)
                 return api.AddGPUResponse(add_gpu_result=api.ADD_INSUFFICIENT, message=str(e))
             except (ReserveError, asyncio.TimeoutError, InjectedFault, LedgerError) as e:
+                # a reservation that failed part-way may leave placeholders its own cleanup
+                # could not delete (candidates of a trim/correction pick among them): the
+                # follow-up releases what no attach holds any more, without waiting for a sweep
+                self._follow_up(pod)
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             keys = self.inv.by_key()
             new = [keys[normalize_device_id(d)] for d in res.device_ids]

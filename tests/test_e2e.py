@@ -1210,3 +1210,42 @@ def test_retry_under_the_key_of_a_failed_attach_does_not_replay_its_leftover():
         assert left[0]["metadata"]["name"] not in names
         assert not await lc.audit("default", "k")
     run(body, worker_overrides={"fault": "devnodes:1.0:after"})
+
+
+def test_candidates_of_a_failed_trim_pick_are_released_by_the_follow_up():
+    """A trim pick holds every free GPU as candidates; confirming the kept ones fails, and so
+    does the pick's own cleanup (apiserver errors). The leftover candidates hold GPUs nobody
+    uses: the follow-up releases them at once instead of the next periodic sweep (none runs
+    here)."""
+    from gpumounter_amd.cluster.placeholder import ReserveError
+
+    async def body(lc):
+        lc.tenant("tp")
+        svc = lc.nodes["node-0"].worker.service
+        real_confirm, real_release = svc.ph.confirm, svc.ph.release
+        calls = {"confirm": 0, "release": 0}
+
+        async def confirm(phs):
+            calls["confirm"] += 1
+            if calls["confirm"] == 1:
+                raise ReserveError("confirming 1 placeholder(s) failed: 503")
+            return await real_confirm(phs)
+
+        async def release(phs, *a, **k):
+            calls["release"] += 1
+            if calls["release"] == 1:
+                raise ReserveError("could not delete 8 placeholder(s): 503")
+            return await real_release(phs, *a, **k)
+        svc.ph.confirm, svc.ph.release = confirm, release
+        code, _ = await lc.add("default", "tp", 1)
+        assert code == 500 and calls["release"] >= 1
+        for _ in range(100):
+            await asyncio.sleep(0.02)
+            if not lc.cluster.placeholders():
+                break
+        assert lc.cluster.placeholders() == []
+        assert not lc.nodes["node-0"].node.allocated
+        assert not await lc.audit("default", "tp")
+        code, _ = await lc.add("default", "tp", 1)          # and the node is usable again
+        assert code == 200
+    run(body, alloc_policy="first-free", worker_overrides={"placement_enforce": "trim"})

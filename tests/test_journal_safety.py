@@ -371,12 +371,14 @@ def test_caller_going_away_mid_attach_does_not_leave_half_an_attach():
             await stub(api.AddGPURequest(pod_name="t", namespace="default", gpu_num=2,
                                          is_entire_mount=False), timeout=0.05)
         assert ei.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED
-        svc = lc.nodes["node-0"].worker.service
+        w = lc.nodes["node-0"].worker
+        svc = w.service
         tenant = lc.cluster.get("default", "t")
-        for _ in range(100):                 # admission takes ~0.2 s here
+        for _ in range(200):                 # admission takes ~0.2 s here, then the mount
             await asyncio.sleep(0.02)
-            if len((await svc.pod_state(tenant, fresh=True)).hot) == 2:
+            if not w._ops:                   # the shielded operation has ended
                 break
+        assert not w._ops
         assert len((await svc.pod_state(tenant, fresh=True)).hot) == 2
         assert all(p["spec"].get("nodeName") for p in lc.cluster.placeholders())
         assert not await lc.audit("default", "t")
