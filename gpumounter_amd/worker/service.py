@@ -243,7 +243,10 @@ class GpuMountService:
         incarnation) or when ``fresh`` is requested (reconciler, status).
         """
         st = PodGpuState()
-        owned = self.ph.owned_by(pod)
+        # a failed attach's placeholder that is still being released is nobody's GPU: a rollback
+        # or a later attach of the same pod must not mount it (it is schedulable once deleted)
+        owned = [p for p in self.ph.owned_by(pod)
+                 if p["metadata"].get("uid") not in self.abandoned]
         uid = podu.uid_of(pod)
         cached = [self.ph.cached(p) for p in owned]
         ledger: Optional[Dict[Tuple[str, str], List[str]]] = ledger_snapshot

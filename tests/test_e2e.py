@@ -1200,6 +1200,9 @@ def test_retry_under_the_key_of_a_failed_attach_does_not_replay_its_leftover():
             b = await r.json()
         assert "replayed" not in b.get("message", "")
         assert [d["placeholder"] for d in b["devices"]] != [left[0]["metadata"]["name"]]
+        # neither the rollback nor the retry mounted the leftover's GPU: once the follow-up
+        # deletes it the scheduler may hand it out, so the tenant must never have reached it
+        assert not await lc.audit("default", "k")
         fail["on"] = False                   # the apiserver is back: the follow-up drops it
         for _ in range(150):
             await asyncio.sleep(0.02)
