@@ -21,11 +21,15 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import contextlib
 import json
 import os
 import random
+import shutil
+import subprocess
 import sys
 import time
+from typing import Dict, List, Optional
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -326,50 +330,83 @@ def chaos(args) -> dict:
     * a Pod whose requests all succeeded since the last check holds exactly what its client
       attached and did not remove (a failed request may or may not have taken effect, so after
       one the client re-reads its state from the ledger).
-    ``converge_ms`` is how long the node took to satisfy the first two after a round."""
+    ``converge_ms`` is how long the node took to satisfy the first two after a round.
+
+    ``--busy``: every hot-mounted GPU is in use by a process of its tenant that ignores SIGTERM
+    (listed in the mock amdsmi's process table, a real child process in the container's
+    cgroup.procs), so every removal is a force removal that has to kill it. Two more
+    invariants: a removal answered with success named only processes that are gone, and a GPU
+    is never released while the process that used it still runs (reference order: kill, then
+    delete the slave pods and wait for them, pkg/util/util.go:112-143,
+    pkg/util/gpu/allocator/allocator.go:128-156)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from gpumounter_amd.fakes.deployment import ProcessCluster
     tenants = [f"x{i}" for i in range(4)]
     rnds = {t: random.Random(args.seed * 17 + i) for i, t in enumerate(tenants)}
     mine = {t: [] for t in tenants}
+    leases = {t: {} for t in tenants}        # uuid -> (earliest, latest) expiry of its lease
+    leased, expired = [0], [0]
     certain = {t: True for t in tenants}
     answered = {t: [] for t in tenants}      # (code, [(placeholder, uuid tail)]) per attach
     ok = failed = kills = restarts = master_kills = recreates = kubelet_restarts = 0
     recreated: set = set()
     problems, converge = [], []
     api_faults = [0]
+    codes: Dict[int, int] = {}
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": str(args.reconcile_period),
            "GM_WARM_POOL_SIZE": str(args.warm_pool), "GM_PLACEMENT_ENFORCE": args.placement}
     if args.log_dir:
         env["GM_LOG_LEVEL"] = "INFO"       # kept logs are for post-mortems
+    busy = _BusyTenants(tenants, args.busy_pool) if args.busy else None
+    if busy is not None:
+        env.update({"GM_AMDSMI_MOCK_PROCS": busy.table, "GM_BUSY_DETECTION": "both",
+                    "GM_KILL_GRACE_S": str(args.kill_grace)})
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
-                        gpu_api=args.gpu_api, log_dir=args.log_dir) as pc:
+                        gpu_api=args.gpu_api, log_dir=args.log_dir) as pc, \
+            (busy or contextlib.nullcontext()):
         for t in tenants:
-            pc.tenant(t)
+            pc.tenant(t, pids={"main": busy.pids(t)} if busy else None)
         if args.api_fault_rate:
             pc.api_faults(args.api_fault_rate, args.seed)
 
         def op(t):
             rnd = rnds[t]
             try:
-                if mine[t] and rnd.random() < 0.5:
-                    groups = mine[t]
+                # leased GPUs are left to their lease: the check sees whether it ended
+                groups = [g for g in mine[t] if not set(g[0]) & set(leases[t])]
+                if groups and rnd.random() < 0.5:
                     pick = list(groups) if any(e for _, e in groups) else \
                         rnd.sample(groups, rnd.randint(1, len(groups)))
-                    code, _ = pc.remove("default", t, [u for g, _ in pick for u in g], force=True)
+                    code, b = pc.remove("default", t, [u for g, _ in pick for u in g], force=True)
                     if code == 200:
                         for g in pick:
-                            groups.remove(g)
+                            mine[t].remove(g)
+                        if busy is not None:
+                            busy.check_killed(t, b.get("killed_pids") or [], problems)
                     return t, code
                 n, entire = rnd.randint(1, 3), rnd.random() < 0.3
-                code, b = pc.add("default", t, n, entire=entire)
+                lease = round(rnd.uniform(0.1, 0.5), 2) if rnd.random() < args.lease_rate else 0
+                sent = time.monotonic()
+                code, b = pc.add("default", t, n, entire=entire, lease_s=lease)
                 answered[t].append((code, [(d.get("placeholder"), d["uuid"][-4:])
                                            for d in (b.get("devices") or [])]
                                     if isinstance(b, dict) else None))
                 if code == 200:
                     uu = [d["uuid"] for d in b["devices"]]
+                    # a GPU attached again was in an earlier lease of this tenant: that lease
+                    # has ended (the ledger never holds a GPU twice)
+                    ended = set(uu) & set(leases[t])
+                    if ended:
+                        mine[t] = [g for g in mine[t] if not set(g[0]) & ended]
+                        for u in ended:
+                            leases[t].pop(u)
+                        expired[0] += len(ended)
                     mine[t].extend([(uu, True)] if entire else [([u], False) for u in uu])
+                    if lease:   # the worker's lease clock started between sending and answer
+                        leases[t].update({u: (sent + lease, time.monotonic() + lease)
+                                          for u in uu})
+                        leased[0] += 1
                 return t, code
             except Exception:  # noqa: BLE001 - the master's connection dropped mid-kill
                 return t, -1
@@ -411,8 +448,18 @@ def chaos(args) -> dict:
                 return False
             return True
 
+        def gpu_views():
+            out = {}
+            for t in tenants:
+                code, g = pc.pod_gpus("default", t)
+                out[t] = {x["uuid"]: x["index"] for x in g.get("gpus", [])
+                          if x.get("source") == "hot-mount"} if code == 200 else None
+            return out
+
         with ThreadPoolExecutor(len(tenants)) as ex:
             for rnd_i in range(args.rounds):
+                if busy is not None:
+                    busy.publish(gpu_views())
                 futs = [ex.submit(op, t) for t in tenants]
                 if args.recreate_rate and random.Random(rnd_i * 11 + 3).random() < args.recreate_rate:
                     # a tenant Pod is deleted and recreated under its name (new UID) mid-round
@@ -445,6 +492,7 @@ def chaos(args) -> dict:
                     certain[t] = False
                 recreated.clear()
                 for t, code in results:
+                    codes[code] = codes.get(code, 0) + 1
                     ok += code == 200
                     failed += code not in (200, 400, 403)   # 400/403 are answers, not failures
                     if code not in (200, 400, 403):
@@ -462,9 +510,28 @@ def chaos(args) -> dict:
                         break
                     time.sleep(0.05)
                 converge.append((time.perf_counter() - t0) * 1e3)
+                if busy is not None:
+                    busy.check_booked(rnd_i, gpu_views(), problems)
                 for t in tenants:
                     hot = ledger(t) or []
-                    want = sorted(u for grp, _ in mine[t] for u in grp)
+                    now = time.monotonic()
+                    # a lease past its expiry is gone, one within it is still there; one that
+                    # expires around now may be either (it is settled at the next check)
+                    overdue = [u for u, (_, hi) in leases[t].items()
+                               if now - hi > args.lease_slack]
+                    late = sorted(set(overdue) & set(hot))
+                    if late:
+                        problems.append(f"round {rnd_i} {t}: leases expired more than "
+                                        f"{args.lease_slack} s ago still attached: {late}")
+                    gone = set(overdue) - set(hot)
+                    for u in gone:
+                        leases[t].pop(u)
+                        expired[0] += 1
+                    if gone:
+                        mine[t] = [g for g in mine[t] if not set(g[0]) & gone]
+                    fuzzy = {u for u, (lo, _) in leases[t].items() if lo <= now}
+                    hot = [u for u in hot if u not in fuzzy]
+                    want = sorted(u for grp, _ in mine[t] for u in grp if u not in fuzzy)
                     if certain[t] and hot != want:
                         mine_phs = [(p["metadata"]["name"],
                                      {k.split("/")[-1]: v for k, v in
@@ -486,10 +553,13 @@ def chaos(args) -> dict:
                               if x.get("source") == "hot-mount"}
                         if len(ph) < len(mine[t]):      # fewer placeholders than GPUs: entire
                             mine[t] = [([u for grp, _ in mine[t] for u in grp], True)]
+                        held_now = {u for grp, _ in mine[t] for u in grp}
+                        leases[t] = {u: e for u, e in leases[t].items() if u in held_now}
                         certain[t] = True
                 if args.api_fault_rate:
                     pc.api_faults(args.api_fault_rate, args.seed * 1000 + rnd_i)
         metrics = pc.worker_metrics()
+        busy_report = busy.report() if busy is not None else {}
     injected = sum(float(ln.split()[-1]) for ln in metrics.splitlines()
                    if ln.startswith("gm_requests_total{") and 'result="INTERNAL"' in ln)
     return {"rounds": args.rounds, "worker_kills": kills, "master_kills": master_kills,
@@ -502,7 +572,97 @@ def chaos(args) -> dict:
             "invariant_violations": len(problems), "violation_examples": problems[:5],
             "faults": CHAOS_FAULTS, "api_fault_rate": args.api_fault_rate,
             "reconcile_period_s": args.reconcile_period, "placement": args.placement,
-            "api_faults_served": api_faults[0]}
+            "api_faults_served": api_faults[0],
+            "answers": {str(k): v for k, v in sorted(codes.items())},
+            "leases": {"rate": args.lease_rate, "attached": leased[0], "seen_expired": expired[0],
+                       "slack_s": args.lease_slack},
+            **busy_report}
+
+
+class _BusyTenants:
+    """chaos --busy: per tenant, a pool of processes that ignore SIGTERM (all in the tenant
+    container's cgroup.procs from the start); the current one is listed in the mock amdsmi
+    process table as the user of every GPU the tenant holds."""
+
+    def __init__(self, tenants: List[str], pool: int):
+        import tempfile
+        self.dir = tempfile.mkdtemp(prefix="gm-busy-")
+        self.table = os.path.join(self.dir, "procs")
+        open(self.table, "w").close()
+        self.procs = {t: [subprocess.Popen(["sh", "-c", "trap '' TERM; exec sleep 3600"],
+                                           stdin=subprocess.DEVNULL,
+                                           start_new_session=True) for _ in range(pool)]
+                      for t in tenants}
+        self.cur = {t: 0 for t in tenants}
+        self.listed: Dict[int, tuple] = {}       # GPU index -> (tenant, Popen) as published
+        self.kills_seen = 0
+        self.exhausted = 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc) -> None:
+        for ps in self.procs.values():
+            for p in ps:
+                if p.poll() is None:
+                    p.kill()
+                    p.wait()
+        shutil.rmtree(self.dir, ignore_errors=True)
+
+    def pids(self, t: str) -> List[int]:
+        return [p.pid for p in self.procs[t]]
+
+    def _current(self, t: str):
+        ps = self.procs[t]
+        while self.cur[t] < len(ps) and ps[self.cur[t]].poll() is not None:
+            self.cur[t] += 1                     # killed by a force removal: the next one
+        if self.cur[t] >= len(ps):
+            self.exhausted += 1
+            return None
+        return ps[self.cur[t]]
+
+    def publish(self, views: Dict[str, Optional[dict]]) -> None:
+        """Every GPU a tenant holds is in use by its current process."""
+        self.listed = {}
+        lines = []
+        for t, v in views.items():
+            p = self._current(t)
+            if p is None or not v:
+                continue
+            for idx in sorted(v.values()):
+                self.listed[idx] = (t, p)
+                lines.append(f"{idx} {p.pid} 4096 sleep\n")
+        tmp = self.table + ".tmp"
+        with open(tmp, "w") as fh:
+            fh.write("".join(lines))
+        os.replace(tmp, self.table)
+
+    def check_killed(self, t: str, pids: List[int], problems: list) -> None:
+        """A removal answered with success: the processes it killed are gone."""
+        by_pid = {p.pid: p for p in self.procs[t]}
+        for pid in pids:
+            self.kills_seen += 1
+            p = by_pid.get(pid)
+            if p is None:
+                problems.append(f"{t}: removal killed {pid}, not one of the tenant's processes")
+            elif p.poll() is None:
+                time.sleep(0.05)                 # reaped by us, not by the worker: allow a beat
+                if p.poll() is None:
+                    problems.append(f"{t}: removal answered success while killed PID {pid} "
+                                    f"still runs")
+
+    def check_booked(self, rnd_i: int, views: Dict[str, Optional[dict]], problems: list) -> None:
+        """A GPU whose listed process still runs is still its tenant's (never released)."""
+        for idx, (t, p) in self.listed.items():
+            if p.poll() is None and views.get(t) is not None and idx not in views[t].values():
+                problems.append(f"round {rnd_i}: GPU {idx} released from {t} while its process "
+                                f"{p.pid} still runs")
+
+    def report(self) -> dict:
+        return {"busy": {"force_kills_answered": self.kills_seen,
+                         "processes_killed": sum(p.poll() is not None
+                                                 for ps in self.procs.values() for p in ps),
+                         "pool_exhausted_rounds": self.exhausted}}
 
 
 async def placement(lc, args) -> dict:
@@ -607,6 +767,18 @@ def main() -> int:
                     help="in-process scenarios: the chaos scenario's stage faults (GM_FAULT) in "
                          "the worker; with --node-ops real every failure path runs against real "
                          "BPF programs and device nodes")
+    ap.add_argument("--lease-rate", type=float, default=0.0,
+                    help="chaos: the share of attaches made with a 0.1-0.5 s lease (?lease=); a "
+                         "lease must have ended within --lease-slack of its expiry")
+    ap.add_argument("--lease-slack", type=float, default=1.5,
+                    help="chaos --lease-rate: how late an expired lease may still be attached")
+    ap.add_argument("--busy", action="store_true",
+                    help="chaos: every hot-mounted GPU is in use by a SIGTERM-ignoring process "
+                         "of its tenant; removals must kill it before releasing the GPU")
+    ap.add_argument("--busy-pool", type=int, default=80,
+                    help="chaos --busy: processes per tenant (one is killed per busy removal)")
+    ap.add_argument("--kill-grace", type=float, default=0.2,
+                    help="chaos --busy: the worker's SIGTERM -> SIGKILL grace (GM_KILL_GRACE_S)")
     ap.add_argument("--log-dir", default="",
                     help="chaos: keep the daemons' logs here (default: the cluster's temp dir)")
     ap.add_argument("--kill-every", type=int, default=10,
@@ -621,6 +793,10 @@ def main() -> int:
     args = ap.parse_args()
     log.setup("WARNING", json_format=False)
     if args.scenario == "chaos":
+        if args.busy and args.lease_rate:
+            ap.error("--busy keeps leased GPUs attached (busy leases are kept): no --lease-rate")
+        if args.busy and args.recreate_rate:
+            ap.error("--busy keeps each tenant's processes in its Pod: no --recreate-rate")
         res = chaos(args)
         res["config"] = {"scenario": "chaos", "deploy": "processes",
                          "amdsmi": args.amdsmi or "libamd_smi", "cgroup": args.cgroup,

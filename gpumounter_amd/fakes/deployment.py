@@ -307,9 +307,11 @@ class ProcessCluster:
             raise RuntimeError(f"tenant create failed: {code} {body[:300]!r}")
         return json.loads(body)
 
-    def add(self, ns: str, pod: str, n: int, entire: bool = False) -> Tuple[int, dict]:
+    def add(self, ns: str, pod: str, n: int, entire: bool = False, lease_s: float = 0.0
+            ) -> Tuple[int, dict]:
+        q = f"?lease={lease_s:g}" if lease_s else ""
         code, body = self._master("GET", f"/addgpu/namespace/{ns}/pod/{pod}/gpu/{n}/"
-                                         f"isEntireMount/{'true' if entire else 'false'}",
+                                         f"isEntireMount/{'true' if entire else 'false'}{q}",
                                   headers={"Accept": "application/json"})
         return code, json.loads(body)
 

@@ -2,7 +2,8 @@
 deployment while the worker injects faults at every mutating stage and is SIGKILLed twice with
 requests in flight, 5 % of the apiserver's Pod requests fail (some after taking effect) and
 tenant containers restart mid-request.
-The ledger invariants hold after every round (see chaos() for the list)."""
+The ledger invariants hold after every round (see chaos() for the list). Variants: every GPU
+busy with a SIGTERM-ignoring process (force removals), and attaches with short leases."""
 import json
 import os
 import subprocess
@@ -19,4 +20,32 @@ def test_chaos_keeps_the_ledger_invariants():
     assert res.returncode == 0, res.stderr[-3000:]
     out = json.loads(res.stdout.strip().splitlines()[-1])
     assert out["worker_kills"] == 2 and out["ops_ok"] > 0 and out["api_faults_served"] > 0
+    assert out["invariant_violations"] == 0, out["violation_examples"]
+
+
+def test_chaos_with_busy_gpus_kills_before_releasing():
+    """--busy: every hot-mounted GPU is used by a SIGTERM-ignoring process of its tenant, so each
+    removal is a force removal that must kill it first; one worker SIGKILL lands mid-drain at
+    some point. No GPU is released while its process runs, and every success names only
+    processes that are gone."""
+    res = subprocess.run([sys.executable, "bench/configs.py", "chaos", "--busy", "--rounds", "10",
+                          "--kill-every", "5", "--seed", "2", "--busy-pool", "12"], cwd=ROOT,
+                         capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out["worker_kills"] == 2 and out["busy"]["force_kills_answered"] > 0
+    assert out["busy"]["processes_killed"] >= out["busy"]["force_kills_answered"]
+    assert out["invariant_violations"] == 0, out["violation_examples"]
+
+
+def test_chaos_with_leases_ends_them_across_worker_kills():
+    """--lease-rate: half the attaches carry a 0.1-0.5 s lease (?lease=). With the worker
+    SIGKILLed twice, every lease has ended within --lease-slack of its expiry and unleased GPUs
+    stay exactly as their client left them."""
+    res = subprocess.run([sys.executable, "bench/configs.py", "chaos", "--lease-rate", "0.5",
+                          "--rounds", "12", "--kill-every", "6", "--seed", "3"], cwd=ROOT,
+                         capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out["worker_kills"] == 2 and out["leases"]["attached"] > 0
     assert out["invariant_violations"] == 0, out["violation_examples"]
