@@ -686,6 +686,7 @@ class GpuMountService:
                                       [keys[normalize_device_id(d)].index for d in ids])[0]
         held = list(res.placeholders)
         extra: List[Placeholder] = []
+        dropped: List[Placeholder] = []      # the admitted placeholder, once let go
         pick = best_of
         try:
             with trace.span("placement_correct", held=len(free)):
@@ -700,8 +701,10 @@ class GpuMountService:
                     if alt and score(alt) <= score(best) + 1e-6:
                         pick = lambda ids: alt          # noqa: E731 - as good, no 2nd round
                     else:
-                        await self.ph.release(held, wait=True)
-                        held = []
+                        # let go before the DELETE: a release that fails after taking effect
+                        # (a lost reply) must not leave it counted as a kept reservation
+                        dropped, held = held, []
+                        await self.ph.release(dropped, wait=True)
                         want_n, got = len(mine), []
                         for delay in (0.0, 0.05, 0.2):
                             if delay:
@@ -720,7 +723,7 @@ class GpuMountService:
                 InjectedFault) as e:
             # QuotaExceeded: in tenant-namespace mode the extra holds count against the
             # tenant's ResourceQuota at the apiserver
-            await self._release_quiet(pod, extra)
+            await self._release_quiet(pod, extra + dropped)
             if held:
                 _log.warning("placement correction failed, keeping the plugin's choice: %s", e)
                 return res

@@ -919,6 +919,43 @@ def test_entire_mount_correction_takes_part_of_the_admitted_set_back():
     run(body, alloc_policy="first-free")
 
 
+def test_entire_mount_correction_never_keeps_a_placeholder_it_let_go():
+    """The second round of an entire-mount correction deletes the admitted placeholder, and that
+    DELETE takes effect but its reply is lost. The attach must not fall back to "keeping the
+    plugin's choice": that placeholder is gone, so its GPUs would be mounted with no booking
+    and handed to the next Pod as well (found by chaos: one GPU attached to two Pods)."""
+    from gpumounter_amd.cluster.placeholder import ReserveError
+
+    async def body(lc):
+        for t in ("a", "b", "t", "u"):
+            lc.tenant(t)
+        assert (await lc.add("default", "a", 3))[0] == 200
+        assert (await lc.add("default", "b", 2))[0] == 200
+        svc = lc.nodes["node-0"].worker.service
+        real_release = svc.ph.release
+        armed = {"on": True}
+
+        async def release(phs, *a, **k):
+            await real_release(phs, *a, **k)
+            if armed["on"] and any(len(p.device_ids) > 1 for p in phs):
+                armed["on"] = False
+                raise ReserveError("DELETE applied, reply lost")
+        svc.ph.release = release
+        code, c = await lc.add("default", "t", 2, entire=True)
+        assert not armed["on"], "the second round did not run"
+        assert code != 200, c
+        for _ in range(100):
+            if len(node_of(lc).allocated) == 5:
+                break
+            await asyncio.sleep(0.02)
+        assert len(node_of(lc).allocated) == 5               # only a's and b's GPUs booked
+        assert not await lc.audit("default", "t")            # nothing left mounted in t
+        code, d = await lc.add("default", "u", 3)            # every free GPU goes to u ...
+        assert code == 200, d
+        assert not await lc.audit("default", "u") and not await lc.audit("default", "t")
+    run(body, alloc_policy="first-free")
+
+
 def test_status_endpoints_answer_json_when_the_worker_is_down():
     async def body(lc):
         lc.tenant("m")
