@@ -39,6 +39,7 @@ class LeaseKeeper:
         self._timers: Dict[str, asyncio.TimerHandle] = {}     # placeholder uid → timer
         self._retry_after: Dict[Tuple[str, str], float] = {}   # owner → not before
         self._retry_timers: Dict[Tuple[str, str], asyncio.TimerHandle] = {}
+        self._errors: Dict[Tuple[str, str], int] = {}          # owner → failed expiries in a row
         self._tasks: set = set()                               # running expiries
         self._stopped = False
         self.expired = 0
@@ -65,9 +66,33 @@ class LeaseKeeper:
         """Timer callback: run one expiry as a tracked task (cancelled by stop())."""
         if self._stopped:
             return
-        task = asyncio.ensure_future(self.expire_owner(ns, name))
+        task = asyncio.ensure_future(self._expire_or_retry(ns, name))
         self._tasks.add(task)
         task.add_done_callback(self._tasks.discard)
+
+    # an expiry that failed (the apiserver or the kubelet erring, a node operation refused) is
+    # retried after these delays, then every lease_retry_s: not left to the periodic sweep
+    ERROR_RETRY_S = (0.1, 0.5, 2.0)
+
+    async def _expire_or_retry(self, ns: str, name: str) -> None:
+        try:
+            await self.expire_owner(ns, name)
+            self._errors.pop((ns, name), None)
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:  # noqa: BLE001 - retried below
+            n = self._errors.get((ns, name), 0)
+            self._errors[(ns, name)] = n + 1
+            delay = self.ERROR_RETRY_S[n] if n < len(self.ERROR_RETRY_S) else \
+                self.svc.cfg.lease_retry_s
+            _log.error("lease expiry of %s/%s failed (attempt %d, retry in %g s): %s",
+                       ns, name, n + 1, delay, e)
+            if not self._stopped:
+                old = self._retry_timers.pop((ns, name), None)
+                if old is not None:
+                    old.cancel()
+                self._retry_timers[(ns, name)] = asyncio.get_running_loop().call_later(
+                    delay, self._spawn, ns, name)
 
     async def stop(self, grace_s: float = 5.0) -> None:
         """Worker shutdown: no timer fires afterwards, and an expiry already detaching is
