@@ -29,6 +29,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import grpc
 
 from gpumounter_amd.api import gpu_mount as api
+from gpumounter_amd.cluster.correction import Correction, ReserveGate, placement_worse
 from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.cluster.placeholder import (InsufficientGPU, Placeholder, PlaceholderManager,
@@ -37,7 +38,7 @@ from gpumounter_amd.cluster.quota import GpuQuota, QuotaExceeded
 from gpumounter_amd.hw import topology
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.device import AmdGpu, gpus_by_key, normalize_device_id
+from gpumounter_amd.models.device import AmdGpu, normalize_device_id
 from gpumounter_amd.models.types import (ANN_IDEMPOTENCY, ANN_MOUNT_MODE, ANN_OWNER_UID,
                                          ERR_INTERNAL, ERR_POLICY, ERR_QUOTA, LABEL_OWNER_NS,
                                          MODE_DRAINING, MODE_STANDBY, MountType)
@@ -49,6 +50,7 @@ from gpumounter_amd.utils.faults import FaultInjector, InjectedFault
 from gpumounter_amd.utils.metrics import Metrics
 from gpumounter_amd.worker.drain import DrainKeeper
 from gpumounter_amd.worker.lease import LeaseKeeper
+from gpumounter_amd.worker import status
 from gpumounter_amd.worker.notify import Notifier
 
 _log = log.get("worker.service")
@@ -82,52 +84,6 @@ def can_mount(mount_type: MountType, entire: bool) -> Tuple[bool, str]:
     return True, ""
 
 
-class _SharedExclusive:
-    """Reservations on one node: ordinary ones run concurrently (shared); the ones that hold
-    every free GPU for a moment (trim, placement correction) and device-plugin intents, which
-    carry no pod identity, run alone (exclusive)."""
-
-    def __init__(self) -> None:
-        self._cond = asyncio.Condition()
-        self._shared = 0
-        self._exclusive = False
-        self._waiting_exclusive = 0
-
-    @contextlib.asynccontextmanager
-    async def shared(self):
-        async with self._cond:
-            if self._exclusive or self._waiting_exclusive:
-                with trace.span("reserve_gate_wait"):
-                    await self._cond.wait_for(lambda: not self._exclusive and
-                                              not self._waiting_exclusive)
-            self._shared += 1
-        try:
-            yield
-        finally:
-            async with self._cond:
-                self._shared -= 1
-                self._cond.notify_all()
-
-    @contextlib.asynccontextmanager
-    async def exclusive(self):
-        async with self._cond:
-            self._waiting_exclusive += 1
-            try:
-                if self._exclusive or self._shared:
-                    with trace.span("reserve_gate_wait"):
-                        await self._cond.wait_for(lambda: not self._exclusive and
-                                                  not self._shared)
-            finally:
-                self._waiting_exclusive -= 1
-            self._exclusive = True
-        try:
-            yield
-        finally:
-            async with self._cond:
-                self._exclusive = False
-                self._cond.notify_all()
-
-
 class GpuMountService:
     def __init__(self, cfg, kube: KubeClient, inv: Inventory, ledger: LedgerClient,
                  placeholders: PlaceholderManager, hotmount: HotMount, node_pods: PodInformer,
@@ -153,7 +109,7 @@ class GpuMountService:
         # * trim briefly holds every free GPU — a concurrent one would see a full node;
         # * device-plugin intents carry no pod identity (GetPreferredAllocation has none), so
         #   two attaches' 1-GPU intents would be indistinguishable to the plugin.
-        self._reserve_gate = _SharedExclusive()
+        self._reserve_gate = ReserveGate()
         # a pod's lock lives while a request holds or awaits it: no entry per pod ever seen
         self._locks: "weakref.WeakValueDictionary[Tuple[str, str], asyncio.Lock]" = \
             weakref.WeakValueDictionary()
@@ -634,109 +590,20 @@ class GpuMountService:
 
     def _placement_worse(self, st: PodGpuState, got: Sequence[str],
                          want: Sequence[str]) -> bool:
-        """The admitted set scores worse (hive split ≫ non-xGMI pair ≫ NUMA split) with the
-        pod's GPUs than the preferred set would have."""
-        if not want or len(want) != len(got):
-            return False
-        keys = self.inv.by_key()
-        try:
-            g = [keys[normalize_device_id(d)].index for d in got]
-            w = [keys[normalize_device_id(d)].index for d in want]
-        except KeyError:
-            return False
-        if sorted(g) == sorted(w):
-            return False
-        table = {x.index: x for x in self.inv.gpus()}
-        att = [x.index for x in st.hot + st.own]
-        links = self.inv.links()
-        return topology.score_set(table, links, att + g)[0] > \
-            topology.score_set(table, links, att + w)[0] + 1e-6
+        return placement_worse(self.inv, st.hot + st.own, got, want)
 
     async def _correct(self, pod: dict, n: int, req, st: PodGpuState, res):
-        """The plugin's choice is worse than the preferred set: hold every other free GPU with
-        1-GPU placeholders next to the admitted ones, keep the best ``n`` and release the rest.
-
-        An entire mount's admitted n-GPU placeholder can only be kept whole. When the best set
-        needs part of it, ``n`` of the new placeholders do as well whenever the topology is
-        symmetric (the common case on an all-to-all xGMI node); otherwise it is released and its
-        GPUs taken back as 1-GPU placeholders — every other free GPU is held by then, so the
-        plugin can only hand out those (retried briefly while the kubelet frees them). Any
-        failure before the admitted placeholder is let go keeps it: a valid, worse-placed
-        reservation rather than a failed attach."""
-        keys = self.inv.by_key()
-        mine = {normalize_device_id(d) for d in res.device_ids}
-        free = [g for g in self._free(st) if not mine.intersection(g.ledger_keys())]
-        if not free:
-            return res
-        attached = st.hot + st.own
-        links = self.inv.links()
-        table = {g.index: g for g in self.inv.gpus()}
-        group = secrets.token_hex(4) if req.is_entire_mount else ""
-        rid = log.request_id.get()
-
-        def best_of(ids: List[str]) -> List[str]:
-            by = {keys[normalize_device_id(d)].index: d for d in ids
-                  if normalize_device_id(d) in keys}
-            plc = topology.choose([table[i] for i in by], n, links, attached=attached,
-                                  policy=self.cfg.topology_policy) if len(by) >= n else None
-            return [by[i] for i in plc.chosen] if plc else list(res.device_ids)
-
-        def score(ids: List[str]) -> float:
-            return topology.score_set(table, links, [g.index for g in attached] +
-                                      [keys[normalize_device_id(d)].index for d in ids])[0]
-        held = list(res.placeholders)
-        extra: List[Placeholder] = []
-        dropped: List[Placeholder] = []      # the admitted placeholder, once let go
-        pick = best_of
-        try:
-            with trace.span("placement_correct", held=len(free)):
-                self.faults.check("placement_correct")
-                extra = await self.ph.hold_singles(pod, len(free), req.is_entire_mount, group,
-                                                   rid, req.container, req.idempotency_key)
-                best = best_of([d for p in held + extra for d in p.device_ids])
-                want = {normalize_device_id(d) for d in best}
-                if req.is_entire_mount and want & mine and not mine <= want:
-                    new_ids = [d for p in extra for d in p.device_ids]
-                    alt = best_of(new_ids) if len(new_ids) >= n else []
-                    if alt and score(alt) <= score(best) + 1e-6:
-                        pick = lambda ids: alt          # noqa: E731 - as good, no 2nd round
-                    else:
-                        # let go before the DELETE: a release that fails after taking effect
-                        # (a lost reply) must not leave it counted as a kept reservation
-                        dropped, held = held, []
-                        await self.ph.release(dropped, wait=True)
-                        want_n, got = len(mine), []
-                        for delay in (0.0, 0.05, 0.2):
-                            if delay:
-                                await asyncio.sleep(delay)
-                            got += await self.ph.hold_singles(
-                                pod, want_n - len(got), True, group, rid, req.container,
-                                req.idempotency_key)
-                            if len(got) >= want_n:
-                                break
-                        extra += got
-                new, surplus = self.ph.keep_picked(held + extra, n, pick)
-                self.faults.check("placement_correct", "after")
-                if sum(len(p.device_ids) for p in new.placeholders) == n:
-                    await self.ph.confirm(new.placeholders)
-        except (ReserveError, InsufficientGPU, QuotaExceeded, asyncio.TimeoutError,
-                InjectedFault) as e:
-            # QuotaExceeded: in tenant-namespace mode the extra holds count against the
-            # tenant's ResourceQuota at the apiserver
-            await self._release_quiet(pod, extra + dropped)
-            if held:
-                _log.warning("placement correction failed, keeping the plugin's choice: %s", e)
-                return res
-            raise
-        if sum(len(p.device_ids) for p in new.placeholders) != n:
-            await self._release_quiet(pod, held + extra)
-            raise InsufficientGPU(f"placement correction could not hold {n} GPUs")
-        self.metrics.placement_corrections.inc()
-        new.preferred = new.device_ids
-        if surplus:
-            with trace.span("placement_release", placeholders=len(surplus)):
-                await self._release_quiet(pod, surplus)
-        return new
+        """Swap the plugin's worse-placed choice for the best free set (cluster/correction.py:
+        hold every other free GPU, keep the best ``n``, release the rest)."""
+        c = Correction(self.ph, self.inv, self._free(st), st.hot + st.own, pod, n,
+                       req.is_entire_mount, secrets.token_hex(4) if req.is_entire_mount else "",
+                       log.request_id.get(), req.container, req.idempotency_key,
+                       self.cfg.topology_policy, self.faults,
+                       lambda phs: self._release_quiet(pod, phs))
+        out = await c.run(res)
+        if c.corrected:
+            self.metrics.placement_corrections.inc()
+        return out
 
     async def _release_quiet(self, pod: dict, phs) -> None:
         try:
@@ -1030,59 +897,4 @@ class GpuMountService:
 
     # ------------------------------------------------------------------------ status
     async def node_status(self, include_processes: bool) -> dict:
-        gpus = self.inv.gpus()
-        try:
-            ledger = await self.ledger.list()
-        except LedgerError as e:
-            ledger = []
-            _log.error("ledger: %s", e)
-        keys = gpus_by_key(gpus)
-        for a in ledger:
-            for d in a.device_ids:
-                g = keys.get(normalize_device_id(d))
-                if g is not None:
-                    g.pod_name, g.namespace, g.container = a.pod, a.namespace, a.container
-                    g.state = g.state.ALLOCATED
-        phs = []
-        for p in self.ph.informer.list(lambda p: not p["metadata"].get("deletionTimestamp")):
-            md = p["metadata"]
-            ann = md.get("annotations") or {}
-            ids = next((a.device_ids for a in ledger
-                        if (a.namespace, a.pod) == (md["namespace"], md["name"])), ())
-            phs.append({"namespace": md["namespace"], "name": md["name"],
-                        "owner": ann.get("gpumounter.amd.com/owner-name", ""),
-                        "owner_namespace": (md.get("labels") or {}).get(
-                            "gpumounter.amd.com/owner-namespace", ""),
-                        "owner_uid": ann.get("gpumounter.amd.com/owner-uid", ""),
-                        "mode": ann.get("gpumounter.amd.com/mount-mode", ""),
-                        "device_ids": list(ids)})
-        out = {"node": self.cfg.node_name,
-               "gpus": [dict(g.to_dict(), healthy=g.index not in self.unhealthy) for g in gpus],
-               "placeholders": phs,
-               "topology": topology.describe(gpus, self.inv.links()),
-               "ledger_api": self.ledger.api_version, "kfd_major": self.inv.kfd_major}
-        if include_processes:
-            def procs():
-                by = {}
-                for g in gpus:
-                    try:
-                        by[g.index] = [p.__dict__ for p in self.inv.processes(g.index)]
-                    except Exception as e:  # noqa: BLE001
-                        by[g.index] = str(e)
-                return by
-            out["processes"] = await asyncio.to_thread(procs)     # amdsmi: off the loop
-        for state in ("GPU_FREE_STATE", "GPU_ALLOCATED_STATE"):
-            self.metrics.ledger_gpus.labels(state=state).set(
-                sum(1 for g in gpus if g.state.value == state))
-        # hot-mounted GPUs per tenant namespace (chargeback: integrate over time in Prometheus)
-        per_ns: Dict[str, int] = {}
-        for ph in phs:
-            if ph["mode"] != "standby" and ph["owner_namespace"]:
-                per_ns[ph["owner_namespace"]] = per_ns.get(ph["owner_namespace"], 0) + \
-                    len(ph["device_ids"])
-        for ns in set(self._ns_seen) - set(per_ns):
-            self.metrics.hot_gpus.labels(namespace=ns).set(0)
-        for ns, n in per_ns.items():
-            self.metrics.hot_gpus.labels(namespace=ns).set(n)
-        self._ns_seen = set(per_ns) | set(self._ns_seen)
-        return out
+        return await status.node_status(self, include_processes)

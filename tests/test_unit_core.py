@@ -329,7 +329,7 @@ def test_reserve_gate_shared_and_exclusive():
     alone, and new ordinary ones queue behind a waiting correction (no starvation)."""
     import asyncio
 
-    from gpumounter_amd.worker.service import _SharedExclusive
+    from gpumounter_amd.cluster.correction import ReserveGate as _SharedExclusive
 
     async def main():
         g = _SharedExclusive()
