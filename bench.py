@@ -184,6 +184,9 @@ def main() -> int:
                          "JSON lines to this file, for tail-latency analysis")
     ap.add_argument("--log-dir", default="",
                     help="--deploy processes: keep the daemons' logs in this directory")
+    ap.add_argument("--no-calib", action="store_true",
+                    help="skip the box calibration (CPU loop, process pingpong, gRPC floor) "
+                         "recorded as \"box\" in the JSON")
     ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
                     help="dra: the node's GPUs come from a DRA driver; placeholders hold "
                          "ResourceClaims (gpu_allocation=dra)")
@@ -208,6 +211,12 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n = args.gpus
+    box = None
+    if rank == 0 and not args.no_calib:
+        # the box's speed next to the value (gpumounter_amd/utils/calib.py): before anything
+        # initialises the GPU, since the calibration forks and spawns
+        from gpumounter_amd.utils import calib
+        box = calib.measure(grpc_floor=True)
     if world > 1 and world != n:
         print(f"WORLD_SIZE={world} must equal --gpus={n}", file=sys.stderr)
         return 2
@@ -319,6 +328,7 @@ def main() -> int:
     pool_cap = info.get("node_gpus", 0) if rank == 0 else 0
     attach_ms, detach_ms, audit_issues, probe_us, stage = [], [], 0, [], {}
     dstage = {}          # detach: worker stage name → ms per timed detach
+    mstage = {}          # attach: master stage name → ms (gm:master_* spans)
     hop_ms = []          # (master handler ms, worker ms) per timed attach
     ar_ms = []
     probe_by_gpu = {}
@@ -340,7 +350,8 @@ def main() -> int:
                     "uuids": [d["uuid"] for d in body["devices"]],
                     "ms": (t1 - t0) * 1e3, "issues": len(issues),
                     "master_ms": body.get("master_ms"), "worker_ms": body.get("total_ms"),
-                    "timings": {t["name"]: t["ms"] for t in body.get("timings", [])}}]
+                    "timings": {t["name"]: t["ms"] for t in body.get("timings", [])},
+                    "mtimings": {t["name"]: t["ms"] for t in body.get("master_timings", [])}}]
         if world > 1:
             dist.broadcast_object_list(obj, src=0)
         st = obj[0]
@@ -401,10 +412,12 @@ def main() -> int:
                 if samples is not None:
                     samples.append({"t": round(time.time(), 4), "attach_ms": round(st["ms"], 4),
                                     "detach_ms": round((t1 - t0) * 1e3, 4),
-                                    "stages": st["timings"]})
+                                    "stages": st["timings"], "master": st["mtimings"]})
                 audit_issues += st["issues"]
                 for k, v in st["timings"].items():
                     stage.setdefault(k, []).append(v)
+                for k, v in st["mtimings"].items():
+                    mstage.setdefault(k, []).append(v)
 
     last_note = [time.time()]
 
@@ -439,6 +452,8 @@ def main() -> int:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         ms_per_step = elapsed * 1e3 / args.steps
+        if box is not None:
+            calib_after = calib.py_loop_us()   # no fork now: this process holds the GPU
         if world > 1:
             t = torch.tensor([ms_per_step], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -586,6 +601,10 @@ def main() -> int:
                 "attach_p999_ms": round(pct(attach_ms, 0.999), 4) if len(attach_ms) >= 1000
                 else None,
                 "attach_max_ms": round(max(attach_ms), 4) if attach_ms else None,
+                # spread of the timed attaches: a wide one with a normal "box" points at
+                # interference during the run (another job on the host), not at the code
+                "attach_iqr_ms": round(pct(attach_ms, 0.75) - pct(attach_ms, 0.25), 4)
+                if attach_ms else None,
                 # where the client-side attach time goes, p50: the worker's whole attach, the
                 # master's handler (incl. the gRPC call to the worker) and what is left
                 # (client ⇄ master HTTP)
@@ -601,6 +620,8 @@ def main() -> int:
                 "stage_p99_ms": {k: round(pct(v, 0.99), 4) for k, v in sorted(stage.items())},
                 "detach_stage_p50_ms": {k: round(statistics.median(v), 4)
                                         for k, v in sorted(dstage.items())},
+                "master_stage_p50_ms": {k: round(statistics.median(v), 4)
+                                        for k, v in sorted(mstage.items())},
                 "probe_quick_p50_us": round(statistics.median(probe_us), 2) if probe_us else None,
                 "probe_gpus_verified": len(probe_by_gpu) if world == 1 else None,
                 "probe_quick_p50_us_by_gpu": {b: round(statistics.median(v), 2)
@@ -626,6 +647,10 @@ def main() -> int:
                 "client_gc_pauses": [list(x) for x in runtime.gc_pauses],
                 "reference_emulated_same_run": ref,
                 "inventory": info,
+                "box": box,
+                "box_after": {"py_loop_us": round(calib_after, 1),
+                              "loadavg_1m": round(os.getloadavg()[0], 2)}
+                if box is not None else None,
             }
             if args.node_ops == "real":
                 out["attach_p50_real_node_ops_ms"] = out["value"]

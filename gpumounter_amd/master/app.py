@@ -29,7 +29,7 @@ from gpumounter_amd.cluster.informer import PodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.master.authz import Authorizer
-from gpumounter_amd.utils import log, runtime
+from gpumounter_amd.utils import log, runtime, trace
 from gpumounter_amd.utils.metrics import Metrics
 
 _log = log.get("master")
@@ -283,18 +283,20 @@ class Master:
         (reference main.go:103-116)."""
         t0 = time.perf_counter()
         for fresh in (False, True):
-            pod, target, err, cached = await self._locate(ns, name, fresh)
+            with trace.span("master_locate"):
+                pod, target, err, cached = await self._locate(ns, name, fresh)
             if err is not None:
                 return err
             stub = self.workers.channel(target).unary_unary(
                 api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
                 response_deserializer=api.AddGPUResponse.FromString)
             try:
-                resp = await stub(api.AddGPURequest(
-                    pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
-                    request_id=rid, container=container, idempotency_key=key,
-                    requested_by=user, lease_s=lease_s),
-                    timeout=self.cfg.rpc_timeout_s)
+                with trace.span("master_rpc"):
+                    resp = await stub(api.AddGPURequest(
+                        pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
+                        request_id=rid, container=container, idempotency_key=key,
+                        requested_by=user, lease_s=lease_s),
+                        timeout=self.cfg.rpc_timeout_s)
             except grpc.aio.AioRpcError as e:
                 if cached and e.code() == grpc.StatusCode.FAILED_PRECONDITION and \
                         "this worker serves" in (e.details() or ""):
@@ -326,16 +328,19 @@ class Master:
         """RemoveGPU through the pod's worker (reference main.go:206-224 mapping)."""
         t0 = time.perf_counter()
         for fresh in (False, True):
-            pod, target, err, cached = await self._locate(ns, name, fresh)
+            with trace.span("master_locate"):
+                pod, target, err, cached = await self._locate(ns, name, fresh)
             if err is not None:
                 return err
             stub = self.workers.channel(target).unary_unary(
                 api.REMOVE_GPU, request_serializer=api.RemoveGPURequest.SerializeToString,
                 response_deserializer=api.RemoveGPUResponse.FromString)
             try:
-                resp = await stub(api.RemoveGPURequest(
-                    pod_name=name, namespace=ns, uuids=uuids, force=force, request_id=rid,
-                    container=container, requested_by=user), timeout=self.cfg.rpc_timeout_s)
+                with trace.span("master_rpc"):
+                    resp = await stub(api.RemoveGPURequest(
+                        pod_name=name, namespace=ns, uuids=uuids, force=force,
+                        request_id=rid, container=container, requested_by=user),
+                        timeout=self.cfg.rpc_timeout_s)
             except grpc.aio.AioRpcError as e:
                 _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name,
                            e.details())
@@ -359,10 +364,16 @@ class Master:
 
     # ------------------------------------------------------------------------ HTTP routes
     async def add_gpu(self, request: web.Request) -> web.Response:
+        # gm:master_* roctx ranges; the stage split is returned as ``master_timings``
+        with trace.span("master_addgpu") as root:
+            return await self._add_gpu(request, root)
+
+    async def _add_gpu(self, request: web.Request, root: trace.Span) -> web.Response:
         route = "addgpu"
         mi = request.match_info
         ns, name = mi["namespace"], mi["pod"]
-        denied = await self._denied(request, route, "create", ns, name=name)
+        with trace.span("master_authz"):
+            denied = await self._denied(request, route, "create", ns, name=name)
         if denied is not None:
             return denied
         rid = log.new_request_id("add")
@@ -386,13 +397,18 @@ class Master:
             ns, name, n, entire, request.query.get("container", ""), rid,
             request.headers.get("Idempotency-Key", "") or rid, request.get(USER_KEY, ""),
             lease_s)
-        return self._reply(request, route, status, text, payload)
+        return self._reply(request, route, status, text, self._stamp(payload, root))
 
     async def remove_gpu(self, request: web.Request) -> web.Response:
+        with trace.span("master_removegpu") as root:
+            return await self._remove_gpu(request, root)
+
+    async def _remove_gpu(self, request: web.Request, root: trace.Span) -> web.Response:
         route = "removegpu"
         mi = request.match_info
         ns, name = mi["namespace"], mi["pod"]
-        denied = await self._denied(request, route, "delete", ns, name=name)
+        with trace.span("master_authz"):
+            denied = await self._denied(request, route, "delete", ns, name=name)
         if denied is not None:
             return denied
         rid = log.new_request_id("rm")
@@ -411,7 +427,16 @@ class Master:
         status, text, payload = await self._remove(ns, name, uuids, force,
                                                    request.query.get("container", ""), rid,
                                                    request.get(USER_KEY, ""))
-        return self._reply(request, route, status, text, payload)
+        return self._reply(request, route, status, text, self._stamp(payload, root))
+
+    @staticmethod
+    def _stamp(payload: dict, root: trace.Span) -> dict:
+        """The master's own stage split so far (authz, locate, rpc, payload), for the JSON
+        reply; the text reply ignores it."""
+        if payload:
+            payload["master_timings"] = [{"name": k, "ms": round(v, 4)}
+                                         for k, v in root.flat().items()]
+        return payload
 
     async def batch(self, request: web.Request) -> web.Response:
         """``POST /api/v1/batch`` {"operations": [{"op": "add", "namespace", "pod", "gpus",
@@ -476,7 +501,8 @@ class Master:
 
     @staticmethod
     def _payload(resp, t0: float) -> dict:
-        d = protodef.to_dict(resp)
+        with trace.span("master_payload"):
+            d = protodef.to_dict(resp)
         d["master_ms"] = (time.perf_counter() - t0) * 1e3
         return d
 

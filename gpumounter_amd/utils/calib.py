@@ -8,13 +8,16 @@ moves with two properties of the machine it runs on, which this module measures 
   median of several repeats: how fast the interpreter runs the handlers;
 * ``pingpong_us`` / ``tcp_rtt_us`` — the round trip between two processes over a socketpair and
   over a loopback TCP connection, median of many: what one hop between the daemons costs before
-  any gpumounter code runs (scheduler wake-up of an idle core, C-state exit, cross-CCX cache).
+  any gpumounter code runs (scheduler wake-up of an idle core, C-state exit, cross-CCX cache);
+* ``grpc_rtt_us`` — a unary AddGPU call between two grpc.aio processes answering at once,
+  plaintext and mTLS: the floor under the master → worker hop.
 
 A value measured on a box whose ``pingpong_us`` is 3× another's is not a regression of the code;
 ``bench.py`` puts this dict into its JSON as ``box`` so every number carries its box.
 """
 from __future__ import annotations
 
+import json
 import os
 import socket
 import statistics
@@ -88,6 +91,91 @@ def pingpong_us(n: int = 2000, tcp: bool = False) -> float:
         os.waitpid(pid, 0)
 
 
+def _grpc_server() -> None:
+    """``python -m gpumounter_amd.utils.calib --grpc-server``: an AddGPU service answering
+    Success at once, plaintext and mTLS ports printed on stdout, until stdin closes."""
+    import asyncio
+    import shutil
+    import sys
+    import tempfile
+
+    import grpc
+
+    from gpumounter_amd.api import gpu_mount as api
+    from gpumounter_amd.fakes.pki import make_pki
+
+    async def run():
+        pki = make_pki(tempfile.mkdtemp(prefix="gm-calib-"))
+
+        async def add(req, ctx):
+            return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS)
+        server = grpc.aio.server()
+        server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(
+            f"{api.PACKAGE}.AddGPUService", {"AddGPU": grpc.unary_unary_rpc_method_handler(
+                add, api.AddGPURequest.FromString, lambda m: m.SerializeToString())}),))
+        rd = lambda p: open(p, "rb").read()   # noqa: E731
+        creds = grpc.ssl_server_credentials([(rd(pki["worker.key"]), rd(pki["worker.crt"]))],
+                                            root_certificates=rd(pki["ca"]),
+                                            require_client_auth=True)
+        plain = server.add_insecure_port("127.0.0.1:0")
+        tls = server.add_secure_port("127.0.0.1:0", creds)
+        await server.start()
+        print(json.dumps({"plain": plain, "tls": tls, "pki": pki}), flush=True)
+        await asyncio.get_running_loop().run_in_executor(None, sys.stdin.read)
+        await server.stop(0)
+        shutil.rmtree(os.path.dirname(pki["ca"]), ignore_errors=True)
+    asyncio.run(run())
+
+
+def grpc_rtt_us(n: int = 1500) -> dict:
+    """Median unary AddGPU round trip, grpc.aio client → grpc.aio server in another process,
+    plaintext and with the shipped mTLS: the floor under the master → worker hop."""
+    import asyncio
+    import subprocess
+    import sys
+
+    import grpc
+
+    from gpumounter_amd.api import gpu_mount as api
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = {**os.environ, "PYTHONPATH": root + os.pathsep + os.environ.get("PYTHONPATH", "")}
+    p = subprocess.Popen([sys.executable, "-m", "gpumounter_amd.utils.calib", "--grpc-server"],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+    try:
+        info = json.loads(p.stdout.readline())
+        rd = lambda f: open(f, "rb").read()   # noqa: E731
+
+        async def one(secure: bool) -> float:
+            if secure:
+                pki = info["pki"]
+                creds = grpc.ssl_channel_credentials(rd(pki["ca"]), rd(pki["master.key"]),
+                                                     rd(pki["master.crt"]))
+                ch = grpc.aio.secure_channel(
+                    f"127.0.0.1:{info['tls']}", creds,
+                    options=[("grpc.ssl_target_name_override", "gpu-mounter-worker")])
+            else:
+                ch = grpc.aio.insecure_channel(f"127.0.0.1:{info['plain']}")
+            stub = ch.unary_unary(api.ADD_GPU,
+                                  request_serializer=api.AddGPURequest.SerializeToString,
+                                  response_deserializer=api.AddGPUResponse.FromString)
+            ts = []
+            for _ in range(n):
+                t0 = time.perf_counter()
+                await stub(api.AddGPURequest(pod_name="t", namespace="default", gpu_num=1),
+                           timeout=10)
+                ts.append((time.perf_counter() - t0) * 1e6)
+            await ch.close()
+            return round(statistics.median(ts[n // 10:]), 1)
+
+        async def both():
+            return {"plain": await one(False), "mtls": await one(True)}
+        return asyncio.run(both())
+    finally:
+        p.stdin.close()
+        p.wait(10)
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as fh:
@@ -107,14 +195,15 @@ def _governor() -> str | None:
         return None
 
 
-def measure() -> dict:
-    """Fixed calibration, about 0.3 s. Safe before or after GPU initialisation (fork only runs
-    pure-Python socket code in the child and ``_exit``s; it never execs)."""
+def measure(grpc_floor: bool = False) -> dict:
+    """Fixed calibration, about 0.3 s (about 2 s more with ``grpc_floor``). Run it before the
+    process initialises the GPU: the pingpong child is a fork (pure-Python socket code, then
+    ``_exit``) and the gRPC server a subprocess."""
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = None
-    return {
+    out = {
         "py_loop_us": round(py_loop_us(), 1),
         "pingpong_us": round(pingpong_us(), 2),
         "tcp_rtt_us": round(pingpong_us(1000, tcp=True), 2),
@@ -124,8 +213,14 @@ def measure() -> dict:
         "loadavg_1m": round(os.getloadavg()[0], 2),
         "governor": _governor(),
     }
+    if grpc_floor:
+        out["grpc_rtt_us"] = grpc_rtt_us()
+    return out
 
 
 if __name__ == "__main__":
-    import json
-    print(json.dumps(measure()))
+    import sys
+    if "--grpc-server" in sys.argv:
+        _grpc_server()
+    else:
+        print(json.dumps(measure(grpc_floor="--grpc" in sys.argv)))

@@ -13,6 +13,7 @@ import asyncio
 import json
 import os
 import signal
+import time
 from typing import Optional
 
 import grpc
@@ -160,11 +161,19 @@ class Worker:
             # the caller goes away: a master killed or a deadline passed mid-request cancels
             # this handler, and a cancellation landing between two steps would leave a
             # placeholder created but never admitted or mounted, or rules without nodes
-            op = asyncio.ensure_future(fn(request))
+            t0 = time.perf_counter()
+            op = asyncio.ensure_future(self._timed(fn, request))
             self._ops.add(op)
             op.add_done_callback(self._ops.discard)
             try:
-                return await asyncio.shield(op)
+                resp, t1, t2 = await asyncio.shield(op)
+                if hasattr(resp, "timings"):
+                    # the handler around the operation: rpc_queue = until the operation's task
+                    # ran, rpc_tail = from its end until the handler resumed. What is left of
+                    # the master's RPC time is gRPC transport (client, server, TLS)
+                    resp.timings.add(name="rpc_queue", ms=(t1 - t0) * 1e3)
+                    resp.timings.add(name="rpc_tail", ms=(time.perf_counter() - t2) * 1e3)
+                return resp
             except asyncio.CancelledError:
                 op.add_done_callback(self._orphan_done)     # its outcome reaches no caller
                 raise
@@ -176,6 +185,11 @@ class Worker:
                 _log.exception("rpc failed")
                 await context.abort(grpc.StatusCode.INTERNAL, f"Service Internal Error: {e}")
         return handler
+
+    @staticmethod
+    async def _timed(fn, request):
+        t1 = time.perf_counter()
+        return await fn(request), t1, time.perf_counter()
 
     @staticmethod
     def _orphan_done(op: asyncio.Future) -> None:
