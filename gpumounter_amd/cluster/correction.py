@@ -95,9 +95,10 @@ class ReserveGate:
 
 
 def placement_worse(inv, attached: Sequence[AmdGpu], got: Sequence[str],
-                    want: Sequence[str]) -> bool:
+                    want: Sequence[str], on: str = "numa") -> bool:
     """The admitted set ``got`` scores worse together with the pod's ``attached`` GPUs than the
-    preferred set ``want`` would have."""
+    preferred set ``want`` would have; ``on="xgmi"``: worse by at least a non-xGMI pair or a
+    hive split (a NUMA split alone does not count)."""
     if not want or len(want) != len(got):
         return False
     keys = inv.by_key()
@@ -111,8 +112,9 @@ def placement_worse(inv, attached: Sequence[AmdGpu], got: Sequence[str],
     table = {x.index: x for x in inv.gpus()}
     att = [x.index for x in attached]
     links = inv.links()
+    margin = topology.W_NON_XGMI - 1e-6 if on == "xgmi" else 1e-6
     return topology.score_set(table, links, att + g)[0] > \
-        topology.score_set(table, links, att + w)[0] + 1e-6
+        topology.score_set(table, links, att + w)[0] + margin
 
 
 class Book(enum.Enum):

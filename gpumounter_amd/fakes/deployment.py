@@ -194,6 +194,7 @@ class ProcessCluster:
                    "GM_METRICS_PORT": "0", "GM_READY_FILE": self._ready_path(f"worker-{node}"),
                    "GM_LOG_LEVEL": "WARNING",
                    "GM_LOG_JSON": "false", "GM_GPU_ALLOCATION": self.gpu_api,
+                   "GM_DEBUG_ENDPOINTS": "1",     # /debug/tasks for chaos post-mortems
                    **self.worker_env}
             self._worker_env[node] = env
             self._spawn(f"worker-{node}", [*self.entry, "worker"], env)

@@ -566,8 +566,10 @@ async def serve(cfg) -> None:
     loop = asyncio.get_running_loop()
     for sig in (signal.SIGTERM, signal.SIGINT):
         loop.add_signal_handler(sig, stop.set)
-    await m.start()
+    # a failed start still stops what it started: no gRPC server or executor thread left
+    # behind keeps a half-started daemon alive
     try:
+        await m.start()
         await stop.wait()
     finally:
         await m.stop()

@@ -165,8 +165,11 @@ class Pinned:
         fd = self.fds.get(pid)
         if fd is None:
             return True
-        r, _, _ = select.select([fd], [], [], 0)   # a pidfd polls readable once it exits
-        return bool(r)
+        # a pidfd polls readable once its process exits; poll(2), not select(2): the drain
+        # keeper holds pidfds for long, and select() refuses any fd ≥ FD_SETSIZE (1024)
+        p = select.poll()
+        p.register(fd, select.POLLIN)
+        return bool(p.poll(0))
 
     def signal(self, pids: Sequence[int], sig: int) -> List[int]:
         """0 or -errno per PID; never reaches a process other than the pinned one."""

@@ -119,8 +119,17 @@ class Config:
     #   when the plugin chose badly);
     # trim: always hold every free GPU with 1-GPU placeholders, keep the topology-chosen ones
     #   (SURVEY §7.4.3);
-    # hint: the preferred set is only an annotation (no shipped device plugin reads it)
+    # hint: the preferred set is only an annotation (no shipped device plugin reads it).
+    # Default auto since round 3 (before: hint, the reference's topology-blind behaviour). A
+    # correction holds one 1-GPU placeholder per free GPU for a moment under the node's
+    # exclusive reservation gate (other attaches on the node wait for it), and in tenant
+    # placeholder-namespace mode those holds count against the tenant's quota;
+    # gm_placement_corrections_total counts them
     placement_enforce: str = "auto"
+    # which worse placement auto corrects: numa = any worse score (hive split, non-xGMI pair or
+    # a NUMA split); xgmi = only a hive split or a non-xGMI pair (fewer corrections on nodes
+    # whose GPUs all share one hive, at the cost of NUMA-split sets)
+    placement_correct_on: str = "numa"
     ledger_get: bool = True            # read admitted placeholders with PodResources v1 Get
     reconcile_on_events: bool = True   # react to placeholder/tenant deletes at once
     # auto: fd scan of the container's PIDs, amdsmi only for PIDs whose fd table is unreadable;
@@ -183,6 +192,9 @@ class Config:
     # unless this is set explicitly (hermetic tests, lab clusters)
     worker_insecure: bool = False
     metrics_period_s: float = 15.0     # refresh of the per-GPU process and ledger gauges
+    # serve /debug/tasks (every asyncio task's stack) on the worker's metrics port; it has no
+    # authentication and that port binds worker_host, so it is off unless asked for
+    debug_endpoints: bool = False
     # --- observability ---------------------------------------------------------------------
     log_level: str = "INFO"            # DEBUG | INFO | WARNING | ERROR
     log_file: str = ""                 # also log to this file, rotated ("" = stderr only)
@@ -245,6 +257,7 @@ class Config:
         _choice("devnode_userns", self.devnode_userns, ("auto", "bind", "off"))
         _choice("topology_policy", self.topology_policy, ("xgmi", "first-fit"))
         _choice("placement_enforce", self.placement_enforce, ("auto", "hint", "trim"))
+        _choice("placement_correct_on", self.placement_correct_on, ("numa", "xgmi"))
         _choice("busy_detection", self.busy_detection, ("auto", "both"))
         _choice("authz_mode", self.authz_mode, ("none", "kube"))
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))

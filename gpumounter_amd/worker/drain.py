@@ -16,10 +16,19 @@ the driver) leaves its placeholder *draining*:
   restarted worker (which holds no pidfds) still knows exactly which processes to wait for;
 * this worker waits on the pidfds (event-driven, no polling) and releases the placeholder the
   moment the last one exits; the reconciler's sweep covers the restart case.
+
+Marking is a PATCH, and it can fail. Until it succeeds the placeholder is *unmarked*: still
+labelled as the tenant's, but its GPU's access is already revoked, so it is left out of the
+tenant's mount state (nothing re-grants it, RemoveGPU does not offer it again) and is never
+released while a killed process runs. The mark is retried (0.1/0.5/2/5/15 s, then every 30 s)
+alongside the pidfd wait; the pending set is kept in ``<state_dir>/drain_pending.json`` so a
+restarted worker resumes it (by ``pid:starttime``) instead of re-granting the GPU.
 """
 from __future__ import annotations
 
 import asyncio
+import json
+import os
 from typing import Dict, List, Sequence, Tuple
 
 from gpumounter_amd.cluster.kube import NotFound
@@ -50,28 +59,62 @@ def parse_pids(value: str) -> List[Tuple[int, int]]:
 
 
 class DrainKeeper:
+    # a failed draining mark is retried after these delays, then every MARK_RETRY_LAST_S
+    MARK_RETRY_S = (0.1, 0.5, 2.0, 5.0, 15.0)
+    MARK_RETRY_LAST_S = 30.0
+
     def __init__(self, service) -> None:
         self.svc = service
         # placeholder uid → (placeholder, the pidfds still waited on)
         self.held: Dict[str, Tuple[Placeholder, procs.Pinned]] = {}
+        # placeholder uid → {"ns", "name", "owner", "pids"}: revoked from its tenant, still
+        # booked, draining mark not written yet (retried; persisted for a restarted worker)
+        self.unmarked: Dict[str, dict] = {}
+        sd = getattr(getattr(service, "cfg", None), "state_dir", "")
+        self._path = os.path.join(sd, "drain_pending.json") if sd else ""
+        self._load()
         self._tasks: set = set()
         self.released = 0
 
-    async def hold(self, owner: dict, phs: Sequence[Placeholder], pinned: procs.Pinned,
-                   pids: Sequence[int]) -> List[Placeholder]:
-        """Turn ``phs`` into draining placeholders waiting for ``pids`` (taking ownership of
-        ``pinned``). Returns the placeholders that could not be marked (the caller keeps them
-        owned by the tenant, so they stay booked either way)."""
-        pinned.keep_only(pids)
-        mark = ",".join(f"{p}:{procs.start_time(p)}" for p in sorted(pids))
-        patch = {"metadata": {
+    # ------------------------------------------------------------------------ pending marks
+    def _load(self) -> None:
+        if not self._path:
+            return
+        try:
+            with open(self._path, encoding="utf-8") as fh:
+                self.unmarked = {k: v for k, v in json.load(fh).items() if isinstance(v, dict)}
+        except FileNotFoundError:
+            pass
+        except (OSError, ValueError) as e:
+            _log.error("drain: unreadable %s (%s); ignoring it", self._path, e)
+
+    def _save(self) -> None:
+        if not self._path:
+            return
+        tmp = self._path + ".tmp"
+        try:
+            os.makedirs(os.path.dirname(self._path), mode=0o700, exist_ok=True)
+            with open(tmp, "w", encoding="utf-8") as fh:
+                fh.write(json.dumps(self.unmarked))
+            os.replace(tmp, self._path)
+        except OSError as e:
+            _log.error("drain: cannot persist pending marks: %s", e)
+
+    def _patch(self, owner: str, mark: str) -> dict:
+        return {"metadata": {
             "labels": {LABEL_OWNER: None, LABEL_OWNER_NS: None},
             "ownerReferences": None,
             "annotations": {ANN_MOUNT_MODE: MODE_DRAINING, ANN_DRAIN_PIDS: mark,
-                            ANN_DRAIN_OWNER: f"{podu.ns_of(owner)}/{podu.name_of(owner)}",
-                            ANN_OWNER_UID: None, ANN_IDEMPOTENCY: None, ANN_GROUP: None}}}
+                            ANN_DRAIN_OWNER: owner, ANN_OWNER_UID: None, ANN_IDEMPOTENCY: None,
+                            ANN_GROUP: None}}}
+
+    async def _mark(self, phs: Sequence[Placeholder], owner: str, mark: str
+                    ) -> List[Placeholder]:
+        """PATCH ``phs`` into draining placeholders; returns those not marked (they stay in
+        :attr:`unmarked`, persisted)."""
         kube = self.svc.ph.kube
         epoch = self.svc.ph.informer.epoch
+        patch = self._patch(owner, mark)
         res = await asyncio.gather(*[kube.patch_pod(p.namespace, p.name, patch) for p in phs],
                                    return_exceptions=True)
         failed = []
@@ -79,30 +122,54 @@ class DrainKeeper:
             if isinstance(r, dict):
                 self.svc.ph.informer.upsert(r, epoch)
                 ph.mode = MODE_DRAINING
+                self.unmarked.pop(ph.uid, None)
+            elif isinstance(r, NotFound):
+                self.unmarked.pop(ph.uid, None)     # gone: nothing left to book
             else:
-                _log.error("mark %s/%s draining: %s", ph.namespace, ph.name, r)
+                _log.error("mark %s/%s draining: %s (retried)", ph.namespace, ph.name, r)
+                self.unmarked[ph.uid] = {"ns": ph.namespace, "name": ph.name, "owner": owner,
+                                         "pids": mark}
                 failed.append(ph)
-        marked = [ph for ph in phs if ph not in failed]
-        if not marked:
-            pinned.close()
-            return failed
-        for ph in marked:
+        self._save()
+        return failed
+
+    def _delays(self):
+        yield from self.MARK_RETRY_S
+        while True:
+            yield self.MARK_RETRY_LAST_S
+
+    # ------------------------------------------------------------------------ hold / wait
+    async def hold(self, owner: dict, phs: Sequence[Placeholder], pinned: procs.Pinned,
+                   pids: Sequence[int]) -> List[Placeholder]:
+        """Turn ``phs`` into draining placeholders waiting for ``pids`` (taking ownership of
+        ``pinned``). Returns the placeholders whose mark failed: they are revoked and booked
+        all the same, and the mark is retried until it lands or the processes are gone."""
+        pinned.keep_only(pids)
+        mark = ",".join(f"{p}:{procs.start_time(p)}" for p in sorted(pids))
+        who = f"{podu.ns_of(owner)}/{podu.name_of(owner)}"
+        failed = await self._mark(phs, who, mark)
+        for ph in phs:
             self.held[ph.uid] = (ph, pinned)
         self.svc.metrics.draining.set(len(self.held))
-        self.svc.metrics.reconcile_actions.labels(action="drain_hold").inc(len(marked))
+        self.svc.metrics.reconcile_actions.labels(action="drain_hold").inc(len(phs))
         log.kv(_log, 30, "GPU held until killed processes exit", pids=list(pids),
-               placeholders=[p.name for p in marked])
-        t = asyncio.ensure_future(self._wait(marked, pinned, list(pids)))
+               placeholders=[p.name for p in phs], unmarked=[p.name for p in failed])
+        t = asyncio.ensure_future(self._wait(list(phs), pinned, list(pids), who, mark))
         self._tasks.add(t)
         t.add_done_callback(self._tasks.discard)
         return failed
 
-    async def _wait(self, phs: List[Placeholder], pinned: procs.Pinned, pids: List[int]) -> None:
+    async def _wait(self, phs: List[Placeholder], pinned: procs.Pinned, pids: List[int],
+                    owner: str, mark: str) -> None:
+        delays = self._delays()
         try:
             while pinned.fds:
-                left = await pinned.wait_exit(pids, 3600.0)
+                pending = [ph for ph in phs if ph.uid in self.unmarked]
+                left = await pinned.wait_exit(pids, next(delays) if pending else 3600.0)
                 if not left:
                     break
+                if pending:
+                    await self._mark(pending, owner, mark)
             pinned.close()
             await self._release(phs)
         except asyncio.CancelledError:
@@ -111,11 +178,43 @@ class DrainKeeper:
         except Exception as e:  # noqa: BLE001 - the reconciler's sweep retries the release
             _log.error("drain release failed: %s", e)
 
+    async def resume(self) -> None:
+        """Worker start-up: marks a previous worker could not write. A placeholder still there
+        is marked (or released once its recorded processes are gone), retried in the
+        background; one gone is forgotten."""
+        for uid, rec in list(self.unmarked.items()):
+            cur = self.svc.ph.informer.cache.get((rec.get("ns"), rec.get("name")))
+            if cur is None or cur["metadata"].get("uid") != uid:
+                self.unmarked.pop(uid, None)
+                continue
+            t = asyncio.ensure_future(self._resume_one(uid, rec))
+            self._tasks.add(t)
+            t.add_done_callback(self._tasks.discard)
+        self._save()
+
+    async def _resume_one(self, uid: str, rec: dict) -> None:
+        ph = Placeholder(rec["ns"], rec["name"], uid)
+        delays = self._delays()
+        while uid in self.unmarked:
+            if not any(procs.same_process(pid, st) for pid, st in parse_pids(rec["pids"])):
+                try:
+                    await self._release([ph])
+                except Exception as e:  # noqa: BLE001 - retried below
+                    _log.error("drain release failed: %s", e)
+                else:
+                    return
+            else:
+                await self._mark([ph], rec["owner"], rec["pids"])
+            if uid in self.unmarked:
+                await asyncio.sleep(next(delays))
+
     async def _release(self, phs: Sequence[Placeholder]) -> None:
         for ph in phs:
             self.held.pop(ph.uid, None)
         self.svc.metrics.draining.set(len(self.held))
         await self.svc.ph.release(list(phs), wait=False)
+        if any(self.unmarked.pop(ph.uid, None) is not None for ph in phs):
+            self._save()
         self.released += len(phs)
         self.svc.metrics.reconcile_actions.labels(action="drain_release").inc(len(phs))
         log.kv(_log, 20, "drained GPU released", placeholders=[p.name for p in phs])

@@ -36,11 +36,15 @@ def expires_of(ph: dict) -> Optional[float]:
 class LeaseKeeper:
     def __init__(self, service) -> None:
         self.svc = service
-        self._timers: Dict[str, asyncio.TimerHandle] = {}     # placeholder uid → timer
+        # placeholder uid → (timer, the expiry it was armed for)
+        self._timers: Dict[str, Tuple[asyncio.TimerHandle, float]] = {}
         self._retry_after: Dict[Tuple[str, str], float] = {}   # owner → not before
         self._retry_timers: Dict[Tuple[str, str], asyncio.TimerHandle] = {}
         self._errors: Dict[Tuple[str, str], int] = {}          # owner → failed expiries in a row
         self._tasks: set = set()                               # running expiries
+        # placeholder uid → expiry this worker granted: the informer learns the annotation only
+        # from the watch echo of our PATCH, which can lag (a dropped stream, a relist)
+        self._granted: Dict[str, float] = {}
         self._stopped = False
         self.expired = 0
 
@@ -49,18 +53,39 @@ class LeaseKeeper:
         """Stamp the expiry on the attach's placeholders and arm a timer. Returns the expiry."""
         expires = time.time() + lease_s
         patch = {"metadata": {"annotations": {ANN_LEASE: f"{expires:.3f}"}}}
-        await asyncio.gather(*[self.svc.kube.patch_pod(p.namespace, p.name, patch)
-                               for p in placeholders])
+        informer = self.svc.ph.informer
+        epoch = informer.epoch
+        res = await asyncio.gather(*[self.svc.kube.patch_pod(p.namespace, p.name, patch)
+                                     for p in placeholders])
+        for r in res:
+            if isinstance(r, dict):
+                informer.upsert(r, epoch)    # visible to expire_owner before the watch echo
         for p in placeholders:
+            if p.uid:
+                self._granted[p.uid] = expires
             self._arm(p.uid, podu.ns_of(pod), podu.name_of(pod), expires)
         return expires
 
+    def granted(self, uid: str) -> bool:
+        return uid in self._granted
+
     def _arm(self, uid: str, ns: str, name: str, expires: float) -> None:
-        if not uid or uid in self._timers or self._stopped:
+        """A timer for the lease of placeholder ``uid`` (one per placeholder; re-arming an
+        armed one for a different expiry replaces it)."""
+        if not uid or self._stopped:
             return
+        old = self._timers.get(uid)
+        if old is not None:
+            if abs(old[1] - expires) < 1e-3:
+                return
+            old[0].cancel()
         loop = asyncio.get_running_loop()
-        self._timers[uid] = loop.call_later(max(0.0, expires - time.time()),
-                                            self._spawn, ns, name)
+        self._timers[uid] = (loop.call_later(max(0.0, expires - time.time()), self._fired,
+                                             uid, ns, name), expires)
+
+    def _fired(self, uid: str, ns: str, name: str) -> None:
+        self._timers.pop(uid, None)          # spent: a later _arm must create a new one
+        self._spawn(ns, name)
 
     def _spawn(self, ns: str, name: str) -> None:
         """Timer callback: run one expiry as a tracked task (cancelled by stop())."""
@@ -100,7 +125,7 @@ class LeaseKeeper:
         nothing runs against the closed clients. The next worker's start-up sweep picks the
         remaining leases up from the placeholder annotations."""
         self._stopped = True
-        for t in list(self._timers.values()) + list(self._retry_timers.values()):
+        for t in [h for h, _ in self._timers.values()] + list(self._retry_timers.values()):
             t.cancel()
         self._timers.clear()
         self._retry_timers.clear()
@@ -110,12 +135,19 @@ class LeaseKeeper:
                 task.cancel()
 
     # ------------------------------------------------------------------------ expiry
-    async def sweep(self) -> int:
+    async def sweep(self, expire_due: bool = True) -> int:
         """Expire every lease that is due (placeholder annotations: survives worker restarts)
-        and re-arm timers for the rest. Returns how many owners were handled."""
+        and re-arm timers for the rest. Returns how many owners were due. A worker re-arms
+        (``expire_due=False``) before it serves its first request, and expires what is due
+        once it is up. A failed expiry is retried like a timer's (0.1/0.5/2 s, then
+        ``lease_retry_s``)."""
         now = time.time()
         due: Dict[Tuple[str, str], List[dict]] = {}
-        for p in self.svc.ph.live():
+        live = self.svc.ph.live()
+        uids = {p["metadata"].get("uid") for p in live}
+        for uid in [u for u in self._granted if u not in uids]:
+            del self._granted[uid]          # released some other way (RemoveGPU, owner gone)
+        for p in live:
             exp = expires_of(p)
             if exp is None:
                 continue
@@ -128,8 +160,9 @@ class LeaseKeeper:
                 due.setdefault((ns, name), []).append(p)
             else:
                 self._arm(md.get("uid", ""), ns, name, exp)
-        for ns, name in due:
-            await self.expire_owner(ns, name)
+        if expire_due:
+            for ns, name in due:
+                await self._expire_or_retry(ns, name)
         return len(due)
 
     async def expire_owner(self, ns: str, name: str) -> None:
@@ -141,20 +174,33 @@ class LeaseKeeper:
             return                          # the owner-gone GC releases its placeholders
         now = time.time()
         st = await svc.pod_state(pod, fresh=True)
-        uuids = []
+        uuids, due = [], []
         for ph in st.placeholders:
             raw = next((p for p in svc.ph.owned_by(pod)
                         if p["metadata"]["name"] == ph.name), None)
             exp = expires_of(raw) if raw is not None else None
-            if exp is not None and exp <= now + 0.001:
+            if exp is None:
+                exp = self._granted.get(ph.uid)
+            if exp is None:
+                continue
+            if exp <= now + 0.001:
+                due.append(ph.uid)
                 uuids += [g.uuid for g in st.by_placeholder[(ph.namespace, ph.name)]]
-                self._timers.pop(ph.uid, None)
+                t = self._timers.pop(ph.uid, None)
+                if t is not None:
+                    t[0].cancel()
+            else:
+                # not due yet (a timer of an earlier lease of this owner, or one that fired a
+                # hair early): keep a timer for this one, it must not be lost
+                self._arm(ph.uid, ns, name, exp)
         if not uuids:
             return
         force = bool(svc.cfg.lease_force)
         resp = await svc.remove_gpu(api.RemoveGPURequest(
             pod_name=name, namespace=ns, uuids=uuids, force=force, requested_by="lease-expiry"))
         if resp.remove_gpu_result == api.REMOVE_SUCCESS:
+            for uid in due:
+                self._granted.pop(uid, None)
             self.expired += 1
             self._retry_after.pop((ns, name), None)
             svc.notify.event(pod, "GPULeaseExpired",

@@ -141,7 +141,7 @@ class Reconciler:
                     tuple(sorted((p.namespace, p.name, p.uid) for p in drop))))
 
     def _kick(self, key: tuple, attempt: int = 0) -> None:
-        if key in self._kicked:
+        if key in self._kicked or self._stopping:
             return
         self._kicked.add(key)
         t = asyncio.ensure_future(self._react(key, attempt))
@@ -149,7 +149,7 @@ class Reconciler:
         t.add_done_callback(self._bg.discard)
 
     def _retry(self, key: tuple, attempt: int) -> None:
-        if attempt > len(self.RETRY_DELAYS) or key in self._timers:
+        if attempt > len(self.RETRY_DELAYS) or key in self._timers or self._stopping:
             return
         loop = asyncio.get_running_loop()
         self._timers[key] = loop.call_later(self.RETRY_DELAYS[attempt - 1], self._fire, key,
@@ -367,6 +367,9 @@ class Reconciler:
                                                                               "Failed")
 
         async def collect(ons: str, oname: str, phs: List[dict]) -> None:
+            # a force-removed GPU whose draining mark is pending stays booked until its killed
+            # processes are gone (worker/drain.py), owner or not
+            phs = [p for p in phs if p["metadata"].get("uid") not in svc.drain.unmarked]
             for p in phs:
                 rep.owner_gone.append(p["metadata"]["name"])
                 m.orphans.labels(kind="owner_gone").inc()

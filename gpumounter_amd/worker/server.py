@@ -245,6 +245,10 @@ class Worker:
             _log.info("device-manager checkpoint %s: %s, inotify %s", self.checkpoint.path,
                       "present" if self.checkpoint.snapshot() is not None else "absent",
                       "on" if watched else "off")
+        # lease timers from the placeholders' annotations, and draining marks a previous worker
+        # could not write, before the first request is served
+        await self.service.lease.sweep(expire_due=False)
+        await self.service.drain.resume()
         if not (self.cfg.tls_cert and self.cfg.tls_key and self.cfg.tls_ca) and \
                 not self.cfg.worker_insecure:
             raise ValueError("worker refuses to serve gRPC without mTLS: set GM_TLS_CERT, "
@@ -281,7 +285,8 @@ class Worker:
             app.router.add_get("/metrics", self._metrics)
             app.router.add_get("/status", self._http_status)
             app.router.add_get("/audit/{namespace}/{pod}", self._http_audit)
-            app.router.add_get("/debug/tasks", self._debug_tasks)
+            if self.cfg.debug_endpoints:    # stacks of every task: not for the open port
+                app.router.add_get("/debug/tasks", self._debug_tasks)
             self.http_runner = web.AppRunner(app, access_log=None)
             await self.http_runner.setup()
             site = web.TCPSite(self.http_runner, self.cfg.worker_host, hp)
@@ -406,6 +411,12 @@ class Worker:
             self._collector.cancel()
         if getattr(self, "_health_task", None) is not None:
             self._health_task.cancel()
+        # no new RPCs; the ones running finish (or roll back) while the keepers they hand work
+        # to (reconciler follow-ups, leases, drains, notifications) still run
+        if self.grpc_server is not None:
+            await self.grpc_server.stop(0.5)
+        if self._ops:
+            await asyncio.wait(list(self._ops), timeout=self.OPS_DRAIN_S)
         await self.pool.stop()
         await self.reconciler.stop()
         await self.service.lease.stop()
@@ -415,10 +426,6 @@ class Worker:
             self.backend.sync.stop()
         if self.plugin is not None:
             await self.plugin.stop()
-        if self.grpc_server is not None:
-            await self.grpc_server.stop(0.5)
-        if self._ops:   # operations whose callers left: let them finish (or roll back)
-            await asyncio.wait(list(self._ops), timeout=self.OPS_DRAIN_S)
         if self.http_runner is not None:
             await self.http_runner.cleanup()
         await self.ph_informer.stop()
@@ -439,8 +446,10 @@ async def serve(cfg) -> None:
     loop = asyncio.get_running_loop()
     for sig in (signal.SIGTERM, signal.SIGINT):
         loop.add_signal_handler(sig, stop.set)
-    await w.start()
+    # a failed start still stops what it started: no gRPC server or executor thread left
+    # behind keeps a half-started daemon alive
     try:
+        await w.start()
         await stop.wait()
     finally:
         await w.stop()

@@ -49,7 +49,7 @@ from gpumounter_amd.utils import log, trace
 from gpumounter_amd.utils.faults import FaultInjector, InjectedFault
 from gpumounter_amd.utils.metrics import Metrics
 from gpumounter_amd.worker.drain import DrainKeeper
-from gpumounter_amd.worker.lease import LeaseKeeper
+from gpumounter_amd.worker.lease import LeaseKeeper, expires_of
 from gpumounter_amd.worker import status
 from gpumounter_amd.worker.notify import Notifier
 
@@ -200,9 +200,11 @@ class GpuMountService:
         """
         st = PodGpuState()
         # a failed attach's placeholder that is still being released is nobody's GPU: a rollback
-        # or a later attach of the same pod must not mount it (it is schedulable once deleted)
+        # or a later attach of the same pod must not mount it (it is schedulable once deleted);
+        # nor is a force-removed one whose draining mark is still being retried (worker/drain.py)
         owned = [p for p in self.ph.owned_by(pod)
-                 if p["metadata"].get("uid") not in self.abandoned]
+                 if p["metadata"].get("uid") not in self.abandoned
+                 and p["metadata"].get("uid") not in self.drain.unmarked]
         uid = podu.uid_of(pod)
         cached = [self.ph.cached(p) for p in owned]
         ledger: Optional[Dict[Tuple[str, str], List[str]]] = ledger_snapshot
@@ -431,7 +433,7 @@ class GpuMountService:
             with trace.span("ledger_read"):
                 st = await self.pod_state(pod)
             if req.idempotency_key:
-                replay = self._replay(pod, st, req.idempotency_key)
+                replay = await self._replay(pod, st, req.idempotency_key, req.lease_s)
                 if replay is not None:
                     return replay
             ok, why = can_mount(st.mount_type, req.is_entire_mount)
@@ -535,14 +537,23 @@ class GpuMountService:
             await self._release(res.placeholders)
             raise
 
-    def _replay(self, pod: dict, st: PodGpuState, key: str):
+    async def _replay(self, pod: dict, st: PodGpuState, key: str, lease_s: float = 0.0):
         """A retried request (same idempotency key) returns the earlier attach instead of adding
-        more GPUs; the mount itself is re-checked (repair) so a half-finished attempt completes."""
-        mine = {p["metadata"]["name"] for p in self.ph.owned_by(pod)
-                if (p["metadata"].get("annotations") or {}).get(ANN_IDEMPOTENCY) == key
-                and p["metadata"].get("uid") not in self.abandoned}
+        more GPUs; the mount itself is re-checked (repair) so a half-finished attempt completes,
+        and so is its lease: an attempt cut off (worker killed) between the mount and the lease
+        annotation would otherwise hand back GPUs that never expire."""
+        raw = {p["metadata"]["name"]: p for p in self.ph.owned_by(pod)
+               if (p["metadata"].get("annotations") or {}).get(ANN_IDEMPOTENCY) == key
+               and p["metadata"].get("uid") not in self.abandoned
+               and p["metadata"].get("uid") not in self.drain.unmarked}
+        mine = set(raw)
         if not mine:
             return None
+        if lease_s > 0:
+            unleased = [ph for ph in st.placeholders if ph.name in mine and
+                        expires_of(raw[ph.name]) is None and not self.lease.granted(ph.uid)]
+            if unleased:
+                await self.lease.grant(pod, unleased, lease_s)
         gs, owner = [], {}
         for ph in st.placeholders:
             if ph.name in mine:
@@ -590,7 +601,8 @@ class GpuMountService:
 
     def _placement_worse(self, st: PodGpuState, got: Sequence[str],
                          want: Sequence[str]) -> bool:
-        return placement_worse(self.inv, st.hot + st.own, got, want)
+        return placement_worse(self.inv, st.hot + st.own, got, want,
+                               getattr(self.cfg, "placement_correct_on", "numa"))
 
     async def _correct(self, pod: dict, n: int, req, st: PodGpuState, res):
         """Swap the plugin's worse-placed choice for the best free set (cluster/correction.py:
@@ -840,10 +852,8 @@ class GpuMountService:
                     phs = [ph for ph in phs if ph not in held]
                     p, pinned = pinned, None
                     with trace.span("drain_hold", placeholders=len(held)):
-                        unmarked = await self.drain.hold(pod, held, p, survivors)
-                    if unmarked:   # still the tenant's: booked, and retried by RemoveGPU
-                        _log.error("placeholders %s stay with %s/%s",
-                                   [u.name for u in unmarked], req.namespace, req.pod_name)
+                        # revoked and booked either way; a failed draining mark is retried
+                        await self.drain.hold(pod, held, p, survivors)
                 else:
                     pinned.close()
                     pinned = None

@@ -1289,3 +1289,18 @@ def test_candidates_of_a_failed_trim_pick_are_released_by_the_follow_up():
         code, _ = await lc.add("default", "tp", 1)          # and the node is usable again
         assert code == 200
     run(body, alloc_policy="first-free", worker_overrides={"placement_enforce": "trim"})
+
+
+def test_placement_correct_on_xgmi_leaves_numa_only_differences_alone():
+    """placement_correct_on=xgmi: on a node whose GPUs all share one hive (the mock MI355X
+    node), a plugin pick that only crosses the socket is kept — no correction round, no
+    exclusive hold of every free GPU (the cost of the default)."""
+    async def body(lc):
+        lc.tenant("other")
+        lc.tenant("t")
+        assert (await lc.add("default", "other", 3))[0] == 200
+        code, b = await lc.add("default", "t", 2)
+        assert code == 200 and _numa_of(lc, b["devices"]) == {0, 1}, b
+        assert lc.nodes["node-0"].worker.metrics.placement_corrections._value.get() == 0
+        assert len(node_of(lc).allocated) == 5 and not await lc.audit("default", "t")
+    run(body, alloc_policy="first-free", worker_overrides={"placement_correct_on": "xgmi"})

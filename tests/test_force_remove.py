@@ -203,3 +203,55 @@ def test_drain_survives_a_real_worker_crash_in_the_process_deployment(tmp_path, 
         if p.poll() is None:
             p.kill()
             p.wait()
+
+
+def test_a_failed_draining_mark_is_retried_and_never_regranted(stubborn, mock_inventory,
+                                                                monkeypatch):
+    """the PATCH that turns a force-removed GPU's placeholder into a draining one
+    fails. Its access is already revoked and the placeholder still names the tenant: the
+    reconciler must not grant the GPU back, the GPU must stay booked while the killed process
+    runs, and the mark is retried until it lands — across a worker restart too."""
+    p, table = stubborn
+    real = procs_mod.Pinned.signal
+    monkeypatch.setattr(procs_mod.Pinned, "signal",
+                        lambda self, pids, sig: [0] * len(pids) if sig == 9 else
+                        real(self, pids, sig))
+
+    async def main():
+        async with one_gpu_cluster(mock_inventory, kill_grace_s=0.1, kill_reap_s=0.1) as lc:
+            lc.tenant("busy", pids={"main": [p.pid]})
+            _, b = await lc.add("default", "busy", 1)
+            dev = b["devices"][0]
+            table.write_text(f"{dev['index']} {p.pid} 4096 python\n")
+            lc.cluster.fail_next("PATCH", 503, count=1000)        # every mark fails for now
+            code, b2 = await lc.remove("default", "busy", [dev["uuid"]], force=True)
+            assert code == 400 and "revoked" in b2["detail"], b2
+            w = lc.nodes["node-0"].worker
+            (ph,) = lc.cluster.placeholders()
+            assert ph["metadata"]["annotations"].get("gpumounter.amd.com/mount-mode") != \
+                "draining"                                       # still labelled the tenant's
+            rep = await w.reconciler.run_once()
+            assert not rep.repaired, rep                         # not granted back
+            st = await w.service.pod_state(lc.cluster.get("default", "busy"), fresh=True)
+            assert st.hot == [] and not await lc.audit("default", "busy")
+            assert len(lc.cluster.placeholders()) == 1           # still booked
+            assert len(w.service.drain.unmarked) == 1            # ... and its mark retried
+            # a restart: the new worker knows the pending mark from its state_dir
+            await lc.stop_worker("node-0")
+            await lc.start_worker("node-0")
+            w = lc.nodes["node-0"].worker
+            assert len(w.service.drain.unmarked) == 1
+            rep = await w.reconciler.run_once()
+            assert not rep.repaired and not await lc.audit("default", "busy")
+            lc.cluster._faults.clear()                           # noqa: SLF001 - PATCH works again
+            for _ in range(200):                                 # the retry lands (≤ 0.5 s)
+                if not w.service.drain.unmarked:
+                    break
+                await asyncio.sleep(0.02)
+            (ph,) = lc.cluster.placeholders()
+            assert ph["metadata"]["annotations"]["gpumounter.amd.com/mount-mode"] == "draining"
+            p.kill()
+            p.wait()
+            rep = await w.reconciler.run_once()
+            assert len(rep.drained) == 1 and lc.cluster.placeholders() == []
+    asyncio.run(main())

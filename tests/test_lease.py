@@ -152,3 +152,61 @@ def test_stop_cancels_timers_and_lets_a_running_expiry_finish():
         await asyncio.sleep(0.02)
     asyncio.run(main())
     assert calls == [("start", "now"), ("done", "now")]
+
+
+def test_a_retried_leased_attach_cut_off_before_its_lease_still_expires():
+    """The worker is killed after mounting a leased attach but before the lease annotation is
+    written; the master retries AddGPU under the same idempotency key on the next worker, which
+    replays the attach. The replay must record the lease, or the GPUs it hands back as leased
+    never expire (chaos --lease-rate: a lease lost across a worker SIGKILL)."""
+    from gpumounter_amd.api import gpu_mount as api
+
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        # the cut-off first attempt: mounted under key K, no lease recorded
+        resp = await svc.add_gpu(api.AddGPURequest(pod_name="t", namespace="default", gpu_num=1,
+                                                   idempotency_key="K", lease_s=0))
+        assert resp.add_gpu_result == api.ADD_SUCCESS
+        url = f"{lc.master_url}/addgpu/namespace/default/pod/t/gpu/1/isEntireMount/false?lease=0.3"
+        async with lc.session.get(url, headers={"Accept": "application/json",
+                                                "Idempotency-Key": "K"}) as r:
+            code, b = r.status, await r.json()
+        assert code == 200 and "(replayed)" in b["detail"], b
+        assert [d["uuid"] for d in b["devices"]] == [resp.devices[0].uuid]
+
+        async def gone():
+            st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+            return not st.hot
+        assert await until(gone, timeout=3.0), "the replayed lease never expired"
+        assert await lc.audit("default", "t") == []
+    run(body)                  # LocalCluster runs no periodic sweep
+
+
+def test_a_lease_whose_watch_echo_lags_still_expires():
+    """The placeholder informer has not seen the lease annotation (the watch echo of the PATCH
+    is late: a dropped stream, a relist) when the lease timer fires. The expiry must not be
+    lost: the timer found nothing due, and nothing re-armed it until the periodic sweep."""
+    import copy
+
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        code, b = await lease_add(lc, "default", "t", 1, 0.3)
+        assert code == 200, b
+        inf = svc.ph.informer
+        (key,) = [k for k, p in inf.cache.items()
+                  if (p["metadata"].get("annotations") or {}).get(ANN_LEASE)]
+        real = inf.cache[key]
+        stale = copy.deepcopy(real)
+        del stale["metadata"]["annotations"][ANN_LEASE]
+        inf.cache[key] = stale                       # the cache as of before our PATCH
+        await asyncio.sleep(0.6)                     # the lease timer fires meanwhile
+        if inf.cache.get(key) is stale:
+            inf.cache[key] = real                    # the late watch event
+
+        async def gone():
+            st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+            return not st.hot
+        assert await until(gone, timeout=3.0), "the lease was lost"
+    run(body)                  # LocalCluster runs no periodic sweep
