@@ -404,18 +404,25 @@ def chaos(args) -> dict:
                         expired[0] += len(ended)
                     mine[t].extend([(uu, True)] if entire else [([u], False) for u in uu])
                     if lease:   # the worker's lease clock started between sending and answer
-                        leases[t].update({u: (sent + lease, time.monotonic() + lease)
-                                          for u in uu})
+                        # (by placeholder: a GPU re-attached by a later attach whose answer was
+                        # lost is held by another placeholder, not by the lease)
+                        leases[t].update({d["uuid"]: (sent + lease, time.monotonic() + lease,
+                                                      d.get("placeholder"))
+                                          for d in b["devices"]})
                         leased[0] += 1
                 return t, code
             except Exception:  # noqa: BLE001 - the master's connection dropped mid-kill
                 return t, -1
 
+        holders = {}    # tenant → {uuid: placeholder holding it} as of the last ledger()
+
         def ledger(t):
             code, g = pc.pod_gpus("default", t)
             if code != 200:
                 return None
-            return sorted(x["uuid"] for x in g.get("gpus", []) if x.get("source") == "hot-mount")
+            hm = [x for x in g.get("gpus", []) if x.get("source") == "hot-mount"]
+            holders[t] = {x["uuid"]: x.get("pod_name") for x in hm}
+            return sorted(x["uuid"] for x in hm)
 
         why = [""]
 
@@ -517,19 +524,20 @@ def chaos(args) -> dict:
                     now = time.monotonic()
                     # a lease past its expiry is gone, one within it is still there; one that
                     # expires around now may be either (it is settled at the next check)
-                    overdue = [u for u, (_, hi) in leases[t].items()
+                    overdue = [u for u, (_, hi, _) in leases[t].items()
                                if now - hi > args.lease_slack]
-                    late = sorted(set(overdue) & set(hot))
+                    late = sorted(u for u in overdue if u in hot and
+                                  holders.get(t, {}).get(u) == leases[t][u][2])
                     if late:
                         problems.append(f"round {rnd_i} {t}: leases expired more than "
                                         f"{args.lease_slack} s ago still attached: {late}")
-                    gone = set(overdue) - set(hot)
+                    gone = set(overdue) - set(late)
                     for u in gone:
                         leases[t].pop(u)
                         expired[0] += 1
                     if gone:
                         mine[t] = [g for g in mine[t] if not set(g[0]) & gone]
-                    fuzzy = {u for u, (lo, _) in leases[t].items() if lo <= now}
+                    fuzzy = {u for u, (lo, _, _) in leases[t].items() if lo <= now}
                     hot = [u for u in hot if u not in fuzzy]
                     want = sorted(u for grp, _ in mine[t] for u in grp if u not in fuzzy)
                     if certain[t] and hot != want:
@@ -553,8 +561,10 @@ def chaos(args) -> dict:
                               if x.get("source") == "hot-mount"}
                         if len(ph) < len(mine[t]):      # fewer placeholders than GPUs: entire
                             mine[t] = [([u for grp, _ in mine[t] for u in grp], True)]
-                        held_now = {u for grp, _ in mine[t] for u in grp}
-                        leases[t] = {u: e for u, e in leases[t].items() if u in held_now}
+                        held_now = {x["uuid"]: x.get("pod_name") for x in g.get("gpus", [])
+                                    if x.get("source") == "hot-mount"}
+                        leases[t] = {u: e for u, e in leases[t].items()
+                                     if held_now.get(u) == e[2]}
                         certain[t] = True
                 if args.api_fault_rate:
                     pc.api_faults(args.api_fault_rate, args.seed * 1000 + rnd_i)

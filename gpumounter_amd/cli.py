@@ -33,8 +33,9 @@ def _cfg(args, **over):
 
 def _run_daemon(serve, cfg) -> int:
     """asyncio.run(serve(cfg)); with GM_PROFILE_OUT=<file> under cProfile, stats written at
-    (SIGTERM-clean) shutdown — for finding the hot spots of a live daemon."""
-    out = os.environ.get("GM_PROFILE_OUT", "")
+    (SIGTERM-clean) shutdown — for finding the hot spots of a live daemon (``{pid}`` in the
+    name is replaced, so several daemons can share the setting)."""
+    out = os.environ.get("GM_PROFILE_OUT", "").replace("{pid}", str(os.getpid()))
     if not out:
         asyncio.run(serve(cfg))
         return 0

@@ -66,7 +66,7 @@ def e8m0(code) -> np.ndarray:
 
 # ------------------------------------------------------------------------------ lane maps
 # v_mfma_scale_f32_16x16x128_f8f6f4 with 8-bit operands, measured on MI355X with exact one-hot
-# data (bench/mx_layout.py: rows and the A↔B pairing; bench/mx_debug2.py: which lane's scale
+# data (round-3 probes, profiles/r3_mx/: rows and the A↔B pairing, which lane's scale
 # multiplies each byte, which fixes the true k). Lane l holds row (A) / column (B) l & 15; its
 # bytes 0-15 are k = 16 (l >> 4) + j and bytes 16-31 are k = 64 + 16 (l >> 4) + (j - 16), so one
 # lane spans two 32-wide scale blocks. The E8M0 scale of row/column r, block s (k in
@@ -171,7 +171,7 @@ def check_fp8(dev: int, seed: int = 0) -> Dict:
 
 def burn_in(dev: int, seconds: float = 10.0, fmt: str = "fp8") -> Dict:
     """Sustained MX-pipe load for ``seconds``: every launch's per-wave sums are compared bit for
-    bit with the first launch's (the kernel is deterministic — bench/mx_det.py measured 0
+    bit with the first launch's (the kernel is deterministic — a round-3 probe measured 0
     differing waves over thousands), so any ``mismatches`` is silent data corruption on the fp8 /
     fp4 matrix path; ``tflops`` the sustained rate (throttling shows up as a low number)."""
     import time

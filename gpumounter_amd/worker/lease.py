@@ -18,7 +18,8 @@ from typing import Dict, List, Optional, Tuple
 
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import LABEL_OWNER_NS
+from gpumounter_amd.models.types import LABEL_OWNER_NS, MountType
+from gpumounter_amd.node.ledger import LedgerError
 from gpumounter_amd.utils import log
 
 _log = log.get("worker.lease")
@@ -174,10 +175,21 @@ class LeaseKeeper:
             return                          # the owner-gone GC releases its placeholders
         now = time.time()
         st = await svc.pod_state(pod, fresh=True)
+        raws = {p["metadata"]["name"]: p for p in svc.ph.owned_by(pod)}
+        if st.mount_type == MountType.UNKNOWN:
+            # the ledger is unreadable right now (kubelet restarting, a claim not in the watch
+            # cache yet): fail, so the expiry is retried shortly — returning would drop it
+            raise LedgerError(f"lease expiry of {ns}/{name}: ledger unavailable")
+        known = {ph.name for ph in st.placeholders}
+        for pname, raw in raws.items():
+            exp = expires_of(raw)
+            if pname not in known and exp is not None and exp <= now + 0.001:
+                # a leased placeholder of this owner the ledger view does not resolve yet
+                raise LedgerError(f"lease expiry of {ns}/{name}: placeholder {pname} is not "
+                                  f"in the ledger yet")
         uuids, due = [], []
         for ph in st.placeholders:
-            raw = next((p for p in svc.ph.owned_by(pod)
-                        if p["metadata"]["name"] == ph.name), None)
+            raw = raws.get(ph.name)
             exp = expires_of(raw) if raw is not None else None
             if exp is None:
                 exp = self._granted.get(ph.uid)

@@ -1,6 +1,6 @@
 """Host side of the block-scaled (MX) MFMA check (gpumounter_amd/ops/mx.py): the OCP e4m3
 decoder, the measured lane map and the reference. The tile runs here on a CPU emulation of the
-map measured on MI355X (bench/mx_layout.py, bench/mx_debug2.py); tests/test_gpu.py runs it on
+map measured on MI355X (round-3 probe scripts, removed; results in profiles/r3_mx/); tests/test_gpu.py runs it on
 the matrix core."""
 import numpy as np
 import pytest
