@@ -153,10 +153,11 @@ def main() -> int:
     ap.add_argument("--device-plugin", action="store_true",
                     help="the worker serves amd.com/gpu itself; the fake kubelet's device manager "
                          "calls GetPreferredAllocation/Allocate on it at admission")
-    ap.add_argument("--ref-steps", type=int, default=20,
+    ap.add_argument("--ref-steps", type=int, default=0,
                     help="after the timed loop, re-run this many attach/detach cycles with the "
-                         "emulated reference protocol on the same cluster (0 = skip; only with "
-                         "--latency zero and no warm pool)")
+                         "emulated reference protocol on the same cluster (only with --latency "
+                         "zero and no warm pool). Off by default: it compares call sequences on "
+                         "a zero-latency fake, not a published reference figure")
     ap.add_argument("--deploy", choices=("inprocess", "processes"), default="processes",
                     help="processes: fake control plane, worker and master each in their own "
                          "process via the production entry points (gpumounter_amd/fakes/"
@@ -184,6 +185,13 @@ def main() -> int:
                          "JSON lines to this file, for tail-latency analysis")
     ap.add_argument("--log-dir", default="",
                     help="--deploy processes: keep the daemons' logs in this directory")
+    ap.add_argument("--cold-steps", type=int, default=10,
+                    help="after the timed loop (--deploy processes): restart the master with "
+                         "authz TTLs of --idle-s/2 and time this many attaches, each after "
+                         "--idle-s of idleness, so each one finds its TokenReview and "
+                         "SubjectAccessReview answers expired (cold_attach_p50_ms); 0 = skip")
+    ap.add_argument("--idle-s", type=float, default=0.3,
+                    help="idle time before each cold attach (see --cold-steps)")
     ap.add_argument("--no-calib", action="store_true",
                     help="skip the box calibration (CPU loop, process pingpong, gRPC floor) "
                          "recorded as \"box\" in the JSON")
@@ -335,6 +343,7 @@ def main() -> int:
     last_bdfs = []
     ar_backend = [None]
     samples = [] if args.dump_samples and rank == 0 else None
+    first_attach = []    # the first attach after the daemons started (cold everything)
 
     def one_step(record: bool):
         nonlocal audit_issues, nccl_group
@@ -345,6 +354,8 @@ def main() -> int:
             t1 = time.perf_counter()
             if code != 200:
                 raise RuntimeError(f"attach failed: {code} {body}")
+            if not first_attach:
+                first_attach.append((t1 - t0) * 1e3)
             issues = cp.audit() if args.protocol == "gpumounter" else []
             obj = [{"bdfs": [d["bdf"] for d in body["devices"]],
                     "uuids": [d["uuid"] for d in body["devices"]],
@@ -507,6 +518,35 @@ def main() -> int:
                 if not tenant_view_pt["ok"]:
                     print(f"bench: tenant-side PyTorch check failed: {tenant_view_pt}",
                           file=sys.stderr)
+            cold = None
+            if args.cold_steps > 0 and args.deploy == "processes" and \
+                    args.protocol == "gpumounter":
+                # the attach an operator makes minutes after the last one: every cached authz
+                # answer expired (the pod index is a watch, so it stays current)
+                import signal as _signal
+                ttl = f"{args.idle_s / 2:g}"
+                cp.pc.restart_master(_signal.SIGTERM, env={"GM_AUTHZ_TOKEN_TTL_S": ttl,
+                                                            "GM_AUTHZ_SAR_TTL_S": ttl})
+                cms, cst = [], {}
+                for i in range(args.cold_steps):
+                    time.sleep(args.idle_s)
+                    ta = time.perf_counter()
+                    code, body = cp.add(n, args.mode == "entire")
+                    tb = time.perf_counter()
+                    if code != 200:
+                        raise RuntimeError(f"cold attach failed: {code} {body}")
+                    cms.append((tb - ta) * 1e3)
+                    for t in body.get("master_timings", []) + [
+                            {"name": "worker", "ms": body.get("total_ms", 0.0)}]:
+                        cst.setdefault(t["name"], []).append(t["ms"])
+                    code, body = cp.remove([d["uuid"] for d in body["devices"]])
+                    if code != 200:
+                        raise RuntimeError(f"cold detach failed: {code} {body}")
+                    progress("cold", i + 1, args.cold_steps)
+                cold = {"steps": args.cold_steps, "idle_s": args.idle_s,
+                        "authz_ttl_s": args.idle_s / 2, "attach_p50_ms": round(pct(cms, 0.5), 4),
+                        "attach_max_ms": round(max(cms), 4),
+                        "stage_p50_ms": {k: round(pct(v, 0.5), 4) for k, v in sorted(cst.items())}}
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
             corrections = cp.corrections() if args.protocol == "gpumounter" else None
             placeholders_left = cp.placeholders_left()
@@ -557,7 +597,6 @@ def main() -> int:
                     progress("reference", i + 1, args.ref_steps + 2)
                 ref = {"steps": args.ref_steps, "attach_p50_ms": round(pct(ra, 0.5), 4),
                        "detach_p50_ms": round(pct(rd, 0.5), 4),
-                       "attach_speedup": round(pct(ra, 0.5) / p50, 2),
                        "kubelet_limit": "count (served, not enforced)"}
                 k1 = ref_cp.kubelet_calls()
                 served = sum(k1[c] - k0[c] for c in ("List", "Get", "GetAllocatableResources"))
@@ -614,6 +653,12 @@ def main() -> int:
                     "client_minus_master": round(pct([a - m for a, (m, _) in
                                                       zip(attach_ms, hop_ms)], 0.5), 4)}
                 if hop_ms and len(hop_ms) == len(attach_ms) else None,
+                # the attach an operator makes after idling past the master's authz TTLs
+                # (TokenReview + SubjectAccessReview asked again), and the very first attach
+                # after the daemons started
+                "cold_attach_p50_ms": cold["attach_p50_ms"] if cold else None,
+                "cold_attach": cold,
+                "first_attach_ms": round(first_attach[0], 4) if first_attach else None,
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),
                 "detach_p99_ms": round(pct(detach_ms, 0.99), 4),
                 "stage_p50_ms": {k: round(statistics.median(v), 4) for k, v in sorted(stage.items())},

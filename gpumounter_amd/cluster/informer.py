@@ -331,3 +331,29 @@ class ClaimInformer(PodInformer):
     def _watch(self, timeout_s: int):
         return self.kube.watch_claims(self.namespace, self.label_selector, self.field_selector,
                                       self.rv, timeout_s=timeout_s)
+
+
+def slim_pod(p: dict) -> dict:
+    """What the master needs of a Pod to route a request: identity, node, phase."""
+    md = p.get("metadata", {})
+    out = {"metadata": {k: md[k] for k in ("name", "namespace", "uid", "resourceVersion",
+                                           "deletionTimestamp") if k in md},
+           "spec": {"nodeName": (p.get("spec") or {}).get("nodeName", "")},
+           "status": {"phase": (p.get("status") or {}).get("phase", "")}}
+    return out
+
+
+class SlimPodInformer(PodInformer):
+    """List+watch of every Pod, cached as :func:`slim_pod` projections (~300 bytes each instead
+    of the whole object: 100k Pods ≈ 30 MB). The master's pod → node index."""
+
+    async def _list(self):
+        items, rv = await super()._list()
+        return [slim_pod(p) for p in items], rv
+
+    async def _get(self, ns: str, name: str):
+        return slim_pod(await super()._get(ns, name))
+
+    async def _watch(self, timeout_s: int):
+        async for etype, obj in super()._watch(timeout_s):
+            yield etype, (slim_pod(obj) if etype not in ("ERROR", "BOOKMARK") else obj)

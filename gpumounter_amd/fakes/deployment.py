@@ -214,9 +214,13 @@ class ProcessCluster:
             self._wait(f"master → {node}", lambda n=node: _http(
                 "GET", f"{self.master_url}/api/v1/nodes/{n}/gpus", headers=self._auth)[0] == 200)
 
-    def restart_master(self, sig: int = signal.SIGKILL) -> None:
+    def restart_master(self, sig: int = signal.SIGKILL,
+                       env: Optional[Dict[str, str]] = None) -> None:
         """Kill the master (SIGKILL: requests in flight lose their client connection; the
-        workers carry on) and start a new one; it serves on a new port (``master_url``)."""
+        workers carry on) and start a new one, with ``env`` added to its environment; it
+        serves on a new port (``master_url``)."""
+        if env:
+            self._master_env = {**self._master_env, **env}
         p = self.procs["master"]
         p.send_signal(sig)
         p.wait(20)

@@ -25,7 +25,7 @@ from aiohttp import web
 
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.api import protodef
-from gpumounter_amd.cluster.informer import PodInformer
+from gpumounter_amd.cluster.informer import PodInformer, SlimPodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.master.authz import Authorizer
@@ -153,6 +153,7 @@ class WorkerDirectory:
 class Master:
     POD_CACHE_TTL_S = 30.0
     POD_CACHE_MAX = 4096
+    POD_INDEX_WAIT_S = 10.0
 
     def __init__(self, cfg, kube: Optional[KubeClient] = None) -> None:
         self.cfg = cfg
@@ -164,6 +165,12 @@ class Master:
         self.runner: Optional[web.AppRunner] = None
         self.port = 0
         self._pod_nodes: Dict[Tuple[str, str], Tuple[str, str, float]] = {}
+        # pod → node without a GET per request (the reference GETs the pod every time,
+        # main.go:52); until its first LIST is in, requests fall back to a GET
+        self.pods: Optional[SlimPodInformer] = SlimPodInformer(
+            self.kube, resync_s=cfg.watch_resync_s) if getattr(cfg, "master_pod_index", True) \
+            else None
+        self._pods_task: Optional[asyncio.Task] = None
 
     # ------------------------------------------------------------------------ app
     def app(self) -> web.Application:
@@ -182,6 +189,11 @@ class Master:
 
     async def start(self, port: Optional[int] = None) -> None:
         await self.workers.start()
+        if self.pods is not None:
+            # serve once the index has synced (as a controller waits for its caches), but not
+            # longer than a few seconds: until then a lookup GETs the pod
+            self._pods_task = asyncio.ensure_future(self._start_pod_index())
+            await asyncio.wait([self._pods_task], timeout=self.POD_INDEX_WAIT_S)
         self.runner = web.AppRunner(self.app(), access_log=None)
         await self.runner.setup()
         site = web.TCPSite(self.runner, self.cfg.master_host,
@@ -194,9 +206,23 @@ class Master:
         runtime.write_ready_file(self.cfg.ready_file, {"port": self.port})
         _log.info("master serving HTTP :%d", self.port)
 
+    async def _start_pod_index(self) -> None:
+        try:
+            await self.pods.start()
+            _log.info("pod index synced: %d pods", len(self.pods.cache))
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:  # noqa: BLE001 - requests GET the pod meanwhile
+            _log.warning("pod index not synced (%s); pod lookups GET the pod", e)
+
     async def stop(self) -> None:
         if self.runner is not None:
             await self.runner.cleanup()
+        if self._pods_task is not None:
+            self._pods_task.cancel()
+        if self.pods is not None:
+            await self.pods.stop()
+        await self.authz.stop()
         await self.workers.stop()
         await self.kube.close()
 
@@ -244,26 +270,46 @@ class Master:
             return web.json_response(payload, status=status)
         return _text(text, status)
 
+    def _stale(self, cached: str, pod: dict) -> bool:
+        """The worker found no such pod although the lookup did: worth one fresh try if the
+        answer came from the 30 s cache, or from the index that has since seen the pod
+        recreated (another UID). A pod deleted meanwhile is reported as the worker saw it."""
+        if cached == "ttl":
+            self._pod_nodes.pop((podu.ns_of(pod), podu.name_of(pod)), None)
+            return True
+        if cached == "index":
+            cur = self.pods.get(podu.ns_of(pod), podu.name_of(pod))
+            return cur is not None and podu.uid_of(cur) != podu.uid_of(pod)
+        return False
+
     async def _locate(self, ns: str, name: str, fresh: bool = False):
         """Pod → node → worker target. Returns (pod, target, error, cached) where error is a
-        (status, text, payload) triple. Recently seen pods come from a small cache (a pod never
-        changes node); a stale entry is detected by the worker and retried fresh."""
+        (status, text, payload) triple and cached where the pod came from ("index", "ttl" or
+        "" for a GET). The pod comes from the master's pod index (a watch of
+        every Pod) or, with the index off or not yet synced, from a small 30 s cache; a pod not
+        found there is read with a GET. A stale answer (the pod was recreated on another node)
+        is detected by the worker and retried fresh."""
         key = (ns, name)
-        hit = None if fresh else self._pod_nodes.get(key)
         now = time.monotonic()
-        if hit is not None and now - hit[2] < self.POD_CACHE_TTL_S:
+        indexed = self.pods is not None and self.pods._synced is not None and \
+            self.pods._synced.is_set()  # noqa: SLF001
+        hit = None if fresh or indexed else self._pod_nodes.get(key)
+        idx = self.pods.get(ns, name) if indexed and not fresh else None
+        if idx is not None and podu.node_of(idx) and not podu.is_terminating(idx):
+            pod, cached = idx, "index"
+        elif hit is not None and now - hit[2] < self.POD_CACHE_TTL_S:
             pod = {"metadata": {"name": name, "namespace": ns, "uid": hit[1]},
                    "spec": {"nodeName": hit[0]}}
-            cached = True
+            cached = "ttl"
         else:
             try:
                 pod = await self.kube.get_pod(ns, name)
             except NotFound:
                 self._pod_nodes.pop(key, None)
-                return None, None, (404, f"No pod: {name} in namespace: {ns}", {}), False
+                return None, None, (404, f"No pod: {name} in namespace: {ns}", {}), ""
             except ApiError as e:
                 return None, None, (500, str(e), {}), False
-            cached = False
+            cached = ""
             if podu.node_of(pod):
                 self._pod_nodes[key] = (podu.node_of(pod), podu.uid_of(pod), now)
                 if len(self._pod_nodes) > self.POD_CACHE_MAX:
@@ -309,9 +355,8 @@ class Master:
                 code = 400 if e.code() == grpc.StatusCode.INVALID_ARGUMENT else 500
                 body = "Service Internal Error" if code == 500 else e.details()
                 return code, body, {"error": e.details()}
-            if cached and resp.add_gpu_result == api.ADD_POD_NOT_FOUND:
-                self._pod_nodes.pop((ns, name), None)       # re-check with a fresh GET (→ 404)
-                continue
+            if resp.add_gpu_result == api.ADD_POD_NOT_FOUND and self._stale(cached, pod):
+                continue                                    # re-check with a fresh GET
             break
         payload = self._payload(resp, t0)
         node = podu.node_of(pod)
@@ -345,8 +390,7 @@ class Master:
                 _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name,
                            e.details())
                 return 500, "Service Internal Error", {"error": e.details()}
-            if cached and resp.remove_gpu_result == api.REMOVE_POD_NOT_FOUND:
-                self._pod_nodes.pop((ns, name), None)
+            if resp.remove_gpu_result == api.REMOVE_POD_NOT_FOUND and self._stale(cached, pod):
                 continue
             break
         payload = self._payload(resp, t0)

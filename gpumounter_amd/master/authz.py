@@ -11,11 +11,19 @@ master can attach GPUs to, or force-kill processes in, any pod. Modes (``GM_AUTH
   ``get`` on ``nodes/gpumount``. Admins grant hot-mount rights with plain RBAC, for example
   ``deploy/rbac-tenant-example.yaml``.
 
-Decisions are cached briefly (TokenReview 60 s, SubjectAccessReview 30 s) so a burst of requests
-costs one review round trip, not one per request.
+Decisions are cached briefly (``authz_token_ttl_s`` 60 s, ``authz_sar_ttl_s`` 30 s) so a burst of
+requests costs no review round trip. The path stays warm and cheap beyond that:
+
+* a cached answer used after half its lifetime is refreshed in the background (single flight),
+  so a caller who keeps working never meets an expired entry;
+* once an entry has expired, a token seen before has its TokenReview and its
+  SubjectAccessReview — asked for the identity the token had last time — sent together: one
+  round trip instead of two. The SAR answer counts only if the TokenReview confirms that same
+  identity; otherwise the SAR is asked again for the new one.
 """
 from __future__ import annotations
 
+import asyncio
 import hashlib
 import hmac
 import time
@@ -37,15 +45,23 @@ class Decision:
 
 
 class Authorizer:
-    def __init__(self, cfg, kube, token_ttl_s: float = 60.0, sar_ttl_s: float = 30.0) -> None:
+    def __init__(self, cfg, kube, token_ttl_s: Optional[float] = None,
+                 sar_ttl_s: Optional[float] = None) -> None:
         self.cfg = cfg
         self.kube = kube
         self.mode = cfg.authz_mode
-        self.token_ttl_s = token_ttl_s
-        self.sar_ttl_s = sar_ttl_s
+        self.token_ttl_s = token_ttl_s if token_ttl_s is not None else \
+            getattr(cfg, "authz_token_ttl_s", 60.0)
+        self.sar_ttl_s = sar_ttl_s if sar_ttl_s is not None else \
+            getattr(cfg, "authz_sar_ttl_s", 30.0)
         self._tokens: Dict[str, Tuple[float, Optional[dict]]] = {}
         self._sar: Dict[tuple, Tuple[float, bool]] = {}
-        self.reviews = {"token": 0, "sar": 0}
+        # token hash → the identity its last TokenReview returned (outlives the TTL: it is only
+        # a guess that lets the SAR start early, never a decision)
+        self._last_user: Dict[str, dict] = {}
+        self._refreshing: set = set()
+        self._bg: set = set()
+        self.reviews = {"token": 0, "sar": 0, "speculative": 0, "refresh": 0}
 
     @staticmethod
     def _bearer(headers) -> str:
@@ -64,15 +80,32 @@ class Authorizer:
         token = self._bearer(headers)
         if not token:
             return Decision(False, 401, "Unauthorized: bearer token required")
+        key = hashlib.sha256(token.encode()).hexdigest()
+        guess = None if self._fresh(self._tokens.get(key), self.token_ttl_s) else \
+            self._last_user.get(key)
+        spec = None
+        if guess is not None:
+            # expired token entry: the SAR for the identity it had goes out with the TokenReview
+            self.reviews["speculative"] += 1
+            spec = asyncio.ensure_future(self._authorize(guess, verb, namespace, resource, name))
         try:
-            user = await self._authenticate(token)
+            user = await self._authenticate(token, key)
         except Exception as e:  # noqa: BLE001
+            if spec is not None:
+                spec.cancel()
             _log.error("TokenReview failed: %s", e)
             return Decision(False, 503, "authentication unavailable")
         if user is None:
+            if spec is not None:
+                spec.cancel()
             return Decision(False, 401, "Unauthorized: token not accepted")
         try:
-            ok = await self._authorize(user, verb, namespace, resource, name)
+            if spec is not None and self._same(user, guess):
+                ok = await spec
+            else:
+                if spec is not None:
+                    spec.cancel()
+                ok = await self._authorize(user, verb, namespace, resource, name)
         except Exception as e:  # noqa: BLE001
             _log.error("SubjectAccessReview failed: %s", e)
             return Decision(False, 503, "authorization unavailable", user["username"])
@@ -82,11 +115,41 @@ class Authorizer:
                                         f"{resource}/{RESOURCE_SUB}{where}", user["username"])
         return Decision(True, 200, "", user["username"])
 
-    async def _authenticate(self, token: str) -> Optional[dict]:
-        key = hashlib.sha256(token.encode()).hexdigest()
-        now = time.monotonic()
+    @staticmethod
+    def _fresh(hit, ttl: float) -> bool:
+        return bool(hit) and time.monotonic() - hit[0] < ttl
+
+    @staticmethod
+    def _same(a: dict, b: dict) -> bool:
+        return (a["username"], a["uid"], sorted(a["groups"]), a["extra"]) == \
+            (b["username"], b["uid"], sorted(b["groups"]), b["extra"])
+
+    def _refresh_ahead(self, what: tuple, hit, ttl: float, coro_fn) -> None:
+        """A cached answer past half its lifetime: renew it in the background (single flight)
+        so the next request still finds a fresh one."""
+        if hit is None or time.monotonic() - hit[0] < ttl / 2 or what in self._refreshing:
+            return
+        self._refreshing.add(what)
+        self.reviews["refresh"] += 1
+
+        async def run():
+            try:
+                await coro_fn()
+            except Exception as e:  # noqa: BLE001 - the entry simply expires
+                _log.debug("background review refresh failed: %s", e)
+            finally:
+                self._refreshing.discard(what)
+        t = asyncio.ensure_future(run())
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)
+
+    async def _authenticate(self, token: str, key: str = "", force: bool = False
+                            ) -> Optional[dict]:
+        key = key or hashlib.sha256(token.encode()).hexdigest()
         hit = self._tokens.get(key)
-        if hit and now - hit[0] < self.token_ttl_s:
+        if not force and self._fresh(hit, self.token_ttl_s):
+            self._refresh_ahead(("token", key), hit, self.token_ttl_s,
+                                lambda: self._authenticate(token, key, force=True))
             return hit[1]
         self.reviews["token"] += 1
         st = await self.kube.token_review(token)
@@ -97,15 +160,22 @@ class Authorizer:
                     "groups": list(u.get("groups") or []), "extra": u.get("extra") or {}}
         if len(self._tokens) > 4096:
             self._tokens.clear()
-        self._tokens[key] = (now, user)
+            self._last_user.clear()
+        self._tokens[key] = (time.monotonic(), user)
+        if user is not None:
+            self._last_user[key] = user
+        else:
+            self._last_user.pop(key, None)
         return user
 
     async def _authorize(self, user: dict, verb: str, namespace: str, resource: str,
-                         name: str) -> bool:
+                         name: str, force: bool = False) -> bool:
         key = (user["username"], tuple(user["groups"]), verb, namespace, resource, name)
-        now = time.monotonic()
         hit = self._sar.get(key)
-        if hit and now - hit[0] < self.sar_ttl_s:
+        if not force and self._fresh(hit, self.sar_ttl_s):
+            self._refresh_ahead(("sar",) + key, hit, self.sar_ttl_s,
+                                lambda: self._authorize(user, verb, namespace, resource, name,
+                                                        force=True))
             return hit[1]
         self.reviews["sar"] += 1
         attrs = {"verb": verb, "resource": resource, "subresource": RESOURCE_SUB,
@@ -118,5 +188,9 @@ class Authorizer:
         ok = bool(st.get("allowed")) and not st.get("denied")
         if len(self._sar) > 16384:
             self._sar.clear()
-        self._sar[key] = (now, ok)
+        self._sar[key] = (time.monotonic(), ok)
         return ok
+
+    async def stop(self) -> None:
+        for t in list(self._bg):
+            t.cancel()

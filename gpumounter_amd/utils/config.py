@@ -179,6 +179,15 @@ class Config:
     # kube: the caller's own token, TokenReview + SubjectAccessReview on pods/gpumount (default);
     # none: open like the reference (SURVEY defect 13) unless api_token is set — opt-in only
     authz_mode: str = "kube"
+    # how long a TokenReview / SubjectAccessReview answer is reused. A decision used after half
+    # its lifetime is refreshed in the background; once expired, the next request re-runs the
+    # TokenReview and, for a token seen before, the SubjectAccessReview at the same time (one
+    # apiserver round trip instead of two)
+    authz_token_ttl_s: float = 60.0
+    authz_sar_ttl_s: float = 30.0      # the same for SubjectAccessReview answers
+    # the master keeps a slim list+watch index of every Pod (name → uid, node, phase) so an
+    # attach needs no Pod GET; off: a GET on a miss, answers cached for 30 s
+    master_pod_index: bool = True
     # master⇄worker gRPC TLS (reference: insecure, main.go:82). cert+key on the worker enable TLS;
     # a CA on the worker requires client certs (mTLS). The master uses the same three files.
     tls_cert: str = ""

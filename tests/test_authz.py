@@ -54,7 +54,7 @@ def test_reviews_are_cached():
             assert code == 200
             assert (await lc.remove("team-a", "a1", [b["devices"][0]["uuid"]],
                                     token="tok-alice"))[0] == 200
-        assert authz.reviews == {"token": 1, "sar": 2}      # one per (user, verb, ns, pod)
+        assert (authz.reviews["token"], authz.reviews["sar"]) == (1, 2)  # per (user, verb, ns, pod)
     run(body)
 
 
@@ -95,3 +95,65 @@ def test_anonymous_callers_are_recorded_by_address():
             (ev,) = lc.cluster.events_for("default", "t")
             assert "(requested by anonymous@127.0.0.1)" in ev["message"]
     asyncio.run(main())
+
+
+def test_an_expired_token_is_reviewed_together_with_its_sar():
+    """Past the TTLs, a known token's TokenReview and SubjectAccessReview go out together (one
+    apiserver round trip, not two); the SAR answer counts only for the identity the TokenReview
+    confirms — a token that now maps to another user is authorized afresh."""
+    async def body(lc):
+        lc.tenant("a1", ns="team-a")
+        authz = lc.master.authz
+        authz.token_ttl_s = authz.sar_ttl_s = 0.05
+        kube = authz.kube
+        spans = []
+        real_tr, real_sar = kube.token_review, kube.subject_access_review
+
+        async def tr(token):
+            t0 = asyncio.get_running_loop().time()
+            out = await real_tr(token)
+            spans.append(("tr", t0, asyncio.get_running_loop().time()))
+            return out
+
+        async def sar(user, attrs):
+            t0 = asyncio.get_running_loop().time()
+            out = await real_sar(user, attrs)
+            spans.append(("sar", t0, asyncio.get_running_loop().time()))
+            return out
+        kube.token_review, kube.subject_access_review = tr, sar
+        code, b = await lc.add("team-a", "a1", 1, token="tok-alice")
+        assert code == 200
+        first = list(spans)
+        assert [k for k, *_ in first] == ["tr", "sar"] and first[1][1] >= first[0][2]  # serial
+        spans.clear()
+        await asyncio.sleep(0.1)                          # both answers expired
+        code, _ = await lc.remove("team-a", "a1", [b["devices"][0]["uuid"]], token="tok-alice")
+        assert code == 200 and authz.reviews["speculative"] == 1
+        (t_tr,) = [x for x in spans if x[0] == "tr"]
+        (t_sar,) = [x for x in spans if x[0] == "sar"]
+        assert t_sar[1] < t_tr[2]                         # the SAR left before the TR answered
+        # the token now belongs to bob, who may not attach in team-a: the guessed SAR (alice)
+        # must not decide
+        lc.cluster.add_user("tok-alice", "bob")
+        await asyncio.sleep(0.1)
+        code, b2 = await lc.add("team-a", "a1", 1, token="tok-alice")
+        assert code == 403 and "bob cannot create" in b2["message"], b2
+    run(body)
+
+
+def test_a_decision_used_late_in_its_life_is_refreshed_in_the_background():
+    async def body(lc):
+        lc.tenant("a1", ns="team-a")
+        authz = lc.master.authz
+        authz.token_ttl_s = authz.sar_ttl_s = 0.4
+        code, b = await lc.add("team-a", "a1", 1, token="tok-alice")
+        assert code == 200
+        await asyncio.sleep(0.25)                         # past half the lifetime
+        code, _ = await lc.remove("team-a", "a1", [b["devices"][0]["uuid"]], token="tok-alice")
+        assert code == 200
+        await asyncio.sleep(0.05)
+        assert authz.reviews["refresh"] >= 1
+        await asyncio.sleep(0.2)                          # the original answer has expired ...
+        code, _ = await lc.add("team-a", "a1", 1, token="tok-alice")
+        assert code == 200 and authz.reviews["speculative"] == 0   # ... but was renewed
+    run(body)

@@ -123,9 +123,10 @@ def test_bench_real_node_ops_reports_stage_split():
     if realnode.available() or not privileged_ok():
         pytest.skip("needs root with mount + bpf (mounts cgroup2/bpffs)")
     env = {**os.environ, "CUDA_VISIBLE_DEVICES": ""}
-    # default --ref-steps: the reference column is skipped with its reason, never a crash
+    # --ref-steps with real node ops: the reference column is skipped with its reason, never
+    # a crash
     res = subprocess.run([sys.executable, "bench.py", "--steps", "10", "--warmup", "2",
-                          "--amdsmi", "mock", "--node-ops", "real"],
+                          "--amdsmi", "mock", "--node-ops", "real", "--ref-steps", "5"],
                          cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
     assert res.returncode == 0, res.stderr[-3000:]
     d = _last_json(res.stdout)

@@ -503,23 +503,30 @@ def test_api_token_guards_mutating_routes():
     run(body)
 
 
-def test_master_pod_cache_revalidates_recreated_and_deleted_pods():
+@pytest.mark.parametrize("index", [True, False])
+def test_master_pod_cache_revalidates_recreated_and_deleted_pods(index):
     async def body(lc):
         lc.tenant("p", node="node-0")
         assert (await lc.add("default", "p", 1))[0] == 200          # fills the cache
         gets = lc.cluster.requests_by_verb.get("GET", 0)
         _, b = await lc.add("default", "p", 1)
-        assert lc.cluster.requests_by_verb.get("GET", 0) == gets     # cache hit: no GET
+        assert lc.cluster.requests_by_verb.get("GET", 0) == gets     # index hit: no GET
         # pod recreated on another node under the same name → worker refuses, master re-GETs
         lc.cluster.delete("default", "p", grace=0)
         lc.tenant("p", node="node-1")
         code, b = await lc.add("default", "p", 1)
         assert code == 200 and lc.cluster.placeholders()[-1]["spec"]["nodeName"] == "node-1"
-        # pod deleted → reference semantics: 404 from the master
+        # pod deleted → reference semantics: 404 from the master (once its pod index has seen
+        # the deletion; a request racing the watch gets the worker's 400 PodNotFound, as a
+        # reference request racing the deletion after its GET does)
         lc.cluster.delete("default", "p", grace=0)
+        for _ in range(100):
+            if lc.master.pods is None or lc.master.pods.get("default", "p") is None:
+                break
+            await asyncio.sleep(0.01)
         code, text = await lc.add("default", "p", 1, accept_json=False)
         assert (code, text) == (404, "No pod: p in namespace: default\n")
-    run(body, n_nodes=2)
+    run(body, n_nodes=2, master_overrides={"master_pod_index": index})
 
 
 def test_idempotency_key_replays_instead_of_adding_more():
