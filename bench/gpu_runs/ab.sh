@@ -17,7 +17,7 @@ for i in $(seq 1 "$ROUNDS"); do
         timeout -k 10 60 python3 -m gpumounter_amd.utils.calib > "$O/$n.calib.json" || exit 1
         (cd "$t" && timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 \
             --dump-samples "$O/$n.samples.jsonl" > "$O/$n.json" 2> "$O/$n.err") || { tail -30 "$O/$n.err"; exit 1; }
-        echo "$n $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['attach_split_p50_ms'], d['probe_quick_p50_us'])" "$O/$n.json")"
+        echo "$n $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d.get('attach_split_p50_ms'), d['probe_quick_p50_us'], d.get('cold_attach_p50_ms'), (d.get('box') or {}).get('grpc_rtt_us'))" "$O/$n.json")"
     done
 done
 # the builder's own longer command, once per tree
@@ -25,5 +25,5 @@ for t in "$A" "$B"; do
     n=$(basename "$t")_long
     (cd "$t" && timeout -k 10 300 python3 bench.py --gpus 1 --steps 100 --warmup 20 --ref-steps 0 \
         > "$O/$n.json" 2> "$O/$n.err") || { tail -30 "$O/$n.err"; exit 1; }
-    echo "$n $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['attach_split_p50_ms'], d['probe_quick_p50_us'])" "$O/$n.json")"
+    echo "$n $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d.get('attach_split_p50_ms'), d['probe_quick_p50_us'])" "$O/$n.json")"
 done

@@ -154,6 +154,9 @@ class LocalCluster:
         ov.setdefault("worker_insecure", not ov.get("tls_ca"))   # hermetic: loopback only
         ov.setdefault("state_dir", h.node.state_dir)
         ov.setdefault("host_dev_path", h.node.host_dev)
+        # like the periodic sweep, the device guard is opt-in for in-process tests (tests that
+        # tamper with a cgroup and then check what the sweep finds would race it)
+        ov.setdefault("device_guard_period_s", 0.0)
         if self.device_plugin:
             ov.setdefault("device_plugin", True)
             ov.setdefault("device_plugin_dir", h.kubelet.plugin_dir)

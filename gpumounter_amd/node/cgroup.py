@@ -215,6 +215,14 @@ class DeviceRuleBackend(ABC):
         it is gone from here — a foreign veto does not make a grant of ours go away."""
         return self.allowed(cgdir)
 
+    def fingerprint(self, cgdir: str) -> object:
+        """A cheap token of the cgroup's device-control state (one syscall or one small read):
+        it changes whenever anyone — the runtime re-attaching its program, ``runc update``,
+        systemd re-realising a unit, a write to devices.allow/deny — changes what the cgroup
+        enforces. The device guard (worker/reconciler.py) compares it every second instead of
+        re-auditing every hot container."""
+        return None
+
     def prune(self) -> int:
         """Drop cached state of cgroups that no longer exist (containers gone without a detach);
         returns how many. Backends that cache nothing have nothing to drop."""
@@ -237,6 +245,20 @@ class V1Backend(DeviceRuleBackend):
         rc = _native.host().gm_cg1_apply(cgdir.encode(), _rule_array(rules), len(rules))
         if rc < 0:
             raise CgroupError(f"devices.allow/deny write in {cgdir}: {os.strerror(-rc)}")
+
+    def fingerprint(self, cgdir):
+        if os.path.exists(os.path.join(cgdir, FAKE_MARKER)):
+            names = ("devices.allow", "devices.deny")
+        else:
+            names = ("devices.list",)
+        out = []
+        for fname in names:
+            try:
+                with open(os.path.join(cgdir, fname), "rb") as fh:
+                    out.append(fh.read())
+            except OSError:
+                out.append(None)
+        return tuple(out)
 
     def allowed(self, cgdir):
         if os.path.exists(os.path.join(cgdir, FAKE_MARKER)):
@@ -358,6 +380,14 @@ class V2BpfBackend(DeviceRuleBackend):
         if rc < 0:
             raise CgroupError(f"bpf query on {cgdir}: {os.strerror(-rc)}")
         return tuple(int(ids[i]) for i in range(min(n.value, 16)))
+
+    def fingerprint(self, cgdir):
+        # the attached program ids (BPF_PROG_QUERY): a swapped or added program changes them;
+        # the set-mode allow map changes only through us
+        try:
+            return self.attached_ids(cgdir)
+        except CgroupError:
+            return None
 
     def apply(self, cgdir, grant, revoke, desired):
         lib = _native.host()
@@ -580,6 +610,13 @@ class V2RecordingBackend(DeviceRuleBackend):
 
     def __init__(self) -> None:
         self._installed: Dict[str, Tuple[bytes, FrozenSet[Tuple[int, int]]]] = {}
+
+    def fingerprint(self, cgdir):
+        try:
+            with open(os.path.join(cgdir, BPF_STATE), "rb") as fh:
+                return fh.read()
+        except OSError:
+            return None
 
     def allowed(self, cgdir):
         path = os.path.join(cgdir, BPF_STATE)

@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models.device import AmdGpu, DeviceNode, kfd_node
@@ -70,6 +70,16 @@ class HotMount:
         self.writer = writer
         self.faults = faults if faults is not None else NONE
         self.journal = journal if journal is not None else InjectionJournal()
+        # cgroup → the backend's fingerprint right after our last change: anything else that
+        # changes the cgroup's device control shows as a different one (the device guard)
+        self.expected: Dict[str, object] = {}
+
+    def _apply(self, cgdir: str, grant, revoke, desired) -> None:
+        try:
+            self.backend.apply(cgdir, grant, revoke, desired)
+        finally:
+            fp = getattr(self.backend, "fingerprint", None)
+            self.expected[cgdir] = fp(cgdir) if fp is not None else None
 
     # ------------------------------------------------------------------------ node sets
     def kfd(self) -> DeviceNode:
@@ -162,7 +172,7 @@ class HotMount:
                 done.append((t, grant, []))
                 with trace.span("cgroup_rule", backend=self.backend.name, rules=len(grant)):
                     self.faults.check("cgroup_rule")
-                    self.backend.apply(t.cgdir, grant, [], after)
+                    self._apply(t.cgdir, grant, [], after)
                 self.faults.check("cgroup_rule", "after")
                 with trace.span("devnodes", nodes=len(after)):
                     self.faults.check("devnodes")
@@ -206,7 +216,7 @@ class HotMount:
                 except Exception:  # noqa: BLE001 - cannot read back: revoke all of it
                     revoke = list(granted)
                 if revoke:
-                    self.backend.apply(t.cgdir, [], revoke, before)
+                    self._apply(t.cgdir, [], revoke, before)
             except Exception as e:  # noqa: BLE001
                 _log.error("rollback revoke in %s failed: %s", t.cgdir, e)
             else:
@@ -241,7 +251,7 @@ class HotMount:
             # reference order: deny → rm → kill (util.go:112,131,139)
             with trace.span("cgroup_rule", backend=self.backend.name, rules=len(revoke)):
                 self.faults.check("unmount")
-                self.backend.apply(t.cgdir, [], revoke, after)
+                self._apply(t.cgdir, [], revoke, after)
             self.faults.check("unmount", "after")
             # only nodes gpumounter created: one the container already had stays (its rule is
             # revoked all the same, so it is as dead as it was before the attach)
@@ -296,7 +306,7 @@ class HotMount:
                                 [((n.major, n.minor), n.path) for n in nodes],
                                 **self._owner(pod, t))
             if rules:
-                self.backend.apply(t.cgdir, rules, [], desired)
+                self._apply(t.cgdir, rules, [], desired)
             if nodes:
                 res = self.writer.create(t.target, nodes)
                 self.journal.settle(t.ref.id, [(n.major, n.minor) for n, r in zip(nodes, res)
@@ -314,7 +324,7 @@ class HotMount:
             unlink = list({(i.major, i.minor): DeviceNode(i.path, i.major, i.minor)
                            for i in mine if i.kind == "stale_node"}.values())
             if rules:
-                self.backend.apply(t.cgdir, [], rules, keep)
+                self._apply(t.cgdir, [], rules, keep)
                 self.journal.forget(t.ref.id, [(n.major, n.minor) for n in rules])
             if unlink:
                 self.writer.remove(t.target, unlink)
@@ -335,7 +345,7 @@ class HotMount:
         out = [AuditIssue(t.ref.name, "stale_rule", n.path, n.major, n.minor) for n in rules]
         out += [AuditIssue(t.ref.name, "stale_node", n.path, n.major, n.minor) for n in nodes]
         if rules:
-            self.backend.apply(t.cgdir, [], rules, [])
+            self._apply(t.cgdir, [], rules, [])
             self.journal.forget(container_id, [(n.major, n.minor) for n in rules])
         if nodes:
             self.writer.remove(t.target, nodes)

@@ -191,6 +191,9 @@ class SystemdPersistingBackend(DeviceRuleBackend):
     def allowed(self, cgdir):
         return self.inner.allowed(cgdir)
 
+    def fingerprint(self, cgdir):
+        return self.inner.fingerprint(cgdir)
+
     def installed(self, cgdir):
         return self.inner.installed(cgdir)
 

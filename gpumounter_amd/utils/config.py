@@ -174,6 +174,10 @@ class Config:
     detach_timeout_s: float = 60.0     # wait for placeholder deletion where waited for
     rpc_timeout_s: float = 180.0       # master→worker gRPC deadline (reference: none)
     reconcile_period_s: float = 30.0   # full reconciler sweep period
+    # every this many seconds, compare each hot container's device-control state (v2: the
+    # attached BPF program ids; v1: devices.list) with what gpumounter last installed, and
+    # repair at once when the runtime, runc update or systemd replaced it (0 = only the sweep)
+    device_guard_period_s: float = 1.0
     watch_resync_s: float = 300.0      # server-side timeout of one watch request
     api_token: str = ""                # if set, add/remove require "Authorization: Bearer <token>"
     # kube: the caller's own token, TokenReview + SubjectAccessReview on pods/gpumount (default);

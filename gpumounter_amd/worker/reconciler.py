@@ -31,6 +31,7 @@ relist wakes the sweep; a sweep that hit errors runs again after a short backoff
 from __future__ import annotations
 
 import asyncio
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -76,6 +77,11 @@ class Reconciler:
         self._wake = asyncio.Event()
         self._last_sweep = 0.0
         self.woken = 0
+        self.guard_period_s = float(getattr(getattr(service, "cfg", None),
+                                            "device_guard_period_s", 0.0) or 0.0)
+        self.guard_repairs = 0
+        self._guard_task = None
+        self._guard_timer = None
 
     # ------------------------------------------------------------------------ events
     def watch_events(self) -> None:
@@ -117,6 +123,60 @@ class Reconciler:
             # the runtime's /dev and device rules, so the GPUs go back in now — not at the next
             # periodic sweep, by which time the restarted process has looked and found none
             self._kick(("reinject", podu.ns_of(pod), podu.name_of(pod)))
+        elif etype == "MODIFIED" and self.guard_period_s > 0 and self._hot_cgroups(pod):
+            # a Pod with hot-mounted GPUs changed (an in-place resize: runc update re-applies
+            # the container's device rules): look again shortly, before the next guard tick
+            self._guard_soon()
+
+    # ------------------------------------------------------------------------ device guard
+    def _hot_cgroups(self, pod: dict) -> List[str]:
+        uid = podu.uid_of(pod)
+        return [e.cgdir for e in self.svc.hm.journal.entries()
+                if e.pod_uid == uid and e.rules and e.cgdir]
+
+    def guard_once(self) -> List[tuple]:
+        """Compare every hot container's device-control fingerprint with the one gpumounter left
+        (node/hotmount.py ``expected``); a container whose state changed behind our back (the
+        runtime re-attached its program, runc update, systemd, a devices.allow/deny write) has
+        its pod reconciled now. Returns the (namespace, pod) pairs kicked."""
+        hm = self.svc.hm
+        kicked = []
+        live = set()
+        for e in hm.journal.entries():
+            if not e.rules or not e.cgdir:
+                continue
+            live.add(e.cgdir)
+            fp = getattr(hm.backend, "fingerprint", lambda d: None)(e.cgdir)
+            if e.cgdir not in hm.expected:
+                hm.expected[e.cgdir] = fp       # first sight (a restarted worker): baseline
+                continue
+            if fp != hm.expected[e.cgdir] and os.path.isdir(e.cgdir):
+                hm.expected[e.cgdir] = fp       # kicked once; the repair records its own
+                self.guard_repairs += 1
+                _log.warning("device control of %s/%s changed outside gpumounter (%s); "
+                             "re-checking its hot-mounted GPUs", e.namespace, e.pod, e.cgdir)
+                key = ("guard", e.namespace, e.pod)
+                self._kick(key)
+                kicked.append(key[1:])
+        for d in [d for d in hm.expected if d not in live]:
+            del hm.expected[d]
+        return kicked
+
+    def _guard_soon(self, delay: float = 0.2) -> None:
+        if self._guard_timer is None and not self._stopping:
+            self._guard_timer = asyncio.get_running_loop().call_later(delay, self._guard_fire)
+
+    def _guard_fire(self) -> None:
+        self._guard_timer = None
+        try:
+            self.guard_once()
+        except Exception as e:  # noqa: BLE001 - the next tick or the sweep retries
+            _log.warning("device guard: %s", e)
+
+    async def _guard_loop(self) -> None:
+        while True:
+            await asyncio.sleep(self.guard_period_s)
+            self._guard_fire()
 
     def _restarted(self, pod: dict) -> bool:
         """A running container of a Pod that holds hot-mounted GPUs has no injection record:
@@ -198,6 +258,11 @@ class Reconciler:
                         svc.notify.event(owner, "GPUReinjected",
                                          f"container restarted; hot-mounted devices restored: "
                                          f"{', '.join(back)}")
+                    elif back and key[0] == "guard":
+                        svc.notify.event(owner, "GPUReinjected",
+                                         f"device rules were replaced outside gpumounter "
+                                         f"(runtime, runc update or systemd); hot-mounted "
+                                         f"access restored: {', '.join(back)}", warning=True)
                 self.event_actions += 1
                 svc.metrics.reconcile_actions.labels(action=f"event_{key[0]}").inc()
         except asyncio.CancelledError:
@@ -228,9 +293,19 @@ class Reconciler:
 
     async def start(self) -> None:
         self._task = asyncio.ensure_future(self._loop())
+        self.start_guard()
+
+    def start_guard(self) -> None:
+        """The device guard runs whether or not the periodic sweep does."""
+        if self.guard_period_s > 0 and self._guard_task is None:
+            self._guard_task = asyncio.ensure_future(self._guard_loop())
 
     async def stop(self) -> None:
         self._stopping = True
+        if self._guard_task is not None:
+            self._guard_task.cancel()
+        if self._guard_timer is not None:
+            self._guard_timer.cancel()
         for h in list(self._timers.values()):
             h.cancel()
         self._timers.clear()

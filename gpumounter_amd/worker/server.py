@@ -294,6 +294,8 @@ class Worker:
             self.http_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
         if reconcile and self.cfg.reconcile_period_s > 0:
             await self.reconciler.start()
+        else:
+            self.reconciler.start_guard()
         if self.plugin is not None:
             await self.plugin.start()
         await self.pool.start()

@@ -18,6 +18,7 @@ import stat
 import subprocess
 import sys
 import tempfile
+import time
 import uuid
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -74,7 +75,8 @@ async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0, userns_pid
                             kfd_major=1,
                             worker_overrides={"drm_major": 1, "bpf_pin_dir": bpffs,
                                               "host_dev_path": hostdev,
-                                              "devnode_stage_dir": stage}) as lc:
+                                              "devnode_stage_dir": stage,
+                                              "device_guard_period_s": float(os.environ.get("GM_TEST_GUARD", "1.0"))}) as lc:
         w = lc.nodes["node-0"].worker
         obs["backend"] = w.backend.name
         lc.tenant("t", pids={"main": [tenant_pid]})
@@ -108,10 +110,35 @@ async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0, userns_pid
                                                                   "/dev/dri/renderD8")}
         obs["audit_final"] = [i.kind for i in await lc.audit("default", "t")]
         obs["pins_left"] = [f for f in os.listdir(bpffs) if f.startswith("gm_")]
+        await guard_flow(lc, cg, obs)
         if shared_pid:
             await shared_dev_flow(lc, hostdev, shared_pid, obs)
         if userns_pid:
             await userns_flow(lc, userns_pid, obs)
+
+
+async def guard_flow(lc, cg, obs):
+    """The runtime attaches a fresh device program next to gpumounter's (runc update, a runtime
+    re-applying its rules): under BPF_F_ALLOW_MULTI it vetoes the hot-mounted GPU until the
+    worker's device guard (1 s period, the shipped default) notices and re-wraps the stack."""
+    code, b = await lc.add("default", "t", 1)
+    obs["guard_add"] = code
+    obs["guard_before_swap"] = probe(cg)
+    attach_runtime_program(cg)
+    t0 = time.monotonic()
+    obs["guard_right_after_swap"] = probe(cg)
+    while time.monotonic() - t0 < 5.0:
+        got = await asyncio.get_running_loop().run_in_executor(None, probe, cg)
+        if got == obs["guard_before_swap"]:
+            break
+        await asyncio.sleep(0.02)
+    obs["guard_restored_s"] = round(time.monotonic() - t0, 3)
+    obs["guard_after"] = probe(cg)
+    obs["guard_repairs"] = lc.nodes["node-0"].worker.reconciler.guard_repairs
+    code, _ = await lc.remove("default", "t", [d["uuid"] for d in b["devices"]])
+    obs["guard_remove"] = code
+    obs["guard_final"] = probe(cg)
+    obs["guard_audit_final"] = [i.kind for i in await lc.audit("default", "t")]
 
 
 USERNS_PROBE = ("import sys\n"

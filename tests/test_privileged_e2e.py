@@ -44,6 +44,14 @@ def test_full_stack_attach_detach_enforced_by_the_kernel(tmp_path):
     assert o["progs_final"] == ["runc_devices"]               # runtime program restored
     assert o["nodes_final"] == {"/dev/kfd": None, "/dev/dri/renderD8": None}
     assert o["audit_final"] == [] and o["pins_left"] == []
+    # the runtime attaches a fresh program next to ours: the GPU is cut, and the device guard
+    # (shipped 1 s period) re-wraps the stack within 1.5 s — not at the 30 s sweep
+    assert o["guard_add"] == 200 and o["guard_before_swap"] == "1110"
+    assert o["guard_right_after_swap"] == "1000"
+    assert o["guard_after"] == "1110" and o["guard_restored_s"] <= 1.5, o
+    assert o["guard_repairs"] >= 1
+    assert o["guard_remove"] == 200 and o["guard_final"] == "1000"
+    assert o["guard_audit_final"] == []
     # a tenant whose /dev is a bind of the host's keeps every node through attach + sweep
     assert o["shared_sees_host_dev"] and o["shared_add"] == 200 and o["shared_gpus"] == [5, 8]
     assert o["shared_after_add_unchanged"] and o["shared_after_sweep_unchanged"]

@@ -189,3 +189,46 @@ def test_journal_protocol_and_persistence(tmp_path):
     # a corrupt record is skipped, not fatal
     (tmp_path / "zzz.json").write_text("{not json")
     assert InjectionJournal(str(tmp_path)).entries() == []
+
+
+@pytest.mark.parametrize("mode", ["v1", "v2"])
+def test_device_guard_repairs_rules_replaced_outside_gpumounter_within_a_second(mode):
+    """a runtime that re-applies a container's device rules
+    (runc update on a resize, a runtime re-attaching its program, a write to devices.deny)
+    cuts new opens of the hot GPUs. The device guard compares each hot container's device
+    control with what gpumounter last installed every device_guard_period_s and repairs at
+    once — not at the 30 s sweep (which does not run at all in this test)."""
+    import os
+    from gpumounter_amd.node.cgroup import BPF_STATE
+
+    async def body(lc):
+        lc.tenant("t")
+        code, b = await lc.add("default", "t", 1)
+        assert code == 200
+        node = lc.nodes["node-0"].node
+        (c,) = [c for c in node.containers.values() if c.pod_name == "t"]
+        w = lc.nodes["node-0"].worker
+        g = b["devices"][0]
+        if mode == "v1":          # someone denies the render node again
+            with open(os.path.join(c.cgroup_dir, "devices.deny"), "a") as fh:
+                fh.write(f"c 226:{g['render_minor']} rw\n")
+        else:                     # the runtime replaced the program: ours is gone
+            os.unlink(os.path.join(c.cgroup_dir, BPF_STATE))
+        assert await lc.audit("default", "t")                   # access is cut
+        t0 = asyncio.get_running_loop().time()
+        while asyncio.get_running_loop().time() - t0 < 3.0:
+            if not await lc.audit("default", "t"):
+                break
+            await asyncio.sleep(0.05)
+        took = asyncio.get_running_loop().time() - t0
+        assert not await lc.audit("default", "t") and took < 1.5, took
+        assert w.reconciler.guard_repairs >= 1
+        await w.service.notify.drain()
+        assert any(e["reason"] == "GPUReinjected" and "outside gpumounter" in e["message"]
+                   for e in lc.cluster.events_for("default", "t"))
+        n0 = w.reconciler.guard_repairs                         # our own changes: no alarm
+        code, _ = await lc.remove("default", "t", [g["uuid"]])
+        assert code == 200
+        await asyncio.sleep(0.4)
+        assert w.reconciler.guard_repairs == n0
+    run(body, cgroup_mode=mode, worker_overrides={"device_guard_period_s": 0.2})
