@@ -1,7 +1,21 @@
-"""Where the slowest attaches spent their time: reads ``bench.py --dump-samples`` files and, per
-file, prints the percentiles, the 10 slowest cycles with their worker stage split, and how much of
-each slow cycle the worker accounts for (the rest is the client → master → worker hops)."""
+"""Where the slowest attaches spent their time.
+
+Reads ``bench.py --dump-samples`` files. Every sample holds the client's attach time, the
+master's stage split (``gm:master_*``: authz, locate, the gRPC call, the reply payload) and the
+worker's (its attach stages plus ``rpc_queue``/``rpc_tail``, the handler around the operation).
+Each attach is cut into components that add up to the client's time:
+
+* ``client_http``  — client ⇄ master HTTP (what the master's handler does not see);
+* ``master_own``   — the master's handler outside the gRPC call (authz, lookup, reply);
+* ``grpc``         — the gRPC call minus the worker's handler (transport, TLS, both loops);
+* ``worker_rpc``   — the worker's handler around the operation (task start, reply hand-off);
+* ``worker:<stage>`` — the worker's attach stages (ledger_reserve, placeholder_wait, mount, ...).
+
+Per file: percentiles, the 10 slowest cycles with their largest component, and for the cycles at
+or above the p99 how much each component exceeds its own median there (the tail's attribution).
+"""
 import json
+import statistics
 import sys
 
 
@@ -14,26 +28,52 @@ def top_level(stages):
     return {k: v for k, v in stages.items() if "." not in k}
 
 
+def components(r):
+    st = top_level(r.get("stages") or {})
+    ms = r.get("master") or {}
+    worker_ops = {k: v for k, v in st.items() if not k.startswith("rpc_")}
+    handler = st.get("rpc_queue", 0.0) + st.get("rpc_tail", 0.0)
+    out = {f"worker:{k}": v for k, v in worker_ops.items()}
+    if ms:
+        master = sum(ms.values())
+        rpc = ms.get("master_rpc", 0.0)
+        out["client_http"] = r["attach_ms"] - master
+        out["master_own"] = master - rpc
+        out["grpc"] = rpc - sum(worker_ops.values()) - handler
+        out["worker_rpc"] = handler
+    else:                       # samples from before the master stages were recorded
+        out["outside_worker"] = r["attach_ms"] - sum(worker_ops.values())
+    return out
+
+
 def report(path):
     rows = [json.loads(line) for line in open(path) if line.strip()]
     att = [r["attach_ms"] for r in rows]
-    worker = [sum(top_level(r["stages"]).values()) for r in rows]
-    slow = sorted(rows, key=lambda r: -r["attach_ms"])[:10]
+    comps = [components(r) for r in rows]
+    keys = sorted({k for c in comps for k in c})
+    med = {k: statistics.median([c.get(k, 0.0) for c in comps]) for k in keys}
+    p99 = pct(att, 0.99)
+    tail = [c for r, c in zip(rows, comps) if r["attach_ms"] >= p99]
+    excess = {k: round(statistics.mean([c.get(k, 0.0) for c in tail]) - med[k], 3)
+              for k in keys} if tail else {}
+    slow = sorted(zip(rows, comps), key=lambda rc: -rc[0]["attach_ms"])[:10]
     t0 = rows[0]["t"] if rows else 0.0
     out = {"file": path, "cycles": len(rows),
            "attach_ms": {q: round(pct(att, p), 3) for q, p in
-                         (("p50", .5), ("p99", .99), ("p999", .999), ("max", 1.0))},
-           "worker_ms": {q: round(pct(worker, p), 3) for q, p in
-                         (("p50", .5), ("p99", .99), ("max", 1.0))},
+                         (("p50", .5), ("p90", .9), ("p99", .99), ("p999", .999),
+                          ("max", 1.0))},
+           "component_p50_ms": {k: round(v, 3) for k, v in med.items()},
+           "tail_cycles": len(tail),
+           # mean over the cycles at or above the p99, minus the component's median
+           "tail_excess_over_p50_ms": dict(sorted(excess.items(), key=lambda kv: -kv[1])),
            "slowest": []}
-    for r in slow:
-        st = top_level(r["stages"])
-        w = sum(st.values())
-        big = max(st.items(), key=lambda kv: kv[1]) if st else ("", 0.0)
+    for r, c in slow:
+        big = max(c.items(), key=lambda kv: kv[1]) if c else ("", 0.0)
         out["slowest"].append({"at_s": round(r["t"] - t0, 2), "attach_ms": r["attach_ms"],
-                               "worker_ms": round(w, 3),
-                               "outside_worker_ms": round(r["attach_ms"] - w, 3),
-                               "largest_stage": [big[0], round(big[1], 3)]})
+                               "largest": [big[0], round(big[1], 3)],
+                               "over_median": {k: round(v - med.get(k, 0.0), 3)
+                                               for k, v in c.items()
+                                               if v - med.get(k, 0.0) > 0.1}})
     return out
 
 
