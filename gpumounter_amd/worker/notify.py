@@ -8,7 +8,10 @@ projects that into the container, where it updates without a restart.
 
 Neither is on the request path: sends are queued and flushed once the worker has had no
 attach/detach in flight for ``notify_idle_ms`` (so the apiserver round trips never share the event
-loop with a request), or after ``notify_max_delay_ms`` under sustained load. Failures are logged,
+loop with a request), or after ``notify_max_delay_ms`` under sustained load. Identical Events
+queued meanwhile (same Pod, reason, message and type — a Pod attached and detached in a loop)
+are sent once with their ``count``, as client-go's event correlator aggregates them, so a flush
+under sustained load is a handful of requests, not one per operation. Failures are logged,
 never surfaced.
 """
 from __future__ import annotations
@@ -38,6 +41,8 @@ class Notifier:
         self._idle = asyncio.Event()
         self._idle.set()
         self.sent = 0
+        # coalescing key → [first timestamp, count] of Events queued and not yet sent
+        self._ev_pending: Dict[tuple, list] = {}
 
     @contextlib.contextmanager
     def operation(self):
@@ -94,6 +99,7 @@ class Notifier:
 
     async def stop(self) -> None:
         self._queue.clear()
+        self._ev_pending.clear()
         for t in list(self._tasks):
             t.cancel()
 
@@ -103,6 +109,13 @@ class Notifier:
             return
         now = datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
         ns, name = podu.ns_of(pod), podu.name_of(pod)
+        key = ("event", ns, name, podu.uid_of(pod), reason, message[:1024], warning)
+        agg = self._ev_pending.get(key)
+        if agg is not None:
+            agg[1] += 1                     # queued already: counted into that one
+            agg[2] = now
+            return
+        self._ev_pending[key] = agg = [now, 1, now]
         ev = {"apiVersion": "v1", "kind": "Event",
               "metadata": {"generateName": f"{name}.", "namespace": ns},
               "involvedObject": {"apiVersion": "v1", "kind": "Pod", "namespace": ns,
@@ -111,10 +124,11 @@ class Notifier:
               "type": "Warning" if warning else "Normal",
               "source": {"component": "gpumounter-worker", "host": self.cfg.node_name},
               "reportingComponent": "gpumounter-amd/worker",
-              "reportingInstance": self.cfg.node_name,
-              "firstTimestamp": now, "lastTimestamp": now, "count": 1}
+              "reportingInstance": self.cfg.node_name}
 
         async def send():
+            self._ev_pending.pop(key, None)
+            ev.update(firstTimestamp=agg[0], lastTimestamp=agg[2], count=agg[1])
             try:
                 await self.kube.create_event(ns, ev)
                 self.sent += 1

@@ -1311,3 +1311,43 @@ def test_placement_correct_on_xgmi_leaves_numa_only_differences_alone():
         assert lc.nodes["node-0"].worker.metrics.placement_corrections._value.get() == 0
         assert len(node_of(lc).allocated) == 5 and not await lc.audit("default", "t")
     run(body, alloc_policy="first-free", worker_overrides={"placement_correct_on": "xgmi"})
+
+
+def test_identical_queued_events_are_sent_once_with_their_count():
+    """A Pod attached and detached in a loop while notifications are held back: the flush sends
+    one Event per (Pod, reason, message) with its count — client-go's aggregation — instead of
+    a burst of one request per operation on the worker's event loop."""
+    from types import SimpleNamespace
+
+    from gpumounter_amd.worker.notify import Notifier
+
+    class Kube:
+        def __init__(self):
+            self.events = []
+
+        async def create_event(self, ns, ev):
+            self.events.append(dict(ev))
+
+    async def body():
+        cfg = SimpleNamespace(emit_events=True, annotate_tenant=False, node_name="n0",
+                              notify_idle_ms=1.0, notify_max_delay_ms=10_000.0)
+        kube = Kube()
+        nt = Notifier(cfg, kube)
+        pod = {"metadata": {"name": "t", "namespace": "default", "uid": "u1"}}
+        g = SimpleNamespace(index=1, bdf="0000:01:00.0", render_minor=129)
+        with nt.operation():
+            for _ in range(50):
+                nt.attached(pod, [g], [g], "entire")
+                nt.detached(pod, [g], [], [])
+            nt.attached(pod, [g], [g], "single")          # another message: its own Event
+        await nt.drain()
+        got = sorted((e["reason"], e["count"], e["message"][:20]) for e in kube.events)
+        assert got == [("GPUAttached", 1, "hot-mounted 1 GPU(s)"),
+                       ("GPUAttached", 50, "hot-mounted 1 GPU(s)"),
+                       ("GPUDetached", 50, "removed 1 GPU(s): 00")], got
+        # after the flush a new one starts a new aggregate
+        with nt.operation():
+            nt.detached(pod, [g], [], [])
+        await nt.drain()
+        assert kube.events[-1]["count"] == 1
+    asyncio.run(body())
