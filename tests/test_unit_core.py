@@ -257,8 +257,19 @@ def test_tail_report_attributes_slow_cycles(tmp_path):
     rep = tr.report(str(f))
     assert rep["cycles"] == 100 and rep["attach_ms"]["max"] == 80.0
     top = rep["slowest"][0]
-    assert top["largest_stage"] == ["ledger_reserve", 79.0]
-    assert top["worker_ms"] == 79.2 and top["outside_worker_ms"] == 0.8   # sub-stages not summed
+    assert top["largest"] == ["worker:ledger_reserve", 79.0]
+    # sub-stages not summed: 1.0 - (0.3 + 0.2) outside the worker, as in every cycle
+    assert rep["component_p50_ms"]["outside_worker"] == 0.5
+    assert rep["tail_excess_over_p50_ms"]["worker:ledger_reserve"] == 78.7
+    # with the master's stages recorded, the outside is split into HTTP / master / gRPC
+    rows = [{"t": 0.0, "attach_ms": 2.0,
+             "stages": {"ledger_reserve": 0.3, "mount": 0.2, "rpc_queue": 0.01, "rpc_tail": 0.04},
+             "master": {"master_authz": 0.01, "master_locate": 0.01, "master_rpc": 1.7,
+                        "master_payload": 0.03}}]
+    f.write_text(json.dumps(rows[0]) + "\n")
+    c = tr.report(str(f))["component_p50_ms"]
+    assert c["client_http"] == 0.25 and c["master_own"] == 0.05 and c["worker_rpc"] == 0.05
+    assert c["grpc"] == 1.15 and c["worker:ledger_reserve"] == 0.3
 
 
 def test_informer_drops_write_through_older_than_a_relist():
