@@ -224,7 +224,8 @@ def main() -> int:
         # the box's speed next to the value (gpumounter_amd/utils/calib.py): before anything
         # initialises the GPU, since the calibration forks and spawns
         from gpumounter_amd.utils import calib
-        box = calib.measure(grpc_floor=True)
+        box = calib.measure(grpc_floor=True,
+                            idle_s=args.idle_s if args.cold_steps > 0 else 0.0)
     if world > 1 and world != n:
         print(f"WORLD_SIZE={world} must equal --gpus={n}", file=sys.stderr)
         return 2

@@ -10,7 +10,9 @@ moves with two properties of the machine it runs on, which this module measures 
   over a loopback TCP connection, median of many: what one hop between the daemons costs before
   any gpumounter code runs (scheduler wake-up of an idle core, C-state exit, cross-CCX cache);
 * ``grpc_rtt_us`` — a unary AddGPU call between two grpc.aio processes answering at once,
-  plaintext and mTLS: the floor under the master → worker hop.
+  plaintext and mTLS: the floor under the master → worker hop;
+* ``pingpong_after_idle_us`` / ``py_loop_after_idle_us`` (with ``idle_s``) — the same round
+  trip and the same Python loop right after ``idle_s`` asleep: what a quiet spell costs.
 
 A value measured on a box whose ``pingpong_us`` is 3× another's is not a regression of the code;
 ``bench.py`` puts this dict into its JSON as ``box`` so every number carries its box.
@@ -47,8 +49,10 @@ def _echo_child(sock: socket.socket, n: int) -> None:
         sock.sendall(b)
 
 
-def pingpong_us(n: int = 2000, tcp: bool = False) -> float:
-    """Median round trip between this process and a forked echo child (socketpair or TCP)."""
+def pingpong_us(n: int = 2000, tcp: bool = False, idle_s: float = 0.0) -> float:
+    """Median round trip between this process and a forked echo child (socketpair or TCP);
+    ``idle_s`` > 0: each round trip after that long asleep (both processes idle), what a
+    request arriving after a quiet spell pays per hop."""
     if tcp:
         lsock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         lsock.bind(("127.0.0.1", 0))
@@ -79,6 +83,8 @@ def pingpong_us(n: int = 2000, tcp: bool = False) -> float:
         rtts = []
         msg = b"x" * 32
         for _ in range(n):
+            if idle_s:
+                time.sleep(idle_s)
             t0 = time.perf_counter()
             s.sendall(msg)
             got = 0
@@ -86,7 +92,7 @@ def pingpong_us(n: int = 2000, tcp: bool = False) -> float:
                 got += len(s.recv(64))
             rtts.append((time.perf_counter() - t0) * 1e6)
         s.close()
-        return statistics.median(rtts[n // 10:])
+        return statistics.median(rtts if idle_s else rtts[n // 10:])
     finally:
         os.waitpid(pid, 0)
 
@@ -195,7 +201,7 @@ def _governor() -> str | None:
         return None
 
 
-def measure(grpc_floor: bool = False) -> dict:
+def measure(grpc_floor: bool = False, idle_s: float = 0.0) -> dict:
     """Fixed calibration, about 0.3 s (about 2 s more with ``grpc_floor``). Run it before the
     process initialises the GPU: the pingpong child is a fork (pure-Python socket code, then
     ``_exit``) and the gRPC server a subprocess."""
@@ -215,6 +221,16 @@ def measure(grpc_floor: bool = False) -> dict:
     }
     if grpc_floor:
         out["grpc_rtt_us"] = grpc_rtt_us()
+    if idle_s:
+        # the same hop and the same Python work after idle_s asleep: what a quiet spell (caches
+        # and cores gone cold, or to other jobs) costs on this box before any gpumounter code
+        out["idle_s"] = idle_s
+        out["pingpong_after_idle_us"] = round(pingpong_us(8, idle_s=idle_s), 2)
+        cold = []
+        for _ in range(5):
+            time.sleep(idle_s)
+            cold.append(_py_loop_once())
+        out["py_loop_after_idle_us"] = round(statistics.median(cold), 1)
     return out
 
 

@@ -22,7 +22,7 @@ from aiohttp import web
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.cluster.informer import ClaimInformer, PodInformer
 from gpumounter_amd.cluster.kube import KubeClient
-from gpumounter_amd.cluster.placeholder import PlaceholderManager
+from gpumounter_amd.cluster.placeholder import LABEL_NODE, PlaceholderManager
 from gpumounter_amd.cluster.pool import WarmPool
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.node import systemd
@@ -95,7 +95,9 @@ class Worker:
         self.ph_informer = PodInformer(self.kube, ph_ns,
                                        PlaceholderManager.selector_for_node(cfg.node_name),
                                        resync_s=cfg.watch_resync_s)
-        self.node_informer = PodInformer(self.kube, None, "",
+        # every pod of this node except the placeholders, which ph_informer watches already:
+        # their events (≈5 per attach/detach cycle) would be parsed twice for nothing
+        self.node_informer = PodInformer(self.kube, None, f"!{LABEL_NODE}",
                                          f"spec.nodeName={cfg.node_name}",
                                          resync_s=cfg.watch_resync_s)
         self.placeholders = PlaceholderManager(cfg, self.kube, self.ledger, self.ph_informer,
