@@ -27,6 +27,7 @@ from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.api import protodef
 from gpumounter_amd.cluster.informer import PodInformer, SlimPodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
+from gpumounter_amd.cluster.placeholder import LABEL_NODE
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.master.authz import Authorizer
 from gpumounter_amd.utils import log, runtime, trace
@@ -167,9 +168,11 @@ class Master:
         self._pod_nodes: Dict[Tuple[str, str], Tuple[str, str, float]] = {}
         # pod → node without a GET per request (the reference GETs the pod every time,
         # main.go:52); until its first LIST is in, requests fall back to a GET
+        # (placeholders excluded: never an attach target, and every attach creates and deletes
+        # some — their events would land on the master's loop while it waits for the worker)
         self.pods: Optional[SlimPodInformer] = SlimPodInformer(
-            self.kube, resync_s=cfg.watch_resync_s) if getattr(cfg, "master_pod_index", True) \
-            else None
+            self.kube, label_selector=f"!{LABEL_NODE}", resync_s=cfg.watch_resync_s) \
+            if getattr(cfg, "master_pod_index", True) else None
         self._pods_task: Optional[asyncio.Task] = None
 
     # ------------------------------------------------------------------------ app
