@@ -341,11 +341,13 @@ class Master:
                 response_deserializer=api.AddGPUResponse.FromString)
             try:
                 with trace.span("master_rpc"):
+                    t_send = time.perf_counter()
                     resp = await stub(api.AddGPURequest(
                         pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
                         request_id=rid, container=container, idempotency_key=key,
                         requested_by=user, lease_s=lease_s),
                         timeout=self.cfg.rpc_timeout_s)
+                    self._legs(resp, t_send, time.perf_counter())
             except grpc.aio.AioRpcError as e:
                 if cached and e.code() == grpc.StatusCode.FAILED_PRECONDITION and \
                         "this worker serves" in (e.details() or ""):
@@ -385,10 +387,12 @@ class Master:
                 response_deserializer=api.RemoveGPUResponse.FromString)
             try:
                 with trace.span("master_rpc"):
+                    t_send = time.perf_counter()
                     resp = await stub(api.RemoveGPURequest(
                         pod_name=name, namespace=ns, uuids=uuids, force=force,
                         request_id=rid, container=container, requested_by=user),
                         timeout=self.cfg.rpc_timeout_s)
+                    self._legs(resp, t_send, time.perf_counter())
             except grpc.aio.AioRpcError as e:
                 _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name,
                            e.details())
@@ -475,6 +479,24 @@ class Master:
                                                    request.query.get("container", ""), rid,
                                                    request.get(USER_KEY, ""))
         return self._reply(request, route, status, text, self._stamp(payload, root))
+
+    @staticmethod
+    def _legs(resp, t_send: float, t_recv: float) -> None:
+        """The worker stamps when its handler started and returned (``clock.in``/``clock.out``,
+        host monotonic ms). On one host that splits the gRPC call into its request leg (master
+        send → worker handler) and response leg (handler return → master receive), recorded as
+        stages of the master's trace; the stamps themselves are dropped from the reply."""
+        stamps = {t.name: t.ms for t in resp.timings if t.name.startswith("clock.")}
+        if not stamps:
+            return
+        keep = [t for t in resp.timings if not t.name.startswith("clock.")]
+        del resp.timings[:]
+        resp.timings.extend(keep)
+        t_in, t_out = stamps.get("clock.in"), stamps.get("clock.out")
+        if t_in is None or t_out is None or not t_send * 1e3 <= t_in <= t_out <= t_recv * 1e3:
+            return                     # another host's clock: the legs are not measurable
+        trace.record("grpc_request", int((t_in - t_send * 1e3) * 1e6))
+        trace.record("grpc_response", int((t_recv * 1e3 - t_out) * 1e6))
 
     @staticmethod
     def _stamp(payload: dict, root: trace.Span) -> dict:

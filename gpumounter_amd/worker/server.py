@@ -156,6 +156,7 @@ class Worker:
 
     def _wrap(self, fn):
         async def handler(request, context):
+            t_in = time.perf_counter()
             if not self._peer_allowed(context):
                 await context.abort(grpc.StatusCode.PERMISSION_DENIED,
                                     "client certificate is not an allowed gpumounter identity")
@@ -174,7 +175,14 @@ class Worker:
                     # ran, rpc_tail = from its end until the handler resumed. What is left of
                     # the master's RPC time is gRPC transport (client, server, TLS)
                     resp.timings.add(name="rpc_queue", ms=(t1 - t0) * 1e3)
-                    resp.timings.add(name="rpc_tail", ms=(time.perf_counter() - t2) * 1e3)
+                    t_out = time.perf_counter()
+                    resp.timings.add(name="rpc_tail", ms=(t_out - t2) * 1e3)
+                    resp.timings.add(name="rpc_peer_check", ms=(t0 - t_in) * 1e3)
+                    # when the handler started and returned on the host's monotonic clock
+                    # (CLOCK_MONOTONIC: the same in every process of the host): a master on the
+                    # same host splits the gRPC hop into its request and response legs
+                    resp.timings.add(name="clock.in", ms=t_in * 1e3)
+                    resp.timings.add(name="clock.out", ms=t_out * 1e3)
                 return resp
             except asyncio.CancelledError:
                 op.add_done_callback(self._orphan_done)     # its outcome reaches no caller
