@@ -424,7 +424,8 @@ def main() -> int:
                 if samples is not None:
                     samples.append({"t": round(time.time(), 4), "attach_ms": round(st["ms"], 4),
                                     "detach_ms": round((t1 - t0) * 1e3, 4),
-                                    "stages": st["timings"], "master": st["mtimings"]})
+                                    "stages": st["timings"], "master": st["mtimings"],
+                                    "worker_ms": st.get("worker_ms")})
                 audit_issues += st["issues"]
                 for k, v in st["timings"].items():
                     stage.setdefault(k, []).append(v)

@@ -8,8 +8,11 @@ Each attach is cut into components that add up to the client's time:
 * ``client_http``  — client ⇄ master HTTP (what the master's handler does not see);
 * ``master_own``   — the master's handler outside the gRPC call (authz, lookup, reply);
 * ``grpc``         — the gRPC call minus the worker's handler (transport, TLS, both loops);
-* ``worker_rpc``   — the worker's handler around the operation (task start, reply hand-off);
-* ``worker:<stage>`` — the worker's attach stages (ledger_reserve, placeholder_wait, mount, ...).
+  with a same-host clock also split into ``grpc:request`` and ``grpc:response`` (not added);
+* ``worker_rpc``   — the worker's handler around the operation (peer check, task start, reply
+  hand-off);
+* ``worker:<stage>`` — the worker's attach stages (ledger_reserve, placeholder_wait, mount, ...),
+  and ``worker:other`` for its time outside them.
 
 Per file: percentiles, the 10 slowest cycles with their largest component, and for the slowest
 1 % of the cycles how much each component exceeds its own median there (the tail's attribution).
@@ -30,17 +33,27 @@ def top_level(stages):
 
 def components(r):
     st = top_level(r.get("stages") or {})
-    ms = r.get("master") or {}
+    ms = top_level(r.get("master") or {})
     worker_ops = {k: v for k, v in st.items() if not k.startswith("rpc_")}
-    handler = st.get("rpc_queue", 0.0) + st.get("rpc_tail", 0.0)
+    handler = sum(v for k, v in st.items() if k.startswith("rpc_"))
     out = {f"worker:{k}": v for k, v in worker_ops.items()}
+    worker = r.get("worker_ms")
+    if worker is not None:
+        # the worker's attach outside its named stages (locks, policy, replies, metrics)
+        out["worker:other"] = worker - sum(worker_ops.values())
+    else:
+        worker = sum(worker_ops.values())
     if ms:
         master = sum(ms.values())
         rpc = ms.get("master_rpc", 0.0)
         out["client_http"] = r["attach_ms"] - master
         out["master_own"] = master - rpc
-        out["grpc"] = rpc - sum(worker_ops.values()) - handler
+        out["grpc"] = rpc - worker - handler
         out["worker_rpc"] = handler
+        legs = r.get("master") or {}
+        if "master_rpc.grpc_request" in legs:    # same-host clock: the two legs of the hop
+            out["grpc:request"] = legs["master_rpc.grpc_request"]
+            out["grpc:response"] = legs["master_rpc.grpc_response"]
     else:                       # samples from before the master stages were recorded
         out["outside_worker"] = r["attach_ms"] - sum(worker_ops.values())
     return out
