@@ -21,9 +21,9 @@ from __future__ import annotations
 import asyncio
 import secrets
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
-from gpumounter_amd.cluster.kube import NotFound
+from gpumounter_amd.cluster.kube import Conflict, NotFound
 from gpumounter_amd.cluster.placeholder import (ANN_GPUS, InsufficientGPU, LABEL_NODE,
                                                 Placeholder,
                                                 PlaceholderManager, Reservation,
@@ -39,6 +39,10 @@ from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTA
 from gpumounter_amd.utils import log, trace
 
 _log = log.get("cluster.pool")
+
+
+class ClaimTaken(Exception):
+    """The standby placeholder was claimed (or deleted) by someone else since it was chosen."""
 
 
 def is_standby(p: dict) -> bool:
@@ -244,10 +248,11 @@ class WarmPool:
                                 ANN_GROUP: group or None, ANN_CANDIDATE: None}}}
             for ph in chosen:
                 self._claimed.add(ph.uid)
+            seen = self._versions()
             with trace.span("pool_claim", placeholders=len(chosen)):
                 epoch = self.ph.informer.epoch
                 res = await asyncio.gather(
-                    *[self.ph.kube.patch_pod(ph.namespace, ph.name, patch) for ph in chosen],
+                    *[self._claim_one(ph, patch, seen.get(ph.uid), attach_id) for ph in chosen],
                     return_exceptions=True)
             ok = [r for r in res if isinstance(r, dict)]
             for r in ok:
@@ -256,11 +261,17 @@ class WarmPool:
                 self._claimed.discard(ph.uid)
             if len(ok) != len(chosen):
                 # undo the partial claim, then let the caller fall back. A PATCH that failed may
-                # still have taken effect (its reply lost), so every chosen placeholder goes
-                # back; one that cannot be put back is deleted — the caller never mounts these,
-                # and a claim left standing would give the owner a GPU it was told it did not get
-                back = await self._standby_patch(chosen)
-                stray = [ph for ph in chosen if ph not in back]
+                # still have taken effect (its reply lost), so every chosen placeholder that is
+                # this attach's goes back; one that cannot be put back is deleted — the caller
+                # never mounts these, and a claim left standing would give the owner a GPU it
+                # was told it did not get. One another claim took is left to its owner.
+                taken = [ph for ph, r in zip(chosen, res) if isinstance(r, ClaimTaken)]
+                mine = [ph for ph in chosen if ph not in taken]
+                back, theirs = await self._unclaim(mine, attach_id)
+                stray = [ph for ph in mine if ph not in back and ph not in theirs]
+                if taken:
+                    _log.info("standby placeholder(s) %s claimed elsewhere; falling back",
+                              [ph.name for ph in taken])
                 if stray:
                     await self.ph.release(stray, wait=False)
                 return None
@@ -271,7 +282,83 @@ class WarmPool:
         self.poke()
         return Reservation(chosen)
 
-    async def _standby_patch(self, phs: Sequence[Placeholder]) -> List[Placeholder]:
+    def _versions(self) -> Dict[str, str]:
+        """uid → resourceVersion of every standby placeholder as the informer last saw it."""
+        return {p["metadata"]["uid"]: p["metadata"].get("resourceVersion", "")
+                for p in self.ph.live() if is_standby(p)}
+
+    @staticmethod
+    def _mine(pod: dict, attach_id: str) -> bool:
+        return bool(attach_id) and \
+            (pod["metadata"].get("annotations") or {}).get(ANN_ATTACH_ID) == attach_id
+
+    async def _claim_one(self, ph: Placeholder, patch: dict, rv: Optional[str],
+                         attach_id: str) -> dict:
+        """Claim one standby placeholder with a merge patch that carries the resourceVersion
+        the choice was made on: it applies only if nothing changed the placeholder since. The
+        informer can be behind the apiserver (after a relist an acknowledged write is not in the
+        cache yet; a worker killed mid-claim may still have a PATCH in flight), and an
+        unconditional claim of a placeholder that is no longer standby hands one GPU to two
+        Pods. On a conflict the placeholder is read back: this attach's own claim (an earlier
+        attempt whose reply was lost) counts as done, one still standby is claimed at its new
+        version, anything else raises :class:`ClaimTaken`."""
+        kube = self.ph.kube
+        for _ in range(3):
+            if not rv:
+                cur = await kube.get_pod(ph.namespace, ph.name)
+                if not self._claimable(cur, ph):
+                    raise ClaimTaken(ph.name)
+                rv = cur["metadata"]["resourceVersion"]
+            try:
+                return await kube.patch_pod(ph.namespace, ph.name, {
+                    "metadata": dict(patch["metadata"], resourceVersion=rv)})
+            except NotFound:
+                raise ClaimTaken(ph.name) from None
+            except Conflict:
+                cur = await kube.get_pod(ph.namespace, ph.name)
+                if cur["metadata"].get("uid") == ph.uid and self._mine(cur, attach_id):
+                    return cur
+                if not self._claimable(cur, ph):
+                    raise ClaimTaken(ph.name) from None
+                rv = cur["metadata"]["resourceVersion"]
+        raise ClaimTaken(ph.name)
+
+    @staticmethod
+    def _claimable(pod: dict, ph: Placeholder) -> bool:
+        md = pod["metadata"]
+        return md.get("uid") == ph.uid and is_standby(pod) and not md.get("deletionTimestamp")
+
+    async def _unclaim(self, phs: Sequence[Placeholder], attach_id: str
+                       ) -> Tuple[List[Placeholder], List[Placeholder]]:
+        """Undo a failed claim: put back into the pool each placeholder this attach claimed (at
+        the version just read, so a claim made since by someone else is never undone). Returns
+        (free again, not this attach's to undo); the rest could not be read or put back."""
+        back: List[Placeholder] = []
+        theirs: List[Placeholder] = []
+
+        async def one(ph: Placeholder) -> None:
+            for _ in range(3):
+                try:
+                    cur = await self.ph.kube.get_pod(ph.namespace, ph.name)
+                except NotFound:
+                    theirs.append(ph)                   # gone: nothing left to undo
+                    return
+                if cur["metadata"].get("uid") != ph.uid or not self._mine(cur, attach_id):
+                    (back if self._claimable(cur, ph) else theirs).append(ph)
+                    return
+                got = await self._standby_patch([ph], cur["metadata"]["resourceVersion"])
+                if got:
+                    back.append(ph)
+                    return
+
+        res = await asyncio.gather(*[one(ph) for ph in phs], return_exceptions=True)
+        for ph, r in zip(phs, res):
+            if isinstance(r, Exception):
+                _log.error("return %s/%s to pool: %s", ph.namespace, ph.name, r)
+        return back, theirs
+
+    async def _standby_patch(self, phs: Sequence[Placeholder],
+                             rv: Optional[str] = None) -> List[Placeholder]:
         patch = {"metadata": {
             "labels": {LABEL_OWNER: None, LABEL_OWNER_NS: None},
             "annotations": {ANN_OWNER_UID: None, ANN_OWNER_NAME: None,
@@ -281,6 +368,8 @@ class WarmPool:
                             # claimed one still marked would be invisible to its new owner's
                             # ledger view, and released under it as an abandoned pick
                             ANN_CANDIDATE: None}}}
+        if rv:                                  # only at the version the caller read
+            patch["metadata"]["resourceVersion"] = rv
         epoch = self.ph.informer.epoch
         res = await asyncio.gather(*[self.ph.kube.patch_pod(p.namespace, p.name, patch)
                                      for p in phs], return_exceptions=True)
@@ -289,7 +378,7 @@ class WarmPool:
             if isinstance(r, dict):
                 self.ph.informer.upsert(r, epoch)
                 back.append(p)
-            elif not isinstance(r, NotFound):
+            elif not isinstance(r, (NotFound, Conflict)):
                 _log.error("return %s/%s to pool: %s", p.namespace, p.name, r)
         return back
 

@@ -534,6 +534,14 @@ class FakeCluster:
         if pod is None:
             return None
         md_patch = patch.get("metadata", {})
+        want_rv = md_patch.get("resourceVersion")
+        if want_rv is not None and want_rv != pod["metadata"].get("resourceVersion"):
+            # a resourceVersion in the patch is a precondition (optimistic concurrency)
+            raise web.HTTPConflict(text=json.dumps({
+                "kind": "Status", "code": 409, "reason": "Conflict",
+                "message": f'Operation cannot be fulfilled on pods "{name}": the object has '
+                           "been modified; please apply your changes to the latest version "
+                           "and try again"}), content_type="application/json")
         merged = merge_patch(pod["metadata"], md_patch)
         pod["metadata"] = merged
         if "spec" in patch:
@@ -594,7 +602,7 @@ class FakeCluster:
                 self.random_faults_served += 1
                 st = rnd.choice((500, 503, 429))
                 if rnd.random() < 0.5:
-                    await handler(request)          # it happened; the reply gets lost
+                    await self._lost_reply(handler, request)
                 return web.json_response({"kind": "Status", "code": st,
                                           "message": "injected failure"}, status=st)
         if self._faults and not request.query.get("watch"):
@@ -602,10 +610,19 @@ class FakeCluster:
                 if m == request.method and path in request.path:
                     del self._faults[i]
                     if after:
-                        await handler(request)      # it happened; the reply gets lost
+                        await self._lost_reply(handler, request)
                     return web.json_response({"kind": "Status", "code": st,
                                               "message": "injected failure"}, status=st)
         return await handler(request)
+
+    @staticmethod
+    async def _lost_reply(handler, request: web.Request) -> None:
+        """The request is served (or refused: a conflict, a missing object), and whatever it
+        answered gets lost on the way back."""
+        try:
+            await handler(request)
+        except web.HTTPException:
+            pass
 
     async def _pre(self, req: web.Request) -> None:
         self.request_count += 1

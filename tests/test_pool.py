@@ -162,6 +162,56 @@ def test_failed_claim_whose_patch_took_effect_is_undone():
     asyncio.run(main())
 
 
+def owner_of(lc, name):
+    return (lc.cluster.get("gpu-pool", name)["metadata"].get("annotations") or {}).get(
+        "gpumounter.amd.com/owner-name")
+
+
+def test_claim_of_a_placeholder_taken_meanwhile_never_double_books():
+    """The worker's cache can be behind the apiserver: after a relist an acknowledged claim is
+    not in it yet, and a worker SIGKILLed mid-claim can still have a PATCH in flight. A claim
+    planned on that cache must not overwrite the other claim (bench/configs.py chaos, warm pool
+    2, seed 90: two Pods answered 200 for the same two GPUs). The claim is conditional on the
+    version it was planned on, so it fails, and the one it lost to keeps the placeholder."""
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 1}) as lc:
+            pool = await wait_pool(lc, 1)
+            lc.tenant("a")
+            lc.tenant("b")
+            (ph,) = pool.standby()
+            # b's claim lands at the apiserver; nothing has yielded to the informer since
+            b = lc.cluster.get("default", "b")
+            lc.cluster.patch("gpu-pool", ph.name, {"metadata": {"annotations": {
+                "gpumounter.amd.com/owner-name": "b",
+                "gpumounter.amd.com/owner-uid": b["metadata"]["uid"],
+                "gpumounter.amd.com/mount-mode": "single",
+                "gpumounter.amd.com/attach-id": "add-b"}}})
+            a = lc.cluster.get("default", "a")
+            got = await pool.claim(a, 1, False, [], attach_id="add-a")
+            assert got is None                      # the caller falls back to creating
+            assert owner_of(lc, ph.name) == "b"     # b's claim stands
+    asyncio.run(main())
+
+
+def test_claim_whose_reply_was_lost_is_kept():
+    """A conditional claim whose first attempt applied but whose reply was lost meets a
+    conflict on its retry; the placeholder read back is this attach's own, so the claim
+    stands (no fallback, no placeholder created)."""
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 2}) as lc:
+            await wait_pool(lc, 2)
+            lc.tenant("t")
+            lc.cluster.fail_next("PATCH", 503, count=1, after=True)
+            code, b = await lc.add("default", "t", 1)
+            assert code == 200
+            stages = {t["name"] for t in b["timings"]}
+            assert "pool_claim" in stages and not any(
+                s.endswith("placeholder_wait") for s in stages), stages
+            assert owner_of(lc, b["devices"][0]["placeholder"]) == "t"
+            assert not await lc.audit("default", "t")
+    asyncio.run(main())
+
+
 def test_pick_surplus_returned_to_the_pool_is_no_candidate_for_its_next_owner():
     """A trim/correction pick holds every free GPU with *candidate* placeholders and gives the
     surplus back to the warm pool. Back in the pool they must lose the candidate mark: a
