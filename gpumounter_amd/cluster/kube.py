@@ -220,12 +220,13 @@ class KubeClient:
             raise
 
     async def delete_pod(self, ns: str, name: str, grace_period_s: Optional[int] = None,
-                         uid: str = "") -> Optional[dict]:
+                         uid: str = "", resource_version: str = "") -> Optional[dict]:
         body: Dict[str, Any] = {"kind": "DeleteOptions", "apiVersion": "v1"}
         if grace_period_s is not None:
             body["gracePeriodSeconds"] = int(grace_period_s)
-        if uid:
-            body["preconditions"] = {"uid": uid}
+        pre = {k: v for k, v in (("uid", uid), ("resourceVersion", resource_version)) if v}
+        if pre:
+            body["preconditions"] = pre
         return await self._req("DELETE", self._pods_path(ns, name), body=body)
 
     # ---- resource.k8s.io/v1 (DRA): ResourceClaims and ResourceSlices -----------------------

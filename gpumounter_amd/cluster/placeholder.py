@@ -38,7 +38,7 @@ from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from gpumounter_amd.cluster.informer import PodInformer
-from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
+from gpumounter_amd.cluster.kube import ApiError, Conflict, KubeClient, NotFound
 from gpumounter_amd.cluster.quota import QuotaExceeded
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTAINER, ANN_GROUP,
@@ -54,6 +54,13 @@ LABEL_NODE = "gpumounter.amd.com/node"
 # number of GPUs a placeholder holds (DRA mode: there is no extended-resource limit to read)
 ANN_GPUS = "gpumounter.amd.com/gpus"
 CLAIM_REQUEST = "gpus"
+# warm-pool placeholders (cluster/pool.py) change hands: claimed by a Pod, given back, claimed
+# by another
+STANDBY_PREFIX = "gpumounter-standby-"
+
+
+class Reowned(Exception):
+    """A pool placeholder that changed owner since the caller decided to release it."""
 
 
 class InsufficientGPU(RuntimeError):
@@ -622,6 +629,34 @@ class PlaceholderManager:
                                f"GPU(s), the kubelet reports {len(ids)}")
 
     # ------------------------------------------------------------------------ release
+    async def _delete(self, p: Placeholder) -> Optional[dict]:
+        """DELETE one placeholder. One made for a Pod belongs to it for life; a warm-pool one
+        is deleted only at a version at which it still has the owner the cache shows, so a
+        release decided on a stale cache never takes a GPU from the Pod that claimed it since
+        (raises :class:`Reowned`)."""
+        if not p.name.startswith(STANDBY_PREFIX):
+            return await self.kube.delete_pod(p.namespace, p.name, grace_period_s=0,
+                                              uid=p.uid or "")
+        seen = self.informer.cache.get((p.namespace, p.name))
+        if seen is None or (p.uid and seen["metadata"].get("uid") != p.uid):
+            seen = await self.kube.get_pod(p.namespace, p.name)
+            if p.uid and seen["metadata"].get("uid") != p.uid:
+                raise NotFound(404, f"{p.name}: another pod of that name")
+        owner = (seen["metadata"].get("annotations") or {}).get(ANN_OWNER_UID)
+        rv = seen["metadata"].get("resourceVersion", "")
+        for _ in range(3):
+            try:
+                return await self.kube.delete_pod(p.namespace, p.name, grace_period_s=0,
+                                                  uid=p.uid or "", resource_version=rv)
+            except Conflict:
+                cur = await self.kube.get_pod(p.namespace, p.name)
+                if p.uid and cur["metadata"].get("uid") != p.uid:
+                    raise NotFound(404, f"{p.name}: another pod of that name") from None
+                if (cur["metadata"].get("annotations") or {}).get(ANN_OWNER_UID) != owner:
+                    raise Reowned(p.name) from None
+                rv = cur["metadata"].get("resourceVersion", "")
+        raise ApiError(409, f"{p.name} kept changing while being deleted")
+
     async def release(self, phs: Sequence[Placeholder], wait: bool = True,
                       timeout: Optional[float] = None) -> None:
         if not phs:
@@ -635,11 +670,15 @@ class PlaceholderManager:
             for p in phs:
                 if p.uid:
                     self.tombstones[p.uid] = now
-            res = await asyncio.gather(
-                *[self.kube.delete_pod(p.namespace, p.name, grace_period_s=0, uid=p.uid or "")
-                  for p in phs], return_exceptions=True)
-            failed = []
+            res = await asyncio.gather(*[self._delete(p) for p in phs], return_exceptions=True)
+            failed, reowned = [], []
             for p, r in zip(phs, res):
+                if isinstance(r, Reowned):          # someone else's now: not ours to delete
+                    _log.info("placeholder %s/%s changed owner; left to it", p.namespace, p.name)
+                    reowned.append(p)
+                    if p.uid:
+                        self.tombstones.pop(p.uid, None)
+                    continue
                 if isinstance(r, Exception) and not isinstance(r, NotFound):
                     _log.error("delete placeholder %s/%s: %s", p.namespace, p.name, r)
                     failed.append(p)
@@ -658,7 +697,8 @@ class PlaceholderManager:
             if self.dra:
                 # the claims hold no device once their Pod is gone (deallocated when
                 # reservedFor empties); deleting them is cleanup, off the critical path
-                gone = [(p.namespace, p.name) for p in phs if p not in failed]
+                gone = [(p.namespace, p.name) for p in phs
+                        if p not in failed and p not in reowned]
                 if gone:
                     t = asyncio.get_running_loop().create_task(self._delete_claims(gone))
                     self._bg.add(t)
@@ -669,7 +709,7 @@ class PlaceholderManager:
             self.faults.check("ledger_release", "after")
             if not wait:
                 return
-            keys = {(p.namespace, p.name): p.uid for p in phs}
+            keys = {(p.namespace, p.name): p.uid for p in phs if p not in reowned}
 
             def gone():
                 for (ns, name), uid in keys.items():

@@ -21,11 +21,11 @@ from __future__ import annotations
 import asyncio
 import secrets
 import time
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from gpumounter_amd.cluster.kube import Conflict, NotFound
-from gpumounter_amd.cluster.placeholder import (ANN_GPUS, InsufficientGPU, LABEL_NODE,
-                                                Placeholder,
+from gpumounter_amd.cluster.placeholder import (ANN_GPUS, STANDBY_PREFIX, InsufficientGPU,
+                                                LABEL_NODE, Placeholder,
                                                 PlaceholderManager, Reservation,
                                                 _label_value)
 from gpumounter_amd.hw import topology
@@ -43,6 +43,10 @@ _log = log.get("cluster.pool")
 
 class ClaimTaken(Exception):
     """The standby placeholder was claimed (or deleted) by someone else since it was chosen."""
+
+
+def _owner_uid(p: dict) -> Optional[str]:
+    return (p["metadata"].get("annotations") or {}).get(ANN_OWNER_UID)
 
 
 def is_standby(p: dict) -> bool:
@@ -96,7 +100,7 @@ class WarmPool:
 
     # ------------------------------------------------------------------------ refill
     def standby_body(self) -> dict:
-        name = f"gpumounter-standby-{_label_value(self.ph.node)[:40]}-{secrets.token_hex(4)}"
+        name = f"{STANDBY_PREFIX}{_label_value(self.ph.node)[:40]}-{secrets.token_hex(4)}"
         body = self.ph.build({"metadata": {"name": "standby", "namespace": "", "uid": ""}},
                              1, MODE_STANDBY)
         md = body["metadata"]
@@ -330,36 +334,27 @@ class WarmPool:
 
     async def _unclaim(self, phs: Sequence[Placeholder], attach_id: str
                        ) -> Tuple[List[Placeholder], List[Placeholder]]:
-        """Undo a failed claim: put back into the pool each placeholder this attach claimed (at
-        the version just read, so a claim made since by someone else is never undone). Returns
-        (free again, not this attach's to undo); the rest could not be read or put back."""
-        back: List[Placeholder] = []
-        theirs: List[Placeholder] = []
+        """Undo a failed claim: put back into the pool each placeholder this attach claimed.
+        Returns (free again, not this attach's to undo); the rest could not be read or put
+        back."""
+        res = await asyncio.gather(*[self._put_back(ph, lambda cur: self._mine(cur, attach_id))
+                                     for ph in phs], return_exceptions=True)
+        return self._sort_back(phs, res)
 
-        async def one(ph: Placeholder) -> None:
-            for _ in range(3):
-                try:
-                    cur = await self.ph.kube.get_pod(ph.namespace, ph.name)
-                except NotFound:
-                    theirs.append(ph)                   # gone: nothing left to undo
-                    return
-                if cur["metadata"].get("uid") != ph.uid or not self._mine(cur, attach_id):
-                    (back if self._claimable(cur, ph) else theirs).append(ph)
-                    return
-                got = await self._standby_patch([ph], cur["metadata"]["resourceVersion"])
-                if got:
-                    back.append(ph)
-                    return
-
-        res = await asyncio.gather(*[one(ph) for ph in phs], return_exceptions=True)
+    def _sort_back(self, phs, res) -> Tuple[List[Placeholder], List[Placeholder]]:
+        back, theirs = [], []
         for ph, r in zip(phs, res):
-            if isinstance(r, Exception):
+            if r is True:
+                back.append(ph)
+            elif r is False:
+                theirs.append(ph)
+            else:
                 _log.error("return %s/%s to pool: %s", ph.namespace, ph.name, r)
         return back, theirs
 
-    async def _standby_patch(self, phs: Sequence[Placeholder],
-                             rv: Optional[str] = None) -> List[Placeholder]:
-        patch = {"metadata": {
+    @staticmethod
+    def _standby_patch(rv: Optional[str]) -> dict:
+        return {"metadata": {
             "labels": {LABEL_OWNER: None, LABEL_OWNER_NS: None},
             "annotations": {ANN_OWNER_UID: None, ANN_OWNER_NAME: None,
                             ANN_MOUNT_MODE: MODE_STANDBY, ANN_ATTACH_ID: None,
@@ -367,31 +362,59 @@ class WarmPool:
                             # surplus of a trim/correction pick comes back as candidates: a
                             # claimed one still marked would be invisible to its new owner's
                             # ledger view, and released under it as an abandoned pick
-                            ANN_CANDIDATE: None}}}
-        if rv:                                  # only at the version the caller read
-            patch["metadata"]["resourceVersion"] = rv
-        epoch = self.ph.informer.epoch
-        res = await asyncio.gather(*[self.ph.kube.patch_pod(p.namespace, p.name, patch)
-                                     for p in phs], return_exceptions=True)
-        back = []
-        for p, r in zip(phs, res):
-            if isinstance(r, dict):
-                self.ph.informer.upsert(r, epoch)
-                back.append(p)
-            elif not isinstance(r, (NotFound, Conflict)):
-                _log.error("return %s/%s to pool: %s", p.namespace, p.name, r)
-        return back
+                            ANN_CANDIDATE: None},
+            # only at a version read while the placeholder was still the caller's
+            "resourceVersion": rv}}
+
+    async def _put_back(self, ph: Placeholder, ours: Callable[[dict], bool],
+                        rv: Optional[str] = None) -> bool:
+        """Return one placeholder to the pool with a merge patch conditional on a version at
+        which it was still ``ours``, so one that someone else has claimed since is never taken
+        from them. True: standby now; False: not ours (left alone). Raises when it could not
+        be read or written."""
+        for _ in range(3):
+            if not rv:
+                try:
+                    cur = await self.ph.kube.get_pod(ph.namespace, ph.name)
+                except NotFound:
+                    return False                        # gone: nothing left to return
+                if cur["metadata"].get("uid") != ph.uid or not ours(cur):
+                    return self._claimable(cur, ph)     # already standby counts as back
+                rv = cur["metadata"]["resourceVersion"]
+            epoch = self.ph.informer.epoch
+            try:
+                r = await self.ph.kube.patch_pod(ph.namespace, ph.name, self._standby_patch(rv))
+            except NotFound:
+                return False
+            except Conflict:
+                rv = None                               # changed since: read it again
+                continue
+            self.ph.informer.upsert(r, epoch)
+            return True
+        raise Conflict(409, f"{ph.name} kept changing while being returned to the pool")
 
     async def give_back(self, phs: Sequence[Placeholder]) -> None:
-        """Return detached placeholders to the pool (up to ``target``); delete the rest."""
+        """Return detached placeholders to the pool (up to ``target``); delete the rest. Each
+        goes back at the version the worker's cache holds, as long as it still has the owner
+        the cache shows (one put back and claimed anew meanwhile stays with its new owner)."""
         async with self._lock:
             # standby being admitted count too, or a refill racing a give-back overfills
             room = max(self.target - len(self.standby()) - self.pending() - self._creating, 0)
             keep = [p for p in phs if p.device_ids and len(p.device_ids) == 1][:room]
             drop = [p for p in phs if p not in keep]
+            cache = {p["metadata"]["uid"]: p for p in self.ph.live()}
+
+            def put(ph: Placeholder):
+                seen = cache.get(ph.uid)
+                if seen is None:
+                    return self._put_back(ph, lambda cur: not is_standby(cur))
+                owner = _owner_uid(seen)
+                return self._put_back(ph, lambda cur: _owner_uid(cur) == owner,
+                                      seen["metadata"].get("resourceVersion"))
             with trace.span("pool_return", placeholders=len(keep)):
-                back = await self._standby_patch(keep)
-            drop += [p for p in keep if p not in back]
+                res = await asyncio.gather(*[put(ph) for ph in keep], return_exceptions=True)
+            back, theirs = self._sort_back(keep, res)
+            drop += [p for p in keep if p not in back and p not in theirs]
         if drop:
             await self.ph.release(drop, wait=False)
         self.poke()

@@ -433,13 +433,17 @@ class FakeCluster:
         return pod
 
     def delete(self, ns: str, name: str, grace: Optional[int] = None,
-               uid_precondition: str = "") -> Optional[dict]:
+               uid_precondition: str = "", rv_precondition: str = "") -> Optional[dict]:
         pod = self.pods.get((ns, name))
         if pod is None:
             return None
         if uid_precondition and pod["metadata"]["uid"] != uid_precondition:
             raise web.HTTPConflict(text=json.dumps({"kind": "Status", "message": "uid mismatch"}),
                                    content_type="application/json")
+        if rv_precondition and pod["metadata"].get("resourceVersion") != rv_precondition:
+            raise web.HTTPConflict(text=json.dumps({
+                "kind": "Status", "message": "resourceVersion mismatch"}),
+                content_type="application/json")
         if grace is None:
             grace = int(pod["spec"].get("terminationGracePeriodSeconds", 30))
         md = pod["metadata"]
@@ -733,7 +737,7 @@ class FakeCluster:
         await self._pre(req)
         ns, name = req.match_info["ns"], req.match_info["name"]
         grace = None
-        uid = ""
+        uid = rv = ""
         if req.can_read_body:
             try:
                 opts = await req.json()
@@ -742,9 +746,10 @@ class FakeCluster:
             if opts.get("gracePeriodSeconds") is not None:
                 grace = int(opts["gracePeriodSeconds"])
             uid = (opts.get("preconditions") or {}).get("uid", "")
+            rv = (opts.get("preconditions") or {}).get("resourceVersion", "")
         if "gracePeriodSeconds" in req.query:
             grace = int(req.query["gracePeriodSeconds"])
-        pod = self.delete(ns, name, grace, uid)
+        pod = self.delete(ns, name, grace, uid, rv)
         if pod is None:
             return self._not_found(ns, name)
         return web.json_response(pod)

@@ -3,6 +3,8 @@ detaches hand GPUs back, entire mounts keep all-or-nothing semantics, the ledger
 import asyncio
 import time
 
+import pytest
+
 from gpumounter_amd.cluster.pool import is_standby
 from gpumounter_amd.fakes.apiserver import LatencyModel
 from gpumounter_amd.fakes.harness import LocalCluster
@@ -190,6 +192,33 @@ def test_claim_of_a_placeholder_taken_meanwhile_never_double_books():
             got = await pool.claim(a, 1, False, [], attach_id="add-a")
             assert got is None                      # the caller falls back to creating
             assert owner_of(lc, ph.name) == "b"     # b's claim stands
+    asyncio.run(main())
+
+
+@pytest.mark.parametrize("room", [False, True], ids=["pool-full-delete", "pool-room-patch"])
+def test_give_back_leaves_a_placeholder_claimed_anew_with_its_new_owner(room):
+    """A give-back planned on a stale cache (the placeholder already went back to the pool and
+    was claimed by another Pod) must not take it from that Pod: neither put it back into the
+    pool (room in the pool) nor delete it (pool full)."""
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 1}) as lc:
+            pool = await wait_pool(lc, 1)
+            svc = lc.nodes["node-0"].worker.service
+            lc.tenant("a")
+            lc.tenant("b")
+            code, _ = await lc.add("default", "a", 1)
+            assert code == 200
+            (p,) = svc.ph.owned_by(lc.cluster.get("default", "a"))
+            ph = svc.ph.cached(p)
+            b = lc.cluster.get("default", "b")
+            lc.cluster.patch("gpu-pool", ph.name, {"metadata": {"annotations": {
+                "gpumounter.amd.com/owner-name": "b",
+                "gpumounter.amd.com/owner-uid": b["metadata"]["uid"],
+                "gpumounter.amd.com/attach-id": "add-b"}}})
+            if room:
+                pool.target = 3
+            await pool.give_back([ph])
+            assert owner_of(lc, ph.name) == "b"
     asyncio.run(main())
 
 
