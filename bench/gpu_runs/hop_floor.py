@@ -10,6 +10,7 @@ process and a grpc.aio client, one call at a time, median round trip minus the h
 --retry   the master's channel options (retries enabled, AddGPU retry policy, keepalive)
 --big     a response the size of a real attach's (20 stage timings, one device)
 --shield  the worker's handler shape: the operation as its own task, awaited through shield
+--sync    the client: a synchronous grpc stub called from a thread (run_in_executor)
 Prints one JSON line."""
 import argparse
 import asyncio
@@ -28,6 +29,30 @@ import grpc  # noqa: E402
 from aiohttp import web  # noqa: E402
 
 from gpumounter_amd.api import gpu_mount as api  # noqa: E402
+
+
+class Spin:
+    """Keeps the event loop from blocking in epoll while work is in flight (and ``tail_s``
+    after), so a completion signalled by another thread needs no wake-up of this one."""
+    def __init__(self, tail_s=0.0003):
+        self.n, self.until, self.tail, self.loop = 0, 0.0, tail_s, None
+
+    def _tick(self):
+        if self.n or time.perf_counter() < self.until:
+            self.loop.call_soon(self._tick)
+        else:
+            self.on = False
+
+    def __enter__(self):
+        self.loop = asyncio.get_running_loop()
+        self.n += 1
+        if not getattr(self, "on", False):
+            self.on = True
+            self.loop.call_soon(self._tick)
+
+    def __exit__(self, *a):
+        self.n -= 1
+        self.until = time.perf_counter() + self.tail
 
 
 def rd(p):
@@ -51,6 +76,8 @@ def server_main(args, q):
 
         async def op(req):
             t0 = time.perf_counter()
+            if args.sleep:
+                await asyncio.sleep(args.sleep)
             if args.http:
                 for _ in range(3):
                     async with sess.post(f"http://127.0.0.1:{hport}/x", json={"a": 1}) as resp:
@@ -66,7 +93,14 @@ def server_main(args, q):
             resp.total_ms = (time.perf_counter() - t0) * 1e3
             return resp
 
+        spin = Spin()
+
         async def add(req, ctx):
+            if args.spin:
+                with spin:
+                    if args.shield:
+                        return await asyncio.shield(asyncio.ensure_future(op(req)))
+                    return await op(req)
             if args.shield:
                 t = asyncio.ensure_future(op(req))
                 return await asyncio.shield(t)
@@ -97,32 +131,51 @@ async def client(args, port, pki, n):
         from gpumounter_amd.master.app import _SERVICE_CONFIG
         opts = [("grpc.keepalive_time_ms", 30000), ("grpc.enable_retries", 1),
                 ("grpc.service_config", _SERVICE_CONFIG)]
+    mod = grpc if args.sync else grpc.aio
     if args.tls:
         creds = grpc.ssl_channel_credentials(rd(pki["ca"]), rd(pki["master.key"]),
                                              rd(pki["master.crt"]))
         opts.append(("grpc.ssl_target_name_override", "gpu-mounter-worker"))
-        ch = grpc.aio.secure_channel(f"127.0.0.1:{port}", creds, options=opts)
+        ch = mod.secure_channel(f"127.0.0.1:{port}", creds, options=opts)
     else:
-        ch = grpc.aio.insecure_channel(f"127.0.0.1:{port}", options=opts)
+        ch = mod.insecure_channel(f"127.0.0.1:{port}", options=opts)
     stub = ch.unary_unary(api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
                           response_deserializer=api.AddGPUResponse.FromString)
+    loop = asyncio.get_running_loop()
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(1)
+
+    spin = Spin(0.0)
+
+    async def call(req):
+        if args.spin:
+            with spin:
+                return await stub(req, timeout=10)
+        if args.sync:
+            return await loop.run_in_executor(pool, lambda: stub(req, timeout=10))
+        return await stub(req, timeout=10)
     ts, inner = [], []
     for _ in range(n):
         t = time.perf_counter()
-        r = await stub(api.AddGPURequest(pod_name="t", namespace="default", gpu_num=1,
+        r = await call(api.AddGPURequest(pod_name="t", namespace="default", gpu_num=1,
                                          request_id="add-0123456789ab",
-                                         idempotency_key="add-0123456789ab"), timeout=10)
+                                         idempotency_key="add-0123456789ab"))
         ts.append((time.perf_counter() - t) * 1e6)
         inner.append(r.total_ms * 1e3)
-    await ch.close()
+    if args.sync:
+        ch.close()
+    else:
+        await ch.close()
     return statistics.median(ts[n // 10:]), statistics.median(inner[n // 10:])
 
 
 def main():
     ap = argparse.ArgumentParser()
-    for f in ("http", "tls", "retry", "big", "shield"):
+    for f in ("http", "tls", "retry", "big", "shield", "sync", "spin"):
         ap.add_argument(f"--{f}", action="store_true")
     ap.add_argument("-n", type=int, default=1500)
+    ap.add_argument("--sleep", type=float, default=0.0,
+                    help="the handler sleeps this long (s) instead of / before its I/O")
     args = ap.parse_args()
     q = mp.Queue()
     p = mp.Process(target=server_main, args=(args, q), daemon=True)
@@ -132,7 +185,7 @@ def main():
         rtt, inner = asyncio.run(client(args, port, pki, args.n))
     finally:
         p.kill()
-    print(json.dumps({"opts": [f for f in ("http", "tls", "retry", "big", "shield")
+    print(json.dumps({"opts": [f for f in ("http", "tls", "retry", "big", "shield", "sync", "spin")
                                if getattr(args, f)],
                       "rtt_us": round(rtt), "handler_us": round(inner),
                       "transport_us": round(rtt - inner)}))

@@ -32,6 +32,7 @@ from gpumounter_amd.models import pod as podu
 from gpumounter_amd.master.authz import Authorizer
 from gpumounter_amd.utils import log, runtime, trace
 from gpumounter_amd.utils.metrics import Metrics
+from gpumounter_amd.utils.spin import LoopSpinner
 
 _log = log.get("master")
 
@@ -163,6 +164,8 @@ class Master:
                                        cfg.worker_port, cfg)
         self.metrics = Metrics()
         self.authz = Authorizer(cfg, self.kube)
+        self.spin = LoopSpinner(getattr(cfg, "loop_spin_us", 0.0),
+                                getattr(cfg, "loop_spin_max_ms", 20.0))
         self.runner: Optional[web.AppRunner] = None
         self.port = 0
         self._pod_nodes: Dict[Tuple[str, str], Tuple[str, str, float]] = {}
@@ -416,7 +419,7 @@ class Master:
     # ------------------------------------------------------------------------ HTTP routes
     async def add_gpu(self, request: web.Request) -> web.Response:
         # gm:master_* roctx ranges; the stage split is returned as ``master_timings``
-        with trace.span("master_addgpu") as root:
+        with self.spin.hold(), trace.span("master_addgpu") as root:
             return await self._add_gpu(request, root)
 
     async def _add_gpu(self, request: web.Request, root: trace.Span) -> web.Response:
@@ -451,7 +454,7 @@ class Master:
         return self._reply(request, route, status, text, self._stamp(payload, root))
 
     async def remove_gpu(self, request: web.Request) -> web.Response:
-        with trace.span("master_removegpu") as root:
+        with self.spin.hold(), trace.span("master_removegpu") as root:
             return await self._remove_gpu(request, root)
 
     async def _remove_gpu(self, request: web.Request, root: trace.Span) -> web.Response:

@@ -173,6 +173,11 @@ class Config:
     attach_timeout_s: float = 120.0    # placeholder admission deadline
     detach_timeout_s: float = 60.0     # wait for placeholder deletion where waited for
     rpc_timeout_s: float = 180.0       # master→worker gRPC deadline (reference: none)
+    # keep the event loop polling (no blocking epoll_wait) while an add/remove request is in
+    # flight and this long after it answered (utils/spin.py): saves the thread wake-ups of its
+    # waits, for one busy core during the request (0 = off)
+    loop_spin_us: float = 0.0
+    loop_spin_max_ms: float = 20.0     # longest stretch of polling; then the loop blocks again
     reconcile_period_s: float = 30.0   # full reconciler sweep period
     # every this many seconds, compare each hot container's device-control state (v2: the
     # attached BPF program ids; v1: devices.list) with what gpumounter last installed, and

@@ -36,6 +36,7 @@ from gpumounter_amd.node.ledger import LedgerClient
 from gpumounter_amd.utils import log, runtime
 from gpumounter_amd.utils.faults import FaultInjector
 from gpumounter_amd.utils.metrics import Metrics
+from gpumounter_amd.utils.spin import LoopSpinner
 from gpumounter_amd.worker.reconciler import Reconciler
 from gpumounter_amd.worker.service import GpuMountService, RpcError
 
@@ -136,6 +137,7 @@ class Worker:
             self.reconciler.watch_events()
         self.grpc_server: Optional[grpc.aio.Server] = None
         self._ops: set = set()          # RPC operations running (see _wrap)
+        self.spin = LoopSpinner(cfg.loop_spin_us, cfg.loop_spin_max_ms)
         self.http_runner: Optional[web.AppRunner] = None
         self.grpc_port = 0
         self.http_port = 0
@@ -154,8 +156,14 @@ class Worker:
                for v in auth.get(k, [])}
         return bool(got & names)
 
-    def _wrap(self, fn):
+    def _wrap(self, fn, spin: bool = True):
         async def handler(request, context):
+            if spin:
+                with self.spin.hold():
+                    return await served(request, context)
+            return await served(request, context)
+
+        async def served(request, context):
             t_in = time.perf_counter()
             if not self._peer_allowed(context):
                 await context.abort(grpc.StatusCode.PERMISSION_DENIED,
@@ -229,7 +237,7 @@ class Worker:
                     api.RemoveGPURequest.FromString, _ser)}),
             grpc.method_handlers_generic_handler("gpu_mount.NodeService", {
                 "GetNodeStatus": grpc.unary_unary_rpc_method_handler(
-                    self._wrap(self._status), api.NodeStatusRequest.FromString, _ser)}),
+                    self._wrap(self._status, spin=False), api.NodeStatusRequest.FromString, _ser)}),
         )
 
     # ------------------------------------------------------------------------ lifecycle
