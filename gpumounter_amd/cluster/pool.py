@@ -32,7 +32,7 @@ from gpumounter_amd.hw import topology
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu, normalize_device_id
 from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTAINER, ANN_GROUP,
-                                         ANN_IDEMPOTENCY, ANN_MOUNT_MODE,
+                                         ANN_IDEMPOTENCY, ANN_LEASE, ANN_MOUNT_MODE,
                                          ANN_OWNER_NAME, ANN_OWNER_UID, LABEL_APP,
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          MODE_STANDBY)
@@ -249,7 +249,8 @@ class WarmPool:
                                 ANN_OWNER_NAME: podu.name_of(owner), ANN_MOUNT_MODE: mode,
                                 ANN_ATTACH_ID: attach_id, ANN_CONTAINER: container,
                                 ANN_IDEMPOTENCY: idempotency_key or None,
-                                ANN_GROUP: group or None, ANN_CANDIDATE: None}}}
+                                ANN_GROUP: group or None, ANN_CANDIDATE: None,
+                                ANN_LEASE: None}}}
             for ph in chosen:
                 self._claimed.add(ph.uid)
             seen = self._versions()
@@ -362,7 +363,9 @@ class WarmPool:
                             # surplus of a trim/correction pick comes back as candidates: a
                             # claimed one still marked would be invisible to its new owner's
                             # ledger view, and released under it as an abandoned pick
-                            ANN_CANDIDATE: None},
+                            ANN_CANDIDATE: None,
+                            # an earlier owner's lease would expire the next owner's GPU
+                            ANN_LEASE: None},
             # only at a version read while the placeholder was still the caller's
             "resourceVersion": rv}}
 

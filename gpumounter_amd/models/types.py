@@ -43,6 +43,8 @@ ANN_DEVICES = "gpumounter.amd.com/devices"
 ANN_OWNER_NAME = "gpumounter.amd.com/owner-name"
 ANN_IDEMPOTENCY = "gpumounter.amd.com/idempotency-key"
 ANN_GROUP = "gpumounter.amd.com/group"      # entire-mount group made of pooled placeholders
+# a ?lease= attach's expiry (Unix seconds) on its placeholders (worker/lease.py)
+ANN_LEASE = "gpumounter.amd.com/lease-expires"
 MODE_STANDBY = "standby"
 # set on the 1-GPU placeholders a trim or placement correction holds while it picks; cleared on
 # the kept ones before they are mounted. A worker that dies mid-pick leaves only candidates

@@ -18,12 +18,12 @@ from typing import Dict, List, Optional, Tuple
 
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import LABEL_OWNER_NS, MountType
+from gpumounter_amd.models.types import ANN_LEASE, ANN_OWNER_UID, LABEL_OWNER_NS, MountType
 from gpumounter_amd.node.ledger import LedgerError
 from gpumounter_amd.utils import log
 
 _log = log.get("worker.lease")
-ANN_LEASE = "gpumounter.amd.com/lease-expires"
+__all__ = ["ANN_LEASE", "LeaseKeeper", "expires_of"]
 
 
 def expires_of(ph: dict) -> Optional[float]:
@@ -43,9 +43,10 @@ class LeaseKeeper:
         self._retry_timers: Dict[Tuple[str, str], asyncio.TimerHandle] = {}
         self._errors: Dict[Tuple[str, str], int] = {}          # owner → failed expiries in a row
         self._tasks: set = set()                               # running expiries
-        # placeholder uid → expiry this worker granted: the informer learns the annotation only
-        # from the watch echo of our PATCH, which can lag (a dropped stream, a relist)
-        self._granted: Dict[str, float] = {}
+        # placeholder uid → (expiry this worker granted, owner pod uid): the informer learns the
+        # annotation only from the watch echo of our PATCH, which can lag (a dropped stream, a
+        # relist). A warm-pool placeholder changes owner, so the grant holds for its owner only
+        self._granted: Dict[str, Tuple[float, str]] = {}
         self._stopped = False
         self.expired = 0
 
@@ -63,7 +64,7 @@ class LeaseKeeper:
                 informer.upsert(r, epoch)    # visible to expire_owner before the watch echo
         for p in placeholders:
             if p.uid:
-                self._granted[p.uid] = expires
+                self._granted[p.uid] = (expires, podu.uid_of(pod))
             self._arm(p.uid, podu.ns_of(pod), podu.name_of(pod), expires)
         return expires
 
@@ -145,9 +146,12 @@ class LeaseKeeper:
         now = time.time()
         due: Dict[Tuple[str, str], List[dict]] = {}
         live = self.svc.ph.live()
-        uids = {p["metadata"].get("uid") for p in live}
-        for uid in [u for u in self._granted if u not in uids]:
-            del self._granted[uid]          # released some other way (RemoveGPU, owner gone)
+        owners = {p["metadata"].get("uid"): (p["metadata"].get("annotations") or {}).get(
+            ANN_OWNER_UID) for p in live}
+        for uid in [u for u, (_, o) in self._granted.items()
+                    if u not in owners or owners[u] != o]:
+            del self._granted[uid]          # released some other way (RemoveGPU, owner gone,
+            #                                 back in the warm pool)
         for p in live:
             exp = expires_of(p)
             if exp is None:
@@ -192,7 +196,8 @@ class LeaseKeeper:
             raw = raws.get(ph.name)
             exp = expires_of(raw) if raw is not None else None
             if exp is None:
-                exp = self._granted.get(ph.uid)
+                g = self._granted.get(ph.uid)
+                exp = g[0] if g is not None and g[1] == podu.uid_of(pod) else None
             if exp is None:
                 continue
             if exp <= now + 0.001:

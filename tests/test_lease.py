@@ -210,3 +210,35 @@ def test_a_lease_whose_watch_echo_lags_still_expires():
             return not st.hot
         assert await until(gone, timeout=3.0), "the lease was lost"
     run(body)                  # LocalCluster runs no periodic sweep
+
+
+def test_a_pool_placeholder_does_not_carry_its_last_owners_lease():
+    """Warm pool: a leased GPU removed before its expiry goes back to the pool, and the next Pod
+    claims that very placeholder. The earlier owner's lease (the annotation, the grant the
+    worker remembers) must not expire the new owner's GPU."""
+    async def body(lc):
+        w = lc.nodes["node-0"].worker
+        svc = w.service
+        pool = w.pool
+        for _ in range(250):
+            if len(pool.standby()) == 1:
+                break
+            await asyncio.sleep(0.02)
+        lc.tenant("a")
+        lc.tenant("b")
+        code, a = await lease_add(lc, "default", "a", 1, 0.4)
+        assert code == 200
+        ph, idx = a["devices"][0]["placeholder"], a["devices"][0]["index"]
+        pool.target = 2                          # room for it back in the pool
+        code, _ = await lc.remove("default", "a", [a["devices"][0]["uuid"]])
+        assert code == 200
+        got = await pool.claim(lc.cluster.get("default", "b"), 1, False, [],
+                               attach_id="add-b", want=[idx])
+        assert got is not None and got.placeholders[0].name == ph     # the same placeholder
+        await asyncio.sleep(0.6)                 # a's lease would be over by now
+        await svc.lease.sweep()
+        await asyncio.sleep(0.1)
+        owner = (lc.cluster.get("gpu-pool", ph)["metadata"].get("annotations") or {}).get(
+            "gpumounter.amd.com/owner-name")
+        assert owner == "b" and svc.lease.expired == 0
+    run(body, worker_overrides={"warm_pool_size": 1})
