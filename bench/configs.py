@@ -565,6 +565,13 @@ def chaos(args) -> dict:
                                     if x.get("source") == "hot-mount"}
                         leases[t] = {u: e for u, e in leases[t].items()
                                      if held_now.get(u) == e[2]}
+                        # a leased attach whose answer was lost: its lease is on the ledger
+                        for x in g.get("gpus", []):
+                            exp = x.get("lease_expires")
+                            if x.get("source") == "hot-mount" and exp and \
+                                    x["uuid"] not in leases[t]:
+                                at = time.monotonic() + (exp - time.time())
+                                leases[t][x["uuid"]] = (at, at, x.get("pod_name"))
                         certain[t] = True
                 if args.api_fault_rate:
                     pc.api_faults(args.api_fault_rate, args.seed * 1000 + rnd_i)

@@ -620,10 +620,12 @@ class Master:
             return web.json_response({"error": f"worker on {podu.node_of(pod)}: "
                                                f"{e.code().name} {e.details()}"}, status=502)
         uid = podu.uid_of(pod)
-        held = {(p["namespace"], p["name"]) for p in st.get("placeholders", [])
+        held = {(p["namespace"], p["name"]): p.get("lease_expires")
+                for p in st.get("placeholders", [])
                 if p["owner"] == name and p["owner_namespace"] == ns and p["owner_uid"] == uid}
-        hot = [dict(g, source="hot-mount") for g in st["gpus"]
-               if (g.get("namespace"), g.get("pod_name")) in held]
+        hot = [dict(g, source="hot-mount",
+                    lease_expires=held[(g.get("namespace"), g.get("pod_name"))])
+               for g in st["gpus"] if (g.get("namespace"), g.get("pod_name")) in held]
         own = [dict(g, source="pod-spec") for g in st["gpus"]
                if (g.get("namespace"), g.get("pod_name")) == (ns, name)]
         return web.json_response({"pod": f"{ns}/{name}", "node": podu.node_of(pod),

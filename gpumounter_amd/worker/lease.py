@@ -39,10 +39,14 @@ class LeaseKeeper:
         self.svc = service
         # placeholder uid → (timer, the expiry it was armed for)
         self._timers: Dict[str, Tuple[asyncio.TimerHandle, float]] = {}
-        self._retry_after: Dict[Tuple[str, str], float] = {}   # owner → not before
+        # placeholder uid → not before: a lease whose GPUs were busy at expiry (lease_force off)
+        # is retried every lease_retry_s. Per placeholder: a later lease of the same owner is
+        # not held back by it
+        self._retry_after: Dict[str, float] = {}
         self._retry_timers: Dict[Tuple[str, str], asyncio.TimerHandle] = {}
         self._errors: Dict[Tuple[str, str], int] = {}          # owner → failed expiries in a row
         self._tasks: set = set()                               # running expiries
+        self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}  # owner → its expiries in turn
         # placeholder uid → (expiry this worker granted, owner pod uid): the informer learns the
         # annotation only from the watch echo of our PATCH, which can lag (a dropped stream, a
         # relist). A warm-pool placeholder changes owner, so the grant holds for its owner only
@@ -102,8 +106,12 @@ class LeaseKeeper:
     ERROR_RETRY_S = (0.1, 0.5, 2.0)
 
     async def _expire_or_retry(self, ns: str, name: str) -> None:
+        # one expiry per owner at a time: the timers of an attach's placeholders fire together,
+        # and a second expiry racing the first would find its GPUs gone (GPUNotFound)
+        lock = self._locks.setdefault((ns, name), asyncio.Lock())
         try:
-            await self.expire_owner(ns, name)
+            async with lock:
+                await self.expire_owner(ns, name)
             self._errors.pop((ns, name), None)
         except asyncio.CancelledError:
             raise
@@ -152,6 +160,10 @@ class LeaseKeeper:
                     if u not in owners or owners[u] != o]:
             del self._granted[uid]          # released some other way (RemoveGPU, owner gone,
             #                                 back in the warm pool)
+        for uid in [u for u in self._retry_after if u not in owners]:
+            del self._retry_after[uid]
+        for key in [k for k, lk in self._locks.items() if not lk.locked()]:
+            del self._locks[key]
         for p in live:
             exp = expires_of(p)
             if exp is None:
@@ -172,8 +184,6 @@ class LeaseKeeper:
 
     async def expire_owner(self, ns: str, name: str) -> None:
         svc = self.svc
-        if time.time() < self._retry_after.get((ns, name), 0):
-            return
         pod = await svc.get_pod(ns, name, fresh=True)
         if pod is None:
             return                          # the owner-gone GC releases its placeholders
@@ -201,6 +211,8 @@ class LeaseKeeper:
             if exp is None:
                 continue
             if exp <= now + 0.001:
+                if now + 0.05 < self._retry_after.get(ph.uid, 0):
+                    continue                # busy at its last expiry: its retry timer runs
                 due.append(ph.uid)
                 uuids += [g.uuid for g in st.by_placeholder[(ph.namespace, ph.name)]]
                 t = self._timers.pop(ph.uid, None)
@@ -218,16 +230,23 @@ class LeaseKeeper:
         if resp.remove_gpu_result == api.REMOVE_SUCCESS:
             for uid in due:
                 self._granted.pop(uid, None)
+                self._retry_after.pop(uid, None)
             self.expired += 1
-            self._retry_after.pop((ns, name), None)
             svc.notify.event(pod, "GPULeaseExpired",
                              f"lease over: {len(uuids)} GPU(s) detached"
                              + (f", processes {list(resp.killed_pids)} signalled"
                                 if resp.killed_pids else ""))
             log.kv(_log, 20, "lease expired", pod=f"{ns}/{name}", gpus=len(uuids))
             return
+        if resp.remove_gpu_result != api.REMOVE_BUSY:
+            # some of them went meanwhile (a client's RemoveGPU, the Pod deleted): read the
+            # ledger again shortly (the error path's 0.1/0.5/2 s retries) for what is left
+            raise LedgerError(
+                f"lease expiry of {ns}/{name}: "
+                f"{api.RemoveGPUResponse.RemoveGPUResult.Name(resp.remove_gpu_result)}")
         retry = svc.cfg.lease_retry_s
-        self._retry_after[(ns, name)] = time.time() + retry
+        for uid in due:
+            self._retry_after[uid] = time.time() + retry
         svc.notify.event(pod, "GPULeaseExpired",
                          f"lease over but the GPUs are still in use "
                          f"({api.RemoveGPUResponse.RemoveGPUResult.Name(resp.remove_gpu_result)}"

@@ -14,6 +14,7 @@ from gpumounter_amd.hw import topology
 from gpumounter_amd.models.device import gpus_by_key, normalize_device_id
 from gpumounter_amd.node.ledger import LedgerError
 from gpumounter_amd.utils import log
+from gpumounter_amd.worker.lease import expires_of
 
 _log = log.get("worker.status")
 
@@ -46,6 +47,8 @@ async def node_status(svc, include_processes: bool) -> dict:
                         "gpumounter.amd.com/owner-namespace", ""),
                     "owner_uid": ann.get("gpumounter.amd.com/owner-uid", ""),
                     "mode": ann.get("gpumounter.amd.com/mount-mode", ""),
+                    # a ?lease= attach's end (Unix seconds), None without a lease
+                    "lease_expires": expires_of(p),
                     "device_ids": list(ids)})
     out = {"node": svc.cfg.node_name,
            "gpus": [dict(g.to_dict(), healthy=g.index not in svc.unhealthy) for g in gpus],

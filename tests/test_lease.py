@@ -106,6 +106,42 @@ def test_expired_lease_on_a_busy_gpu_is_kept_unless_forced(tmp_path):
             sleeper.kill()
 
 
+def test_a_busy_expired_lease_does_not_hold_back_the_owners_next_lease(tmp_path):
+    """An expired lease whose GPU is busy is retried every lease_retry_s. That retry gate is
+    the busy placeholder's: a second lease of the same Pod on another GPU still ends on time
+    (it used to wait for the whole retry period, found by chaos with the warm pool and leases:
+    a concurrent RemoveGPU made an expiry answer GPU_NOT_FOUND and gated the owner)."""
+    sleeper = subprocess.Popen(["sleep", "60"])
+    procs = tmp_path / "procs"
+    try:
+        async def body(lc):
+            _native.mock_smi().gm_mock_set_procs_file(str(procs).encode())
+            lc.tenant("busy", pids={"main": [sleeper.pid]})
+            code, b = await lease_add(lc, "default", "busy", 1, 1.0)
+            assert code == 200
+            procs.write_text(f"{b['devices'][0]['index']} {sleeper.pid} 4096 python\n")
+            svc = lc.nodes["node-0"].worker.service
+
+            async def warned():
+                await svc.notify.drain()
+                return any(e["reason"] == "GPULeaseExpired" and e["type"] == "Warning"
+                           for e in lc.cluster.events_for("default", "busy"))
+            assert await until(warned)
+            code, c = await lease_add(lc, "default", "busy", 1, 0.3)
+            assert code == 200
+            second = c["devices"][0]["uuid"]
+
+            async def second_gone():
+                st = await svc.pod_state(lc.cluster.get("default", "busy"), fresh=True)
+                return second not in {g.uuid for g in st.hot} and len(st.hot) == 1
+            assert await until(second_gone, timeout=3.0)
+        run(body, worker_overrides={"busy_detection": "both", "lease_retry_s": 30.0})
+    finally:
+        _native.mock_smi().gm_mock_set_procs_file(b"")
+        sleeper.kill()
+        sleeper.wait(timeout=10)
+
+
 def test_lease_survives_a_worker_restart():
     async def body(lc):
         lc.tenant("t")
