@@ -267,8 +267,9 @@ class V1Backend(DeviceRuleBackend):
                 try:
                     with open(os.path.join(cgdir, fname)) as fh:
                         for line in fh:
-                            if line.strip():
-                                net[line.strip()] = net.get(line.strip(), 0) + sign
+                            rule = line.strip()
+                            if rule:
+                                net[rule] = net.get(rule, 0) + sign
                 except FileNotFoundError:
                     pass
             out = set()

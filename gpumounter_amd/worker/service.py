@@ -50,7 +50,7 @@ from gpumounter_amd.utils.faults import FaultInjector, InjectedFault
 from gpumounter_amd.utils.metrics import Metrics
 from gpumounter_amd.worker.drain import DrainKeeper
 from gpumounter_amd.worker.lease import LeaseKeeper, expires_of
-from gpumounter_amd.worker import status
+from gpumounter_amd.worker import planning, status
 from gpumounter_amd.worker.notify import Notifier
 
 _log = log.get("worker.service")
@@ -687,22 +687,8 @@ class GpuMountService:
             await self.ph.release(phs, wait=False)
 
     def _plan_with_pool(self, n: int, st: PodGpuState):
-        """Place over standby ∪ free GPUs together: (standby indices to claim, device IDs to
-        create placeholders for). The pool only saves latency; it does not decide placement."""
-        keys = self.inv.by_key()
-        standby: Dict[int, AmdGpu] = {}
-        for ph in self.pool.standby():
-            g = keys.get(normalize_device_id(ph.device_ids[0])) if ph.device_ids else None
-            if g is not None:
-                standby[g.index] = g
-        cands = list(standby.values()) + [g for g in self._free(st) if g.index not in standby]
-        plc = topology.choose(cands, n, self.inv.links(), attached=st.hot + st.own,
-                              policy=self.cfg.topology_policy, prefer=standby)
-        if plc is None:
-            return None
-        by_index = {g.index: g for g in cands}
-        return ([i for i in plc.chosen if i in standby],
-                [by_index[i].bdf for i in plc.chosen if i not in standby])
+        return planning.plan_with_pool(self.inv, self.cfg.topology_policy, self.pool.standby(),
+                                       n, st, self._free(st))
 
     async def _reserve_trim(self, pod: dict, n: int, req, st: PodGpuState, width: int):
         keys = self.inv.by_key()
@@ -726,27 +712,12 @@ class GpuMountService:
         return res
 
     def _free(self, st: PodGpuState) -> List[AmdGpu]:
-        """GPUs free in the last ledger view (minus placeholders we created since)."""
-        allocated = {normalize_device_id(d) for ids in st.ledger.values() for d in ids}
-        allocated.update(normalize_device_id(d) for uid, ids in self.ph.device_ids.items()
-                         if uid not in self.ph.tombstones for d in ids)
-        return [g for g in self.inv.gpus() if not allocated.intersection(g.ledger_keys())
-                and g.index not in self.unhealthy]
+        return planning.free_gpus(self.inv, self.ph, self.unhealthy, st)
 
     def _preferred(self, n: int, st: PodGpuState, free: Optional[List[AmdGpu]] = None
                    ) -> List[str]:
-        """xGMI/NUMA-aware preferred device IDs among the GPUs free in the last ledger view."""
-        gpus = self.inv.gpus()
-        if free is None:
-            free = self._free(st)
-        plc = topology.choose(free, n, self.inv.links(), attached=st.hot + st.own,
-                              policy=self.cfg.topology_policy)
-        if plc is None:
-            return []
-        by_index = {g.index: g for g in gpus}
-        # the device plugin's own spelling of the ID is unknown here; BDF is what the ROCm plugin
-        # advertises, the fake node honours any ledger key
-        return [by_index[i].bdf for i in plc.chosen]
+        return planning.preferred(self.inv, self.cfg.topology_policy, n, st,
+                                  self._free(st) if free is None else free)
 
     # ------------------------------------------------------------------------ RemoveGPU
     async def remove_gpu(self, req) -> "api.RemoveGPUResponse":
@@ -885,25 +856,7 @@ class GpuMountService:
                                          devices=self._devices(selected, owner),
                                          killed_pids=killed, message="Remove GPU Success")
 
-    @staticmethod
-    def select_removal(st: PodGpuState, ids: List[str]) -> List[AmdGpu]:
-        """Reference allocator.go:101-126: only hot-mounted GPUs are removable; entire mounts are
-        removed as a whole; any unmatched id makes the whole request invalid (empty result)."""
-        if not ids:
-            return []
-        want = {normalize_device_id(i) for i in ids}
-        if len(want) != len(ids):
-            return []
-        if st.mount_type == MountType.ENTIRE:
-            candidates = list(st.hot)
-            matched = {k for g in candidates for k in g.ledger_keys()}
-            if len(want) != len(candidates) or not want <= matched:
-                return []
-            return candidates
-        selected = [g for g in st.hot if want.intersection(g.ledger_keys())]
-        if len(selected) != len(want):
-            return []
-        return selected
+    select_removal = staticmethod(planning.select_removal)
 
     # ------------------------------------------------------------------------ status
     async def node_status(self, include_processes: bool) -> dict:
