@@ -106,6 +106,20 @@ class WorkerDirectory:
 
     async def start(self) -> None:
         await self.informer.start()
+        self.informer.handlers.append(lambda etype, pod: self.warm())
+        self.warm()
+
+    def warm(self) -> None:
+        """Open the channel to every running worker ahead of its first request: the TCP
+        connect and the TLS handshake then happen in the background, not in an attach
+        (reference: a new insecure connection per request, main.go:82)."""
+        for p in self.informer.cache.values():
+            t = self.target(podu.node_of(p))
+            if t is not None:
+                try:
+                    self.channel(t).get_state(try_to_connect=True)
+                except RuntimeError:         # no running loop (stopping)
+                    return
 
     async def stop(self) -> None:
         await self.informer.stop()
