@@ -1351,3 +1351,24 @@ def test_identical_queued_events_are_sent_once_with_their_count():
         await nt.drain()
         assert kube.events[-1]["count"] == 1
     asyncio.run(body())
+
+
+def test_master_opens_worker_channels_before_the_first_request():
+    """The master connects to every running worker it discovers (TCP, and TLS where set), so
+    the first attach does not pay the handshake."""
+    import grpc
+
+    async def main():
+        async with LocalCluster() as lc:
+            wd = lc.master.workers
+            target = wd.target("node-0")
+            assert target is not None
+            state = None
+            for _ in range(250):
+                ch = wd._channels.get(target)                       # noqa: SLF001
+                state = ch.get_state() if ch is not None else None
+                if state == grpc.ChannelConnectivity.READY:
+                    break
+                await asyncio.sleep(0.02)
+            assert state == grpc.ChannelConnectivity.READY
+    asyncio.run(main())
