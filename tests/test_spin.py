@@ -48,3 +48,25 @@ def test_capped_per_stretch_and_nested_holds():
             await asyncio.sleep(0.002)
         assert sp.ticks > n
     asyncio.run(main())
+
+
+def test_attach_and_detach_with_polling_loops():
+    """loop_spin_us on the master and the worker: requests are served as without it, the loops
+    polled during them, and polling stops once they are answered."""
+    from gpumounter_amd.fakes.harness import LocalCluster
+
+    async def main():
+        async with LocalCluster(worker_overrides={"loop_spin_us": 300},
+                                master_overrides={"loop_spin_us": 300}) as lc:
+            lc.tenant("t")
+            code, b = await lc.add("default", "t", 1)
+            assert code == 200
+            code, _ = await lc.remove("default", "t", [b["devices"][0]["uuid"]])
+            assert code == 200 and not await lc.audit("default", "t")
+            spinners = [lc.master.spin, lc.nodes["node-0"].worker.spin]
+            assert all(s.enabled and s.ticks > 0 for s in spinners)
+            await asyncio.sleep(0.05)
+            before = [s.ticks for s in spinners]
+            await asyncio.sleep(0.05)
+            assert [s.ticks for s in spinners] == before
+    asyncio.run(main())
