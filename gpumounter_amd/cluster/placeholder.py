@@ -79,6 +79,10 @@ class Placeholder:
     device_ids: Tuple[str, ...] = ()
     mode: str = "single"
     candidate: bool = False      # held by a trim/correction pick, not yet confirmed
+    # the owner Pod's uid as the view this object came from shows it ("" = none: standby). A
+    # warm-pool placeholder changes hands; its release applies only while it still has this
+    # owner (see _delete)
+    owner_uid: str = ""
 
 
 @dataclass
@@ -448,7 +452,8 @@ class PlaceholderManager:
                 return_exceptions=True)
         created = [Placeholder(r["metadata"]["namespace"], r["metadata"]["name"],
                                r["metadata"]["uid"], (),
-                               r["metadata"]["annotations"].get(ANN_MOUNT_MODE, "single"))
+                               r["metadata"]["annotations"].get(ANN_MOUNT_MODE, "single"),
+                               owner_uid=r["metadata"]["annotations"].get(ANN_OWNER_UID, ""))
                    for r in results if isinstance(r, dict)]
         for r in results:
             if isinstance(r, dict):
@@ -631,9 +636,9 @@ class PlaceholderManager:
     # ------------------------------------------------------------------------ release
     async def _delete(self, p: Placeholder) -> Optional[dict]:
         """DELETE one placeholder. One made for a Pod belongs to it for life; a warm-pool one
-        is deleted only at a version at which it still has the owner the cache shows, so a
-        release decided on a stale cache never takes a GPU from the Pod that claimed it since
-        (raises :class:`Reowned`)."""
+        is deleted only at a version at which it still has the owner the caller's view showed
+        (``p.owner_uid``), so a release decided on a stale view never takes a GPU from the Pod
+        that claimed it since (raises :class:`Reowned`)."""
         if not p.name.startswith(STANDBY_PREFIX):
             return await self.kube.delete_pod(p.namespace, p.name, grace_period_s=0,
                                               uid=p.uid or "")
@@ -642,7 +647,7 @@ class PlaceholderManager:
             seen = await self.kube.get_pod(p.namespace, p.name)
             if p.uid and seen["metadata"].get("uid") != p.uid:
                 raise NotFound(404, f"{p.name}: another pod of that name")
-        owner = (seen["metadata"].get("annotations") or {}).get(ANN_OWNER_UID)
+        owner = p.owner_uid
         rv = seen["metadata"].get("resourceVersion", "")
         for _ in range(3):
             try:
@@ -652,7 +657,7 @@ class PlaceholderManager:
                 cur = await self.kube.get_pod(p.namespace, p.name)
                 if p.uid and cur["metadata"].get("uid") != p.uid:
                     raise NotFound(404, f"{p.name}: another pod of that name") from None
-                if (cur["metadata"].get("annotations") or {}).get(ANN_OWNER_UID) != owner:
+                if ((cur["metadata"].get("annotations") or {}).get(ANN_OWNER_UID) or "") != owner:
                     raise Reowned(p.name) from None
                 rv = cur["metadata"].get("resourceVersion", "")
         raise ApiError(409, f"{p.name} kept changing while being deleted")
@@ -727,7 +732,7 @@ class PlaceholderManager:
         ann = md.get("annotations") or {}
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""),
                            tuple(ledger_ids.get(key, ())), ann.get(ANN_MOUNT_MODE, "single"),
-                           ANN_CANDIDATE in ann)
+                           ANN_CANDIDATE in ann, ann.get(ANN_OWNER_UID) or "")
 
     def cached(self, p: dict) -> Optional[Placeholder]:
         """Placeholder with its device IDs from the admission cache (None if unknown)."""
@@ -737,4 +742,5 @@ class PlaceholderManager:
             return None
         ann = md.get("annotations") or {}
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""), ids,
-                           ann.get(ANN_MOUNT_MODE, "single"), ANN_CANDIDATE in ann)
+                           ann.get(ANN_MOUNT_MODE, "single"), ANN_CANDIDATE in ann,
+                           ann.get(ANN_OWNER_UID) or "")

@@ -282,6 +282,7 @@ class WarmPool:
                 return None
             for ph in chosen:
                 ph.mode = mode
+                ph.owner_uid = podu.uid_of(owner)
             if self.metrics is not None:
                 self.metrics.reconcile_actions.labels(action="pool_claim").inc(len(chosen))
         self.poke()
@@ -408,12 +409,11 @@ class WarmPool:
             cache = {p["metadata"]["uid"]: p for p in self.ph.live()}
 
             def put(ph: Placeholder):
+                # at the cached version, while it has the owner the caller's view showed
                 seen = cache.get(ph.uid)
-                if seen is None:
-                    return self._put_back(ph, lambda cur: not is_standby(cur))
-                owner = _owner_uid(seen)
-                return self._put_back(ph, lambda cur: _owner_uid(cur) == owner,
-                                      seen["metadata"].get("resourceVersion"))
+                rv = seen["metadata"].get("resourceVersion") if seen is not None else None
+                return self._put_back(ph, lambda cur: (_owner_uid(cur) or "") == ph.owner_uid,
+                                      rv)
             with trace.span("pool_return", placeholders=len(keep)):
                 res = await asyncio.gather(*[put(ph) for ph in keep], return_exceptions=True)
             back, theirs = self._sort_back(keep, res)

@@ -122,6 +122,7 @@ class DrainKeeper:
             if isinstance(r, dict):
                 self.svc.ph.informer.upsert(r, epoch)
                 ph.mode = MODE_DRAINING
+                ph.owner_uid = ""                       # the mark removes the owner
                 self.unmarked.pop(ph.uid, None)
             elif isinstance(r, NotFound):
                 self.unmarked.pop(ph.uid, None)     # gone: nothing left to book
@@ -193,7 +194,10 @@ class DrainKeeper:
         self._save()
 
     async def _resume_one(self, uid: str, rec: dict) -> None:
-        ph = Placeholder(rec["ns"], rec["name"], uid)
+        cur = self.svc.ph.informer.cache.get((rec["ns"], rec["name"])) or {"metadata": {}}
+        # unmarked: it still names the Pod it was removed from as its owner
+        ph = Placeholder(rec["ns"], rec["name"], uid, owner_uid=(
+            cur["metadata"].get("annotations") or {}).get(ANN_OWNER_UID) or "")
         delays = self._delays()
         while uid in self.unmarked:
             if not any(procs.same_process(pid, st) for pid, st in parse_pids(rec["pids"])):

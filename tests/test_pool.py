@@ -276,3 +276,27 @@ def test_pick_surplus_returned_to_the_pool_is_no_candidate_for_its_next_owner():
             assert len(svc.ph.owned_by(lc.cluster.get("default", "b"))) == len(owned)
             assert not await lc.audit("default", "b")
     asyncio.run(main())
+
+
+def test_release_of_a_claimed_placeholder_behind_a_stale_cache_still_deletes_it():
+    """The worker's cache can still show a placeholder as standby after this worker claimed it
+    (the claim's write-through was dropped by a relist). Releasing it for its owner must still
+    delete it: the owner that counts is the one the releasing caller's view holds, not the
+    stale cache's."""
+    import copy
+
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 1}) as lc:
+            pool = await wait_pool(lc, 1)
+            svc = lc.nodes["node-0"].worker.service
+            lc.tenant("a")
+            (ph,) = pool.standby()
+            key = (ph.namespace, ph.name)
+            stale = copy.deepcopy(svc.ph.informer.cache[key])
+            got = await pool.claim(lc.cluster.get("default", "a"), 1, False, [],
+                                   attach_id="add-a")
+            assert got is not None and got.placeholders[0].owner_uid
+            svc.ph.informer.cache[key] = stale          # the claim never reached the cache
+            await svc.ph.release(got.placeholders, wait=False)
+            assert lc.cluster.get(*key) is None
+    asyncio.run(main())
