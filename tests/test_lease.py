@@ -1,6 +1,7 @@
 """GPU leases (gpumounter_amd/worker/lease.py): ``?lease=<s>`` attaches that detach themselves."""
 import asyncio
 import subprocess
+import time
 
 from gpumounter_amd import _native
 from gpumounter_amd.fakes.harness import LocalCluster
@@ -278,3 +279,21 @@ def test_a_pool_placeholder_does_not_carry_its_last_owners_lease():
             "gpumounter.amd.com/owner-name")
         assert owner == "b" and svc.lease.expired == 0
     run(body, worker_overrides={"warm_pool_size": 1})
+
+
+def test_the_pod_gpu_view_shows_when_a_lease_ends():
+    async def body(lc):
+        lc.tenant("t")
+        code, plain = await lc.add("default", "t", 1)
+        assert code == 200
+        code, leased = await lease_add(lc, "default", "t", 1, 60)
+        assert code == 200
+        url = f"{lc.master_url}/api/v1/namespaces/default/pods/t/gpus"
+        async with lc.session.get(url) as r:
+            assert r.status == 200
+            view = {g["uuid"]: g for g in (await r.json())["gpus"]
+                    if g["source"] == "hot-mount"}
+        assert view[plain["devices"][0]["uuid"]]["lease_expires"] is None
+        exp = view[leased["devices"][0]["uuid"]]["lease_expires"]
+        assert exp is not None and 50 < exp - time.time() <= 60
+    run(body)
