@@ -563,8 +563,20 @@ def chaos(args) -> dict:
                             mine[t] = [([u for grp, _ in mine[t] for u in grp], True)]
                         held_now = {x["uuid"]: x.get("pod_name") for x in g.get("gpus", [])
                                     if x.get("source") == "hot-mount"}
+                        # a lease still stands if its placeholder holds the GPU *with that lease*:
+                        # a warm-pool placeholder given back and claimed again (by this Pod's
+                        # later attach, answer lost) has the same name and no lease
+                        on_ledger = {x["uuid"]: x.get("lease_expires")
+                                     for x in g.get("gpus", []) if x.get("source") == "hot-mount"}
+
+                        def same_lease(u, e):
+                            exp = on_ledger.get(u)
+                            if not exp:
+                                return False
+                            at = time.monotonic() + (exp - time.time())
+                            return e[0] - 1.0 <= at <= e[1] + 1.0
                         leases[t] = {u: e for u, e in leases[t].items()
-                                     if held_now.get(u) == e[2]}
+                                     if held_now.get(u) == e[2] and same_lease(u, e)}
                         # a leased attach whose answer was lost: its lease is on the ledger
                         for x in g.get("gpus", []):
                             exp = x.get("lease_expires")

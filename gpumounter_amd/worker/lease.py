@@ -18,12 +18,19 @@ from typing import Dict, List, Optional, Tuple
 
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import ANN_LEASE, ANN_OWNER_UID, LABEL_OWNER_NS, MountType
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_LEASE, ANN_OWNER_UID,
+                                         LABEL_OWNER_NS, MountType)
 from gpumounter_amd.node.ledger import LedgerError
 from gpumounter_amd.utils import log
 
 _log = log.get("worker.lease")
 __all__ = ["ANN_LEASE", "LeaseKeeper", "expires_of"]
+
+
+def _holder(ph: dict) -> Tuple[str, str]:
+    """The attach a placeholder serves now: (owner pod uid, attach id)."""
+    ann = ph["metadata"].get("annotations") or {}
+    return ann.get(ANN_OWNER_UID) or "", ann.get(ANN_ATTACH_ID) or ""
 
 
 def expires_of(ph: dict) -> Optional[float]:
@@ -47,10 +54,12 @@ class LeaseKeeper:
         self._errors: Dict[Tuple[str, str], int] = {}          # owner → failed expiries in a row
         self._tasks: set = set()                               # running expiries
         self._locks: Dict[Tuple[str, str], asyncio.Lock] = {}  # owner → its expiries in turn
-        # placeholder uid → (expiry this worker granted, owner pod uid): the informer learns the
-        # annotation only from the watch echo of our PATCH, which can lag (a dropped stream, a
-        # relist). A warm-pool placeholder changes owner, so the grant holds for its owner only
-        self._granted: Dict[str, Tuple[float, str]] = {}
+        # placeholder uid → (expiry this worker granted, the holding attach: owner pod uid,
+        # attach id): the informer learns the annotation only from the watch echo of our PATCH,
+        # which can lag (a dropped stream, a relist). A warm-pool placeholder changes hands, also
+        # back to the same Pod by a later attach, so a grant holds only for the attach it was
+        # made for (see _holder)
+        self._granted: Dict[str, Tuple[float, Tuple[str, str]]] = {}
         self._stopped = False
         self.expired = 0
 
@@ -63,17 +72,19 @@ class LeaseKeeper:
         epoch = informer.epoch
         res = await asyncio.gather(*[self.svc.kube.patch_pod(p.namespace, p.name, patch)
                                      for p in placeholders])
-        for r in res:
+        for p, r in zip(placeholders, res):
             if isinstance(r, dict):
                 informer.upsert(r, epoch)    # visible to expire_owner before the watch echo
-        for p in placeholders:
-            if p.uid:
-                self._granted[p.uid] = (expires, podu.uid_of(pod))
+                if p.uid:
+                    self._granted[p.uid] = (expires, _holder(r))
             self._arm(p.uid, podu.ns_of(pod), podu.name_of(pod), expires)
         return expires
 
-    def granted(self, uid: str) -> bool:
-        return uid in self._granted
+    def granted(self, raw: dict) -> Optional[float]:
+        """The expiry this worker granted to placeholder ``raw`` for the attach that holds it
+        now (None: none, or granted to an earlier holder of a warm-pool placeholder)."""
+        g = self._granted.get(raw["metadata"].get("uid", ""))
+        return g[0] if g is not None and g[1] == _holder(raw) else None
 
     def _arm(self, uid: str, ns: str, name: str, expires: float) -> None:
         """A timer for the lease of placeholder ``uid`` (one per placeholder; re-arming an
@@ -154,8 +165,7 @@ class LeaseKeeper:
         now = time.time()
         due: Dict[Tuple[str, str], List[dict]] = {}
         live = self.svc.ph.live()
-        owners = {p["metadata"].get("uid"): (p["metadata"].get("annotations") or {}).get(
-            ANN_OWNER_UID) for p in live}
+        owners = {p["metadata"].get("uid"): _holder(p) for p in live}
         for uid in [u for u, (_, o) in self._granted.items()
                     if u not in owners or owners[u] != o]:
             del self._granted[uid]          # released some other way (RemoveGPU, owner gone,
@@ -205,9 +215,8 @@ class LeaseKeeper:
         for ph in st.placeholders:
             raw = raws.get(ph.name)
             exp = expires_of(raw) if raw is not None else None
-            if exp is None:
-                g = self._granted.get(ph.uid)
-                exp = g[0] if g is not None and g[1] == podu.uid_of(pod) else None
+            if exp is None and raw is not None:
+                exp = self.granted(raw)
             if exp is None:
                 continue
             if exp <= now + 0.001:

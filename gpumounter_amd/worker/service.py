@@ -551,7 +551,8 @@ class GpuMountService:
             return None
         if lease_s > 0:
             unleased = [ph for ph in st.placeholders if ph.name in mine and
-                        expires_of(raw[ph.name]) is None and not self.lease.granted(ph.uid)]
+                        expires_of(raw[ph.name]) is None and
+                        self.lease.granted(raw[ph.name]) is None]
             if unleased:
                 await self.lease.grant(pod, unleased, lease_s)
         gs, owner = [], {}

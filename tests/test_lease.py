@@ -297,3 +297,31 @@ def test_the_pod_gpu_view_shows_when_a_lease_ends():
         exp = view[leased["devices"][0]["uuid"]]["lease_expires"]
         assert exp is not None and 50 < exp - time.time() <= 60
     run(body)
+
+
+def test_a_pool_placeholder_reclaimed_by_the_same_pod_does_not_inherit_its_old_lease():
+    """The same Pod gives a leased pool placeholder back before the lease ends and a later
+    attach of that Pod (no lease) claims the same placeholder: the worker's memory of the old
+    grant is for the earlier attach only (found by chaos: warm pool 2, leases, seed 33)."""
+    async def body(lc):
+        w = lc.nodes["node-0"].worker
+        svc, pool = w.service, w.pool
+        for _ in range(250):
+            if len(pool.standby()) == 1:
+                break
+            await asyncio.sleep(0.02)
+        lc.tenant("a")
+        code, a = await lease_add(lc, "default", "a", 1, 0.4)
+        assert code == 200
+        ph, idx = a["devices"][0]["placeholder"], a["devices"][0]["index"]
+        pool.target = 2
+        code, _ = await lc.remove("default", "a", [a["devices"][0]["uuid"]])
+        assert code == 200
+        got = await pool.claim(lc.cluster.get("default", "a"), 1, False, [],
+                               attach_id="add-again", want=[idx])
+        assert got is not None and got.placeholders[0].name == ph
+        await asyncio.sleep(0.6)
+        await svc.lease.sweep()
+        await asyncio.sleep(0.1)
+        assert lc.cluster.get("gpu-pool", ph) is not None and svc.lease.expired == 0
+    run(body, worker_overrides={"warm_pool_size": 1})
