@@ -1,6 +1,7 @@
 # Attach latency of the other shipped modes on one MI355X box (the headline is the default mode):
 #   gpurun --timeout 900 -- bash bench/gpu_runs/modes.sh <tag>
-# warm pool (claim instead of create), DRA placeholders, trim placement, own device plugin.
+# warm pool (claim instead of create), DRA placeholders, trim placement, own device plugin (the
+# fake kubelet drives the plugin in-process, so that run is --deploy inprocess).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-modes}
@@ -21,4 +22,4 @@ run default
 run pool --warm-pool 2
 run dra --gpu-api dra
 run trim --placement trim
-run plugin --device-plugin
+run plugin --device-plugin --deploy inprocess
