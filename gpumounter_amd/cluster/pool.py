@@ -278,6 +278,8 @@ class WarmPool:
                     _log.info("standby placeholder(s) %s claimed elsewhere; falling back",
                               [ph.name for ph in taken])
                 if stray:
+                    for ph in stray:            # deleted only while still this Pod's
+                        ph.owner_uid = podu.uid_of(owner)
                     await self.ph.release(stray, wait=False)
                 return None
             for ph in chosen:

@@ -9,7 +9,8 @@ schedule,
   held by two claims at once;
 * every placeholder a claim holds is, at the apiserver, owned by that claim's Pod until the
   claim gives it back;
-* a give-back never changes the owner of a placeholder some other claim holds.
+* a give-back never changes the owner of a placeholder some other claim holds;
+* a claim refused without an error leaves none of its placeholders claimed.
 
 The explicit example is the chaos finding of round 4 (`profiles/r4_chaos_full/`): the second
 incarnation's cache still shows a placeholder as standby after the first one claimed it. With
@@ -167,6 +168,9 @@ OPS = s.lists(s.one_of(
 
 # the chaos finding: incarnation 1's cache is behind incarnation 0's claim of the only standby
 SCENARIO = {"ops": [("claim", 0, 0, 1), ("claim", 1, 1, 1)], "schedule": []}
+# a claim PATCH applied behind a lost reply, then the undo's read fails: the placeholder is
+# deleted as this attach's stray, which must not be mistaken for someone else's
+STRAY = {"ops": [("claim", 0, 0, 1)], "schedule": ["lost", "before"]}
 
 
 def run_scenario(inv, ops, schedule):
@@ -195,7 +199,14 @@ def run_scenario(inv, ops, schedule):
                 try:
                     res = await pool.claim(owners[oi], n, False, [], attach_id=f"add-{step}")
                 except (ApiError, ReserveError):
-                    res = None          # failed: the worker's follow-up cleans up after it
+                    res = False         # failed: the worker's follow-up cleans up after it
+                if res is None:         # refused cleanly: nothing of this attach stays claimed
+                    left = [nm for nm, p in kube.pods.items()
+                            if (p["metadata"].get("annotations") or {}).get(
+                                "gpumounter.amd.com/attach-id") == f"add-{step}"]
+                    if left:
+                        problems.append(f"step {step}: claim refused but {left} stay claimed "
+                                        f"by t{oi}")
                 for ph in (res.placeholders if res else []):
                     if ph.name in held:
                         problems.append(f"step {step}: {ph.name} claimed by t{oi} while t"
@@ -236,6 +247,7 @@ def inv(mock_inventory):
           suppress_health_check=[HealthCheck.function_scoped_fixture])
 @given(ops=OPS, schedule=s.lists(OUTCOMES, max_size=20))
 @example(**SCENARIO)
+@example(**STRAY)
 def test_a_standby_placeholder_is_never_held_by_two_claims(inv, ops, schedule):
     problems = run_scenario(inv, ops, schedule)
     assert not problems, problems[:3]
