@@ -10,7 +10,8 @@ schedule,
 * every placeholder a claim holds is, at the apiserver, owned by that claim's Pod until the
   claim gives it back;
 * a give-back never changes the owner of a placeholder some other claim holds;
-* a claim refused without an error leaves none of its placeholders claimed.
+* a claim refused without an error leaves none of its placeholders claimed, and a give-back
+  that returns leaves none of them with the Pod that gave them back.
 
 The explicit example is the chaos finding of round 4 (`profiles/r4_chaos_full/`): the second
 incarnation's cache still shows a placeholder as standby after the first one claimed it. With
@@ -227,7 +228,13 @@ def run_scenario(inv, ops, schedule):
                     try:
                         await pool.give_back(phs)
                     except (ApiError, ReserveError):
-                        pass            # given up by the caller either way
+                        continue        # failed: the worker's follow-up retries the release
+                    mine_left = [ph.name for ph in phs if (
+                        (kube.pods.get(ph.name) or {}).get("metadata", {}).get(
+                            "annotations") or {}).get(ANN_OWNER_UID) == ph.owner_uid]
+                    if mine_left:
+                        problems.append(f"step {step}: t{oi} gave back {mine_left} and still "
+                                        f"owns them")
             for name, (o, _) in held.items():
                 pod = kube.pods.get(name)
                 got = ((pod or {}).get("metadata", {}).get("annotations") or {}).get(ANN_OWNER_UID)
