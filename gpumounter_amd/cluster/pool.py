@@ -401,8 +401,9 @@ class WarmPool:
 
     async def give_back(self, phs: Sequence[Placeholder]) -> None:
         """Return detached placeholders to the pool (up to ``target``); delete the rest. Each
-        goes back at the version the worker's cache holds, as long as it still has the owner
-        the cache shows (one put back and claimed anew meanwhile stays with its new owner)."""
+        goes back only at a version at which it has the owner the caller's view showed
+        (``Placeholder.owner_uid``): one put back and claimed anew meanwhile stays with its new
+        owner."""
         async with self._lock:
             # standby being admitted count too, or a refill racing a give-back overfills
             room = max(self.target - len(self.standby()) - self.pending() - self._creating, 0)
@@ -411,11 +412,14 @@ class WarmPool:
             cache = {p["metadata"]["uid"]: p for p in self.ph.live()}
 
             def put(ph: Placeholder):
-                # at the cached version, while it has the owner the caller's view showed
+                # at the cached version if the cache agrees it has the owner the caller's view
+                # showed, else at a version read now
+                def ours(cur):
+                    return (_owner_uid(cur) or "") == ph.owner_uid
                 seen = cache.get(ph.uid)
-                rv = seen["metadata"].get("resourceVersion") if seen is not None else None
-                return self._put_back(ph, lambda cur: (_owner_uid(cur) or "") == ph.owner_uid,
-                                      rv)
+                rv = seen["metadata"].get("resourceVersion") \
+                    if seen is not None and ours(seen) else None
+                return self._put_back(ph, ours, rv)
             with trace.span("pool_return", placeholders=len(keep)):
                 res = await asyncio.gather(*[put(ph) for ph in keep], return_exceptions=True)
             back, theirs = self._sort_back(keep, res)
