@@ -642,12 +642,19 @@ class PlaceholderManager:
         if not p.name.startswith(STANDBY_PREFIX):
             return await self.kube.delete_pod(p.namespace, p.name, grace_period_s=0,
                                               uid=p.uid or "")
+        owner = p.owner_uid
+
+        def owner_of(pod: dict) -> str:
+            return (pod["metadata"].get("annotations") or {}).get(ANN_OWNER_UID) or ""
+        # the cached version only if the cache agrees on the owner; else one read now
         seen = self.informer.cache.get((p.namespace, p.name))
-        if seen is None or (p.uid and seen["metadata"].get("uid") != p.uid):
+        if seen is None or (p.uid and seen["metadata"].get("uid") != p.uid) or \
+                owner_of(seen) != owner:
             seen = await self.kube.get_pod(p.namespace, p.name)
             if p.uid and seen["metadata"].get("uid") != p.uid:
                 raise NotFound(404, f"{p.name}: another pod of that name")
-        owner = p.owner_uid
+            if owner_of(seen) != owner:
+                raise Reowned(p.name)
         rv = seen["metadata"].get("resourceVersion", "")
         for _ in range(3):
             try:
@@ -657,7 +664,7 @@ class PlaceholderManager:
                 cur = await self.kube.get_pod(p.namespace, p.name)
                 if p.uid and cur["metadata"].get("uid") != p.uid:
                     raise NotFound(404, f"{p.name}: another pod of that name") from None
-                if ((cur["metadata"].get("annotations") or {}).get(ANN_OWNER_UID) or "") != owner:
+                if owner_of(cur) != owner:
                     raise Reowned(p.name) from None
                 rv = cur["metadata"].get("resourceVersion", "")
         raise ApiError(409, f"{p.name} kept changing while being deleted")
