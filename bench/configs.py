@@ -348,7 +348,7 @@ def chaos(args) -> dict:
     leases = {t: {} for t in tenants}        # uuid -> (earliest, latest) expiry of its lease
     leased, expired = [0], [0]
     certain = {t: True for t in tenants}
-    answered = {t: [] for t in tenants}      # (code, [(placeholder, uuid tail)]) per attach
+    answered = {t: [] for t in tenants}      # (code, [(placeholder, uuid tail)], lease) per attach
     ok = failed = kills = restarts = master_kills = recreates = kubelet_restarts = 0
     recreated: set = set()
     problems, converge = [], []
@@ -391,7 +391,7 @@ def chaos(args) -> dict:
                 code, b = pc.add("default", t, n, entire=entire, lease_s=lease)
                 answered[t].append((code, [(d.get("placeholder"), d["uuid"][-4:])
                                            for d in (b.get("devices") or [])]
-                                    if isinstance(b, dict) else None))
+                                    if isinstance(b, dict) else None, lease))
                 if code == 200:
                     uu = [d["uuid"] for d in b["devices"]]
                     # a GPU attached again was in an earlier lease of this tenant: that lease
@@ -530,7 +530,9 @@ def chaos(args) -> dict:
                                   holders.get(t, {}).get(u) == leases[t][u][2])
                     if late:
                         problems.append(f"round {rnd_i} {t}: leases expired more than "
-                                        f"{args.lease_slack} s ago still attached: {late}")
+                                        f"{args.lease_slack} s ago still attached: {late}; "
+                                        f"held by {[holders.get(t, {}).get(u) for u in late]}; "
+                                        f"last answers {answered[t][-4:]}")
                     gone = set(overdue) - set(late)
                     for u in gone:
                         leases[t].pop(u)

@@ -50,6 +50,9 @@ class PodInformer:
         self._pending: Dict[Key, str] = {}
         self.resolved = 0        # objects re-read with a GET after a relist (see _relist)
         self._bg: set = set()
+        # keys whose write-through a relist overtook, being re-read (see upsert): until then
+        # the cache may show them older than this process's own acknowledged writes
+        self._resolving: Dict[Key, int] = {}
         self.handlers: List[Callable[[str, dict], None]] = []
 
     async def start(self) -> None:
@@ -246,11 +249,31 @@ class PodInformer:
             loop = asyncio.get_running_loop()
         except RuntimeError:
             return
+        self._resolving[key] = self._resolving.get(key, 0) + 1
         t = loop.create_task(self._resolve(key))
         self._bg.add(t)
         t.add_done_callback(self._bg.discard)
 
+    @property
+    def settled(self) -> bool:
+        """No write-through of ours is waiting to be re-read after a relist: the cache holds
+        every write this process has had acknowledged."""
+        return not self._resolving
+
     async def _resolve(self, key: Key, tries: int = 3) -> None:
+        try:
+            await self._resolve_once(key, tries)
+        finally:
+            n = self._resolving.get(key, 0) - 1
+            if n > 0:
+                self._resolving[key] = n
+            else:
+                self._resolving.pop(key, None)
+            if self._cond is not None:
+                async with self._cond:
+                    self._cond.notify_all()
+
+    async def _resolve_once(self, key: Key, tries: int) -> None:
         """Replace the cached ``key`` with a fresh GET, unless another relist overtook the GET
         (then the GET may be older than that list: try again)."""
         for _ in range(tries):

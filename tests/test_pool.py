@@ -300,3 +300,48 @@ def test_release_of_a_claimed_placeholder_behind_a_stale_cache_still_deletes_it(
             await svc.ph.release(got.placeholders, wait=False)
             assert lc.cluster.get(*key) is None
     asyncio.run(main())
+
+
+def test_a_claim_overtaken_by_a_relist_is_not_revoked_by_the_reconciler():
+    """A relist between a claim PATCH and its reply drops the claim's write-through: until a GET
+    settles the key the cache shows the placeholder standby. A reconcile of the owner in that
+    window saw its just-mounted GPU as stale and revoked it, and nothing repaired it until the
+    next sweep (chaos: trim + warm pool + leases, seed 72). reconcile_pod now waits for the view
+    to settle."""
+    import copy
+
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 1}) as lc:
+            pool = await wait_pool(lc, 1)
+            svc = lc.nodes["node-0"].worker.service
+            inf = svc.ph.informer
+            lc.tenant("a")
+            (ph,) = pool.standby()
+            key = (ph.namespace, ph.name)
+            before = copy.deepcopy(inf.cache[key])
+            real_patch, real_fetch = svc.ph.kube.patch_pod, inf._fetch     # noqa: SLF001
+
+            async def patch(ns, name, body):
+                out = await real_patch(ns, name, body)
+                if name == ph.name and (body["metadata"].get("annotations") or {}).get(
+                        "gpumounter.amd.com/owner-name") == "a":
+                    inf.epoch += 1                   # a relist listed the pre-claim version
+                    inf.cache[key] = copy.deepcopy(before)
+                return out
+
+            async def slow_fetch(k):
+                if k == key:
+                    await asyncio.sleep(0.3)
+                return await real_fetch(k)
+            svc.ph.kube.patch_pod, inf._fetch = patch, slow_fetch               # noqa: SLF001
+            inf._task.cancel()          # the resumed watch has not delivered the claim yet
+            await asyncio.sleep(0)
+            code, b = await lc.add("default", "a", 1)
+            assert code == 200 and b["devices"][0]["placeholder"] == ph.name
+            assert not getattr(inf, "settled", False)      # the GET is still on its way
+            await svc.reconcile_pod(lc.cluster.get("default", "a"))
+            await asyncio.sleep(0.5)                 # the GET has settled the view
+            assert inf.cache[key]["metadata"]["annotations"].get(
+                "gpumounter.amd.com/owner-name") == "a"
+            assert not await lc.audit("default", "a")   # still mounted: nothing was revoked
+    asyncio.run(main())
