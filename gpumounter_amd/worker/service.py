@@ -85,7 +85,7 @@ def can_mount(mount_type: MountType, entire: bool) -> Tuple[bool, str]:
 
 
 class GpuMountService:
-    SETTLE_WAIT_S = 2.0          # reconcile_pod: longest wait for the placeholder view to settle
+    SETTLE_WAIT_S = 2.0          # pod_state: longest wait for the placeholder view to settle
     def __init__(self, cfg, kube: KubeClient, inv: Inventory, ledger: LedgerClient,
                  placeholders: PlaceholderManager, hotmount: HotMount, node_pods: PodInformer,
                  metrics: Optional[Metrics] = None, faults: Optional[FaultInjector] = None) -> None:
@@ -200,6 +200,19 @@ class GpuMountService:
         incarnation) or when ``fresh`` is requested (reconciler, status).
         """
         st = PodGpuState()
+        # a relist that overtook one of this worker's own writes (a pool claim, a lease) leaves
+        # the cache older than what the worker has done until a GET settles it. A view from
+        # that cache would, e.g., let a reconcile revoke a just-attached GPU from its Pod, or an
+        # attach's complete desired set leave it out: wait for the view to settle
+        inf = self.ph.informer
+        if not getattr(inf, "settled", True):
+            try:
+                await inf.wait_for(lambda: inf.settled, self.SETTLE_WAIT_S)
+            except asyncio.TimeoutError:
+                _log.error("placeholder view not settled %g s after a relist",
+                           self.SETTLE_WAIT_S)
+                st.mount_type = MountType.UNKNOWN
+                return st
         # a failed attach's placeholder that is still being released is nobody's GPU: a rollback
         # or a later attach of the same pod must not mount it (it is schedulable once deleted);
         # nor is a force-removed one whose draining mark is still being retried (worker/drain.py)
@@ -266,15 +279,6 @@ class GpuMountService:
         ``authoritative=False`` (the reconciler, once its sweep has cross-checked the checkpoint
         against PodResources) reads the ledger from the device-manager checkpoint.
         """
-        # a relist that overtook one of our own writes (a pool claim, a lease) leaves the cache
-        # older than what this worker has done until a GET settles it: revoking from that view
-        # would take a just-attached GPU from its Pod
-        inf = self.ph.informer
-        if not getattr(inf, "settled", True):
-            try:
-                await inf.wait_for(lambda: inf.settled, self.SETTLE_WAIT_S)
-            except asyncio.TimeoutError:
-                raise LedgerError("placeholder view not settled after a relist") from None
         st = await self.pod_state(pod, fresh=True, ledger_snapshot=ledger_snapshot,
                                   authoritative=authoritative)
         if st.mount_type == MountType.UNKNOWN:

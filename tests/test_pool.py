@@ -345,3 +345,45 @@ def test_a_claim_overtaken_by_a_relist_is_not_revoked_by_the_reconciler():
                 "gpumounter.amd.com/owner-name") == "a"
             assert not await lc.audit("default", "a")   # still mounted: nothing was revoked
     asyncio.run(main())
+
+
+def test_a_second_attach_behind_an_overtaken_claim_keeps_the_first_gpu():
+    """The same window for the attach path: a Pod's next attach computes the complete set of
+    nodes its container keeps (cgroup v2 writes the whole allow set) from the Pod's view. Taken
+    before the relist-overtaken claim settles, that set left the first GPU out and its access was
+    revoked by the second attach."""
+    import copy
+
+    async def main():
+        async with LocalCluster(cgroup_mode="v2", worker_overrides={"warm_pool_size": 1}) as lc:
+            pool = await wait_pool(lc, 1)
+            svc = lc.nodes["node-0"].worker.service
+            inf = svc.ph.informer
+            lc.tenant("a")
+            (ph,) = pool.standby()
+            key = (ph.namespace, ph.name)
+            before = copy.deepcopy(inf.cache[key])
+            real_patch, real_fetch = svc.ph.kube.patch_pod, inf._fetch     # noqa: SLF001
+
+            async def patch(ns, name, body):
+                out = await real_patch(ns, name, body)
+                if name == ph.name and (body["metadata"].get("annotations") or {}).get(
+                        "gpumounter.amd.com/owner-name") == "a":
+                    inf.epoch += 1
+                    inf.cache[key] = copy.deepcopy(before)
+                return out
+
+            async def slow_fetch(k):
+                if k == key:
+                    await asyncio.sleep(0.3)
+                return await real_fetch(k)
+            svc.ph.kube.patch_pod, inf._fetch = patch, slow_fetch               # noqa: SLF001
+            inf._task.cancel()
+            await asyncio.sleep(0)
+            code, first = await lc.add("default", "a", 1)
+            assert code == 200 and first["devices"][0]["placeholder"] == ph.name
+            code, second = await lc.add("default", "a", 1)
+            assert code == 200
+            await asyncio.sleep(0.5)
+            assert not await lc.audit("default", "a")
+    asyncio.run(main())
