@@ -79,10 +79,18 @@ class Placeholder:
     device_ids: Tuple[str, ...] = ()
     mode: str = "single"
     candidate: bool = False      # held by a trim/correction pick, not yet confirmed
-    # the owner Pod's uid as the view this object came from shows it ("" = none: standby). A
-    # warm-pool placeholder changes hands; its release applies only while it still has this
-    # owner (see _delete)
+    # the holder as the view this object came from shows it: the owner Pod's uid ("" = none:
+    # standby) and the attach that claimed or created it. A warm-pool placeholder changes hands,
+    # also back to the same Pod by a later attach; its release applies only while it still has
+    # this holder (see _delete)
     owner_uid: str = ""
+    attach_id: str = ""
+
+    def held_by_me(self, pod: dict) -> bool:
+        """``pod`` (the placeholder as the apiserver has it) still has this object's holder."""
+        ann = pod["metadata"].get("annotations") or {}
+        return (ann.get(ANN_OWNER_UID) or "") == self.owner_uid and \
+            (not self.attach_id or (ann.get(ANN_ATTACH_ID) or "") == self.attach_id)
 
 
 @dataclass
@@ -453,7 +461,8 @@ class PlaceholderManager:
         created = [Placeholder(r["metadata"]["namespace"], r["metadata"]["name"],
                                r["metadata"]["uid"], (),
                                r["metadata"]["annotations"].get(ANN_MOUNT_MODE, "single"),
-                               owner_uid=r["metadata"]["annotations"].get(ANN_OWNER_UID, ""))
+                               owner_uid=r["metadata"]["annotations"].get(ANN_OWNER_UID, ""),
+                               attach_id=r["metadata"]["annotations"].get(ANN_ATTACH_ID, ""))
                    for r in results if isinstance(r, dict)]
         for r in results:
             if isinstance(r, dict):
@@ -642,18 +651,14 @@ class PlaceholderManager:
         if not p.name.startswith(STANDBY_PREFIX):
             return await self.kube.delete_pod(p.namespace, p.name, grace_period_s=0,
                                               uid=p.uid or "")
-        owner = p.owner_uid
-
-        def owner_of(pod: dict) -> str:
-            return (pod["metadata"].get("annotations") or {}).get(ANN_OWNER_UID) or ""
-        # the cached version only if the cache agrees on the owner; else one read now
+        # the cached version only if the cache agrees on the holder; else one read now
         seen = self.informer.cache.get((p.namespace, p.name))
         if seen is None or (p.uid and seen["metadata"].get("uid") != p.uid) or \
-                owner_of(seen) != owner:
+                not p.held_by_me(seen):
             seen = await self.kube.get_pod(p.namespace, p.name)
             if p.uid and seen["metadata"].get("uid") != p.uid:
                 raise NotFound(404, f"{p.name}: another pod of that name")
-            if owner_of(seen) != owner:
+            if not p.held_by_me(seen):
                 raise Reowned(p.name)
         rv = seen["metadata"].get("resourceVersion", "")
         for _ in range(3):
@@ -664,7 +669,7 @@ class PlaceholderManager:
                 cur = await self.kube.get_pod(p.namespace, p.name)
                 if p.uid and cur["metadata"].get("uid") != p.uid:
                     raise NotFound(404, f"{p.name}: another pod of that name") from None
-                if owner_of(cur) != owner:
+                if not p.held_by_me(cur):
                     raise Reowned(p.name) from None
                 rv = cur["metadata"].get("resourceVersion", "")
         raise ApiError(409, f"{p.name} kept changing while being deleted")
@@ -739,7 +744,8 @@ class PlaceholderManager:
         ann = md.get("annotations") or {}
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""),
                            tuple(ledger_ids.get(key, ())), ann.get(ANN_MOUNT_MODE, "single"),
-                           ANN_CANDIDATE in ann, ann.get(ANN_OWNER_UID) or "")
+                           ANN_CANDIDATE in ann, ann.get(ANN_OWNER_UID) or "",
+                           ann.get(ANN_ATTACH_ID) or "")
 
     def cached(self, p: dict) -> Optional[Placeholder]:
         """Placeholder with its device IDs from the admission cache (None if unknown)."""
@@ -750,4 +756,4 @@ class PlaceholderManager:
         ann = md.get("annotations") or {}
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""), ids,
                            ann.get(ANN_MOUNT_MODE, "single"), ANN_CANDIDATE in ann,
-                           ann.get(ANN_OWNER_UID) or "")
+                           ann.get(ANN_OWNER_UID) or "", ann.get(ANN_ATTACH_ID) or "")

@@ -45,10 +45,6 @@ class ClaimTaken(Exception):
     """The standby placeholder was claimed (or deleted) by someone else since it was chosen."""
 
 
-def _owner_uid(p: dict) -> Optional[str]:
-    return (p["metadata"].get("annotations") or {}).get(ANN_OWNER_UID)
-
-
 def is_standby(p: dict) -> bool:
     return (p["metadata"].get("annotations") or {}).get(ANN_MOUNT_MODE) == MODE_STANDBY
 
@@ -278,13 +274,13 @@ class WarmPool:
                     _log.info("standby placeholder(s) %s claimed elsewhere; falling back",
                               [ph.name for ph in taken])
                 if stray:
-                    for ph in stray:            # deleted only while still this Pod's
-                        ph.owner_uid = podu.uid_of(owner)
+                    for ph in stray:            # deleted only while still this attach's
+                        ph.owner_uid, ph.attach_id = podu.uid_of(owner), attach_id
                     await self.ph.release(stray, wait=False)
                 return None
             for ph in chosen:
                 ph.mode = mode
-                ph.owner_uid = podu.uid_of(owner)
+                ph.owner_uid, ph.attach_id = podu.uid_of(owner), attach_id
             if self.metrics is not None:
                 self.metrics.reconcile_actions.labels(action="pool_claim").inc(len(chosen))
         self.poke()
@@ -412,14 +408,12 @@ class WarmPool:
             cache = {p["metadata"]["uid"]: p for p in self.ph.live()}
 
             def put(ph: Placeholder):
-                # at the cached version if the cache agrees it has the owner the caller's view
+                # at the cached version if the cache agrees it has the holder the caller's view
                 # showed, else at a version read now
-                def ours(cur):
-                    return (_owner_uid(cur) or "") == ph.owner_uid
                 seen = cache.get(ph.uid)
                 rv = seen["metadata"].get("resourceVersion") \
-                    if seen is not None and ours(seen) else None
-                return self._put_back(ph, ours, rv)
+                    if seen is not None and ph.held_by_me(seen) else None
+                return self._put_back(ph, ph.held_by_me, rv)
             with trace.span("pool_return", placeholders=len(keep)):
                 res = await asyncio.gather(*[put(ph) for ph in keep], return_exceptions=True)
             back, theirs = self._sort_back(keep, res)

@@ -172,6 +172,9 @@ SCENARIO = {"ops": [("claim", 0, 0, 1), ("claim", 1, 1, 1)], "schedule": []}
 # a claim PATCH applied behind a lost reply, then the undo's read fails: the placeholder is
 # deleted as this attach's stray, which must not be mistaken for someone else's
 STRAY = {"ops": [("claim", 0, 0, 1)], "schedule": ["lost", "before"]}
+# the same Pod claims through a stale cache what its earlier attach holds, and every read after
+# the conflict fails: the failed attach's clean-up must not delete the earlier attach's claim
+SAME_POD = {"ops": [("claim", 0, 0, 1), ("claim", 1, 0, 1)], "schedule": ["ok", "before", "before"]}
 
 
 def run_scenario(inv, ops, schedule):
@@ -255,6 +258,7 @@ def inv(mock_inventory):
 @given(ops=OPS, schedule=s.lists(OUTCOMES, max_size=20))
 @example(**SCENARIO)
 @example(**STRAY)
+@example(**SAME_POD)
 def test_a_standby_placeholder_is_never_held_by_two_claims(inv, ops, schedule):
     problems = run_scenario(inv, ops, schedule)
     assert not problems, problems[:3]
