@@ -449,6 +449,22 @@ class PlaceholderManager:
                 # an unreserved claim holds no device; the reconciler deletes leftovers
                 _log.warning("delete resourceclaim %s/%s: %s", ns, n, r)
 
+    async def _delete_unused_claims(self, keys: Sequence[Tuple[str, str]]) -> None:
+        """After a failed Pod create: delete the ResourceClaims of the Pods that do not exist.
+        A create whose reply was lost may have happened, and a warm-pool placeholder created so
+        can already be claimed by an attach: its claim holds that attach's GPU. A claim whose
+        Pod could not be read is left to the reconciler, which deletes claims without a Pod."""
+        async def absent(ns: str, name: str) -> bool:
+            try:
+                await self.kube.get_pod(ns, name)
+            except NotFound:
+                return True
+            except Exception:  # noqa: BLE001 - unknown: keep it
+                return False
+            return False
+        gone = await asyncio.gather(*[absent(ns, n) for ns, n in keys])
+        await self._delete_claims([k for k, g in zip(keys, gone) if g])
+
     async def _create(self, bodies: List[dict]) -> List[Placeholder]:
         with trace.span("ledger_reserve", placeholders=len(bodies)):
             self.faults.check("ledger_reserve")
@@ -471,9 +487,9 @@ class PlaceholderManager:
         if errors:
             await self.release(created, wait=False)
             if self.dra:
-                await self._delete_claims([(b["metadata"]["namespace"], b["metadata"]["name"])
-                                           for b, r in zip(bodies, results)
-                                           if not isinstance(r, dict)])
+                await self._delete_unused_claims(
+                    [(b["metadata"]["namespace"], b["metadata"]["name"])
+                     for b, r in zip(bodies, results) if not isinstance(r, dict)])
             quota = [e for e in errors if isinstance(e, ApiError) and e.status == 403
                      and "exceeded quota" in _message(e)]
             if quota:   # tenant-namespace placeholders: the apiserver's quota admission said no

@@ -183,8 +183,8 @@ class WarmPool:
                     pod = await self.ph.kube.create_pod(self.cfg.pool_namespace, body)
                 except Exception as e:  # noqa: BLE001
                     _log.warning("standby create failed: %s", e)
-                    if self.ph.dra:
-                        await self.ph._delete_claims(  # noqa: SLF001
+                    if self.ph.dra:     # unless the create happened after all (see there)
+                        await self.ph._delete_unused_claims(  # noqa: SLF001
                             [(self.cfg.pool_namespace, body["metadata"]["name"])])
                     break
                 self.ph.informer.upsert(pod, epoch)  # pending() counts it from here on

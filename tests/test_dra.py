@@ -313,3 +313,30 @@ def test_dra_tenant_own_claim_gpus_are_not_removable():
         assert (code, text) == (400, "Invalid UUIDs: " + own_uuid + "\n")
         assert not await lc.audit("default", "t")
     run(body)
+
+
+def test_dra_a_standby_created_behind_a_failed_reply_keeps_its_claim():
+    """The pool's create of a standby placeholder can fail after it happened (reply lost, the
+    retry meets 409 because an attach already claimed the new placeholder and changed it). Its
+    ResourceClaim then holds that attach's GPU: deleting it as the failed create's leftover took
+    the GPU from the ledger under the mounted Pod (chaos: DRA + warm pool 3 + leases, seed 83)."""
+    from gpumounter_amd.cluster.kube import Conflict
+
+    async def body(lc):
+        pool = lc.nodes["node-0"].worker.pool
+        await until(lambda: len(pool.standby()) == 1)
+        kube = pool.ph.kube
+        real_create = kube.create_pod
+        made = []
+
+        async def create(ns, pod):
+            out = await real_create(ns, pod)
+            made.append(out["metadata"]["name"])
+            raise Conflict(409, f'pods "{out["metadata"]["name"]}" already exists')
+        kube.create_pod = create
+        pool.target = 2
+        await pool.refill()
+        kube.create_pod = real_create
+        assert made and ("gpu-pool", made[0]) in claims(lc)    # the Pod exists: its claim stays
+        assert lc.cluster.get("gpu-pool", made[0]) is not None
+    run(body, worker_overrides={"warm_pool_size": 1})
