@@ -357,7 +357,7 @@ def chaos(args) -> dict:
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": str(args.reconcile_period),
            "GM_WARM_POOL_SIZE": str(args.warm_pool), "GM_PLACEMENT_ENFORCE": args.placement}
     if args.log_dir:
-        env["GM_LOG_LEVEL"] = "INFO"       # kept logs are for post-mortems
+        env["GM_LOG_LEVEL"] = "DEBUG"      # kept logs are for post-mortems
     busy = _BusyTenants(tenants, args.busy_pool) if args.busy else None
     if busy is not None:
         env.update({"GM_AMDSMI_MOCK_PROCS": busy.table, "GM_BUSY_DETECTION": "both",
@@ -510,10 +510,19 @@ def chaos(args) -> dict:
                 while not converged():
                     if time.perf_counter() - t0 > 20:
                         problems.append(f"round {rnd_i}: not converged after 20 s: {why[0]}")
-                        if args.log_dir:      # what the worker is waiting for
+                        if args.log_dir:      # what the worker is waiting for, and the state
                             with open(os.path.join(args.log_dir,
                                                    f"tasks_round{rnd_i}.txt"), "w") as fh:
                                 fh.write(pc.worker_tasks())
+                            with open(os.path.join(args.log_dir,
+                                                   f"state_round{rnd_i}.json"), "w") as fh:
+                                json.dump({"audit": {t: pc.audit("default", t) for t in tenants},
+                                           "placeholders": [
+                                               {"name": p["metadata"]["name"],
+                                                "rv": p["metadata"].get("resourceVersion"),
+                                                "annotations": p["metadata"].get("annotations"),
+                                                "phase": p["status"].get("phase")}
+                                               for p in pc.placeholders()]}, fh, indent=1)
                         break
                     time.sleep(0.05)
                 converge.append((time.perf_counter() - t0) * 1e3)

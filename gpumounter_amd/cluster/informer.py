@@ -53,6 +53,14 @@ class PodInformer:
         # keys whose write-through a relist overtook, being re-read (see upsert): until then
         # the cache may show them older than this process's own acknowledged writes
         self._resolving: Dict[Key, int] = {}
+        # a relist replaces the cache with its list, which can be older than writes of ours
+        # acknowledged while it was in flight (a create the list does not hold at all): those
+        # are kept here and re-read once the relist is installed (see _relist)
+        self._relisting = False
+        self._written: Dict[Key, dict] = {}
+        # per key, how many write-throughs were acknowledged: a GET sent before one of them
+        # may answer with an older version, which must not replace it (see _resolve_once)
+        self._writes: Dict[Key, int] = {}
         self.handlers: List[Callable[[str, dict], None]] = []
 
     async def start(self) -> None:
@@ -90,6 +98,19 @@ class PodInformer:
             return None
 
     async def _relist(self) -> None:
+        self._relisting, self._written = True, {}
+        try:
+            written = await self._relist_once()
+        finally:
+            self._relisting, self._written = False, {}
+        # a write acknowledged while the relist was in flight may be older or newer than the
+        # list (or, a create, missing from it): a GET, newer than both, settles it. Queued
+        # before the RELIST handlers run, so whatever they trigger waits for it (``settled``)
+        for k in written:
+            self._resolve_soon(k)
+        await self._notify("RELIST", {})
+
+    async def _relist_once(self) -> List[Key]:
         items, rv = await self._list()
         fresh = {(p["metadata"]["namespace"], p["metadata"]["name"]): p for p in items}
         # our acknowledged writes the watch had not echoed yet: where the list holds another
@@ -118,9 +139,13 @@ class PodInformer:
             self.resolved += len(suspects)
         else:
             pending = {}
+        # our writes acknowledged meanwhile stand in for what the list lacks until re-read
+        written = dict(self._written)
         self._seen = {k: self._seen[k] for k in fresh if k in self._seen}
         for k, p in fresh.items():
             self._note(k, p["metadata"].get("resourceVersion", ""))
+        for k, p in written.items():
+            fresh.setdefault(k, p)
         for k in set(self.cache) - set(fresh):
             self._forget(k, self.cache[k]["metadata"].get("uid", ""))
         self.cache = fresh
@@ -129,7 +154,7 @@ class PodInformer:
         # a fetched version is newer than the list: the resumed watch's older events for
         # that key are skipped until it delivers this version (see _run)
         self._pending = {k: v for k, v in pending.items() if v}
-        await self._notify("RELIST", {})
+        return list(written)
 
     async def _notify(self, etype: str, pod: dict) -> None:
         for h in list(self.handlers):
@@ -202,6 +227,7 @@ class PodInformer:
                 backoff = min(backoff * 2, 5.0)
 
     def _forget(self, key: Key, uid: str) -> None:
+        self._writes.pop(key, None)
         self.deleted.pop(key, None)
         self.deleted[key] = uid
         while len(self.deleted) > DELETED_KEEP:
@@ -231,6 +257,7 @@ class PodInformer:
         rv = md.get("resourceVersion", "")
         if rv and rv in self._seen.get(key, ()):
             return
+        self._writes[key] = self._writes.get(key, 0) + 1
         if epoch is not None and epoch != self.epoch:
             cur = self.cache.get(key)
             if cur is not None and cur["metadata"].get("uid") == md.get("uid"):
@@ -243,6 +270,8 @@ class PodInformer:
         self.cache[key] = pod
         if rv:
             self._pending[key] = rv
+        if self._relisting:
+            self._written[key] = pod
 
     def _resolve_soon(self, key: Key) -> None:
         try:
@@ -277,13 +306,13 @@ class PodInformer:
         """Replace the cached ``key`` with a fresh GET, unless another relist overtook the GET
         (then the GET may be older than that list: try again)."""
         for _ in range(tries):
-            epoch = self.epoch
+            epoch, writes = self.epoch, self._writes.get(key, 0)
             try:
                 obj = await self._fetch(key)
             except Exception:  # noqa: BLE001 - the watch still converges; this only shortens it
                 return
-            if epoch != self.epoch:
-                continue
+            if epoch != self.epoch or writes != self._writes.get(key, 0):
+                continue        # a relist or a write of ours overtook the GET: maybe older
             self.resolved += 1
             if obj is not None and obj["metadata"].get("resourceVersion", "") in \
                     self._seen.get(key, ()):

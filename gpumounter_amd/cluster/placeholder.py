@@ -134,6 +134,9 @@ class PlaceholderManager:
     # consecutive "admitted per the apiserver, absent from the checkpoint" reads after which
     # the checkpoint counts as not maintained by this kubelet
     CHECKPOINT_MISSES = 3
+    # how long a tombstone outlives its object in the cache: a relist whose list is older than
+    # our delete still gets the DELETED event from the resumed watch (see _on_event)
+    TOMBSTONE_KEEP_S = 60.0
 
     def __init__(self, cfg, kube: KubeClient, ledger: LedgerClient, informer: PodInformer,
                  node_name: str, faults=None) -> None:
@@ -181,7 +184,12 @@ class PlaceholderManager:
             self._foreign_seen.pop(uid, None)
         elif etype == "RELIST":
             live = {p["metadata"].get("uid") for p in self.informer.cache.values()}
-            for uid in [u for u in self.tombstones if u not in live]:
+            # the watch resumes from the list's version, which can be older than a delete of
+            # ours: that DELETED event is still to come, and without its tombstone it reads as
+            # a foreign delete (a revocation under the Pod). Tombstones of deletes the list
+            # already left out go once they are old enough that no event for them is pending
+            old = asyncio.get_running_loop().time() - self.TOMBSTONE_KEEP_S
+            for uid in [u for u, t in self.tombstones.items() if u not in live and t < old]:
                 self.tombstones.pop(uid, None)
             for uid in [u for u in self.device_ids if u not in live]:
                 self.device_ids.pop(uid, None)
@@ -660,13 +668,11 @@ class PlaceholderManager:
 
     # ------------------------------------------------------------------------ release
     async def _delete(self, p: Placeholder) -> Optional[dict]:
-        """DELETE one placeholder. One made for a Pod belongs to it for life; a warm-pool one
-        is deleted only at a version at which it still has the owner the caller's view showed
-        (``p.owner_uid``), so a release decided on a stale view never takes a GPU from the Pod
-        that claimed it since (raises :class:`Reowned`)."""
-        if not p.name.startswith(STANDBY_PREFIX):
-            return await self.kube.delete_pod(p.namespace, p.name, grace_period_s=0,
-                                              uid=p.uid or "")
+        """DELETE one placeholder, only at a version at which it still has the holder the
+        caller's view showed (``p.owner_uid``, ``p.attach_id``), so a release decided on a stale
+        view never takes a GPU from the Pod that claimed it since (raises :class:`Reowned`).
+        Any placeholder can change hands, whatever its name: the surplus of a trim pick goes
+        back to the warm pool under its ``<pod>-slave-pod-`` name and is claimed from there."""
         # the cached version only if the cache agrees on the holder; else one read now
         seen = self.informer.cache.get((p.namespace, p.name))
         if seen is None or (p.uid and seen["metadata"].get("uid") != p.uid) or \
@@ -718,6 +724,8 @@ class PlaceholderManager:
                     if p.uid:
                         self.tombstones.pop(p.uid, None)
                 else:
+                    _log.debug("deleted placeholder %s/%s (owner %s)", p.namespace, p.name,
+                               p.owner_uid or "?")
                     # grace 0 + no finalizers: the object is gone from the apiserver (and the
                     # scheduler's books) once DELETE returns; drop it from the cached views
                     if p.uid:

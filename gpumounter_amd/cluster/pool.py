@@ -281,6 +281,8 @@ class WarmPool:
             for ph in chosen:
                 ph.mode = mode
                 ph.owner_uid, ph.attach_id = podu.uid_of(owner), attach_id
+            _log.debug("claimed %s for %s/%s attach %s", [ph.name for ph in chosen],
+                       podu.ns_of(owner), podu.name_of(owner), attach_id)
             if self.metrics is not None:
                 self.metrics.reconcile_actions.labels(action="pool_claim").inc(len(chosen))
         self.poke()
@@ -392,6 +394,7 @@ class WarmPool:
                 rv = None                               # changed since: read it again
                 continue
             self.ph.informer.upsert(r, epoch)
+            _log.debug("returned %s to the pool (was %s)", ph.name, ph.owner_uid or "?")
             return True
         raise Conflict(409, f"{ph.name} kept changing while being returned to the pool")
 

@@ -38,11 +38,33 @@ from typing import Dict, List, Optional
 
 from gpumounter_amd.cluster.kube import NotFound
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import (ANN_CANDIDATE, ANN_CONTAINER, ANN_INCARNATION,
-                                         ANN_OWNER_UID)
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTAINER,
+                                         ANN_INCARNATION, ANN_OWNER_UID)
 from gpumounter_amd.utils import log
 
 _log = log.get("worker.reconciler")
+
+Owner = tuple   # (name, namespace, uid) as a placeholder's labels and annotations name it
+
+
+def _held(p: dict) -> tuple:
+    """(namespace, name, uid, owner uid, attach id) of a placeholder as the cache holds it."""
+    md = p["metadata"]
+    ann = md.get("annotations") or {}
+    return (md["namespace"], md["name"], md.get("uid", ""), ann.get(ANN_OWNER_UID) or "",
+            ann.get(ANN_ATTACH_ID) or "")
+
+
+def _owner_of(p: dict) -> Optional[Owner]:
+    """The tenant a placeholder is booked for; None for warm-pool capacity (owned by the pool)
+    and a force-removed GPU waiting for its killed processes (worker/drain.py)."""
+    md = p["metadata"]
+    ann = md.get("annotations") or {}
+    if ann.get("gpumounter.amd.com/mount-mode") in ("standby", "draining"):
+        return None
+    return (ann.get("gpumounter.amd.com/owner-name", ""),
+            (md.get("labels") or {}).get("gpumounter.amd.com/owner-namespace", ""),
+            ann.get(ANN_OWNER_UID, ""))
 
 
 @dataclass
@@ -198,7 +220,8 @@ class Reconciler:
         ``drop`` that still exist, then reconcile the Pod to its ledger. Retried with backoff
         (the kubelet restarting, the apiserver failing) like an event reaction."""
         self._kick(("followup", ns, name,
-                    tuple(sorted((p.namespace, p.name, p.uid) for p in drop))))
+                    tuple(sorted((p.namespace, p.name, p.uid, p.owner_uid, p.attach_id)
+                                 for p in drop))))
 
     def _kick(self, key: tuple, attempt: int = 0) -> None:
         if key in self._kicked or self._stopping:
@@ -241,8 +264,7 @@ class Reconciler:
                         cands = [] if owner is None else [
                             p for p in svc.ph.owned_by(owner, candidates=True)
                             if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})]
-                        drop = set(key[3]) | {(p["metadata"]["namespace"], p["metadata"]["name"],
-                                               p["metadata"].get("uid", "")) for p in cands}
+                        drop = set(key[3]) | {_held(p) for p in cands}
                         if drop:
                             await self._drop(sorted(drop))
                     if owner is None or podu.phase_of(owner) != "Running":
@@ -278,18 +300,24 @@ class Reconciler:
             self._retry(key, attempt + 1)
 
     async def _drop(self, phs) -> None:
-        """Release the placeholders of a failed attach that still exist (same UID)."""
+        """Release the placeholders of a failed attach that still exist (same UID), each only
+        while it has the holder the attach left it with: one that went back to the warm pool
+        and was claimed since (by another Pod, or by a later attach of this one) is not the
+        failed attach's to release (cluster/placeholder.py ``_delete``, pool ``give_back``)."""
         svc = self.svc
         left = []
-        for ns, name, uid in phs:
+        for ns, name, uid, owner_uid, attach_id in phs:
             p = svc.ph.informer.cache.get((ns, name))
             if p is not None and (not uid or p["metadata"].get("uid") == uid) and \
                     not p["metadata"].get("deletionTimestamp"):
-                left.append(svc.ph.cached(p) or svc.ph.from_pod(p, {}))
+                ph = svc.ph.cached(p) or svc.ph.from_pod(p, {})
+                ph.owner_uid, ph.attach_id = owner_uid, attach_id
+                left.append(ph)
         if left:
             await svc._release(left)
             svc.metrics.reconcile_actions.labels(action="followup_release").inc(len(left))
-        svc.abandoned.difference_update(uid for _, _, uid in phs)
+        for _, _, uid, _, _ in phs:
+            svc.abandoned.pop(uid, None)
 
     async def start(self) -> None:
         self._task = asyncio.ensure_future(self._loop())
@@ -393,6 +421,19 @@ class Reconciler:
             svc.metrics.reconcile_actions.labels(action="claim_delete").inc(len(out))
         return out
 
+    async def _owned_now(self, owner: Owner) -> Optional[List[dict]]:
+        """``owner``'s placeholders as the informer holds them now, once no write-through of
+        ours is waiting to be re-read after a relist (see ``WorkerService.pod_state``); None if
+        the view did not settle in time."""
+        inf = self.svc.ph.informer
+        if not getattr(inf, "settled", True):
+            try:
+                await inf.wait_for(lambda: inf.settled,
+                                   getattr(self.svc, "SETTLE_WAIT_S", 2.0))
+            except asyncio.TimeoutError:
+                return None
+        return [p for p in self.svc.ph.live() if _owner_of(p) == owner]
+
     async def run_once(self) -> ReconcileReport:
         svc = self.svc
         rep = ReconcileReport()
@@ -419,17 +460,11 @@ class Reconciler:
         ck = svc.ph.checkpoint
         from_ckpt = ck is not None and ck.trusted and ck.snapshot() is not None
         placeholders = svc.ph.live()
-        by_owner: Dict[tuple, List[dict]] = {}
+        by_owner: Dict[Owner, List[dict]] = {}
         for p in placeholders:
-            ann = p["metadata"].get("annotations") or {}
-            if ann.get("gpumounter.amd.com/mount-mode") in ("standby", "draining"):
-                # warm-pool capacity (owned by the pool), or a force-removed GPU waiting for
-                # its killed processes to exit (worker/drain.py): no tenant to audit
-                continue
-            owner = (ann.get("gpumounter.amd.com/owner-name", ""),
-                     (p["metadata"].get("labels") or {}).get("gpumounter.amd.com/owner-namespace", ""),
-                     ann.get(ANN_OWNER_UID, ""))
-            by_owner.setdefault(owner, []).append(p)
+            owner = _owner_of(p)
+            if owner is not None:
+                by_owner.setdefault(owner, []).append(p)
         now = time.monotonic()
         async def fresh(ns: str, name: str):
             try:
@@ -450,7 +485,8 @@ class Reconciler:
                 m.orphans.labels(kind="owner_gone").inc()
             await svc.ph.release([svc.ph.from_pod(p, {}) for p in phs], wait=False)
 
-        for (oname, ons, ouid), phs in by_owner.items():
+        for key in by_owner:
+            oname, ons, ouid = key
             # the node informer already holds every pod of this node; the apiserver is only
             # asked to confirm an owner the cache shows gone/replaced, or whose repair failed
             owner = svc.node_pods.get(ons, oname)
@@ -459,21 +495,34 @@ class Reconciler:
             lock = svc.pod_lock(ons, oname)
             if gone(owner, ouid):
                 async with lock:
-                    await collect(ons, oname, phs)
+                    phs = await self._owned_now(key)
+                    if phs is None:
+                        rep.errors.append(f"{ons}/{oname}: placeholder view not settled")
+                    elif phs:
+                        await collect(ons, oname, phs)
                 continue
             if lock.locked():
                 continue  # an attach/detach is in flight for this owner
             async with lock:
+                # the snapshot above is older than this lock: an attach that held it meanwhile
+                # confirmed its pick (candidates no more) or added or released placeholders.
+                # Judged from that snapshot, a just-confirmed pick reads as abandoned and is
+                # released under the Pod it was mounted in
+                phs = await self._owned_now(key)
+                if phs is None:
+                    rep.errors.append(f"{ons}/{oname}: placeholder view not settled")
+                    continue
                 # candidates of a trim/correction pick whose attach is not running (its worker
                 # died mid-pick): never the owner's, never mounted — give the GPUs back
                 # and placeholders of failed attaches whose release the follow-up gave up on
                 cands = [p for p in phs
                          if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})
-                         or p["metadata"].get("uid") in svc.abandoned]
+                         or svc.is_abandoned(p)]
                 if cands:
                     rep.stuck += [p["metadata"]["name"] for p in cands]
                     await svc.ph.release([svc.ph.from_pod(p, {}) for p in cands], wait=False)
-                    svc.abandoned.difference_update(p["metadata"].get("uid") for p in cands)
+                    for p in cands:
+                        svc.abandoned.pop(p["metadata"].get("uid", ""), None)
                     phs = [p for p in phs if p not in cands]
                     m.reconcile_actions.labels(action="candidate_release").inc(len(cands))
                 # stuck placeholders (never admitted). One that an earlier worker process

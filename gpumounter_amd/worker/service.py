@@ -39,7 +39,8 @@ from gpumounter_amd.hw import topology
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu, normalize_device_id
-from gpumounter_amd.models.types import (ANN_IDEMPOTENCY, ANN_MOUNT_MODE, ANN_OWNER_UID,
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_IDEMPOTENCY, ANN_MOUNT_MODE,
+                                         ANN_OWNER_UID,
                                          ERR_INTERNAL, ERR_POLICY, ERR_QUOTA, LABEL_OWNER_NS,
                                          MODE_DRAINING, MODE_STANDBY, MountType)
 from gpumounter_amd.node import procs
@@ -125,8 +126,10 @@ class GpuMountService:
         # the periodic sweep (30 s as shipped)
         self.followup = None
         # placeholders of failed attaches whose release is being retried: never replayed as a
-        # success under the attach's idempotency key (the client was told it failed)
-        self.abandoned: set = set()
+        # success under the attach's idempotency key (the client was told it failed). uid →
+        # (owner uid, attach id): one that went back to the warm pool and was claimed since is
+        # its new holder's, not abandoned
+        self.abandoned: Dict[str, Tuple[str, str]] = {}
 
     # ------------------------------------------------------------------------ helpers
     def pod_lock(self, ns: str, name: str) -> asyncio.Lock:
@@ -217,7 +220,7 @@ class GpuMountService:
         # or a later attach of the same pod must not mount it (it is schedulable once deleted);
         # nor is a force-removed one whose draining mark is still being retried (worker/drain.py)
         owned = [p for p in self.ph.owned_by(pod)
-                 if p["metadata"].get("uid") not in self.abandoned
+                 if not self.is_abandoned(p)
                  and p["metadata"].get("uid") not in self.drain.unmarked]
         uid = podu.uid_of(pod)
         cached = [self.ph.cached(p) for p in owned]
@@ -288,6 +291,9 @@ class GpuMountService:
             return []
         missing = [i for i in issues if i.kind.startswith("missing")]
         stale = [i for i in issues if i.kind.startswith("stale")]
+        log.kv(_log, 20, "repairing", pod=f"{podu.ns_of(pod)}/{podu.name_of(pod)}",
+               hot=[g.bdf for g in st.hot], placeholders=[ph.name for ph in st.placeholders],
+               issues=sorted({f"{i.kind} {i.path}" for i in issues}))
         if missing:
             self.hm.repair(pod, missing, st.hot, st.own)
         if stale:
@@ -356,10 +362,19 @@ class GpuMountService:
             self._follow_up(pod)
         return False
 
+    def is_abandoned(self, p: dict) -> bool:
+        """``p`` is a failed attach's placeholder, still held by that attach."""
+        held = self.abandoned.get(p["metadata"].get("uid", ""))
+        if held is None:
+            return False
+        ann = p["metadata"].get("annotations") or {}
+        return (ann.get(ANN_OWNER_UID) or "") == held[0] and \
+            (not held[1] or (ann.get(ANN_ATTACH_ID) or "") == held[1])
+
     def _follow_up(self, pod: dict, drop: Sequence[Placeholder] = ()) -> None:
         """Hand what this operation could not finish to the reconciler's retrying follow-up:
         release ``drop`` (placeholders of a failed attach) and reconcile the pod to its ledger."""
-        self.abandoned.update(p.uid for p in drop if p.uid)
+        self.abandoned.update({p.uid: (p.owner_uid, p.attach_id) for p in drop if p.uid})
         if self.followup is not None:
             self.followup(podu.ns_of(pod), podu.name_of(pod), drop)
 
@@ -558,7 +573,7 @@ class GpuMountService:
         annotation would otherwise hand back GPUs that never expire."""
         raw = {p["metadata"]["name"]: p for p in self.ph.owned_by(pod)
                if (p["metadata"].get("annotations") or {}).get(ANN_IDEMPOTENCY) == key
-               and p["metadata"].get("uid") not in self.abandoned
+               and not self.is_abandoned(p)
                and p["metadata"].get("uid") not in self.drain.unmarked}
         mine = set(raw)
         if not mine:

@@ -166,7 +166,7 @@ def make_service(inv, api):
     svc.faults = FaultInjector("")
     svc.metrics = Metrics()
     svc.unhealthy = set()
-    svc.abandoned = set()
+    svc.abandoned = {}
     svc.drops = []
     svc.followup = lambda ns, name, drop: svc.drops.append(list(drop))
     return svc
@@ -239,7 +239,7 @@ def test_correction_never_mounts_an_unbooked_gpu_and_leaks_nothing(inv, taken, n
         svc.drops.append([])
     if out is not None:
         check_booked(api, out, n)
-        assert not {p.uid for p in out.placeholders} & svc.abandoned
+        assert not {p.uid for p in out.placeholders} & set(svc.abandoned)
     follow_up(api, svc)
     mine = {p.uid for p in out.placeholders} if out is not None else set()
     assert set(api.pods) == mine, (api.calls, api.pods, mine)

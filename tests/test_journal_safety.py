@@ -276,6 +276,47 @@ def test_candidates_left_by_a_dead_pick_are_never_mounted_and_are_released():
     run(body, worker_overrides={"reconcile_on_events": False})
 
 
+def test_a_sweep_does_not_release_a_pick_confirmed_after_its_snapshot():
+    """A sweep lists the placeholders once, then takes each owner's lock in turn. A trim pick
+    that held the lock when the list was taken has confirmed its kept placeholder by the time
+    the sweep gets the lock. Judged from the list, that placeholder was still a candidate of a
+    pick that is not running, so the sweep released it and revoked a GPU the tenant had been
+    answered (chaos seed 110: a trim attach answered 200, and its GPU left the ledger 12 ms
+    later). The sweep judges what the owner holds once it has the lock."""
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        snap = []
+        confirm = svc.ph.confirm
+
+        async def confirm_spy(phs):
+            snap.append(svc.ph.live())            # the sweep's list, taken mid-pick
+            await confirm(phs)
+        svc.ph.confirm = confirm_spy
+        code, b = await lc.add("default", "t", 1)
+        assert code == 200 and snap
+        svc.ph.confirm = confirm
+        # the sweep lists before it takes the first owner's lock; everything after reads now
+        live, pod_lock, listing = svc.ph.live, svc.pod_lock, [True]
+
+        def listed():
+            return snap[0] if listing[0] else live()
+
+        def lock(ns, name):
+            listing[0] = False
+            return pod_lock(ns, name)
+        svc.ph.live, svc.pod_lock = listed, lock
+        try:
+            rep = await lc.nodes["node-0"].worker.reconciler.run_once()
+        finally:
+            svc.ph.live, svc.pod_lock = live, pod_lock
+        assert not listing[0] and not rep.stuck, rep
+        st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+        assert [g.uuid for g in st.hot] == [b["devices"][0]["uuid"]]
+        assert not await lc.audit("default", "t")
+    run(body, worker_overrides={"reconcile_on_events": False, "placement_enforce": "trim"})
+
+
 # ------------------------------------------------------------------------------ long-lived worker
 def test_per_pod_caches_do_not_grow_with_pods_that_left():
     """A worker lives for the node's lifetime and sees many short-lived tenants: the per-pod

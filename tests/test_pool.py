@@ -8,6 +8,7 @@ import pytest
 from gpumounter_amd.cluster.pool import is_standby
 from gpumounter_amd.fakes.apiserver import LatencyModel
 from gpumounter_amd.fakes.harness import LocalCluster
+from gpumounter_amd.models.device import normalize_device_id
 
 
 async def wait_pool(lc, n, timeout=5.0):
@@ -219,6 +220,43 @@ def test_give_back_leaves_a_placeholder_claimed_anew_with_its_new_owner(room):
                 pool.target = 3
             await pool.give_back([ph])
             assert owner_of(lc, ph.name) == "b"
+    asyncio.run(main())
+
+
+@pytest.mark.parametrize("room", [True, False])
+def test_a_late_follow_up_leaves_a_slave_pod_claimed_from_the_pool_with_its_holder(room):
+    """A failed attach hands its placeholders to the reconciler's follow-up. One of them, a
+    ``<pod>-slave-pod-`` (not a ``gpumounter-standby-`` name: a pick's surplus goes back to the
+    pool under its own name), went back to the pool and another Pod claimed it. The follow-up
+    must neither return it to the pool nor delete it, and the failed attach's 'abandoned' mark
+    must not hide it from its new owner's ledger view (chaos seed 114 saw a slave pod claimed
+    from the pool; the delete path only checked holders of ``gpumounter-standby-`` names)."""
+    async def main():
+        async with LocalCluster(worker_overrides={"warm_pool_size": 1,
+                                                  "reconcile_on_events": False}) as lc:
+            pool = await wait_pool(lc, 1)
+            w = lc.nodes["node-0"].worker
+            svc = w.service
+            lc.tenant("a")
+            lc.tenant("b")
+            a, b = lc.cluster.get("default", "a"), lc.cluster.get("default", "b")
+            res = await svc.ph.reserve(a, 1, False, attach_id="add-a")
+            (ph,) = res.placeholders
+            assert ph.name.startswith("a-slave-pod-") and ph.owner_uid == a["metadata"]["uid"]
+            assert await pool._put_back(ph, ph.held_by_me) is True       # back in the pool
+            idx = lc.inventory.by_key()[normalize_device_id(ph.device_ids[0])].index
+            got = await pool.claim(b, 1, False, [], attach_id="add-b", want=[idx])
+            assert got is not None and got.placeholders[0].name == ph.name
+            if not room:
+                pool.target = 0
+            svc._follow_up(a, [ph])            # the failed attach's follow-up, late
+            for _ in range(100):
+                await asyncio.sleep(0.01)
+                if not svc.abandoned:
+                    break
+            assert owner_of(lc, ph.name) == "b"
+            st = await svc.pod_state(lc.cluster.get("default", "b"), fresh=True)
+            assert [p.name for p in st.placeholders] == [ph.name]
     asyncio.run(main())
 
 

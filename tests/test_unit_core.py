@@ -437,6 +437,140 @@ def test_informer_relist_resolves_our_unechoed_writes_with_a_get():
     asyncio.run(main())
 
 
+def test_informer_relist_keeps_writes_acknowledged_while_it_was_in_flight():
+    """A relist installs its list only after the GETs of its suspects, which a rate-limiting
+    apiserver can stretch to hundreds of ms. A create and a PATCH of ours acknowledged in that
+    window went into the cache the relist then replaced with a list served before them: the
+    just-created placeholders vanished from the view, and a reconcile revoked the GPUs they had
+    just had mounted (chaos seed 114). They stand in until a GET settles them."""
+    import asyncio
+
+    from gpumounter_amd.cluster.informer import PodInformer
+
+    def pod(name, rv, v):
+        return {"metadata": {"namespace": "ns", "name": name, "uid": "u-" + name,
+                             "resourceVersion": rv, "annotations": {"v": v}}}
+
+    server = {"a": pod("a", "1", "v1")}
+    gate = asyncio.Event()
+
+    class Kube:
+        async def get_pod(self, ns, name):
+            if name == "a" and not gate.is_set():
+                await gate.wait()                   # the suspect's GET is slow
+            if name not in server:
+                from gpumounter_amd.cluster.kube import NotFound
+                raise NotFound(404, name)
+            return server[name]
+
+    class Feed(PodInformer):
+        def __init__(self):
+            super().__init__(kube=Kube())
+            self.listed = [pod("a", "1", "v1")]
+
+        async def _list(self):
+            return list(self.listed), "2"
+
+        async def _watch(self, timeout_s):
+            await asyncio.Event().wait()
+            yield                                   # never delivers
+
+    async def main():
+        inf = Feed()
+        await inf.start()
+        inf.upsert(pod("a", "2", "ours"), inf.epoch)    # unechoed: a suspect of the relist
+        inf.listed = [pod("a", "1", "v1")]
+        relist = asyncio.ensure_future(inf._relist())
+        await asyncio.sleep(0.01)                       # listed; its GET is in flight
+        server["a"] = pod("a", "3", "patched")
+        inf.upsert(pod("a", "3", "patched"), inf.epoch)     # acknowledged meanwhile
+        server["b"] = pod("b", "4", "created")
+        inf.upsert(pod("b", "4", "created"), inf.epoch)
+        gate.set()
+        await relist
+        assert inf.get("ns", "b") is not None, "a create acknowledged during the relist is lost"
+        await inf.wait_for(lambda: inf.settled, 1.0)
+        assert inf.get("ns", "a")["metadata"]["annotations"]["v"] == "patched"
+        assert inf.get("ns", "b")["metadata"]["annotations"]["v"] == "created"
+        await inf.stop()
+    asyncio.run(main())
+
+
+def test_a_delete_of_ours_older_than_the_relist_is_not_read_as_foreign():
+    """Our DELETE lands after a relist's list was served: the relist leaves the object out (its
+    suspect GET found it gone), and the watch, resumed from the list's version, then delivers
+    the DELETED event. Pruning the tombstone at the relist made that event a foreign delete: a
+    revocation reaction under the owner (chaos seed 114, 'deleted externally' for a pick's
+    surplus the attach had just released)."""
+    import asyncio
+
+    from gpumounter_amd.cluster.informer import PodInformer
+    from gpumounter_amd.cluster.placeholder import PlaceholderManager
+
+    async def main():
+        inf = PodInformer(kube=None)
+        ph = PlaceholderManager(None, None, None, inf, "node-0")
+        foreign = []
+        ph.on_foreign_delete.append(foreign.append)
+        now = asyncio.get_running_loop().time()
+        ph.tombstones["u1"] = now                                   # our DELETE just went out
+        ph.tombstones["u0"] = now - ph.TOMBSTONE_KEEP_S - 1         # an old one, event missed
+        ph._on_event("RELIST", {})                                   # the list holds neither
+        assert "u0" not in ph.tombstones and "u1" in ph.tombstones
+        ph._on_event("DELETED", {"metadata": {"namespace": "p", "name": "x", "uid": "u1"}})
+        assert not foreign
+    asyncio.run(main())
+
+
+def test_informer_resolve_does_not_replace_a_newer_write_of_ours():
+    """A GET that settles a key after a relist was sent before our next PATCH of that key and
+    answers after it: its (older) object must not replace the PATCH's, or the cache would also
+    skip the watch's event for the PATCH as older than what it holds."""
+    import asyncio
+
+    from gpumounter_amd.cluster.informer import PodInformer
+
+    def pod(rv, v):
+        return {"metadata": {"namespace": "ns", "name": "p", "uid": "u", "resourceVersion": rv,
+                             "annotations": {"v": v}}}
+
+    server = {"obj": pod("5", "first")}
+    answers = []
+
+    class Kube:
+        async def get_pod(self, ns, name):
+            obj = server["obj"]                     # read when the request is served...
+            if not answers:
+                answers.append(obj)
+                await asyncio.sleep(0.05)           # ...answered late the first time
+            return obj
+
+    class Feed(PodInformer):
+        def __init__(self):
+            super().__init__(kube=Kube())
+
+        async def _list(self):
+            return [pod("1", "listed")], "1"
+
+        async def _watch(self, timeout_s):
+            await asyncio.Event().wait()
+            yield
+
+    async def main():
+        inf = Feed()
+        await inf.start()
+        ep = inf.epoch
+        await inf._relist()
+        inf.upsert(pod("5", "first"), ep)           # overtaken by the relist: a GET settles it
+        await asyncio.sleep(0.01)                   # the GET is served (rv 5), reply on its way
+        server["obj"] = pod("6", "second")
+        inf.upsert(pod("6", "second"), inf.epoch)   # our next PATCH, acknowledged first
+        await inf.wait_for(lambda: inf.settled, 1.0)
+        assert inf.get("ns", "p")["metadata"]["annotations"]["v"] == "second"
+        await inf.stop()
+    asyncio.run(main())
+
+
 def test_informer_relist_newer_than_our_write_does_not_stall_the_key():
     """The list holds a version newer than our unechoed write (someone wrote after us): the GET
     returns that same version, which the resumed watch will never deliver again — the key must
