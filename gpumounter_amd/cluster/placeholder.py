@@ -137,6 +137,8 @@ class PlaceholderManager:
     # how long a tombstone outlives its object in the cache: a relist whose list is older than
     # our delete still gets the DELETED event from the resumed watch (see _on_event)
     TOMBSTONE_KEEP_S = 60.0
+    # conditional DELETEs of one placeholder before a release gives up (see _delete)
+    DELETE_ATTEMPTS = 10
 
     def __init__(self, cfg, kube: KubeClient, ledger: LedgerClient, informer: PodInformer,
                  node_name: str, faults=None) -> None:
@@ -683,11 +685,15 @@ class PlaceholderManager:
             if not p.held_by_me(seen):
                 raise Reowned(p.name)
         rv = seen["metadata"].get("resourceVersion", "")
-        for _ in range(3):
+        for attempt in range(self.DELETE_ATTEMPTS):
             try:
                 return await self.kube.delete_pod(p.namespace, p.name, grace_period_s=0,
                                                   uid=p.uid or "", resource_version=rv)
             except Conflict:
+                # a placeholder being admitted changes with every status the kubelet posts: a
+                # conflict with the holder unchanged is that churn, which ends once it runs
+                if attempt >= 2:
+                    await asyncio.sleep(0.005 * attempt)
                 cur = await self.kube.get_pod(p.namespace, p.name)
                 if p.uid and cur["metadata"].get("uid") != p.uid:
                     raise NotFound(404, f"{p.name}: another pod of that name") from None

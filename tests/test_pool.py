@@ -260,6 +260,32 @@ def test_a_late_follow_up_leaves_a_slave_pod_claimed_from_the_pool_with_its_hold
     asyncio.run(main())
 
 
+def test_release_of_a_placeholder_in_status_churn_still_deletes_it():
+    """Releases are conditional on the placeholder's version. One being admitted changes with
+    every status the kubelet posts, so a release right after its create meets conflicts with
+    the holder unchanged: it must retry through them, not give up after three and leave the
+    GPU booked under an attach that failed (chaos seeds 120, 121, 123)."""
+    async def main():
+        async with LocalCluster() as lc:
+            svc = lc.nodes["node-0"].worker.service
+            lc.tenant("a")
+            res = await svc.ph.reserve(lc.cluster.get("default", "a"), 1, False,
+                                       attach_id="add-a")
+            (ph,) = res.placeholders
+            delete, churn = svc.ph.kube.delete_pod, [5]
+
+            async def churning(ns, name, **kw):
+                if churn[0]:                   # a status update lands first, five times
+                    churn[0] -= 1
+                    lc.cluster.patch(ns, name, {"metadata": {"annotations": {
+                        "churn": str(churn[0])}}})
+                return await delete(ns, name, **kw)
+            svc.ph.kube.delete_pod = churning
+            await svc.ph.release([ph], wait=False)
+            assert lc.cluster.get(ph.namespace, ph.name) is None
+    asyncio.run(main())
+
+
 def test_claim_whose_reply_was_lost_is_kept():
     """A conditional claim whose first attempt applied but whose reply was lost meets a
     conflict on its retry; the placeholder read back is this attach's own, so the claim
