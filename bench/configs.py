@@ -363,6 +363,7 @@ def chaos(args) -> dict:
         env.update({"GM_AMDSMI_MOCK_PROCS": busy.table, "GM_BUSY_DETECTION": "both",
                     "GM_KILL_GRACE_S": str(args.kill_grace)})
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
+                        master_env={"GM_LOG_LEVEL": "DEBUG"} if args.log_dir else None,
                         gpu_api=args.gpu_api, log_dir=args.log_dir) as pc, \
             (busy or contextlib.nullcontext()):
         for t in tenants:
@@ -416,9 +417,16 @@ def chaos(args) -> dict:
 
         holders = {}    # tenant → {uuid: placeholder holding it} as of the last ledger()
 
+        ledger_err = {}     # tenant → (code, answer, seconds) of its last failed ledger read
+
         def ledger(t):
-            code, g = pc.pod_gpus("default", t)
+            t0 = time.perf_counter()
+            try:
+                code, g = pc.pod_gpus("default", t)
+            except Exception as e:  # noqa: BLE001 - the master restarting, a read timeout
+                code, g = -1, {"error": repr(e)}
             if code != 200:
+                ledger_err[t] = (code, str(g)[:200], round(time.perf_counter() - t0, 3))
                 return None
             hm = [x for x in g.get("gpus", []) if x.get("source") == "hot-mount"]
             holders[t] = {x["uuid"]: x.get("pod_name") for x in hm}
@@ -431,7 +439,7 @@ def chaos(args) -> dict:
             for t in tenants:
                 hot = ledger(t)
                 if hot is None:
-                    why[0] = f"{t}: no ledger view"
+                    why[0] = f"{t}: no ledger view {ledger_err.get(t)}"
                     return False
                 issues = pc.audit("default", t)
                 if issues:
@@ -517,6 +525,8 @@ def chaos(args) -> dict:
                             with open(os.path.join(args.log_dir,
                                                    f"state_round{rnd_i}.json"), "w") as fh:
                                 json.dump({"audit": {t: pc.audit("default", t) for t in tenants},
+                                           "pod_gpus": {t: pc.pod_gpus("default", t)
+                                                        for t in tenants},
                                            "placeholders": [
                                                {"name": p["metadata"]["name"],
                                                 "rv": p["metadata"].get("resourceVersion"),

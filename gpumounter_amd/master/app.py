@@ -103,6 +103,7 @@ class WorkerDirectory:
         self.cfg = cfg
         self._channels: Dict[str, grpc.aio.Channel] = {}
         self._loop = None
+        self._targets: Dict[str, Optional[str]] = {}
 
     async def start(self) -> None:
         await self.informer.start()
@@ -113,6 +114,11 @@ class WorkerDirectory:
         """Open the channel to every running worker ahead of its first request: the TCP
         connect and the TLS handshake then happen in the background, not in an attach
         (reference: a new insecure connection per request, main.go:82)."""
+        targets = {podu.node_of(p): self.target(podu.node_of(p))
+                   for p in self.informer.cache.values()}
+        if targets != self._targets:
+            _log.debug("worker targets: %s", targets)
+            self._targets = targets
         for p in self.informer.cache.values():
             t = self.target(podu.node_of(p))
             if t is not None:
