@@ -418,10 +418,14 @@ class FakeCluster:
             return ctr.id
 
     def create_running_pod(self, ns: str, body: dict, node: str,
-                           pids: Optional[Dict[str, List[int]]] = None) -> dict:
-        """Test helper: a tenant pod that is already bound, admitted and running."""
+                           pids: Optional[Dict[str, List[int]]] = None,
+                           pod_ip: str = "") -> dict:
+        """Test helper: a tenant pod that is already bound, admitted and running (at
+        ``pod_ip`` from its first Running version on, when given)."""
         pod = self.create_pod(ns, body, schedule=False)
         pod["spec"]["nodeName"] = node
+        if pod_ip:
+            pod["status"]["podIP"] = pod_ip
         n = self.nodes[node]
         for c in pod["spec"].get("containers", []):
             want = int(podu.parse_quantity(

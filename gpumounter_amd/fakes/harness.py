@@ -185,14 +185,15 @@ class LocalCluster:
         wp = self.cluster.get("kube-system", f"gpu-mounter-worker-{name}")
         if wp is not None:
             self.cluster._remove("kube-system", wp["metadata"]["name"])  # noqa: SLF001
+        # reachable from its first Running version on: a master that read a placeholder
+        # address would send its next request to an unroutable IP and wait out the TCP
+        # connect (chaos: a 20 s ledger-read stall right after a worker restart)
         self.cluster.create_running_pod("kube-system", {
             "metadata": {"name": f"gpu-mounter-worker-{name}",
                          "labels": {"app": "gpu-mounter-worker"},
                          "annotations": {ANN_WORKER_PORT: str(port)}},
-            "spec": {"containers": [{"name": "worker", "image": "gpumounter-amd:dev"}]}}, name)
-        wpod = self.cluster.get("kube-system", f"gpu-mounter-worker-{name}")
-        wpod["status"]["podIP"] = ip
-        self.cluster._bump("MODIFIED", wpod)  # noqa: SLF001
+            "spec": {"containers": [{"name": "worker", "image": "gpumounter-amd:dev"}]}}, name,
+            pod_ip=ip)
 
     async def stop_worker(self, name: str) -> None:
         h = self.nodes[name]

@@ -502,7 +502,11 @@ class Reconciler:
                         await collect(ons, oname, phs)
                 continue
             if lock.locked():
-                continue  # an attach/detach is in flight for this owner
+                # an attach/detach is in flight for this owner: audit it right after, not a
+                # period later (the events this sweep stands in for, a container restart
+                # missed by a relist, say, will not come again)
+                self.follow_up(ons, oname)
+                continue
             async with lock:
                 # the snapshot above is older than this lock: an attach that held it meanwhile
                 # confirmed its pick (candidates no more) or added or released placeholders.
@@ -584,6 +588,7 @@ class Reconciler:
             key = (ent.namespace, ent.pod)
             lock = svc.pod_lock(*key)
             if lock.locked():
+                self.follow_up(*key)        # as above: once the operation in flight is done
                 continue
             async with lock:
                 if svc.ph.owned_by(pod):

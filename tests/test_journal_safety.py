@@ -13,6 +13,7 @@ import pytest
 
 from gpumounter_amd import _native
 from gpumounter_amd.fakes.harness import LocalCluster
+from gpumounter_amd.models import pod as podu
 from gpumounter_amd.node.hotmount import HotMount
 from gpumounter_amd.node.journal import InjectionJournal
 
@@ -315,6 +316,36 @@ def test_a_sweep_does_not_release_a_pick_confirmed_after_its_snapshot():
         assert [g.uuid for g in st.hot] == [b["devices"][0]["uuid"]]
         assert not await lc.audit("default", "t")
     run(body, worker_overrides={"reconcile_on_events": False, "placement_enforce": "trim"})
+
+
+def test_a_sweep_audits_an_owner_it_skipped_as_busy_once_the_operation_is_done():
+    """A relist can carry a tenant's container restart without any MODIFIED event: the sweep it
+    wakes is then the only repair. An owner whose lock an operation holds is skipped by the
+    sweep, and its new container stayed without its hot GPUs until the next periodic sweep,
+    30 s later (chaos seed 148: a failed attach of the same Pod held the lock). The skipped
+    owner is audited as soon as the operation ends."""
+    async def body(lc):
+        lc.tenant("t")
+        code, _ = await lc.add("default", "t", 1)
+        assert code == 200
+        w = lc.nodes["node-0"].worker
+        svc = w.service
+        lc.cluster.restart_container("default", "t", "main")   # no event reaction: relisted
+        for _ in range(100):
+            await asyncio.sleep(0.01)
+            cur = svc.node_pods.get("default", "t")
+            if cur and podu.running_containers(cur)[0].id == lc.container_ids("default", "t")[0]:
+                break
+        assert await lc.audit("default", "t")                  # the new container lacks it
+        async with svc.pod_lock("default", "t"):               # an operation in flight
+            rep = await w.reconciler.run_once()
+            assert not rep.repaired
+        for _ in range(200):
+            await asyncio.sleep(0.01)
+            if not await lc.audit("default", "t"):
+                break
+        assert not await lc.audit("default", "t")
+    run(body, worker_overrides={"reconcile_on_events": False})
 
 
 # ------------------------------------------------------------------------------ long-lived worker
