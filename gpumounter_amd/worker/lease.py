@@ -18,8 +18,8 @@ from typing import Dict, List, Optional, Tuple
 
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_LEASE, ANN_OWNER_UID,
-                                         LABEL_OWNER_NS, MountType)
+from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_GROUP, ANN_LEASE,
+                                         ANN_OWNER_UID, LABEL_OWNER_NS, MountType)
 from gpumounter_amd.node.ledger import LedgerError
 from gpumounter_amd.utils import log
 
@@ -233,6 +233,16 @@ class LeaseKeeper:
                 self._arm(ph.uid, ns, name, exp)
         if not uuids:
             return
+        # an entire mount comes and goes whole: a lease on part of its group (the grant was
+        # cut off by a worker restart) ends the whole group, or the removal is refused as partial
+        def group(ph) -> str:
+            raw = raws.get(ph.name)
+            return ((raw or {}).get("metadata", {}).get("annotations") or {}).get(ANN_GROUP) or ""
+        groups = {group(ph) for ph in st.placeholders if ph.uid in due} - {""}
+        for ph in st.placeholders:
+            if ph.uid not in due and group(ph) in groups:
+                due.append(ph.uid)
+                uuids += [g.uuid for g in st.by_placeholder[(ph.namespace, ph.name)]]
         force = bool(svc.cfg.lease_force)
         resp = await svc.remove_gpu(api.RemoveGPURequest(
             pod_name=name, namespace=ns, uuids=uuids, force=force, requested_by="lease-expiry"))

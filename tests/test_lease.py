@@ -325,3 +325,35 @@ def test_a_pool_placeholder_reclaimed_by_the_same_pod_does_not_inherit_its_old_l
         await asyncio.sleep(0.1)
         assert lc.cluster.get("gpu-pool", ph) is not None and svc.lease.expired == 0
     run(body, worker_overrides={"warm_pool_size": 1})
+
+
+def test_a_lease_granted_to_part_of_an_entire_mount_group_ends_the_whole_group():
+    """An entire mount from the warm pool is a group of 1-GPU placeholders. A worker killed
+    while granting its lease leaves the annotation on some of them only; the successor's
+    expiry then asked to remove part of an entire mount, which is refused, and the lease was
+    retried for 30 s and more while its GPUs stayed attached (chaos seed rpl150). The whole
+    group goes when any part of it expires."""
+    async def body(lc):
+        w = lc.nodes["node-0"].worker
+        svc = w.service
+        for _ in range(200):
+            if len(w.pool.standby()) >= 3:
+                break
+            await asyncio.sleep(0.01)
+        lc.tenant("t")
+        code, b = await lc.add("default", "t", 3, entire=True)
+        assert code == 200 and len(b["devices"]) == 3
+        names = sorted({d["placeholder"] for d in b["devices"]})
+        assert len(names) == 3                              # a group of pool placeholders
+        past = str(time.time() - 1)
+        for n in names[:2]:                                 # the grant reached two of three
+            lc.cluster.patch("gpu-pool", n, {"metadata": {"annotations": {ANN_LEASE: past}}})
+
+        async def gone():
+            st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+            return not st.hot
+        await asyncio.sleep(0.05)                           # the watch delivers the patch
+        await svc.lease.expire_owner("default", "t")
+        assert await until(gone, 2.0)
+        assert not await lc.audit("default", "t")
+    run(body, worker_overrides={"warm_pool_size": 3})
