@@ -39,6 +39,18 @@ def _run_daemon(serve, cfg) -> int:
     if not out:
         asyncio.run(serve(cfg))
         return 0
+    if os.environ.get("GM_PROFILE_MODE", "cprofile") == "sample":
+        # statistical: setitimer(ITIMER_PROF) stack samples (gpumounter_amd/utils/sampler.py)
+        from gpumounter_amd.utils.sampler import Sampler
+
+        smp = Sampler(1.0 / float(os.environ.get("GM_PROFILE_HZ", "2000")))
+        smp.start()
+        try:
+            asyncio.run(serve(cfg))
+        finally:
+            smp.stop()
+            smp.dump(out, {"argv": sys.argv[1:]})
+        return 0
     import cProfile
 
     prof = cProfile.Profile()

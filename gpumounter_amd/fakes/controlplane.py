@@ -9,7 +9,8 @@ the DaemonSet/Deployment (see :mod:`gpumounter_amd.fakes.deployment`).
 
 Besides the Kubernetes API it serves these test hooks:
   ``POST /_fake/tenant``  {"name", "ns", "node", "gpus", "containers", "pids"} → a Running pod
-  ``POST /_fake/worker``  {"node", "port"}  → the worker DaemonSet pod the master discovers
+  ``POST /_fake/worker``  {"node", "port", "wire_port"}  → the worker DaemonSet pod the master
+  discovers
   ``GET  /_fake/kubelet``  → each node's PodResources call counters (served, rejected, over_limit)
   ``POST /_fake/kubelet/restart`` {"node", "down_s"} → kubelet down for down_s, PodResources
                           socket recreated
@@ -49,7 +50,8 @@ def _hooks(lc_ref: list):
 
         async def worker(req: web.Request) -> web.Response:
             b = await req.json()
-            lc_ref[0].register_worker(b["node"], int(b["port"]), b.get("ip", "127.0.0.1"))
+            lc_ref[0].register_worker(b["node"], int(b["port"]), b.get("ip", "127.0.0.1"),
+                                      int(b.get("wire_port", 0)))
             return web.json_response({"ok": True}, status=201)
 
         async def kubelet(req: web.Request) -> web.Response:

@@ -190,7 +190,7 @@ class ProcessCluster:
                    "GM_CONTAINER_ROOT_PREFIX": n["rootfs_root"], "GM_AMDSMI_LIB": self.amdsmi_lib,
                    "GM_STATE_DIR": n["state_dir"], "GM_HOST_DEV_PATH": n["host_dev"],
                    **({} if self.secure else {"GM_WORKER_INSECURE": "1"}), **tls_w,
-                   "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": "0",
+                   "GM_WORKER_HOST": "127.0.0.1", "GM_WORKER_PORT": "0", "GM_WIRE_PORT": "0",
                    "GM_METRICS_PORT": "0", "GM_READY_FILE": self._ready_path(f"worker-{node}"),
                    "GM_LOG_LEVEL": "WARNING",
                    "GM_LOG_JSON": "false", "GM_GPU_ALLOCATION": self.gpu_api,
@@ -246,7 +246,8 @@ class ProcessCluster:
         self._wait(f"worker {node}",
                    lambda: _http("GET", f"http://127.0.0.1:{mport}/readyz")[0] == 200)
         code, _ = _http("POST", f"{self.info['api_url']}/_fake/worker",
-                        json.dumps({"node": node, "port": gport}).encode(),
+                        json.dumps({"node": node, "port": gport,
+                                    "wire_port": int(r.get("wire_port") or 0)}).encode(),
                         {"Content-Type": "application/json"})
         if code != 201:
             raise RuntimeError(f"worker registration for {node} failed: {code}")

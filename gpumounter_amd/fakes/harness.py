@@ -26,7 +26,7 @@ from gpumounter_amd.fakes.apiserver import FakeCluster, LatencyModel
 from gpumounter_amd.fakes.kubelet import FakeKubelet
 from gpumounter_amd.fakes.node import FakeNode
 from gpumounter_amd.hw.inventory import Inventory
-from gpumounter_amd.master.app import ANN_WORKER_PORT, Master
+from gpumounter_amd.master.app import ANN_WIRE_PORT, ANN_WORKER_PORT, Master
 from gpumounter_amd.utils.config import Config
 from gpumounter_amd.worker.server import Worker
 
@@ -175,13 +175,16 @@ class LocalCluster:
                           reconcile_period_s=self.reconcile_period_s, log_json=False,
                           metrics_period_s=ov.pop("metrics_period_s", 0), **ov)
         w = Worker(cfg, inventory=self.inventory)
-        await w.start(grpc_port=0, http_port=0, reconcile=self.reconcile_period_s > 0)
+        await w.start(grpc_port=0, http_port=0, reconcile=self.reconcile_period_s > 0,
+                      wire_port=0)
         h.worker, h.cfg = w, cfg
-        self.register_worker(name, w.grpc_port)
+        self.register_worker(name, w.grpc_port, wire_port=w.wire_port)
         return w
 
-    def register_worker(self, name: str, port: int, ip: str = "127.0.0.1") -> None:
-        """Create the worker DaemonSet pod of node ``name`` so the master can discover it."""
+    def register_worker(self, name: str, port: int, ip: str = "127.0.0.1",
+                        wire_port: int = 0) -> None:
+        """Create the worker DaemonSet pod of node ``name`` so the master can discover it
+        (``wire_port`` > 0: it also serves gm-wire there, as the DaemonSet annotates)."""
         wp = self.cluster.get("kube-system", f"gpu-mounter-worker-{name}")
         if wp is not None:
             self.cluster._remove("kube-system", wp["metadata"]["name"])  # noqa: SLF001
@@ -191,7 +194,9 @@ class LocalCluster:
         self.cluster.create_running_pod("kube-system", {
             "metadata": {"name": f"gpu-mounter-worker-{name}",
                          "labels": {"app": "gpu-mounter-worker"},
-                         "annotations": {ANN_WORKER_PORT: str(port)}},
+                         "annotations": {ANN_WORKER_PORT: str(port),
+                                         **({ANN_WIRE_PORT: str(wire_port)}
+                                            if wire_port > 0 else {})}},
             "spec": {"containers": [{"name": "worker", "image": "gpumounter-amd:dev"}]}}, name,
             pod_ip=ip)
 

@@ -21,22 +21,23 @@ import time
 from typing import Dict, Optional, Tuple
 
 import grpc
-from aiohttp import web
 
 from gpumounter_amd.api import gpu_mount as api
-from gpumounter_amd.api import protodef
+from gpumounter_amd.api import protodef, wire
 from gpumounter_amd.cluster.informer import PodInformer, SlimPodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.cluster.placeholder import LABEL_NODE
 from gpumounter_amd.models import pod as podu
+from gpumounter_amd.master import httpd
 from gpumounter_amd.master.authz import Authorizer
+from gpumounter_amd.master.httpd import Request, Response
 from gpumounter_amd.utils import log, runtime, trace
 from gpumounter_amd.utils.metrics import Metrics
-from gpumounter_amd.utils.spin import LoopSpinner
 
 _log = log.get("master")
 
 ANN_WORKER_PORT = "gpumounter.amd.com/grpc-port"
+ANN_WIRE_PORT = "gpumounter.amd.com/wire-port"     # the worker serves gm-wire (api/wire.py)
 _TRUE = {"1", "t", "T", "TRUE", "true", "True"}
 _FALSE = {"0", "f", "F", "FALSE", "false", "False"}
 
@@ -74,10 +75,9 @@ def parse_lease(v: str) -> Optional[float]:
     return f if 0 < f < 10 * 365 * 86400 else None
 
 
-def _text(body: str, status: int = 200) -> web.Response:
+def _text(body: str, status: int = 200) -> Response:
     # Go's http.Error / fmt.Fprintf write text/plain with a trailing newline
-    return web.Response(text=body if body.endswith("\n") else body + "\n", status=status,
-                        content_type="text/plain", charset="utf-8")
+    return httpd.text(body if body.endswith("\n") else body + "\n", status)
 
 
 # AddGPU is retried when the worker answers UNAVAILABLE (restarting, draining). That is safe
@@ -90,11 +90,30 @@ _SERVICE_CONFIG = json.dumps({"methodConfig": [{
                     "backoffMultiplier": 2, "retryableStatusCodes": ["UNAVAILABLE"]}}]})
 
 
-USER_KEY = web.RequestKey("gm_user", str)   # the caller's identity, set by _denied()
+USER_KEY = "gm_user"       # the caller's identity, set by _denied()
+
+
+# method → (gRPC path, request class, response class, gm-wire method id)
+_METHODS = {
+    "add": (api.ADD_GPU, api.AddGPURequest, api.AddGPUResponse, wire.METHOD_ADD),
+    "remove": (api.REMOVE_GPU, api.RemoveGPURequest, api.RemoveGPUResponse, wire.METHOD_REMOVE),
+    "status": (api.NODE_STATUS, api.NodeStatusRequest, api.NodeStatusResponse,
+               wire.METHOD_STATUS),
+}
+# what a failed worker call raises, whichever transport carried it (both have code()/details())
+RPC_ERRORS = (grpc.aio.AioRpcError, wire.WireError)
 
 
 class WorkerDirectory:
-    """node name → worker gRPC target, from a watch on the worker DaemonSet pods."""
+    """node name → worker endpoint, from a watch on the worker DaemonSet pods; pooled channels.
+
+    A worker pod that advertises a gm-wire port (``ANN_WIRE_PORT``) is called over gm-wire
+    (api/wire.py) unless ``master_transport=grpc``; one whose gm-wire port cannot be reached is
+    called over gRPC for the next ``WIRE_RETRY_S`` seconds. gRPC is the reference's transport
+    (main.go:82-96, a new insecure connection per request); here the channel is kept."""
+
+    WIRE_RETRY_S = 10.0
+    ADD_ATTEMPTS = 4           # AddGPU on UNAVAILABLE, as the gRPC retry policy (_SERVICE_CONFIG)
 
     def __init__(self, kube: KubeClient, namespace: str, label: str, default_port: int,
                  cfg=None) -> None:
@@ -102,6 +121,10 @@ class WorkerDirectory:
         self.default_port = default_port
         self.cfg = cfg
         self._channels: Dict[str, grpc.aio.Channel] = {}
+        self._stubs: Dict[Tuple[str, str], object] = {}
+        self._wires: Dict[str, wire.WireChannel] = {}
+        self._wire_of: Dict[str, Optional[str]] = {}     # gRPC target → gm-wire target
+        self._wire_down: Dict[str, float] = {}           # gm-wire target → retry after
         self._loop = None
         self._targets: Dict[str, Optional[str]] = {}
 
@@ -119,57 +142,127 @@ class WorkerDirectory:
         if targets != self._targets:
             _log.debug("worker targets: %s", targets)
             self._targets = targets
-        for p in self.informer.cache.values():
-            t = self.target(podu.node_of(p))
-            if t is not None:
-                try:
-                    self.channel(t).get_state(try_to_connect=True)
-                except RuntimeError:         # no running loop (stopping)
-                    return
+        for t in set(targets.values()):
+            if t is None:
+                continue
+            try:
+                self.channel(t).get_state(try_to_connect=True)
+                wt = self._wire_of.get(t)
+                if wt is not None:
+                    self.wire_channel(wt).warm()
+            except RuntimeError:         # no running loop (stopping)
+                return
 
     async def stop(self) -> None:
         await self.informer.stop()
         for ch in self._channels.values():
             await ch.close()
+        for w in self._wires.values():
+            await w.close()
         self._channels.clear()
+        self._stubs.clear()
+        self._wires.clear()
 
     def target(self, node: str) -> Optional[str]:
         best = None
+        wire_port = None
         for p in self.informer.cache.values():
             if podu.node_of(p) != node or podu.is_terminating(p):
                 continue
             ip = p.get("status", {}).get("podIP")
             if not ip or podu.phase_of(p) != "Running":
                 continue
-            port = (p["metadata"].get("annotations") or {}).get(ANN_WORKER_PORT,
-                                                                 str(self.default_port))
+            ann = p["metadata"].get("annotations") or {}
+            port = ann.get(ANN_WORKER_PORT, str(self.default_port))
             best = f"{ip}:{port}"
+            wire_port = ann.get(ANN_WIRE_PORT)
+            wire_port = f"{ip}:{wire_port}" if wire_port and self._wire_enabled() else None
+        if best is not None:
+            self._wire_of[best] = wire_port
         return best
 
-    def channel(self, target: str) -> grpc.aio.Channel:
+    def _wire_enabled(self) -> bool:
+        return getattr(self.cfg, "master_transport", "auto") == "auto"
+
+    def _check_loop(self) -> None:
         loop = asyncio.get_running_loop()
         if self._loop is not loop:
-            self._channels = {}
+            self._channels, self._stubs, self._wires = {}, {}, {}
             self._loop = loop
+
+    def channel(self, target: str) -> grpc.aio.Channel:
+        self._check_loop()
         ch = self._channels.get(target)
         if ch is None:
             opts = [("grpc.keepalive_time_ms", 30000), ("grpc.enable_retries", 1),
                     ("grpc.service_config", _SERVICE_CONFIG)]
             cfg = self.cfg
             if cfg is not None and cfg.tls_ca:
-                def rd(p):
-                    with open(p, "rb") as fh:
-                        return fh.read()
                 creds = grpc.ssl_channel_credentials(
-                    root_certificates=rd(cfg.tls_ca),
-                    private_key=rd(cfg.tls_key) if cfg.tls_key else None,
-                    certificate_chain=rd(cfg.tls_cert) if cfg.tls_cert else None)
+                    root_certificates=_read(cfg.tls_ca),
+                    private_key=_read(cfg.tls_key) if cfg.tls_key else None,
+                    certificate_chain=_read(cfg.tls_cert) if cfg.tls_cert else None)
                 opts.append(("grpc.ssl_target_name_override", cfg.tls_server_name))
                 ch = grpc.aio.secure_channel(target, creds, options=opts)
             else:
                 ch = grpc.aio.insecure_channel(target, options=opts)
             self._channels[target] = ch
         return ch
+
+    def wire_channel(self, target: str) -> wire.WireChannel:
+        self._check_loop()
+        ch = self._wires.get(target)
+        if ch is None:
+            host, port = target.rsplit(":", 1)
+            cfg = self.cfg
+            ctx = wire.client_context(cfg.tls_ca, cfg.tls_cert, cfg.tls_key) \
+                if cfg is not None and cfg.tls_ca else None
+            ch = self._wires[target] = wire.WireChannel(
+                host, int(port), ctx, cfg.tls_server_name if ctx is not None else "")
+        return ch
+
+    def _stub(self, target: str, method: str):
+        """The gRPC multicallable, built once per channel and method."""
+        self._check_loop()
+        stub = self._stubs.get((target, method))
+        if stub is None:
+            path, req_cls, resp_cls, _ = _METHODS[method]
+            stub = self._stubs[(target, method)] = self.channel(target).unary_unary(
+                path, request_serializer=req_cls.SerializeToString,
+                response_deserializer=resp_cls.FromString)
+        return stub
+
+    async def unary(self, target: str, method: str, req, timeout: float):
+        """One worker call over gm-wire when the worker offers it, else gRPC. Failures raise
+        one of :data:`RPC_ERRORS`."""
+        wt = self._wire_of.get(target)
+        if wt is not None and self._wire_down.get(wt, 0.0) <= time.monotonic():
+            _, _, resp_cls, mid = _METHODS[method]
+            ch = self.wire_channel(wt)
+            payload = req.SerializeToString()
+            attempts = self.ADD_ATTEMPTS if method == "add" else 1
+            for i in range(attempts):
+                try:
+                    return resp_cls.FromString(await ch.call(mid, payload, timeout))
+                except wire.WireError as e:
+                    if e.code() != grpc.StatusCode.UNAVAILABLE:
+                        raise
+                    if not e.sent:
+                        # never reached the worker: gRPC instead, for a while
+                        _log.warning("gm-wire to %s unavailable (%s); using gRPC for %gs",
+                                     wt, e.details(), self.WIRE_RETRY_S)
+                        self._wire_down[wt] = time.monotonic() + self.WIRE_RETRY_S
+                        break
+                    if i == attempts - 1:
+                        raise
+                    # the idempotency key makes a repeated AddGPU replay the first one
+                    await asyncio.sleep(min(0.05 * 2 ** i, 1.0))
+        return await self._stub(target, method)(req, timeout=timeout)
+
+
+def _read(path: str) -> bytes:
+    with open(path, "rb") as fh:
+        return fh.read()
 
 
 class Master:
@@ -184,9 +277,7 @@ class Master:
                                        cfg.worker_port, cfg)
         self.metrics = Metrics()
         self.authz = Authorizer(cfg, self.kube)
-        self.spin = LoopSpinner(getattr(cfg, "loop_spin_us", 0.0),
-                                getattr(cfg, "loop_spin_max_ms", 20.0))
-        self.runner: Optional[web.AppRunner] = None
+        self.http: Optional[httpd.HttpServer] = None
         self.port = 0
         self._pod_nodes: Dict[Tuple[str, str], Tuple[str, str, float]] = {}
         # pod → node without a GET per request (the reference GETs the pod every time,
@@ -199,9 +290,8 @@ class Master:
         self._pods_task: Optional[asyncio.Task] = None
 
     # ------------------------------------------------------------------------ app
-    def app(self) -> web.Application:
-        app = web.Application()
-        r = app.router
+    def router(self) -> httpd.Router:
+        r = httpd.Router()
         r.add_get("/", self.index)
         r.add_get("/addgpu/namespace/{namespace}/pod/{pod}/gpu/{gpuNum}/isEntireMount/"
                   "{isEntireMount}", self.add_gpu)
@@ -211,7 +301,7 @@ class Master:
         r.add_get("/api/v1/nodes/{node}/gpus", self.node_gpus)
         r.add_get("/healthz", self.healthz)
         r.add_get("/metrics", self.metrics_handler)
-        return app
+        return r
 
     async def start(self, port: Optional[int] = None) -> None:
         await self.workers.start()
@@ -220,12 +310,9 @@ class Master:
             # longer than a few seconds: until then a lookup GETs the pod
             self._pods_task = asyncio.ensure_future(self._start_pod_index())
             await asyncio.wait([self._pods_task], timeout=self.POD_INDEX_WAIT_S)
-        self.runner = web.AppRunner(self.app(), access_log=None)
-        await self.runner.setup()
-        site = web.TCPSite(self.runner, self.cfg.master_host,
-                           self.cfg.master_port if port is None else port)
-        await site.start()
-        self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+        self.http = httpd.HttpServer(self.router())
+        self.port = await self.http.start(self.cfg.master_host,
+                                          self.cfg.master_port if port is None else port)
         if self.cfg.gc_tune:
             runtime.tune_gc()
             runtime.watch_gc_pauses(5.0, _log)
@@ -242,8 +329,8 @@ class Master:
             _log.warning("pod index not synced (%s); pod lookups GET the pod", e)
 
     async def stop(self) -> None:
-        if self.runner is not None:
-            await self.runner.cleanup()
+        if self.http is not None:
+            await self.http.stop()
         if self._pods_task is not None:
             self._pods_task.cancel()
         if self.pods is not None:
@@ -253,21 +340,21 @@ class Master:
         await self.kube.close()
 
     # ------------------------------------------------------------------------ handlers
-    async def healthz(self, request: web.Request) -> web.Response:
-        return web.Response(text="ok")
+    async def healthz(self, request: Request) -> Response:
+        return httpd.text("ok")
 
-    async def metrics_handler(self, request: web.Request) -> web.Response:
-        return web.Response(body=self.metrics.render(), content_type="text/plain")
+    async def metrics_handler(self, request: Request) -> Response:
+        return Response(self.metrics.render(), content_type="text/plain; version=0.0.4")
 
-    async def index(self, request: web.Request) -> web.Response:
+    async def index(self, request: Request) -> Response:
         return _text("This is gpu mounter api!")
 
     @staticmethod
-    def _wants_json(request: web.Request) -> bool:
+    def _wants_json(request: Request) -> bool:
         return "application/json" in request.headers.get("Accept", "")
 
-    async def _denied(self, request: web.Request, route: str, verb: str, ns: str = "",
-                      resource: str = "pods", name: str = "") -> Optional[web.Response]:
+    async def _denied(self, request: Request, route: str, verb: str, ns: str = "",
+                      resource: str = "pods", name: str = "") -> Optional[Response]:
         """None if allowed, else the 401/403/503 reply (master/authz.py; the reference has no
         authn/authz at all: SURVEY defect 13)."""
         d = await self.authz.check(request.headers, verb, ns, resource, name)
@@ -276,7 +363,7 @@ class Master:
             return None
         return self._reply(request, route, d.status, d.reason, {})
 
-    def _identity(self, request: web.Request, d) -> str:
+    def _identity(self, request: Request, d) -> str:
         """Who asked, for the audit trail (Events, logs): the authenticated Kubernetes user, the
         shared-token holder, or the anonymous caller's address."""
         if d.user:
@@ -285,7 +372,7 @@ class Master:
             return "api-token"
         return f"anonymous@{request.remote or '?'}"
 
-    def _reply(self, request, route: str, status: int, text: str, payload: dict) -> web.Response:
+    def _reply(self, request, route: str, status: int, text: str, payload: dict) -> Response:
         self.metrics.http_requests.labels(route=route, code=str(status)).inc()
         if self._wants_json(request):
             payload = dict(payload)
@@ -293,7 +380,7 @@ class Master:
                 payload["detail"] = payload["message"]
             payload["message"] = text.rstrip("\n")
             payload["code"] = status
-            return web.json_response(payload, status=status)
+            return httpd.json_response(payload, status=status)
         return _text(text, status)
 
     def _stale(self, cached: str, pod: dict) -> bool:
@@ -359,19 +446,15 @@ class Master:
                 pod, target, err, cached = await self._locate(ns, name, fresh)
             if err is not None:
                 return err
-            stub = self.workers.channel(target).unary_unary(
-                api.ADD_GPU, request_serializer=api.AddGPURequest.SerializeToString,
-                response_deserializer=api.AddGPUResponse.FromString)
             try:
                 with trace.span("master_rpc"):
                     t_send = time.perf_counter()
-                    resp = await stub(api.AddGPURequest(
+                    resp = await self.workers.unary(target, "add", api.AddGPURequest(
                         pod_name=name, namespace=ns, gpu_num=n, is_entire_mount=entire,
                         request_id=rid, container=container, idempotency_key=key,
-                        requested_by=user, lease_s=lease_s),
-                        timeout=self.cfg.rpc_timeout_s)
+                        requested_by=user, lease_s=lease_s), self.cfg.rpc_timeout_s)
                     self._legs(resp, t_send, time.perf_counter())
-            except grpc.aio.AioRpcError as e:
+            except RPC_ERRORS as e:
                 if cached and e.code() == grpc.StatusCode.FAILED_PRECONDITION and \
                         "this worker serves" in (e.details() or ""):
                     self._pod_nodes.pop((ns, name), None)   # pod was recreated elsewhere
@@ -405,18 +488,15 @@ class Master:
                 pod, target, err, cached = await self._locate(ns, name, fresh)
             if err is not None:
                 return err
-            stub = self.workers.channel(target).unary_unary(
-                api.REMOVE_GPU, request_serializer=api.RemoveGPURequest.SerializeToString,
-                response_deserializer=api.RemoveGPUResponse.FromString)
             try:
                 with trace.span("master_rpc"):
                     t_send = time.perf_counter()
-                    resp = await stub(api.RemoveGPURequest(
+                    resp = await self.workers.unary(target, "remove", api.RemoveGPURequest(
                         pod_name=name, namespace=ns, uuids=uuids, force=force,
                         request_id=rid, container=container, requested_by=user),
-                        timeout=self.cfg.rpc_timeout_s)
+                        self.cfg.rpc_timeout_s)
                     self._legs(resp, t_send, time.perf_counter())
-            except grpc.aio.AioRpcError as e:
+            except RPC_ERRORS as e:
                 _log.error("RemoveGPU rpc to %s failed: %s %s", target, e.code().name,
                            e.details())
                 return 500, "Service Internal Error", {"error": e.details()}
@@ -437,12 +517,12 @@ class Master:
         return 500, "Service Internal Error", payload
 
     # ------------------------------------------------------------------------ HTTP routes
-    async def add_gpu(self, request: web.Request) -> web.Response:
+    async def add_gpu(self, request: Request) -> Response:
         # gm:master_* roctx ranges; the stage split is returned as ``master_timings``
-        with self.spin.hold(), trace.span("master_addgpu") as root:
+        with trace.span("master_addgpu") as root:
             return await self._add_gpu(request, root)
 
-    async def _add_gpu(self, request: web.Request, root: trace.Span) -> web.Response:
+    async def _add_gpu(self, request: Request, root: trace.Span) -> Response:
         route = "addgpu"
         mi = request.match_info
         ns, name = mi["namespace"], mi["pod"]
@@ -473,11 +553,11 @@ class Master:
             lease_s)
         return self._reply(request, route, status, text, self._stamp(payload, root))
 
-    async def remove_gpu(self, request: web.Request) -> web.Response:
-        with self.spin.hold(), trace.span("master_removegpu") as root:
+    async def remove_gpu(self, request: Request) -> Response:
+        with trace.span("master_removegpu") as root:
             return await self._remove_gpu(request, root)
 
-    async def _remove_gpu(self, request: web.Request, root: trace.Span) -> web.Response:
+    async def _remove_gpu(self, request: Request, root: trace.Span) -> Response:
         route = "removegpu"
         mi = request.match_info
         ns, name = mi["namespace"], mi["pod"]
@@ -530,7 +610,7 @@ class Master:
                                          for k, v in root.flat().items()]
         return payload
 
-    async def batch(self, request: web.Request) -> web.Response:
+    async def batch(self, request: Request) -> Response:
         """``POST /api/v1/batch`` {"operations": [{"op": "add", "namespace", "pod", "gpus",
         "entire", "container", "idempotency_key"} | {"op": "remove", "namespace", "pod",
         "uuids", "force", "container"}]} → results in order; operations run concurrently
@@ -545,7 +625,7 @@ class Master:
             ops = body["operations"]
             assert isinstance(ops, list)
         except Exception:  # noqa: BLE001
-            return web.json_response({"error": "body must be {\"operations\": [...]}"},
+            return httpd.json_response({"error": "body must be {\"operations\": [...]}"},
                                      status=400)
 
         async def one(op):
@@ -589,7 +669,7 @@ class Master:
             d.update(code=status, message=text)
             out.append(d)
             self.metrics.http_requests.labels(route=route, code=str(status)).inc()
-        return web.json_response({"results": out})
+        return httpd.json_response({"results": out})
 
     @staticmethod
     def _payload(resp, t0: float) -> dict:
@@ -598,26 +678,23 @@ class Master:
         d["master_ms"] = (time.perf_counter() - t0) * 1e3
         return d
 
-    async def node_gpus(self, request: web.Request) -> web.Response:
+    async def node_gpus(self, request: Request) -> Response:
         node = request.match_info["node"]
         denied = await self._denied(request, "nodegpus", "get", resource="nodes", name=node)
         if denied is not None:
             return denied
         target = self.workers.target(node)
         if target is None:
-            return web.json_response({"error": f"no worker on node {node}"}, status=404)
-        stub = self.workers.channel(target).unary_unary(
-            api.NODE_STATUS, request_serializer=api.NodeStatusRequest.SerializeToString,
-            response_deserializer=api.NodeStatusResponse.FromString)
+            return httpd.json_response({"error": f"no worker on node {node}"}, status=404)
         try:
-            resp = await stub(api.NodeStatusRequest(
-                include_processes=request.query.get("processes") == "1"), timeout=30)
-        except grpc.aio.AioRpcError as e:
-            return web.json_response({"error": f"worker on {node}: {e.code().name} "
+            resp = await self.workers.unary(target, "status", api.NodeStatusRequest(
+                include_processes=request.query.get("processes") == "1"), 30.0)
+        except RPC_ERRORS as e:
+            return httpd.json_response({"error": f"worker on {node}: {e.code().name} "
                                                f"{e.details()}"}, status=502)
-        return web.json_response(json.loads(resp.json))
+        return httpd.json_response(json.loads(resp.json))
 
-    async def pod_gpus(self, request: web.Request) -> web.Response:
+    async def pod_gpus(self, request: Request) -> Response:
         ns, name = request.match_info["namespace"], request.match_info["pod"]
         denied = await self._denied(request, "podgpus", "get", ns, name=name)
         if denied is not None:
@@ -625,19 +702,17 @@ class Master:
         try:
             pod = await self.kube.get_pod(ns, name)
         except NotFound:
-            return web.json_response({"error": "pod not found"}, status=404)
+            return httpd.json_response({"error": "pod not found"}, status=404)
         except ApiError as e:
-            return web.json_response({"error": str(e)}, status=500)
+            return httpd.json_response({"error": str(e)}, status=500)
         target = self.workers.target(podu.node_of(pod))
         if target is None:
-            return web.json_response({"error": "no worker"}, status=500)
-        stub = self.workers.channel(target).unary_unary(
-            api.NODE_STATUS, request_serializer=api.NodeStatusRequest.SerializeToString,
-            response_deserializer=api.NodeStatusResponse.FromString)
+            return httpd.json_response({"error": "no worker"}, status=500)
         try:
-            st = json.loads((await stub(api.NodeStatusRequest(), timeout=30)).json)
-        except grpc.aio.AioRpcError as e:
-            return web.json_response({"error": f"worker on {podu.node_of(pod)}: "
+            st = json.loads((await self.workers.unary(target, "status", api.NodeStatusRequest(),
+                                                      30.0)).json)
+        except RPC_ERRORS as e:
+            return httpd.json_response({"error": f"worker on {podu.node_of(pod)}: "
                                                f"{e.code().name} {e.details()}"}, status=502)
         uid = podu.uid_of(pod)
         held = {(p["namespace"], p["name"]): p.get("lease_expires")
@@ -648,7 +723,7 @@ class Master:
                for g in st["gpus"] if (g.get("namespace"), g.get("pod_name")) in held]
         own = [dict(g, source="pod-spec") for g in st["gpus"]
                if (g.get("namespace"), g.get("pod_name")) == (ns, name)]
-        return web.json_response({"pod": f"{ns}/{name}", "node": podu.node_of(pod),
+        return httpd.json_response({"pod": f"{ns}/{name}", "node": podu.node_of(pod),
                                   "gpus": own + hot})
 
 

@@ -26,6 +26,12 @@ class Config:
     master_port: int = 8080            # master HTTP API (reference: main.go:237)
     worker_host: str = "0.0.0.0"       # worker gRPC bind address
     worker_port: int = 1200            # worker gRPC (reference: worker main.go:24)
+    # worker gm-wire port (api/wire.py): the gpu_mount messages for gpumounter's own master on
+    # one persistent (m)TLS connection, next to the reference-compatible gRPC port; -1 = off
+    wire_port: int = 1201
+    # how the master calls a worker: auto = gm-wire when the worker pod advertises its port
+    # (annotation gpumounter.amd.com/wire-port), else gRPC; grpc = always gRPC
+    master_transport: str = "auto"
     metrics_port: int = 9400           # worker /metrics and /healthz
     # after start-up the daemon writes the ports it actually bound ({"grpc_port", "http_port"}
     # or {"port"}) here, atomically; with ports 0 (ephemeral) that is how a supervisor finds
@@ -173,11 +179,6 @@ class Config:
     attach_timeout_s: float = 120.0    # placeholder admission deadline
     detach_timeout_s: float = 60.0     # wait for placeholder deletion where waited for
     rpc_timeout_s: float = 180.0       # master→worker gRPC deadline (reference: none)
-    # keep the event loop polling (no blocking epoll_wait) while an add/remove request is in
-    # flight and this long after it answered (utils/spin.py): saves the thread wake-ups of its
-    # waits, for one busy core during the request (0 = off)
-    loop_spin_us: float = 0.0
-    loop_spin_max_ms: float = 20.0     # longest stretch of polling; then the loop blocks again
     reconcile_period_s: float = 30.0   # full reconciler sweep period
     # every this many seconds, compare each hot container's device-control state (v2: the
     # attached BPF program ids; v1: devices.list) with what gpumounter last installed, and
@@ -282,10 +283,12 @@ class Config:
         _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
         _choice("ledger_source", self.ledger_source, ("auto", "podresources"))
         _choice("gpu_allocation", self.gpu_allocation, ("device-plugin", "dra"))
+        _choice("master_transport", self.master_transport, ("auto", "grpc"))
         if self.gpu_allocation == "dra" and self.device_plugin:
             raise ValueError("device_plugin serves the extended resource; with "
                              "gpu_allocation=dra the GPUs belong to the DRA driver")
-        if not (0 <= self.worker_port < 65536 and 0 <= self.master_port < 65536):
+        if not (0 <= self.worker_port < 65536 and 0 <= self.master_port < 65536 and
+                -1 <= self.wire_port < 65536):
             raise ValueError("ports out of range")
 
     def as_dict(self) -> Dict[str, Any]:

@@ -20,6 +20,7 @@ import grpc
 from aiohttp import web
 
 from gpumounter_amd.api import gpu_mount as api
+from gpumounter_amd.api import wire
 from gpumounter_amd.cluster.informer import ClaimInformer, PodInformer
 from gpumounter_amd.cluster.kube import KubeClient
 from gpumounter_amd.cluster.placeholder import LABEL_NODE, PlaceholderManager
@@ -36,7 +37,6 @@ from gpumounter_amd.node.ledger import LedgerClient
 from gpumounter_amd.utils import log, runtime
 from gpumounter_amd.utils.faults import FaultInjector
 from gpumounter_amd.utils.metrics import Metrics
-from gpumounter_amd.utils.spin import LoopSpinner
 from gpumounter_amd.worker.reconciler import Reconciler
 from gpumounter_amd.worker.service import GpuMountService, RpcError
 
@@ -136,8 +136,9 @@ class Worker:
         if cfg.reconcile_on_events:
             self.reconciler.watch_events()
         self.grpc_server: Optional[grpc.aio.Server] = None
-        self._ops: set = set()          # RPC operations running (see _wrap)
-        self.spin = LoopSpinner(cfg.loop_spin_us, cfg.loop_spin_max_ms)
+        self.wire_server: Optional[wire.WireServer] = None
+        self.wire_port = 0
+        self._ops: set = set()          # RPC operations running (see run_op)
         self.http_runner: Optional[web.AppRunner] = None
         self.grpc_port = 0
         self.http_port = 0
@@ -156,52 +157,63 @@ class Worker:
                for v in auth.get(k, [])}
         return bool(got & names)
 
-    def _wrap(self, fn, spin: bool = True):
-        async def handler(request, context):
-            if spin:
-                with self.spin.hold():
-                    return await served(request, context)
-            return await served(request, context)
+    async def run_op(self, fn, request, t_in: float):
+        """Run one AddGPU/RemoveGPU/GetNodeStatus for either transport (gRPC or gm-wire).
+        Failures leave as :class:`RpcError`; ``t_in`` is when the transport handed it over.
 
-        async def served(request, context):
+        An attach or detach, once started, runs to its end (done, or rolled back) even if the
+        caller goes away: a master killed or a deadline passed mid-request cancels the
+        transport's handler, and a cancellation landing between two steps would leave a
+        placeholder created but never admitted or mounted, or rules without nodes."""
+        t0 = time.perf_counter()
+        op = asyncio.ensure_future(self._timed(fn, request))
+        self._ops.add(op)
+        op.add_done_callback(self._ops.discard)
+        try:
+            resp, t1, t2 = await asyncio.shield(op)
+        except asyncio.CancelledError:
+            op.add_done_callback(self._orphan_done)     # its outcome reaches no caller
+            raise
+        except RpcError:
+            raise
+        except Exception as e:  # noqa: BLE001
+            _log.exception("rpc failed")
+            raise RpcError(grpc.StatusCode.INTERNAL, f"Service Internal Error: {e}") from e
+        if hasattr(resp, "timings"):
+            # the handler around the operation: rpc_queue = until the operation's task ran,
+            # rpc_tail = from its end until the handler resumed. What is left of the master's
+            # RPC time is transport (client, server, TLS)
+            resp.timings.add(name="rpc_queue", ms=(t1 - t0) * 1e3)
+            t_out = time.perf_counter()
+            resp.timings.add(name="rpc_tail", ms=(t_out - t2) * 1e3)
+            resp.timings.add(name="rpc_peer_check", ms=(t0 - t_in) * 1e3)
+            # when the handler started and returned on the host's monotonic clock
+            # (CLOCK_MONOTONIC: the same in every process of the host): a master on the same
+            # host splits the hop into its request and response legs
+            resp.timings.add(name="clock.in", ms=t_in * 1e3)
+            resp.timings.add(name="clock.out", ms=t_out * 1e3)
+        return resp
+
+    def _wrap(self, fn):
+        """gRPC adapter of :meth:`run_op` (peer identity checked per call)."""
+        async def handler(request, context):
             t_in = time.perf_counter()
             if not self._peer_allowed(context):
                 await context.abort(grpc.StatusCode.PERMISSION_DENIED,
                                     "client certificate is not an allowed gpumounter identity")
-            # An attach or detach, once started, runs to its end (done, or rolled back) even if
-            # the caller goes away: a master killed or a deadline passed mid-request cancels
-            # this handler, and a cancellation landing between two steps would leave a
-            # placeholder created but never admitted or mounted, or rules without nodes
-            t0 = time.perf_counter()
-            op = asyncio.ensure_future(self._timed(fn, request))
-            self._ops.add(op)
-            op.add_done_callback(self._ops.discard)
             try:
-                resp, t1, t2 = await asyncio.shield(op)
-                if hasattr(resp, "timings"):
-                    # the handler around the operation: rpc_queue = until the operation's task
-                    # ran, rpc_tail = from its end until the handler resumed. What is left of
-                    # the master's RPC time is gRPC transport (client, server, TLS)
-                    resp.timings.add(name="rpc_queue", ms=(t1 - t0) * 1e3)
-                    t_out = time.perf_counter()
-                    resp.timings.add(name="rpc_tail", ms=(t_out - t2) * 1e3)
-                    resp.timings.add(name="rpc_peer_check", ms=(t0 - t_in) * 1e3)
-                    # when the handler started and returned on the host's monotonic clock
-                    # (CLOCK_MONOTONIC: the same in every process of the host): a master on the
-                    # same host splits the gRPC hop into its request and response legs
-                    resp.timings.add(name="clock.in", ms=t_in * 1e3)
-                    resp.timings.add(name="clock.out", ms=t_out * 1e3)
-                return resp
-            except asyncio.CancelledError:
-                op.add_done_callback(self._orphan_done)     # its outcome reaches no caller
-                raise
+                return await self.run_op(fn, request, t_in)
             except RpcError as e:
                 await context.abort(e.code, e.msg)
-            except grpc.aio.AbortError:
-                raise
-            except Exception as e:  # noqa: BLE001
-                _log.exception("rpc failed")
-                await context.abort(grpc.StatusCode.INTERNAL, f"Service Internal Error: {e}")
+        return handler
+
+    def _wire(self, fn):
+        """gm-wire adapter of :meth:`run_op` (peer identity checked per connection)."""
+        async def handler(request):
+            try:
+                return await self.run_op(fn, request, time.perf_counter())
+            except RpcError as e:
+                raise wire.WireStatus(e.code, e.msg) from None
         return handler
 
     @staticmethod
@@ -237,12 +249,19 @@ class Worker:
                     api.RemoveGPURequest.FromString, _ser)}),
             grpc.method_handlers_generic_handler("gpu_mount.NodeService", {
                 "GetNodeStatus": grpc.unary_unary_rpc_method_handler(
-                    self._wrap(self._status, spin=False), api.NodeStatusRequest.FromString, _ser)}),
+                    self._wrap(self._status), api.NodeStatusRequest.FromString, _ser)}),
         )
+
+    def wire_handlers(self):
+        return {wire.METHOD_ADD: (api.AddGPURequest.FromString,
+                                  self._wire(lambda r: self.service.add_gpu(r))),
+                wire.METHOD_REMOVE: (api.RemoveGPURequest.FromString,
+                                     self._wire(lambda r: self.service.remove_gpu(r))),
+                wire.METHOD_STATUS: (api.NodeStatusRequest.FromString, self._wire(self._status))}
 
     # ------------------------------------------------------------------------ lifecycle
     async def start(self, grpc_port: Optional[int] = None, http_port: Optional[int] = None,
-                    reconcile: bool = True) -> None:
+                    reconcile: bool = True, wire_port: Optional[int] = None) -> None:
         await self.ph_informer.start()
         await self.node_informer.start()
         if self.claim_informer is not None:
@@ -295,6 +314,19 @@ class Worker:
         if self.grpc_port == 0:
             raise OSError(f"cannot bind gRPC {self.cfg.worker_host}:{port}")
         await self.grpc_server.start()
+        if self.cfg.wire_port >= 0:
+            # gm-wire (api/wire.py): the same messages for gpumounter's own master, on one
+            # persistent connection; the same certificates and client identities as gRPC
+            ctx = wire.server_context(self.cfg.tls_cert, self.cfg.tls_key, self.cfg.tls_ca) \
+                if self.cfg.tls_cert and self.cfg.tls_key else None
+            names = [n.strip() for n in self.cfg.tls_client_names.split(",")] \
+                if self.cfg.tls_ca else []
+            self.wire_server = wire.WireServer(self.wire_handlers(), ctx, names)
+            wp = self.cfg.wire_port if wire_port is None else wire_port
+            try:
+                self.wire_port = await self.wire_server.start(self.cfg.worker_host, wp)
+            except OSError as e:
+                raise OSError(f"cannot bind gm-wire {self.cfg.worker_host}:{wp}: {e}") from e
         hp = self.cfg.metrics_port if http_port is None else http_port
         if hp is not None and hp >= 0:
             app = web.Application()
@@ -328,9 +360,11 @@ class Worker:
             runtime.watch_gc_pauses(5.0, _log)
         self.ready = True
         runtime.write_ready_file(self.cfg.ready_file, {"grpc_port": self.grpc_port,
-                                                       "http_port": self.http_port})
-        _log.info("worker %s serving gRPC :%d http :%d (cgroup %s/%s, devnodes %s, ledger %s)",
-                  self.cfg.node_name, self.grpc_port, self.http_port, self.resolver.mode,
+                                                       "http_port": self.http_port,
+                                                       "wire_port": self.wire_port})
+        _log.info("worker %s serving gRPC :%d gm-wire :%d http :%d (cgroup %s/%s, devnodes %s, ledger %s)",
+                  self.cfg.node_name, self.grpc_port, self.wire_port, self.http_port,
+                  self.resolver.mode,
                   self.backend.name, self.cfg.devnode_mode, self.ledger.api_version)
 
     async def _healthz(self, request):
@@ -433,6 +467,8 @@ class Worker:
             self._health_task.cancel()
         # no new RPCs; the ones running finish (or roll back) while the keepers they hand work
         # to (reconciler follow-ups, leases, drains, notifications) still run
+        if self.wire_server is not None:
+            await self.wire_server.stop()
         if self.grpc_server is not None:
             await self.grpc_server.stop(0.5)
         if self._ops:

@@ -26,7 +26,8 @@ def test_worker_daemonset_shape():
     assert spec["hostPID"] is True
     c = spec["containers"][0]
     assert c["securityContext"]["privileged"] is True
-    assert {p["containerPort"] for p in c["ports"]} == {cfg.worker_port, cfg.metrics_port}
+    assert {p["containerPort"] for p in c["ports"]} == {cfg.worker_port, cfg.wire_port,
+                                                        cfg.metrics_port}
     mounts = {m["mountPath"] for m in c["volumeMounts"]}
     assert {"/sys/fs/cgroup", "/sys/fs/bpf", "/var/lib/kubelet/pod-resources", "/dev",
             "/sys/class/kfd"} <= mounts
@@ -124,10 +125,18 @@ def test_master_and_network_policy_are_secure_by_default():
     (np,) = load("networkpolicy.yaml")
     assert np["spec"]["podSelector"]["matchLabels"] == {"app": "gpu-mounter-worker"}
     rules = np["spec"]["ingress"]
-    grpc_rule = [r for r in rules if any(p["port"] == 1200 for p in r["ports"])]
-    assert len(grpc_rule) == 1
-    assert grpc_rule[0]["from"] == [{"podSelector": {"matchLabels":
-                                                     {"app": "gpu-mounter-master"}}}]
+    for port in (1200, 1201):        # gRPC and gm-wire: the master only
+        grpc_rule = [r for r in rules if any(p["port"] == port for p in r["ports"])]
+        assert len(grpc_rule) == 1
+        assert grpc_rule[0]["from"] == [{"podSelector": {"matchLabels":
+                                                         {"app": "gpu-mounter-master"}}}]
+    # the DaemonSet advertises the gm-wire port the worker binds by default
+    (ds,) = load("gpu-mounter-workers.yaml")
+    tmpl = ds["spec"]["template"]
+    assert tmpl["metadata"]["annotations"]["gpumounter.amd.com/wire-port"] == \
+        str(Config.load(env={}).wire_port)
+    ports = {p["containerPort"] for p in tmpl["spec"]["containers"][0]["ports"]}
+    assert {1200, 1201} <= ports
     with open(os.path.join(ROOT, "deploy", "kustomization.yaml")) as fh:
         assert "networkpolicy.yaml" in yaml.safe_load(fh)["resources"]
     with open(os.path.join(ROOT, "deploy.sh")) as fh:
