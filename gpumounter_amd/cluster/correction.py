@@ -189,7 +189,7 @@ class Correction:
         # RELEASING before the DELETE is sent: one that takes effect and then fails (a lost
         # reply) must never be counted as a kept reservation again
         self._set(phs, Book.RELEASING)
-        await self.ph.release(list(phs), wait=True)
+        await self.ph.release(list(phs))
         self._set(phs, Book.RELEASED)
 
     async def _keep(self, phs: Sequence[Placeholder]) -> None:

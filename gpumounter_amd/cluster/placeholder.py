@@ -258,6 +258,11 @@ class PlaceholderManager:
         return {"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": spec}
 
     @property
+    def reownable(self) -> bool:
+        """Placeholders can change holder (warm-pool claims and give-backs, cluster/pool.py)."""
+        return getattr(self.cfg, "warm_pool_size", 0) > 0
+
+    @property
     def dra(self) -> bool:
         return getattr(self.cfg, "gpu_allocation", "device-plugin") == "dra"
 
@@ -327,7 +332,7 @@ class PlaceholderManager:
                 await self._await_admission(created, self.cfg.attach_timeout_s)
                 self.faults.check("placeholder_wait", "after")
         except InsufficientGPU:
-            await self.release(created, wait=False)
+            await self.release(created)
             if not (self.dra and len(preferred) == total):
                 raise
             # DRA selectors are hard constraints: the chosen devices went to someone else
@@ -337,7 +342,7 @@ class PlaceholderManager:
             return await self.reserve(owner, total, entire, (), attach_id, container,
                                       idempotency_key)
         except BaseException:
-            await self.release(created, wait=False)
+            await self.release(created)
             raise
         return Reservation(created)
 
@@ -366,10 +371,10 @@ class PlaceholderManager:
                                                      tolerant=True)
                 self.faults.check("placeholder_wait", "after")
         except BaseException:
-            await self.release(created, wait=False)
+            await self.release(created)
             raise
         if failed:
-            await self.release(failed, wait=False)
+            await self.release(failed)
         return [p for p in created if p not in failed]
 
     async def reserve_trim(self, owner: dict, total: int, entire: bool, width: int,
@@ -388,13 +393,13 @@ class PlaceholderManager:
                                            secrets.token_hex(4) if entire else "", attach_id,
                                            container, idempotency_key)
         if len(admitted) < total:
-            await self.release(admitted, wait=False)
+            await self.release(admitted)
             raise InsufficientGPU(f"only {len(admitted)} of {total} GPUs admitted")
         res, surplus = self.keep_picked(admitted, total, pick)
         try:
             await self.confirm(res.placeholders)
         except BaseException:
-            await self.release(admitted, wait=False)
+            await self.release(admitted)
             raise
         return res, surplus
 
@@ -495,7 +500,7 @@ class PlaceholderManager:
                 self.informer.upsert(r, epoch)  # visible to owned_by() before the watch echo
         errors = [r for r in results if not isinstance(r, dict)]
         if errors:
-            await self.release(created, wait=False)
+            await self.release(created)
             if self.dra:
                 await self._delete_unused_claims(
                     [(b["metadata"]["namespace"], b["metadata"]["name"])
@@ -508,7 +513,7 @@ class PlaceholderManager:
         try:
             self.faults.check("ledger_reserve", "after")
         except BaseException:
-            await self.release(created, wait=False)
+            await self.release(created)
             raise
         return created
 
@@ -675,6 +680,12 @@ class PlaceholderManager:
         view never takes a GPU from the Pod that claimed it since (raises :class:`Reowned`).
         Any placeholder can change hands, whatever its name: the surplus of a trim pick goes
         back to the warm pool under its ``<pod>-slave-pod-`` name and is claimed from there."""
+        if not self.reownable and p.uid:
+            # no warm pool: nothing ever claims a placeholder from another holder, so the UID
+            # alone pins the object the caller saw. (A version precondition would also trip
+            # over the kubelet's status updates, a GET and a second DELETE per detach.)
+            return await self.kube.delete_pod(p.namespace, p.name, grace_period_s=0,
+                                              uid=p.uid)
         # the cached version only if the cache agrees on the holder; else one read now
         seen = self.informer.cache.get((p.namespace, p.name))
         if seen is None or (p.uid and seen["metadata"].get("uid") != p.uid) or \
@@ -702,8 +713,16 @@ class PlaceholderManager:
                 rv = cur["metadata"].get("resourceVersion", "")
         raise ApiError(409, f"{p.name} kept changing while being deleted")
 
-    async def release(self, phs: Sequence[Placeholder], wait: bool = True,
-                      timeout: Optional[float] = None) -> None:
+    async def release(self, phs: Sequence[Placeholder]) -> None:
+        """Delete the placeholders (grace 0, conditional on the holder the caller saw).
+
+        A DELETE answered 200 or 404 ends the release: with grace 0 and no finalizers the
+        object is gone from the apiserver, and so from the scheduler's books, when the reply
+        comes (the reference's detach also ends at NotFound, allocator.go:284-317). Nothing
+        waits for the watch's DELETED echo: the UIDs stay tombstoned until it arrives, so
+        every later view (owned_by, live, the free set) already leaves them out. A DELETE whose
+        outcome is unknown (5xx, a lost reply, retries exhausted) raises ReserveError and the
+        caller's follow-up retries it."""
         if not phs:
             return
         with trace.span("ledger_release", placeholders=len(phs)):
@@ -754,18 +773,6 @@ class PlaceholderManager:
                 raise ReserveError(f"could not delete {len(failed)} placeholder(s): "
                                    f"{[p.name for p in failed]}")
             self.faults.check("ledger_release", "after")
-            if not wait:
-                return
-            keys = {(p.namespace, p.name): p.uid for p in phs if p not in reowned}
-
-            def gone():
-                for (ns, name), uid in keys.items():
-                    cur = self.informer.cache.get((ns, name))
-                    if cur is not None and (not uid or cur["metadata"].get("uid") == uid):
-                        return False
-                return True
-
-            await self.informer.wait_for(gone, timeout or self.cfg.detach_timeout_s)
 
     @staticmethod
     def from_pod(p: dict, ledger_ids: Dict[Tuple[str, str], List[str]]) -> Placeholder:

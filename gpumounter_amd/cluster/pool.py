@@ -203,7 +203,7 @@ class WarmPool:
             # the node is full: drop the standby placeholders that could not be admitted
             self.exhausted = True
             unadmitted = [c for c in created if not c.device_ids]
-            await self.ph.release(unadmitted, wait=False)
+            await self.ph.release(unadmitted)
         await self.ph.informer.poke()
         return len(created)
 
@@ -276,7 +276,7 @@ class WarmPool:
                 if stray:
                     for ph in stray:            # deleted only while still this attach's
                         ph.owner_uid, ph.attach_id = podu.uid_of(owner), attach_id
-                    await self.ph.release(stray, wait=False)
+                    await self.ph.release(stray)
                 return None
             for ph in chosen:
                 ph.mode = mode
@@ -422,5 +422,5 @@ class WarmPool:
             back, theirs = self._sort_back(keep, res)
             drop += [p for p in keep if p not in back and p not in theirs]
         if drop:
-            await self.ph.release(drop, wait=False)
+            await self.ph.release(drop)
         self.poke()

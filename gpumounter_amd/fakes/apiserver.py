@@ -157,6 +157,9 @@ class FakeCluster:
         self._faults: List[Tuple[str, int, bool, str]] = []
         self._random_faults: Optional[Tuple[float, Any]] = None   # (rate, random.Random)
         self.random_faults_served = 0
+        # every pod watch event reaches its watchers this much later (a slow watch cache, a
+        # congested apiserver); order is kept
+        self.watch_delay_s = 0.0
         from gpumounter_amd.fakes.dra import DraState
         self.dra = DraState(self)     # resource.k8s.io/v1 claims and slices (fakes/dra.py)
 
@@ -176,9 +179,10 @@ class FakeCluster:
         self.events.append((self.rv, etype, data))
         if len(self.events) > self.HISTORY:
             del self.events[: len(self.events) - self.HISTORY]
+        t = time.monotonic()
         for q, ns, lsel, fsel in list(self.watchers):
             if self._matches(pod, ns, lsel, fsel):
-                q.put_nowait((etype, data))
+                q.put_nowait((etype, data, t))
 
     @staticmethod
     def _matches(pod: dict, ns: str, lsel, fsel) -> bool:
@@ -499,11 +503,23 @@ class FakeCluster:
         self.dra.pod_gone(pod)
         self._unschedulable.discard((ns, name))
         node = self.nodes.get(podu.node_of(pod))
+        self._bump("DELETED", pod)
+        self._gc(pod)
+        if node is not None:
+            node.pending_release.add((ns, name))
+        # The apiserver answers the DELETE once the object is gone from storage; the kubelet
+        # learns of it from its own watch and tears the pod down afterwards (containers,
+        # device-manager entry, checkpoint). Modelled as the next loop turn: after this
+        # request's reply, before any later request's admission (allocate() also frees it)
+        try:
+            asyncio.get_running_loop().call_soon(self._teardown, node, ns, name)
+        except RuntimeError:                 # no loop (synchronous test helpers)
+            self._teardown(node, ns, name)
+
+    def _teardown(self, node: Optional[FakeNode], ns: str, name: str) -> None:
         if node is not None:
             node.release_pod(ns, name)
             node.stop_pod_containers(ns, name)
-        self._bump("DELETED", pod)
-        self._gc(pod)
         # capacity freed: retry unschedulable pods (scheduler queue)
         for key in list(self._unschedulable):
             self._spawn(self._schedule(*key))
@@ -701,7 +717,7 @@ class FakeCluster:
                 if req.transport is None or req.transport.is_closing():
                     break  # client went away
                 try:
-                    et, obj = await asyncio.wait_for(q.get(), timeout=min(left, 0.5))
+                    item = await asyncio.wait_for(q.get(), timeout=min(left, 0.5))
                 except asyncio.TimeoutError:
                     idle += 0.5
                     if idle >= 30:
@@ -711,6 +727,11 @@ class FakeCluster:
                         ).encode() + b"\n")
                     continue
                 idle = 0.0
+                et, obj = item[0], item[1]
+                if len(item) > 2 and self.watch_delay_s > 0:
+                    lag = item[2] + self.watch_delay_s - time.monotonic()
+                    if lag > 0:
+                        await asyncio.sleep(lag)
                 rf = self._random_faults
                 if rf is not None and rf[1].random() < rf[0] / 4:
                     # random_failures also disrupts watches: the stream ends before this event

@@ -109,6 +109,10 @@ class FakeNode:
         # device id → (ns, pod, container), and the owning pod's UID
         self.allocated: Dict[str, Tuple[str, str, str]] = {}
         self.alloc_uid: Dict[str, str] = {}
+        # pods deleted at the apiserver whose teardown the kubelet has not run yet: their
+        # devices are freed by that teardown or, whichever comes first, by the next Allocate
+        # (the device manager's UpdateAllocatedDevices drops pods that are no longer active)
+        self.pending_release: set = set()
         # the device manager's checkpoint, rewritten (tmp + rename) after every allocation
         # change like the kubelet's (node/checkpoint.py); write_checkpoint=False models a kubelet
         # that does not maintain it
@@ -172,6 +176,7 @@ class FakeNode:
 
     def free_ids(self) -> List[str]:
         with self._lock:
+            self.release_pending()
             return [d for d in self.device_ids() if d not in self.allocated]
 
     def _checkpoint(self) -> None:
@@ -205,6 +210,7 @@ class FakeNode:
         Only gpumounter's own device plugin (``deviceplugin/plugin.py``, registered through
         the FakeKubelet's device manager) steers placeholders to a chosen set."""
         with self._lock:
+            self.release_pending()
             free = [g for g in self.gpus if self.device_id(g) not in self.allocated]
             if len(free) < n:
                 return None
@@ -228,6 +234,7 @@ class FakeNode:
                uid: str = "") -> bool:
         """Commit an allocation chosen elsewhere (device-plugin path); False if any is taken."""
         with self._lock:
+            self.release_pending()
             if any(d in self.allocated for d in ids):
                 return False
             for d in ids:
@@ -237,8 +244,14 @@ class FakeNode:
             self._checkpoint()
             return True
 
+    def release_pending(self) -> None:
+        with self._lock:
+            while self.pending_release:
+                self.release_pod(*self.pending_release.pop())
+
     def release_pod(self, ns: str, pod: str) -> List[str]:
         with self._lock:
+            self.pending_release.discard((ns, pod))
             ids = [d for d, (n, p, _) in self.allocated.items() if n == ns and p == pod]
             for d in ids:
                 del self.allocated[d]

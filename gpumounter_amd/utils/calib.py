@@ -10,7 +10,9 @@ moves with two properties of the machine it runs on, which this module measures 
   over a loopback TCP connection, median of many: what one hop between the daemons costs before
   any gpumounter code runs (scheduler wake-up of an idle core, C-state exit, cross-CCX cache);
 * ``grpc_rtt_us`` — a unary AddGPU call between two grpc.aio processes answering at once,
-  plaintext and mTLS: the floor under the master → worker hop;
+  plaintext and mTLS: the floor under a gRPC master → worker hop;
+* ``wire_rtt_us`` — the same call over gm-wire (api/wire.py), plaintext and mTLS: the floor
+  under the master → worker hop as shipped;
 * ``pingpong_after_idle_us`` / ``py_loop_after_idle_us`` (with ``idle_s``) — the same round
   trip and the same Python loop right after ``idle_s`` asleep: what a quiet spell costs.
 
@@ -126,8 +128,18 @@ def _grpc_server() -> None:
         plain = server.add_insecure_port("127.0.0.1:0")
         tls = server.add_secure_port("127.0.0.1:0", creds)
         await server.start()
-        print(json.dumps({"plain": plain, "tls": tls, "pki": pki}), flush=True)
+        from gpumounter_amd.api import wire
+        handlers = {wire.METHOD_ADD: (api.AddGPURequest.FromString, lambda r: add(r, None))}
+        wplain = wire.WireServer(handlers)
+        wtls = wire.WireServer(handlers, wire.server_context(pki["worker.crt"],
+                                                             pki["worker.key"], pki["ca"]),
+                               ["gpu-mounter-master"])
+        ports = {"wire_plain": await wplain.start("127.0.0.1", 0),
+                 "wire_tls": await wtls.start("127.0.0.1", 0)}
+        print(json.dumps({"plain": plain, "tls": tls, "pki": pki, **ports}), flush=True)
         await asyncio.get_running_loop().run_in_executor(None, sys.stdin.read)
+        await wplain.stop()
+        await wtls.stop()
         await server.stop(0)
         shutil.rmtree(os.path.dirname(pki["ca"]), ignore_errors=True)
     asyncio.run(run())
@@ -135,7 +147,8 @@ def _grpc_server() -> None:
 
 def grpc_rtt_us(n: int = 1500) -> dict:
     """Median unary AddGPU round trip, grpc.aio client → grpc.aio server in another process,
-    plaintext and with the shipped mTLS: the floor under the master → worker hop."""
+    plaintext and with mTLS, and the same over gm-wire (``wire_plain``, ``wire_mtls``): the
+    floors under the master → worker hop."""
     import asyncio
     import subprocess
     import sys
@@ -174,8 +187,27 @@ def grpc_rtt_us(n: int = 1500) -> dict:
             await ch.close()
             return round(statistics.median(ts[n // 10:]), 1)
 
+        async def wire_one(secure: bool) -> float:
+            from gpumounter_amd.api import wire
+            pki = info["pki"]
+            if secure:
+                ch = wire.WireChannel("127.0.0.1", info["wire_tls"], wire.client_context(
+                    pki["ca"], pki["master.crt"], pki["master.key"]), "gpu-mounter-worker")
+            else:
+                ch = wire.WireChannel("127.0.0.1", info["wire_plain"])
+            payload = api.AddGPURequest(pod_name="t", namespace="default",
+                                        gpu_num=1).SerializeToString()
+            ts = []
+            for _ in range(n):
+                t0 = time.perf_counter()
+                api.AddGPUResponse.FromString(await ch.call(wire.METHOD_ADD, payload, 10))
+                ts.append((time.perf_counter() - t0) * 1e6)
+            await ch.close()
+            return round(statistics.median(ts[n // 10:]), 1)
+
         async def both():
-            return {"plain": await one(False), "mtls": await one(True)}
+            return {"plain": await one(False), "mtls": await one(True),
+                    "wire_plain": await wire_one(False), "wire_mtls": await wire_one(True)}
         return asyncio.run(both())
     finally:
         p.stdin.close()

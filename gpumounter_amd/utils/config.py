@@ -177,7 +177,6 @@ class Config:
     kill_reap_s: float = 2.0
     # --- timeouts / loops ------------------------------------------------------------------
     attach_timeout_s: float = 120.0    # placeholder admission deadline
-    detach_timeout_s: float = 60.0     # wait for placeholder deletion where waited for
     rpc_timeout_s: float = 180.0       # master→worker gRPC deadline (reference: none)
     reconcile_period_s: float = 30.0   # full reconciler sweep period
     # every this many seconds, compare each hot container's device-control state (v2: the

@@ -216,7 +216,7 @@ class DrainKeeper:
         for ph in phs:
             self.held.pop(ph.uid, None)
         self.svc.metrics.draining.set(len(self.held))
-        await self.svc.ph.release(list(phs), wait=False)
+        await self.svc.ph.release(list(phs))
         if any(self.unmarked.pop(ph.uid, None) is not None for ph in phs):
             self._save()
         self.released += len(phs)

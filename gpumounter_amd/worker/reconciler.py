@@ -483,7 +483,7 @@ class Reconciler:
             for p in phs:
                 rep.owner_gone.append(p["metadata"]["name"])
                 m.orphans.labels(kind="owner_gone").inc()
-            await svc.ph.release([svc.ph.from_pod(p, {}) for p in phs], wait=False)
+            await svc.ph.release([svc.ph.from_pod(p, {}) for p in phs])
 
         for key in by_owner:
             oname, ons, ouid = key
@@ -524,7 +524,7 @@ class Reconciler:
                          or svc.is_abandoned(p)]
                 if cands:
                     rep.stuck += [p["metadata"]["name"] for p in cands]
-                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in cands], wait=False)
+                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in cands])
                     for p in cands:
                         svc.abandoned.pop(p["metadata"].get("uid", ""), None)
                     phs = [p for p in phs if p not in cands]
@@ -550,7 +550,7 @@ class Reconciler:
                             stuck.append(p)
                 if stuck:
                     rep.stuck += [p["metadata"]["name"] for p in stuck]
-                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in stuck], wait=False)
+                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in stuck])
                 if podu.phase_of(owner) != "Running":
                     continue
                 try:

@@ -714,7 +714,7 @@ class GpuMountService:
         if self.pool is not None and self.pool.enabled:
             await self.pool.give_back(phs)
         else:
-            await self.ph.release(phs, wait=False)
+            await self.ph.release(phs)
 
     def _plan_with_pool(self, n: int, st: PodGpuState):
         return planning.plan_with_pool(self.inv, self.cfg.topology_policy, self.pool.standby(),

@@ -111,7 +111,7 @@ class FakePH:
         self.tombstones = {}
         self.keep_picked = PlaceholderManager.keep_picked
 
-    async def release(self, phs, wait=True, timeout=None):
+    async def release(self, phs):
         failed = []
         for p in phs:
             err = self.api.delete(p.uid)
@@ -134,11 +134,11 @@ class FakePH:
             else:
                 errors.append(err)
         if errors:
-            await self.release(created, wait=False)
+            await self.release(created)
             raise ReserveError(f"placeholder create failed: {errors[0]}")
         failed = [p for p in created if not p.device_ids]
         if failed:
-            await self.release(failed, wait=False)
+            await self.release(failed)
         out = [p for p in created if p.device_ids]
         for p in out:
             self.device_ids[p.uid] = p.device_ids

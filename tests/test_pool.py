@@ -281,7 +281,7 @@ def test_release_of_a_placeholder_in_status_churn_still_deletes_it():
                         "churn": str(churn[0])}}})
                 return await delete(ns, name, **kw)
             svc.ph.kube.delete_pod = churning
-            await svc.ph.release([ph], wait=False)
+            await svc.ph.release([ph])
             assert lc.cluster.get(ph.namespace, ph.name) is None
     asyncio.run(main())
 
@@ -361,7 +361,7 @@ def test_release_of_a_claimed_placeholder_behind_a_stale_cache_still_deletes_it(
                                    attach_id="add-a")
             assert got is not None and got.placeholders[0].owner_uid
             svc.ph.informer.cache[key] = stale          # the claim never reached the cache
-            await svc.ph.release(got.placeholders, wait=False)
+            await svc.ph.release(got.placeholders)
             assert lc.cluster.get(*key) is None
     asyncio.run(main())
 
