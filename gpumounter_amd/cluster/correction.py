@@ -133,12 +133,14 @@ class Correction:
     def __init__(self, ph, inv, free: Sequence[AmdGpu], attached: Sequence[AmdGpu], owner: dict,
                  n: int, entire: bool, group: str, attach_id: str, container: str,
                  idempotency_key: str, policy: str, faults,
-                 release_quiet: Callable[[Sequence[Placeholder]], "asyncio.Future"]) -> None:
+                 release_quiet: Callable[[Sequence[Placeholder]], "asyncio.Future"],
+                 lease_expires: float = 0.0) -> None:
         self.ph, self.inv, self.faults = ph, inv, faults
         self.free, self.attached, self.owner = list(free), list(attached), owner
         self.n, self.entire, self.group = n, entire, group
         self.attach_id, self.container, self.key = attach_id, container, idempotency_key
         self.policy = policy
+        self.lease_expires = lease_expires      # the attach's lease, on every hold it makes
         self.release_quiet = release_quiet
         self.entries: List[List] = []            # [placeholder, Book]
         self.corrected = False
@@ -181,7 +183,8 @@ class Correction:
     # ------------------------------------------------------------------------ transitions
     async def _hold(self, width: int) -> List[Placeholder]:
         got = await self.ph.hold_singles(self.owner, width, self.entire, self.group,
-                                         self.attach_id, self.container, self.key)
+                                         self.attach_id, self.container, self.key,
+                                         self.lease_expires)
         self._add(got, Book.HELD)
         return got
 

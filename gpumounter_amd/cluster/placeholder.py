@@ -42,7 +42,7 @@ from gpumounter_amd.cluster.kube import ApiError, Conflict, KubeClient, NotFound
 from gpumounter_amd.cluster.quota import QuotaExceeded
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTAINER, ANN_GROUP,
-                                         ANN_IDEMPOTENCY, ANN_INCARNATION,
+                                         ANN_IDEMPOTENCY, ANN_INCARNATION, ANN_LEASE,
                                          ANN_MOUNT_MODE, ANN_OWNER_UID, ANN_PREFERRED, LABEL_APP,
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          SLAVE_SUFFIX)
@@ -209,7 +209,11 @@ class PlaceholderManager:
         return f"{LABEL_APP}={LABEL_APP_VALUE},{LABEL_NODE}={_label_value(node)}"
 
     def build(self, owner: dict, n_gpus: int, mode: str, preferred: Sequence[str] = (),
-              attach_id: str = "", container: str = "", idempotency_key: str = "") -> dict:
+              attach_id: str = "", container: str = "", idempotency_key: str = "",
+              lease_expires: float = 0.0) -> dict:
+        """The placeholder Pod for ``owner``. ``lease_expires`` (Unix seconds, 0 = none) is
+        written at creation, so a leased GPU is never booked without its lease (reference:
+        every slave-pod field is set in the create, allocator.go:189-234)."""
         ns = self.namespace_for(owner)
         name = podu.name_of(owner)[: 253 - 20] + SLAVE_SUFFIX + secrets.token_hex(3)
         md = {
@@ -228,6 +232,8 @@ class PlaceholderManager:
             md["annotations"][ANN_PREFERRED] = ",".join(preferred)
         if idempotency_key:
             md["annotations"][ANN_IDEMPOTENCY] = idempotency_key
+        if lease_expires > 0:
+            md["annotations"][ANN_LEASE] = f"{lease_expires:.3f}"
         if ns == podu.ns_of(owner):
             md["ownerReferences"] = [{"apiVersion": "v1", "kind": "Pod",
                                       "name": podu.name_of(owner), "uid": podu.uid_of(owner),
@@ -313,7 +319,7 @@ class PlaceholderManager:
     # ------------------------------------------------------------------------ reserve
     async def reserve(self, owner: dict, total: int, entire: bool, preferred: Sequence[str] = (),
                       attach_id: str = "", container: str = "",
-                      idempotency_key: str = "") -> Reservation:
+                      idempotency_key: str = "", lease_expires: float = 0.0) -> Reservation:
         """Entire mount = one placeholder holding ``total`` GPUs (all-or-nothing at the
         scheduler, reference QuickStart.md:52); single mount = ``total`` placeholders × 1 GPU."""
         if total <= 0:
@@ -324,7 +330,7 @@ class PlaceholderManager:
         prefs = [list(preferred[i * per_pod:(i + 1) * per_pod]) for i in range(k)] \
             if len(preferred) == total else [[] for _ in range(k)]
         bodies = [self.build(owner, per_pod, mode, prefs[i], attach_id, container,
-                             idempotency_key) for i in range(k)]
+                             idempotency_key, lease_expires) for i in range(k)]
         created = await self._create(bodies)
         try:
             with trace.span("placeholder_wait"):
@@ -340,7 +346,7 @@ class PlaceholderManager:
             _log.info("preferred devices %s not allocatable; retrying unpinned",
                       list(preferred))
             return await self.reserve(owner, total, entire, (), attach_id, container,
-                                      idempotency_key)
+                                      idempotency_key, lease_expires)
         except BaseException:
             await self.release(created)
             raise
@@ -348,15 +354,16 @@ class PlaceholderManager:
 
     async def hold_singles(self, owner: dict, width: int, entire: bool, group: str = "",
                            attach_id: str = "", container: str = "",
-                           idempotency_key: str = "") -> List[Placeholder]:
+                           idempotency_key: str = "", lease_expires: float = 0.0
+                           ) -> List[Placeholder]:
         """Create ``width`` 1-GPU placeholders at once and wait for their admission; returns
         the admitted ones (those the scheduler could not place are released). An entire mount
         ties them by ``group`` (``ANN_GROUP``)."""
         if width <= 0:
             return []
         mode = "entire" if entire else "single"
-        bodies = [self.build(owner, 1, mode, (), attach_id, container, idempotency_key)
-                  for _ in range(width)]
+        bodies = [self.build(owner, 1, mode, (), attach_id, container, idempotency_key,
+                             lease_expires) for _ in range(width)]
         for b in bodies:
             b["metadata"]["annotations"][ANN_CANDIDATE] = attach_id or "1"
             if group:
@@ -379,7 +386,8 @@ class PlaceholderManager:
 
     async def reserve_trim(self, owner: dict, total: int, entire: bool, width: int,
                            pick: Callable[[List[str]], Sequence[str]], attach_id: str = "",
-                           container: str = "", idempotency_key: str = ""
+                           container: str = "", idempotency_key: str = "",
+                           lease_expires: float = 0.0
                            ) -> Tuple[Reservation, List[Placeholder]]:
         """Topology-pinned reservation. Which GPU the device plugin hands a
         placeholder is opaque to us, so hold ``width`` (= every free GPU) 1-GPU placeholders at
@@ -391,7 +399,7 @@ class PlaceholderManager:
             raise ValueError(f"bad trim reservation {total}/{width}")
         admitted = await self.hold_singles(owner, width, entire,
                                            secrets.token_hex(4) if entire else "", attach_id,
-                                           container, idempotency_key)
+                                           container, idempotency_key, lease_expires)
         if len(admitted) < total:
             await self.release(admitted)
             raise InsufficientGPU(f"only {len(admitted)} of {total} GPUs admitted")

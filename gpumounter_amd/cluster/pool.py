@@ -211,9 +211,12 @@ class WarmPool:
     async def claim(self, owner: dict, n: int, entire: bool, attached: Sequence[AmdGpu],
                     attach_id: str = "", container: str = "",
                     idempotency_key: str = "",
-                    want: Optional[Sequence[int]] = None) -> Optional[Reservation]:
+                    want: Optional[Sequence[int]] = None,
+                    lease_expires: float = 0.0) -> Optional[Reservation]:
         """Claim ``n`` standby GPUs for ``owner`` (exactly the GPU indices ``want`` when the
-        caller planned the placement over standby ∪ free GPUs); None if the pool cannot."""
+        caller planned the placement over standby ∪ free GPUs); None if the pool cannot.
+        ``lease_expires`` goes into the same conditional claim PATCH, so a leased claim is
+        never recorded without its lease (and an unleased one clears any earlier owner's)."""
         async with self._lock:
             pool = self.standby()
             if len(pool) < n:
@@ -246,7 +249,8 @@ class WarmPool:
                                 ANN_ATTACH_ID: attach_id, ANN_CONTAINER: container,
                                 ANN_IDEMPOTENCY: idempotency_key or None,
                                 ANN_GROUP: group or None, ANN_CANDIDATE: None,
-                                ANN_LEASE: None}}}
+                                ANN_LEASE: f"{lease_expires:.3f}" if lease_expires > 0
+                                else None}}}
             for ph in chosen:
                 self._claimed.add(ph.uid)
             seen = self._versions()

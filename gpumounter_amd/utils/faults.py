@@ -3,12 +3,15 @@
 Spec: ``stage:prob[:mode][,stage:prob[:mode]...]`` where ``stage`` is one of
 ``pod_lookup, ledger_read, ledger_reserve, placeholder_wait, cgroup_rule, devnodes, busy_check,
 unmount, ledger_release`` (the span names of :mod:`gpumounter_amd.utils.trace`), ``prob`` in
-[0, 1], and ``mode`` ``raise`` (default) or ``after`` (fail *after* the stage's side effect, the
-hard case for rollback). The reference has no such hooks; the test suite uses them
-to prove every failure path restores a consistent ledger and leaves no orphaned rules or nodes.
+[0, 1], and ``mode`` ``raise`` (default), ``after`` (fail *after* the stage's side effect, the
+hard case for rollback) or ``exit`` (the process dies at once, before the stage, as under a
+SIGKILL: exit status 137, nothing cleaned up). The reference has no such hooks; the
+test suite uses them to prove every failure path restores a consistent ledger and leaves no
+orphaned rules or nodes.
 """
 from __future__ import annotations
 
+import os
 import random
 import threading
 from dataclasses import dataclass
@@ -36,7 +39,7 @@ class FaultInjector:
             if len(bits) < 2:
                 raise ValueError(f"bad fault spec {part!r} (want stage:prob[:mode])")
             mode = bits[2] if len(bits) > 2 else "raise"
-            if mode not in ("raise", "after"):
+            if mode not in ("raise", "after", "exit"):
                 raise ValueError(f"bad fault mode {mode!r}")
             self.rules[bits[0]] = Rule(float(bits[1]), mode)
 
@@ -47,13 +50,15 @@ class FaultInjector:
         """Raise :class:`InjectedFault` if ``stage`` is armed for this phase (``raise`` = before
         the side effect, ``after`` = after it)."""
         r = self.rules.get(stage)
-        if r is None or r.mode != when:
+        if r is None or (r.mode != when and not (r.mode == "exit" and when == "raise")):
             return
         with self._lock:
             fire = self._rnd.random() < r.prob
             if fire:
                 r.hits += 1
         if fire:
+            if r.mode == "exit":
+                os._exit(137)            # a SIGKILL at this point: no finally, no cleanup
             raise InjectedFault(f"injected fault at {stage} ({when})")
 
 

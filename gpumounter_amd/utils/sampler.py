@@ -38,8 +38,9 @@ def _short(path: str) -> str:
 
 
 def _lib(short: str) -> str:
-    """``gpumounter_amd/worker/x.py`` → ``gpumounter_amd/worker``; ``lib/python3.10/
-    dist-packages/grpc/aio/_call.py`` → ``grpc``; ``lib/python3.10/json/decoder.py`` → ``json``."""
+    """``gpumounter_amd/worker/x.py`` → ``gpumounter_amd/worker``;
+    ``lib/python3.10/dist-packages/grpc/aio/_call.py`` → ``grpc``;
+    ``lib/python3.10/json/decoder.py`` → ``json``."""
     parts = short.split("/")
     if parts[0] == "gpumounter_amd":
         return "/".join(parts[:2])

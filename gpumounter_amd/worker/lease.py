@@ -65,7 +65,9 @@ class LeaseKeeper:
 
     # ------------------------------------------------------------------------ grant
     async def grant(self, pod: dict, placeholders, lease_s: float) -> float:
-        """Stamp the expiry on the attach's placeholders and arm a timer. Returns the expiry."""
+        """Stamp the expiry on placeholders booked without it and arm a timer; returns the
+        expiry. Attaches write their lease with the booking (:meth:`booked`); this is for the
+        replay of an attach an older worker (one PATCH after the mount) left unleased."""
         expires = time.time() + lease_s
         patch = {"metadata": {"annotations": {ANN_LEASE: f"{expires:.3f}"}}}
         informer = self.svc.ph.informer
@@ -79,6 +81,15 @@ class LeaseKeeper:
                     self._granted[p.uid] = (expires, _holder(r))
             self._arm(p.uid, podu.ns_of(pod), podu.name_of(pod), expires)
         return expires
+
+    def booked(self, pod: dict, placeholders, expires: float) -> None:
+        """An attach whose placeholders were created or claimed with the lease annotation
+        (cluster/placeholder.py ``build``, cluster/pool.py ``claim``): remember the grant and arm
+        the timers; nothing is written."""
+        for p in placeholders:
+            if p.uid:
+                self._granted[p.uid] = (expires, (p.owner_uid, p.attach_id))
+            self._arm(p.uid, podu.ns_of(pod), podu.name_of(pod), expires)
 
     def granted(self, raw: dict) -> Optional[float]:
         """The expiry this worker granted to placeholder ``raw`` for the attach that holds it

@@ -362,7 +362,8 @@ class Worker:
         runtime.write_ready_file(self.cfg.ready_file, {"grpc_port": self.grpc_port,
                                                        "http_port": self.http_port,
                                                        "wire_port": self.wire_port})
-        _log.info("worker %s serving gRPC :%d gm-wire :%d http :%d (cgroup %s/%s, devnodes %s, ledger %s)",
+        _log.info("worker %s serving gRPC :%d gm-wire :%d http :%d (cgroup %s/%s, devnodes %s, "
+                  "ledger %s)",
                   self.cfg.node_name, self.grpc_port, self.wire_port, self.http_port,
                   self.resolver.mode,
                   self.backend.name, self.cfg.devnode_mode, self.ledger.api_version)

@@ -472,9 +472,12 @@ class GpuMountService:
             with trace.span("placement"):
                 free = self._free(st)
                 preferred = self._preferred(n, st, free)
+            # a lease is part of the booking: every placeholder is created (or claimed) with it,
+            # so no crash can leave a leased GPU booked without one
+            lease_exp = time.time() + req.lease_s if req.lease_s > 0 else 0.0
             try:
                 async with self._quota_guard(req.namespace, n):
-                    res = await self._reserve(pod, n, req, st, preferred, len(free))
+                    res = await self._reserve(pod, n, req, st, preferred, len(free), lease_exp)
                     await self._quota_recheck(req.namespace, n, res)
             except QuotaExceeded as e:
                 _log.info("quota refused %d GPU(s) for %s/%s: %s", n, req.namespace,
@@ -524,16 +527,9 @@ class GpuMountService:
                                               message=f"pod went away during the attach: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             msg = "Add GPU Success"
-            if req.lease_s > 0:
-                try:
-                    expires = await self.lease.grant(pod, res.placeholders, req.lease_s)
-                except Exception as e:  # noqa: BLE001 - a lease must not be silently dropped
-                    _log.error("lease on %s/%s not recorded: %s", req.namespace, req.pod_name, e)
-                    await self._release_or_follow_up(pod, res.placeholders, "an unrecorded lease")
-                    await self._rollback(pod, "attach")
-                    raise RpcError(grpc.StatusCode.INTERNAL,
-                                   f"{ERR_INTERNAL}: lease not recorded: {e}") from e
-                msg += time.strftime(" (lease until %Y-%m-%dT%H:%M:%SZ)", time.gmtime(expires))
+            if lease_exp:
+                self.lease.booked(pod, res.placeholders, lease_exp)     # timers; no write
+                msg += time.strftime(" (lease until %Y-%m-%dT%H:%M:%SZ)", time.gmtime(lease_exp))
             log.kv(_log, 20, "attached", pod=f"{req.namespace}/{req.pod_name}",
                    gpus=[g.bdf for g in new], by=req.requested_by, lease_s=req.lease_s)
             self.notify.attached(pod, new, list(st.hot) + new,
@@ -600,7 +596,7 @@ class GpuMountService:
                                   message="Add GPU Success (replayed)")
 
     async def _reserve(self, pod: dict, n: int, req, st: PodGpuState, preferred: List[str],
-                       n_free: int = 0):
+                       n_free: int = 0, lease_exp: float = 0.0):
         """Claim from the warm pool first (if enabled), create placeholders for the rest.
 
         Placement (``placement_enforce``): the device plugin decides which GPUs a placeholder
@@ -614,17 +610,17 @@ class GpuMountService:
         mode = self.cfg.placement_enforce
         if (mode != "trim" or dra) and self.plugin is None:
             async with self._reserve_gate.shared():
-                res = await self._reserve_unlocked(pod, n, req, st, preferred, n_free)
+                res = await self._reserve_unlocked(pod, n, req, st, preferred, n_free, lease_exp)
             if mode == "auto" and not dra and res.corrigible and \
                     self._placement_worse(st, res.device_ids, preferred):
                 async with self._reserve_gate.exclusive():
-                    res = await self._correct(pod, n, req, st, res)
+                    res = await self._correct(pod, n, req, st, res, lease_exp)
             return res
         async with self._reserve_gate.exclusive():
             # recompute against the ledger as it is now that we hold the node
             free = self._free(st)
             preferred = self._preferred(n, st, free)
-            res = await self._reserve_unlocked(pod, n, req, st, preferred, len(free))
+            res = await self._reserve_unlocked(pod, n, req, st, preferred, len(free), lease_exp)
             if not res.preferred:
                 res.preferred = list(preferred)
             return res
@@ -634,14 +630,15 @@ class GpuMountService:
         return placement_worse(self.inv, st.hot + st.own, got, want,
                                getattr(self.cfg, "placement_correct_on", "numa"))
 
-    async def _correct(self, pod: dict, n: int, req, st: PodGpuState, res):
+    async def _correct(self, pod: dict, n: int, req, st: PodGpuState, res,
+                       lease_exp: float = 0.0):
         """Swap the plugin's worse-placed choice for the best free set (cluster/correction.py:
         hold every other free GPU, keep the best ``n``, release the rest)."""
         c = Correction(self.ph, self.inv, self._free(st), st.hot + st.own, pod, n,
                        req.is_entire_mount, secrets.token_hex(4) if req.is_entire_mount else "",
                        log.request_id.get(), req.container, req.idempotency_key,
                        self.cfg.topology_policy, self.faults,
-                       lambda phs: self._release_quiet(pod, phs))
+                       lambda phs: self._release_quiet(pod, phs), lease_exp)
         out = await c.run(res)
         if c.corrected:
             self.metrics.placement_corrections.inc()
@@ -656,7 +653,7 @@ class GpuMountService:
             self._follow_up(pod, phs)
 
     async def _reserve_unlocked(self, pod: dict, n: int, req, st: PodGpuState,
-                                preferred: List[str], n_free: int):
+                                preferred: List[str], n_free: int, lease_exp: float = 0.0):
         claimed = None
         create_pref = preferred
         if self.pool is not None and self.pool.enabled and self.pool.standby():
@@ -666,7 +663,7 @@ class GpuMountService:
                 claimed = await self.pool.claim(pod, len(claim_idx), req.is_entire_mount,
                                                 st.hot + st.own, log.request_id.get(),
                                                 req.container, req.idempotency_key,
-                                                want=claim_idx)
+                                                want=claim_idx, lease_expires=lease_exp)
                 if claimed is not None:
                     create_pref = plan_pref
         got = len(claimed.placeholders) if claimed else 0
@@ -678,7 +675,7 @@ class GpuMountService:
         if not got and preferred and self.cfg.placement_enforce == "trim" and n_free > n \
                 and self.cfg.gpu_allocation != "dra":
             try:
-                return await self._reserve_trim(pod, n, req, st, n_free)
+                return await self._reserve_trim(pod, n, req, st, n_free, lease_exp)
             except QuotaExceeded as e:
                 # tenant-namespace placeholders: holding every free GPU can exceed the
                 # tenant's quota although the request fits; reserve it plainly instead
@@ -693,7 +690,8 @@ class GpuMountService:
             rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
                                          attach_id=log.request_id.get(),
                                          container=req.container,
-                                         idempotency_key=req.idempotency_key)
+                                         idempotency_key=req.idempotency_key,
+                                         lease_expires=lease_exp)
         except BaseException:
             if claimed:
                 await self.pool.give_back(claimed.placeholders)
@@ -720,7 +718,8 @@ class GpuMountService:
         return planning.plan_with_pool(self.inv, self.cfg.topology_policy, self.pool.standby(),
                                        n, st, self._free(st))
 
-    async def _reserve_trim(self, pod: dict, n: int, req, st: PodGpuState, width: int):
+    async def _reserve_trim(self, pod: dict, n: int, req, st: PodGpuState, width: int,
+                            lease_exp: float = 0.0):
         keys = self.inv.by_key()
         attached = st.hot + st.own
 
@@ -734,7 +733,8 @@ class GpuMountService:
 
         res, surplus = await self.ph.reserve_trim(
             pod, n, req.is_entire_mount, width, pick, attach_id=log.request_id.get(),
-            container=req.container, idempotency_key=req.idempotency_key)
+            container=req.container, idempotency_key=req.idempotency_key,
+            lease_expires=lease_exp)
         res.preferred = res.device_ids                    # trim keeps exactly what it picked
         if surplus:
             with trace.span("placement_release", placeholders=len(surplus)):

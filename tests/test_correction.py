@@ -123,7 +123,7 @@ class FakePH:
             raise ReserveError(f"could not delete {len(failed)} placeholder(s)")
 
     async def hold_singles(self, owner, width, entire, group="", attach_id="", container="",
-                           idempotency_key=""):
+                           idempotency_key="", lease_expires=0.0):
         if width <= 0:
             return []
         created, errors = [], []

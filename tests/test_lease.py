@@ -3,6 +3,8 @@ import asyncio
 import subprocess
 import time
 
+import pytest
+
 from gpumounter_amd import _native
 from gpumounter_amd.fakes.harness import LocalCluster
 from gpumounter_amd.worker.lease import ANN_LEASE
@@ -357,3 +359,110 @@ def test_a_lease_granted_to_part_of_an_entire_mount_group_ends_the_whole_group()
         assert await until(gone, 2.0)
         assert not await lc.audit("default", "t")
     run(body, worker_overrides={"warm_pool_size": 3})
+
+
+def _writes(lc):
+    v = lc.cluster.requests_by_verb
+    return {k: v.get(k, 0) for k in ("POST", "PATCH", "DELETE")}
+
+
+def _count(before, after):
+    return {k: after[k] - before[k] for k in after}
+
+
+@pytest.mark.parametrize("mode", ["plain", "pool", "dra", "trim"])
+def test_a_leased_attach_writes_no_more_than_an_unleased_one(mode):
+    """The lease travels in the booking itself (placeholder POST, pool claim PATCH, the DRA
+    placeholder): no write is added for it (round 4: one PATCH per placeholder after the
+    mount, and a crash window between "GPU granted" and "lease recorded")."""
+    kw = {"worker_overrides": {}}
+    if mode == "pool":
+        kw["worker_overrides"]["warm_pool_size"] = 4
+    if mode == "dra":
+        kw["gpu_api"] = "dra"
+    if mode == "trim":
+        kw["worker_overrides"]["placement_enforce"] = "trim"
+
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        if mode == "pool":
+            await svc.ph.informer.wait_for(lambda: len(svc.pool.standby()) >= 4, 10)
+        counts = {}
+        for lease in ("", "3600"):
+            await asyncio.sleep(0.05)
+            before = _writes(lc)
+            code, b = await lease_add(lc, "default", "t", 2, lease) if lease else \
+                await lc.add("default", "t", 2)
+            assert code == 200, b
+            counts[lease] = _count(before, _writes(lc))
+            leased = [p for p in lc.cluster.placeholders()
+                      if (p["metadata"].get("annotations") or {}).get(
+                          "gpumounter.amd.com/owner-name") == "t"
+                      and (p["metadata"].get("annotations") or {}).get(ANN_LEASE)]
+            assert len(leased) == (2 if lease else 0), leased
+            code, _ = await lc.remove("default", "t", [d["uuid"] for d in b["devices"]])
+            assert code == 200
+            if mode == "pool":
+                await svc.ph.informer.wait_for(lambda: len(svc.pool.standby()) >= 4, 10)
+        assert counts["3600"] == counts[""], counts
+    run(body, **kw)
+
+
+@pytest.mark.parametrize("pool", [0, 2])
+def test_a_worker_killed_between_booking_and_mount_leaves_no_unleased_placeholder(pool):
+    """GM_FAULT=cgroup_rule:1:exit: the worker process dies (as under SIGKILL) after its
+    placeholders are booked and admitted, before anything is mounted. Every placeholder the
+    attach booked already carries the lease; the next worker finishes the attach on the
+    client's retry (same idempotency key) and the lease ends it on time."""
+    import json as _json
+
+    from gpumounter_amd.fakes.deployment import ProcessCluster
+
+    with ProcessCluster(worker_env={"GM_FAULT": "cgroup_rule:1.0:exit",
+                                    "GM_WARM_POOL_SIZE": str(pool)}) as pc:
+        pc.tenant("t")
+        if pool:
+            end = time.time() + 20
+            while time.time() < end and sum(
+                    1 for p in pc.placeholders()
+                    if (p["metadata"].get("annotations") or {}).get(
+                        "gpumounter.amd.com/mount-mode") == "standby") < pool:
+                time.sleep(0.05)
+        q = "/addgpu/namespace/default/pod/t/gpu/2/isEntireMount/false?lease=2"
+        code, body = pc._master("GET", q, headers={"Accept": "application/json",   # noqa: SLF001
+                                                   "Idempotency-Key": "K1"})
+        assert code == 500, body
+        assert pc.procs["worker-node-0"].wait(10) == 137
+        mine = [p for p in pc.placeholders()
+                if (p["metadata"].get("annotations") or {}).get(
+                    "gpumounter.amd.com/owner-name") == "t"]
+        assert mine, "the booking happened before the crash"
+        assert all((p["metadata"].get("annotations") or {}).get(ANN_LEASE) for p in mine), \
+            [p["metadata"]["annotations"] for p in mine]
+        # a worker without the fault: the client's retry replays the attach with its lease
+        pc._worker_env["node-0"].pop("GM_FAULT")                    # noqa: SLF001
+        pc.restart_worker("node-0")
+        end = time.time() + 10
+        while True:          # until the master's worker watch has the new address
+            code, body = pc._master("GET", q, headers={                        # noqa: SLF001
+                "Accept": "application/json", "Idempotency-Key": "K1"})
+            if code == 200 or time.time() > end:
+                break
+            time.sleep(0.1)
+        assert code == 200, body
+        body = _json.loads(body)
+        assert len(body["devices"]) == 2
+        end = time.time() + 10
+        left = None
+        while time.time() < end:
+            left = [p for p in pc.placeholders()
+                    if (p["metadata"].get("annotations") or {}).get(
+                        "gpumounter.amd.com/owner-name") == "t"
+                    and (p["metadata"].get("annotations") or {}).get(
+                        "gpumounter.amd.com/mount-mode") != "standby"]
+            if not left:
+                break
+            time.sleep(0.1)
+        assert not left, "the lease never ended the attach"
+        assert pc.audit("default", "t") == []
