@@ -104,6 +104,7 @@ class Reconciler:
         self.guard_repairs = 0
         self._guard_task = None
         self._guard_timer = None
+        self._guard_running: Optional[asyncio.Task] = None   # one pass at a time
 
     # ------------------------------------------------------------------------ events
     def watch_events(self) -> None:
@@ -156,27 +157,37 @@ class Reconciler:
         return [e.cgdir for e in self.svc.hm.journal.entries()
                 if e.pod_uid == uid and e.rules and e.cgdir]
 
-    def guard_once(self) -> List[tuple]:
-        """Compare every hot container's device-control fingerprint with the one gpumounter left
-        (node/hotmount.py ``expected``); a container whose state changed behind our back (the
-        runtime re-attached its program, runc update, systemd, a devices.allow/deny write) has
-        its pod reconciled now. Returns the (namespace, pod) pairs kicked."""
+    def _guard_targets(self) -> List[tuple]:
+        """(journal entry, cgroup dir) of every hot container with device rules."""
+        return [(e, e.cgdir) for e in self.svc.hm.journal.entries() if e.rules and e.cgdir]
+
+    @staticmethod
+    def _fingerprints(fingerprint, dirs: List[str]) -> List[object]:
+        """One syscall (BPF_PROG_QUERY) or one small read (devices.list) per cgroup, and
+        whether the directory still exists: the part of a guard pass that touches the kernel,
+        run off the event loop."""
+        return [(fingerprint(d), os.path.isdir(d)) for d in dirs]
+
+    def _guard_compare(self, targets: List[tuple], seen: List[object],
+                       before: Dict[str, object]) -> List[tuple]:
+        """The loop-side half of a pass: compare fingerprints taken at ``before`` (the expected
+        state then) with what gpumounter expects now."""
         hm = self.svc.hm
         kicked = []
         live = set()
-        for e in hm.journal.entries():
-            if not e.rules or not e.cgdir:
+        for (e, d), (fp, exists) in zip(targets, seen):
+            live.add(d)
+            if d not in before:
+                if d not in hm.expected:
+                    hm.expected[d] = fp         # first sight (a restarted worker): baseline
                 continue
-            live.add(e.cgdir)
-            fp = getattr(hm.backend, "fingerprint", lambda d: None)(e.cgdir)
-            if e.cgdir not in hm.expected:
-                hm.expected[e.cgdir] = fp       # first sight (a restarted worker): baseline
-                continue
-            if fp != hm.expected[e.cgdir] and os.path.isdir(e.cgdir):
-                hm.expected[e.cgdir] = fp       # kicked once; the repair records its own
+            if hm.expected.get(d) is not before[d]:
+                continue                        # gpumounter changed it meanwhile: next pass
+            if fp != hm.expected[d] and exists:
+                hm.expected[d] = fp             # kicked once; the repair records its own
                 self.guard_repairs += 1
                 _log.warning("device control of %s/%s changed outside gpumounter (%s); "
-                             "re-checking its hot-mounted GPUs", e.namespace, e.pod, e.cgdir)
+                             "re-checking its hot-mounted GPUs", e.namespace, e.pod, d)
                 key = ("guard", e.namespace, e.pod)
                 self._kick(key)
                 kicked.append(key[1:])
@@ -184,14 +195,45 @@ class Reconciler:
             del hm.expected[d]
         return kicked
 
+    def guard_once(self) -> List[tuple]:
+        """Compare every hot container's device-control fingerprint with the one gpumounter left
+        (node/hotmount.py ``expected``); a container whose state changed behind our back (the
+        runtime re-attached its program, runc update, systemd, a devices.allow/deny write) has
+        its pod reconciled now. Returns the (namespace, pod) pairs kicked. Synchronous: the
+        periodic guard runs :meth:`guard_pass`, which fingerprints in a thread."""
+        targets = self._guard_targets()
+        fp = getattr(self.svc.hm.backend, "fingerprint", lambda d: None)
+        before = dict(self.svc.hm.expected)
+        return self._guard_compare(targets, self._fingerprints(fp, [d for _, d in targets]),
+                                   before)
+
+    async def guard_pass(self) -> List[tuple]:
+        """:meth:`guard_once` with the kernel reads in the default executor: a node with many
+        hot containers (CPX partitions: up to 64 per node) costs the RPC loop only the compare.
+        A fingerprint taken while an attach or detach changed that cgroup is not compared (the
+        expected state it was taken against is gone); the next pass looks again."""
+        targets = self._guard_targets()
+        if not targets:
+            return self._guard_compare([], [], {})
+        fp = getattr(self.svc.hm.backend, "fingerprint", lambda d: None)
+        before = dict(self.svc.hm.expected)
+        seen = await asyncio.to_thread(self._fingerprints, fp, [d for _, d in targets])
+        return self._guard_compare(targets, seen, before)
+
     def _guard_soon(self, delay: float = 0.2) -> None:
         if self._guard_timer is None and not self._stopping:
             self._guard_timer = asyncio.get_running_loop().call_later(delay, self._guard_fire)
 
     def _guard_fire(self) -> None:
         self._guard_timer = None
+        if self._guard_running is None or self._guard_running.done():
+            self._guard_running = asyncio.ensure_future(self._guard_safe())
+
+    async def _guard_safe(self) -> None:
         try:
-            self.guard_once()
+            await self.guard_pass()
+        except asyncio.CancelledError:
+            raise
         except Exception as e:  # noqa: BLE001 - the next tick or the sweep retries
             _log.warning("device guard: %s", e)
 
@@ -334,6 +376,8 @@ class Reconciler:
             self._guard_task.cancel()
         if self._guard_timer is not None:
             self._guard_timer.cancel()
+        if self._guard_running is not None:
+            self._guard_running.cancel()
         for h in list(self._timers.values()):
             h.cancel()
         self._timers.clear()

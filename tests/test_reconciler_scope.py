@@ -232,3 +232,53 @@ def test_device_guard_repairs_rules_replaced_outside_gpumounter_within_a_second(
         await asyncio.sleep(0.4)
         assert w.reconciler.guard_repairs == n0
     run(body, cgroup_mode=mode, worker_overrides={"device_guard_period_s": 0.2})
+
+
+def test_guard_pass_reads_the_kernel_off_the_loop_and_skips_cgroups_changed_meanwhile(
+        tmp_path):
+    """The periodic device guard fingerprints in a worker thread (worker/reconciler.py
+    guard_pass). A cgroup whose expected state gpumounter itself changed while the thread ran
+    (an attach or detach on that container) is not judged on the stale reading; a cgroup
+    changed by someone else is kicked."""
+    import threading
+    from types import SimpleNamespace
+
+    from gpumounter_amd.worker.reconciler import Reconciler
+
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    os.makedirs(a)
+    os.makedirs(b)
+    state = {a: "A1", b: "B1"}
+    loop_thread = threading.get_ident()
+    threads = set()
+
+    def fingerprint(d):
+        threads.add(threading.get_ident())
+        return state[d]
+
+    entries = [SimpleNamespace(rules=["x"], cgdir=d, namespace="ns", pod=d[-1])
+               for d in sorted(state)]
+    hm = SimpleNamespace(journal=SimpleNamespace(entries=lambda: entries), expected={},
+                         backend=SimpleNamespace(fingerprint=fingerprint))
+    rec = Reconciler.__new__(Reconciler)
+    kicked = []
+    rec.svc, rec.guard_repairs, rec._stopping = SimpleNamespace(hm=hm), 0, False
+    rec._kick = kicked.append
+
+    async def main():
+        assert await rec.guard_pass() == []          # first sight: baselines
+        assert hm.expected == {a: "A1", b: "B1"}
+        state[a] = "A2"                              # changed behind gpumounter's back
+        state[b] = "B2"                              # ... and changed by gpumounter, which
+        real = rec._fingerprints
+
+        def racing(fp, dirs):
+            out = real(fp, dirs)
+            hm.expected[b] = "B2"                    # records its own state meanwhile
+            return out
+        rec._fingerprints = racing
+        got = await rec.guard_pass()
+        assert got == [("ns", "a")]
+        assert kicked == [("guard", "ns", "a")]
+    asyncio.run(main())
+    assert threads and loop_thread not in threads
