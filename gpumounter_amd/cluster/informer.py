@@ -22,6 +22,10 @@ DELETED_KEEP = 65536
 
 
 class PodInformer:
+    # a re-read after a relist (``_resolve``) gives up after this long; below the worker's
+    # SETTLE_WAIT_S, so a stalled GET delays pod views by at most this, never fails them
+    RESOLVE_TIMEOUT_S = 1.5
+
     def __init__(self, kube: KubeClient, namespace: Optional[str] = None, label_selector: str = "",
                  field_selector: str = "", resync_s: float = 300.0) -> None:
         self.kube = kube
@@ -308,7 +312,11 @@ class PodInformer:
         for _ in range(tries):
             epoch, writes = self.epoch, self._writes.get(key, 0)
             try:
-                obj = await self._fetch(key)
+                # bounded well below the kube client's 30 s: while any re-read is out the view
+                # is not ``settled``, and every pod view on the node waits for that (worker
+                # service pod_state, up to its SETTLE_WAIT_S). One slow GET must not hold up
+                # the node's attaches and detaches for half a minute
+                obj = await asyncio.wait_for(self._fetch(key), self.RESOLVE_TIMEOUT_S)
             except Exception:  # noqa: BLE001 - the watch still converges; this only shortens it
                 return
             if epoch != self.epoch or writes != self._writes.get(key, 0):

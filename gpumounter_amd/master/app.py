@@ -384,16 +384,15 @@ class Master:
         return _text(text, status)
 
     def _stale(self, cached: str, pod: dict) -> bool:
-        """The worker found no such pod although the lookup did: worth one fresh try if the
-        answer came from the 30 s cache, or from the index that has since seen the pod
-        recreated (another UID). A pod deleted meanwhile is reported as the worker saw it."""
+        """The worker found no such pod although the lookup did: worth one fresh try (a GET)
+        if the answer came from the 30 s cache or from the index, whose watch may not have
+        delivered the deletion or the re-creation yet. The GET then answers as the reference
+        does on every request (main.go:52): 404 for a pod that is gone. Only this failure path
+        pays for the GET."""
         if cached == "ttl":
             self._pod_nodes.pop((podu.ns_of(pod), podu.name_of(pod)), None)
             return True
-        if cached == "index":
-            cur = self.pods.get(podu.ns_of(pod), podu.name_of(pod))
-            return cur is not None and podu.uid_of(cur) != podu.uid_of(pod)
-        return False
+        return cached == "index"
 
     async def _locate(self, ns: str, name: str, fresh: bool = False):
         """Pod → node → worker target. Returns (pod, target, error, cached) where error is a

@@ -36,6 +36,15 @@ _log = log.get("master.authz")
 RESOURCE_SUB = "gpumount"
 
 
+def _drop(task: Optional[asyncio.Future]) -> None:
+    """Abandon a speculative review: cancel it, and retrieve its outcome once it is done (a SAR
+    that already failed would otherwise log "Task exception was never retrieved")."""
+    if task is None:
+        return
+    task.cancel()
+    task.add_done_callback(lambda f: f.cancelled() or f.exception())
+
+
 @dataclass
 class Decision:
     allowed: bool
@@ -91,20 +100,17 @@ class Authorizer:
         try:
             user = await self._authenticate(token, key)
         except Exception as e:  # noqa: BLE001
-            if spec is not None:
-                spec.cancel()
+            _drop(spec)
             _log.error("TokenReview failed: %s", e)
             return Decision(False, 503, "authentication unavailable")
         if user is None:
-            if spec is not None:
-                spec.cancel()
+            _drop(spec)
             return Decision(False, 401, "Unauthorized: token not accepted")
         try:
             if spec is not None and self._same(user, guess):
                 ok = await spec
             else:
-                if spec is not None:
-                    spec.cancel()
+                _drop(spec)
                 ok = await self._authorize(user, verb, namespace, resource, name)
         except Exception as e:  # noqa: BLE001
             _log.error("SubjectAccessReview failed: %s", e)

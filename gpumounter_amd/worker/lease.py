@@ -142,8 +142,20 @@ class LeaseKeeper:
             self._errors[(ns, name)] = n + 1
             delay = self.ERROR_RETRY_S[n] if n < len(self.ERROR_RETRY_S) else \
                 self.svc.cfg.lease_retry_s
-            _log.error("lease expiry of %s/%s failed (attempt %d, retry in %g s): %s",
-                       ns, name, n + 1, delay, e)
+            fast = len(self.ERROR_RETRY_S)
+            _log.log(40 if n <= fast else 30,
+                     "lease expiry of %s/%s failed (attempt %d, retry in %g s): %s",
+                     ns, name, n + 1, delay, e)
+            if n == fast:
+                # the quick retries did not get through: tell the Pod's owner once, then keep
+                # trying at the slow period (the ledger is re-read every time)
+                pod = self.svc.node_pods.get(ns, name) if hasattr(self.svc, "node_pods") \
+                    else None
+                if pod is not None:
+                    self.svc.notify.event(
+                        pod, "GPULeaseExpired",
+                        f"lease over, but the GPUs could not be detached: {e}; retrying "
+                        f"every {self.svc.cfg.lease_retry_s:g} s", warning=True)
             if not self._stopped:
                 old = self._retry_timers.pop((ns, name), None)
                 if old is not None:

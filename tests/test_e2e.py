@@ -516,14 +516,10 @@ def test_master_pod_cache_revalidates_recreated_and_deleted_pods(index):
         lc.tenant("p", node="node-1")
         code, b = await lc.add("default", "p", 1)
         assert code == 200 and lc.cluster.placeholders()[-1]["spec"]["nodeName"] == "node-1"
-        # pod deleted → reference semantics: 404 from the master (once its pod index has seen
-        # the deletion; a request racing the watch gets the worker's 400 PodNotFound, as a
-        # reference request racing the deletion after its GET does)
+        # pod deleted → reference semantics: 404 from the master, also for a request that
+        # still finds the pod in the index (the watch has not delivered the deletion): the
+        # worker's PodNotFound sends the master to a GET, which answers 404
         lc.cluster.delete("default", "p", grace=0)
-        for _ in range(100):
-            if lc.master.pods is None or lc.master.pods.get("default", "p") is None:
-                break
-            await asyncio.sleep(0.01)
         code, text = await lc.add("default", "p", 1, accept_json=False)
         assert (code, text) == (404, "No pod: p in namespace: default\n")
     run(body, n_nodes=2, master_overrides={"master_pod_index": index})

@@ -466,3 +466,36 @@ def test_a_worker_killed_between_booking_and_mount_leaves_no_unleased_placeholde
             time.sleep(0.1)
         assert not left, "the lease never ended the attach"
         assert pc.audit("default", "t") == []
+
+
+def test_an_expiry_that_keeps_failing_tells_the_pod():
+    """a RemoveGPU refusal that does not go away (here GPUNotFound on every try)
+    was retried every lease_retry_s with only ERROR logs; after the quick retries the Pod now
+    gets a GPULeaseExpired warning Event naming the failure (once), and retries continue."""
+    from gpumounter_amd.api import gpu_mount as api
+
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        svc.lease.ERROR_RETRY_S = (0.05, 0.05, 0.05)
+        calls = []
+
+        async def refuse(req):
+            calls.append(req)
+            return api.RemoveGPUResponse(remove_gpu_result=api.REMOVE_GPU_NOT_FOUND)
+        code, b = await lease_add(lc, "default", "t", 1, 0.1)
+        assert code == 200, b
+        real = svc.remove_gpu
+        svc.remove_gpu = refuse
+
+        async def warned():
+            return any(e["reason"] == "GPULeaseExpired" and e["type"] == "Warning" and
+                       "could not be detached" in e["message"]
+                       for e in lc.cluster.events_for("default", "t"))
+        assert await until(warned, timeout=5.0), lc.cluster.events_for("default", "t")
+        assert len(calls) >= 4
+        n = sum(1 for e in lc.cluster.events_for("default", "t")
+                if "could not be detached" in e["message"])
+        assert n == 1
+        svc.remove_gpu = real
+    run(body, worker_overrides={"lease_retry_s": 0.2})

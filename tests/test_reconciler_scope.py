@@ -282,3 +282,39 @@ def test_guard_pass_reads_the_kernel_off_the_loop_and_skips_cgroups_changed_mean
         assert kicked == [("guard", "ns", "a")]
     asyncio.run(main())
     assert threads and loop_thread not in threads
+
+
+def test_a_stalled_reread_after_a_relist_does_not_stall_the_node():
+    """after a relist the placeholder view is not ``settled`` until the
+    re-read GETs of our overtaken writes answer, and every pod view on the node waits for it.
+    A GET that hangs (the kube client's total timeout is 30 s) must not turn every attach on
+    the node into "ledger unavailable": the re-read gives up after RESOLVE_TIMEOUT_S."""
+    import time as _time
+
+    from gpumounter_amd.fakes.harness import LocalCluster
+
+    async def main():
+        async with LocalCluster() as lc:
+            lc.tenant("a")
+            lc.tenant("b")
+            svc = lc.nodes["node-0"].worker.service
+            inf = svc.ph.informer
+            code, b = await lc.add("default", "a", 1)
+            assert code == 200
+            key = next(iter(inf.cache))
+            real_get = inf._get
+
+            async def stalled(ns, name):
+                await asyncio.sleep(60)
+                return await real_get(ns, name)
+            inf._get = stalled
+            inf._resolve_soon(key)          # what a relist does for an overtaken write
+            assert not inf.settled
+            t0 = _time.monotonic()
+            code, got = await lc.add("default", "b", 1)
+            took = _time.monotonic() - t0
+            assert code == 200, got
+            assert took < inf.RESOLVE_TIMEOUT_S + 1.0, took
+            assert inf.settled
+            inf._get = real_get
+    asyncio.run(main())
