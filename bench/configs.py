@@ -416,6 +416,16 @@ def chaos(args) -> dict:
                 return t, -1
 
         holders = {}    # tenant → {uuid: placeholder holding it} as of the last ledger()
+        lease_now = {}  # tenant → {uuid: lease_expires on the ledger} as of the last ledger()
+
+        def still_leased(t, u) -> bool:
+            """The ledger still shows GPU ``u`` under the lease the client recorded (not a
+            later, unleased claim of the same warm-pool placeholder whose answer was lost)."""
+            exp = lease_now.get(t, {}).get(u)
+            if not exp:
+                return False
+            at = time.monotonic() + (exp - time.time())
+            return leases[t][u][0] - 1.0 <= at <= leases[t][u][1] + 1.0
 
         ledger_err = {}     # tenant → (code, answer, seconds) of its last failed ledger read
 
@@ -430,6 +440,7 @@ def chaos(args) -> dict:
                 return None
             hm = [x for x in g.get("gpus", []) if x.get("source") == "hot-mount"]
             holders[t] = {x["uuid"]: x.get("pod_name") for x in hm}
+            lease_now[t] = {x["uuid"]: x.get("lease_expires") for x in hm}
             return sorted(x["uuid"] for x in hm)
 
         why = [""]
@@ -545,8 +556,12 @@ def chaos(args) -> dict:
                     # expires around now may be either (it is settled at the next check)
                     overdue = [u for u, (_, hi, _) in leases[t].items()
                                if now - hi > args.lease_slack]
+                    # after a lost answer (not certain) the tenant may have re-attached the GPU
+                    # under the same placeholder without a lease: only the ledger's own lease
+                    # annotation tells (the client resyncs from the ledger further down)
                     late = sorted(u for u in overdue if u in hot and
-                                  holders.get(t, {}).get(u) == leases[t][u][2])
+                                  holders.get(t, {}).get(u) == leases[t][u][2] and
+                                  (certain[t] or still_leased(t, u)))
                     if late:
                         problems.append(f"round {rnd_i} {t}: leases expired more than "
                                         f"{args.lease_slack} s ago still attached: {late}; "
