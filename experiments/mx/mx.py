@@ -1,9 +1,10 @@
-"""Block-scaled (MX) matrix-core checks: gfx950's ``v_mfma_scale_f32_16x16x128_f8f6f4``.
+"""Block-scaled (MX) matrix-core probes: gfx950's ``v_mfma_scale_f32_16x16x128_f8f6f4``.
 
-MI355X runs fp8 at twice and fp4 at four times the bf16 MFMA rate (MI355X_MICROARCH.md), and
-inference kernels live on that pipe, so a GPU handed to an inference Pod should be checked
-there too; the bf16 probe never touches it. Nothing in the reference validates a mounted GPU
-(reference: pkg/util/util.go:64-70 treats "mknod returned 0" as success).
+An experiment kept next to gpumounter-amd, not part of it (moved out of ``gpumounter_amd/ops``
+in round 5: the attach path validates a GPU with the wave64 liveness kernel only, and the
+round-3 review ruled the fp8/fp4 pipes out of the product's scope). MI355X runs fp8 at twice
+and fp4 at four times the bf16 MFMA rate. Library: ``libgm_mx.so`` next to this file
+(``make -C native mx``).
 
 * :func:`peak` — register-resident MX-MFMA throughput (fp8 or fp4) plus one sum per wave; the
   kernel is deterministic, so two runs (or two GPUs) must agree bit for bit;
@@ -18,12 +19,14 @@ infinities, 0x7F/0xFF NaN; e2m1 = 1 sign, 2 exponent (bias 1), 1 mantissa bit; E
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, Optional, Tuple
 
 import numpy as np
 
 from gpumounter_amd import _native
 
+HERE = os.path.dirname(os.path.abspath(__file__))
 FMT = {"fp8": 0, "fp4": 4}
 
 
@@ -31,9 +34,31 @@ class MxError(RuntimeError):
     pass
 
 
+_lib = []
+
+
+def lib() -> C.CDLL:
+    """``libgm_mx.so`` (``make -C native mx``), typed."""
+    if not _lib:
+        path = os.path.join(HERE, "libgm_mx.so")
+        if not os.path.exists(path):
+            raise MxError(f"{path} missing: make -C native mx")
+        L = C.CDLL(path)
+        L.gm_mx_peak.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                 C.POINTER(C.c_double)]
+        L.gm_mx_peak_variant.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_void_p, C.c_int, C.POINTER(C.c_double)]
+        L.gm_mx_tile.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.c_void_p]
+        L.gm_mx_strerror.argtypes = [C.c_int]
+        L.gm_mx_strerror.restype = C.c_char_p
+        _lib.append(L)
+    return _lib[0]
+
+
 def _check(rc: int, what: str) -> None:
     if rc != 0:
-        msg = _native.probe().gm_probe_strerror(rc).decode(errors="replace")
+        msg = lib().gm_mx_strerror(rc).decode(errors="replace")
         raise MxError(f"{what}: {msg} ({rc})")
 
 
@@ -115,7 +140,7 @@ def tile(dev: int, afrag: np.ndarray, bfrag: np.ndarray, sa: np.ndarray, sb: np.
     if a.shape != (64, 32) or b.shape != (64, 32) or sa.shape != (64,) or sb.shape != (64,):
         raise ValueError("afrag/bfrag must be 64×32 bytes, sa/sb 64 bytes")
     c = np.zeros((64, 4), np.float32)
-    _check(_native.probe().gm_probe_mx_tile(dev, FMT[fmt], a.ctypes.data, b.ctypes.data,
+    _check(lib().gm_mx_tile(dev, FMT[fmt], a.ctypes.data, b.ctypes.data,
                                             sa.ctypes.data, sb.ctypes.data, c.ctypes.data),
            "mx tile")
     return c
@@ -129,13 +154,12 @@ def peak(dev: int, fmt: str = "fp8", iters: int = 10000, blocks_per_cu: int = 8,
     """(dense TF/s, per-wave sums) of the register-resident MX-MFMA loop. variant 0: 16x16x128
     × 8 chains; 1: 32x32x64 × 4; 2: 32x32x64 × 8; None: the measured best for ``fmt``."""
     variant = BEST_VARIANT[fmt] if variant is None else variant
-    lib = _native.probe()
     p = _native.ProbeProps()
-    _check(lib.gm_probe_props(dev, C.byref(p)), "props")
+    _check(_native.probe().gm_probe_props(dev, C.byref(p)), "props")
     n = p.cu_count * blocks_per_cu * 4
     sums = np.zeros(n, np.float32)
     t = C.c_double(0)
-    _check(lib.gm_probe_mx_peak_variant(dev, FMT[fmt], variant, iters, blocks_per_cu,
+    _check(lib().gm_mx_peak_variant(dev, FMT[fmt], variant, iters, blocks_per_cu,
                                         sums.ctypes.data, n, C.byref(t)), "mx peak")
     return t.value, sums
 

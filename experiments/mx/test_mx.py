@@ -1,11 +1,16 @@
-"""Host side of the block-scaled (MX) MFMA check (gpumounter_amd/ops/mx.py): the OCP e4m3
+"""Host side of the block-scaled (MX) MFMA check (experiments/mx/mx.py): the OCP e4m3
 decoder, the measured lane map and the reference. The tile runs here on a CPU emulation of the
 map measured on MI355X (round-3 probe scripts, removed; results in profiles/r3_mx/); tests/test_gpu.py runs it on
 the matrix core."""
 import numpy as np
 import pytest
 
-from gpumounter_amd.ops import mx
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import mx  # noqa: E402
 
 
 def emulate(af, bf, sa, sb, k_of=mx.k_index):

@@ -258,12 +258,6 @@ def probe() -> C.CDLL:
                                             C.POINTER(C.c_double), C.POINTER(C.c_double)]
         lib.gm_probe_p2p.argtypes = [C.c_int, C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_int),
                                      C.POINTER(C.c_double)]
-        lib.gm_probe_mx_peak.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
-                                         C.POINTER(C.c_double)]
-        lib.gm_probe_mx_peak_variant.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                                 C.c_void_p, C.c_int, C.POINTER(C.c_double)]
-        lib.gm_probe_mx_tile.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                                         C.c_void_p, C.c_void_p]
         lib.gm_probe_strerror.argtypes = [C.c_int]
         lib.gm_probe_strerror.restype = C.c_char_p
         lib._gm_typed = True

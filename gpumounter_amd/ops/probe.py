@@ -179,9 +179,6 @@ class VerifyResult:
     mfma_tflops: Optional[float] = None
     gemm_max_abs_err: Optional[float] = None
     gemm_tflops: Optional[float] = None
-    mx_fp8_tile_ok: Optional[bool] = None
-    mx_fp8_tflops: Optional[float] = None
-    mx_fp4_tflops: Optional[float] = None
 
     def to_dict(self) -> Dict:
         return asdict(self)
@@ -202,9 +199,5 @@ def verify(bdfs: List[str], full: bool = False) -> List[VerifyResult]:
             r.mfma_tflops = mfma_tflops(dev)
             r.gemm_max_abs_err = gemm_check(dev)["max_abs_err"]
             r.gemm_tflops = gemm_tflops(dev, 4096, 4096, 4096, 10)
-            from gpumounter_amd.ops import mx
-            r.mx_fp8_tile_ok = mx.check_fp8(dev)["ok"]
-            r.mx_fp8_tflops = mx.peak(dev, "fp8")[0]
-            r.mx_fp4_tflops = mx.peak(dev, "fp4")[0]
         out.append(r)
     return out

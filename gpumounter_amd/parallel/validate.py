@@ -3,16 +3,14 @@
 Run inside the pod once GPUs were hot-mounted. It answers the questions a tenant has before
 starting a job on them — the reference offers nothing here:
 
-1. every visible GPU runs a gfx950 kernel (wave64 liveness probe, :mod:`gpumounter_amd.ops.probe`)
-   and computes one block-scaled fp8 MFMA tile right (:func:`gpumounter_amd.ops.mx.check_fp8`);
+1. every visible GPU runs a gfx950 kernel (wave64 liveness probe, :mod:`gpumounter_amd.ops.probe`);
 2. every pair has peer access and xGMI-class copy bandwidth (:func:`collectives.xgmi_matrix`);
 3. RCCL works across all of them: one process per GPU, ``torch.distributed`` with backend
    ``nccl`` (RCCL on ROCm), a checked bf16 all-reduce with ring bus bandwidth
    (:func:`collectives.allreduce_check`);
 4. optionally (``--burn-in SECONDS``) all GPUs under sustained MFMA load at once, each
-   result bit-compared with the first: bf16 GEMMs for SECONDS (:func:`probe.burn_in`), then the
-   fp8 and fp4 MX pipes for SECONDS/2 each (:func:`mx.burn_in`). Catches silent data corruption
-   and throttling that a short probe misses.
+   result bit-compared with the first: bf16 GEMMs for SECONDS (:func:`probe.burn_in`). Catches
+   silent data corruption and throttling that a short probe misses.
 
 Prints one JSON document; exit code 0 only if every check passed. ``--cpu-ranks N`` runs step 3
 with N gloo ranks on the CPU (hermetic tests).
@@ -86,13 +84,9 @@ def main(argv=None) -> int:
             print(json.dumps({"ok": False, "error": "no GPU visible (nothing attached?)"}))
             return 1
         devs = list(range(n))
-        from gpumounter_amd.ops import mx
-
         report["gpus"] = [{"device": d, "bdf": probe.props(d)["pci_bus_id"],
-                           "arch": probe.props(d)["gcn_arch"], "quick_us": probe.quick(d),
-                           "mx_fp8_tile_ok": mx.check_fp8(d)["ok"]}
+                           "arch": probe.props(d)["gcn_arch"], "quick_us": probe.quick(d)}
                           for d in devs]
-        report["ok"] &= all(g["mx_fp8_tile_ok"] for g in report["gpus"])
         if n > 1 and not args.no_p2p:
             m = xgmi_matrix(devs)
             report["p2p"] = m
@@ -110,12 +104,8 @@ def main(argv=None) -> int:
         from gpumounter_amd.ops import probe
 
         # all GPUs at once (shared power/thermal envelope); ctypes drops the GIL in the call
-        from gpumounter_amd.ops import mx
-
         with ThreadPoolExecutor(max_workers=world) as ex:
             burn = list(ex.map(lambda d: probe.burn_in(d, args.burn_in), range(world)))
-            for fmt in ("fp8", "fp4"):
-                burn += list(ex.map(lambda d: mx.burn_in(d, args.burn_in / 2, fmt), range(world)))
         report["burn_in"] = burn
         report["ok"] &= all(b["ok"] for b in burn)
     print(json.dumps(report))
