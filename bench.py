@@ -42,6 +42,20 @@ def pct(xs, q):
     return xs[lo] + (xs[hi] - xs[lo]) * (k - lo)
 
 
+def calls_summary(runs) -> dict:
+    """Per process: calls by kind and serial round trips, from the cycle with the median
+    number of serial round trips (all cycles' round trips listed too)."""
+    from gpumounter_amd.utils import calls
+    # Events are queued and sent once no operation is in flight (worker/notify.py): they can
+    # land in the window but are never waited for
+    per = [{who: calls.summary([c for c in cs if c[2] != "apiserver POST events"])
+            for who, cs in run.items()} for run in runs]
+    depth = [sum(p["serial_round_trips"] for p in r.values()) for r in per]
+    mid = sorted(range(len(per)), key=lambda i: depth[i])[len(per) // 2]
+    return {"by_process": per[mid], "serial_round_trips": depth[mid],
+            "serial_round_trips_all_cycles": depth}
+
+
 class _LocalCP:
     """Control-plane adapter: everything on one event loop thread (LocalCluster)."""
 
@@ -70,6 +84,10 @@ class _LocalCP:
         node = self.lc.nodes["node-0"].node
         (c,) = [c for c in node.containers.values() if c.pod_name == "tenant"]
         return c.root_dir, c.cgroup_dir
+
+    def calls(self, t0: float, t1: float) -> dict:
+        from gpumounter_amd.utils import calls   # one process: master and worker share the log
+        return {"master+worker": calls.since(t0, t1)}
 
     def wait_pool(self, want: int) -> None:
         pool = self.lc.nodes["node-0"].worker.pool
@@ -116,6 +134,9 @@ class _ProcCP:
         cid = cs[0]["containerID"].split("://", 1)[1]
         n = self.pc.info["nodes"]["node-0"]
         return tenant.locate(n["rootfs_root"], n["cgroup_root"], cid)
+
+    def calls(self, t0: float, t1: float) -> dict:
+        return self.pc.calls(t0, t1)
 
     def wait_pool(self, want: int) -> None:
         from gpumounter_amd.models.types import ANN_MOUNT_MODE, MODE_STANDBY
@@ -195,6 +216,10 @@ def main() -> int:
     ap.add_argument("--no-calib", action="store_true",
                     help="skip the box calibration (CPU loop, process pingpong, gRPC floor) "
                          "recorded as \"box\" in the JSON")
+    ap.add_argument("--call-cycles", type=int, default=5,
+                    help="after the timed loop: this many attach/detach cycles whose outbound "
+                         "apiserver/kubelet calls are read from the daemons' call logs "
+                         "(serial_calls_per_attach / _detach); 0 = skip")
     ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
                     help="dra: the node's GPUs come from a DRA driver; placeholders hold "
                          "ResourceClaims (gpu_allocation=dra)")
@@ -520,6 +545,40 @@ def main() -> int:
                 if not tenant_view_pt["ok"]:
                     print(f"bench: tenant-side PyTorch check failed: {tenant_view_pt}",
                           file=sys.stderr)
+            # the control-plane calls one attach and one detach wait for, counted on the fake:
+            # by kind, and how many of them are serial (a real cluster charges each serial round
+            # trip a millisecond or more; gpumounter_amd/utils/calls.py)
+            accounting = None
+            if args.protocol == "gpumounter" and args.call_cycles > 0:
+                acc = {"attach": [], "detach": []}
+                waits = []
+                for i in range(args.call_cycles):
+                    time.sleep(0.02)               # quiet: nothing else in the window
+                    ta = time.monotonic()
+                    code, body = cp.add(n, args.mode == "entire")
+                    tb = time.monotonic()
+                    if code != 200:
+                        raise RuntimeError(f"attach failed: {code} {body}")
+                    code, body2 = cp.remove([d["uuid"] for d in body["devices"]])
+                    tc = time.monotonic()
+                    if code != 200:
+                        raise RuntimeError(f"detach failed: {code} {body2}")
+                    if args.warm_pool:
+                        cp.wait_pool(min(args.warm_pool, pool_cap))
+                    logs = cp.calls(ta, tc)
+                    for op, (lo, hi) in (("attach", (ta, tb)), ("detach", (tb, tc))):
+                        acc[op].append({who: [c for c in cs if lo <= c[0] <= hi]
+                                        for who, cs in logs.items()})
+                    # besides calls, an attach that creates placeholders waits for the scheduler
+                    # to bind them and the kubelet to admit them (no call of ours: a watch / the
+                    # checkpoint tells); a warm-pool claim does not
+                    st = {t["name"]: t["ms"] for t in body.get("timings", [])}
+                    waits.append(st.get("placeholder_wait"))
+                accounting = {op: calls_summary(runs) for op, runs in acc.items()}
+                w = [x for x in waits if x is not None]
+                accounting["attach"]["admission_waits"] = 1 if len(w) * 2 > len(waits) else 0
+                accounting["attach"]["admission_wait_p50_ms"] = round(pct(w, 0.5), 4) \
+                    if w else None
             cold = None
             if args.cold_steps > 0 and args.deploy == "processes" and \
                     args.protocol == "gpumounter":
@@ -673,6 +732,10 @@ def main() -> int:
                 "cold_attach_p50_ms": cold["attach_p50_ms"] if cold else None,
                 "cold_attach": cold,
                 "first_attach_ms": round(first_attach[0], 4) if first_attach else None,
+                # control-plane calls per operation on the critical path, by process and kind,
+                # with the serial round trips (the median cycle of --call-cycles)
+                "serial_calls_per_attach": accounting["attach"] if accounting else None,
+                "serial_calls_per_detach": accounting["detach"] if accounting else None,
                 "detach_p50_ms": round(pct(detach_ms, 0.5), 4),
                 "detach_p99_ms": round(pct(detach_ms, 0.99), 4),
                 "stage_p50_ms": {k: round(statistics.median(v), 4) for k, v in sorted(stage.items())},

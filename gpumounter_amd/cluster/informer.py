@@ -13,7 +13,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.models.pod import jcopy
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import calls, log
 
 _log = log.get("cluster.informer")
 
@@ -175,6 +175,7 @@ class PodInformer:
         the BOOKMARKs the server sends while idle, keep it current — so there is no relist per
         resync period. Only an error relists: 410 Gone (the version left the server's history)
         at once, anything else after a backoff."""
+        calls.mark_background()
         backoff = 0.05
         need_list = initial_list
         while True:
@@ -294,6 +295,7 @@ class PodInformer:
         return not self._resolving
 
     async def _resolve(self, key: Key, tries: int = 3) -> None:
+        calls.mark_background()
         try:
             await self._resolve_once(key, tries)
         finally:

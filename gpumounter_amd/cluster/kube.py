@@ -20,9 +20,19 @@ from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
 import aiohttp
 import yaml
 
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import calls, log
 
 _log = log.get("kube")
+_RESOURCES = {"pods", "events", "resourceclaims", "resourceslices", "resourcequotas",
+              "tokenreviews", "subjectaccessreviews", "nodes"}
+
+
+def _kind(method: str, path: str) -> str:
+    """``apiserver POST pods`` for the call log (utils/calls.py)."""
+    for seg in reversed(path.split("/")):
+        if seg in _RESOURCES:
+            return f"apiserver {method} {seg}"
+    return f"apiserver {method}"
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
@@ -168,6 +178,10 @@ class KubeClient:
         if body is not None:
             data = json.dumps(body)
             headers["Content-Type"] = content_type
+        with calls.span(_kind(method, path)):
+            return await self._send(sess, method, path, params, data, headers)
+
+    async def _send(self, sess, method: str, path: str, params, data, headers) -> Any:
         async with sess.request(method, self.base + path, params=params, data=data,
                                 headers=headers) as resp:
             text = await resp.text()

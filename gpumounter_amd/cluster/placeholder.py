@@ -47,7 +47,7 @@ from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTA
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          SLAVE_SUFFIX)
 from gpumounter_amd.node.ledger import LedgerClient
-from gpumounter_amd.utils import log, trace
+from gpumounter_amd.utils import calls, log, trace
 
 _log = log.get("cluster.placeholder")
 LABEL_NODE = "gpumounter.amd.com/node"
@@ -464,7 +464,10 @@ class PlaceholderManager:
                 raise QuotaExceeded(_message(quota[0]))
             raise ReserveError(f"resourceclaim create failed: {errors[0]}")
 
-    async def _delete_claims(self, keys: Sequence[Tuple[str, str]]) -> None:
+    async def _delete_claims(self, keys: Sequence[Tuple[str, str]],
+                             background: bool = False) -> None:
+        if background:
+            calls.mark_background()
         res = await asyncio.gather(*[self.kube.delete_claim(ns, n) for ns, n in keys],
                                    return_exceptions=True)
         for (ns, n), r in zip(keys, res):
@@ -774,7 +777,8 @@ class PlaceholderManager:
                 gone = [(p.namespace, p.name) for p in phs
                         if p not in failed and p not in reowned]
                 if gone:
-                    t = asyncio.get_running_loop().create_task(self._delete_claims(gone))
+                    t = asyncio.get_running_loop().create_task(
+                        self._delete_claims(gone, background=True))
                     self._bg.add(t)
                     t.add_done_callback(self._bg.discard)
             if failed:

@@ -21,7 +21,7 @@ from __future__ import annotations
 import asyncio
 import secrets
 import time
-from typing import Callable, Dict, List, Optional, Sequence, Tuple
+from typing import Awaitable, Callable, Dict, List, Optional, Sequence, Tuple
 
 from gpumounter_amd.cluster.kube import Conflict, NotFound
 from gpumounter_amd.cluster.placeholder import (ANN_GPUS, STANDBY_PREFIX, InsufficientGPU,
@@ -36,7 +36,7 @@ from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTA
                                          ANN_OWNER_NAME, ANN_OWNER_UID, LABEL_APP,
                                          LABEL_APP_VALUE, LABEL_OWNER, LABEL_OWNER_NS,
                                          MODE_STANDBY)
-from gpumounter_amd.utils import log, trace
+from gpumounter_amd.utils import calls, log, trace
 
 _log = log.get("cluster.pool")
 
@@ -65,6 +65,10 @@ class WarmPool:
         self.exhausted = False               # last refill hit InsufficientGPU
         self._alloc_cache: Optional[tuple] = None   # (monotonic time, allocatable IDs)
         self._creating = 0        # standby placeholders a refill is about to create
+        # awaited before each refill (the worker sets Notifier.quiet): the POST and the
+        # admission of a new standby wait until no attach/detach is in flight, instead of
+        # sharing the worker's loop with the attach that emptied the pool
+        self.quiet: Optional[Callable[[], Awaitable[None]]] = None
 
     @property
     def enabled(self) -> bool:
@@ -129,10 +133,13 @@ class WarmPool:
             self._wake.set()
 
     async def _refill_loop(self) -> None:
+        calls.mark_background()
         while True:
             await self._wake.wait()
             self._wake.clear()
             try:
+                if self.quiet is not None:
+                    await self.quiet()
                 await self.refill()
             except asyncio.CancelledError:
                 raise

@@ -201,6 +201,7 @@ class ProcessCluster:
         for node in self._worker_env:
             self._await_worker(node)
         self._master_env = {"GM_KUBE_API": api, "GM_MASTER_HOST": "127.0.0.1", **tls_m,
+                            "GM_DEBUG_ENDPOINTS": "1",     # /debug/calls (bench accounting)
                             "GM_MASTER_PORT": "0", "GM_READY_FILE": self._ready_path("master"),
                             "GM_LOG_LEVEL": "WARNING", "GM_LOG_JSON": "false",
                             **self.master_env}
@@ -385,6 +386,20 @@ class ProcessCluster:
         if code != 200:
             raise RuntimeError(f"audit {ns}/{pod}: {code} {body[:300]!r}")
         return json.loads(body)["issues"]
+
+    def calls(self, since: float, until: float, node: str = "node-0") -> dict:
+        """Outbound control-plane calls of the master and the node's worker that started in
+        [since, until] (CLOCK_MONOTONIC, shared by the host's processes)."""
+        q = f"?since={since!r}&until={until!r}"
+        out = {}
+        for who, url in (("master", f"{self.master_url}/debug/calls{q}"),
+                         ("worker", f"http://127.0.0.1:{self.worker_ports[node][1]}"
+                                    f"/debug/calls{q}")):
+            code, body = _http("GET", url, headers=self._auth)
+            if code != 200:
+                raise RuntimeError(f"{who} /debug/calls: {code} {body[:200]!r}")
+            out[who] = [tuple(c) for c in json.loads(body)]
+        return out
 
     def worker_tasks(self, node: str = "node-0") -> str:
         """The worker's asyncio tasks and their stacks (``/debug/tasks``)."""

@@ -31,7 +31,7 @@ from gpumounter_amd.models import pod as podu
 from gpumounter_amd.master import httpd
 from gpumounter_amd.master.authz import Authorizer
 from gpumounter_amd.master.httpd import Request, Response
-from gpumounter_amd.utils import log, runtime, trace
+from gpumounter_amd.utils import calls, log, runtime, trace
 from gpumounter_amd.utils.metrics import Metrics
 
 _log = log.get("master")
@@ -301,7 +301,15 @@ class Master:
         r.add_get("/api/v1/nodes/{node}/gpus", self.node_gpus)
         r.add_get("/healthz", self.healthz)
         r.add_get("/metrics", self.metrics_handler)
+        if getattr(self.cfg, "debug_endpoints", False):
+            r.add_get("/debug/calls", self.debug_calls)
         return r
+
+    async def debug_calls(self, request: Request) -> Response:
+        """Outbound control-plane calls (utils/calls.py) that started in [since, until]."""
+        q = request.query
+        return httpd.json_response(calls.since(float(q.get("since", "0")),
+                                               float(q.get("until", "inf"))))
 
     async def start(self, port: Optional[int] = None) -> None:
         await self.workers.start()

@@ -39,9 +39,10 @@ import ctypes.util
 import json
 import os
 import struct
+import time
 from typing import Callable, Dict, List, Optional, Tuple
 
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import calls, log
 
 _log = log.get("node.checkpoint")
 
@@ -138,6 +139,8 @@ class DeviceCheckpoint:
         metadata cannot stand in for the content: the kubelet's tmp-and-rename reuses the inode
         number just freed, two rewrites within one timestamp tick share an mtime, and a rewrite
         that swaps one UID for another keeps the size."""
+        t = time.monotonic()
+        calls.record("checkpoint read", t, t)
         try:
             with open(self.path, "rb") as fh:
                 blob = fh.read()

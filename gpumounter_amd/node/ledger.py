@@ -17,7 +17,7 @@ from typing import Dict, List, Optional, Tuple
 import grpc
 
 from gpumounter_amd.api.podresources import V1, V1ALPHA1
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import calls, log
 from gpumounter_amd.utils.ratelimit import TokenBucket
 
 _log = log.get("node.ledger")
@@ -91,6 +91,10 @@ class LedgerClient:
         rate limiter) is retried with jittered backoff (10 ms doubling to 200 ms) until the call's
         deadline; on UNAVAILABLE (kubelet restarting: socket gone or recreated) the channel is
         rebuilt and the call retried once, waiting up to 2 s for the new socket."""
+        with calls.span("kubelet " + path.rsplit("/", 1)[-1]):
+            return await self._call_paced(path, req_cls, resp_cls, req)
+
+    async def _call_paced(self, path: str, req_cls, resp_cls, req):
         loop = asyncio.get_running_loop()
         deadline = loop.time() + self.timeout_s
         backoff = 0.010

@@ -21,7 +21,7 @@ from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_GROUP, ANN_LEASE,
                                          ANN_OWNER_UID, LABEL_OWNER_NS, MountType)
 from gpumounter_amd.node.ledger import LedgerError
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import calls, log
 
 _log = log.get("worker.lease")
 __all__ = ["ANN_LEASE", "LeaseKeeper", "expires_of"]
@@ -128,6 +128,7 @@ class LeaseKeeper:
     ERROR_RETRY_S = (0.1, 0.5, 2.0)
 
     async def _expire_or_retry(self, ns: str, name: str) -> None:
+        calls.mark_background()
         # one expiry per owner at a time: the timers of an attach's placeholders fire together,
         # and a second expiry racing the first would find its GPUs gone (GPUNotFound)
         lock = self._locks.setdefault((ns, name), asyncio.Lock())

@@ -23,7 +23,7 @@ from typing import Awaitable, Callable, Dict, List, Optional, Sequence, Set, Tup
 
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.device import AmdGpu
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import calls, log
 
 _log = log.get("worker.notify")
 ANN_DEVICES = "gpumounter.amd.com/devices"
@@ -83,7 +83,14 @@ class Notifier:
             except asyncio.TimeoutError:
                 return
 
+    async def quiet(self) -> None:
+        """Until no attach/detach has been in flight for ``notify_idle_ms`` (at most
+        ``notify_max_delay_ms``): background work that should not share the event loop with a
+        request (Events, the warm pool's refill) waits for this."""
+        await self._wait_idle()
+
     async def _flush(self) -> None:
+        calls.mark_background()
         while self._queue:
             await self._wait_idle()
             batch, self._queue = self._queue, []

@@ -40,7 +40,7 @@ from gpumounter_amd.cluster.kube import NotFound
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.models.types import (ANN_ATTACH_ID, ANN_CANDIDATE, ANN_CONTAINER,
                                          ANN_INCARNATION, ANN_OWNER_UID)
-from gpumounter_amd.utils import log
+from gpumounter_amd.utils import calls, log
 
 _log = log.get("worker.reconciler")
 
@@ -285,6 +285,7 @@ class Reconciler:
         self._kick(key, attempt)
 
     async def _react(self, key: tuple, attempt: int = 0) -> None:
+        calls.mark_background()
         svc = self.svc
         await asyncio.sleep(0)  # coalesce a burst of events for one owner
         self._kicked.discard(key)
@@ -398,6 +399,7 @@ class Reconciler:
     WAKE_MIN_INTERVAL_S = 1.0
 
     async def _loop(self) -> None:
+        calls.mark_background()
         # the first sweep runs at once: whatever changed while no worker was running (a
         # container restarted, a Pod deleted, an attach cut off by the previous worker's death)
         # sent its events to nobody, and the next periodic sweep may be 30 s away

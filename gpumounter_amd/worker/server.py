@@ -34,13 +34,17 @@ from gpumounter_amd.node.dra import DraLedger
 from gpumounter_amd.node.hotmount import HotMount
 from gpumounter_amd.node.journal import InjectionJournal
 from gpumounter_amd.node.ledger import LedgerClient
-from gpumounter_amd.utils import log, runtime
+from gpumounter_amd.utils import calls, log, runtime
 from gpumounter_amd.utils.faults import FaultInjector
 from gpumounter_amd.utils.metrics import Metrics
 from gpumounter_amd.worker.reconciler import Reconciler
 from gpumounter_amd.worker.service import GpuMountService, RpcError
 
 _log = log.get("worker")
+
+
+def _calls_window(q) -> list:
+    return calls.since(float(q.get("since", "0")), float(q.get("until", "inf")))
 
 
 def _ser(m) -> bytes:
@@ -121,6 +125,7 @@ class Worker:
                                        self.hotmount, self.node_informer, self.metrics,
                                        self.faults)
         self.pool = WarmPool(cfg, self.placeholders, self.inv, self.metrics)
+        self.pool.quiet = self.service.notify.quiet
         self.service.pool = self.pool
         self.plugin = None
         if cfg.device_plugin:
@@ -337,6 +342,7 @@ class Worker:
             app.router.add_get("/audit/{namespace}/{pod}", self._http_audit)
             if self.cfg.debug_endpoints:    # stacks of every task: not for the open port
                 app.router.add_get("/debug/tasks", self._debug_tasks)
+                app.router.add_get("/debug/calls", self._debug_calls)
             self.http_runner = web.AppRunner(app, access_log=None)
             await self.http_runner.setup()
             site = web.TCPSite(self.http_runner, self.cfg.worker_host, hp)
@@ -383,6 +389,11 @@ class Worker:
             for f in t.get_stack():
                 out.append(f"    {f.f_code.co_filename}:{f.f_lineno} {f.f_code.co_name}")
         return web.Response(text="\n".join(out) + "\n")
+
+    async def _debug_calls(self, request):
+        """Outbound control-plane calls that started in [since, until] (monotonic seconds):
+        utils/calls.py, for the bench's per-operation call accounting."""
+        return web.json_response(_calls_window(request.query))
 
     async def _readyz(self, request):
         return web.Response(text="ready" if self.ready else "starting",

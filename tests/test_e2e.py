@@ -1064,7 +1064,7 @@ def test_failed_attach_whose_cleanup_fails_is_followed_up_before_the_periodic_sw
                     or {}).get("gpumounter.amd.com/owner-name") == "f"]
         code, _ = await lc.add("default", "f", 1)
         assert code == 500
-        for _ in range(100):
+        for _ in range(250):           # retries at 0.1, 0.5 s: a loaded host needs longer
             await asyncio.sleep(0.02)
             if not held() and not await lc.audit("default", "f"):
                 break

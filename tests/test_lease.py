@@ -268,6 +268,10 @@ def test_a_pool_placeholder_does_not_carry_its_last_owners_lease():
         code, a = await lease_add(lc, "default", "a", 1, 0.4)
         assert code == 200
         ph, idx = a["devices"][0]["placeholder"], a["devices"][0]["index"]
+        for _ in range(250):                     # the refill (once the attach is over)
+            if len(pool.standby()) == 1 and not pool.pending():
+                break
+            await asyncio.sleep(0.02)
         pool.target = 2                          # room for it back in the pool
         code, _ = await lc.remove("default", "a", [a["devices"][0]["uuid"]])
         assert code == 200
