@@ -370,6 +370,7 @@ def main() -> int:
     ar_backend = [None]
     samples = [] if args.dump_samples and rank == 0 else None
     first_attach = []    # the first attach after the daemons started (cold everything)
+    first_stages = {}    # ... and where its time went
 
     def one_step(record: bool):
         nonlocal audit_issues, nccl_group
@@ -382,6 +383,14 @@ def main() -> int:
                 raise RuntimeError(f"attach failed: {code} {body}")
             if not first_attach:
                 first_attach.append((t1 - t0) * 1e3)
+                first_stages.update({"client": round((t1 - t0) * 1e3, 4),
+                                     "master": body.get("master_ms"),
+                                     "worker": body.get("total_ms"),
+                                     **{f"master.{t['name']}": t["ms"]
+                                        for t in body.get("master_timings", [])},
+                                     **{f"worker.{t['name']}": t["ms"]
+                                        for t in body.get("timings", [])
+                                        if "." not in t["name"]}})
             issues = cp.audit() if args.protocol == "gpumounter" else []
             obj = [{"bdfs": [d["bdf"] for d in body["devices"]],
                     "uuids": [d["uuid"] for d in body["devices"]],
@@ -732,6 +741,7 @@ def main() -> int:
                 "cold_attach_p50_ms": cold["attach_p50_ms"] if cold else None,
                 "cold_attach": cold,
                 "first_attach_ms": round(first_attach[0], 4) if first_attach else None,
+                "first_attach_stages_ms": first_stages or None,
                 # control-plane calls per operation on the critical path, by process and kind,
                 # with the serial round trips (the median cycle of --call-cycles)
                 "serial_calls_per_attach": accounting["attach"] if accounting else None,

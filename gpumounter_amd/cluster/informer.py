@@ -395,6 +395,22 @@ class ClaimInformer(PodInformer):
                                       self.rv, timeout_s=timeout_s)
 
 
+class QuotaInformer(PodInformer):
+    """List+watch of ResourceQuotas (cluster-wide): the namespace GPU quota check reads
+    ``spec.hard`` and the quota controller's ``status.used`` from here instead of a LIST per
+    attach (cluster/quota.py)."""
+
+    def _list(self):
+        return self.kube.list_quotas_rv(self.namespace, self.label_selector)
+
+    def _get(self, ns: str, name: str):
+        return self.kube.get_quota(ns, name)
+
+    def _watch(self, timeout_s: int):
+        return self.kube.watch_quotas(self.namespace, self.label_selector, self.field_selector,
+                                      self.rv, timeout_s=timeout_s)
+
+
 def slim_pod(p: dict) -> dict:
     """What the master needs of a Pod to route a request: identity, node, phase."""
     md = p.get("metadata", {})

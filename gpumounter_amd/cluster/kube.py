@@ -298,6 +298,26 @@ class KubeClient:
         out = await self._req("GET", f"/api/v1/namespaces/{ns}/resourcequotas")
         return out.get("items", [])
 
+    @staticmethod
+    def _quotas_path(ns: Optional[str]) -> str:
+        return f"/api/v1/namespaces/{ns}/resourcequotas" if ns else "/api/v1/resourcequotas"
+
+    async def list_quotas_rv(self, ns: Optional[str] = None, label_selector: str = ""
+                             ) -> Tuple[List[dict], str]:
+        params = {"labelSelector": label_selector} if label_selector else None
+        out = await self._req("GET", self._quotas_path(ns), params=params)
+        return out.get("items", []), out.get("metadata", {}).get("resourceVersion", "")
+
+    async def get_quota(self, ns: str, name: str) -> dict:
+        return await self._req("GET", f"{self._quotas_path(ns)}/{name}")
+
+    async def watch_quotas(self, ns: Optional[str] = None, label_selector: str = "",
+                           field_selector: str = "", resource_version: str = "",
+                           timeout_s: int = 300) -> AsyncIterator[Tuple[str, dict]]:
+        async for ev in self.watch(self._quotas_path(ns), label_selector, field_selector,
+                                   resource_version, timeout_s):
+            yield ev
+
     async def create_event(self, ns: str, event: dict) -> dict:
         return await self._req("POST", f"/api/v1/namespaces/{ns}/events", body=event)
 

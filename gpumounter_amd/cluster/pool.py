@@ -65,6 +65,7 @@ class WarmPool:
         self.exhausted = False               # last refill hit InsufficientGPU
         self._alloc_cache: Optional[tuple] = None   # (monotonic time, allocatable IDs)
         self._creating = 0        # standby placeholders a refill is about to create
+        self._stopping = False
         # awaited before each refill (the worker sets Notifier.quiet): the POST and the
         # admission of a new standby wait until no attach/detach is in flight, instead of
         # sharing the worker's loop with the attach that emptied the pool
@@ -121,6 +122,7 @@ class WarmPool:
         self._wake.set()
 
     async def stop(self) -> None:
+        self._stopping = True
         if self._refill_task is not None:
             self._refill_task.cancel()
             try:
@@ -134,7 +136,7 @@ class WarmPool:
 
     async def _refill_loop(self) -> None:
         calls.mark_background()
-        while True:
+        while not self._stopping:
             await self._wake.wait()
             self._wake.clear()
             try:

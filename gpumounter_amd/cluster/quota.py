@@ -13,8 +13,10 @@ quota's ``status.used`` (kept by the quota controller) gives the first term; the
 from the placeholder labels in the pool namespace. In ``tenant`` placeholder mode the placeholders
 live in N itself, so the apiserver's own quota admission already enforces it and nothing is added.
 
-Quotas are read through a short TTL cache (a quota change applies within ``ttl_s``, the quota
-controller itself is asynchronous). Concurrent attaches into one namespace on one node are
+Quotas come from a list+watch of ResourceQuotas (:class:`~gpumounter_amd.cluster.informer.
+QuotaInformer`, set by the worker): an attach into a namespace without a GPU quota makes no
+apiserver call for it. Until that watch has synced (or without it) they are read through a short
+TTL cache (a quota change applies within ``ttl_s``; the quota controller itself is asynchronous). Concurrent attaches into one namespace on one node are
 serialised; across nodes, :meth:`GpuQuota.recheck` after the placeholders exist catches an
 overshoot and rolls the attach back (two racing attaches may then both be refused, never both
 admitted past the quota).
@@ -70,6 +72,7 @@ class GpuQuota:
             # DRA: devices requested by the namespace's claims of the GPU device class
             self.keys = (f"{cfg.dra_device_class}{DEVICECLASS_QUOTA_SUFFIX}",)
         self._cache: Dict[str, Tuple[float, List[Limit]]] = {}
+        self.informer = None     # QuotaInformer (Worker.start), else the TTL cache
         self._locks: Dict[str, asyncio.Lock] = {}
         self.checks = 0
         self.refusals = 0
@@ -85,6 +88,9 @@ class GpuQuota:
         return lk
 
     async def limits(self, ns: str) -> List[Limit]:
+        inf = self.informer
+        if inf is not None and inf._synced is not None and inf._synced.is_set():  # noqa: SLF001
+            return self._limits(q for (qns, _), q in list(inf.cache.items()) if qns == ns)
         now = time.monotonic()
         hit = self._cache.get(ns)
         if hit is not None and now - hit[0] < self.ttl_s:
@@ -96,6 +102,11 @@ class GpuQuota:
                 items = []
             else:
                 raise
+        out = self._limits(items)
+        self._cache[ns] = (now, out)
+        return out
+
+    def _limits(self, items) -> List[Limit]:
         out: List[Limit] = []
         for q in items:
             hard = (q.get("spec") or {}).get("hard") or {}
@@ -104,7 +115,6 @@ class GpuQuota:
                 if k in hard:
                     out.append(Limit(q["metadata"]["name"], k, _qty(hard[k]), _qty(used.get(k, 0))))
                     break
-        self._cache[ns] = (now, out)
         return out
 
     async def hot_in_namespace(self, ns: str) -> int:

@@ -143,6 +143,9 @@ class FakeCluster:
         self.events: List[Tuple[int, str, dict]] = []
         self.k8s_events: List[dict] = []     # core/v1 Event objects (not the watch history)
         self.quotas: Dict[Tuple[str, str], dict] = {}   # ResourceQuota objects (spec.hard)
+        # ResourceQuota watch: the quota controller's status.used updates, as events
+        self.quota_events: List[Tuple[int, str, bytes]] = []
+        self.quota_watchers: List[Tuple[asyncio.Queue, str, Any, Any]] = []
         self.tokens: Dict[str, dict] = {}    # TokenReview: bearer token → user info
         self.rbac: List[dict] = []           # SubjectAccessReview rules (see grant())
         self.sar_count = 0
@@ -183,6 +186,8 @@ class FakeCluster:
         for q, ns, lsel, fsel in list(self.watchers):
             if self._matches(pod, ns, lsel, fsel):
                 q.put_nowait((etype, data, t))
+        if self.quotas:
+            self.quota_touch(pod["metadata"].get("namespace", ""))
 
     @staticmethod
     def _matches(pod: dict, ns: str, lsel, fsel) -> bool:
@@ -233,7 +238,30 @@ class FakeCluster:
              "metadata": {"name": name, "namespace": ns, "uid": str(uuid.uuid4())},
              "spec": {"hard": dict(hard)}}
         self.quotas[(ns, name)] = q
+        self._quota_bump("ADDED", q)
         return q
+
+    def _quota_bump(self, etype: str, q: dict) -> None:
+        """A quota object changed, or its status.used did (the quota controller rewrites the
+        status as the namespace's pods and claims change): an event for its watchers."""
+        self.rv += 1
+        q["metadata"]["resourceVersion"] = str(self.rv)
+        data = json.dumps(self._quota_view(q)).encode()
+        self.quota_events.append((self.rv, etype, data))
+        if len(self.quota_events) > self.HISTORY:
+            del self.quota_events[: len(self.quota_events) - self.HISTORY]
+        t = time.monotonic()
+        for wq, ns, lsel, fsel in list(self.quota_watchers):
+            if self._matches(q, ns, lsel, fsel):
+                wq.put_nowait((etype, data, t))
+
+    def quota_touch(self, ns: str) -> None:
+        """The namespace's usage may have changed: re-publish its quotas (no-op without)."""
+        if not self.quotas:
+            return
+        for (qns, _), q in list(self.quotas.items()):
+            if qns == ns:
+                self._quota_bump("MODIFIED", q)
 
     def _quota_used(self, ns: str, key: str) -> int:
         """What the quota controller reports: requests of the namespace's non-terminal pods
@@ -589,6 +617,7 @@ class FakeCluster:
         r.add_patch("/api/v1/namespaces/{ns}/pods/{name}", self._h_patch)
         r.add_get("/api/v1/nodes", self._h_nodes)
         r.add_get("/api/v1/namespaces/{ns}/resourcequotas", self._h_quota_list)
+        r.add_get("/api/v1/resourcequotas", self._h_quota_list)
         r.add_post("/apis/authentication.k8s.io/v1/tokenreviews", self._h_token_review)
         r.add_post("/apis/authorization.k8s.io/v1/subjectaccessreviews", self._h_sar)
         r.add_post("/api/v1/namespaces/{ns}/events", self._h_event_create)
@@ -845,11 +874,20 @@ class FakeCluster:
         return [e for e in self.k8s_events if e["metadata"]["namespace"] == ns
                 and e.get("involvedObject", {}).get("name") == pod]
 
-    async def _h_quota_list(self, req: web.Request) -> web.Response:
+    async def _h_quota_list(self, req: web.Request):
         await self._pre(req)
-        ns = req.match_info["ns"]
-        items = [self._quota_view(q) for (qns, _), q in self.quotas.items() if qns == ns]
-        return web.json_response({"kind": "ResourceQuotaList", "items": items})
+        ns = req.match_info.get("ns", "")
+        if req.query.get("watch") in ("true", "1"):
+            return await self._watch(
+                req, ns, _parse_selector(req.query.get("labelSelector", "")), [],
+                history=self.quota_events, watchers=self.quota_watchers,
+                current=lambda: [self._quota_view(q) for q in self.quotas.values()],
+                kind="ResourceQuota")
+        items = [self._quota_view(q) for (qns, _), q in self.quotas.items()
+                 if not ns or qns == ns]
+        return web.json_response({"kind": "ResourceQuotaList",
+                                  "metadata": {"resourceVersion": str(self.rv)},
+                                  "items": items})
 
     async def _h_nodes(self, req: web.Request) -> web.Response:
         await self._pre(req)

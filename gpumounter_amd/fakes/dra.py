@@ -71,6 +71,7 @@ class DraState:
         for q, ns, lsel, fsel in list(self.watchers):
             if self.cluster._matches(claim, ns, lsel, fsel):   # noqa: SLF001
                 q.put_nowait((etype, data))
+        self.cluster.quota_touch(claim["metadata"].get("namespace", ""))
 
     # ------------------------------------------------------------------------ slices
     def slices(self, node_name: str = "") -> List[dict]:

@@ -78,9 +78,15 @@ class Notifier:
             left = deadline - loop.time()
             if left <= 0:
                 return
+            # asyncio.wait, not wait_for: on Python 3.10 wait_for can swallow a cancellation
+            # that arrives as the inner wait completes (the waiter's task then never stops)
+            waiter = asyncio.ensure_future(self._idle.wait())
             try:
-                await asyncio.wait_for(self._idle.wait(), left)
-            except asyncio.TimeoutError:
+                done, _ = await asyncio.wait({waiter}, timeout=left)
+            finally:
+                if not waiter.done():
+                    waiter.cancel()
+            if not done:
                 return
 
     async def quiet(self) -> None:

@@ -405,7 +405,9 @@ class Reconciler:
         # sent its events to nobody, and the next periodic sweep may be 30 s away
         delay, failures = 0.0, 0
         loop = asyncio.get_running_loop()
-        while True:
+        # not `while True`: on Python 3.10 asyncio.wait_for can swallow the stop's cancellation
+        # when the wake-up lands at the same moment; the flag ends the loop regardless
+        while not self._stopping:
             if delay:
                 try:
                     await asyncio.wait_for(self._wake.wait(), delay)

@@ -21,7 +21,7 @@ from aiohttp import web
 
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.api import wire
-from gpumounter_amd.cluster.informer import ClaimInformer, PodInformer
+from gpumounter_amd.cluster.informer import ClaimInformer, PodInformer, QuotaInformer
 from gpumounter_amd.cluster.kube import KubeClient
 from gpumounter_amd.cluster.placeholder import LABEL_NODE, PlaceholderManager
 from gpumounter_amd.cluster.pool import WarmPool
@@ -124,6 +124,9 @@ class Worker:
         self.service = GpuMountService(cfg, self.kube, self.inv, self.ledger, self.placeholders,
                                        self.hotmount, self.node_informer, self.metrics,
                                        self.faults)
+        # ResourceQuotas for the namespace GPU quota check, from a watch (no LIST per attach)
+        self.quota_informer = QuotaInformer(self.kube, None, resync_s=cfg.watch_resync_s) \
+            if self.service.quota.active else None
         self.pool = WarmPool(cfg, self.placeholders, self.inv, self.metrics)
         self.pool.quiet = self.service.notify.quiet
         self.service.pool = self.pool
@@ -269,6 +272,15 @@ class Worker:
                     reconcile: bool = True, wire_port: Optional[int] = None) -> None:
         await self.ph_informer.start()
         await self.node_informer.start()
+        if self.quota_informer is not None:
+            try:
+                await self.quota_informer.start()
+                self.service.quota.informer = self.quota_informer
+            except Exception as e:  # noqa: BLE001 - no list/watch grant: per-attach reads
+                _log.warning("ResourceQuota watch unavailable (%s); quotas are read per attach",
+                             e)
+                await self.quota_informer.stop()
+                self.quota_informer = None
         if self.claim_informer is not None:
             await self.claim_informer.start()
             # a claim allocated for a placeholder can complete its admission
@@ -500,6 +512,8 @@ class Worker:
         await self.node_informer.stop()
         if self.claim_informer is not None:
             await self.claim_informer.stop()
+        if self.quota_informer is not None:
+            await self.quota_informer.stop()
         if self.checkpoint is not None:
             self.checkpoint.close()
         await self.ledger.close()

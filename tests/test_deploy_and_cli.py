@@ -194,6 +194,9 @@ def test_cluster_role_grants_every_api_call_the_daemons_make():
         "token_review": ("authentication.k8s.io", "tokenreviews", "create"),
         "subject_access_review": ("authorization.k8s.io", "subjectaccessreviews", "create"),
         "list_resource_quotas": ("", "resourcequotas", "list"),
+        "list_quotas_rv": ("", "resourcequotas", "list"),
+        "get_quota": ("", "resourcequotas", "get"),
+        "watch_quotas": ("", "resourcequotas", "watch"),
         "create_event": ("", "events", "create"),
     }
     calls = {n for n, f in inspect.getmembers(KubeClient)
