@@ -35,6 +35,9 @@ def _run_daemon(serve, cfg) -> int:
     """asyncio.run(serve(cfg)); with GM_PROFILE_OUT=<file> under cProfile, stats written at
     (SIGTERM-clean) shutdown — for finding the hot spots of a live daemon (``{pid}`` in the
     name is replaced, so several daemons can share the setting)."""
+    if getattr(cfg, "cpu_affinity", ""):
+        from gpumounter_amd.utils import runtime
+        runtime.pin_cpus(cfg.cpu_affinity)
     out = os.environ.get("GM_PROFILE_OUT", "").replace("{pid}", str(os.getpid()))
     if not out:
         asyncio.run(serve(cfg))

@@ -217,10 +217,14 @@ class KubeClient:
         out = await self._req("GET", self._pods_path(ns), params=params)
         return out.get("items", []), out.get("metadata", {}).get("resourceVersion", "")
 
-    async def create_pod(self, ns: str, pod: dict) -> dict:
+    async def create_pod(self, ns: str, pod: dict, dry_run: bool = False) -> dict:
         """Create; retried on transient errors when the name is explicit (a retry that finds
-        the pod already created by the lost first attempt returns that pod)."""
+        the pod already created by the lost first attempt returns that pod). ``dry_run``: the
+        apiserver validates and admits it but stores nothing (``?dryRun=All``)."""
         name = (pod.get("metadata") or {}).get("name", "")
+        if dry_run:
+            return await self._req("POST", self._pods_path(ns), params={"dryRun": "All"},
+                                   body=pod, idempotent=True)
         try:
             return await self._req("POST", self._pods_path(ns), body=pod, idempotent=bool(name))
         except Conflict:

@@ -784,6 +784,15 @@ class FakeCluster:
         await self._pre(req)
         ns = req.match_info["ns"]
         body = await req.json()
+        if req.query.get("dryRun") == "All":
+            # validated and admitted (quota included), nothing stored, no watch event
+            pod = podu.jcopy(body)
+            md = pod.setdefault("metadata", {})
+            md["namespace"] = ns
+            md.setdefault("uid", str(uuid.uuid4()))
+            self._quota_admit(ns, pod)
+            pod["status"] = {"phase": "Pending"}
+            return web.json_response(pod, status=201)
         pod = self.create_pod(ns, body)
         return web.json_response(pod, status=201)
 

@@ -129,6 +129,9 @@ class FakeNode:
         # out; "dra": a DRA driver publishes them in a ResourceSlice (fakes/dra.py) and the
         # device manager never sees them (no checkpoint entries)
         self.gpu_api = "device-plugin"
+        # a kubelet's device manager writes its checkpoint when it starts (registered devices,
+        # no allocations yet), not only at the first Allocate
+        self._checkpoint()
 
     def _populate_host_dev(self) -> None:
         os.makedirs(os.path.join(self.host_dev, "dri"), exist_ok=True)

@@ -321,11 +321,31 @@ class Master:
         self.http = httpd.HttpServer(self.router())
         self.port = await self.http.start(self.cfg.master_host,
                                           self.cfg.master_port if port is None else port)
+        try:
+            self.warm_up()
+        except Exception as e:  # noqa: BLE001 - only a head start
+            _log.warning("request path warm-up: %s", e)
         if self.cfg.gc_tune:
             runtime.tune_gc()
             runtime.watch_gc_pauses(5.0, _log)
         runtime.write_ready_file(self.cfg.ready_file, {"port": self.port})
         _log.info("master serving HTTP :%d", self.port)
+
+    def warm_up(self) -> None:
+        """The request path's in-process work once before the first request: the roctx library,
+        a worker reply through the payload and JSON reply code, the metric children of the
+        add/remove routes. Nothing leaves the process."""
+        trace._roctx_lib()                                       # noqa: SLF001
+        with trace.span("master_addgpu") as root:
+            with trace.span("master_rpc"):
+                resp = api.AddGPUResponse.FromString(api.AddGPUResponse(
+                    devices=[api.Device(uuid="warm-up", bdf="0000:00:00.0")], message="warm-up",
+                    timings=[api.StageTiming(name="warm-up", ms=0.0)]).SerializeToString())
+        payload = self._stamp(self._payload(resp, time.perf_counter()), root)
+        httpd.json_response(dict(payload, message="warm-up", code=200))
+        for route in ("addgpu", "removegpu"):
+            for code in ("200", "400", "500"):
+                self.metrics.http_requests.labels(route=route, code=code)
 
     async def _start_pod_index(self) -> None:
         try:

@@ -142,6 +142,10 @@ class Config:
     # both: always union with amdsmi's process table
     busy_detection: str = "auto"
     gc_tune: bool = True               # gc.freeze() after startup + larger young-gen threshold
+    # pin the daemon to these CPUs at start ("2-3,8", cpuset list format; "" = unpinned): on a
+    # node whose kubelet runs the static CPU manager, give the DaemonSet a Guaranteed CPU and
+    # the same list here, so request wake-ups land on a core nothing else uses
+    cpu_affinity: str = ""
     emit_events: bool = True           # core/v1 Events on the tenant pod (kubectl describe)
     annotate_tenant: bool = False      # keep gpumounter.amd.com/devices on the tenant pod current
     # Events/annotations are sent once the worker has had no attach/detach in flight for

@@ -288,7 +288,8 @@ class Worker:
                 lambda et, c: asyncio.ensure_future(self.ph_informer.poke()))
         # warm the ledger channel (fails fast if the kubelet socket is wrong); the authoritative
         # read also cross-checks the device-manager checkpoint before admission relies on it
-        await self.service.read_ledger(authoritative=True)
+        led = await self.service.read_ledger(authoritative=True)
+        self.service.prime(led)
         try:   # grants from before the journal existed become revocable (node/hotmount.py adopt)
             await self.service.adopt_existing()
         except Exception as e:  # noqa: BLE001 - the reconciler retries
@@ -373,6 +374,10 @@ class Worker:
         await self.service.lease.sweep()   # re-arm (or expire) leases from before a restart
         if self.cfg.health_period_s > 0:
             self._health_task = asyncio.ensure_future(self._health_loop())
+        try:
+            await self.service.warm_up()
+        except Exception as e:  # noqa: BLE001 - only a head start; the first attach pays it
+            _log.warning("attach path warm-up: %s", e)
         if self.cfg.gc_tune:
             runtime.tune_gc()
             runtime.watch_gc_pauses(5.0, _log)
