@@ -99,6 +99,18 @@ class WarmPool:
                    and not self.ph.last_ledger.get((p["metadata"]["namespace"],
                                                     p["metadata"]["name"])))
 
+    def refilling(self) -> bool:
+        """Standby placeholders are being created or admitted (they hold GPUs already)."""
+        return self._creating > 0 or self.pending() > 0
+
+    async def admitted(self, timeout: float) -> bool:
+        """Wait, at most ``timeout``, until no standby placeholder is being created or
+        admitted; True if the pool then has standby GPUs to claim."""
+        end = time.monotonic() + timeout
+        while self.refilling() and time.monotonic() < end:
+            await asyncio.sleep(0.005)
+        return bool(self.standby())
+
     # ------------------------------------------------------------------------ refill
     def standby_body(self) -> dict:
         name = f"{STANDBY_PREFIX}{_label_value(self.ph.node)[:40]}-{secrets.token_hex(4)}"

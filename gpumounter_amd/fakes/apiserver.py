@@ -629,6 +629,13 @@ class FakeCluster:
     async def _h_healthz(self, req: web.Request) -> web.Response:
         return web.Response(text="ok")
 
+    def expire_watches(self) -> None:
+        """Every open pod watch ends with 410 Gone (its resourceVersion left the history, as
+        after an apiserver restart or a compaction): the clients relist."""
+        t = time.monotonic()
+        for q, _, _, _ in list(self.watchers):
+            q.put_nowait(("__EXPIRE__", b"", t))
+
     def fail_next(self, method: str, status: int = 503, count: int = 1,
                   after: bool = False, path: str = "/pods") -> None:
         """Fault injection: the next ``count`` requests with ``method`` whose path contains
@@ -757,6 +764,11 @@ class FakeCluster:
                     continue
                 idle = 0.0
                 et, obj = item[0], item[1]
+                if et == "__EXPIRE__":
+                    await resp.write(json.dumps({"type": "ERROR", "object": {
+                        "kind": "Status", "code": 410, "reason": "Expired",
+                        "message": "too old resource version"}}).encode() + b"\n")
+                    break
                 if len(item) > 2 and self.watch_delay_s > 0:
                     lag = item[2] + self.watch_delay_s - time.monotonic()
                     if lag > 0:

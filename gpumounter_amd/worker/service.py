@@ -652,6 +652,21 @@ class GpuMountService:
         exact path is used instead when one exists — gpumounter's own device plugin (intents
         answered by GetPreferredAllocation) or a DRA claim pinned by a CEL selector. ``trim``
         always holds every free GPU; ``hint`` only annotates the preferred set."""
+        pool = self.pool if self.pool is not None and self.pool.enabled else None
+        planned = {p.uid for p in pool.standby()} if pool is not None else set()
+        try:
+            return await self._reserve_once(pod, n, req, st, preferred, n_free, lease_exp)
+        except InsufficientGPU:
+            # a refill that started before this attach held GPUs this attach's plan took for
+            # free (its standby placeholders were not admitted yet): claim those instead
+            if pool is None or not await pool.admitted(self.cfg.attach_timeout_s) or \
+                    not {p.uid for p in pool.standby()} - planned:
+                raise
+            _log.info("attach refused while the pool refilled; claiming its new standby GPUs")
+            return await self._reserve_once(pod, n, req, st, preferred, n_free, lease_exp)
+
+    async def _reserve_once(self, pod: dict, n: int, req, st: PodGpuState,
+                            preferred: List[str], n_free: int = 0, lease_exp: float = 0.0):
         dra = self.cfg.gpu_allocation == "dra"     # the claim's selector pins the devices
         mode = self.cfg.placement_enforce
         if (mode != "trim" or dra) and self.plugin is None:

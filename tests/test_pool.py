@@ -113,6 +113,33 @@ def test_pool_takes_scheduling_and_admission_off_the_attach_path():
     asyncio.run(main())
 
 
+def test_attach_during_a_refill_claims_the_new_standby_gpus():
+    """A refill that started before an attach holds the node's last free GPUs in standby
+    placeholders that are bound but not admitted yet. The attach's plan sees those GPUs as
+    free and its creates are unschedulable: it then waits for the refill's admission and
+    claims the new standby GPUs instead of answering "insufficient" with GPUs to spare
+    (found by the ledger state machine, tests/test_ledger_model.py)."""
+    lat = LatencyModel(schedule_ms=2, admit_ms=400)
+
+    async def main():
+        async with LocalCluster(latency=lat, worker_overrides={"warm_pool_size": 2}) as lc:
+            pool = await wait_pool(lc, 2, timeout=10)
+            lc.tenant("a")
+            lc.tenant("b")
+            code, b = await lc.add("default", "a", 5)          # 2 claimed + 3 created: 3 free
+            assert code == 200
+            t0 = time.monotonic()
+            while not pool.refilling():
+                assert time.monotonic() - t0 < 5, "the refill never started"
+                await asyncio.sleep(0.002)
+            assert not pool.standby()                           # bound, not admitted yet
+            code, b = await lc.add("default", "b", 2)
+            assert code == 200, b
+            assert {t["name"] for t in b["timings"]} >= {"pool_claim"}
+            assert not await lc.audit("default", "b") and not await lc.audit("default", "a")
+    asyncio.run(main())
+
+
 def test_pool_claims_released_when_tenant_disappears():
     async def main():
         async with LocalCluster(worker_overrides={"warm_pool_size": 4}) as lc:
