@@ -216,6 +216,10 @@ def main() -> int:
     ap.add_argument("--no-calib", action="store_true",
                     help="skip the box calibration (CPU loop, process pingpong, gRPC floor) "
                          "recorded as \"box\" in the JSON")
+    ap.add_argument("--pin", default="",
+                    help="--deploy processes: pin the worker and the master to CPUs "
+                         "(\"WORKER_CPUS:MASTER_CPUS\", cpuset lists, e.g. \"8:9\"; config "
+                         "cpu_affinity, as with a static CPU manager); \"\" = unpinned")
     ap.add_argument("--call-cycles", type=int, default=5,
                     help="after the timed loop: this many attach/detach cycles whose outbound "
                          "apiserver/kubelet calls are read from the daemons' call logs "
@@ -314,13 +318,16 @@ def main() -> int:
                       "plugin in-process)", file=sys.stderr)
                 return 2
             from gpumounter_amd.fakes.deployment import ProcessCluster
+            wpin, _, mpin = args.pin.partition(":")
             pc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=args.latency,
                                 gpu_bdfs=node_bdfs, protocol=args.protocol,
                                 secure=args.security == "shipped" and args.protocol == "gpumounter",
                                 gpu_api=args.gpu_api, log_dir=args.log_dir,
                                 kernel_fs=args.kernel_fs,
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
-                                            "GM_PLACEMENT_ENFORCE": args.placement}).start()
+                                            "GM_PLACEMENT_ENFORCE": args.placement,
+                                            **({"GM_CPU_AFFINITY": wpin} if wpin else {})},
+                                master_env={"GM_CPU_AFFINITY": mpin} if mpin else None).start()
             pc.tenant_pod = pc.tenant("tenant", pids={"main": [tenant_pid]})
             cp = _ProcCP(pc)
         else:
@@ -589,8 +596,7 @@ def main() -> int:
                 accounting["attach"]["admission_wait_p50_ms"] = round(pct(w, 0.5), 4) \
                     if w else None
             cold = None
-            if args.cold_steps > 0 and args.deploy == "processes" and \
-                    args.protocol == "gpumounter":
+            if args.cold_steps > 0 and args.protocol == "gpumounter":
                 # the attach an operator makes minutes after the last one: every cached authz
                 # answer expired (the pod index is a watch, so it stays current)
                 import signal as _signal
@@ -618,17 +624,23 @@ def main() -> int:
                                              for k, v in sorted(cst.items())}}
                 # 1) idle only (authz answers still cached): what idling alone costs on this box
                 idle_only = idle_cycles("idle")
-                # 2) idle past the authz TTLs: TokenReview + SubjectAccessReview asked again
-                ttl = f"{args.idle_s / 2:g}"
-                cp.pc.restart_master(_signal.SIGTERM, env={"GM_AUTHZ_TOKEN_TTL_S": ttl,
-                                                            "GM_AUTHZ_SAR_TTL_S": ttl})
-                # the restarted master's first request opens its gRPC channel: not counted
-                code, body = cp.add(n, args.mode == "entire")
-                if code != 200 or cp.remove([d["uuid"] for d in body["devices"]])[0] != 200:
-                    raise RuntimeError(f"attach after the master restart failed: {code} {body}")
-                cold = {"steps": args.cold_steps, "idle_s": args.idle_s,
-                        "authz_ttl_s": args.idle_s / 2, **idle_cycles("cold"),
-                        "idle_only": idle_only}
+                if args.deploy == "processes":
+                    # 2) idle past the authz TTLs: TokenReview + SubjectAccessReview asked again
+                    ttl = f"{args.idle_s / 2:g}"
+                    cp.pc.restart_master(_signal.SIGTERM, env={"GM_AUTHZ_TOKEN_TTL_S": ttl,
+                                                                "GM_AUTHZ_SAR_TTL_S": ttl})
+                    # the restarted master's first request opens its channels: not counted
+                    code, body = cp.add(n, args.mode == "entire")
+                    if code != 200 or \
+                            cp.remove([d["uuid"] for d in body["devices"]])[0] != 200:
+                        raise RuntimeError(f"attach after the master restart failed: "
+                                           f"{code} {body}")
+                    cold = {"steps": args.cold_steps, "idle_s": args.idle_s,
+                            "authz_ttl_s": args.idle_s / 2, **idle_cycles("cold"),
+                            "idle_only": idle_only}
+                else:        # one process, no authz (LocalCluster): idling alone
+                    cold = {"steps": args.cold_steps, "idle_s": args.idle_s,
+                            "authz_ttl_s": None, **idle_only, "idle_only": idle_only}
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
             corrections = cp.corrections() if args.protocol == "gpumounter" else None
             placeholders_left = cp.placeholders_left()
@@ -714,6 +726,7 @@ def main() -> int:
                     "warm_pool": args.warm_pool, "placement": args.placement,
                     "device_plugin": args.device_plugin, "deploy": args.deploy,
                     "gpu_allocation": args.gpu_api,
+                    "daemon_cpus": args.pin or None,
                     "security": "mTLS master-worker + TokenReview/SAR authz (cached)"
                     if args.deploy == "processes" and args.security == "shipped" and
                     args.protocol == "gpumounter" else "off (insecure gRPC, no authz)",

@@ -42,6 +42,7 @@ HDR = struct.Struct(">IIBB")          # length, stream, kind, code
 MAX_FRAME = 4 << 20
 KIND_REQ, KIND_RESP, KIND_ERR = 0, 1, 2
 METHOD_ADD, METHOD_REMOVE, METHOD_STATUS = 1, 2, 3
+METHOD_PING = 0        # answered by the server itself with an empty response (warm-up)
 _CODES = {c.value[0]: c for c in grpc.StatusCode}
 
 
@@ -172,6 +173,10 @@ class _ServerConn(asyncio.Protocol):
 
     async def _serve(self, stream: int, method: int, body: bytes) -> None:
         h = self.srv.handlers.get(method)
+        if h is None and method == METHOD_PING:
+            if self.t is not None:
+                self.t.write(_frame(stream, KIND_RESP, 0, b""))
+            return
         try:
             if h is None:
                 raise WireStatus(grpc.StatusCode.UNIMPLEMENTED, f"method {method}")
@@ -301,13 +306,20 @@ class WireChannel:
         return proto
 
     def warm(self) -> None:
-        """Open the connection in the background (TCP and TLS handshakes off the request)."""
+        """Open the connection in the background (TCP and TLS handshakes off the request) and
+        send one ping over it, so the first request's frame path is not a cold one on either
+        side."""
         if (self._conn is None or self._conn.t is None) and \
                 (self._connecting is None or self._connecting.done()) and not self._closed:
             self._connecting = asyncio.ensure_future(self._open())
             # an unreachable worker is reported by the call that needs it
-            self._connecting.add_done_callback(
-                lambda f: f.cancelled() or f.exception())
+            self._connecting.add_done_callback(self._opened)
+
+    def _opened(self, f: asyncio.Future) -> None:
+        if f.cancelled() or f.exception() is not None or self._closed:
+            return
+        ping = asyncio.ensure_future(self.call(METHOD_PING, b"", self.CONNECT_TIMEOUT_S))
+        ping.add_done_callback(lambda p: p.cancelled() or p.exception())
 
     async def call(self, method: int, payload: bytes, timeout: float) -> bytes:
         loop = asyncio.get_running_loop()

@@ -323,6 +323,7 @@ class Master:
                                           self.cfg.master_port if port is None else port)
         try:
             self.warm_up()
+            await self._warm_http()
         except Exception as e:  # noqa: BLE001 - only a head start
             _log.warning("request path warm-up: %s", e)
         if self.cfg.gc_tune:
@@ -343,9 +344,25 @@ class Master:
                     timings=[api.StageTiming(name="warm-up", ms=0.0)]).SerializeToString())
         payload = self._stamp(self._payload(resp, time.perf_counter()), root)
         httpd.json_response(dict(payload, message="warm-up", code=200))
+        for req in (api.AddGPURequest(pod_name="warm-up", namespace="default", gpu_num=1),
+                    api.RemoveGPURequest(pod_name="warm-up", namespace="default",
+                                         uuids=["warm-up"])):
+            req.SerializeToString()
         for route in ("addgpu", "removegpu"):
             for code in ("200", "400", "500"):
                 self.metrics.http_requests.labels(route=route, code=code)
+
+    async def _warm_http(self) -> None:
+        """One request through the HTTP server over loopback (accept, parse, route, reply):
+        the server half of a client's first request is then not cold code."""
+        host = "127.0.0.1" if self.cfg.master_host in ("", "0.0.0.0", "::") else \
+            self.cfg.master_host
+        r, w = await asyncio.wait_for(asyncio.open_connection(host, self.port), 2.0)
+        try:
+            w.write(b"GET /healthz HTTP/1.1\r\nHost: warm-up\r\nConnection: close\r\n\r\n")
+            await asyncio.wait_for(r.read(), 2.0)
+        finally:
+            w.close()
 
     async def _start_pod_index(self) -> None:
         try:

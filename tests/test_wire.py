@@ -90,6 +90,30 @@ def test_round_trip_statuses_and_multiplexing():
     asyncio.run(main())
 
 
+def test_warm_opens_and_pings():
+    """warm() connects in the background and pings: the server answers PING itself (no
+    handler runs) and the channel is connected before the first real call."""
+    async def main():
+        log = []
+        srv = wire.WireServer(_handlers(log))
+        port = await srv.start("127.0.0.1", 0)
+        ch = wire.WireChannel("127.0.0.1", port)
+        try:
+            ch.warm()
+            for _ in range(100):
+                if ch._conn is not None and ch._stream > 1:   # noqa: SLF001
+                    break
+                await asyncio.sleep(0.01)
+            assert ch._stream == 3                            # noqa: SLF001 - one ping sent
+            assert await ch.call(wire.METHOD_PING, b"", 2.0) == b""
+            assert log == []
+            assert (await _call(ch, "p")).message == "p"
+        finally:
+            await ch.close()
+            await srv.stop()
+    asyncio.run(main())
+
+
 def test_connection_loss_and_unreachable():
     async def main():
         srv = wire.WireServer(_handlers())
