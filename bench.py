@@ -390,6 +390,12 @@ def main() -> int:
                 raise RuntimeError(f"attach failed: {code} {body}")
             if not first_attach:
                 first_attach.append((t1 - t0) * 1e3)
+                mc = body.get("master_clock") or {}
+                if mc:   # perf_counter is CLOCK_MONOTONIC, the master's clock, on Linux
+                    first_stages.update({
+                        "http.request_leg": round((mc["in"] - t0) * 1e3, 4),
+                        "http.master_in_to_out": round((mc["out"] - mc["in"]) * 1e3, 4),
+                        "http.response_leg": round((t1 - mc["out"]) * 1e3, 4)})
                 first_stages.update({"client": round((t1 - t0) * 1e3, 4),
                                      "master": body.get("master_ms"),
                                      "worker": body.get("total_ms"),
@@ -612,8 +618,15 @@ def main() -> int:
                             raise RuntimeError(f"cold attach failed: {code} {body}")
                         cms.append((tb - ta) * 1e3)
                         for t in body.get("master_timings", []) + [
-                                {"name": "worker", "ms": body.get("total_ms", 0.0)}]:
+                                {"name": "worker", "ms": body.get("total_ms", 0.0)}] + [
+                                {"name": f"worker.{t['name']}", "ms": t["ms"]}
+                                for t in body.get("timings", []) if "." not in t["name"]]:
                             cst.setdefault(t["name"], []).append(t["ms"])
+                        mc = body.get("master_clock") or {}
+                        if mc:
+                            for k, v in (("http.request_leg", mc["in"] - ta),
+                                         ("http.response_leg", tb - mc["out"])):
+                                cst.setdefault(k, []).append(v * 1e3)
                         code, body = cp.remove([d["uuid"] for d in body["devices"]])
                         if code != 200:
                             raise RuntimeError(f"cold detach failed: {code} {body}")

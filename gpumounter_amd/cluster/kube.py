@@ -71,6 +71,9 @@ class KubeClient:
                 self._ssl = ctx
         self._session: Optional[aiohttp.ClientSession] = None
         self._session_loop = None
+        # a request may carry another bearer token (a self-review as the caller) only when the
+        # apiserver authenticates this client by its token, not by a TLS client certificate
+        self.bearer_only = client_cert is None
 
     # ------------------------------------------------------------------------- construction
     @classmethod
@@ -147,7 +150,7 @@ class KubeClient:
 
     async def _req(self, method: str, path: str, params: Optional[dict] = None,
                    body: Any = None, content_type: str = "application/json",
-                   idempotent: Optional[bool] = None) -> Any:
+                   idempotent: Optional[bool] = None, as_token: str = "") -> Any:
         """One API request. GET/PATCH/DELETE (and POSTs the caller marks ``idempotent``) are
         retried on 429/5xx and transport errors; a transport failure surfaces as
         ``ApiError(503)`` so callers handle one exception type."""
@@ -155,7 +158,8 @@ class KubeClient:
         delays = self.RETRY_DELAYS if retry else ()
         for attempt in range(len(delays) + 1):
             try:
-                return await self._req_once(method, path, params, body, content_type)
+                return await self._req_once(method, path, params, body, content_type,
+                                            as_token)
             except ApiError as e:
                 if e.status not in self.RETRY_STATUS or attempt == len(delays):
                     raise
@@ -171,10 +175,10 @@ class KubeClient:
         raise AssertionError("unreachable")
 
     async def _req_once(self, method: str, path: str, params: Optional[dict], body: Any,
-                        content_type: str) -> Any:
+                        content_type: str, as_token: str = "") -> Any:
         sess = self._sess()
         data = None
-        headers = {}
+        headers = {"Authorization": f"Bearer {as_token}"} if as_token else {}
         if body is not None:
             data = json.dumps(body)
             headers["Content-Type"] = content_type
@@ -296,6 +300,17 @@ class KubeClient:
                                              "groups": user.get("groups", []),
                                              "extra": user.get("extra", {}),
                                              "resourceAttributes": resource_attributes}})
+        return (out or {}).get("status") or {}
+
+    async def self_subject_access_review(self, token: str, resource_attributes: dict) -> dict:
+        """A SelfSubjectAccessReview sent with the caller's ``token``: the apiserver
+        authenticates the token and answers for that user (allowed to every authenticated user
+        by the default ``system:basic-user`` role)."""
+        out = await self._req("POST", "/apis/authorization.k8s.io/v1/selfsubjectaccessreviews",
+                              body={"apiVersion": "authorization.k8s.io/v1",
+                                    "kind": "SelfSubjectAccessReview",
+                                    "spec": {"resourceAttributes": resource_attributes}},
+                              idempotent=True, as_token=token)
         return (out or {}).get("status") or {}
 
     async def list_resource_quotas(self, ns: str) -> List[dict]:

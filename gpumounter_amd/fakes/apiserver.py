@@ -149,6 +149,8 @@ class FakeCluster:
         self.tokens: Dict[str, dict] = {}    # TokenReview: bearer token → user info
         self.rbac: List[dict] = []           # SubjectAccessReview rules (see grant())
         self.sar_count = 0
+        self.ssar_count = 0
+        self.serve_self_review = True     # False: /selfsubjectaccessreviews answers 404
         self.watchers: List[Tuple[asyncio.Queue, str, Any, Any]] = []
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self.request_count = 0
@@ -620,6 +622,7 @@ class FakeCluster:
         r.add_get("/api/v1/resourcequotas", self._h_quota_list)
         r.add_post("/apis/authentication.k8s.io/v1/tokenreviews", self._h_token_review)
         r.add_post("/apis/authorization.k8s.io/v1/subjectaccessreviews", self._h_sar)
+        r.add_post("/apis/authorization.k8s.io/v1/selfsubjectaccessreviews", self._h_ssar)
         r.add_post("/api/v1/namespaces/{ns}/events", self._h_event_create)
         r.add_get("/api/v1/namespaces/{ns}/events", self._h_event_list)
         r.add_get("/healthz", self._h_healthz)
@@ -861,15 +864,35 @@ class FakeCluster:
         await self._pre(req)
         body = await req.json()
         spec = body.get("spec", {})
-        ra = spec.get("resourceAttributes", {})
-        res = ra.get("resource", "") + (f"/{ra['subresource']}" if ra.get("subresource") else "")
-        who = {spec.get("user", "")} | {f"group:{g}" for g in spec.get("groups", [])}
-        allowed = any(r["subject"] in who and ra.get("verb") in r["verbs"]
-                      and r["resource"] == res
-                      and ("*" in r["namespaces"] or ra.get("namespace", "") in r["namespaces"])
-                      for r in self.rbac)
+        allowed = self._allowed(spec.get("user", ""), spec.get("groups", []),
+                                spec.get("resourceAttributes", {}))
         self.sar_count += 1
         return web.json_response({**body, "status": {"allowed": allowed}}, status=201)
+
+    def _allowed(self, user: str, groups, ra: dict) -> bool:
+        res = ra.get("resource", "") + (f"/{ra['subresource']}" if ra.get("subresource") else "")
+        who = {user} | {f"group:{g}" for g in groups}
+        return any(r["subject"] in who and ra.get("verb") in r["verbs"]
+                   and r["resource"] == res
+                   and ("*" in r["namespaces"] or ra.get("namespace", "") in r["namespaces"])
+                   for r in self.rbac)
+
+    async def _h_ssar(self, req: web.Request) -> web.Response:
+        """SelfSubjectAccessReview: the request's own bearer token is the subject (401 for an
+        unknown token; ``serve_self_review = False`` answers 404, as an apiserver without
+        the API would)."""
+        await self._pre(req)
+        if not self.serve_self_review:
+            return web.json_response({"kind": "Status", "code": 404}, status=404)
+        auth = req.headers.get("Authorization", "")
+        user = self.tokens.get(auth[7:] if auth.startswith("Bearer ") else "")
+        if user is None:
+            return web.json_response({"kind": "Status", "code": 401}, status=401)
+        body = await req.json()
+        ra = body.get("spec", {}).get("resourceAttributes", {})
+        self.ssar_count += 1
+        return web.json_response({**body, "status": {
+            "allowed": self._allowed(user["username"], user["groups"], ra)}}, status=201)
 
     async def _h_event_create(self, req: web.Request) -> web.Response:
         await self._pre(req)

@@ -595,7 +595,7 @@ class Master:
             ns, name, n, entire, request.query.get("container", ""), rid,
             request.headers.get("Idempotency-Key", "") or rid, request.get(USER_KEY, ""),
             lease_s)
-        return self._reply(request, route, status, text, self._stamp(payload, root))
+        return self._reply(request, route, status, text, self._stamp(payload, root, request))
 
     async def remove_gpu(self, request: Request) -> Response:
         with trace.span("master_removegpu") as root:
@@ -625,7 +625,7 @@ class Master:
         status, text, payload = await self._remove(ns, name, uuids, force,
                                                    request.query.get("container", ""), rid,
                                                    request.get(USER_KEY, ""))
-        return self._reply(request, route, status, text, self._stamp(payload, root))
+        return self._reply(request, route, status, text, self._stamp(payload, root, request))
 
     @staticmethod
     def _legs(resp, t_send: float, t_recv: float) -> None:
@@ -646,12 +646,16 @@ class Master:
         trace.record("grpc_response", int((t_recv * 1e3 - t_out) * 1e6))
 
     @staticmethod
-    def _stamp(payload: dict, root: trace.Span) -> dict:
+    def _stamp(payload: dict, root: trace.Span, request: Optional[Request] = None) -> dict:
         """The master's own stage split so far (authz, locate, rpc, payload), for the JSON
-        reply; the text reply ignores it."""
+        reply; the text reply ignores it. ``master_clock``: CLOCK_MONOTONIC when the request
+        began to arrive and when its reply is encoded, so a client on the same host can split
+        its own round trip (bench.py ``first_attach_stages_ms``)."""
         if payload:
             payload["master_timings"] = [{"name": k, "ms": round(v, 4)}
                                          for k, v in root.flat().items()]
+            if request is not None and request.t_in:
+                payload["master_clock"] = {"in": request.t_in, "out": time.monotonic()}
         return payload
 
     async def batch(self, request: Request) -> Response:

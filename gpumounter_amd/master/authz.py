@@ -19,7 +19,11 @@ requests costs no review round trip. The path stays warm and cheap beyond that:
 * once an entry has expired, a token seen before has its TokenReview and its
   SubjectAccessReview — asked for the identity the token had last time — sent together: one
   round trip instead of two. The SAR answer counts only if the TokenReview confirms that same
-  identity; otherwise the SAR is asked again for the new one.
+  identity; otherwise the SAR is asked again for the new one;
+* a token seen for the first time has its TokenReview and a SelfSubjectAccessReview made with
+  the token itself sent together (``authz_self_review``): the apiserver answers for whoever the
+  token authenticates as, so no identity has to be guessed. Where the self-review is not
+  served (or not allowed), the SubjectAccessReview follows the TokenReview as before.
 """
 from __future__ import annotations
 
@@ -70,7 +74,9 @@ class Authorizer:
         self._last_user: Dict[str, dict] = {}
         self._refreshing: set = set()
         self._bg: set = set()
-        self.reviews = {"token": 0, "sar": 0, "speculative": 0, "refresh": 0}
+        self.reviews = {"token": 0, "sar": 0, "speculative": 0, "refresh": 0, "self": 0}
+        self.self_review = bool(getattr(cfg, "authz_self_review", True)) and \
+            bool(getattr(kube, "bearer_only", False))
 
     @staticmethod
     def _bearer(headers) -> str:
@@ -92,22 +98,31 @@ class Authorizer:
         key = hashlib.sha256(token.encode()).hexdigest()
         guess = None if self._fresh(self._tokens.get(key), self.token_ttl_s) else \
             self._last_user.get(key)
-        spec = None
+        spec = own = None
         if guess is not None:
             # expired token entry: the SAR for the identity it had goes out with the TokenReview
             self.reviews["speculative"] += 1
             spec = asyncio.ensure_future(self._authorize(guess, verb, namespace, resource, name))
+        elif self.self_review and key not in self._tokens:
+            # a token never seen: the apiserver reviews it as itself, alongside the TokenReview
+            self.reviews["self"] += 1
+            own = asyncio.ensure_future(self._self_review(token, verb, namespace, resource, name))
         try:
             user = await self._authenticate(token, key)
         except Exception as e:  # noqa: BLE001
             _drop(spec)
+            _drop(own)
             _log.error("TokenReview failed: %s", e)
             return Decision(False, 503, "authentication unavailable")
         if user is None:
             _drop(spec)
+            _drop(own)
             return Decision(False, 401, "Unauthorized: token not accepted")
         try:
-            if spec is not None and self._same(user, guess):
+            ok = await self._own_answer(own)
+            if ok is not None:
+                self._remember(user, verb, namespace, resource, name, ok)
+            elif spec is not None and self._same(user, guess):
                 ok = await spec
             else:
                 _drop(spec)
@@ -174,6 +189,41 @@ class Authorizer:
             self._last_user.pop(key, None)
         return user
 
+    @staticmethod
+    def _attrs(verb: str, namespace: str, resource: str, name: str) -> dict:
+        attrs = {"verb": verb, "resource": resource, "subresource": RESOURCE_SUB,
+                 "group": "", "version": "v1"}
+        if namespace:
+            attrs["namespace"] = namespace
+        if name:
+            attrs["name"] = name
+        return attrs
+
+    @staticmethod
+    async def _own_answer(own: Optional[asyncio.Future]) -> Optional[bool]:
+        """The self-review's answer; None if there was none or it failed (the API not served,
+        the self-review not allowed to this user): a SubjectAccessReview decides instead."""
+        if own is None:
+            return None
+        try:
+            return await own
+        except Exception as e:  # noqa: BLE001
+            _log.debug("SelfSubjectAccessReview: %s; SubjectAccessReview instead", e)
+            return None
+
+    async def _self_review(self, token: str, verb: str, namespace: str, resource: str,
+                           name: str) -> bool:
+        st = await self.kube.self_subject_access_review(
+            token, self._attrs(verb, namespace, resource, name))
+        return bool(st.get("allowed")) and not st.get("denied")
+
+    def _remember(self, user: dict, verb: str, namespace: str, resource: str, name: str,
+                  ok: bool) -> None:
+        if len(self._sar) > 16384:
+            self._sar.clear()
+        self._sar[(user["username"], tuple(user["groups"]), verb, namespace, resource, name)] = \
+            (time.monotonic(), ok)
+
     async def _authorize(self, user: dict, verb: str, namespace: str, resource: str,
                          name: str, force: bool = False) -> bool:
         key = (user["username"], tuple(user["groups"]), verb, namespace, resource, name)
@@ -184,17 +234,10 @@ class Authorizer:
                                                         force=True))
             return hit[1]
         self.reviews["sar"] += 1
-        attrs = {"verb": verb, "resource": resource, "subresource": RESOURCE_SUB,
-                 "group": "", "version": "v1"}
-        if namespace:
-            attrs["namespace"] = namespace
-        if name:
-            attrs["name"] = name
-        st = await self.kube.subject_access_review(user, attrs)
+        st = await self.kube.subject_access_review(
+            user, self._attrs(verb, namespace, resource, name))
         ok = bool(st.get("allowed")) and not st.get("denied")
-        if len(self._sar) > 16384:
-            self._sar.clear()
-        self._sar[key] = (time.monotonic(), ok)
+        self._remember(user, verb, namespace, resource, name, ok)
         return ok
 
     async def stop(self) -> None:

@@ -72,7 +72,7 @@ def json_response(data, status: int = 200) -> Response:
 
 class Request:
     __slots__ = ("method", "path", "query_string", "version", "headers", "body", "match_info",
-                 "remote", "_query", "_vals")
+                 "remote", "_query", "_vals", "t_in")
 
     def __init__(self, method: str, path: str, query_string: str, version: str,
                  headers: CIMultiDict, body: bytes, remote: Optional[str]) -> None:
@@ -86,6 +86,7 @@ class Request:
         self.match_info: Dict[str, str] = {}
         self._query: Optional[MultiDict] = None
         self._vals: Dict[str, object] = {}
+        self.t_in = 0.0          # time.monotonic() of the data_received that began it
 
     @property
     def query(self) -> MultiDict:
@@ -176,6 +177,7 @@ class _Conn(asyncio.Protocol):
         self.remote: Optional[str] = None
         self.idle: Optional[asyncio.TimerHandle] = None
         self._continued = False        # "100 Continue" sent for the request being read
+        self.t_first = 0.0             # when the request being read began to arrive
 
     # ------------------------------------------------------------------ transport callbacks
     def connection_made(self, transport) -> None:
@@ -192,6 +194,8 @@ class _Conn(asyncio.Protocol):
             self.idle.cancel()
 
     def data_received(self, data: bytes) -> None:
+        if not self.buf:
+            self.t_first = time.monotonic()
         self.buf += data
         if not self.busy:
             self._next()
@@ -267,6 +271,9 @@ class _Conn(asyncio.Protocol):
         conn_hdr = headers.get("Connection", "").lower()
         keep = conn_hdr == "keep-alive" if version == "HTTP/1.0" else conn_hdr != "close"
         req = Request(method, path, qs, version, headers, body, self.remote)
+        req.t_in = self.t_first
+        if buf:
+            self.t_first = time.monotonic()  # a pipelined request: already (partly) here
         self.busy = True
         if self.idle is not None:
             self.idle.cancel()

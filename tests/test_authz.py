@@ -54,8 +54,68 @@ def test_reviews_are_cached():
             assert code == 200
             assert (await lc.remove("team-a", "a1", [b["devices"][0]["uuid"]],
                                     token="tok-alice"))[0] == 200
-        assert (authz.reviews["token"], authz.reviews["sar"]) == (1, 2)  # per (user, verb, ns, pod)
+        # per (user, verb, ns, pod): the first (create) answered by the self-review that went
+        # out with the TokenReview, the delete by a SubjectAccessReview
+        assert (authz.reviews["token"], authz.reviews["self"], authz.reviews["sar"]) == (1, 1, 1)
     run(body)
+
+
+def test_a_new_token_is_reviewed_as_itself_in_one_round_trip():
+    """First sight of a token: TokenReview ∥ SelfSubjectAccessReview sent with that token (the
+    apiserver answers for whoever it authenticates as); where the self-review is not served the
+    SubjectAccessReview follows the TokenReview, with the same decisions."""
+    async def body(lc):
+        lc.tenant("a1", ns="team-a")
+        lc.tenant("d1", ns="default")
+        authz, c = lc.master.authz, lc.cluster
+        kube = authz.kube
+        spans = []
+        real_tr, real_ssar = kube.token_review, kube.self_subject_access_review
+
+        async def tr(token):
+            t0 = asyncio.get_running_loop().time()
+            out = await real_tr(token)
+            spans.append(("tr", t0, asyncio.get_running_loop().time()))
+            return out
+
+        async def ssar(token, attrs):
+            t0 = asyncio.get_running_loop().time()
+            out = await real_ssar(token, attrs)
+            spans.append(("ssar", t0, asyncio.get_running_loop().time()))
+            return out
+        kube.token_review, kube.self_subject_access_review = tr, ssar
+        code, b = await lc.add("team-a", "a1", 1, token="tok-alice")
+        assert code == 200 and c.ssar_count == 1 and c.sar_count == 0
+        (t_tr,), (t_own,) = [x for x in spans if x[0] == "tr"], [x for x in spans if x[0] == "ssar"]
+        assert t_own[1] < t_tr[2]                          # sent before the TokenReview answered
+        code, b2 = await lc.add("default", "d1", 1, token="tok-bob")
+        assert code == 403 and "bob cannot create" in b2["message"] and c.ssar_count == 2
+        assert (await lc.add("team-a", "a1", 1, token="nope"))[0] == 401
+        # an apiserver without the self-review API: TokenReview, then SubjectAccessReview
+        c.serve_self_review = False
+        assert (await lc.add("default", "d1", 1, token="tok-ops"))[0] == 200
+        c.add_user("tok-carol", "carol")
+        code, b3 = await lc.add("team-a", "a1", 1, token="tok-carol")
+        assert code == 403 and "carol cannot create" in b3["message"]
+        assert c.sar_count == 2 and authz.reviews["self"] == 5
+    run(body)
+
+
+def test_no_self_review_when_the_master_authenticates_by_certificate():
+    """With a TLS client certificate the apiserver would review the master itself, not the
+    caller: the master then asks SubjectAccessReviews only."""
+    from gpumounter_amd.master.authz import Authorizer
+
+    class Cfg:
+        authz_mode, api_token, authz_self_review = "kube", "", True
+
+    class Kube:
+        bearer_only = False
+    assert not Authorizer(Cfg(), Kube()).self_review
+    Kube.bearer_only = True
+    assert Authorizer(Cfg(), Kube()).self_review
+    Cfg.authz_self_review = False
+    assert not Authorizer(Cfg(), Kube()).self_review
 
 
 def test_batch_checks_every_operation():
@@ -121,6 +181,7 @@ def test_an_expired_token_is_reviewed_together_with_its_sar():
             spans.append(("sar", t0, asyncio.get_running_loop().time()))
             return out
         kube.token_review, kube.subject_access_review = tr, sar
+        authz.self_review = False        # first sight as on an apiserver without the API
         code, b = await lc.add("team-a", "a1", 1, token="tok-alice")
         assert code == 200
         first = list(spans)

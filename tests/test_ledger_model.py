@@ -44,6 +44,10 @@ CONVERGE_S = 15.0
 
 EXAMPLES = int(os.environ.get("GM_MODEL_EXAMPLES", "4"))
 STEPS = int(os.environ.get("GM_MODEL_STEPS", "10"))
+# GM_MODEL_REFUSALS=off: do not flag an attach refused for too few GPUs while the model
+# counts enough free ones (the refill race found by this model is in every tree before its fix;
+# off isolates the other findings on old trees, bench/model_parents.sh)
+REFUSALS = os.environ.get("GM_MODEL_REFUSALS", "strict") != "off"
 # GM_MODEL_SHRINK=0: report the first failing sequence as found (a cluster run is
 # nondeterministic: shrinking replays it many times and can end in a Flaky report)
 PHASES = [Phase.explicit, Phase.reuse, Phase.generate] + \
@@ -129,7 +133,7 @@ class LedgerModel(RuleBasedStateMachine):
                   f"{t}: refused as a mount-mode conflict; steps {self.steps}")
             return
         if code == 500 and body.get("add_gpu_result") == "InsufficientGPU":
-            check(excused or self.room() < n,
+            check(excused or not REFUSALS or self.room() < n,
                   f"{t}: {n} GPU(s) refused with {self.room()} free; steps {self.steps}")
             return
         check(excused, f"{t}: {code} {body} with no fault injected; steps {self.steps}")
