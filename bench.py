@@ -220,6 +220,9 @@ def main() -> int:
                     help="--deploy processes: pin the worker and the master to CPUs "
                          "(\"WORKER_CPUS:MASTER_CPUS\", cpuset lists, e.g. \"8:9\"; config "
                          "cpu_affinity, as with a static CPU manager); \"\" = unpinned")
+    ap.add_argument("--daemon-env", action="append", default=[], metavar="KEY=VALUE",
+                    help="--deploy processes: an environment setting for both daemons (a GM_* "
+                         "config override, e.g. GM_AUTHZ_SELF_REVIEW=false); repeatable")
     ap.add_argument("--call-cycles", type=int, default=5,
                     help="after the timed loop: this many attach/detach cycles whose outbound "
                          "apiserver/kubelet calls are read from the daemons' call logs "
@@ -319,6 +322,7 @@ def main() -> int:
                 return 2
             from gpumounter_amd.fakes.deployment import ProcessCluster
             wpin, _, mpin = args.pin.partition(":")
+            denv = dict(kv.split("=", 1) for kv in args.daemon_env)
             pc = ProcessCluster(amdsmi_lib=amdsmi, cgroup_mode=args.cgroup, latency=args.latency,
                                 gpu_bdfs=node_bdfs, protocol=args.protocol,
                                 secure=args.security == "shipped" and args.protocol == "gpumounter",
@@ -326,8 +330,10 @@ def main() -> int:
                                 kernel_fs=args.kernel_fs,
                                 worker_env={"GM_WARM_POOL_SIZE": str(args.warm_pool),
                                             "GM_PLACEMENT_ENFORCE": args.placement,
-                                            **({"GM_CPU_AFFINITY": wpin} if wpin else {})},
-                                master_env={"GM_CPU_AFFINITY": mpin} if mpin else None).start()
+                                            **({"GM_CPU_AFFINITY": wpin} if wpin else {}),
+                                            **denv},
+                                master_env={**({"GM_CPU_AFFINITY": mpin} if mpin else {}),
+                                            **denv}).start()
             pc.tenant_pod = pc.tenant("tenant", pids={"main": [tenant_pid]})
             cp = _ProcCP(pc)
         else:
@@ -740,6 +746,7 @@ def main() -> int:
                     "device_plugin": args.device_plugin, "deploy": args.deploy,
                     "gpu_allocation": args.gpu_api,
                     "daemon_cpus": args.pin or None,
+                    "daemon_env": args.daemon_env or None,
                     "security": "mTLS master-worker + TokenReview/SAR authz (cached)"
                     if args.deploy == "processes" and args.security == "shipped" and
                     args.protocol == "gpumounter" else "off (insecure gRPC, no authz)",

@@ -131,7 +131,11 @@ class KubeClient:
             headers = {"Accept": "application/json"}
             if self.token:
                 headers["Authorization"] = f"Bearer {self.token}"
-            conn = aiohttp.TCPConnector(limit=64, ssl=self._ssl if self._ssl is not None else None)
+            # idle keep-alive connections live a minute (aiohttp: 15 s), so requests a minute
+            # apart (an operator's attaches, the reviews of an expired authz answer) connect
+            # nothing
+            conn = aiohttp.TCPConnector(limit=64, keepalive_timeout=60.0,
+                                        ssl=self._ssl if self._ssl is not None else None)
             self._session = aiohttp.ClientSession(headers=headers, connector=conn,
                                                   timeout=self.timeout)
             self._session_loop = loop

@@ -324,6 +324,7 @@ class Master:
         try:
             self.warm_up()
             await self._warm_http()
+            await asyncio.wait_for(self.authz.warm_up(), 2.0)
         except Exception as e:  # noqa: BLE001 - only a head start
             _log.warning("request path warm-up: %s", e)
         if self.cfg.gc_tune:

@@ -20,10 +20,11 @@ requests costs no review round trip. The path stays warm and cheap beyond that:
   SubjectAccessReview — asked for the identity the token had last time — sent together: one
   round trip instead of two. The SAR answer counts only if the TokenReview confirms that same
   identity; otherwise the SAR is asked again for the new one;
-* a token seen for the first time has its TokenReview and a SelfSubjectAccessReview made with
-  the token itself sent together (``authz_self_review``): the apiserver answers for whoever the
-  token authenticates as, so no identity has to be guessed. Where the self-review is not
-  served (or not allowed), the SubjectAccessReview follows the TokenReview as before.
+* with ``authz_self_review`` (off by default), a token seen for the first time has its
+  TokenReview and a SelfSubjectAccessReview made with the token itself sent together: the
+  apiserver answers for whoever the token authenticates as, so no identity has to be guessed.
+  Where the self-review is not served (or not allowed), the SubjectAccessReview follows the
+  TokenReview as before.
 """
 from __future__ import annotations
 
@@ -75,7 +76,7 @@ class Authorizer:
         self._refreshing: set = set()
         self._bg: set = set()
         self.reviews = {"token": 0, "sar": 0, "speculative": 0, "refresh": 0, "self": 0}
-        self.self_review = bool(getattr(cfg, "authz_self_review", True)) and \
+        self.self_review = bool(getattr(cfg, "authz_self_review", False)) and \
             bool(getattr(kube, "bearer_only", False))
 
     @staticmethod
@@ -239,6 +240,16 @@ class Authorizer:
         ok = bool(st.get("allowed")) and not st.get("denied")
         self._remember(user, verb, namespace, resource, name, ok)
         return ok
+
+    async def warm_up(self) -> None:
+        """Open as many keep-alive connections to the apiserver as a first request's reviews
+        run at once (two with the self-review), with TokenReviews of a token nobody holds:
+        the reviews of the first request then connect nothing."""
+        if self.mode != "kube":
+            return
+        n = 2 if self.self_review else 1
+        await asyncio.gather(*(self.kube.token_review("gm-warm-up-not-a-token")
+                               for _ in range(n)))
 
     async def stop(self) -> None:
         for t in list(self._bg):

@@ -199,11 +199,13 @@ class Config:
     authz_token_ttl_s: float = 60.0
     authz_sar_ttl_s: float = 30.0      # the same for SubjectAccessReview answers
     # a token seen for the first time: its TokenReview and a SelfSubjectAccessReview made with
-    # the caller's own token go out together (one round trip instead of two; falls back to a
-    # SubjectAccessReview where the self-review is not served). Only when the master itself
-    # talks to the apiserver with a bearer token: with a client certificate the apiserver
-    # would review the master
-    authz_self_review: bool = True
+    # the caller's own token go out together (one round trip instead of two where the
+    # apiserver's round trip is network-bound; falls back to a SubjectAccessReview where the
+    # self-review is not served). Off by default: against the single-process fake apiserver
+    # the two concurrent reviews cost 0.2 ms more than two serial ones (profiles/r5_cold/).
+    # Only when the master talks to the apiserver with a bearer token: with a client
+    # certificate the apiserver would review the master
+    authz_self_review: bool = False
     # the master keeps a slim list+watch index of every Pod (name → uid, node, phase) so an
     # attach needs no Pod GET; off: a GET on a miss, answers cached for 30 s
     master_pod_index: bool = True

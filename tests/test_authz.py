@@ -5,9 +5,10 @@ import asyncio
 from gpumounter_amd.fakes.harness import LocalCluster
 
 
-def run(body):
+def run(body, self_review=True):
     async def main():
-        async with LocalCluster(master_overrides={"authz_mode": "kube"}) as lc:
+        async with LocalCluster(master_overrides={"authz_mode": "kube",
+                                                  "authz_self_review": self_review}) as lc:
             c = lc.cluster
             c.add_user("tok-alice", "alice", groups=["team-a"])
             c.add_user("tok-bob", "bob")

@@ -14,9 +14,11 @@ invariants after *every* step:
 * a lease that ended more than ``SLACK`` seconds ago no longer holds its GPU.
 
 Rules: attach (single or entire mount, with or without a lease), detach, force-remove, let
-time pass (leases end), a container restart, a watch relist (410 Gone), a worker restart, and
-a lost or failed reply on the next POST / PATCH / DELETE. Variants: the device-plugin ledger,
-the warm pool, DRA with a warm pool, trim placement with a warm pool.
+time pass (leases end), a container restart, a watch relist (410 Gone), the kubelet's status
+churn on every placeholder, a worker restart, an attach or detach with one of those events in
+flight (and a container restart that only a relist carries), and a lost or failed reply on the
+next one or two of POST / PATCH / DELETE / GET. Variants: the device-plugin ledger, the warm
+pool, DRA with a warm pool, trim placement with a warm pool.
 
 The reference has no locking and no recovery at all (pkg/server/gpu-mount/server.go:34-179,
 SURVEY defect 7). Round-4 bug parents this model fails on: ``bench/model_parents.sh``
@@ -207,15 +209,16 @@ class LedgerModel(RuleBasedStateMachine):
             for u in uuids:
                 self.leases[t].pop(u, None)
 
+    EVENTS = st.sampled_from(["container restart", "relist", "restart in relist",
+                              "status churn", "worker restart"])
+
     @rule(t=st.sampled_from(TENANTS), n=st.integers(1, 2), entire=st.booleans(),
-          event=st.sampled_from(["container restart", "relist", "worker restart"]),
-          delay=st.sampled_from([0.0, 0.001, 0.003]))
+          event=EVENTS, delay=st.sampled_from([0.0, 0.001, 0.003]))
     def attach_racing(self, t, n, entire, event, delay):
         """An attach with a container restart, a relist or a worker restart in flight."""
         self._attach(t, n, entire, 0.0, (event, t), delay)
 
-    @rule(t=st.sampled_from(TENANTS), picks=PICKS,
-          event=st.sampled_from(["container restart", "relist", "worker restart"]),
+    @rule(t=st.sampled_from(TENANTS), picks=PICKS, event=EVENTS,
           delay=st.sampled_from([0.0, 0.001, 0.003]))
     def detach_racing(self, t, picks, event, delay):
         self._detach(t, False, picks, (event, t), delay)
@@ -229,9 +232,12 @@ class LedgerModel(RuleBasedStateMachine):
         if what == "container restart":
             self.lc.cluster.restart_container("default", t, "main")
         elif what == "relist":
-            expire = getattr(self.lc.cluster, "expire_watches", None)
-            if expire is not None:
-                expire()
+            self._expire()
+        elif what == "restart in relist":     # the restart reaches the worker only by the relist
+            self._expire()
+            self.lc.cluster.restart_container("default", t, "main")
+        elif what == "status churn":
+            self._churn()
         else:
             await self.lc.stop_worker("node-0")
             w = await self.lc.start_worker("node-0")
@@ -254,11 +260,30 @@ class LedgerModel(RuleBasedStateMachine):
 
     @rule()
     def watch_relist(self):
-        expire = getattr(self.lc.cluster, "expire_watches", None)
-        if expire is None:             # an older fake without the hook
-            return
         self.steps.append("watches expire (410): relist")
-        self.tc.call(_sync(expire))
+        self.tc.call(_sync(self._expire))
+
+    @rule()
+    def status_churn(self):
+        """The kubelet updates every placeholder's status (a new resourceVersion each)."""
+        self.steps.append("placeholder status churn")
+        self.tc.call(_sync(self._churn))
+
+    def _expire(self) -> None:
+        expire = getattr(self.lc.cluster, "expire_watches", None)
+        if expire is not None:         # an older fake without the hook: no relist
+            expire()
+
+    def _churn(self) -> None:
+        c = self.lc.cluster
+        for p in c.placeholders():
+            pod = c.pods.get((p["metadata"]["namespace"], p["metadata"]["name"]))
+            if pod is None:
+                continue
+            conds = pod.setdefault("status", {}).setdefault("conditions", [])
+            conds[:] = [x for x in conds if x.get("type") != "GMChurn"] + [
+                {"type": "GMChurn", "status": "True", "lastProbeTime": repr(time.time())}]
+            c._bump("MODIFIED", pod)                               # noqa: SLF001
 
     @rule()
     def worker_restart(self):
@@ -268,12 +293,14 @@ class LedgerModel(RuleBasedStateMachine):
         target = f"127.0.0.1:{w.grpc_port}"
         self._until(lambda: self.lc.master.workers.target("node-0") == target, 10)
 
-    @rule(method=st.sampled_from(["POST", "PATCH", "DELETE"]), after=st.booleans())
-    def lost_reply(self, method, after):
-        """The next {method} on a pod fails: before it takes effect, or after it (the reply is
-        lost). Whatever the next operation is, it must converge."""
-        self.steps.append(f"next {method} fails {'after' if after else 'before'} applying")
-        self.tc.call(_sync(self.lc.cluster.fail_next, method, 503, 1, after))
+    @rule(faults=st.lists(st.tuples(st.sampled_from(["POST", "PATCH", "DELETE", "GET"]),
+                                    st.booleans()), min_size=1, max_size=2))
+    def lost_reply(self, faults):
+        """The next request with each method on a pod fails: before it takes effect, or after
+        it (the reply is lost). Whatever the next operations are, they must converge."""
+        for method, after in faults:
+            self.steps.append(f"next {method} fails {'after' if after else 'before'} applying")
+            self.tc.call(_sync(self.lc.cluster.fail_next, method, 503, 1, after))
 
     # ------------------------------------------------------------------------ invariants
     async def _view(self):
