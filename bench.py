@@ -231,7 +231,8 @@ def main() -> int:
                     help="dra: the node's GPUs come from a DRA driver; placeholders hold "
                          "ResourceClaims (gpu_allocation=dra)")
     args = ap.parse_args()
-    if args.amdsmi == "mock" and os.path.exists("/dev/kfd"):
+    # the amdgpu driver's KFD topology, not a /dev/kfd node (which any test or tool can mknod)
+    if args.amdsmi == "mock" and os.path.isdir("/sys/class/kfd/kfd/topology/nodes"):
         # on a GPU box the mock inventory's GPUs are not the box's: the control plane is
         # measured alone (without a GPU the rank check still runs, on gloo)
         args.no_verify = True

@@ -1,4 +1,5 @@
-"""Minimal async Kubernetes REST client (pods + watch) on aiohttp.
+"""Minimal async Kubernetes REST client (pods + watch) on a lean HTTP/1.1 client
+(``cluster/http1.py``).
 
 Reference: client-go clientset singleton, always in-cluster, panicking on error, with a
 placeholder out-of-cluster kubeconfig path (reference: pkg/config/config.go:11-45). Only
@@ -17,14 +18,14 @@ import ssl
 import tempfile
 from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
 
-import aiohttp
 import yaml
 
+from gpumounter_amd.cluster import http1
 from gpumounter_amd.utils import calls, log
 
 _log = log.get("kube")
 _RESOURCES = {"pods", "events", "resourceclaims", "resourceslices", "resourcequotas",
-              "tokenreviews", "subjectaccessreviews", "nodes"}
+              "tokenreviews", "subjectaccessreviews", "selfsubjectaccessreviews", "nodes"}
 
 
 def _kind(method: str, path: str) -> str:
@@ -59,7 +60,7 @@ class KubeClient:
                  timeout_s: float = 30.0) -> None:
         self.base = base_url.rstrip("/")
         self.token = token
-        self.timeout = aiohttp.ClientTimeout(total=timeout_s)
+        self.timeout_s = timeout_s
         self._ssl: Any = None
         if self.base.startswith("https"):
             if insecure:
@@ -69,8 +70,8 @@ class KubeClient:
                 if client_cert:
                     ctx.load_cert_chain(*client_cert)
                 self._ssl = ctx
-        self._session: Optional[aiohttp.ClientSession] = None
-        self._session_loop = None
+        self._pool: Optional[http1.Pool] = None
+        self._pool_loop = None
         # a request may carry another bearer token (a self-review as the caller) only when the
         # apiserver authenticates this client by its token, not by a TLS client certificate
         self.bearer_only = client_cert is None
@@ -125,26 +126,23 @@ class KubeClient:
                    insecure=bool(cluster.get("insecure-skip-tls-verify")))
 
     # ------------------------------------------------------------------------- plumbing
-    def _sess(self) -> aiohttp.ClientSession:
+    def _http(self) -> http1.Pool:
         loop = asyncio.get_running_loop()
-        if self._session is None or self._session.closed or self._session_loop is not loop:
+        if self._pool is None or self._pool_loop is not loop:
             headers = {"Accept": "application/json"}
             if self.token:
                 headers["Authorization"] = f"Bearer {self.token}"
-            # idle keep-alive connections live a minute (aiohttp: 15 s), so requests a minute
-            # apart (an operator's attaches, the reviews of an expired authz answer) connect
-            # nothing
-            conn = aiohttp.TCPConnector(limit=64, keepalive_timeout=60.0,
-                                        ssl=self._ssl if self._ssl is not None else None)
-            self._session = aiohttp.ClientSession(headers=headers, connector=conn,
-                                                  timeout=self.timeout)
-            self._session_loop = loop
-        return self._session
+            # idle keep-alive connections live a minute, so requests a minute apart (an
+            # operator's attaches, the reviews of an expired authz answer) connect nothing
+            self._pool = http1.Pool(self.base, self._ssl, headers, keepalive_s=60.0,
+                                    timeout_s=self.timeout_s)
+            self._pool_loop = loop
+        return self._pool
 
     async def close(self) -> None:
-        if self._session is not None and not self._session.closed:
-            await self._session.close()
-        self._session = None
+        if self._pool is not None:
+            await self._pool.close()
+        self._pool = None
 
     # transient apiserver trouble (a control-plane node restarting, an overloaded apiserver
     # shedding load with 429/5xx): retried with backoff for requests that are safe to repeat
@@ -168,7 +166,7 @@ class KubeClient:
                 if e.status not in self.RETRY_STATUS or attempt == len(delays):
                     raise
                 why = f"HTTP {e.status}"
-            except (aiohttp.ClientError, asyncio.TimeoutError, OSError) as e:
+            except (asyncio.TimeoutError, OSError) as e:
                 if attempt == len(delays):
                     raise ApiError(503, f"apiserver unreachable: {e!r}") from e
                 why = repr(e)
@@ -180,31 +178,28 @@ class KubeClient:
 
     async def _req_once(self, method: str, path: str, params: Optional[dict], body: Any,
                         content_type: str, as_token: str = "") -> Any:
-        sess = self._sess()
+        pool = self._http()
         data = None
         headers = {"Authorization": f"Bearer {as_token}"} if as_token else {}
         if body is not None:
-            data = json.dumps(body)
+            data = json.dumps(body).encode()
             headers["Content-Type"] = content_type
         with calls.span(_kind(method, path)):
-            return await self._send(sess, method, path, params, data, headers)
-
-    async def _send(self, sess, method: str, path: str, params, data, headers) -> Any:
-        async with sess.request(method, self.base + path, params=params, data=data,
-                                headers=headers) as resp:
-            text = await resp.text()
-            if resp.status >= 400:
-                try:
-                    payload = json.loads(text)
-                except ValueError:
-                    payload = text
-                reason = payload.get("message", text) if isinstance(payload, dict) else text
-                if resp.status == 404:
-                    raise NotFound(404, reason, payload)
-                if resp.status == 409:
-                    raise Conflict(409, reason, payload)
-                raise ApiError(resp.status, reason, payload)
-            return json.loads(text) if text else None
+            status, _, raw = await pool.request(method, pool.target(path, params),
+                                                headers or None, data)
+        if status >= 400:
+            text = raw.decode("utf-8", "replace")
+            try:
+                payload = json.loads(text)
+            except ValueError:
+                payload = text
+            reason = payload.get("message", text) if isinstance(payload, dict) else text
+            if status == 404:
+                raise NotFound(404, reason, payload)
+            if status == 409:
+                raise Conflict(409, reason, payload)
+            raise ApiError(status, reason, payload)
+        return json.loads(raw) if raw else None
 
     @staticmethod
     def _pods_path(ns: Optional[str], name: str = "") -> str:
@@ -381,18 +376,15 @@ class KubeClient:
             params["fieldSelector"] = field_selector
         if resource_version:
             params["resourceVersion"] = resource_version
-        sess = self._sess()
-        async with sess.get(self.base + path, params=params,
-                            timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30)
-                            ) as resp:
-            if resp.status >= 400:
-                raise ApiError(resp.status, await resp.text())
-            buf = b""
-            async for chunk in resp.content.iter_any():
-                buf += chunk
-                while b"\n" in buf:
-                    line, buf = buf.split(b"\n", 1)
-                    if not line.strip():
-                        continue
-                    ev = json.loads(line)
-                    yield ev.get("type", ""), ev.get("object", {})
+        pool = self._http()
+        status, _, lines = await pool.stream("GET", pool.target(path, params),
+                                             read_timeout_s=timeout_s + 30)
+        try:
+            if status >= 400:
+                raise ApiError(status, b"\n".join([ln async for ln in lines]).decode(
+                    "utf-8", "replace"))
+            async for line in lines:
+                ev = json.loads(line)
+                yield ev.get("type", ""), ev.get("object", {})
+        finally:
+            lines.close()

@@ -90,6 +90,30 @@ class DevNodeWriter:
             arr[i].uid, arr[i].gid = owner
         return arr
 
+    # ------------------------------------------------------------------ which process
+    def _mntns(self, pid) -> Optional[str]:
+        try:
+            return os.readlink(f"{self.proc_root}/{pid}/ns/mnt")
+        except OSError:
+            return None
+
+    def root_pid(self, pids: Sequence[int]) -> int:
+        """The process whose ``/proc/<pid>/root`` is the container's filesystem: the first of
+        the cgroup's ``pids`` in a mount namespace other than this worker's. A process that was
+        moved into the container's cgroup from outside it (a debugging tool, ``nsenter`` without
+        ``-m``, a test probe) shares the worker's mount namespace, and its root is the worker's
+        own: device nodes written through it would land in the worker's (or the host's) /dev.
+        0 when there is no such process (the caller reports "no process to resolve its root
+        from"). The reference always used the first PID of the cgroup (pkg/util/util.go:152)."""
+        if self.mode == "emulate":
+            return pids[0] if pids else 0
+        own = self._mntns("self")
+        for pid in pids:
+            ns = self._mntns(pid)
+            if ns is not None and ns != own:
+                return pid
+        return 0
+
     # ------------------------------------------------------------------ user-namespaced targets
     def _userns_id(self, pid) -> Optional[Tuple[int, int]]:
         try:

@@ -122,7 +122,7 @@ class HotMount:
             if self.cfg.container_root_prefix:
                 t = Target(root=os.path.join(self.cfg.container_root_prefix, r.id))
             else:
-                t = Target(pid=pids[0] if pids else 0)
+                t = Target(pid=self.writer.root_pid(pids))
             out.append(ContainerTarget(r, cgdir, t, pids))
         return out
 

@@ -455,3 +455,23 @@ def test_caller_going_away_mid_attach_does_not_leave_half_an_attach():
         assert all(p["spec"].get("nodeName") for p in lc.cluster.placeholders())
         assert not await lc.audit("default", "t")
     run(body, latency=LatencyModel(schedule_ms=100.0, admit_ms=100.0))
+
+
+def test_device_nodes_go_through_a_process_of_the_container_not_one_moved_in_from_outside(
+        tmp_path):
+    """The cgroup of a container can hold a process that was moved in from outside it (a debug
+    tool, nsenter without -m, a test probe writing its PID to cgroup.procs). Its /proc/<pid>/root
+    is the worker's own root: nodes written through it landed in the worker's /dev. The writer
+    takes the first process in another mount namespace, and none at all when there is none."""
+    from gpumounter_amd.node.devnodes import DevNodeWriter
+    proc = tmp_path / "proc"
+    for pid, ns in (("self", "mnt:[4026531840]"), ("100", "mnt:[4026531840]"),
+                    ("200", "mnt:[4026532999]"), ("300", "mnt:[4026532999]")):
+        (proc / pid / "ns").mkdir(parents=True)
+        os.symlink(ns, proc / pid / "ns" / "mnt")
+    w = DevNodeWriter("procroot", proc_root=str(proc))
+    assert w.root_pid([100, 200, 300]) == 200      # 100 shares the worker's mount namespace
+    assert w.root_pid([300]) == 300
+    assert w.root_pid([100]) == 0                  # only an outsider: no root to write through
+    assert w.root_pid([999, 200]) == 200           # exited meanwhile: skipped
+    assert DevNodeWriter("emulate", proc_root=str(proc)).root_pid([100, 200]) == 100

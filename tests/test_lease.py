@@ -320,6 +320,10 @@ def test_a_pool_placeholder_reclaimed_by_the_same_pod_does_not_inherit_its_old_l
         code, a = await lease_add(lc, "default", "a", 1, 0.4)
         assert code == 200
         ph, idx = a["devices"][0]["placeholder"], a["devices"][0]["index"]
+        for _ in range(250):        # the refill after the claim is done: room for one give-back
+            if len(pool.standby()) == 1 and not pool.refilling():
+                break
+            await asyncio.sleep(0.02)
         pool.target = 2
         code, _ = await lc.remove("default", "a", [a["devices"][0]["uuid"]])
         assert code == 200
