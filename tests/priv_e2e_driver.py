@@ -61,6 +61,22 @@ def prog_names(cg):
     return out
 
 
+HOST_PATHS = ("/dev/kfd", "/dev/dri/renderD5", "/dev/dri/card7")
+
+
+def host_dev_state():
+    """The worker's own /dev entries the tenant's nodes would be named like: whether each
+    exists and which inode it is (compared before and after, not assumed absent)."""
+    out = {}
+    for p in HOST_PATHS:
+        try:
+            st = os.lstat(p)
+            out[p] = [st.st_ino, st.st_ctime_ns]
+        except FileNotFoundError:
+            out[p] = None
+    return out
+
+
 def chr_node(pid, rel):
     try:
         st = os.stat(f"/proc/{pid}/root{rel}")
@@ -78,6 +94,7 @@ async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0, userns_pid
                                               "devnode_stage_dir": stage,
                                               "device_guard_period_s": float(os.environ.get("GM_TEST_GUARD", "1.0"))}) as lc:
         w = lc.nodes["node-0"].worker
+        host_before = host_dev_state()
         obs["backend"] = w.backend.name
         lc.tenant("t", pids={"main": [tenant_pid]})
         node = lc.nodes["node-0"].node
@@ -92,7 +109,7 @@ async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0, userns_pid
         obs["progs_after_add1"] = prog_names(cg)
         obs["nodes_after_add1"] = {p: chr_node(tenant_pid, p) for p in
                                    ("/dev/kfd", "/dev/dri/renderD5", "/dev/dri/card7")}
-        obs["host_dev_untouched"] = not os.path.exists("/dev/dri/renderD5")
+        obs["host_dev_untouched"] = host_dev_state() == host_before
         obs["audit_after_add1"] = [i.kind for i in await lc.audit("default", "t")]
         code, b2 = await lc.add("default", "t", 1)
         obs["add2"] = [code, [d["bdf"] for d in b2.get("devices", [])]]
@@ -115,6 +132,7 @@ async def flow(mnt, bpffs, tenant_pid, obs, hostdev="", shared_pid=0, userns_pid
             await shared_dev_flow(lc, hostdev, shared_pid, obs)
         if userns_pid:
             await userns_flow(lc, userns_pid, obs)
+        obs["host_dev_untouched_at_end"] = host_dev_state() == host_before
 
 
 async def guard_flow(lc, cg, obs):

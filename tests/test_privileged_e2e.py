@@ -36,6 +36,9 @@ def test_full_stack_attach_detach_enforced_by_the_kernel(tmp_path):
     assert o["nodes_after_add1"] == {"/dev/kfd": [1, 0], "/dev/dri/renderD5": [1, 5],
                                      "/dev/dri/card7": [1, 7]}
     assert o["host_dev_untouched"] and o["audit_after_add1"] == []
+    # the probes join the tenant's cgroup from the worker's mount namespace: the worker
+    # writes nodes only through the tenant's own process, never into its own /dev
+    assert o["host_dev_untouched_at_end"]
     assert o["add2"][0] == 200 and o["after_add2"] == "1111"
     assert o["remove1"] == 200 and o["after_remove1"] == "1001"
     assert o["nodes_after_remove1"] == {"/dev/kfd": [1, 0], "/dev/dri/renderD5": None,
