@@ -114,11 +114,16 @@ class InjectionJournal:
                 pass
             return
         tmp = path + ".tmp"
-        # dumps (the C encoder) + one write: json.dump streams through the pure-Python
-        # encoder, which cost more than the rest of a journal update on the attach path
-        blob = json.dumps(e.to_json(), separators=(",", ":"))
-        with open(tmp, "w", encoding="utf-8") as fh:
-            fh.write(blob)
+        # dumps (the C encoder) + one write(2): json.dump streams through the pure-Python
+        # encoder, and a text file object costs more than the write itself on the attach path
+        blob = json.dumps(e.to_json(), separators=(",", ":")).encode()
+        fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | os.O_CLOEXEC, 0o600)
+        try:
+            view = memoryview(blob)
+            while view:
+                view = view[os.write(fd, view):]
+        finally:
+            os.close(fd)
         os.replace(tmp, path)
 
     # ------------------------------------------------------------------------ queries
