@@ -28,9 +28,9 @@ from gpumounter_amd.cluster.informer import PodInformer, SlimPodInformer
 from gpumounter_amd.cluster.kube import ApiError, KubeClient, NotFound
 from gpumounter_amd.cluster.placeholder import LABEL_NODE
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.master import httpd
+from gpumounter_amd.utils import httpd
 from gpumounter_amd.master.authz import Authorizer
-from gpumounter_amd.master.httpd import Request, Response
+from gpumounter_amd.utils.httpd import Request, Response
 from gpumounter_amd.utils import calls, log, runtime, trace
 from gpumounter_amd.utils.metrics import Metrics
 

@@ -33,7 +33,7 @@ from multidict import CIMultiDict, MultiDict
 
 from gpumounter_amd.utils import log
 
-_log = log.get("master.httpd")
+_log = log.get("httpd")
 
 MAX_HEAD = 16 << 10
 MAX_BODY = 10 << 20

@@ -17,7 +17,6 @@ import time
 from typing import Optional
 
 import grpc
-from aiohttp import web
 
 from gpumounter_amd.api import gpu_mount as api
 from gpumounter_amd.api import wire
@@ -34,7 +33,7 @@ from gpumounter_amd.node.dra import DraLedger
 from gpumounter_amd.node.hotmount import HotMount
 from gpumounter_amd.node.journal import InjectionJournal
 from gpumounter_amd.node.ledger import LedgerClient
-from gpumounter_amd.utils import calls, log, runtime
+from gpumounter_amd.utils import calls, httpd, log, runtime
 from gpumounter_amd.utils.faults import FaultInjector
 from gpumounter_amd.utils.metrics import Metrics
 from gpumounter_amd.worker.reconciler import Reconciler
@@ -147,7 +146,7 @@ class Worker:
         self.wire_server: Optional[wire.WireServer] = None
         self.wire_port = 0
         self._ops: set = set()          # RPC operations running (see run_op)
-        self.http_runner: Optional[web.AppRunner] = None
+        self.http: Optional[httpd.HttpServer] = None
         self.grpc_port = 0
         self.http_port = 0
         self.ready = False
@@ -347,20 +346,17 @@ class Worker:
                 raise OSError(f"cannot bind gm-wire {self.cfg.worker_host}:{wp}: {e}") from e
         hp = self.cfg.metrics_port if http_port is None else http_port
         if hp is not None and hp >= 0:
-            app = web.Application()
-            app.router.add_get("/healthz", self._healthz)
-            app.router.add_get("/readyz", self._readyz)
-            app.router.add_get("/metrics", self._metrics)
-            app.router.add_get("/status", self._http_status)
-            app.router.add_get("/audit/{namespace}/{pod}", self._http_audit)
+            r = httpd.Router()
+            r.add_get("/healthz", self._healthz)
+            r.add_get("/readyz", self._readyz)
+            r.add_get("/metrics", self._metrics)
+            r.add_get("/status", self._http_status)
+            r.add_get("/audit/{namespace}/{pod}", self._http_audit)
             if self.cfg.debug_endpoints:    # stacks of every task: not for the open port
-                app.router.add_get("/debug/tasks", self._debug_tasks)
-                app.router.add_get("/debug/calls", self._debug_calls)
-            self.http_runner = web.AppRunner(app, access_log=None)
-            await self.http_runner.setup()
-            site = web.TCPSite(self.http_runner, self.cfg.worker_host, hp)
-            await site.start()
-            self.http_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+                r.add_get("/debug/tasks", self._debug_tasks)
+                r.add_get("/debug/calls", self._debug_calls)
+            self.http = httpd.HttpServer(r)
+            self.http_port = await self.http.start(self.cfg.worker_host, hp)
         if reconcile and self.cfg.reconcile_period_s > 0:
             await self.reconciler.start()
         else:
@@ -392,10 +388,11 @@ class Worker:
                   self.backend.name, self.cfg.devnode_mode, self.ledger.api_version)
 
     async def _healthz(self, request):
-        return web.Response(text="ok")
+        return httpd.text("ok")
 
     async def _metrics(self, request):
-        return web.Response(body=self.metrics.render(), content_type="text/plain")
+        return httpd.Response(self.metrics.render(), 200,
+                              "text/plain; version=0.0.4; charset=utf-8")
 
     async def _debug_tasks(self, request):
         """Every asyncio task of the worker with the stack it is suspended in — what a stuck
@@ -405,20 +402,19 @@ class Worker:
             out.append(f"{t.get_name()} {t.get_coro()!r}")
             for f in t.get_stack():
                 out.append(f"    {f.f_code.co_filename}:{f.f_lineno} {f.f_code.co_name}")
-        return web.Response(text="\n".join(out) + "\n")
+        return httpd.text("\n".join(out) + "\n")
 
     async def _debug_calls(self, request):
         """Outbound control-plane calls that started in [since, until] (monotonic seconds):
         utils/calls.py, for the bench's per-operation call accounting."""
-        return web.json_response(_calls_window(request.query))
+        return httpd.json_response(_calls_window(request.query))
 
     async def _readyz(self, request):
-        return web.Response(text="ready" if self.ready else "starting",
-                            status=200 if self.ready else 503)
+        return httpd.text("ready" if self.ready else "starting", 200 if self.ready else 503)
 
     async def _http_status(self, request):
         st = await self.service.node_status(request.query.get("processes") == "1")
-        return web.json_response(st)
+        return httpd.json_response(st)
 
     async def _http_audit(self, request):
         """Ledger-vs-node consistency of one pod: [] when its cgroup rules and device nodes are
@@ -426,10 +422,10 @@ class Worker:
         ns, name = request.match_info["namespace"], request.match_info["pod"]
         pod = await self.service.get_pod(ns, name, fresh=True)
         if pod is None:
-            return web.json_response({"error": "pod not found"}, status=404)
+            return httpd.json_response({"error": "pod not found"}, status=404)
         st = await self.service.pod_state(pod, fresh=True)
         issues = self.service.hm.audit(pod, st.hot, st.own)
-        return web.json_response({"pod": f"{ns}/{name}", "consistent": not issues,
+        return httpd.json_response({"pod": f"{ns}/{name}", "consistent": not issues,
                                   "issues": [vars(i) for i in issues]})
 
     async def check_health(self) -> None:
@@ -511,8 +507,8 @@ class Worker:
             self.backend.sync.stop()
         if self.plugin is not None:
             await self.plugin.stop()
-        if self.http_runner is not None:
-            await self.http_runner.cleanup()
+        if self.http is not None:
+            await self.http.stop()
         await self.ph_informer.stop()
         await self.node_informer.stop()
         if self.claim_informer is not None:

@@ -1,10 +1,10 @@
-"""The master's HTTP/1.1 server (master/httpd.py): framing, persistence, routing answers as
-httprouter gives them (reference: cmd/GPUMounter-master/main.go:227-246), Go ParseForm bodies."""
+"""The HTTP/1.1 server of the master and the worker (utils/httpd.py): framing, persistence,
+routing answers as httprouter gives them (reference: cmd/GPUMounter-master/main.go:227-246), Go ParseForm bodies."""
 import asyncio
 
 import pytest
 
-from gpumounter_amd.master import httpd
+from gpumounter_amd.utils import httpd
 
 
 def _server():
