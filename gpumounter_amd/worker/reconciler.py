@@ -77,6 +77,8 @@ class ReconcileReport:
     errors: List[str] = field(default_factory=list)
     claims_deleted: List[str] = field(default_factory=list)   # DRA mode: orphan claims
     drained: List[str] = field(default_factory=list)   # draining placeholders released
+    # owners an attach/detach held locked: audited by a follow-up, swept again soon
+    skipped: List[str] = field(default_factory=list)
 
     def to_dict(self) -> dict:
         return self.__dict__.copy()
@@ -394,6 +396,10 @@ class Reconciler:
     # a sweep that could not finish everything (the kubelet restarting, the apiserver failing, a
     # kernel call refused) runs again after these delays rather than a whole period later
     SWEEP_RETRY_DELAYS = (0.5, 2.0, 5.0, 10.0)
+    # a sweep that skipped an owner an operation held sweeps again this soon (found by chaos:
+    # a restarted worker's first sweep skipped the owner its lease expiry held, and that
+    # owner's placeholders from the dead worker's last attach stayed unbound for a period)
+    SKIPPED_RESWEEP_S = 2.0
     # woken sweeps (relists) run at most this often: a flapping watch must not turn into a
     # PodResources List per relist
     WAKE_MIN_INTERVAL_S = 1.0
@@ -418,8 +424,10 @@ class Reconciler:
                     pass
             self._wake.clear()
             self._last_sweep = loop.time()
+            skipped = False
             try:
-                ok = not (await self.run_once()).errors
+                rep = await self.run_once()
+                ok, skipped = not rep.errors, bool(rep.skipped)
             except asyncio.CancelledError:
                 if self._stopping:
                     raise
@@ -432,6 +440,8 @@ class Reconciler:
                 ok = False
             if ok:
                 delay, failures = self.period_s, 0
+                if skipped:
+                    delay = min(self.period_s, self.SKIPPED_RESWEEP_S)
             else:
                 delay = min(self.period_s, self.SWEEP_RETRY_DELAYS[
                     min(failures, len(self.SWEEP_RETRY_DELAYS) - 1)])
@@ -552,8 +562,11 @@ class Reconciler:
             if lock.locked():
                 # an attach/detach is in flight for this owner: audit it right after, not a
                 # period later (the events this sweep stands in for, a container restart
-                # missed by a relist, say, will not come again)
+                # missed by a relist, say, will not come again); its placeholders (a dead
+                # worker's unadmitted ones, a failed pick's) wait for the next sweep, which
+                # comes SKIPPED_RESWEEP_S later instead of a period
                 self.follow_up(ons, oname)
+                rep.skipped.append(f"{ons}/{oname}")
                 continue
             async with lock:
                 # the snapshot above is older than this lock: an attach that held it meanwhile
@@ -637,6 +650,7 @@ class Reconciler:
             lock = svc.pod_lock(*key)
             if lock.locked():
                 self.follow_up(*key)        # as above: once the operation in flight is done
+                rep.skipped.append("/".join(key))
                 continue
             async with lock:
                 if svc.ph.owned_by(pod):

@@ -475,3 +475,37 @@ def test_device_nodes_go_through_a_process_of_the_container_not_one_moved_in_fro
     assert w.root_pid([100]) == 0                  # only an outsider: no root to write through
     assert w.root_pid([999, 200]) == 200           # exited meanwhile: skipped
     assert DevNodeWriter("emulate", proc_root=str(proc)).root_pid([100, 200]) == 100
+
+
+def test_a_sweep_that_skipped_a_busy_owner_sweeps_again_soon():
+    """A restarted worker's first sweep skipped the owner its lease expiry held; that owner's
+    placeholders from the dead worker's last attach (never admitted: nothing waits for them)
+    stayed unbound until the next periodic sweep, 30 s later (chaos rpl211). A sweep that
+    skipped an owner now sweeps again SKIPPED_RESWEEP_S later."""
+    from gpumounter_amd.cluster.placeholder import ANN_INCARNATION
+
+    async def body(lc):
+        pod = lc.tenant("t")
+        w = lc.nodes["node-0"].worker
+        svc = w.service
+        body_ = svc.ph.build(pod, 9, "single")        # more GPUs than the node has: Pending
+        body_["metadata"]["annotations"][ANN_INCARNATION] = "a-dead-worker"
+        ph = await svc.kube.create_pod(body_["metadata"]["namespace"], body_)
+        name = ph["metadata"]["name"]
+        for _ in range(200):
+            if any(p["metadata"]["name"] == name for p in svc.ph.owned_by(pod)):
+                break
+            await asyncio.sleep(0.01)
+        async with svc.pod_lock("default", "t"):       # an operation in flight
+            w.reconciler.wake()
+            for _ in range(300):
+                if "default/t" in w.reconciler.last.skipped:
+                    break
+                await asyncio.sleep(0.01)
+            assert "default/t" in w.reconciler.last.skipped
+            assert lc.cluster.get("gpu-pool", name) is not None
+        t0 = asyncio.get_running_loop().time()
+        while lc.cluster.get("gpu-pool", name) is not None:
+            assert asyncio.get_running_loop().time() - t0 < 6, "not released within a re-sweep"
+            await asyncio.sleep(0.05)
+    run(body, reconcile_period_s=30.0)
