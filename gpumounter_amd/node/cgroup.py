@@ -153,21 +153,23 @@ class CgroupResolver:
         """PIDs in the cgroup (and, for v2 container scopes, its sub-cgroups)."""
         lib = _native.host()
         out: List[int] = []
-        dirs = [cgdir]
-        if recursive:
-            for dirpath, dirnames, _ in os.walk(cgdir):
-                for d in dirnames:
-                    dirs.append(os.path.join(dirpath, d))
-        for d in dirs:
+        buf = (C.c_int32 * 4096)()
+        n = C.c_int(0)
+        stack = [cgdir]
+        while stack:
+            d = stack.pop()
             path = os.path.join(d, "cgroup.procs")
-            if not os.path.exists(path):
-                continue
-            buf = (C.c_int32 * 4096)()
-            n = C.c_int(0)
             rc = lib.gm_proc_read_pids(path.encode(), buf, 4096, C.byref(n))
-            if rc < 0:
+            if rc < 0 and rc != -errno.ENOENT:      # ENOENT: not a cgroup directory
                 raise CgroupError(f"read {path}: {os.strerror(-rc)}")
-            out.extend(int(buf[i]) for i in range(min(n.value, 4096)))
+            if rc >= 0:
+                out.extend(buf[:min(n.value, 4096)])
+            if recursive:
+                try:
+                    with os.scandir(d) as it:
+                        stack.extend(e.path for e in it if e.is_dir(follow_symlinks=False))
+                except (FileNotFoundError, NotADirectoryError):
+                    pass
         return sorted(set(out))
 
 

@@ -229,7 +229,9 @@ class Config:
     log_level: str = "INFO"            # DEBUG | INFO | WARNING | ERROR
     log_file: str = ""                 # also log to this file, rotated ("" = stderr only)
     log_json: bool = True              # one JSON object per line, with request ids
-    roctx: bool = True                 # roctx ranges per stage (rocprofv3 --marker-trace)
+    # roctx ranges per stage (rocprofv3 --marker-trace): emitted when a profiler is attached
+    # (its preloaded tool library) or GM_ROCTX=on; without one they are pure cost
+    roctx: bool = True
     fault: str = ""                    # fault injection: "stage:prob[,stage:prob]"
     extra: Dict[str, Any] = field(default_factory=dict)
 

@@ -10,6 +10,7 @@ when ``librocprofiler-sdk-roctx`` is present — emitted as roctx push/pop range
 from __future__ import annotations
 
 import contextvars
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -22,6 +23,22 @@ _roctx = None  # resolved lazily: native host lib or False
 _sinks: List[Callable[["Span"], None]] = []
 
 
+_names: Dict[str, bytes] = {}     # span name → its encoded roctx range name
+
+
+def _profiled() -> bool:
+    """Ranges are emitted when a profiler is attached (rocprofv3 preloads its tool library
+    and exports ROCPROF* variables) or when ``GM_ROCTX=on``; ``GM_ROCTX=off`` never. Without a
+    profiler the two ctypes calls per span are pure cost on the attach path."""
+    mode = os.environ.get("GM_ROCTX", "auto").lower()
+    if mode in ("on", "1", "true"):
+        return True
+    if mode in ("off", "0", "false"):
+        return False
+    return "rocprofiler" in os.environ.get("LD_PRELOAD", "") or \
+        any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+
+
 def _roctx_lib():
     global _roctx
     if _roctx is None:
@@ -31,7 +48,7 @@ def _roctx_lib():
                     from gpumounter_amd import _native
 
                     lib = _native.host()
-                    _roctx = lib if lib.gm_roctx_available() else False
+                    _roctx = lib if _profiled() and lib.gm_roctx_available() else False
                 except Exception:  # noqa: BLE001 - tracing must never break the data path
                     _roctx = False
     return _roctx or None
@@ -102,7 +119,10 @@ class span:
         if self._lib is not None:
             # start/stop ranges, not push/pop: spans of concurrent asyncio tasks interleave on
             # one thread, which a per-thread range stack would mis-nest
-            self._rid = self._lib.gm_roctx_start(f"gm:{self.s.name}".encode())
+            name = _names.get(self.s.name)
+            if name is None:
+                name = _names[self.s.name] = f"gm:{self.s.name}".encode()
+            self._rid = self._lib.gm_roctx_start(name)
         self.s.start_ns = time.perf_counter_ns()
         return self.s
 
