@@ -44,6 +44,7 @@ class FakeApi:
         self.pods = {}                                 # uid → {"gpus": [...], "candidate": bool}
         self.policy = policy
         self.schedule = list(schedule)
+        self.stages = []           # stage faults around a release (FakePH.release)
         self.seq = 0
         self.calls = []
 
@@ -112,6 +113,12 @@ class FakePH:
         self.keep_picked = PlaceholderManager.keep_picked
 
     async def release(self, phs):
+        # the worker's stage fault around a release (faults "ledger_release"), as chaos injects
+        # it: before any DELETE, or after every DELETE took effect
+        stage = self.api.stages.pop(0) if self.api.stages else "ok"
+        self.api.calls.append(("RELEASE", stage))
+        if stage == "before":
+            raise InjectedFault("injected fault at ledger_release (raise)")
         failed = []
         for p in phs:
             err = self.api.delete(p.uid)
@@ -121,6 +128,8 @@ class FakePH:
                 self.device_ids.pop(p.uid, None)
         if failed:
             raise ReserveError(f"could not delete {len(failed)} placeholder(s)")
+        if stage == "after":
+            raise InjectedFault("injected fault at ledger_release (after)")
 
     async def hold_singles(self, owner, width, entire, group="", attach_id="", container="",
                            idempotency_key="", lease_expires=0.0):
@@ -211,11 +220,13 @@ def inv(mock_inventory):
 @given(taken=s.lists(s.integers(0, 7), max_size=6, unique=True),
        n=s.sampled_from([1, 2, 3, 4]), entire=s.booleans(),
        policy=s.sampled_from(["first-free", "last-free", "rot1", "rot2", "rot3", "rot5"]),
-       schedule=s.lists(s.sampled_from(["ok", "ok", "before", "after"]), max_size=14))
-@example(**SCENARIO)
+       schedule=s.lists(s.sampled_from(["ok", "ok", "before", "after"]), max_size=14),
+       stages=s.lists(s.sampled_from(["ok", "ok", "before", "after"]), max_size=4))
+@example(**SCENARIO, stages=[])
 def test_correction_never_mounts_an_unbooked_gpu_and_leaks_nothing(inv, taken, n, entire,
-                                                                  policy, schedule):
+                                                                  policy, schedule, stages):
     api = FakeApi(inv, taken, policy, schedule)
+    api.stages = list(stages)
     assume(len(api.gpus) - len(taken) > n)         # else no other free GPU: nothing to correct
     svc = make_service(inv, api)
     # the plugin's admission of the attach itself (no faults: the correction's input)
@@ -240,6 +251,13 @@ def test_correction_never_mounts_an_unbooked_gpu_and_leaks_nothing(inv, taken, n
     if out is not None:
         check_booked(api, out, n)
         assert not {p.uid for p in out.placeholders} & set(svc.abandoned)
+    # until the follow-up has run, the owner's ledger view counts every live placeholder that
+    # is neither a candidate nor handed over as abandoned: nothing beyond the answer may be one
+    mine_now = {p.uid for p in out.placeholders} if out is not None else set()
+    counted = [u for u, p in api.pods.items()
+               if u not in mine_now and not p["candidate"] and u not in svc.abandoned]
+    assert not counted, ("placeholders the owner's ledger counts beyond the answer",
+                         counted, api.calls)
     follow_up(api, svc)
     mine = {p.uid for p in out.placeholders} if out is not None else set()
     assert set(api.pods) == mine, (api.calls, api.pods, mine)
