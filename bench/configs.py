@@ -348,6 +348,7 @@ def chaos(args) -> dict:
     leases = {t: {} for t in tenants}        # uuid -> (earliest, latest) expiry of its lease
     leased, expired = [0], [0]
     certain = {t: True for t in tenants}
+    resyncs = {t: 0 for t in tenants}   # ledger reads left before a failed tenant is certain
     answered = {t: [] for t in tenants}      # (code, [(placeholder, uuid tail)], lease) per attach
     ok = failed = kills = restarts = master_kills = recreates = kubelet_restarts = 0
     recreated: set = set()
@@ -516,13 +517,18 @@ def chaos(args) -> dict:
                     results = [f.result() for f in futs]
                 for t in recreated:
                     certain[t] = False
+                    resyncs[t] = 2
                 recreated.clear()
                 for t, code in results:
                     codes[code] = codes.get(code, 0) + 1
                     ok += code == 200
                     failed += code not in (200, 400, 403)   # 400/403 are answers, not failures
                     if code not in (200, 400, 403):
+                        # resynchronised from the ledger at this check and the next: a request
+                        # whose master was killed under it goes on in the worker (its operations
+                        # are shielded) and can finish after this round's read of the ledger
                         certain[t] = False
+                        resyncs[t] = 2
                 if args.api_fault_rate:
                     api_faults[0] += pc.api_faults(0)        # the checks read a healthy API
                 t0 = time.perf_counter()
@@ -620,7 +626,8 @@ def chaos(args) -> dict:
                                     x["uuid"] not in leases[t]:
                                 at = time.monotonic() + (exp - time.time())
                                 leases[t][x["uuid"]] = (at, at, x.get("pod_name"))
-                        certain[t] = True
+                        resyncs[t] = resyncs.get(t, 1) - 1
+                        certain[t] = resyncs[t] <= 0
                 if args.api_fault_rate:
                     pc.api_faults(args.api_fault_rate, args.seed * 1000 + rnd_i)
         metrics = pc.worker_metrics()
