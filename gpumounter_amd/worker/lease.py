@@ -60,6 +60,8 @@ class LeaseKeeper:
         # back to the same Pod by a later attach, so a grant holds only for the attach it was
         # made for (see _holder)
         self._granted: Dict[str, Tuple[float, Tuple[str, str]]] = {}
+        # placeholder uid → times its expired lease was found not admitted yet (backoff)
+        self._waits: Dict[str, int] = {}
         self._stopped = False
         self.expired = 0
 
@@ -196,6 +198,8 @@ class LeaseKeeper:
             #                                 back in the warm pool)
         for uid in [u for u in self._retry_after if u not in owners]:
             del self._retry_after[uid]
+        for uid in [u for u in self._waits if u not in owners]:
+            del self._waits[uid]
         for key in [k for k, lk in self._locks.items() if not lk.locked()]:
             del self._locks[key]
         for p in live:
@@ -246,6 +250,17 @@ class LeaseKeeper:
             if exp <= now + 0.001:
                 if now + 0.05 < self._retry_after.get(ph.uid, 0):
                     continue                # busy at its last expiry: its retry timer runs
+                if not st.by_placeholder.get((ph.namespace, ph.name)):
+                    # not admitted yet (a dead worker's attach, a scheduler slower than the
+                    # lease): its GPU comes with admission, and the reconciler mounts it. Looked
+                    # at again shortly (backing off to lease_retry_s) until it holds GPUs or is
+                    # gone, not left to the next periodic sweep
+                    n = self._waits.get(ph.uid, 0)
+                    self._waits[ph.uid] = n + 1
+                    self._arm(ph.uid, ns, name,
+                              now + min(0.1 * 2 ** n, self.svc.cfg.lease_retry_s))
+                    continue
+                self._waits.pop(ph.uid, None)
                 due.append(ph.uid)
                 uuids += [g.uuid for g in st.by_placeholder[(ph.namespace, ph.name)]]
                 t = self._timers.pop(ph.uid, None)

@@ -251,6 +251,40 @@ def test_a_lease_whose_watch_echo_lags_still_expires():
     run(body)                  # LocalCluster runs no periodic sweep
 
 
+def test_a_leased_placeholder_admitted_after_its_lease_timer_fired_still_expires():
+    """A leased attach's placeholder was still Pending (no GPU free: a dead worker's attach, a
+    scheduler slower than the lease) when its lease timer fired: the expiry found nothing to
+    detach. The scheduler admits it later and the reconciler mounts it; its lease is long over,
+    and nothing but the next periodic sweep (30 s) would expire it (chaos tpr241: a GPU held
+    2.6 s past its lease, until the next worker restart)."""
+    async def body(lc):
+        lc.tenant("hog")
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        code, b = await lc.add("default", "hog", 8)
+        assert code == 200, b
+        t = lc.cluster.get("default", "t")
+        ph = svc.ph.build(t, 1, "single", [], "add-dead-worker", "", "", time.time() + 0.2)
+        await svc.kube.create_pod(ph["metadata"]["namespace"], ph)
+        await until(lambda: _seen(svc, ph))
+        await svc.lease.sweep(expire_due=False)      # a restarted worker re-arms its timer
+        await asyncio.sleep(0.5)                     # fired: the placeholder holds no GPU yet
+        code, _ = await lc.remove("default", "hog", [d["uuid"] for d in b["devices"]])
+        assert code == 200
+
+        async def admitted_and_gone():
+            live = [p for p in svc.ph.live()
+                    if p["metadata"]["name"] == ph["metadata"]["name"]]
+            return not live and not (await svc.pod_state(t, fresh=True)).hot
+        assert await until(admitted_and_gone, timeout=3.0), "the late-admitted lease stayed"
+        assert await lc.audit("default", "t") == []
+    run(body)                  # LocalCluster runs no periodic sweep
+
+
+async def _seen(svc, ph):
+    return any(p["metadata"]["name"] == ph["metadata"]["name"] for p in svc.ph.live())
+
+
 def test_a_pool_placeholder_does_not_carry_its_last_owners_lease():
     """Warm pool: a leased GPU removed before its expiry goes back to the pool, and the next Pod
     claims that very placeholder. The earlier owner's lease (the annotation, the grant the
