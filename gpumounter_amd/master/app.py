@@ -766,7 +766,8 @@ class Master:
         uid = podu.uid_of(pod)
         held = {(p["namespace"], p["name"]): p.get("lease_expires")
                 for p in st.get("placeholders", [])
-                if p["owner"] == name and p["owner_namespace"] == ns and p["owner_uid"] == uid}
+                if p["owner"] == name and p["owner_namespace"] == ns and p["owner_uid"] == uid
+                and not p.get("releasing")}
         hot = [dict(g, source="hot-mount",
                     lease_expires=held[(g.get("namespace"), g.get("pod_name"))])
                for g in st["gpus"] if (g.get("namespace"), g.get("pod_name")) in held]

@@ -12,6 +12,7 @@ from typing import Dict
 
 from gpumounter_amd.hw import topology
 from gpumounter_amd.models.device import gpus_by_key, normalize_device_id
+from gpumounter_amd.models.types import ANN_CANDIDATE
 from gpumounter_amd.node.ledger import LedgerError
 from gpumounter_amd.utils import log
 from gpumounter_amd.worker.lease import expires_of
@@ -49,6 +50,11 @@ async def node_status(svc, include_processes: bool) -> dict:
                     "mode": ann.get("gpumounter.amd.com/mount-mode", ""),
                     # a ?lease= attach's end (Unix seconds), None without a lease
                     "lease_expires": expires_of(p),
+                    # not the owner's GPUs (the owner's ledger view, WorkerService.pod_state,
+                    # leaves them out): an unconfirmed trim/correction candidate, a failed
+                    # attach's leftover the follow-up is deleting, a drained one
+                    "releasing": ANN_CANDIDATE in ann or svc.is_abandoned(p) or
+                                 md.get("uid") in svc.drain.unmarked,
                     "device_ids": list(ids)})
     out = {"node": svc.cfg.node_name,
            "gpus": [dict(g.to_dict(), healthy=g.index not in svc.unhealthy) for g in gpus],
@@ -71,7 +77,7 @@ async def node_status(svc, include_processes: bool) -> dict:
     # hot-mounted GPUs per tenant namespace (chargeback: integrate over time in Prometheus)
     per_ns: Dict[str, int] = {}
     for ph in phs:
-        if ph["mode"] != "standby" and ph["owner_namespace"]:
+        if ph["mode"] != "standby" and ph["owner_namespace"] and not ph["releasing"]:
             per_ns[ph["owner_namespace"]] = per_ns.get(ph["owner_namespace"], 0) + \
                 len(ph["device_ids"])
     for ns in set(svc._ns_seen) - set(per_ns):

@@ -339,6 +339,39 @@ def test_the_pod_gpu_view_shows_when_a_lease_ends():
     run(body)
 
 
+def test_the_pod_gpu_view_leaves_out_placeholders_being_released():
+    """A failed attach's leftover that the follow-up is still deleting (chaos v1pl235: a
+    placement correction's held GPU whose release failed) and an unconfirmed candidate are not
+    the Pod's GPUs: the worker's own ledger view leaves them out, and so must the API's."""
+    from gpumounter_amd.models.types import ANN_CANDIDATE
+
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        code, b = await lc.add("default", "t", 3)
+        assert code == 200
+        phs = sorted(svc.ph.owned_by(lc.cluster.get("default", "t")),
+                     key=lambda p: p["metadata"]["name"])
+        assert len(phs) == 3
+        left, cand = phs[0], phs[1]
+        svc.abandoned[left["metadata"]["uid"]] = (
+            left["metadata"]["annotations"]["gpumounter.amd.com/owner-uid"], "")
+        key = (cand["metadata"]["namespace"], cand["metadata"]["name"])
+        await svc.kube.patch_pod(*key, {"metadata": {"annotations": {ANN_CANDIDATE: "add-x"}}})
+
+        async def marked():
+            return ANN_CANDIDATE in svc.ph.informer.cache[key]["metadata"]["annotations"]
+        assert await until(marked)
+        url = f"{lc.master_url}/api/v1/namespaces/default/pods/t/gpus"
+        async with lc.session.get(url) as r:
+            assert r.status == 200
+            hot = [g for g in (await r.json())["gpus"] if g["source"] == "hot-mount"]
+        st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+        assert sorted(g["uuid"] for g in hot) == sorted(g.uuid for g in st.hot)
+        assert len(hot) == 1
+    run(body)
+
+
 def test_a_pool_placeholder_reclaimed_by_the_same_pod_does_not_inherit_its_old_lease():
     """The same Pod gives a leased pool placeholder back before the lease ends and a later
     attach of that Pod (no lease) claims the same placeholder: the worker's memory of the old
