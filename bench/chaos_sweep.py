@@ -13,6 +13,7 @@ import argparse
 import concurrent.futures as cf
 import json
 import os
+import shutil
 import subprocess
 import sys
 import time
@@ -52,6 +53,8 @@ def one(mode: str, seed: int, out: str, timeout: float) -> dict:
         res = {"error": f"timed out after {timeout:g}s"}
     res.update(run=key, mode=mode, seed=seed, wall_s=round(time.time() - t0, 1),
                argv=argv[2:])
+    if res.get("invariant_violations") == 0 and "error" not in res:
+        shutil.rmtree(logs, ignore_errors=True)     # a clean run's logs are not kept
     return res
 
 
