@@ -92,6 +92,8 @@ NODES = [DeviceNode("/dev/kfd", 511, 0), DeviceNode("/dev/dri/renderD130", 226, 
 
 @pytest.mark.parametrize("mode", ["emulate", "procroot"])
 def test_devnodes_create_idempotent_remove(tmp_path, mode):
+    if mode == "procroot" and os.geteuid() != 0:
+        pytest.skip("mknod of a character device needs CAP_MKNOD (a GPU box runs as a user)")
     root = tmp_path / "root"
     (root / "dev").mkdir(parents=True)
     w = DevNodeWriter(mode)
