@@ -258,7 +258,7 @@ class LeaseKeeper:
                     # at again shortly (backing off to lease_retry_s) until it holds GPUs or is
                     # gone, not left to the next periodic sweep
                     n = self._waits.get(ph.uid, 0)
-                    self._waits[ph.uid] = n + 1
+                    self._waits[ph.uid] = min(n + 1, 16)
                     self._arm(ph.uid, ns, name,
                               now + min(0.1 * 2 ** n, self.svc.cfg.lease_retry_s))
                     continue
