@@ -237,6 +237,65 @@ class DeviceRuleBackend(ABC):
         return len(gone)
 
 
+V1_SYNC_STATE = ".gm_v1_applied"
+
+
+def v1_fake_sync(cgdir: str) -> List[str]:
+    """The kernel's side of an emulated v1 devices cgroup (one with ``FAKE_MARKER``): fold the
+    ``devices.allow``/``devices.deny`` lines written since the last sync into the set of rules
+    granted beyond the runtime's defaults, with the kernel's set semantics (an allow adds the
+    rule, a deny removes it; both are idempotent), and return that set. Counting allow lines
+    against deny lines, as the emulation did before, is not the kernel: a redundant deny
+    (harmless on a real node) left a rule's count below zero and made the next allow read as
+    missing. Lines that arrived on both files since the last sync are taken denies first, the
+    order :meth:`V1Backend.apply` writes them in (it syncs after every call). A file that
+    shrank was emptied by the emulation (a container's fresh device state): the set starts
+    over. Serialised across processes by a lock on the state file."""
+    import fcntl
+    state = os.path.join(cgdir, V1_SYNC_STATE)
+    try:
+        fd = os.open(state, os.O_RDWR | os.O_CREAT, 0o644)
+    except FileNotFoundError:
+        return []                                # the cgroup is gone
+    try:
+        fcntl.flock(fd, fcntl.LOCK_EX)
+        raw = b""
+        while True:
+            chunk = os.read(fd, 65536)
+            if not chunk:
+                break
+            raw += chunk
+        try:
+            st = json.loads(raw) if raw else {}
+        except ValueError:
+            st = {}
+        rules: List[str] = st.get("rules", [])
+        data = {}
+        for name in ("deny", "allow"):
+            try:
+                with open(os.path.join(cgdir, f"devices.{name}"), "rb") as fh:
+                    data[name] = fh.read()
+            except FileNotFoundError:
+                data[name] = b""
+        if any(len(data[n]) < st.get(n, 0) for n in data):
+            st, rules = {}, []
+        new = {n: [ln.strip() for ln in data[n][st.get(n, 0):].decode().splitlines()
+                   if ln.strip()] for n in data}
+        if new["deny"] or new["allow"] or not raw:
+            for rule in new["deny"]:
+                rules = [r for r in rules if r != rule]
+            for rule in new["allow"]:
+                if rule not in rules:
+                    rules.append(rule)
+            os.lseek(fd, 0, os.SEEK_SET)
+            os.ftruncate(fd, 0)
+            os.write(fd, json.dumps({"deny": len(data["deny"]), "allow": len(data["allow"]),
+                                     "rules": rules}).encode())
+        return rules
+    finally:
+        os.close(fd)
+
+
 class V1Backend(DeviceRuleBackend):
     name = "cgroup-v1"
 
@@ -244,9 +303,15 @@ class V1Backend(DeviceRuleBackend):
         rules = rules_for(revoke, allow=False) + rules_for(grant, allow=True)
         if not rules:
             return
+        if _log.isEnabledFor(10):
+            _log.debug("devices rules in %s: deny %s allow %s", cgdir,
+                       sorted((n.major, n.minor) for n in revoke),
+                       sorted((n.major, n.minor) for n in grant))
         rc = _native.host().gm_cg1_apply(cgdir.encode(), _rule_array(rules), len(rules))
         if rc < 0:
             raise CgroupError(f"devices.allow/deny write in {cgdir}: {os.strerror(-rc)}")
+        if os.path.exists(os.path.join(cgdir, FAKE_MARKER)):
+            v1_fake_sync(cgdir)          # an emulated cgroup: the kernel's part, in write order
 
     def fingerprint(self, cgdir):
         if os.path.exists(os.path.join(cgdir, FAKE_MARKER)):
@@ -264,23 +329,12 @@ class V1Backend(DeviceRuleBackend):
 
     def allowed(self, cgdir):
         if os.path.exists(os.path.join(cgdir, FAKE_MARKER)):
-            net: Dict[str, int] = {}
-            for fname, sign in (("devices.allow", 1), ("devices.deny", -1)):
-                try:
-                    with open(os.path.join(cgdir, fname)) as fh:
-                        for line in fh:
-                            rule = line.strip()
-                            if rule:
-                                net[rule] = net.get(rule, 0) + sign
-                except FileNotFoundError:
-                    pass
-            out = set()
-            for rule, cnt in net.items():
-                if cnt > 0:
-                    parts = rule.split()
-                    if len(parts) == 3 and parts[0] == "c" and "*" not in parts[1]:
-                        ma, mi = parts[1].split(":")
-                        out.add((int(ma), int(mi)))
+            out = set()                  # writes by others (a test, the runtime) land first
+            for rule in v1_fake_sync(cgdir):
+                parts = rule.split()
+                if len(parts) == 3 and parts[0] == "c" and "*" not in parts[1]:
+                    ma, mi = parts[1].split(":")
+                    out.add((int(ma), int(mi)))
             return out
         out = set()
         try:
