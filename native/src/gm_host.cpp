@@ -671,7 +671,13 @@ int create_one(Walker& w, const gm_dev_node_t& n, int flags) {
     int err = try_mknod ? errno : EPERM;
     if (!(err == EPERM && (flags & GM_DEV_EMULATE))) return -err;
     w.mknod_denied = true;  // unprivileged: the rest of this call goes straight to markers
-    int fd = openat(pfd, leaf.c_str(), O_CREAT | O_EXCL | O_WRONLY | O_NOFOLLOW | O_CLOEXEC,
+    // The marker appears whole or not at all: written under a hidden temporary name, then
+    // linked into place. Created in place, a worker killed between the create and the write
+    // left an empty file, which reads as "something else lives there": never replaced, never
+    // removed, the node missing for good (chaos on an unprivileged GPU box).
+    const std::string tmp = "." + leaf + ".gm-" + std::to_string(getpid());
+    unlinkat(pfd, tmp.c_str(), 0);
+    int fd = openat(pfd, tmp.c_str(), O_CREAT | O_EXCL | O_WRONLY | O_NOFOLLOW | O_CLOEXEC,
                     n.mode & 07777);
     if (fd < 0) return -errno;
     char buf[48];
@@ -679,6 +685,8 @@ int create_one(Walker& w, const gm_dev_node_t& n, int flags) {
     int wr = write_all(fd, buf, (size_t)len);
     if (wr == 0 && fchmod(fd, n.mode & 07777) < 0) wr = -errno;  // exact mode despite umask
     close(fd);
+    if (wr == 0 && linkat(pfd, tmp.c_str(), pfd, leaf.c_str(), 0) < 0) wr = -errno;
+    unlinkat(pfd, tmp.c_str(), 0);
     if (wr < 0) return wr;
   } else if (fchmodat(pfd, leaf.c_str(), n.mode & 07777, 0) < 0) {
     // mknod honours the umask; set the exact mode the tenant needs (reference used -m 666,

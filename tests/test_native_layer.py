@@ -359,3 +359,35 @@ def test_tenant_view_library_resolves_through_emulated_state(tmp_path):
     assert got["/dev/kfd"] in (0, errno.ENXIO)                 # granted: the host's node
     env = tenant.tenant_env(str(root), str(cg))
     assert env["LD_PRELOAD"].endswith("libgm_tenant_view.so")
+
+
+def test_emulated_markers_appear_whole_and_leave_no_temporaries(tmp_path):
+    """Without CAP_MKNOD (an unprivileged GPU box) emulate mode writes marker files. A marker is
+    written under a hidden name and linked into place: created in place, a worker killed
+    between the create and the write left an empty file that read as someone else's and was
+    never replaced (chaos on the GPU box: nodes missing for good, "mknod failed: File
+    exists")."""
+    import shutil
+    setpriv = shutil.which("setpriv")
+    if setpriv is None or os.geteuid() != 0:
+        pytest.skip("needs root and setpriv to drop CAP_MKNOD")
+    root = tmp_path / "root"
+    (root / "dev").mkdir(parents=True)
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from gpumounter_amd.node.devnodes import DevNodeWriter, Target\n"
+        "from gpumounter_amd.models.device import DeviceNode\n"
+        "nodes = [DeviceNode('/dev/kfd', 511, 0), DeviceNode('/dev/dri/renderD130', 226, 130)]\n"
+        "w = DevNodeWriter('emulate'); t = Target(root=%r)\n"
+        "print(w.create(t, nodes), w.create(t, nodes), [w.present(t, n) for n in nodes])\n"
+        % (ROOT, str(root)))
+    out = subprocess.run([setpriv, "--bounding-set=-mknod", "--inh-caps=-mknod", "--",
+                          sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split("\n")[0] == "[0, 0] [1, 1] [True, True]", out.stdout
+    for p, want in ((root / "dev/kfd", "gm-chr 511:0"),
+                    (root / "dev/dri/renderD130", "gm-chr 226:130")):
+        assert stat.S_ISREG(os.lstat(p).st_mode) and open(p).read().strip() == want
+    left = [f for d in (root / "dev", root / "dev/dri") for f in os.listdir(d)
+            if f.startswith(".")]
+    assert left == []
