@@ -685,7 +685,13 @@ int create_one(Walker& w, const gm_dev_node_t& n, int flags) {
     int wr = write_all(fd, buf, (size_t)len);
     if (wr == 0 && fchmod(fd, n.mode & 07777) < 0) wr = -errno;  // exact mode despite umask
     close(fd);
-    if (wr == 0 && linkat(pfd, tmp.c_str(), pfd, leaf.c_str(), 0) < 0) wr = -errno;
+    if (wr == 0 && linkat(pfd, tmp.c_str(), pfd, leaf.c_str(), 0) < 0) {
+      wr = -errno;
+      // a filesystem without hard links: a rename that will not replace does the same
+      if ((wr == -EPERM || wr == -EOPNOTSUPP) &&
+          syscall(SYS_renameat2, pfd, tmp.c_str(), pfd, leaf.c_str(), 1 /* NOREPLACE */) == 0)
+        wr = 0;
+    }
     unlinkat(pfd, tmp.c_str(), 0);
     if (wr < 0) return wr;
   } else if (fchmodat(pfd, leaf.c_str(), n.mode & 07777, 0) < 0) {
