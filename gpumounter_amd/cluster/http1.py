@@ -10,10 +10,17 @@ reference's client-go is a compiled client with a connection pool; this is the s
 an asyncio process.
 
 * ``Pool.request`` sends one request and returns ``(status, headers, body)``. Connections are
-  kept for ``keepalive_s`` when idle. A request that finds its reused connection closed by the
-  server before any byte of an answer (the idle-close race) is sent once more on a new one.
+  kept for ``keepalive_s`` when idle. A *replayable* request (GET/HEAD, or one the caller marks
+  so) that finds its reused connection closed by the server before any byte of an answer (the
+  idle-close race) is sent once more on a new one; any other request surfaces the error, since
+  the server may have processed it (Go's transport draws the same line).
 * ``Pool.stream`` opens a connection of its own for a watch and yields the decoded JSON lines;
-  ``read_timeout_s`` without a byte ends it with ``asyncio.TimeoutError``.
+  ``read_timeout_s`` without a byte ends it with ``asyncio.TimeoutError``. A line longer than
+  ``MAX_LINE`` ends it with ``HttpError``; while ``MAX_QUEUED`` bytes of lines wait for the
+  consumer the connection stops reading (TCP backpressure on the apiserver).
+* The parser accepts ASCII digits only (status, Content-Length, chunk sizes) and bounds every
+  line it waits for, so a malformed or hostile answer is an ``HttpError``, never an unbounded
+  buffer or an exception of another type.
 * Transport failures are ``ConnectionError``/``OSError`` (``HttpError`` for a malformed or cut
   answer), timeouts ``asyncio.TimeoutError``, as the callers expect from any client.
 """
@@ -27,7 +34,22 @@ import urllib.parse
 from typing import Callable, Deque, Dict, Optional, Tuple
 
 MAX_HEAD = 64 * 1024
-MAX_BODY = 256 * 1024 * 1024
+# one response body: every LIST is paged (cluster/kube.py list_pages, 500 objects a page), so
+# an answer this large is a broken or hostile server
+MAX_BODY = 32 * 1024 * 1024
+MAX_LINE = 16 * 1024 * 1024     # one watch event (etcd objects are at most ~1.5 MiB)
+MAX_QUEUED = 8 * 1024 * 1024    # watch bytes parsed but not consumed before reading pauses
+MAX_CHUNK_LINE = 1024           # a chunk-size or trailer line
+_DIGITS = frozenset(b"0123456789")
+_HEX = frozenset(b"0123456789abcdefABCDEF")
+
+
+def _ascii_int(b: bytes, base: int = 10) -> int:
+    """A non-negative integer of ASCII digits only (``int()`` also takes signs, spaces,
+    underscores and non-ASCII digits such as "²")."""
+    if not b or len(b) > 18 or not set(b) <= (_DIGITS if base == 10 else _HEX):
+        raise HttpError(f"bad number {bytes(b[:20])!r}")
+    return int(b, base)
 
 
 class HttpError(ConnectionError):
@@ -128,18 +150,24 @@ class _Conn(asyncio.Protocol):
                     if len(buf) > MAX_HEAD:
                         raise HttpError("response head too large")
                     return
+                if end > MAX_HEAD:
+                    raise HttpError("response head too large")
                 lines = bytes(buf[:end]).decode("latin-1").split("\r\n")
                 del buf[:end + 4]
                 parts = lines[0].split(" ", 2)
                 if len(parts) < 2 or not parts[0].startswith("HTTP/1.") or \
-                        not parts[1].isdigit():
+                        len(parts[1]) != 3 or not set(parts[1].encode()) <= _DIGITS:
                     raise HttpError(f"malformed status line {lines[0][:80]!r}")
                 status = int(parts[1])
                 headers: Dict[str, str] = {}
                 for ln in lines[1:]:
                     k, sep, v = ln.partition(":")
                     if sep:
-                        headers[k.strip().lower()] = v.strip()
+                        k = k.strip().lower()
+                        if k == "content-length" and k in headers and \
+                                headers[k] != v.strip():
+                            raise HttpError("conflicting Content-Length headers")
+                        headers[k] = v.strip()
                 if 100 <= status < 200:
                     continue                             # 100 Continue and friends
                 self._status, self._headers = status, headers
@@ -151,10 +179,9 @@ class _Conn(asyncio.Protocol):
                 elif te == "chunked":
                     self._state = "chunk_size"
                 elif "content-length" in headers:
-                    try:
-                        self._left = int(headers["content-length"])
-                    except ValueError:
-                        raise HttpError("bad Content-Length") from None
+                    self._left = _ascii_int(headers["content-length"].encode("latin-1"))
+                    if self._left > MAX_BODY and self.sink is None:
+                        raise HttpError("response body too large")
                     self._state = "length" if self._left else "done"
                 else:
                     self._state, self._keep = "close", False
@@ -171,15 +198,14 @@ class _Conn(asyncio.Protocol):
                 if self._left == 0:
                     self._state = "done"
             elif st == "chunk_size":
-                eol = buf.find(b"\r\n")
+                eol = buf.find(b"\r\n", 0, MAX_CHUNK_LINE + 2)
                 if eol < 0:
+                    if len(buf) > MAX_CHUNK_LINE:
+                        raise HttpError("chunk-size line too long")
                     return
-                size_s = bytes(buf[:eol]).split(b";", 1)[0].strip()
+                size_s = bytes(buf[:eol]).split(b";", 1)[0].strip(b" \t")
                 del buf[:eol + 2]
-                try:
-                    self._left = int(size_s, 16)
-                except ValueError:
-                    raise HttpError("bad chunk size") from None
+                self._left = _ascii_int(size_s, 16)
                 self._state = "chunk" if self._left else "trailer"
             elif st == "chunk":
                 if len(buf) < self._left + 2:
@@ -196,8 +222,10 @@ class _Conn(asyncio.Protocol):
                 self._deliver(piece)
                 self._state = "chunk_size"
             elif st == "trailer":
-                end = buf.find(b"\r\n")
+                end = buf.find(b"\r\n", 0, MAX_CHUNK_LINE + 2)
                 if end < 0:
+                    if len(buf) > MAX_CHUNK_LINE:
+                        raise HttpError("trailer line too long")
                     return
                 line = bytes(buf[:end])
                 del buf[:end + 2]
@@ -307,8 +335,12 @@ class Pool:
 
     # ------------------------------------------------------------------ requests
     async def request(self, method: str, target: str, headers: Optional[Dict[str, str]] = None,
-                      body: Optional[bytes] = None, timeout_s: Optional[float] = None
-                      ) -> Tuple[int, Dict[str, str], bytes]:
+                      body: Optional[bytes] = None, timeout_s: Optional[float] = None,
+                      replayable: Optional[bool] = None) -> Tuple[int, Dict[str, str], bytes]:
+        """``replayable``: the request may be sent a second time when a reused connection
+        turns out closed (default: GET and HEAD only)."""
+        if replayable is None:
+            replayable = method in ("GET", "HEAD")
         if self._closed:
             raise HttpError("client closed")
         msg = self._head(method, target, headers, body)
@@ -329,7 +361,7 @@ class Pool:
             try:
                 out = await fut
             except HttpError:
-                if reused and attempt == 0 and not conn.got_bytes:
+                if replayable and reused and attempt == 0 and not conn.got_bytes:
                     # the server closed the idle connection as we sent: a new one
                     self._busy.discard(conn)
                     continue
@@ -391,7 +423,9 @@ class _Lines:
         self.conn = conn
         self.read_timeout_s = read_timeout_s
         self.lines: Deque[bytes] = collections.deque()
-        self.partial = b""
+        self.partial = bytearray()
+        self.queued = 0               # bytes in ``lines``
+        self.paused = False
         self.done = False
         self.error: Optional[BaseException] = None
         self.waiter: Optional[asyncio.Future] = None
@@ -401,16 +435,38 @@ class _Lines:
     def feed(self, piece: Optional[bytes], exc: Optional[BaseException]) -> None:
         if piece is None:
             self.done, self.error = True, exc
-            if self.partial.strip():
-                self.lines.append(self.partial)
-            self.partial = b""
+            if bytes(self.partial).strip():
+                self._push(bytes(self.partial))
+            self.partial = bytearray()
         else:
-            data = self.partial + piece
-            *full, self.partial = data.split(b"\n")
-            self.lines.extend(ln for ln in full if ln.strip())
+            # only the new piece is scanned for line ends: a long line arriving in small pieces
+            # costs linear time, not quadratic
+            start = 0
+            while True:
+                nl = piece.find(b"\n", start)
+                if nl < 0:
+                    self.partial += piece[start:]
+                    break
+                if self.partial:
+                    self.partial += piece[start:nl]
+                    line, self.partial = bytes(self.partial), bytearray()
+                else:
+                    line = piece[start:nl]
+                if line.strip():
+                    self._push(line)
+                start = nl + 1
+            if len(self.partial) > MAX_LINE:
+                raise HttpError(f"watch line longer than {MAX_LINE} bytes")
+            if self.queued > MAX_QUEUED and not self.paused and self.conn.t is not None:
+                self.paused = True
+                self.conn.t.pause_reading()
         w = self.waiter
         if w is not None and not w.done() and (self.lines or self.done):
             w.set_result(None)
+
+    def _push(self, line: bytes) -> None:
+        self.lines.append(line)
+        self.queued += len(line)
 
     def _stall(self) -> None:
         self.error = asyncio.TimeoutError(f"no data for {self.read_timeout_s:g}s")
@@ -437,7 +493,12 @@ class _Lines:
             finally:
                 self._timer.cancel()
                 self.waiter = None
-        return self.lines.popleft()
+        line = self.lines.popleft()
+        self.queued -= len(line)
+        if self.paused and self.queued <= MAX_QUEUED // 2 and self.conn.t is not None:
+            self.paused = False
+            self.conn.t.resume_reading()
+        return line
 
     def close(self) -> None:
         t = self.conn.t

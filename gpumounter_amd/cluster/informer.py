@@ -426,8 +426,15 @@ class SlimPodInformer(PodInformer):
     of the whole object: 100k Pods ≈ 30 MB). The master's pod → node index."""
 
     async def _list(self):
-        items, rv = await super()._list()
-        return [slim_pod(p) for p in items], rv
+        # page by page: only the projections are kept, never a whole cluster's Pods at once
+        items, rv = [], ""
+        async for page, rv in self.kube.list_pages(self.kube._pods_path(self.namespace),  # noqa: SLF001
+                                                   self.label_selector, self.field_selector):
+            if page is None:          # the list restarted (continue token expired)
+                items = []
+                continue
+            items.extend(slim_pod(p) for p in page)
+        return items, rv
 
     async def _get(self, ns: str, name: str):
         return slim_pod(await super()._get(ns, name))

@@ -17,6 +17,7 @@ import os
 import ssl
 import tempfile
 from typing import Any, AsyncIterator, Dict, List, Optional, Tuple
+from urllib.parse import quote
 
 import yaml
 
@@ -25,17 +26,27 @@ from gpumounter_amd.utils import calls, log
 
 _log = log.get("kube")
 _RESOURCES = {"pods", "events", "resourceclaims", "resourceslices", "resourcequotas",
-              "tokenreviews", "subjectaccessreviews", "selfsubjectaccessreviews", "nodes"}
+              "tokenreviews", "subjectaccessreviews", "selfsubjectaccessreviews", "nodes",
+              "priorityclasses"}
 
 
 def _kind(method: str, path: str) -> str:
     """``apiserver POST pods`` for the call log (utils/calls.py)."""
-    for seg in reversed(path.split("/")):
-        if seg in _RESOURCES:
-            return f"apiserver {method} {seg}"
+    for part in reversed(path.split("/")):
+        if part in _RESOURCES:
+            return f"apiserver {method} {part}"
     return f"apiserver {method}"
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+def seg(s: str) -> str:
+    """One path segment of an apiserver URL: percent-quoted, so a name can never add a
+    segment ("/"), walk up one ("..") or end the path ("?", "#"). Names the apiserver could
+    not hold (empty, "." or "..") raise ValueError before anything is sent."""
+    if not s or s in (".", ".."):
+        raise ValueError(f"invalid object name {s!r}")
+    return quote(s, safe="")
 
 
 class ApiError(Exception):
@@ -161,7 +172,7 @@ class KubeClient:
         for attempt in range(len(delays) + 1):
             try:
                 return await self._req_once(method, path, params, body, content_type,
-                                            as_token)
+                                            as_token, replayable=retry)
             except ApiError as e:
                 if e.status not in self.RETRY_STATUS or attempt == len(delays):
                     raise
@@ -177,7 +188,10 @@ class KubeClient:
         raise AssertionError("unreachable")
 
     async def _req_once(self, method: str, path: str, params: Optional[dict], body: Any,
-                        content_type: str, as_token: str = "") -> Any:
+                        content_type: str, as_token: str = "", replayable: bool = False) -> Any:
+        """``replayable``: the transport may resend the request on a fresh connection when a
+        kept-alive one turns out closed (only requests ``_req`` would retry anyway: a POST
+        that may have been processed is never sent twice behind the caller's back)."""
         pool = self._http()
         data = None
         headers = {"Authorization": f"Bearer {as_token}"} if as_token else {}
@@ -186,7 +200,7 @@ class KubeClient:
             headers["Content-Type"] = content_type
         with calls.span(_kind(method, path)):
             status, _, raw = await pool.request(method, pool.target(path, params),
-                                                headers or None, data)
+                                                headers or None, data, replayable=replayable)
         if status >= 400:
             text = raw.decode("utf-8", "replace")
             try:
@@ -203,22 +217,69 @@ class KubeClient:
 
     @staticmethod
     def _pods_path(ns: Optional[str], name: str = "") -> str:
-        base = f"/api/v1/namespaces/{ns}/pods" if ns else "/api/v1/pods"
-        return f"{base}/{name}" if name else base
+        base = f"/api/v1/namespaces/{seg(ns)}/pods" if ns else "/api/v1/pods"
+        return f"{base}/{seg(name)}" if name else base
 
     # ------------------------------------------------------------------------- pods
     async def get_pod(self, ns: str, name: str) -> dict:
         return await self._req("GET", self._pods_path(ns, name))
 
     async def list_pods(self, ns: Optional[str] = None, label_selector: str = "",
-                        field_selector: str = "") -> Tuple[List[dict], str]:
-        params = {}
-        if label_selector:
-            params["labelSelector"] = label_selector
-        if field_selector:
-            params["fieldSelector"] = field_selector
-        out = await self._req("GET", self._pods_path(ns), params=params)
-        return out.get("items", []), out.get("metadata", {}).get("resourceVersion", "")
+                        field_selector: str = "", limit: int = 0) -> Tuple[List[dict], str]:
+        """All matching Pods and the list's resourceVersion, read in pages of ``limit``
+        (``PAGE`` by default) so no single response holds the whole collection."""
+        items: List[dict] = []
+        rv = ""
+        async for page, rv in self.list_pages(self._pods_path(ns), label_selector,
+                                              field_selector, limit):
+            if page is None:            # the list restarted: earlier pages are stale
+                items = []
+                continue
+            items.extend(page)
+        return items, rv
+
+    # page size of every LIST (client-go's reflector pages by 500 too)
+    PAGE = 500
+    # a continue token that expired mid-list (410) restarts the list this many times before
+    # the error is raised to the caller (a watch-based caller relists on its own schedule)
+    PAGE_RESTARTS = 3
+
+    async def list_pages(self, path: str, label_selector: str = "", field_selector: str = "",
+                         limit: int = 0) -> AsyncIterator[Tuple[List[dict], str]]:
+        """Yield ``(items, resourceVersion)`` page by page (``limit`` + ``continue``). The
+        resourceVersion is the list's, the same on every page of one consistent snapshot.
+        A continue token that the apiserver no longer serves (410 Expired, the snapshot was
+        compacted) restarts the list from the first page; the caller sees a ``None`` page
+        first, meaning: drop what the earlier pages gave you."""
+        limit = limit or self.PAGE
+        restarts = 0
+        cont = ""
+        while True:
+            params = {"limit": str(limit)}
+            if label_selector:
+                params["labelSelector"] = label_selector
+            if field_selector:
+                params["fieldSelector"] = field_selector
+            if cont:
+                params["continue"] = cont
+            try:
+                out = await self._req("GET", path, params=params)
+            except ApiError as e:
+                if e.status != 410 or not cont or restarts >= self.PAGE_RESTARTS:
+                    raise
+                restarts += 1
+                _log.info("LIST %s: continue token expired; restarting the list", path)
+                cont = ""
+                yield None, ""          # type: ignore[misc]
+                continue
+            md = out.get("metadata", {}) or {}
+            yield out.get("items", []) or [], md.get("resourceVersion", "")
+            cont = md.get("continue") or ""
+            if not cont:
+                return
+
+    async def get_priority_class(self, name: str) -> dict:
+        return await self._req("GET", f"/apis/scheduling.k8s.io/v1/priorityclasses/{seg(name)}")
 
     async def create_pod(self, ns: str, pod: dict, dry_run: bool = False) -> dict:
         """Create; retried on transient errors when the name is explicit (a retry that finds
@@ -256,7 +317,7 @@ class KubeClient:
     async def create_claim(self, ns: str, claim: dict) -> dict:
         name = (claim.get("metadata") or {}).get("name", "")
         try:
-            return await self._req("POST", f"{self._DRA}/namespaces/{ns}/resourceclaims",
+            return await self._req("POST", f"{self._DRA}/namespaces/{seg(ns)}/resourceclaims",
                                    body=claim, idempotent=bool(name))
         except Conflict:
             cur = await self.get_claim(ns, name)
@@ -267,10 +328,10 @@ class KubeClient:
             raise
 
     async def get_claim(self, ns: str, name: str) -> dict:
-        return await self._req("GET", f"{self._DRA}/namespaces/{ns}/resourceclaims/{name}")
+        return await self._req("GET", f"{self._DRA}/namespaces/{seg(ns)}/resourceclaims/{seg(name)}")
 
     async def delete_claim(self, ns: str, name: str) -> Optional[dict]:
-        return await self._req("DELETE", f"{self._DRA}/namespaces/{ns}/resourceclaims/{name}")
+        return await self._req("DELETE", f"{self._DRA}/namespaces/{seg(ns)}/resourceclaims/{seg(name)}")
 
     async def list_claims(self, ns: str = "", label_selector: str = "") -> List[dict]:
         return (await self.list_claims_rv(ns, label_selector))[0]
@@ -313,21 +374,29 @@ class KubeClient:
         return (out or {}).get("status") or {}
 
     async def list_resource_quotas(self, ns: str) -> List[dict]:
-        out = await self._req("GET", f"/api/v1/namespaces/{ns}/resourcequotas")
-        return out.get("items", [])
+        return (await self._list_all(f"/api/v1/namespaces/{seg(ns)}/resourcequotas"))[0]
 
     @staticmethod
     def _quotas_path(ns: Optional[str]) -> str:
-        return f"/api/v1/namespaces/{ns}/resourcequotas" if ns else "/api/v1/resourcequotas"
+        return f"/api/v1/namespaces/{seg(ns)}/resourcequotas" if ns else "/api/v1/resourcequotas"
 
     async def list_quotas_rv(self, ns: Optional[str] = None, label_selector: str = ""
                              ) -> Tuple[List[dict], str]:
-        params = {"labelSelector": label_selector} if label_selector else None
-        out = await self._req("GET", self._quotas_path(ns), params=params)
-        return out.get("items", []), out.get("metadata", {}).get("resourceVersion", "")
+        return await self._list_all(self._quotas_path(ns), label_selector)
+
+    async def _list_all(self, path: str, label_selector: str = "", field_selector: str = ""
+                        ) -> Tuple[List[dict], str]:
+        items: List[dict] = []
+        rv = ""
+        async for page, rv in self.list_pages(path, label_selector, field_selector):
+            if page is None:
+                items = []
+                continue
+            items.extend(page)
+        return items, rv
 
     async def get_quota(self, ns: str, name: str) -> dict:
-        return await self._req("GET", f"{self._quotas_path(ns)}/{name}")
+        return await self._req("GET", f"{self._quotas_path(ns)}/{seg(name)}")
 
     async def watch_quotas(self, ns: Optional[str] = None, label_selector: str = "",
                            field_selector: str = "", resource_version: str = "",
@@ -337,7 +406,7 @@ class KubeClient:
             yield ev
 
     async def create_event(self, ns: str, event: dict) -> dict:
-        return await self._req("POST", f"/api/v1/namespaces/{ns}/events", body=event)
+        return await self._req("POST", f"/api/v1/namespaces/{seg(ns)}/events", body=event)
 
     async def watch_pods(self, ns: Optional[str] = None, label_selector: str = "",
                          field_selector: str = "", resource_version: str = "",
@@ -348,14 +417,12 @@ class KubeClient:
             yield ev
 
     def _claims_path(self, ns: Optional[str]) -> str:
-        return f"{self._DRA}/namespaces/{ns}/resourceclaims" if ns else \
+        return f"{self._DRA}/namespaces/{seg(ns)}/resourceclaims" if ns else \
             f"{self._DRA}/resourceclaims"
 
     async def list_claims_rv(self, ns: Optional[str] = None, label_selector: str = ""
                              ) -> Tuple[List[dict], str]:
-        params = {"labelSelector": label_selector} if label_selector else None
-        out = await self._req("GET", self._claims_path(ns), params=params)
-        return out.get("items", []), out.get("metadata", {}).get("resourceVersion", "")
+        return await self._list_all(self._claims_path(ns), label_selector)
 
     async def watch_claims(self, ns: Optional[str] = None, label_selector: str = "",
                            field_selector: str = "", resource_version: str = "",

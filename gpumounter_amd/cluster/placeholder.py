@@ -28,7 +28,13 @@ Unschedulable → InsufficientGPU mapping. Changed:
 * on DRA clusters (``gpu_allocation=dra``) a placeholder holds a ResourceClaim of its own name
   instead of an extended-resource limit, and the topology-chosen devices are a CEL selector of
   that claim: the scheduler allocates exactly them (no trim needed). If they were taken
-  meanwhile, the reservation is retried once without the selector.
+  meanwhile, the reservation is retried once without the selector;
+* a placeholder never ranks below the tenant whose GPU it books (:meth:`priority_for`): the
+  reference's slave pods have priority 0, so any higher-priority Pod requesting a GPU on a
+  full node makes the scheduler preempt one, and the GPU is revoked under a running job.
+  Placeholders get the floor class ``placeholder_priority_class`` (shipped: value 1000000,
+  ``preemptionPolicy: Never``, so they never preempt anyone either), or the tenant's own class
+  when the tenant ranks higher.
 """
 from __future__ import annotations
 
@@ -59,6 +65,10 @@ CLAIM_REQUEST = "gpus"
 STANDBY_PREFIX = "gpumounter-standby-"
 
 
+# the Priority admission plugin's refusal of a class that does not exist
+_NO_CLASS = "no PriorityClass with name"
+
+
 class Reowned(Exception):
     """A pool placeholder that changed owner since the caller decided to release it."""
 
@@ -85,6 +95,7 @@ class Placeholder:
     # this holder (see _delete)
     owner_uid: str = ""
     attach_id: str = ""
+    priority: int = 0            # spec.priority (immutable for the Pod's lifetime)
 
     def held_by_me(self, pod: dict) -> bool:
         """``pod`` (the placeholder as the apiserver has it) still has this object's holder."""
@@ -168,6 +179,10 @@ class PlaceholderManager:
         self.on_foreign_delete: List[Callable[[dict], None]] = []
         self._foreign_seen: Dict[str, float] = {}
         self._bg: set = set()       # background claim deletions (DRA mode)
+        # PriorityClass name → value; None: the class does not exist in the cluster. Read at
+        # start (resolve_priority); a class missing at create time is marked here too
+        self.class_values: Dict[str, Optional[int]] = {}
+        self.priority_fallbacks = 0     # placeholders created without their floor class
 
     def _on_event(self, etype: str, pod: dict) -> None:
         md = pod.get("metadata", {})
@@ -197,6 +212,60 @@ class PlaceholderManager:
                 self.device_ids.pop(uid, None)
             for uid in [u for u in self._foreign_seen if u not in live]:
                 self._foreign_seen.pop(uid, None)
+
+    # ------------------------------------------------------------------------ priority
+    async def resolve_priority(self) -> None:
+        """Read the values of the configured classes (the floor, the pool's). A class the
+        apiserver does not have is recorded as absent: placeholders then fall back to their
+        tenant's class (still never below it) and the doctor reports the missing class."""
+        names = {self.cfg.placeholder_priority_class,
+                 getattr(self.cfg, "pool_priority_class", "")} - {""}
+        for name in sorted(names):
+            try:
+                pc = await self.kube.get_priority_class(name)
+                self.class_values[name] = int(pc.get("value", 0))
+            except NotFound:
+                self.class_values[name] = None
+                _log.error("PriorityClass %s does not exist: placeholders fall back to their "
+                           "tenant's priority (apply deploy/placeholder-priority.yaml)", name)
+            except Exception as e:  # noqa: BLE001 - RBAC without priorityclasses: config value
+                _log.info("PriorityClass %s not readable (%s); assuming value %d", name, e,
+                          self.cfg.placeholder_priority_value)
+
+    def class_value(self, name: str) -> Optional[int]:
+        """Value of ``name``; the configured floor value when it could not be read."""
+        if name in self.class_values:
+            return self.class_values[name]
+        if name == self.cfg.placeholder_priority_class:
+            return int(self.cfg.placeholder_priority_value)
+        return None
+
+    def priority_for(self, owner: dict) -> Tuple[str, int]:
+        """(priorityClassName, priority) of a placeholder that books a GPU for ``owner``:
+        the floor class, or the owner's own class when the owner ranks higher (or when the
+        floor is off or missing). Never below the owner."""
+        spec = owner.get("spec") or {}
+        o_cls, o_prio = spec.get("priorityClassName") or "", podu.priority_of(owner)
+        floor = self.cfg.placeholder_priority_class
+        fv = self.class_value(floor) if floor else None
+        if fv is None or (o_prio > fv and getattr(self.cfg, "placeholder_priority_inherit",
+                                                  True)):
+            return o_cls, o_prio
+        return floor, fv
+
+    def standby_class(self) -> Tuple[str, int]:
+        """(class, value) of warm-pool standby placeholders: ``pool_priority_class``, else the
+        floor class; no class when the chosen one is missing."""
+        name = getattr(self.cfg, "pool_priority_class", "") or \
+            self.cfg.placeholder_priority_class
+        v = self.class_value(name) if name else None
+        return (name, v) if v is not None else ("", 0)
+
+    def _class_missing(self, e: BaseException) -> Optional[str]:
+        """The class a create failed on because it does not exist (None: another error)."""
+        if isinstance(e, ApiError) and e.status == 403 and _NO_CLASS in _message(e):
+            return _message(e).split(_NO_CLASS, 1)[1].split()[0]
+        return None
 
     # ------------------------------------------------------------------------ spec
     def namespace_for(self, owner: dict) -> str:
@@ -259,8 +328,9 @@ class PlaceholderManager:
             res.pop("limits")
             res["claims"] = [{"name": CLAIM_REQUEST}]
             spec["resourceClaims"] = [{"name": CLAIM_REQUEST, "resourceClaimName": name}]
-        if self.cfg.placeholder_priority_class:
-            spec["priorityClassName"] = self.cfg.placeholder_priority_class
+        pclass, _ = self.priority_for(owner)
+        if pclass:
+            spec["priorityClassName"] = pclass
         return {"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": spec}
 
     @property
@@ -331,7 +401,7 @@ class PlaceholderManager:
             if len(preferred) == total else [[] for _ in range(k)]
         bodies = [self.build(owner, per_pod, mode, prefs[i], attach_id, container,
                              idempotency_key, lease_expires) for i in range(k)]
-        created = await self._create(bodies)
+        created = await self._create(bodies, owner)
         try:
             with trace.span("placeholder_wait"):
                 self.faults.check("placeholder_wait")
@@ -368,7 +438,7 @@ class PlaceholderManager:
             b["metadata"]["annotations"][ANN_CANDIDATE] = attach_id or "1"
             if group:
                 b["metadata"]["annotations"][ANN_GROUP] = group
-        created = await self._create(bodies)
+        created = await self._create(bodies, owner)
         for p in created:
             p.candidate = True
         try:
@@ -491,20 +561,44 @@ class PlaceholderManager:
         gone = await asyncio.gather(*[absent(ns, n) for ns, n in keys])
         await self._delete_claims([k for k, g in zip(keys, gone) if g])
 
-    async def _create(self, bodies: List[dict]) -> List[Placeholder]:
+    async def create_pod(self, body: dict, fallback_class: str = "") -> dict:
+        """POST one placeholder. If the apiserver refuses its PriorityClass as nonexistent
+        (deleted since start, or never applied), the class is recorded as absent and the
+        placeholder is created once more with ``fallback_class`` (its tenant's class)."""
+        try:
+            return await self.kube.create_pod(body["metadata"]["namespace"], body)
+        except ApiError as e:
+            missing = self._class_missing(e)
+            spec = body["spec"]
+            if missing is None or spec.get("priorityClassName") != missing:
+                raise
+            if self.class_values.get(missing, 0) is not None:
+                _log.error("PriorityClass %s does not exist: placeholders fall back to their "
+                           "tenant's priority (apply deploy/placeholder-priority.yaml)", missing)
+            self.class_values[missing] = None
+            self.priority_fallbacks += 1
+            if fallback_class and fallback_class != missing:
+                spec["priorityClassName"] = fallback_class
+            else:
+                spec.pop("priorityClassName", None)
+            return await self.kube.create_pod(body["metadata"]["namespace"], body)
+
+    async def _create(self, bodies: List[dict], owner: Optional[dict] = None
+                      ) -> List[Placeholder]:
+        fb = ((owner or {}).get("spec") or {}).get("priorityClassName") or ""
         with trace.span("ledger_reserve", placeholders=len(bodies)):
             self.faults.check("ledger_reserve")
             if self.dra:
                 await self._create_claims(bodies)
             epoch = self.informer.epoch
-            results = await asyncio.gather(
-                *[self.kube.create_pod(b["metadata"]["namespace"], b) for b in bodies],
-                return_exceptions=True)
+            results = await asyncio.gather(*[self.create_pod(b, fb) for b in bodies],
+                                           return_exceptions=True)
         created = [Placeholder(r["metadata"]["namespace"], r["metadata"]["name"],
                                r["metadata"]["uid"], (),
                                r["metadata"]["annotations"].get(ANN_MOUNT_MODE, "single"),
                                owner_uid=r["metadata"]["annotations"].get(ANN_OWNER_UID, ""),
-                               attach_id=r["metadata"]["annotations"].get(ANN_ATTACH_ID, ""))
+                               attach_id=r["metadata"]["annotations"].get(ANN_ATTACH_ID, ""),
+                               priority=podu.priority_of(r))
                    for r in results if isinstance(r, dict)]
         for r in results:
             if isinstance(r, dict):
@@ -569,6 +663,10 @@ class PlaceholderManager:
                             return True
                         continue
                     msg = podu.is_unschedulable(pod)
+                    if msg and podu.nominated_node(pod):
+                        # it preempts lower-priority Pods (a placeholder of a tenant whose own
+                        # class preempts) and is bound once they are gone: not a refusal
+                        msg = None
                     ids = ck.lookup(pending[key].uid) if ck is not None else None
                     if ids is None and reserved is not None:
                         ids = reserved(key[0], key[1], pending[key].uid)
@@ -794,7 +892,7 @@ class PlaceholderManager:
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""),
                            tuple(ledger_ids.get(key, ())), ann.get(ANN_MOUNT_MODE, "single"),
                            ANN_CANDIDATE in ann, ann.get(ANN_OWNER_UID) or "",
-                           ann.get(ANN_ATTACH_ID) or "")
+                           ann.get(ANN_ATTACH_ID) or "", podu.priority_of(p))
 
     def cached(self, p: dict) -> Optional[Placeholder]:
         """Placeholder with its device IDs from the admission cache (None if unknown)."""
@@ -805,4 +903,5 @@ class PlaceholderManager:
         ann = md.get("annotations") or {}
         return Placeholder(md["namespace"], md["name"], md.get("uid", ""), ids,
                            ann.get(ANN_MOUNT_MODE, "single"), ANN_CANDIDATE in ann,
-                           ann.get(ANN_OWNER_UID) or "", ann.get(ANN_ATTACH_ID) or "")
+                           ann.get(ANN_OWNER_UID) or "", ann.get(ANN_ATTACH_ID) or "",
+                           podu.priority_of(p))

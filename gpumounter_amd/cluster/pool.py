@@ -15,6 +15,16 @@ like any hot-mounted GPU (the ledger stays consistent), but belong to no tenant.
 Entire mounts claim K standby placeholders as one group (``gpumounter.amd.com/group``) and keep
 the reference's all-or-nothing add/remove semantics. When the pool cannot cover a request the
 worker falls back to creating placeholders as usual.
+
+Priority. A claimed standby books a GPU its new tenant uses, so it must rank at least as high as
+that tenant (cluster/placeholder.py ``priority_for``); a Pod's priority is immutable, so only
+standbys created at that rank or higher can be claimed. By default standbys get the same floor
+class as every placeholder (``placeholder_priority_class``): they cannot be preempted, and every
+claim keeps the pool's latency. With a lower ``pool_priority_class`` idle standbys are
+preemptible by higher-priority Pods (the scheduler evicts them, the pool refills when capacity
+frees), and an attach that needs their GPUs *yields* them (:meth:`yield_low`: a conditional
+DELETE while still standby) and books the GPUs with placeholders at tenant priority — the cold
+path's latency, never a GPU held by a placeholder that ranks below its tenant.
 """
 from __future__ import annotations
 
@@ -76,11 +86,14 @@ class WarmPool:
         return self.target > 0
 
     # ------------------------------------------------------------------------ state
-    def standby(self) -> List[Placeholder]:
-        """Admitted standby placeholders (device IDs known)."""
+    def standby(self, min_priority: Optional[int] = None) -> List[Placeholder]:
+        """Admitted standby placeholders (device IDs known); ``min_priority``: only those that
+        rank at least that high (claimable by a tenant whose placeholders need that rank)."""
         out = []
         for p in self.ph.live():
             if not is_standby(p) or p["metadata"].get("uid") in self._claimed:
+                continue
+            if min_priority is not None and podu.priority_of(p) < min_priority:
                 continue
             c = self.ph.cached(p)
             if c is None:
@@ -116,6 +129,11 @@ class WarmPool:
         name = f"{STANDBY_PREFIX}{_label_value(self.ph.node)[:40]}-{secrets.token_hex(4)}"
         body = self.ph.build({"metadata": {"name": "standby", "namespace": "", "uid": ""}},
                              1, MODE_STANDBY)
+        pclass, _ = self.ph.standby_class()
+        if pclass:
+            body["spec"]["priorityClassName"] = pclass
+        else:
+            body["spec"].pop("priorityClassName", None)
         md = body["metadata"]
         md["name"] = name
         md["namespace"] = self.cfg.pool_namespace
@@ -201,7 +219,7 @@ class WarmPool:
                     if self.ph.dra:                     # its ResourceClaim first
                         await self.ph._create_claims([body])  # noqa: SLF001
                     epoch = self.ph.informer.epoch
-                    pod = await self.ph.kube.create_pod(self.cfg.pool_namespace, body)
+                    pod = await self.ph.create_pod(body)
                 except Exception as e:  # noqa: BLE001
                     _log.warning("standby create failed: %s", e)
                     if self.ph.dra:     # unless the create happened after all (see there)
@@ -233,13 +251,16 @@ class WarmPool:
                     attach_id: str = "", container: str = "",
                     idempotency_key: str = "",
                     want: Optional[Sequence[int]] = None,
-                    lease_expires: float = 0.0) -> Optional[Reservation]:
+                    lease_expires: float = 0.0,
+                    min_priority: Optional[int] = None) -> Optional[Reservation]:
         """Claim ``n`` standby GPUs for ``owner`` (exactly the GPU indices ``want`` when the
         caller planned the placement over standby ∪ free GPUs); None if the pool cannot.
+        ``min_priority``: only standbys that rank at least that high (the owner's placeholder
+        rank, see the module docstring).
         ``lease_expires`` goes into the same conditional claim PATCH, so a leased claim is
         never recorded without its lease (and an unleased one clears any earlier owner's)."""
         async with self._lock:
-            pool = self.standby()
+            pool = self.standby(min_priority)
             if len(pool) < n:
                 return None
             keys = self.inv.by_key()
@@ -312,6 +333,43 @@ class WarmPool:
                 self.metrics.reconcile_actions.labels(action="pool_claim").inc(len(chosen))
         self.poke()
         return Reservation(chosen)
+
+    async def yield_low(self, n: int, min_priority: int, attached: Sequence[AmdGpu] = ()
+                        ) -> List[Placeholder]:
+        """Give up to ``n`` standby GPUs that rank below ``min_priority`` back to the scheduler
+        (DELETE, conditional on each still being standby), so an attach at that rank can book
+        them with placeholders of its own; the best-placed ones for ``attached`` go first.
+        Returns those released. The pool refills later from whatever is free then."""
+        async with self._lock:
+            low = [ph for ph in self.standby() if ph.priority < min_priority]
+            if not low or n <= 0:
+                return []
+            keys = self.inv.by_key()
+            by_gpu = {}
+            for ph in low:
+                g = keys.get(normalize_device_id(ph.device_ids[0]))
+                if g is not None:
+                    by_gpu[g.index] = ph
+            k = min(n, len(low))
+            plc = topology.choose([keys[normalize_device_id(ph.device_ids[0])]
+                                   for ph in by_gpu.values()], k, self.inv.links(),
+                                  attached=attached, policy=self.cfg.topology_policy) \
+                if len(by_gpu) >= k else None
+            chosen = [by_gpu[i] for i in plc.chosen] if plc is not None else low[:k]
+            for ph in chosen:
+                ph.owner_uid, ph.attach_id = "", ""     # released only while still standby
+            with trace.span("pool_yield", placeholders=len(chosen)):
+                try:
+                    await self.ph.release(chosen)
+                except Exception as e:  # noqa: BLE001 - what was released still counts
+                    _log.warning("yielding standby placeholders: %s", e)
+            gone = [ph for ph in chosen if (ph.namespace, ph.name) not in self.ph.informer.cache
+                    or ph.uid in self.ph.tombstones]
+            if self.metrics is not None and gone:
+                self.metrics.reconcile_actions.labels(action="pool_yield").inc(len(gone))
+            _log.info("yielded %d low-priority standby GPU(s) to an attach at priority %d",
+                      len(gone), min_priority)
+            return gone
 
     def _versions(self) -> Dict[str, str]:
         """uid → resourceVersion of every standby placeholder as the informer last saw it."""
@@ -431,7 +489,13 @@ class WarmPool:
         async with self._lock:
             # standby being admitted count too, or a refill racing a give-back overfills
             room = max(self.target - len(self.standby()) - self.pending() - self._creating, 0)
-            keep = [p for p in phs if p.device_ids and len(p.device_ids) == 1][:room]
+            # with a low pool class, a placeholder that booked a tenant's GPU (at tenant rank)
+            # does not become an idle standby: standbys must stay preemptible. It is deleted
+            # and the refill creates a standby at the pool's class
+            cap = self.ph.standby_class()[1] if getattr(self.cfg, "pool_priority_class", "") \
+                else None
+            keep = [p for p in phs if p.device_ids and len(p.device_ids) == 1
+                    and (cap is None or p.priority <= cap)][:room]
             drop = [p for p in phs if p not in keep]
             cache = {p["metadata"]["uid"]: p for p in self.ph.live()}
 

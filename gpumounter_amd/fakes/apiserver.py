@@ -167,11 +167,79 @@ class FakeCluster:
         self.watch_delay_s = 0.0
         from gpumounter_amd.fakes.dra import DraState
         self.dra = DraState(self)     # resource.k8s.io/v1 claims and slices (fakes/dra.py)
+        # scheduling.k8s.io/v1 PriorityClasses: the two every cluster has; the harness applies
+        # the shipped deploy's classes on top (deploy/placeholder-priority.yaml)
+        self.priority_classes: Dict[str, dict] = {}
+        self.add_priority_class("system-cluster-critical", 2000000000)
+        self.add_priority_class("system-node-critical", 2000001000)
+        self.preemptions = 0          # victims the scheduler evicted for a higher-priority Pod
+        self.victims: List[dict] = []  # each victim as it was when preempted (last 1000)
 
     # ------------------------------------------------------------------------ nodes
     def add_node(self, node: FakeNode) -> FakeNode:
         self.nodes[node.name] = node
         return node
+
+    # ------------------------------------------------------------------------ priority
+    def add_priority_class(self, name: str, value: int,
+                           preemption_policy: str = "PreemptLowerPriority",
+                           global_default: bool = False, description: str = "") -> dict:
+        pc = {"apiVersion": "scheduling.k8s.io/v1", "kind": "PriorityClass",
+              "metadata": {"name": name, "uid": str(uuid.uuid4())}, "value": int(value),
+              "preemptionPolicy": preemption_policy, "globalDefault": bool(global_default)}
+        if description:
+            pc["description"] = description
+        self.priority_classes[name] = pc
+        return pc
+
+    def apply_priority_classes(self, docs) -> List[str]:
+        """Create the PriorityClass objects among ``docs`` (parsed manifests), as
+        ``kubectl apply`` of the deploy would; returns their names."""
+        out = []
+        for d in docs:
+            if isinstance(d, dict) and d.get("kind") == "PriorityClass":
+                self.add_priority_class(d["metadata"]["name"], int(d["value"]),
+                                        d.get("preemptionPolicy") or "PreemptLowerPriority",
+                                        bool(d.get("globalDefault")), d.get("description", ""))
+                out.append(d["metadata"]["name"])
+        return out
+
+    def _priority_admit(self, pod: dict) -> None:
+        """The Priority admission plugin: ``spec.priority`` and ``spec.preemptionPolicy`` come
+        from the PriorityClass named (or the global default); a Pod naming a class that does
+        not exist, or giving values that differ from the class's, is refused with 403."""
+        spec = pod.setdefault("spec", {})
+        pname = pod.get("metadata", {}).get("name", "")
+        name = spec.get("priorityClassName") or ""
+        if not name:
+            d = next((c for c in self.priority_classes.values() if c.get("globalDefault")), None)
+            if d is not None:
+                name = spec["priorityClassName"] = d["metadata"]["name"]
+        value, policy = 0, "PreemptLowerPriority"
+        if name:
+            pc = self.priority_classes.get(name)
+            if pc is None:
+                raise self._forbidden(f'pods "{pname}" is forbidden: no PriorityClass with '
+                                      f"name {name} was found")
+            value, policy = int(pc["value"]), pc.get("preemptionPolicy") or policy
+        if spec.get("priority") is not None and int(spec["priority"]) != value:
+            raise self._forbidden(
+                f'pods "{pname}" is forbidden: the integer value of priority '
+                f'({spec["priority"]}) must not be provided in pod spec; priority admission '
+                f"controller computed {value} from the given PriorityClass name")
+        if spec.get("preemptionPolicy") and spec["preemptionPolicy"] != policy:
+            raise self._forbidden(
+                f'pods "{pname}" is forbidden: the string value of PreemptionPolicy '
+                f'({spec["preemptionPolicy"]}) must not be provided in pod spec; priority '
+                f"admission controller computed {policy} from the given PriorityClass name")
+        spec["priority"] = value
+        spec["preemptionPolicy"] = policy
+
+    @staticmethod
+    def _forbidden(msg: str) -> web.HTTPForbidden:
+        return web.HTTPForbidden(text=json.dumps({"kind": "Status", "reason": "Forbidden",
+                                                  "code": 403, "message": msg}),
+                                 content_type="application/json")
 
     # ------------------------------------------------------------------------ events
     def _bump(self, etype: str, pod: dict) -> None:
@@ -223,6 +291,7 @@ class FakeCluster:
         md.setdefault("labels", {})
         md.setdefault("annotations", {})
         pod.setdefault("spec", {})
+        self._priority_admit(pod)
         self._quota_admit(ns, pod)
         pod["status"] = {"phase": "Pending", "conditions": []}
         self.pods[(ns, md["name"])] = pod
@@ -309,6 +378,72 @@ class FakeCluster:
             total += podu.resource_limit(p, resource)
         return total
 
+    def _nominated(self, node: str, resource: str, pod: dict) -> int:
+        """What Pods nominated to ``node`` by a preemption (not bound yet) need, counted
+        against ``pod`` when they rank at least as high: the scheduler keeps the room a
+        preemption freed for the preemptor, so a lower-priority Pod cannot take it back."""
+        prio, me = podu.priority_of(pod), podu.uid_of(pod)
+        return sum(podu.resource_limit(p, resource) for p in self.pods.values()
+                   if podu.nominated_node(p) == node and not podu.node_of(p)
+                   and podu.uid_of(p) != me and podu.priority_of(p) >= prio
+                   and not podu.is_terminating(p))
+
+    def _victims(self, pod: dict, node: FakeNode) -> Optional[List[dict]]:
+        """The fewest lowest-priority Pods on ``node`` whose eviction makes ``pod`` fit (Pods of
+        lower priority only; those already terminating count as gone): None if even evicting
+        all of them would not."""
+        prio = podu.priority_of(pod)
+        want = podu.resource_limit(pod, node.resource)
+        need = self._used(node.name, node.resource, (podu.ns_of(pod), podu.name_of(pod))) + \
+            self._nominated(node.name, node.resource, pod) + want - node.capacity
+        cands = sorted((p for p in self.pods.values()
+                        if podu.node_of(p) == node.name and not podu.is_terminating(p)
+                        and p["status"].get("phase") not in ("Succeeded", "Failed")
+                        and podu.priority_of(p) < prio
+                        and podu.resource_limit(p, node.resource) > 0),
+                       key=lambda p: (podu.priority_of(p),
+                                      p["metadata"].get("creationTimestamp", "")))
+        out: List[dict] = []
+        for p in cands:
+            if need <= 0:
+                break
+            out.append(p)
+            need -= podu.resource_limit(p, node.resource)
+        return out if need <= 0 else None
+
+    def _preempt(self, pod: dict, nodes: List[FakeNode]) -> str:
+        """Default preemption: on the node where it costs least (lowest highest-victim
+        priority, then fewest victims), evict lower-priority Pods with a DisruptionTarget
+        condition and their own grace period, and nominate the node for ``pod``; it is bound
+        when the victims are gone (the retry on freed capacity). Returns the message suffix."""
+        if podu.nominated_node(pod):
+            return f"; waiting for preemption on {podu.nominated_node(pod)}"
+        best = None
+        for n in nodes:
+            v = self._victims(pod, n)
+            if v:
+                cost = (max(podu.priority_of(p) for p in v), len(v))
+                if best is None or cost < best[0]:
+                    best = (cost, n, v)
+        if best is None:
+            return "; preemption: no lower-priority victims would make room"
+        _, node, victims = best
+        pod["status"]["nominatedNodeName"] = node.name
+        for v in victims:
+            conds = v["status"].setdefault("conditions", [])
+            conds.append({"type": "DisruptionTarget", "status": "True",
+                          "reason": "PreemptionByScheduler",
+                          "message": f"{podu.ns_of(pod)}: preempting to accommodate a higher "
+                                     f"priority pod", "lastTransitionTime": _now()})
+            self._bump("MODIFIED", v)
+            self.preemptions += 1
+            self.victims = self.victims[-999:] + [podu.jcopy(v)]
+            _log.info("preempting %s/%s (priority %d) for %s/%s (priority %d)",
+                      podu.ns_of(v), podu.name_of(v), podu.priority_of(v), podu.ns_of(pod),
+                      podu.name_of(pod), podu.priority_of(pod))
+            self.delete(podu.ns_of(v), podu.name_of(v))
+        return f"; preempting {len(victims)} pod(s) on {node.name}"
+
     async def _sleep(self, ms: float) -> None:
         if ms > 0:
             await asyncio.sleep(ms / 1e3)
@@ -344,22 +479,29 @@ class FakeCluster:
         else:
             sel = pod["spec"].get("nodeSelector", {}) or {}
             node_name = ""
-            for n in self.nodes.values():
-                if not all(n.labels.get(k) == v for k, v in sel.items()):
-                    continue
+            fits = [n for n in self.nodes.values()
+                    if all(n.labels.get(k) == v for k, v in sel.items())]
+            for n in fits:
                 want = podu.resource_limit(pod, n.resource)
-                if self._used(n.name, n.resource, (ns, name)) + want <= n.capacity:
+                if self._used(n.name, n.resource, (ns, name)) + \
+                        self._nominated(n.name, n.resource, pod) + want <= n.capacity:
                     node_name = n.name
                     break
             if not node_name:
+                why = "insufficient resources"
+                if pod["spec"].get("preemptionPolicy", "PreemptLowerPriority") != "Never":
+                    why += self._preempt(pod, fits)
+                elif any(self._victims(pod, n) is not None for n in fits):
+                    why += "; preemption is not allowed for this Pod (preemptionPolicy Never)"
                 pod["status"]["conditions"] = [{
                     "type": "PodScheduled", "status": "False", "reason": "Unschedulable",
-                    "message": "0/%d nodes are available: insufficient resources" % len(self.nodes),
+                    "message": "0/%d nodes are available: %s" % (len(self.nodes), why),
                     "lastTransitionTime": _now()}]
                 self._unschedulable.add((ns, name))
                 self._bump("MODIFIED", pod)
                 return
             pod["spec"]["nodeName"] = node_name
+            pod["status"].pop("nominatedNodeName", None)
         self._unschedulable.discard((ns, name))
         pod["status"]["conditions"] = [{"type": "PodScheduled", "status": "True",
                                         "lastTransitionTime": _now()}]
@@ -626,6 +768,8 @@ class FakeCluster:
         r.add_post("/api/v1/namespaces/{ns}/events", self._h_event_create)
         r.add_get("/api/v1/namespaces/{ns}/events", self._h_event_list)
         r.add_get("/healthz", self._h_healthz)
+        r.add_get("/apis/scheduling.k8s.io/v1/priorityclasses", self._h_pc_list)
+        r.add_get("/apis/scheduling.k8s.io/v1/priorityclasses/{name}", self._h_pc_get)
         self.dra.install(r, self._pre)
         return app
 
@@ -805,6 +949,7 @@ class FakeCluster:
             md = pod.setdefault("metadata", {})
             md["namespace"] = ns
             md.setdefault("uid", str(uuid.uuid4()))
+            self._priority_admit(pod)
             self._quota_admit(ns, pod)
             pod["status"] = {"phase": "Pending"}
             return web.json_response(pod, status=201)
@@ -932,6 +1077,22 @@ class FakeCluster:
         return web.json_response({"kind": "ResourceQuotaList",
                                   "metadata": {"resourceVersion": str(self.rv)},
                                   "items": items})
+
+    async def _h_pc_get(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        pc = self.priority_classes.get(req.match_info["name"])
+        if pc is None:
+            return web.json_response(
+                {"kind": "Status", "status": "Failure", "reason": "NotFound", "code": 404,
+                 "message": f'priorityclasses.scheduling.k8s.io "{req.match_info["name"]}" '
+                            "not found"}, status=404)
+        return web.json_response(pc)
+
+    async def _h_pc_list(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        return web.json_response({"kind": "PriorityClassList",
+                                  "apiVersion": "scheduling.k8s.io/v1",
+                                  "items": list(self.priority_classes.values())})
 
     async def _h_nodes(self, req: web.Request) -> web.Response:
         await self._pre(req)

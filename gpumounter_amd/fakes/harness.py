@@ -20,6 +20,7 @@ from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional
 
 import aiohttp
+import yaml
 from aiohttp import web
 
 from gpumounter_amd.fakes.apiserver import FakeCluster, LatencyModel
@@ -29,6 +30,16 @@ from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.master.app import ANN_WIRE_PORT, ANN_WORKER_PORT, Master
 from gpumounter_amd.utils.config import Config
 from gpumounter_amd.worker.server import Worker
+
+
+_DEPLOY_PRIORITY = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))), "deploy", "placeholder-priority.yaml")
+
+
+def deploy_priority_classes() -> List[dict]:
+    """The PriorityClass objects of the shipped deploy."""
+    with open(_DEPLOY_PRIORITY, encoding="utf-8") as fh:
+        return [d for d in yaml.safe_load_all(fh) if d]
 
 
 @dataclass
@@ -55,8 +66,11 @@ class LocalCluster:
                  kubelet_rate_limit: Optional[tuple] = (100.0, 10),
                  kubelet_limit_mode: str = "enforce", gpu_api: str = "device-plugin",
                  app_hook: Optional[Callable[[web.Application], None]] = None,
-                 kernel_fs_dir: str = "") -> None:
+                 kernel_fs_dir: str = "", priority_classes: bool = True) -> None:
         self.n_nodes = n_nodes
+        # apply the shipped deploy's PriorityClasses (deploy/placeholder-priority.yaml), as
+        # `kubectl apply -k deploy/` does; False: a cluster where they were never applied
+        self.priority_classes = priority_classes
         self.kernel_fs_dir = kernel_fs_dir     # see FakeNode; removed by stop()
         self.amdsmi_lib = amdsmi_lib
         self.cgroup_mode = cgroup_mode
@@ -103,6 +117,8 @@ class LocalCluster:
         port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
         self.api_url = f"http://127.0.0.1:{port}"
         self.cluster.loop = asyncio.get_running_loop()
+        if self.priority_classes:
+            self.cluster.apply_priority_classes(deploy_priority_classes())
         for i in range(self.n_nodes):
             await self._add_node(f"node-{i}")
         if self.start_master:

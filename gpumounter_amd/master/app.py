@@ -236,14 +236,20 @@ class WorkerDirectory:
         """One worker call over gm-wire when the worker offers it, else gRPC. Failures raise
         one of :data:`RPC_ERRORS`."""
         wt = self._wire_of.get(target)
+        # one deadline for every attempt, as gRPC's retry policy keeps one for the call
+        deadline = time.monotonic() + timeout
         if wt is not None and self._wire_down.get(wt, 0.0) <= time.monotonic():
             _, _, resp_cls, mid = _METHODS[method]
             ch = self.wire_channel(wt)
             payload = req.SerializeToString()
             attempts = self.ADD_ATTEMPTS if method == "add" else 1
             for i in range(attempts):
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    raise wire.WireError(grpc.StatusCode.DEADLINE_EXCEEDED,
+                                         f"no answer from {wt} within {timeout:g}s")
                 try:
-                    return resp_cls.FromString(await ch.call(mid, payload, timeout))
+                    return resp_cls.FromString(await ch.call(mid, payload, left))
                 except wire.WireError as e:
                     if e.code() != grpc.StatusCode.UNAVAILABLE:
                         raise
@@ -256,8 +262,13 @@ class WorkerDirectory:
                     if i == attempts - 1:
                         raise
                     # the idempotency key makes a repeated AddGPU replay the first one
-                    await asyncio.sleep(min(0.05 * 2 ** i, 1.0))
-        return await self._stub(target, method)(req, timeout=timeout)
+                    await asyncio.sleep(min(0.05 * 2 ** i, 1.0,
+                                            max(deadline - time.monotonic(), 0.0)))
+        left = deadline - time.monotonic()
+        if left <= 0:
+            raise wire.WireError(grpc.StatusCode.DEADLINE_EXCEEDED,
+                                 f"no answer from {target} within {timeout:g}s")
+        return await self._stub(target, method)(req, timeout=left)
 
 
 def _read(path: str) -> bytes:
@@ -571,6 +582,9 @@ class Master:
         route = "addgpu"
         mi = request.match_info
         ns, name = mi["namespace"], mi["pod"]
+        bad = podu.name_error(ns, name)
+        if bad is not None:
+            return self._reply(request, route, 400, bad, {})
         with trace.span("master_authz"):
             denied = await self._denied(request, route, "create", ns, name=name)
         if denied is not None:
@@ -606,6 +620,9 @@ class Master:
         route = "removegpu"
         mi = request.match_info
         ns, name = mi["namespace"], mi["pod"]
+        bad = podu.name_error(ns, name)
+        if bad is not None:
+            return self._reply(request, route, 400, bad, {})
         with trace.span("master_authz"):
             denied = await self._denied(request, route, "delete", ns, name=name)
         if denied is not None:
@@ -681,6 +698,10 @@ class Master:
             try:
                 kind = op["op"]
                 ns, name = op.get("namespace", "default"), op["pod"]
+                bad = podu.name_error(ns, name) if isinstance(ns, str) and \
+                    isinstance(name, str) else "namespace and pod must be strings"
+                if bad is not None:
+                    return 400, bad, {}
                 user = request.get(USER_KEY, "")
                 if self.authz.mode == "kube":   # per operation: namespaces may differ
                     d = await self.authz.check(request.headers,
@@ -729,6 +750,8 @@ class Master:
 
     async def node_gpus(self, request: Request) -> Response:
         node = request.match_info["node"]
+        if not podu.is_dns1123_subdomain(node):
+            return httpd.json_response({"error": f"invalid node name {node!r}"}, status=400)
         denied = await self._denied(request, "nodegpus", "get", resource="nodes", name=node)
         if denied is not None:
             return denied
@@ -745,6 +768,9 @@ class Master:
 
     async def pod_gpus(self, request: Request) -> Response:
         ns, name = request.match_info["namespace"], request.match_info["pod"]
+        bad = podu.name_error(ns, name)
+        if bad is not None:
+            return httpd.json_response({"error": bad}, status=400)
         denied = await self._denied(request, "podgpus", "get", ns, name=name)
         if denied is not None:
             return denied

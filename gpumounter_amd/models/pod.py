@@ -154,6 +154,19 @@ def is_terminating(pod: dict) -> bool:
     return bool(meta(pod).get("deletionTimestamp"))
 
 
+def priority_of(pod: dict) -> int:
+    """``spec.priority`` as the Priority admission plugin resolved it (0 when absent)."""
+    try:
+        return int(pod.get("spec", {}).get("priority") or 0)
+    except (TypeError, ValueError):
+        return 0
+
+
+def nominated_node(pod: dict) -> str:
+    """The node the scheduler reserved for a Pod whose preemption is under way."""
+    return pod.get("status", {}).get("nominatedNodeName", "") or ""
+
+
 def resource_limit(pod: dict, resource: str) -> int:
     total = 0
     for c in pod.get("spec", {}).get("containers", []) or []:
@@ -172,3 +185,27 @@ def jcopy(x):
     if t is list:
         return [jcopy(v) for v in x]
     return x
+
+
+_DNS1123_LABEL = re.compile(r"[a-z0-9]([-a-z0-9]*[a-z0-9])?")
+_DNS1123_SUBDOMAIN = re.compile(r"[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*")
+
+
+def is_dns1123_label(s: str) -> bool:
+    """A namespace name (Kubernetes ``IsDNS1123Label``: ≤ 63 chars of [a-z0-9-])."""
+    return len(s) <= 63 and bool(_DNS1123_LABEL.fullmatch(s))
+
+
+def is_dns1123_subdomain(s: str) -> bool:
+    """A Pod or node name (``IsDNS1123Subdomain``: ≤ 253 chars, dot-separated labels)."""
+    return len(s) <= 253 and bool(_DNS1123_SUBDOMAIN.fullmatch(s))
+
+
+def name_error(ns: str, name: str) -> Optional[str]:
+    """Why ``ns``/``name`` cannot name a Pod (None: they can). Such a request is refused
+    before anything else looks at it: no name the apiserver would refuse reaches a URL."""
+    if not is_dns1123_label(ns):
+        return f"Invalid param namespace: {ns!r}(must be a DNS-1123 label)"
+    if not is_dns1123_subdomain(name):
+        return f"Invalid param pod: {name!r}(must be a DNS-1123 subdomain)"
+    return None

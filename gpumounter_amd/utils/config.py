@@ -63,11 +63,28 @@ class Config:
     dra_bdf_attribute: str = "pciAddr"    # ResourceSlice device attribute holding the PCI BDF
     placeholder_image: str = "registry.k8s.io/pause:3.9"  # placeholder container image
     placeholder_pull_policy: str = "IfNotPresent"  # no registry round trip per attach
-    placeholder_priority_class: str = ""  # PriorityClass of placeholders ("" = none)
+    # The floor PriorityClass of placeholders (deploy/placeholder-priority.yaml: value 1000000,
+    # preemptionPolicy Never). A placeholder backs a GPU its tenant is using, so it must never
+    # rank below that tenant: it gets this class, or the tenant's own class when the tenant
+    # ranks higher (placeholder_priority_inherit). If the class does not exist in the cluster
+    # the tenant's class is used ("" = no floor: always the tenant's class). The reference sets
+    # no priority (allocator.go:189-234): any higher-priority amd.com/gpu Pod could preempt a
+    # slave pod and take a GPU out from under its running tenant.
+    placeholder_priority_class: str = "gpumounter-placeholder"
+    placeholder_priority_inherit: bool = True  # tenants above the floor: their own class
+    # The floor class's value when the worker may not read PriorityClasses (RBAC) — it reads it
+    # from the apiserver otherwise
+    placeholder_priority_value: int = 1000000
     # Warm pool: standby placeholders that keep this many GPUs per node pre-admitted for
     # hot-mount (0 = off, the reference's behaviour). Claiming is a metadata patch, so attach
     # latency no longer includes scheduling + kubelet admission; the price is reserved capacity.
     warm_pool_size: int = 0
+    # PriorityClass of standby placeholders ("" = placeholder_priority_class: standbys are not
+    # preemptible and a claim keeps the pool's latency). A lower class (gpumounter-standby,
+    # value -10) lets higher-priority Pods preempt idle standbys; because Pod priority is
+    # immutable, an attach then cannot keep a low standby: it yields it (DELETE) and books the
+    # GPU with a placeholder at tenant priority — the cold path's latency (docs/CONFIG.md)
+    pool_priority_class: str = ""
     # --- kubelet PodResources --------------------------------------------------------------
     kubelet_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"  # PodResources API
     kubelet_timeout_s: float = 10.0    # per PodResources call (reference: types.go:7)

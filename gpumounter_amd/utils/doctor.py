@@ -217,12 +217,45 @@ async def _check_apiserver(cfg) -> List[Check]:
         return [Check("apiserver", "fail", f"no credentials: {e}")]
     try:
         pods, _ = await kube.list_pods(cfg.pool_namespace)
-        return [Check("apiserver", "ok", f"{kube.base}: {len(pods)} pod(s) in "
-                                         f"{cfg.pool_namespace}")]
+        out = [Check("apiserver", "ok", f"{kube.base}: {len(pods)} pod(s) in "
+                                        f"{cfg.pool_namespace}")]
     except Exception as e:  # noqa: BLE001
+        await kube.close()
         return [Check("apiserver", "fail", f"{kube.base}: {e}")]
+    try:
+        return out + await _check_priority(cfg, kube)
     finally:
         await kube.close()
+
+
+async def _check_priority(cfg, kube) -> List[Check]:
+    """The placeholders' floor PriorityClass exists (and the pool's, when one is set). Without
+    it placeholders rank as their tenants do, and a higher-priority Pod can preempt a
+    placeholder — revoking a GPU a tenant is using."""
+    from gpumounter_amd.cluster.kube import NotFound
+
+    out = []
+    for what, name in (("placeholder", cfg.placeholder_priority_class),
+                       ("pool", getattr(cfg, "pool_priority_class", ""))):
+        if not name:
+            if what == "placeholder":
+                out.append(Check("priority", "warn", "no placeholder_priority_class: "
+                                 "placeholders rank as their tenants"))
+            continue
+        try:
+            pc = await kube.get_priority_class(name)
+        except NotFound:
+            out.append(Check("priority", "fail", f"{what} PriorityClass {name} missing "
+                                                 f"(kubectl apply -f deploy/placeholder-"
+                                                 f"priority.yaml)"))
+            continue
+        except Exception as e:  # noqa: BLE001
+            out.append(Check("priority", "warn", f"{what} PriorityClass {name}: {e}"))
+            continue
+        out.append(Check("priority", "ok", f"{what} PriorityClass {name}: value "
+                                           f"{pc.get('value')}, preemptionPolicy "
+                                           f"{pc.get('preemptionPolicy', 'PreemptLowerPriority')}"))
+    return out
 
 
 def check_gpus(cfg, burn_in_s: float = 0.0) -> List[Check]:

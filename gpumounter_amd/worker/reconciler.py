@@ -107,6 +107,7 @@ class Reconciler:
         self._guard_task = None
         self._guard_timer = None
         self._guard_running: Optional[asyncio.Task] = None   # one pass at a time
+        self._why: Dict[Tuple[str, str], str] = {}   # owner → cause of a pending revocation
 
     # ------------------------------------------------------------------------ events
     def watch_events(self) -> None:
@@ -128,19 +129,42 @@ class Reconciler:
         md = ph["metadata"]
         ann = md.get("annotations") or {}
         if ann.get("gpumounter.amd.com/mount-mode") in ("standby", "draining"):
-            return   # pool capacity / a drain: no tenant has access to revoke
+            # pool capacity / a drain: no tenant has access to revoke. A standby preempted by a
+            # higher-priority Pod (low pool_priority_class) is made up from what is free
+            if ann.get("gpumounter.amd.com/mount-mode") == "standby":
+                self._poke_pool()
+            return
         ons = (md.get("labels") or {}).get("gpumounter.amd.com/owner-namespace", "")
         oname = ann.get("gpumounter.amd.com/owner-name", "")
         if oname:
-            _log.warning("placeholder %s/%s deleted externally; revoking from %s/%s",
-                         md.get("namespace"), md.get("name"), ons, oname)
+            preempted = any(c.get("type") == "DisruptionTarget" and
+                            c.get("reason") == "PreemptionByScheduler"
+                            for c in (ph.get("status") or {}).get("conditions") or [])
+            if preempted:
+                # only a placeholder that ranks below a pending Pod can be a victim: the floor
+                # PriorityClass is missing or was overridden (utils/doctor.py checks it)
+                _log.error("placeholder %s/%s was PREEMPTED by the scheduler; revoking from "
+                           "%s/%s", md.get("namespace"), md.get("name"), ons, oname)
+                self.svc.metrics.reconcile_actions.labels(action="placeholder_preempted").inc()
+                self._why[(ons, oname)] = "placeholder preempted by the scheduler"
+            else:
+                _log.warning("placeholder %s/%s deleted externally; revoking from %s/%s",
+                             md.get("namespace"), md.get("name"), ons, oname)
             self._kick(("revoke", ons, oname))
+
+    def _poke_pool(self) -> None:
+        pool = getattr(self.svc, "pool", None)
+        if pool is not None and pool.enabled:
+            pool.poke()
 
     def _on_node_pod(self, etype: str, pod: dict) -> None:
         if etype == "RELIST":
             self.wake()
             return
         if etype == "DELETED" or podu.phase_of(pod) in ("Succeeded", "Failed"):
+            pool = getattr(self.svc, "pool", None)
+            if pool is not None and pool.enabled and pool.exhausted:
+                self._poke_pool()           # capacity freed on this node: refill the pool
             if self.svc.ph.owned_by(pod, candidates=True):
                 self._kick(("release", podu.ns_of(pod), podu.name_of(pod), podu.uid_of(pod)))
         elif etype == "MODIFIED" and self._restarted(pod):
@@ -317,10 +341,11 @@ class Reconciler:
                     fixed = await svc.reconcile_pod(owner)
                     gone = sorted({i.path for i in fixed if i.kind.startswith("stale")})
                     back = sorted({i.path for i in fixed if i.kind.startswith("missing")})
+                    why = self._why.pop((ns, name), "placeholder deleted outside gpumounter")
                     if gone:
                         svc.notify.event(owner, "GPURevoked",
-                                         f"placeholder deleted outside gpumounter; access "
-                                         f"revoked: {', '.join(gone)}", warning=True)
+                                         f"{why}; access revoked: {', '.join(gone)}",
+                                         warning=True)
                     if back and key[0] == "reinject":
                         svc.notify.event(owner, "GPUReinjected",
                                          f"container restarted; hot-mounted devices restored: "

@@ -363,6 +363,7 @@ class Worker:
             self.reconciler.start_guard()
         if self.plugin is not None:
             await self.plugin.start()
+        await self.placeholders.resolve_priority()
         await self.pool.start()
         if self.cfg.metrics_period_s > 0:
             self._collector = asyncio.ensure_future(self._collect_loop())

@@ -455,6 +455,7 @@ class GpuMountService:
                 for g in gs]
 
     SLOW_ATTACH_MS = 50.0
+    YIELD_RETRY_S = 0.05     # after yielding standbys: the kubelet's teardown of them
 
     def _count_error(self, op: str, e: BaseException) -> None:
         """RPCs that end in a gRPC error count under its status name (RESOURCE_EXHAUSTED = quota,
@@ -492,7 +493,14 @@ class GpuMountService:
             self.metrics.observe_trace("attach", root)
         return resp
 
+    @staticmethod
+    def _check_names(req) -> None:
+        bad = podu.name_error(req.namespace, req.pod_name)
+        if bad is not None:
+            raise RpcError(grpc.StatusCode.INVALID_ARGUMENT, bad)
+
     async def _add_gpu(self, req):
+        self._check_names(req)
         n = int(req.gpu_num)
         if n <= 0 or n > self.cfg.max_gpus_per_request:
             raise RpcError(grpc.StatusCode.INVALID_ARGUMENT, f"invalid gpu_num {n}")
@@ -730,14 +738,19 @@ class GpuMountService:
                                 preferred: List[str], n_free: int, lease_exp: float = 0.0):
         claimed = None
         create_pref = preferred
-        if self.pool is not None and self.pool.enabled and self.pool.standby():
-            plan = self._plan_with_pool(n, st)
+        # standbys this Pod may claim: those that rank at least as high as a placeholder of
+        # its own would (cluster/placeholder.py priority_for; priority is immutable)
+        rank = self.ph.priority_for(pod)[1]
+        pool_on = self.pool is not None and self.pool.enabled
+        if pool_on and self.pool.standby(rank):
+            plan = self._plan_with_pool(n, st, rank)
             if plan is not None and plan[0]:
                 claim_idx, plan_pref = plan
                 claimed = await self.pool.claim(pod, len(claim_idx), req.is_entire_mount,
                                                 st.hot + st.own, log.request_id.get(),
                                                 req.container, req.idempotency_key,
-                                                want=claim_idx, lease_expires=lease_exp)
+                                                want=claim_idx, lease_expires=lease_exp,
+                                                min_priority=rank)
                 if claimed is not None:
                     create_pref = plan_pref
         got = len(claimed.placeholders) if claimed else 0
@@ -754,6 +767,20 @@ class GpuMountService:
                 # tenant-namespace placeholders: holding every free GPU can exceed the
                 # tenant's quota although the request fits; reserve it plainly instead
                 _log.info("trim refused by the tenant's quota (%s); plain reservation", e)
+        yielded = []
+        if pool_on and n - got > 0:
+            free_now = self._free(st)
+            if len(free_now) < n - got:
+                # the rest is held by standbys that rank below this Pod: give them back to the
+                # scheduler and book their GPUs at this Pod's rank instead
+                yielded = await self.pool.yield_low(n - got - len(free_now), rank,
+                                                    st.hot + st.own)
+                if yielded:
+                    keys = self.inv.by_key()
+                    back = [keys[normalize_device_id(ph.device_ids[0])] for ph in yielded
+                            if normalize_device_id(ph.device_ids[0]) in keys]
+                    preferred = planning.preferred(self.inv, self.cfg.topology_policy, n - got,
+                                                   st, free_now + back)
         token = ""
         if self.plugin is not None and preferred:
             # our own device plugin answers GetPreferredAllocation for these placeholders
@@ -761,11 +788,23 @@ class GpuMountService:
             for ids in ([preferred] if req.is_entire_mount else [[d] for d in preferred]):
                 self.plugin.intend(ids, token)
         try:
-            rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
-                                         attach_id=log.request_id.get(),
-                                         container=req.container,
-                                         idempotency_key=req.idempotency_key,
-                                         lease_expires=lease_exp)
+            try:
+                rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
+                                             attach_id=log.request_id.get(),
+                                             container=req.container,
+                                             idempotency_key=req.idempotency_key,
+                                             lease_expires=lease_exp)
+            except InsufficientGPU:
+                if not yielded:
+                    raise
+                # a kubelet that has not torn the yielded standbys down yet refuses their
+                # devices at admission (UnexpectedAdmissionError): once more, a moment later
+                await asyncio.sleep(self.YIELD_RETRY_S)
+                rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
+                                             attach_id=log.request_id.get(),
+                                             container=req.container,
+                                             idempotency_key=req.idempotency_key,
+                                             lease_expires=lease_exp)
         except BaseException:
             if claimed:
                 await self.pool.give_back(claimed.placeholders)
@@ -788,9 +827,9 @@ class GpuMountService:
         else:
             await self.ph.release(phs)
 
-    def _plan_with_pool(self, n: int, st: PodGpuState):
-        return planning.plan_with_pool(self.inv, self.cfg.topology_policy, self.pool.standby(),
-                                       n, st, self._free(st))
+    def _plan_with_pool(self, n: int, st: PodGpuState, rank: Optional[int] = None):
+        return planning.plan_with_pool(self.inv, self.cfg.topology_policy,
+                                       self.pool.standby(rank), n, st, self._free(st))
 
     async def _reserve_trim(self, pod: dict, n: int, req, st: PodGpuState, width: int,
                             lease_exp: float = 0.0):
@@ -845,6 +884,7 @@ class GpuMountService:
         return resp
 
     async def _remove_gpu(self, req):
+        self._check_names(req)
         with trace.span("pod_lookup"):
             self.faults.check("pod_lookup")
             pod = await self.get_pod(req.namespace, req.pod_name)

@@ -77,7 +77,7 @@ def test_rbac_is_least_privilege():
     resources = {r for role in roles for rule in role["rules"] for r in rule["resources"]}
     assert resources <= {"pods", "pods/finalizers", "nodes", "events", "tokenreviews",
                          "subjectaccessreviews", "resourcequotas", "resourceclaims",
-                         "resourceslices"}
+                         "resourceslices", "priorityclasses"}
     assert {v for role in roles for rule in role["rules"] if "pods/finalizers" in
             rule["resources"] for v in rule["verbs"]} == {"update"}
     dra = [rule for role in roles for rule in role["rules"]
@@ -200,10 +200,11 @@ def test_cluster_role_grants_every_api_call_the_daemons_make():
         "get_quota": ("", "resourcequotas", "get"),
         "watch_quotas": ("", "resourcequotas", "watch"),
         "create_event": ("", "events", "create"),
+        "get_priority_class": ("scheduling.k8s.io", "priorityclasses", "get"),
     }
     calls = {n for n, f in inspect.getmembers(KubeClient)
              if (inspect.iscoroutinefunction(f) or inspect.isasyncgenfunction(f))
-             and not n.startswith("_") and n not in ("close", "watch")}
+             and not n.startswith("_") and n not in ("close", "watch", "list_pages")}
     assert calls == set(needs), ("map new KubeClient calls to their RBAC verb",
                                  calls ^ set(needs))
     docs = list(yaml.safe_load_all(open(os.path.join(ROOT, "deploy", "rbac.yaml"))))

@@ -16,9 +16,11 @@ invariants after *every* step:
 Rules: attach (single or entire mount, with or without a lease), detach, force-remove, let
 time pass (leases end), a container restart, a watch relist (410 Gone), the kubelet's status
 churn on every placeholder, a worker restart, an attach or detach with one of those events in
-flight (and a container restart that only a relist carries), and a lost or failed reply on the
-next one or two of POST / PATCH / DELETE / GET. Variants: the device-plugin ledger, the warm
-pool, DRA with a warm pool, trim placement with a warm pool.
+flight (and a container restart that only a relist carries), a lost or failed reply on the
+next one or two of POST / PATCH / DELETE / GET, and a Pod that outranks every tenant arriving
+for GPUs (the scheduler may preempt idle standbys, never a tenant's placeholder). Variants: the
+device-plugin ledger, the warm pool, DRA with a warm pool, trim placement with a warm pool, a
+warm pool whose standbys are preemptible (low ``pool_priority_class``).
 
 The reference has no locking and no recovery at all (pkg/server/gpu-mount/server.go:34-179,
 SURVEY defect 7). Round-4 bug parents this model fails on: ``bench/model_parents.sh``
@@ -37,6 +39,7 @@ from hypothesis import strategies as st
 from hypothesis.stateful import RuleBasedStateMachine, invariant, rule
 
 from gpumounter_amd.fakes.harness import ThreadedCluster
+from gpumounter_amd.models import pod as podu
 
 TENANTS = ("x0", "x1", "x2")
 LEASE = "gpumounter.amd.com/lease-expires"
@@ -82,6 +85,8 @@ class LedgerModel(RuleBasedStateMachine):
         self.leases = {t: {} for t in TENANTS}        # uuid → (not before, not after, holder)
         self.certain = {t: True for t in TENANTS}
         self.steps = []
+        # a Pod class above every tenant's (they have none: priority 0), below the placeholders'
+        self.lc.cluster.add_priority_class("model-high", 1000)
         pool = self.VARIANT.get("worker_overrides", {}).get("warm_pool_size", 0)
         if pool:
             self._until(lambda: len(self._worker().pool.standby()) >= pool, 20)
@@ -293,6 +298,36 @@ class LedgerModel(RuleBasedStateMachine):
         target = f"127.0.0.1:{w.grpc_port}"
         self._until(lambda: self.lc.master.workers.target("node-0") == target, 10)
 
+    @rule(n=st.integers(1, 3))
+    def preemptor_arrives(self, n):
+        """A Pod that outranks every tenant asks for ``n`` GPUs on the node, then goes away. It
+        may get free GPUs, or (low pool class) preempt idle standbys; it must never preempt a
+        placeholder that books a tenant's GPU — the invariant then sees the revocation."""
+        c = self.lc.cluster
+        name = f"hp-{len(self.steps)}"
+        seen = c.preemptions
+
+        def arrive():
+            return c.create_pod("default", {
+                "metadata": {"name": name},
+                "spec": {"priorityClassName": "model-high",
+                         "nodeSelector": {"kubernetes.io/hostname": "node-0"},
+                         "containers": [{"name": "c", "image": "x:1", "resources": {
+                             "limits": {"amd.com/gpu": str(n)}}}]}})
+        hp = self.tc.call(_sync(arrive))
+        self._until(lambda: podu.node_of(hp) or (podu.is_unschedulable(hp) and
+                                                 not podu.nominated_node(hp)), 3)
+        victims = c.victims[len(c.victims) - (c.preemptions - seen):] \
+            if c.preemptions > seen else []
+        self.steps.append(f"preemptor wants {n} → "
+                          f"{'bound' if podu.node_of(hp) else 'pending'}, "
+                          f"{len(victims)} victim(s)")
+        booked = [v["metadata"]["name"] for v in victims
+                  if (v["metadata"].get("labels") or {}).get("app") == "gpu-pool"
+                  and (v["metadata"].get("annotations") or {}).get(MODE) != "standby"]
+        check(not booked, f"placeholders of tenants preempted: {booked}; steps {self.steps}")
+        self.tc.call(_sync(c.delete, "default", name, 0))
+
     @rule(faults=st.lists(st.tuples(st.sampled_from(["POST", "PATCH", "DELETE", "GET"]),
                                     st.booleans()), min_size=1, max_size=2))
     def lost_reply(self, faults):
@@ -389,3 +424,6 @@ TestLedgerDraPool = _case("LedgerDraPool", {"gpu_api": "dra",
                                             "worker_overrides": {"warm_pool_size": 2}})
 TestLedgerTrimPool = _case("LedgerTrimPool", {"worker_overrides": {
     "warm_pool_size": 2, "placement_enforce": "trim"}})
+# idle standbys preemptible (gpumounter-standby, value -10); attaches yield them
+TestLedgerLowPool = _case("LedgerLowPool", {"worker_overrides": {
+    "warm_pool_size": 2, "pool_priority_class": "gpumounter-standby"}})
