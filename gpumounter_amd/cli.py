@@ -192,14 +192,31 @@ def client_token(args) -> str:
     return ""
 
 
-async def _http(method: str, url: str, data=None, token: str = "") -> int:
+def client_tls(args):
+    """How an https master is verified: against --ca / $GM_MASTER_CA, the system roots
+    otherwise; --insecure skips verification (labs only). None for http URLs."""
+    import ssl
+
+    if not getattr(args, "master", "").startswith("https://"):
+        return None
+    if getattr(args, "insecure", False):
+        return False
+    ca = getattr(args, "ca", "") or os.environ.get("GM_MASTER_CA", "")
+    return ssl.create_default_context(cafile=ca or None)
+
+
+async def _http(method: str, url: str, data=None, token: str = "", tls=None) -> int:
     import aiohttp
 
     headers = {"Accept": "application/json"}
     if token:
         headers["Authorization"] = f"Bearer {token}"
+        if url.startswith("http://") and not url.startswith(("http://127.", "http://localhost")):
+            print("warning: sending a bearer token over plain HTTP; use the master's https:// "
+                  "URL", file=sys.stderr)
     async with aiohttp.ClientSession() as s:
-        async with s.request(method, url, data=data, headers=headers) as r:
+        async with s.request(method, url, data=data, headers=headers,
+                             ssl=tls if tls is not None else True) as r:
             body = await r.text()
             print(body)
             if r.status == 401 and not token:
@@ -216,7 +233,7 @@ def cmd_add(args) -> int:
     q = {k: v for k, v in (("container", args.container), ("lease", args.lease)) if v}
     if q:
         url += "?" + urlencode(q)
-    return asyncio.run(_http("GET", url, token=client_token(args)))
+    return asyncio.run(_http("GET", url, token=client_token(args), tls=client_tls(args)))
 
 
 def cmd_remove(args) -> int:
@@ -227,7 +244,7 @@ def cmd_remove(args) -> int:
     data = aiohttp.FormData()
     for u in args.uuid:
         data.add_field("uuids", u)
-    return asyncio.run(_http("POST", url, data, token=client_token(args)))
+    return asyncio.run(_http("POST", url, data, token=client_token(args), tls=client_tls(args)))
 
 
 def cmd_status(args) -> int:
@@ -235,7 +252,7 @@ def cmd_status(args) -> int:
         url = f"{args.master.rstrip('/')}/api/v1/namespaces/{args.ns}/pods/{args.pod}/gpus"
     else:
         url = f"{args.master.rstrip('/')}/api/v1/nodes/{args.node}/gpus"
-    return asyncio.run(_http("GET", url, token=client_token(args)))
+    return asyncio.run(_http("GET", url, token=client_token(args), tls=client_tls(args)))
 
 
 def disassemble(insns: List[int]) -> List[str]:
@@ -340,6 +357,10 @@ def build_parser() -> argparse.ArgumentParser:
                        "$GM_TOKEN, --token-file, the service-account token, the kubeconfig "
                        "user's token)")
         p.add_argument("--token-file", default="")
+        p.add_argument("--ca", default="", help="CA bundle that signed the master's HTTPS "
+                       "certificate (default: $GM_MASTER_CA, else the system roots)")
+        p.add_argument("--insecure", action="store_true",
+                       help="do not verify the master's HTTPS certificate (labs only)")
         if name == "add":
             p.add_argument("-n", type=int, required=True)
             p.add_argument("--entire", action="store_true")

@@ -20,6 +20,7 @@ control plane; the default is zero (pure plumbing).
 from __future__ import annotations
 
 import asyncio
+import base64
 import json
 import secrets
 import threading
@@ -174,6 +175,11 @@ class FakeCluster:
         self.add_priority_class("system-node-critical", 2000001000)
         self.preemptions = 0          # victims the scheduler evicted for a higher-priority Pod
         self.victims: List[dict] = []  # each victim as it was when preempted (last 1000)
+        # Pod LISTs: pages served, the largest response body, and a switch that makes the next
+        # continue tokens expire (410), as after an etcd compaction
+        self.list_pages = 0
+        self.max_list_bytes = 0
+        self.expire_continue = False
 
     # ------------------------------------------------------------------------ nodes
     def add_node(self, node: FakeNode) -> FakeNode:
@@ -858,9 +864,34 @@ class FakeCluster:
         fsel = _parse_selector(req.query.get("fieldSelector", ""))
         if req.query.get("watch") in ("true", "1"):
             return await self._watch(req, ns, lsel, fsel)
-        items = [p for p in self.pods.values() if self._matches(p, ns, lsel, fsel)]
-        return web.json_response({"kind": "PodList", "apiVersion": "v1",
-                                  "metadata": {"resourceVersion": str(self.rv)}, "items": items})
+        limit = int(req.query.get("limit", "0") or 0)
+        cont = req.query.get("continue", "")
+        rv, after = str(self.rv), None
+        if cont:
+            try:
+                tok = json.loads(base64.urlsafe_b64decode(cont.encode()))
+                rv, after = tok["rv"], tuple(tok["key"])
+            except (ValueError, KeyError, TypeError):
+                return web.json_response({"kind": "Status", "code": 400, "reason": "BadRequest",
+                                          "message": "invalid continue token"}, status=400)
+            if self.events and int(rv) < self.events[0][0] - 1 or self.expire_continue:
+                # the snapshot the token points into was compacted
+                return web.json_response(
+                    {"kind": "Status", "code": 410, "reason": "Expired",
+                     "message": "The provided continue parameter is too old to display a "
+                                "consistent list result."}, status=410)
+        keys = sorted(k for k, p in self.pods.items() if self._matches(p, ns, lsel, fsel)
+                      and (after is None or k > after))
+        md = {"resourceVersion": rv}
+        if limit and len(keys) > limit:
+            keys = keys[:limit]
+            md["continue"] = base64.urlsafe_b64encode(json.dumps(
+                {"rv": rv, "key": list(keys[-1])}).encode()).decode()
+        body = json.dumps({"kind": "PodList", "apiVersion": "v1", "metadata": md,
+                           "items": [self.pods[k] for k in keys]}).encode()
+        self.list_pages += 1
+        self.max_list_bytes = max(self.max_list_bytes, len(body))
+        return web.Response(body=body, content_type="application/json")
 
     async def _watch(self, req: web.Request, ns: str, lsel, fsel, history=None, watchers=None,
                      current=None, kind: str = "Pod") -> web.StreamResponse:

@@ -23,6 +23,7 @@ import json
 import os
 import shutil
 import signal
+import ssl
 import subprocess
 import sys
 import tempfile
@@ -37,10 +38,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 def _http(method: str, url: str, body: Optional[bytes] = None, headers: Optional[dict] = None,
-          timeout: float = 60.0) -> Tuple[int, bytes]:
+          timeout: float = 60.0, context: Optional[ssl.SSLContext] = None) -> Tuple[int, bytes]:
     req = urllib.request.Request(url, data=body, method=method, headers=headers or {})
     try:
-        with urllib.request.urlopen(req, timeout=timeout) as r:
+        with urllib.request.urlopen(req, timeout=timeout, context=context) as r:
             return r.status, r.read()
     except urllib.error.HTTPError as e:
         return e.code, e.read()
@@ -86,6 +87,8 @@ class ProcessCluster:
         self.worker_ports: Dict[str, Tuple[int, int]] = {}   # node → (grpc, metrics)
         self._worker_env: Dict[str, Dict[str, str]] = {}
         self.master_url = ""
+        self.ca = ""            # secure: the CA that signed the master's HTTPS certificate
+        self.tls: Optional[ssl.SSLContext] = None    # secure: verifies the master
         self._local = threading.local()   # one keep-alive connection to the master per thread
         self._conns: List[http.client.HTTPConnection] = []
 
@@ -95,8 +98,10 @@ class ProcessCluster:
         for attempt in (0, 1):
             conn = getattr(self._local, "conn", None)
             if conn is None:
-                host, port = self.master_url[len("http://"):].split(":")
-                conn = self._local.conn = http.client.HTTPConnection(host, int(port), timeout=120)
+                host, port = self.master_url.split("://", 1)[1].split(":")
+                conn = self._local.conn = http.client.HTTPSConnection(
+                    host, int(port), timeout=120, context=self.tls) if self.tls is not None \
+                    else http.client.HTTPConnection(host, int(port), timeout=120)
                 self._conns.append(conn)
             try:
                 conn.request(method, path, body=body, headers={**self._auth, **(headers or {})})
@@ -163,14 +168,19 @@ class ProcessCluster:
         with open(info_path) as fh:
             self.info = json.load(fh)
         api = self.info["api_url"]
-        tls_w, tls_m = {}, {"GM_AUTHZ_MODE": "none"}
+        tls_w, tls_m = {"GM_AUTHZ_MODE": "none"}, {"GM_AUTHZ_MODE": "none"}
         if self.secure:
             from gpumounter_amd.fakes.pki import make_pki
             pki = make_pki(os.path.join(self.workdir, "pki"))
             tls_w = {"GM_TLS_CERT": pki["worker.crt"], "GM_TLS_KEY": pki["worker.key"],
-                     "GM_TLS_CA": pki["ca"]}
-            tls_m = {"GM_TLS_CERT": pki["master.crt"], "GM_TLS_KEY": pki["master.key"],
                      "GM_TLS_CA": pki["ca"], "GM_AUTHZ_MODE": "kube"}
+            # the shipped master: HTTPS on its API port, callers' tokens reviewed
+            tls_m = {"GM_TLS_CERT": pki["master.crt"], "GM_TLS_KEY": pki["master.key"],
+                     "GM_TLS_CA": pki["ca"], "GM_AUTHZ_MODE": "kube",
+                     "GM_MASTER_TLS_CERT": pki["master-https.crt"],
+                     "GM_MASTER_TLS_KEY": pki["master-https.key"]}
+            self.ca = pki["ca"]
+            self.tls = ssl.create_default_context(cafile=self.ca)
             code, _ = _http("POST", f"{api}/_fake/user", json.dumps(
                 {"token": self.token, "user": "gm-hermetic-client",
                  "verbs": ["create", "delete", "get"], "resource": "pods/gpumount"}).encode(),
@@ -210,10 +220,17 @@ class ProcessCluster:
 
     def _start_master(self) -> None:
         self._spawn("master", [*self.entry, "master"], self._master_env)
-        self.master_url = f"http://127.0.0.1:{self._ready('master')['port']}"
+        scheme = "https" if self._master_env.get("GM_MASTER_TLS_CERT") else "http"
+        self.master_url = f"{scheme}://127.0.0.1:{self._ready('master')['port']}"
         for node in self.info["nodes"]:   # the master has discovered every worker
-            self._wait(f"master → {node}", lambda n=node: _http(
-                "GET", f"{self.master_url}/api/v1/nodes/{n}/gpus", headers=self._auth)[0] == 200)
+            self._wait(f"master → {node}", lambda n=node: self.http(
+                "GET", f"/api/v1/nodes/{n}/gpus", headers=self._auth)[0] == 200)
+
+    def http(self, method: str, path: str, body: Optional[bytes] = None,
+             headers: Optional[dict] = None, timeout: float = 60.0) -> Tuple[int, bytes]:
+        """One request to the master on a fresh connection (HTTPS verified against the
+        deployment's CA when secure)."""
+        return _http(method, self.master_url + path, body, headers, timeout, self.tls)
 
     def restart_master(self, sig: int = signal.SIGKILL,
                        env: Optional[Dict[str, str]] = None) -> None:
@@ -332,8 +349,8 @@ class ProcessCluster:
         return code, json.loads(body)
 
     def pod_gpus(self, ns: str, pod: str) -> Tuple[int, dict]:
-        code, body = _http("GET", f"{self.master_url}/api/v1/namespaces/{ns}/pods/{pod}/gpus",
-                           headers={"Accept": "application/json", **self._auth})
+        code, body = self.http("GET", f"/api/v1/namespaces/{ns}/pods/{pod}/gpus",
+                               headers={"Accept": "application/json", **self._auth})
         return code, json.loads(body)
 
     def kubelet_calls(self, node: str = "node-0") -> Dict[str, int]:
@@ -382,7 +399,8 @@ class ProcessCluster:
         return json.loads(body).get("items", []) if code == 200 else []
 
     def audit(self, ns: str, pod: str, node: str = "node-0") -> list:
-        code, body = _http("GET", f"http://127.0.0.1:{self.worker_ports[node][1]}/audit/{ns}/{pod}")
+        code, body = _http("GET", f"http://127.0.0.1:{self.worker_ports[node][1]}/audit/{ns}/{pod}",
+                           headers=self._auth)
         if code != 200:
             raise RuntimeError(f"audit {ns}/{pod}: {code} {body[:300]!r}")
         return json.loads(body)["issues"]
@@ -395,7 +413,8 @@ class ProcessCluster:
         for who, url in (("master", f"{self.master_url}/debug/calls{q}"),
                          ("worker", f"http://127.0.0.1:{self.worker_ports[node][1]}"
                                     f"/debug/calls{q}")):
-            code, body = _http("GET", url, headers=self._auth)
+            code, body = _http("GET", url, headers=self._auth,
+                               context=self.tls if who == "master" else None)
             if code != 200:
                 raise RuntimeError(f"{who} /debug/calls: {code} {body[:200]!r}")
             out[who] = [tuple(c) for c in json.loads(body)]

@@ -17,6 +17,7 @@ from __future__ import annotations
 import asyncio
 import json
 import signal
+import ssl
 import time
 from typing import Dict, Optional, Tuple
 
@@ -330,8 +331,13 @@ class Master:
             self._pods_task = asyncio.ensure_future(self._start_pod_index())
             await asyncio.wait([self._pods_task], timeout=self.POD_INDEX_WAIT_S)
         self.http = httpd.HttpServer(self.router())
+        tls = self.server_tls()
         self.port = await self.http.start(self.cfg.master_host,
-                                          self.cfg.master_port if port is None else port)
+                                          self.cfg.master_port if port is None else port,
+                                          ssl=tls)
+        if tls is None and self.authz.mode == "kube":
+            _log.warning("master API is plain HTTP and callers send Kubernetes bearer tokens "
+                         "(authz_mode=kube): set master_tls_cert/master_tls_key")
         try:
             self.warm_up()
             await self._warm_http()
@@ -364,12 +370,25 @@ class Master:
             for code in ("200", "400", "500"):
                 self.metrics.http_requests.labels(route=route, code=code)
 
+    def server_tls(self) -> Optional[ssl.SSLContext]:
+        """The API port's TLS context (None: plain HTTP)."""
+        if not getattr(self.cfg, "master_tls_cert", ""):
+            return None
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        ctx.load_cert_chain(self.cfg.master_tls_cert, self.cfg.master_tls_key)
+        return ctx
+
     async def _warm_http(self) -> None:
         """One request through the HTTP server over loopback (accept, parse, route, reply):
         the server half of a client's first request is then not cold code."""
         host = "127.0.0.1" if self.cfg.master_host in ("", "0.0.0.0", "::") else \
             self.cfg.master_host
-        r, w = await asyncio.wait_for(asyncio.open_connection(host, self.port), 2.0)
+        ctx = None
+        if self.http is not None and self.http.tls:
+            ctx = ssl.create_default_context()     # our own loopback: nothing to verify
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        r, w = await asyncio.wait_for(asyncio.open_connection(host, self.port, ssl=ctx), 2.0)
         try:
             w.write(b"GET /healthz HTTP/1.1\r\nHost: warm-up\r\nConnection: close\r\n\r\n")
             await asyncio.wait_for(r.read(), 2.0)

@@ -238,6 +238,15 @@ class Config:
     # the worker refuses to serve its gRPC API (which can kill tenant processes) without mTLS
     # unless this is set explicitly (hermetic tests, lab clusters)
     worker_insecure: bool = False
+    # HTTPS on the master's API port: callers send bearer tokens (authz_mode=kube), which must
+    # not cross the pod network in clear. cert+key set = TLS only on master_port (the shipped
+    # deploy sets both; the reference served plain HTTP, main.go:235-240)
+    master_tls_cert: str = ""
+    master_tls_key: str = ""           # private key of master_tls_cert
+    # who may read the worker's /status (every Pod's GPUs on the node) and /audit/{ns}/{pod}:
+    # auto = authz_mode (kube: "get" on nodes/gpumount resp. pods/gpumount, as the master's
+    # read routes ask); none = open. /healthz, /readyz and /metrics stay open for probes
+    status_authz: str = "auto"
     metrics_period_s: float = 15.0     # refresh of the per-GPU process and ledger gauges
     # serve /debug/tasks (every asyncio task's stack) on the worker's metrics port; it has no
     # authentication and that port binds worker_host, so it is off unless asked for
@@ -309,6 +318,9 @@ class Config:
         _choice("placement_correct_on", self.placement_correct_on, ("numa", "xgmi"))
         _choice("busy_detection", self.busy_detection, ("auto", "both"))
         _choice("authz_mode", self.authz_mode, ("none", "kube"))
+        _choice("status_authz", self.status_authz, ("auto", "none", "kube"))
+        if bool(self.master_tls_cert) != bool(self.master_tls_key):
+            raise ValueError("master_tls_cert and master_tls_key go together")
         _choice("placeholder_namespace_mode", self.placeholder_namespace_mode, ("pool", "tenant"))
         _choice("podresources_api", self.podresources_api, ("auto", "v1", "v1alpha1"))
         _choice("ledger_source", self.ledger_source, ("auto", "podresources"))

@@ -25,6 +25,7 @@ from gpumounter_amd.cluster.kube import KubeClient
 from gpumounter_amd.cluster.placeholder import LABEL_NODE, PlaceholderManager
 from gpumounter_amd.cluster.pool import WarmPool
 from gpumounter_amd.hw.inventory import Inventory
+from gpumounter_amd.models import pod as podu
 from gpumounter_amd.node import systemd
 from gpumounter_amd.node.cgroup import CgroupResolver, make_backend
 from gpumounter_amd.node.checkpoint import DeviceCheckpoint
@@ -69,6 +70,11 @@ class Worker:
         self.inv = inventory or Inventory(cfg.amdsmi_lib, cfg.kfd_major, cfg.kfd_dev_path)
         self.inv.ecc_policy = cfg.ecc_policy
         self.metrics = Metrics()
+        # /status and /audit list other tenants' Pods and GPUs: the master's read-route rights
+        from gpumounter_amd.master.authz import Authorizer
+        self.status_authz = Authorizer(cfg, self.kube)
+        mode = getattr(cfg, "status_authz", "auto")
+        self.status_authz.mode = cfg.authz_mode if mode == "auto" else mode
         if cfg.gpu_allocation == "dra":
             # GPUs come from a DRA driver: the allocations are in ResourceClaims, not in the
             # kubelet's device manager
@@ -413,7 +419,21 @@ class Worker:
     async def _readyz(self, request):
         return httpd.text("ready" if self.ready else "starting", 200 if self.ready else 503)
 
+    async def _status_denied(self, request, ns: str = "", name: str = ""):
+        """None if the caller may read this (``status_authz``), else its 401/403/503."""
+        if ns:
+            d = await self.status_authz.check(request.headers, "get", ns, name=name)
+        else:
+            d = await self.status_authz.check(request.headers, "get", resource="nodes",
+                                              name=self.cfg.node_name)
+        if d.allowed:
+            return None
+        return httpd.json_response({"error": d.reason}, status=d.status)
+
     async def _http_status(self, request):
+        denied = await self._status_denied(request)
+        if denied is not None:
+            return denied
         st = await self.service.node_status(request.query.get("processes") == "1")
         return httpd.json_response(st)
 
@@ -421,6 +441,12 @@ class Worker:
         """Ledger-vs-node consistency of one pod: [] when its cgroup rules and device nodes are
         exactly what its placeholders hold (the check the reconciler runs)."""
         ns, name = request.match_info["namespace"], request.match_info["pod"]
+        bad = podu.name_error(ns, name)
+        if bad is not None:
+            return httpd.json_response({"error": bad}, status=400)
+        denied = await self._status_denied(request, ns, name)
+        if denied is not None:
+            return denied
         pod = await self.service.get_pod(ns, name, fresh=True)
         if pod is None:
             return httpd.json_response({"error": "pod not found"}, status=404)
@@ -510,6 +536,7 @@ class Worker:
             await self.plugin.stop()
         if self.http is not None:
             await self.http.stop()
+        await self.status_authz.stop()
         await self.ph_informer.stop()
         await self.node_informer.stop()
         if self.claim_informer is not None:

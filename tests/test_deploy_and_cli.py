@@ -94,7 +94,7 @@ def test_service_and_master_ports():
     (svc,) = load("gpu-mounter-svc.yaml")
     (dep,) = load("gpu-mounter-master.yaml")
     cfg = Config.load(env={})
-    assert svc["spec"]["ports"][0]["port"] == 80
+    assert svc["spec"]["ports"][0]["port"] == 443 and svc["spec"]["ports"][0]["name"] == "https"
     assert svc["spec"]["ports"][0]["targetPort"] == cfg.master_port
     assert svc["spec"]["selector"] == dep["spec"]["template"]["metadata"]["labels"]
     assert load("namespace.yaml")[0]["metadata"]["name"] == cfg.pool_namespace
@@ -122,6 +122,23 @@ def test_master_and_network_policy_are_secure_by_default():
     env = {e["name"]: e.get("value") for e in c["env"]}
     cfg = Config.load(env={k: v for k, v in env.items() if v is not None})
     assert cfg.authz_mode == "kube" and cfg.tls_ca and cfg.tls_cert and cfg.tls_key
+    # no cleartext token path: callers' bearer tokens reach the master over HTTPS only, its
+    # certificate is in the Secret deploy.sh creates, and the probes speak HTTPS
+    assert cfg.master_tls_cert and cfg.master_tls_key
+    items = {i["key"] for v in dep["spec"]["template"]["spec"]["volumes"]
+             for i in (v.get("secret") or {}).get("items", [])}
+    assert {"master-https.crt", "master-https.key"} <= items
+    for probe in ("readinessProbe", "livenessProbe"):
+        assert c[probe]["httpGet"]["scheme"] == "HTTPS"
+    with open(os.path.join(ROOT, "deploy.sh")) as fh:
+        assert "master-https.crt" in fh.read()
+    # the workers' status routes are authorized as the master's read routes are
+    (ds,) = load("gpu-mounter-workers.yaml")
+    wenv = {e["name"]: e.get("value") for e in
+            ds["spec"]["template"]["spec"]["containers"][0]["env"]}
+    wcfg = Config.load(env={k: v for k, v in wenv.items() if v is not None and
+                            k.startswith("GM_")})
+    assert wcfg.status_authz in ("auto", "kube") and wcfg.authz_mode == "kube"
     (np,) = load("networkpolicy.yaml")
     assert np["spec"]["podSelector"]["matchLabels"] == {"app": "gpu-mounter-worker"}
     rules = np["spec"]["ingress"]
@@ -152,7 +169,9 @@ def test_cli_add_and_remove_authenticate_against_the_shipped_master(tmp_path):
 
     with ProcessCluster() as pc:
         pc.tenant("cli")
-        env = {**os.environ, "KUBECONFIG": str(tmp_path / "none"), "GM_TOKEN": ""}
+        assert pc.master_url.startswith("https://")
+        env = {**os.environ, "KUBECONFIG": str(tmp_path / "none"), "GM_TOKEN": "",
+               "GM_MASTER_CA": pc.ca}
         base = [sys.executable, "-m", "gpumounter_amd"]
         r = subprocess.run(base + ["add", "--master", pc.master_url, "--pod", "cli", "-n", "1"],
                            capture_output=True, text=True, cwd=ROOT, env=env, timeout=120)
@@ -163,6 +182,12 @@ def test_cli_add_and_remove_authenticate_against_the_shipped_master(tmp_path):
                            capture_output=True, text=True, cwd=ROOT, env=env, timeout=120)
         assert r.returncode == 0, r.stdout + r.stderr
         uuid = json.loads(r.stdout)["devices"][0]["uuid"]
+        # the master's certificate is verified: without the CA the CLI refuses to talk to it
+        r2 = subprocess.run(base + ["status", "--master", pc.master_url, "--node", "node-0",
+                                    "--token-file", str(tmp_path / "tok")],
+                            capture_output=True, text=True, cwd=ROOT,
+                            env={**env, "GM_MASTER_CA": ""}, timeout=120)
+        assert r2.returncode != 0 and "CERTIFICATE_VERIFY_FAILED" in r2.stderr
         r = subprocess.run(base + ["remove", "--master", pc.master_url, "--pod", "cli",
                                    "--uuid", uuid],
                            capture_output=True, text=True, cwd=ROOT,

@@ -39,9 +39,19 @@ def test_daemons_as_processes_attach_detach_and_exit_cleanly_on_sigterm():
         # deployed as shipped: no bearer token → 401 at the master; the worker's gRPC port
         # refuses a caller without the master's client certificate
         from gpumounter_amd.fakes.deployment import _http
-        code, body = _http("GET", f"{pc.master_url}/addgpu/namespace/default/pod/t0/gpu/1/"
-                                  "isEntireMount/false")
+        code, body = pc.http("GET", "/addgpu/namespace/default/pod/t0/gpu/1/isEntireMount/false")
         assert code == 401, body
+        # the token path is HTTPS only: a plain-HTTP request gets no answer from the API port
+        assert pc.master_url.startswith("https://")
+        with pytest.raises(OSError):
+            _http("GET", "http" + pc.master_url[5:] + "/healthz", timeout=5)
+        # and an unauthenticated caller reads nothing on the worker's status port
+        wport = pc.worker_ports["node-0"][1]
+        assert _http("GET", f"http://127.0.0.1:{wport}/audit/default/t0")[0] == 401
+        assert _http("GET", f"http://127.0.0.1:{wport}/status")[0] == 401
+        assert _http("GET", f"http://127.0.0.1:{wport}/status",
+                     headers={"Authorization": "Bearer not-a-token"})[0] == 401
+        assert _http("GET", f"http://127.0.0.1:{wport}/healthz")[0] == 200
         import grpc
 
         from gpumounter_amd.api import gpu_mount as api

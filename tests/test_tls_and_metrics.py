@@ -174,16 +174,72 @@ done
               f'NS=kube-system; SECRET=gpu-mounter-tls; pki')
     subprocess.run(["bash", "-c", script], check=True, timeout=120,
                    env={**os.environ, "PATH": f"{bindir}:{os.environ['PATH']}"})
-    assert sorted(p.name for p in out.iterdir()) == ["ca.crt", "master.crt", "master.key",
-                                                      "worker.crt", "worker.key"]
+    assert sorted(p.name for p in out.iterdir()) == [
+        "ca.crt", "master-https.crt", "master-https.key", "master.crt", "master.key",
+        "worker.crt", "worker.key"]
     w = {"tls_cert": str(out / "worker.crt"), "tls_key": str(out / "worker.key"),
          "tls_ca": str(out / "ca.crt")}
     m = {"tls_cert": str(out / "master.crt"), "tls_key": str(out / "master.key"),
-         "tls_ca": str(out / "ca.crt")}
+         "tls_ca": str(out / "ca.crt"), "master_tls_cert": str(out / "master-https.crt"),
+         "master_tls_key": str(out / "master-https.key")}
 
     async def main():
+        import ssl
+
         async with LocalCluster(worker_overrides=w, master_overrides=m) as lc:
             lc.tenant("t")
-            code, b = await lc.add("default", "t", 1)
-            assert code == 200, b
+            # the master's API is HTTPS, verifiable against the deploy's CA by the Service's
+            # in-cluster name and by localhost (kubectl port-forward)
+            assert lc.master.http.tls
+            ctx = ssl.create_default_context(cafile=str(out / "ca.crt"))
+            for host in ("localhost", "gpu-mounter-service.kube-system.svc", "127.0.0.1"):
+                r, wr = await asyncio.open_connection(
+                    "127.0.0.1", lc.master.port, ssl=ctx, server_hostname=host)
+                wr.write(b"GET /healthz HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+                assert (await r.read()).startswith(b"HTTP/1.1 200 ")
+                wr.close()
+            url = f"https://127.0.0.1:{lc.master.port}/addgpu/namespace/default/pod/t/gpu/1/" \
+                  "isEntireMount/false"
+            async with lc.session.get(url, ssl=ctx,
+                                      headers={"Accept": "application/json"}) as resp:
+                assert resp.status == 200, await resp.text()
+            # plain HTTP on the same port is not served
+            with pytest.raises(Exception):
+                async with lc.session.get(url.replace("https", "http")) as resp:
+                    await resp.read()
+    asyncio.run(main())
+
+
+def test_worker_status_routes_need_rbac_like_the_masters_read_routes():
+    """/status lists every Pod's GPUs on the node and /audit one Pod's rules: a caller without
+    a token gets 401, one RBAC does not allow gets 403 (the shipped networkpolicy leaves the
+    port open for Prometheus and probes, which keep /metrics, /healthz, /readyz)."""
+    async def main():
+        async with LocalCluster(worker_overrides={"status_authz": "kube"}) as lc:
+            lc.tenant("t")
+            c = lc.cluster
+            c.add_user("tok-nobody", "nobody")
+            c.add_user("tok-tenant", "tenant")
+            c.grant("tenant", ["get"], "pods/gpumount", ["default"])
+            c.add_user("tok-admin", "admin")
+            c.grant("admin", ["get"], "nodes/gpumount")
+            port = lc.nodes["node-0"].worker.http_port
+            base = f"http://127.0.0.1:{port}"
+
+            async def get(path, token=""):
+                h = {"Authorization": f"Bearer {token}"} if token else {}
+                async with lc.session.get(base + path, headers=h) as r:
+                    return r.status
+            assert await get("/audit/default/t") == 401
+            assert await get("/status") == 401
+            assert await get("/audit/default/t", "tok-nobody") == 403
+            assert await get("/status", "tok-nobody") == 403
+            assert await get("/audit/default/t", "tok-tenant") == 200
+            assert await get("/audit/other/t", "tok-tenant") == 403
+            assert await get("/status", "tok-tenant") == 403
+            assert await get("/status", "tok-admin") == 200
+            assert await get("/audit/default/a%2Fb", "tok-tenant") == 404     # not a route
+            assert await get("/audit/default/Not_A_Name", "tok-tenant") == 400  # not a name
+            for open_path in ("/healthz", "/readyz", "/metrics"):
+                assert await get(open_path) == 200
     asyncio.run(main())
