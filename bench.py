@@ -138,6 +138,12 @@ class _ProcCP:
     def calls(self, t0: float, t1: float) -> dict:
         return self.pc.calls(t0, t1)
 
+    def expire_authz(self) -> None:
+        """Age the master's cached authz answers (as a long idle would), same process."""
+        code, body = self.pc.http("POST", "/debug/authz-expire")
+        if code != 200:
+            raise RuntimeError(f"authz expire: {code} {body[:200]!r}")
+
     def wait_pool(self, want: int) -> None:
         from gpumounter_amd.models.types import ANN_MOUNT_MODE, MODE_STANDBY
         t_wait = time.time()
@@ -611,56 +617,60 @@ def main() -> int:
             cold = None
             if args.cold_steps > 0 and args.protocol == "gpumounter":
                 # the attach an operator makes minutes after the last one: every cached authz
-                # answer expired (the pod index is a watch, so it stays current)
-                import signal as _signal
+                # answer expired (the pod index is a watch, so it stays current). Two kinds of
+                # cold cycle, interleaved A B A B on the same master process (round 5 ran all A
+                # before a master restart and all B after it, and B came out faster than A with
+                # more work: the order and the fresh process, not the work, decided):
+                #   A "idle": idle_s of idle, authz answers still cached
+                #   B "cold": idle_s of idle, authz answers expired (TokenReview + SAR again)
+                expire = cp.expire_authz if args.deploy == "processes" else None
+                runs = {"idle": ([], {}), "cold": ([], {})}
 
-                def idle_cycles(tag):
-                    cms, cst = [], {}
-                    for i in range(args.cold_steps):
-                        time.sleep(args.idle_s)
-                        ta = time.perf_counter()
-                        code, body = cp.add(n, args.mode == "entire")
-                        tb = time.perf_counter()
-                        if code != 200:
-                            raise RuntimeError(f"cold attach failed: {code} {body}")
-                        cms.append((tb - ta) * 1e3)
-                        for t in body.get("master_timings", []) + [
-                                {"name": "worker", "ms": body.get("total_ms", 0.0)}] + [
-                                {"name": f"worker.{t['name']}", "ms": t["ms"]}
-                                for t in body.get("timings", []) if "." not in t["name"]]:
-                            cst.setdefault(t["name"], []).append(t["ms"])
-                        mc = body.get("master_clock") or {}
-                        if mc:
-                            for k, v in (("http.request_leg", mc["in"] - ta),
-                                         ("http.response_leg", tb - mc["out"])):
-                                cst.setdefault(k, []).append(v * 1e3)
-                        code, body = cp.remove([d["uuid"] for d in body["devices"]])
-                        if code != 200:
-                            raise RuntimeError(f"cold detach failed: {code} {body}")
-                        progress(tag, i + 1, args.cold_steps)
+                def cycle(kind):
+                    cms, cst = runs[kind]
+                    time.sleep(args.idle_s)
+                    if kind == "cold":
+                        expire()
+                    ta = time.perf_counter()
+                    code, body = cp.add(n, args.mode == "entire")
+                    tb = time.perf_counter()
+                    if code != 200:
+                        raise RuntimeError(f"{kind} attach failed: {code} {body}")
+                    cms.append((tb - ta) * 1e3)
+                    for t in body.get("master_timings", []) + [
+                            {"name": "worker", "ms": body.get("total_ms", 0.0)}] + [
+                            {"name": f"worker.{t['name']}", "ms": t["ms"]}
+                            for t in body.get("timings", []) if "." not in t["name"]]:
+                        cst.setdefault(t["name"], []).append(t["ms"])
+                    mc = body.get("master_clock") or {}
+                    if mc:
+                        for k, v in (("http.request_leg", mc["in"] - ta),
+                                     ("http.response_leg", tb - mc["out"])):
+                            cst.setdefault(k, []).append(v * 1e3)
+                    code, body = cp.remove([d["uuid"] for d in body["devices"]])
+                    if code != 200:
+                        raise RuntimeError(f"{kind} detach failed: {code} {body}")
+
+                def summary(kind):
+                    cms, cst = runs[kind]
                     return {"attach_p50_ms": round(pct(cms, 0.5), 4),
                             "attach_max_ms": round(max(cms), 4),
+                            "attach_ms": [round(x, 4) for x in cms],
                             "stage_p50_ms": {k: round(pct(v, 0.5), 4)
                                              for k, v in sorted(cst.items())}}
-                # 1) idle only (authz answers still cached): what idling alone costs on this box
-                idle_only = idle_cycles("idle")
-                if args.deploy == "processes":
-                    # 2) idle past the authz TTLs: TokenReview + SubjectAccessReview asked again
-                    ttl = f"{args.idle_s / 2:g}"
-                    cp.pc.restart_master(_signal.SIGTERM, env={"GM_AUTHZ_TOKEN_TTL_S": ttl,
-                                                                "GM_AUTHZ_SAR_TTL_S": ttl})
-                    # the restarted master's first request opens its channels: not counted
-                    code, body = cp.add(n, args.mode == "entire")
-                    if code != 200 or \
-                            cp.remove([d["uuid"] for d in body["devices"]])[0] != 200:
-                        raise RuntimeError(f"attach after the master restart failed: "
-                                           f"{code} {body}")
+                kinds = ("idle", "cold") if expire is not None else ("idle",)
+                for i in range(args.cold_steps):
+                    for kind in (kinds if i % 2 == 0 else kinds[::-1]):   # ABBA ABBA: no
+                        cycle(kind)                                        # kind always first
+                    progress("cold", i + 1, args.cold_steps)
+                idle_only = summary("idle")
+                if expire is not None:
                     cold = {"steps": args.cold_steps, "idle_s": args.idle_s,
-                            "authz_ttl_s": args.idle_s / 2, **idle_cycles("cold"),
-                            "idle_only": idle_only}
+                            "authz": "expired", "order": "ABBA, one master process",
+                            **summary("cold"), "idle_only": idle_only}
                 else:        # one process, no authz (LocalCluster): idling alone
                     cold = {"steps": args.cold_steps, "idle_s": args.idle_s,
-                            "authz_ttl_s": None, **idle_only, "idle_only": idle_only}
+                            "authz": None, **idle_only, "idle_only": idle_only}
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
             corrections = cp.corrections() if args.protocol == "gpumounter" else None
             placeholders_left = cp.placeholders_left()
@@ -748,7 +758,8 @@ def main() -> int:
                     "gpu_allocation": args.gpu_api,
                     "daemon_cpus": args.pin or None,
                     "daemon_env": args.daemon_env or None,
-                    "security": "mTLS master-worker + TokenReview/SAR authz (cached)"
+                    "security": "HTTPS client-master + mTLS master-worker + "
+                                "TokenReview/SAR authz (cached)"
                     if args.deploy == "processes" and args.security == "shipped" and
                     args.protocol == "gpumounter" else "off (insecure gRPC, no authz)",
                 },

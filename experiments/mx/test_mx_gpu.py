@@ -9,7 +9,11 @@ import pytest
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
-pytestmark = pytest.mark.skipif(not os.path.exists("/dev/kfd"), reason="needs an MI355X")
+# a real KFD with GPU nodes (a bare /dev/kfd node without the driver behind it is not one: bench.py
+# uses the same probe), and the gpu marker so a CPU run (-m "not gpu") never collects them
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not os.path.isdir("/sys/class/kfd/kfd/topology/nodes"),
+                                 reason="needs an MI355X")]
 
 
 # ------------------------------------------------------------------ block-scaled (MX) MFMA

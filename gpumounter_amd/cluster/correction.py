@@ -130,6 +130,12 @@ class Correction:
     pod's lock). ``ph`` is the PlaceholderManager; ``release_quiet(phs)`` releases leftovers,
     handing what it cannot delete to the reconciler's follow-up."""
 
+    # second round: how long to wait for the released placeholders' DELETED echo, then the
+    # re-hold attempts while the scheduler and the kubelet catch up (a real cluster's kubelet
+    # frees the devices when it has seen the deletion, tens to hundreds of ms later)
+    ECHO_WAIT_S = 1.0
+    REHOLD_DELAYS_S = (0.0, 0.05, 0.2, 0.5, 1.0)
+
     def __init__(self, ph, inv, free: Sequence[AmdGpu], attached: Sequence[AmdGpu], owner: dict,
                  n: int, entire: bool, group: str, attach_id: str, container: str,
                  idempotency_key: str, policy: str, faults,
@@ -195,6 +201,22 @@ class Correction:
         await self.ph.release(list(phs))
         self._set(phs, Book.RELEASED)
 
+    async def _observed_gone(self, phs: Sequence[Placeholder]) -> None:
+        """Wait (at most ``ECHO_WAIT_S``) until the watch has delivered the DELETED events of
+        ``phs``: the scheduler and the kubelet act on the same deletion, so a re-hold sent
+        before the echo mostly finds the GPUs still booked. The apiserver answered the DELETEs
+        already; the echo only paces the second round."""
+        uids = {p.uid for p in phs if p.uid}
+        informer = getattr(self.ph, "informer", None)
+        if not uids or informer is None:
+            return
+        try:
+            await informer.wait_for(
+                lambda: not uids & set(getattr(self.ph, "tombstones", ())), self.ECHO_WAIT_S)
+        except asyncio.TimeoutError:
+            _log.info("correction: DELETED echo of %d placeholder(s) not seen within %.1fs",
+                      len(uids), self.ECHO_WAIT_S)
+
     async def _keep(self, phs: Sequence[Placeholder]) -> None:
         await self.ph.confirm(phs)        # clears the candidate mark of the HELD ones
         self._set(phs, Book.KEPT)
@@ -215,9 +237,11 @@ class Correction:
                 if pick is None:
                     # the best set needs part of the admitted n-GPU placeholder, which can only be
                     # kept whole: a second round takes its GPUs back as 1-GPU placeholders
-                    await self._let_go(self.of(Book.ADMITTED))
+                    let_go = self.of(Book.ADMITTED)
+                    await self._let_go(let_go)
+                    await self._observed_gone(let_go)
                     want_n, got = len(mine), 0
-                    for delay in (0.0, 0.05, 0.2):   # while the kubelet frees them
+                    for delay in self.REHOLD_DELAYS_S:   # while the kubelet frees them
                         if delay:
                             await asyncio.sleep(delay)
                         got += len(await self._hold(want_n - got))

@@ -315,7 +315,13 @@ class Master:
         r.add_get("/metrics", self.metrics_handler)
         if getattr(self.cfg, "debug_endpoints", False):
             r.add_get("/debug/calls", self.debug_calls)
+            r.add_post("/debug/authz-expire", self.debug_authz_expire)
         return r
+
+    async def debug_authz_expire(self, request: Request) -> Response:
+        """Age the authz caches as a long idle period would (bench: cold attaches interleaved
+        with warm ones on the same master process)."""
+        return httpd.json_response({"aged": self.authz.expire()})
 
     async def debug_calls(self, request: Request) -> Response:
         """Outbound control-plane calls (utils/calls.py) that started in [since, until]."""

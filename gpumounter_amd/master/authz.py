@@ -137,6 +137,15 @@ class Authorizer:
                                         f"{resource}/{RESOURCE_SUB}{where}", user["username"])
         return Decision(True, 200, "", user["username"])
 
+    def expire(self) -> int:
+        """Age every cached TokenReview and SubjectAccessReview answer past its TTL, as a long
+        idle period would (the identities a token had stay known, as they do then). For the
+        bench's cold-attach phase: the same process, caches expired. Returns the entries aged."""
+        old = time.monotonic() - max(self.token_ttl_s, self.sar_ttl_s) - 1.0
+        self._tokens = {k: (old, v) for k, (_, v) in self._tokens.items()}
+        self._sar = {k: (old, v) for k, (_, v) in self._sar.items()}
+        return len(self._tokens) + len(self._sar)
+
     @staticmethod
     def _fresh(hit, ttl: float) -> bool:
         return bool(hit) and time.monotonic() - hit[0] < ttl

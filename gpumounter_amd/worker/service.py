@@ -456,6 +456,7 @@ class GpuMountService:
 
     SLOW_ATTACH_MS = 50.0
     YIELD_RETRY_S = 0.05     # after yielding standbys: the kubelet's teardown of them
+    LEASE_REBASE_S = 1.0     # an attach slower than this re-stamps its lease (_lease_booked)
 
     def _count_error(self, op: str, e: BaseException) -> None:
         """RPCs that end in a gRPC error count under its status name (RESOURCE_EXHAUSTED = quota,
@@ -595,7 +596,8 @@ class GpuMountService:
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
             msg = "Add GPU Success"
             if lease_exp:
-                self.lease.booked(pod, res.placeholders, lease_exp)     # timers; no write
+                lease_exp = await self._lease_booked(pod, res.placeholders, lease_exp,
+                                                     req.lease_s)
                 msg += time.strftime(" (lease until %Y-%m-%dT%H:%M:%SZ)", time.gmtime(lease_exp))
             log.kv(_log, 20, "attached", pod=f"{req.namespace}/{req.pod_name}",
                    gpus=[g.bdf for g in new], by=req.requested_by, lease_s=req.lease_s)
@@ -604,6 +606,24 @@ class GpuMountService:
                                  by=req.requested_by)
             return api.AddGPUResponse(add_gpu_result=api.ADD_SUCCESS,
                                       devices=self._devices(new, owner), message=msg)
+
+    async def _lease_booked(self, pod: dict, phs, lease_exp: float, lease_s: float) -> float:
+        """Arm the lease the placeholders were booked with. The booking stamped it when the
+        request arrived, so an attach that waited long for admission (a slow scheduler, up to
+        ``attach_timeout_s``) would have spent part of the lease before the tenant got the GPU
+        — all of it, for a lease shorter than the wait. Past ``LEASE_REBASE_S`` the lease is
+        re-stamped from now (one PATCH per placeholder); the booking carried a lease from the
+        start either way, so no crash leaves a leased GPU without one."""
+        if time.time() - (lease_exp - lease_s) <= self.LEASE_REBASE_S:
+            self.lease.booked(pod, phs, lease_exp)      # timers; no write
+            return lease_exp
+        try:
+            return await self.lease.grant(pod, phs, lease_s)
+        except Exception as e:  # noqa: BLE001 - the booked lease still holds
+            _log.warning("re-stamping the lease of %s/%s after a slow attach: %s",
+                         podu.ns_of(pod), podu.name_of(pod), e)
+            self.lease.booked(pod, phs, lease_exp)
+            return lease_exp
 
     @contextlib.asynccontextmanager
     async def _quota_guard(self, ns: str, n: int):

@@ -277,3 +277,76 @@ def test_the_lost_reply_scenario_reaches_the_second_round(inv):
     with pytest.raises((ReserveError, InsufficientGPU)):
         asyncio.run(svc._correct(OWNER, 2, req, st, Reservation([first])))
     assert ("DELETE", "after") in api.calls
+
+
+class LaggingApi(FakeApi):
+    """The kubelet frees a deleted placeholder's devices ``lag_s`` after the DELETE (it acts on
+    its own watch of the deletion): a re-hold sent earlier finds them still booked."""
+
+    def __init__(self, *a, lag_s=0.3, **k):
+        super().__init__(*a, **k)
+        self.lag_s = lag_s
+        self.freed_at = {}          # gpu index → monotonic time it becomes allocatable
+
+    def delete(self, uid):
+        import time
+
+        p = self.pods.get(uid)
+        err = super().delete(uid)
+        if p is not None and uid not in self.pods:
+            for i in p["gpus"] or ():
+                self.freed_at[i] = time.monotonic() + self.lag_s
+        return err
+
+    def _schedule(self, uid, k):
+        import time
+
+        now = time.monotonic()
+        lagging = {i for i, t in self.freed_at.items() if t > now}
+        free = [i for i in self.gpus if i not in self.alloc and i not in lagging]
+        if len(free) < k:
+            return None
+        saved = self.alloc
+        self.alloc = {**saved, **{i: "lag" for i in lagging}}
+        try:
+            got = super()._schedule(uid, k)
+        finally:
+            for i in lagging:
+                self.alloc.pop(i, None)
+            self.alloc.update({i: uid for i in got or ()})
+        return got
+
+
+def test_second_round_outlasts_a_slow_kubelet_release(inv):
+    """the second round of an entire-mount correction re-holds GPUs it just let go.
+    With the kubelet 0.3 s behind the DELETE, the round-5 retry budget (0, 50, 200 ms) gave up
+    and the attach kept the worse placement; the re-hold now outlasts the lag and the
+    correction lands on the best set."""
+    from gpumounter_amd.cluster.correction import Correction
+
+    api = LaggingApi(inv, SCENARIO["taken"], SCENARIO["policy"], [], lag_s=0.3)
+    svc = make_service(inv, api)
+    first, _ = api.create(2, candidate=False, faults=False)
+    req = types.SimpleNamespace(is_entire_mount=True, container="", idempotency_key="k")
+    st = PodGpuState(ledger={("x", f"o{i}"): [api.bdf[i]] for i in SCENARIO["taken"]})
+    best = svc._preferred(2, st)
+    assert svc._placement_worse(st, first.device_ids, best)
+    svc.ph.device_ids[first.uid] = first.device_ids
+    out = asyncio.run(svc._correct(OWNER, 2, req, st, Reservation([first])))
+    assert sorted(out.device_ids) == sorted(best), (out.device_ids, best, api.calls)
+    check_booked(api, out, 2)
+    # the round-5 budget is not enough for this kubelet
+    old = Correction.REHOLD_DELAYS_S
+    try:
+        Correction.REHOLD_DELAYS_S = (0.0, 0.05, 0.2)
+        api2 = LaggingApi(inv, SCENARIO["taken"], SCENARIO["policy"], [], lag_s=0.3)
+        svc2 = make_service(inv, api2)
+        first2, _ = api2.create(2, candidate=False, faults=False)
+        svc2.ph.device_ids[first2.uid] = first2.device_ids
+        try:
+            out2 = asyncio.run(svc2._correct(OWNER, 2, req, st, Reservation([first2])))
+            assert sorted(out2.device_ids) != sorted(best)
+        except (ReserveError, InsufficientGPU):
+            pass
+    finally:
+        Correction.REHOLD_DELAYS_S = old

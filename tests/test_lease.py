@@ -574,3 +574,31 @@ def test_an_expiry_that_keeps_failing_tells_the_pod():
         assert n == 1
         svc.remove_gpu = real
     run(body, worker_overrides={"lease_retry_s": 0.2})
+
+
+def test_a_slow_attach_gets_its_whole_lease():
+    """the lease is booked when the request arrives; an attach that waits long for
+    admission must not spend its lease in that wait. Past LEASE_REBASE_S the lease starts at
+    the mount (and the reply says so)."""
+    from gpumounter_amd.fakes.apiserver import LatencyModel
+
+    async def body(lc):
+        lc.tenant("t")
+        svc = lc.nodes["node-0"].worker.service
+        t0 = time.time()
+        code, b = await lease_add(lc, "default", "t", 1, 2.0)    # admission alone takes 1.5 s
+        t1 = time.time()
+        assert code == 200 and t1 - t0 >= 1.5
+        (p,) = [p for p in lc.cluster.placeholders()
+                if (p["metadata"].get("annotations") or {}).get(ANN_LEASE)]
+        until_ = float(p["metadata"]["annotations"][ANN_LEASE])
+        assert until_ >= t1 + 1.8, (until_ - t1)            # counted from the mount, not t0
+        await asyncio.sleep(1.0)                            # past t0 + 2 s: still attached
+        st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+        assert len(st.hot) == 1
+
+        async def gone():
+            st = await svc.pod_state(lc.cluster.get("default", "t"), fresh=True)
+            return not st.hot
+        assert await until(gone, 5.0)
+    run(body, latency=LatencyModel(schedule_ms=1500.0))
