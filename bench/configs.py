@@ -873,7 +873,8 @@ def main() -> int:
         res["config"] = {"scenario": "chaos", "deploy": "processes",
                          "amdsmi": args.amdsmi or "libamd_smi", "cgroup": args.cgroup,
                          "warm_pool": args.warm_pool, "gpu_allocation": args.gpu_api,
-                         "latency": "zero", "security": "mTLS + TokenReview/SAR authz"}
+                         "latency": "zero",
+                         "security": "HTTPS + mTLS + TokenReview/SAR authz"}
         print(json.dumps(res))
         return 0
     if args.deploy == "processes":
@@ -882,7 +883,8 @@ def main() -> int:
         res = contention_processes(args)
         res["config"] = {"scenario": "contention", "deploy": "processes",
                          "amdsmi": args.amdsmi or "libamd_smi", "cgroup": args.cgroup,
-                         "latency": "zero", "security": "mTLS + TokenReview/SAR authz"}
+                         "latency": "zero",
+                         "security": "HTTPS + mTLS + TokenReview/SAR authz"}
         print(json.dumps(res))
         return 0
 
