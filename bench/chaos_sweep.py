@@ -35,6 +35,9 @@ MODES = {
     "hpl": CHURN + ["--placement", "hint", "--warm-pool", "2", "--lease-rate", "0.3"],
     "tpr": ["--restart-rate", "0.2", "--placement", "trim", "--warm-pool", "2",
             "--lease-rate", "0.3"],
+    # round 6: idle standbys at the low pool class; every attach that needs them yields them
+    "lpl": CHURN + ["--warm-pool", "2", "--pool-priority-class", "gpumounter-standby",
+                    "--lease-rate", "0.3"],
 }
 
 

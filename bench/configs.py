@@ -357,6 +357,8 @@ def chaos(args) -> dict:
     codes: Dict[int, int] = {}
     env = {"GM_FAULT": CHAOS_FAULTS, "GM_RECONCILE_PERIOD_S": str(args.reconcile_period),
            "GM_WARM_POOL_SIZE": str(args.warm_pool), "GM_PLACEMENT_ENFORCE": args.placement}
+    if args.pool_priority_class:
+        env["GM_POOL_PRIORITY_CLASS"] = args.pool_priority_class
     if args.log_dir:
         env["GM_LOG_LEVEL"] = "DEBUG"      # kept logs are for post-mortems
     busy = _BusyTenants(tenants, args.busy_pool) if args.busy else None
@@ -813,6 +815,9 @@ def main() -> int:
                          "pod-blind topology choice")
     ap.add_argument("--device-plugin", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0)
+    ap.add_argument("--pool-priority-class", default="",
+                    help="GM_POOL_PRIORITY_CLASS for the workers (chaos, processes): e.g. "
+                         "gpumounter-standby, idle standbys preemptible and yielded to attaches")
     ap.add_argument("--rounds", type=int, default=50)
     ap.add_argument("--cycles", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
