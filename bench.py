@@ -138,9 +138,10 @@ class _ProcCP:
     def calls(self, t0: float, t1: float) -> dict:
         return self.pc.calls(t0, t1)
 
-    def expire_authz(self) -> None:
-        """Age the master's cached authz answers (as a long idle would), same process."""
-        code, body = self.pc.http("POST", "/debug/authz-expire")
+    def expire_authz(self, age: bool = True) -> None:
+        """Age the master's cached authz answers (as a long idle would), same process;
+        ``age=False`` sends the same request and ages nothing (the control cycles)."""
+        code, body = self.pc.http("POST", "/debug/authz-expire" + ("" if age else "?age=0"))
         if code != 200:
             raise RuntimeError(f"authz expire: {code} {body[:200]!r}")
 
@@ -623,14 +624,18 @@ def main() -> int:
                 # more work: the order and the fresh process, not the work, decided):
                 #   A "idle": idle_s of idle, authz answers still cached
                 #   B "cold": idle_s of idle, authz answers expired (TokenReview + SAR again)
+                # Before each attach both send one request to the master's debug port (B's ages
+                # the caches, A's does not): what remains between them is the review itself
                 expire = cp.expire_authz if args.deploy == "processes" else None
                 runs = {"idle": ([], {}), "cold": ([], {})}
 
                 def cycle(kind):
                     cms, cst = runs[kind]
                     time.sleep(args.idle_s)
-                    if kind == "cold":
-                        expire()
+                    if expire is not None:
+                        # both kinds send the same request to the master first (only "cold"
+                        # ages the caches), so both wake the master the same way
+                        expire(kind == "cold")
                     ta = time.perf_counter()
                     code, body = cp.add(n, args.mode == "entire")
                     tb = time.perf_counter()

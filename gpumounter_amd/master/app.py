@@ -320,7 +320,10 @@ class Master:
 
     async def debug_authz_expire(self, request: Request) -> Response:
         """Age the authz caches as a long idle period would (bench: cold attaches interleaved
-        with warm ones on the same master process)."""
+        with warm ones on the same master process). ``?age=0``: the same request, nothing aged
+        (the control cycles send it too, so both kinds wake the master alike)."""
+        if request.query.get("age") == "0":
+            return httpd.json_response({"aged": 0})
         return httpd.json_response({"aged": self.authz.expire()})
 
     async def debug_calls(self, request: Request) -> Response:
