@@ -146,11 +146,14 @@ class _ProcCP:
             raise RuntimeError(f"authz expire: {code} {body[:200]!r}")
 
     def wait_pool(self, want: int) -> None:
+        """Until ``want`` standby placeholders are admitted (the kubelet has posted their
+        container statuses), as the in-process adapter's ``pool.standby()`` counts them."""
         from gpumounter_amd.models.types import ANN_MOUNT_MODE, MODE_STANDBY
         t_wait = time.time()
         while sum(1 for p in self.pc.placeholders()
                   if (p["metadata"].get("annotations") or {}).get(ANN_MOUNT_MODE) == MODE_STANDBY
-                  and not p["metadata"].get("deletionTimestamp")) < want:
+                  and not p["metadata"].get("deletionTimestamp")
+                  and (p.get("status") or {}).get("containerStatuses")) < want:
             if time.time() - t_wait > 120:
                 raise RuntimeError("warm pool did not fill")
             time.sleep(0.002)

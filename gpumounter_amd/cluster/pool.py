@@ -334,6 +334,26 @@ class WarmPool:
         self.poke()
         return Reservation(chosen)
 
+    async def cancel_pending_low(self, min_priority: int) -> int:
+        """Delete standby placeholders that rank below ``min_priority`` and are not admitted
+        yet (a refill in flight): their GPUs look free to an attach at that rank, which would
+        then lose the race for them to a standby it cannot claim. Returns how many."""
+        async with self._lock:
+            pend = [PlaceholderManager.from_pod(p, {}) for p in self.ph.live()
+                    if is_standby(p) and podu.priority_of(p) < min_priority
+                    and self.ph.cached(p) is None
+                    and not self.ph.last_ledger.get((p["metadata"]["namespace"],
+                                                     p["metadata"]["name"]))]
+            if not pend:
+                return 0
+            for ph in pend:
+                ph.owner_uid, ph.attach_id = "", ""
+            try:
+                await self.ph.release(pend)
+            except Exception as e:  # noqa: BLE001 - the attach's own retry covers the rest
+                _log.warning("cancelling pending standby placeholders: %s", e)
+            return len(pend)
+
     async def yield_low(self, n: int, min_priority: int, attached: Sequence[AmdGpu] = ()
                         ) -> List[Placeholder]:
         """Give up to ``n`` standby GPUs that rank below ``min_priority`` back to the scheduler

@@ -789,6 +789,9 @@ class GpuMountService:
                 _log.info("trim refused by the tenant's quota (%s); plain reservation", e)
         yielded = []
         if pool_on and n - got > 0:
+            if self.pool.refilling():
+                # low standbys being admitted would take GPUs that look free here
+                await self.pool.cancel_pending_low(rank)
             free_now = self._free(st)
             if len(free_now) < n - got:
                 # the rest is held by standbys that rank below this Pod: give them back to the

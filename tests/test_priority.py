@@ -242,3 +242,34 @@ def test_fake_scheduler_keeps_a_preemptors_room_for_it():
             await _until(lambda: podu.node_of(hp) == "node-0", 5, what="hp bound")
             assert c.preemptions == 2 and not podu.node_of(late)
     asyncio.run(main())
+
+
+def test_attach_during_a_low_refill_cancels_it_instead_of_racing_it():
+    """Right after a detach the pool refills with a low standby; an attach at tenant rank that
+    arrives while that standby is being admitted cannot claim it, and would lose the last free
+    GPU to it (then wait for its admission, yield it and book again: two admissions). The
+    pending standby is cancelled first: one admission."""
+    from gpumounter_amd.fakes.apiserver import LatencyModel
+
+    async def main():
+        ov = {"warm_pool_size": 1, "pool_priority_class": "gpumounter-standby"}
+        lat = LatencyModel(schedule_ms=100.0, admit_ms=100.0)
+        async with LocalCluster(worker_overrides=ov, latency=lat) as lc:
+            pool = lc.nodes["node-0"].worker.pool
+            lc.tenant("a")
+            lc.tenant("b")
+            code, _ = await lc.add("default", "a", 7)          # 7 booked, 1 left for the pool
+            assert code == 200
+            await _until(lambda: len(pool.standby()) == 1, 10, what="pool filled")
+            code, b1 = await lc.add("default", "b", 1)         # yields the standby
+            assert code == 200
+            code, _ = await lc.remove("default", "b", [d["uuid"] for d in b1["devices"]])
+            assert code == 200
+            await _until(lambda: pool.refilling(), 5, what="refill in flight")
+            t0 = time.monotonic()
+            code, b2 = await lc.add("default", "b", 1)
+            took = time.monotonic() - t0
+            assert code == 200, b2
+            assert took < 0.33, took                           # one admission (0.2 s), not two
+            assert not await lc.audit("default", "b")
+    asyncio.run(main())
