@@ -350,7 +350,14 @@ class _Conn(asyncio.Protocol):
             self.t_first = time.monotonic()
         self.buf += data
         if len(self.buf) > MAX_HEAD + MAX_BODY + (64 << 10):
-            self._fail(413)                # only while busy can this much pile up
+            # only a transport that ignored pause_reading while a request is in flight gets
+            # here: an answer now would overtake that request's, so the connection just ends
+            self.buf.clear()
+            self._req = None
+            if self.busy:
+                self.t.close()
+            else:
+                self._fail(413)
             return
         if self.busy:
             # one request at a time: later bytes stay in the kernel until it is answered
@@ -560,7 +567,7 @@ class _Conn(asyncio.Protocol):
                 self._arm_idle()
 
     def _write(self, resp: Response, close: bool) -> None:
-        if self.t is None:
+        if self.t is None or self.t.is_closing():
             return
         head = [b"HTTP/1.1 %d %s\r\n" % (resp.status, _REASONS.get(resp.status, "").encode())]
         if resp.content_type:
