@@ -38,6 +38,11 @@ MODES = {
     # round 6: idle standbys at the low pool class; every attach that needs them yields them
     "lpl": CHURN + ["--warm-pool", "2", "--pool-priority-class", "gpumounter-standby",
                     "--lease-rate", "0.3"],
+    # round 6: a higher-priority Pod that wants node-0's GPUs arrives and leaves between
+    # rounds; the scheduler preempts the lowest-priority pods it can (standbys, tenants)
+    "pre": CHURN + ["--warm-pool", "2", "--pool-priority-class", "gpumounter-standby",
+                    "--preempt-rate", "0.5"],
+    "pre0": CHURN + ["--preempt-rate", "0.5"],
 }
 
 

@@ -318,6 +318,17 @@ CHAOS_FAULTS = ("ledger_reserve:0.04,placeholder_wait:0.03,cgroup_rule:0.04,devn
                 "ledger_release:0.04:after")
 
 
+def _http_json(method: str, url: str, body=None):
+    """One JSON request to the hermetic apiserver: (status, decoded body or {})."""
+    from gpumounter_amd.fakes.deployment import _http
+    code, raw = _http(method, url, json.dumps(body).encode() if body is not None else None,
+                      {"Content-Type": "application/json"} if body is not None else None)
+    try:
+        return code, json.loads(raw) if raw else {}
+    except ValueError:
+        return code, {}
+
+
 def chaos(args) -> dict:
     """Contention under failure, against the deployment shape (ProcessCluster, mTLS + authz):
     four Pods attach and detach concurrently over HTTP while the worker injects faults at every
@@ -373,6 +384,36 @@ def chaos(args) -> dict:
             pc.tenant(t, pids={"main": busy.pids(t)} if busy else None)
         if args.api_fault_rate:
             pc.api_faults(args.api_fault_rate, args.seed)
+        api = pc.info["api_url"]
+        preemptors: List[str] = []
+        preempted = [0, 0]          # preemptors created, of them bound
+        if args.preempt_rate:
+            code, _ = _http_json("POST", f"{api}/apis/scheduling.k8s.io/v1/priorityclasses",
+                                 {"metadata": {"name": "chaos-high"}, "value": 1000})
+            if code not in (201, 409):
+                raise RuntimeError(f"priority class create: {code}")
+
+        def preemptor_churn(rnd_i):
+            """Delete last round's preemptor; maybe send a new one (see --preempt-rate)."""
+            while preemptors:
+                name = preemptors.pop()
+                code, body = _http_json("GET", f"{api}/api/v1/namespaces/default/pods/{name}")
+                if code == 200 and body.get("spec", {}).get("nodeName"):
+                    preempted[1] += 1
+                _http_json("DELETE", f"{api}/api/v1/namespaces/default/pods/{name}",
+                           {"gracePeriodSeconds": 0})
+            rnd = random.Random(args.seed * 131 + rnd_i)
+            if rnd.random() < args.preempt_rate:
+                name = f"preemptor-{rnd_i}"
+                code, _ = _http_json("POST", f"{api}/api/v1/namespaces/default/pods", {
+                    "metadata": {"name": name},
+                    "spec": {"priorityClassName": "chaos-high",
+                             "nodeSelector": {"kubernetes.io/hostname": "node-0"},
+                             "containers": [{"name": "c", "image": "x:1", "resources": {
+                                 "limits": {"amd.com/gpu": str(rnd.randint(1, 2))}}}]}})
+                if code == 201:
+                    preemptors.append(name)
+                    preempted[0] += 1
 
         def op(t):
             rnd = rnds[t]
@@ -490,6 +531,8 @@ def chaos(args) -> dict:
                 if busy is not None:
                     busy.publish(gpu_views())
                 futs = [ex.submit(op, t) for t in tenants]
+                if args.preempt_rate:
+                    preemptor_churn(rnd_i)
                 if args.recreate_rate and random.Random(rnd_i * 11 + 3).random() < args.recreate_rate:
                     # a tenant Pod is deleted and recreated under its name (new UID) mid-round
                     t = random.Random(rnd_i + 9).choice(tenants)
@@ -644,6 +687,7 @@ def chaos(args) -> dict:
             "converge_p50_ms": round(pct(converge, 0.5), 1),
             "converge_max_ms": round(max(converge), 1),
             "invariant_violations": len(problems), "violation_examples": problems[:5],
+            "preemptors": preempted[0], "preemptors_bound": preempted[1],
             "faults": CHAOS_FAULTS, "api_fault_rate": args.api_fault_rate,
             "reconcile_period_s": args.reconcile_period, "placement": args.placement,
             "api_faults_served": api_faults[0],
@@ -815,6 +859,12 @@ def main() -> int:
                          "pod-blind topology choice")
     ap.add_argument("--device-plugin", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0)
+    ap.add_argument("--preempt-rate", type=float, default=0.0,
+                    help="chaos: per round, the chance that a Pod of priority 1000 (above every "
+                         "tenant, below the placeholders' floor) asks for 1-2 GPUs on the node; "
+                         "it is deleted the next round. It may take free GPUs or preempt idle "
+                         "low-class standbys, never a tenant's placeholder (the ledger check "
+                         "would see the revocation)")
     ap.add_argument("--pool-priority-class", default="",
                     help="GM_POOL_PRIORITY_CLASS for the workers (chaos, processes): e.g. "
                          "gpumounter-standby, idle standbys preemptible and yielded to attaches")

@@ -776,6 +776,7 @@ class FakeCluster:
         r.add_get("/healthz", self._h_healthz)
         r.add_get("/apis/scheduling.k8s.io/v1/priorityclasses", self._h_pc_list)
         r.add_get("/apis/scheduling.k8s.io/v1/priorityclasses/{name}", self._h_pc_get)
+        r.add_post("/apis/scheduling.k8s.io/v1/priorityclasses", self._h_pc_create)
         self.dra.install(r, self._pre)
         return app
 
@@ -1118,6 +1119,20 @@ class FakeCluster:
                  "message": f'priorityclasses.scheduling.k8s.io "{req.match_info["name"]}" '
                             "not found"}, status=404)
         return web.json_response(pc)
+
+    async def _h_pc_create(self, req: web.Request) -> web.Response:
+        await self._pre(req)
+        body = await req.json()
+        name = (body.get("metadata") or {}).get("name", "")
+        if not name or "value" not in body:
+            return web.json_response({"kind": "Status", "code": 422, "reason": "Invalid",
+                                      "message": "name and value are required"}, status=422)
+        if name in self.priority_classes:
+            return web.json_response({"kind": "Status", "code": 409, "reason": "AlreadyExists",
+                                      "message": f'priorityclasses "{name}" already exists'},
+                                     status=409)
+        return web.json_response(self.apply_priority_classes(
+            [dict(body, kind="PriorityClass")]) and self.priority_classes[name], status=201)
 
     async def _h_pc_list(self, req: web.Request) -> web.Response:
         await self._pre(req)
