@@ -228,7 +228,9 @@ def test_server_parses_what_h11_parses(raw, cuts):
 @FUZZ
 @given(st.lists(requests(), min_size=2, max_size=4), CUTS)
 def test_server_pipelined_requests_each_answered_in_order(raws, cuts):
-    keep = [r for r in raws if b"HTTP/1.1\r\n" in r.split(b"\r\n\r\n", 1)[0] + b"\r\n"]
+    # HTTP/1.0 requests close the connection after their answer: pipeline 1.1 ones only
+    # (by the request line: a header value may read "HTTP/1.1" too)
+    keep = [r for r in raws if r.split(b"\r\n", 1)[0].endswith(b" HTTP/1.1")]
     if len(keep) < 2:
         return
     c, t = _serve(b"".join(keep), [x * 3 for x in cuts])
