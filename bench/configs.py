@@ -370,6 +370,8 @@ def chaos(args) -> dict:
            "GM_WARM_POOL_SIZE": str(args.warm_pool), "GM_PLACEMENT_ENFORCE": args.placement}
     if args.pool_priority_class:
         env["GM_POOL_PRIORITY_CLASS"] = args.pool_priority_class
+    if args.no_placeholder_priority:
+        env["GM_PLACEHOLDER_PRIORITY_CLASS"] = ""       # the reference's priority 0
     if args.log_dir:
         env["GM_LOG_LEVEL"] = "DEBUG"      # kept logs are for post-mortems
     busy = _BusyTenants(tenants, args.busy_pool) if args.busy else None
@@ -400,8 +402,11 @@ def chaos(args) -> dict:
                 code, body = _http_json("GET", f"{api}/api/v1/namespaces/default/pods/{name}")
                 if code == 200 and body.get("spec", {}).get("nodeName"):
                     preempted[1] += 1
-                _http_json("DELETE", f"{api}/api/v1/namespaces/default/pods/{name}",
-                           {"gracePeriodSeconds": 0})
+                for _ in range(20):      # the apiserver's injected faults hit these too
+                    code, _ = _http_json("DELETE", f"{api}/api/v1/namespaces/default/pods/{name}",
+                                         {"gracePeriodSeconds": 0})
+                    if code in (200, 404):
+                        break
             rnd = random.Random(args.seed * 131 + rnd_i)
             if rnd.random() < args.preempt_rate:
                 name = f"preemptor-{rnd_i}"
@@ -410,9 +415,9 @@ def chaos(args) -> dict:
                     "spec": {"priorityClassName": "chaos-high",
                              "nodeSelector": {"kubernetes.io/hostname": "node-0"},
                              "containers": [{"name": "c", "image": "x:1", "resources": {
-                                 "limits": {"amd.com/gpu": str(rnd.randint(1, 2))}}}]}})
+                                 "limits": {"amd.com/gpu": str(args.preempt_gpus or rnd.randint(1, 2))}}}]}})
+                preemptors.append(name)     # a failed POST may have taken effect: delete it too
                 if code == 201:
-                    preemptors.append(name)
                     preempted[0] += 1
 
         def op(t):
@@ -677,6 +682,14 @@ def chaos(args) -> dict:
                     pc.api_faults(args.api_fault_rate, args.seed * 1000 + rnd_i)
         metrics = pc.worker_metrics()
         busy_report = busy.report() if busy is not None else {}
+        code, preempt = _http_json("GET", f"{api}/_fake/preemptions")
+        if code != 200:
+            raise RuntimeError(f"preemptions: {code}")
+        if preempt["victims"]["placeholder"]:
+            # the shipped floor class outranks every preemptor here: a placeholder that books
+            # a tenant's GPU is never a victim (only standbys at the low class may be)
+            problems.append(f"{preempt['victims']['placeholder']} placeholder(s) booking a "
+                            f"tenant's GPU preempted")
     injected = sum(float(ln.split()[-1]) for ln in metrics.splitlines()
                    if ln.startswith("gm_requests_total{") and 'result="INTERNAL"' in ln)
     return {"rounds": args.rounds, "worker_kills": kills, "master_kills": master_kills,
@@ -688,6 +701,7 @@ def chaos(args) -> dict:
             "converge_max_ms": round(max(converge), 1),
             "invariant_violations": len(problems), "violation_examples": problems[:5],
             "preemptors": preempted[0], "preemptors_bound": preempted[1],
+            "preempted": preempt["victims"],
             "faults": CHAOS_FAULTS, "api_fault_rate": args.api_fault_rate,
             "reconcile_period_s": args.reconcile_period, "placement": args.placement,
             "api_faults_served": api_faults[0],
@@ -859,12 +873,17 @@ def main() -> int:
                          "pod-blind topology choice")
     ap.add_argument("--device-plugin", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0)
+    ap.add_argument("--no-placeholder-priority", action="store_true",
+                    help="chaos: placeholders without the floor PriorityClass (the reference's "
+                         "priority 0), the negative control for --preempt-rate")
+    ap.add_argument("--preempt-gpus", type=int, default=0,
+                    help="chaos: GPUs each --preempt-rate Pod requests (0: 1 or 2 at random)")
     ap.add_argument("--preempt-rate", type=float, default=0.0,
                     help="chaos: per round, the chance that a Pod of priority 1000 (above every "
                          "tenant, below the placeholders' floor) asks for 1-2 GPUs on the node; "
                          "it is deleted the next round. It may take free GPUs or preempt idle "
-                         "low-class standbys, never a tenant's placeholder (the ledger check "
-                         "would see the revocation)")
+                         "low-class standbys, never a placeholder that books a tenant's GPU "
+                         "(checked through the fake scheduler's victims)")
     ap.add_argument("--pool-priority-class", default="",
                     help="GM_POOL_PRIORITY_CLASS for the workers (chaos, processes): e.g. "
                          "gpumounter-standby, idle standbys preemptible and yielded to attaches")

@@ -19,6 +19,8 @@ Besides the Kubernetes API it serves these test hooks:
   ``POST /_fake/restart`` {"ns", "pod", "container"} → the container restarts (new id, cgroup, /dev)
   ``POST /_fake/faults``  {"rate", "seed"} → Pod/ResourceClaim requests fail at random (500/503/
                           429, half after taking effect); answers how many were served so far
+  ``GET  /_fake/preemptions`` → how many Pods the scheduler preempted, by kind (standby,
+                          placeholder booking a tenant's GPU, other)
   ``POST /_fake/user``    {"token", "user", "verbs", "resource", "namespaces"} → a bearer token
                           TokenReview accepts, and an RBAC rule SubjectAccessReview honours
 The info file lists the apiserver URL and each node's kubelet socket, cgroup root and rootfs root.
@@ -97,6 +99,20 @@ def _hooks(lc_ref: list):
             pod = lc.tenant(name, ns=ns, node=b.get("node", "node-0"))
             return web.json_response({"uid": pod["metadata"]["uid"]}, status=201)
 
+        async def preemptions(req: web.Request) -> web.Response:
+            from gpumounter_amd.cluster.pool import is_standby
+            from gpumounter_amd.models.types import LABEL_APP, LABEL_APP_VALUE
+            api = lc_ref[0].cluster
+            kinds = {"standby": 0, "placeholder": 0, "other": 0}
+            for v in api.victims:
+                if is_standby(v):
+                    kinds["standby"] += 1
+                elif (v["metadata"].get("labels") or {}).get(LABEL_APP) == LABEL_APP_VALUE:
+                    kinds["placeholder"] += 1
+                else:
+                    kinds["other"] += 1
+            return web.json_response({"preemptions": api.preemptions, "victims": kinds})
+
         app.router.add_post("/_fake/faults", faults)
         app.router.add_post("/_fake/kubelet/restart", kubelet_restart)
         app.router.add_post("/_fake/recreate", recreate)
@@ -105,6 +121,7 @@ def _hooks(lc_ref: list):
         app.router.add_post("/_fake/user", user)
         app.router.add_post("/_fake/worker", worker)
         app.router.add_get("/_fake/kubelet", kubelet)
+        app.router.add_get("/_fake/preemptions", preemptions)
     return install
 
 

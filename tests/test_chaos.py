@@ -49,3 +49,25 @@ def test_chaos_with_leases_ends_them_across_worker_kills():
     out = json.loads(res.stdout.strip().splitlines()[-1])
     assert out["worker_kills"] == 2 and out["leases"]["attached"] > 0
     assert out["invariant_violations"] == 0, out["violation_examples"]
+
+
+def test_chaos_with_preemptors_never_takes_a_tenants_gpu():
+    """--preempt-rate: a priority-1000 Pod that wants every GPU of node-0 comes and goes while
+    the worker is SIGKILLed. Under the shipped floor class no placeholder that books a tenant's
+    GPU is ever its victim — only idle standbys at the low pool class are. The negative control,
+    placeholders at the reference's priority 0, has the scheduler preempt them."""
+    base = [sys.executable, "bench/configs.py", "chaos", "--rounds", "8", "--kill-every", "4",
+            "--seed", "5", "--restart-rate", "0.3", "--preempt-rate", "1", "--preempt-gpus", "8"]
+    res = subprocess.run(base + ["--warm-pool", "2", "--pool-priority-class",
+                                 "gpumounter-standby"], cwd=ROOT, capture_output=True, text=True,
+                         timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out["preemptors"] > 0 and out["preempted"]["placeholder"] == 0
+    assert out["invariant_violations"] == 0, out["violation_examples"]
+    res = subprocess.run(base + ["--no-placeholder-priority"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out["preempted"]["placeholder"] > 0
+    assert any("preempted" in v for v in out["violation_examples"]), out["violation_examples"]
