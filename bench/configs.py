@@ -410,12 +410,13 @@ def chaos(args) -> dict:
             rnd = random.Random(args.seed * 131 + rnd_i)
             if rnd.random() < args.preempt_rate:
                 name = f"preemptor-{rnd_i}"
+                want = args.preempt_gpus or rnd.randint(1, 2)
                 code, _ = _http_json("POST", f"{api}/api/v1/namespaces/default/pods", {
                     "metadata": {"name": name},
                     "spec": {"priorityClassName": "chaos-high",
                              "nodeSelector": {"kubernetes.io/hostname": "node-0"},
                              "containers": [{"name": "c", "image": "x:1", "resources": {
-                                 "limits": {"amd.com/gpu": str(args.preempt_gpus or rnd.randint(1, 2))}}}]}})
+                                 "limits": {"amd.com/gpu": str(want)}}}]}})
                 preemptors.append(name)     # a failed POST may have taken effect: delete it too
                 if code == 201:
                     preempted[0] += 1

@@ -9,8 +9,9 @@ import sys
 
 def main(dirs) -> int:
     print("| sweep | seeds | runs | worker / master kills | kubelet restarts | container "
-          "restarts / Pod re-creations | ops ok | invariant violations |")
-    print("|---|---|---|---|---|---|---|---|")
+          "restarts / Pod re-creations | preemptors / standbys preempted | ops ok | invariant "
+          "violations |")
+    print("|---|---|---|---|---|---|---|---|---|")
     total = 0
     for d in dirs:
         rows = [json.loads(ln) for ln in open(f"{d}/runs.jsonl") if ln.strip()]
@@ -19,10 +20,13 @@ def main(dirs) -> int:
             return sum(int(r.get(k) or 0) for r in rows)
         seeds = sorted({int(r["seed"]) for r in rows})
         v = tot("invariant_violations")
+        standby = sum((r.get("preempted") or {}).get("standby", 0) for r in rows)
         total += v
         print(f"| `{d.rstrip('/').split('/')[-1]}` | {seeds[0]}–{seeds[-1]} | {len(rows)} | "
               f"{tot('worker_kills')} / {tot('master_kills')} | {tot('kubelet_restarts')} | "
-              f"{tot('container_restarts')} / {tot('pod_recreates')} | {tot('ops_ok')} | "
+              f"{tot('container_restarts')} / {tot('pod_recreates')} | "
+              f"{tot('preemptors')} / {standby} | "
+              f"{tot('ops_ok')} | "
               f"**{v}** |")
     return 1 if total else 0
 
