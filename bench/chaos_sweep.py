@@ -43,6 +43,10 @@ MODES = {
     "pre": CHURN + ["--warm-pool", "2", "--pool-priority-class", "gpumounter-standby",
                     "--preempt-rate", "0.5"],
     "pre0": CHURN + ["--preempt-rate", "0.5"],
+    # placeholders bound to the node at creation (no scheduling cycle), racing preemptors the
+    # scheduler binds, with a warm pool and leases
+    "dir": CHURN + ["--placeholder-binding", "direct", "--preempt-rate", "0.5",
+                    "--warm-pool", "2", "--lease-rate", "0.3"],
 }
 
 

@@ -370,6 +370,8 @@ def chaos(args) -> dict:
            "GM_WARM_POOL_SIZE": str(args.warm_pool), "GM_PLACEMENT_ENFORCE": args.placement}
     if args.pool_priority_class:
         env["GM_POOL_PRIORITY_CLASS"] = args.pool_priority_class
+    if args.placeholder_binding:
+        env["GM_PLACEHOLDER_BINDING"] = args.placeholder_binding
     if args.no_placeholder_priority:
         env["GM_PLACEHOLDER_PRIORITY_CLASS"] = ""       # the reference's priority 0
     if args.log_dir:
@@ -874,6 +876,8 @@ def main() -> int:
                          "pod-blind topology choice")
     ap.add_argument("--device-plugin", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0)
+    ap.add_argument("--placeholder-binding", default="", choices=("", "scheduler", "direct"),
+                    help="chaos: GM_PLACEHOLDER_BINDING for the workers (default: the shipped)")
     ap.add_argument("--no-placeholder-priority", action="store_true",
                     help="chaos: placeholders without the floor PriorityClass (the reference's "
                          "priority 0), the negative control for --preempt-rate")

@@ -323,6 +323,8 @@ class PlaceholderManager:
             }],
         }
         md["annotations"][ANN_GPUS] = str(n_gpus)
+        if self.direct:
+            spec["nodeName"] = self.node        # the kubelet admits it; no scheduling cycle
         if self.dra:
             res = spec["containers"][0]["resources"]
             res.pop("limits")
@@ -337,6 +339,11 @@ class PlaceholderManager:
     def reownable(self) -> bool:
         """Placeholders can change holder (warm-pool claims and give-backs, cluster/pool.py)."""
         return getattr(self.cfg, "warm_pool_size", 0) > 0
+
+    @property
+    def direct(self) -> bool:
+        """Placeholders are bound to this node at creation (placeholder_binding=direct)."""
+        return getattr(self.cfg, "placeholder_binding", "scheduler") == "direct"
 
     @property
     def dra(self) -> bool:
@@ -684,8 +691,10 @@ class PlaceholderManager:
                         bound_keys.append(key)
                         news = seen.get(key) != pod["metadata"].get("resourceVersion")
                         if ck is None:
-                            if news:
-                                fresh.append(key)     # bound, and news since our last read
+                            if news and (not self.direct or _admitted(pod)):
+                                # bound, and news since our last read (bound at creation:
+                                # once the kubelet has admitted it)
+                                fresh.append(key)
                         else:
                             if news and _admitted(pod):
                                 # the kubelet writes the checkpoint at Allocate, before it

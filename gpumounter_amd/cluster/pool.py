@@ -108,6 +108,7 @@ class WarmPool:
 
     def pending(self) -> int:
         return sum(1 for p in self.ph.live() if is_standby(p)
+                   and podu.phase_of(p) != "Failed"
                    and self.ph.cached(p) is None
                    and not self.ph.last_ledger.get((p["metadata"]["namespace"],
                                                     p["metadata"]["name"])))
@@ -182,6 +183,14 @@ class WarmPool:
 
     async def refill(self) -> int:
         """Create standby placeholders until ``target`` are admitted or pending."""
+        # standbys the kubelet refused at admission (placeholder_binding=direct on a full node;
+        # their refill's worker died before it could drop them): terminal, they hold nothing
+        failed = [PlaceholderManager.from_pod(p, {}) for p in self.ph.live()
+                  if is_standby(p) and podu.phase_of(p) == "Failed"]
+        if failed:
+            for ph in failed:
+                ph.owner_uid, ph.attach_id = "", ""
+            await self.ph.release(failed)
         missing = self.target - len(self.standby()) - self.pending()
         if missing <= 0:
             return 0

@@ -455,7 +455,11 @@ class FakeCluster:
             await asyncio.sleep(ms / 1e3)
 
     async def _schedule(self, ns: str, name: str) -> None:
-        await self._sleep(self.latency.schedule_ms)
+        pod = self.pods.get((ns, name))
+        direct = pod is not None and bool(podu.node_of(pod)) and not self.dra.refs(pod)
+        if not direct:
+            # a Pod created with spec.nodeName is the kubelet's at once: no scheduling cycle
+            await self._sleep(self.latency.schedule_ms)
         pod = self.pods.get((ns, name))
         if pod is None or podu.is_terminating(pod):
             return
@@ -482,6 +486,20 @@ class FakeCluster:
             pod["spec"]["nodeName"] = node_name
         elif podu.node_of(pod):
             node_name = podu.node_of(pod)
+            n = self.nodes.get(node_name)
+            if n is not None and direct:
+                # the kubelet's own admission (GeneralPredicates): what the Pods bound to the
+                # node request, against its capacity; nominations are the scheduler's business
+                want = podu.resource_limit(pod, n.resource)
+                used = self._used(n.name, n.resource, (ns, name))
+                if want and used + want > n.capacity:
+                    pod["status"]["phase"] = "Failed"
+                    pod["status"]["reason"] = f"OutOf{n.resource}"
+                    pod["status"]["message"] = (
+                        f"Pod was rejected: Node didn't have enough resource: {n.resource}, "
+                        f"requested: {want}, used: {used}, capacity: {n.capacity}")
+                    self._bump("MODIFIED", pod)
+                    return
         else:
             sel = pod["spec"].get("nodeSelector", {}) or {}
             node_name = ""

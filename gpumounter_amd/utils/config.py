@@ -63,6 +63,13 @@ class Config:
     dra_bdf_attribute: str = "pciAddr"    # ResourceSlice device attribute holding the PCI BDF
     placeholder_image: str = "registry.k8s.io/pause:3.9"  # placeholder container image
     placeholder_pull_policy: str = "IfNotPresent"  # no registry round trip per attach
+    # How placeholders reach the node: "scheduler" = a nodeSelector, kube-scheduler binds them
+    # (the reference: allocator.go:189-234); "direct" = spec.nodeName set at creation, so the
+    # kubelet admits them without a scheduling cycle and bind write. Direct binding bypasses the
+    # scheduler: its nominations for preemptors and a Pod it binds to the node at the same
+    # moment (which the kubelet may then reject, OutOfamd.com/gpu). Not with gpu_allocation=dra
+    # (the scheduler allocates ResourceClaims)
+    placeholder_binding: str = "scheduler"
     # The floor PriorityClass of placeholders (deploy/placeholder-priority.yaml: value 1000000,
     # preemptionPolicy Never). A placeholder backs a GPU its tenant is using, so it must never
     # rank below that tenant: it gets this class, or the tenant's own class when the tenant
@@ -326,6 +333,10 @@ class Config:
         _choice("ledger_source", self.ledger_source, ("auto", "podresources"))
         _choice("gpu_allocation", self.gpu_allocation, ("device-plugin", "dra"))
         _choice("master_transport", self.master_transport, ("auto", "grpc"))
+        _choice("placeholder_binding", self.placeholder_binding, ("scheduler", "direct"))
+        if self.gpu_allocation == "dra" and self.placeholder_binding == "direct":
+            raise ValueError("placeholder_binding=direct: with gpu_allocation=dra the scheduler "
+                             "must allocate the placeholders' ResourceClaims")
         if self.gpu_allocation == "dra" and self.device_plugin:
             raise ValueError("device_plugin serves the extended resource; with "
                              "gpu_allocation=dra the GPUs belong to the DRA driver")

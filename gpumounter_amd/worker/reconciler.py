@@ -630,6 +630,13 @@ class Reconciler:
                             ann.get(ANN_INCARNATION) != svc.ph.incarnation:
                         stuck.append(p)
                         m.reconcile_actions.labels(action="dead_attach_release").inc()
+                    elif podu.phase_of(p) == "Failed" and led is not None and \
+                            not led.get((p["metadata"]["namespace"], name)):
+                        # refused at admission (OutOf<resource>: a directly bound placeholder
+                        # on a full node) and no attach of this owner is running (its lock is
+                        # held): terminal, it holds no device
+                        stuck.append(p)
+                        m.reconcile_actions.labels(action="failed_release").inc()
                     elif podu.is_unschedulable(p) or podu.phase_of(p) == "Failed":
                         first = self._first_seen.setdefault(name, now)
                         if now - first >= self.stuck_after_s:
