@@ -427,3 +427,6 @@ TestLedgerTrimPool = _case("LedgerTrimPool", {"worker_overrides": {
 # idle standbys preemptible (gpumounter-standby, value -10); attaches yield them
 TestLedgerLowPool = _case("LedgerLowPool", {"worker_overrides": {
     "warm_pool_size": 2, "pool_priority_class": "gpumounter-standby"}})
+# placeholders bound to the node at creation: the kubelet refuses those without room
+TestLedgerDirectPool = _case("LedgerDirectPool", {"worker_overrides": {
+    "warm_pool_size": 2, "placeholder_binding": "direct"}})
