@@ -792,12 +792,20 @@ class PlaceholderManager:
                                f"GPU(s), the kubelet reports {len(ids)}")
 
     # ------------------------------------------------------------------------ release
-    async def _delete(self, p: Placeholder) -> Optional[dict]:
+    async def _delete(self, p: Placeholder, candidate_only: bool = False) -> Optional[dict]:
         """DELETE one placeholder, only at a version at which it still has the holder the
         caller's view showed (``p.owner_uid``, ``p.attach_id``), so a release decided on a stale
         view never takes a GPU from the Pod that claimed it since (raises :class:`Reowned`).
         Any placeholder can change hands, whatever its name: the surplus of a trim pick goes
-        back to the warm pool under its ``<pod>-slave-pod-`` name and is claimed from there."""
+        back to the warm pool under its ``<pod>-slave-pod-`` name and is claimed from there.
+
+        ``candidate_only``: released *because* the caller's view shows it an unconfirmed
+        candidate of a pick. That view may be a relisted cache from before the pick confirmed
+        it (the confirm's write-through is dropped across a relist until a GET re-reads it), and
+        a confirmed pick is mounted — so the apiserver's version decides, and the DELETE is
+        conditional on it (raises :class:`Reowned` when it is no candidate any more)."""
+        if candidate_only:
+            return await self._delete_candidate(p)
         if not self.reownable and p.uid:
             # no warm pool: nothing ever claims a placeholder from another holder, so the UID
             # alone pins the object the caller saw. (A version precondition would also trip
@@ -831,7 +839,23 @@ class PlaceholderManager:
                 rv = cur["metadata"].get("resourceVersion", "")
         raise ApiError(409, f"{p.name} kept changing while being deleted")
 
-    async def release(self, phs: Sequence[Placeholder]) -> None:
+    async def _delete_candidate(self, p: Placeholder) -> Optional[dict]:
+        for _ in range(self.DELETE_ATTEMPTS):
+            cur = await self.kube.get_pod(p.namespace, p.name)
+            if p.uid and cur["metadata"].get("uid") != p.uid:
+                raise NotFound(404, f"{p.name}: another pod of that name")
+            if ANN_CANDIDATE not in (cur["metadata"].get("annotations") or {}) or \
+                    not p.held_by_me(cur):
+                raise Reowned(p.name)       # confirmed (or claimed) since the caller looked
+            try:
+                return await self.kube.delete_pod(
+                    p.namespace, p.name, grace_period_s=0, uid=p.uid or "",
+                    resource_version=cur["metadata"].get("resourceVersion", ""))
+            except Conflict:
+                continue                    # it changed since the GET: look again
+        raise ApiError(409, f"{p.name} kept changing while being deleted")
+
+    async def release(self, phs: Sequence[Placeholder], candidates_only: bool = False) -> None:
         """Delete the placeholders (grace 0, conditional on the holder the caller saw).
 
         A DELETE answered 200 or 404 ends the release: with grace 0 and no finalizers the
@@ -840,7 +864,8 @@ class PlaceholderManager:
         waits for the watch's DELETED echo: the UIDs stay tombstoned until it arrives, so
         every later view (owned_by, live, the free set) already leaves them out. A DELETE whose
         outcome is unknown (5xx, a lost reply, retries exhausted) raises ReserveError and the
-        caller's follow-up retries it."""
+        caller's follow-up retries it. ``candidates_only``: each only while the apiserver still
+        shows it an unconfirmed candidate of a pick (:meth:`_delete`)."""
         if not phs:
             return
         with trace.span("ledger_release", placeholders=len(phs)):
@@ -852,11 +877,13 @@ class PlaceholderManager:
             for p in phs:
                 if p.uid:
                     self.tombstones[p.uid] = now
-            res = await asyncio.gather(*[self._delete(p) for p in phs], return_exceptions=True)
+            res = await asyncio.gather(*[self._delete(p, candidates_only) for p in phs],
+                                       return_exceptions=True)
             failed, reowned = [], []
             for p, r in zip(phs, res):
                 if isinstance(r, Reowned):          # someone else's now: not ours to delete
-                    _log.info("placeholder %s/%s changed owner; left to it", p.namespace, p.name)
+                    _log.info("placeholder %s/%s changed owner or was confirmed; left to it",
+                              p.namespace, p.name)
                     reowned.append(p)
                     if p.uid:
                         self.tombstones.pop(p.uid, None)

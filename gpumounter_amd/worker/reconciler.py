@@ -328,14 +328,18 @@ class Reconciler:
                 else:
                     owner = svc.node_pods.get(ns, name)
                     if key[0] == "followup":
+                        if key[3]:
+                            await self._drop(sorted(key[3]))
                         # candidates of a pick are never an owner's; under the pod's lock no
-                        # pick is running, so any left belong to a failed one
+                        # pick is running, so any left belong to a failed one. The cache may
+                        # predate the pick's confirm (a relist), so each goes only if the
+                        # apiserver still shows it a candidate
                         cands = [] if owner is None else [
                             p for p in svc.ph.owned_by(owner, candidates=True)
                             if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})]
-                        drop = set(key[3]) | {_held(p) for p in cands}
-                        if drop:
-                            await self._drop(sorted(drop))
+                        if cands:
+                            await self._drop(sorted({_held(p) for p in cands} - set(key[3])),
+                                             candidates_only=True)
                     if owner is None or podu.phase_of(owner) != "Running":
                         return
                     fixed = await svc.reconcile_pod(owner)
@@ -369,11 +373,13 @@ class Reconciler:
             svc.metrics.reconcile_actions.labels(action="event_retry").inc()
             self._retry(key, attempt + 1)
 
-    async def _drop(self, phs) -> None:
+    async def _drop(self, phs, candidates_only: bool = False) -> None:
         """Release the placeholders of a failed attach that still exist (same UID), each only
         while it has the holder the attach left it with: one that went back to the warm pool
         and was claimed since (by another Pod, or by a later attach of this one) is not the
-        failed attach's to release (cluster/placeholder.py ``_delete``, pool ``give_back``)."""
+        failed attach's to release (cluster/placeholder.py ``_delete``, pool ``give_back``).
+        ``candidates_only``: found as unconfirmed candidates in the cache, each deleted only
+        while the apiserver still shows it one."""
         svc = self.svc
         left = []
         for ns, name, uid, owner_uid, attach_id in phs:
@@ -384,7 +390,10 @@ class Reconciler:
                 ph.owner_uid, ph.attach_id = owner_uid, attach_id
                 left.append(ph)
         if left:
-            await svc._release(left)
+            if candidates_only:
+                await svc.ph.release(left, candidates_only=True)
+            else:
+                await svc._release(left)
             svc.metrics.reconcile_actions.labels(action="followup_release").inc(len(left))
         for _, _, uid, _, _ in phs:
             svc.abandoned.pop(uid, None)
@@ -605,12 +614,18 @@ class Reconciler:
                 # candidates of a trim/correction pick whose attach is not running (its worker
                 # died mid-pick): never the owner's, never mounted — give the GPUs back
                 # and placeholders of failed attaches whose release the follow-up gave up on
-                cands = [p for p in phs
-                         if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})
-                         or svc.is_abandoned(p)]
+                marked = [p for p in phs
+                          if ANN_CANDIDATE in (p["metadata"].get("annotations") or {})
+                          and not svc.is_abandoned(p)]
+                cands = marked + [p for p in phs if svc.is_abandoned(p)]
                 if cands:
                     rep.stuck += [p["metadata"]["name"] for p in cands]
-                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in cands])
+                    # a candidate mark in the cache is only gone once the confirm's write is
+                    # re-read: the apiserver decides (cluster/placeholder.py _delete)
+                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in marked],
+                                         candidates_only=True)
+                    await svc.ph.release([svc.ph.from_pod(p, {}) for p in cands
+                                          if p not in marked])
                     for p in cands:
                         svc.abandoned.pop(p["metadata"].get("uid", ""), None)
                     phs = [p for p in phs if p not in cands]

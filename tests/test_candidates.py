@@ -1,0 +1,35 @@
+"""A pick's candidate mark seen in a stale cache (worker/reconciler.py follow-up and sweep,
+cluster/placeholder.py ``_delete(candidate_only=True)``)."""
+import asyncio
+import copy
+
+from gpumounter_amd.cluster.pool import is_standby
+from gpumounter_amd.fakes.harness import LocalCluster
+from gpumounter_amd.models.types import ANN_CANDIDATE
+
+
+def test_a_stale_candidate_mark_never_releases_a_mounted_placeholder():
+    """Chaos sweep4 f644: a pick's confirm PATCH landed while the placeholder watch relisted;
+    the relisted cache still showed the candidate mark, and the attach's follow-up (its
+    surplus release had failed) took the mark for a failed pick's and deleted a mounted
+    placeholder — the GPU was revoked from the Pod after a 200. The follow-up and the sweep
+    now delete a candidate only while the apiserver still shows it one."""
+    async def main():
+        async with LocalCluster() as lc:
+            w = lc.nodes["node-0"].worker
+            lc.tenant("t")
+            code, b = await lc.add("default", "t", 1)
+            assert code == 200
+            ph = next(p for p in lc.cluster.placeholders() if not is_standby(p))
+            key = (ph["metadata"]["namespace"], ph["metadata"]["name"])
+            stale = copy.deepcopy(w.service.ph.informer.cache[key])
+            stale["metadata"].setdefault("annotations", {})[ANN_CANDIDATE] = "x"
+            w.service.ph.informer.cache[key] = stale        # the relisted, pre-confirm view
+            w.reconciler.follow_up("default", "t")
+            await asyncio.sleep(0.3)
+            assert lc.cluster.get(*key) is not None, "mounted placeholder deleted"
+            w.service.ph.informer.cache[key] = stale
+            await w.reconciler.run_once()
+            assert lc.cluster.get(*key) is not None, "mounted placeholder deleted by the sweep"
+            assert not await lc.audit("default", "t")
+    asyncio.run(main())

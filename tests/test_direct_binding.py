@@ -117,3 +117,4 @@ def test_placeholders_refused_at_admission_are_released_at_once():
             assert ph["metadata"]["name"] not in names and sb["metadata"]["name"] not in names
             assert not await lc.audit("default", "t")
     asyncio.run(main())
+
