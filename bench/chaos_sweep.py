@@ -23,6 +23,18 @@ BASE = ["--rounds", "100", "--kill-every", "5", "--master-kill-every", "3",
         "--api-fault-rate", "0.1", "--kubelet-restart-every", "7", "--reconcile-period", "30",
         "--faults", "--deploy", "processes"]
 CHURN = ["--restart-rate", "0.3", "--recreate-rate", "0.1"]
+
+
+def _commit() -> str:
+    """The code under test (the frozen worktree's HEAD); "" outside git (a GPU box copy)."""
+    try:
+        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"],
+                              capture_output=True, text=True, timeout=10).stdout.strip()
+    except (OSError, subprocess.SubprocessError):
+        return ""
+
+
+COMMIT = _commit()
 MODES = {
     "f": CHURN,
     "pool": CHURN + ["--warm-pool", "2"],
@@ -64,7 +76,7 @@ def one(mode: str, seed: int, out: str, timeout: float) -> dict:
     except subprocess.TimeoutExpired:
         res = {"error": f"timed out after {timeout:g}s"}
     res.update(run=key, mode=mode, seed=seed, wall_s=round(time.time() - t0, 1),
-               argv=argv[2:])
+               argv=argv[2:], commit=COMMIT)
     if res.get("invariant_violations") == 0 and "error" not in res:
         shutil.rmtree(logs, ignore_errors=True)     # a clean run's logs are not kept
     return res
