@@ -32,9 +32,15 @@ def lib_path(name: str) -> str:
 
 
 def build(target: str = "all", quiet: bool = True) -> None:
-    """Run the native Makefile (``host`` needs only g++; ``all`` also needs hipcc)."""
+    """Run the native Makefile (``host`` needs only g++; ``all`` also needs hipcc). Processes
+    that autobuild at the same time (daemons started together in a fresh tree) take turns on
+    a lock file; the Makefile renames each library into place whole."""
+    import fcntl
     cmd = ["make", "-C", NATIVE_DIR, target, f"-j{min(8, os.cpu_count() or 1)}"]
-    res = subprocess.run(cmd, capture_output=quiet, text=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    with open(os.path.join(LIB_DIR, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        res = subprocess.run(cmd, capture_output=quiet, text=True)
     if res.returncode != 0:
         raise NativeError(f"native build failed ({' '.join(cmd)}):\n{res.stdout}\n{res.stderr}")
 

@@ -612,6 +612,12 @@ class PlaceholderManager:
                 self.informer.upsert(r, epoch)  # visible to owned_by() before the watch echo
         errors = [r for r in results if not isinstance(r, dict)]
         if errors:
+            # a POST that failed may still have created its placeholder (an error after the
+            # write, a reply lost after the retries): no watch event need have arrived yet, so
+            # neither a follow-up nor a sweep would see it for a while — reap it by its name,
+            # which is this attach's alone, before anything else can fail
+            await self._reap_unknown([b for b, r in zip(bodies, results)
+                                      if not isinstance(r, dict)])
             await self.release(created)
             if self.dra:
                 await self._delete_unused_claims(
@@ -628,6 +634,40 @@ class PlaceholderManager:
             await self.release(created)
             raise
         return created
+
+    async def _reap_unknown(self, bodies: Sequence[dict]) -> None:
+        """Delete whatever exists under the names of ``bodies``, whose create failed: each was
+        generated for one attach, so an object of that name with its owner and attach id is a
+        create of ours that took effect. The UID comes from a GET (tombstoned first, so the
+        DELETED echo is not taken for a foreign delete). What cannot be read or deleted here is
+        left to the sweep (a candidate mark or a dead attach gives it away)."""
+        for b in bodies:
+            md = b["metadata"]
+            ann = md.get("annotations") or {}
+            try:
+                cur = await self.kube.get_pod(md["namespace"], md["name"])
+            except NotFound:
+                continue                            # the create did not take effect
+            except Exception as e:  # noqa: BLE001
+                _log.warning("placeholder %s/%s: create failed and the read back failed too: "
+                             "%s", md["namespace"], md["name"], e)
+                continue
+            theirs = cur["metadata"].get("annotations") or {}
+            if any(theirs.get(k) != ann.get(k) for k in (ANN_OWNER_UID, ANN_ATTACH_ID)):
+                continue
+            uid = cur["metadata"].get("uid", "")
+            self.tombstones[uid] = asyncio.get_running_loop().time()
+            try:
+                await self.kube.delete_pod(md["namespace"], md["name"], grace_period_s=0,
+                                           uid=uid)
+                _log.info("placeholder %s/%s: its create failed but had taken effect; "
+                          "deleted", md["namespace"], md["name"])
+            except NotFound:
+                pass
+            except Exception as e:  # noqa: BLE001
+                self.tombstones.pop(uid, None)
+                _log.warning("placeholder %s/%s: create failed but had taken effect, and the "
+                             "delete failed: %s", md["namespace"], md["name"], e)
 
     async def _await_admission(self, phs: List[Placeholder], timeout: float,
                                tolerant: bool = False) -> List[Placeholder]:

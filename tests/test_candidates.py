@@ -33,3 +33,23 @@ def test_a_stale_candidate_mark_never_releases_a_mounted_placeholder():
             assert lc.cluster.get(*key) is not None, "mounted placeholder deleted by the sweep"
             assert not await lc.audit("default", "t")
     asyncio.run(main())
+
+
+def test_a_create_that_failed_after_taking_effect_is_reaped_at_once():
+    """Chaos sweep6 pre0660: a placeholder POST took effect but every answer was lost; the
+    reservation failed and released what it knew of, and the placeholder it did not know of
+    held a GPU until the next periodic sweep (30 s). Its name is the attach's own, so the
+    failed reservation reads it back and deletes it at once."""
+    async def main():
+        async with LocalCluster(worker_overrides={"reconcile_on_events": False}) as lc:
+            lc.tenant("t")
+            lc.cluster.fail_next("POST", 503, count=20, after=True)
+            code, _ = await lc.add("default", "t", 1)
+            assert code == 500
+            await asyncio.sleep(0.2)
+            left = [p["metadata"]["name"] for p in lc.cluster.placeholders()]
+            assert not left, f"placeholders left behind: {left}"
+            lc.cluster._faults.clear()            # noqa: SLF001 - any left unconsumed
+            code, b = await lc.add("default", "t", 8)
+            assert code == 200 and len(b["devices"]) == 8
+    asyncio.run(main())
