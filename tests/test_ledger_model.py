@@ -337,6 +337,14 @@ class LedgerModel(RuleBasedStateMachine):
             self.steps.append(f"next {method} fails {'after' if after else 'before'} applying")
             self.tc.call(_sync(self.lc.cluster.fail_next, method, 503, 1, after))
 
+    @rule(method=st.sampled_from(["POST", "PATCH", "DELETE"]), after=st.booleans())
+    def apiserver_outage(self, method, after):
+        """The next five requests with a method on a pod fail — every retry of one request (a
+        write that took effect with all its replies lost, when ``after``): the operation fails
+        for good and must leave nothing behind that outlives its clean-up."""
+        self.steps.append(f"next 5 {method}s fail {'after' if after else 'before'} applying")
+        self.tc.call(_sync(self.lc.cluster.fail_next, method, 503, 5, after))
+
     # ------------------------------------------------------------------------ invariants
     async def _view(self):
         """(why not converged | None, {tenant: {uuid: (placeholder, lease_expires, entire)}})."""
