@@ -163,6 +163,7 @@ class FakeCluster:
         self._faults: List[Tuple[str, int, bool, str]] = []
         self._random_faults: Optional[Tuple[float, Any]] = None   # (rate, random.Random)
         self.random_faults_served = 0
+        self.last_fault_at = 0.0    # time.monotonic() when an injected failure was last served
         # every pod watch event reaches its watchers this much later (a slow watch cache, a
         # congested apiserver); order is kept
         self.watch_delay_s = 0.0
@@ -841,6 +842,7 @@ class FakeCluster:
             for i, (m, st, after, path) in enumerate(self._faults):
                 if m == request.method and path in request.path:
                     del self._faults[i]
+                    self.last_fault_at = time.monotonic()
                     if after:
                         await self._lost_reply(handler, request)
                     return web.json_response({"kind": "Status", "code": st,
