@@ -49,6 +49,9 @@ class LatencyModel:
     pull_ms: float = 0.0       # image pull when required by pull policy
     start_ms: float = 0.0      # container start → Running
     stop_ms: float = 0.0       # SIGTERM → exit for images that handle SIGTERM
+    # a deleted Pod → its containers and sandbox stopped on the node: until then the kubelet
+    # counts it active and its devices stay allocated (0 = the next loop turn)
+    teardown_ms: float = 0.0
     grace_scale: float = 0.0   # fraction of terminationGracePeriodSeconds waited when an image
                                # ignores SIGTERM (1.0 = real time)
 
@@ -56,7 +59,7 @@ class LatencyModel:
     def realistic(cls) -> "LatencyModel":
         """Order-of-magnitude figures for a small on-prem cluster (documented in BASELINE.md)."""
         return cls(api_ms=1.0, schedule_ms=10.0, admit_ms=15.0, sandbox_ms=300.0, pull_ms=1200.0,
-                   start_ms=120.0, stop_ms=50.0, grace_scale=1.0)
+                   start_ms=120.0, stop_ms=50.0, grace_scale=1.0, teardown_ms=50.0)
 
 
 def _now() -> str:
@@ -702,15 +705,23 @@ class FakeCluster:
         node = self.nodes.get(podu.node_of(pod))
         self._bump("DELETED", pod)
         self._gc(pod)
-        if node is not None:
-            node.pending_release.add((ns, name))
         # The apiserver answers the DELETE once the object is gone from storage; the kubelet
         # learns of it from its own watch and tears the pod down afterwards (containers,
         # device-manager entry, checkpoint). Modelled as the next loop turn: after this
-        # request's reply, before any later request's admission (allocate() also frees it)
+        # request's reply, before any later request's admission (allocate() also frees it);
+        # or, with latency.teardown_ms, that much later (the Pod stays active until then)
         try:
-            asyncio.get_running_loop().call_soon(self._teardown, node, ns, name)
+            loop = asyncio.get_running_loop()
         except RuntimeError:                 # no loop (synchronous test helpers)
+            loop = None
+        if loop is not None and self.latency.teardown_ms > 0:
+            loop.call_later(self.latency.teardown_ms / 1e3, self._teardown, node, ns, name)
+            return
+        if node is not None:
+            node.pending_release.add((ns, name))
+        if loop is not None:
+            loop.call_soon(self._teardown, node, ns, name)
+        else:
             self._teardown(node, ns, name)
 
     def _teardown(self, node: Optional[FakeNode], ns: str, name: str) -> None:

@@ -455,7 +455,11 @@ class GpuMountService:
                 for g in gs]
 
     SLOW_ATTACH_MS = 50.0
-    YIELD_RETRY_S = 0.05     # after yielding standbys: the kubelet's teardown of them
+    # after yielding standbys, the kubelet frees their devices once it has stopped them (tens
+    # to hundreds of ms): until then it refuses a placeholder that needs them at admission
+    # (UnexpectedAdmissionError, or OutOf<resource> for a directly bound one). Retried after
+    # these delays, each time with a new placeholder
+    YIELD_RETRY_S = (0.05, 0.1, 0.2, 0.4)
     LEASE_REBASE_S = 1.0     # an attach slower than this re-stamps its lease (_lease_booked)
 
     def _count_error(self, op: str, e: BaseException) -> None:
@@ -811,23 +815,21 @@ class GpuMountService:
             for ids in ([preferred] if req.is_entire_mount else [[d] for d in preferred]):
                 self.plugin.intend(ids, token)
         try:
-            try:
-                rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
-                                             attach_id=log.request_id.get(),
-                                             container=req.container,
-                                             idempotency_key=req.idempotency_key,
-                                             lease_expires=lease_exp)
-            except InsufficientGPU:
-                if not yielded:
-                    raise
-                # a kubelet that has not torn the yielded standbys down yet refuses their
-                # devices at admission (UnexpectedAdmissionError): once more, a moment later
-                await asyncio.sleep(self.YIELD_RETRY_S)
-                rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
-                                             attach_id=log.request_id.get(),
-                                             container=req.container,
-                                             idempotency_key=req.idempotency_key,
-                                             lease_expires=lease_exp)
+            delays = list(self.YIELD_RETRY_S) if yielded else []
+            while True:
+                try:
+                    rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
+                                                 attach_id=log.request_id.get(),
+                                                 container=req.container,
+                                                 idempotency_key=req.idempotency_key,
+                                                 lease_expires=lease_exp)
+                    break
+                except InsufficientGPU:
+                    if not delays:
+                        raise
+                    # a kubelet that has not torn the yielded standbys down yet refuses their
+                    # devices at admission: again, a moment later
+                    await asyncio.sleep(delays.pop(0))
         except BaseException:
             if claimed:
                 await self.pool.give_back(claimed.placeholders)
