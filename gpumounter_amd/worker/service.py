@@ -455,11 +455,13 @@ class GpuMountService:
                 for g in gs]
 
     SLOW_ATTACH_MS = 50.0
-    # after yielding standbys, the kubelet frees their devices once it has stopped them (tens
-    # to hundreds of ms): until then it refuses a placeholder that needs them at admission
-    # (UnexpectedAdmissionError, or OutOf<resource> for a directly bound one). Retried after
-    # these delays, each time with a new placeholder
-    YIELD_RETRY_S = (0.05, 0.1, 0.2, 0.4)
+    # a deleted Pod's devices are freed by the kubelet once it has stopped the Pod (tens to
+    # hundreds of ms after the DELETE's answer): until then it refuses a placeholder that needs
+    # them at admission (UnexpectedAdmissionError, or OutOf<resource> for a directly bound one)
+    # although the scheduler, and our own ledger view, count them free — after a detach or a
+    # yield of standbys. Such a refusal is retried after these delays, each time with a new
+    # placeholder; a refusal with no GPU free in our view is answered at once
+    ADMISSION_RETRY_S = (0.05, 0.1, 0.2, 0.4)
     LEASE_REBASE_S = 1.0     # an attach slower than this re-stamps its lease (_lease_booked)
 
     def _count_error(self, op: str, e: BaseException) -> None:
@@ -815,7 +817,7 @@ class GpuMountService:
             for ids in ([preferred] if req.is_entire_mount else [[d] for d in preferred]):
                 self.plugin.intend(ids, token)
         try:
-            delays = list(self.YIELD_RETRY_S) if yielded else []
+            delays = list(self.ADMISSION_RETRY_S)
             while True:
                 try:
                     rest = await self.ph.reserve(pod, n - got, req.is_entire_mount, preferred,
@@ -824,11 +826,14 @@ class GpuMountService:
                                                  idempotency_key=req.idempotency_key,
                                                  lease_expires=lease_exp)
                     break
-                except InsufficientGPU:
-                    if not delays:
+                except InsufficientGPU as e:
+                    kubelet = str(e).startswith(("UnexpectedAdmissionError", "OutOf"))
+                    if not delays or not (yielded or (kubelet and self._room(st) >= n - got)):
                         raise
-                    # a kubelet that has not torn the yielded standbys down yet refuses their
-                    # devices at admission: again, a moment later
+                    # a kubelet that has not torn a deleted Pod down yet refuses its devices
+                    # at admission: again, a moment later
+                    _log.info("placeholder refused at admission (%s) with GPUs free in the "
+                              "ledger; retrying in %g s", e, delays[0])
                     await asyncio.sleep(delays.pop(0))
         except BaseException:
             if claimed:
@@ -881,6 +886,20 @@ class GpuMountService:
 
     def _free(self, st: PodGpuState) -> List[AmdGpu]:
         return planning.free_gpus(self.inv, self.ph, self.unhealthy, st)
+
+    def _room(self, st: PodGpuState) -> int:
+        """GPUs free once the kubelet has torn down the Pods gone from the apiserver: those no
+        live Pod holds in the ledger view (which can still list deleted Pods, or be older than
+        the teardown) nor a placeholder of ours."""
+        held = {normalize_device_id(d) for uid, ids in self.ph.device_ids.items()
+                if uid not in self.ph.tombstones for d in ids}
+        for (ns, name), ids in st.ledger.items():
+            p = self.node_pods.get(ns, name) or self.ph.informer.cache.get((ns, name))
+            if p is not None and p["metadata"].get("uid") not in self.ph.tombstones and \
+                    not p["metadata"].get("deletionTimestamp"):
+                held.update(normalize_device_id(d) for d in ids)
+        return sum(1 for g in self.inv.gpus()
+                   if not held.intersection(g.ledger_keys()) and g.index not in self.unhealthy)
 
     def _preferred(self, n: int, st: PodGpuState, free: Optional[List[AmdGpu]] = None
                    ) -> List[str]:

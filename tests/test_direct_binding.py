@@ -118,3 +118,29 @@ def test_placeholders_refused_at_admission_are_released_at_once():
             assert not await lc.audit("default", "t")
     asyncio.run(main())
 
+
+
+@pytest.mark.parametrize("binding", [{}, DIRECT], ids=["scheduler", "direct"])
+def test_an_attach_right_after_a_detach_outlasts_the_kubelets_teardown(binding):
+    """The kubelet frees a deleted Pod's devices only once it has stopped it (here 150 ms after
+    the DELETE's answer). The scheduler, and the worker's own ledger view, count them free at
+    once, so an attach that needs them is refused at admission (UnexpectedAdmissionError; with
+    direct binding OutOfamd.com/gpu). The worker retries such a refusal with backoff while its
+    view has room, instead of answering a full node's 'Insufficient GPU'."""
+    async def main():
+        lat = LatencyModel(teardown_ms=150.0)
+        async with LocalCluster(latency=lat, worker_overrides=binding) as lc:
+            lc.tenant("a")
+            lc.tenant("b")
+            code, b = await lc.add("default", "a", 8)
+            assert code == 200
+            code, _ = await lc.remove("default", "a", [d["uuid"] for d in b["devices"]])
+            assert code == 200
+            code, b = await lc.add("default", "b", 8)
+            assert code == 200 and len(b["devices"]) == 8, b
+            assert not await lc.audit("default", "b")
+            # a node that is really full is still refused at once
+            t0 = time.perf_counter()
+            code, _ = await lc.add("default", "a", 1)
+            assert code == 500 and time.perf_counter() - t0 < 0.5
+    asyncio.run(main())
