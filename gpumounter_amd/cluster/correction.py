@@ -150,6 +150,7 @@ class Correction:
         self.release_quiet = release_quiet
         self.entries: List[List] = []            # [placeholder, Book]
         self.corrected = False
+        self.error: Optional[BaseException] = None  # why the correction gave up, if it did
         self._keys = inv.by_key()
         self._links = inv.links()
         self._table = {g.index: g for g in inv.gpus()}
@@ -275,6 +276,7 @@ class Correction:
 
     async def settle(self, res: Reservation, error: Optional[BaseException]) -> Reservation:
         """The outcome, from the book states alone."""
+        self.error = error
         kept = self.of(Book.KEPT)
         if error is None and self._gpus(kept) == self.n:
             out, self.corrected = Reservation(kept), True

@@ -39,6 +39,7 @@ Unschedulable → InsufficientGPU mapping. Changed:
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import secrets
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -458,7 +459,14 @@ class PlaceholderManager:
             await self.release(created)
             raise
         if failed:
-            await self.release(failed)
+            try:
+                await self.release(failed)
+            except BaseException:
+                # the caller never learns of the admitted ones either: let them go too (the
+                # candidate mark leads the follow-up and the sweep to any this cannot delete)
+                with contextlib.suppress(Exception):
+                    await self.release([p for p in created if p not in failed])
+                raise
         return [p for p in created if p not in failed]
 
     async def reserve_trim(self, owner: dict, total: int, entire: bool, width: int,

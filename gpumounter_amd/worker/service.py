@@ -747,7 +747,14 @@ class GpuMountService:
                        log.request_id.get(), req.container, req.idempotency_key,
                        self.cfg.topology_policy, self.faults,
                        lambda phs: self._release_quiet(pod, phs), lease_exp)
-        out = await c.run(res)
+        try:
+            out = await c.run(res)
+        finally:
+            if c.error is not None:
+                # a hold that failed part-way may have left candidates no book of the
+                # correction holds: the follow-up finds them by their mark, now rather than at
+                # the next periodic sweep
+                self._follow_up(pod)
         if c.corrected:
             self.metrics.placement_corrections.inc()
         return out

@@ -53,3 +53,30 @@ def test_a_create_that_failed_after_taking_effect_is_reaped_at_once():
             code, b = await lc.add("default", "t", 8)
             assert code == 200 and len(b["devices"]) == 8
     asyncio.run(main())
+
+
+def test_a_hold_whose_unschedulable_release_fails_lets_its_admitted_ones_go_too():
+    """Chaos sweep9 pre0692: a correction's hold (hold_singles: 1-GPU candidates for every free
+    GPU) got some admitted and some unschedulable; releasing the unschedulable ones failed after
+    taking effect, the hold raised, and the admitted candidates — which the correction never
+    learned of — held their GPUs until the next periodic sweep. Now the hold lets them go too
+    (and a correction that gave up hands the Pod to the follow-up)."""
+    from gpumounter_amd.utils.faults import FaultInjector, InjectedFault
+
+    async def main():
+        async with LocalCluster() as lc:
+            ph = lc.nodes["node-0"].worker.service.ph
+            owner = lc.tenant("t")
+            ph.faults = FaultInjector("ledger_release:1:after")
+            try:
+                await ph.hold_singles(owner, 10, False, "", "add-x")    # 8 GPUs: 2 refused
+            except InjectedFault:
+                pass
+            else:
+                raise AssertionError("the injected release fault did not fire")
+            finally:
+                ph.faults = FaultInjector("")
+            await asyncio.sleep(0.1)
+            left = [p["metadata"]["name"] for p in lc.cluster.placeholders()]
+            assert not left, f"admitted candidates left behind: {left}"
+    asyncio.run(main())
