@@ -80,6 +80,9 @@ class WarmPool:
         # admission of a new standby wait until no attach/detach is in flight, instead of
         # sharing the worker's loop with the attach that emptied the pool
         self.quiet: Optional[Callable[[], Awaitable[None]]] = None
+        # UIDs of the node's Pods the apiserver still has (the worker sets it): a checkpoint
+        # entry of any other Pod is one being torn down, whose GPUs the next Allocate frees
+        self.live_uids: Optional[Callable[[], set]] = None
 
     @property
     def enabled(self) -> bool:
@@ -161,7 +164,15 @@ class WarmPool:
             except (asyncio.CancelledError, Exception):  # noqa: BLE001
                 pass
 
+    # refill retries after a kubelet refused standbys at admission (a teardown in flight)
+    REFUSED_RETRY_S = (0.1, 0.3, 1.0, 3.0)
+    _refused = 0
+
     def poke(self) -> None:
+        self._refused = 0            # news of capacity: a refusal gets its retries again
+        self._wake_retry()
+
+    def _wake_retry(self) -> None:
         if self._wake is not None:
             self._wake.set()
 
@@ -195,14 +206,17 @@ class WarmPool:
         if missing <= 0:
             return 0
         # only ask for what the node can actually admit (allocatable − allocated). Allocated
-        # comes from the device-manager checkpoint when it is in use (a terminated pod's entry
-        # can linger there until the kubelet's next Allocate: that only under-fills the pool),
-        # else from PodResources; the allocatable set changes only with the plugin's device
-        # list and is re-read every ALLOCATABLE_TTL_S
+        # comes from the device-manager checkpoint when it is in use, counting only Pods the
+        # apiserver still has (a deleted Pod's entry lingers there until the kubelet's next
+        # Allocate, which frees it; one still being torn down gets a standby refused, and the
+        # refill looks again shortly), else from PodResources; the allocatable set changes only
+        # with the plugin's device list and is re-read every ALLOCATABLE_TTL_S
         ck = self.ph.checkpoint
         snap = ck.snapshot() if ck is not None and ck.trusted else None
         if snap is not None:
-            allocated = {normalize_device_id(d) for ids in snap.values() for d in ids}
+            live = self.live_uids() if self.live_uids is not None else None
+            allocated = {normalize_device_id(d) for uid, ids in snap.items()
+                         if live is None or uid in live for d in ids}
         else:
             led = await self.ph.ledger.by_pod()
             self.ph.last_ledger = led
@@ -247,11 +261,20 @@ class WarmPool:
         try:
             await self.ph._await_admission(created, self.cfg.attach_timeout_s)  # noqa: SLF001
             self.exhausted = False
-        except InsufficientGPU:
+            self._refused = 0
+        except InsufficientGPU as e:
             # the node is full: drop the standby placeholders that could not be admitted
             self.exhausted = True
             unadmitted = [c for c in created if not c.device_ids]
             await self.ph.release(unadmitted)
+            if str(e).startswith(("UnexpectedAdmissionError", "OutOf")):
+                # refused by the kubelet, not the scheduler: it still counts GPUs of Pods
+                # deleted a moment ago (their teardown frees them without any event we see),
+                # so look again shortly rather than at the next capacity event
+                if self._refused < len(self.REFUSED_RETRY_S):
+                    delay = self.REFUSED_RETRY_S[self._refused]
+                    self._refused += 1
+                    asyncio.get_running_loop().call_later(delay, self._wake_retry)
         await self.ph.informer.poke()
         return len(created)
 

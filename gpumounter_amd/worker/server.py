@@ -134,6 +134,7 @@ class Worker:
             if self.service.quota.active else None
         self.pool = WarmPool(cfg, self.placeholders, self.inv, self.metrics)
         self.pool.quiet = self.service.notify.quiet
+        self.pool.live_uids = self._live_uids
         self.service.pool = self.pool
         self.plugin = None
         if cfg.device_plugin:
@@ -158,6 +159,15 @@ class Worker:
         self.ready = False
 
     # ------------------------------------------------------------------------ gRPC glue
+
+    def _live_uids(self) -> set:
+        """UIDs of the Pods on this node the apiserver still has (placeholders not released by
+        us included): the kubelet's checkpoint can still list deleted ones."""
+        tomb = self.placeholders.tombstones
+        out = {podu.uid_of(p) for p in self.node_informer.cache.values()}
+        out.update(u for u in (podu.uid_of(p) for p in self.ph_informer.cache.values()
+                               if not p["metadata"].get("deletionTimestamp")) if u not in tomb)
+        return out
     def _peer_allowed(self, context) -> bool:
         """Under mTLS, only the configured client identities (the master's certificate) may call:
         a certificate from the same CA for another component is not enough."""

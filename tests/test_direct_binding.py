@@ -144,3 +144,30 @@ def test_an_attach_right_after_a_detach_outlasts_the_kubelets_teardown(binding):
             code, _ = await lc.add("default", "a", 1)
             assert code == 500 and time.perf_counter() - t0 < 0.5
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("binding", [{}, DIRECT], ids=["scheduler", "direct"])
+def test_the_pool_refills_after_the_kubelet_refused_it_during_a_teardown(binding):
+    """Another workload holds every other GPU, and an operator deletes the standby: the refill
+    that the delete triggers finds the kubelet still counting the standby's GPU (its teardown
+    takes 150 ms here, and a real kubelet's checkpoint keeps a deleted Pod's entry until its
+    next Allocate) and no event follows the teardown. The pool counts only Pods the apiserver
+    still has, and a kubelet refusal is looked at again shortly: it refills without waiting
+    for the next capacity event."""
+    async def main():
+        lat = LatencyModel(teardown_ms=150.0)
+        async with LocalCluster(latency=lat,
+                                worker_overrides={**binding, "warm_pool_size": 1}) as lc:
+            pool = lc.nodes["node-0"].worker.pool
+            end = time.monotonic() + 5
+            while len(pool.standby()) < 1:
+                assert time.monotonic() < end, "pool not filled at start"
+                await asyncio.sleep(0.02)
+            sb = pool.standby()[0]
+            lc.tenant("hog", gpus=7)                     # every other GPU
+            lc.cluster.delete(sb.namespace, sb.name, grace=0)   # an operator deletes the standby
+            end = time.monotonic() + 3
+            while not [p for p in pool.standby() if p.uid != sb.uid]:
+                assert time.monotonic() < end, "pool not refilled after the teardown"
+                await asyncio.sleep(0.02)
+    asyncio.run(main())
