@@ -460,8 +460,9 @@ class GpuMountService:
     # them at admission (UnexpectedAdmissionError, or OutOf<resource> for a directly bound one)
     # although the scheduler, and our own ledger view, count them free — after a detach or a
     # yield of standbys. Such a refusal is retried after these delays, each time with a new
-    # placeholder; a refusal with no GPU free in our view is answered at once
-    ADMISSION_RETRY_S = (0.05, 0.1, 0.2, 0.4)
+    # placeholder (whose own scheduling and admission take time too, so the first retry goes
+    # at once); a refusal with no GPU free in our view is answered at once
+    ADMISSION_RETRY_S = (0.0, 0.02, 0.05, 0.1, 0.2, 0.4)
     LEASE_REBASE_S = 1.0     # an attach slower than this re-stamps its lease (_lease_booked)
 
     def _count_error(self, op: str, e: BaseException) -> None:
@@ -841,7 +842,9 @@ class GpuMountService:
                     # at admission: again, a moment later
                     _log.info("placeholder refused at admission (%s) with GPUs free in the "
                               "ledger; retrying in %g s", e, delays[0])
-                    await asyncio.sleep(delays.pop(0))
+                    delay = delays.pop(0)
+                    if delay:
+                        await asyncio.sleep(delay)
         except BaseException:
             if claimed:
                 await self.pool.give_back(claimed.placeholders)
