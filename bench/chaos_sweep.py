@@ -59,6 +59,12 @@ MODES = {
     # scheduler binds, with a warm pool and leases
     "dir": CHURN + ["--placeholder-binding", "direct", "--preempt-rate", "0.5",
                     "--warm-pool", "2", "--lease-rate", "0.3"],
+    # a kubelet that frees a deleted Pod's devices 50 ms after the DELETE: attaches and pool
+    # refills right after a detach are refused at admission and retried
+    "td": CHURN + ["--latency", "teardown", "--warm-pool", "2", "--pool-priority-class",
+                   "gpumounter-standby", "--lease-rate", "0.3"],
+    "tdd": CHURN + ["--latency", "teardown", "--placeholder-binding", "direct",
+                    "--preempt-rate", "0.5"],
 }
 
 

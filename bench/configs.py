@@ -382,7 +382,8 @@ def chaos(args) -> dict:
                     "GM_KILL_GRACE_S": str(args.kill_grace)})
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
                         master_env={"GM_LOG_LEVEL": "DEBUG"} if args.log_dir else None,
-                        gpu_api=args.gpu_api, log_dir=args.log_dir) as pc, \
+                        gpu_api=args.gpu_api, log_dir=args.log_dir,
+                        latency=args.latency) as pc, \
             (busy or contextlib.nullcontext()):
         for t in tenants:
             pc.tenant(t, pids={"main": busy.pids(t)} if busy else None)
@@ -867,7 +868,9 @@ def main() -> int:
     ap.add_argument("scenario", choices=sorted(SCENARIOS))
     ap.add_argument("--amdsmi", default="mock", help='"mock" (default) or "" for libamd_smi')
     ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
-    ap.add_argument("--latency", choices=("zero", "realistic"), default="zero")
+    ap.add_argument("--latency", choices=("zero", "realistic", "teardown"), default="zero",
+                    help="control-plane latency model; teardown: zero, but the kubelet frees "
+                         "a deleted Pod's devices 50 ms after the DELETE (chaos only)")
     ap.add_argument("--placement", choices=("auto", "hint", "trim"), default="auto")
     ap.add_argument("--alloc-policy", choices=("first-free", "random", "topology"),
                     default="first-free",
@@ -979,7 +982,8 @@ def main() -> int:
         wov["bpf_pin_dir"] = args.sandbox.bpffs
 
     async def run():
-        lat = LatencyModel.realistic() if args.latency == "realistic" else LatencyModel()
+        lat = LatencyModel.realistic() if args.latency == "realistic" else \
+            LatencyModel(teardown_ms=50.0) if args.latency == "teardown" else LatencyModel()
         async with LocalCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, latency=lat,
                                 device_plugin=args.device_plugin, worker_overrides=wov,
                                 alloc_policy=args.alloc_policy, **kw) as lc:

@@ -715,7 +715,9 @@ class FakeCluster:
         except RuntimeError:                 # no loop (synchronous test helpers)
             loop = None
         if loop is not None and self.latency.teardown_ms > 0:
-            loop.call_later(self.latency.teardown_ms / 1e3, self._teardown, node, ns, name)
+            # by UID: the same name may be a new Pod by then (a re-created tenant)
+            loop.call_later(self.latency.teardown_ms / 1e3, self._teardown, node, ns, name,
+                            pod["metadata"]["uid"])
             return
         if node is not None:
             node.pending_release.add((ns, name))
@@ -724,10 +726,10 @@ class FakeCluster:
         else:
             self._teardown(node, ns, name)
 
-    def _teardown(self, node: Optional[FakeNode], ns: str, name: str) -> None:
+    def _teardown(self, node: Optional[FakeNode], ns: str, name: str, uid: str = "") -> None:
         if node is not None:
-            node.release_pod(ns, name)
-            node.stop_pod_containers(ns, name)
+            node.release_pod(ns, name, uid)
+            node.stop_pod_containers(ns, name, uid)
         # capacity freed: retry unschedulable pods (scheduler queue)
         for key in list(self._unschedulable):
             self._spawn(self._schedule(*key))

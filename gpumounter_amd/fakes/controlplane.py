@@ -125,10 +125,20 @@ def _hooks(lc_ref: list):
     return install
 
 
+def _latency(name: str):
+    """``zero`` (none), ``realistic`` (LatencyModel.realistic) or ``teardown`` (zero, except that
+    the kubelet frees a deleted Pod's devices 50 ms after the DELETE: admission refusals)."""
+    if name == "realistic":
+        return LatencyModel.realistic()
+    if name == "teardown":
+        return LatencyModel(teardown_ms=50.0)
+    return None
+
+
 async def run(args) -> None:
     ref: list = [None]
     lc = LocalCluster(n_nodes=args.nodes, amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup,
-                      latency=LatencyModel.realistic() if args.latency == "realistic" else None,
+                      latency=_latency(args.latency),
                       workdir=args.workdir, start_master=False, start_workers=False,
                       node_gpu_bdfs=[b for b in args.gpu_bdfs.split(",") if b] or None,
                       kubelet_limit_mode=args.kubelet_limit, gpu_api=args.gpu_api,
@@ -170,7 +180,7 @@ def main(argv=None) -> int:
                     help="directory (a tmpfs) for the emulated cgroupfs and /dev trees")
     ap.add_argument("--amdsmi", default="mock")
     ap.add_argument("--cgroup", choices=("v1", "v2"), default="v2")
-    ap.add_argument("--latency", choices=("zero", "realistic"), default="zero")
+    ap.add_argument("--latency", choices=("zero", "realistic", "teardown"), default="zero")
     ap.add_argument("--kubelet-limit", choices=("enforce", "count"), default="enforce",
                     help="PodResources limiter (100 qps, burst 10): reject over-budget calls "
                          "with RESOURCE_EXHAUSTED, or serve them and only count them")

@@ -399,8 +399,13 @@ class ProcessCluster:
         return json.loads(body).get("items", []) if code == 200 else []
 
     def audit(self, ns: str, pod: str, node: str = "node-0") -> list:
-        code, body = _http("GET", f"http://127.0.0.1:{self.worker_ports[node][1]}/audit/{ns}/{pod}",
-                           headers=self._auth)
+        for _ in range(5):
+            code, body = _http("GET",
+                               f"http://127.0.0.1:{self.worker_ports[node][1]}/audit/{ns}/{pod}",
+                               headers=self._auth)
+            if code != 409:                 # 409: a container restarting under the audit
+                break
+            time.sleep(0.1)
         if code != 200:
             raise RuntimeError(f"audit {ns}/{pod}: {code} {body[:300]!r}")
         return json.loads(body)["issues"]

@@ -252,10 +252,13 @@ class FakeNode:
             while self.pending_release:
                 self.release_pod(*self.pending_release.pop())
 
-    def release_pod(self, ns: str, pod: str) -> List[str]:
+    def release_pod(self, ns: str, pod: str, uid: str = "") -> List[str]:
+        """Free the pod's devices (``uid``: only that incarnation's — a Pod re-created under
+        the same name keeps its own)."""
         with self._lock:
             self.pending_release.discard((ns, pod))
-            ids = [d for d, (n, p, _) in self.allocated.items() if n == ns and p == pod]
+            ids = [d for d, (n, p, _) in self.allocated.items() if n == ns and p == pod
+                   and (not uid or self.alloc_uid.get(d, "") == uid)]
             for d in ids:
                 del self.allocated[d]
                 self.alloc_uid.pop(d, None)
@@ -360,10 +363,10 @@ class FakeNode:
         else:
             shutil.rmtree(c.root_dir, ignore_errors=True)
 
-    def stop_pod_containers(self, ns: str, pod: str) -> None:
+    def stop_pod_containers(self, ns: str, pod: str, uid: str = "") -> None:
         with self._lock:
             for cid, c in list(self.containers.items()):
-                if c.pod_ns == ns and c.pod_name == pod:
+                if c.pod_ns == ns and c.pod_name == pod and (not uid or c.pod_uid == uid):
                     shutil.rmtree(c.cgroup_dir, ignore_errors=True)
                     # prune empty pod-level cgroup dir like kubelet does
                     parent = os.path.dirname(c.cgroup_dir)

@@ -27,7 +27,7 @@ from gpumounter_amd.cluster.pool import WarmPool
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models import pod as podu
 from gpumounter_amd.node import systemd
-from gpumounter_amd.node.cgroup import CgroupResolver, make_backend
+from gpumounter_amd.node.cgroup import CgroupError, CgroupResolver, make_backend
 from gpumounter_amd.node.checkpoint import DeviceCheckpoint
 from gpumounter_amd.node.devnodes import DevNodeWriter
 from gpumounter_amd.node.dra import DraLedger
@@ -457,11 +457,19 @@ class Worker:
         denied = await self._status_denied(request, ns, name)
         if denied is not None:
             return denied
-        pod = await self.service.get_pod(ns, name, fresh=True)
-        if pod is None:
-            return httpd.json_response({"error": "pod not found"}, status=404)
-        st = await self.service.pod_state(pod, fresh=True)
-        issues = self.service.hm.audit(pod, st.hot, st.own)
+        for attempt in range(3):
+            pod = await self.service.get_pod(ns, name, fresh=True)
+            if pod is None:
+                return httpd.json_response({"error": "pod not found"}, status=404)
+            st = await self.service.pod_state(pod, fresh=True)
+            try:
+                issues = self.service.hm.audit(pod, st.hot, st.own)
+                break
+            except CgroupError as e:
+                # a container restarted between the read and the audit: read the pod again
+                if attempt == 2:
+                    return httpd.json_response({"error": f"pod changing: {e}"}, status=409)
+                await asyncio.sleep(0.05)
         return httpd.json_response({"pod": f"{ns}/{name}", "consistent": not issues,
                                   "issues": [vars(i) for i in issues]})
 
