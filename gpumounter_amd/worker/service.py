@@ -462,7 +462,7 @@ class GpuMountService:
     # yield of standbys. Such a refusal is retried after these delays, each time with a new
     # placeholder (whose own scheduling and admission take time too, so the first retry goes
     # at once); a refusal with no GPU free in our view is answered at once
-    ADMISSION_RETRY_S = (0.0, 0.02, 0.05, 0.1, 0.2, 0.4)
+    ADMISSION_RETRY_S = (0.0, 0.01, 0.02, 0.04, 0.08, 0.16, 0.32)
     LEASE_REBASE_S = 1.0     # an attach slower than this re-stamps its lease (_lease_booked)
 
     def _count_error(self, op: str, e: BaseException) -> None:
