@@ -22,7 +22,8 @@ next one or two of POST / PATCH / DELETE / GET, an outage that fails every retry
 every tenant arriving for GPUs (the scheduler may preempt idle standbys, never a tenant's
 placeholder). Variants: the device-plugin ledger, the warm pool, DRA with a warm pool, trim
 placement with a warm pool, a warm pool whose standbys are preemptible (low
-``pool_priority_class``), direct binding with a warm pool.
+``pool_priority_class``), direct binding with a warm pool, and a kubelet that frees a deleted
+Pod's devices 50 ms late (direct binding, preemptible standbys).
 
 The reference has no locking and no recovery at all (pkg/server/gpu-mount/server.go:34-179,
 SURVEY defect 7). Round-4 bug parents this model fails on: ``bench/model_parents.sh``
@@ -40,6 +41,7 @@ from hypothesis import HealthCheck, Phase, settings
 from hypothesis import strategies as st
 from hypothesis.stateful import RuleBasedStateMachine, invariant, rule
 
+from gpumounter_amd.fakes.apiserver import LatencyModel
 from gpumounter_amd.fakes.harness import ThreadedCluster
 from gpumounter_amd.models import pod as podu
 
@@ -444,3 +446,9 @@ TestLedgerLowPool = _case("LedgerLowPool", {"worker_overrides": {
 # placeholders bound to the node at creation: the kubelet refuses those without room
 TestLedgerDirectPool = _case("LedgerDirectPool", {"worker_overrides": {
     "warm_pool_size": 2, "placeholder_binding": "direct"}})
+# a kubelet that frees a deleted Pod's devices 50 ms after the DELETE (admission refusals and
+# re-bookings after every detach), with direct binding and a pool of preemptible standbys
+TestLedgerTeardown = _case("LedgerTeardown", {
+    "latency": LatencyModel(teardown_ms=50.0),
+    "worker_overrides": {"warm_pool_size": 2, "placeholder_binding": "direct",
+                         "pool_priority_class": "gpumounter-standby"}})
