@@ -39,6 +39,11 @@ class Metrics:
                                        "attaches rolled back because the read-back "
                                        "(attach_verify) found rules or nodes missing",
                                        registry=r)
+        self.admission_refusals = Counter(
+            "gm_admission_refusals_total",
+            "placeholders the kubelet refused at admission (UnexpectedAdmissionError / "
+            "OutOf<resource>), by what followed: booked again while a teardown was in flight, "
+            "or answered as too few GPUs", ["outcome"], registry=r)
         self.gpu_busy = Gauge("gm_gpu_processes", "processes on a GPU (amdsmi)", ["gpu"],
                               registry=r)
         self.plugin_rpcs = Counter("gm_device_plugin_rpcs_total",

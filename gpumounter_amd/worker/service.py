@@ -837,7 +837,10 @@ class GpuMountService:
                 except InsufficientGPU as e:
                     kubelet = str(e).startswith(("UnexpectedAdmissionError", "OutOf"))
                     if not delays or not (yielded or (kubelet and self._room(st) >= n - got)):
+                        if kubelet:
+                            self.metrics.admission_refusals.labels(outcome="refused").inc()
                         raise
+                    self.metrics.admission_refusals.labels(outcome="rebooked").inc()
                     # a kubelet that has not torn a deleted Pod down yet refuses its devices
                     # at admission: again, a moment later
                     _log.info("placeholder refused at admission (%s) with GPUs free in the "
