@@ -601,6 +601,15 @@ class GpuMountService:
                     return api.AddGPUResponse(add_gpu_result=api.ADD_POD_NOT_FOUND,
                                               message=f"pod went away during the attach: {e}")
                 raise RpcError(grpc.StatusCode.INTERNAL, f"{ERR_INTERNAL}: {e}") from e
+            if self._owner_gone(pod):
+                # deleted (maybe re-created under its name) while the attach ran, before the
+                # placeholders existed: the DELETED event's release found nothing to release
+                _log.warning("pod %s/%s was deleted during the attach; releasing its GPUs",
+                             req.namespace, req.pod_name)
+                await self._release_or_follow_up(pod, res.placeholders, "an attach into a "
+                                                                         "deleted pod")
+                return api.AddGPUResponse(add_gpu_result=api.ADD_POD_NOT_FOUND,
+                                          message="pod went away during the attach")
             msg = "Add GPU Success"
             if lease_exp:
                 lease_exp = await self._lease_booked(pod, res.placeholders, lease_exp,
@@ -899,6 +908,15 @@ class GpuMountService:
 
     def _free(self, st: PodGpuState) -> List[AmdGpu]:
         return planning.free_gpus(self.inv, self.ph, self.unhealthy, st)
+
+    def _owner_gone(self, pod: dict) -> bool:
+        """The node-pod watch has seen ``pod`` (this UID) deleted, or its name taken by a new
+        Pod."""
+        key, uid = (podu.ns_of(pod), podu.name_of(pod)), podu.uid_of(pod)
+        if getattr(self.node_pods, "deleted", {}).get(key) == uid:
+            return True
+        cur = self.node_pods.cache.get(key)
+        return cur is not None and podu.uid_of(cur) != uid
 
     def _room(self, st: PodGpuState) -> int:
         """GPUs free once the kubelet has torn down the Pods gone from the apiserver: those no

@@ -80,3 +80,36 @@ def test_a_hold_whose_unschedulable_release_fails_lets_its_admitted_ones_go_too(
             left = [p["metadata"]["name"] for p in lc.cluster.placeholders()]
             assert not left, f"admitted candidates left behind: {left}"
     asyncio.run(main())
+
+
+def test_an_attach_into_a_pod_deleted_before_its_placeholders_existed_is_undone():
+    """Chaos (box sweep 3, td702): the tenant was deleted and re-created under its name while
+    an attach ran, before the attach had created its placeholders. The DELETED event's release
+    found nothing to release, the kubelet had not stopped the old containers yet (its teardown
+    lags the DELETE), so the mount succeeded and the attach answered 200 — and the placeholders
+    of a Pod that no longer existed held their GPUs until the periodic sweep. The attach now
+    checks its Pod at the end, releases what it booked and answers PodNotFound."""
+    from gpumounter_amd.fakes.apiserver import LatencyModel
+
+    async def main():
+        async with LocalCluster(latency=LatencyModel(teardown_ms=500.0),
+                                worker_overrides={"reconcile_on_events": True}) as lc:
+            svc = lc.nodes["node-0"].worker.service
+            old = lc.tenant("t")
+            orig = svc.ph.reserve
+
+            async def reserve(*a, **kw):
+                svc.ph.reserve = orig
+                lc.cluster.delete("default", "t", grace=0)
+                lc.tenant("t")                              # the same name, a new UID
+                await asyncio.sleep(0.1)                    # the worker's watch sees both
+                return await orig(*a, **kw)
+            svc.ph.reserve = reserve
+            code, body = await lc.add("default", "t", 2)
+            assert code != 200, body
+            await asyncio.sleep(0.2)
+            mine = [p["metadata"]["name"] for p in lc.cluster.placeholders()
+                    if (p["metadata"].get("annotations") or {}).get(
+                        "gpumounter.amd.com/owner-uid") == old["metadata"]["uid"]]
+            assert not mine, f"placeholders of the deleted Pod left: {mine}"
+    asyncio.run(main())
