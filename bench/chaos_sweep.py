@@ -65,6 +65,9 @@ MODES = {
                    "gpumounter-standby", "--lease-rate", "0.3"],
     "tdd": CHURN + ["--latency", "teardown", "--placeholder-binding", "direct",
                     "--preempt-rate", "0.5"],
+    # the kubelet's checkpoint keeps deleted Pods until the next Allocate, as a real one does
+    "lz": CHURN + ["--lazy-checkpoint", "--latency", "teardown", "--warm-pool", "2",
+                   "--lease-rate", "0.3"],
 }
 
 

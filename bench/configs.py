@@ -383,7 +383,7 @@ def chaos(args) -> dict:
     with ProcessCluster(amdsmi_lib=args.amdsmi, cgroup_mode=args.cgroup, worker_env=env,
                         master_env={"GM_LOG_LEVEL": "DEBUG"} if args.log_dir else None,
                         gpu_api=args.gpu_api, log_dir=args.log_dir,
-                        latency=args.latency) as pc, \
+                        latency=args.latency, lazy_checkpoint=args.lazy_checkpoint) as pc, \
             (busy or contextlib.nullcontext()):
         for t in tenants:
             pc.tenant(t, pids={"main": busy.pids(t)} if busy else None)
@@ -879,6 +879,9 @@ def main() -> int:
                          "pod-blind topology choice")
     ap.add_argument("--device-plugin", action="store_true")
     ap.add_argument("--warm-pool", type=int, default=0)
+    ap.add_argument("--lazy-checkpoint", action="store_true",
+                    help="chaos: the fake kubelet keeps a deleted Pod in its device-manager "
+                         "checkpoint until the next Allocate, as a real one does")
     ap.add_argument("--placeholder-binding", default="", choices=("", "scheduler", "direct"),
                     help="chaos: GM_PLACEHOLDER_BINDING for the workers (default: the shipped)")
     ap.add_argument("--no-placeholder-priority", action="store_true",

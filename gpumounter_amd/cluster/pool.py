@@ -167,6 +167,7 @@ class WarmPool:
     # refill retries after a kubelet refused standbys at admission (a teardown in flight)
     REFUSED_RETRY_S = (0.1, 0.3, 1.0, 3.0)
     _refused = 0
+    refusals = 0              # standby refills the kubelet refused (a running count)
 
     def poke(self) -> None:
         self._refused = 0            # news of capacity: a refusal gets its retries again
@@ -271,6 +272,7 @@ class WarmPool:
                 # refused by the kubelet, not the scheduler: it still counts GPUs of Pods
                 # deleted a moment ago (their teardown frees them without any event we see),
                 # so look again shortly rather than at the next capacity event
+                self.refusals += 1
                 if self._refused < len(self.REFUSED_RETRY_S):
                     delay = self.REFUSED_RETRY_S[self._refused]
                     self._refused += 1

@@ -142,6 +142,7 @@ async def run(args) -> None:
                       workdir=args.workdir, start_master=False, start_workers=False,
                       node_gpu_bdfs=[b for b in args.gpu_bdfs.split(",") if b] or None,
                       kubelet_limit_mode=args.kubelet_limit, gpu_api=args.gpu_api,
+                      lazy_checkpoint=args.lazy_checkpoint,
                       app_hook=_hooks(ref), kernel_fs_dir=args.kernel_fs_dir)
     ref[0] = lc
     stop = asyncio.Event()
@@ -185,6 +186,9 @@ def main(argv=None) -> int:
                     help="PodResources limiter (100 qps, burst 10): reject over-budget calls "
                          "with RESOURCE_EXHAUSTED, or serve them and only count them")
     ap.add_argument("--gpu-bdfs", default="", help="comma-separated: the node's GPUs (default all)")
+    ap.add_argument("--lazy-checkpoint", action="store_true",
+                    help="the device manager keeps a deleted Pod in its checkpoint until the "
+                         "next Allocate, as a real kubelet does")
     ap.add_argument("--gpu-api", choices=("device-plugin", "dra"), default="device-plugin",
                     help="dra: the GPUs are published in ResourceSlices (fakes/dra.py)")
     args = ap.parse_args(argv)

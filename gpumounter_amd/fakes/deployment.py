@@ -54,7 +54,7 @@ class ProcessCluster:
                  master_env: Optional[Dict[str, str]] = None, log_dir: str = "",
                  protocol: str = "gpumounter", kubelet_limit: str = "enforce",
                  secure: Optional[bool] = None, gpu_api: str = "device-plugin",
-                 kernel_fs: str = "disk") -> None:
+                 kernel_fs: str = "disk", lazy_checkpoint: bool = False) -> None:
         """``protocol="reference"`` runs worker and master with the reference's call sequence
         (gpumounter_amd/fakes/refproto.py) in the same deployment shape, for comparison; it is
         insecure like the reference unless ``secure`` says otherwise.
@@ -73,6 +73,7 @@ class ProcessCluster:
         self.latency = latency
         self.kubelet_limit = kubelet_limit
         self.gpu_bdfs = gpu_bdfs or []
+        self.lazy_checkpoint = lazy_checkpoint
         self.gpu_api = gpu_api
         self.worker_env = worker_env or {}
         self.master_env = master_env or {}
@@ -163,7 +164,8 @@ class ProcessCluster:
                                      "--kubelet-limit", self.kubelet_limit,
                                      "--gpu-bdfs", ",".join(self.gpu_bdfs),
                                      "--gpu-api", self.gpu_api,
-                                     "--kernel-fs-dir", self.kernel_fs_dir], {})
+                                     "--kernel-fs-dir", self.kernel_fs_dir]
+                                    + (["--lazy-checkpoint"] if self.lazy_checkpoint else []), {})
         self._wait("control plane", lambda: os.path.exists(info_path))
         with open(info_path) as fh:
             self.info = json.load(fh)

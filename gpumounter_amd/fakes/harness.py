@@ -66,8 +66,12 @@ class LocalCluster:
                  kubelet_rate_limit: Optional[tuple] = (100.0, 10),
                  kubelet_limit_mode: str = "enforce", gpu_api: str = "device-plugin",
                  app_hook: Optional[Callable[[web.Application], None]] = None,
-                 kernel_fs_dir: str = "", priority_classes: bool = True) -> None:
+                 kernel_fs_dir: str = "", priority_classes: bool = True,
+                 lazy_checkpoint: bool = False) -> None:
         self.n_nodes = n_nodes
+        # the device manager keeps a deleted Pod in its checkpoint until the next Allocate, as
+        # a real kubelet does (fakes/node.py FakeNode.lazy_checkpoint)
+        self.lazy_checkpoint = lazy_checkpoint
         # apply the shipped deploy's PriorityClasses (deploy/placeholder-priority.yaml), as
         # `kubectl apply -k deploy/` does; False: a cluster where they were never applied
         self.priority_classes = priority_classes
@@ -148,6 +152,7 @@ class LocalCluster:
                         if self.real_cgroup_root else "",
                         kernel_fs_dir=os.path.join(self.kernel_fs_dir, name)
                         if self.kernel_fs_dir else "")
+        node.lazy_checkpoint = self.lazy_checkpoint
         if self.gpu_api == "dra":
             node.gpu_api = "dra"
             node.write_checkpoint = False    # the device manager does not see DRA devices

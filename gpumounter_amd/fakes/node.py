@@ -120,6 +120,12 @@ class FakeNode:
         os.makedirs(self.plugin_dir, exist_ok=True)
         self.checkpoint_path = os.path.join(self.plugin_dir, CHECKPOINT_NAME)
         self.write_checkpoint = True
+        # lazy_checkpoint models the real device manager more closely: it drops a deleted
+        # Pod's devices from its books (and the checkpoint) only at the next Allocate
+        # (UpdateAllocatedDevices), so the file keeps listing the Pod until then. What the
+        # released devices were last checkpointed as: device → (pod uid, container)
+        self.lazy_checkpoint = False
+        self._stale: Dict[str, Tuple[str, str]] = {}
         self.containers: Dict[str, Container] = {}  # container id → Container
         self.alloc_log: Deque[Tuple[str, str, List[str]]] = deque(maxlen=4096)
         # a registered device plugin (FakeKubelet device manager) replaces allocate()
@@ -186,8 +192,11 @@ class FakeNode:
         if not self.write_checkpoint:
             return
         per: Dict[Tuple[str, str], Dict[int, List[str]]] = {}
-        for d, (_, _, c) in sorted(self.allocated.items()):
-            uid = self.alloc_uid.get(d, "")
+        entries = [(d, self.alloc_uid.get(d, ""), c)
+                   for d, (_, _, c) in sorted(self.allocated.items())]
+        entries += [(d, uid, c) for d, (uid, c) in sorted(self._stale.items())
+                    if d not in self.allocated]
+        for d, uid, c in entries:
             if uid:
                 per.setdefault((uid, c), {}).setdefault(max(self.numa_of(d), 0), []).append(d)
         ckpt.write_atomic(self.checkpoint_path, ckpt.render(
@@ -214,6 +223,9 @@ class FakeNode:
         the FakeKubelet's device manager) steers placeholders to a chosen set."""
         with self._lock:
             self.release_pending()
+            if self._stale:                  # UpdateAllocatedDevices: inactive pods dropped
+                self._stale.clear()
+                self._checkpoint()
             free = [g for g in self.gpus if self.device_id(g) not in self.allocated]
             if len(free) < n:
                 return None
@@ -238,6 +250,9 @@ class FakeNode:
         """Commit an allocation chosen elsewhere (device-plugin path); False if any is taken."""
         with self._lock:
             self.release_pending()
+            if self._stale:
+                self._stale.clear()
+                self._checkpoint()
             if any(d in self.allocated for d in ids):
                 return False
             for d in ids:
@@ -260,9 +275,11 @@ class FakeNode:
             ids = [d for d, (n, p, _) in self.allocated.items() if n == ns and p == pod
                    and (not uid or self.alloc_uid.get(d, "") == uid)]
             for d in ids:
+                if self.lazy_checkpoint and self.alloc_uid.get(d):
+                    self._stale[d] = (self.alloc_uid[d], self.allocated[d][2])
                 del self.allocated[d]
                 self.alloc_uid.pop(d, None)
-            if ids:
+            if ids and not self.lazy_checkpoint:
                 self._checkpoint()
             return ids
 

@@ -711,15 +711,19 @@ class GpuMountService:
         always holds every free GPU; ``hint`` only annotates the preferred set."""
         pool = self.pool if self.pool is not None and self.pool.enabled else None
         planned = {p.uid for p in pool.standby()} if pool is not None else set()
+        refused = pool.refusals if pool is not None else 0
         try:
             return await self._reserve_once(pod, n, req, st, preferred, n_free, lease_exp)
         except InsufficientGPU:
             # a refill that started before this attach held GPUs this attach's plan took for
-            # free (its standby placeholders were not admitted yet): claim those instead
-            if pool is None or not await pool.admitted(self.cfg.attach_timeout_s) or \
-                    not {p.uid for p in pool.standby()} - planned:
+            # free (its standby placeholders were not admitted yet): claim those instead — or,
+            # when the kubelet refused the refill (a teardown in flight) and it gave them up,
+            # book them again
+            if pool is None or not await pool.admitted(self.cfg.attach_timeout_s):
                 raise
-            _log.info("attach refused while the pool refilled; claiming its new standby GPUs")
+            if not {p.uid for p in pool.standby()} - planned and pool.refusals == refused:
+                raise
+            _log.info("attach refused while the pool refilled; booking again")
             return await self._reserve_once(pod, n, req, st, preferred, n_free, lease_exp)
 
     async def _reserve_once(self, pod: dict, n: int, req, st: PodGpuState,

@@ -171,3 +171,26 @@ def test_the_pool_refills_after_the_kubelet_refused_it_during_a_teardown(binding
                 assert time.monotonic() < end, "pool not refilled after the teardown"
                 await asyncio.sleep(0.02)
     asyncio.run(main())
+
+
+def test_the_pool_refills_although_the_kubelets_checkpoint_still_lists_a_deleted_pod():
+    """A real device manager drops a deleted Pod from its books, and from the checkpoint file,
+    only at the next Allocate. A pool that counted the checkpoint's entries as allocated would
+    see no free GPU after another workload left a full node, create no standby, and so never
+    trigger that Allocate. The pool counts only Pods the apiserver still has."""
+    async def main():
+        async with LocalCluster(lazy_checkpoint=True,
+                                worker_overrides={"warm_pool_size": 1}) as lc:
+            pool = lc.nodes["node-0"].worker.pool
+            end = time.monotonic() + 5
+            while len(pool.standby()) < 1:
+                assert time.monotonic() < end, "pool not filled at start"
+                await asyncio.sleep(0.02)
+            sb = pool.standby()[0]
+            lc.tenant("hog", gpus=7)
+            lc.cluster.delete(sb.namespace, sb.name, grace=0)
+            end = time.monotonic() + 3
+            while not [p for p in pool.standby() if p.uid != sb.uid]:
+                assert time.monotonic() < end, "pool not refilled"
+                await asyncio.sleep(0.02)
+    asyncio.run(main())

@@ -452,3 +452,8 @@ TestLedgerTeardown = _case("LedgerTeardown", {
     "latency": LatencyModel(teardown_ms=50.0),
     "worker_overrides": {"warm_pool_size": 2, "placeholder_binding": "direct",
                          "pool_priority_class": "gpumounter-standby"}})
+# the device manager's checkpoint keeps a deleted Pod until the next Allocate (a real kubelet's
+# behaviour), with the teardown delay and a warm pool
+TestLedgerLazyCheckpoint = _case("LedgerLazyCheckpoint", {
+    "lazy_checkpoint": True, "latency": LatencyModel(teardown_ms=50.0),
+    "worker_overrides": {"warm_pool_size": 2}})
