@@ -71,3 +71,19 @@ def test_chaos_with_preemptors_never_takes_a_tenants_gpu():
     out = json.loads(res.stdout.strip().splitlines()[-1])
     assert out["preempted"]["placeholder"] > 0
     assert any("preempted" in v for v in out["violation_examples"]), out["violation_examples"]
+
+
+def test_chaos_with_a_kubelet_that_tears_down_late_and_keeps_deleted_pods_checkpointed():
+    """--latency teardown --lazy-checkpoint: the fake kubelet frees a deleted Pod's devices
+    50 ms after the DELETE and keeps it in its device-manager checkpoint until the next
+    Allocate, as a real kubelet does. Attaches and pool refills right after a detach are
+    refused at admission and book again; the ledger invariants hold across worker kills."""
+    res = subprocess.run([sys.executable, "bench/configs.py", "chaos", "--rounds", "10",
+                          "--kill-every", "5", "--seed", "6", "--restart-rate", "0.3",
+                          "--latency", "teardown", "--lazy-checkpoint", "--warm-pool", "2",
+                          "--placeholder-binding", "direct"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert out["worker_kills"] == 2 and out["ops_ok"] > 0
+    assert out["invariant_violations"] == 0, out["violation_examples"]
