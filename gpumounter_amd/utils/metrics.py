@@ -42,8 +42,9 @@ class Metrics:
         self.admission_refusals = Counter(
             "gm_admission_refusals_total",
             "placeholders the kubelet refused at admission (UnexpectedAdmissionError / "
-            "OutOf<resource>), by what followed: booked again while a teardown was in flight, "
-            "or answered as too few GPUs", ["outcome"], registry=r)
+            "OutOf<resource>), by what followed: rebooked (a teardown was in flight), full (no "
+            "room in gpumounter's view either: answered as too few GPUs), exhausted (the GPUs "
+            "looked free throughout and the re-bookings ran out)", ["outcome"], registry=r)
         self.gpu_busy = Gauge("gm_gpu_processes", "processes on a GPU (amdsmi)", ["gpu"],
                               registry=r)
         self.plugin_rpcs = Counter("gm_device_plugin_rpcs_total",

@@ -849,9 +849,14 @@ class GpuMountService:
                     break
                 except InsufficientGPU as e:
                     kubelet = str(e).startswith(("UnexpectedAdmissionError", "OutOf"))
-                    if not delays or not (yielded or (kubelet and self._room(st) >= n - got)):
+                    transient = yielded or (kubelet and self._room(st) >= n - got)
+                    if not delays or not transient:
                         if kubelet:
-                            self.metrics.admission_refusals.labels(outcome="refused").inc()
+                            # "full": no room in our view either (the kubelet's refusal of a
+                            # directly bound placeholder on a full node); "exhausted": the GPUs
+                            # looked free the whole time, and the kubelet kept refusing
+                            self.metrics.admission_refusals.labels(
+                                outcome="exhausted" if transient else "full").inc()
                         raise
                     self.metrics.admission_refusals.labels(outcome="rebooked").inc()
                     # a kubelet that has not torn a deleted Pod down yet refuses its devices
