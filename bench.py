@@ -80,6 +80,11 @@ class _LocalCP:
     def corrections(self) -> int:
         return int(self.lc.nodes["node-0"].worker.metrics.placement_corrections._value.get())
 
+    def admission_refusals(self) -> dict:
+        m = self.lc.nodes["node-0"].worker.metrics.admission_refusals
+        return {s.labels["outcome"]: int(s.value) for metric in m.collect()
+                for s in metric.samples if s.name.endswith("_total")}
+
     def tenant_view(self):
         node = self.lc.nodes["node-0"].node
         (c,) = [c for c in node.containers.values() if c.pod_name == "tenant"]
@@ -127,6 +132,14 @@ class _ProcCP:
             if ln.startswith("gm_placement_corrections_total "):
                 return int(float(ln.split()[1]))
         return 0
+
+    def admission_refusals(self) -> dict:
+        out = {}
+        for ln in self.pc.worker_metrics().splitlines():
+            if ln.startswith("gm_admission_refusals_total{"):
+                outcome = ln.split('outcome="', 1)[1].split('"', 1)[0]
+                out[outcome] = int(float(ln.split()[-1]))
+        return out
 
     def tenant_view(self):
         from gpumounter_amd.ops import tenant
@@ -681,6 +694,7 @@ def main() -> int:
                             "authz": None, **idle_only, "idle_only": idle_only}
             orphan_issues = len(cp.audit()) if args.protocol == "gpumounter" else None
             corrections = cp.corrections() if args.protocol == "gpumounter" else None
+            refusals = cp.admission_refusals() if args.protocol == "gpumounter" else None
             placeholders_left = cp.placeholders_left()
             kcalls = cp.kubelet_calls()
             p50 = pct(attach_ms, 0.5)
@@ -819,6 +833,9 @@ def main() -> int:
                 "tenant_view": tenant_view, "tenant_view_pytorch": tenant_view_pt,
                 # attaches whose plugin-chosen GPUs were swapped for a better-placed set
                 "placement_corrections": corrections,
+                # placeholders the kubelet refused at admission and what followed (a teardown
+                # on the attach path: rebooked)
+                "admission_refusals": refusals,
                 "attached_hives": att_hives, "attached_numa_nodes": att_numa,
                 "non_xgmi_pairs": att_nx, "p2p": p2p,
                 "ledger_audit_issues": audit_issues,
