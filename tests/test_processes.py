@@ -276,3 +276,34 @@ print(json.dumps({{"a": a.pid, "b": b, "res": res, "b_alive": alive}}))
     o = json.loads(r.stdout.strip().splitlines()[-1])
     assert o["a"] == o["b"], o                 # the number really was recycled
     assert o["res"] == [-3] and o["b_alive"]   # ESRCH, and B untouched
+
+
+def test_one_nodes_worker_down_leaves_the_other_node_served():
+    """Two nodes; node-0's worker is SIGKILLed. Attaches to Pods on node-1 go on being served,
+    one to a Pod on node-0 fails promptly (the master finds no live worker there, instead of
+    hanging on it), and once the worker is back node-0 is served again with its ledger intact
+    (the GPUs attached before the crash are still the Pod's)."""
+    import time
+
+    pc = ProcessCluster(n_nodes=2)
+    try:
+        pc.start()
+        pc.tenant("t0", node="node-0")
+        pc.tenant("t1", node="node-1")
+        code, b0 = pc.add("default", "t0", 1)
+        assert code == 200, b0
+        pc.kill_worker("node-0")
+        code, b1 = pc.add("default", "t1", 2)
+        assert code == 200, b1
+        t = time.monotonic()
+        code, body = pc.add("default", "t0", 1)
+        assert code == 500 and time.monotonic() - t < 30, (code, body)
+        pc.restart_worker("node-0")
+        code, g = pc.pod_gpus("default", "t0")
+        assert code == 200 and [x["uuid"] for x in g["gpus"] if x["source"] == "hot-mount"] \
+            == [d["uuid"] for d in b0["devices"]], g
+        code, b2 = pc.add("default", "t0", 1)
+        assert code == 200, b2
+        assert pc.audit("default", "t0") == [] and pc.audit("default", "t1", "node-1") == []
+    finally:
+        pc.stop()
