@@ -140,6 +140,11 @@ class Inventory:
         _log.info("inventory: %d GPU(s) via %s, kfd major %d", count, self.lib_path,
                   self.kfd_major)
 
+    @property
+    def is_mock(self) -> bool:
+        """The mock amdsmi library: its GPUs and process table are synthetic, not this node's."""
+        return os.path.abspath(self.lib_path) == os.path.abspath(_native.mock_smi_path())
+
     def gpus(self) -> List[AmdGpu]:
         """Fresh copies (callers mutate ledger fields)."""
         with self._lock:

@@ -5,7 +5,15 @@ Reference: busy ⇔ some NVML graphics/compute PID of the GPU is in the containe
 (pkg/device/nvidia.go:58-87), and force-removal runs ``kill <pids>`` through nsenter
 (namespace.go:191-201). Here the PID set comes from the cached amdsmi session
 (``amdsmi_get_gpu_process_list``), with a ``/proc/*/fd`` scan for the GPU's render node as
-fallback when amdsmi cannot report processes. Force-removal pins the container's processes
+fallback when amdsmi cannot report processes.
+
+Both process tables, KFD's ``/sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>`` and amdsmi's list
+(which reads the same table), name processes by their PID in the host's PID namespace. Measured
+on an MI355X box (``profiles/r6_kfd_probe/``): a tenant that is PID 340 in its container is
+``2370128`` in both tables, whose ``vram_<gpu_id>`` holds exactly its 256 MiB allocation. So the
+tables are intersected with ``cgroup.procs`` only when the worker itself runs in the host PID
+namespace (``hostPID: true``, :func:`host_pid_ns`); anywhere else a table PID could equal the
+number of an unrelated container process. Force-removal pins the container's processes
 with pidfds *before* the busy check (:class:`Pinned`): membership in the container's cgroup is
 re-read after pinning, and SIGTERM, the liveness wait and the SIGKILL escalation all go through
 those pidfds — so a PID the kernel recycles between the snapshot and the kill can never be hit.
@@ -19,7 +27,7 @@ import errno
 import os
 import select
 import signal as _sig   # Pinned.signal shadows the module name inside the class body
-from typing import Dict, Iterable, List, Sequence, Tuple
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 from gpumounter_amd import _native
 from gpumounter_amd.hw.inventory import Inventory
@@ -72,28 +80,91 @@ def scan_devs(pids: Sequence[int], devs: Sequence[Tuple[int, int]]
             [int(bad[i]) for i in range(nbad)])
 
 
+KFD_PROC = "/sys/class/kfd/kfd/proc"
+PROC_PID_INIT_INO = 0xEFFFFFFC      # the initial PID namespace's inode (linux/proc_ns.h)
+_host_ns: Dict[str, bool] = {}
+_warned: List[bool] = []          # the not-in-host-namespace warning, once per process
+
+
+def host_pid_ns(proc_root: str = "/proc") -> bool:
+    """This process runs in the host's (initial) PID namespace, so its PIDs are the numbers
+    KFD and amdsmi report. ``/proc/self/status`` cannot tell (a container's /proc shows one
+    NSpid too); the namespace inode can: the initial one has a fixed number."""
+    if proc_root not in _host_ns:
+        try:
+            link = os.readlink(os.path.join(proc_root, "self/ns/pid"))
+        except OSError:
+            link = ""
+        _host_ns[proc_root] = link == f"pid:[{PROC_PID_INIT_INO}]"
+    return _host_ns[proc_root]
+
+
+def kfd_table(root: str = KFD_PROC) -> Dict[int, Dict[int, int]]:
+    """KFD's process table: KFD gpu_id → {host PID: VRAM bytes}. A process is listed under a
+    GPU once it has bound that GPU (``vram_<gpu_id>`` in its directory). Raises OSError if the
+    table cannot be read (no KFD, or sysfs not mounted at ``root``)."""
+    out: Dict[int, Dict[int, int]] = {}
+    for name in os.listdir(root):
+        if not name.isdigit():
+            continue
+        pid = int(name)
+        try:
+            files = os.listdir(os.path.join(root, name))
+        except OSError:
+            continue                    # exited between the two reads
+        for f in files:
+            if not f.startswith("vram_") or not f[5:].isdigit():
+                continue
+            try:
+                with open(os.path.join(root, name, f), "rb") as fh:
+                    vram = int(fh.read().strip() or 0)
+            except (OSError, ValueError):
+                continue
+            out.setdefault(int(f[5:]), {})[pid] = vram
+    return out
+
+
 def busy_pids(inv: Inventory, gpus: Sequence[AmdGpu], container_pids: Iterable[int],
-              drm_major: int = DRM_MAJOR, mode: str = "auto") -> Dict[int, List[int]]:
+              drm_major: int = DRM_MAJOR, mode: str = "auto", kfd_root: str = KFD_PROC,
+              tables: bool = True) -> Dict[int, List[int]]:
     """GPU index → container PIDs that hold that GPU.
 
     Primary source: one scan of *only the container's* PIDs for the GPUs' render nodes. A
     process cannot use a GPU without that fd (KFD binds a GPU's VM through its DRM render fd,
     and ROCr keeps it open for the process lifetime), so when every fd table is readable the
-    scan is complete. amdsmi's per-GPU process table (KFD contexts, host PIDs) covers the PIDs
-    whose fd table could not be read; ``mode="both"`` always takes the union (slower: amdsmi
-    walks every KFD process on the node).
+    scan is complete. The process tables cover the PIDs whose fd table could not be read:
+    KFD's sysfs table when ``kfd_root`` is readable (a few small reads), else amdsmi's.
+    ``mode="both"`` always takes the union. ``tables=False`` (the worker is not in the host
+    PID namespace, see the module docstring) leaves the tables out: their PIDs are not this
+    namespace's.
     """
     cpids = sorted(set(container_pids))
     hits, unreadable = scan_devs(cpids, [(drm_major, g.render_minor) for g in gpus])
     ask = set(cpids) if mode == "both" else set(unreadable)
+    if ask and not tables:
+        if not _warned:
+            _warned.append(True)
+            _log.warning("busy check: not in the host PID namespace, so the KFD/amdsmi process "
+                         "tables cannot vouch for PIDs such as %s (run the worker with "
+                         "hostPID: true)", sorted(ask)[:8])
+        ask = set()
+    kfd: Optional[Dict[int, Dict[int, int]]] = None
+    if ask and kfd_root:
+        try:
+            kfd = kfd_table(kfd_root)
+        except OSError:
+            kfd = None
     out: Dict[int, List[int]] = {}
     for j, g in enumerate(gpus):
         hit = {cpids[i] for i in range(len(cpids)) if hits[i][j]}
         if ask:
-            try:
-                hit.update(ask.intersection(p.pid for p in inv.processes(g.index)))
-            except NotImplementedError:
-                pass
+            if kfd is not None and g.kfd_gpu_id:
+                hit.update(ask.intersection(kfd.get(g.kfd_gpu_id, {})))
+            else:
+                try:
+                    hit.update(ask.intersection(p.pid for p in inv.processes(g.index)))
+                except NotImplementedError:
+                    pass
         if hit:
             out[g.index] = sorted(hit)
     return out

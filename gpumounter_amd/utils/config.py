@@ -139,6 +139,9 @@ class Config:
     drm_major: int = 226               # /dev/dri/* character-device major
     kfd_major: int = 0                 # 0 → read /sys/class/kfd/kfd/dev (fallback 511)
     kfd_dev_path: str = "/sys/class/kfd/kfd/dev"  # sysfs file holding the KFD major:minor
+    # KFD's process table (<host pid>/vram_<gpu_id>): busy detection's source for PIDs whose
+    # fd table is unreadable, before amdsmi; "" = amdsmi only
+    kfd_proc_path: str = "/sys/class/kfd/kfd/proc"
     inject_card_nodes: bool = True     # also inject /dev/dri/card<N> (rocm-smi reads it)
     device_file_mode: int = 0o666      # reference: nvidia.go:39 "666"
     # --- policy ----------------------------------------------------------------------------
@@ -162,8 +165,9 @@ class Config:
     placement_correct_on: str = "numa"
     ledger_get: bool = True            # read admitted placeholders with PodResources v1 Get
     reconcile_on_events: bool = True   # react to placeholder/tenant deletes at once
-    # auto: fd scan of the container's PIDs, amdsmi only for PIDs whose fd table is unreadable;
-    # both: always union with amdsmi's process table
+    # auto: fd scan of the container's PIDs, the KFD/amdsmi process table only for PIDs whose
+    # fd table is unreadable; both: always union with the table. The tables name host-namespace
+    # PIDs, so the worker consults them only when it runs with hostPID: true
     busy_detection: str = "auto"
     gc_tune: bool = True               # gc.freeze() after startup + larger young-gen threshold
     # pin the daemon to these CPUs at start ("2-3,8", cpuset list format; "" = unpinned): on a

@@ -1003,8 +1003,11 @@ class GpuMountService:
                     if pinned.fds:
                         pinned.restrict({p for t in everyone
                                          for p in self.hm.resolver.pids(t.cgdir)})
+                    real = not self.inv.is_mock
                     busy = procs.busy_pids(self.inv, selected, pinned.pids(),
-                                           self.cfg.drm_major, self.cfg.busy_detection)
+                                           self.cfg.drm_major, self.cfg.busy_detection,
+                                           kfd_root=self.cfg.kfd_proc_path if real else "",
+                                           tables=not real or procs.host_pid_ns())
                     busy = {k: [p for p in v if not pinned.exited(p)] for k, v in busy.items()}
                     busy = {k: v for k, v in busy.items() if v}
             except (MountError, InjectedFault) as e:

@@ -343,6 +343,42 @@ def test_busy_detection_with_real_hip_process(real_inventory):
         child.wait()
 
 
+def test_kfd_table_names_tenant_by_host_pid(real_inventory):
+    """KFD's sysfs process table and amdsmi's list agree, name a tenant by its host-namespace
+    PID (the box runs us in a container: the child's own PID is another number), and carry its
+    VRAM; outside the host PID namespace busy detection leaves both tables out and still finds
+    the tenant through its render fd."""
+    from gpumounter_amd.node import procs
+
+    inv = real_inventory
+    g = inv.gpus()[0]
+    assert g.kfd_gpu_id
+    before = procs.kfd_table().get(g.kfd_gpu_id, {})
+    child = subprocess.Popen([sys.executable, "-c", _hip_child_code()], stdout=subprocess.PIPE,
+                             text=True)
+    try:
+        assert child.stdout.readline().strip() == "ready"
+        table = procs.kfd_table().get(g.kfd_gpu_id, {})
+        smi = {p.pid: p.vram_bytes for p in inv.processes(g.index)}
+        new = {p: v for p, v in table.items() if p not in before}
+        print(f"kfd table gpu {g.kfd_gpu_id}: {table}; amdsmi: {smi}; child {child.pid}")
+        assert len(new) == 1, new
+        (hpid, vram), = new.items()
+        assert vram >= 4 << 20                     # the child's 4 MiB tensor, at least
+        assert smi.get(hpid) == vram               # amdsmi reads the same table
+        host = procs.host_pid_ns()
+        assert (hpid == child.pid) == host
+        busy = procs.busy_pids(inv, [g], [child.pid], mode="both", tables=host)
+        assert busy == {g.index: [child.pid]}
+    finally:
+        child.kill()
+        child.wait()
+    t0 = time.time()
+    while hpid in procs.kfd_table().get(g.kfd_gpu_id, {}) and time.time() - t0 < 10:
+        time.sleep(0.1)
+    assert hpid not in procs.kfd_table().get(g.kfd_gpu_id, {})
+
+
 def test_tenant_validate_tool_runs_kernel_p2p_and_rccl():
     """``python -m gpumounter_amd.parallel.validate``: liveness kernel on every visible GPU,
     pairwise peer copies, an RCCL all-reduce with one process per GPU, and the bf16 burn-in."""
