@@ -127,6 +127,28 @@ def check_devnodes(cfg) -> List[Check]:
                   "(hostUsers: false) will fail; other Pods are unaffected")]
 
 
+def check_pidns(cfg) -> List[Check]:
+    """Busy detection's process tables (KFD's and amdsmi's) name host-namespace PIDs
+    (``profiles/r6_kfd_probe/``); the worker uses them only in the host PID namespace."""
+    from gpumounter_amd.node import procs
+
+    host = procs.host_pid_ns()
+    table = ""
+    if cfg.kfd_proc_path:
+        try:
+            n = len({p for t in procs.kfd_table(cfg.kfd_proc_path).values() for p in t})
+            table = f"; KFD process table readable ({n} process(es) on a GPU)"
+        except OSError as e:
+            table = f"; KFD process table {cfg.kfd_proc_path}: {e.strerror} (amdsmi's is used)"
+    if host:
+        return [Check("pidns", "ok", "host PID namespace (hostPID): busy detection can use the "
+                                     "KFD/amdsmi process tables" + table)]
+    return [Check("pidns", "warn",
+                  "not in the host PID namespace: busy detection relies on the render-fd scan "
+                  "alone (the KFD/amdsmi tables name host PIDs); run the DaemonSet with "
+                  "hostPID: true" + table)]
+
+
 def check_systemd(cfg) -> List[Check]:
     from gpumounter_amd.node import systemd
 
@@ -306,7 +328,7 @@ def check_gpus(cfg, burn_in_s: float = 0.0) -> List[Check]:
 def run(cfg, skip_cluster: bool = False, gpu: bool = False,
         burn_in_s: float = 0.0) -> List[Check]:
     checks = check_inventory(cfg) + check_cgroup(cfg) + check_devnodes(cfg) + \
-        check_systemd(cfg)
+        check_pidns(cfg) + check_systemd(cfg)
     if gpu:
         checks += check_gpus(cfg, burn_in_s)
     if not skip_cluster:

@@ -68,3 +68,17 @@ def test_doctor_reports_bind_mode_for_user_namespaced_pods():
         assert c.status == "ok", c.detail            # CAP_SYS_ADMIN: open_tree works
     else:
         assert c.status == "warn" and "hostUsers" in c.detail
+
+
+def test_doctor_reports_the_pid_namespace(tmp_path, monkeypatch):
+    from gpumounter_amd.node import procs
+
+    (tmp_path / "4242").mkdir()
+    (tmp_path / "4242" / "vram_49070").write_text("4096\n")
+    cfg = Config(kfd_proc_path=str(tmp_path))
+    monkeypatch.setattr(procs, "host_pid_ns", lambda proc_root="/proc": True)
+    (c,) = doctor.check_pidns(cfg)
+    assert c.status == "ok" and "1 process(es)" in c.detail, c
+    monkeypatch.setattr(procs, "host_pid_ns", lambda proc_root="/proc": False)
+    (c,) = doctor.check_pidns(Config(kfd_proc_path=str(tmp_path / "none")))
+    assert c.status == "warn" and "hostPID: true" in c.detail and "amdsmi's is used" in c.detail

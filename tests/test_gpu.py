@@ -201,6 +201,9 @@ def test_doctor_gpu_checks_pass():
     gpu = [c for c in checks if c["name"].startswith("gpu")]
     assert gpu and all(c["status"] == "ok" for c in gpu), gpu
     assert all("0 mismatching words" in c["detail"] for c in gpu if c["name"] != "gpu"), gpu
+    # the box runs us in a container's PID namespace, with KFD's process table readable
+    (pidns,) = [c for c in checks if c["name"] == "pidns"]
+    assert "KFD process table readable" in pidns["detail"], pidns
 
 
 def test_gemm_check_host_reference():
