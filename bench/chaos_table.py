@@ -14,7 +14,8 @@ COMMITS = {"sweep1": "≥ `dfe7c34`", "sweep2": "≥ `dfe7c34`", "sweep3": "`f28
            "sweep7": "`3155cd6`", "sweep8": "`61b3c08`", "sweep9": "`61b3c08`",
            "sweep10": "`7840df0`", "sweep11": "`7840df0`", "sweep12": "`0a02c8c`",
            "sweep13": "`0a02c8c`", "sweep14": "`197ce4f`", "sweep15": "`197ce4f`",
-           "sweep16": "`197ce4f`", "sweep17": "`197ce4f`", "box1": "`47fda63`",
+           "sweep16": "`197ce4f`", "sweep17": "`197ce4f`",
+           "sweep18": "`0fded3c`", "box1": "`47fda63`",
            "box2": "`c89abea`", "box3": "`7de522a`", "box4": "`9880c89`", "box5": "`3bfbd67`",
            "box6": "`197ce4f`", "box7": "`197ce4f`", "box8": "`bbeb156`"}
 
