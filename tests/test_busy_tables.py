@@ -94,3 +94,62 @@ def test_host_pid_ns_reads_the_namespace_inode(tmp_path):
         assert procs.host_pid_ns(str(tmp_path / name)) is want
     assert procs.host_pid_ns(str(tmp_path / "nothing")) is False
     assert procs.PROC_PID_INIT_INO == 4026531836
+
+
+IDLE = "import time; print('ready', flush=True); time.sleep(120)"
+
+
+def test_worker_detach_takes_the_table_the_namespace_allows(tmp_path, monkeypatch,
+                                                             mock_inventory):
+    """End to end through the worker's detach: with the real library (``is_mock`` patched off)
+    the KFD table at ``kfd_proc_path`` decides, and outside the host PID namespace neither the
+    KFD table nor amdsmi's can make the GPU busy."""
+    import asyncio
+    import subprocess
+    import sys
+
+    from gpumounter_amd import _native
+    from gpumounter_amd.fakes.harness import LocalCluster
+    from gpumounter_amd.hw.inventory import Inventory
+
+    g0 = mock_inventory.gpus()[0]
+    p = subprocess.Popen([sys.executable, "-c", IDLE], stdout=subprocess.PIPE)
+    assert p.stdout.readline().strip() == b"ready"
+    smi_table = tmp_path / "smi"
+    _native.mock_smi().gm_mock_set_procs_file(str(smi_table).encode())
+    kfd = tmp_path / "kfd"
+    (kfd / str(p.pid)).mkdir(parents=True)
+    (kfd / str(p.pid) / f"vram_{g0.kfd_gpu_id}").write_text("4096\n")
+    monkeypatch.setattr(Inventory, "is_mock", property(lambda self: False))
+
+    async def cycle(lc, name, smi):
+        lc.tenant(name, pids={"main": [p.pid]})
+        code, b = await lc.add("default", name, 1)
+        assert code == 200, b
+        dev = b["devices"][0]
+        smi_table.write_text(f"{dev['index']} {p.pid} 4096 python\n" if smi else "")
+        code, b2 = await lc.remove("default", name, [dev["uuid"]], force=False)
+        smi_table.write_text("")
+        if code != 200:
+            code3, b3 = await lc.remove("default", name, [dev["uuid"]], force=True)
+            assert code3 == 200, b3
+        return code, b2
+
+    async def main(host):
+        monkeypatch.setattr(procs, "host_pid_ns", lambda proc_root="/proc": host)
+        async with LocalCluster(node_gpu_bdfs=[g0.bdf],
+                                worker_overrides={"busy_detection": "both",
+                                                  "kfd_proc_path": str(kfd)}) as lc:
+            # in the host namespace amdsmi's table stays empty: the KFD table alone decides
+            return await cycle(lc, f"t{int(host)}", smi=not host)
+    try:
+        code, b = asyncio.run(main(True))
+        assert code == 400 and "running processes" in b["message"], b
+        # outside the host namespace: the same tables, and no table is asked
+        code, b = asyncio.run(main(False))
+        assert code == 200, b
+    finally:
+        _native.mock_smi().gm_mock_set_procs_file(b"")
+        if p.poll() is None:
+            p.kill()
+        p.wait()
