@@ -26,7 +26,7 @@ from gpumounter_amd.cluster.placeholder import LABEL_NODE, PlaceholderManager
 from gpumounter_amd.cluster.pool import WarmPool
 from gpumounter_amd.hw.inventory import Inventory
 from gpumounter_amd.models import pod as podu
-from gpumounter_amd.node import systemd
+from gpumounter_amd.node import procs, systemd
 from gpumounter_amd.node.cgroup import CgroupError, CgroupResolver, make_backend
 from gpumounter_amd.node.checkpoint import DeviceCheckpoint
 from gpumounter_amd.node.devnodes import DevNodeWriter
@@ -328,6 +328,10 @@ class Worker:
             _log.warning("worker gRPC is UNAUTHENTICATED (worker_insecure=1): anyone who can "
                          "reach :%d can attach GPUs or kill tenant GPU processes",
                          self.cfg.worker_port)
+        if not self.inv.is_mock and not procs.host_pid_ns():
+            _log.warning("not in the host PID namespace: busy detection uses the render-fd scan "
+                         "only, since the KFD/amdsmi process tables name host PIDs (the "
+                         "DaemonSet runs with hostPID: true)")
         self.grpc_server = grpc.aio.server(options=[("grpc.so_reuseport", 0)])
         self.grpc_server.add_generic_rpc_handlers(self.handlers())
         port = self.cfg.worker_port if grpc_port is None else grpc_port

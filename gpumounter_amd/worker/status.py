@@ -14,6 +14,7 @@ from gpumounter_amd.hw import topology
 from gpumounter_amd.models.device import gpus_by_key, normalize_device_id
 from gpumounter_amd.models.types import ANN_CANDIDATE
 from gpumounter_amd.node.ledger import LedgerError
+from gpumounter_amd.node.procs import host_pid_ns
 from gpumounter_amd.utils import log
 from gpumounter_amd.worker.lease import expires_of
 
@@ -71,6 +72,8 @@ async def node_status(svc, include_processes: bool) -> dict:
                     by[g.index] = str(e)
             return by
         out["processes"] = await asyncio.to_thread(procs)     # amdsmi: off the loop
+        # those PIDs are host-namespace numbers: comparable with this worker's only with hostPID
+        out["host_pid_ns"] = host_pid_ns()
     for state in ("GPU_FREE_STATE", "GPU_ALLOCATED_STATE"):
         svc.metrics.ledger_gpus.labels(state=state).set(
             sum(1 for g in gpus if g.state.value == state))

@@ -153,3 +153,18 @@ def test_worker_detach_takes_the_table_the_namespace_allows(tmp_path, monkeypatc
         if p.poll() is None:
             p.kill()
         p.wait()
+
+
+def test_node_status_says_whose_pids_the_process_tables_hold(mock_inventory):
+    import asyncio
+
+    from gpumounter_amd.fakes.harness import LocalCluster
+
+    async def main():
+        async with LocalCluster(node_gpu_bdfs=[mock_inventory.gpus()[0].bdf],
+                                start_master=False) as lc:
+            svc = lc.nodes["node-0"].worker.service
+            return await svc.node_status(True), await svc.node_status(False)
+    with_procs, without = asyncio.run(main())
+    assert with_procs["host_pid_ns"] is procs.host_pid_ns() and "processes" in with_procs
+    assert "host_pid_ns" not in without
