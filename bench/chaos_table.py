@@ -15,11 +15,12 @@ COMMITS = {"sweep1": "≥ `dfe7c34`", "sweep2": "≥ `dfe7c34`", "sweep3": "`f28
            "sweep10": "`7840df0`", "sweep11": "`7840df0`", "sweep12": "`0a02c8c`",
            "sweep13": "`0a02c8c`", "sweep14": "`197ce4f`", "sweep15": "`197ce4f`",
            "sweep16": "`197ce4f`", "sweep17": "`197ce4f`",
-           "sweep18": "`0fded3c`", "sweep19": "`ec95933`",
+           "sweep18": "`0fded3c`", "sweep19": "`ec95933`", "sweep20": "`6fef154`",
            "box1": "`47fda63`",
            "box2": "`c89abea`", "box3": "`7de522a`", "box4": "`9880c89`", "box5": "`3bfbd67`",
            "box6": "`197ce4f`", "box7": "`197ce4f`", "box8": "`bbeb156`",
-           "box9": "`f9547fe`", "box10": "`ec95933`"}
+           "box9": "`f9547fe`", "box10": "`ec95933`",
+           "box11": "`d797c3e`"}
 
 
 def main(root: str) -> int:
