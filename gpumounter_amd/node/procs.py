@@ -125,7 +125,7 @@ def kfd_table(root: str = KFD_PROC) -> Dict[int, Dict[int, int]]:
 
 
 def busy_pids(inv: Inventory, gpus: Sequence[AmdGpu], container_pids: Iterable[int],
-              drm_major: int = DRM_MAJOR, mode: str = "auto", kfd_root: str = KFD_PROC,
+              drm_major: int = DRM_MAJOR, mode: str = "auto", kfd_root: str = "",
               tables: bool = True) -> Dict[int, List[int]]:
     """GPU index → container PIDs that hold that GPU.
 
@@ -133,7 +133,9 @@ def busy_pids(inv: Inventory, gpus: Sequence[AmdGpu], container_pids: Iterable[i
     process cannot use a GPU without that fd (KFD binds a GPU's VM through its DRM render fd,
     and ROCr keeps it open for the process lifetime), so when every fd table is readable the
     scan is complete. The process tables cover the PIDs whose fd table could not be read:
-    KFD's sysfs table when ``kfd_root`` is readable (a few small reads), else amdsmi's.
+    KFD's sysfs table when ``kfd_root`` is given and readable (a few small reads), else
+    amdsmi's. The worker passes ``kfd_root`` only with the real amdsmi library: the mock
+    library's GPUs are not this node's KFD nodes.
     ``mode="both"`` always takes the union. ``tables=False`` (the worker is not in the host
     PID namespace, see the module docstring) leaves the tables out: their PIDs are not this
     namespace's.

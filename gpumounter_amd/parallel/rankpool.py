@@ -117,7 +117,9 @@ def _rank_main(rank: int, world: int) -> int:
     import torch.distributed as dist
 
     rdv = os.environ.get("GM_RANKPOOL_RDV") or "env://"
-    on_gpu = torch.cuda.is_available()
+    # GM_RANKPOOL_CPU=1: gloo on the CPU even where a GPU is visible (the hermetic test on a
+    # GPU box, where an empty CUDA_VISIBLE_DEVICES does not hide the ROCm devices)
+    on_gpu = os.environ.get("GM_RANKPOOL_CPU") != "1" and torch.cuda.is_available()
     backend = "nccl" if on_gpu else "gloo"
     dev = None
     bound = ""

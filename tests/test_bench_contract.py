@@ -150,7 +150,8 @@ def test_rank_pool_two_ranks_on_cpu():
             "r2 = p.allreduce(['0000:15:00.0', '0000:05:00.0'], 1024); "
             "print(json.dumps([r, r2, p.close()]))")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
-                         timeout=180, cwd=ROOT, env={**os.environ, "CUDA_VISIBLE_DEVICES": ""})
+                         timeout=180, cwd=ROOT, env={**os.environ, "CUDA_VISIBLE_DEVICES": "",
+                                                     "GM_RANKPOOL_CPU": "1"})
     assert out.returncode == 0, out.stderr[-3000:]
     r, r2, codes = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["ok"] and r2["ok"] and r["backend"] == "gloo"
