@@ -20,7 +20,8 @@ COMMITS = {"sweep1": "≥ `dfe7c34`", "sweep2": "≥ `dfe7c34`", "sweep3": "`f28
            "box2": "`c89abea`", "box3": "`7de522a`", "box4": "`9880c89`", "box5": "`3bfbd67`",
            "box6": "`197ce4f`", "box7": "`197ce4f`", "box8": "`bbeb156`",
            "box9": "`f9547fe`", "box10": "`ec95933`",
-           "box11": "`d797c3e`", "box12": "`be874bf`"}
+           "box11": "`d797c3e`", "box12": "`be874bf`",
+           "box13": "`28b1cd0`"}
 
 
 def main(root: str) -> int:
