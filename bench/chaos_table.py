@@ -21,7 +21,8 @@ COMMITS = {"sweep1": "≥ `dfe7c34`", "sweep2": "≥ `dfe7c34`", "sweep3": "`f28
            "box6": "`197ce4f`", "box7": "`197ce4f`", "box8": "`bbeb156`",
            "box9": "`f9547fe`", "box10": "`ec95933`",
            "box11": "`d797c3e`", "box12": "`be874bf`",
-           "box13": "`28b1cd0`", "box14": "`046af1b`"}
+           "box13": "`28b1cd0`", "box14": "`046af1b`",
+           "box15": "`756693b`"}
 
 
 def main(root: str) -> int:
